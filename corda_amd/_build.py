@@ -1,0 +1,63 @@
+"""In-tree build of libcordahip.so for gfx950 (hipcc; no JIT cache, the .so travels with the repo)."""
+from __future__ import annotations
+
+import os
+import subprocess
+import sys
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(PKG)
+CSRC = os.path.join(PKG, "csrc")
+LIB = os.path.join(PKG, "libcordahip.so")
+SOURCES = ["runtime.hip", "ed25519.hip", "ecdsa.hip", "txid.hip", "uniq.hip"]
+HEADERS = ["common.hpp", "fe25519_dev.hpp", "scalar_dev.hpp", "sha2_dev.hpp", "runtime.hpp", "curve_consts.hpp",
+           "p256_dev.hpp"]
+GEN = os.path.join(ROOT, "tools", "gen_constants.py")
+CONSTS = os.path.join(CSRC, "curve_consts.hpp")
+
+
+def _mtime(p):
+    return os.path.getmtime(p) if os.path.exists(p) else 0.0
+
+
+def sources():
+    return [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+
+
+def needs_rebuild() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    deps = sources() + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "cordahip.h"), GEN]
+    lm = _mtime(LIB)
+    return any(_mtime(d) > lm for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if _mtime(CONSTS) < _mtime(GEN):
+        subprocess.check_call([sys.executable, GEN, CONSTS])
+    if not force and not needs_rebuild():
+        return LIB
+    hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+    objs = []
+    procs = []
+    os.makedirs(os.path.join(PKG, "build"), exist_ok=True)
+    for src in sources():
+        obj = os.path.join(PKG, "build", os.path.basename(src) + ".o")
+        objs.append(obj)
+        cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
+               "-I", os.path.join(ROOT, "include")]
+        if verbose:
+            print(" ".join(cmd))
+        procs.append((cmd, subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT)))
+    for cmd, p in procs:
+        out, _ = p.communicate()
+        if p.returncode != 0:
+            raise RuntimeError("hipcc failed: %s\n%s" % (" ".join(cmd), out.decode(errors="replace")))
+    tmp = LIB + ".tmp"
+    subprocess.check_call([hipcc, "--offload-arch=gfx950", "-shared", "-fPIC", "-o", tmp] + objs)
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force="--force" in sys.argv, verbose=True))

@@ -1,0 +1,356 @@
+// runtime.hip — libcordahip C-ABI (include/cordahip.h): context, device workspaces, staging,
+// the classify/compaction and bitmap kernels (K5), and the per-path launch sequence.
+//
+// One context per GPU (one process per GPU).  A verify call is one stream-ordered pipeline:
+//   memset(counters) -> key prep (Ed25519, ECDSA) -> classify + compact -> per-scheme verify
+//   -> status -> bitmap (ballot)
+// Everything after the caller's H2D is asynchronous on one HIP stream, so the device-pointer
+// entry point can be captured in a hipGraph by the caller.
+#include <mutex>
+#include <string>
+#include <vector>
+#include <cstring>
+#include <cstdio>
+#include "runtime.hpp"
+
+struct DevBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+        size_t want = bytes + bytes / 4 + 256;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+struct chip_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    std::string err;
+    // verify workspaces
+    DevBuf meta, abytes, edtab, ectab, lists, counts;
+    // host-path mirrors of the caller's buffers
+    DevBuf h_key_idx, h_msg_idx, h_sig_data, h_sig_off, h_sig_len, h_key_data, h_key_off, h_key_len, h_msg_data,
+        h_msg_off, h_msg_len, h_status, h_bitmap;
+    // txid
+    DevBuf t_salts, t_start, t_group, t_internal, t_data, t_off, t_len, t_ids, t_scratch;
+    hipEvent_t ev0 = nullptr, ev1 = nullptr, tev0 = nullptr, tev1 = nullptr;
+    bool ev_pending = false, tev_pending = false;
+    chip_stats stats{};
+};
+
+static int fail(chip_ctx* c, int code, const std::string& msg) {
+    if (c) c->err = msg;
+    return code;
+}
+#define HIPCHK(ctx, x)                                                                              \
+    do {                                                                                            \
+        hipError_t e_ = (x);                                                                        \
+        if (e_ != hipSuccess)                                                                       \
+            return fail(ctx, e_ == hipErrorOutOfMemory ? CHIP_E_NOMEM : CHIP_E_DEVICE,              \
+                        std::string(#x) + ": " + hipGetErrorString(e_));                           \
+    } while (0)
+
+// ---------------------------------------------------------------------------------------
+// classify: status precedence of Crypto.doVerify (Crypto.kt:522-536 + engine order) and
+// wave-aggregated compaction of the signatures that need arithmetic into per-scheme lists.
+__global__ void __launch_bounds__(256) k_classify(uint64_t n, const uint32_t* __restrict__ key_idx,
+                                                  const uint32_t* __restrict__ msg_idx,
+                                                  const uint32_t* __restrict__ sig_len,
+                                                  const uint32_t* __restrict__ msg_len, uint64_t n_keys,
+                                                  uint64_t n_msgs, const KeyMeta* __restrict__ meta,
+                                                  uint8_t* __restrict__ status, uint32_t* __restrict__ lists,
+                                                  uint32_t* __restrict__ counts) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    int list = -1;
+    if (i < n) {
+        const uint32_t k = key_idx[i], m = msg_idx[i];
+        uint8_t st = 0xff;
+        if (k >= n_keys || m >= n_msgs) {
+            st = CHIP_UNSUPPORTED;   // malformed batch entry: hand back to the JCA path
+        } else {
+            const KeyMeta km = meta[k];
+            const uint32_t sl = sig_len[i];
+            if (km.scheme == 0) st = CHIP_UNSUPPORTED;          // findSignatureScheme / require(supported)
+            else if (sl == 0) st = CHIP_EMPTY_SIG;              // Crypto.kt:528
+            else if (msg_len[m] == 0) st = CHIP_EMPTY_CLEAR;    // Crypto.kt:529
+            else if (!km.ok) st = CHIP_KEY_INVALID;             // key never constructible
+            else if (km.scheme == CHIP_SCHEME_ED25519 && sl != 64) st = CHIP_SIG_DECODE;  // length is wrong
+            else list = km.scheme == CHIP_SCHEME_ED25519 ? LIST_ED25519 : (km.scheme == CHIP_SCHEME_R1 ? LIST_R1 : LIST_K1);
+        }
+        if (list < 0) status[i] = st;
+    }
+    const uint32_t lane = threadIdx.x & 63;
+#pragma unroll
+    for (int L = 0; L < N_LISTS; L++) {
+        const uint64_t mask = __ballot(list == L);
+        if (!mask) continue;
+        uint32_t base = 0;
+        if (lane == (uint32_t)__builtin_ctzll(mask)) base = atomicAdd(&counts[L], (uint32_t)__popcll(mask));
+        base = __shfl(base, __builtin_ctzll(mask));
+        if (list == L) {
+            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+            lists[(uint64_t)L * n + base + rank] = (uint32_t)i;
+        }
+    }
+}
+
+// status -> bitmap: one wave per 64 signatures, bit = VALID
+__global__ void __launch_bounds__(256) k_bitmap(uint64_t n, const uint8_t* __restrict__ status, uint64_t* __restrict__ bitmap) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool v = (i < n) && status[i] == CHIP_VALID;
+    const uint64_t b = __ballot(v);
+    if ((threadIdx.x & 63) == 0 && i < n) bitmap[i >> 6] = b;
+}
+
+template <class T>
+static int stage(chip_ctx* c, DevBuf& d, const T* src, uint64_t count, hipStream_t st) {
+    const size_t bytes = count * sizeof(T);
+    HIPCHK(c, d.ensure(bytes + 16));
+    if (bytes) HIPCHK(c, hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, st));
+    return CHIP_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+extern "C" {
+
+int chip_abi_version(void) { return CHIP_ABI_VERSION; }
+
+int chip_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+int chip_init(const chip_config* cfg, chip_ctx** out) {
+    if (!out) return CHIP_E_ARG;
+    *out = nullptr;
+    int dev = cfg ? cfg->device : 0;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) return CHIP_E_DEVICE;
+    if (dev < 0 || dev >= n) return CHIP_E_ARG;
+    chip_ctx* c = new chip_ctx();
+    c->device = dev;
+    if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
+        hipEventCreate(&c->tev0) != hipSuccess || hipEventCreate(&c->tev1) != hipSuccess) {
+        delete c;
+        return CHIP_E_DEVICE;
+    }
+    if (cfg && cfg->reserve_sigs) {
+        (void)c->lists.ensure(cfg->reserve_sigs * 4 * N_LISTS);
+    }
+    *out = c;
+    return CHIP_OK;
+}
+
+void chip_shutdown(chip_ctx* c) {
+    if (!c) return;
+    hipSetDevice(c->device);
+    hipStreamSynchronize(c->stream);
+    DevBuf* bufs[] = {&c->meta, &c->abytes, &c->edtab, &c->ectab, &c->lists, &c->counts, &c->h_key_idx, &c->h_msg_idx,
+                      &c->h_sig_data, &c->h_sig_off, &c->h_sig_len, &c->h_key_data, &c->h_key_off, &c->h_key_len,
+                      &c->h_msg_data, &c->h_msg_off, &c->h_msg_len, &c->h_status, &c->h_bitmap, &c->t_salts,
+                      &c->t_start, &c->t_group, &c->t_internal, &c->t_data, &c->t_off, &c->t_len, &c->t_ids,
+                      &c->t_scratch};
+    for (DevBuf* b : bufs) b->release();
+    hipEventDestroy(c->ev0);
+    hipEventDestroy(c->ev1);
+    hipEventDestroy(c->tev0);
+    hipEventDestroy(c->tev1);
+    hipStreamDestroy(c->stream);
+    delete c;
+}
+
+const char* chip_last_error(const chip_ctx* c) { return c ? c->err.c_str() : "null context"; }
+
+static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap, hipStream_t st) {
+    const uint64_t n = b->n, nk = b->n_keys;
+    if (n > 0xffffffffull) return fail(c, CHIP_E_ARG, "batch too large (n >= 2^32)");
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, c->meta.ensure(nk * sizeof(KeyMeta) + 16));
+    HIPCHK(c, c->abytes.ensure(nk * 32 + 16));
+    HIPCHK(c, c->edtab.ensure(nk * ED_KEY_TABLE_WORDS * 4 + 16));
+    HIPCHK(c, c->ectab.ensure(nk * EC_KEY_TABLE_WORDS * 4 + 16));
+    HIPCHK(c, c->lists.ensure(n * 4 * N_LISTS + 16));
+    HIPCHK(c, c->counts.ensure(64));
+    HIPCHK(c, hipEventRecord(c->ev0, st));
+    HIPCHK(c, hipMemsetAsync(c->counts.p, 0, 64, st));
+    if (nk) HIPCHK(c, hipMemsetAsync(c->meta.p, 0, nk * sizeof(KeyMeta), st));
+    KeyMeta* meta = c->meta.as<KeyMeta>();
+    launch_ed25519_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->abytes.as<uint32_t>(),
+                            c->edtab.as<uint32_t>());
+    launch_ecdsa_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->ectab.as<uint32_t>());
+    if (n) {
+        const uint32_t blocks = (uint32_t)((n + 255) / 256);
+        uint32_t* lists = c->lists.as<uint32_t>();
+        uint32_t* counts = c->counts.as<uint32_t>();
+        hipLaunchKernelGGL(k_classify, dim3(blocks), dim3(256), 0, st, n, b->key_idx, b->msg_idx, b->sig_len, b->msg_len,
+                           nk, b->n_msgs, meta, status, lists, counts);
+        launch_ed25519_verify(st, n, lists + (uint64_t)LIST_ED25519 * n, counts + LIST_ED25519, b,
+                              c->abytes.as<uint32_t>(), c->edtab.as<uint32_t>(), status);
+        launch_ecdsa_verify(st, CHIP_SCHEME_R1, n, lists + (uint64_t)LIST_R1 * n, counts + LIST_R1, b,
+                            c->ectab.as<uint32_t>(), status);
+        launch_ecdsa_verify(st, CHIP_SCHEME_K1, n, lists + (uint64_t)LIST_K1 * n, counts + LIST_K1, b,
+                            c->ectab.as<uint32_t>(), status);
+        if (bitmap) hipLaunchKernelGGL(k_bitmap, dim3(blocks), dim3(256), 0, st, n, status, bitmap);
+    }
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->ev1, st));
+    c->ev_pending = true;
+    c->stats.batches++;
+    c->stats.sigs += n;
+    c->stats.keys_prepared += nk;
+    return CHIP_OK;
+}
+
+int chip_verify_batch_device(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap, void* stream) {
+    if (!c || !b || !status) return fail(c, CHIP_E_ARG, "null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    return verify_device_locked(c, b, status, bitmap, st);
+}
+
+int chip_verify_batch(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap) {
+    if (!c || !b) return fail(c, CHIP_E_ARG, "null argument");
+    const uint64_t n = b->n, nk = b->n_keys, nm = b->n_msgs;
+    if ((n && (!b->key_idx || !b->msg_idx || !b->sig_off || !b->sig_len)) ||
+        (nk && (!b->key_data || !b->key_off || !b->key_len)) || (nm && (!b->msg_data || !b->msg_off || !b->msg_len)))
+        return fail(c, CHIP_E_ARG, "null batch array");
+    // bounds: pools must contain every (offset, length) range and indices must be in range
+    for (uint64_t i = 0; i < n; i++) {
+        if (b->key_idx[i] >= nk || b->msg_idx[i] >= nm) return fail(c, CHIP_E_ARG, "key_idx/msg_idx out of range");
+        if (b->sig_off[i] + b->sig_len[i] > b->sig_bytes) return fail(c, CHIP_E_ARG, "signature outside sig pool");
+    }
+    for (uint64_t k = 0; k < nk; k++)
+        if (b->key_off[k] + b->key_len[k] > b->key_bytes) return fail(c, CHIP_E_ARG, "key outside key pool");
+    for (uint64_t m = 0; m < nm; m++)
+        if (b->msg_off[m] + b->msg_len[m] > b->msg_bytes) return fail(c, CHIP_E_ARG, "message outside msg pool");
+    std::lock_guard<std::mutex> g(c->mu);
+    hipStream_t st = c->stream;
+    HIPCHK(c, hipSetDevice(c->device));
+    int r;
+    if ((r = stage(c, c->h_key_idx, b->key_idx, n, st)) || (r = stage(c, c->h_msg_idx, b->msg_idx, n, st)) ||
+        (r = stage(c, c->h_sig_data, b->sig_data, b->sig_bytes, st)) || (r = stage(c, c->h_sig_off, b->sig_off, n, st)) ||
+        (r = stage(c, c->h_sig_len, b->sig_len, n, st)) || (r = stage(c, c->h_key_data, b->key_data, b->key_bytes, st)) ||
+        (r = stage(c, c->h_key_off, b->key_off, nk, st)) || (r = stage(c, c->h_key_len, b->key_len, nk, st)) ||
+        (r = stage(c, c->h_msg_data, b->msg_data, b->msg_bytes, st)) || (r = stage(c, c->h_msg_off, b->msg_off, nm, st)) ||
+        (r = stage(c, c->h_msg_len, b->msg_len, nm, st)))
+        return r;
+    HIPCHK(c, c->h_status.ensure(n + 16));
+    const uint64_t nw = (n + 63) / 64;
+    HIPCHK(c, c->h_bitmap.ensure(nw * 8 + 16));
+    chip_sig_batch d = *b;
+    d.key_idx = c->h_key_idx.as<uint32_t>();
+    d.msg_idx = c->h_msg_idx.as<uint32_t>();
+    d.sig_data = c->h_sig_data.as<uint8_t>();
+    d.sig_off = c->h_sig_off.as<uint64_t>();
+    d.sig_len = c->h_sig_len.as<uint32_t>();
+    d.key_data = c->h_key_data.as<uint8_t>();
+    d.key_off = c->h_key_off.as<uint64_t>();
+    d.key_len = c->h_key_len.as<uint32_t>();
+    d.msg_data = c->h_msg_data.as<uint8_t>();
+    d.msg_off = c->h_msg_off.as<uint64_t>();
+    d.msg_len = c->h_msg_len.as<uint32_t>();
+    if ((r = verify_device_locked(c, &d, c->h_status.as<uint8_t>(), c->h_bitmap.as<uint64_t>(), st))) return r;
+    if (status && n) HIPCHK(c, hipMemcpyAsync(status, c->h_status.p, n, hipMemcpyDeviceToHost, st));
+    if (bitmap && nw) HIPCHK(c, hipMemcpyAsync(bitmap, c->h_bitmap.p, nw * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->stats.last_verify_kernel_ms = ms;
+    c->ev_pending = false;
+    if (status)
+        for (uint64_t i = 0; i < n; i++) c->stats.status_count[status[i] & 7]++;
+    return CHIP_OK;
+}
+
+int chip_get_stats(const chip_ctx* cc, chip_stats* out) {
+    if (!cc || !out) return CHIP_E_ARG;
+    chip_ctx* c = const_cast<chip_ctx*>(cc);
+    std::lock_guard<std::mutex> g(c->mu);
+    float ms;
+    if (c->ev_pending && hipEventQuery(c->ev1) == hipSuccess && hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) {
+        c->stats.last_verify_kernel_ms = ms;
+        c->ev_pending = false;
+    }
+    if (c->tev_pending && hipEventQuery(c->tev1) == hipSuccess && hipEventElapsedTime(&ms, c->tev0, c->tev1) == hipSuccess) {
+        c->stats.last_txid_kernel_ms = ms;
+        c->tev_pending = false;
+    }
+    *out = c->stats;
+    return CHIP_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// tx ids
+int chip_txid_batch_device(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids, void* stream) {
+    if (!c || !b || (!ids && b->ntx)) return fail(c, CHIP_E_ARG, "null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(c, hipSetDevice(c->device));
+    const uint64_t scratch_words = b->ntx * 64 * 8 + b->ncomp * 8 + 64;
+    HIPCHK(c, c->t_scratch.ensure(scratch_words * 4));
+    HIPCHK(c, hipEventRecord(c->tev0, st));
+    launch_txid(st, b, ids, c->t_scratch.as<uint32_t>(), scratch_words);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipEventRecord(c->tev1, st));
+    c->tev_pending = true;
+    c->stats.txids += b->ntx;
+    return CHIP_OK;
+}
+
+int chip_txid_batch(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids) {
+    if (!c || !b) return fail(c, CHIP_E_ARG, "null argument");
+    const uint64_t ntx = b->ntx, nc = b->ncomp;
+    if (ntx && (!b->salts || !b->tx_comp_start || !ids)) return fail(c, CHIP_E_ARG, "null tx array");
+    if (nc && (!b->comp_group || !b->comp_internal || !b->comp_off || !b->comp_len || !b->data))
+        return fail(c, CHIP_E_ARG, "null component array");
+    if (ntx && b->tx_comp_start[ntx] > nc) return fail(c, CHIP_E_ARG, "tx_comp_start out of range");
+    for (uint64_t t = 0; t < ntx; t++)
+        if (b->tx_comp_start[t] > b->tx_comp_start[t + 1]) return fail(c, CHIP_E_ARG, "tx_comp_start not monotone");
+    for (uint64_t k = 0; k < nc; k++)
+        if (b->comp_off[k] + b->comp_len[k] > b->data_bytes) return fail(c, CHIP_E_ARG, "component outside data pool");
+    hipStream_t st = c->stream;
+    int r;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        HIPCHK(c, hipSetDevice(c->device));
+        if ((r = stage(c, c->t_salts, b->salts, ntx * 32, st)) ||
+            (r = stage(c, c->t_start, b->tx_comp_start, ntx ? ntx + 1 : 0, st)) ||
+            (r = stage(c, c->t_group, b->comp_group, nc, st)) || (r = stage(c, c->t_internal, b->comp_internal, nc, st)) ||
+            (r = stage(c, c->t_data, b->data, b->data_bytes, st)) || (r = stage(c, c->t_off, b->comp_off, nc, st)) ||
+            (r = stage(c, c->t_len, b->comp_len, nc, st)))
+            return r;
+        HIPCHK(c, c->t_ids.ensure(ntx * 32 + 16));
+    }
+    chip_tx_batch d = *b;
+    d.salts = c->t_salts.as<uint8_t>();
+    d.tx_comp_start = c->t_start.as<uint64_t>();
+    d.comp_group = c->t_group.as<uint32_t>();
+    d.comp_internal = c->t_internal.as<uint32_t>();
+    d.data = c->t_data.as<uint8_t>();
+    d.comp_off = c->t_off.as<uint64_t>();
+    d.comp_len = c->t_len.as<uint32_t>();
+    if ((r = chip_txid_batch_device(c, &d, c->t_ids.as<uint8_t>(), st))) return r;
+    std::lock_guard<std::mutex> g(c->mu);
+    if (ntx) HIPCHK(c, hipMemcpyAsync(ids, c->t_ids.p, ntx * 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    float ms = 0;
+    if (hipEventElapsedTime(&ms, c->tev0, c->tev1) == hipSuccess) c->stats.last_txid_kernel_ms = ms;
+    c->tev_pending = false;
+    return CHIP_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,264 @@
+"""ctypes binding of libcordahip.so (the C-ABI in include/cordahip.h).
+
+The product path: every call here goes to the HIP kernels.  There is no CPU fallback — if the
+library is missing or no GPU is present, calls raise NativeUnavailable.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+from . import _build
+
+_lib = None
+
+
+class NativeUnavailable(RuntimeError):
+    pass
+
+
+class ChipError(RuntimeError):
+    def __init__(self, code, msg):
+        super().__init__("libcordahip error %d: %s" % (code, msg))
+        self.code = code
+
+
+VALID, INVALID, SIG_DECODE, EMPTY_SIG, EMPTY_CLEAR, UNSUPPORTED, KEY_INVALID = range(7)
+STATUS_NAMES = ["VALID", "INVALID", "SIG_DECODE", "EMPTY_SIG", "EMPTY_CLEAR", "UNSUPPORTED", "KEY_INVALID"]
+SCHEME_K1, SCHEME_R1, SCHEME_ED25519 = 2, 3, 4
+
+# exported symbols declared in include/cordahip.h
+EXPORTS = ["chip_abi_version", "chip_device_count", "chip_init", "chip_shutdown", "chip_last_error",
+           "chip_verify_batch", "chip_verify_batch_device", "chip_txid_batch", "chip_txid_batch_device",
+           "chip_uniq_open", "chip_uniq_close", "chip_uniq_size", "chip_uniq_rebuild", "chip_uniq_commit_batch",
+           "chip_get_stats"]
+
+u8p = ctypes.POINTER(ctypes.c_uint8)
+u32p = ctypes.POINTER(ctypes.c_uint32)
+u64p = ctypes.POINTER(ctypes.c_uint64)
+
+
+class ChipConfig(ctypes.Structure):
+    _fields_ = [("device", ctypes.c_int), ("flags", ctypes.c_uint32), ("reserve_sigs", ctypes.c_uint64)]
+
+
+class ChipSigBatch(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("key_idx", ctypes.c_void_p), ("msg_idx", ctypes.c_void_p),
+                ("sig_data", ctypes.c_void_p), ("sig_off", ctypes.c_void_p), ("sig_len", ctypes.c_void_p),
+                ("n_keys", ctypes.c_uint64), ("key_data", ctypes.c_void_p), ("key_off", ctypes.c_void_p),
+                ("key_len", ctypes.c_void_p), ("n_msgs", ctypes.c_uint64), ("msg_data", ctypes.c_void_p),
+                ("msg_off", ctypes.c_void_p), ("msg_len", ctypes.c_void_p), ("sig_bytes", ctypes.c_uint64),
+                ("key_bytes", ctypes.c_uint64), ("msg_bytes", ctypes.c_uint64)]
+
+
+class ChipTxBatch(ctypes.Structure):
+    _fields_ = [("ntx", ctypes.c_uint64), ("salts", ctypes.c_void_p), ("tx_comp_start", ctypes.c_void_p),
+                ("ncomp", ctypes.c_uint64), ("comp_group", ctypes.c_void_p), ("comp_internal", ctypes.c_void_p),
+                ("data", ctypes.c_void_p), ("comp_off", ctypes.c_void_p), ("comp_len", ctypes.c_void_p),
+                ("data_bytes", ctypes.c_uint64)]
+
+
+class ChipConflict(ctypes.Structure):
+    _fields_ = [("tx", ctypes.c_uint64), ("input_index", ctypes.c_uint32), ("consumed_index", ctypes.c_uint32),
+                ("consuming_tx", ctypes.c_uint8 * 32), ("consuming_caller", ctypes.c_uint32),
+                ("pad", ctypes.c_uint32)]
+
+
+class ChipStats(ctypes.Structure):
+    _fields_ = [("batches", ctypes.c_uint64), ("sigs", ctypes.c_uint64), ("keys_prepared", ctypes.c_uint64),
+                ("status_count", ctypes.c_uint64 * 8), ("txids", ctypes.c_uint64), ("uniq_commits", ctypes.c_uint64),
+                ("last_verify_kernel_ms", ctypes.c_double), ("last_txid_kernel_ms", ctypes.c_double)]
+
+
+def lib_path() -> str:
+    return _build.LIB
+
+
+def load(build_if_missing: bool = False):
+    """Load libcordahip.so.  Raises NativeUnavailable if it has not been built."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    path = lib_path()
+    if not os.path.exists(path):
+        if build_if_missing:
+            _build.build()
+        else:
+            raise NativeUnavailable("libcordahip.so not built (run __graft_entry__.build())")
+    lib = ctypes.CDLL(path)
+    lib.chip_last_error.restype = ctypes.c_char_p
+    lib.chip_last_error.argtypes = [ctypes.c_void_p]
+    lib.chip_init.argtypes = [ctypes.POINTER(ChipConfig), ctypes.POINTER(ctypes.c_void_p)]
+    lib.chip_shutdown.argtypes = [ctypes.c_void_p]
+    lib.chip_verify_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipSigBatch), ctypes.c_void_p, ctypes.c_void_p]
+    lib.chip_verify_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipSigBatch), ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_void_p]
+    lib.chip_txid_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipTxBatch), ctypes.c_void_p]
+    lib.chip_txid_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipTxBatch), ctypes.c_void_p,
+                                           ctypes.c_void_p]
+    lib.chip_uniq_open.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]
+    lib.chip_uniq_close.argtypes = [ctypes.c_void_p]
+    lib.chip_uniq_size.argtypes = [ctypes.c_void_p]
+    lib.chip_uniq_size.restype = ctypes.c_uint64
+    lib.chip_uniq_rebuild.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                      ctypes.c_void_p, ctypes.c_void_p]
+    lib.chip_uniq_commit_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
+    lib.chip_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipStats)]
+    _lib = lib
+    return lib
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, int):
+        return a
+    if hasattr(a, "data_ptr"):          # torch tensor (device-resident path)
+        return a.data_ptr()
+    return a.ctypes.data
+
+
+def make_sig_batch(b) -> ChipSigBatch:
+    """Build a ChipSigBatch from an object with the SoA fields (numpy arrays or torch tensors)."""
+    def nbytes(a):
+        if a is None:
+            return 0
+        if hasattr(a, "numel"):
+            return int(a.numel() * a.element_size())
+        return int(a.nbytes)
+    s = ChipSigBatch()
+    s.n = len(b.key_idx)
+    s.key_idx, s.msg_idx = _ptr(b.key_idx), _ptr(b.msg_idx)
+    s.sig_data, s.sig_off, s.sig_len = _ptr(b.sig_data), _ptr(b.sig_off), _ptr(b.sig_len)
+    s.n_keys = len(b.key_off)
+    s.key_data, s.key_off, s.key_len = _ptr(b.key_data), _ptr(b.key_off), _ptr(b.key_len)
+    s.n_msgs = len(b.msg_off)
+    s.msg_data, s.msg_off, s.msg_len = _ptr(b.msg_data), _ptr(b.msg_off), _ptr(b.msg_len)
+    s.sig_bytes, s.key_bytes, s.msg_bytes = nbytes(b.sig_data), nbytes(b.key_data), nbytes(b.msg_data)
+    return s
+
+
+def make_tx_batch(t) -> ChipTxBatch:
+    def nbytes(a):
+        if hasattr(a, "numel"):
+            return int(a.numel() * a.element_size())
+        return int(a.nbytes)
+    s = ChipTxBatch()
+    s.ntx = t.ntx
+    s.salts, s.tx_comp_start = _ptr(t.salts), _ptr(t.tx_comp_start)
+    s.ncomp = len(t.comp_group)
+    s.comp_group, s.comp_internal = _ptr(t.comp_group), _ptr(t.comp_internal)
+    s.data, s.comp_off, s.comp_len = _ptr(t.data), _ptr(t.comp_off), _ptr(t.comp_len)
+    s.data_bytes = nbytes(t.data)
+    return s
+
+
+class Context:
+    """One libcordahip context = one GPU (one process per GPU)."""
+
+    def __init__(self, device: int = 0, reserve_sigs: int = 0):
+        self.lib = load()
+        cfg = ChipConfig(device, 0, reserve_sigs)
+        h = ctypes.c_void_p()
+        rc = self.lib.chip_init(ctypes.byref(cfg), ctypes.byref(h))
+        if rc != 0:
+            raise NativeUnavailable("chip_init(device=%d) failed with %d (no GPU?)" % (device, rc))
+        self.h = h
+        self.device = device
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.chip_shutdown(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check(self, rc):
+        if rc != 0:
+            raise ChipError(rc, self.lib.chip_last_error(self.h).decode(errors="replace"))
+
+    # ---- signatures ----
+    def verify_batch(self, b):
+        """Host SoA batch -> (status u8[n], bitmap u64[ceil(n/64)])."""
+        s = make_sig_batch(b)
+        status = np.zeros(s.n, dtype=np.uint8)
+        bitmap = np.zeros((s.n + 63) // 64, dtype=np.uint64)
+        self._check(self.lib.chip_verify_batch(self.h, ctypes.byref(s), _ptr(status), _ptr(bitmap)))
+        return status, bitmap
+
+    def verify_batch_device(self, dev_batch, status, bitmap, stream=None):
+        """Device-resident batch (torch tensors on this GPU); enqueued on `stream` (int handle)."""
+        s = make_sig_batch(dev_batch)
+        self._check(self.lib.chip_verify_batch_device(self.h, ctypes.byref(s), _ptr(status), _ptr(bitmap),
+                                                      stream or None))
+
+    # ---- tx ids ----
+    def txid_batch(self, t) -> np.ndarray:
+        s = make_tx_batch(t)
+        ids = np.zeros(s.ntx * 32, dtype=np.uint8)
+        self._check(self.lib.chip_txid_batch(self.h, ctypes.byref(s), _ptr(ids)))
+        return ids.reshape(s.ntx, 32)
+
+    def txid_batch_device(self, dev_tx, ids, stream=None):
+        s = make_tx_batch(dev_tx)
+        self._check(self.lib.chip_txid_batch_device(self.h, ctypes.byref(s), _ptr(ids), stream or None))
+
+    def stats(self) -> ChipStats:
+        st = ChipStats()
+        self._check(self.lib.chip_get_stats(self.h, ctypes.byref(st)))
+        return st
+
+    # ---- uniqueness ----
+    def uniq_open(self, capacity: int):
+        return UniqTable(self, capacity)
+
+
+class UniqTable:
+    """GPU-resident StateRef -> ConsumingTx table (PersistentUniquenessProvider semantics)."""
+
+    def __init__(self, ctx: Context, capacity: int):
+        self.ctx = ctx
+        h = ctypes.c_void_p()
+        ctx._check(ctx.lib.chip_uniq_open(ctx.h, ctypes.c_uint64(capacity), ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.ctx.lib.chip_uniq_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def size(self) -> int:
+        return int(self.ctx.lib.chip_uniq_size(self.h))
+
+    def rebuild(self, refs36, tx32, idx, caller):
+        n = len(idx)
+        self.ctx._check(self.ctx.lib.chip_uniq_rebuild(self.h, ctypes.c_uint64(n), _ptr(refs36), _ptr(tx32),
+                                                       _ptr(idx), _ptr(caller)))
+
+    def commit_batch(self, tx_ref_start, refs36, tx_ids, callers, cap=None):
+        ntx = len(tx_ref_start) - 1
+        st = np.zeros(ntx, dtype=np.uint8)
+        if cap is None:
+            cap = int(tx_ref_start[-1]) + 1
+        out = (ChipConflict * max(cap, 1))()
+        nout = ctypes.c_uint64()
+        self.ctx._check(self.ctx.lib.chip_uniq_commit_batch(self.h, ctypes.c_uint64(ntx), _ptr(tx_ref_start),
+                                                            _ptr(refs36), _ptr(tx_ids), _ptr(callers), _ptr(st),
+                                                            out, ctypes.c_uint64(cap), ctypes.byref(nout)))
+        recs = [(c.tx, c.input_index, c.consumed_index, bytes(c.consuming_tx), c.consuming_caller)
+                for c in out[:min(nout.value, cap)]]
+        return st, recs

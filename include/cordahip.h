@@ -1,0 +1,190 @@
+/*
+ * cordahip.h — C-ABI of libcordahip, the MI355X-native batch transaction-verification engine
+ * for Corda's signature / tx-id / notary-uniqueness hot path.
+ *
+ * Plain C: pointers + sizes, no C++ or HIP types in any signature.  One context per GPU
+ * (one process per GPU).  Every function returns 0 on success or a negative CHIP_E* code;
+ * chip_last_error(ctx) then holds a message.  The caller owns every input/output buffer; the
+ * library owns device memory (key tables, workspaces, the uniqueness table) and retains no
+ * caller pointer after a call returns.
+ *
+ * Reference interfaces each entry point replaces (paths under /root/reference):
+ *   chip_verify_batch   -> TransactionWithSignatures.checkSignaturesAreValid's loop
+ *                          `for (sig in sigs) sig.verify(id)`
+ *                          core/src/main/kotlin/net/corda/core/transactions/TransactionWithSignatures.kt:62-66
+ *                          -> TransactionSignature.verify  core/.../crypto/TransactionSignature.kt:26-40
+ *                          -> Crypto.doVerify(PublicKey, ByteArray, ByteArray)  core/.../crypto/Crypto.kt:502-536
+ *                          -> Crypto.isValid(SignatureScheme, ...)             core/.../crypto/Crypto.kt:615-625
+ *                          (JCA engines: i2p eddsa 0.2.0 via X509EdDSAEngine.kt:40; BC 1.57 SHA256withECDSA)
+ *   chip_txid_batch     -> WireTransaction.id / merkleTree / groupHashes / availableComponentHashes
+ *                          core/.../transactions/WireTransaction.kt:63,139-189, MerkleTree.kt:27-66,
+ *                          CryptoUtils.kt:216-233 (componentHash / computeNonce)
+ *   chip_uniq_*         -> UniquenessProvider.commit  core/.../node/services/UniquenessProvider.kt:15-17
+ *                          PersistentUniquenessProvider.commit  node/.../transactions/PersistentUniquenessProvider.kt:92-113
+ *                          TrustedAuthorityNotaryService.commitInputStates  core/.../node/services/NotaryService.kt:61-75
+ *
+ * Status bytes (per signature) mirror what Crypto.doVerify does with that input:
+ *   CHIP_VALID        returns true
+ *   CHIP_INVALID      isValid false -> SignatureException("Signature Verification failed!")   Crypto.kt:534
+ *   CHIP_SIG_DECODE   engine SignatureException: Ed25519 "signature length is wrong",
+ *                     ECDSA "error decoding signature bytes." (DER)
+ *   CHIP_EMPTY_SIG    IllegalArgumentException("Signature data is empty!")                    Crypto.kt:528
+ *   CHIP_EMPTY_CLEAR  IllegalArgumentException("Clear data is empty, nothing to verify!")     Crypto.kt:529
+ *   CHIP_UNSUPPORTED  key algorithm is not Ed25519 / ECDSA secp256r1 / secp256k1 (RSA, SPHINCS,
+ *                     composite, unknown): the caller falls back to the JCA path
+ *   CHIP_KEY_INVALID  key bytes are not a valid curve point: the JVM could never have built this
+ *                     PublicKey (InvalidKeyException / IllegalArgumentException at key decode)
+ * The bitmap holds bit i = (status[i] == CHIP_VALID), word i/64, bit i%64.
+ */
+#ifndef CORDAHIP_H
+#define CORDAHIP_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CHIP_ABI_VERSION 1
+
+enum chip_sig_status {
+    CHIP_VALID = 0,
+    CHIP_INVALID = 1,
+    CHIP_SIG_DECODE = 2,
+    CHIP_EMPTY_SIG = 3,
+    CHIP_EMPTY_CLEAR = 4,
+    CHIP_UNSUPPORTED = 5,
+    CHIP_KEY_INVALID = 6
+};
+
+/* SignatureScheme.schemeNumberID (Crypto.kt:84-128) */
+enum chip_scheme { CHIP_SCHEME_K1 = 2, CHIP_SCHEME_R1 = 3, CHIP_SCHEME_ED25519 = 4 };
+
+enum chip_error {
+    CHIP_OK = 0,
+    CHIP_E_ARG = -1,      /* bad argument (null pointer, index out of range, ...) */
+    CHIP_E_DEVICE = -2,   /* HIP runtime error                                    */
+    CHIP_E_NOMEM = -3,    /* device allocation failed                             */
+    CHIP_E_CAPACITY = -4  /* output capacity too small (chip_uniq_commit_batch)   */
+};
+
+typedef struct chip_ctx chip_ctx;
+
+typedef struct {
+    int device;             /* HIP device ordinal for this context (one context per GPU)   */
+    uint32_t flags;         /* reserved, 0                                                  */
+    uint64_t reserve_sigs;  /* optional: pre-size workspaces for this many signatures      */
+} chip_config;
+
+int chip_abi_version(void);
+int chip_device_count(void);
+int chip_init(const chip_config* cfg, chip_ctx** out);
+void chip_shutdown(chip_ctx* ctx);
+const char* chip_last_error(const chip_ctx* ctx);
+
+/* ---------------------------------------------------------------------------------------
+ * Signature batch, structure-of-arrays.  One entry per TransactionSignature:
+ *   key    = TransactionSignature.by.encoded  (X.509 SubjectPublicKeyInfo bytes; the scheme is
+ *            taken from its algorithm OID exactly as Crypto.findSignatureScheme(PublicKey) does,
+ *            Crypto.kt:263-267).  Keys are de-duplicated by the caller: key_idx[i] < n_keys.
+ *   sig    = TransactionSignature.bytes       (Ed25519: raw R||S; ECDSA: DER)
+ *   msg    = SignableData(txId, signatureMetadata).serialize().bytes  (Crypto.kt:552-555),
+ *            de-duplicated: msg_idx[i] < n_msgs (signers of one tx share it).
+ * Pools are byte arrays addressed by (offset, length). */
+typedef struct {
+    uint64_t n;
+    const uint32_t* key_idx;   /* [n]          */
+    const uint32_t* msg_idx;   /* [n]          */
+    const uint8_t* sig_data;   /* pool         */
+    const uint64_t* sig_off;   /* [n]          */
+    const uint32_t* sig_len;   /* [n]          */
+    uint64_t n_keys;
+    const uint8_t* key_data;   /* pool (SPKI)  */
+    const uint64_t* key_off;   /* [n_keys]     */
+    const uint32_t* key_len;   /* [n_keys]     */
+    uint64_t n_msgs;
+    const uint8_t* msg_data;   /* pool         */
+    const uint64_t* msg_off;   /* [n_msgs]     */
+    const uint32_t* msg_len;   /* [n_msgs]     */
+    uint64_t sig_bytes, key_bytes, msg_bytes;  /* pool sizes in bytes */
+} chip_sig_batch;
+
+/* Host buffers in, host buffers out (staged through pinned memory; blocking).
+ * status: [n] bytes (may be NULL); bitmap: [ceil(n/64)] words (may be NULL). */
+int chip_verify_batch(chip_ctx* ctx, const chip_sig_batch* batch, uint8_t* status, uint64_t* bitmap);
+
+/* Every pointer in `batch`, `status` and `bitmap` is device memory of this context's GPU.
+ * Enqueued on `stream` (a hipStream_t; NULL = the context's stream); returns without waiting. */
+int chip_verify_batch_device(chip_ctx* ctx, const chip_sig_batch* batch, uint8_t* status,
+                             uint64_t* bitmap, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Transaction-id batch (WireTransaction.id).  Components of transaction t are
+ * comp[tx_comp_start[t] .. tx_comp_start[t+1]); comp_group = ComponentGroup.groupIndex
+ * (ComponentGroupEnum ordinal, unknown ordinals >= 6 allowed), comp_internal = the
+ * component's index inside its group (components of one group appear in increasing
+ * internal order).  salts: [ntx * 32] PrivacySalt bytes.  ids: [ntx * 32] out.
+ * Invariant violations (WireTransaction.kt:53-60) are the caller's to reject first; a
+ * transaction with no components yields an all-zero id and tx_status 1. */
+typedef struct {
+    uint64_t ntx;
+    const uint8_t* salts;
+    const uint64_t* tx_comp_start;   /* [ntx + 1]  */
+    uint64_t ncomp;
+    const uint32_t* comp_group;      /* [ncomp]    */
+    const uint32_t* comp_internal;   /* [ncomp]    */
+    const uint8_t* data;             /* pool       */
+    const uint64_t* comp_off;        /* [ncomp]    */
+    const uint32_t* comp_len;        /* [ncomp]    */
+    uint64_t data_bytes;
+} chip_tx_batch;
+
+int chip_txid_batch(chip_ctx* ctx, const chip_tx_batch* batch, uint8_t* ids);
+int chip_txid_batch_device(chip_ctx* ctx, const chip_tx_batch* batch, uint8_t* ids, void* stream);
+
+/* ---------------------------------------------------------------------------------------
+ * Notary uniqueness (GPU-resident StateRef -> ConsumingTx table).
+ * StateRef key = 32-byte txhash || little-endian u32 index (36 bytes).
+ * ConsumingTx  = (32-byte consuming tx id, u32 inputIndex, u32 caller) where caller is the
+ *                caller's party id (the JNI layer interns Party.owningKey -> u32).
+ * commit_batch applies PersistentUniquenessProvider.commit to each tx in batch order, with
+ * TrustedAuthorityNotaryService.commitInputStates' idempotency filter:
+ *   tx_status 0 COMMITTED, 1 IDEMPOTENT (every conflict is this tx's own earlier commit),
+ *             2 CONFLICT (nothing inserted; conflict records describe every already-consumed input)
+ * A tx that fails inserts nothing, so later txs in the same batch may consume its inputs. */
+typedef struct chip_uniq chip_uniq;
+
+typedef struct {
+    uint64_t tx;               /* batch-local tx index                 */
+    uint32_t input_index;      /* position in that tx's input list     */
+    uint32_t consumed_index;   /* ConsumingTx.inputIndex               */
+    uint8_t consuming_tx[32];  /* ConsumingTx.id                       */
+    uint32_t consuming_caller; /* ConsumingTx.requestingParty (interned)*/
+    uint32_t pad;
+} chip_conflict;
+
+int chip_uniq_open(chip_ctx* ctx, uint64_t capacity, chip_uniq** out);
+void chip_uniq_close(chip_uniq* u);
+uint64_t chip_uniq_size(const chip_uniq* u);
+/* AppendOnlyPersistentMap.allPersisted: reload committed rows (e.g. at node start). */
+int chip_uniq_rebuild(chip_uniq* u, uint64_t n, const uint8_t* refs36, const uint8_t* tx32,
+                      const uint32_t* input_index, const uint32_t* caller);
+int chip_uniq_commit_batch(chip_uniq* u, uint64_t ntx, const uint64_t* tx_ref_start,
+                           const uint8_t* refs36, const uint8_t* tx_ids, const uint32_t* callers,
+                           uint8_t* tx_status, chip_conflict* out, uint64_t cap, uint64_t* n_out);
+
+/* ---------------------------------------------------------------------------------------
+ * Counters (observability; OutOfProcessTransactionVerifierService.kt:35-46 analogue). */
+typedef struct {
+    uint64_t batches, sigs, keys_prepared;
+    uint64_t status_count[8];
+    uint64_t txids, uniq_commits;
+    double last_verify_kernel_ms;  /* device time of the last verify batch (HIP events) */
+    double last_txid_kernel_ms;
+} chip_stats;
+int chip_get_stats(const chip_ctx* ctx, chip_stats* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

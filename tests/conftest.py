@@ -1,0 +1,29 @@
+import os
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+for p in (ROOT, os.path.join(ROOT, "tests"), os.path.join(ROOT, "tools")):
+    if p not in sys.path:
+        sys.path.insert(0, p)
+
+
+def pytest_configure(config):
+    config.addinivalue_line("markers", "gpu: needs an MI355X (runs the HIP path through the C-ABI)")
+
+
+@pytest.fixture(scope="session")
+def ctx():
+    """One libcordahip context on cuda:0 for the whole GPU session."""
+    import corda_amd
+    c = corda_amd.Context(0)
+    yield c
+    c.close()
+
+
+@pytest.fixture(scope="session")
+def oracle():
+    import oracle_bind
+    oracle_bind.lib()
+    return oracle_bind

@@ -1,0 +1,293 @@
+#!/usr/bin/env python3
+"""Generate the committed golden fixtures under tests/golden/.
+
+Sources of truth, per fixture:
+  * OpenSSL 3.0.2 (tools/cordagen.c) signs and verifies every canonical case; its verdict is
+    recorded as `openssl` and must equal `expected` wherever the reference semantics agree with
+    OpenSSL (canonical inputs).
+  * The reference's own deterministic test material: TestConstants.kt:27-72
+    (entropyToKeyPair(20..100) -> seed = BigInteger.toByteArray() right-padded to 32 bytes,
+    Crypto.kt:828-834) and X509EdDSAEngineTest.kt:27-60 (SEED 20170920, 2000 bytes from
+    java.util.Random(SEED), restated below).
+  * i2p/BC-specific cases where OpenSSL disagrees (S >= L, slide() carry drop, small-order and
+    non-canonical keys, DER non-minimal integers) carry `expected` from the construction and
+    are marked `unpinned` where no reference test covers them.
+  * Tx-id vectors use Python hashlib only (independent of oracle/ and of the GPU path).
+Re-run:  python tests/golden/make_golden.py
+"""
+import hashlib
+import json
+import os
+import struct
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(ROOT, "tools"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+import cordagen as G  # noqa: E402
+
+P = 2**255 - 19
+L = G.L_ED
+
+
+def java_random_bytes(seed, n):
+    """java.util.Random(seed).nextBytes(n) — the LCG specified in the Java SE API."""
+    mask = (1 << 48) - 1
+    s = (seed ^ 0x5DEECE66D) & mask
+    out = bytearray()
+
+    def next_int():
+        nonlocal s
+        s = (s * 0x5DEECE66D + 0xB) & mask
+        v = s >> 16
+        return v - (1 << 32) if v >= (1 << 31) else v
+
+    while len(out) < n:
+        r = next_int()
+        for _ in range(min(n - len(out), 4)):
+            out.append(r & 0xFF)
+            r >>= 8
+    return bytes(out)
+
+
+def entropy_seed(v: int) -> bytes:
+    """BigInteger.valueOf(v).toByteArray().copyOf(32) (Crypto.kt:830)."""
+    b = v.to_bytes((v.bit_length() + 8) // 8, "big", signed=True)
+    return (b + bytes(32))[:32]
+
+
+def slide_drops(s: int) -> int:
+    """Independent Python restatement of i2p GroupElement.slide(): dropped carries."""
+    r = [(s >> i) & 1 for i in range(256)]
+    drops = 0
+    for i in range(256):
+        if not r[i]:
+            continue
+        for b in range(1, 7):
+            if i + b >= 256:
+                break
+            if not r[i + b]:
+                continue
+            if r[i] + (r[i + b] << b) <= 15:
+                r[i] += r[i + b] << b
+                r[i + b] = 0
+            elif r[i] - (r[i + b] << b) >= -15:
+                r[i] -= r[i + b] << b
+                k = i + b
+                while k < 256:
+                    if not r[k]:
+                        r[k] = 1
+                        break
+                    r[k] = 0
+                    k += 1
+                if k == 256:
+                    drops += 1
+            else:
+                break
+    return drops
+
+
+def clamp_scalar(seed: bytes) -> int:
+    h = bytearray(hashlib.sha512(seed).digest()[:32])
+    h[0] &= 248
+    h[31] &= 127
+    h[31] |= 64
+    return int.from_bytes(h, "little")
+
+
+def ed_case(label, spki, sig, msg, expected, source, unpinned=False, msg_repeat=None):
+    """msg_repeat=(pattern, count) stores a long message compactly (the test expands it)."""
+    d = dict(label=label, spki=spki.hex(), sig=sig.hex(), expected=expected, source=source, unpinned=unpinned,
+             openssl=G.ossl_verify(spki, sig, msg) if sig and msg else None)
+    if msg_repeat:
+        d["msg_repeat"] = [msg_repeat[0].hex(), msg_repeat[1]]
+    else:
+        d["msg"] = msg.hex()
+    return d
+
+
+def ed25519_cases():
+    cases = []
+    msg = b"corda\x00\x00\x01" + hashlib.sha256(b"golden-msg").digest() * 6
+    # reference deterministic keys (TestConstants.kt:27-72)
+    for v in (20, 30, 40, 50, 60, 70, 80, 90, 100):
+        seed = entropy_seed(v)
+        a = G.ed25519_pub(seed)
+        sig = G.ed25519_sign(seed, msg)
+        cases.append(ed_case("entropyToKeyPair(%d)" % v, G.spki_ed25519(a), sig, msg, 0, "TestConstants.kt:27-72"))
+        bad = bytearray(sig)
+        bad[0] ^= 1   # signedData[0]++ style corruption (CryptoUtilsTest.kt:123-286)
+        cases.append(ed_case("entropyToKeyPair(%d) R corrupted" % v, G.spki_ed25519(a), bytes(bad), msg, 1,
+                             "CryptoUtilsTest.kt:123-286"))
+    # X509EdDSAEngineTest: SEED, 2000 random bytes from java.util.Random(SEED)
+    for sd in (20170920, 20170921):
+        seed = entropy_seed(sd)
+        data = java_random_bytes(20170920, 2000)
+        a = G.ed25519_pub(seed)
+        sig = G.ed25519_sign(seed, data)
+        cases.append(ed_case("X509EdDSAEngineTest seed %d" % sd, G.spki_ed25519(a), sig, data, 0,
+                             "X509EdDSAEngineTest.kt:27-75"))
+    # 100 zero bytes and 1 MB messages (CryptoUtilsTest full process)
+    seed = entropy_seed(70)
+    a = G.ed25519_pub(seed)
+    for pat, cnt in ((bytes(100), 1), (bytes(range(256)), 4096)):
+        m = pat * cnt
+        cases.append(ed_case("message len %d" % len(m), G.spki_ed25519(a), G.ed25519_sign(seed, m), m, 0,
+                             "CryptoUtilsTest.kt:123-286", msg_repeat=(pat, cnt)))
+    # doVerify argument checks (Crypto.kt:528-529) and engine length check
+    sig = G.ed25519_sign(seed, msg)
+    cases.append(ed_case("empty signature", G.spki_ed25519(a), b"", msg, 3, "Crypto.kt:528"))
+    cases.append(ed_case("empty clear data", G.spki_ed25519(a), sig, b"", 4, "Crypto.kt:529"))
+    cases.append(ed_case("signature 63 bytes", G.spki_ed25519(a), sig[:63], msg, 2, "i2p engineVerify length"))
+    cases.append(ed_case("signature 65 bytes", G.spki_ed25519(a), sig + b"\x00", msg, 2, "i2p engineVerify length"))
+    # unsupported key algorithm (RSA SPKI prefix) and a key that is not a curve point
+    rsa_spki = bytes.fromhex("30820122300d06092a864886f70d01010105000382010f00") + bytes(270)
+    cases.append(ed_case("RSA key -> unsupported", rsa_spki, sig, msg, 5, "Crypto.kt:263-267"))
+    y = 2
+    while True:   # smallest y with no square root for x
+        u = (y * y - 1) % P
+        v = (G_D * y * y + 1) % P
+        x2 = u * pow(v, P - 2, P) % P
+        if pow(x2, (P - 1) // 2, P) not in (0, 1):
+            break
+        y += 1
+    cases.append(ed_case("key not on curve (y=%d)" % y, G.spki_ed25519(y.to_bytes(32, "little")), sig, msg, 6,
+                         "i2p GroupElement decode"))
+    # S + L: i2p 0.2.0 has no S < L check (CVE-2020-36843) -> VALID; OpenSSL rejects
+    S = int.from_bytes(sig[32:], "little")
+    for k in (1, 2, 3):
+        s2 = S + k * L
+        if s2 < 2**256:
+            exp = 0 if slide_drops(s2) == 0 else 1
+            cases.append(ed_case("S + %dL" % k, G.spki_ed25519(a), sig[:32] + s2.to_bytes(32, "little"), msg, exp,
+                                 "i2p 0.2.0 no S<L check", unpinned=True))
+    # S >= 2^255: multiples S + kL whose slide() recoding drops a carry (effective scalar
+    # S + kL - 2^256 -> INVALID) or does not (-> VALID), over several signatures
+    found_drop = found_nodrop = 0
+    for j in range(200):
+        if found_drop >= 4 and found_nodrop >= 3:
+            break
+        mj = msg + struct.pack(">I", j)
+        sj = G.ed25519_sign(seed, mj)
+        Sj = int.from_bytes(sj[32:], "little")
+        for k in range(8, 20):
+            s2 = Sj + k * L
+            if s2 >= 2**256:
+                break
+            if s2 < 2**255:
+                continue
+            d = slide_drops(s2)
+            if d and found_drop < 4:
+                found_drop += 1
+                cases.append(ed_case("S + %dL >= 2^255 with slide carry drop (msg %d)" % (k, j), G.spki_ed25519(a),
+                                     sj[:32] + s2.to_bytes(32, "little"), mj, 1, "i2p slide() carry drop",
+                                     unpinned=True))
+            elif not d and found_nodrop < 3:
+                found_nodrop += 1
+                cases.append(ed_case("S + %dL >= 2^255 no carry drop (msg %d)" % (k, j), G.spki_ed25519(a),
+                                     sj[:32] + s2.to_bytes(32, "little"), mj, 0, "i2p slide()", unpinned=True))
+    # identity key (small order 1) forgeries: R = [S]B for any S -> VALID in i2p
+    ident = bytes([1] + [0] * 31)
+    for j, s_seed in enumerate([b"f1", b"f2"]):
+        sd = hashlib.sha256(s_seed).digest()
+        R = G.ed25519_pub(sd)
+        s = clamp_scalar(sd)
+        cases.append(ed_case("identity key forgery %d" % j, G.spki_ed25519(ident), R + s.to_bytes(32, "little"), msg,
+                             0, "no small-order check (Crypto.kt:874-924 unused)", unpinned=True))
+    # non-canonical encodings of the identity key: y = 1 + p, and x = 0 with the sign bit set
+    sd = hashlib.sha256(b"f3").digest()
+    R = G.ed25519_pub(sd)
+    s = clamp_scalar(sd)
+    noncanon_1 = (1 + P).to_bytes(32, "little")
+    signed_0 = bytes([1] + [0] * 30 + [0x80])
+    cases.append(ed_case("key y = 1 + p (non-canonical)", G.spki_ed25519(noncanon_1), R + s.to_bytes(32, "little"),
+                         msg, 0, "i2p decode tolerates y >= p; h over canonical Abyte", unpinned=True))
+    cases.append(ed_case("key x = 0 with sign bit", G.spki_ed25519(signed_0), R + s.to_bytes(32, "little"), msg, 0,
+                         "i2p decode tolerates -0", unpinned=True))
+    # non-canonical R: identity as y = 1 + p with identity key and S = 0 -> canonical(R') != R
+    cases.append(ed_case("R non-canonical (1 + p)", G.spki_ed25519(ident), noncanon_1 + bytes(32), msg, 1,
+                         "bytewise compare with canonical encode", unpinned=True))
+    cases.append(ed_case("R canonical identity, S = 0", G.spki_ed25519(ident), ident + bytes(32), msg, 0,
+                         "identity key, S = 0", unpinned=True))
+    cases.append(ed_case("all-zero signature", G.spki_ed25519(ident), bytes(64), msg, 1, "R = 00.. (y = 0)",
+                         unpinned=True))
+    # order-4 key (y = 0) and order-2 key (y = -1): decodes fine, arithmetic decides
+    for lab, enc in (("order-4 key (y=0)", bytes(32)), ("order-2 key (y=-1)", (P - 1).to_bytes(32, "little"))):
+        cases.append(ed_case(lab + " with random sig", G.spki_ed25519(enc), sig, msg, 1, "no small-order check",
+                             unpinned=True))
+    return cases
+
+
+G_D = (-121665 * pow(121666, P - 2, P)) % P
+
+
+def txid_reference(salt, groups):
+    """hashlib-only restatement of WireTransaction.id (WireTransaction.kt:139-189)."""
+    def sha(b):
+        return hashlib.sha256(b).digest()
+
+    def merkle(leaves):
+        n = 1
+        while n < len(leaves):
+            n *= 2
+        lvl = list(leaves) + [bytes(32)] * (n - len(leaves))
+        while len(lvl) > 1:
+            lvl = [sha(lvl[i] + lvl[i + 1]) for i in range(0, len(lvl), 2)]
+        return lvl[0]
+
+    present = {g: comps for g, comps in groups}
+    maxg = max(present)
+    tops = []
+    for g in range(maxg + 1):
+        if g in present:
+            leaves = []
+            for i, c in enumerate(present[g]):
+                nonce = sha(sha(salt + struct.pack(">ii", g, i)))
+                leaves.append(sha(sha(nonce + c)))
+            tops.append(merkle(leaves))
+        else:
+            tops.append(b"\xff" * 32)
+    return merkle(tops)
+
+
+def txid_cases():
+    cases = []
+    rng = G.PRNG(0xC0DA, b"txid")
+    def rb(n):
+        return rng.bytes(n)
+    shapes = [
+        ("issue: outputs, commands, notary", [(1, [rb(640)]), (2, [rb(320)]), (4, [rb(384)])]),
+        ("move: inputs, outputs, commands, notary", [(0, [rb(96), rb(96)]), (1, [rb(640), rb(640)]), (2, [rb(320)]),
+                                                      (4, [rb(384)])]),
+        ("cfg4 profile (6 groups, 8 components)", [(0, [rb(96), rb(96)]), (1, [rb(640), rb(640)]), (2, [rb(320)]),
+                                                   (3, [rb(96)]), (4, [rb(384)]), (5, [rb(96)])]),
+        ("single component (1-leaf tree = leaf)", [(0, [rb(1)])]),
+        ("odd group sizes 3 and 5", [(0, [rb(10), rb(20), rb(30)]), (1, [rb(5)] * 5)]),
+        ("unknown group ordinal 20 (CompatibleTransactionTests.kt:151-164)", [(0, [rb(40)]), (2, [rb(50)]),
+                                                                               (20, [rb(60)])]),
+        ("group order of insertion irrelevant (sorted here)", [(1, [rb(33)]), (3, [rb(64)])]),
+        ("component lengths around SHA block edges", [(0, [rb(n) for n in (0, 22, 23, 55, 56, 64, 87, 88, 119, 120)])]),
+        ("large component 64 KB", [(1, [rb(1 << 16)])]),
+        ("max group ordinal 63", [(63, [rb(8)])]),
+    ]
+    for label, groups in shapes:
+        salt = rb(32)
+        cases.append(dict(label=label, salt=salt.hex(), groups=[[g, [c.hex() for c in comps]] for g, comps in groups],
+                          id=txid_reference(salt, groups).hex()))
+    return cases
+
+
+def main():
+    G.build()
+    ed = ed25519_cases()
+    with open(os.path.join(HERE, "ed25519_cases.json"), "w") as f:
+        json.dump(ed, f, indent=1)
+    tx = txid_cases()
+    with open(os.path.join(HERE, "txid_cases.json"), "w") as f:
+        json.dump(tx, f, indent=1)
+    print("ed25519 cases:", len(ed), " txid cases:", len(tx))
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,179 @@
+"""ctypes binding of oracle/liboracle.so — the CPU restatement (test infrastructure only).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB_PATH = os.path.join(ORACLE_DIR, "liboracle.so")
+_lib = None
+
+VALID, INVALID, SIG_DECODE, EMPTY_SIG, EMPTY_CLEAR, UNSUPPORTED, KEY_INVALID = range(7)
+
+
+def build() -> str:
+    subprocess.check_call(["make", "-s", "-C", ORACLE_DIR])
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(LIB_PATH)
+        _lib.orc_uniq_new.restype = ctypes.c_void_p
+        _lib.orc_uniq_size.restype = ctypes.c_uint64
+        _lib.orc_uniq_size.argtypes = [ctypes.c_void_p]
+        _lib.orc_uniq_free.argtypes = [ctypes.c_void_p]
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def sha256(b: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().orc_sha256(b, ctypes.c_size_t(len(b)), out)
+    return out.raw
+
+
+def sha512(b: bytes) -> bytes:
+    out = ctypes.create_string_buffer(64)
+    lib().orc_sha512(b, ctypes.c_size_t(len(b)), out)
+    return out.raw
+
+
+def do_verify(spki: bytes, sig: bytes, msg: bytes) -> int:
+    return lib().orc_do_verify(spki, ctypes.c_size_t(len(spki)), sig, ctypes.c_size_t(len(sig)), msg,
+                               ctypes.c_size_t(len(msg)))
+
+
+def ed25519_verify(a: bytes, sig: bytes, msg: bytes) -> int:
+    return lib().orc_ed25519_verify(a, sig, ctypes.c_size_t(len(sig)), msg, ctypes.c_size_t(len(msg)))
+
+
+def ed25519_decode_key(a: bytes):
+    out = ctypes.create_string_buffer(32)
+    r = lib().orc_ed25519_decode_key(a, out)
+    return out.raw if r == 0 else None
+
+
+def ed25519_slide(s: bytes):
+    r = (ctypes.c_int8 * 256)()
+    drops = lib().orc_ed25519_slide(s, r)
+    return list(r), drops
+
+
+def ed25519_scalarmult_base(s: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().orc_ed25519_scalarmult_base(s, out)
+    return out.raw
+
+
+def ed25519_double_scalarmult_plain(p: bytes, a: bytes, b: bytes):
+    out = ctypes.create_string_buffer(32)
+    r = lib().orc_ed25519_double_scalarmult_plain(p, a, b, out)
+    return out.raw if r == 0 else None
+
+
+def sc_reduce64(b: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().orc_ed25519_sc_reduce64(b, out)
+    return out.raw
+
+
+def der_decode(sig: bytes):
+    r = ctypes.create_string_buffer(32)
+    s = ctypes.create_string_buffer(32)
+    ro, so = ctypes.c_int(), ctypes.c_int()
+    rc = lib().orc_der_decode(sig, ctypes.c_size_t(len(sig)), r, s, ctypes.byref(ro), ctypes.byref(so))
+    if rc != 0:
+        return None
+    return r.raw, s.raw, ro.value, so.value
+
+
+def ecdsa_scalarmult_base(scheme: int, k: bytes):
+    out = ctypes.create_string_buffer(64)
+    r = lib().orc_ecdsa_scalarmult_base(scheme, k, out)
+    return out.raw if r == 0 else None
+
+
+def ecdsa_decode_key(scheme: int, pt: bytes):
+    out = ctypes.create_string_buffer(64)
+    r = lib().orc_ecdsa_decode_key(scheme, pt, ctypes.c_size_t(len(pt)), out)
+    return out.raw if r == 0 else None
+
+
+def verify_batch(b, threads: int = 1) -> np.ndarray:
+    st = np.zeros(b.n, dtype=np.uint8)
+    lib().orc_verify_batch(ctypes.c_uint64(b.n), _p(b.key_idx), _p(b.msg_idx), _p(b.sig_data), _p(b.sig_off),
+                           _p(b.sig_len), _p(b.key_data), _p(b.key_off), _p(b.key_len), _p(b.msg_data),
+                           _p(b.msg_off), _p(b.msg_len), _p(st), threads)
+    return st
+
+
+def compute_nonce(salt: bytes, g: int, i: int) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    lib().orc_compute_nonce(salt, ctypes.c_uint32(g), ctypes.c_uint32(i), out)
+    return out.raw
+
+
+def merkle_root(leaves) -> bytes:
+    buf = b"".join(leaves)
+    out = ctypes.create_string_buffer(32)
+    lib().orc_merkle_root(buf, ctypes.c_uint32(len(leaves)), out)
+    return out.raw
+
+
+def txid_batch(tb, threads: int = 1) -> np.ndarray:
+    ids = np.zeros(tb.ntx * 32, dtype=np.uint8)
+    lib().orc_txid_batch(ctypes.c_uint64(tb.ntx), _p(tb.salts), _p(tb.tx_comp_start), _p(tb.comp_group),
+                         _p(tb.comp_internal), _p(tb.data), _p(tb.comp_off), _p(tb.comp_len), _p(ids), threads)
+    return ids.reshape(tb.ntx, 32)
+
+
+class OrcConflict(ctypes.Structure):
+    _fields_ = [("tx", ctypes.c_uint64), ("input_index", ctypes.c_uint32), ("consumed_index", ctypes.c_uint32),
+                ("consuming_tx", ctypes.c_uint8 * 32), ("consuming_caller", ctypes.c_uint32),
+                ("pad", ctypes.c_uint32)]
+
+
+class Uniq:
+    """PersistentUniquenessProvider restatement with batch commit."""
+
+    def __init__(self, capacity: int = 1024):
+        self.h = ctypes.c_void_p(lib().orc_uniq_new(ctypes.c_uint64(capacity)))
+
+    def __del__(self):
+        if getattr(self, "h", None):
+            lib().orc_uniq_free(self.h)
+            self.h = None
+
+    def size(self) -> int:
+        return lib().orc_uniq_size(self.h)
+
+    def preload(self, refs36, tx32, idx, caller):
+        n = len(idx)
+        lib().orc_uniq_preload(self.h, ctypes.c_uint64(n), _p(refs36), _p(tx32), _p(idx), _p(caller))
+
+    def commit_batch(self, tx_ref_start, refs36, tx_ids, callers, cap=None):
+        ntx = len(tx_ref_start) - 1
+        st = np.zeros(ntx, dtype=np.uint8)
+        if cap is None:
+            cap = int(tx_ref_start[-1]) + 1
+        out = (OrcConflict * max(cap, 1))()
+        nout = ctypes.c_uint64()
+        lib().orc_uniq_commit_batch(self.h, ctypes.c_uint64(ntx), _p(tx_ref_start), _p(refs36), _p(tx_ids),
+                                    _p(callers), _p(st), out, ctypes.c_uint64(cap), ctypes.byref(nout))
+        recs = [(c.tx, c.input_index, c.consumed_index, bytes(c.consuming_tx), c.consuming_caller)
+                for c in out[:min(nout.value, cap)]]
+        return st, recs

@@ -1,0 +1,65 @@
+"""GPU parity: Ed25519 verification through the C-ABI vs the CPU restatement (oracle).
+
+Bit-exact on status bytes (CHIP_* codes) and the VALID bitmap, on seeded synthetic batches
+with every corruption class of cfg2 plus hand-built edge cases."""
+import hashlib
+
+import numpy as np
+import pytest
+
+import cordagen as G
+
+pytestmark = pytest.mark.gpu
+
+
+def bitmap_of(status):
+    n = len(status)
+    words = np.zeros((n + 63) // 64, dtype=np.uint64)
+    for i in np.nonzero(status == 0)[0]:
+        words[i // 64] |= np.uint64(1) << np.uint64(i % 64)
+    return words
+
+
+def test_ed25519_batch_matches_oracle(ctx, oracle):
+    b = G.ed25519_batch(3000, n_keys=64, corrupt=0.4, seed=11)
+    st, bm = ctx.verify_batch(b)
+    ref = oracle.verify_batch(b, threads=8)
+    bad = np.nonzero(st != ref)[0]
+    assert len(bad) == 0, [(int(i), int(b.kind[i]), int(st[i]), int(ref[i])) for i in bad[:20]]
+    assert np.array_equal(st, b.expected)
+    assert np.array_equal(bm, bitmap_of(ref))
+
+
+def test_ed25519_edge_cases(ctx, oracle):
+    import golden_cases
+    b = golden_cases.ed25519_edge_batch()
+    st, _ = ctx.verify_batch(b)
+    ref = oracle.verify_batch(b)
+    assert st.tolist() == ref.tolist()
+    assert st.tolist() == b.expected.tolist()
+
+
+@pytest.mark.parametrize("msg_len", [1, 55, 56, 63, 64, 111, 112, 127, 128, 200, 1000])
+def test_ed25519_message_lengths(ctx, oracle, msg_len):
+    # SHA-512 block boundaries (64 + |M| + 17 crossing 128-byte multiples)
+    seed = hashlib.sha256(b"len%d" % msg_len).digest()
+    a = G.ed25519_pub(seed)
+    msgs, sigs = [], []
+    for j in range(64):
+        m = hashlib.sha512(b"m%d" % j).digest() * (msg_len // 64 + 1)
+        m = m[:msg_len]
+        msgs.append(m)
+        s = bytearray(G.ed25519_sign(seed, m))
+        if j % 3 == 1:
+            s[5] ^= 4
+        sigs.append(bytes(s))
+    b = G.SigBatch()
+    b.key_data, b.key_off, b.key_len = G.pools_from_list([G.spki_ed25519(a)])
+    b.msg_data, b.msg_off, b.msg_len = G.pools_from_list(msgs)
+    b.sig_data, b.sig_off, b.sig_len = G.pools_from_list(sigs)
+    b.key_idx = np.zeros(64, dtype=np.uint32)
+    b.msg_idx = np.arange(64, dtype=np.uint32)
+    st, _ = ctx.verify_batch(b)
+    ref = oracle.verify_batch(b)
+    assert st.tolist() == ref.tolist()
+    assert st.tolist() == [1 if j % 3 == 1 else 0 for j in range(64)]

@@ -1,0 +1,462 @@
+"""Python front-end of tools/libcordagen.so (OpenSSL-backed synthetic workload generator).
+
+Used by bench.py (input generation, outside the timed region) and by the fixture scripts in
+tests/golden/.  Independent of oracle/: OpenSSL is the third party whose verdicts pin the
+oracle on canonical inputs.  Workload shapes follow SURVEY.md §8(d).
+"""
+from __future__ import annotations
+
+import ctypes
+import hashlib
+import os
+import struct
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "libcordagen.so")
+_lib = None
+
+SCHEME_K1, SCHEME_R1, SCHEME_ED25519 = 2, 3, 4
+
+# SubjectPublicKeyInfo prefixes (what PublicKey.encoded yields for the three schemes)
+SPKI_ED25519 = bytes.fromhex("302a300506032b6570032100")
+SPKI_R1 = bytes.fromhex("3059301306072a8648ce3d020106082a8648ce3d030107034200")
+SPKI_K1 = bytes.fromhex("3056301006072a8648ce3d020106052b8104000a034200")
+
+L_ED = 2**252 + 27742317777372353535851937790883648493
+N_R1 = 0xFFFFFFFF00000000FFFFFFFFFFFFFFFFBCE6FAADA7179E84F3B9CAC2FC632551
+N_K1 = 0xFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFFEBAAEDCE6AF48A03BBFD25E8CD0364141
+
+
+def build(force: bool = False) -> str:
+    src = os.path.join(_HERE, "cordagen.c")
+    if force or not os.path.exists(_LIB_PATH) or os.path.getmtime(_LIB_PATH) < os.path.getmtime(src):
+        subprocess.check_call(["gcc", "-O2", "-fPIC", "-shared", "-Wall", "-o", _LIB_PATH, src,
+                               "-lcrypto", "-lpthread"])
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        _lib = ctypes.CDLL(_LIB_PATH)
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def ed25519_pub(seed: bytes) -> bytes:
+    out = ctypes.create_string_buffer(32)
+    if lib().gen_ed25519_pub(seed, out) != 0:
+        raise RuntimeError("ed25519 keygen failed")
+    return out.raw
+
+
+def ed25519_sign(seed: bytes, msg: bytes) -> bytes:
+    out = ctypes.create_string_buffer(64)
+    if lib().gen_ed25519_sign(seed, msg, ctypes.c_size_t(len(msg)), out) != 0:
+        raise RuntimeError("ed25519 sign failed")
+    return out.raw
+
+
+def ec_pub(scheme: int, d: bytes) -> bytes:
+    out = ctypes.create_string_buffer(65)
+    if lib().gen_ec_pub(scheme, d, out) != 0:
+        raise RuntimeError("ec keygen failed")
+    return out.raw
+
+
+def ec_sign(scheme: int, d: bytes, k: bytes, msg: bytes):
+    der = ctypes.create_string_buffer(72)
+    r = ctypes.create_string_buffer(32)
+    s = ctypes.create_string_buffer(32)
+    n = lib().gen_ec_sign(scheme, d, k, msg, ctypes.c_size_t(len(msg)), der, r, s)
+    if n < 0:
+        raise RuntimeError("ec sign failed")
+    return der.raw[:n], r.raw, s.raw
+
+
+def ossl_verify(spki: bytes, sig: bytes, msg: bytes) -> int:
+    return lib().ossl_verify_spki(spki, ctypes.c_size_t(len(spki)), sig, ctypes.c_size_t(len(sig)),
+                                  msg, ctypes.c_size_t(len(msg)))
+
+
+def spki_ed25519(a: bytes) -> bytes:
+    return SPKI_ED25519 + a
+
+
+def spki_ec(scheme: int, pub65: bytes) -> bytes:
+    return (SPKI_R1 if scheme == SCHEME_R1 else SPKI_K1) + pub65
+
+
+def der_encode_int(v: int) -> bytes:
+    """Minimal DER INTEGER (two's complement) of a non-negative int."""
+    b = v.to_bytes(max(1, (v.bit_length() + 8) // 8), "big")
+    while len(b) > 1 and b[0] == 0 and not (b[1] & 0x80):
+        b = b[1:]
+    return b"\x02" + bytes([len(b)]) + b
+
+
+def der_sig(r: int, s: int) -> bytes:
+    body = der_encode_int(r) + der_encode_int(s)
+    return b"\x30" + bytes([len(body)]) + body
+
+
+class PRNG:
+    """Counter-mode SHA-256 stream: deterministic bytes from a seed."""
+
+    def __init__(self, seed: int, label: bytes = b""):
+        self.key = struct.pack("<Q", seed) + label
+        self.ctr = 0
+
+    def bytes(self, n: int) -> bytes:
+        out = bytearray()
+        while len(out) < n:
+            out += hashlib.sha256(self.key + struct.pack("<Q", self.ctr)).digest()
+            self.ctr += 1
+        return bytes(out[:n])
+
+    def np_bytes(self, n: int) -> np.ndarray:
+        # fast bulk stream: numpy generator seeded from the SHA-256 stream (deterministic)
+        seed = int.from_bytes(self.bytes(16), "little")
+        return np.random.Generator(np.random.PCG64(seed)).integers(0, 256, size=n, dtype=np.uint8)
+
+
+def key_seed(i: int) -> bytes:
+    return hashlib.sha256(b"cordahip-key" + struct.pack("<Q", i)).digest()
+
+
+class SigBatch:
+    """SoA signature batch in the chip_sig_batch layout of include/cordahip.h."""
+
+    def __init__(self):
+        self.key_idx = None   # u32[n]
+        self.msg_idx = None   # u32[n]
+        self.sig_data = None  # u8 pool
+        self.sig_off = None   # u64[n]
+        self.sig_len = None   # u32[n]
+        self.key_data = None  # u8 pool (SPKI)
+        self.key_off = None   # u64[k]
+        self.key_len = None   # u32[k]
+        self.msg_data = None
+        self.msg_off = None
+        self.msg_len = None
+        self.expected = None  # u8[n] intended outcome (generator's label, not a verdict)
+        self.kind = None      # u8[n] corruption class
+
+    @property
+    def n(self):
+        return len(self.key_idx)
+
+
+def pools_from_list(items, stride=None):
+    """Pack a list of bytes into (data u8, off u64, len u32)."""
+    lens = np.fromiter((len(x) for x in items), dtype=np.uint32, count=len(items))
+    off = np.zeros(len(items), dtype=np.uint64)
+    if len(items):
+        off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    data = np.frombuffer(b"".join(items), dtype=np.uint8).copy() if items else np.zeros(0, np.uint8)
+    return data, off, lens
+
+
+def signable_message(rng_bytes: bytes, tx_id: bytes, scheme_id: int, platform_version: int = 1) -> bytes:
+    """SignableData-shaped message (~200 B): Kryo header 'corda\\0\\0\\1' (SerializationScheme.kt:251),
+    class-name-like filler, txId and SignatureMetadata(platformVersion, schemeNumberID)."""
+    return (b"corda\x00\x00\x01" + rng_bytes[:150] + tx_id + struct.pack(">ii", platform_version, scheme_id))[:200]
+
+
+# Corruption classes of cfg2
+ED_KINDS = ["valid", "r_flip", "s_flip", "msg_flip", "wrong_key", "len63", "s_plus_l", "noncanon_r",
+            "small_order_forgery"]
+
+
+def ed25519_batch(n: int, n_keys: int = 4096, msg_len: int = 200, corrupt: float = 0.10,
+                  seed: int = 0x5EED0002, threads: int = 8) -> SigBatch:
+    """cfg2: n Ed25519 signatures, 2 per tx (one shared SignableData message per tx),
+    `corrupt` fraction spread evenly over the 8 corruption classes."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    seeds = b"".join(key_seed(i) for i in range(n_keys))
+    seeds_np = np.frombuffer(seeds, dtype=np.uint8).copy()
+    pubs = np.zeros(n_keys * 32, dtype=np.uint8)
+    if lib().gen_pubs_many(SCHEME_ED25519, ctypes.c_uint64(n_keys), _p(seeds_np), _p(pubs)) != 0:
+        raise RuntimeError("keygen failed")
+    # extra key: the identity point (small-order key, i2p accepts forged R = [S]B)
+    ident = bytes([1] + [0] * 31)
+    key_items = [spki_ed25519(pubs[32 * i:32 * i + 32].tobytes()) for i in range(n_keys)] + [spki_ed25519(ident)]
+    ntx = (n + 1) // 2
+    body = PRNG(seed, b"msg").np_bytes(ntx * msg_len).reshape(ntx, msg_len)
+    body[:, :8] = np.frombuffer(b"corda\x00\x00\x01", dtype=np.uint8)
+    msgs = body.reshape(-1)
+    msg_off = (np.arange(ntx, dtype=np.uint64) * msg_len)
+    msg_lenv = np.full(ntx, msg_len, dtype=np.uint32)
+    msg_idx = (np.arange(n, dtype=np.uint32) // 2)
+    key_of = rng.integers(0, n_keys, size=n, dtype=np.uint32)
+    # second signer of a tx differs from the first
+    same = (np.arange(n) % 2 == 1) & (key_of == np.roll(key_of, 1))
+    key_of[same] = (key_of[same] + 1) % n_keys
+    kind = np.zeros(n, dtype=np.uint8)
+    ncor = int(n * corrupt)
+    cidx = rng.choice(n, size=ncor, replace=False)
+    kind[cidx] = 1 + (np.arange(ncor) % 8)
+    # msg_flip: sign a flipped copy of the message; append those messages to the pool
+    mf = np.nonzero(kind == 3)[0]
+    sign_msg = msg_idx.copy()
+    if len(mf):
+        extra = msgs.reshape(ntx, msg_len)[msg_idx[mf]].copy()
+        bitpos = rng.integers(0, msg_len * 8, size=len(mf))
+        extra[np.arange(len(mf)), bitpos // 8] ^= (1 << (bitpos % 8)).astype(np.uint8)
+        sign_msg[mf] = ntx + np.arange(len(mf), dtype=np.uint32)
+        msgs_all = np.concatenate([msgs, extra.reshape(-1)])
+        msg_off_all = np.concatenate([msg_off, (ntx + np.arange(len(mf), dtype=np.uint64)) * msg_len])
+        msg_len_all = np.concatenate([msg_lenv, np.full(len(mf), msg_len, np.uint32)])
+    else:
+        msgs_all, msg_off_all, msg_len_all = msgs, msg_off, msg_lenv
+    sigs = np.zeros(n * 64, dtype=np.uint8)
+    sig_len = np.zeros(n, dtype=np.uint32)
+    err = lib().gen_sign_many(SCHEME_ED25519, ctypes.c_uint64(n), _p(seeds_np), _p(key_of), _p(msgs_all),
+                              _p(msg_off_all), _p(msg_len_all), _p(sign_msg), None, _p(sigs), _p(sig_len),
+                              ctypes.c_uint32(64), threads)
+    if err:
+        raise RuntimeError("signing failed")
+    sigs = sigs.reshape(n, 64)
+    expected = np.zeros(n, dtype=np.uint8)
+    key_idx = key_of.copy()
+    # apply corruptions
+    for i in np.nonzero(kind)[0]:
+        k = kind[i]
+        if k == 1:    # R bit flip
+            b = int(rng.integers(0, 256)); sigs[i, b // 8] ^= 1 << (b % 8); expected[i] = 1
+        elif k == 2:  # S bit flip (low 252 bits so S stays < 2^253: reference rejects by arithmetic)
+            b = int(rng.integers(0, 252)); sigs[i, 32 + b // 8] ^= 1 << (b % 8); expected[i] = 1
+        elif k == 3:  # signature over a different message
+            expected[i] = 1
+        elif k == 4:  # wrong key
+            key_idx[i] = (key_of[i] + 1 + int(rng.integers(0, n_keys - 1))) % n_keys; expected[i] = 1
+        elif k == 5:  # 63-byte signature -> "signature length is wrong"
+            sig_len[i] = 63; expected[i] = 2
+        elif k == 6:  # S + L: i2p 0.2.0 has no S < L check -> reference-VALID
+            S = int.from_bytes(sigs[i, 32:].tobytes(), "little") + L_ED
+            sigs[i, 32:] = np.frombuffer(S.to_bytes(32, "little"), dtype=np.uint8); expected[i] = 0
+        elif k == 7:  # non-canonical R: identity encoded as y = 1 + p, identity key, S = 0 -> INVALID
+            key_idx[i] = n_keys
+            sigs[i, :32] = np.frombuffer(bytes([0xee] + [0xff] * 30 + [0x7f]), dtype=np.uint8)
+            sigs[i, 32:] = 0; expected[i] = 1
+        elif k == 8:  # identity key, R = [S]B with S = clamp(SHA512(seed)) -> reference-VALID forgery
+            s_seed = key_seed(1_000_000 + i)
+            h = hashlib.sha512(s_seed).digest()
+            a = bytearray(h[:32]); a[0] &= 248; a[31] &= 127; a[31] |= 64
+            key_idx[i] = n_keys
+            sigs[i, :32] = np.frombuffer(ed25519_pub(s_seed), dtype=np.uint8)
+            sigs[i, 32:] = np.frombuffer(bytes(a), dtype=np.uint8); expected[i] = 0
+    b = SigBatch()
+    b.key_idx = key_idx.astype(np.uint32)
+    b.msg_idx = msg_idx.astype(np.uint32)
+    b.sig_data = sigs.reshape(-1)
+    b.sig_off = np.arange(n, dtype=np.uint64) * 64
+    b.sig_len = sig_len
+    b.key_data, b.key_off, b.key_len = pools_from_list(key_items)
+    b.msg_data, b.msg_off, b.msg_len = msgs_all, msg_off_all.astype(np.uint64), msg_len_all.astype(np.uint32)
+    b.expected = expected
+    b.kind = kind
+    return b
+
+
+EC_KINDS = ["valid", "r_flip", "s_flip", "msg_flip", "wrong_key", "wrong_curve", "r_zero", "s_ge_n",
+            "high_s", "der_long_len", "der_extra_elem", "der_trailing", "der_nonminimal_int"]
+
+
+def ecdsa_batch(n: int, n_keys: int = 4096, msg_len: int = 200, corrupt: float = 0.10,
+                seed: int = 0x5EED0003, threads: int = 8) -> SigBatch:
+    """cfg3: n ECDSA signatures, r1/k1 interleaved (even index r1, odd k1), one message per tx of 2."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    nk = n_keys
+    privs = {}
+    pubs = {}
+    key_items = []
+    for sch in (SCHEME_R1, SCHEME_K1):
+        order = N_R1 if sch == SCHEME_R1 else N_K1
+        ds = []
+        for i in range(nk):
+            d = int.from_bytes(hashlib.sha256(b"cordahip-eckey" + struct.pack("<QB", i, sch)).digest(), "big") % (order - 1) + 1
+            ds.append(d.to_bytes(32, "big"))
+        privs[sch] = np.frombuffer(b"".join(ds), dtype=np.uint8).copy()
+        pb = np.zeros(nk * 65, dtype=np.uint8)
+        if lib().gen_pubs_many(sch, ctypes.c_uint64(nk), _p(privs[sch]), _p(pb)) != 0:
+            raise RuntimeError("ec keygen failed")
+        pubs[sch] = pb
+        key_items += [spki_ec(sch, pb[65 * i:65 * i + 65].tobytes()) for i in range(nk)]
+    # key table: [0, nk) r1, [nk, 2nk) k1
+    ntx = (n + 1) // 2
+    body = PRNG(seed, b"msg").np_bytes(ntx * msg_len).reshape(ntx, msg_len)
+    body[:, :8] = np.frombuffer(b"corda\x00\x00\x01", dtype=np.uint8)
+    msgs = body.reshape(-1)
+    msg_off = np.arange(ntx, dtype=np.uint64) * msg_len
+    msg_lenv = np.full(ntx, msg_len, dtype=np.uint32)
+    msg_idx = (np.arange(n, dtype=np.uint32) // 2)
+    scheme = np.where(np.arange(n) % 2 == 0, SCHEME_R1, SCHEME_K1).astype(np.uint8)
+    key_local = rng.integers(0, nk, size=n, dtype=np.uint32)
+    kind = np.zeros(n, dtype=np.uint8)
+    ncor = int(n * corrupt)
+    cidx = rng.choice(n, size=ncor, replace=False)
+    kind[cidx] = 1 + (np.arange(ncor) % (len(EC_KINDS) - 1))
+    nonces = PRNG(seed, b"nonce").np_bytes(n * 32)
+    stride = 80
+    sigs = np.zeros(n * stride, dtype=np.uint8)
+    sig_len = np.zeros(n, dtype=np.uint32)
+    mf = np.nonzero(kind == 3)[0]
+    sign_msg = msg_idx.copy()
+    if len(mf):
+        extra = msgs.reshape(ntx, msg_len)[msg_idx[mf]].copy()
+        bitpos = rng.integers(0, msg_len * 8, size=len(mf))
+        extra[np.arange(len(mf)), bitpos // 8] ^= (1 << (bitpos % 8)).astype(np.uint8)
+        sign_msg[mf] = ntx + np.arange(len(mf), dtype=np.uint32)
+        msgs_all = np.concatenate([msgs, extra.reshape(-1)])
+        msg_off_all = np.concatenate([msg_off, (ntx + np.arange(len(mf), dtype=np.uint64)) * msg_len])
+        msg_len_all = np.concatenate([msg_lenv, np.full(len(mf), msg_len, np.uint32)])
+    else:
+        msgs_all, msg_off_all, msg_len_all = msgs, msg_off, msg_lenv
+    for sch in (SCHEME_R1, SCHEME_K1):
+        sel = np.nonzero(scheme == sch)[0]
+        m = len(sel)
+        out = np.zeros(m * stride, dtype=np.uint8)
+        ol = np.zeros(m, dtype=np.uint32)
+        ko = key_local[sel].copy()
+        so = sign_msg[sel].copy()
+        nn = np.frombuffer(nonces, dtype=np.uint8).reshape(n, 32)[sel].copy() if isinstance(nonces, bytes) \
+            else nonces.reshape(n, 32)[sel].copy()
+        err = lib().gen_sign_many(sch, ctypes.c_uint64(m), _p(privs[sch]), _p(ko), _p(msgs_all), _p(msg_off_all),
+                                  _p(msg_len_all), _p(so), _p(nn), _p(out), _p(ol), ctypes.c_uint32(stride), threads)
+        if err:
+            raise RuntimeError("ecdsa signing failed")
+        sigs.reshape(n, stride)[sel] = out.reshape(m, stride)
+        sig_len[sel] = ol
+    sigs = sigs.reshape(n, stride)
+    key_idx = np.where(scheme == SCHEME_R1, key_local, key_local + nk).astype(np.uint32)
+    expected = np.zeros(n, dtype=np.uint8)
+
+    def parse(i):
+        raw = sigs[i, :sig_len[i]].tobytes()
+        lr = raw[3]
+        r = int.from_bytes(raw[4:4 + lr], "big")
+        ls = raw[5 + lr]
+        s = int.from_bytes(raw[6 + lr:6 + lr + ls], "big")
+        return r, s
+
+    def put(i, der):
+        sigs[i, :] = 0
+        sigs[i, :len(der)] = np.frombuffer(der, dtype=np.uint8)
+        sig_len[i] = len(der)
+
+    for i in np.nonzero(kind)[0]:
+        k = int(kind[i])
+        order = N_R1 if scheme[i] == SCHEME_R1 else N_K1
+        r, s = parse(i)
+        if k == 1:
+            put(i, der_sig(r ^ (1 << int(rng.integers(0, 250))), s)); expected[i] = 1
+        elif k == 2:
+            put(i, der_sig(r, s ^ (1 << int(rng.integers(0, 250))))); expected[i] = 1
+        elif k == 3:
+            expected[i] = 1
+        elif k == 4:
+            key_idx[i] = (key_idx[i] // nk) * nk + (key_local[i] + 1) % nk; expected[i] = 1
+        elif k == 5:  # the same scalar's key on the other curve
+            key_idx[i] = (key_local[i] + nk) if scheme[i] == SCHEME_R1 else key_local[i]; expected[i] = 1
+        elif k == 6:
+            put(i, der_sig(0, s)); expected[i] = 1
+        elif k == 7:
+            put(i, der_sig(r, s + order)); expected[i] = 1
+        elif k == 8:  # high-s: (r, n - s) is also valid in BC (no low-s rule)
+            put(i, der_sig(r, order - s)); expected[i] = 0
+        elif k == 9:  # long-form length for a short length -> DER re-encode mismatch
+            der = der_sig(r, s)
+            put(i, b"\x30\x81" + der[1:2] + der[2:]); expected[i] = 2
+        elif k == 10:  # a third INTEGER element
+            body = der_encode_int(r) + der_encode_int(s) + der_encode_int(1)
+            put(i, b"\x30" + bytes([len(body)]) + body); expected[i] = 2
+        elif k == 11:  # trailing byte after the SEQUENCE
+            put(i, der_sig(r, s) + b"\x00"); expected[i] = 2
+        elif k == 12:  # non-minimal INTEGER padding (BC 1.57 keeps the bytes: unpinned, restated VALID)
+            rb = b"\x00" + r.to_bytes(33, "big")
+            body = b"\x02" + bytes([len(rb)]) + rb + der_encode_int(s)
+            put(i, b"\x30" + bytes([len(body)]) + body); expected[i] = 0
+    b = SigBatch()
+    b.key_idx = key_idx
+    b.msg_idx = msg_idx.astype(np.uint32)
+    b.sig_data = sigs.reshape(-1)
+    b.sig_off = np.arange(n, dtype=np.uint64) * stride
+    b.sig_len = sig_len
+    b.key_data, b.key_off, b.key_len = pools_from_list(key_items)
+    b.msg_data, b.msg_off, b.msg_len = msgs_all, msg_off_all.astype(np.uint64), msg_len_all.astype(np.uint32)
+    b.expected = expected
+    b.kind = kind
+    b.scheme = scheme
+    return b
+
+
+class TxBatch:
+    """SoA transaction batch in the chip_tx_batch layout (include/cordahip.h)."""
+    ntx = 0
+    salts = None          # u8[ntx*32]
+    tx_comp_start = None  # u64[ntx+1]
+    comp_group = None     # u32[ncomp]
+    comp_internal = None  # u32[ncomp]
+    data = None           # u8 pool
+    comp_off = None       # u64[ncomp]
+    comp_len = None       # u32[ncomp]
+
+
+# cfg4 profile: (group ordinal, [component sizes])
+CFG4_PROFILE = [(0, [96, 96]), (1, [640, 640]), (2, [320]), (3, [96]), (4, [384]), (5, [96])]
+
+
+def tx_batch(ntx: int, profile=CFG4_PROFILE, seed: int = 0x5EED0004, shuffle_groups: bool = False) -> TxBatch:
+    """ntx WireTransaction-shaped component sets with random non-zero 32-byte salts."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    sizes = [s for _, ss in profile for s in ss]
+    groups = [g for g, ss in profile for _ in ss]
+    internal = [i for _, ss in profile for i in range(len(ss))]
+    per_tx = len(sizes)
+    tb = TxBatch()
+    tb.ntx = ntx
+    salts = PRNG(seed, b"salt").np_bytes(ntx * 32).reshape(ntx, 32)
+    salts[:, 0] |= 1  # never all-zero (PrivacySalt invariant, Structures.kt:268-276)
+    tb.salts = salts.reshape(-1).copy()
+    tb.tx_comp_start = (np.arange(ntx + 1, dtype=np.uint64) * per_tx)
+    tb.comp_group = np.tile(np.array(groups, dtype=np.uint32), ntx)
+    tb.comp_internal = np.tile(np.array(internal, dtype=np.uint32), ntx)
+    lens = np.tile(np.array(sizes, dtype=np.uint32), ntx)
+    tb.comp_len = lens
+    off = np.zeros(len(lens), dtype=np.uint64)
+    off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    tb.comp_off = off
+    tb.data = PRNG(seed, b"data").np_bytes(int(lens.sum()))
+    return tb
+
+
+def tx_batch_from_lists(txs) -> TxBatch:
+    """txs: list of (salt32, [(group, [bytes, ...]), ...]) in component-group order."""
+    tb = TxBatch()
+    tb.ntx = len(txs)
+    salts, start, grp, internal, items = [], [0], [], [], []
+    for salt, groups in txs:
+        salts.append(salt)
+        for g, comps in groups:
+            for i, c in enumerate(comps):
+                grp.append(g)
+                internal.append(i)
+                items.append(c)
+        start.append(len(grp))
+    tb.salts = np.frombuffer(b"".join(salts), dtype=np.uint8).copy() if salts else np.zeros(0, np.uint8)
+    tb.tx_comp_start = np.array(start, dtype=np.uint64)
+    tb.comp_group = np.array(grp, dtype=np.uint32)
+    tb.comp_internal = np.array(internal, dtype=np.uint32)
+    tb.data, tb.comp_off, tb.comp_len = pools_from_list(items)
+    if len(tb.data) == 0:
+        tb.data = np.zeros(1, dtype=np.uint8)
+    return tb
