@@ -121,8 +121,10 @@ CHIP_DEV void st8(uint32_t* p, const uint32_t v[8]) {
     q[1] = make_uint4(v[4], v[5], v[6], v[7]);
 }
 
-// in-place Merkle root over slots[0..n) where slot j < n_real is real, [n_real, n) absent
-// (absent = allOnes when ones=true), positions >= n are the zeroHash padding.
+// in-place Merkle root over slots[0..n) (MerkleTree.getMerkleTree): leaves are padded with
+// zeroHash to m = 2^ceil(log2 n); a node whose whole subtree is padding equals Z_k (Z_0 = zeroHash,
+// Z_{k+1} = SHA256(Z_k || Z_k)) and is produced without re-hashing the padding.  For the top
+// tree (top=true) a leaf j < n whose group is absent is allOnesHash (WireTransaction.kt:146-155).
 CHIP_DEV void merkle_inplace(uint32_t root[8], uint32_t* slots, uint32_t n, uint32_t present_mask_lo,
                              uint32_t present_mask_hi, bool top) {
     if (n == 1) {
@@ -136,39 +138,45 @@ CHIP_DEV void merkle_inplace(uint32_t root[8], uint32_t* slots, uint32_t n, uint
     }
     uint32_t m = 1;
     while (m < n) m <<= 1;
-    uint32_t cnt = n;   // live nodes at this level (rest are zeroHash)
+    uint32_t cnt = n;   // nodes at this level with at least one real leaf below them
+    uint32_t z[8];      // Z_k for the current level
+#pragma unroll
+    for (int q = 0; q < 8; q++) z[q] = 0;
     bool first = true;
     while (m > 1) {
         const uint32_t half = m >> 1;
-        for (uint32_t j = 0; j < half; j++) {
+        const uint32_t live = (cnt + 1) >> 1;
+        for (uint32_t j = 0; j < live; j++) {
             uint32_t l[8], r[8], h[8];
             const uint32_t a = 2 * j, b = 2 * j + 1;
-            if (a < cnt) {
-                const bool pres = !(top && first) || ((a < 32 ? (present_mask_lo >> a) : (present_mask_hi >> (a - 32))) & 1u);
-                if (pres) ld8(l, slots + 8 * a);
-                else {
+            // a < cnt always
+            const bool pa = !(top && first) || ((a < 32 ? (present_mask_lo >> a) : (present_mask_hi >> (a - 32))) & 1u);
+            if (pa) ld8(l, slots + 8 * a);
+            else {
 #pragma unroll
-                    for (int q = 0; q < 8; q++) l[q] = 0xffffffffu;
-                }
-            } else {
-#pragma unroll
-                for (int q = 0; q < 8; q++) l[q] = 0;
+                for (int q = 0; q < 8; q++) l[q] = 0xffffffffu;
             }
             if (b < cnt) {
-                const bool pres = !(top && first) || ((b < 32 ? (present_mask_lo >> b) : (present_mask_hi >> (b - 32))) & 1u);
-                if (pres) ld8(r, slots + 8 * b);
+                const bool pb = !(top && first) || ((b < 32 ? (present_mask_lo >> b) : (present_mask_hi >> (b - 32))) & 1u);
+                if (pb) ld8(r, slots + 8 * b);
                 else {
 #pragma unroll
                     for (int q = 0; q < 8; q++) r[q] = 0xffffffffu;
                 }
             } else {
 #pragma unroll
-                for (int q = 0; q < 8; q++) r[q] = 0;
+                for (int q = 0; q < 8; q++) r[q] = z[q];
             }
             hash_concat(h, l, r);
             st8(slots + 8 * j, h);
         }
-        cnt = (cnt + 1) >> 1;
+        if (live < half) {   // next level's padding value
+            uint32_t h[8];
+            hash_concat(h, z, z);
+#pragma unroll
+            for (int q = 0; q < 8; q++) z[q] = h[q];
+        }
+        cnt = live;
         m = half;
         first = false;
     }
