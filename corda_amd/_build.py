@@ -11,7 +11,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libcordahip.so")
 SOURCES = ["runtime.hip", "ed25519.hip", "ecdsa.hip", "txid.hip", "uniq.hip"]
 HEADERS = ["common.hpp", "fe25519_dev.hpp", "scalar_dev.hpp", "sha2_dev.hpp", "runtime.hpp", "curve_consts.hpp",
-           "p256_dev.hpp"]
+           "ec_dev.hpp"]
 GEN = os.path.join(ROOT, "tools", "gen_constants.py")
 CONSTS = os.path.join(CSRC, "curve_consts.hpp")
 

@@ -49,6 +49,44 @@ struct chip_ctx {
     hipEvent_t ev0 = nullptr, ev1 = nullptr, tev0 = nullptr, tev1 = nullptr;
     bool ev_pending = false, tev_pending = false;
     chip_stats stats{};
+    // per-kernel timing: a ring of event pairs recorded on the launch stream
+    struct KEv {
+        hipEvent_t a = nullptr, b = nullptr;
+        int kind = -1;
+        bool pending = false;
+    };
+    static const int KRING = 64;
+    KEv kring[KRING];
+    int knext = 0;
+    void kresolve(KEv& e) {
+        if (!e.pending) return;
+        float ms = 0;
+        if (hipEventSynchronize(e.b) == hipSuccess && hipEventElapsedTime(&ms, e.a, e.b) == hipSuccess) {
+            stats.kernel_ms_total[e.kind] += ms;
+            stats.kernel_launches[e.kind]++;
+        }
+        e.pending = false;
+    }
+    int kbegin(int kind, hipStream_t st) {
+        const int i = knext;
+        knext = (knext + 1) % KRING;
+        KEv& e = kring[i];
+        kresolve(e);
+        if (!e.a) {
+            hipEventCreate(&e.a);
+            hipEventCreate(&e.b);
+        }
+        e.kind = kind;
+        hipEventRecord(e.a, st);
+        return i;
+    }
+    void kend(int i, hipStream_t st) {
+        hipEventRecord(kring[i].b, st);
+        kring[i].pending = true;
+    }
+    void kresolve_all() {
+        for (int i = 0; i < KRING; i++) kresolve(kring[i]);
+    }
 };
 
 static int fail(chip_ctx* c, int code, const std::string& msg) {
@@ -166,6 +204,10 @@ void chip_shutdown(chip_ctx* c) {
                       &c->t_start, &c->t_group, &c->t_internal, &c->t_data, &c->t_off, &c->t_len, &c->t_ids,
                       &c->t_scratch};
     for (DevBuf* b : bufs) b->release();
+    for (int i = 0; i < chip_ctx::KRING; i++) {
+        if (c->kring[i].a) hipEventDestroy(c->kring[i].a);
+        if (c->kring[i].b) hipEventDestroy(c->kring[i].b);
+    }
     hipEventDestroy(c->ev0);
     hipEventDestroy(c->ev1);
     hipEventDestroy(c->tev0);
@@ -190,21 +232,29 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     HIPCHK(c, hipMemsetAsync(c->counts.p, 0, 64, st));
     if (nk) HIPCHK(c, hipMemsetAsync(c->meta.p, 0, nk * sizeof(KeyMeta), st));
     KeyMeta* meta = c->meta.as<KeyMeta>();
+    int ke = c->kbegin(CHIP_K_KEYPREP, st);
     launch_ed25519_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->abytes.as<uint32_t>(),
                             c->edtab.as<uint32_t>());
     launch_ecdsa_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->ectab.as<uint32_t>());
+    c->kend(ke, st);
     if (n) {
         const uint32_t blocks = (uint32_t)((n + 255) / 256);
         uint32_t* lists = c->lists.as<uint32_t>();
         uint32_t* counts = c->counts.as<uint32_t>();
         hipLaunchKernelGGL(k_classify, dim3(blocks), dim3(256), 0, st, n, b->key_idx, b->msg_idx, b->sig_len, b->msg_len,
                            nk, b->n_msgs, meta, status, lists, counts);
+        ke = c->kbegin(CHIP_K_ED25519, st);
         launch_ed25519_verify(st, n, lists + (uint64_t)LIST_ED25519 * n, counts + LIST_ED25519, b,
                               c->abytes.as<uint32_t>(), c->edtab.as<uint32_t>(), status);
+        c->kend(ke, st);
+        ke = c->kbegin(CHIP_K_ECDSA_R1, st);
         launch_ecdsa_verify(st, CHIP_SCHEME_R1, n, lists + (uint64_t)LIST_R1 * n, counts + LIST_R1, b,
                             c->ectab.as<uint32_t>(), status);
+        c->kend(ke, st);
+        ke = c->kbegin(CHIP_K_ECDSA_K1, st);
         launch_ecdsa_verify(st, CHIP_SCHEME_K1, n, lists + (uint64_t)LIST_K1 * n, counts + LIST_K1, b,
                             c->ectab.as<uint32_t>(), status);
+        c->kend(ke, st);
         if (bitmap) hipLaunchKernelGGL(k_bitmap, dim3(blocks), dim3(256), 0, st, n, status, bitmap);
     }
     HIPCHK(c, hipGetLastError());
@@ -289,7 +339,16 @@ int chip_get_stats(const chip_ctx* cc, chip_stats* out) {
         c->stats.last_txid_kernel_ms = ms;
         c->tev_pending = false;
     }
+    c->kresolve_all();
     *out = c->stats;
+    return CHIP_OK;
+}
+
+int chip_reset_stats(chip_ctx* c) {
+    if (!c) return CHIP_E_ARG;
+    std::lock_guard<std::mutex> g(c->mu);
+    c->kresolve_all();
+    c->stats = chip_stats{};
     return CHIP_OK;
 }
 
@@ -303,7 +362,9 @@ int chip_txid_batch_device(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids, vo
     const uint64_t scratch_words = b->ntx * 64 * 8 + b->ncomp * 8 + 64;
     HIPCHK(c, c->t_scratch.ensure(scratch_words * 4));
     HIPCHK(c, hipEventRecord(c->tev0, st));
+    const int ke = c->kbegin(CHIP_K_TXID, st);
     launch_txid(st, b, ids, c->t_scratch.as<uint32_t>(), scratch_words);
+    c->kend(ke, st);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->tev1, st));
     c->tev_pending = true;

@@ -98,13 +98,47 @@ CHIP_DEV void sha512_compress(uint64_t h[8], uint64_t w[16]) {
     h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
 }
 
-// Byte j of a virtual message  prefix(len pl, held in big-endian u32 words) || pool bytes (len ml)
-// followed by SHA padding; total padded length is a multiple of `blk` bytes.
-// Used to assemble block words without materialising the message.
-CHIP_DEV uint32_t msg_byte(uint64_t j, const uint32_t* prefix_be, uint32_t pl, const uint8_t* m, uint32_t ml) {
-    if (j < pl) return (prefix_be[j >> 2] >> (24 - 8 * (j & 3))) & 0xffu;
-    j -= pl;
-    if (j < ml) return m[j];
-    if (j == ml) return 0x80u;
-    return 0u;
+// big-endian word at byte offset q of a pool byte string p[0..len) followed by the SHA-2 padding
+// byte 0x80 and zeros (q may be negative: those bytes read as 0).  Aligned dword loads when the
+// word lies inside the string.
+CHIP_DEV uint32_t comp_word(const uint8_t* p, uint32_t len, int64_t q) {
+    if (q >= 0 && q + 4 <= (int64_t)len) {
+        const uintptr_t a = (uintptr_t)(p + q);
+        const uint32_t sh = (uint32_t)(a & 3u);
+        const uint32_t* ap = (const uint32_t*)(a & ~(uintptr_t)3);
+        uint32_t lo = ap[0];
+        uint32_t v = lo;
+        if (sh) {
+            const uint32_t hi = ap[1];   // in bounds: q + 4 <= len and the word straddles
+            v = __builtin_amdgcn_alignbyte(hi, lo, sh);
+        }
+        return __builtin_bswap32(v);
+    }
+    uint32_t v = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const int64_t j = q + k;
+        uint32_t by = 0;
+        if (j >= 0 && j < (int64_t)len) by = p[j];
+        else if (j == (int64_t)len) by = 0x80u;
+        v = (v << 8) | by;
+    }
+    return v;
+}
+
+// SHA-256 of pool bytes p[0..len): state words in H (big-endian digest words)
+CHIP_DEV void sha256_bytes(uint32_t H[8], const uint8_t* p, uint32_t len) {
+    uint32_t w[16];
+    sha256_init(H);
+    const uint64_t total = len;
+    const uint32_t nblocks = (uint32_t)((total + 9 + 63) / 64);
+    for (uint32_t b = 0; b < nblocks; b++) {
+#pragma unroll
+        for (int j = 0; j < 16; j++) w[j] = comp_word(p, len, (int64_t)b * 64 + 4 * j);
+        if (b == nblocks - 1) {
+            w[14] = (uint32_t)((total * 8) >> 32);
+            w[15] = (uint32_t)(total * 8);
+        }
+        sha256_compress(H, w);
+    }
 }

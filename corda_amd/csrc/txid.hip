@@ -14,33 +14,6 @@
 
 #define TX_MAX_GROUPS 64
 
-// big-endian word of a component byte stream (bytes beyond len follow SHA-256 padding of a
-// message whose total length is `total` and which is `pre` bytes longer before the component)
-CHIP_DEV uint32_t comp_word(const uint8_t* p, uint32_t len, int64_t q) {
-    if (q >= 0 && q + 4 <= (int64_t)len) {
-        const uintptr_t a = (uintptr_t)(p + q);
-        const uint32_t sh = (uint32_t)(a & 3u);
-        const uint32_t* ap = (const uint32_t*)(a & ~(uintptr_t)3);
-        uint32_t lo = ap[0];
-        uint32_t v = lo;
-        if (sh) {
-            const uint32_t hi = ap[1];   // in bounds: q + 4 <= len and the word straddles
-            v = __builtin_amdgcn_alignbyte(hi, lo, sh);
-        }
-        return __builtin_bswap32(v);
-    }
-    uint32_t v = 0;
-#pragma unroll
-    for (int k = 0; k < 4; k++) {
-        const int64_t j = q + k;
-        uint32_t by = 0;
-        if (j >= 0 && j < (int64_t)len) by = p[j];
-        else if (j == (int64_t)len) by = 0x80u;
-        v = (v << 8) | by;
-    }
-    return v;
-}
-
 // SHA256(SHA256(prefix32 || bytes[0:len]))  (componentHash with prefix = nonce)
 CHIP_DEV void sha256d_prefixed(uint32_t out[8], const uint32_t pre[8], const uint8_t* p, uint32_t len) {
     uint32_t H[8], w[16];

@@ -33,7 +33,7 @@ SCHEME_K1, SCHEME_R1, SCHEME_ED25519 = 2, 3, 4
 EXPORTS = ["chip_abi_version", "chip_device_count", "chip_init", "chip_shutdown", "chip_last_error",
            "chip_verify_batch", "chip_verify_batch_device", "chip_txid_batch", "chip_txid_batch_device",
            "chip_uniq_open", "chip_uniq_close", "chip_uniq_size", "chip_uniq_rebuild", "chip_uniq_commit_batch",
-           "chip_get_stats"]
+           "chip_get_stats", "chip_reset_stats"]
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
 u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -66,10 +66,14 @@ class ChipConflict(ctypes.Structure):
                 ("pad", ctypes.c_uint32)]
 
 
+K_ED25519, K_ECDSA_R1, K_ECDSA_K1, K_TXID, K_KEYPREP, K_UNIQ, N_KERNELS = range(7)
+
+
 class ChipStats(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_uint64), ("sigs", ctypes.c_uint64), ("keys_prepared", ctypes.c_uint64),
                 ("status_count", ctypes.c_uint64 * 8), ("txids", ctypes.c_uint64), ("uniq_commits", ctypes.c_uint64),
-                ("last_verify_kernel_ms", ctypes.c_double), ("last_txid_kernel_ms", ctypes.c_double)]
+                ("last_verify_kernel_ms", ctypes.c_double), ("last_txid_kernel_ms", ctypes.c_double),
+                ("kernel_ms_total", ctypes.c_double * N_KERNELS), ("kernel_launches", ctypes.c_uint64 * N_KERNELS)]
 
 
 def lib_path() -> str:
@@ -108,6 +112,7 @@ def load(build_if_missing: bool = False):
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
     lib.chip_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipStats)]
+    lib.chip_reset_stats.argtypes = [ctypes.c_void_p]
     _lib = lib
     return lib
 
@@ -215,6 +220,9 @@ class Context:
         st = ChipStats()
         self._check(self.lib.chip_get_stats(self.h, ctypes.byref(st)))
         return st
+
+    def reset_stats(self):
+        self._check(self.lib.chip_reset_stats(self.h))
 
     # ---- uniqueness ----
     def uniq_open(self, capacity: int):

@@ -175,14 +175,22 @@ int chip_uniq_commit_batch(chip_uniq* u, uint64_t ntx, const uint64_t* tx_ref_st
 
 /* ---------------------------------------------------------------------------------------
  * Counters (observability; OutOfProcessTransactionVerifierService.kt:35-46 analogue). */
+enum chip_kernel { CHIP_K_ED25519 = 0, CHIP_K_ECDSA_R1 = 1, CHIP_K_ECDSA_K1 = 2, CHIP_K_TXID = 3,
+                   CHIP_K_KEYPREP = 4, CHIP_K_UNIQ = 5, CHIP_N_KERNELS = 6 };
 typedef struct {
     uint64_t batches, sigs, keys_prepared;
     uint64_t status_count[8];
     uint64_t txids, uniq_commits;
-    double last_verify_kernel_ms;  /* device time of the last verify batch (HIP events) */
+    double last_verify_kernel_ms;  /* device time of the last verify pipeline (HIP events) */
     double last_txid_kernel_ms;
+    /* per-kernel device time (HIP events recorded on the launch stream around each launch),
+     * accumulated over every launch since chip_init / chip_reset_stats */
+    double kernel_ms_total[CHIP_N_KERNELS];
+    uint64_t kernel_launches[CHIP_N_KERNELS];
 } chip_stats;
+/* Resolves pending timing events (waits for them) and copies the counters. */
 int chip_get_stats(const chip_ctx* ctx, chip_stats* out);
+int chip_reset_stats(chip_ctx* ctx);
 
 #ifdef __cplusplus
 }

@@ -278,8 +278,162 @@ def txid_cases():
     return cases
 
 
+# ---------------- ECDSA (BC 1.57 SHA256withECDSA) ----------------
+EC = {
+    G.SCHEME_R1: dict(p=0xFFFFFFFF00000001000000000000000000000000FFFFFFFFFFFFFFFFFFFFFFFF, n=G.N_R1,
+                      a=-3, b=0x5AC635D8AA3A93E7B3EBBD55769886BC651D06B0CC53B0F63BCE3C3E27D2604B,
+                      g=(0x6B17D1F2E12C4247F8BCE6E563A440F277037D812DEB33A0F4A13945D898C296,
+                         0x4FE342E2FE1A7F9B8EE7EB4A7C0F9E162BCE33576B315ECECBB6406837BF51F5)),
+    G.SCHEME_K1: dict(p=2**256 - 2**32 - 977, n=G.N_K1, a=0, b=7,
+                      g=(0x79BE667EF9DCBBAC55A06295CE870B07029BFCDB2DCE28D959F2815B16F81798,
+                         0x483ADA7726A3C4655DA4FBFC0E1108A8FD17B448A68554199C47D08FFB10D4B8)),
+}
+
+
+def ec_add(c, P1, P2):
+    p = c["p"]
+    if P1 is None:
+        return P2
+    if P2 is None:
+        return P1
+    (x1, y1), (x2, y2) = P1, P2
+    if x1 == x2:
+        if (y1 + y2) % p == 0:
+            return None
+        lam = (3 * x1 * x1 + c["a"]) * pow(2 * y1, -1, p) % p
+    else:
+        lam = (y2 - y1) * pow(x2 - x1, -1, p) % p
+    x3 = (lam * lam - x1 - x2) % p
+    return (x3, (lam * (x1 - x3) - y1) % p)
+
+
+def ec_mul(c, k, P):
+    R = None
+    for bit in bin(k)[2:]:
+        R = ec_add(c, R, R)
+        if bit == "1":
+            R = ec_add(c, R, P)
+    return R
+
+
+def ec_spki(scheme, P, compressed=False):
+    if compressed:
+        pt = bytes([2 + (P[1] & 1)]) + P[0].to_bytes(32, "big")
+        pfx = bytes.fromhex("3039301306072a8648ce3d020106082a8648ce3d030107032200") if scheme == G.SCHEME_R1 else \
+            bytes.fromhex("3036301006072a8648ce3d020106052b8104000a032200")
+        return pfx + pt
+    return G.spki_ec(scheme, b"\x04" + P[0].to_bytes(32, "big") + P[1].to_bytes(32, "big"))
+
+
+def ec_case(label, spki, sig, msg, expected, source, unpinned=False):
+    return dict(label=label, spki=spki.hex(), sig=sig.hex(), msg=msg.hex(), expected=expected, source=source,
+                unpinned=unpinned, openssl=G.ossl_verify(spki, sig, msg) if sig and msg else None)
+
+
+def ecdsa_cases():
+    cases = []
+    msg = b"corda\x00\x00\x01" + hashlib.sha256(b"golden-ec").digest() * 6
+    for scheme, name in ((G.SCHEME_R1, "r1"), (G.SCHEME_K1, "k1")):
+        c = EC[scheme]
+        n = c["n"]
+        d = int.from_bytes(hashlib.sha256(b"ec-golden-key" + name.encode()).digest(), "big") % (n - 1) + 1
+        pub = G.ec_pub(scheme, d.to_bytes(32, "big"))
+        P = (int.from_bytes(pub[1:33], "big"), int.from_bytes(pub[33:], "big"))
+        assert ec_mul(c, d, c["g"]) == P
+        spki = G.spki_ec(scheme, pub)
+        k = hashlib.sha256(b"nonce" + name.encode()).digest()
+        der, rb, sb = G.ec_sign(scheme, d.to_bytes(32, "big"), k, msg)
+        r, s_ = int.from_bytes(rb, "big"), int.from_bytes(sb, "big")
+        src = "CryptoUtilsTest.kt:123-286 (%s full process)" % name
+        cases.append(ec_case("%s valid" % name, spki, der, msg, 0, src))
+        cases.append(ec_case("%s valid, compressed key" % name, ec_spki(scheme, P, True), der, msg, 0,
+                             "BC decodePoint compressed"))
+        cases.append(ec_case("%s 100 zero-byte message" % name, spki,
+                             G.ec_sign(scheme, d.to_bytes(32, "big"), k, bytes(100))[0], bytes(100), 0, src))
+        cases.append(ec_case("%s message changed" % name, spki, der, msg + b"x", 1, src))
+        cases.append(ec_case("%s r+1" % name, spki, G.der_sig(r + 1 if r + 1 < n else r - 1, s_), msg, 1, src))
+        cases.append(ec_case("%s high-s (n - s) is valid in BC" % name, spki, G.der_sig(r, n - s_), msg, 0,
+                             "ECDSASigner.verifySignature has no low-s rule"))
+        cases.append(ec_case("%s r = 0" % name, spki, G.der_sig(0, s_), msg, 1, "r in [1, n-1]"))
+        cases.append(ec_case("%s s = 0" % name, spki, G.der_sig(r, 0), msg, 1, "s in [1, n-1]"))
+        cases.append(ec_case("%s r = n" % name, spki, G.der_sig(n, s_), msg, 1, "r in [1, n-1]"))
+        cases.append(ec_case("%s s = n + s" % name, spki, G.der_sig(r, n + s_), msg, 1, "s in [1, n-1]"))
+        rneg = b"\x02\x20" + (r | (1 << 255)).to_bytes(32, "big")   # top bit set, no 00 pad: negative INTEGER
+        body = rneg + G.der_encode_int(s_)
+        cases.append(ec_case("%s negative r (two's complement)" % name, spki, b"\x30" + bytes([len(body)]) + body, msg,
+                             1, "BigInteger negative -> r < 1"))
+        big = b"\x02\x21\x01" + r.to_bytes(32, "big")   # 2^256 + r
+        body = big + G.der_encode_int(s_)
+        cases.append(ec_case("%s r >= 2^256" % name, spki, b"\x30" + bytes([len(body)]) + body, msg, 1, "r >= n"))
+        # DER structure (StdDSAEncoder.decode + re-encode equality) -> SignatureException
+        cases.append(ec_case("%s DER long-form length" % name, spki, b"\x30\x81" + der[1:2] + der[2:], msg, 2,
+                             "DER re-encode mismatch (BC 1.56+)"))
+        cases.append(ec_case("%s DER indefinite length" % name, spki, b"\x30\x80" + der[2:] + b"\x00\x00", msg, 2,
+                             "BER indefinite length"))
+        body = G.der_encode_int(r) + G.der_encode_int(s_) + G.der_encode_int(5)
+        cases.append(ec_case("%s DER three elements" % name, spki, b"\x30" + bytes([len(body)]) + body, msg, 2,
+                             "s.size() != 2"))
+        body = G.der_encode_int(r)
+        cases.append(ec_case("%s DER one element" % name, spki, b"\x30" + bytes([len(body)]) + body, msg, 2,
+                             "s.size() != 2"))
+        cases.append(ec_case("%s DER trailing byte" % name, spki, der + b"\x00", msg, 2, "re-encode mismatch"))
+        cases.append(ec_case("%s DER truncated" % name, spki, der[:-1], msg, 2, "parse error"))
+        cases.append(ec_case("%s DER outer tag SET" % name, spki, b"\x31" + der[1:], msg, 2, "not a SEQUENCE"))
+        cases.append(ec_case("%s DER BIT STRING element" % name, spki, der[:2] + b"\x03" + der[3:], msg, 2,
+                             "ASN1Integer.getInstance fails"))
+        body = b"\x02\x00" + G.der_encode_int(s_)
+        cases.append(ec_case("%s DER empty INTEGER" % name, spki, b"\x30" + bytes([len(body)]) + body, msg, 2,
+                             "BigInteger of zero length"))
+        rpad = b"\x00\x00" + r.to_bytes(32, "big")
+        body = b"\x02" + bytes([len(rpad)]) + rpad + G.der_encode_int(s_)
+        cases.append(ec_case("%s DER non-minimal INTEGER padding" % name, spki, b"\x30" + bytes([len(body)]) + body,
+                             msg, 0, "BC 1.57 keeps INTEGER bytes (unpinned: no reference test)", unpinned=True))
+        cases.append(ec_case("%s raw r||s (not DER)" % name, spki, rb + sb, msg, 2, "not DER"))
+        cases.append(ec_case("%s empty signature" % name, spki, b"", msg, 3, "Crypto.kt:528"))
+        cases.append(ec_case("%s empty clear data" % name, spki, der, b"", 4, "Crypto.kt:529"))
+        # keys
+        bad = b"\x04" + P[0].to_bytes(32, "big") + ((P[1] + 1) % c["p"]).to_bytes(32, "big")
+        cases.append(ec_case("%s key not on curve" % name, G.spki_ec(scheme, bad), der, msg, 6, "ECPoint.isValid"))
+        bad = b"\x04" + (P[0] + c["p"]).to_bytes(33, "big")[1:] + P[1].to_bytes(32, "big") \
+            if P[0] + c["p"] < 2**256 else b"\x04" + bytes([0xff] * 32) + P[1].to_bytes(32, "big")
+        cases.append(ec_case("%s key x >= p" % name, G.spki_ec(scheme, bad), der, msg, 6, "fromBigInteger range"))
+        cases.append(ec_case("%s key infinity encoding" % name, G.spki_ec(scheme, b"\x00" * 65), der, msg, 6,
+                             "point at infinity"))
+        # generator and -generator as keys (exceptional additions inside the joint mult)
+        for dd, lab in ((1, "key = G"), (n - 1, "key = -G"), (2, "key = 2G")):
+            pk = ec_mul(c, dd, c["g"])
+            kk = hashlib.sha256(b"nk" + lab.encode() + name.encode()).digest()
+            dder = G.ec_sign(scheme, dd.to_bytes(32, "big"), kk, msg)[0]
+            cases.append(ec_case("%s %s" % (name, lab), ec_spki(scheme, pk), dder, msg, 0, "exceptional point adds"))
+        # x(R) in [n, p): accept through the r + n branch (Q constructed from a chosen R)
+        x = n + 1
+        while True:
+            rhs = (x ** 3 + c["a"] * x + c["b"]) % c["p"]
+            y = pow(rhs, (c["p"] + 1) // 4, c["p"])
+            if y * y % c["p"] == rhs:
+                break
+            x += 1
+        Rpt = (x, y)
+        rr = x % n
+        ss = int.from_bytes(hashlib.sha256(b"s" + name.encode()).digest(), "big") % n
+        e = int.from_bytes(hashlib.sha256(msg).digest(), "big") % n
+        w = pow(ss, -1, n)
+        u1, u2 = e * w % n, rr * w % n
+        # Q = (R - u1 G) * u2^-1
+        negu1G = ec_mul(c, (n - u1) % n, c["g"])
+        Qpt = ec_mul(c, pow(u2, -1, n), ec_add(c, Rpt, negu1G))
+        cases.append(ec_case("%s x(R) >= n accepted via r + n" % name, ec_spki(scheme, Qpt), G.der_sig(rr, ss), msg, 0,
+                             "ECDSASigner r*Z^2 loop at r, r+n"))
+    # wrong-curve key: r1 signature checked against the k1 key with the same scalar
+    return cases
+
+
 def main():
     G.build()
+    ec = ecdsa_cases()
+    with open(os.path.join(HERE, "ecdsa_cases.json"), "w") as f:
+        json.dump(ec, f, indent=1)
+    print("ecdsa cases:", len(ec))
     ed = ed25519_cases()
     with open(os.path.join(HERE, "ed25519_cases.json"), "w") as f:
         json.dump(ed, f, indent=1)

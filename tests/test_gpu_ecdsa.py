@@ -1,0 +1,36 @@
+"""GPU parity: ECDSA secp256r1 / secp256k1 verification (K2) vs the oracle and the committed
+golden vectors (BC 1.57 DER rules, range checks, high-s, r + n branch, exceptional points)."""
+import numpy as np
+import pytest
+
+import cordagen as G
+import golden_cases
+
+pytestmark = pytest.mark.gpu
+
+
+def test_ecdsa_golden(ctx, oracle):
+    b = golden_cases.ecdsa_edge_batch()
+    st, _ = ctx.verify_batch(b)
+    labels = [c["label"] for c in golden_cases.ecdsa_cases()]
+    bad = [(labels[i], int(st[i]), int(b.expected[i])) for i in range(len(st)) if st[i] != b.expected[i]]
+    assert not bad, bad
+    assert np.array_equal(st, oracle.verify_batch(b))
+
+
+def test_ecdsa_mixed_batch_matches_oracle(ctx, oracle):
+    b = G.ecdsa_batch(4000, n_keys=64, corrupt=0.4, seed=17)
+    st, bm = ctx.verify_batch(b)
+    ref = oracle.verify_batch(b, threads=8)
+    bad = np.nonzero(st != ref)[0]
+    assert len(bad) == 0, [(int(i), int(b.kind[i]), int(b.scheme[i]), int(st[i]), int(ref[i])) for i in bad[:20]]
+    assert np.array_equal(st, b.expected)
+
+
+def test_mixed_ed25519_and_ecdsa_one_batch(ctx, oracle):
+    e = golden_cases.ed25519_cases()
+    c = golden_cases.ecdsa_cases()
+    b = golden_cases.sig_batch_from_cases(e + c)
+    st, _ = ctx.verify_batch(b)
+    assert np.array_equal(st, b.expected)
+    assert np.array_equal(st, oracle.verify_batch(b))

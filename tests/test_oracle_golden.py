@@ -113,3 +113,19 @@ def test_compute_nonce_layout():
     salt = bytes(range(32))
     exp = hashlib.sha256(hashlib.sha256(salt + (3).to_bytes(4, "big") + (7).to_bytes(4, "big")).digest()).digest()
     assert O.compute_nonce(salt, 3, 7) == exp
+
+
+@pytest.mark.parametrize("case", golden_cases.ecdsa_cases(), ids=lambda c: c["label"][:48])
+def test_oracle_ecdsa_golden(case):
+    spki = bytes.fromhex(case["spki"])
+    sig = bytes.fromhex(case["sig"])
+    msg = bytes.fromhex(case["msg"])
+    assert O.do_verify(spki, sig, msg) == case["expected"]
+    if not case["unpinned"] and case["openssl"] in (0, 1) and case["expected"] in (0, 1):
+        assert (case["expected"] == 0) == (case["openssl"] == 1)
+
+
+def test_oracle_ecdsa_random_batch_labels():
+    b = G.ecdsa_batch(600, n_keys=8, corrupt=0.5, seed=3)
+    st = O.verify_batch(b, threads=4)
+    assert np.array_equal(st, b.expected)
