@@ -33,7 +33,10 @@ import numpy as np  # noqa: E402
 # Fixed algorithmic work per unit (kept constant across rounds)
 ED25519_OPS_PER_VERIFY = 2.4e5        # ~3,400 GF(2^255-19) mults x 64 32x32 partial products + 3 SHA-512 blocks
 TXID_OPS_PER_COMPRESSION = 3.3e3      # SHA-256 compression (64 rounds + schedule)
-INT32_PEAK_TOPS = 39.3                # 256 CU x 2.4 GHz x 64 lanes (MI355X_MICROARCH.md clocks)
+# VALU issue peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6e12 lane-ops/s (= FP32 vector 157.3 TFLOPS / 2,
+# MI355X_MICROARCH.md chip table).  BASELINE.md's 39.3e12 assumed 64 lanes/CU/clk; a 64-bit MAC
+# (v_mad_u64_u32) issues at half this rate (tools/microbench_mul.hip, profiles/microbench_mul_r01.txt).
+INT32_PEAK_TOPS = 78.6
 HBM_PEAK_GBS = 8000.0
 
 
@@ -48,6 +51,8 @@ def parse():
     ap.add_argument("--cpu-sample", type=int, default=32768)
     ap.add_argument("--no-txid", action="store_true", help="skip the secondary tx-id measurement")
     ap.add_argument("--txid-n", type=int, default=1_000_000)
+    ap.add_argument("--no-ecdsa", action="store_true", help="skip the secondary ECDSA measurement")
+    ap.add_argument("--ecdsa-n", type=int, default=500_000, help="cfg3 share per GPU (4M over 8 GPUs)")
     return ap.parse_args()
 
 
@@ -183,6 +188,41 @@ def main():
             "txid_roofline_frac": (comp_per_tx * TXID_OPS_PER_COMPRESSION * tb.ntx / (tx_ms * 1e-3) / 1e12) / INT32_PEAK_TOPS,
         }
         del dt, ids
+
+    # ---- secondary: cfg3 mixed ECDSA r1/k1 (500k per GPU = 4M over 8 GPUs) ----
+    if not args.no_ecdsa:
+        eb = G.ecdsa_batch(args.ecdsa_n, n_keys=args.keys, seed=0x5EED0003 + rank, threads=threads)
+        de = upload_sig_batch(eb, torch, dev)
+        est = torch.empty(eb.n, dtype=torch.uint8, device=dev)
+        ebm = torch.empty((eb.n + 63) // 64, dtype=torch.int64, device=dev)
+        for _ in range(2):
+            ctx.verify_batch_device(de, est, ebm, stream=stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        ecorrect = bool(np.array_equal(est.cpu().numpy(), eb.expected))
+        ctx.reset_stats()
+        ts = max(2, args.steps)
+        t1 = time.perf_counter()
+        for _ in range(ts):
+            ctx.verify_batch_device(de, est, ebm, stream=stream.cuda_stream)
+        torch.cuda.synchronize(dev)
+        eel = time.perf_counter() - t1
+        if world > 1:
+            e = torch.tensor([eel], dtype=torch.float64, device=dev)
+            dist.all_reduce(e, op=dist.ReduceOp.MAX)
+            eel = float(e.item())
+        s3 = ctx.stats()
+        r1_ms = s3.kernel_ms_total[native.K_ECDSA_R1] / max(1, s3.kernel_launches[native.K_ECDSA_R1])
+        k1_ms = s3.kernel_ms_total[native.K_ECDSA_K1] / max(1, s3.kernel_launches[native.K_ECDSA_K1])
+        n_r1 = int((eb.scheme == G.SCHEME_R1).sum())
+        secondary.update({
+            "ecdsa_mixed_sigs_per_s": world * eb.n * ts / eel,
+            "ecdsa_workload": "cfg3 share: %d ECDSA sigs per GPU (r1/k1 interleaved, 10%% corrupted)" % eb.n,
+            "ecdsa_correct_vs_labels": ecorrect,
+            "ecdsa_p256_kernel_ms": r1_ms, "ecdsa_k1_kernel_ms": k1_ms,
+            "ecdsa_p256_sigs_per_s_kernel": world * n_r1 / (r1_ms * 1e-3),
+            "ecdsa_roofline_frac": (ED25519_OPS_PER_VERIFY * eb.n / ((r1_ms + k1_ms) * 1e-3) / 1e12) / INT32_PEAK_TOPS,
+        })
+        del de, est, ebm
 
     # ---- CPU baseline (rank 0, N = 1 only): the oracle restatement on host cores ----
     cpu = None

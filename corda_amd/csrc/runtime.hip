@@ -166,6 +166,9 @@ extern "C" {
 
 int chip_abi_version(void) { return CHIP_ABI_VERSION; }
 
+// internal (not in cordahip.h): the device ordinal of a context, used by uniq.hip
+int chip_ctx_device(const chip_ctx* c) { return c ? c->device : 0; }
+
 int chip_device_count(void) {
     int n = 0;
     if (hipGetDeviceCount(&n) != hipSuccess) return 0;

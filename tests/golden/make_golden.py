@@ -428,8 +428,54 @@ def ecdsa_cases():
     return cases
 
 
+def uniq_cases():
+    """Hand-built notary scenarios; `expected` restates the reference semantics (not the oracle):
+    PersistentUniquenessProviderTests.kt:35-61, NotaryServiceTests.kt:98-145, SURVEY.md §8a."""
+    def ref(name, i):
+        return G.state_ref(hashlib.sha256(name.encode()).digest(), i).hex()
+
+    def tx(name):
+        return hashlib.sha256(b"tx:" + name.encode()).hexdigest()
+    a, b_, c, d = ref("a", 0), ref("b", 0), ref("c", 1), ref("d", 2)
+    cases = [
+        dict(label="commit then re-commit by another tx -> conflict",
+             source="PersistentUniquenessProviderTests.kt:35-61",
+             batches=[[[tx("t1"), [a], 1]], [[tx("t2"), [a], 2]]], expected=[[0], [2]]),
+        dict(label="double spend across txs in one batch", source="NotaryServiceTests.kt:118-145",
+             batches=[[[tx("t1"), [a, b_], 1], [tx("t2"), [b_, c], 1]]], expected=[[0, 2]]),
+        dict(label="identical tx notarised twice is idempotent", source="NotaryServiceTests.kt:98-116",
+             batches=[[[tx("t1"), [a, b_], 7]], [[tx("t1"), [a, b_], 7]]], expected=[[0], [1]]),
+        dict(label="identical tx twice in one batch", source="NotaryServiceTests.kt:98-116",
+             batches=[[[tx("t1"), [a, b_], 7], [tx("t1"), [a, b_], 7]]], expected=[[0, 1]]),
+        dict(label="same tx id, other caller -> conflict", source="ConsumingTx equality incl. requestingParty",
+             batches=[[[tx("t1"), [a], 1], [tx("t1"), [a], 2]]], expected=[[0, 2]]),
+        dict(label="failed tx consumes nothing: tx1{a}, tx2{a,b}, tx3{b}", source="SURVEY.md §7 / §8a",
+             batches=[[[tx("t1"), [a], 1], [tx("t2"), [a, b_], 1], [tx("t3"), [b_], 1]]], expected=[[0, 2, 0]]),
+        dict(label="chain of failures: tx2 blocked by tx1, tx3 by nothing, tx4 by tx3",
+             source="sequential commit order",
+             batches=[[[tx("t1"), [a], 1], [tx("t2"), [a, b_], 1], [tx("t3"), [b_, c], 1], [tx("t4"), [c, d], 1]]],
+             expected=[[0, 2, 0, 2]]),
+        dict(label="duplicate input inside one tx commits (first index wins)",
+             source="AppendOnlyPersistentMap.kt:51-92", batches=[[[tx("t1"), [a, a], 1]]], expected=[[0]]),
+        dict(label="re-submitting a tx with a duplicated input is a real conflict (index 1 != 0)",
+             source="NotaryService.kt:61-75 index-aware idempotency",
+             batches=[[[tx("t1"), [a, a], 1]], [[tx("t1"), [a, a], 1]]], expected=[[0], [2]]),
+        dict(label="partial overlap with own earlier commit is idempotent, inserts nothing",
+             source="NotaryService.kt:61-75", batches=[[[tx("t1"), [a, b_], 3]], [[tx("t1"), [a, b_], 3],
+                                                                                  [tx("t5"), [b_], 3]]],
+             expected=[[0], [1, 2]]),
+        dict(label="tx with no inputs commits", source="commit(emptyList)",
+             batches=[[[tx("t1"), [], 1]]], expected=[[0]]),
+    ]
+    return cases
+
+
 def main():
     G.build()
+    uq = uniq_cases()
+    with open(os.path.join(HERE, "uniq_cases.json"), "w") as f:
+        json.dump(uq, f, indent=1)
+    print("uniq cases:", len(uq))
     ec = ecdsa_cases()
     with open(os.path.join(HERE, "ecdsa_cases.json"), "w") as f:
         json.dump(ec, f, indent=1)

@@ -129,3 +129,29 @@ def test_oracle_ecdsa_random_batch_labels():
     b = G.ecdsa_batch(600, n_keys=8, corrupt=0.5, seed=3)
     st = O.verify_batch(b, threads=4)
     assert np.array_equal(st, b.expected)
+
+
+@pytest.mark.parametrize("case", golden_cases.uniq_cases(), ids=lambda c: c["label"][:48])
+def test_oracle_uniq_golden(case):
+    u = O.Uniq(64)
+    for bt, want in zip(case["batches"], case["expected"]):
+        b = G.uniq_batch_from_lists([(bytes.fromhex(tx), [bytes.fromhex(s) for s in ins], c) for tx, ins, c in bt])
+        st, recs = u.commit_batch(b.tx_ref_start, b.refs, b.tx_ids, b.callers)
+        assert st.tolist() == want
+
+
+def test_oracle_uniq_conflict_records():
+    # Conflict.stateHistory: (StateRef -> ConsumingTx(id, inputIndex, party)) for every consumed input
+    a = G.state_ref(b"\x01" * 32, 0)
+    b_ = G.state_ref(b"\x02" * 32, 3)
+    t1, t2 = b"\x11" * 32, b"\x22" * 32
+    u = O.Uniq(64)
+    u.commit_batch(*_ub([(t1, [a, b_], 5)]))
+    st, recs = u.commit_batch(*_ub([(t2, [b_, a, b_], 6)]))
+    assert st.tolist() == [2]
+    assert recs == [(0, 0, 1, t1, 5), (0, 1, 0, t1, 5)]
+
+
+def _ub(txs):
+    b = G.uniq_batch_from_lists(txs)
+    return b.tx_ref_start, b.refs, b.tx_ids, b.callers

@@ -460,3 +460,89 @@ def tx_batch_from_lists(txs) -> TxBatch:
     if len(tb.data) == 0:
         tb.data = np.zeros(1, dtype=np.uint8)
     return tb
+
+
+def state_ref(txhash: bytes, index: int) -> bytes:
+    """StateRef (Structures.kt:143-145) as the 36-byte key of the C-ABI: txhash || LE u32 index."""
+    return txhash + struct.pack("<I", index)
+
+
+class UniqBatch:
+    """chip_uniq_commit_batch layout: tx_ref_start u64[ntx+1], refs u8[nref*36], tx_ids u8[ntx*32], callers u32[ntx]."""
+    tx_ref_start = None
+    refs = None
+    tx_ids = None
+    callers = None
+
+    @property
+    def ntx(self):
+        return len(self.tx_ref_start) - 1
+
+
+def uniq_batch_from_lists(txs) -> UniqBatch:
+    """txs: list of (tx_id32, [StateRef36, ...], caller)"""
+    b = UniqBatch()
+    start = [0]
+    refs = []
+    for _, ins, _ in txs:
+        refs += ins
+        start.append(len(refs))
+    b.tx_ref_start = np.array(start, dtype=np.uint64)
+    b.refs = np.frombuffer(b"".join(refs), dtype=np.uint8).copy() if refs else np.zeros(36, np.uint8)
+    b.tx_ids = np.frombuffer(b"".join(t[0] for t in txs), dtype=np.uint8).copy()
+    b.callers = np.array([t[2] for t in txs], dtype=np.uint32)
+    return b
+
+
+def uniq_workload(ntx: int, n_pre: int, seed: int = 0x5EED0005, pre_hit: float = 0.01, dbl: float = 0.005,
+                  resubmit: float = 0.001, n_callers: int = 64):
+    """cfg5-shaped notary batch: 1-4 inputs per tx (mean 2.5), index 0-3; a pre-committed table of
+    n_pre StateRefs; `pre_hit` of inputs hit pre-committed states, `dbl` are intra-batch double
+    spends (earlier tx's input reused, including chains), `resubmit` of txs are exact re-submissions
+    of an earlier tx of the batch (idempotent).  Returns (pre rows, UniqBatch)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    pre_hash = PRNG(seed, b"pre").np_bytes(n_pre * 32).reshape(n_pre, 32)
+    pre_idx = rng.integers(0, 4, size=n_pre, dtype=np.uint32)
+    pre_refs = np.concatenate([pre_hash, pre_idx.view(np.uint8).reshape(n_pre, 4)], axis=1)
+    pre_tx = PRNG(seed, b"pretx").np_bytes(n_pre * 32).reshape(n_pre, 32)
+    pre_pos = rng.integers(0, 4, size=n_pre, dtype=np.uint32)
+    pre_caller = rng.integers(0, n_callers, size=n_pre, dtype=np.uint32)
+    nin = rng.integers(1, 5, size=ntx)
+    start = np.zeros(ntx + 1, dtype=np.uint64)
+    start[1:] = np.cumsum(nin)
+    nref = int(start[-1])
+    hashes = PRNG(seed, b"in").np_bytes(nref * 32).reshape(nref, 32)
+    idx = rng.integers(0, 4, size=nref, dtype=np.uint32)
+    refs = np.concatenate([hashes, idx.view(np.uint8).reshape(nref, 4)], axis=1)
+    u = rng.random(nref)
+    hit = np.nonzero(u < pre_hit)[0]
+    refs[hit] = pre_refs[rng.integers(0, n_pre, size=len(hit))] if n_pre else refs[hit]
+    dsp = np.nonzero((u >= pre_hit) & (u < pre_hit + dbl))[0]
+    ref_tx = np.repeat(np.arange(ntx), nin)
+    for r in dsp:                                  # reuse an input of an earlier tx (chains form naturally)
+        t = ref_tx[r]
+        if t == 0:
+            continue
+        t2 = int(rng.integers(max(0, t - 64), t))
+        r2 = int(start[t2] + rng.integers(0, nin[t2]))
+        refs[r] = refs[r2]
+    tx_ids = PRNG(seed, b"txid").np_bytes(ntx * 32).reshape(ntx, 32)
+    callers = rng.integers(0, n_callers, size=ntx, dtype=np.uint32)
+    # exact re-submissions: copy an earlier tx (same id, inputs, caller) when the input counts match
+    rs = np.nonzero(rng.random(ntx) < resubmit)[0]
+    for t in rs:
+        if t == 0:
+            continue
+        t2 = int(rng.integers(max(0, t - 256), t))
+        if nin[t2] != nin[t]:
+            continue
+        refs[int(start[t]):int(start[t + 1])] = refs[int(start[t2]):int(start[t2 + 1])]
+        tx_ids[t] = tx_ids[t2]
+        callers[t] = callers[t2]
+    b = UniqBatch()
+    b.tx_ref_start = start
+    b.refs = refs.reshape(-1).copy()
+    b.tx_ids = tx_ids.reshape(-1).copy()
+    b.callers = callers
+    pre = (pre_refs.reshape(-1).copy(), pre_tx.reshape(-1).copy(), pre_pos, pre_caller)
+    return pre, b
