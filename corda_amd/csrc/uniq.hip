@@ -20,7 +20,8 @@
 //      tx3{b} -> tx1 ok, tx2 conflict, tx3 ok).  The globally smallest undecided tx is decided in
 //      every round, and a sparse conflict graph settles in a few rounds.
 //   4. failed txs are IDEMPOTENT when every consumed input was consumed by (txId, i, caller)
-//      itself, else CONFLICT with one record per consumed distinct input     k_uniq_classify
+//      itself, else CONFLICT; either way the UniquenessException's Conflict.stateHistory is
+//      emitted: one record per consumed distinct input                       k_uniq_classify
 //   5. committed inputs are inserted (first index wins for an input repeated in one tx)  k_uniq_insert
 #include <mutex>
 #include <string>
@@ -240,8 +241,7 @@ __global__ void k_uniq_classify(uint64_t ntx, const uint64_t* __restrict__ start
             if (bslot[r2] == bslot[r]) { dup = true; break; }
         if (!dup) nrec++;
     }
-    if (!real) { st[t] = 1; return; }
-    st[t] = 2;
+    st[t] = real ? 2 : 1;
     const unsigned long long base = atomicAdd(nout, (unsigned long long)nrec);
     uint64_t w = base;
     for (uint64_t r = a; r < e; r++) {

@@ -1,0 +1,489 @@
+// corda/verify.hpp — header-only C++17 mirror of the reference's hot-path API over the C-ABI
+// (include/cordahip.h).  Same names, argument meaning and exceptions as the Kotlin sources it
+// mirrors, so call sites (and tests) read like the reference's:
+//
+//   Crypto.doVerify / isValid / findSignatureScheme   core/.../crypto/Crypto.kt:235-267,502-625
+//   TransactionSignature.verify                        core/.../crypto/TransactionSignature.kt:26-40
+//   TransactionWithSignatures.checkSignaturesAreValid / verifySignaturesExcept /
+//     verifyRequiredSignatures / getMissingSigners     core/.../transactions/TransactionWithSignatures.kt:29-85
+//   SignedTransaction.SignaturesMissingException       core/.../transactions/SignedTransaction.kt:228-229
+//   WireTransaction.id                                 core/.../transactions/WireTransaction.kt:63,139-189
+//   UniquenessProvider / PersistentUniquenessProvider.commit / UniquenessException
+//                                                      core/.../node/services/UniquenessProvider.kt:15-36,
+//                                                      node/.../transactions/PersistentUniquenessProvider.kt:92-113
+//   TrustedAuthorityNotaryService.commitInputStates    core/.../node/services/NotaryService.kt:61-75
+//
+// Batching is the point: a list of signatures (one transaction, or many transactions gathered by a
+// caller such as ResolveTransactionsFlow) is verified by one chip_verify_batch call; the exception
+// a caller sees is the one the reference's sequential loop would have thrown first.
+// Kryo serialization of SignableData is out of scope: a TransactionSignature carries the bytes the
+// JVM's SignableData(txId, metadata).serialize() produced (or a serializer callback builds them).
+#pragma once
+#include <algorithm>
+#include <cstdint>
+#include <exception>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <set>
+#include <stdexcept>
+#include <string>
+#include <utility>
+#include <vector>
+
+#include "../cordahip.h"
+
+namespace corda {
+
+using Bytes = std::vector<uint8_t>;
+
+// ---- exceptions (java.security / IllegalArgumentException / Corda exceptions) ----
+struct SignatureException : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+struct InvalidKeyException : std::runtime_error {
+    using std::runtime_error::runtime_error;
+};
+struct IllegalArgumentException : std::invalid_argument {
+    using std::invalid_argument::invalid_argument;
+};
+struct EngineException : std::runtime_error {   // libcordahip / HIP failure (not a reference exception)
+    using std::runtime_error::runtime_error;
+};
+
+struct SecureHash {
+    uint8_t bytes[32] = {};
+    bool operator<(const SecureHash& o) const { return std::memcmp(bytes, o.bytes, 32) < 0; }
+    bool operator==(const SecureHash& o) const { return std::memcmp(bytes, o.bytes, 32) == 0; }
+    bool operator!=(const SecureHash& o) const { return !(*this == o); }
+};
+
+// PublicKey: its X.509 SubjectPublicKeyInfo encoding (PublicKey.encoded)
+struct PublicKey {
+    Bytes encoded;
+    bool operator<(const PublicKey& o) const { return encoded < o.encoded; }
+    bool operator==(const PublicKey& o) const { return encoded == o.encoded; }
+};
+
+struct SignatureScheme {
+    int schemeNumberID;
+    const char* schemeCodeName;
+};
+inline const SignatureScheme ECDSA_SECP256K1_SHA256{2, "ECDSA_SECP256K1_SHA256"};
+inline const SignatureScheme ECDSA_SECP256R1_SHA256{3, "ECDSA_SECP256R1_SHA256"};
+inline const SignatureScheme EDDSA_ED25519_SHA512{4, "EDDSA_ED25519_SHA512"};
+
+// SignatureMetadata(platformVersion, schemeNumberID)  SignatureMetadata.kt:14-15
+struct SignatureMetadata {
+    int platformVersion = 1;
+    int schemeNumberID = 4;
+};
+
+// One libcordahip context (one GPU).
+class Engine {
+  public:
+    explicit Engine(int device = 0) {
+        chip_config cfg{device, 0, 0};
+        if (chip_init(&cfg, &ctx_) != 0) throw EngineException("chip_init failed (no GPU?)");
+    }
+    ~Engine() { chip_shutdown(ctx_); }
+    Engine(const Engine&) = delete;
+    Engine& operator=(const Engine&) = delete;
+    chip_ctx* get() const { return ctx_; }
+    void check(int rc) const {
+        if (rc != 0) throw EngineException(std::string("libcordahip: ") + chip_last_error(ctx_));
+    }
+
+  private:
+    chip_ctx* ctx_ = nullptr;
+};
+
+namespace detail {
+// SubjectPublicKeyInfo prefixes of the three accelerated schemes (Crypto.algorithmMap, Crypto.kt:188-191)
+inline int scheme_of(const Bytes& k) {
+    static const uint8_t ed[12] = {0x30, 0x2a, 0x30, 0x05, 0x06, 0x03, 0x2b, 0x65, 0x70, 0x03, 0x21, 0x00};
+    static const uint8_t r1oid[10] = {0x06, 0x08, 0x2a, 0x86, 0x48, 0xce, 0x3d, 0x03, 0x01, 0x07};
+    static const uint8_t k1oid[7] = {0x06, 0x05, 0x2b, 0x81, 0x04, 0x00, 0x0a};
+    if (k.size() == 44 && std::memcmp(k.data(), ed, 12) == 0) return 4;
+    if ((k.size() == 91 || k.size() == 59) && std::memcmp(k.data() + 13, r1oid, 10) == 0) return 3;
+    if ((k.size() == 88 || k.size() == 56) && std::memcmp(k.data() + 13, k1oid, 7) == 0) return 2;
+    return 0;
+}
+
+struct Item {
+    const Bytes* key;
+    const Bytes* sig;
+    const Bytes* msg;
+};
+
+// status of every item, one batch call (keys and messages de-duplicated)
+inline std::vector<uint8_t> verify_items(Engine& e, const std::vector<Item>& items) {
+    std::map<Bytes, uint32_t> kid, mid;
+    std::vector<const Bytes*> keys, msgs;
+    std::vector<uint32_t> key_idx, msg_idx, sig_len;
+    std::vector<uint64_t> sig_off;
+    Bytes sig_pool;
+    for (const Item& it : items) {
+        auto k = kid.emplace(*it.key, (uint32_t)keys.size());
+        if (k.second) keys.push_back(it.key);
+        auto m = mid.emplace(*it.msg, (uint32_t)msgs.size());
+        if (m.second) msgs.push_back(it.msg);
+        key_idx.push_back(k.first->second);
+        msg_idx.push_back(m.first->second);
+        sig_off.push_back(sig_pool.size());
+        sig_len.push_back((uint32_t)it.sig->size());
+        sig_pool.insert(sig_pool.end(), it.sig->begin(), it.sig->end());
+    }
+    auto pack = [](const std::vector<const Bytes*>& v, Bytes& pool, std::vector<uint64_t>& off, std::vector<uint32_t>& len) {
+        for (const Bytes* b : v) {
+            off.push_back(pool.size());
+            len.push_back((uint32_t)b->size());
+            pool.insert(pool.end(), b->begin(), b->end());
+        }
+        if (pool.empty()) pool.push_back(0);
+    };
+    Bytes key_pool, msg_pool;
+    std::vector<uint64_t> key_off, msg_off;
+    std::vector<uint32_t> key_len, msg_len;
+    pack(keys, key_pool, key_off, key_len);
+    pack(msgs, msg_pool, msg_off, msg_len);
+    if (sig_pool.empty()) sig_pool.push_back(0);
+    chip_sig_batch b{};
+    b.n = items.size();
+    b.key_idx = key_idx.data();
+    b.msg_idx = msg_idx.data();
+    b.sig_data = sig_pool.data();
+    b.sig_off = sig_off.data();
+    b.sig_len = sig_len.data();
+    b.n_keys = keys.size();
+    b.key_data = key_pool.data();
+    b.key_off = key_off.data();
+    b.key_len = key_len.data();
+    b.n_msgs = msgs.size();
+    b.msg_data = msg_pool.data();
+    b.msg_off = msg_off.data();
+    b.msg_len = msg_len.data();
+    b.sig_bytes = sig_pool.size();
+    b.key_bytes = key_pool.size();
+    b.msg_bytes = msg_pool.size();
+    std::vector<uint8_t> status(items.size());
+    if (!items.empty()) e.check(chip_verify_batch(e.get(), &b, status.data(), nullptr));
+    return status;
+}
+
+// the exception Crypto.doVerify would throw for a non-VALID status
+[[noreturn]] inline void throw_for(uint8_t st, const Bytes& key) {
+    const int sch = scheme_of(key);
+    switch (st) {
+        case CHIP_INVALID: throw SignatureException("Signature Verification failed!");
+        case CHIP_SIG_DECODE:
+            throw SignatureException(sch == 4 ? "signature length is wrong" : "error decoding signature bytes.");
+        case CHIP_EMPTY_SIG: throw IllegalArgumentException("Signature data is empty!");
+        case CHIP_EMPTY_CLEAR: throw IllegalArgumentException("Clear data is empty, nothing to verify!");
+        case CHIP_KEY_INVALID: throw InvalidKeyException("invalid key: not a valid point");
+        default: throw IllegalArgumentException("Unsupported key/algorithm");
+    }
+}
+}  // namespace detail
+
+// Crypto (object)
+struct Crypto {
+    static SignatureScheme findSignatureScheme(const PublicKey& key) {
+        switch (detail::scheme_of(key.encoded)) {
+            case 2: return ECDSA_SECP256K1_SHA256;
+            case 3: return ECDSA_SECP256R1_SHA256;
+            case 4: return EDDSA_ED25519_SHA512;
+            default: throw IllegalArgumentException("Unrecognised algorithm");
+        }
+    }
+    // Crypto.doVerify(PublicKey, ByteArray, ByteArray): true or throws   Crypto.kt:502-536
+    static bool doVerify(Engine& e, const PublicKey& key, const Bytes& signatureData, const Bytes& clearData) {
+        const uint8_t st = detail::verify_items(e, {{&key.encoded, &signatureData, &clearData}})[0];
+        if (st != CHIP_VALID) detail::throw_for(st, key.encoded);
+        return true;
+    }
+    // Crypto.isValid(PublicKey, ByteArray, ByteArray): false on a bad signature; engine decode
+    // errors still throw SignatureException   Crypto.kt:600-625
+    static bool isValid(Engine& e, const PublicKey& key, const Bytes& signatureData, const Bytes& clearData) {
+        const uint8_t st = detail::verify_items(e, {{&key.encoded, &signatureData, &clearData}})[0];
+        if (st == CHIP_VALID) return true;
+        if (st == CHIP_INVALID) return false;
+        detail::throw_for(st, key.encoded);
+    }
+};
+
+// SignableData(txId, metadata).serialize().bytes is produced by the JVM (Kryo); a deployment plugs
+// its serializer here, TransactionSignature may also carry the bytes directly.
+using SignableDataSerializer = std::function<Bytes(const SecureHash&, const SignatureMetadata&)>;
+
+struct TransactionSignature {
+    Bytes bytes;
+    PublicKey by;
+    SignatureMetadata signatureMetadata;
+    Bytes signableBytes;   // precomputed SignableData bytes (optional)
+
+    Bytes signable(const SecureHash& txId, const SignableDataSerializer& ser) const {
+        if (!signableBytes.empty() || !ser) return signableBytes;
+        return ser(txId, signatureMetadata);
+    }
+    // TransactionSignature.verify(txId) = Crypto.doVerify(txId, this)
+    bool verify(Engine& e, const SecureHash& txId, const SignableDataSerializer& ser = nullptr) const {
+        return Crypto::doVerify(e, by, bytes, signable(txId, ser));
+    }
+};
+
+// SignedTransaction.SignaturesMissingException
+struct SignaturesMissingException : SignatureException {
+    std::set<PublicKey> missing;
+    std::vector<std::string> descriptions;
+    SecureHash id;
+    SignaturesMissingException(std::set<PublicKey> m, std::vector<std::string> d, const SecureHash& i)
+        : SignatureException("Missing signatures for " + std::to_string(m.size()) + " keys"),
+          missing(std::move(m)), descriptions(std::move(d)), id(i) {}
+};
+
+// TransactionWithSignatures / SignedTransaction (signature part)
+struct SignedTransaction {
+    SecureHash id;
+    std::vector<TransactionSignature> sigs;
+    std::set<PublicKey> requiredSigningKeys;
+    SignableDataSerializer serializer;
+
+    SignedTransaction() = default;
+    SignedTransaction(SecureHash i, std::vector<TransactionSignature> s, std::set<PublicKey> req)
+        : id(i), sigs(std::move(s)), requiredSigningKeys(std::move(req)) {
+        // SignedTransaction.kt:46  require(sigs.isNotEmpty())
+        if (sigs.empty()) throw IllegalArgumentException("Tried to instantiate a SignedTransaction without any signatures ");
+    }
+    // TransactionWithSignatures.kt:62-66 — the first failing signature in list order throws
+    void checkSignaturesAreValid(Engine& e) const {
+        std::vector<Bytes> msgs;
+        msgs.reserve(sigs.size());
+        for (const auto& s : sigs) msgs.push_back(s.signable(id, serializer));
+        std::vector<detail::Item> items;
+        for (size_t i = 0; i < sigs.size(); i++) items.push_back({&sigs[i].by.encoded, &sigs[i].bytes, &msgs[i]});
+        const auto st = detail::verify_items(e, items);
+        for (size_t i = 0; i < st.size(); i++)
+            if (st[i] != CHIP_VALID) detail::throw_for(st[i], sigs[i].by.encoded);
+    }
+    // TransactionWithSignatures.kt:79-85 (plain keys: isFulfilledBy == membership)
+    std::set<PublicKey> getMissingSigners() const {
+        std::set<PublicKey> sigKeys;
+        for (const auto& s : sigs) sigKeys.insert(s.by);
+        std::set<PublicKey> missing;
+        for (const auto& k : requiredSigningKeys)
+            if (!sigKeys.count(k)) missing.insert(k);
+        return missing;
+    }
+    // TransactionWithSignatures.kt:44-50
+    void verifySignaturesExcept(Engine& e, const std::vector<PublicKey>& allowedToBeMissing = {}) const {
+        checkSignaturesAreValid(e);
+        auto needed = getMissingSigners();
+        for (const auto& k : allowedToBeMissing) needed.erase(k);
+        if (!needed.empty()) throw SignaturesMissingException(needed, {}, id);
+    }
+    void verifyRequiredSignatures(Engine& e) const { verifySignaturesExcept(e); }
+};
+
+// Batch site (ResolveTransactionsFlow.kt:91-98 style): many transactions, one device batch.
+// result[i] is null when transaction i passes checkSignaturesAreValid, else the exception its
+// own sequential loop would have thrown first.
+inline std::vector<std::exception_ptr> checkSignaturesAreValidBatch(Engine& e,
+                                                                     const std::vector<const SignedTransaction*>& txs) {
+    std::vector<Bytes> msgs;
+    std::vector<detail::Item> items;
+    std::vector<std::pair<size_t, size_t>> owner;
+    for (size_t t = 0; t < txs.size(); t++)
+        for (const auto& s : txs[t]->sigs) msgs.push_back(s.signable(txs[t]->id, txs[t]->serializer));
+    size_t m = 0;
+    for (size_t t = 0; t < txs.size(); t++)
+        for (size_t i = 0; i < txs[t]->sigs.size(); i++, m++) {
+            items.push_back({&txs[t]->sigs[i].by.encoded, &txs[t]->sigs[i].bytes, &msgs[m]});
+            owner.emplace_back(t, i);
+        }
+    const auto st = detail::verify_items(e, items);
+    std::vector<std::exception_ptr> res(txs.size());
+    for (size_t k = 0; k < st.size(); k++) {
+        const size_t t = owner[k].first;
+        if (st[k] != CHIP_VALID && !res[t]) {
+            try {
+                detail::throw_for(st[k], items[k].key[0]);
+            } catch (...) {
+                res[t] = std::current_exception();
+            }
+        }
+    }
+    return res;
+}
+
+// ---- WireTransaction.id ----
+struct ComponentGroup {
+    int groupIndex;
+    std::vector<Bytes> components;   // OpaqueBytes of the serialized components
+};
+struct WireTransaction {
+    std::vector<ComponentGroup> componentGroups;
+    uint8_t privacySalt[32] = {};
+
+    // WireTransaction.kt:53-56 invariants the id depends on
+    void checkInvariants() const {
+        std::set<int> seen;
+        for (const auto& g : componentGroups) {
+            if (g.components.empty()) throw IllegalArgumentException("Empty component groups are not allowed");
+            if (!seen.insert(g.groupIndex).second) throw IllegalArgumentException("Duplicated component groups detected");
+            if (g.groupIndex < 0 || g.groupIndex >= 64) throw IllegalArgumentException("group ordinal outside [0, 64)");
+        }
+        if (componentGroups.empty()) throw IllegalArgumentException("A transaction must contain components");
+    }
+    // batch id computation (one chip_txid_batch call)
+    static std::vector<SecureHash> ids(Engine& e, const std::vector<WireTransaction>& txs) {
+        std::vector<uint8_t> salts;
+        std::vector<uint64_t> start{0}, off;
+        std::vector<uint32_t> grp, internal, len;
+        Bytes data;
+        for (const auto& tx : txs) {
+            tx.checkInvariants();
+            salts.insert(salts.end(), tx.privacySalt, tx.privacySalt + 32);
+            // groups in ordinal order (insertion order is irrelevant to the id)
+            std::vector<const ComponentGroup*> gs;
+            for (const auto& g : tx.componentGroups) gs.push_back(&g);
+            std::sort(gs.begin(), gs.end(), [](auto* a, auto* b) { return a->groupIndex < b->groupIndex; });
+            for (const auto* g : gs)
+                for (size_t i = 0; i < g->components.size(); i++) {
+                    grp.push_back((uint32_t)g->groupIndex);
+                    internal.push_back((uint32_t)i);
+                    off.push_back(data.size());
+                    len.push_back((uint32_t)g->components[i].size());
+                    data.insert(data.end(), g->components[i].begin(), g->components[i].end());
+                }
+            start.push_back(grp.size());
+        }
+        if (data.empty()) data.push_back(0);
+        chip_tx_batch b{};
+        b.ntx = txs.size();
+        b.salts = salts.data();
+        b.tx_comp_start = start.data();
+        b.ncomp = grp.size();
+        b.comp_group = grp.data();
+        b.comp_internal = internal.data();
+        b.data = data.data();
+        b.comp_off = off.data();
+        b.comp_len = len.data();
+        b.data_bytes = data.size();
+        std::vector<SecureHash> out(txs.size());
+        if (!txs.empty()) e.check(chip_txid_batch(e.get(), &b, reinterpret_cast<uint8_t*>(out.data())));
+        return out;
+    }
+    SecureHash id(Engine& e) const { return ids(e, {*this})[0]; }
+};
+
+// ---- notary uniqueness ----
+struct StateRef {
+    SecureHash txhash;
+    uint32_t index = 0;
+    bool operator<(const StateRef& o) const { return txhash != o.txhash ? txhash < o.txhash : index < o.index; }
+    bool operator==(const StateRef& o) const { return txhash == o.txhash && index == o.index; }
+};
+// ConsumingTx(id, inputIndex, requestingParty) — the party is interned to a u32 by the caller
+struct ConsumingTx {
+    SecureHash id;
+    uint32_t inputIndex = 0;
+    uint32_t requestingParty = 0;
+    bool operator==(const ConsumingTx& o) const {
+        return id == o.id && inputIndex == o.inputIndex && requestingParty == o.requestingParty;
+    }
+};
+struct Conflict {
+    std::vector<std::pair<StateRef, ConsumingTx>> stateHistory;   // LinkedHashMap order
+};
+struct UniquenessException : std::runtime_error {
+    Conflict error;
+    explicit UniquenessException(Conflict c) : std::runtime_error("UniquenessException"), error(std::move(c)) {}
+};
+struct NotaryException : std::runtime_error {   // NotaryError.Conflict(txId, conflict)
+    SecureHash txId;
+    Conflict conflict;
+    NotaryException(const SecureHash& t, Conflict c) : std::runtime_error("Notary conflict"), txId(t), conflict(std::move(c)) {}
+};
+
+class PersistentUniquenessProvider {
+  public:
+    struct Request {
+        std::vector<StateRef> states;
+        SecureHash txId;
+        uint32_t callerIdentity;
+    };
+    struct Outcome {
+        uint8_t status;   // 0 committed, 1 idempotent (commit threw, commitInputStates accepts), 2 conflict
+        Conflict conflict;
+    };
+
+    PersistentUniquenessProvider(Engine& e, uint64_t capacity = 1 << 20) : e_(e) {
+        e_.check(chip_uniq_open(e_.get(), capacity, &u_));
+    }
+    ~PersistentUniquenessProvider() { chip_uniq_close(u_); }
+    PersistentUniquenessProvider(const PersistentUniquenessProvider&) = delete;
+    PersistentUniquenessProvider& operator=(const PersistentUniquenessProvider&) = delete;
+
+    uint64_t size() const { return chip_uniq_size(u_); }
+
+    // batch of commits applied in order (the notary's batching layer)
+    std::vector<Outcome> commitBatch(const std::vector<Request>& reqs) {
+        std::vector<uint64_t> start{0};
+        std::vector<uint8_t> refs, ids;
+        std::vector<uint32_t> callers;
+        for (const auto& r : reqs) {
+            for (const auto& s : r.states) {
+                refs.insert(refs.end(), s.txhash.bytes, s.txhash.bytes + 32);
+                for (int b = 0; b < 4; b++) refs.push_back((uint8_t)(s.index >> (8 * b)));
+            }
+            start.push_back(start.back() + r.states.size());
+            ids.insert(ids.end(), r.txId.bytes, r.txId.bytes + 32);
+            callers.push_back(r.callerIdentity);
+        }
+        if (refs.empty()) refs.resize(36);
+        std::vector<uint8_t> st(reqs.size());
+        std::vector<chip_conflict> out(start.back() + 1);
+        uint64_t nout = 0;
+        if (!reqs.empty())
+            e_.check(chip_uniq_commit_batch(u_, reqs.size(), start.data(), refs.data(), ids.data(), callers.data(),
+                                            st.data(), out.data(), out.size(), &nout));
+        std::vector<Outcome> res(reqs.size());
+        for (size_t t = 0; t < reqs.size(); t++) res[t].status = st[t];
+        for (uint64_t k = 0; k < nout; k++) {
+            const chip_conflict& c = out[k];
+            ConsumingTx ct;
+            std::memcpy(ct.id.bytes, c.consuming_tx, 32);
+            ct.inputIndex = c.consumed_index;
+            ct.requestingParty = c.consuming_caller;
+            res[c.tx].conflict.stateHistory.emplace_back(reqs[c.tx].states[c.input_index], ct);
+        }
+        return res;
+    }
+    // UniquenessProvider.commit: throws UniquenessException when any input is already committed
+    void commit(const std::vector<StateRef>& states, const SecureHash& txId, uint32_t callerIdentity) {
+        auto r = commitBatch({{states, txId, callerIdentity}})[0];
+        if (r.status != 0) throw UniquenessException(r.conflict);
+    }
+
+  private:
+    Engine& e_;
+    chip_uniq* u_ = nullptr;
+};
+
+// TrustedAuthorityNotaryService.commitInputStates (NotaryService.kt:61-75)
+inline void commitInputStates(PersistentUniquenessProvider& p, const std::vector<StateRef>& inputs,
+                              const SecureHash& txId, uint32_t caller) {
+    try {
+        p.commit(inputs, txId, caller);
+    } catch (const UniquenessException& e) {
+        bool real = false;
+        for (size_t i = 0; i < inputs.size(); i++)
+            for (const auto& h : e.error.stateHistory)
+                if (h.first == inputs[i] && !(h.second == ConsumingTx{txId, (uint32_t)i, caller})) real = true;
+        if (real) throw NotaryException(txId, e.error);
+    }
+}
+
+}  // namespace corda

@@ -149,9 +149,13 @@ int chip_txid_batch_device(chip_ctx* ctx, const chip_tx_batch* batch, uint8_t* i
  *                caller's party id (the JNI layer interns Party.owningKey -> u32).
  * commit_batch applies PersistentUniquenessProvider.commit to each tx in batch order, with
  * TrustedAuthorityNotaryService.commitInputStates' idempotency filter:
- *   tx_status 0 COMMITTED, 1 IDEMPOTENT (every conflict is this tx's own earlier commit),
- *             2 CONFLICT (nothing inserted; conflict records describe every already-consumed input)
- * A tx that fails inserts nothing, so later txs in the same batch may consume its inputs. */
+ *   tx_status 0 COMMITTED, 1 IDEMPOTENT (every conflict is this tx's own earlier commit:
+ *             commit threw, commitInputStates swallowed it), 2 CONFLICT (NotaryException)
+ * For every tx with status 1 or 2 nothing is inserted and `out` receives the
+ * UniquenessException's Conflict.stateHistory: one record per already-consumed distinct input,
+ * ordered by (tx, input_index).  A failed tx inserts nothing, so later txs in the same batch may
+ * consume its inputs.  Returns CHIP_E_CAPACITY (after committing) when more than `cap` records
+ * exist; *n_out is then the full count and the first `cap` records are written. */
 typedef struct chip_uniq chip_uniq;
 
 typedef struct {

@@ -94,11 +94,10 @@ void orc_uniq_commit_batch(orc_uniq* u, uint64_t ntx, const uint64_t* start, con
         if (!any) {
             for (uint64_t k = a; k < b; k++) put(u, refs36 + 36 * k, tx_ids + 32 * t, (uint32_t)(k - a), callers[t]);
             tx_status[t] = 0;
-        } else if (!real) {
-            tx_status[t] = 1;
         } else {
-            tx_status[t] = 2;
-            /* Conflict.stateHistory: every input already committed (LinkedHashMap order) */
+            tx_status[t] = real ? 2 : 1;
+            /* UniquenessException's Conflict.stateHistory: every input already committed, in
+             * input order (LinkedHashMap), for IDEMPOTENT and CONFLICT alike */
             for (uint64_t k = a; k < b; k++) {
                 slot* s = find(u, refs36 + 36 * k);
                 if (!s->used) continue;
