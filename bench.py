@@ -30,13 +30,18 @@ for _p in (ROOT, os.path.join(ROOT, "tools"), os.path.join(ROOT, "tests")):
 
 import numpy as np  # noqa: E402
 
-# Fixed algorithmic work per unit (kept constant across rounds)
-ED25519_OPS_PER_VERIFY = 2.4e5        # ~3,400 GF(2^255-19) mults x 64 32x32 partial products + 3 SHA-512 blocks
+# Fixed algorithmic work per unit (pinned from the algorithm each kernel runs)
+ED25519_OPS_PER_VERIFY = 2.4e5        # SURVEY §8d canonical count (~3,400 field mults x 64 + 3 SHA-512 blocks)
+# k_ed_comb_verify: 32x32->64 multiply-accumulates (v_mad_u64_u32) per signature, counted from the
+# schedule: 64 cached adds (4 mults) + 63 p1p1->p3 (4) + 1 conversion (4) + 32 Niels adds (3) + 31
+# conversions (4) + 3 final = 735 GF(2^255-19) multiplications x 100 limb products (radix 2^25.5)
+ED_COMB_MACS_PER_VERIFY = 73_500
 TXID_OPS_PER_COMPRESSION = 3.3e3      # SHA-256 compression (64 rounds + schedule)
 # VALU issue peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6e12 lane-ops/s (= FP32 vector 157.3 TFLOPS / 2,
-# MI355X_MICROARCH.md chip table).  BASELINE.md's 39.3e12 assumed 64 lanes/CU/clk; a 64-bit MAC
-# (v_mad_u64_u32) issues at half this rate (tools/microbench_mul.hip, profiles/microbench_mul_r01.txt).
+# MI355X_MICROARCH.md chip table).  v_mad_u64_u32 issues at a quarter of that: 19.66e12 MACs/s
+# (tools/microbench_mul.hip measures 18.0e12 including a dependent xor per MAC).
 INT32_PEAK_TOPS = 78.6
+MAC_PEAK_T = 78.6 / 4
 HBM_PEAK_GBS = 8000.0
 
 
@@ -151,12 +156,19 @@ def main():
         dist.all_reduce(c, op=dist.ReduceOp.MIN)
         correct = bool(c.item())
     s = ctx.stats()
-    ed_launches = max(1, s.kernel_launches[native.K_ED25519])
-    ed_ms = s.kernel_ms_total[native.K_ED25519] / ed_launches
-    kp_ms = s.kernel_ms_total[native.K_KEYPREP] / max(1, s.kernel_launches[native.K_KEYPREP])
+
+    def kms(k):
+        return s.kernel_ms_total[k] / max(1, s.kernel_launches[k])
+    comb_ms, fin_ms, tab_ms, straus_ms, kp_ms = (kms(native.K_ED_COMB), kms(native.K_ED_FINISH),
+                                                 kms(native.K_ED_TABLES), kms(native.K_ED25519),
+                                                 kms(native.K_KEYPREP))
     ms_per_step = elapsed / args.steps * 1e3
     value = world * n * args.steps / elapsed
-    achieved_tops = ED25519_OPS_PER_VERIFY * n_arith / (ed_ms * 1e-3) / 1e12
+    # signatures on the comb path: arithmetic-needing signatures of keys with >= 4 of them (default policy)
+    arith = (batch.expected == 0) | (batch.expected == 1)
+    per_key = np.bincount(batch.key_idx[arith], minlength=len(batch.key_off))
+    n_comb = int(per_key[per_key >= 4].sum())
+    achieved = ED_COMB_MACS_PER_VERIFY * n_comb / (comb_ms * 1e-3) / 1e12
 
     # ---- secondary: tx ids/s on cfg4-shaped transactions (1 GPU per rank, same weak scaling) ----
     secondary = {}
@@ -254,17 +266,20 @@ def main():
             "higher_is_better": True,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "u32 (radix-2^25.5 GF(2^255-19) limbs, 64-bit MACs)",
+            "dtype": "u32 (radix-2^25.5 GF(2^255-19) limbs, 32x32->64 MACs)",
             "data": "synthetic (OpenSSL-signed, seeded; SURVEY.md §8d cfg2 corruption mix)",
             "config": {"workload": "cfg2: %d-signature EDDSA_ED25519_SHA512 batch per GPU, %d keys, 200-B messages, "
                                    "10%% corrupted" % (n, args.keys),
                        "sigs_per_gpu": n, "keys": args.keys, "msg_len": 200, "corrupt": 0.10,
                        "parallelism": "dp%d (batch sharded by transaction, RCCL bitmap all-gather)" % world},
             "correct_vs_labels": correct,
-            "roofline": {"bound": "valu", "achieved": achieved_tops, "peak": INT32_PEAK_TOPS, "unit": "Tops/s (int32)",
-                         "frac": achieved_tops / INT32_PEAK_TOPS, "traffic": None,
-                         "kernel": "k_ed25519_verify", "kernel_ms": ed_ms, "units_per_launch": n_arith,
-                         "ops_per_unit": ED25519_OPS_PER_VERIFY, "keyprep_ms": kp_ms},
+            "roofline": {"bound": "valu", "achieved": achieved, "peak": MAC_PEAK_T,
+                         "unit": "T MAC/s (v_mad_u64_u32 32x32->64)", "frac": achieved / MAC_PEAK_T,
+                         "traffic": None, "kernel": "k_ed_comb_verify", "kernel_ms": comb_ms,
+                         "units_per_launch": n_comb, "macs_per_unit": ED_COMB_MACS_PER_VERIFY,
+                         "pipeline_ms": {"keyprep": kp_ms, "comb_tables": tab_ms, "comb_verify": comb_ms,
+                                         "comb_finish": fin_ms, "straus_verify": straus_ms},
+                         "canonical_tops": ED25519_OPS_PER_VERIFY * n_arith / (ms_per_step * 1e-3) / 1e12 / world},
             "cpu_baseline": cpu,
             "secondary": secondary,
             "gen_s": gen_s,

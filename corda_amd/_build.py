@@ -9,11 +9,12 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libcordahip.so")
-SOURCES = ["runtime.hip", "ed25519.hip", "ecdsa.hip", "txid.hip", "uniq.hip"]
+SOURCES = ["runtime.hip", "ed25519.hip", "ed25519_comb.hip", "ecdsa.hip", "txid.hip", "uniq.hip"]
 HEADERS = ["common.hpp", "fe25519_dev.hpp", "scalar_dev.hpp", "sha2_dev.hpp", "runtime.hpp", "curve_consts.hpp",
-           "ec_dev.hpp"]
+           "ec_dev.hpp", "ed_common_dev.hpp", "comb_tables.hpp"]
 GEN = os.path.join(ROOT, "tools", "gen_constants.py")
 CONSTS = os.path.join(CSRC, "curve_consts.hpp")
+COMB = os.path.join(CSRC, "comb_tables.hpp")   # generated, git-ignored (3 MB of fixed-base tables)
 
 
 def _mtime(p):
@@ -35,6 +36,8 @@ def needs_rebuild() -> bool:
 def build(force: bool = False, verbose: bool = False) -> str:
     if _mtime(CONSTS) < _mtime(GEN):
         subprocess.check_call([sys.executable, GEN, CONSTS])
+    if _mtime(COMB) < _mtime(GEN):
+        subprocess.check_call([sys.executable, GEN, "--comb", COMB])
     if not force and not needs_rebuild():
         return LIB
     hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")

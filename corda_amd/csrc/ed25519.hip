@@ -10,9 +10,7 @@
 // fixed-window schedule (no divergence) — signed radix-16 digits for A from a per-key table
 // of 0..8 x (-A) in global memory, signed radix-256 digits for B from a 129-entry affine table
 // staged in LDS; 252 doublings + 64 A-adds + 32 B-adds per signature.
-#include "fe25519_dev.hpp"
-#include "scalar_dev.hpp"
-#include "sha2_dev.hpp"
+#include "ed_common_dev.hpp"
 #include "runtime.hpp"
 
 #define ED_TAB_ENTRIES 9
@@ -21,21 +19,12 @@
 // SPKI prefix of an Ed25519 key (X509 SubjectPublicKeyInfo, OID 1.3.101.112)
 __device__ __constant__ const uint8_t SPKI_ED[12] = {0x30, 0x2a, 0x30, 0x05, 0x06, 0x03, 0x2b, 0x65, 0x70, 0x03, 0x21, 0x00};
 
-CHIP_DEV void store_cached(uint32_t* dst, const ge_cached& c) {
-#pragma unroll
-    for (int i = 0; i < 10; i++) {
-        dst[i] = c.YpX.v[i];
-        dst[10 + i] = c.YmX.v[i];
-        dst[20 + i] = c.Z.v[i];
-        dst[30 + i] = c.T2d.v[i];
-    }
-}
-
 // ---- K1b: per unique key.  Ed25519 keys only; other schemes are handled by ecdsa.hip ----
 __global__ void __launch_bounds__(256) k_ed25519_key_prep(uint64_t n_keys, const uint8_t* __restrict__ key_data,
                                                           const uint64_t* __restrict__ key_off,
                                                           const uint32_t* __restrict__ key_len, KeyMeta* meta,
-                                                          uint32_t* __restrict__ abytes, uint32_t* __restrict__ table) {
+                                                          uint32_t* __restrict__ abytes, uint32_t* __restrict__ table,
+                                                          uint32_t* __restrict__ nega) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_keys) return;
     const uint8_t* p = key_data + key_off[k];
@@ -71,85 +60,26 @@ __global__ void __launch_bounds__(256) k_ed25519_key_prep(uint64_t n_keys, const
     fe_carry(nA.X);
     fe_neg(nA.T, A.T);
     fe_carry(nA.T);
+    if (nega) ed_store_p3(nega + k * 40, nA);   // -A in extended form: base of the per-key comb (ed25519_comb.hip)
     uint32_t* tab = table + k * ED_TAB_WORDS;
     ge_cached c, c1;
     fe_1(c.YpX); fe_1(c.YmX); fe_1(c.Z); fe_0(c.T2d);
-    store_cached(tab, c);
+    ed_store_cached(tab, c);
     ge_p3_to_cached(c1, nA);
-    store_cached(tab + 40, c1);
+    ed_store_cached(tab + 40, c1);
     ge_p1p1 t;
     ge_p3 P;
     ge_p3_dbl(t, nA);
     ge_p1p1_to_p3(P, t);
     ge_p3_to_cached(c, P);
-    store_cached(tab + 80, c);
+    ed_store_cached(tab + 80, c);
     for (int j = 3; j <= 8; j++) {
         ge_add_cached(t, P, c1, false);
         ge_p1p1_to_p3(P, t);
         ge_p3_to_cached(c, P);
-        store_cached(tab + 40 * j, c);
+        ed_store_cached(tab + 40 * j, c);
     }
     meta[k] = m;
-}
-
-// SHA-512(R || Abyte || M) as a little-endian 512-bit integer (16 words)
-CHIP_DEV void ed_challenge(uint32_t hx[16], const uint32_t R[8], const uint32_t Ab[8], const uint8_t* m, uint32_t ml) {
-    uint64_t H[8];
-    sha512_init(H);
-    const uint64_t total = 64ull + ml;
-    const uint32_t nblocks = (uint32_t)((total + 17 + 127) / 128);
-    for (uint32_t b = 0; b < nblocks; b++) {
-        uint64_t w[16];
-#pragma unroll
-        for (int j = 0; j < 16; j++) {
-            uint64_t v = 0;
-            if (b == 0 && j < 8) {
-                const uint32_t lo = (j < 4) ? R[2 * j] : Ab[2 * (j - 4)];
-                const uint32_t hi = (j < 4) ? R[2 * j + 1] : Ab[2 * (j - 4) + 1];
-                v = ((uint64_t)__builtin_bswap32(lo) << 32) | __builtin_bswap32(hi);
-            } else {
-                const int64_t base = (int64_t)b * 128 + 8 * j - 64;
-#pragma unroll
-                for (int q = 0; q < 8; q++) {
-                    const int64_t pos = base + q;
-                    uint32_t by = 0;
-                    if (pos < (int64_t)ml) by = m[pos];
-                    else if (pos == (int64_t)ml) by = 0x80;
-                    v = (v << 8) | by;
-                }
-            }
-            w[j] = v;
-        }
-        if (b == nblocks - 1) {
-            w[14] = 0;
-            w[15] = total * 8;
-        }
-        sha512_compress(H, w);
-    }
-    // digest bytes are big-endian state words; as a little-endian integer word 2j = bswap(hi32(H_j))
-#pragma unroll
-    for (int j = 0; j < 8; j++) {
-        hx[2 * j] = __builtin_bswap32((uint32_t)(H[j] >> 32));
-        hx[2 * j + 1] = __builtin_bswap32((uint32_t)H[j]);
-    }
-}
-
-CHIP_DEV void load_cached(ge_cached& c, const uint32_t* __restrict__ src) {
-    const uint4* s4 = reinterpret_cast<const uint4*>(src);
-#pragma unroll
-    for (int q = 0; q < 10; q++) {
-        const uint4 x = s4[q];
-        const uint32_t vals[4] = {x.x, x.y, x.z, x.w};
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-            const int idx = 4 * q + e;
-            const int f = idx / 10, l = idx % 10;
-            if (f == 0) c.YpX.v[l] = vals[e];
-            else if (f == 1) c.YmX.v[l] = vals[e];
-            else if (f == 2) c.Z.v[l] = vals[e];
-            else c.T2d.v[l] = vals[e];
-        }
-    }
 }
 
 // ---- K1: batch verify over the compacted list of Ed25519 signatures needing arithmetic ----
@@ -188,14 +118,7 @@ __global__ void __launch_bounds__(256) k_ed25519_verify(const uint32_t* __restri
     ed_challenge(hx, R, Ab, msg_data + msg_off[mi], msg_len[mi]);
     sc_reduce512(h, hx);
     // effective S (slide() carry drop) reduced mod L
-    sc_reduce256(s, S);
-    if (S[7] >> 31) {
-        const uint32_t d = slide_drops(S);
-        uint32_t k2[8];
-#pragma unroll
-        for (int q = 0; q < 8; q++) k2[q] = ED_2_256_MOD_L[q];
-        for (uint32_t t = 0; t < d; t++) sc_sub(s, s, k2);
-    }
+    ed_effective_s(s, S);
     uint32_t ea[8], eb[8];
     sc_recode16(ea, h);
     sc_recode256(eb, s);
@@ -225,7 +148,7 @@ __global__ void __launch_bounds__(256) k_ed25519_verify(const uint32_t* __restri
         const int da = (int)(ea[7] >> 28) - 8;
         shl256(ea, 4);
         const uint32_t ia = (uint32_t)(da < 0 ? -da : da);
-        load_cached(ca, tab + 40 * ia);
+        ed_load_cached(ca, tab + 40 * ia);
         ge_add_cached(t, u, ca, da < 0);
         if ((w & 1) == 0) {
             // B digit (radix 256) at every even nibble position
@@ -257,11 +180,12 @@ __global__ void __launch_bounds__(256) k_ed25519_verify(const uint32_t* __restri
 
 // ---------------------------------------------------------------------------------------
 void launch_ed25519_key_prep(hipStream_t st, uint64_t n_keys, const uint8_t* key_data, const uint64_t* key_off,
-                             const uint32_t* key_len, KeyMeta* meta, uint32_t* abytes, uint32_t* table) {
+                             const uint32_t* key_len, KeyMeta* meta, uint32_t* abytes, uint32_t* table,
+                             uint32_t* nega) {
     if (!n_keys) return;
     const uint32_t blocks = (uint32_t)((n_keys + 255) / 256);
     hipLaunchKernelGGL(k_ed25519_key_prep, dim3(blocks), dim3(256), 0, st, n_keys, key_data, key_off, key_len, meta,
-                       abytes, table);
+                       abytes, table, nega);
 }
 
 void launch_ed25519_verify(hipStream_t st, uint64_t n, const uint32_t* list, const uint32_t* count,

@@ -1,0 +1,358 @@
+// ed25519_comb.hip — K1c: Ed25519 batch verification with per-key comb tables, for keys that sign
+// several signatures of a batch (every Corda party / notary key does).
+//
+// Semantics are those of k_ed25519_verify (ed25519.hip; i2p eddsa 0.2.0 EdDSAEngine.engineVerify as
+// reached from Crypto.isValid, core/.../crypto/Crypto.kt:615-625, through X509EdDSAEngine.kt:40):
+//   h = SHA-512(R || Abyte || M) mod L;  S not range checked, slide() carry drop for S >= 2^255;
+//   R' = [h](-A) + [S]B;  accept iff canonical encode(R') == R bytewise.
+// R' is a group element, so any exact schedule gives the same bytes.  This one has no doublings:
+//   [h](-A) = sum_w d_w (2^(W w) (-A)),  d_w the signed radix-2^W digits of h, read from a per-key
+//             table of ED_COMB_AWIN windows x (2^(W-1)+1) cached multiples built for the batch by
+//             k_ed_comb_chain (the W-fold doubling chain, one lane per key) and k_ed_comb_fill
+//             (the multiples, one lane per key x window);
+//   [S]B    = sum_w e_w (256^w B),       e_w the signed radix-256 digits of S, read from the fixed
+//             table ED_B_COMB (32 x 129 affine Niels rows, 528 KB, L2-resident).
+// 64 + 32 additions per signature (736 field multiplications) instead of 252 doublings + 96
+// additions (2,766).  The projective R' is inverted in batches of ED_FIN_G by k_ed_comb_finish
+// (Montgomery's trick: ~21 instead of 265 multiplications per signature).
+//
+// Work list: k_ed_comb_partition groups the signatures of one key contiguously (counting sort on
+// the key index), and k_ed_comb_verify maps consecutive blocks of the list onto one XCD, so a key's
+// 92 KB table is read from one XCD's L2.  Keys with fewer than min_sigs signatures (or beyond the
+// table budget) keep the Straus kernel.
+#include "ed_common_dev.hpp"
+#include "runtime.hpp"
+#include "comb_tables.hpp"
+
+#define ED_COMB_ABIAS (1 << (ED_COMB_W - 1))
+#define ED_COMB_ADW ((ED_COMB_AWIN + 3) / 4)   // digit words, 4 biased digits per word
+
+// signed radix-2^W digits of a (< 2^253), each biased by 2^(W-1) into one byte, NDIG digits
+template <int W, int NDIG>
+CHIP_DEV void recode_bytes(uint32_t out[(NDIG + 3) / 4], const uint32_t a[8]) {
+    int carry = 0;
+#pragma unroll
+    for (int q = 0; q < (NDIG + 3) / 4; q++) out[q] = 0;
+#pragma unroll
+    for (int d = 0; d < NDIG; d++) {
+        const int bit = d * W, wi = bit >> 5, sh = bit & 31;
+        const uint64_t two = ((uint64_t)(wi + 1 < 8 ? a[wi + 1] : 0u) << 32) | (wi < 8 ? a[wi] : 0u);
+        int v = (int)((uint32_t)(two >> sh) & ((1u << W) - 1)) + carry;
+        carry = (v + (1 << (W - 1))) >> W;
+        v -= carry << W;
+        out[d >> 2] |= (uint32_t)(v + (1 << (W - 1))) << (8 * (d & 3));
+    }
+}
+
+CHIP_DEV void ed_load_niels(ge_niels& q, const uint32_t* __restrict__ src) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(src);
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        const uint4 x = s4[k];
+        const uint32_t vals[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int idx = 4 * k + e;
+            if (idx < 10) q.ypx.v[idx] = vals[e];
+            else if (idx < 20) q.ymx.v[idx - 10] = vals[e];
+            else if (idx < 30) q.xy2d.v[idx - 20] = vals[e];
+        }
+    }
+}
+
+// ---- work list: key slots, counting sort by key ----
+// A key gets a comb slot when it is a valid Ed25519 key with at least min_sigs signatures in the
+// batch and the table budget allows; its signatures then occupy comb_list[base, base + count).
+__global__ void __launch_bounds__(256) k_ed_comb_slots(uint64_t n_keys, const KeyMeta* __restrict__ meta,
+                                                       const uint32_t* __restrict__ key_count, uint32_t min_sigs,
+                                                       uint32_t max_slots, int32_t* __restrict__ key_slot,
+                                                       uint32_t* __restrict__ key_base, uint32_t* __restrict__ slot_key,
+                                                       uint32_t* __restrict__ ctr) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_keys) return;
+    int32_t slot = -1;
+    const uint32_t c = key_count[k];
+    const KeyMeta m = meta[k];
+    if (m.scheme == CHIP_SCHEME_ED25519 && m.ok && c > 0 && c >= min_sigs) {
+        const uint32_t s = atomicAdd(&ctr[0], 1u);
+        if (s < max_slots) {
+            slot = (int32_t)s;
+            slot_key[s] = (uint32_t)k;
+            key_base[k] = atomicAdd(&ctr[1], c);
+        }
+    }
+    key_slot[k] = slot;
+}
+
+__global__ void __launch_bounds__(256) k_ed_comb_partition(const uint32_t* __restrict__ ed_list,
+                                                           const uint32_t* __restrict__ ed_count,
+                                                           const uint32_t* __restrict__ key_idx,
+                                                           const int32_t* __restrict__ key_slot,
+                                                           const uint32_t* __restrict__ key_base,
+                                                           uint32_t* __restrict__ key_cur, uint32_t* __restrict__ comb_list,
+                                                           uint32_t* __restrict__ straus_list, uint32_t* __restrict__ ctr) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    bool straus = false;
+    uint32_t i = 0;
+    if (g < *ed_count) {
+        i = ed_list[g];
+        const uint32_t k = key_idx[i];
+        if (key_slot[k] >= 0) comb_list[key_base[k] + atomicAdd(&key_cur[k], 1u)] = i;
+        else straus = true;
+    }
+    const uint64_t mask = __ballot(straus);
+    if (!mask) return;
+    const uint32_t lane = threadIdx.x & 63;
+    const uint32_t leader = (uint32_t)__builtin_ctzll(mask);
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(&ctr[2], (uint32_t)__popcll(mask));
+    base = __shfl(base, leader);
+    if (straus) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+        straus_list[base + rank] = i;
+    }
+}
+
+// ---- per-key tables ----
+// chain: P_w = 2^(W w) (-A) for every window, stashed (extended form) in row 1 of window w.
+// One lane per key: 4 (W) doublings per window, the only serial part of the comb path.
+__global__ void __launch_bounds__(64) k_ed_comb_chain(const uint32_t* __restrict__ ctr, uint32_t max_slots,
+                                                      const uint32_t* __restrict__ slot_key,
+                                                      const uint32_t* __restrict__ nega, uint32_t* __restrict__ ctab) {
+    const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t nslots = min(ctr[0], max_slots);
+    if (s >= nslots) return;
+    const uint32_t k = slot_key[s];
+    ge_p3 P;
+    ed_load_p3(P, nega + (uint64_t)k * 40);
+    uint32_t* tab = ctab + (uint64_t)s * ED_COMB_KEY_WORDS;
+    for (int w = 0; w < ED_COMB_AWIN; w++) {
+        ed_store_p3(tab + ((uint32_t)w * ED_COMB_AENT + 1) * 40, P);
+        if (w + 1 == ED_COMB_AWIN) break;
+        ge_p2 r;
+        ge_p3_to_p2(r, P);
+        ge_p1p1 t;
+#pragma unroll 1
+        for (int b = 0; b < ED_COMB_W - 1; b++) {
+            ge_p2_dbl(t, r);
+            ge_p1p1_to_p2(r, t);
+        }
+        ge_p2_dbl(t, r);
+        ge_p1p1_to_p3(P, t);
+    }
+}
+
+// fill: rows j = 0..2^(W-1) of window w: j * P_w in cached form (row 0 = identity)
+__global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict__ ctr, uint32_t max_slots,
+                                                      uint32_t* __restrict__ ctab) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t s = g / ED_COMB_AWIN, w = g % ED_COMB_AWIN;
+    if (s >= min(ctr[0], max_slots)) return;
+    uint32_t* e = ctab + (uint64_t)s * ED_COMB_KEY_WORDS + (uint64_t)w * ED_COMB_AENT * 40;
+    ge_p3 P;
+    ed_load_p3(P, e + 40);
+    ge_cached c1, c;
+    fe_1(c.YpX);
+    fe_1(c.YmX);
+    fe_1(c.Z);
+    fe_0(c.T2d);
+    ed_store_cached(e, c);
+    ge_p3_to_cached(c1, P);
+    ed_store_cached(e + 40, c1);
+    ge_p3 Q = P;
+    ge_p1p1 t;
+    for (int j = 2; j < ED_COMB_AENT; j++) {
+        ge_add_cached(t, Q, c1, false);
+        ge_p1p1_to_p3(Q, t);
+        ge_p3_to_cached(c, Q);
+        ed_store_cached(e + 40 * j, c);
+    }
+}
+
+// ---- verify: one lane per comb-list position ----
+// blocks b, b+8, b+16, ... are dispatched to one XCD: give them consecutive work (grid % 8 == 0)
+CHIP_DEV uint32_t xcd_block(uint32_t b, uint32_t nb) { return (b & 7u) * (nb >> 3) + (b >> 3); }
+
+__global__ void __launch_bounds__(256) k_ed_comb_verify(const uint32_t* __restrict__ list, const uint32_t* __restrict__ ctr,
+                                                        const uint32_t* __restrict__ key_idx,
+                                                        const uint32_t* __restrict__ msg_idx,
+                                                        const uint8_t* __restrict__ sig_data,
+                                                        const uint64_t* __restrict__ sig_off,
+                                                        const uint8_t* __restrict__ msg_data,
+                                                        const uint64_t* __restrict__ msg_off,
+                                                        const uint32_t* __restrict__ msg_len,
+                                                        const uint32_t* __restrict__ abytes,
+                                                        const int32_t* __restrict__ key_slot,
+                                                        const uint32_t* __restrict__ ctab, uint32_t* __restrict__ xyz,
+                                                        uint64_t cap) {
+    const uint32_t p = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+    if (p >= ctr[1]) return;
+    const uint32_t i = list[p];
+    const uint32_t k = key_idx[i];
+    const uint32_t mi = msg_idx[i];
+    const uint8_t* sig = sig_data + sig_off[i];
+    uint32_t R[8], S[8], Ab[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) {
+        R[q] = ld_le32(sig + 4 * q);
+        S[q] = ld_le32(sig + 32 + 4 * q);
+        Ab[q] = abytes[(uint64_t)k * 8 + q];
+    }
+    uint32_t hx[16], h[8], s[8];
+    ed_challenge(hx, R, Ab, msg_data + msg_off[mi], msg_len[mi]);
+    sc_reduce512(h, hx);
+    ed_effective_s(s, S);
+    uint32_t da[ED_COMB_ADW], db[8];
+    recode_bytes<ED_COMB_W, ED_COMB_AWIN>(da, h);
+    recode_bytes<8, 32>(db, s);
+    const uint32_t* tab = ctab + (uint64_t)key_slot[k] * ED_COMB_KEY_WORDS;
+
+    // [h](-A): one cached addition per window (extended coordinates, unified = complete formulas)
+    ge_p3 u;
+    ge_p3_0(u);
+    ge_p1p1 t;
+    ge_cached ca;
+    for (int wd = 0; wd < ED_COMB_ADW; wd++) {
+        const uint32_t cur = da[0];
+#pragma unroll
+        for (int q = 0; q < ED_COMB_ADW - 1; q++) da[q] = da[q + 1];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int w = wd * 4 + e;
+            if (w < ED_COMB_AWIN) {
+                const int d = (int)((cur >> (8 * e)) & 0xffu) - ED_COMB_ABIAS;
+                const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+                ed_load_cached(ca, tab + ((uint32_t)w * ED_COMB_AENT + ad) * 40);
+                if (w > 0) ge_p1p1_to_p3(u, t);
+                ge_add_cached(t, u, ca, d < 0);
+            }
+        }
+    }
+    // [S]B: one mixed (affine Niels) addition per window; the accumulator carries 2Z for madd
+    fe z2;
+    fe_mul(u.X, t.X, t.T);
+    fe_mul(u.Y, t.Z, t.Y);
+    fe_mul2(z2, t.Z, t.T);
+    fe_mul(u.T, t.X, t.Y);
+    ge_niels nb;
+    for (int wd = 0; wd < 8; wd++) {
+        const uint32_t cur = db[0];
+#pragma unroll
+        for (int q = 0; q < 7; q++) db[q] = db[q + 1];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int w = wd * 4 + e;
+            const int d = (int)((cur >> (8 * e)) & 0xffu) - 128;
+            const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+            ed_load_niels(nb, ED_B_COMB + ((uint32_t)w * ED_COMB_BENT + ad) * ED_COMB_BSTRIDE);
+            if (w > 0) {
+                fe_mul(u.X, t.X, t.T);
+                fe_mul(u.Y, t.Z, t.Y);
+                fe_mul2(z2, t.Z, t.T);
+                fe_mul(u.T, t.X, t.Y);
+            }
+            ge_madd(t, u, z2, nb, d < 0);
+        }
+    }
+    // projective R' = (X : Y : Z), stored structure-of-arrays for the finish kernel
+    fe X, Y, Z;
+    fe_mul(X, t.X, t.T);
+    fe_mul(Y, t.Z, t.Y);
+    fe_mul(Z, t.Z, t.T);
+#pragma unroll
+    for (int q = 0; q < 10; q++) {
+        xyz[(uint64_t)q * cap + p] = X.v[q];
+        xyz[(uint64_t)(10 + q) * cap + p] = Y.v[q];
+        xyz[(uint64_t)(20 + q) * cap + p] = Z.v[q];
+    }
+}
+
+// ---- finish: batched inversion of Z, canonical encoding, compare with R ----
+// Lane l owns positions l, l + lanes, l + 2 lanes, ... (coalesced SoA reads).  Z != 0 always: the
+// unified Edwards formulas are complete for a = -1, d non-square, and A, B are curve points.
+CHIP_DEV void ld_fe_soa(fe& f, const uint32_t* __restrict__ base, uint64_t cap, uint64_t p) {
+#pragma unroll
+    for (int q = 0; q < 10; q++) f.v[q] = base[(uint64_t)q * cap + p];
+}
+__global__ void __launch_bounds__(256) k_ed_comb_finish(const uint32_t* __restrict__ list, const uint32_t* __restrict__ ctr,
+                                                        const uint8_t* __restrict__ sig_data,
+                                                        const uint64_t* __restrict__ sig_off,
+                                                        const uint32_t* __restrict__ xyz, uint32_t* __restrict__ zpre,
+                                                        uint64_t cap, uint8_t* __restrict__ status) {
+    const uint32_t n = ctr[1];
+    const uint32_t lanes = (n + ED_FIN_G - 1) / ED_FIN_G;
+    const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
+    if (l >= lanes) return;
+    const uint32_t ne = min((uint32_t)ED_FIN_G, (n - l + lanes - 1) / lanes);
+    const uint32_t* Zs = xyz + 20 * cap;
+    fe acc, z;
+    for (uint32_t e = 0; e < ne; e++) {
+        const uint64_t p = l + (uint64_t)e * lanes;
+        ld_fe_soa(z, Zs, cap, p);
+        if (e == 0) acc = z;
+        else fe_mul(acc, acc, z);
+#pragma unroll
+        for (int q = 0; q < 10; q++) zpre[(uint64_t)q * cap + p] = acc.v[q];
+    }
+    fe inv;
+    fe_invert(inv, acc);
+    for (int e = (int)ne - 1; e >= 0; e--) {
+        const uint64_t p = l + (uint64_t)e * lanes;
+        fe zi;
+        if (e > 0) {
+            fe prev;
+            ld_fe_soa(prev, zpre, cap, p - lanes);
+            fe_mul(zi, inv, prev);
+            ld_fe_soa(z, Zs, cap, p);
+            fe_mul(inv, inv, z);
+        } else {
+            zi = inv;
+        }
+        fe X, Y, x, y;
+        ld_fe_soa(X, xyz, cap, p);
+        ld_fe_soa(Y, xyz + 10 * cap, cap, p);
+        fe_mul(x, X, zi);
+        fe_mul(y, Y, zi);
+        uint32_t enc[8];
+        fe_tobytes(enc, y);
+        enc[7] |= fe_isnegative(x) << 31;
+        const uint32_t i = list[p];
+        const uint8_t* sig = sig_data + sig_off[i];
+        bool eq = true;
+#pragma unroll
+        for (int q = 0; q < 8; q++) eq = eq && (enc[q] == ld_le32(sig + 4 * q));
+        status[i] = eq ? CHIP_VALID : CHIP_INVALID;
+    }
+}
+
+// ---------------------------------------------------------------------------------------
+static inline uint32_t nblk(uint64_t n, uint32_t bs) { return (uint32_t)((n + bs - 1) / bs); }
+
+void launch_ed_comb_tables(hipStream_t st, uint64_t n, uint64_t n_keys, const uint32_t* ed_list,
+                           const uint32_t* ed_count, const chip_sig_batch* b, const KeyMeta* meta, const EdCombWs& w) {
+    if (!n || !n_keys) return;
+    hipLaunchKernelGGL(k_ed_comb_slots, dim3(nblk(n_keys, 256)), dim3(256), 0, st, n_keys, meta, w.key_count,
+                       w.min_sigs, w.max_slots, w.key_slot, w.key_base, w.slot_key, w.ctr);
+    hipLaunchKernelGGL(k_ed_comb_partition, dim3(nblk(n, 256)), dim3(256), 0, st, ed_list, ed_count, b->key_idx,
+                       w.key_slot, w.key_base, w.key_cur, w.comb_list, w.straus_list, w.ctr);
+    if (!w.max_slots) return;
+    hipLaunchKernelGGL(k_ed_comb_chain, dim3(nblk(w.max_slots, 64)), dim3(64), 0, st, w.ctr, w.max_slots, w.slot_key,
+                       w.nega, w.ctab);
+    hipLaunchKernelGGL(k_ed_comb_fill, dim3(nblk((uint64_t)w.max_slots * ED_COMB_AWIN, 256)), dim3(256), 0, st, w.ctr,
+                       w.max_slots, w.ctab);
+}
+
+void launch_ed_comb_verify(hipStream_t st, uint64_t n, const chip_sig_batch* b, const uint32_t* abytes,
+                           const EdCombWs& w) {
+    if (!n || !w.max_slots) return;
+    const uint32_t blocks = (nblk(n, 256) + 7) & ~7u;   // multiple of 8 for the XCD remap
+    hipLaunchKernelGGL(k_ed_comb_verify, dim3(blocks), dim3(256), 0, st, w.comb_list, w.ctr, b->key_idx, b->msg_idx,
+                       b->sig_data, b->sig_off, b->msg_data, b->msg_off, b->msg_len, abytes, w.key_slot, w.ctab, w.xyz,
+                       (uint64_t)n);
+}
+
+void launch_ed_comb_finish(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w, uint8_t* status) {
+    if (!n || !w.max_slots) return;
+    hipLaunchKernelGGL(k_ed_comb_finish, dim3(nblk((n + ED_FIN_G - 1) / ED_FIN_G, 256)), dim3(256), 0, st, w.comb_list,
+                       w.ctr, b->sig_data, b->sig_off, w.xyz, w.zpre, (uint64_t)n, status);
+}

@@ -11,6 +11,8 @@
 #include <vector>
 #include <cstring>
 #include <cstdio>
+#include <cstdlib>
+#include <algorithm>
 #include "runtime.hpp"
 
 struct DevBuf {
@@ -36,11 +38,17 @@ struct DevBuf {
 
 struct chip_ctx {
     int device = 0;
+    uint32_t flags = 0;
+    uint32_t comb_min_sigs = 4;                   // Ed25519 comb threshold (signatures per key)
+    uint64_t comb_budget = 8ull << 30;            // bytes of per-key comb tables
     hipStream_t stream = nullptr;
     std::mutex mu;
     std::string err;
     // verify workspaces
     DevBuf meta, abytes, edtab, ectab, lists, counts;
+    // Ed25519 comb path
+    DevBuf c_key_count, c_key_slot, c_key_base, c_key_cur, c_slot_key, c_ctr, c_comb_list, c_straus_list, c_ctab,
+        c_xyz, c_zpre, c_nega;
     // host-path mirrors of the caller's buffers
     DevBuf h_key_idx, h_msg_idx, h_sig_data, h_sig_off, h_sig_len, h_key_data, h_key_off, h_key_len, h_msg_data,
         h_msg_off, h_msg_len, h_status, h_bitmap;
@@ -110,7 +118,7 @@ __global__ void __launch_bounds__(256) k_classify(uint64_t n, const uint32_t* __
                                                   const uint32_t* __restrict__ msg_len, uint64_t n_keys,
                                                   uint64_t n_msgs, const KeyMeta* __restrict__ meta,
                                                   uint8_t* __restrict__ status, uint32_t* __restrict__ lists,
-                                                  uint32_t* __restrict__ counts) {
+                                                  uint32_t* __restrict__ counts, uint32_t* __restrict__ key_count) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     int list = -1;
     if (i < n) {
@@ -127,6 +135,7 @@ __global__ void __launch_bounds__(256) k_classify(uint64_t n, const uint32_t* __
             else if (!km.ok) st = CHIP_KEY_INVALID;             // key never constructible
             else if (km.scheme == CHIP_SCHEME_ED25519 && sl != 64) st = CHIP_SIG_DECODE;  // length is wrong
             else list = km.scheme == CHIP_SCHEME_ED25519 ? LIST_ED25519 : (km.scheme == CHIP_SCHEME_R1 ? LIST_R1 : LIST_K1);
+            if (list == LIST_ED25519 && key_count) atomicAdd(&key_count[k], 1u);   // comb-path histogram
         }
         if (list < 0) status[i] = st;
     }
@@ -190,6 +199,10 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
         delete c;
         return CHIP_E_DEVICE;
     }
+    if (cfg) c->flags = cfg->flags;
+    if (c->flags & CHIP_FLAG_FORCE_COMB) c->comb_min_sigs = 1;
+    if (const char* e = getenv("CHIP_COMB_MIN_SIGS")) c->comb_min_sigs = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("CHIP_COMB_BUDGET_MB")) c->comb_budget = (uint64_t)strtoull(e, nullptr, 10) << 20;
     if (cfg && cfg->reserve_sigs) {
         (void)c->lists.ensure(cfg->reserve_sigs * 4 * N_LISTS);
     }
@@ -201,7 +214,9 @@ void chip_shutdown(chip_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->meta, &c->abytes, &c->edtab, &c->ectab, &c->lists, &c->counts, &c->h_key_idx, &c->h_msg_idx,
+    DevBuf* bufs[] = {&c->meta, &c->abytes, &c->edtab, &c->ectab, &c->lists, &c->counts, &c->c_key_count,
+                      &c->c_key_slot, &c->c_key_base, &c->c_key_cur, &c->c_slot_key, &c->c_ctr, &c->c_comb_list,
+                      &c->c_straus_list, &c->c_ctab, &c->c_xyz, &c->c_zpre, &c->c_nega, &c->h_key_idx, &c->h_msg_idx,
                       &c->h_sig_data, &c->h_sig_off, &c->h_sig_len, &c->h_key_data, &c->h_key_off, &c->h_key_len,
                       &c->h_msg_data, &c->h_msg_off, &c->h_msg_len, &c->h_status, &c->h_bitmap, &c->t_salts,
                       &c->t_start, &c->t_group, &c->t_internal, &c->t_data, &c->t_off, &c->t_len, &c->t_ids,
@@ -231,13 +246,53 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     HIPCHK(c, c->ectab.ensure(nk * EC_KEY_TABLE_WORDS * 4 + 16));
     HIPCHK(c, c->lists.ensure(n * 4 * N_LISTS + 16));
     HIPCHK(c, c->counts.ensure(64));
+    // Ed25519 comb workspaces: slots <= min(keys, signatures / threshold, table budget)
+    const bool comb = !(c->flags & CHIP_FLAG_NO_COMB) && n && nk;
+    EdCombWs w{};
+    if (comb) {
+        const uint64_t key_bytes = (uint64_t)ED_COMB_KEY_WORDS * 4;
+        uint64_t slots = nk;
+        slots = std::min<uint64_t>(slots, n / std::max<uint32_t>(1u, c->comb_min_sigs));
+        slots = std::min<uint64_t>(slots, c->comb_budget / key_bytes);
+        HIPCHK(c, c->c_key_count.ensure(nk * 4 + 16));
+        HIPCHK(c, c->c_key_slot.ensure(nk * 4 + 16));
+        HIPCHK(c, c->c_key_base.ensure(nk * 4 + 16));
+        HIPCHK(c, c->c_key_cur.ensure(nk * 4 + 16));
+        HIPCHK(c, c->c_slot_key.ensure(slots * 4 + 16));
+        HIPCHK(c, c->c_ctr.ensure(64));
+        HIPCHK(c, c->c_comb_list.ensure(n * 4 + 16));
+        HIPCHK(c, c->c_straus_list.ensure(n * 4 + 16));
+        HIPCHK(c, c->c_ctab.ensure(slots * key_bytes + 16));
+        HIPCHK(c, c->c_xyz.ensure(n * 30 * 4 + 16));
+        HIPCHK(c, c->c_zpre.ensure(n * 10 * 4 + 16));
+        HIPCHK(c, c->c_nega.ensure(nk * 40 * 4 + 16));
+        w.key_count = c->c_key_count.as<uint32_t>();
+        w.key_slot = c->c_key_slot.as<int32_t>();
+        w.key_base = c->c_key_base.as<uint32_t>();
+        w.key_cur = c->c_key_cur.as<uint32_t>();
+        w.slot_key = c->c_slot_key.as<uint32_t>();
+        w.ctr = c->c_ctr.as<uint32_t>();
+        w.comb_list = c->c_comb_list.as<uint32_t>();
+        w.straus_list = c->c_straus_list.as<uint32_t>();
+        w.ctab = c->c_ctab.as<uint32_t>();
+        w.xyz = c->c_xyz.as<uint32_t>();
+        w.zpre = c->c_zpre.as<uint32_t>();
+        w.nega = c->c_nega.as<uint32_t>();
+        w.max_slots = (uint32_t)slots;
+        w.min_sigs = c->comb_min_sigs;
+    }
     HIPCHK(c, hipEventRecord(c->ev0, st));
     HIPCHK(c, hipMemsetAsync(c->counts.p, 0, 64, st));
     if (nk) HIPCHK(c, hipMemsetAsync(c->meta.p, 0, nk * sizeof(KeyMeta), st));
+    if (comb) {
+        HIPCHK(c, hipMemsetAsync(w.ctr, 0, 64, st));
+        HIPCHK(c, hipMemsetAsync(w.key_count, 0, nk * 4, st));
+        HIPCHK(c, hipMemsetAsync(w.key_cur, 0, nk * 4, st));
+    }
     KeyMeta* meta = c->meta.as<KeyMeta>();
     int ke = c->kbegin(CHIP_K_KEYPREP, st);
     launch_ed25519_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->abytes.as<uint32_t>(),
-                            c->edtab.as<uint32_t>());
+                            c->edtab.as<uint32_t>(), comb ? w.nega : nullptr);
     launch_ecdsa_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->ectab.as<uint32_t>());
     c->kend(ke, st);
     if (n) {
@@ -245,10 +300,24 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         uint32_t* lists = c->lists.as<uint32_t>();
         uint32_t* counts = c->counts.as<uint32_t>();
         hipLaunchKernelGGL(k_classify, dim3(blocks), dim3(256), 0, st, n, b->key_idx, b->msg_idx, b->sig_len, b->msg_len,
-                           nk, b->n_msgs, meta, status, lists, counts);
+                           nk, b->n_msgs, meta, status, lists, counts, comb ? w.key_count : nullptr);
+        const uint32_t* ed_list = lists + (uint64_t)LIST_ED25519 * n;
+        const uint32_t* ed_count = counts + LIST_ED25519;
+        if (comb) {
+            ke = c->kbegin(CHIP_K_ED_TABLES, st);
+            launch_ed_comb_tables(st, n, nk, ed_list, ed_count, b, meta, w);
+            c->kend(ke, st);
+            ke = c->kbegin(CHIP_K_ED_COMB, st);
+            launch_ed_comb_verify(st, n, b, c->abytes.as<uint32_t>(), w);
+            c->kend(ke, st);
+            ke = c->kbegin(CHIP_K_ED_FINISH, st);
+            launch_ed_comb_finish(st, n, b, w, status);
+            c->kend(ke, st);
+            ed_list = w.straus_list;
+            ed_count = w.ctr + 2;
+        }
         ke = c->kbegin(CHIP_K_ED25519, st);
-        launch_ed25519_verify(st, n, lists + (uint64_t)LIST_ED25519 * n, counts + LIST_ED25519, b,
-                              c->abytes.as<uint32_t>(), c->edtab.as<uint32_t>(), status);
+        launch_ed25519_verify(st, n, ed_list, ed_count, b, c->abytes.as<uint32_t>(), c->edtab.as<uint32_t>(), status);
         c->kend(ke, st);
         ke = c->kbegin(CHIP_K_ECDSA_R1, st);
         launch_ecdsa_verify(st, CHIP_SCHEME_R1, n, lists + (uint64_t)LIST_R1 * n, counts + LIST_R1, b,

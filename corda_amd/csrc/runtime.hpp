@@ -7,7 +7,8 @@
 enum { LIST_ED25519 = 0, LIST_R1 = 1, LIST_K1 = 2, N_LISTS = 3 };
 
 void launch_ed25519_key_prep(hipStream_t st, uint64_t n_keys, const uint8_t* key_data, const uint64_t* key_off,
-                             const uint32_t* key_len, KeyMeta* meta, uint32_t* abytes, uint32_t* table);
+                             const uint32_t* key_len, KeyMeta* meta, uint32_t* abytes, uint32_t* table,
+                             uint32_t* nega);
 void launch_ed25519_verify(hipStream_t st, uint64_t n, const uint32_t* list, const uint32_t* count,
                            const chip_sig_batch* b, const uint32_t* abytes, const uint32_t* table, uint8_t* status);
 
@@ -21,3 +22,35 @@ void launch_txid(hipStream_t st, const chip_tx_batch* b, uint8_t* ids, uint32_t*
 // sizes of the per-key device tables (words per key)
 #define ED_KEY_TABLE_WORDS (9 * 40)
 #define EC_KEY_TABLE_WORDS (9 * 16 + 16)
+
+// ---- Ed25519 per-key comb path (ed25519_comb.hip) ----
+// A comb geometry: signed radix-2^ED_COMB_W digits of h (< L < 2^253), one table window per digit
+#ifndef ED_COMB_W
+#define ED_COMB_W 4
+#endif
+#define ED_COMB_AWIN ((253 + ED_COMB_W - 1) / ED_COMB_W)   // W=4: 64 windows (top digit <= 2)
+#define ED_COMB_AENT ((1 << (ED_COMB_W - 1)) + 1)          // multiples 0..2^(W-1)
+#define ED_COMB_KEY_WORDS (ED_COMB_AWIN * ED_COMB_AENT * 40)
+#define ED_FIN_G 16                                        // signatures per batched inversion
+
+struct EdCombWs {
+    uint32_t* key_count;    // [n_keys] Ed25519 signatures per key needing arithmetic (k_classify)
+    int32_t* key_slot;      // [n_keys] comb-table slot or -1 (Straus path)
+    uint32_t* key_base;     // [n_keys] first position of the key's signatures in comb_list
+    uint32_t* key_cur;      // [n_keys] fill cursor (zeroed per batch)
+    uint32_t* slot_key;     // [max_slots]
+    uint32_t* ctr;          // [0] slots claimed, [1] comb signatures, [2] Straus signatures
+    uint32_t* comb_list;    // [n] signature indices grouped by key
+    uint32_t* straus_list;  // [n]
+    uint32_t* ctab;         // [max_slots][ED_COMB_KEY_WORDS]
+    uint32_t* xyz;          // [30][n] projective R' (SoA), comb path
+    uint32_t* zpre;         // [10][n] prefix products of the batched inversion
+    uint32_t* nega;         // [n_keys][40] -A in extended coordinates (key prep)
+    uint32_t max_slots, min_sigs;
+};
+
+void launch_ed_comb_tables(hipStream_t st, uint64_t n, uint64_t n_keys, const uint32_t* ed_list,
+                           const uint32_t* ed_count, const chip_sig_batch* b, const KeyMeta* meta, const EdCombWs& w);
+void launch_ed_comb_verify(hipStream_t st, uint64_t n, const chip_sig_batch* b, const uint32_t* abytes,
+                           const EdCombWs& w);
+void launch_ed_comb_finish(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w, uint8_t* status);

@@ -66,7 +66,8 @@ class ChipConflict(ctypes.Structure):
                 ("pad", ctypes.c_uint32)]
 
 
-K_ED25519, K_ECDSA_R1, K_ECDSA_K1, K_TXID, K_KEYPREP, K_UNIQ, N_KERNELS = range(7)
+K_ED25519, K_ECDSA_R1, K_ECDSA_K1, K_TXID, K_KEYPREP, K_UNIQ, K_ED_COMB, K_ED_FINISH, K_ED_TABLES, N_KERNELS = range(10)
+FLAG_NO_COMB, FLAG_FORCE_COMB = 0x1, 0x2
 
 
 class ChipStats(ctypes.Structure):
@@ -165,9 +166,9 @@ def make_tx_batch(t) -> ChipTxBatch:
 class Context:
     """One libcordahip context = one GPU (one process per GPU)."""
 
-    def __init__(self, device: int = 0, reserve_sigs: int = 0):
+    def __init__(self, device: int = 0, reserve_sigs: int = 0, flags: int = 0):
         self.lib = load()
-        cfg = ChipConfig(device, 0, reserve_sigs)
+        cfg = ChipConfig(device, flags, reserve_sigs)
         h = ctypes.c_void_p()
         rc = self.lib.chip_init(ctypes.byref(cfg), ctypes.byref(h))
         if rc != 0:

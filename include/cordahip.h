@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define CHIP_ABI_VERSION 1
+#define CHIP_ABI_VERSION 2
 
 enum chip_sig_status {
     CHIP_VALID = 0,
@@ -72,9 +72,15 @@ typedef struct chip_ctx chip_ctx;
 
 typedef struct {
     int device;             /* HIP device ordinal for this context (one context per GPU)   */
-    uint32_t flags;         /* reserved, 0                                                  */
+    uint32_t flags;         /* CHIP_FLAG_* (0 = defaults)                                   */
     uint64_t reserve_sigs;  /* optional: pre-size workspaces for this many signatures      */
 } chip_config;
+
+/* Ed25519 schedule policy.  By default a key with at least 4 signatures needing arithmetic in a
+ * batch gets a per-key comb table (no doublings per signature; ed25519_comb.hip), the others the
+ * windowed Straus kernel.  Results are identical either way; the flags exist for tests/benchmarks. */
+#define CHIP_FLAG_NO_COMB 0x1u      /* every key on the Straus kernel                  */
+#define CHIP_FLAG_FORCE_COMB 0x2u   /* every key on the comb kernel (threshold 1)      */
 
 int chip_abi_version(void);
 int chip_device_count(void);
@@ -180,7 +186,8 @@ int chip_uniq_commit_batch(chip_uniq* u, uint64_t ntx, const uint64_t* tx_ref_st
 /* ---------------------------------------------------------------------------------------
  * Counters (observability; OutOfProcessTransactionVerifierService.kt:35-46 analogue). */
 enum chip_kernel { CHIP_K_ED25519 = 0, CHIP_K_ECDSA_R1 = 1, CHIP_K_ECDSA_K1 = 2, CHIP_K_TXID = 3,
-                   CHIP_K_KEYPREP = 4, CHIP_K_UNIQ = 5, CHIP_N_KERNELS = 6 };
+                   CHIP_K_KEYPREP = 4, CHIP_K_UNIQ = 5, CHIP_K_ED_COMB = 6, CHIP_K_ED_FINISH = 7,
+                   CHIP_K_ED_TABLES = 8, CHIP_N_KERNELS = 9 };
 typedef struct {
     uint64_t batches, sigs, keys_prepared;
     uint64_t status_count[8];

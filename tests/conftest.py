@@ -27,3 +27,16 @@ def oracle():
     import oracle_bind
     oracle_bind.lib()
     return oracle_bind
+
+
+@pytest.fixture(scope="session")
+def ctx_modes():
+    """Contexts for each Ed25519 schedule: default policy, every key on the per-key comb, every key
+    on the windowed Straus kernel.  Results must be identical (bit-exact status bytes)."""
+    import corda_amd
+    from corda_amd import native
+    cs = {"default": corda_amd.Context(0), "comb": corda_amd.Context(0, flags=native.FLAG_FORCE_COMB),
+          "straus": corda_amd.Context(0, flags=native.FLAG_NO_COMB)}
+    yield cs
+    for c in cs.values():
+        c.close()

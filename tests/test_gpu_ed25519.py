@@ -20,7 +20,12 @@ def bitmap_of(status):
     return words
 
 
-def test_ed25519_batch_matches_oracle(ctx, oracle):
+MODES = ["default", "comb", "straus"]
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_ed25519_batch_matches_oracle(ctx_modes, oracle, mode):
+    ctx = ctx_modes[mode]
     b = G.ed25519_batch(3000, n_keys=64, corrupt=0.4, seed=11)
     st, bm = ctx.verify_batch(b)
     ref = oracle.verify_batch(b, threads=8)
@@ -30,8 +35,10 @@ def test_ed25519_batch_matches_oracle(ctx, oracle):
     assert np.array_equal(bm, bitmap_of(ref))
 
 
-def test_ed25519_edge_cases(ctx, oracle):
+@pytest.mark.parametrize("mode", MODES)
+def test_ed25519_edge_cases(ctx_modes, oracle, mode):
     import golden_cases
+    ctx = ctx_modes[mode]
     b = golden_cases.ed25519_edge_batch()
     st, _ = ctx.verify_batch(b)
     ref = oracle.verify_batch(b)
@@ -39,8 +46,10 @@ def test_ed25519_edge_cases(ctx, oracle):
     assert st.tolist() == b.expected.tolist()
 
 
+@pytest.mark.parametrize("mode", ["comb", "straus"])
 @pytest.mark.parametrize("msg_len", [1, 55, 56, 63, 64, 111, 112, 127, 128, 200, 1000])
-def test_ed25519_message_lengths(ctx, oracle, msg_len):
+def test_ed25519_message_lengths(ctx_modes, oracle, msg_len, mode):
+    ctx = ctx_modes[mode]
     # SHA-512 block boundaries (64 + |M| + 17 crossing 128-byte multiples)
     seed = hashlib.sha256(b"len%d" % msg_len).digest()
     a = G.ed25519_pub(seed)
@@ -63,3 +72,25 @@ def test_ed25519_message_lengths(ctx, oracle, msg_len):
     ref = oracle.verify_batch(b)
     assert st.tolist() == ref.tolist()
     assert st.tolist() == [1 if j % 3 == 1 else 0 for j in range(64)]
+
+
+def test_ed25519_mixed_policy_large(ctx_modes):
+    """200k signatures with a skewed key distribution (hot keys on the comb, singletons on Straus in
+    the default policy): every schedule gives the labels' status bytes."""
+    b = G.ed25519_batch(200_000, n_keys=20_000, corrupt=0.1, seed=77)
+    outs = {m: ctx_modes[m].verify_batch(b)[0] for m in MODES}
+    for m in MODES:
+        assert np.array_equal(outs[m], b.expected), m
+
+
+def test_ed25519_comb_stats(ctx_modes):
+    """The default policy routes repeated keys through the comb kernels (native path observable)."""
+    from corda_amd import native
+    c = ctx_modes["default"]
+    c.reset_stats()
+    b = G.ed25519_batch(4096, n_keys=16, corrupt=0.1, seed=5)
+    st, _ = c.verify_batch(b)
+    assert np.array_equal(st, b.expected)
+    s = c.stats()
+    assert s.kernel_launches[native.K_ED_COMB] >= 1
+    assert s.kernel_launches[native.K_ED_FINISH] >= 1
