@@ -4,47 +4,94 @@
 //   TrustedAuthorityNotaryService.commitInputStates   core/.../node/services/NotaryService.kt:61-75
 // applied to a batch of transactions as if they were committed one after another in batch order.
 //
-// Table: open addressing (linear probing) in HBM, load factor <= 1/2, slots of
-//   key  = 36-byte StateRef (32-byte txhash || LE u32 index), 9 words
-//   val  = consuming tx id (8 words) || inputIndex || caller, 10 words
-//   used = u32 flag
-// Batch algorithm ("ordered-commit rounds", exact sequential semantics):
-//   1. lookup every input in the table (pre-committed?)                      k_uniq_lookup
-//   2. intern every distinct state of the batch in a scratch table           k_uniq_intern
-//   3. rounds until every tx is decided:                                     k_uniq_round_min / k_uniq_decide
-//        first(s) = min tx index among the still-live (undecided or committed) referencers of s;
-//        tx t commits when no input is pre-committed and first(s) == t for every input s;
-//        t fails when an input is pre-committed or first(s) is an earlier COMMITTED tx;
-//        otherwise t waits for an earlier undecided referencer.
-//      A failed tx inserts nothing, so later txs may still consume its inputs (tx1{a}, tx2{a,b},
-//      tx3{b} -> tx1 ok, tx2 conflict, tx3 ok).  The globally smallest undecided tx is decided in
-//      every round, and a sparse conflict graph settles in a few rounds.
-//   4. failed txs are IDEMPOTENT when every consumed input was consumed by (txId, i, caller)
-//      itself, else CONFLICT; either way the UniquenessException's Conflict.stateHistory is
-//      emitted: one record per consumed distinct input                       k_uniq_classify
-//   5. committed inputs are inserted (first index wins for an input repeated in one tx)  k_uniq_insert
+// Table: open addressing (linear probing) in HBM, load factor <= 1/2, one 128-byte slot per
+// StateRef (= one L2 line; a probe touches one line and compares in registers):
+//   words [0..8]   key  = 36-byte StateRef (32-byte txhash || LE u32 index)
+//   word  [9]      used flag (claimed with one CAS)
+//   words [10..17] ConsumingTx.id, [18] ConsumingTx.inputIndex, [19] requestingParty (interned)
+//
+// Batch algorithm ("ordered-commit rounds", exact sequential semantics).  One shard = the slice of
+// the key space one GPU owns (all of it on a single GPU).  A shard sees every transaction of the
+// batch but only its own inputs ("local refs", grouped by tx, each carrying its position in the
+// tx's input list):
+//   begin     lookup every local input in the table (pre-committed?)               k_uniq_lookup
+//             intern the distinct states of the batch in a scratch table            k_uniq_intern
+//   rounds    vote: first(s) = min tx among the live (not failed) referencers of s; k_uniq_round_min
+//                   for every undecided tx t: 2 (fail) when a local input is pre-committed or
+//                   first(s) is an earlier COMMITTED tx, else 1 (wait) when first(s) is an earlier
+//                   undecided tx, else 0 (commit as far as this shard knows)          k_uniq_vote
+//             decision = max over shards (RCCL all-reduce MAX on u8 across GPUs; identity on one)
+//             apply: 0 -> COMMITTED (records its inputs' consumer), 2 -> FAILED, 1 -> next round
+//                                                                                    k_uniq_apply
+//             A failed tx inserts nothing, so later txs may still consume its inputs (tx1{a},
+//             tx2{a,b}, tx3{b} -> tx1 ok, tx2 conflict, tx3 ok).  The smallest undecided tx is
+//             decided in every round, and a sparse conflict graph settles in a few rounds.
+//   classify  failed tx: 2 (CONFLICT) when some consumed input was consumed by anything but
+//             (txId, i, caller), else 1 (IDEMPOTENT); decision = max over shards  k_uniq_classify
+//   finish    Conflict.stateHistory records (one per consumed distinct input, ordered by
+//             (tx, input index) through a prefix sum), inserts of committed txs (first index of a
+//             repeated input wins), final status bytes       k_uniq_flag / k_uniq_emit / k_uniq_insert
 #include <mutex>
 #include <string>
 #include <vector>
 #include <algorithm>
+#include <hipcub/hipcub.hpp>
 #include "runtime.hpp"
 
-#define KW 9    // key words
-#define VW 10   // value words
+#define KW 9          // key words
+#define SLOT_W 32     // words per slot (128 B)
+#define S_USED 9
+#define S_VAL 10      // tx id (8 words), inputIndex, caller
 #define ST_UNDECIDED 0xffu
 #define ST_COMMITTED 0x10u
 #define ST_FAILED 0x20u
+#define NO_SLOT 0xffffffffu
+
+namespace {
+
+struct UBuf {
+    void* p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes) {
+        if (bytes <= cap) return hipSuccess;
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = bytes + bytes / 4 + 256;
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess) cap = want;
+        return e;
+    }
+    void release() {
+        if (p) hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+    template <class T> T* as() const { return reinterpret_cast<T*>(p); }
+};
+
+}  // namespace
 
 struct chip_uniq {
     chip_ctx* ctx = nullptr;
     int device = 0;
     hipStream_t stream = nullptr;
     uint64_t cap = 0, size = 0;
-    uint32_t *key = nullptr, *val = nullptr, *used = nullptr;
-    // batch scratch
-    void* scratch = nullptr;
-    size_t scratch_cap = 0;
+    uint32_t* tab = nullptr;   // [cap][SLOT_W]
     std::string err;
+    // batch in flight (between shard_begin and shard_finish)
+    bool open = false;
+    uint64_t ntx = 0, nref = 0, bcap = 0;
+    hipStream_t bst = nullptr;
+    const uint64_t* start = nullptr;
+    const uint8_t* refs = nullptr;
+    const uint32_t* pos = nullptr;
+    const uint8_t* ids = nullptr;
+    const uint32_t* callers = nullptr;
+    // scratch
+    UBuf reftx, pre, bslot, bowner, bmin, bcommit, st, flag, scan, cub, ctr, refpos;
+    // staging of the host entry points
+    UBuf h_start, h_refs, h_ids, h_call, h_st, h_vote, h_out;
 };
 
 CHIP_DEV uint32_t fmix32(uint32_t h) {
@@ -72,76 +119,54 @@ CHIP_DEV bool key_eq(const uint32_t* a, const uint32_t k[KW]) {
     return d == 0;
 }
 
-// ---- persistent table ----
-// probe: slot index of k or -1
-CHIP_DEV int64_t tab_find(const uint32_t* key, const uint32_t* used, uint64_t cap, const uint32_t k[KW]) {
+// probe: slot index of k or NO_SLOT.  A slot's first 40 bytes (key + used) are read as 2x16 B + 8 B.
+CHIP_DEV uint32_t tab_find(const uint32_t* __restrict__ tab, uint64_t cap, const uint32_t k[KW]) {
     uint64_t i = key_hash(k) & (cap - 1);
     for (uint64_t n = 0; n < cap; n++) {
-        if (!__hip_atomic_load(&used[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) return -1;
-        if (key_eq(key + i * KW, k)) return (int64_t)i;
+        const uint32_t* s = tab + i * SLOT_W;
+        const uint4 a = *reinterpret_cast<const uint4*>(s);
+        const uint4 b = *reinterpret_cast<const uint4*>(s + 4);
+        const uint2 c = *reinterpret_cast<const uint2*>(s + 8);
+        if (!c.y) return NO_SLOT;
+        const uint32_t d = (a.x ^ k[0]) | (a.y ^ k[1]) | (a.z ^ k[2]) | (a.w ^ k[3]) | (b.x ^ k[4]) | (b.y ^ k[5]) |
+                           (b.z ^ k[6]) | (b.w ^ k[7]) | (c.x ^ k[8]);
+        if (!d) return (uint32_t)i;
         i = (i + 1) & (cap - 1);
     }
-    return -1;
+    return NO_SLOT;
 }
 
-__global__ void k_uniq_lookup(uint64_t nref, const uint8_t* __restrict__ refs, const uint32_t* __restrict__ key,
-                              const uint32_t* __restrict__ used, uint64_t cap, int64_t* __restrict__ pre) {
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nref) return;
-    uint32_t k[KW];
-    load_key(k, refs, r);
-    pre[r] = tab_find(key, used, cap, k);
-}
-
-// insert (key -> val) for the refs selected by `want` (keys guaranteed absent from the table and
-// distinct among the selected refs, so a slot is claimed with one CAS and never compared)
-//   commit path: refs of COMMITTED txs, first occurrence of a state inside its tx (the first
-//                index wins, AppendOnlyPersistentMap.set); rebuild path: first occurrence of a key
-//                in the rebuild batch that is not in the table yet
-CHIP_DEV bool first_in_tx(const uint32_t* bslot, uint64_t a, uint64_t r) {
-    for (uint64_t r2 = a; r2 < r; r2++)
-        if (bslot[r2] == bslot[r]) return false;
-    return true;
-}
-__global__ void k_uniq_insert(uint64_t nref, const uint8_t* __restrict__ refs, const uint32_t* __restrict__ ref_tx,
-                              const uint32_t* __restrict__ ref_pos, const uint64_t* __restrict__ start,
-                              const uint8_t* __restrict__ tx_status, const int64_t* __restrict__ pre,
-                              const uint32_t* __restrict__ bslot, const uint32_t* __restrict__ bowner,
-                              const uint8_t* __restrict__ tx_ids, const uint32_t* __restrict__ callers,
-                              uint32_t* key, uint32_t* val, uint32_t* used, uint64_t cap,
-                              unsigned long long* __restrict__ inserted) {
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nref) return;
-    const uint32_t t = ref_tx[r];
-    if (tx_status) {   // commit path
-        if (tx_status[t] != ST_COMMITTED) return;
-        if (!first_in_tx(bslot, start[t], r)) return;
-    } else {           // rebuild path
-        if (pre[r] >= 0 || bowner[bslot[r]] != (uint32_t)(r + 1)) return;
-    }
-    uint32_t k[KW];
-    load_key(k, refs, r);
+// claim an empty slot for k (k absent from the table and distinct among concurrent inserters)
+CHIP_DEV void tab_put(uint32_t* tab, uint64_t cap, const uint32_t k[KW], const uint32_t v[10]) {
     uint64_t i = key_hash(k) & (cap - 1);
     for (uint64_t n = 0; n < cap; n++) {
-        if (atomicCAS(&used[i], 0u, 1u) == 0u) {
-#pragma unroll
-            for (int q = 0; q < KW; q++) key[i * KW + q] = k[q];
-            const uint32_t* id = reinterpret_cast<const uint32_t*>(tx_ids + 32ull * t);
-#pragma unroll
-            for (int q = 0; q < 8; q++) val[i * VW + q] = id[q];
-            val[i * VW + 8] = ref_pos[r];
-            val[i * VW + 9] = callers[t];
-            atomicAdd(inserted, 1ull);
+        uint32_t* s = tab + i * SLOT_W;
+        if (atomicCAS(&s[S_USED], 0u, 1u) == 0u) {
+            *reinterpret_cast<uint4*>(s) = make_uint4(k[0], k[1], k[2], k[3]);
+            *reinterpret_cast<uint4*>(s + 4) = make_uint4(k[4], k[5], k[6], k[7]);
+            s[8] = k[8];
+            *reinterpret_cast<uint2*>(s + 10) = make_uint2(v[0], v[1]);
+            *reinterpret_cast<uint4*>(s + 12) = make_uint4(v[2], v[3], v[4], v[5]);
+            *reinterpret_cast<uint4*>(s + 16) = make_uint4(v[6], v[7], v[8], v[9]);
             return;
         }
         i = (i + 1) & (cap - 1);
     }
 }
 
-// ---- batch scratch table: distinct states of the batch ----
-// bowner[s] = 1 + ref index of the first inserter (0 = empty)
-__global__ void k_uniq_intern(uint64_t nref, const uint8_t* __restrict__ refs, uint32_t* bowner, uint64_t bcap,
-                              uint32_t* __restrict__ bslot) {
+__global__ void __launch_bounds__(256) k_uniq_lookup(uint64_t nref, const uint8_t* __restrict__ refs,
+                                                     const uint32_t* __restrict__ tab, uint64_t cap,
+                                                     uint32_t* __restrict__ pre) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nref) return;
+    uint32_t k[KW];
+    load_key(k, refs, r);
+    pre[r] = tab_find(tab, cap, k);
+}
+
+// batch scratch table of the distinct states: bowner[s] = 1 + ref index of the first inserter
+__global__ void __launch_bounds__(256) k_uniq_intern(uint64_t nref, const uint8_t* __restrict__ refs, uint32_t* bowner,
+                                                     uint64_t bcap, uint32_t* __restrict__ bslot) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nref) return;
     uint32_t k[KW];
@@ -163,151 +188,247 @@ __global__ void k_uniq_intern(uint64_t nref, const uint8_t* __restrict__ refs, u
     }
 }
 
-__global__ void k_uniq_round_min(uint64_t nref, const uint32_t* __restrict__ ref_tx, const uint32_t* __restrict__ bslot,
-                                 const uint8_t* __restrict__ st, uint32_t* __restrict__ bmin) {
+__global__ void __launch_bounds__(256) k_ref_tx(uint64_t ntx, const uint64_t* __restrict__ start,
+                                                uint32_t* __restrict__ ref_tx, uint32_t* __restrict__ ref_pos) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntx) return;
+    for (uint64_t r = start[t]; r < start[t + 1]; r++) {
+        if (ref_tx) ref_tx[r] = (uint32_t)t;
+        if (ref_pos) ref_pos[r] = (uint32_t)(r - start[t]);
+    }
+}
+
+__global__ void __launch_bounds__(256) k_uniq_round_min(uint64_t nref, const uint32_t* __restrict__ ref_tx,
+                                                        const uint32_t* __restrict__ bslot,
+                                                        const uint8_t* __restrict__ st, uint32_t* __restrict__ bmin) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nref) return;
     const uint32_t t = ref_tx[r];
     if (st[t] != ST_FAILED) atomicMin(&bmin[bslot[r]], t);
 }
 
-// bcommit[s] = (t << 32) | position of s in the committing tx t (first occurrence)
-__global__ void k_uniq_decide(uint64_t ntx, const uint64_t* __restrict__ start, const int64_t* __restrict__ pre,
-                              const uint32_t* __restrict__ bslot, const uint32_t* __restrict__ bmin, uint8_t* st,
-                              unsigned long long* bcommit, uint32_t* __restrict__ undecided) {
+// votes read only the previous round's status bytes (st is written by k_uniq_apply alone), so a
+// round's outcome does not depend on thread scheduling
+__global__ void __launch_bounds__(256) k_uniq_vote(uint64_t ntx, const uint64_t* __restrict__ start,
+                                                   const uint32_t* __restrict__ pre, const uint32_t* __restrict__ bslot,
+                                                   const uint32_t* __restrict__ bmin, const uint8_t* __restrict__ st,
+                                                   uint8_t* __restrict__ vote) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntx) return;
-    if (st[t] != ST_UNDECIDED) return;
-    const uint64_t a = start[t], e = start[t + 1];
-    bool fail = false, all_first = true;
-    for (uint64_t r = a; r < e; r++) {
-        if (pre[r] >= 0) { fail = true; break; }
-        const uint32_t m = bmin[bslot[r]];
-        if (m < t) {
-            all_first = false;
-            if (__hip_atomic_load(&st[m], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == ST_COMMITTED) {
-                fail = true;
-                break;
+    uint8_t v = 0;
+    if (st[t] == ST_UNDECIDED) {
+        for (uint64_t r = start[t], e = start[t + 1]; r < e; r++) {
+            if (pre[r] != NO_SLOT) { v = 2; break; }
+            const uint32_t m = bmin[bslot[r]];
+            if (m < t) {
+                if (st[m] == ST_COMMITTED) { v = 2; break; }
+                v = 1;
             }
         }
     }
-    if (fail) {
-        st[t] = ST_FAILED;
-    } else if (all_first) {
-        for (uint64_t r = a; r < e; r++)
-            atomicMin(&bcommit[bslot[r]], ((unsigned long long)t << 32) | (unsigned long long)(r - a));
-        __threadfence();
-        __hip_atomic_store(&st[t], (uint8_t)ST_COMMITTED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-        atomicAdd(undecided, 1u);
-    }
+    vote[t] = v;
 }
 
-// failed txs: IDEMPOTENT or CONFLICT; conflict records appended (order restored on the host)
-__global__ void k_uniq_classify(uint64_t ntx, const uint64_t* __restrict__ start, const uint8_t* __restrict__ refs,
-                                const int64_t* __restrict__ pre, const uint32_t* __restrict__ bslot,
-                                const unsigned long long* __restrict__ bcommit, const uint8_t* __restrict__ tx_ids,
-                                const uint32_t* __restrict__ callers, const uint32_t* __restrict__ tval,
-                                uint8_t* st, chip_conflict* __restrict__ out, uint64_t cap,
-                                unsigned long long* __restrict__ nout) {
+// bcommit[s] = (t << 32) | input index of s in the committing tx t (first occurrence wins via min)
+__global__ void __launch_bounds__(256) k_uniq_apply(uint64_t ntx, const uint64_t* __restrict__ start,
+                                                    const uint32_t* __restrict__ bslot, const uint32_t* __restrict__ pos,
+                                                    const uint8_t* __restrict__ decision, uint8_t* __restrict__ st,
+                                                    unsigned long long* __restrict__ bcommit,
+                                                    unsigned int* __restrict__ undecided) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= ntx) return;
-    if (st[t] == ST_COMMITTED) { st[t] = 0; return; }
-    const uint64_t a = start[t], e = start[t + 1];
-    const uint32_t* myid = reinterpret_cast<const uint32_t*>(tx_ids + 32ull * t);
-    bool real = false;
-    uint32_t nrec = 0;
-    for (uint64_t r = a; r < e; r++) {
-        const uint32_t* cid;
-        uint32_t cidx, ccal;
-        if (pre[r] >= 0) {
-            const uint32_t* v = tval + (uint64_t)pre[r] * VW;
-            cid = v; cidx = v[8]; ccal = v[9];
+    bool wait = false;
+    if (t < ntx && st[t] == ST_UNDECIDED) {
+        const uint8_t d = decision[t];
+        if (d == 0) {
+            for (uint64_t r = start[t], e = start[t + 1]; r < e; r++)
+                atomicMin(&bcommit[bslot[r]], ((unsigned long long)t << 32) | (unsigned long long)pos[r]);
+            st[t] = ST_COMMITTED;
+        } else if (d >= 2) {
+            st[t] = ST_FAILED;
         } else {
-            const unsigned long long bc = bcommit[bslot[r]];
-            const uint32_t c = (uint32_t)(bc >> 32);
-            if (bc == ~0ull || c >= t) continue;      // not consumed before t
-            cid = reinterpret_cast<const uint32_t*>(tx_ids + 32ull * c);
-            cidx = (uint32_t)bc;
-            ccal = callers[c];
+            wait = true;
         }
-        bool same = (cidx == (uint32_t)(r - a)) && (ccal == callers[t]);
-#pragma unroll
-        for (int q = 0; q < 8; q++) same = same && (cid[q] == myid[q]);
-        if (!same) real = true;
-        // distinct state (first occurrence in this tx) -> one record
-        bool dup = false;
-        for (uint64_t r2 = a; r2 < r; r2++)
-            if (bslot[r2] == bslot[r]) { dup = true; break; }
-        if (!dup) nrec++;
     }
-    st[t] = real ? 2 : 1;
-    const unsigned long long base = atomicAdd(nout, (unsigned long long)nrec);
-    uint64_t w = base;
-    for (uint64_t r = a; r < e; r++) {
-        const uint32_t* cid;
-        uint32_t cidx, ccal;
-        if (pre[r] >= 0) {
-            const uint32_t* v = tval + (uint64_t)pre[r] * VW;
-            cid = v; cidx = v[8]; ccal = v[9];
-        } else {
-            const unsigned long long bc = bcommit[bslot[r]];
-            const uint32_t c = (uint32_t)(bc >> 32);
-            if (bc == ~0ull || c >= t) continue;
-            cid = reinterpret_cast<const uint32_t*>(tx_ids + 32ull * c);
-            cidx = (uint32_t)bc;
-            ccal = callers[c];
-        }
-        bool dup = false;
-        for (uint64_t r2 = a; r2 < r; r2++)
-            if (bslot[r2] == bslot[r]) { dup = true; break; }
-        if (dup) continue;
-        if (w < cap) {
-            chip_conflict cf;
-            cf.tx = t;
-            cf.input_index = (uint32_t)(r - a);
-            cf.consumed_index = cidx;
-            uint32_t* d = reinterpret_cast<uint32_t*>(cf.consuming_tx);
-#pragma unroll
-            for (int q = 0; q < 8; q++) d[q] = cid[q];
-            cf.consuming_caller = ccal;
-            cf.pad = 0;
-            out[w] = cf;
-        }
-        w++;
-    }
+    const uint64_t m = __ballot(wait);
+    if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(undecided, (unsigned int)__popcll(m));
 }
 
-__global__ void k_ref_tx(uint64_t ntx, const uint64_t* __restrict__ start, uint32_t* __restrict__ ref_tx,
-                         uint32_t* __restrict__ ref_pos) {
+// the ConsumingTx that consumed local input r before tx t, if any
+struct Consumer {
+    const uint32_t* id;
+    uint32_t idx, caller;
+};
+CHIP_DEV bool consumed_before(uint64_t r, uint32_t t, const uint32_t* __restrict__ pre, const uint32_t* __restrict__ tab,
+                              const unsigned long long* __restrict__ bcommit, const uint32_t* __restrict__ bslot,
+                              const uint8_t* __restrict__ tx_ids, const uint32_t* __restrict__ callers, Consumer& c) {
+    if (pre[r] != NO_SLOT) {
+        const uint32_t* v = tab + (uint64_t)pre[r] * SLOT_W + S_VAL;
+        c.id = v;
+        c.idx = v[8];
+        c.caller = v[9];
+        return true;
+    }
+    const unsigned long long bc = bcommit[bslot[r]];
+    const uint32_t ct = (uint32_t)(bc >> 32);
+    if (bc == ~0ull || ct >= t) return false;
+    c.id = reinterpret_cast<const uint32_t*>(tx_ids + 32ull * ct);
+    c.idx = (uint32_t)bc;
+    c.caller = callers[ct];
+    return true;
+}
+
+// failed tx: 1 IDEMPOTENT (every consumed local input was consumed by (txId, i, caller) itself),
+// 2 CONFLICT; 0 for committed txs and for failed txs with no consumed input on this shard
+__global__ void __launch_bounds__(256) k_uniq_classify(uint64_t ntx, const uint64_t* __restrict__ start,
+                                                       const uint32_t* __restrict__ pos, const uint32_t* __restrict__ pre,
+                                                       const uint32_t* __restrict__ bslot,
+                                                       const unsigned long long* __restrict__ bcommit,
+                                                       const uint8_t* __restrict__ tx_ids,
+                                                       const uint32_t* __restrict__ callers,
+                                                       const uint32_t* __restrict__ tab, const uint8_t* __restrict__ st,
+                                                       uint8_t* __restrict__ vote) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntx) return;
-    for (uint64_t r = start[t]; r < start[t + 1]; r++) {
-        ref_tx[r] = (uint32_t)t;
-        ref_pos[r] = (uint32_t)(r - start[t]);
+    uint8_t v = 0;
+    if (st[t] == ST_FAILED) {
+        const uint32_t* myid = reinterpret_cast<const uint32_t*>(tx_ids + 32ull * t);
+        for (uint64_t r = start[t], e = start[t + 1]; r < e; r++) {
+            Consumer c;
+            if (!consumed_before(r, (uint32_t)t, pre, tab, bcommit, bslot, tx_ids, callers, c)) continue;
+            bool same = (c.idx == pos[r]) && (c.caller == callers[t]);
+#pragma unroll
+            for (int q = 0; q < 8; q++) same = same && (c.id[q] == myid[q]);
+            v = same ? (v > 1 ? v : 1) : 2;
+        }
     }
+    vote[t] = v;
+}
+
+CHIP_DEV bool first_in_tx(const uint32_t* __restrict__ bslot, uint64_t a, uint64_t r) {
+    for (uint64_t r2 = a; r2 < r; r2++)
+        if (bslot[r2] == bslot[r]) return false;
+    return true;
+}
+
+// flag[r] = 1 when local input r yields a Conflict.stateHistory record
+__global__ void __launch_bounds__(256) k_uniq_flag(uint64_t nref, const uint32_t* __restrict__ ref_tx,
+                                                   const uint64_t* __restrict__ start, const uint32_t* __restrict__ pre,
+                                                   const uint32_t* __restrict__ bslot,
+                                                   const unsigned long long* __restrict__ bcommit,
+                                                   const uint8_t* __restrict__ st, uint32_t* __restrict__ flag) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nref) return;
+    const uint32_t t = ref_tx[r];
+    uint32_t f = 0;
+    if (st[t] == ST_FAILED) {
+        bool consumed = pre[r] != NO_SLOT;
+        if (!consumed) {
+            const unsigned long long bc = bcommit[bslot[r]];
+            consumed = bc != ~0ull && (uint32_t)(bc >> 32) < t;
+        }
+        f = consumed && first_in_tx(bslot, start[t], r);
+    }
+    flag[r] = f;
+}
+
+__global__ void __launch_bounds__(256) k_uniq_emit(uint64_t nref, const uint32_t* __restrict__ ref_tx,
+                                                   const uint32_t* __restrict__ pos, const uint32_t* __restrict__ pre,
+                                                   const uint32_t* __restrict__ bslot,
+                                                   const unsigned long long* __restrict__ bcommit,
+                                                   const uint8_t* __restrict__ tx_ids,
+                                                   const uint32_t* __restrict__ callers,
+                                                   const uint32_t* __restrict__ tab, const uint32_t* __restrict__ flag,
+                                                   const uint32_t* __restrict__ at, chip_conflict* __restrict__ out,
+                                                   uint64_t cap) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nref || !flag[r] || at[r] >= cap) return;
+    const uint32_t t = ref_tx[r];
+    Consumer c;
+    consumed_before(r, t, pre, tab, bcommit, bslot, tx_ids, callers, c);
+    chip_conflict cf;
+    cf.tx = t;
+    cf.input_index = pos[r];
+    cf.consumed_index = c.idx;
+    uint32_t* d = reinterpret_cast<uint32_t*>(cf.consuming_tx);
+#pragma unroll
+    for (int q = 0; q < 8; q++) d[q] = c.id[q];
+    cf.consuming_caller = c.caller;
+    cf.pad = 0;
+    out[at[r]] = cf;
+}
+
+// inserts: inputs of COMMITTED txs, first occurrence of a state inside its tx
+__global__ void __launch_bounds__(256) k_uniq_insert(uint64_t nref, const uint8_t* __restrict__ refs,
+                                                     const uint32_t* __restrict__ ref_tx,
+                                                     const uint32_t* __restrict__ pos, const uint64_t* __restrict__ start,
+                                                     const uint8_t* __restrict__ st, const uint32_t* __restrict__ bslot,
+                                                     const uint8_t* __restrict__ tx_ids,
+                                                     const uint32_t* __restrict__ callers, uint32_t* tab, uint64_t cap,
+                                                     unsigned long long* __restrict__ inserted) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool ins = false;
+    if (r < nref) {
+        const uint32_t t = ref_tx[r];
+        if (st[t] == ST_COMMITTED && first_in_tx(bslot, start[t], r)) {
+            uint32_t k[KW], v[10];
+            load_key(k, refs, r);
+            const uint32_t* id = reinterpret_cast<const uint32_t*>(tx_ids + 32ull * t);
+#pragma unroll
+            for (int q = 0; q < 8; q++) v[q] = id[q];
+            v[8] = pos[r];
+            v[9] = callers[t];
+            tab_put(tab, cap, k, v);
+            ins = true;
+        }
+    }
+    const uint64_t m = __ballot(ins);
+    if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(inserted, (unsigned long long)__popcll(m));
+}
+
+__global__ void __launch_bounds__(256) k_uniq_status(uint64_t ntx, const uint8_t* __restrict__ st,
+                                                     const uint8_t* __restrict__ decision, uint8_t* __restrict__ out) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntx) return;
+    out[t] = st[t] == ST_COMMITTED ? 0 : (decision[t] >= 2 ? 2 : 1);
+}
+
+// rebuild (AppendOnlyPersistentMap.allPersisted): rows absent from the table, first of equal keys
+__global__ void __launch_bounds__(256) k_uniq_rebuild(uint64_t n, const uint8_t* __restrict__ refs,
+                                                      const uint8_t* __restrict__ tx32, const uint32_t* __restrict__ idx,
+                                                      const uint32_t* __restrict__ caller, const uint32_t* __restrict__ pre,
+                                                      const uint32_t* __restrict__ bslot,
+                                                      const uint32_t* __restrict__ bowner, uint32_t* tab, uint64_t cap,
+                                                      unsigned long long* __restrict__ inserted) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    bool ins = false;
+    if (r < n && pre[r] == NO_SLOT && bowner[bslot[r]] == (uint32_t)(r + 1)) {
+        uint32_t k[KW], v[10];
+        load_key(k, refs, r);
+        const uint32_t* id = reinterpret_cast<const uint32_t*>(tx32 + 32ull * r);
+#pragma unroll
+        for (int q = 0; q < 8; q++) v[q] = id[q];
+        v[8] = idx[r];
+        v[9] = caller[r];
+        tab_put(tab, cap, k, v);
+        ins = true;
+    }
+    const uint64_t m = __ballot(ins);
+    if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(inserted, (unsigned long long)__popcll(m));
 }
 
 // rehash every used slot of an old table into a new one
-__global__ void k_uniq_rehash(uint64_t ocap, const uint32_t* __restrict__ okey, const uint32_t* __restrict__ oval,
-                              const uint32_t* __restrict__ oused, uint32_t* key, uint32_t* val, uint32_t* used,
-                              uint64_t cap) {
+__global__ void __launch_bounds__(256) k_uniq_rehash(uint64_t ocap, const uint32_t* __restrict__ old, uint32_t* tab,
+                                                     uint64_t cap) {
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (s >= ocap || !oused[s]) return;
-    uint32_t k[KW];
+    if (s >= ocap) return;
+    const uint32_t* o = old + s * SLOT_W;
+    if (!o[S_USED]) return;
+    uint32_t k[KW], v[10];
 #pragma unroll
-    for (int q = 0; q < KW; q++) k[q] = okey[s * KW + q];
-    uint64_t i = key_hash(k) & (cap - 1);
-    for (uint64_t n = 0; n < cap; n++) {
-        if (atomicCAS(&used[i], 0u, 1u) == 0u) {
+    for (int q = 0; q < KW; q++) k[q] = o[q];
 #pragma unroll
-            for (int q = 0; q < KW; q++) key[i * KW + q] = k[q];
-#pragma unroll
-            for (int q = 0; q < VW; q++) val[i * VW + q] = oval[s * VW + q];
-            return;
-        }
-        i = (i + 1) & (cap - 1);
-    }
+    for (int q = 0; q < 10; q++) v[q] = o[S_VAL + q];
+    tab_put(tab, cap, k, v);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -329,49 +450,43 @@ static uint64_t pow2_at_least(uint64_t x) {
 }
 static inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + 255) / 256); }
 
-static int alloc_table(chip_uniq* u, uint64_t cap, uint32_t** key, uint32_t** val, uint32_t** used) {
-    UCHK(u, hipMalloc(key, cap * KW * 4));
-    UCHK(u, hipMalloc(val, cap * VW * 4));
-    UCHK(u, hipMalloc(used, cap * 4));
-    UCHK(u, hipMemsetAsync(*used, 0, cap * 4, u->stream));
-    return CHIP_OK;
-}
-
 // make room for `extra` more entries at load factor <= 1/2
-static int ensure_capacity(chip_uniq* u, uint64_t extra) {
+static int ensure_capacity(chip_uniq* u, uint64_t extra, hipStream_t st) {
     if (2 * (u->size + extra) <= u->cap) return CHIP_OK;
     const uint64_t ncap = pow2_at_least(2 * (u->size + extra));
-    uint32_t *k, *v, *us;
-    int r = alloc_table(u, ncap, &k, &v, &us);
-    if (r) return r;
+    uint32_t* t = nullptr;
+    UCHK(u, hipMalloc(&t, ncap * SLOT_W * 4));
+    UCHK(u, hipMemsetAsync(t, 0, ncap * SLOT_W * 4, st));
     if (u->cap) {
-        hipLaunchKernelGGL(k_uniq_rehash, dim3(blocks_for(u->cap)), dim3(256), 0, u->stream, u->cap, u->key, u->val,
-                           u->used, k, v, us, ncap);
-        UCHK(u, hipStreamSynchronize(u->stream));
-        hipFree(u->key);
-        hipFree(u->val);
-        hipFree(u->used);
+        hipLaunchKernelGGL(k_uniq_rehash, dim3(blocks_for(u->cap)), dim3(256), 0, st, u->cap, u->tab, t, ncap);
+        UCHK(u, hipGetLastError());
+        UCHK(u, hipStreamSynchronize(st));
+        hipFree(u->tab);
     }
-    u->key = k;
-    u->val = v;
-    u->used = us;
+    u->tab = t;
     u->cap = ncap;
     return CHIP_OK;
 }
 
-static void* scratch(chip_uniq* u, size_t bytes) {
-    if (bytes > u->scratch_cap) {
-        if (u->scratch) hipFree(u->scratch);
-        u->scratch = nullptr;
-        u->scratch_cap = 0;
-        if (hipMalloc(&u->scratch, bytes) != hipSuccess) return nullptr;
-        u->scratch_cap = bytes;
-    }
-    return u->scratch;
-}
-
 struct chip_ctx;
 extern "C" int chip_ctx_device(const chip_ctx* c);
+
+// batch scratch for nref local inputs and ntx transactions
+static int batch_scratch(chip_uniq* u, uint64_t ntx, uint64_t nref) {
+    const uint64_t bcap = pow2_at_least(2 * (nref + 1));
+    UCHK(u, u->reftx.ensure(nref * 4 + 16));
+    UCHK(u, u->pre.ensure(nref * 4 + 16));
+    UCHK(u, u->bslot.ensure(nref * 4 + 16));
+    UCHK(u, u->flag.ensure(nref * 4 + 16));
+    UCHK(u, u->scan.ensure(nref * 4 + 16));
+    UCHK(u, u->bowner.ensure(bcap * 4));
+    UCHK(u, u->bmin.ensure(bcap * 4));
+    UCHK(u, u->bcommit.ensure(bcap * 8));
+    UCHK(u, u->st.ensure(ntx + 16));
+    UCHK(u, u->ctr.ensure(64));
+    u->bcap = bcap;
+    return CHIP_OK;
+}
 
 extern "C" {
 
@@ -385,14 +500,12 @@ int chip_uniq_open(chip_ctx* ctx, uint64_t capacity, chip_uniq** out) {
         delete u;
         return CHIP_E_DEVICE;
     }
-    int r = ensure_capacity(u, capacity ? capacity : 1024);
-    if (r) {
+    int r = ensure_capacity(u, capacity ? capacity : 1024, u->stream);
+    if (r || hipStreamSynchronize(u->stream) != hipSuccess) {
+        if (u->tab) hipFree(u->tab);
+        hipStreamDestroy(u->stream);
         delete u;
-        return r;
-    }
-    if (hipStreamSynchronize(u->stream) != hipSuccess) {
-        delete u;
-        return CHIP_E_DEVICE;
+        return r ? r : CHIP_E_DEVICE;
     }
     *out = u;
     return CHIP_OK;
@@ -402,64 +515,224 @@ void chip_uniq_close(chip_uniq* u) {
     if (!u) return;
     hipSetDevice(u->device);
     hipStreamSynchronize(u->stream);
-    if (u->key) hipFree(u->key);
-    if (u->val) hipFree(u->val);
-    if (u->used) hipFree(u->used);
-    if (u->scratch) hipFree(u->scratch);
+    if (u->tab) hipFree(u->tab);
+    UBuf* bufs[] = {&u->reftx, &u->pre,    &u->bslot, &u->bowner, &u->bmin,   &u->bcommit, &u->st,
+                    &u->flag,  &u->scan,   &u->cub,   &u->ctr,    &u->refpos, &u->h_start, &u->h_refs,
+                    &u->h_ids, &u->h_call, &u->h_st,  &u->h_vote, &u->h_out};
+    for (UBuf* b : bufs) b->release();
     hipStreamDestroy(u->stream);
     delete u;
 }
 
 uint64_t chip_uniq_size(const chip_uniq* u) { return u ? u->size : 0; }
 
+const char* chip_uniq_last_error(const chip_uniq* u) { return u ? u->err.c_str() : "null table"; }
+
 int chip_uniq_rebuild(chip_uniq* u, uint64_t n, const uint8_t* refs36, const uint8_t* tx32, const uint32_t* idx,
                       const uint32_t* caller) {
     if (!u || (n && (!refs36 || !tx32 || !idx || !caller))) return CHIP_E_ARG;
     if (!n) return CHIP_OK;
-    if (n >= 0xffffffffull) return ufail(u, CHIP_E_ARG, "rebuild batch too large");
+    if (u->open) return ufail(u, CHIP_E_ARG, "a shard batch is in flight");
+    if (n >= 0x7fffffffull) return ufail(u, CHIP_E_ARG, "rebuild batch too large");
     UCHK(u, hipSetDevice(u->device));
-    int r = ensure_capacity(u, n);
-    if (r) return r;
-    // each row is a one-input "transaction" whose id / caller / index are the row's ConsumingTx
-    const uint64_t bcap = pow2_at_least(2 * (n + 1));
-    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
-    size_t off = 0;
-    const size_t o_refs = off; off += al(n * 36);
-    const size_t o_tx = off; off += al(n * 32);
-    const size_t o_pos = off; off += al(n * 4);
-    const size_t o_call = off; off += al(n * 4);
-    const size_t o_reftx = off; off += al(n * 4);
-    const size_t o_pre = off; off += al(n * 8);
-    const size_t o_bslot = off; off += al(n * 4);
-    const size_t o_bowner = off; off += al(bcap * 4);
-    const size_t o_ctr = off; off += 64;
-    uint8_t* s = (uint8_t*)scratch(u, off);
-    if (!s) return ufail(u, CHIP_E_NOMEM, "scratch");
-    std::vector<uint32_t> rt(n);
-    for (uint64_t i = 0; i < n; i++) rt[i] = (uint32_t)i;
     hipStream_t st = u->stream;
-    UCHK(u, hipMemcpyAsync(s + o_refs, refs36, n * 36, hipMemcpyHostToDevice, st));
-    UCHK(u, hipMemcpyAsync(s + o_tx, tx32, n * 32, hipMemcpyHostToDevice, st));
-    UCHK(u, hipMemcpyAsync(s + o_pos, idx, n * 4, hipMemcpyHostToDevice, st));
-    UCHK(u, hipMemcpyAsync(s + o_call, caller, n * 4, hipMemcpyHostToDevice, st));
-    UCHK(u, hipMemcpyAsync(s + o_reftx, rt.data(), n * 4, hipMemcpyHostToDevice, st));
-    UCHK(u, hipMemsetAsync(s + o_bowner, 0, bcap * 4, st));
-    UCHK(u, hipMemsetAsync(s + o_ctr, 0, 64, st));
-    hipLaunchKernelGGL(k_uniq_lookup, dim3(blocks_for(n)), dim3(256), 0, st, n, s + o_refs, u->key, u->used, u->cap,
-                       (int64_t*)(s + o_pre));
-    hipLaunchKernelGGL(k_uniq_intern, dim3(blocks_for(n)), dim3(256), 0, st, n, s + o_refs, (uint32_t*)(s + o_bowner),
-                       bcap, (uint32_t*)(s + o_bslot));
-    hipLaunchKernelGGL(k_uniq_insert, dim3(blocks_for(n)), dim3(256), 0, st, n, s + o_refs, (uint32_t*)(s + o_reftx),
-                       (uint32_t*)(s + o_pos), (const uint64_t*)nullptr, (const uint8_t*)nullptr,
-                       (int64_t*)(s + o_pre), (uint32_t*)(s + o_bslot), (uint32_t*)(s + o_bowner), s + o_tx,
-                       (uint32_t*)(s + o_call), u->key, u->val, u->used, u->cap,
-                       (unsigned long long*)(s + o_ctr));
+    int r = ensure_capacity(u, n, st);
+    if (r || (r = batch_scratch(u, 0, n))) return r;
+    UCHK(u, u->h_refs.ensure(n * 36 + 16));
+    UCHK(u, u->h_ids.ensure(n * 32 + 16));
+    UCHK(u, u->h_call.ensure(n * 4 + 16));
+    UCHK(u, u->refpos.ensure(n * 4 + 16));
+    UCHK(u, hipMemcpyAsync(u->h_refs.p, refs36, n * 36, hipMemcpyHostToDevice, st));
+    UCHK(u, hipMemcpyAsync(u->h_ids.p, tx32, n * 32, hipMemcpyHostToDevice, st));
+    UCHK(u, hipMemcpyAsync(u->refpos.p, idx, n * 4, hipMemcpyHostToDevice, st));
+    UCHK(u, hipMemcpyAsync(u->h_call.p, caller, n * 4, hipMemcpyHostToDevice, st));
+    UCHK(u, hipMemsetAsync(u->bowner.p, 0, u->bcap * 4, st));
+    UCHK(u, hipMemsetAsync(u->ctr.p, 0, 64, st));
+    const uint8_t* d_refs = u->h_refs.as<uint8_t>();
+    hipLaunchKernelGGL(k_uniq_lookup, dim3(blocks_for(n)), dim3(256), 0, st, n, d_refs, u->tab, u->cap,
+                       u->pre.as<uint32_t>());
+    hipLaunchKernelGGL(k_uniq_intern, dim3(blocks_for(n)), dim3(256), 0, st, n, d_refs, u->bowner.as<uint32_t>(), u->bcap,
+                       u->bslot.as<uint32_t>());
+    hipLaunchKernelGGL(k_uniq_rebuild, dim3(blocks_for(n)), dim3(256), 0, st, n, d_refs, u->h_ids.as<uint8_t>(),
+                       u->refpos.as<uint32_t>(), u->h_call.as<uint32_t>(), u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(),
+                       u->bowner.as<uint32_t>(), u->tab, u->cap, u->ctr.as<unsigned long long>());
     UCHK(u, hipGetLastError());
     unsigned long long ins = 0;
-    UCHK(u, hipMemcpyAsync(&ins, s + o_ctr, 8, hipMemcpyDeviceToHost, st));
+    UCHK(u, hipMemcpyAsync(&ins, u->ctr.p, 8, hipMemcpyDeviceToHost, st));
     UCHK(u, hipStreamSynchronize(st));
     u->size += ins;
     return CHIP_OK;
+}
+
+// ---- sharded commit: phase API (device pointers; see cordahip.h) ----
+int chip_uniq_shard_begin(chip_uniq* u, const chip_uniq_shard_batch* b, void* stream) {
+    if (!u || !b) return CHIP_E_ARG;
+    if (u->open) return ufail(u, CHIP_E_ARG, "a shard batch is already in flight");
+    const uint64_t ntx = b->ntx, nref = b->nref;
+    if (ntx && (!b->ref_start || !b->tx_ids || !b->callers)) return ufail(u, CHIP_E_ARG, "null batch array");
+    if (ntx >= 0xffffffffull || nref >= 0x7fffffffull) return ufail(u, CHIP_E_ARG, "batch too large");
+    if (nref && (!b->refs36 || !b->ref_pos)) return ufail(u, CHIP_E_ARG, "null ref array");
+    UCHK(u, hipSetDevice(u->device));
+    hipStream_t st = stream ? (hipStream_t)stream : u->stream;
+    int r = ensure_capacity(u, nref, st);
+    if (r || (r = batch_scratch(u, ntx, nref))) return r;
+    u->ntx = ntx;
+    u->nref = nref;
+    u->bst = st;
+    u->start = b->ref_start;
+    u->refs = b->refs36;
+    u->pos = b->ref_pos;
+    u->ids = b->tx_ids;
+    u->callers = b->callers;
+    UCHK(u, hipMemsetAsync(u->bowner.p, 0, u->bcap * 4, st));
+    UCHK(u, hipMemsetAsync(u->bcommit.p, 0xff, u->bcap * 8, st));
+    if (ntx) UCHK(u, hipMemsetAsync(u->st.p, ST_UNDECIDED, ntx, st));
+    UCHK(u, hipMemsetAsync(u->ctr.p, 0, 64, st));
+    if (ntx)
+        hipLaunchKernelGGL(k_ref_tx, dim3(blocks_for(ntx)), dim3(256), 0, st, ntx, u->start, u->reftx.as<uint32_t>(),
+                           (uint32_t*)nullptr);
+    if (nref) {
+        hipLaunchKernelGGL(k_uniq_lookup, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->refs, u->tab, u->cap,
+                           u->pre.as<uint32_t>());
+        hipLaunchKernelGGL(k_uniq_intern, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->refs,
+                           u->bowner.as<uint32_t>(), u->bcap, u->bslot.as<uint32_t>());
+    }
+    UCHK(u, hipGetLastError());
+    u->open = true;
+    return CHIP_OK;
+}
+
+int chip_uniq_shard_vote(chip_uniq* u, uint8_t* vote) {
+    if (!u) return CHIP_E_ARG;
+    if (!u->open || (u->ntx && !vote)) return ufail(u, CHIP_E_ARG, "no batch in flight / null vote");
+    hipStream_t st = u->bst;
+    UCHK(u, hipMemsetAsync(u->bmin.p, 0xff, u->bcap * 4, st));
+    if (u->nref)
+        hipLaunchKernelGGL(k_uniq_round_min, dim3(blocks_for(u->nref)), dim3(256), 0, st, u->nref,
+                           u->reftx.as<uint32_t>(), u->bslot.as<uint32_t>(), u->st.as<uint8_t>(), u->bmin.as<uint32_t>());
+    if (u->ntx)
+        hipLaunchKernelGGL(k_uniq_vote, dim3(blocks_for(u->ntx)), dim3(256), 0, st, u->ntx, u->start,
+                           u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->bmin.as<uint32_t>(), u->st.as<uint8_t>(),
+                           vote);
+    UCHK(u, hipGetLastError());
+    return CHIP_OK;
+}
+
+int chip_uniq_shard_apply(chip_uniq* u, const uint8_t* decision, uint64_t* undecided) {
+    if (!u) return CHIP_E_ARG;
+    if (!u->open || !undecided || (u->ntx && !decision)) return ufail(u, CHIP_E_ARG, "no batch in flight / null argument");
+    hipStream_t st = u->bst;
+    unsigned int* d_und = u->ctr.as<unsigned int>();
+    UCHK(u, hipMemsetAsync(d_und, 0, 4, st));
+    if (u->ntx)
+        hipLaunchKernelGGL(k_uniq_apply, dim3(blocks_for(u->ntx)), dim3(256), 0, st, u->ntx, u->start,
+                           u->bslot.as<uint32_t>(), u->pos, decision, u->st.as<uint8_t>(),
+                           u->bcommit.as<unsigned long long>(), d_und);
+    UCHK(u, hipGetLastError());
+    unsigned int und = 0;
+    UCHK(u, hipMemcpyAsync(&und, d_und, 4, hipMemcpyDeviceToHost, st));
+    UCHK(u, hipStreamSynchronize(st));
+    *undecided = und;
+    return CHIP_OK;
+}
+
+int chip_uniq_shard_classify(chip_uniq* u, uint8_t* vote) {
+    if (!u) return CHIP_E_ARG;
+    if (!u->open || (u->ntx && !vote)) return ufail(u, CHIP_E_ARG, "no batch in flight / null vote");
+    if (u->ntx)
+        hipLaunchKernelGGL(k_uniq_classify, dim3(blocks_for(u->ntx)), dim3(256), 0, u->bst, u->ntx, u->start, u->pos,
+                           u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->bcommit.as<unsigned long long>(), u->ids,
+                           u->callers, u->tab, u->st.as<uint8_t>(), vote);
+    UCHK(u, hipGetLastError());
+    return CHIP_OK;
+}
+
+int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_status, chip_conflict* out, uint64_t cap,
+                           uint64_t* n_out) {
+    if (!u) return CHIP_E_ARG;
+    if (!u->open || !n_out || (u->ntx && (!decision || !tx_status)) || (cap && !out))
+        return ufail(u, CHIP_E_ARG, "no batch in flight / null argument");
+    hipStream_t st = u->bst;
+    const uint64_t nref = u->nref, ntx = u->ntx;
+    u->open = false;
+    uint32_t* flag = u->flag.as<uint32_t>();
+    uint32_t* at = u->scan.as<uint32_t>();
+    unsigned long long* d_ins = u->ctr.as<unsigned long long>() + 1;
+    UCHK(u, hipMemsetAsync(d_ins, 0, 8, st));
+    uint32_t last[2] = {0, 0};
+    unsigned long long ins = 0;
+    if (nref) {
+        hipLaunchKernelGGL(k_uniq_flag, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->reftx.as<uint32_t>(), u->start,
+                           u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->bcommit.as<unsigned long long>(),
+                           u->st.as<uint8_t>(), flag);
+        size_t tmp = 0;
+        UCHK(u, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, flag, at, (int)nref, st));
+        UCHK(u, u->cub.ensure(tmp + 16));
+        UCHK(u, hipcub::DeviceScan::ExclusiveSum(u->cub.p, tmp, flag, at, (int)nref, st));
+        hipLaunchKernelGGL(k_uniq_emit, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->reftx.as<uint32_t>(), u->pos,
+                           u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->bcommit.as<unsigned long long>(), u->ids,
+                           u->callers, u->tab, flag, at, out, cap);
+        // inserts after the records: emit reads pre-committed slots, inserts only fill empty ones
+        hipLaunchKernelGGL(k_uniq_insert, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->refs, u->reftx.as<uint32_t>(),
+                           u->pos, u->start, u->st.as<uint8_t>(), u->bslot.as<uint32_t>(), u->ids, u->callers, u->tab,
+                           u->cap, d_ins);
+        UCHK(u, hipMemcpyAsync(&last[0], at + nref - 1, 4, hipMemcpyDeviceToHost, st));
+        UCHK(u, hipMemcpyAsync(&last[1], flag + nref - 1, 4, hipMemcpyDeviceToHost, st));
+        UCHK(u, hipMemcpyAsync(&ins, d_ins, 8, hipMemcpyDeviceToHost, st));
+    }
+    if (ntx)
+        hipLaunchKernelGGL(k_uniq_status, dim3(blocks_for(ntx)), dim3(256), 0, st, ntx, u->st.as<uint8_t>(), decision,
+                           tx_status);
+    UCHK(u, hipGetLastError());
+    UCHK(u, hipStreamSynchronize(st));
+    const uint64_t nout = (uint64_t)last[0] + last[1];
+    u->size += ins;
+    *n_out = nout;
+    return nout > cap ? ufail(u, CHIP_E_CAPACITY, "more conflict records than capacity") : CHIP_OK;
+}
+
+// one shard owning the whole key space: rounds with decision = vote
+static int commit_device(chip_uniq* u, const chip_uniq_shard_batch* b, uint8_t* tx_status, chip_conflict* out,
+                         uint64_t cap, uint64_t* n_out, hipStream_t st) {
+    int r = chip_uniq_shard_begin(u, b, st);
+    if (r) return r;
+    if (u->h_vote.ensure(b->ntx + 16) != hipSuccess) {
+        u->open = false;
+        return ufail(u, CHIP_E_NOMEM, "vote buffer");
+    }
+    uint8_t* vote = u->h_vote.as<uint8_t>();
+    for (uint64_t round = 0; round <= b->ntx; round++) {
+        uint64_t und = 0;
+        if ((r = chip_uniq_shard_vote(u, vote)) || (r = chip_uniq_shard_apply(u, vote, &und))) {
+            u->open = false;
+            return r;
+        }
+        if (!und) break;
+    }
+    if ((r = chip_uniq_shard_classify(u, vote))) {
+        u->open = false;
+        return r;
+    }
+    return chip_uniq_shard_finish(u, vote, tx_status, out, cap, n_out);
+}
+
+int chip_uniq_commit_batch_device(chip_uniq* u, uint64_t ntx, const uint64_t* start, uint64_t nref,
+                                  const uint8_t* refs36, const uint8_t* tx_ids, const uint32_t* callers,
+                                  uint8_t* tx_status, chip_conflict* out, uint64_t cap, uint64_t* n_out, void* stream) {
+    if (!u || !n_out) return CHIP_E_ARG;
+    *n_out = 0;
+    if (!ntx) return CHIP_OK;
+    if (u->open) return ufail(u, CHIP_E_ARG, "a shard batch is in flight");
+    if (!start || !tx_ids || !callers || !tx_status || (nref && !refs36)) return ufail(u, CHIP_E_ARG, "null argument");
+    if (nref >= 0x7fffffffull || ntx >= 0xffffffffull) return ufail(u, CHIP_E_ARG, "batch too large");
+    UCHK(u, hipSetDevice(u->device));
+    hipStream_t st = stream ? (hipStream_t)stream : u->stream;
+    UCHK(u, u->refpos.ensure(nref * 4 + 16));
+    hipLaunchKernelGGL(k_ref_tx, dim3(blocks_for(ntx)), dim3(256), 0, st, ntx, start, (uint32_t*)nullptr,
+                       u->refpos.as<uint32_t>());
+    UCHK(u, hipGetLastError());
+    chip_uniq_shard_batch b{ntx, start, nref, refs36, u->refpos.as<uint32_t>(), tx_ids, callers};
+    return commit_device(u, &b, tx_status, out, cap, n_out, st);
 }
 
 int chip_uniq_commit_batch(chip_uniq* u, uint64_t ntx, const uint64_t* start, const uint8_t* refs36,
@@ -470,103 +743,34 @@ int chip_uniq_commit_batch(chip_uniq* u, uint64_t ntx, const uint64_t* start, co
     if (!ntx) return CHIP_OK;
     const uint64_t nref = start[ntx];
     if (nref && !refs36) return CHIP_E_ARG;
+    if (start[0] != 0) return ufail(u, CHIP_E_ARG, "tx_ref_start[0] != 0");
     for (uint64_t t = 0; t < ntx; t++)
         if (start[t] > start[t + 1]) return ufail(u, CHIP_E_ARG, "tx_ref_start not monotone");
-    if (ntx >= 0xffffffffull || nref >= 0xffffffffull) return ufail(u, CHIP_E_ARG, "batch too large");
+    if (ntx >= 0xffffffffull || nref >= 0x7fffffffull) return ufail(u, CHIP_E_ARG, "batch too large");
+    if (u->open) return ufail(u, CHIP_E_ARG, "a shard batch is in flight");
     UCHK(u, hipSetDevice(u->device));
-    int rc = ensure_capacity(u, nref);
-    if (rc) return rc;
-    const uint64_t bcap = pow2_at_least(2 * (nref + 1));
-    // scratch layout (16-byte aligned pieces)
-    auto al = [](size_t x) { return (x + 15) & ~(size_t)15; };
-    size_t off = 0;
-    const size_t o_refs = off; off += al(nref * 36);
-    const size_t o_start = off; off += al((ntx + 1) * 8);
-    const size_t o_ids = off; off += al(ntx * 32);
-    const size_t o_call = off; off += al(ntx * 4);
-    const size_t o_pre = off; off += al(nref * 8);
-    const size_t o_bslot = off; off += al(nref * 4);
-    const size_t o_reftx = off; off += al(nref * 4);
-    const size_t o_refpos = off; off += al(nref * 4);
-    const size_t o_bowner = off; off += al(bcap * 4);
-    const size_t o_bmin = off; off += al(bcap * 4);
-    const size_t o_bcommit = off; off += al(bcap * 8);
-    const size_t o_st = off; off += al(ntx);
-    const size_t o_ctr = off; off += 64;
-    const size_t o_out = off; off += al((nref + 1) * sizeof(chip_conflict));
-    uint8_t* s = (uint8_t*)scratch(u, off);
-    if (!s) return ufail(u, CHIP_E_NOMEM, "scratch");
-    uint8_t* d_refs = s + o_refs;
-    uint64_t* d_start = (uint64_t*)(s + o_start);
-    uint8_t* d_ids = s + o_ids;
-    uint32_t* d_call = (uint32_t*)(s + o_call);
-    int64_t* d_pre = (int64_t*)(s + o_pre);
-    uint32_t* d_bslot = (uint32_t*)(s + o_bslot);
-    uint32_t* d_reftx = (uint32_t*)(s + o_reftx);
-    uint32_t* d_refpos = (uint32_t*)(s + o_refpos);
-    uint32_t* d_bowner = (uint32_t*)(s + o_bowner);
-    uint32_t* d_bmin = (uint32_t*)(s + o_bmin);
-    unsigned long long* d_bcommit = (unsigned long long*)(s + o_bcommit);
-    uint8_t* d_st = s + o_st;
-    uint32_t* d_undec = (uint32_t*)(s + o_ctr);
-    unsigned long long* d_nout = (unsigned long long*)(s + o_ctr + 16);
-    unsigned long long* d_ins = (unsigned long long*)(s + o_ctr + 32);
-    chip_conflict* d_out = (chip_conflict*)(s + o_out);
     hipStream_t st = u->stream;
-    if (nref) UCHK(u, hipMemcpyAsync(d_refs, refs36, nref * 36, hipMemcpyHostToDevice, st));
-    UCHK(u, hipMemcpyAsync(d_start, start, (ntx + 1) * 8, hipMemcpyHostToDevice, st));
-    UCHK(u, hipMemcpyAsync(d_ids, tx_ids, ntx * 32, hipMemcpyHostToDevice, st));
-    UCHK(u, hipMemcpyAsync(d_call, callers, ntx * 4, hipMemcpyHostToDevice, st));
-    UCHK(u, hipMemsetAsync(d_bowner, 0, bcap * 4, st));
-    UCHK(u, hipMemsetAsync(d_bcommit, 0xff, bcap * 8, st));
-    UCHK(u, hipMemsetAsync(d_st, ST_UNDECIDED, ntx, st));
-    UCHK(u, hipMemsetAsync(s + o_ctr, 0, 64, st));
-    hipLaunchKernelGGL(k_ref_tx, dim3(blocks_for(ntx)), dim3(256), 0, st, ntx, d_start, d_reftx, d_refpos);
-    if (nref) {
-        hipLaunchKernelGGL(k_uniq_lookup, dim3(blocks_for(nref)), dim3(256), 0, st, nref, d_refs, u->key, u->used, u->cap,
-                           d_pre);
-        hipLaunchKernelGGL(k_uniq_intern, dim3(blocks_for(nref)), dim3(256), 0, st, nref, d_refs, d_bowner, bcap,
-                           d_bslot);
-    }
-    // ordered-commit rounds
-    for (uint64_t round = 0; round <= ntx; round++) {
-        UCHK(u, hipMemsetAsync(d_bmin, 0xff, bcap * 4, st));
-        UCHK(u, hipMemsetAsync(d_undec, 0, 4, st));
-        if (nref)
-            hipLaunchKernelGGL(k_uniq_round_min, dim3(blocks_for(nref)), dim3(256), 0, st, nref, d_reftx, d_bslot, d_st,
-                               d_bmin);
-        hipLaunchKernelGGL(k_uniq_decide, dim3(blocks_for(ntx)), dim3(256), 0, st, ntx, d_start, d_pre, d_bslot, d_bmin,
-                           d_st, d_bcommit, d_undec);
-        uint32_t und = 0;
-        UCHK(u, hipMemcpyAsync(&und, d_undec, 4, hipMemcpyDeviceToHost, st));
-        UCHK(u, hipStreamSynchronize(st));
-        if (!und) break;
-    }
-    // inserts of committed txs before classification reuses the status bytes
-    if (nref)
-        hipLaunchKernelGGL(k_uniq_insert, dim3(blocks_for(nref)), dim3(256), 0, st, nref, d_refs, d_reftx, d_refpos,
-                           d_start, d_st, d_pre, d_bslot, d_bowner, d_ids, d_call, u->key, u->val, u->used, u->cap,
-                           d_ins);
-    hipLaunchKernelGGL(k_uniq_classify, dim3(blocks_for(ntx)), dim3(256), 0, st, ntx, d_start, d_refs, d_pre, d_bslot,
-                       d_bcommit, d_ids, d_call, u->val, d_st, d_out, nref + 1, d_nout);
-    UCHK(u, hipGetLastError());
-    unsigned long long nout = 0, ins = 0;
-    UCHK(u, hipMemcpyAsync(tx_status, d_st, ntx, hipMemcpyDeviceToHost, st));
-    UCHK(u, hipMemcpyAsync(&nout, d_nout, 8, hipMemcpyDeviceToHost, st));
-    UCHK(u, hipMemcpyAsync(&ins, d_ins, 8, hipMemcpyDeviceToHost, st));
-    UCHK(u, hipStreamSynchronize(st));
-    u->size += ins;
-    std::vector<chip_conflict> recs(nout);
-    if (nout) {
-        UCHK(u, hipMemcpy(recs.data(), d_out, nout * sizeof(chip_conflict), hipMemcpyDeviceToHost));
-        std::sort(recs.begin(), recs.end(), [](const chip_conflict& x, const chip_conflict& y) {
-            return x.tx != y.tx ? x.tx < y.tx : x.input_index < y.input_index;
-        });
-    }
+    UCHK(u, u->h_start.ensure((ntx + 1) * 8));
+    UCHK(u, u->h_refs.ensure(nref * 36 + 16));
+    UCHK(u, u->h_ids.ensure(ntx * 32));
+    UCHK(u, u->h_call.ensure(ntx * 4));
+    UCHK(u, u->h_st.ensure(ntx + 16));
+    UCHK(u, u->h_out.ensure((nref + 1) * sizeof(chip_conflict)));
+    if (nref) UCHK(u, hipMemcpyAsync(u->h_refs.p, refs36, nref * 36, hipMemcpyHostToDevice, st));
+    UCHK(u, hipMemcpyAsync(u->h_start.p, start, (ntx + 1) * 8, hipMemcpyHostToDevice, st));
+    UCHK(u, hipMemcpyAsync(u->h_ids.p, tx_ids, ntx * 32, hipMemcpyHostToDevice, st));
+    UCHK(u, hipMemcpyAsync(u->h_call.p, callers, ntx * 4, hipMemcpyHostToDevice, st));
+    uint64_t nout = 0;
+    int r = chip_uniq_commit_batch_device(u, ntx, u->h_start.as<uint64_t>(), nref, u->h_refs.as<uint8_t>(),
+                                          u->h_ids.as<uint8_t>(), u->h_call.as<uint32_t>(), u->h_st.as<uint8_t>(),
+                                          u->h_out.as<chip_conflict>(), nref + 1, &nout, st);
+    if (r) return r;
+    UCHK(u, hipMemcpyAsync(tx_status, u->h_st.p, ntx, hipMemcpyDeviceToHost, st));
     const uint64_t w = std::min<uint64_t>(nout, cap);
-    if (w && out) std::copy(recs.begin(), recs.begin() + w, out);
+    if (w && out) UCHK(u, hipMemcpyAsync(out, u->h_out.p, w * sizeof(chip_conflict), hipMemcpyDeviceToHost, st));
+    UCHK(u, hipStreamSynchronize(st));
     *n_out = nout;
-    return (nout > cap) ? CHIP_E_CAPACITY : CHIP_OK;
+    return nout > cap ? ufail(u, CHIP_E_CAPACITY, "more conflict records than capacity") : CHIP_OK;
 }
 
 }  // extern "C"

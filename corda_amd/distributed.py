@@ -74,3 +74,132 @@ def verify_sharded(verify_fn, batch, group=None):
     lo, hi = ranges[rank]
     local = verify_fn(sub_batch(batch, lo, hi))
     return gather_status(local, ranges, group)
+
+
+# ---------------------------------------------------------------------------------------
+# Notary uniqueness across GPUs.  The StateRef key space is partitioned: the
+# owner of a state is a hash of its key, every rank holds its slice of the commit log in its own
+# HBM (chip_uniq), the host routes each input to its owner (no all-to-all), and the ordered-commit
+# rounds exchange one u8 vote per transaction per round with an all-reduce MAX (RCCL over xGMI).
+_MIX1 = np.uint64(0xff51afd7ed558ccd)
+_MIX2 = np.uint64(0xc4ceb9fe1a85ec53)
+_GOLD = np.uint64(0x9E3779B97F4A7C15)
+
+
+def state_owner(refs36, world: int) -> np.ndarray:
+    """Owner rank of each 36-byte StateRef key (32-byte txhash || LE u32 index): a 64-bit mix of
+    the txhash prefix and the index.  Deterministic, so every rank computes the same map."""
+    r = np.ascontiguousarray(np.asarray(refs36, dtype=np.uint8)).reshape(-1, 36)
+    if world == 1 or len(r) == 0:
+        return np.zeros(len(r), dtype=np.int64)
+    h = np.ascontiguousarray(r[:, 0:8]).view("<u8").reshape(-1).copy()
+    idx = np.ascontiguousarray(r[:, 32:36]).view("<u4").reshape(-1).astype(np.uint64)
+    with np.errstate(over="ignore"):
+        h ^= idx * _GOLD
+        h ^= h >> np.uint64(33)
+        h *= _MIX1
+        h ^= h >> np.uint64(33)
+        h *= _MIX2
+        h ^= h >> np.uint64(33)
+    return (h % np.uint64(world)).astype(np.int64)
+
+
+class UniqShard:
+    """The inputs of a batch one rank owns, grouped by transaction in input order:
+    tx t's local inputs are refs[ref_start[t]:ref_start[t+1]], ref_pos their positions in t's
+    full input list (chip_uniq_shard_batch layout)."""
+
+    def __init__(self, ref_start, refs, ref_pos):
+        self.ref_start = ref_start
+        self.refs = refs
+        self.ref_pos = ref_pos
+
+    @property
+    def nref(self):
+        return int(self.ref_start[-1])
+
+
+def route_uniq_batch(tx_ref_start, refs36, world: int):
+    """Split a commit batch (tx_ref_start u64[ntx+1], refs 36-byte keys) into one UniqShard per rank."""
+    start = np.asarray(tx_ref_start, dtype=np.uint64)
+    ntx = len(start) - 1
+    nref = int(start[-1]) if ntx >= 0 else 0
+    refs = np.asarray(refs36, dtype=np.uint8)[:nref * 36].reshape(nref, 36)
+    counts = np.diff(start.astype(np.int64))
+    ref_tx = np.repeat(np.arange(ntx, dtype=np.int64), counts)
+    pos = (np.arange(nref, dtype=np.int64) - start[:-1].astype(np.int64)[ref_tx]).astype(np.uint32)
+    own = state_owner(refs, world)
+    shards = []
+    for r in range(world):
+        sel = np.nonzero(own == r)[0]
+        ls = np.zeros(ntx + 1, dtype=np.uint64)
+        if ntx:
+            ls[1:] = np.cumsum(np.bincount(ref_tx[sel], minlength=ntx)).astype(np.uint64)
+        shards.append(UniqShard(ls, np.ascontiguousarray(refs[sel]).reshape(-1), pos[sel].copy()))
+    return shards
+
+
+def route_rows(refs36, world: int):
+    """Committed rows (e.g. AppendOnlyPersistentMap.allPersisted) -> row indices each rank owns."""
+    own = state_owner(refs36, world)
+    return [np.nonzero(own == r)[0] for r in range(world)]
+
+
+def merge_records(per_shard):
+    """Union of the shards' Conflict.stateHistory records in (tx, input_index) order."""
+    out = [rec for recs in per_shard for rec in recs]
+    out.sort(key=lambda rec: (rec[0], rec[1]))
+    return out
+
+
+def commit_sharded_local(engines, batch):
+    """All shards in one process (tests, one-GPU rehearsal of the protocol): the MAX all-reduce is an
+    element-wise maximum over the shards' vote tensors.  `engines[r]` owns state_owner(...) == r."""
+    import torch
+    shards = route_uniq_batch(batch.tx_ref_start, batch.refs, len(engines))
+    for e, s in zip(engines, shards):
+        e.begin(s, batch.tx_ids, batch.callers)
+
+    def reduce_max(votes):
+        d = votes[0].clone()
+        for v in votes[1:]:
+            d = torch.maximum(d, v.to(d.device))
+        return d
+    rounds = 0
+    while True:
+        d = reduce_max([e.vote() for e in engines])
+        und = [e.apply(d.to(e.vote_buf.device) if hasattr(e, "vote_buf") else d) for e in engines]
+        rounds += 1
+        assert len(set(und)) == 1, "shards disagree on the undecided count"
+        if und[0] == 0:
+            break
+    d = reduce_max([e.classify() for e in engines])
+    outs = [e.finish(d.to(e.vote_buf.device) if hasattr(e, "vote_buf") else d) for e in engines]
+    return outs[0][0], merge_records([o[1] for o in outs]), rounds
+
+
+def commit_sharded(engine, batch, group=None, shard=None):
+    """This rank's part of a multi-GPU commit: route the batch, run the ordered-commit rounds with
+    one all-reduce MAX of the per-tx vote bytes per round, classify the failed transactions with one
+    more, and all-gather the conflict records.  Returns (status u8[ntx], records, rounds) on every
+    rank.  `shard` may be this rank's pre-uploaded shard (engine.upload) to keep inputs resident."""
+    import torch.distributed as dist
+    world, rank = dist.get_world_size(group), dist.get_rank(group)
+    if shard is None:
+        shard = route_uniq_batch(batch.tx_ref_start, batch.refs, world)[rank]
+        engine.begin(shard, batch.tx_ids, batch.callers)
+    else:
+        engine.begin(shard)
+    rounds = 0
+    while True:
+        v = engine.vote()
+        dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
+        rounds += 1
+        if engine.apply(v) == 0:
+            break
+    v = engine.classify()
+    dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
+    status, recs = engine.finish(v)
+    gathered = [None] * world
+    dist.all_gather_object(gathered, recs, group=group)
+    return status, merge_records(gathered), rounds

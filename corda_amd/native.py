@@ -33,6 +33,8 @@ SCHEME_K1, SCHEME_R1, SCHEME_ED25519 = 2, 3, 4
 EXPORTS = ["chip_abi_version", "chip_device_count", "chip_init", "chip_shutdown", "chip_last_error",
            "chip_verify_batch", "chip_verify_batch_device", "chip_txid_batch", "chip_txid_batch_device",
            "chip_uniq_open", "chip_uniq_close", "chip_uniq_size", "chip_uniq_rebuild", "chip_uniq_commit_batch",
+           "chip_uniq_commit_batch_device", "chip_uniq_last_error", "chip_uniq_shard_begin", "chip_uniq_shard_vote",
+           "chip_uniq_shard_apply", "chip_uniq_shard_classify", "chip_uniq_shard_finish",
            "chip_get_stats", "chip_reset_stats"]
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -58,6 +60,12 @@ class ChipTxBatch(ctypes.Structure):
                 ("ncomp", ctypes.c_uint64), ("comp_group", ctypes.c_void_p), ("comp_internal", ctypes.c_void_p),
                 ("data", ctypes.c_void_p), ("comp_off", ctypes.c_void_p), ("comp_len", ctypes.c_void_p),
                 ("data_bytes", ctypes.c_uint64)]
+
+
+class ChipUniqShardBatch(ctypes.Structure):
+    _fields_ = [("ntx", ctypes.c_uint64), ("ref_start", ctypes.c_void_p), ("nref", ctypes.c_uint64),
+                ("refs36", ctypes.c_void_p), ("ref_pos", ctypes.c_void_p), ("tx_ids", ctypes.c_void_p),
+                ("callers", ctypes.c_void_p)]
 
 
 class ChipConflict(ctypes.Structure):
@@ -111,6 +119,18 @@ def load(build_if_missing: bool = False):
                                       ctypes.c_void_p, ctypes.c_void_p]
     lib.chip_uniq_commit_batch.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
+    lib.chip_uniq_commit_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint64,
+                                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                  ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64),
+                                                  ctypes.c_void_p]
+    lib.chip_uniq_last_error.restype = ctypes.c_char_p
+    lib.chip_uniq_last_error.argtypes = [ctypes.c_void_p]
+    lib.chip_uniq_shard_begin.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipUniqShardBatch), ctypes.c_void_p]
+    lib.chip_uniq_shard_vote.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.chip_uniq_shard_apply.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.POINTER(ctypes.c_uint64)]
+    lib.chip_uniq_shard_classify.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    lib.chip_uniq_shard_finish.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
     lib.chip_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipStats)]
     lib.chip_reset_stats.argtypes = [ctypes.c_void_p]
@@ -253,10 +273,24 @@ class UniqTable:
     def size(self) -> int:
         return int(self.ctx.lib.chip_uniq_size(self.h))
 
+    def _check(self, rc):
+        if rc != 0:
+            raise ChipError(rc, self.ctx.lib.chip_uniq_last_error(self.h).decode(errors="replace"))
+
     def rebuild(self, refs36, tx32, idx, caller):
         n = len(idx)
-        self.ctx._check(self.ctx.lib.chip_uniq_rebuild(self.h, ctypes.c_uint64(n), _ptr(refs36), _ptr(tx32),
-                                                       _ptr(idx), _ptr(caller)))
+        self._check(self.ctx.lib.chip_uniq_rebuild(self.h, ctypes.c_uint64(n), _ptr(refs36), _ptr(tx32),
+                                                   _ptr(idx), _ptr(caller)))
+
+    def commit_batch_device(self, tx_ref_start, nref, refs36, tx_ids, callers, tx_status, out, cap, stream=None):
+        """Device-resident commit (torch tensors on this GPU).  Returns the full conflict-record count;
+        the first min(count, cap) records are in `out` (ChipConflict layout, 48 bytes each)."""
+        ntx = tx_ref_start.numel() - 1
+        nout = ctypes.c_uint64()
+        self._check(self.ctx.lib.chip_uniq_commit_batch_device(
+            self.h, ctypes.c_uint64(ntx), _ptr(tx_ref_start), ctypes.c_uint64(nref), _ptr(refs36), _ptr(tx_ids),
+            _ptr(callers), _ptr(tx_status), _ptr(out), ctypes.c_uint64(cap), ctypes.byref(nout), stream or None))
+        return nout.value
 
     def commit_batch(self, tx_ref_start, refs36, tx_ids, callers, cap=None):
         ntx = len(tx_ref_start) - 1
@@ -265,9 +299,88 @@ class UniqTable:
             cap = int(tx_ref_start[-1]) + 1
         out = (ChipConflict * max(cap, 1))()
         nout = ctypes.c_uint64()
-        self.ctx._check(self.ctx.lib.chip_uniq_commit_batch(self.h, ctypes.c_uint64(ntx), _ptr(tx_ref_start),
+        self._check(self.ctx.lib.chip_uniq_commit_batch(self.h, ctypes.c_uint64(ntx), _ptr(tx_ref_start),
                                                             _ptr(refs36), _ptr(tx_ids), _ptr(callers), _ptr(st),
                                                             out, ctypes.c_uint64(cap), ctypes.byref(nout)))
         recs = [(c.tx, c.input_index, c.consumed_index, bytes(c.consuming_tx), c.consuming_caller)
                 for c in out[:min(nout.value, cap)]]
         return st, recs
+
+
+def records_from_bytes(raw: bytes):
+    """ChipConflict records (48 bytes each) -> [(tx, input_index, consumed_index, consuming_tx, caller)]."""
+    n = len(raw) // ctypes.sizeof(ChipConflict)
+    arr = (ChipConflict * n).from_buffer_copy(raw[:n * ctypes.sizeof(ChipConflict)])
+    return [(c.tx, c.input_index, c.consumed_index, bytes(c.consuming_tx), c.consuming_caller) for c in arr]
+
+
+class UniqShardEngine:
+    """One GPU's slice of the notary table driven through the chip_uniq_shard_* phases (the
+    multi-GPU protocol is corda_amd.distributed.commit_sharded).  Device buffers are torch tensors
+    on the table's GPU; the phases run on torch's current stream, so RCCL collectives issued by
+    torch on that stream's tensors are ordered with them."""
+
+    def __init__(self, table: UniqTable):
+        self.table = table
+        self.lib = table.ctx.lib
+        self.device = table.ctx.device
+        self._keep = None
+
+    def upload(self, shard, tx_ids, callers):
+        """Host shard arrays -> device tensors (outside any timed region)."""
+        import torch
+        dev = torch.device("cuda", self.device)
+
+        def t(a, dt):
+            a = np.ascontiguousarray(a)
+            if a.size == 0:
+                a = np.zeros(16, dtype=a.dtype)
+            return torch.from_numpy(a.view(dt)).to(dev)
+        ntx = len(shard.ref_start) - 1
+        return {"ntx": ntx, "nref": int(shard.ref_start[-1]),
+                "start": t(np.asarray(shard.ref_start, dtype=np.uint64), np.int64),
+                "refs": t(np.asarray(shard.refs, dtype=np.uint8), np.uint8),
+                "pos": t(np.asarray(shard.ref_pos, dtype=np.uint32), np.int32),
+                "ids": t(np.asarray(tx_ids, dtype=np.uint8), np.uint8),
+                "callers": t(np.asarray(callers, dtype=np.uint32), np.int32)}
+
+    def begin(self, shard, tx_ids=None, callers=None):
+        """`shard`: a host UniqShard (uploaded here) or the dict upload() returned (device-resident)."""
+        import torch
+        d = shard if isinstance(shard, dict) else self.upload(shard, tx_ids, callers)
+        self._keep = d
+        self.ntx = d["ntx"]
+        dev = torch.device("cuda", self.device)
+        self.vote_buf = torch.zeros(max(1, self.ntx), dtype=torch.uint8, device=dev)
+        self.status = torch.zeros(max(1, self.ntx), dtype=torch.uint8, device=dev)
+        b = ChipUniqShardBatch(self.ntx, d["start"].data_ptr(), d["nref"], d["refs"].data_ptr(), d["pos"].data_ptr(),
+                               d["ids"].data_ptr(), d["callers"].data_ptr())
+        stream = torch.cuda.current_stream(dev).cuda_stream
+        self.table._check(self.lib.chip_uniq_shard_begin(self.table.h, ctypes.byref(b), stream or None))
+
+    def vote(self):
+        self.table._check(self.lib.chip_uniq_shard_vote(self.table.h, self.vote_buf.data_ptr()))
+        return self.vote_buf[:self.ntx]
+
+    def apply(self, decision) -> int:
+        und = ctypes.c_uint64()
+        self.table._check(self.lib.chip_uniq_shard_apply(self.table.h, decision.data_ptr(), ctypes.byref(und)))
+        return und.value
+
+    def classify(self):
+        self.table._check(self.lib.chip_uniq_shard_classify(self.table.h, self.vote_buf.data_ptr()))
+        return self.vote_buf[:self.ntx]
+
+    def finish(self, decision):
+        """-> (status u8[ntx] numpy, this shard's conflict records)."""
+        import torch
+        cap = int(self._keep["nref"]) + 1
+        out = torch.empty(cap * ctypes.sizeof(ChipConflict), dtype=torch.uint8,
+                          device=torch.device("cuda", self.device))
+        nout = ctypes.c_uint64()
+        self.table._check(self.lib.chip_uniq_shard_finish(self.table.h, decision.data_ptr(), self.status.data_ptr(),
+                                                          out.data_ptr(), ctypes.c_uint64(cap), ctypes.byref(nout)))
+        n = min(nout.value, cap)
+        raw = out[:n * ctypes.sizeof(ChipConflict)].cpu().numpy().tobytes()
+        self._keep = None
+        return self.status[:self.ntx].cpu().numpy(), records_from_bytes(raw)

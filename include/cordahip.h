@@ -182,6 +182,46 @@ int chip_uniq_rebuild(chip_uniq* u, uint64_t n, const uint8_t* refs36, const uin
 int chip_uniq_commit_batch(chip_uniq* u, uint64_t ntx, const uint64_t* tx_ref_start,
                            const uint8_t* refs36, const uint8_t* tx_ids, const uint32_t* callers,
                            uint8_t* tx_status, chip_conflict* out, uint64_t cap, uint64_t* n_out);
+/* The same with every array in device memory of the table's GPU (nref = tx_ref_start[ntx], passed
+ * by the caller since the offsets are on the device).  `out` (device, `cap` records) is written in
+ * (tx, input_index) order; *n_out (host) is the full record count.  Returns after completion. */
+int chip_uniq_commit_batch_device(chip_uniq* u, uint64_t ntx, const uint64_t* tx_ref_start, uint64_t nref,
+                                  const uint8_t* refs36, const uint8_t* tx_ids, const uint32_t* callers,
+                                  uint8_t* tx_status, chip_conflict* out, uint64_t cap, uint64_t* n_out,
+                                  void* stream);
+/* Message of the last failing chip_uniq_* call on this table. */
+const char* chip_uniq_last_error(const chip_uniq* u);
+
+/* ---------------------------------------------------------------------------------------
+ * Multi-GPU notary uniqueness: the key space is partitioned across GPUs (owner =
+ * a hash of the StateRef, chosen by the host), each GPU's chip_uniq holds its slice.  Every shard
+ * sees every transaction of the batch (ids, callers) but only the inputs it owns: ref_start[t] ..
+ * ref_start[t+1] are tx t's local inputs, in input order, ref_pos their positions in the tx's full
+ * input list.  The commit runs in ordered-commit rounds; between the phases the caller combines
+ * the per-tx u8 votes of all shards with an element-wise MAX (RCCL all-reduce over xGMI) and hands
+ * the result back as `decision` (on one GPU: decision = vote).  All arrays are device memory of the
+ * shard's GPU and must stay valid until shard_finish; the phases run on the stream given to begin.
+ *   begin                                     lookup + intern
+ *   loop { vote(v); v := allreduce_max(v); apply(v, &undecided) } until undecided == 0
+ *   classify(v); v := allreduce_max(v); finish(v, status, out, cap, &n)
+ * finish writes this shard's Conflict.stateHistory records (device `out`, ordered by (tx,
+ * input_index)); the union over shards merged by (tx, input_index) is the single-GPU record list. */
+typedef struct {
+    uint64_t ntx;
+    const uint64_t* ref_start;   /* [ntx + 1]        */
+    uint64_t nref;               /* = ref_start[ntx] */
+    const uint8_t* refs36;       /* [nref * 36]      */
+    const uint32_t* ref_pos;     /* [nref]           */
+    const uint8_t* tx_ids;       /* [ntx * 32]       */
+    const uint32_t* callers;     /* [ntx]            */
+} chip_uniq_shard_batch;
+
+int chip_uniq_shard_begin(chip_uniq* u, const chip_uniq_shard_batch* b, void* stream);
+int chip_uniq_shard_vote(chip_uniq* u, uint8_t* vote);
+int chip_uniq_shard_apply(chip_uniq* u, const uint8_t* decision, uint64_t* undecided);
+int chip_uniq_shard_classify(chip_uniq* u, uint8_t* vote);
+int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_status, chip_conflict* out,
+                           uint64_t cap, uint64_t* n_out);
 
 /* ---------------------------------------------------------------------------------------
  * Counters (observability; OutOfProcessTransactionVerifierService.kt:35-46 analogue). */

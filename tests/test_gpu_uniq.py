@@ -1,5 +1,6 @@
 """GPU parity: notary uniqueness (K4) vs the oracle restatement of PersistentUniquenessProvider.commit
 + TrustedAuthorityNotaryService.commitInputStates, and the reference's own scenarios."""
+import ctypes
 import hashlib
 
 import numpy as np
@@ -65,3 +66,61 @@ def test_uniq_multi_batch_and_growth(ctx, oracle):
     for g, r in outs:
         assert np.array_equal(g[0], r[0])
         assert g[1] == r[1]
+
+
+def test_uniq_device_entry_matches_host_entry(ctx, oracle):
+    """chip_uniq_commit_batch_device (inputs resident in HBM) == the host entry == the oracle."""
+    import torch
+    from corda_amd import native
+    pre, b = G.uniq_workload(30000, 40000, seed=9, pre_hit=0.02, dbl=0.02, resubmit=0.01)
+    dev = torch.device("cuda", 0)
+    t = ctx.uniq_open(1 << 17)
+    t.rebuild(*pre)
+    o = oracle.Uniq(1 << 17)
+    o.preload(*pre)
+    nref = int(b.tx_ref_start[-1])
+    d_start = torch.from_numpy(b.tx_ref_start.view(np.int64)).to(dev)
+    d_refs = torch.from_numpy(b.refs).to(dev)
+    d_ids = torch.from_numpy(b.tx_ids).to(dev)
+    d_call = torch.from_numpy(b.callers.view(np.int32)).to(dev)
+    d_st = torch.empty(b.ntx, dtype=torch.uint8, device=dev)
+    cap = nref + 1
+    rec = ctypes.sizeof(native.ChipConflict)
+    d_out = torch.empty(cap * rec, dtype=torch.uint8, device=dev)
+    n = t.commit_batch_device(d_start, nref, d_refs, d_ids, d_call, d_st, d_out, cap)
+    torch.cuda.synchronize()
+    recs = native.records_from_bytes(d_out[:min(n, cap) * rec].cpu().numpy().tobytes())
+    ws, wr = o.commit_batch(b.tx_ref_start, b.refs, b.tx_ids, b.callers)
+    assert np.array_equal(d_st.cpu().numpy(), ws)
+    assert recs == wr and n == len(wr)
+    assert t.size() == o.size()
+    t.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_uniq_sharded_gpu_shards_match_oracle(ctx, oracle, world):
+    """The multi-GPU protocol with `world` GPU shard tables (chip_uniq_shard_* kernels) on one
+    device; the all-reduce MAX is an element-wise max here.  Two batches, pre-committed rows routed
+    to their owners: statuses, records and table sizes equal the single-process oracle."""
+    from corda_amd import distributed as D
+    from corda_amd import native
+    pre, b = G.uniq_workload(20000, 30000, seed=12, pre_hit=0.02, dbl=0.03, resubmit=0.01)
+    _, b2 = G.uniq_workload(8000, 0, seed=13, pre_hit=0.0, dbl=0.03)
+    b2.refs[:36 * 4000] = b.refs[:36 * 4000]
+    tables = [ctx.uniq_open(1 << 14) for _ in range(world)]
+    refs, tx, idx, caller = pre
+    for r, rows in enumerate(D.route_rows(refs, world)):
+        tables[r].rebuild(refs.reshape(-1, 36)[rows].reshape(-1).copy(), tx.reshape(-1, 32)[rows].reshape(-1).copy(),
+                          idx[rows].copy(), caller[rows].copy())
+    engines = [native.UniqShardEngine(t) for t in tables]
+    o = oracle.Uniq(1 << 14)
+    o.preload(*pre)
+    for batch in (b, b2):
+        st, recs, rounds = D.commit_sharded_local(engines, batch)
+        ws, wr = o.commit_batch(batch.tx_ref_start, batch.refs, batch.tx_ids, batch.callers)
+        assert np.array_equal(st, ws)
+        assert recs == wr
+        assert rounds >= 2
+    assert sum(t.size() for t in tables) == o.size()
+    for t in tables:
+        t.close()
