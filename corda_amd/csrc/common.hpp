@@ -22,3 +22,27 @@ struct KeyMeta {
     uint8_t ok;
     uint8_t pad[2];
 };
+
+// Wave-level aggregation of per-key counters.  Lanes with `valid` set and equal `key` form a group;
+// every member learns its group's leader lane and its rank inside the group, the leader also the
+// group size.  One atomic per distinct key per wave instead of one per lane: a batch signed by a
+// single notary key would otherwise serialize on one address.  The loop is wave-uniform.
+CHIP_DEV void wave_group(bool valid, uint32_t key, uint32_t& leader, uint32_t& count, uint32_t& rank) {
+    const uint32_t lane = __lane_id();
+    uint64_t todo = __ballot(valid);
+    leader = 0;
+    count = 0;
+    rank = 0;
+    while (todo) {
+        const uint32_t l = (uint32_t)__builtin_ctzll(todo);
+        const uint32_t kl = __shfl(key, (int)l);
+        const bool mine = valid && key == kl;
+        const uint64_t m = __ballot(mine);
+        if (mine) {
+            leader = l;
+            rank = (uint32_t)__popcll(m & ((1ull << lane) - 1ull));
+        }
+        if (lane == l) count = (uint32_t)__popcll(m);
+        todo &= ~m;
+    }
+}

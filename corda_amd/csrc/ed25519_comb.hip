@@ -92,24 +92,31 @@ __global__ void __launch_bounds__(256) k_ed_comb_partition(const uint32_t* __res
                                                            uint32_t* __restrict__ key_cur, uint32_t* __restrict__ comb_list,
                                                            uint32_t* __restrict__ straus_list, uint32_t* __restrict__ ctr) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    bool straus = false;
-    uint32_t i = 0;
+    const uint32_t lane = threadIdx.x & 63;
+    bool straus = false, comb = false;
+    uint32_t i = 0, k = 0;
     if (g < *ed_count) {
         i = ed_list[g];
-        const uint32_t k = key_idx[i];
-        if (key_slot[k] >= 0) comb_list[key_base[k] + atomicAdd(&key_cur[k], 1u)] = i;
-        else straus = true;
+        k = key_idx[i];
+        comb = key_slot[k] >= 0;
+        straus = !comb;
     }
+    // one fill-cursor atomic per key per wave (a single-key batch must not serialize on key_cur)
+    uint32_t leader, cnt, rank;
+    wave_group(comb, k, leader, cnt, rank);
+    uint32_t cur = 0;
+    if (comb && lane == leader) cur = atomicAdd(&key_cur[k], cnt);
+    cur = __shfl(cur, (int)leader);
+    if (comb) comb_list[key_base[k] + cur + rank] = i;
     const uint64_t mask = __ballot(straus);
     if (!mask) return;
-    const uint32_t lane = threadIdx.x & 63;
-    const uint32_t leader = (uint32_t)__builtin_ctzll(mask);
+    const uint32_t sl = (uint32_t)__builtin_ctzll(mask);
     uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(&ctr[2], (uint32_t)__popcll(mask));
-    base = __shfl(base, leader);
+    if (lane == sl) base = atomicAdd(&ctr[2], (uint32_t)__popcll(mask));
+    base = __shfl(base, sl);
     if (straus) {
-        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
-        straus_list[base + rank] = i;
+        const uint32_t sr = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
+        straus_list[base + sr] = i;
     }
 }
 

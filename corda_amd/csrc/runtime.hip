@@ -54,6 +54,8 @@ struct chip_ctx {
         h_msg_off, h_msg_len, h_status, h_bitmap;
     // txid
     DevBuf t_salts, t_start, t_group, t_internal, t_data, t_off, t_len, t_ids, t_scratch;
+    // fused tx verification: device-built SignableData messages + staging of the host entry
+    DevBuf f_pool, f_moff, f_mlen, f_midx, f_htx, f_htm, f_tdata, f_toff, f_tlen, f_tid;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, tev0 = nullptr, tev1 = nullptr;
     bool ev_pending = false, tev_pending = false;
     chip_stats stats{};
@@ -121,8 +123,10 @@ __global__ void __launch_bounds__(256) k_classify(uint64_t n, const uint32_t* __
                                                   uint32_t* __restrict__ counts, uint32_t* __restrict__ key_count) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     int list = -1;
+    uint32_t k = 0;
     if (i < n) {
-        const uint32_t k = key_idx[i], m = msg_idx[i];
+        const uint32_t m = msg_idx[i];
+        k = key_idx[i];
         uint8_t st = 0xff;
         if (k >= n_keys || m >= n_msgs) {
             st = CHIP_UNSUPPORTED;   // malformed batch entry: hand back to the JCA path
@@ -135,11 +139,16 @@ __global__ void __launch_bounds__(256) k_classify(uint64_t n, const uint32_t* __
             else if (!km.ok) st = CHIP_KEY_INVALID;             // key never constructible
             else if (km.scheme == CHIP_SCHEME_ED25519 && sl != 64) st = CHIP_SIG_DECODE;  // length is wrong
             else list = km.scheme == CHIP_SCHEME_ED25519 ? LIST_ED25519 : (km.scheme == CHIP_SCHEME_R1 ? LIST_R1 : LIST_K1);
-            if (list == LIST_ED25519 && key_count) atomicAdd(&key_count[k], 1u);   // comb-path histogram
         }
         if (list < 0) status[i] = st;
     }
     const uint32_t lane = threadIdx.x & 63;
+    if (key_count) {   // comb-path histogram: signatures per Ed25519 key, one atomic per key per wave
+        uint32_t leader, cnt, rank;
+        const bool ed = list == LIST_ED25519;
+        wave_group(ed, k, leader, cnt, rank);
+        if (ed && lane == leader) atomicAdd(&key_count[k], cnt);
+    }
 #pragma unroll
     for (int L = 0; L < N_LISTS; L++) {
         const uint64_t mask = __ballot(list == L);
@@ -160,6 +169,49 @@ __global__ void __launch_bounds__(256) k_bitmap(uint64_t n, const uint8_t* __res
     const bool v = (i < n) && status[i] == CHIP_VALID;
     const uint64_t b = __ballot(v);
     if ((threadIdx.x & 63) == 0 && i < n) bitmap[i >> 6] = b;
+}
+
+// SignableData messages from templates: message m = tx * nt + t, stride-aligned in the pool;
+// one lane per output dword (coalesced stores), bytes from the template or the 32-byte id.
+__global__ void __launch_bounds__(256) k_build_msgs(uint64_t ntx, uint64_t nt, uint32_t stride,
+                                                    const uint8_t* __restrict__ ids, const uint8_t* __restrict__ tdata,
+                                                    const uint64_t* __restrict__ toff, const uint32_t* __restrict__ tlen,
+                                                    const uint32_t* __restrict__ tid_at, uint8_t* __restrict__ pool,
+                                                    uint64_t* __restrict__ moff, uint32_t* __restrict__ mlen) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t wpm = stride / 4;
+    const uint64_t m = g / wpm;
+    const uint32_t q = (uint32_t)(g % wpm);
+    if (m >= ntx * nt) return;
+    const uint64_t tx = m / nt, t = m % nt;
+    const uint32_t L = tlen[t], at = tid_at[t];
+    const uint8_t* tp = tdata + toff[t];
+    const uint8_t* id = ids + 32 * tx;
+    uint32_t w = 0;
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const uint32_t b = 4 * q + k;
+        uint32_t v = 0;
+        if (b < at) v = tp[b];
+        else if (b < at + 32) v = id[b - at];
+        else if (b < L + 32) v = tp[b - 32];
+        w |= v << (8 * k);
+    }
+    reinterpret_cast<uint32_t*>(pool + m * stride)[q] = w;
+    if (q == 0) {
+        moff[m] = m * stride;
+        mlen[m] = L + 32;
+    }
+}
+
+// msg_idx of each signature; out-of-range tx / template -> an index past the pool (UNSUPPORTED)
+__global__ void __launch_bounds__(256) k_sig_msg_idx(uint64_t n, const uint32_t* __restrict__ tx_idx,
+                                                     const uint32_t* __restrict__ tmpl_idx, uint64_t ntx, uint64_t nt,
+                                                     uint32_t* __restrict__ msg_idx) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t tx = tx_idx[i], t = tmpl_idx[i];
+    msg_idx[i] = (tx < ntx && t < nt) ? (uint32_t)(tx * nt + t) : 0xffffffffu;
 }
 
 template <class T>
@@ -220,7 +272,8 @@ void chip_shutdown(chip_ctx* c) {
                       &c->h_sig_data, &c->h_sig_off, &c->h_sig_len, &c->h_key_data, &c->h_key_off, &c->h_key_len,
                       &c->h_msg_data, &c->h_msg_off, &c->h_msg_len, &c->h_status, &c->h_bitmap, &c->t_salts,
                       &c->t_start, &c->t_group, &c->t_internal, &c->t_data, &c->t_off, &c->t_len, &c->t_ids,
-                      &c->t_scratch};
+                      &c->t_scratch, &c->f_pool, &c->f_moff, &c->f_mlen, &c->f_midx, &c->f_htx, &c->f_htm,
+                      &c->f_tdata, &c->f_toff, &c->f_tlen, &c->f_tid};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < chip_ctx::KRING; i++) {
         if (c->kring[i].a) hipEventDestroy(c->kring[i].a);
@@ -426,10 +479,7 @@ int chip_reset_stats(chip_ctx* c) {
 
 // ---------------------------------------------------------------------------------------
 // tx ids
-int chip_txid_batch_device(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids, void* stream) {
-    if (!c || !b || (!ids && b->ntx)) return fail(c, CHIP_E_ARG, "null argument");
-    std::lock_guard<std::mutex> g(c->mu);
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+static int txid_device_locked(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids, hipStream_t st) {
     HIPCHK(c, hipSetDevice(c->device));
     const uint64_t scratch_words = b->ntx * 64 * 8 + b->ncomp * 8 + 64;
     HIPCHK(c, c->t_scratch.ensure(scratch_words * 4));
@@ -442,6 +492,12 @@ int chip_txid_batch_device(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids, vo
     c->tev_pending = true;
     c->stats.txids += b->ntx;
     return CHIP_OK;
+}
+
+int chip_txid_batch_device(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids, void* stream) {
+    if (!c || !b || (!ids && b->ntx)) return fail(c, CHIP_E_ARG, "null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    return txid_device_locked(c, b, ids, stream ? (hipStream_t)stream : c->stream);
 }
 
 int chip_txid_batch(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids) {
@@ -482,6 +538,140 @@ int chip_txid_batch(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids) {
     HIPCHK(c, hipStreamSynchronize(st));
     float ms = 0;
     if (hipEventElapsedTime(&ms, c->tev0, c->tev1) == hipSuccess) c->stats.last_txid_kernel_ms = ms;
+    c->tev_pending = false;
+    return CHIP_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// fused: ids -> SignableData messages -> signer verification, one stream-ordered pipeline
+static int verify_tx_device_locked(chip_ctx* c, const chip_tx_batch* tb, const chip_msg_templates* tm,
+                                   const chip_signer_batch* sb, uint8_t* ids, uint8_t* status, uint64_t* bitmap,
+                                   hipStream_t st) {
+    const uint64_t ntx = tb->ntx, nt = tm->n, n = sb->n;
+    if (ntx * (nt ? nt : 1) >= 0xffffffffull || n >= 0xffffffffull) return fail(c, CHIP_E_ARG, "batch too large");
+    int r = txid_device_locked(c, tb, ids, st);
+    if (r) return r;
+    const uint32_t stride = (tm->max_len + 32 + 15) & ~15u;
+    const uint64_t nm = ntx * nt;
+    HIPCHK(c, c->f_pool.ensure(nm * stride + 16));
+    HIPCHK(c, c->f_moff.ensure(nm * 8 + 16));
+    HIPCHK(c, c->f_mlen.ensure(nm * 4 + 16));
+    HIPCHK(c, c->f_midx.ensure(n * 4 + 16));
+    if (nm) {
+        const uint64_t words = nm * (stride / 4);
+        hipLaunchKernelGGL(k_build_msgs, dim3((uint32_t)((words + 255) / 256)), dim3(256), 0, st, ntx, nt, stride, ids,
+                           tm->data, tm->off, tm->len, tm->id_at, c->f_pool.as<uint8_t>(), c->f_moff.as<uint64_t>(),
+                           c->f_mlen.as<uint32_t>());
+    }
+    if (n)
+        hipLaunchKernelGGL(k_sig_msg_idx, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, n, sb->tx_idx,
+                           sb->tmpl_idx, ntx, nt, c->f_midx.as<uint32_t>());
+    HIPCHK(c, hipGetLastError());
+    chip_sig_batch d{};
+    d.n = n;
+    d.key_idx = sb->key_idx;
+    d.msg_idx = c->f_midx.as<uint32_t>();
+    d.sig_data = sb->sig_data;
+    d.sig_off = sb->sig_off;
+    d.sig_len = sb->sig_len;
+    d.n_keys = sb->n_keys;
+    d.key_data = sb->key_data;
+    d.key_off = sb->key_off;
+    d.key_len = sb->key_len;
+    d.n_msgs = nm;
+    d.msg_data = c->f_pool.as<uint8_t>();
+    d.msg_off = c->f_moff.as<uint64_t>();
+    d.msg_len = c->f_mlen.as<uint32_t>();
+    d.sig_bytes = sb->sig_bytes;
+    d.key_bytes = sb->key_bytes;
+    d.msg_bytes = nm * stride;
+    return verify_device_locked(c, &d, status, bitmap, st);
+}
+
+int chip_verify_tx_batch_device(chip_ctx* c, const chip_tx_batch* tb, const chip_msg_templates* tm,
+                                const chip_signer_batch* sb, uint8_t* ids, uint8_t* status, uint64_t* bitmap,
+                                void* stream) {
+    if (!c || !tb || !tm || !sb || !status || (tb->ntx && !ids)) return fail(c, CHIP_E_ARG, "null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    return verify_tx_device_locked(c, tb, tm, sb, ids, status, bitmap, stream ? (hipStream_t)stream : c->stream);
+}
+
+int chip_verify_tx_batch(chip_ctx* c, const chip_tx_batch* b, const chip_msg_templates* tm, const chip_signer_batch* sb,
+                         uint8_t* ids, uint8_t* status, uint64_t* bitmap) {
+    if (!c || !b || !tm || !sb) return fail(c, CHIP_E_ARG, "null argument");
+    const uint64_t ntx = b->ntx, nc = b->ncomp, n = sb->n, nk = sb->n_keys, nt = tm->n;
+    if (ntx && (!b->salts || !b->tx_comp_start || !ids)) return fail(c, CHIP_E_ARG, "null tx array");
+    if (nc && (!b->comp_group || !b->comp_internal || !b->comp_off || !b->comp_len || !b->data))
+        return fail(c, CHIP_E_ARG, "null component array");
+    if (ntx && b->tx_comp_start[ntx] > nc) return fail(c, CHIP_E_ARG, "tx_comp_start out of range");
+    for (uint64_t t = 0; t < ntx; t++)
+        if (b->tx_comp_start[t] > b->tx_comp_start[t + 1]) return fail(c, CHIP_E_ARG, "tx_comp_start not monotone");
+    for (uint64_t k = 0; k < nc; k++)
+        if (b->comp_off[k] + b->comp_len[k] > b->data_bytes) return fail(c, CHIP_E_ARG, "component outside data pool");
+    if (nt && (!tm->data || !tm->off || !tm->len || !tm->id_at)) return fail(c, CHIP_E_ARG, "null template array");
+    for (uint64_t t = 0; t < nt; t++)
+        if (tm->off[t] + tm->len[t] > tm->data_bytes || tm->id_at[t] > tm->len[t] || tm->len[t] > tm->max_len)
+            return fail(c, CHIP_E_ARG, "template outside pool / id offset past its end / len > max_len");
+    if (n && (!sb->tx_idx || !sb->tmpl_idx || !sb->key_idx || !sb->sig_off || !sb->sig_len || !status))
+        return fail(c, CHIP_E_ARG, "null signer array");
+    if (nk && (!sb->key_data || !sb->key_off || !sb->key_len)) return fail(c, CHIP_E_ARG, "null key array");
+    for (uint64_t i = 0; i < n; i++) {
+        if (sb->key_idx[i] >= nk) return fail(c, CHIP_E_ARG, "key_idx out of range");
+        if (sb->sig_off[i] + sb->sig_len[i] > sb->sig_bytes) return fail(c, CHIP_E_ARG, "signature outside sig pool");
+    }
+    for (uint64_t k = 0; k < nk; k++)
+        if (sb->key_off[k] + sb->key_len[k] > sb->key_bytes) return fail(c, CHIP_E_ARG, "key outside key pool");
+    std::lock_guard<std::mutex> g(c->mu);
+    hipStream_t st = c->stream;
+    HIPCHK(c, hipSetDevice(c->device));
+    int r;
+    if ((r = stage(c, c->t_salts, b->salts, ntx * 32, st)) ||
+        (r = stage(c, c->t_start, b->tx_comp_start, ntx ? ntx + 1 : 0, st)) ||
+        (r = stage(c, c->t_group, b->comp_group, nc, st)) || (r = stage(c, c->t_internal, b->comp_internal, nc, st)) ||
+        (r = stage(c, c->t_data, b->data, b->data_bytes, st)) || (r = stage(c, c->t_off, b->comp_off, nc, st)) ||
+        (r = stage(c, c->t_len, b->comp_len, nc, st)) || (r = stage(c, c->f_tdata, tm->data, tm->data_bytes, st)) ||
+        (r = stage(c, c->f_toff, tm->off, nt, st)) || (r = stage(c, c->f_tlen, tm->len, nt, st)) ||
+        (r = stage(c, c->f_tid, tm->id_at, nt, st)) || (r = stage(c, c->f_htx, sb->tx_idx, n, st)) ||
+        (r = stage(c, c->f_htm, sb->tmpl_idx, n, st)) || (r = stage(c, c->h_key_idx, sb->key_idx, n, st)) ||
+        (r = stage(c, c->h_sig_data, sb->sig_data, sb->sig_bytes, st)) || (r = stage(c, c->h_sig_off, sb->sig_off, n, st)) ||
+        (r = stage(c, c->h_sig_len, sb->sig_len, n, st)) || (r = stage(c, c->h_key_data, sb->key_data, sb->key_bytes, st)) ||
+        (r = stage(c, c->h_key_off, sb->key_off, nk, st)) || (r = stage(c, c->h_key_len, sb->key_len, nk, st)))
+        return r;
+    HIPCHK(c, c->t_ids.ensure(ntx * 32 + 16));
+    HIPCHK(c, c->h_status.ensure(n + 16));
+    const uint64_t nw = (n + 63) / 64;
+    HIPCHK(c, c->h_bitmap.ensure(nw * 8 + 16));
+    chip_tx_batch dt = *b;
+    dt.salts = c->t_salts.as<uint8_t>();
+    dt.tx_comp_start = c->t_start.as<uint64_t>();
+    dt.comp_group = c->t_group.as<uint32_t>();
+    dt.comp_internal = c->t_internal.as<uint32_t>();
+    dt.data = c->t_data.as<uint8_t>();
+    dt.comp_off = c->t_off.as<uint64_t>();
+    dt.comp_len = c->t_len.as<uint32_t>();
+    chip_msg_templates dm = *tm;
+    dm.data = c->f_tdata.as<uint8_t>();
+    dm.off = c->f_toff.as<uint64_t>();
+    dm.len = c->f_tlen.as<uint32_t>();
+    dm.id_at = c->f_tid.as<uint32_t>();
+    chip_signer_batch ds = *sb;
+    ds.tx_idx = c->f_htx.as<uint32_t>();
+    ds.tmpl_idx = c->f_htm.as<uint32_t>();
+    ds.key_idx = c->h_key_idx.as<uint32_t>();
+    ds.sig_data = c->h_sig_data.as<uint8_t>();
+    ds.sig_off = c->h_sig_off.as<uint64_t>();
+    ds.sig_len = c->h_sig_len.as<uint32_t>();
+    ds.key_data = c->h_key_data.as<uint8_t>();
+    ds.key_off = c->h_key_off.as<uint64_t>();
+    ds.key_len = c->h_key_len.as<uint32_t>();
+    if ((r = verify_tx_device_locked(c, &dt, &dm, &ds, c->t_ids.as<uint8_t>(), c->h_status.as<uint8_t>(),
+                                     c->h_bitmap.as<uint64_t>(), st)))
+        return r;
+    if (ntx) HIPCHK(c, hipMemcpyAsync(ids, c->t_ids.p, ntx * 32, hipMemcpyDeviceToHost, st));
+    if (status && n) HIPCHK(c, hipMemcpyAsync(status, c->h_status.p, n, hipMemcpyDeviceToHost, st));
+    if (bitmap && nw) HIPCHK(c, hipMemcpyAsync(bitmap, c->h_bitmap.p, nw * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    c->ev_pending = false;
     c->tev_pending = false;
     return CHIP_OK;
 }

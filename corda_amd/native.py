@@ -35,6 +35,7 @@ EXPORTS = ["chip_abi_version", "chip_device_count", "chip_init", "chip_shutdown"
            "chip_uniq_open", "chip_uniq_close", "chip_uniq_size", "chip_uniq_rebuild", "chip_uniq_commit_batch",
            "chip_uniq_commit_batch_device", "chip_uniq_last_error", "chip_uniq_shard_begin", "chip_uniq_shard_vote",
            "chip_uniq_shard_apply", "chip_uniq_shard_classify", "chip_uniq_shard_finish",
+           "chip_verify_tx_batch", "chip_verify_tx_batch_device",
            "chip_get_stats", "chip_reset_stats"]
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -60,6 +61,20 @@ class ChipTxBatch(ctypes.Structure):
                 ("ncomp", ctypes.c_uint64), ("comp_group", ctypes.c_void_p), ("comp_internal", ctypes.c_void_p),
                 ("data", ctypes.c_void_p), ("comp_off", ctypes.c_void_p), ("comp_len", ctypes.c_void_p),
                 ("data_bytes", ctypes.c_uint64)]
+
+
+class ChipMsgTemplates(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("data", ctypes.c_void_p), ("off", ctypes.c_void_p), ("len", ctypes.c_void_p),
+                ("id_at", ctypes.c_void_p), ("data_bytes", ctypes.c_uint64), ("max_len", ctypes.c_uint32),
+                ("pad", ctypes.c_uint32)]
+
+
+class ChipSignerBatch(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("tx_idx", ctypes.c_void_p), ("tmpl_idx", ctypes.c_void_p),
+                ("key_idx", ctypes.c_void_p), ("sig_data", ctypes.c_void_p), ("sig_off", ctypes.c_void_p),
+                ("sig_len", ctypes.c_void_p), ("n_keys", ctypes.c_uint64), ("key_data", ctypes.c_void_p),
+                ("key_off", ctypes.c_void_p), ("key_len", ctypes.c_void_p), ("sig_bytes", ctypes.c_uint64),
+                ("key_bytes", ctypes.c_uint64)]
 
 
 class ChipUniqShardBatch(ctypes.Structure):
@@ -111,6 +126,12 @@ def load(build_if_missing: bool = False):
     lib.chip_txid_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipTxBatch), ctypes.c_void_p]
     lib.chip_txid_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipTxBatch), ctypes.c_void_p,
                                            ctypes.c_void_p]
+    lib.chip_verify_tx_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipTxBatch), ctypes.POINTER(ChipMsgTemplates),
+                                         ctypes.POINTER(ChipSignerBatch), ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p]
+    lib.chip_verify_tx_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipTxBatch),
+                                                ctypes.POINTER(ChipMsgTemplates), ctypes.POINTER(ChipSignerBatch),
+                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     lib.chip_uniq_open.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]
     lib.chip_uniq_close.argtypes = [ctypes.c_void_p]
     lib.chip_uniq_size.argtypes = [ctypes.c_void_p]
@@ -183,6 +204,35 @@ def make_tx_batch(t) -> ChipTxBatch:
     return s
 
 
+def _nbytes(a):
+    if a is None:
+        return 0
+    if hasattr(a, "numel"):
+        return int(a.numel() * a.element_size())
+    return int(a.nbytes)
+
+
+def make_templates(t) -> ChipMsgTemplates:
+    """SignableData message templates: fields data, off, len, id_at (+ max_len int)."""
+    s = ChipMsgTemplates()
+    s.n = len(t.off)
+    s.data, s.off, s.len, s.id_at = _ptr(t.data), _ptr(t.off), _ptr(t.len), _ptr(t.id_at)
+    s.data_bytes = _nbytes(t.data)
+    s.max_len = int(t.max_len)
+    return s
+
+
+def make_signers(b) -> ChipSignerBatch:
+    s = ChipSignerBatch()
+    s.n = len(b.key_idx)
+    s.tx_idx, s.tmpl_idx, s.key_idx = _ptr(b.tx_idx), _ptr(b.tmpl_idx), _ptr(b.key_idx)
+    s.sig_data, s.sig_off, s.sig_len = _ptr(b.sig_data), _ptr(b.sig_off), _ptr(b.sig_len)
+    s.n_keys = len(b.key_off)
+    s.key_data, s.key_off, s.key_len = _ptr(b.key_data), _ptr(b.key_off), _ptr(b.key_len)
+    s.sig_bytes, s.key_bytes = _nbytes(b.sig_data), _nbytes(b.key_data)
+    return s
+
+
 class Context:
     """One libcordahip context = one GPU (one process per GPU)."""
 
@@ -236,6 +286,23 @@ class Context:
     def txid_batch_device(self, dev_tx, ids, stream=None):
         s = make_tx_batch(dev_tx)
         self._check(self.lib.chip_txid_batch_device(self.h, ctypes.byref(s), _ptr(ids), stream or None))
+
+    # ---- fused: ids + required-signer verification against the recomputed ids ----
+    def verify_tx_batch(self, t, templates, signers):
+        """Host arrays -> (ids u8[ntx,32], status u8[n], bitmap u64[ceil(n/64)])."""
+        tb, tm, sb = make_tx_batch(t), make_templates(templates), make_signers(signers)
+        ids = np.zeros(tb.ntx * 32, dtype=np.uint8)
+        status = np.zeros(sb.n, dtype=np.uint8)
+        bitmap = np.zeros((sb.n + 63) // 64, dtype=np.uint64)
+        self._check(self.lib.chip_verify_tx_batch(self.h, ctypes.byref(tb), ctypes.byref(tm), ctypes.byref(sb),
+                                                  _ptr(ids), _ptr(status), _ptr(bitmap)))
+        return ids.reshape(tb.ntx, 32), status, bitmap
+
+    def verify_tx_batch_device(self, dev_tx, dev_templates, dev_signers, ids, status, bitmap, stream=None):
+        tb, tm, sb = make_tx_batch(dev_tx), make_templates(dev_templates), make_signers(dev_signers)
+        self._check(self.lib.chip_verify_tx_batch_device(self.h, ctypes.byref(tb), ctypes.byref(tm),
+                                                         ctypes.byref(sb), _ptr(ids), _ptr(status), _ptr(bitmap),
+                                                         stream or None))
 
     def stats(self) -> ChipStats:
         st = ChipStats()

@@ -149,6 +149,49 @@ int chip_txid_batch(chip_ctx* ctx, const chip_tx_batch* batch, uint8_t* ids);
 int chip_txid_batch_device(chip_ctx* ctx, const chip_tx_batch* batch, uint8_t* ids, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Fused transaction verification: ids, then every required signer against the recomputed id
+ * (SignedTransaction.verifySignaturesExcept's signature part for a batch of transactions:
+ * WireTransaction.id, WireTransaction.kt:63, then TransactionSignature.verify(id) for each sig,
+ * TransactionWithSignatures.kt:62-66).  The signed message of a TransactionSignature is
+ * SignableData(txId, signatureMetadata).serialize() (Crypto.kt:552-555): for one metadata value
+ * its bytes are a fixed template with the 32-byte id spliced in, so the library builds every
+ * message on the device from the ids it just computed:
+ *   message(sig i) = tmpl[t][0:id_at[t]] || id[tx_idx[i]] || tmpl[t][id_at[t]:len[t]],  t = tmpl_idx[i]
+ * A signature whose tx_idx / tmpl_idx is out of range gets CHIP_UNSUPPORTED. */
+typedef struct {
+    uint64_t n;                /* templates (one per SignatureMetadata in use)          */
+    const uint8_t* data;       /* template bytes without the id                          */
+    const uint64_t* off;       /* [n]                                                    */
+    const uint32_t* len;       /* [n] bytes excluding the id                             */
+    const uint32_t* id_at;     /* [n] byte offset of the id in the message (<= len)      */
+    uint64_t data_bytes;
+    uint32_t max_len;          /* max(len): sizes the message pool (host-side value)     */
+    uint32_t pad;
+} chip_msg_templates;
+
+typedef struct {
+    uint64_t n;                /* signatures                                             */
+    const uint32_t* tx_idx;    /* [n] transaction in the chip_tx_batch                   */
+    const uint32_t* tmpl_idx;  /* [n] message template                                   */
+    const uint32_t* key_idx;   /* [n] into the key pool (SPKI bytes, as chip_sig_batch)  */
+    const uint8_t* sig_data;
+    const uint64_t* sig_off;   /* [n] */
+    const uint32_t* sig_len;   /* [n] */
+    uint64_t n_keys;
+    const uint8_t* key_data;
+    const uint64_t* key_off;
+    const uint32_t* key_len;
+    uint64_t sig_bytes, key_bytes;
+} chip_signer_batch;
+
+/* ids: [ntx * 32] out; status: [n] out (CHIP_* per signature); bitmap: [ceil(n/64)] (may be NULL). */
+int chip_verify_tx_batch(chip_ctx* ctx, const chip_tx_batch* txs, const chip_msg_templates* tmpl,
+                         const chip_signer_batch* sigs, uint8_t* ids, uint8_t* status, uint64_t* bitmap);
+int chip_verify_tx_batch_device(chip_ctx* ctx, const chip_tx_batch* txs, const chip_msg_templates* tmpl,
+                                const chip_signer_batch* sigs, uint8_t* ids, uint8_t* status, uint64_t* bitmap,
+                                void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Notary uniqueness (GPU-resident StateRef -> ConsumingTx table).
  * StateRef key = 32-byte txhash || little-endian u32 index (36 bytes).
  * ConsumingTx  = (32-byte consuming tx id, u32 inputIndex, u32 caller) where caller is the

@@ -155,3 +155,19 @@ def test_oracle_uniq_conflict_records():
 def _ub(txs):
     b = G.uniq_batch_from_lists(txs)
     return b.tx_ref_start, b.refs, b.tx_ids, b.callers
+
+
+def test_generator_txids_agree_with_oracle():
+    """tools/cordagen.c's OpenSSL tx ids (used to sign cfg4/cfg5 workloads) == the oracle's."""
+    import oracle_bind as O
+    for seed in (1, 2):
+        tb = G.tx_batch(300, seed=seed)
+        assert np.array_equal(G.txids(tb, threads=4), O.txid_batch(tb, threads=4))
+    rng = np.random.Generator(np.random.PCG64(9))
+    txs = []
+    for _ in range(100):
+        groups = [(int(g), [rng.bytes(int(rng.integers(0, 200))) for _ in range(int(rng.integers(1, 5)))])
+                  for g in sorted(rng.choice(22, size=int(rng.integers(1, 5)), replace=False))]
+        txs.append((rng.bytes(32), groups))
+    tb = G.tx_batch_from_lists(txs)
+    assert np.array_equal(G.txids(tb), O.txid_batch(tb))

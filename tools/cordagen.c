@@ -16,6 +16,7 @@
 #include <pthread.h>
 #include <stdint.h>
 #include <string.h>
+#include <stdlib.h>
 
 int gen_ed25519_pub(const uint8_t seed[32], uint8_t pub[32]) {
     EVP_PKEY* k = EVP_PKEY_new_raw_private_key(EVP_PKEY_ED25519, NULL, seed, 32);
@@ -221,3 +222,75 @@ int gen_pubs_many(int scheme, uint64_t n, const uint8_t* privs, uint8_t* out) {
 
 /* SHA-256 of many messages (for generator-side tx ids etc.) */
 void gen_sha256(const uint8_t* m, size_t n, uint8_t out[32]) { SHA256(m, n, out); }
+
+/* ---- generator-side WireTransaction ids (OpenSSL SHA-256), for signing cfg4 / cfg5 workloads:
+ * nonce = SHA256d(salt || BE32 g || BE32 i), leaf = SHA256d(nonce || bytes), group roots and the top
+ * tree over groups 0..max (absent = 32 x FF) padded with 32 x 00 to a power of two
+ * (WireTransaction.kt:139-189, CryptoUtils.kt:216-233, MerkleTree.kt:27-66). ---- */
+static void sha256d(const uint8_t* a, size_t na, const uint8_t* b, size_t nb, uint8_t out[32]) {
+    SHA256_CTX c;
+    uint8_t h[32];
+    SHA256_Init(&c);
+    SHA256_Update(&c, a, na);
+    if (nb) SHA256_Update(&c, b, nb);
+    SHA256_Final(h, &c);
+    SHA256(h, 32, out);
+}
+static void merkle(uint8_t* lvl, uint32_t n, uint8_t root[32]) {   /* lvl has room for pow2(n) x 32 */
+    uint32_t m = 1;
+    while (m < n) m <<= 1;
+    memset(lvl + 32ull * n, 0, 32ull * (m - n));
+    while (m > 1) {
+        for (uint32_t k = 0; k < m / 2; k++) SHA256(lvl + 64ull * k, 64, lvl + 32ull * k);
+        m /= 2;
+    }
+    memcpy(root, lvl, 32);
+}
+typedef struct {
+    uint64_t lo, hi;
+    const uint8_t* salts; const uint64_t* start; const uint32_t* grp; const uint32_t* internal;
+    const uint8_t* data; const uint64_t* off; const uint32_t* len; uint8_t* ids;
+} idjob;
+static void* idworker(void* p) {
+    idjob* j = (idjob*)p;
+    uint8_t* leaves = (uint8_t*)malloc(32 * 4096);
+    uint8_t groups[64 * 32];
+    for (uint64_t t = j->lo; t < j->hi; t++) {
+        const uint64_t a = j->start[t], e = j->start[t + 1];
+        uint32_t maxg = 0;
+        for (uint64_t k = a; k < e; k++) if (j->grp[k] > maxg) maxg = j->grp[k];
+        if (a == e || maxg >= 64 || e - a > 2048) { memset(j->ids + 32 * t, 0, 32); continue; }
+        for (uint32_t g = 0; g <= maxg; g++) {
+            uint32_t cnt = 0;
+            for (uint64_t k = a; k < e; k++) {
+                if (j->grp[k] != g) continue;
+                uint8_t buf[40], nonce[32];
+                memcpy(buf, j->salts + 32 * t, 32);
+                const uint32_t ii = j->internal[k];
+                buf[32] = g >> 24; buf[33] = g >> 16; buf[34] = g >> 8; buf[35] = g;
+                buf[36] = ii >> 24; buf[37] = ii >> 16; buf[38] = ii >> 8; buf[39] = ii;
+                sha256d(buf, 40, NULL, 0, nonce);
+                sha256d(nonce, 32, j->data + j->off[k], j->len[k], leaves + 32 * cnt);
+                cnt++;
+            }
+            if (!cnt) memset(groups + 32 * g, 0xff, 32);
+            else merkle(leaves, cnt, groups + 32 * g);
+        }
+        merkle(groups, maxg + 1, j->ids + 32 * t);
+    }
+    free(leaves);
+    return NULL;
+}
+void gen_txids(uint64_t ntx, const uint8_t* salts, const uint64_t* start, const uint32_t* grp,
+               const uint32_t* internal, const uint8_t* data, const uint64_t* off, const uint32_t* len,
+               uint8_t* ids, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 128) threads = 128;
+    pthread_t th[128];
+    idjob jobs[128];
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (idjob){ntx * t / threads, ntx * (t + 1) / threads, salts, start, grp, internal, data, off, len, ids};
+        pthread_create(&th[t], NULL, idworker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+}

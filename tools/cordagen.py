@@ -546,3 +546,141 @@ def uniq_workload(ntx: int, n_pre: int, seed: int = 0x5EED0005, pre_hit: float =
     b.callers = callers
     pre = (pre_refs.reshape(-1).copy(), pre_tx.reshape(-1).copy(), pre_pos, pre_caller)
     return pre, b
+
+
+def txids(tb: TxBatch, threads: int = 8) -> np.ndarray:
+    """Generator-side WireTransaction ids (OpenSSL SHA-256 in tools/cordagen.c), [ntx, 32]."""
+    ids = np.zeros(tb.ntx * 32, dtype=np.uint8)
+    lib().gen_txids(ctypes.c_uint64(tb.ntx), _p(tb.salts), _p(tb.tx_comp_start), _p(tb.comp_group),
+                    _p(tb.comp_internal), _p(tb.data), _p(tb.comp_off), _p(tb.comp_len), _p(ids), threads)
+    return ids.reshape(tb.ntx, 32)
+
+
+# Stand-in for SignableData(txId, SignatureMetadata(platformVersion, schemeNumberID)).serialize():
+# Kryo's bytes are unpinned without a JVM (SURVEY.md §8a A4), but for one metadata value they are a
+# fixed byte string with the 32-byte id at a fixed offset — which is all the engine relies on.
+_SIGNABLE_HEAD = (b"corda\x00\x00\x01" + b"\x01\x00net.corda.core.crypto.SignableData\x01\x01"
+                  b"net.corda.core.crypto.SecureHash$SHA256\x01\x02net.corda.core.crypto.SignatureMetadata")
+
+
+class Templates:
+    """chip_msg_templates layout: data pool, off u64[n], len u32[n], id_at u32[n], max_len."""
+    data = off = len = id_at = None
+    max_len = 0
+
+
+def signable_template(scheme_id: int, platform_version: int = 1, total: int = 200):
+    """(template bytes without the id, id offset): a `total`-byte SignableData-shaped message."""
+    head = (_SIGNABLE_HEAD + bytes(200))[:total - 32 - 8]
+    return head + struct.pack(">ii", platform_version, scheme_id), len(head)
+
+
+def templates_from_list(items) -> Templates:
+    """items: [(template_bytes, id_at)]"""
+    t = Templates()
+    t.data, t.off, t.len = pools_from_list([b for b, _ in items])
+    t.id_at = np.array([a for _, a in items], dtype=np.uint32)
+    t.max_len = int(t.len.max()) if len(items) else 0
+    return t
+
+
+def messages_from_templates(ids: np.ndarray, tmpl: bytes, id_at: int) -> np.ndarray:
+    """[ntx, len(tmpl) + 32] messages tmpl[:id_at] || id || tmpl[id_at:] (host side, for signing)."""
+    ntx = len(ids)
+    t = np.frombuffer(tmpl, dtype=np.uint8)
+    out = np.empty((ntx, len(tmpl) + 32), dtype=np.uint8)
+    out[:, :id_at] = t[:id_at]
+    out[:, id_at:id_at + 32] = ids
+    out[:, id_at + 32:] = t[id_at:]
+    return out
+
+
+class SignerBatch:
+    """chip_signer_batch layout (+ expected labels)."""
+    tx_idx = tmpl_idx = key_idx = None
+    sig_data = sig_off = sig_len = None
+    key_data = key_off = key_len = None
+    expected = None
+
+    @property
+    def n(self):
+        return len(self.key_idx)
+
+
+def ed25519_signers(ids: np.ndarray, signer_keys: np.ndarray, n_keys: int, corrupt: float = 0.0,
+                    seed: int = 0x5EED0004, threads: int = 8, extra_key_seeds=()):
+    """One Ed25519 signature per (tx, key) pair over the SignableData template of scheme 4.
+    signer_keys: [ntx, s] key indices into key_seed(0..n_keys-1) followed by extra_key_seeds.
+    `corrupt` of the signatures get one R bit flipped (expected INVALID)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    ntx, s = signer_keys.shape
+    seeds = b"".join(key_seed(i) for i in range(n_keys)) + b"".join(extra_key_seeds)
+    seeds_np = np.frombuffer(seeds, dtype=np.uint8).copy()
+    nk = len(seeds_np) // 32
+    pubs = np.zeros(nk * 32, dtype=np.uint8)
+    if lib().gen_pubs_many(SCHEME_ED25519, ctypes.c_uint64(nk), _p(seeds_np), _p(pubs)) != 0:
+        raise RuntimeError("keygen failed")
+    tmpl, at = signable_template(SCHEME_ED25519)
+    msgs = messages_from_templates(ids, tmpl, at)
+    mlen = msgs.shape[1]
+    n = ntx * s
+    tx_idx = np.repeat(np.arange(ntx, dtype=np.uint32), s)
+    key_of = signer_keys.reshape(-1).astype(np.uint32)
+    # sign grouped by key (the generator caches one EVP key per run of equal keys)
+    order = np.argsort(key_of, kind="stable")
+    sig_sorted = np.zeros(n * 64, dtype=np.uint8)
+    sl = np.zeros(n, dtype=np.uint32)
+    err = lib().gen_sign_many(SCHEME_ED25519, ctypes.c_uint64(n), _p(seeds_np), _p(np.ascontiguousarray(key_of[order])),
+                              _p(msgs.reshape(-1)), _p(np.arange(ntx, dtype=np.uint64) * mlen),
+                              _p(np.full(ntx, mlen, dtype=np.uint32)), _p(np.ascontiguousarray(tx_idx[order])), None,
+                              _p(sig_sorted), _p(sl), ctypes.c_uint32(64), threads)
+    if err:
+        raise RuntimeError("signing failed")
+    sigs = np.zeros((n, 64), dtype=np.uint8)
+    sigs[order] = sig_sorted.reshape(n, 64)
+    expected = np.zeros(n, dtype=np.uint8)
+    bad = np.nonzero(rng.random(n) < corrupt)[0]
+    for i in bad:
+        b = int(rng.integers(0, 256))
+        sigs[i, b // 8] ^= 1 << (b % 8)
+        expected[i] = 1
+    sb = SignerBatch()
+    sb.tx_idx = tx_idx
+    sb.tmpl_idx = np.zeros(n, dtype=np.uint32)
+    sb.key_idx = key_of
+    sb.sig_data = sigs.reshape(-1)
+    sb.sig_off = np.arange(n, dtype=np.uint64) * 64
+    sb.sig_len = np.full(n, 64, dtype=np.uint32)
+    sb.key_data, sb.key_off, sb.key_len = pools_from_list([spki_ed25519(pubs[32 * i:32 * i + 32].tobytes())
+                                                           for i in range(nk)])
+    sb.expected = expected
+    return sb, templates_from_list([(tmpl, at)]), msgs
+
+
+NOTARY_SEED = hashlib.sha256(b"cordahip-notary").digest()
+
+
+def cfg4_workload(ntx: int, n_keys: int = 4096, seed: int = 0x5EED0004, corrupt: float = 0.01, threads: int = 8):
+    """cfg4: ntx WireTransactions of the 8-component profile + 2 Ed25519 required
+    signers per tx (owner from n_keys parties, the notary) signing SignableData(id)."""
+    tb = tx_batch(ntx, seed=seed)
+    ids = txids(tb, threads)
+    rng = np.random.Generator(np.random.PCG64(seed + 1))
+    keys = np.stack([rng.integers(0, n_keys, size=ntx), np.full(ntx, n_keys)], axis=1)
+    sb, tm, msgs = ed25519_signers(ids, keys, n_keys, corrupt=corrupt, seed=seed + 2, threads=threads,
+                                   extra_key_seeds=(NOTARY_SEED,))
+    return tb, tm, sb, ids, msgs
+
+
+def signer_sig_batch(sb: SignerBatch, msgs: np.ndarray) -> SigBatch:
+    """The same signatures as a plain chip_sig_batch over host-built messages (oracle / cross-check)."""
+    b = SigBatch()
+    b.key_idx, b.sig_data, b.sig_off, b.sig_len = sb.key_idx, sb.sig_data, sb.sig_off, sb.sig_len
+    b.key_data, b.key_off, b.key_len = sb.key_data, sb.key_off, sb.key_len
+    ntx, ml = msgs.shape
+    b.msg_idx = sb.tx_idx.astype(np.uint32)
+    b.msg_data = msgs.reshape(-1)
+    b.msg_off = np.arange(ntx, dtype=np.uint64) * ml
+    b.msg_len = np.full(ntx, ml, dtype=np.uint32)
+    b.expected = sb.expected
+    return b
