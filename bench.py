@@ -41,9 +41,13 @@ ED25519_OPS_PER_VERIFY = 2.4e5        # SURVEY §8d canonical count (~3,400 fiel
 # schedule: 64 cached adds (4 mults) + 63 p1p1->p3 (4) + 1 conversion (4) + 32 Niels adds (3) + 31
 # conversions (4) + 3 final = 735 GF(2^255-19) multiplications x 100 limb products (radix 2^25.5)
 ED_COMB_MACS_PER_VERIFY = 73_500
-# SHA-256 compression as the gfx950 compiler issues it (SQ_INSTS_VALU per
-# compression measured with rocprofv3 on k_txid, profiles/r01c/)
-TXID_OPS_PER_COMPRESSION = 1_600
+# SHA-256 compression as the gfx950 compiler issues it: k_txid's SQ_INSTS_VALU x 64 lanes per
+# (tx x compression), measured with rocprofv3 (profiles/r01c/pmc_sq.csv: 2.331e9 wave-instructions
+# for 1M cfg4 transactions of 89 compressions) — includes the loads and tree bookkeeping
+TXID_OPS_PER_COMPRESSION = 1_676
+# HBM traffic per launch comes from the committed PMC passes of the same command (tools/profile.sh):
+# FETCH_SIZE + WRITE_SIZE (KiB) of the launch with the same grid
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r01c")
 # VALU issue peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6e12 lane-ops/s (= FP32 vector 157.3 TFLOPS / 2,
 # MI355X_MICROARCH.md chip table).  v_mad_u64_u32 issues at a quarter of that: 19.66e12 MACs/s
 # (tools/microbench_mul.hip measures 18.0e12 including a dependent xor per MAC).
@@ -102,6 +106,24 @@ def max_over_ranks(x, world, torch, dev, dist):
     e = torch.tensor([x], dtype=torch.float64, device=dev)
     dist.all_reduce(e, op=dist.ReduceOp.MAX)
     return float(e.item())
+
+
+def profile_traffic(kernel, grid):
+    """HBM bytes of one launch of `kernel` with `grid` threads from the committed rocprofv3 PMC
+    passes (FETCH_SIZE + WRITE_SIZE, KiB), or None when the profile has no such launch.  FETCH_SIZE is
+    uncalibrated for gathers on gfx950 (MI355X_MICROARCH.md §HBM), so this is reported as measured."""
+    import csv
+    tot = 0.0
+    for name, ctr in (("pmc_fetch_size.csv", "FETCH_SIZE"), ("pmc_write_size.csv", "WRITE_SIZE")):
+        path = os.path.join(PROFILE_DIR, name)
+        if not os.path.exists(path):
+            return None
+        vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+                if r["Kernel_Name"] == kernel and int(r["Grid_Size"]) == grid and r["Counter_Name"] == ctr]
+        if not vals:
+            return None
+        tot += sum(vals) / len(vals) * 1024.0
+    return tot
 
 
 def sha256_compressions(tb):
@@ -198,6 +220,8 @@ def main():
     per_key = np.bincount(batch.key_idx[arith], minlength=len(batch.key_off))
     n_comb = int(per_key[per_key >= 4].sum())
     achieved = ED_COMB_MACS_PER_VERIFY * n_comb / (comb_ms * 1e-3) / 1e12
+    comb_grid = (((n + 255) // 256 + 7) & ~7) * 256
+    traffic = profile_traffic("k_ed_comb_verify", comb_grid)
     del db, status, bitmap, gathered
 
     secondary = {}
@@ -231,6 +255,8 @@ def main():
             "txid_kernel_ms": tx_ms,
             "txid_roofline_frac": (comp_per_tx * TXID_OPS_PER_COMPRESSION * tb.ntx / (tx_ms * 1e-3) / 1e12)
                                   / INT32_PEAK_TOPS,
+            "txid_traffic": profile_traffic("k_txid", (tb.ntx + 255) // 256 * 256),
+            "txid_algorithmic_bytes": int(tb.data.nbytes + tb.salts.nbytes + 32 * tb.ntx + 20 * len(tb.comp_len)),
         })
         # fused: ids -> SignableData messages -> 2 signers per tx
         dm = upload(tm, ("data", "off", "len", "id_at"), torch, dev)
@@ -334,7 +360,11 @@ def main():
             "correct_vs_labels": correct,
             "roofline": {"bound": "valu", "achieved": achieved, "peak": MAC_PEAK_T,
                          "unit": "T MAC/s (v_mad_u64_u32 32x32->64)", "frac": achieved / MAC_PEAK_T,
-                         "traffic": None, "kernel": "k_ed_comb_verify", "kernel_ms": comb_ms,
+                         "traffic": traffic,
+                         "traffic_note": "FETCH_SIZE+WRITE_SIZE bytes per launch, %s (same grid); vs ~%d B/sig "
+                                         "algorithmic (sig 64 + shared msg 100 + Abyte 32 + indices 16 + R' 120)"
+                                         % (os.path.relpath(PROFILE_DIR, ROOT), 332),
+                         "kernel": "k_ed_comb_verify", "kernel_ms": comb_ms,
                          "units_per_launch": n_comb, "macs_per_unit": ED_COMB_MACS_PER_VERIFY,
                          "pipeline_ms": {"keyprep": kp_ms, "comb_tables": tab_ms, "comb_verify": comb_ms,
                                          "comb_finish": fin_ms, "straus_verify": straus_ms},
