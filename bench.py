@@ -213,6 +213,7 @@ def main():
     comb_ms, fin_ms, tab_ms, straus_ms, kp_ms = (kms(s, native.K_ED_COMB), kms(s, native.K_ED_FINISH),
                                                  kms(s, native.K_ED_TABLES), kms(s, native.K_ED25519),
                                                  kms(s, native.K_KEYPREP))
+    plan_ms = kms(s, native.K_ED_PLAN)
     ms_per_step = elapsed / args.steps * 1e3
     value = world * n * args.steps / elapsed
     # signatures on the comb path: arithmetic-needing signatures of keys with >= 4 of them (default policy)
@@ -366,8 +367,8 @@ def main():
                                          % (os.path.relpath(PROFILE_DIR, ROOT), 332),
                          "kernel": "k_ed_comb_verify", "kernel_ms": comb_ms,
                          "units_per_launch": n_comb, "macs_per_unit": ED_COMB_MACS_PER_VERIFY,
-                         "pipeline_ms": {"keyprep": kp_ms, "comb_tables": tab_ms, "comb_verify": comb_ms,
-                                         "comb_finish": fin_ms, "straus_verify": straus_ms},
+                         "pipeline_ms": {"keyprep": kp_ms, "comb_plan": plan_ms, "comb_tables_aux_stream": tab_ms,
+                                         "comb_verify": comb_ms, "comb_finish": fin_ms, "straus_verify": straus_ms},
                          "canonical_tops": ED25519_OPS_PER_VERIFY * n_arith / (ms_per_step * 1e-3) / 1e12 / world},
             "cpu_baseline": cpu,
             "secondary": secondary,

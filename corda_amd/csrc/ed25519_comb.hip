@@ -63,18 +63,23 @@ CHIP_DEV void ed_load_niels(ge_niels& q, const uint32_t* __restrict__ src) {
 // ---- work list: key slots, counting sort by key ----
 // A key gets a comb slot when it is a valid Ed25519 key with at least min_sigs signatures in the
 // batch and the table budget allows; its signatures then occupy comb_list[base, base + count).
+// Eager mode (many signatures per key): every valid Ed25519 key's table was built at slot = key
+// index on the second stream while classify ran, so only the work list is assigned here.
+CHIP_DEV bool ed_key_ok(const KeyMeta* meta, uint32_t k) {
+    const KeyMeta m = meta[k];
+    return m.scheme == CHIP_SCHEME_ED25519 && m.ok;
+}
 __global__ void __launch_bounds__(256) k_ed_comb_slots(uint64_t n_keys, const KeyMeta* __restrict__ meta,
                                                        const uint32_t* __restrict__ key_count, uint32_t min_sigs,
-                                                       uint32_t max_slots, int32_t* __restrict__ key_slot,
+                                                       uint32_t max_slots, uint32_t eager, int32_t* __restrict__ key_slot,
                                                        uint32_t* __restrict__ key_base, uint32_t* __restrict__ slot_key,
                                                        uint32_t* __restrict__ ctr) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_keys) return;
     int32_t slot = -1;
     const uint32_t c = key_count[k];
-    const KeyMeta m = meta[k];
-    if (m.scheme == CHIP_SCHEME_ED25519 && m.ok && c > 0 && c >= min_sigs) {
-        const uint32_t s = atomicAdd(&ctr[0], 1u);
+    if (ed_key_ok(meta, (uint32_t)k) && c > 0 && c >= min_sigs) {
+        const uint32_t s = eager ? (uint32_t)k : atomicAdd(&ctr[0], 1u);
         if (s < max_slots) {
             slot = (int32_t)s;
             slot_key[s] = (uint32_t)k;
@@ -124,12 +129,14 @@ __global__ void __launch_bounds__(256) k_ed_comb_partition(const uint32_t* __res
 // chain: P_w = 2^(W w) (-A) for every window, stashed (extended form) in row 1 of window w.
 // One lane per key: 4 (W) doublings per window, the only serial part of the comb path.
 __global__ void __launch_bounds__(64) k_ed_comb_chain(const uint32_t* __restrict__ ctr, uint32_t max_slots,
+                                                      uint32_t eager, const KeyMeta* __restrict__ meta,
                                                       const uint32_t* __restrict__ slot_key,
                                                       const uint32_t* __restrict__ nega, uint32_t* __restrict__ ctab) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t nslots = min(ctr[0], max_slots);
+    const uint32_t nslots = eager ? max_slots : min(ctr[0], max_slots);
     if (s >= nslots) return;
-    const uint32_t k = slot_key[s];
+    if (eager && !ed_key_ok(meta, s)) return;
+    const uint32_t k = eager ? s : slot_key[s];
     ge_p3 P;
     ed_load_p3(P, nega + (uint64_t)k * 40);
     uint32_t* tab = ctab + (uint64_t)s * ED_COMB_KEY_WORDS;
@@ -151,10 +158,12 @@ __global__ void __launch_bounds__(64) k_ed_comb_chain(const uint32_t* __restrict
 
 // fill: rows j = 0..2^(W-1) of window w: j * P_w in cached form (row 0 = identity)
 __global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict__ ctr, uint32_t max_slots,
+                                                      uint32_t eager, const KeyMeta* __restrict__ meta,
                                                       uint32_t* __restrict__ ctab) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t s = g / ED_COMB_AWIN, w = g % ED_COMB_AWIN;
-    if (s >= min(ctr[0], max_slots)) return;
+    if (s >= (eager ? max_slots : min(ctr[0], max_slots))) return;
+    if (eager && !ed_key_ok(meta, s)) return;
     uint32_t* e = ctab + (uint64_t)s * ED_COMB_KEY_WORDS + (uint64_t)w * ED_COMB_AENT * 40;
     ge_p3 P;
     ed_load_p3(P, e + 40);
@@ -335,18 +344,25 @@ __global__ void __launch_bounds__(256) k_ed_comb_finish(const uint32_t* __restri
 // ---------------------------------------------------------------------------------------
 static inline uint32_t nblk(uint64_t n, uint32_t bs) { return (uint32_t)((n + bs - 1) / bs); }
 
-void launch_ed_comb_tables(hipStream_t st, uint64_t n, uint64_t n_keys, const uint32_t* ed_list,
-                           const uint32_t* ed_count, const chip_sig_batch* b, const KeyMeta* meta, const EdCombWs& w) {
+void launch_ed_comb_plan(hipStream_t st, uint64_t n, uint64_t n_keys, const uint32_t* ed_list,
+                         const uint32_t* ed_count, const chip_sig_batch* b, const KeyMeta* meta, const EdCombWs& w,
+                         bool partition) {
     if (!n || !n_keys) return;
-    hipLaunchKernelGGL(k_ed_comb_slots, dim3(nblk(n_keys, 256)), dim3(256), 0, st, n_keys, meta, w.key_count,
-                       w.min_sigs, w.max_slots, w.key_slot, w.key_base, w.slot_key, w.ctr);
+    if (!partition) {
+        hipLaunchKernelGGL(k_ed_comb_slots, dim3(nblk(n_keys, 256)), dim3(256), 0, st, n_keys, meta, w.key_count,
+                           w.min_sigs, w.max_slots, w.eager, w.key_slot, w.key_base, w.slot_key, w.ctr);
+        return;
+    }
     hipLaunchKernelGGL(k_ed_comb_partition, dim3(nblk(n, 256)), dim3(256), 0, st, ed_list, ed_count, b->key_idx,
                        w.key_slot, w.key_base, w.key_cur, w.comb_list, w.straus_list, w.ctr);
-    if (!w.max_slots) return;
-    hipLaunchKernelGGL(k_ed_comb_chain, dim3(nblk(w.max_slots, 64)), dim3(64), 0, st, w.ctr, w.max_slots, w.slot_key,
-                       w.nega, w.ctab);
+}
+
+void launch_ed_comb_build(hipStream_t st, uint64_t n, uint64_t n_keys, const KeyMeta* meta, const EdCombWs& w) {
+    if (!n || !n_keys || !w.max_slots) return;
+    hipLaunchKernelGGL(k_ed_comb_chain, dim3(nblk(w.max_slots, 64)), dim3(64), 0, st, w.ctr, w.max_slots, w.eager, meta,
+                       w.slot_key, w.nega, w.ctab);
     hipLaunchKernelGGL(k_ed_comb_fill, dim3(nblk((uint64_t)w.max_slots * ED_COMB_AWIN, 256)), dim3(256), 0, st, w.ctr,
-                       w.max_slots, w.ctab);
+                       w.max_slots, w.eager, meta, w.ctab);
 }
 
 void launch_ed_comb_verify(hipStream_t st, uint64_t n, const chip_sig_batch* b, const uint32_t* abytes,

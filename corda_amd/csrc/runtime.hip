@@ -42,6 +42,8 @@ struct chip_ctx {
     uint32_t comb_min_sigs = 4;                   // Ed25519 comb threshold (signatures per key)
     uint64_t comb_budget = 8ull << 30;            // bytes of per-key comb tables
     hipStream_t stream = nullptr;
+    hipStream_t aux = nullptr;                    // second stream: per-key comb tables
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
     std::mutex mu;
     std::string err;
     // verify workspaces
@@ -247,7 +249,10 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
     c->device = dev;
     if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
-        hipEventCreate(&c->tev0) != hipSuccess || hipEventCreate(&c->tev1) != hipSuccess) {
+        hipEventCreate(&c->tev0) != hipSuccess || hipEventCreate(&c->tev1) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return CHIP_E_DEVICE;
     }
@@ -283,6 +288,10 @@ void chip_shutdown(chip_ctx* c) {
     hipEventDestroy(c->ev1);
     hipEventDestroy(c->tev0);
     hipEventDestroy(c->tev1);
+    hipStreamSynchronize(c->aux);
+    hipEventDestroy(c->ev_fork);
+    hipEventDestroy(c->ev_join);
+    hipStreamDestroy(c->aux);
     hipStreamDestroy(c->stream);
     delete c;
 }
@@ -304,9 +313,14 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     EdCombWs w{};
     if (comb) {
         const uint64_t key_bytes = (uint64_t)ED_COMB_KEY_WORDS * 4;
+        // eager: many signatures per key and every key's table fits the budget -> build all tables
+        // (slot = key index) on the aux stream while classify runs; else tables for hot keys only
+        w.eager = (n >= 16 * nk && nk * key_bytes <= c->comb_budget && !(c->flags & CHIP_FLAG_FORCE_COMB)) ? 1u : 0u;
         uint64_t slots = nk;
-        slots = std::min<uint64_t>(slots, n / std::max<uint32_t>(1u, c->comb_min_sigs));
-        slots = std::min<uint64_t>(slots, c->comb_budget / key_bytes);
+        if (!w.eager) {
+            slots = std::min<uint64_t>(slots, n / std::max<uint32_t>(1u, c->comb_min_sigs));
+            slots = std::min<uint64_t>(slots, c->comb_budget / key_bytes);
+        }
         HIPCHK(c, c->c_key_count.ensure(nk * 4 + 16));
         HIPCHK(c, c->c_key_slot.ensure(nk * 4 + 16));
         HIPCHK(c, c->c_key_base.ensure(nk * 4 + 16));
@@ -346,6 +360,16 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     int ke = c->kbegin(CHIP_K_KEYPREP, st);
     launch_ed25519_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->abytes.as<uint32_t>(),
                             c->edtab.as<uint32_t>(), comb ? w.nega : nullptr);
+    if (comb && w.eager && n) {
+        // fork: per-key comb tables on the aux stream, concurrent with ECDSA key prep, classify and
+        // the work-list partition on the main stream (the chain is a serial 252-doubling latency)
+        HIPCHK(c, hipEventRecord(c->ev_fork, st));
+        HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+        const int kt = c->kbegin(CHIP_K_ED_TABLES, c->aux);
+        launch_ed_comb_build(c->aux, n, nk, meta, w);
+        c->kend(kt, c->aux);
+        HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
+    }
     launch_ecdsa_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->ectab.as<uint32_t>());
     c->kend(ke, st);
     if (n) {
@@ -357,9 +381,17 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         const uint32_t* ed_list = lists + (uint64_t)LIST_ED25519 * n;
         const uint32_t* ed_count = counts + LIST_ED25519;
         if (comb) {
-            ke = c->kbegin(CHIP_K_ED_TABLES, st);
-            launch_ed_comb_tables(st, n, nk, ed_list, ed_count, b, meta, w);
+            ke = c->kbegin(CHIP_K_ED_PLAN, st);
+            launch_ed_comb_plan(st, n, nk, ed_list, ed_count, b, meta, w, false);
+            launch_ed_comb_plan(st, n, nk, ed_list, ed_count, b, meta, w, true);
             c->kend(ke, st);
+            if (w.eager) {
+                HIPCHK(c, hipStreamWaitEvent(st, c->ev_join, 0));
+            } else {
+                ke = c->kbegin(CHIP_K_ED_TABLES, st);
+                launch_ed_comb_build(st, n, nk, meta, w);
+                c->kend(ke, st);
+            }
             ke = c->kbegin(CHIP_K_ED_COMB, st);
             launch_ed_comb_verify(st, n, b, c->abytes.as<uint32_t>(), w);
             c->kend(ke, st);

@@ -47,10 +47,15 @@ struct EdCombWs {
     uint32_t* zpre;         // [10][n] prefix products of the batched inversion
     uint32_t* nega;         // [n_keys][40] -A in extended coordinates (key prep)
     uint32_t max_slots, min_sigs;
+    uint32_t eager;         // tables for every Ed25519 key at slot = key index, built during classify
 };
 
-void launch_ed_comb_tables(hipStream_t st, uint64_t n, uint64_t n_keys, const uint32_t* ed_list,
-                           const uint32_t* ed_count, const chip_sig_batch* b, const KeyMeta* meta, const EdCombWs& w);
+// slots (partition = false) or the key-grouped work list (partition = true)
+void launch_ed_comb_plan(hipStream_t st, uint64_t n, uint64_t n_keys, const uint32_t* ed_list,
+                         const uint32_t* ed_count, const chip_sig_batch* b, const KeyMeta* meta, const EdCombWs& w,
+                         bool partition);
+// per-key comb tables (chain + fill); in eager mode independent of the signatures (second stream)
+void launch_ed_comb_build(hipStream_t st, uint64_t n, uint64_t n_keys, const KeyMeta* meta, const EdCombWs& w);
 void launch_ed_comb_verify(hipStream_t st, uint64_t n, const chip_sig_batch* b, const uint32_t* abytes,
                            const EdCombWs& w);
 void launch_ed_comb_finish(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w, uint8_t* status);

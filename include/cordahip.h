@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define CHIP_ABI_VERSION 2
+#define CHIP_ABI_VERSION 3
 
 enum chip_sig_status {
     CHIP_VALID = 0,
@@ -268,9 +268,12 @@ int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_st
 
 /* ---------------------------------------------------------------------------------------
  * Counters (observability; OutOfProcessTransactionVerifierService.kt:35-46 analogue). */
+/* CHIP_K_ED_COMB = k_ed_comb_verify, CHIP_K_ED_TABLES = per-key comb table build (on the context's
+ * second stream when every key gets a table), CHIP_K_ED_PLAN = slot assignment + key-grouped work
+ * list; kind 9 is unused */
 enum chip_kernel { CHIP_K_ED25519 = 0, CHIP_K_ECDSA_R1 = 1, CHIP_K_ECDSA_K1 = 2, CHIP_K_TXID = 3,
                    CHIP_K_KEYPREP = 4, CHIP_K_UNIQ = 5, CHIP_K_ED_COMB = 6, CHIP_K_ED_FINISH = 7,
-                   CHIP_K_ED_TABLES = 8, CHIP_N_KERNELS = 9 };
+                   CHIP_K_ED_TABLES = 8, CHIP_K_ED_PLAN = 10, CHIP_N_KERNELS = 11 };
 typedef struct {
     uint64_t batches, sigs, keys_prepared;
     uint64_t status_count[8];
