@@ -1,0 +1,453 @@
+"""Host-side mirror of the reference's hot-path API over the libcordahip engine (Python).
+
+Same names, argument meaning and exceptions as the Kotlin it mirrors, so call sites and tests read
+like the reference's:
+
+  Crypto.findSignatureScheme / doVerify / isValid      core/.../crypto/Crypto.kt:235-267,502-625
+  TransactionSignature.verify                          core/.../crypto/TransactionSignature.kt:26-40
+  SignedTransaction / TransactionWithSignatures        core/.../transactions/TransactionWithSignatures.kt:29-85,
+    .checkSignaturesAreValid / getMissingSigners /       SignedTransaction.kt:37-76,136-173,228-229
+     verifySignaturesExcept / verifyRequiredSignatures
+  WireTransaction.id / requiredSigningKeys / invariants core/.../transactions/WireTransaction.kt:53-75,139-189
+  PersistentUniquenessProvider.commit                  node/.../transactions/PersistentUniquenessProvider.kt:92-113
+  TrustedAuthorityNotaryService.commitInputStates      core/.../node/services/NotaryService.kt:61-75
+
+Every cryptographic operation is one batched engine call.  `engine` is a corda_amd.Context (the HIP
+path); any object with the same verify_batch / txid_batch / uniq_open methods can stand in (the CPU
+tests plug the oracle in to exercise the host logic without a GPU).  There is no CPU fallback here.
+"""
+from __future__ import annotations
+
+import struct
+from dataclasses import dataclass, field
+from typing import Callable, Dict, Iterable, List, Optional, Sequence, Set, Tuple
+
+import numpy as np
+
+from .native import (VALID, INVALID, SIG_DECODE, EMPTY_SIG, EMPTY_CLEAR, UNSUPPORTED, KEY_INVALID)
+
+
+# ---- exceptions (java.security / IllegalArgumentException / Corda exceptions) ----
+class SignatureException(Exception):
+    pass
+
+
+class InvalidKeyException(Exception):
+    pass
+
+
+class IllegalArgumentException(ValueError):
+    pass
+
+
+class UnsupportedSchemeError(IllegalArgumentException):
+    """CHIP_UNSUPPORTED: RSA / SPHINCS / composite keys stay on the JCA path (not accelerated)."""
+
+
+class SignaturesMissingException(SignatureException):
+    """SignedTransaction.SignaturesMissingException (SignedTransaction.kt:228-229)."""
+
+    def __init__(self, missing: Set[bytes], descriptions: List[str], id: bytes):
+        super().__init__("Missing signatures for %s on transaction %s for %s" %
+                         (len(missing), id.hex().upper(), ", ".join(descriptions)))
+        self.missing = missing
+        self.descriptions = descriptions
+        self.id = id
+
+
+class UniquenessException(Exception):
+    def __init__(self, conflict: "Conflict"):
+        super().__init__("UniquenessException")
+        self.error = conflict
+
+
+class NotaryException(Exception):
+    def __init__(self, tx_id: bytes, conflict: "Conflict"):
+        super().__init__("Notary conflict for %s" % tx_id.hex())
+        self.tx_id = tx_id
+        self.conflict = conflict
+
+
+# ---- signature schemes (Crypto.kt:84-128) and key -> scheme (Crypto.findSignatureScheme) ----
+@dataclass(frozen=True)
+class SignatureScheme:
+    scheme_number_id: int
+    scheme_code_name: str
+
+
+ECDSA_SECP256K1_SHA256 = SignatureScheme(2, "ECDSA_SECP256K1_SHA256")
+ECDSA_SECP256R1_SHA256 = SignatureScheme(3, "ECDSA_SECP256R1_SHA256")
+EDDSA_ED25519_SHA512 = SignatureScheme(4, "EDDSA_ED25519_SHA512")
+
+_SPKI_ED25519 = bytes.fromhex("302a300506032b6570032100")
+_OID_R1 = bytes.fromhex("06082a8648ce3d030107")
+_OID_K1 = bytes.fromhex("06052b8104000a")
+
+
+def find_signature_scheme(key: bytes) -> SignatureScheme:
+    """The scheme of an X.509 SubjectPublicKeyInfo (PublicKey.encoded), from its algorithm OID."""
+    if len(key) == 44 and key[:12] == _SPKI_ED25519:
+        return EDDSA_ED25519_SHA512
+    if len(key) in (91, 59) and key[13:23] == _OID_R1:
+        return ECDSA_SECP256R1_SHA256
+    if len(key) in (88, 56) and key[13:20] == _OID_K1:
+        return ECDSA_SECP256K1_SHA256
+    raise IllegalArgumentException("Unsupported key/algorithm for schemeCodeName")
+
+
+def _raise_for(status: int, key: bytes):
+    """The exception Crypto.doVerify throws for a non-VALID status byte."""
+    if status == INVALID:
+        raise SignatureException("Signature Verification failed!")
+    if status == SIG_DECODE:
+        try:
+            ed = find_signature_scheme(key) == EDDSA_ED25519_SHA512
+        except IllegalArgumentException:
+            ed = False
+        raise SignatureException("signature length is wrong" if ed else "error decoding signature bytes.")
+    if status == EMPTY_SIG:
+        raise IllegalArgumentException("Signature data is empty!")
+    if status == EMPTY_CLEAR:
+        raise IllegalArgumentException("Clear data is empty, nothing to verify!")
+    if status == KEY_INVALID:
+        raise InvalidKeyException("invalid key: not a valid curve point")
+    if status == UNSUPPORTED:
+        raise UnsupportedSchemeError("Unsupported key/algorithm (JCA path)")
+    raise SignatureException("unknown status %d" % status)
+
+
+# ---- batch packing (chip_sig_batch SoA layout; keys and messages de-duplicated) ----
+class SigBatch:
+    def __init__(self, items: Sequence[Tuple[bytes, bytes, bytes]]):
+        kid: Dict[bytes, int] = {}
+        mid: Dict[bytes, int] = {}
+        keys: List[bytes] = []
+        msgs: List[bytes] = []
+        key_idx, msg_idx, sigs = [], [], []
+        for k, s, m in items:
+            if k not in kid:
+                kid[k] = len(keys)
+                keys.append(k)
+            if m not in mid:
+                mid[m] = len(msgs)
+                msgs.append(m)
+            key_idx.append(kid[k])
+            msg_idx.append(mid[m])
+            sigs.append(s)
+        self.key_idx = np.array(key_idx, dtype=np.uint32)
+        self.msg_idx = np.array(msg_idx, dtype=np.uint32)
+        self.sig_data, self.sig_off, self.sig_len = _pool(sigs)
+        self.key_data, self.key_off, self.key_len = _pool(keys)
+        self.msg_data, self.msg_off, self.msg_len = _pool(msgs)
+
+    @property
+    def n(self):
+        return len(self.key_idx)
+
+
+def _pool(items: List[bytes]):
+    lens = np.fromiter((len(x) for x in items), dtype=np.uint32, count=len(items))
+    off = np.zeros(len(items), dtype=np.uint64)
+    if len(items) > 1:
+        off[1:] = np.cumsum(lens[:-1].astype(np.uint64))
+    data = np.frombuffer(b"".join(items), dtype=np.uint8).copy() if items else np.zeros(0, np.uint8)
+    if len(data) == 0:
+        data = np.zeros(1, dtype=np.uint8)
+    return data, off, lens
+
+
+def verify_statuses(engine, items: Sequence[Tuple[bytes, bytes, bytes]]) -> np.ndarray:
+    """CHIP_* status of every (key, signature, clear data) triple, one engine call."""
+    if not items:
+        return np.zeros(0, dtype=np.uint8)
+    status, _ = engine.verify_batch(SigBatch(items))
+    return status
+
+
+class Crypto:
+    """net.corda.core.crypto.Crypto (verification half)."""
+
+    @staticmethod
+    def find_signature_scheme(key: bytes) -> SignatureScheme:
+        return find_signature_scheme(key)
+
+    @staticmethod
+    def do_verify(engine, public_key: bytes, signature_data: bytes, clear_data: bytes) -> bool:
+        """True, or the exception Crypto.doVerify(PublicKey, ByteArray, ByteArray) throws (Crypto.kt:502-536)."""
+        st = int(verify_statuses(engine, [(public_key, signature_data, clear_data)])[0])
+        if st != VALID:
+            _raise_for(st, public_key)
+        return True
+
+    @staticmethod
+    def is_valid(engine, public_key: bytes, signature_data: bytes, clear_data: bytes) -> bool:
+        """False on a bad signature; engine decode errors still throw (Crypto.kt:600-625)."""
+        st = int(verify_statuses(engine, [(public_key, signature_data, clear_data)])[0])
+        if st == VALID:
+            return True
+        if st == INVALID:
+            return False
+        _raise_for(st, public_key)
+
+
+# ---- SignableData(txId, SignatureMetadata).serialize() ----
+@dataclass(frozen=True)
+class SignatureMetadata:
+    platform_version: int = 1
+    scheme_number_id: int = 4
+
+
+_SIGNABLE_HEAD = (b"corda\x00\x00\x01" + b"\x01\x00net.corda.core.crypto.SignableData\x01\x01"
+                  b"net.corda.core.crypto.SecureHash$SHA256\x01\x02net.corda.core.crypto.SignatureMetadata")
+
+
+def signable_template(meta: SignatureMetadata, total: int = 200) -> Tuple[bytes, int]:
+    """(template bytes without the id, id offset) of the SignableData bytes for `meta`: Kryo's exact
+    bytes are unpinned without a JVM; for one metadata value they are a fixed byte
+    string with the 32-byte id at a fixed offset, which is what chip_verify_tx_batch relies on."""
+    head = (_SIGNABLE_HEAD + bytes(200))[:total - 32 - 8]
+    return head + struct.pack(">ii", meta.platform_version, meta.scheme_number_id), len(head)
+
+
+def signable_data_bytes(tx_id: bytes, meta: SignatureMetadata) -> bytes:
+    t, at = signable_template(meta)
+    return t[:at] + tx_id + t[at:]
+
+
+Serializer = Callable[[bytes, SignatureMetadata], bytes]
+
+
+@dataclass
+class TransactionSignature:
+    bytes: bytes
+    by: bytes                                  # PublicKey.encoded (SPKI)
+    signature_metadata: SignatureMetadata = field(default_factory=SignatureMetadata)
+
+    def verify(self, engine, tx_id: bytes, serializer: Serializer = signable_data_bytes) -> bool:
+        """TransactionSignature.verify(txId) = Crypto.doVerify(txId, this) (TransactionSignature.kt:26-30)."""
+        return Crypto.do_verify(engine, self.by, self.bytes, serializer(tx_id, self.signature_metadata))
+
+
+class SignedTransaction:
+    """The signature half of SignedTransaction / TransactionWithSignatures."""
+
+    def __init__(self, id: bytes, sigs: List[TransactionSignature], required_signing_keys: Iterable[bytes],
+                 serializer: Serializer = signable_data_bytes, key_descriptions: Optional[Dict[bytes, str]] = None):
+        if not sigs:   # SignedTransaction.kt:46
+            raise IllegalArgumentException("Tried to instantiate a SignedTransaction without any signatures ")
+        self.id = id
+        self.sigs = sigs
+        self.required_signing_keys = set(required_signing_keys)
+        self.serializer = serializer
+        self.key_descriptions = key_descriptions or {}
+
+    def _items(self):
+        return [(s.by, s.bytes, self.serializer(self.id, s.signature_metadata)) for s in self.sigs]
+
+    def check_signatures_are_valid(self, engine):
+        """TransactionWithSignatures.kt:62-66: the first failing signature in list order throws."""
+        for st, s in zip(verify_statuses(engine, self._items()), self.sigs):
+            if st != VALID:
+                _raise_for(int(st), s.by)
+
+    def get_missing_signers(self) -> Set[bytes]:
+        """TransactionWithSignatures.kt:79-85 (plain keys: isFulfilledBy is set membership)."""
+        sig_keys = {s.by for s in self.sigs}
+        return {k for k in self.required_signing_keys if k not in sig_keys}
+
+    def verify_signatures_except(self, engine, *allowed_to_be_missing: bytes):
+        """TransactionWithSignatures.kt:44-50."""
+        self.check_signatures_are_valid(engine)
+        self._check_missing(allowed_to_be_missing)
+
+    def verify_required_signatures(self, engine):
+        self.verify_signatures_except(engine)
+
+    def _check_missing(self, allowed):
+        needed = self.get_missing_signers() - set(allowed)
+        if needed:
+            desc = sorted(self.key_descriptions.get(k, k.hex()[-16:]) for k in needed)
+            raise SignaturesMissingException(needed, desc, self.id)
+
+
+def verify_signatures_except_batch(engine, txs: Sequence[SignedTransaction],
+                                   allowed_to_be_missing: Iterable[bytes] = ()) -> List[Optional[Exception]]:
+    """Batch site (ResolveTransactionsFlow.kt:91-98 style): every transaction's signatures in ONE
+    engine call.  result[i] is None when transaction i passes verifySignaturesExcept, else the exception
+    its own sequential call would have raised first."""
+    items, owner = [], []
+    for t, tx in enumerate(txs):
+        for k, it in enumerate(tx._items()):
+            items.append(it)
+            owner.append((t, k))
+    st = verify_statuses(engine, items)
+    res: List[Optional[Exception]] = [None] * len(txs)
+    allowed = tuple(allowed_to_be_missing)
+    pos = 0
+    for t, tx in enumerate(txs):
+        n = len(tx.sigs)
+        for k in range(n):
+            if st[pos + k] != VALID:
+                try:
+                    _raise_for(int(st[pos + k]), tx.sigs[k].by)
+                except Exception as e:   # noqa: BLE001 - the reference exception is the result
+                    res[t] = e
+                break
+        pos += n
+        if res[t] is None:
+            try:
+                tx._check_missing(allowed)
+            except SignaturesMissingException as e:
+                res[t] = e
+    return res
+
+
+# ---- WireTransaction ----
+INPUTS_GROUP, OUTPUTS_GROUP, COMMANDS_GROUP, ATTACHMENTS_GROUP, NOTARY_GROUP, TIMEWINDOW_GROUP = range(6)
+
+
+class TxBatch:
+    """chip_tx_batch SoA layout."""
+
+    def __init__(self, txs: Sequence["WireTransaction"]):
+        salts, start, grp, internal, items = [], [0], [], [], []
+        for tx in txs:
+            tx.check_invariants()
+            salts.append(tx.privacy_salt)
+            for g, comps in sorted(tx.component_groups, key=lambda x: x[0]):
+                for i, c in enumerate(comps):
+                    grp.append(g)
+                    internal.append(i)
+                    items.append(c)
+            start.append(len(grp))
+        self.ntx = len(txs)
+        self.salts = np.frombuffer(b"".join(salts), dtype=np.uint8).copy() if salts else np.zeros(0, np.uint8)
+        self.tx_comp_start = np.array(start, dtype=np.uint64)
+        self.comp_group = np.array(grp, dtype=np.uint32)
+        self.comp_internal = np.array(internal, dtype=np.uint32)
+        self.data, self.comp_off, self.comp_len = _pool(items)
+
+
+class WireTransaction:
+    """Component groups [(groupIndex, [serialized component bytes])] + PrivacySalt.  The required
+    signers are carried as keys (the serialized commands are opaque to this layer)."""
+
+    def __init__(self, component_groups: List[Tuple[int, List[bytes]]], privacy_salt: bytes,
+                 command_signers: Iterable[bytes] = (), notary_key: Optional[bytes] = None):
+        self.component_groups = component_groups
+        self.privacy_salt = privacy_salt
+        self.command_signers = list(command_signers)
+        self.notary_key = notary_key
+
+    def _group(self, g):
+        for gi, comps in self.component_groups:
+            if gi == g:
+                return comps
+        return []
+
+    def check_invariants(self):
+        """WireTransaction.kt:53-60 (the invariants the id depends on)."""
+        idx = [g for g, _ in self.component_groups]
+        if any(not comps for _, comps in self.component_groups):
+            raise IllegalArgumentException("Empty component groups are not allowed")
+        if len(set(idx)) != len(idx):
+            raise IllegalArgumentException("Duplicated component groups detected")
+        if any(g < 0 or g >= 64 for g in idx):
+            raise IllegalArgumentException("component group ordinal outside [0, 64)")
+        if not self._group(INPUTS_GROUP) and not self._group(OUTPUTS_GROUP):
+            raise IllegalArgumentException("A transaction must contain at least one input or output state")
+        if not self._group(COMMANDS_GROUP):
+            raise IllegalArgumentException("A transaction must contain at least one command")
+        if self._group(TIMEWINDOW_GROUP) and not self._group(NOTARY_GROUP):
+            raise IllegalArgumentException("Transactions with time-windows must be notarised")
+        if len(self.privacy_salt) != 32 or self.privacy_salt == bytes(32):
+            raise IllegalArgumentException("Privacy salt should be 32 bytes and not all zeros")
+
+    @property
+    def required_signing_keys(self) -> Set[bytes]:
+        """WireTransaction.kt:66-75."""
+        keys = set(self.command_signers)
+        if self.notary_key is not None and (self._group(INPUTS_GROUP) or self._group(TIMEWINDOW_GROUP)):
+            keys.add(self.notary_key)
+        return keys
+
+    def id(self, engine) -> bytes:
+        return WireTransaction.ids(engine, [self])[0]
+
+    @staticmethod
+    def ids(engine, txs: Sequence["WireTransaction"]) -> List[bytes]:
+        """Batch WireTransaction.id (one chip_txid_batch call)."""
+        if not txs:
+            return []
+        out = engine.txid_batch(TxBatch(txs))
+        return [bytes(r) for r in np.asarray(out).reshape(len(txs), 32)]
+
+
+# ---- notary uniqueness ----
+@dataclass(frozen=True)
+class StateRef:
+    txhash: bytes
+    index: int
+
+    def key(self) -> bytes:
+        return self.txhash + struct.pack("<I", self.index)
+
+
+@dataclass(frozen=True)
+class ConsumingTx:
+    id: bytes
+    input_index: int
+    requesting_party: int
+
+
+@dataclass
+class Conflict:
+    state_history: List[Tuple[StateRef, ConsumingTx]]
+
+
+class PersistentUniquenessProvider:
+    """UniquenessProvider backed by the GPU commit log (chip_uniq_*)."""
+
+    def __init__(self, engine, capacity: int = 1 << 20):
+        self.table = engine.uniq_open(capacity)
+
+    def size(self) -> int:
+        return self.table.size()
+
+    def commit_batch(self, requests: Sequence[Tuple[List[StateRef], bytes, int]]):
+        """[(states, txId, callerIdentity)] applied in order -> [(status, Conflict)]; status 0 committed,
+        1 re-notarisation of the same tx (commitInputStates accepts it), 2 conflict."""
+        start = [0]
+        refs, ids, callers = [], [], []
+        for states, tx_id, caller in requests:
+            refs += [s.key() for s in states]
+            start.append(len(refs))
+            ids.append(tx_id)
+            callers.append(caller)
+        st, recs = self.table.commit_batch(np.array(start, dtype=np.uint64),
+                                           np.frombuffer(b"".join(refs) or bytes(36), dtype=np.uint8).copy(),
+                                           np.frombuffer(b"".join(ids), dtype=np.uint8).copy(),
+                                           np.array(callers, dtype=np.uint32))
+        out = [(int(s), Conflict([])) for s in st]
+        for tx, i, ci, cid, cc in recs:
+            out[tx][1].state_history.append((requests[tx][0][i], ConsumingTx(cid, ci, cc)))
+        return out
+
+    def commit(self, states: List[StateRef], tx_id: bytes, caller_identity: int):
+        """UniquenessProvider.commit: raises UniquenessException when an input is already consumed."""
+        st, conflict = self.commit_batch([(states, tx_id, caller_identity)])[0]
+        if st != 0:
+            raise UniquenessException(conflict)
+
+
+def commit_input_states(provider: PersistentUniquenessProvider, inputs: List[StateRef], tx_id: bytes,
+                        caller: int):
+    """TrustedAuthorityNotaryService.commitInputStates (NotaryService.kt:61-75)."""
+    try:
+        provider.commit(inputs, tx_id, caller)
+    except UniquenessException as e:
+        history = dict(e.error.state_history)
+        conflicts = [ref for i, ref in enumerate(inputs)
+                     if ref in history and history[ref] != ConsumingTx(tx_id, i, caller)]
+        if conflicts:
+            raise NotaryException(tx_id, e.error)
