@@ -58,6 +58,9 @@ struct chip_ctx {
     DevBuf t_salts, t_start, t_group, t_internal, t_data, t_off, t_len, t_ids, t_scratch;
     // fused tx verification: device-built SignableData messages + staging of the host entry
     DevBuf f_pool, f_moff, f_mlen, f_midx, f_htx, f_htm, f_tdata, f_toff, f_tlen, f_tid;
+    // filtered transactions: kernel scratch + staging of the host entry
+    DevBuf x_scratch, x_ids, x_ghs, x_gh, x_fgs, x_fgi, x_cs, x_cd, x_co, x_cl, x_nonce, x_pts, x_ptt, x_pth, x_cv,
+        x_st, x_rs;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, tev0 = nullptr, tev1 = nullptr;
     bool ev_pending = false, tev_pending = false;
     chip_stats stats{};
@@ -278,7 +281,9 @@ void chip_shutdown(chip_ctx* c) {
                       &c->h_msg_data, &c->h_msg_off, &c->h_msg_len, &c->h_status, &c->h_bitmap, &c->t_salts,
                       &c->t_start, &c->t_group, &c->t_internal, &c->t_data, &c->t_off, &c->t_len, &c->t_ids,
                       &c->t_scratch, &c->f_pool, &c->f_moff, &c->f_mlen, &c->f_midx, &c->f_htx, &c->f_htm,
-                      &c->f_tdata, &c->f_toff, &c->f_tlen, &c->f_tid};
+                      &c->f_tdata, &c->f_toff, &c->f_tlen, &c->f_tid, &c->x_scratch, &c->x_ids, &c->x_ghs,
+                      &c->x_gh, &c->x_fgs, &c->x_fgi, &c->x_cs, &c->x_cd, &c->x_co, &c->x_cl, &c->x_nonce,
+                      &c->x_pts, &c->x_ptt, &c->x_pth, &c->x_cv, &c->x_st, &c->x_rs};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < chip_ctx::KRING; i++) {
         if (c->kring[i].a) hipEventDestroy(c->kring[i].a);
@@ -705,6 +710,88 @@ int chip_verify_tx_batch(chip_ctx* c, const chip_tx_batch* b, const chip_msg_tem
     HIPCHK(c, hipStreamSynchronize(st));
     c->ev_pending = false;
     c->tev_pending = false;
+    return CHIP_OK;
+}
+
+// ---------------------------------------------------------------------------------------
+// filtered transactions
+int chip_ftx_verify_batch_device(chip_ctx* c, const chip_ftx_batch* b, uint8_t* status, uint8_t* reason,
+                                 void* stream) {
+    if (!c || !b || (b->ntx && !status)) return fail(c, CHIP_E_ARG, "null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, c->x_scratch.ensure(ftx_scratch_words(b->ntx) * 4 + 16));
+    const int ke = c->kbegin(CHIP_K_TXID, st);
+    launch_ftx_verify(st, b, status, reason, c->x_scratch.as<uint32_t>());
+    c->kend(ke, st);
+    HIPCHK(c, hipGetLastError());
+    return CHIP_OK;
+}
+
+int chip_ftx_verify_batch(chip_ctx* c, const chip_ftx_batch* b, uint8_t* status, uint8_t* reason) {
+    if (!c || !b) return fail(c, CHIP_E_ARG, "null argument");
+    const uint64_t ntx = b->ntx;
+    if (!ntx) return CHIP_OK;
+    if (!b->ids || !b->gh_start || !b->fg_start || !status) return fail(c, CHIP_E_ARG, "null tx array");
+    if (b->gh_start[0] != 0 || b->fg_start[0] != 0) return fail(c, CHIP_E_ARG, "start arrays must begin at 0");
+    for (uint64_t t = 0; t < ntx; t++)
+        if (b->gh_start[t] > b->gh_start[t + 1] || b->fg_start[t] > b->fg_start[t + 1])
+            return fail(c, CHIP_E_ARG, "gh_start / fg_start not monotone");
+    const uint64_t ngh = b->gh_start[ntx], nfg = b->fg_start[ntx];
+    if ((ngh && !b->group_hashes) || (nfg && (!b->fg_index || !b->comp_start || !b->pt_start)))
+        return fail(c, CHIP_E_ARG, "null group array");
+    uint64_t ncomp = 0, nnodes = 0;
+    if (nfg) {
+        if (b->comp_start[0] != 0 || b->pt_start[0] != 0) return fail(c, CHIP_E_ARG, "start arrays must begin at 0");
+        for (uint64_t g = 0; g < nfg; g++)
+            if (b->comp_start[g] > b->comp_start[g + 1] || b->pt_start[g] > b->pt_start[g + 1])
+                return fail(c, CHIP_E_ARG, "comp_start / pt_start not monotone");
+        ncomp = b->comp_start[nfg];
+        nnodes = b->pt_start[nfg];
+    }
+    if ((ncomp && (!b->comp_data || !b->comp_off || !b->comp_len || !b->nonces)) || (nnodes && (!b->pt_tag || !b->pt_hash)))
+        return fail(c, CHIP_E_ARG, "null component / tree array");
+    for (uint64_t k = 0; k < ncomp; k++)
+        if (b->comp_off[k] + b->comp_len[k] > b->comp_bytes) return fail(c, CHIP_E_ARG, "component outside pool");
+    hipStream_t st = c->stream;
+    int r;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        HIPCHK(c, hipSetDevice(c->device));
+        if ((r = stage(c, c->x_ids, b->ids, ntx * 32, st)) || (r = stage(c, c->x_ghs, b->gh_start, ntx + 1, st)) ||
+            (r = stage(c, c->x_gh, b->group_hashes, ngh * 32, st)) || (r = stage(c, c->x_fgs, b->fg_start, ntx + 1, st)) ||
+            (r = stage(c, c->x_fgi, b->fg_index, nfg, st)) ||
+            (r = stage(c, c->x_cs, b->comp_start, nfg ? nfg + 1 : 0, st)) ||
+            (r = stage(c, c->x_cd, b->comp_data, b->comp_bytes, st)) || (r = stage(c, c->x_co, b->comp_off, ncomp, st)) ||
+            (r = stage(c, c->x_cl, b->comp_len, ncomp, st)) || (r = stage(c, c->x_nonce, b->nonces, ncomp * 32, st)) ||
+            (r = stage(c, c->x_pts, b->pt_start, nfg ? nfg + 1 : 0, st)) || (r = stage(c, c->x_ptt, b->pt_tag, nnodes, st)) ||
+            (r = stage(c, c->x_pth, b->pt_hash, nnodes * 32, st)) ||
+            (r = stage(c, c->x_cv, b->check_visible, b->check_visible ? ntx : 0, st)))
+            return r;
+        HIPCHK(c, c->x_st.ensure(ntx + 16));
+        HIPCHK(c, c->x_rs.ensure(ntx + 16));
+    }
+    chip_ftx_batch d = *b;
+    d.ids = c->x_ids.as<uint8_t>();
+    d.gh_start = c->x_ghs.as<uint64_t>();
+    d.group_hashes = c->x_gh.as<uint8_t>();
+    d.fg_start = c->x_fgs.as<uint64_t>();
+    d.fg_index = c->x_fgi.as<uint32_t>();
+    d.comp_start = c->x_cs.as<uint64_t>();
+    d.comp_data = c->x_cd.as<uint8_t>();
+    d.comp_off = c->x_co.as<uint64_t>();
+    d.comp_len = c->x_cl.as<uint32_t>();
+    d.nonces = c->x_nonce.as<uint8_t>();
+    d.pt_start = c->x_pts.as<uint64_t>();
+    d.pt_tag = c->x_ptt.as<uint8_t>();
+    d.pt_hash = c->x_pth.as<uint8_t>();
+    d.check_visible = b->check_visible ? c->x_cv.as<int32_t>() : nullptr;
+    if ((r = chip_ftx_verify_batch_device(c, &d, c->x_st.as<uint8_t>(), c->x_rs.as<uint8_t>(), st))) return r;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipMemcpyAsync(status, c->x_st.p, ntx, hipMemcpyDeviceToHost, st));
+    if (reason) HIPCHK(c, hipMemcpyAsync(reason, c->x_rs.p, ntx, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
     return CHIP_OK;
 }
 

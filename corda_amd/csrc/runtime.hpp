@@ -18,6 +18,8 @@ void launch_ecdsa_verify(hipStream_t st, int scheme, uint64_t n, const uint32_t*
                          const chip_sig_batch* b, const uint32_t* ectab, uint8_t* status);
 
 void launch_txid(hipStream_t st, const chip_tx_batch* b, uint8_t* ids, uint32_t* scratch, uint64_t scratch_words);
+uint64_t ftx_scratch_words(uint64_t ntx);
+void launch_ftx_verify(hipStream_t st, const chip_ftx_batch* b, uint8_t* status, uint8_t* reason, uint32_t* scratch);
 
 // sizes of the per-key device tables (words per key)
 #define ED_KEY_TABLE_WORDS (9 * 40)

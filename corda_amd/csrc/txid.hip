@@ -9,6 +9,7 @@
 // One lane per transaction (the unit the caller batches; no cross-lane divergence for
 // same-shaped transactions).  Leaf and group-root levels are reduced in place in a per-tx
 // scratch slab in HBM (64 slots x 32 B; group ordinals must be < 64).
+#include <algorithm>
 #include "sha2_dev.hpp"
 #include "runtime.hpp"
 
@@ -217,4 +218,157 @@ void launch_txid(hipStream_t st, const chip_tx_batch* b, uint8_t* ids, uint32_t*
     const uint32_t blocks = (uint32_t)((b->ntx + 255) / 256);
     hipLaunchKernelGGL(k_txid, dim3(blocks), dim3(256), 0, st, b->ntx, b->salts, b->tx_comp_start, b->comp_group,
                        b->comp_internal, b->data, b->comp_off, b->comp_len, ids, leaves, slots);
+}
+
+// ---------------------------------------------------------------------------------------
+// K3b: FilteredTransaction.verify() + checkAllComponentsVisible() (the non-validating notary's
+// check, NonValidatingNotaryFlow.kt:27-29), one lane per filtered transaction:
+//   groupHashes non-empty (reason 1); MerkleTree(groupHashes).hash == id (2)   MerkleTransaction.kt:176-179
+//   per filtered group: groupIndex < |groupHashes| (3); partial-tree root == groupHashes[groupIndex] (4);
+//   the IncludedLeaf hashes == componentHash(nonce_i, component_i) as multisets (5)  :185-190,
+//   PartialMerkleTree.kt:133-160; a partial tree whose post-order encoding is not one tree (9)
+//   checkAllComponentsVisible(ordinal)                                         MerkleTransaction.kt:218-234
+//     group absent: ordinal >= |groupHashes| or groupHashes[ordinal] == allOnesHash (6);
+//     present: index in range (7), MerkleTree(all visible component hashes) == groupHashes[index] (8)
+// Per-lane scratch slab in HBM: 64 group-hash slots | 64-deep tree stack | 256 component hashes.
+#define FTX_MAX_STACK 64
+#define FTX_MAX_COMPS 256
+#define FTX_SLOTS (TX_MAX_GROUPS + FTX_MAX_STACK + FTX_MAX_COMPS)
+
+CHIP_DEV void ld8_be(uint32_t v[8], const uint8_t* p) {
+#pragma unroll
+    for (int j = 0; j < 8; j++) v[j] = ld_be32(p + 4 * j);
+}
+CHIP_DEV bool eq8(const uint32_t* a, const uint32_t* b) {
+    uint32_t d = 0;
+#pragma unroll
+    for (int j = 0; j < 8; j++) d |= a[j] ^ b[j];
+    return d == 0;
+}
+
+__global__ void __launch_bounds__(256) k_ftx_verify(chip_ftx_batch b, uint8_t* __restrict__ status,
+                                                    uint8_t* __restrict__ reason, uint32_t* __restrict__ scratch) {
+    const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t lanes = (uint64_t)gridDim.x * blockDim.x;
+    uint32_t* top = scratch + lane * (FTX_SLOTS * 8);
+    uint32_t* stk = top + TX_MAX_GROUPS * 8;
+    uint32_t* comps = stk + FTX_MAX_STACK * 8;
+    for (uint64_t t = lane; t < b.ntx; t += lanes) {
+        uint8_t st = 0, rs = 0;
+        const uint64_t g0 = b.gh_start[t], ngh = b.gh_start[t + 1] - g0;
+        uint32_t id[8], h[8];
+        ld8_be(id, b.ids + 32 * t);
+        if (ngh == 0) { st = 1; rs = 1; }
+        else if (ngh > TX_MAX_GROUPS) { st = 1; rs = 9; }
+        if (!st) {
+            for (uint64_t k = 0; k < ngh; k++) {
+                ld8_be(h, b.group_hashes + 32 * (g0 + k));
+                st8(top + 8 * k, h);
+            }
+            merkle_inplace(h, top, (uint32_t)ngh, 0xffffffffu, 0xffffffffu, false);
+            if (!eq8(h, id)) { st = 1; rs = 2; }
+        }
+        for (uint64_t g = b.fg_start[t]; !st && g < b.fg_start[t + 1]; g++) {
+            const uint32_t gi = b.fg_index[g];
+            if (gi >= ngh) { st = 1; rs = 3; break; }
+            const uint64_t c0 = b.comp_start[g], nc = b.comp_start[g + 1] - c0;
+            if (nc > FTX_MAX_COMPS) { st = 1; rs = 9; break; }
+            for (uint64_t c = 0; c < nc; c++) {
+                uint32_t nonce[8], leaf[8];
+                ld8_be(nonce, b.nonces + 32 * (c0 + c));
+                sha256d_prefixed(leaf, nonce, b.comp_data + b.comp_off[c0 + c], b.comp_len[c0 + c]);
+                st8(comps + 8 * c, leaf);
+            }
+            // post-order evaluation (rootAndUsedHashes); IncludedLeaf hashes matched against the
+            // component hashes one-to-one (multiset equality, PartialMerkleTree.verify's groupBy)
+            uint32_t matched[FTX_MAX_COMPS / 32];
+#pragma unroll
+            for (int q = 0; q < FTX_MAX_COMPS / 32; q++) matched[q] = 0;
+            uint32_t sp = 0, nused = 0;
+            bool bad_tree = false, unmatched = false;
+            for (uint64_t k = b.pt_start[g]; k < b.pt_start[g + 1]; k++) {
+                const uint8_t tag = b.pt_tag[k];
+                if (tag == 2) {
+                    if (sp < 2) { bad_tree = true; break; }
+                    uint32_t l[8], r[8];
+                    ld8(r, stk + 8 * (sp - 1));
+                    ld8(l, stk + 8 * (sp - 2));
+                    hash_concat(h, l, r);
+                    sp -= 2;
+                } else if (tag <= 1) {
+                    ld8_be(h, b.pt_hash + 32 * k);
+                    if (tag == 0) {
+                        nused++;
+                        bool hit = false;
+                        for (uint64_t c = 0; c < nc && !hit; c++) {
+                            if ((matched[c >> 5] >> (c & 31)) & 1u) continue;
+                            if (eq8(comps + 8 * c, h)) {
+                                matched[c >> 5] |= 1u << (c & 31);
+                                hit = true;
+                            }
+                        }
+                        unmatched = unmatched || !hit;
+                    }
+                } else {
+                    bad_tree = true;
+                    break;
+                }
+                if (sp >= FTX_MAX_STACK) { bad_tree = true; break; }
+                st8(stk + 8 * sp, h);
+                sp++;
+            }
+            if (bad_tree || sp != 1) { st = 1; rs = 9; break; }
+            uint32_t want[8];
+            ld8(h, stk);
+            ld8_be(want, b.group_hashes + 32 * (g0 + gi));
+            if (!eq8(h, want)) { st = 1; rs = 4; break; }
+            if (unmatched || nused != nc) { st = 1; rs = 5; break; }
+        }
+        const int32_t cv = b.check_visible ? b.check_visible[t] : -1;
+        if (!st && cv >= 0) {
+            int64_t found = -1;
+            for (uint64_t g = b.fg_start[t]; g < b.fg_start[t + 1]; g++)
+                if (b.fg_index[g] == (uint32_t)cv) { found = (int64_t)g; break; }
+            if (found < 0) {
+                bool ok = (uint64_t)cv >= ngh;
+                if (!ok) {
+                    ld8_be(h, b.group_hashes + 32 * (g0 + cv));
+                    ok = true;
+#pragma unroll
+                    for (int j = 0; j < 8; j++) ok = ok && h[j] == 0xffffffffu;
+                }
+                if (!ok) { st = 2; rs = 6; }
+            } else {
+                const uint32_t gi = b.fg_index[found];
+                const uint64_t c0 = b.comp_start[found], nc = b.comp_start[found + 1] - c0;
+                if (gi >= ngh) { st = 2; rs = 7; }
+                else if (nc == 0 || nc > FTX_MAX_COMPS) { st = 2; rs = 8; }
+                else {
+                    for (uint64_t c = 0; c < nc; c++) {
+                        uint32_t nonce[8], leaf[8];
+                        ld8_be(nonce, b.nonces + 32 * (c0 + c));
+                        sha256d_prefixed(leaf, nonce, b.comp_data + b.comp_off[c0 + c], b.comp_len[c0 + c]);
+                        st8(comps + 8 * c, leaf);
+                    }
+                    uint32_t want[8];
+                    merkle_inplace(h, comps, (uint32_t)nc, 0xffffffffu, 0xffffffffu, false);
+                    ld8_be(want, b.group_hashes + 32 * (g0 + gi));
+                    if (!eq8(h, want)) { st = 2; rs = 8; }
+                }
+            }
+        }
+        status[t] = st;
+        if (reason) reason[t] = rs;
+    }
+}
+
+uint64_t ftx_scratch_words(uint64_t ntx) {
+    const uint64_t blocks = std::min<uint64_t>((ntx + 255) / 256, 256);
+    return blocks * 256 * FTX_SLOTS * 8;
+}
+
+void launch_ftx_verify(hipStream_t st, const chip_ftx_batch* b, uint8_t* status, uint8_t* reason, uint32_t* scratch) {
+    if (!b->ntx) return;
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>((b->ntx + 255) / 256, 256);
+    hipLaunchKernelGGL(k_ftx_verify, dim3(blocks), dim3(256), 0, st, *b, status, reason, scratch);
 }

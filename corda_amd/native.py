@@ -35,7 +35,8 @@ EXPORTS = ["chip_abi_version", "chip_device_count", "chip_init", "chip_shutdown"
            "chip_uniq_open", "chip_uniq_close", "chip_uniq_size", "chip_uniq_rebuild", "chip_uniq_commit_batch",
            "chip_uniq_commit_batch_device", "chip_uniq_last_error", "chip_uniq_shard_begin", "chip_uniq_shard_vote",
            "chip_uniq_shard_apply", "chip_uniq_shard_classify", "chip_uniq_shard_finish",
-           "chip_verify_tx_batch", "chip_verify_tx_batch_device",
+           "chip_verify_tx_batch", "chip_verify_tx_batch_device", "chip_ftx_verify_batch",
+           "chip_ftx_verify_batch_device",
            "chip_get_stats", "chip_reset_stats"]
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -75,6 +76,28 @@ class ChipSignerBatch(ctypes.Structure):
                 ("sig_len", ctypes.c_void_p), ("n_keys", ctypes.c_uint64), ("key_data", ctypes.c_void_p),
                 ("key_off", ctypes.c_void_p), ("key_len", ctypes.c_void_p), ("sig_bytes", ctypes.c_uint64),
                 ("key_bytes", ctypes.c_uint64)]
+
+
+class ChipFtxBatch(ctypes.Structure):
+    _fields_ = [("ntx", ctypes.c_uint64), ("ids", ctypes.c_void_p), ("gh_start", ctypes.c_void_p),
+                ("group_hashes", ctypes.c_void_p), ("fg_start", ctypes.c_void_p), ("fg_index", ctypes.c_void_p),
+                ("comp_start", ctypes.c_void_p), ("comp_data", ctypes.c_void_p), ("comp_off", ctypes.c_void_p),
+                ("comp_len", ctypes.c_void_p), ("nonces", ctypes.c_void_p), ("pt_start", ctypes.c_void_p),
+                ("pt_tag", ctypes.c_void_p), ("pt_hash", ctypes.c_void_p), ("check_visible", ctypes.c_void_p),
+                ("comp_bytes", ctypes.c_uint64)]
+
+
+FTX_FIELDS = ("ids", "gh_start", "group_hashes", "fg_start", "fg_index", "comp_start", "comp_data", "comp_off",
+              "comp_len", "nonces", "pt_start", "pt_tag", "pt_hash", "check_visible")
+
+
+def make_ftx_batch(f) -> ChipFtxBatch:
+    s = ChipFtxBatch()
+    s.ntx = int(f.ntx)
+    for name in FTX_FIELDS:
+        setattr(s, name, _ptr(getattr(f, name, None)))
+    s.comp_bytes = _nbytes(f.comp_data)
+    return s
 
 
 class ChipUniqShardBatch(ctypes.Structure):
@@ -134,6 +157,10 @@ def load(build_if_missing: bool = False):
     lib.chip_verify_tx_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipTxBatch),
                                                 ctypes.POINTER(ChipMsgTemplates), ctypes.POINTER(ChipSignerBatch),
                                                 ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.chip_ftx_verify_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipFtxBatch), ctypes.c_void_p,
+                                          ctypes.c_void_p]
+    lib.chip_ftx_verify_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipFtxBatch), ctypes.c_void_p,
+                                                 ctypes.c_void_p, ctypes.c_void_p]
     lib.chip_uniq_open.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]
     lib.chip_uniq_close.argtypes = [ctypes.c_void_p]
     lib.chip_uniq_size.argtypes = [ctypes.c_void_p]
@@ -305,6 +332,20 @@ class Context:
         self._check(self.lib.chip_verify_tx_batch_device(self.h, ctypes.byref(tb), ctypes.byref(tm),
                                                          ctypes.byref(sb), _ptr(ids), _ptr(status), _ptr(bitmap),
                                                          stream or None))
+
+    # ---- FilteredTransaction.verify + checkAllComponentsVisible ----
+    def ftx_verify_batch(self, f):
+        """Host arrays (chip_ftx_batch layout) -> (status u8[ntx], reason u8[ntx])."""
+        s = make_ftx_batch(f)
+        status = np.zeros(s.ntx, dtype=np.uint8)
+        reason = np.zeros(s.ntx, dtype=np.uint8)
+        self._check(self.lib.chip_ftx_verify_batch(self.h, ctypes.byref(s), _ptr(status), _ptr(reason)))
+        return status, reason
+
+    def ftx_verify_batch_device(self, dev_f, status, reason=None, stream=None):
+        s = make_ftx_batch(dev_f)
+        self._check(self.lib.chip_ftx_verify_batch_device(self.h, ctypes.byref(s), _ptr(status), _ptr(reason),
+                                                          stream or None))
 
     def stats(self) -> ChipStats:
         st = ChipStats()

@@ -149,6 +149,54 @@ int chip_txid_batch(chip_ctx* ctx, const chip_tx_batch* batch, uint8_t* ids);
 int chip_txid_batch_device(chip_ctx* ctx, const chip_tx_batch* batch, uint8_t* ids, void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * FilteredTransaction verification (the non-validating notary's check before commitInputStates,
+ * NonValidatingNotaryFlow.kt:27-29): FilteredTransaction.verify() (MerkleTransaction.kt:175-191,
+ * PartialMerkleTree.kt:133-160) followed, when check_visible[t] >= 0, by
+ * checkAllComponentsVisible(ComponentGroupEnum ordinal check_visible[t]) (MerkleTransaction.kt:218-234).
+ * Per filtered tx t: id (32 B), groupHashes rows gh_start[t] .. gh_start[t+1] (32 B each), filtered
+ * component groups fg_start[t] .. fg_start[t+1]; per filtered group g: groupIndex fg_index[g], its
+ * visible components comp_start[g] .. comp_start[g+1] (bytes in the comp pool, one 32-byte nonce each)
+ * and its PartialMerkleTree flattened in post-order: pt_start[g] .. pt_start[g+1] nodes, tag 0
+ * IncludedLeaf / 1 Leaf (hash in pt_hash) / 2 Node.  Limits: <= 64 group hashes, <= 256 visible
+ * components per group, tree depth <= 63 (else reason CHIP_FTX_MALFORMED).
+ * status[t]: 0 OK, 1 FilteredTransactionVerificationException, 2 ComponentVisibilityException;
+ * reason[t] (may be NULL): which check failed, in the reference's order: */
+enum chip_ftx_reason {
+    CHIP_FTX_OK = 0,
+    CHIP_FTX_NO_GROUP_HASHES = 1,      /* "At least one component group hash is required"               */
+    CHIP_FTX_TOP_ROOT = 2,             /* "Top level Merkle tree cannot be verified against transaction's id" */
+    CHIP_FTX_GROUP_INDEX = 3,          /* "There is no matching component group hash for group"         */
+    CHIP_FTX_PARTIAL_ROOT = 4,         /* "Partial Merkle tree root and advertised full Merkle tree root ..." */
+    CHIP_FTX_VISIBLE_LEAVES = 5,       /* "Visible components in group ... cannot be verified ..."       */
+    CHIP_FTX_VIS_ABSENT_GROUP = 6,     /* visibility: "Did not receive components for group ..."         */
+    CHIP_FTX_VIS_GROUP_INDEX = 7,      /* visibility: "There is no matching component group hash ..."    */
+    CHIP_FTX_VIS_FULL_ROOT = 8,        /* visibility: "The partial Merkle tree root does not match ..."  */
+    CHIP_FTX_MALFORMED = 9             /* partial-tree encoding is not one tree / past the limits        */
+};
+typedef struct {
+    uint64_t ntx;
+    const uint8_t* ids;             /* [ntx * 32]            */
+    const uint64_t* gh_start;       /* [ntx + 1]             */
+    const uint8_t* group_hashes;    /* [gh_start[ntx] * 32]  */
+    const uint64_t* fg_start;       /* [ntx + 1]             */
+    const uint32_t* fg_index;       /* [nfg]                 */
+    const uint64_t* comp_start;     /* [nfg + 1]             */
+    const uint8_t* comp_data;       /* pool                  */
+    const uint64_t* comp_off;       /* [ncomp]               */
+    const uint32_t* comp_len;       /* [ncomp]               */
+    const uint8_t* nonces;          /* [ncomp * 32]          */
+    const uint64_t* pt_start;       /* [nfg + 1]             */
+    const uint8_t* pt_tag;          /* [nnodes]              */
+    const uint8_t* pt_hash;         /* [nnodes * 32]         */
+    const int32_t* check_visible;   /* [ntx] or NULL         */
+    uint64_t comp_bytes;
+} chip_ftx_batch;
+
+int chip_ftx_verify_batch(chip_ctx* ctx, const chip_ftx_batch* batch, uint8_t* status, uint8_t* reason);
+int chip_ftx_verify_batch_device(chip_ctx* ctx, const chip_ftx_batch* batch, uint8_t* status, uint8_t* reason,
+                                 void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Fused transaction verification: ids, then every required signer against the recomputed id
  * (SignedTransaction.verifySignaturesExcept's signature part for a batch of transactions:
  * WireTransaction.id, WireTransaction.kt:63, then TransactionSignature.verify(id) for each sig,

@@ -121,6 +121,18 @@ void orc_uniq_commit_batch(orc_uniq*, uint64_t ntx, const uint64_t* tx_ref_start
                            const uint8_t* refs36, const uint8_t* tx_ids, const uint32_t* callers,
                            uint8_t* tx_status, orc_conflict* out, uint64_t cap, uint64_t* n_out);
 
+/* ---- FilteredTransaction.verify + checkAllComponentsVisible (MerkleTransaction.kt:175-234,
+ *      PartialMerkleTree.kt:133-160), chip_ftx_batch layout; partial trees in post-order ---- */
+int orc_ftx_verify(const uint8_t id[32], uint64_t ngh, const uint8_t* gh, uint64_t nfg, const uint32_t* fg_index,
+                   const uint64_t* comp_start, const uint8_t* comp_data, const uint64_t* comp_off,
+                   const uint32_t* comp_len, const uint8_t* nonces, const uint64_t* pt_start, const uint8_t* pt_tag,
+                   const uint8_t* pt_hash, int32_t check_visible, int* reason);
+void orc_ftx_verify_batch(uint64_t ntx, const uint8_t* ids, const uint64_t* gh_start, const uint8_t* gh,
+                          const uint64_t* fg_start, const uint32_t* fg_index, const uint64_t* comp_start,
+                          const uint8_t* comp_data, const uint64_t* comp_off, const uint32_t* comp_len,
+                          const uint8_t* nonces, const uint64_t* pt_start, const uint8_t* pt_tag,
+                          const uint8_t* pt_hash, const int32_t* check_visible, uint8_t* status, uint8_t* reason);
+
 #ifdef __cplusplus
 }
 #endif

@@ -177,3 +177,14 @@ class Uniq:
         recs = [(c.tx, c.input_index, c.consumed_index, bytes(c.consuming_tx), c.consuming_caller)
                 for c in out[:min(nout.value, cap)]]
         return st, recs
+
+
+def ftx_verify_batch(f):
+    """FilteredTransaction.verify + checkAllComponentsVisible over the chip_ftx_batch layout."""
+    st = np.zeros(f.ntx, dtype=np.uint8)
+    rs = np.zeros(f.ntx, dtype=np.uint8)
+    lib().orc_ftx_verify_batch(ctypes.c_uint64(f.ntx), _p(f.ids), _p(f.gh_start), _p(f.group_hashes), _p(f.fg_start),
+                               _p(f.fg_index), _p(f.comp_start), _p(f.comp_data), _p(f.comp_off), _p(f.comp_len),
+                               _p(f.nonces), _p(f.pt_start), _p(f.pt_tag), _p(f.pt_hash), _p(f.check_visible),
+                               _p(st), _p(rs))
+    return st, rs
