@@ -15,6 +15,22 @@
 
 #define TX_MAX_GROUPS 64
 
+// N big-endian words from p (any alignment): N (+1 when unaligned) independent aligned dword loads,
+// funnel-shifted — one batch of loads per block instead of a dependent chain of byte gathers.  The
+// extra word shares its aligned dword with the last wanted byte, so it never crosses a page.
+template <int N>
+CHIP_DEV void load_be_words(uint32_t* w, const uint8_t* p) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t sh = (uint32_t)(a & 3u);
+    const uint32_t* ap = reinterpret_cast<const uint32_t*>(a - sh);
+    uint32_t d[N + 1];
+#pragma unroll
+    for (int k = 0; k < N; k++) d[k] = ap[k];
+    d[N] = sh ? ap[N] : 0u;
+#pragma unroll
+    for (int k = 0; k < N; k++) w[k] = __builtin_bswap32(__builtin_amdgcn_alignbyte(d[k + 1], d[k], sh));
+}
+
 // SHA256(SHA256(prefix32 || bytes[0:len]))  (componentHash with prefix = nonce)
 CHIP_DEV void sha256d_prefixed(uint32_t out[8], const uint32_t pre[8], const uint8_t* p, uint32_t len) {
     uint32_t H[8], w[16];
@@ -22,10 +38,19 @@ CHIP_DEV void sha256d_prefixed(uint32_t out[8], const uint32_t pre[8], const uin
     const uint64_t total = 32ull + len;
     const uint32_t nblocks = (uint32_t)((total + 9 + 63) / 64);
     for (uint32_t b = 0; b < nblocks; b++) {
+        const int64_t q0 = (int64_t)b * 64 - 32;   // first component byte of this block
+        if (b > 0 && q0 + 64 <= (int64_t)len) {
+            load_be_words<16>(w, p + q0);           // whole block inside the component
+        } else if (b == 0 && len >= 32) {
 #pragma unroll
-        for (int j = 0; j < 16; j++) {
-            if (b == 0 && j < 8) w[j] = pre[j];
-            else w[j] = comp_word(p, len, (int64_t)b * 64 + 4 * j - 32);
+            for (int j = 0; j < 8; j++) w[j] = pre[j];
+            load_be_words<8>(w + 8, p);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; j++) {
+                if (b == 0 && j < 8) w[j] = pre[j];
+                else w[j] = comp_word(p, len, q0 + 4 * j);
+            }
         }
         if (b == nblocks - 1) {
             w[14] = (uint32_t)((total * 8) >> 32);

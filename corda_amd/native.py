@@ -140,6 +140,13 @@ def load(build_if_missing: bool = False):
             _build.build()
         else:
             raise NativeUnavailable("libcordahip.so not built (run __graft_entry__.build())")
+    # PyTorch-ROCm bundles its own HIP/HSA runtimes; when both are used in one process (device
+    # tensors, streams, RCCL) torch's must initialise the GPU first or its device enumeration fails
+    # after libcordahip's runtime has opened the device.  Loading torch here keeps that order.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(path)
     lib.chip_last_error.restype = ctypes.c_char_p
     lib.chip_last_error.argtypes = [ctypes.c_void_p]
