@@ -61,7 +61,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--n", type=int, default=1_000_000, help="signatures per rank")
+    ap.add_argument("--sigs", "--n", dest="n", type=int, default=1_000_000, help="cfg2 signatures per rank")
     ap.add_argument("--keys", type=int, default=4096)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=32768)
@@ -100,11 +100,27 @@ SIG_FIELDS = ("key_idx", "msg_idx", "sig_data", "sig_off", "sig_len", "key_data"
 TX_FIELDS = ("salts", "tx_comp_start", "comp_group", "comp_internal", "data", "comp_off", "comp_len")
 
 
+# The driver launches N ranks over RCCL ("nccl").  CORDA_BENCH_BACKEND=gloo rehearses the N > 1 code
+# path on a one-GPU box (every rank on device 0, collectives staged through host memory); its
+# timings are not scaling numbers.
+BACKEND = os.environ.get("CORDA_BENCH_BACKEND", "nccl")
+
+
+def all_reduce(t, op, dist):
+    if BACKEND == "nccl" or not t.is_cuda:
+        dist.all_reduce(t, op=op)
+        return t
+    c = t.cpu()
+    dist.all_reduce(c, op=op)
+    t.copy_(c)
+    return t
+
+
 def max_over_ranks(x, world, torch, dev, dist):
     if world == 1:
         return x
     e = torch.tensor([x], dtype=torch.float64, device=dev)
-    dist.all_reduce(e, op=dist.ReduceOp.MAX)
+    all_reduce(e, dist.ReduceOp.MAX, dist)
     return float(e.item())
 
 
@@ -162,7 +178,8 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", rank=rank, world_size=world)
+        dist.init_process_group(BACKEND, rank=rank, world_size=world)
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     ctx = corda_amd.Context(local)
@@ -182,7 +199,12 @@ def main():
     def step():
         ctx.verify_batch_device(db, status, bitmap, stream=stream.cuda_stream)
         if world > 1:
-            dist.all_gather_into_tensor(gathered, bitmap)
+            if BACKEND == "nccl":
+                dist.all_gather_into_tensor(gathered, bitmap)
+            else:
+                parts = [torch.empty_like(bitmap, device="cpu") for _ in range(world)]
+                dist.all_gather(parts, bitmap.cpu())
+                gathered.copy_(torch.cat(parts))
 
     for _ in range(args.warmup):
         step()
@@ -204,7 +226,7 @@ def main():
     elapsed = max_over_ranks(time.perf_counter() - t0, world, torch, dev, dist)
     if world > 1:
         c = torch.tensor([int(correct)], dtype=torch.int32, device=dev)
-        dist.all_reduce(c, op=dist.ReduceOp.MIN)
+        all_reduce(c, dist.ReduceOp.MIN, dist)
         correct = bool(c.item())
     s = ctx.stats()
 

@@ -190,15 +190,24 @@ def commit_sharded(engine, batch, group=None, shard=None):
         engine.begin(shard, batch.tx_ids, batch.callers)
     else:
         engine.begin(shard)
+    # RCCL reduces device tensors in place; a CPU process group (gloo) gets host copies
+    host = dist.get_backend(group) != "nccl"
+
+    def reduce_max(v):
+        if host and getattr(v, "is_cuda", False):
+            c = v.cpu()
+            dist.all_reduce(c, op=dist.ReduceOp.MAX, group=group)
+            v.copy_(c)
+        else:
+            dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
+        return v
     rounds = 0
     while True:
-        v = engine.vote()
-        dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
+        v = reduce_max(engine.vote())
         rounds += 1
         if engine.apply(v) == 0:
             break
-    v = engine.classify()
-    dist.all_reduce(v, op=dist.ReduceOp.MAX, group=group)
+    v = reduce_max(engine.classify())
     status, recs = engine.finish(v)
     gathered = [None] * world
     dist.all_gather_object(gathered, recs, group=group)

@@ -434,8 +434,8 @@ def records_from_bytes(raw: bytes):
 class UniqShardEngine:
     """One GPU's slice of the notary table driven through the chip_uniq_shard_* phases (the
     multi-GPU protocol is corda_amd.distributed.commit_sharded).  Device buffers are torch tensors
-    on the table's GPU; the phases run on torch's current stream, so RCCL collectives issued by
-    torch on that stream's tensors are ordered with them."""
+    on the table's GPU; the phases run on the engine's own stream, ordered against torch's current
+    stream (where the collectives and copies of the vote tensors run) with stream waits."""
 
     def __init__(self, table: UniqTable):
         self.table = table
@@ -472,20 +472,34 @@ class UniqShardEngine:
         self.status = torch.zeros(max(1, self.ntx), dtype=torch.uint8, device=dev)
         b = ChipUniqShardBatch(self.ntx, d["start"].data_ptr(), d["nref"], d["refs"].data_ptr(), d["pos"].data_ptr(),
                                d["ids"].data_ptr(), d["callers"].data_ptr())
-        stream = torch.cuda.current_stream(dev).cuda_stream
-        self.table._check(self.lib.chip_uniq_shard_begin(self.table.h, ctypes.byref(b), stream or None))
+        self.stream = torch.cuda.Stream(device=dev)
+        self.stream.wait_stream(torch.cuda.current_stream(dev))   # inputs / buffers written by torch
+        self.table._check(self.lib.chip_uniq_shard_begin(self.table.h, ctypes.byref(b), self.stream.cuda_stream))
+
+    def _to_torch(self):
+        import torch
+        torch.cuda.current_stream(torch.device("cuda", self.device)).wait_stream(self.stream)
+
+    def _from_torch(self):
+        import torch
+        self.stream.wait_stream(torch.cuda.current_stream(torch.device("cuda", self.device)))
 
     def vote(self):
+        self._from_torch()
         self.table._check(self.lib.chip_uniq_shard_vote(self.table.h, self.vote_buf.data_ptr()))
+        self._to_torch()
         return self.vote_buf[:self.ntx]
 
     def apply(self, decision) -> int:
+        self._from_torch()
         und = ctypes.c_uint64()
         self.table._check(self.lib.chip_uniq_shard_apply(self.table.h, decision.data_ptr(), ctypes.byref(und)))
         return und.value
 
     def classify(self):
+        self._from_torch()
         self.table._check(self.lib.chip_uniq_shard_classify(self.table.h, self.vote_buf.data_ptr()))
+        self._to_torch()
         return self.vote_buf[:self.ntx]
 
     def finish(self, decision):
@@ -494,6 +508,7 @@ class UniqShardEngine:
         cap = int(self._keep["nref"]) + 1
         out = torch.empty(cap * ctypes.sizeof(ChipConflict), dtype=torch.uint8,
                           device=torch.device("cuda", self.device))
+        self._from_torch()
         nout = ctypes.c_uint64()
         self.table._check(self.lib.chip_uniq_shard_finish(self.table.h, decision.data_ptr(), self.status.data_ptr(),
                                                           out.data_ptr(), ctypes.c_uint64(cap), ctypes.byref(nout)))
