@@ -382,3 +382,435 @@ void launch_ecdsa_verify(hipStream_t st, int scheme, uint64_t n, const uint32_t*
                            b->msg_idx, b->sig_data, b->sig_off, b->sig_len, b->msg_data, b->msg_off, b->msg_len,
                            ectab, status);
 }
+
+// ---------------------------------------------------------------------------------------
+// K2c: per-key comb path (keys that sign many signatures of a batch).  R = u1 G + u2 Q with no
+// doublings: u2 in signed radix-16 digits over 65 windows from a per-key table of 2^(4w) {1..8} Q
+// (built for the batch by k_ecdsa_comb_chain / k_ecdsa_comb_fill on the second stream, normalised to
+// affine so every addition is a mixed one), u1 in signed radix-256 digits over 33 windows from the
+// fixed tables EC_<C>_G_COMB.  s^-1 is one Fermat inversion per EC_INV_BATCH signatures (Montgomery's
+// trick, k_ecdsa_comb_inv).  96 mixed additions instead of 256 doublings + 96 mixed additions; the same
+// BC 1.57 semantics as k_ecdsa_verify (identical DER / range / x(R) mod n checks).
+#include "comb_tables.hpp"
+
+#define EC_COMB_QWIN 65
+#define EC_COMB_QENT 8
+#define EC_COMB_JW 24
+// affine table per key, then (after all keys) the Jacobian scratch it is normalised from
+#define EC_COMB_KEY_WORDS (EC_COMB_QWIN * EC_COMB_QENT * 16)
+#define EC_COMB_JAC_WORDS (EC_COMB_QWIN * EC_COMB_QENT * EC_COMB_JW)
+#define EC_INV_BATCH 16
+
+CHIP_DEV void store_jpt(uint32_t* d, const jpt& p) {
+    uint4* d4 = reinterpret_cast<uint4*>(d);
+    d4[0] = make_uint4(p.X.w[0], p.X.w[1], p.X.w[2], p.X.w[3]);
+    d4[1] = make_uint4(p.X.w[4], p.X.w[5], p.X.w[6], p.X.w[7]);
+    d4[2] = make_uint4(p.Y.w[0], p.Y.w[1], p.Y.w[2], p.Y.w[3]);
+    d4[3] = make_uint4(p.Y.w[4], p.Y.w[5], p.Y.w[6], p.Y.w[7]);
+    d4[4] = make_uint4(p.Z.w[0], p.Z.w[1], p.Z.w[2], p.Z.w[3]);
+    d4[5] = make_uint4(p.Z.w[4], p.Z.w[5], p.Z.w[6], p.Z.w[7]);
+}
+CHIP_DEV void store_u256(uint32_t* d, const u256& v) {
+    uint4* d4 = reinterpret_cast<uint4*>(d);
+    d4[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
+    d4[1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
+}
+CHIP_DEV void load_u256(u256& v, const uint32_t* s) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(s);
+    const uint4 a = s4[0], b = s4[1];
+    v.w[0] = a.x; v.w[1] = a.y; v.w[2] = a.z; v.w[3] = a.w;
+    v.w[4] = b.x; v.w[5] = b.y; v.w[6] = b.z; v.w[7] = b.w;
+}
+CHIP_DEV void load_jpt(jpt& p, const uint32_t* s) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(s);
+    uint4 v;
+    v = s4[0]; p.X.w[0] = v.x; p.X.w[1] = v.y; p.X.w[2] = v.z; p.X.w[3] = v.w;
+    v = s4[1]; p.X.w[4] = v.x; p.X.w[5] = v.y; p.X.w[6] = v.z; p.X.w[7] = v.w;
+    v = s4[2]; p.Y.w[0] = v.x; p.Y.w[1] = v.y; p.Y.w[2] = v.z; p.Y.w[3] = v.w;
+    v = s4[3]; p.Y.w[4] = v.x; p.Y.w[5] = v.y; p.Y.w[6] = v.z; p.Y.w[7] = v.w;
+    v = s4[4]; p.Z.w[0] = v.x; p.Z.w[1] = v.y; p.Z.w[2] = v.z; p.Z.w[3] = v.w;
+    v = s4[5]; p.Z.w[4] = v.x; p.Z.w[5] = v.y; p.Z.w[6] = v.z; p.Z.w[7] = v.w;
+}
+
+// r = p + q, both Jacobian (add-2007-bl); exact for infinity, p == q and p == -q.  r may alias p.
+template <int C> CHIP_DEV void jadd(jpt& r, const jpt& p, const jpt& q) {
+    if (u256_is_zero(p.Z)) { r = q; return; }
+    if (u256_is_zero(q.Z)) { r = p; return; }
+    u256 Z1Z1, Z2Z2, U1, U2, S1, S2, H, I, J, rr, V, t;
+    fp_sqr<C>(Z1Z1, p.Z);
+    fp_sqr<C>(Z2Z2, q.Z);
+    fp_mul<C>(U1, p.X, Z2Z2);
+    fp_mul<C>(U2, q.X, Z1Z1);
+    fp_mul<C>(S1, p.Y, q.Z);
+    fp_mul<C>(S1, S1, Z2Z2);
+    fp_mul<C>(S2, q.Y, p.Z);
+    fp_mul<C>(S2, S2, Z1Z1);
+    fp_sub<C>(H, U2, U1);
+    fp_sub<C>(rr, S2, S1);
+    if (u256_is_zero(H)) {
+        if (u256_is_zero(rr)) {
+            jdbl<C>(r, p);
+        } else {
+#pragma unroll
+            for (int i = 0; i < 8; i++) r.X.w[i] = r.Y.w[i] = r.Z.w[i] = 0;
+        }
+        return;
+    }
+    fp_add<C>(rr, rr, rr);
+    fp_add<C>(I, H, H);
+    fp_sqr<C>(I, I);
+    fp_mul<C>(J, H, I);
+    fp_mul<C>(V, U1, I);
+    jpt o;
+    fp_sqr<C>(o.X, rr);
+    fp_sub<C>(o.X, o.X, J);
+    fp_sub<C>(o.X, o.X, V);
+    fp_sub<C>(o.X, o.X, V);
+    fp_sub<C>(t, V, o.X);
+    fp_mul<C>(o.Y, rr, t);
+    fp_mul<C>(t, S1, J);
+    fp_add<C>(t, t, t);
+    fp_sub<C>(o.Y, o.Y, t);
+    fp_add<C>(t, p.Z, q.Z);
+    fp_sqr<C>(t, t);
+    fp_sub<C>(t, t, Z1Z1);
+    fp_sub<C>(t, t, Z2Z2);
+    fp_mul<C>(o.Z, t, H);
+    r = o;
+}
+
+CHIP_DEV bool ec_key_ok(const KeyMeta* meta, uint64_t k, int scheme) {
+    const KeyMeta m = meta[k];
+    return m.scheme == scheme && m.ok;
+}
+
+// chain: P_w = 2^(4w) Q for w = 0..64 into entry 1 of every window of the Jacobian scratch
+// (256 serial doublings per key)
+template <int C>
+CHIP_DEV void ec_comb_chain(const uint32_t* __restrict__ ectab, uint32_t* __restrict__ jac, uint64_t k) {
+    apt q;
+    load_apt(q, ectab + k * EC_TAB_STRIDE + 16);
+    jpt P;
+    P.X = q.x;
+    P.Y = q.y;
+#pragma unroll
+    for (int i = 0; i < 8; i++) P.Z.w[i] = (i == 0);
+    uint32_t* tab = jac + k * EC_COMB_JAC_WORDS;
+    for (int w = 0; w < EC_COMB_QWIN; w++) {
+        store_jpt(tab + (uint32_t)w * EC_COMB_QENT * EC_COMB_JW, P);
+        if (w + 1 == EC_COMB_QWIN) break;
+#pragma unroll 1
+        for (int b = 0; b < 4; b++) jdbl<C>(P, P);
+    }
+}
+// fill: entries j = 2..8 of window w = j P_w (Jacobian scratch), then to affine.  A lane takes
+// EC_FILL_GROUP windows so that one Fermat inversion serves 8 EC_FILL_GROUP entries (Montgomery's
+// trick; the prefix products are parked in the x slots of the affine entries)
+#define EC_FILL_GROUP 8
+#define EC_FILL_LANES ((EC_COMB_QWIN - 1) / EC_FILL_GROUP)
+template <int C>
+CHIP_DEV void ec_comb_fill(uint32_t* __restrict__ jac, uint32_t* __restrict__ out, uint32_t w0, uint32_t w1) {
+    u256 acc, z, t;
+#pragma unroll
+    for (int i = 0; i < 8; i++) acc.w[i] = (i == 0);
+    for (uint32_t w = w0; w < w1; w++) {
+        uint32_t* e = jac + w * EC_COMB_QENT * EC_COMB_JW;
+        uint32_t* o = out + w * EC_COMB_QENT * 16;
+        jpt P, A;
+        load_jpt(P, e);
+        store_u256(o, acc);
+        fp_mul<C>(acc, acc, P.Z);
+        jdbl<C>(A, P);
+        store_jpt(e + EC_COMB_JW, A);
+        store_u256(o + 16, acc);
+        fp_mul<C>(acc, acc, A.Z);
+#pragma unroll 1
+        for (int j = 3; j <= EC_COMB_QENT; j++) {
+            jadd<C>(A, A, P);
+            store_jpt(e + (uint32_t)(j - 1) * EC_COMB_JW, A);
+            store_u256(o + (uint32_t)(j - 1) * 16, acc);
+            fp_mul<C>(acc, acc, A.Z);
+        }
+    }
+    fp_inv<C>(acc, acc);   // entries are j 2^(4w) Q, never infinity for a valid key
+    for (uint32_t w = w1; w-- > w0;) {
+        const uint32_t* e = jac + w * EC_COMB_QENT * EC_COMB_JW;
+        uint32_t* o = out + w * EC_COMB_QENT * 16;
+#pragma unroll 1
+        for (int j = EC_COMB_QENT - 1; j >= 0; j--) {
+            u256 zi, zi2, pre, x, y;
+            load_u256(pre, o + (uint32_t)j * 16);
+            load_u256(z, e + (uint32_t)j * EC_COMB_JW + 16);
+            fp_mul<C>(zi, acc, pre);
+            fp_mul<C>(acc, acc, z);
+            fp_sqr<C>(zi2, zi);
+            load_u256(x, e + (uint32_t)j * EC_COMB_JW);
+            load_u256(y, e + (uint32_t)j * EC_COMB_JW + 8);
+            fp_mul<C>(x, x, zi2);
+            fp_mul<C>(t, zi2, zi);
+            fp_mul<C>(y, y, t);
+            store_u256(o + (uint32_t)j * 16, x);
+            store_u256(o + (uint32_t)j * 16 + 8, y);
+        }
+    }
+}
+// one launch for both curves: r1 and k1 keys build concurrently (lane per key)
+__global__ void __launch_bounds__(64) k_ecdsa_comb_chain(uint64_t n_keys, const KeyMeta* __restrict__ meta,
+                                                         const uint32_t* __restrict__ ectab, uint32_t* __restrict__ jac) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_keys) return;
+    if (ec_key_ok(meta, k, CHIP_SCHEME_R1)) ec_comb_chain<CURVE_R1>(ectab, jac, k);
+    else if (ec_key_ok(meta, k, CHIP_SCHEME_K1)) ec_comb_chain<CURVE_K1>(ectab, jac, k);
+}
+// lane per key x group of windows (the last group also takes window 64)
+__global__ void __launch_bounds__(256) k_ecdsa_comb_fill(uint64_t n_keys, const KeyMeta* __restrict__ meta,
+                                                         uint32_t* __restrict__ ctab, uint32_t* __restrict__ jac) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t k = g / EC_FILL_LANES;
+    const uint32_t grp = (uint32_t)(g % EC_FILL_LANES);
+    if (k >= n_keys) return;
+    const uint32_t w0 = grp * EC_FILL_GROUP;
+    const uint32_t w1 = (grp + 1 == EC_FILL_LANES) ? EC_COMB_QWIN : w0 + EC_FILL_GROUP;
+    uint32_t* e = jac + k * EC_COMB_JAC_WORDS;
+    uint32_t* out = ctab + k * EC_COMB_KEY_WORDS;
+    if (ec_key_ok(meta, k, CHIP_SCHEME_R1)) ec_comb_fill<CURVE_R1>(e, out, w0, w1);
+    else if (ec_key_ok(meta, k, CHIP_SCHEME_K1)) ec_comb_fill<CURVE_K1>(e, out, w0, w1);
+}
+
+// hand-off between the kernels, SoA by list position: acc X/Y/Z (24 words), u2 (8), r (8), state (1).
+// Before k_ecdsa_comb_g the X slots hold e, the Y slots s R and the Z slots s^-1 R.
+#define EC_MID_WORDS 41
+
+CHIP_DEV void mid_store(uint32_t* mid, uint64_t cap, uint32_t gid, int slot, const u256& v) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) mid[(uint64_t)(slot + k) * cap + gid] = v.w[k];
+}
+CHIP_DEV void mid_load(u256& v, const uint32_t* mid, uint64_t cap, uint32_t gid, int slot) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) v.w[k] = mid[(uint64_t)(slot + k) * cap + gid];
+}
+
+// DER, range checks, e = SHA-256(M), s R (Montgomery form mod n)
+template <int C>
+__global__ void __launch_bounds__(256) k_ecdsa_comb_pre(const uint32_t* __restrict__ list,
+                                                        const uint32_t* __restrict__ count,
+                                                        const uint32_t* __restrict__ msg_idx,
+                                                        const uint8_t* __restrict__ sig_data,
+                                                        const uint64_t* __restrict__ sig_off,
+                                                        const uint32_t* __restrict__ sig_len,
+                                                        const uint8_t* __restrict__ msg_data,
+                                                        const uint64_t* __restrict__ msg_off,
+                                                        const uint32_t* __restrict__ msg_len, uint32_t* __restrict__ mid,
+                                                        uint64_t cap, uint8_t* __restrict__ status) {
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= *count) return;
+    const uint32_t i = list[gid];
+    const ec_curve_c& cv = curve<C>();
+    uint32_t* st_word = mid + (uint64_t)40 * cap + gid;
+    u256 r, s;
+    bool roor, soor;
+    if (!der_decode(sig_data + sig_off[i], sig_len[i], r, roor, s, soor)) {
+        status[i] = CHIP_SIG_DECODE;
+        *st_word = 0;
+        return;
+    }
+    if (roor || soor || u256_is_zero(r) || u256_is_zero(s) || u256_ge(r, cv.n) || u256_ge(s, cv.n)) {
+        status[i] = CHIP_INVALID;
+        *st_word = 0;
+        return;
+    }
+    const uint32_t mi = msg_idx[i];
+    uint32_t H[8];
+    sha256_bytes(H, msg_data + msg_off[mi], msg_len[mi]);
+    u256 e;
+#pragma unroll
+    for (int k = 0; k < 8; k++) e.w[k] = H[7 - k];
+    {
+        u256 t;
+        if (!u256_sub(t, e, cv.n)) e = t;
+    }
+    u256 r2n, sm;
+    u256_from_c(r2n, cv.r2_n);
+    mn_mul<C>(sm, s, r2n);
+    mid_store(mid, cap, gid, 0, e);
+    mid_store(mid, cap, gid, 8, sm);
+    mid_store(mid, cap, gid, 32, r);
+    *st_word = 1;
+}
+
+// s^-1 R for EC_INV_BATCH signatures per lane: prefix products of s R (parked in the Z slots), one
+// Fermat inversion of the product, then back to front.  Rejected signatures count as 1.  Lane l of a
+// wave takes positions base + j 64 + l, so every step is a coalesced row.
+template <int C>
+__global__ void __launch_bounds__(64) k_ecdsa_comb_inv(const uint32_t* __restrict__ count, uint32_t* __restrict__ mid,
+                                                       uint64_t cap) {
+    const uint32_t n = *count;
+    const uint32_t base = blockIdx.x * 64u * EC_INV_BATCH + threadIdx.x;
+    if (base >= n) return;
+    const ec_curve_c& cv = curve<C>();
+    u256 acc, sm;
+    u256_from_c(acc, cv.one_n);
+    for (int j = 0; j < EC_INV_BATCH; j++) {
+        const uint32_t gid = base + 64u * j;
+        if (gid >= n) break;
+        if (!mid[(uint64_t)40 * cap + gid]) continue;
+        mid_store(mid, cap, gid, 16, acc);
+        mid_load(sm, mid, cap, gid, 8);
+        mn_mul<C>(acc, acc, sm);
+    }
+    mn_pow<C>(acc, acc, cv.n_minus_2);
+    for (int j = EC_INV_BATCH - 1; j >= 0; j--) {
+        const uint32_t gid = base + 64u * j;
+        if (gid >= n || !mid[(uint64_t)40 * cap + gid]) continue;
+        u256 pre, w;
+        mid_load(pre, mid, cap, gid, 16);
+        mid_load(sm, mid, cap, gid, 8);
+        mn_mul<C>(w, acc, pre);
+        mn_mul<C>(acc, acc, sm);
+        mid_store(mid, cap, gid, 16, w);
+    }
+}
+
+// u1 = e s^-1, u2 = r s^-1 and u1 G from the fixed comb
+template <int C>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k_ecdsa_comb_g(const uint32_t* __restrict__ count, uint32_t* __restrict__ mid,
+                                                      uint64_t cap) {
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= *count || !mid[(uint64_t)40 * cap + gid]) return;
+    u256 e, r, wm, u1, u2;
+    mid_load(e, mid, cap, gid, 0);
+    mid_load(wm, mid, cap, gid, 16);
+    mid_load(r, mid, cap, gid, 32);
+    mn_mul<C>(u1, e, wm);
+    mn_mul<C>(u2, r, wm);
+    uint32_t dg[8];
+    const uint32_t cg = recode<8>(dg, u1);
+    jpt acc;
+#pragma unroll
+    for (int k = 0; k < 8; k++) acc.X.w[k] = acc.Y.w[k] = acc.Z.w[k] = 0;
+    const uint32_t* G = (C == CURVE_R1) ? EC_R1_G_COMB : EC_K1_G_COMB;
+    apt ga;
+#pragma unroll 1
+    for (int wd = 0; wd < 8; wd++) {
+        const uint32_t cur = dg[wd];
+#pragma unroll 1
+        for (int q = 0; q < 4; q++) {
+            const int d = (int)((cur >> (8 * q)) & 255u) - 128;
+            if (!d) continue;
+            const uint32_t w = (uint32_t)(wd * 4 + q);
+            load_apt(ga, G + (w * EC_COMB_GENT + (uint32_t)(d < 0 ? -d : d)) * 16);
+            add_digit<C>(acc, ga, d);
+        }
+    }
+    if (cg) {
+        load_apt(ga, G + (32u * EC_COMB_GENT + 1u) * 16);
+        add_digit<C>(acc, ga, 1);
+    }
+    mid_store(mid, cap, gid, 0, acc.X);
+    mid_store(mid, cap, gid, 8, acc.Y);
+    mid_store(mid, cap, gid, 16, acc.Z);
+    mid_store(mid, cap, gid, 24, u2);
+}
+
+// u2 Q half: one mixed addition per non-zero radix-16 digit from the key's affine table, then
+// x(R) mod n == r exactly as k_ecdsa_verify checks it
+template <int C>
+__global__ void __launch_bounds__(256) k_ecdsa_comb_q(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
+                                                      const uint32_t* __restrict__ key_idx,
+                                                      const uint32_t* __restrict__ ctab, const uint32_t* __restrict__ mid,
+                                                      uint64_t cap, uint8_t* __restrict__ status) {
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if (gid >= *count || !mid[(uint64_t)40 * cap + gid]) return;
+    const uint32_t i = list[gid];
+    const ec_curve_c& cv = curve<C>();
+    jpt acc;
+    apt ent;
+    u256 u2, r;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        acc.X.w[k] = mid[(uint64_t)k * cap + gid];
+        acc.Y.w[k] = mid[(uint64_t)(8 + k) * cap + gid];
+        acc.Z.w[k] = mid[(uint64_t)(16 + k) * cap + gid];
+        u2.w[k] = mid[(uint64_t)(24 + k) * cap + gid];
+        r.w[k] = mid[(uint64_t)(32 + k) * cap + gid];
+    }
+    uint32_t dq[8];
+    const uint32_t cq = recode<4>(dq, u2);
+    const uint32_t* qt = ctab + (uint64_t)key_idx[i] * EC_COMB_KEY_WORDS;
+#pragma unroll 1
+    for (int wd = 0; wd < 8; wd++) {
+        const uint32_t cur = dq[wd];
+#pragma unroll 1
+        for (int q = 0; q < 8; q++) {
+            const int d = (int)((cur >> (4 * q)) & 15u) - 8;
+            if (!d) continue;
+            const uint32_t w = (uint32_t)(wd * 8 + q);
+            load_apt(ent, qt + (w * EC_COMB_QENT + (uint32_t)(d < 0 ? -d : d) - 1) * 16);
+            add_digit<C>(acc, ent, d);
+        }
+    }
+    if (cq) {
+        load_apt(ent, qt + (64u * EC_COMB_QENT) * 16);
+        add_digit<C>(acc, ent, 1);
+    }
+    if (u256_is_zero(acc.Z)) {
+        status[i] = CHIP_INVALID;
+        return;
+    }
+    u256 z2, t;
+    fp_sqr<C>(z2, acc.Z);
+    fp_mul<C>(t, r, z2);
+    bool ok = u256_eq(t, acc.X);
+    if (!ok) {
+        u256 rn;
+        const uint32_t c = u256_add(rn, r, cv.n);
+        if (!c && !u256_ge(rn, cv.p)) {
+            fp_mul<C>(t, rn, z2);
+            ok = u256_eq(t, acc.X);
+        }
+    }
+    status[i] = ok ? CHIP_VALID : CHIP_INVALID;
+}
+
+uint64_t ecdsa_comb_key_words() { return EC_COMB_KEY_WORDS + EC_COMB_JAC_WORDS; }
+
+void launch_ecdsa_comb_build(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, const uint32_t* ectab,
+                             uint32_t* ctab) {
+    if (!n_keys) return;
+    uint32_t* jac = ctab + n_keys * EC_COMB_KEY_WORDS;
+    hipLaunchKernelGGL(k_ecdsa_comb_chain, dim3((uint32_t)((n_keys + 63) / 64)), dim3(64), 0, st, n_keys, meta, ectab,
+                       jac);
+    hipLaunchKernelGGL(k_ecdsa_comb_fill, dim3((uint32_t)((n_keys * EC_FILL_LANES + 255) / 256)), dim3(256), 0, st, n_keys,
+                       meta, ctab, jac);
+}
+
+uint64_t ecdsa_comb_mid_words() { return EC_MID_WORDS; }
+
+template <int C>
+static void comb_pre(hipStream_t st, uint64_t n, const uint32_t* list, const uint32_t* count, const chip_sig_batch* b,
+                     uint32_t* mid, uint8_t* status) {
+    hipLaunchKernelGGL(k_ecdsa_comb_pre<C>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, list, count,
+                       b->msg_idx, b->sig_data, b->sig_off, b->sig_len, b->msg_data, b->msg_off, b->msg_len, mid,
+                       (uint64_t)n, status);
+    hipLaunchKernelGGL(k_ecdsa_comb_inv<C>, dim3((uint32_t)((n + 64 * EC_INV_BATCH - 1) / (64 * EC_INV_BATCH))), dim3(64),
+                       0, st, count, mid, (uint64_t)n);
+    hipLaunchKernelGGL(k_ecdsa_comb_g<C>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, count, mid, (uint64_t)n);
+}
+
+void launch_ecdsa_comb_pre(hipStream_t st, int scheme, uint64_t n, const uint32_t* list, const uint32_t* count,
+                           const chip_sig_batch* b, uint32_t* mid, uint8_t* status) {
+    if (!n) return;
+    if (scheme == CHIP_SCHEME_R1) comb_pre<CURVE_R1>(st, n, list, count, b, mid, status);
+    else comb_pre<CURVE_K1>(st, n, list, count, b, mid, status);
+}
+void launch_ecdsa_comb_q(hipStream_t st, int scheme, uint64_t n, const uint32_t* list, const uint32_t* count,
+                         const chip_sig_batch* b, const uint32_t* ctab, const uint32_t* mid, uint8_t* status) {
+    if (!n) return;
+    const uint32_t blocks = (uint32_t)((n + 255) / 256);
+    if (scheme == CHIP_SCHEME_R1)
+        hipLaunchKernelGGL(k_ecdsa_comb_q<CURVE_R1>, dim3(blocks), dim3(256), 0, st, list, count, b->key_idx, ctab, mid,
+                           (uint64_t)n, status);
+    else
+        hipLaunchKernelGGL(k_ecdsa_comb_q<CURVE_K1>, dim3(blocks), dim3(256), 0, st, list, count, b->key_idx, ctab, mid,
+                           (uint64_t)n, status);
+}

@@ -43,14 +43,14 @@ struct chip_ctx {
     uint64_t comb_budget = 8ull << 30;            // bytes of per-key comb tables
     hipStream_t stream = nullptr;
     hipStream_t aux = nullptr;                    // second stream: per-key comb tables
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fork2 = nullptr, ev_join2 = nullptr;
     std::mutex mu;
     std::string err;
     // verify workspaces
     DevBuf meta, abytes, edtab, ectab, lists, counts;
     // Ed25519 comb path
     DevBuf c_key_count, c_key_slot, c_key_base, c_key_cur, c_slot_key, c_ctr, c_comb_list, c_straus_list, c_ctab,
-        c_xyz, c_zpre, c_nega;
+        c_xyz, c_zpre, c_nega, e_ctab, e_mid;
     // host-path mirrors of the caller's buffers
     DevBuf h_key_idx, h_msg_idx, h_sig_data, h_sig_off, h_sig_len, h_key_data, h_key_off, h_key_len, h_msg_data,
         h_msg_off, h_msg_len, h_status, h_bitmap;
@@ -255,7 +255,9 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
         hipEventCreate(&c->tev0) != hipSuccess || hipEventCreate(&c->tev1) != hipSuccess ||
         hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_fork2, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return CHIP_E_DEVICE;
     }
@@ -276,7 +278,7 @@ void chip_shutdown(chip_ctx* c) {
     hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->meta, &c->abytes, &c->edtab, &c->ectab, &c->lists, &c->counts, &c->c_key_count,
                       &c->c_key_slot, &c->c_key_base, &c->c_key_cur, &c->c_slot_key, &c->c_ctr, &c->c_comb_list,
-                      &c->c_straus_list, &c->c_ctab, &c->c_xyz, &c->c_zpre, &c->c_nega, &c->h_key_idx, &c->h_msg_idx,
+                      &c->c_straus_list, &c->c_ctab, &c->c_xyz, &c->c_zpre, &c->c_nega, &c->e_ctab, &c->e_mid, &c->h_key_idx, &c->h_msg_idx,
                       &c->h_sig_data, &c->h_sig_off, &c->h_sig_len, &c->h_key_data, &c->h_key_off, &c->h_key_len,
                       &c->h_msg_data, &c->h_msg_off, &c->h_msg_len, &c->h_status, &c->h_bitmap, &c->t_salts,
                       &c->t_start, &c->t_group, &c->t_internal, &c->t_data, &c->t_off, &c->t_len, &c->t_ids,
@@ -296,6 +298,8 @@ void chip_shutdown(chip_ctx* c) {
     hipStreamSynchronize(c->aux);
     hipEventDestroy(c->ev_fork);
     hipEventDestroy(c->ev_join);
+    hipEventDestroy(c->ev_fork2);
+    hipEventDestroy(c->ev_join2);
     hipStreamDestroy(c->aux);
     hipStreamDestroy(c->stream);
     delete c;
@@ -353,6 +357,14 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         w.max_slots = (uint32_t)slots;
         w.min_sigs = c->comb_min_sigs;
     }
+    // ECDSA per-key comb tables for every EC key when keys sign many signatures (slot = key index)
+    const uint64_t ec_key_bytes = ecdsa_comb_key_words() * 4;
+    const bool ec_comb = !(c->flags & CHIP_FLAG_NO_COMB) && n && nk && nk * ec_key_bytes <= c->comb_budget &&
+                         (n >= 16 * nk || (c->flags & CHIP_FLAG_FORCE_COMB));
+    if (ec_comb) {
+        HIPCHK(c, c->e_ctab.ensure(nk * ec_key_bytes + 16));
+        HIPCHK(c, c->e_mid.ensure(2 * n * ecdsa_comb_mid_words() * 4 + 16));
+    }
     HIPCHK(c, hipEventRecord(c->ev0, st));
     HIPCHK(c, hipMemsetAsync(c->counts.p, 0, 64, st));
     if (nk) HIPCHK(c, hipMemsetAsync(c->meta.p, 0, nk * sizeof(KeyMeta), st));
@@ -376,6 +388,14 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
     }
     launch_ecdsa_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->ectab.as<uint32_t>());
+    if (ec_comb) {
+        HIPCHK(c, hipEventRecord(c->ev_fork2, st));
+        HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork2, 0));
+        const int kt = c->kbegin(CHIP_K_EC_TABLES, c->aux);
+        launch_ecdsa_comb_build(c->aux, nk, meta, c->ectab.as<uint32_t>(), c->e_ctab.as<uint32_t>());
+        c->kend(kt, c->aux);
+        HIPCHK(c, hipEventRecord(c->ev_join2, c->aux));
+    }
     c->kend(ke, st);
     if (n) {
         const uint32_t blocks = (uint32_t)((n + 255) / 256);
@@ -409,14 +429,34 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         ke = c->kbegin(CHIP_K_ED25519, st);
         launch_ed25519_verify(st, n, ed_list, ed_count, b, c->abytes.as<uint32_t>(), c->edtab.as<uint32_t>(), status);
         c->kend(ke, st);
-        ke = c->kbegin(CHIP_K_ECDSA_R1, st);
-        launch_ecdsa_verify(st, CHIP_SCHEME_R1, n, lists + (uint64_t)LIST_R1 * n, counts + LIST_R1, b,
-                            c->ectab.as<uint32_t>(), status);
-        c->kend(ke, st);
-        ke = c->kbegin(CHIP_K_ECDSA_K1, st);
-        launch_ecdsa_verify(st, CHIP_SCHEME_K1, n, lists + (uint64_t)LIST_K1 * n, counts + LIST_K1, b,
-                            c->ectab.as<uint32_t>(), status);
-        c->kend(ke, st);
+        if (ec_comb) {
+            // table-free halves first (overlap the per-key table build on the aux stream), then the
+            // u2 Q halves once the tables are there
+            uint32_t* mid_r1 = c->e_mid.as<uint32_t>();
+            uint32_t* mid_k1 = mid_r1 + n * ecdsa_comb_mid_words();
+            ke = c->kbegin(CHIP_K_ECDSA_R1, st);
+            launch_ecdsa_comb_pre(st, CHIP_SCHEME_R1, n, lists + (uint64_t)LIST_R1 * n, counts + LIST_R1, b, mid_r1,
+                                  status);
+            launch_ecdsa_comb_pre(st, CHIP_SCHEME_K1, n, lists + (uint64_t)LIST_K1 * n, counts + LIST_K1, b, mid_k1,
+                                  status);
+            HIPCHK(c, hipStreamWaitEvent(st, c->ev_join2, 0));
+            launch_ecdsa_comb_q(st, CHIP_SCHEME_R1, n, lists + (uint64_t)LIST_R1 * n, counts + LIST_R1, b,
+                                c->e_ctab.as<uint32_t>(), mid_r1, status);
+            c->kend(ke, st);
+            ke = c->kbegin(CHIP_K_ECDSA_K1, st);
+            launch_ecdsa_comb_q(st, CHIP_SCHEME_K1, n, lists + (uint64_t)LIST_K1 * n, counts + LIST_K1, b,
+                                c->e_ctab.as<uint32_t>(), mid_k1, status);
+            c->kend(ke, st);
+        } else {
+            ke = c->kbegin(CHIP_K_ECDSA_R1, st);
+            launch_ecdsa_verify(st, CHIP_SCHEME_R1, n, lists + (uint64_t)LIST_R1 * n, counts + LIST_R1, b,
+                                c->ectab.as<uint32_t>(), status);
+            c->kend(ke, st);
+            ke = c->kbegin(CHIP_K_ECDSA_K1, st);
+            launch_ecdsa_verify(st, CHIP_SCHEME_K1, n, lists + (uint64_t)LIST_K1 * n, counts + LIST_K1, b,
+                                c->ectab.as<uint32_t>(), status);
+            c->kend(ke, st);
+        }
         if (bitmap) hipLaunchKernelGGL(k_bitmap, dim3(blocks), dim3(256), 0, st, n, status, bitmap);
     }
     HIPCHK(c, hipGetLastError());

@@ -17,6 +17,17 @@ void launch_ecdsa_key_prep(hipStream_t st, uint64_t n_keys, const uint8_t* key_d
 void launch_ecdsa_verify(hipStream_t st, int scheme, uint64_t n, const uint32_t* list, const uint32_t* count,
                          const chip_sig_batch* b, const uint32_t* ectab, uint8_t* status);
 
+// ECDSA per-key comb path (ecdsa.hip): tables of 2^(4w) {1..8} Q per key (slot = key index)
+uint64_t ecdsa_comb_key_words();
+void launch_ecdsa_comb_build(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, const uint32_t* ectab,
+                             uint32_t* ctab);
+uint64_t ecdsa_comb_mid_words();
+// table-free half (DER, SHA-256, s^-1, u1 G) and the u2 Q half of the comb verify
+void launch_ecdsa_comb_pre(hipStream_t st, int scheme, uint64_t n, const uint32_t* list, const uint32_t* count,
+                           const chip_sig_batch* b, uint32_t* mid, uint8_t* status);
+void launch_ecdsa_comb_q(hipStream_t st, int scheme, uint64_t n, const uint32_t* list, const uint32_t* count,
+                         const chip_sig_batch* b, const uint32_t* ctab, const uint32_t* mid, uint8_t* status);
+
 void launch_txid(hipStream_t st, const chip_tx_batch* b, uint8_t* ids, uint32_t* scratch, uint64_t scratch_words);
 uint64_t ftx_scratch_words(uint64_t ntx);
 void launch_ftx_verify(hipStream_t st, const chip_ftx_batch* b, uint8_t* status, uint8_t* reason, uint32_t* scratch);

@@ -112,7 +112,7 @@ class ChipConflict(ctypes.Structure):
                 ("pad", ctypes.c_uint32)]
 
 
-(K_ED25519, K_ECDSA_R1, K_ECDSA_K1, K_TXID, K_KEYPREP, K_UNIQ, K_ED_COMB, K_ED_FINISH, K_ED_TABLES, _K_UNUSED9,
+(K_ED25519, K_ECDSA_R1, K_ECDSA_K1, K_TXID, K_KEYPREP, K_UNIQ, K_ED_COMB, K_ED_FINISH, K_ED_TABLES, K_EC_TABLES,
  K_ED_PLAN) = range(11)
 N_KERNELS = 11
 FLAG_NO_COMB, FLAG_FORCE_COMB = 0x1, 0x2

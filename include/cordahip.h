@@ -316,12 +316,12 @@ int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_st
 
 /* ---------------------------------------------------------------------------------------
  * Counters (observability; OutOfProcessTransactionVerifierService.kt:35-46 analogue). */
-/* CHIP_K_ED_COMB = k_ed_comb_verify, CHIP_K_ED_TABLES = per-key comb table build (on the context's
- * second stream when every key gets a table), CHIP_K_ED_PLAN = slot assignment + key-grouped work
- * list; kind 9 is unused */
+/* CHIP_K_ED_COMB = k_ed_comb_verify, CHIP_K_ED_TABLES / CHIP_K_EC_TABLES = per-key comb table builds
+ * (on the context's second stream when every key gets a table), CHIP_K_ED_PLAN = slot assignment +
+ * key-grouped work list; CHIP_K_ECDSA_R1/K1 time whichever ECDSA kernel ran (comb or windowed) */
 enum chip_kernel { CHIP_K_ED25519 = 0, CHIP_K_ECDSA_R1 = 1, CHIP_K_ECDSA_K1 = 2, CHIP_K_TXID = 3,
                    CHIP_K_KEYPREP = 4, CHIP_K_UNIQ = 5, CHIP_K_ED_COMB = 6, CHIP_K_ED_FINISH = 7,
-                   CHIP_K_ED_TABLES = 8, CHIP_K_ED_PLAN = 10, CHIP_N_KERNELS = 11 };
+                   CHIP_K_ED_TABLES = 8, CHIP_K_EC_TABLES = 9, CHIP_K_ED_PLAN = 10, CHIP_N_KERNELS = 11 };
 typedef struct {
     uint64_t batches, sigs, keys_prepared;
     uint64_t status_count[8];

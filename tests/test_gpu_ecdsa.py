@@ -9,7 +9,14 @@ import golden_cases
 pytestmark = pytest.mark.gpu
 
 
-def test_ecdsa_golden(ctx, oracle):
+MODES = ["default", "comb", "straus"]
+
+
+@pytest.mark.parametrize("mode", MODES)
+def test_ecdsa_golden(ctx_modes, oracle, mode):
+    """Every schedule (per-key comb tables / windowed) gives the golden statuses, incl. the
+    exceptional-point and r + n cases."""
+    ctx = ctx_modes[mode]
     b = golden_cases.ecdsa_edge_batch()
     st, _ = ctx.verify_batch(b)
     labels = [c["label"] for c in golden_cases.ecdsa_cases()]
@@ -18,7 +25,9 @@ def test_ecdsa_golden(ctx, oracle):
     assert np.array_equal(st, oracle.verify_batch(b))
 
 
-def test_ecdsa_mixed_batch_matches_oracle(ctx, oracle):
+@pytest.mark.parametrize("mode", MODES)
+def test_ecdsa_mixed_batch_matches_oracle(ctx_modes, oracle, mode):
+    ctx = ctx_modes[mode]
     b = G.ecdsa_batch(4000, n_keys=64, corrupt=0.4, seed=17)
     st, bm = ctx.verify_batch(b)
     ref = oracle.verify_batch(b, threads=8)
@@ -34,3 +43,16 @@ def test_mixed_ed25519_and_ecdsa_one_batch(ctx, oracle):
     st, _ = ctx.verify_batch(b)
     assert np.array_equal(st, b.expected)
     assert np.array_equal(st, oracle.verify_batch(b))
+
+
+def test_ecdsa_comb_stats_and_large_batch(ctx_modes):
+    """Default policy: a batch with many signatures per key takes the per-key comb kernels (table
+    build observable in the stats); 60k signatures, every corruption class, labels reproduced."""
+    from corda_amd import native
+    c = ctx_modes["default"]
+    c.reset_stats()
+    b = G.ecdsa_batch(60000, n_keys=256, corrupt=0.1, seed=23)
+    st, _ = c.verify_batch(b)
+    assert np.array_equal(st, b.expected)
+    s = c.stats()
+    assert s.kernel_launches[native.K_EC_TABLES] >= 1
