@@ -47,7 +47,7 @@ ED_COMB_MACS_PER_VERIFY = 73_500
 TXID_OPS_PER_COMPRESSION = 1_676
 # HBM traffic per launch comes from the committed PMC passes of the same command (tools/profile.sh):
 # FETCH_SIZE + WRITE_SIZE (KiB) of the launch with the same grid
-PROFILE_DIR = os.path.join(ROOT, "profiles", "r01c")
+PROFILE_DIR = os.path.join(ROOT, "profiles", "r01d")
 # VALU issue peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6e12 lane-ops/s (= FP32 vector 157.3 TFLOPS / 2,
 # MI355X_MICROARCH.md chip table).  v_mad_u64_u32 issues at a quarter of that: 19.66e12 MACs/s
 # (tools/microbench_mul.hip measures 18.0e12 including a dependent xor per MAC).
