@@ -124,6 +124,12 @@ def max_over_ranks(x, world, torch, dev, dist):
     return float(e.item())
 
 
+def kernel_base(name):
+    """'void k_foo<1>(unsigned int const*, ...)' -> 'k_foo<1>' (rocprofv3 CSVs carry full signatures)."""
+    name = name.split("(", 1)[0].strip()
+    return name[5:] if name.startswith("void ") else name
+
+
 def profile_traffic(kernel, grid):
     """HBM bytes of one launch of `kernel` with `grid` threads from the committed rocprofv3 PMC
     passes (FETCH_SIZE + WRITE_SIZE, KiB), or None when the profile has no such launch.  FETCH_SIZE is
@@ -135,7 +141,7 @@ def profile_traffic(kernel, grid):
         if not os.path.exists(path):
             return None
         vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-                if r["Kernel_Name"] == kernel and int(r["Grid_Size"]) == grid and r["Counter_Name"] == ctr]
+                if kernel_base(r["Kernel_Name"]) == kernel and int(r["Grid_Size"]) == grid and r["Counter_Name"] == ctr]
         if not vals:
             return None
         tot += sum(vals) / len(vals) * 1024.0
