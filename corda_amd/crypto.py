@@ -25,6 +25,7 @@ from typing import Callable, Dict, Iterable, List, Optional, Sequence, Set, Tupl
 import numpy as np
 
 from .native import (VALID, INVALID, SIG_DECODE, EMPTY_SIG, EMPTY_CLEAR, UNSUPPORTED, KEY_INVALID)
+from .composite import CompositeKey, as_key, is_fulfilled_by
 
 
 # ---- exceptions (java.security / IllegalArgumentException / Corda exceptions) ----
@@ -251,9 +252,10 @@ class SignedTransaction:
                 _raise_for(int(st), s.by)
 
     def get_missing_signers(self) -> Set[bytes]:
-        """TransactionWithSignatures.kt:79-85 (plain keys: isFulfilledBy is set membership)."""
-        sig_keys = {s.by for s in self.sigs}
-        return {k for k in self.required_signing_keys if k not in sig_keys}
+        """TransactionWithSignatures.kt:79-85: required keys not fulfilled by the signers' keys (set
+        membership for a plain key; weighted thresholds for a CompositeKey, corda_amd.composite)."""
+        sig_keys = [s.by for s in self.sigs]
+        return {k for k in self.required_signing_keys if not is_fulfilled_by(k, sig_keys)}
 
     def verify_signatures_except(self, engine, *allowed_to_be_missing: bytes):
         """TransactionWithSignatures.kt:44-50."""
@@ -266,8 +268,33 @@ class SignedTransaction:
     def _check_missing(self, allowed):
         needed = self.get_missing_signers() - set(allowed)
         if needed:
-            desc = sorted(self.key_descriptions.get(k, k.hex()[-16:]) for k in needed)
+            desc = sorted(self.key_descriptions.get(k, _short(k)) for k in needed)
             raise SignaturesMissingException(needed, desc, self.id)
+
+
+def _short(k) -> str:
+    return ("composite:" + k.encoded.hex()[-16:]) if isinstance(k, CompositeKey) else k.hex()[-16:]
+
+
+def composite_signature_verify(engine, verify_key, sigs: Sequence[TransactionSignature], clear_data: bytes,
+                               serializer: Serializer = signable_data_bytes) -> bool:
+    """CompositeSignature.State.engineVerify (CompositeSignature.kt:78-86): the composite key must be
+    fulfilled by the signers, then every component signature must be valid over SHA256(clear_data) as
+    a transaction id (TransactionSignature.isValid) — all of them in one engine call."""
+    import hashlib
+    key = as_key(verify_key)
+    if not isinstance(key, CompositeKey):
+        raise IllegalArgumentException("verify key is not a CompositeKey")
+    if not key.is_fulfilled_by([s.by for s in sigs]):
+        return False
+    tx_id = hashlib.sha256(clear_data).digest()
+    items = [(s.by, s.bytes, serializer(tx_id, s.signature_metadata)) for s in sigs]
+    for st, s in zip(verify_statuses(engine, items), sigs):
+        if st == INVALID:      # isValid: false; decode / argument failures throw as Crypto.isValid does
+            return False
+        if st != VALID:
+            _raise_for(int(st), s.by)
+    return True
 
 
 def verify_signatures_except_batch(engine, txs: Sequence[SignedTransaction],

@@ -42,3 +42,31 @@ def test_uniqueness_mirror_on_gpu(ctx):
         C.commit_input_states(p, [a], h("tx3"), 7)
     p.commit([b], h("tx4"), 9)
     assert p.size() == 2
+
+
+def test_composite_keys_on_gpu(ctx):
+    """CompositeKey requirements (corda_amd.composite) with the signatures verified by the HIP engine:
+    2-of-3 over Ed25519 leaves, getMissingSigners and CompositeSignature verify; same answers as the
+    oracle engine."""
+    import cordagen as G
+    from cash_workload import entropy_seed
+    from corda_amd.composite import CompositeKey
+    seeds = [entropy_seed(v) for v in (20, 30, 40)]
+    keys = [G.spki_ed25519(G.ed25519_pub(s)) for s in seeds]
+    k = CompositeKey.Builder().add_keys(*keys).build(threshold=2)
+    clear = b"composite on gpu"
+    tx_id = hashlib.sha256(clear).digest()
+    meta = C.SignatureMetadata(1, 4)
+    sigs = [C.TransactionSignature(G.ed25519_sign(s, C.signable_data_bytes(tx_id, meta)), key, meta)
+            for s, key in zip(seeds, keys)]
+    broken = C.TransactionSignature(sigs[0].bytes, keys[1], meta)
+    cases = [[sigs[0]], [sigs[0], sigs[1]], [sigs[1], sigs[2]], [sigs[0], broken], sigs]
+    oracle = OracleEngine()
+    for cs in cases:
+        assert (C.composite_signature_verify(ctx, k, cs, clear)
+                == C.composite_signature_verify(oracle, k, cs, clear))
+    stxs = [C.SignedTransaction(tx_id, cs, [k]) for cs in cases]
+    got = [outcome(e) for e in C.verify_signatures_except_batch(ctx, stxs)]
+    ref = [outcome(e) for e in C.verify_signatures_except_batch(oracle, stxs)]
+    assert got == ref
+    assert [g is None for g in got] == [False, True, True, False, True]
