@@ -432,14 +432,87 @@ class Conflict:
     state_history: List[Tuple[StateRef, ConsumingTx]]
 
 
-class PersistentUniquenessProvider:
-    """UniquenessProvider backed by the GPU commit log (chip_uniq_*)."""
+# notary_commit_log row (PersistentUniquenessProvider.kt:50-53): StateRef (32-B txhash + LE u32 index,
+# the 36-B table key), consuming tx id, consuming input index, requesting party (interned id)
+COMMIT_LOG_DTYPE = np.dtype([("ref", "u1", 36), ("tx", "u1", 32), ("idx", "<u4"), ("caller", "<u4")])
 
-    def __init__(self, engine, capacity: int = 1 << 20):
+
+class CommitLog:
+    """Append-only on-disk commit log of the notary (the role of the `notary_commit_log` table behind
+    AppendOnlyPersistentMap, PersistentUniquenessProvider.kt:50-89): fixed 76-byte rows, appended in
+    commit order after each batch; `load()` memory-maps the file for the table rebuild at open
+    (AppendOnlyPersistentMap.allPersisted).  A torn final row (crash mid-append) is ignored."""
+
+    def __init__(self, path: str, fsync: bool = False):
+        self.path = path
+        self.fsync = fsync
+        self._f = open(path, "ab")
+
+    def load(self) -> np.ndarray:
+        import os
+        n = os.path.getsize(self.path) // COMMIT_LOG_DTYPE.itemsize
+        if n == 0:
+            return np.zeros(0, dtype=COMMIT_LOG_DTYPE)
+        return np.memmap(self.path, dtype=COMMIT_LOG_DTYPE, mode="r", shape=(n,))
+
+    def append(self, rows: np.ndarray):
+        if len(rows):
+            import os
+            self._f.seek(0, os.SEEK_END)
+            size = self._f.tell()
+            torn = size % COMMIT_LOG_DTYPE.itemsize
+            if torn:                        # drop a torn row before appending whole ones
+                self._f.truncate(size - torn)
+            self._f.write(rows.tobytes())
+            self._f.flush()
+            if self.fsync:
+                os.fsync(self._f.fileno())
+
+    def close(self):
+        if self._f:
+            self._f.close()
+            self._f = None
+
+
+class PersistentUniquenessProvider:
+    """UniquenessProvider backed by the GPU commit log (chip_uniq_*).  With `log_path`, committed rows
+    are also appended to an on-disk CommitLog and the table is rebuilt from it at open, so a restarted
+    notary rejects double spends of states committed before the restart."""
+
+    def __init__(self, engine, capacity: int = 1 << 20, log_path: Optional[str] = None, fsync: bool = False):
         self.table = engine.uniq_open(capacity)
+        self.log = None
+        if log_path is not None:
+            self.log = CommitLog(log_path, fsync)
+            rows = self.log.load()
+            if len(rows):
+                self.table.rebuild(np.ascontiguousarray(rows["ref"]).reshape(-1),
+                                   np.ascontiguousarray(rows["tx"]).reshape(-1),
+                                   np.ascontiguousarray(rows["idx"]), np.ascontiguousarray(rows["caller"]))
+            del rows
 
     def size(self) -> int:
         return self.table.size()
+
+    def close(self):
+        if self.log is not None:
+            self.log.close()
+
+    def _log_committed(self, requests, statuses):
+        """Rows of the transactions this batch committed, in batch order; a StateRef repeated inside
+        one transaction keeps its first index (AppendOnlyPersistentMap.set)."""
+        rows = []
+        for (states, tx_id, caller), st in zip(requests, statuses):
+            if st != 0:
+                continue
+            seen = set()
+            for i, sref in enumerate(states):
+                k = sref.key()
+                if k in seen:
+                    continue
+                seen.add(k)
+                rows.append((np.frombuffer(k, np.uint8), np.frombuffer(tx_id, np.uint8), i, caller))
+        self.log.append(np.array(rows, dtype=COMMIT_LOG_DTYPE))
 
     def commit_batch(self, requests: Sequence[Tuple[List[StateRef], bytes, int]]):
         """[(states, txId, callerIdentity)] applied in order -> [(status, Conflict)]; status 0 committed,
@@ -458,6 +531,8 @@ class PersistentUniquenessProvider:
         out = [(int(s), Conflict([])) for s in st]
         for tx, i, ci, cid, cc in recs:
             out[tx][1].state_history.append((requests[tx][0][i], ConsumingTx(cid, ci, cc)))
+        if self.log is not None:
+            self._log_committed(requests, [o[0] for o in out])
         return out
 
     def commit(self, states: List[StateRef], tx_id: bytes, caller_identity: int):

@@ -124,3 +124,10 @@ def test_uniq_sharded_gpu_shards_match_oracle(ctx, oracle, world):
     assert sum(t.size() for t in tables) == o.size()
     for t in tables:
         t.close()
+
+
+def test_commit_log_restart_on_gpu(ctx, tmp_path):
+    """The notary commit log rebuilt into the GPU table at open answers like a provider that never
+    restarted (tests/commit_log_case.py)."""
+    from commit_log_case import run
+    assert run(ctx, tmp_path) > 0
