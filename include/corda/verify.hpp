@@ -66,6 +66,230 @@ struct PublicKey {
     bool operator==(const PublicKey& o) const { return encoded == o.encoded; }
 };
 
+// ---- CompositeKey (CompositeKey.kt:22-270, CryptoUtils.kt:100-112) ----
+// A composite key travels as its DER SubjectPublicKeyInfo (algorithm OID
+// 2.25.30086077608615255153862931087626791002, CordaSecurityProvider.kt:35) holding
+// SEQUENCE { threshold INTEGER, SEQUENCE OF SEQUENCE { BIT STRING child.encoded, INTEGER weight } }
+// with children sorted by (weight, encoded bytes).  Fulfilment is host-side set logic.
+namespace detail {
+inline void der_tlv(Bytes& out, uint8_t tag, const Bytes& body) {
+    out.push_back(tag);
+    const size_t n = body.size();
+    if (n < 0x80) out.push_back((uint8_t)n);
+    else {
+        uint8_t tmp[8];
+        int k = 0;
+        for (size_t v = n; v; v >>= 8) tmp[k++] = (uint8_t)(v & 0xff);
+        out.push_back((uint8_t)(0x80 | k));
+        while (k) out.push_back(tmp[--k]);
+    }
+    out.insert(out.end(), body.begin(), body.end());
+}
+inline Bytes der_int(int64_t v) {   // minimal two's complement
+    Bytes b;
+    for (int i = 7; i >= 0; i--) b.push_back((uint8_t)(((uint64_t)v >> (8 * i)) & 0xff));
+    while (b.size() > 1 && ((b[0] == 0x00 && !(b[1] & 0x80)) || (b[0] == 0xff && (b[1] & 0x80)))) b.erase(b.begin());
+    Bytes out;
+    der_tlv(out, 0x02, b);
+    return out;
+}
+inline const Bytes& composite_oid_tlv() {
+    static const Bytes tlv = [] {
+        // 2.25.30086077608615255153862931087626791002: first byte 2*40+25, then the 125-bit arc in base 128
+        const char* dec = "30086077608615255153862931087626791002";
+        std::vector<uint32_t> num;   // big number, base 2^16 limbs little-endian
+        for (const char* c = dec; *c; c++) {
+            uint32_t carry = (uint32_t)(*c - '0');
+            for (auto& l : num) { const uint32_t v = l * 10 + carry; l = v & 0xffff; carry = v >> 16; }
+            if (carry) num.push_back(carry);
+        }
+        Bytes groups;   // base-128 digits, least significant first
+        while (!num.empty()) {
+            uint32_t rem = 0;
+            for (size_t i = num.size(); i-- > 0;) { const uint32_t v = (rem << 16) | num[i]; num[i] = v >> 7; rem = v & 0x7f; }
+            groups.push_back((uint8_t)rem);
+            while (!num.empty() && num.back() == 0) num.pop_back();
+        }
+        Bytes body{(uint8_t)(2 * 40 + 25)};
+        for (size_t i = groups.size(); i-- > 0;) body.push_back((uint8_t)(groups[i] | (i ? 0x80 : 0)));
+        Bytes out;
+        der_tlv(out, 0x06, body);
+        return out;
+    }();
+    return tlv;
+}
+struct DerReader {
+    const uint8_t* p;
+    size_t n, pos = 0;
+    bool next(uint8_t& tag, const uint8_t*& body, size_t& len) {
+        if (pos + 2 > n) return false;
+        tag = p[pos];
+        size_t l = p[pos + 1];
+        pos += 2;
+        if (l & 0x80) {
+            const size_t k = l & 0x7f;
+            if (k == 0 || k > 4 || pos + k > n) return false;
+            l = 0;
+            for (size_t i = 0; i < k; i++) l = (l << 8) | p[pos + i];
+            pos += k;
+        }
+        if (pos + l > n) return false;
+        body = p + pos;
+        len = l;
+        pos += l;
+        return true;
+    }
+};
+}  // namespace detail
+
+struct CompositeKey {
+    struct Node { PublicKey key; int weight; };
+    int threshold = 0;
+    std::vector<Node> children;   // sorted by (weight, key.encoded)
+
+    static bool isComposite(const PublicKey& k) {
+        detail::DerReader r{k.encoded.data(), k.encoded.size()};
+        uint8_t tag = 0; const uint8_t* body = nullptr; size_t len = 0;
+        if (!r.next(tag, body, len) || tag != 0x30) return false;
+        detail::DerReader s{body, len};
+        if (!s.next(tag, body, len) || tag != 0x30) return false;
+        detail::DerReader a{body, len};
+        const Bytes& oid = detail::composite_oid_tlv();
+        if (!a.next(tag, body, len) || tag != 0x06 || len + 2 != oid.size()) return false;
+        return std::memcmp(body, oid.data() + 2, len) == 0;
+    }
+    // CompositeKey.getInstance (CompositeKey.kt:28-46) + checkConstraints (:60-72)
+    static CompositeKey decode(const PublicKey& k) {
+        if (!isComposite(k)) throw IllegalArgumentException("not a composite key");
+        auto bad = [] { return IllegalArgumentException("malformed CompositeKey encoding"); };
+        detail::DerReader r{k.encoded.data(), k.encoded.size()};
+        uint8_t tag = 0; const uint8_t* body = nullptr; size_t len = 0;
+        r.next(tag, body, len);
+        detail::DerReader spki{body, len};
+        spki.next(tag, body, len);   // algorithm
+        if (!spki.next(tag, body, len) || tag != 0x03 || len < 1 || body[0] != 0) throw bad();
+        detail::DerReader bits{body + 1, len - 1};
+        if (!bits.next(tag, body, len) || tag != 0x30) throw bad();
+        detail::DerReader seq{body, len};
+        CompositeKey ck;
+        if (!seq.next(tag, body, len) || tag != 0x02 || len == 0 || len > 4) throw bad();
+        int64_t t = (body[0] & 0x80) ? -1 : 0;
+        for (size_t i = 0; i < len; i++) t = (t << 8) | body[i];
+        ck.threshold = (int)t;
+        if (!seq.next(tag, body, len) || tag != 0x30) throw bad();
+        detail::DerReader kids{body, len};
+        while (kids.pos < kids.n) {
+            if (!kids.next(tag, body, len) || tag != 0x30) throw bad();
+            detail::DerReader kid{body, len};
+            if (!kid.next(tag, body, len) || tag != 0x03 || len < 1 || body[0] != 0) throw bad();
+            PublicKey child{Bytes(body + 1, body + len)};
+            if (!kid.next(tag, body, len) || tag != 0x02 || len == 0 || len > 4) throw bad();
+            int64_t w = (body[0] & 0x80) ? -1 : 0;
+            for (size_t i = 0; i < len; i++) w = (w << 8) | body[i];
+            if (w <= 0) throw IllegalArgumentException("A non-positive weight was detected.");
+            ck.children.push_back({std::move(child), (int)w});
+        }
+        ck.checkConstraints();
+        return ck;
+    }
+    void checkConstraints() const {
+        for (size_t i = 0; i < children.size(); i++)
+            for (size_t j = i + 1; j < children.size(); j++)
+                if (children[i].weight == children[j].weight && children[i].key == children[j].key)
+                    throw IllegalArgumentException("CompositeKey with duplicated child nodes detected.");
+        if (children.size() <= 1) throw IllegalArgumentException("CompositeKey must consist of two or more child nodes.");
+        if (threshold <= 0) throw IllegalArgumentException("CompositeKey threshold should be a positive integer.");
+        int64_t total = 0;
+        for (const auto& c : children) {
+            if (c.weight <= 0) throw IllegalArgumentException("Non-positive weight detected.");
+            total += c.weight;
+            if (total > INT32_MAX) throw std::overflow_error("integer overflow");
+        }
+        if (threshold > total)
+            throw IllegalArgumentException("CompositeKey threshold cannot be bigger than aggregated weight of child nodes");
+    }
+    // CompositeKey.Builder.build (CompositeKey.kt:251-268): a single child is returned unwrapped
+    static PublicKey build(std::vector<Node> nodes, int thr = 0 /* 0: sum of weights */) {
+        for (const auto& c : nodes)
+            if (c.weight <= 0) throw IllegalArgumentException("A non-positive weight was detected.");
+        if (nodes.size() == 1) {
+            if (thr != 0 && thr != nodes[0].weight)
+                throw IllegalArgumentException("Trying to build invalid CompositeKey, threshold value different than "
+                                               "weight of single child node.");
+            return nodes[0].key;
+        }
+        if (nodes.empty()) throw std::logic_error("Trying to build CompositeKey without child nodes.");
+        CompositeKey ck;
+        if (thr == 0) {
+            uint32_t sum = 0;   // Kotlin Int sum wraps
+            for (const auto& c : nodes) sum += (uint32_t)c.weight;
+            ck.threshold = (int32_t)sum;
+        } else {
+            ck.threshold = thr;
+        }
+        std::sort(nodes.begin(), nodes.end(), [](const Node& a, const Node& b) {
+            return a.weight != b.weight ? a.weight < b.weight : a.key.encoded < b.key.encoded;
+        });
+        ck.children = std::move(nodes);
+        ck.checkConstraints();
+        return ck.encoded();
+    }
+    PublicKey encoded() const {   // CompositeKey.kt:161-170
+        Bytes kids;
+        for (const auto& c : children) {
+            Bytes bit{0x00};
+            bit.insert(bit.end(), c.key.encoded.begin(), c.key.encoded.end());
+            Bytes node;
+            detail::der_tlv(node, 0x03, bit);
+            const Bytes w = detail::der_int(c.weight);
+            node.insert(node.end(), w.begin(), w.end());
+            detail::der_tlv(kids, 0x30, node);
+        }
+        Bytes body = detail::der_int(threshold);
+        detail::der_tlv(body, 0x30, kids);
+        Bytes inner;
+        detail::der_tlv(inner, 0x30, body);
+        Bytes bit{0x00};
+        bit.insert(bit.end(), inner.begin(), inner.end());
+        Bytes alg;
+        detail::der_tlv(alg, 0x30, detail::composite_oid_tlv());
+        detail::der_tlv(alg, 0x03, bit);
+        Bytes out;
+        detail::der_tlv(out, 0x30, alg);
+        return PublicKey{out};
+    }
+    static bool encoded_roundtrip_ok(const PublicKey& k) { return decode(k).encoded() == k; }
+    // checkFulfilledBy (CompositeKey.kt:175-185)
+    bool fulfilledBy(const std::set<PublicKey>& keys) const {
+        for (const auto& k : keys)
+            if (isComposite(k)) return false;
+        int64_t total = 0;
+        for (const auto& c : children) {
+            const bool ok = isComposite(c.key) ? decode(c.key).fulfilledBy(keys) : keys.count(c.key) > 0;
+            if (ok) total += c.weight;
+        }
+        return total >= threshold;
+    }
+    // leafKeys (CompositeKey.kt:203-204)
+    std::set<PublicKey> leafKeys() const {
+        std::set<PublicKey> out;
+        for (const auto& c : children) {
+            if (isComposite(c.key)) {
+                const auto sub = decode(c.key).leafKeys();
+                out.insert(sub.begin(), sub.end());
+            } else {
+                out.insert(c.key);
+            }
+        }
+        return out;
+    }
+};
+
+// PublicKey.isFulfilledBy (CryptoUtils.kt:103-105)
+inline bool isFulfilledBy(const PublicKey& key, const std::set<PublicKey>& keys) {
+    return CompositeKey::isComposite(key) ? CompositeKey::decode(key).fulfilledBy(keys) : keys.count(key) > 0;
+}
+
 struct SignatureScheme {
     int schemeNumberID;
     const char* schemeCodeName;
@@ -267,13 +491,14 @@ struct SignedTransaction {
         for (size_t i = 0; i < st.size(); i++)
             if (st[i] != CHIP_VALID) detail::throw_for(st[i], sigs[i].by.encoded);
     }
-    // TransactionWithSignatures.kt:79-85 (plain keys: isFulfilledBy == membership)
+    // TransactionWithSignatures.kt:79-85: required keys not fulfilled by the signers (membership for a
+    // plain key, weighted thresholds for a CompositeKey)
     std::set<PublicKey> getMissingSigners() const {
         std::set<PublicKey> sigKeys;
         for (const auto& s : sigs) sigKeys.insert(s.by);
         std::set<PublicKey> missing;
         for (const auto& k : requiredSigningKeys)
-            if (!sigKeys.count(k)) missing.insert(k);
+            if (!isFulfilledBy(k, sigKeys)) missing.insert(k);
         return missing;
     }
     // TransactionWithSignatures.kt:44-50
