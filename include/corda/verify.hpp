@@ -21,6 +21,7 @@
 #pragma once
 #include <algorithm>
 #include <cstdint>
+#include <cstdio>
 #include <exception>
 #include <cstring>
 #include <functional>
@@ -647,7 +648,42 @@ class PersistentUniquenessProvider {
     PersistentUniquenessProvider(Engine& e, uint64_t capacity = 1 << 20) : e_(e) {
         e_.check(chip_uniq_open(e_.get(), capacity, &u_));
     }
-    ~PersistentUniquenessProvider() { chip_uniq_close(u_); }
+    // With a commit log (the notary_commit_log table's role, PersistentUniquenessProvider.kt:50-89):
+    // the table is rebuilt from the log at open (AppendOnlyPersistentMap.allPersisted) and committed
+    // rows are appended after each batch.  Rows are 76 bytes — StateRef key (32-B txhash, LE u32
+    // index), consuming tx id, LE u32 input index, LE u32 caller — the same file format as
+    // corda_amd.crypto.CommitLog; a torn final row is ignored.
+    PersistentUniquenessProvider(Engine& e, uint64_t capacity, const std::string& logPath)
+        : PersistentUniquenessProvider(e, capacity) {
+        std::vector<uint8_t> raw;
+        if (FILE* f = std::fopen(logPath.c_str(), "rb")) {
+            uint8_t buf[1 << 16];
+            size_t got;
+            while ((got = std::fread(buf, 1, sizeof buf, f)) > 0) raw.insert(raw.end(), buf, buf + got);
+            std::fclose(f);
+        }
+        const size_t n = raw.size() / kLogRow;
+        if (n) {
+            std::vector<uint8_t> refs(n * 36), tx(n * 32);
+            std::vector<uint32_t> idx(n), caller(n);
+            for (size_t i = 0; i < n; i++) {
+                const uint8_t* r = raw.data() + i * kLogRow;
+                std::memcpy(refs.data() + 36 * i, r, 36);
+                std::memcpy(tx.data() + 32 * i, r + 36, 32);
+                idx[i] = le32(r + 68);
+                caller[i] = le32(r + 72);
+            }
+            e_.check(chip_uniq_rebuild(u_, n, refs.data(), tx.data(), idx.data(), caller.data()));
+        }
+        log_ = std::fopen(logPath.c_str(), "r+b");
+        if (!log_) log_ = std::fopen(logPath.c_str(), "w+b");
+        if (!log_) throw std::runtime_error("cannot open commit log " + logPath);
+        std::fseek(log_, (long)(n * kLogRow), SEEK_SET);   // overwrite a torn tail
+    }
+    ~PersistentUniquenessProvider() {
+        if (log_) std::fclose(log_);
+        chip_uniq_close(u_);
+    }
     PersistentUniquenessProvider(const PersistentUniquenessProvider&) = delete;
     PersistentUniquenessProvider& operator=(const PersistentUniquenessProvider&) = delete;
 
@@ -684,6 +720,7 @@ class PersistentUniquenessProvider {
             ct.requestingParty = c.consuming_caller;
             res[c.tx].conflict.stateHistory.emplace_back(reqs[c.tx].states[c.input_index], ct);
         }
+        if (log_) appendLog(reqs, res);
         return res;
     }
     // UniquenessProvider.commit: throws UniquenessException when any input is already committed
@@ -693,8 +730,40 @@ class PersistentUniquenessProvider {
     }
 
   private:
+    static constexpr size_t kLogRow = 76;
+    static uint32_t le32(const uint8_t* p) {
+        return (uint32_t)p[0] | (uint32_t)p[1] << 8 | (uint32_t)p[2] << 16 | (uint32_t)p[3] << 24;
+    }
+    // rows of the committed transactions in batch order; a StateRef repeated inside one transaction
+    // keeps its first index (AppendOnlyPersistentMap.set)
+    void appendLog(const std::vector<Request>& reqs, const std::vector<Outcome>& res) {
+        std::vector<uint8_t> rows;
+        for (size_t t = 0; t < reqs.size(); t++) {
+            if (res[t].status != 0) continue;
+            std::set<std::pair<SecureHash, uint32_t>> seen;
+            for (size_t i = 0; i < reqs[t].states.size(); i++) {
+                const StateRef& s = reqs[t].states[i];
+                if (!seen.insert({s.txhash, s.index}).second) continue;
+                uint8_t r[kLogRow];
+                std::memcpy(r, s.txhash.bytes, 32);
+                const uint32_t vals[3] = {s.index, (uint32_t)i, reqs[t].callerIdentity};
+                for (int b = 0; b < 4; b++) {
+                    r[32 + b] = (uint8_t)(vals[0] >> (8 * b));
+                    r[68 + b] = (uint8_t)(vals[1] >> (8 * b));
+                    r[72 + b] = (uint8_t)(vals[2] >> (8 * b));
+                }
+                std::memcpy(r + 36, reqs[t].txId.bytes, 32);
+                rows.insert(rows.end(), r, r + kLogRow);
+            }
+        }
+        if (!rows.empty()) {
+            if (std::fwrite(rows.data(), 1, rows.size(), log_) != rows.size() || std::fflush(log_) != 0)
+                throw std::runtime_error("commit log write failed");
+        }
+    }
     Engine& e_;
     chip_uniq* u_ = nullptr;
+    FILE* log_ = nullptr;
 };
 
 // TrustedAuthorityNotaryService.commitInputStates (NotaryService.kt:61-75)
