@@ -2,8 +2,9 @@
 // ECDSA_SECP256K1_SHA256 (scheme 2) with BouncyCastle 1.57 semantics as selected by
 // Crypto.isValid (core/.../crypto/Crypto.kt:615-625):
 //   - StdDSAEncoder.decode: exactly one DER SEQUENCE of exactly two INTEGERs, minimal definite
-//     lengths, no trailing bytes (DER re-encoding must equal the input); INTEGER contents kept as
-//     given; empty INTEGER -> exception.  Failure -> CHIP_SIG_DECODE.
+//     lengths, no trailing bytes (DER re-encoding must equal the input); an empty INTEGER or one
+//     ASN1Integer calls malformed (redundant leading 00 / FF byte) -> exception.  Failure ->
+//     CHIP_SIG_DECODE.
 //   - e = SHA-256(M) (256-bit n: no truncation); r, s outside [1, n-1] -> INVALID (negative / zero
 //     DER integers land here); w = s^-1, u1 = e w, u2 = r w mod n; R = u1 G + u2 Q;
 //     R = infinity -> INVALID; accept iff x(R) mod n == r (checked projectively as BC does:
@@ -205,7 +206,9 @@ CHIP_DEV bool der_decode(const uint8_t* sig, uint32_t len, u256& r, bool& roor, 
         if (!der_len(p + 1, rem - 1, h2, l2)) return false;
         if (1 + h2 + l2 > rem) return false;
         if (l2 == 0) return false;
-        val[k] = p + 1 + h2;
+        const uint8_t* c = p + 1 + h2;   // ASN1Integer malformed-integer rule
+        if (l2 > 1 && ((c[0] == 0x00 && !(c[1] & 0x80)) || (c[0] == 0xff && (c[1] & 0x80)))) return false;
+        val[k] = c;
         vl[k] = l2;
         p += 1 + h2 + l2;
         rem -= 1 + h2 + l2;

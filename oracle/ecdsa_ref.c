@@ -6,8 +6,10 @@
  * (SURVEY.md §8a "ECDSA contract"):
  *   - DER: exactly one SEQUENCE of exactly two INTEGERs, definite minimal lengths, DER
  *     re-encoding must equal the input (so no trailing bytes, no long-form short lengths);
- *     INTEGER contents are kept as given (non-minimal padding survives the re-encode check);
- *     empty INTEGER content -> exception.  Any failure -> SignatureException (SIG_DECODE).
+ *     an INTEGER whose content is malformed in ASN1Integer's sense (a redundant leading 00 or FF
+ *     byte) or empty -> exception.  Any failure -> SignatureException (SIG_DECODE).
+ *     (The malformed-INTEGER rule is restated from BC's ASN1Integer.isMalformed; no reference test
+ *     pins it — parity unpinned for that one case.)
  *   - e = SHA-256(M) as a big-endian integer (n is 256 bits: no truncation).
  *   - r or s outside [1, n-1] -> false.  w = s^-1, u1 = e w, u2 = r w (mod n),
  *     R = u1 G + u2 Q; R = infinity -> false; accept iff x(R) mod n == r.  High-s is valid.
@@ -336,6 +338,8 @@ int orc_der_decode(const uint8_t* sig, size_t len, uint8_t r[32], uint8_t s[32],
         if (der_len(p + 1, rem - 1, &h2, &l2)) return -1;
         if (1 + h2 + l2 > rem) return -1;
         if (l2 == 0) return -1;                    /* BigInteger of zero length          */
+        const uint8_t* c = p + 1 + h2;             /* ASN1Integer: malformed integer     */
+        if (l2 > 1 && ((c[0] == 0x00 && !(c[1] & 0x80)) || (c[0] == 0xff && (c[1] & 0x80)))) return -1;
         val[k] = p + 1 + h2;
         vlen[k] = l2;
         p += 1 + h2 + l2;

@@ -387,7 +387,8 @@ def ecdsa_cases():
         rpad = b"\x00\x00" + r.to_bytes(32, "big")
         body = b"\x02" + bytes([len(rpad)]) + rpad + G.der_encode_int(s_)
         cases.append(ec_case("%s DER non-minimal INTEGER padding" % name, spki, b"\x30" + bytes([len(body)]) + body,
-                             msg, 0, "BC 1.57 keeps INTEGER bytes (unpinned: no reference test)", unpinned=True))
+                             msg, 2, "ASN1Integer rejects a malformed (non-minimal) INTEGER -> 'error decoding signature "
+                             "bytes.' (BC 1.57 as restated; unpinned: no reference test)", unpinned=True))
         cases.append(ec_case("%s raw r||s (not DER)" % name, spki, rb + sb, msg, 2, "not DER"))
         cases.append(ec_case("%s empty signature" % name, spki, b"", msg, 3, "Crypto.kt:528"))
         cases.append(ec_case("%s empty clear data" % name, spki, der, b"", 4, "Crypto.kt:529"))

@@ -381,10 +381,10 @@ def ecdsa_batch(n: int, n_keys: int = 4096, msg_len: int = 200, corrupt: float =
             put(i, b"\x30" + bytes([len(body)]) + body); expected[i] = 2
         elif k == 11:  # trailing byte after the SEQUENCE
             put(i, der_sig(r, s) + b"\x00"); expected[i] = 2
-        elif k == 12:  # non-minimal INTEGER padding (BC 1.57 keeps the bytes: unpinned, restated VALID)
+        elif k == 12:  # non-minimal INTEGER padding: ASN1Integer's malformed-integer check (unpinned)
             rb = b"\x00" + r.to_bytes(33, "big")
             body = b"\x02" + bytes([len(rb)]) + rb + der_encode_int(s)
-            put(i, b"\x30" + bytes([len(body)]) + body); expected[i] = 0
+            put(i, b"\x30" + bytes([len(body)]) + body); expected[i] = 2
     b = SigBatch()
     b.key_idx = key_idx
     b.msg_idx = msg_idx.astype(np.uint32)

@@ -31,7 +31,7 @@ __global__ void k_mul_lo_u32(uint64_t* out, uint32_t seed) {
     for (int c = 0; c < CHAINS; c++) acc[c] = seed + c + threadIdx.x;
     for (int i = 0; i < ITERS; i++) {
 #pragma unroll
-        for (int c = 0; c < CHAINS; c++) acc[c] = acc[c] * b;
+        for (int c = 0; c < CHAINS; c++) acc[c] = (acc[c] ^ (uint32_t)i) * b;   // the xor keeps the loop from folding into b^ITERS
     }
     uint32_t s = 0;
 #pragma unroll
