@@ -26,12 +26,14 @@ struct KeyMeta {
 // Wave-level aggregation of per-key counters.  Lanes with `valid` set and equal `key` form a group;
 // every member learns its group's leader lane and its rank inside the group, the leader also the
 // group size.  One atomic per distinct key per wave instead of one per lane: a batch signed by a
-// single notary key would otherwise serialize on one address.  The loop is wave-uniform.
+// single notary key would otherwise serialize on one address.  The loop is wave-uniform.  (Capping
+// it at a few rounds and letting the rest of the lanes use one atomic each measured no faster on
+// the 4,096-key cfg2 batch: the atomics, not the ballot rounds, set the time.)
 CHIP_DEV void wave_group(bool valid, uint32_t key, uint32_t& leader, uint32_t& count, uint32_t& rank) {
     const uint32_t lane = __lane_id();
     uint64_t todo = __ballot(valid);
-    leader = 0;
-    count = 0;
+    leader = lane;
+    count = 1;
     rank = 0;
     while (todo) {
         const uint32_t l = (uint32_t)__builtin_ctzll(todo);

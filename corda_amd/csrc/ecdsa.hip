@@ -9,12 +9,25 @@
 //     DER integers land here); w = s^-1, u1 = e w, u2 = r w mod n; R = u1 G + u2 Q;
 //     R = infinity -> INVALID; accept iff x(R) mod n == r (checked projectively as BC does:
 //     X == r Z^2 or, when r + n < p, X == (r + n) Z^2).  High-s is valid.
-// Schedule (lane-uniform, no divergence except the rare exceptional additions): 4-bit signed
-// windows for u2 from a per-key affine table {1..8}Q built by K2b, 8-bit signed windows for u1
-// from a 129-entry affine G table staged in LDS.
+//
+// Two schedules, identical results:
+//   * windowed (k_ecdsa_verify, keys with few signatures): 4-bit signed windows for u2 from a
+//     per-key affine table {1..8}Q (k_ecdsa_key_table), 8-bit signed windows for u1 from a 129-entry
+//     affine G table staged in LDS; 256 doublings per signature.
+//   * comb (keys that sign many signatures of the batch): no doublings per signature.  Work lists
+//     grouped by key (k_ec_group_*), then
+//       k_ecdsa_comb_pre<C> DER, range checks, e = SHA-256(M), s R and the wavefront-level part of the
+//                           batched s^-1: prefix / suffix products across the 64 lanes (shuffles)
+//       k_ecdsa_comb_inv    one inversion per wave product (binary extended Euclid), both curves
+//       k_ecdsa_comb_g<C>   s^-1 = (wave product)^-1 * prefix * suffix, u1, u2, and u1 G from the
+//                           fixed radix-2^EC_GW comb (built on the device at context start)
+//       k_ecdsa_comb_q<C>   u2 Q from the per-key radix-16 table (65 windows x {1..8}) + the x(R) check
+//     the per-key tables (k_ecdsa_comb_chain / _fill) are built on the context's second stream while
+//     the main stream runs classify, pre, inv and g.
 #include "ec_dev.hpp"
 #include "sha2_dev.hpp"
 #include "runtime.hpp"
+#include <cstdlib>
 
 #define EC_TAB_STRIDE EC_KEY_TABLE_WORDS
 
@@ -41,6 +54,22 @@ CHIP_DEV void load_be256(u256& r, const uint8_t* p) {
     for (int i = 0; i < 8; i++) r.w[7 - i] = ld_be32(p + 4 * i);
 }
 
+// x^3 + a x + b
+template <int C>
+CHIP_DEV void curve_rhs(u256& rhs, const u256& x) {
+    u256 t, b;
+    fp_sqr<C>(rhs, x);
+    fp_mul<C>(rhs, rhs, x);
+    if (EC_CURVE(C) == CURVE_R1) {   // - 3x
+        fp_add<C>(t, x, x);
+        fp_add<C>(t, t, x);
+        fp_sub<C>(rhs, rhs, t);
+    }
+    u256_from_c(b, curve<C>().b);
+    fp_add<C>(rhs, rhs, b);
+}
+
+// BC ECCurve.decodePoint: uncompressed 04||X||Y or compressed 02/03||X, coordinates < p, on the curve
 template <int C>
 CHIP_DEV bool ec_decode_point(apt& q, const uint8_t* pt, uint32_t len) {
     const ec_curve_c& cv = curve<C>();
@@ -51,43 +80,30 @@ CHIP_DEV bool ec_decode_point(apt& q, const uint8_t* pt, uint32_t len) {
     } else if (len == 33 && (pt[0] == 0x02 || pt[0] == 0x03)) {
         load_be256(q.x, pt + 1);
         if (u256_ge(q.x, cv.p)) return false;
-        u256 rhs, t;
-        fp_sqr<C>(rhs, q.x);
-        fp_mul<C>(rhs, rhs, q.x);
-        if (C == CURVE_R1) {   // - 3x
-            fp_add<C>(t, q.x, q.x);
-            fp_add<C>(t, t, q.x);
-            fp_sub<C>(rhs, rhs, t);
-        }
-        u256 b;
-        u256_from_c(b, cv.b);
-        fp_add<C>(rhs, rhs, b);
+        u256 rhs;
+        curve_rhs<C>(rhs, q.x);
         fp_pow<C>(q.y, rhs, cv.p_plus_1_div_4);
-        if ((q.y.w[0] & 1u) != (uint32_t)(pt[0] & 1)) fp_neg<C>(q.y, q.y);
+        fp_canon<C>(q.y, q.y);
+        if ((q.y.w[0] & 1u) != (uint32_t)(pt[0] & 1)) {
+            fp_neg<C>(q.y, q.y);
+            fp_canon<C>(q.y, q.y);
+        }
     } else {
         return false;
     }
     // on-curve: y^2 == x^3 + a x + b
-    u256 lhs, rhs, t, b;
+    u256 lhs, rhs;
     fp_sqr<C>(lhs, q.y);
-    fp_sqr<C>(rhs, q.x);
-    fp_mul<C>(rhs, rhs, q.x);
-    if (C == CURVE_R1) {
-        fp_add<C>(t, q.x, q.x);
-        fp_add<C>(t, t, q.x);
-        fp_sub<C>(rhs, rhs, t);
-    }
-    u256_from_c(b, cv.b);
-    fp_add<C>(rhs, rhs, b);
-    return u256_eq(lhs, rhs);
+    curve_rhs<C>(rhs, q.x);
+    return fp_eq<C>(lhs, rhs);
 }
 
 CHIP_DEV void store_apt(uint32_t* dst, const apt& a) {
-#pragma unroll
-    for (int i = 0; i < 8; i++) {
-        dst[i] = a.x.w[i];
-        dst[8 + i] = a.y.w[i];
-    }
+    uint4* d4 = reinterpret_cast<uint4*>(dst);
+    d4[0] = make_uint4(a.x.w[0], a.x.w[1], a.x.w[2], a.x.w[3]);
+    d4[1] = make_uint4(a.x.w[4], a.x.w[5], a.x.w[6], a.x.w[7]);
+    d4[2] = make_uint4(a.y.w[0], a.y.w[1], a.y.w[2], a.y.w[3]);
+    d4[3] = make_uint4(a.y.w[4], a.y.w[5], a.y.w[6], a.y.w[7]);
 }
 CHIP_DEV void load_apt(apt& a, const uint32_t* src) {
     const uint4* s4 = reinterpret_cast<const uint4*>(src);
@@ -97,37 +113,84 @@ CHIP_DEV void load_apt(apt& a, const uint32_t* src) {
     a.y.w[0] = v2.x; a.y.w[1] = v2.y; a.y.w[2] = v2.z; a.y.w[3] = v2.w;
     a.y.w[4] = v3.x; a.y.w[5] = v3.y; a.y.w[6] = v3.z; a.y.w[7] = v3.w;
 }
-
-// {1..8} Q in affine form: Jacobian multiples, one shared inversion (Montgomery's trick)
+CHIP_DEV void store_jpt(uint32_t* d, const jpt& p) {
+    uint4* d4 = reinterpret_cast<uint4*>(d);
+    d4[0] = make_uint4(p.X.w[0], p.X.w[1], p.X.w[2], p.X.w[3]);
+    d4[1] = make_uint4(p.X.w[4], p.X.w[5], p.X.w[6], p.X.w[7]);
+    d4[2] = make_uint4(p.Y.w[0], p.Y.w[1], p.Y.w[2], p.Y.w[3]);
+    d4[3] = make_uint4(p.Y.w[4], p.Y.w[5], p.Y.w[6], p.Y.w[7]);
+    d4[4] = make_uint4(p.Z.w[0], p.Z.w[1], p.Z.w[2], p.Z.w[3]);
+    d4[5] = make_uint4(p.Z.w[4], p.Z.w[5], p.Z.w[6], p.Z.w[7]);
+}
+CHIP_DEV void store_u256(uint32_t* d, const u256& v) {
+    uint4* d4 = reinterpret_cast<uint4*>(d);
+    d4[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
+    d4[1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
+}
+CHIP_DEV void load_u256(u256& v, const uint32_t* s) {
+    const uint4* s4 = reinterpret_cast<const uint4*>(s);
+    const uint4 a = s4[0], b = s4[1];
+    v.w[0] = a.x; v.w[1] = a.y; v.w[2] = a.z; v.w[3] = a.w;
+    v.w[4] = b.x; v.w[5] = b.y; v.w[6] = b.z; v.w[7] = b.w;
+}
+CHIP_DEV void load_jpt(jpt& p, const uint32_t* s) {
+    load_u256(p.X, s);
+    load_u256(p.Y, s + 8);
+    load_u256(p.Z, s + 16);
+}
+CHIP_DEV void jpt_inf(jpt& p) {
+    u256_set_word(p.X, 0);
+    u256_set_word(p.Y, 0);
+    u256_set_word(p.Z, 0);
+}
+CHIP_DEV void jpt_from_aff(jpt& p, const apt& a) {
+    p.X = a.x;
+    p.Y = a.y;
+    u256_set_word(p.Z, 1);
+}
+// affine (x, y) = (X / Z^2, Y / Z^3) given zi = 1 / Z
 template <int C>
-CHIP_DEV void ec_build_table(uint32_t* tab, const apt& q) {
-    jpt P[8];
-    P[0].X = q.x;
-    P[0].Y = q.y;
-#pragma unroll
-    for (int i = 0; i < 8; i++) P[0].Z.w[i] = (i == 0);
-    jdbl<C>(P[1], P[0]);
-    for (int k = 2; k < 8; k++) jmadd<C>(P[k], P[k - 1], q);
-    u256 acc[8];
+CHIP_DEV void jpt_to_aff(apt& a, const jpt& p, const u256& zi) {
+    u256 zi2, zi3;
+    fp_sqr<C>(zi2, zi);
+    fp_mul<C>(zi3, zi2, zi);
+    fp_mul<C>(a.x, p.X, zi2);
+    fp_mul<C>(a.y, p.Y, zi3);
+}
+
+// {1..8} Q in affine form: Jacobian multiples, one shared inversion (Montgomery's trick).  The
+// windowed schedule's per-key table; entry 1 (= Q) was stored by the key prep.
+template <int C>
+CHIP_DEV void ec_build_table(uint32_t* tab) {
+    apt q;
+    load_apt(q, tab + 16);
+    jpt A, P[7];
+    jpt_from_aff(A, q);
+    jdbl<C>(P[0], A);                               // 2Q
+#pragma unroll 1
+    for (int k = 1; k < 7; k++) jmadd<C>(P[k], P[k - 1], q);
+    u256 acc[7];
     acc[0] = P[0].Z;
-    for (int k = 1; k < 8; k++) fp_mul<C>(acc[k], acc[k - 1], P[k].Z);
+#pragma unroll 1
+    for (int k = 1; k < 7; k++) fp_mul<C>(acc[k], acc[k - 1], P[k].Z);
     u256 inv;
-    fp_inv<C>(inv, acc[7]);
-    for (int k = 7; k >= 0; k--) {
-        u256 zi, zi2, zi3;
-        if (k > 0) fp_mul<C>(zi, inv, acc[k - 1]);
-        else zi = inv;
-        if (k > 0) fp_mul<C>(inv, inv, P[k].Z);
-        fp_sqr<C>(zi2, zi);
-        fp_mul<C>(zi3, zi2, zi);
+    fp_inv_vt<C>(inv, acc[6]);
+#pragma unroll 1
+    for (int k = 6; k >= 0; k--) {
+        u256 zi;
+        if (k > 0) {
+            fp_mul<C>(zi, inv, acc[k - 1]);
+            fp_mul<C>(inv, inv, P[k].Z);
+        } else {
+            zi = inv;
+        }
         apt a;
-        fp_mul<C>(a.x, P[k].X, zi2);
-        fp_mul<C>(a.y, P[k].Y, zi3);
-        store_apt(tab + 16 * (k + 1), a);
+        jpt_to_aff<C>(a, P[k], zi);
+        store_apt(tab + 16 * (k + 2), a);
     }
 }
 
-// ---- K2b: per unique key ----
+// ---- K2b: per unique key: SPKI scheme lookup + decode (Crypto.findSignatureScheme, decodePoint) ----
 __global__ void __launch_bounds__(256) k_ecdsa_key_prep(uint64_t n_keys, const uint8_t* __restrict__ key_data,
                                                         const uint64_t* __restrict__ key_off,
                                                         const uint32_t* __restrict__ key_len, KeyMeta* meta,
@@ -148,17 +211,21 @@ __global__ void __launch_bounds__(256) k_ecdsa_key_prep(uint64_t n_keys, const u
     m.scheme = (uint8_t)scheme;
     m.pad[0] = m.pad[1] = 0;
     apt q;
-    bool ok;
-    uint32_t* tab = table + k * EC_TAB_STRIDE;
-    if (scheme == CHIP_SCHEME_R1) {
-        ok = ec_decode_point<CURVE_R1>(q, pt, ptlen);
-        if (ok) ec_build_table<CURVE_R1>(tab, q);
-    } else {
-        ok = ec_decode_point<CURVE_K1>(q, pt, ptlen);
-        if (ok) ec_build_table<CURVE_K1>(tab, q);
-    }
+    const bool ok = scheme == CHIP_SCHEME_R1 ? ec_decode_point<CURVE_R1>(q, pt, ptlen)
+                                             : ec_decode_point<CURVE_K1>(q, pt, ptlen);
+    if (ok) store_apt(table + k * EC_TAB_STRIDE + 16, q);
     m.ok = ok ? 1 : 0;
     meta[k] = m;
+}
+
+__global__ void __launch_bounds__(64) k_ecdsa_key_table(uint64_t n_keys, const KeyMeta* __restrict__ meta,
+                                                        uint32_t* __restrict__ table) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_keys) return;
+    const KeyMeta m = meta[k];
+    if (!m.ok) return;
+    if (m.scheme == CHIP_SCHEME_R1) ec_build_table<CURVE_R1>(table + k * EC_TAB_STRIDE);
+    else if (m.scheme == CHIP_SCHEME_K1) ec_build_table<CURVE_K1>(table + k * EC_TAB_STRIDE);
 }
 
 // ---- DER (BC 1.57 StdDSAEncoder + re-encode equality) ----
@@ -219,6 +286,39 @@ CHIP_DEV bool der_decode(const uint8_t* sig, uint32_t len, u256& r, bool& roor, 
     return true;
 }
 
+// DER, range checks and e = SHA-256(M) reduced mod n.  Returns the status to report when the
+// signature stops here (0xff: go on with the arithmetic).
+template <int C>
+CHIP_DEV uint32_t ecdsa_front(u256& r, u256& s, u256& e, const uint8_t* sig, uint32_t siglen, const uint8_t* msg,
+                              uint32_t msglen) {
+    const ec_curve_c& cv = curve<C>();
+    bool roor, soor;
+    if (!der_decode(sig, siglen, r, roor, s, soor)) return CHIP_SIG_DECODE;
+    if (roor || soor || u256_is_zero(r) || u256_is_zero(s) || u256_ge(r, cv.n) || u256_ge(s, cv.n)) return CHIP_INVALID;
+    uint32_t H[8];
+    sha256_bytes(H, msg, msglen);
+#pragma unroll
+    for (int k = 0; k < 8; k++) e.w[k] = H[7 - k];
+    u256 t;
+    if (!u256_sub(t, e, cv.n)) e = t;   // e < 2^256 < 2n
+    return 0xffu;
+}
+
+// x(R) mod n == r  <=>  X == r Z^2  or  (r + n < p and X == (r + n) Z^2); R = infinity -> false
+template <int C>
+CHIP_DEV bool ecdsa_check(const jpt& acc, const u256& r) {
+    if (fp_is_zero<C>(acc.Z)) return false;
+    u256 z2, t;
+    fp_sqr<C>(z2, acc.Z);
+    fp_mul<C>(t, r, z2);
+    if (fp_eq<C>(t, acc.X)) return true;
+    u256 rn;
+    const uint32_t c = u256_add(rn, r, curve<C>().n);
+    if (c || u256_ge(rn, curve<C>().p)) return false;
+    fp_mul<C>(t, rn, z2);
+    return fp_eq<C>(t, acc.X);
+}
+
 // signed radix-2^w recoding of a 256-bit scalar: ndig digits biased by 2^(w-1), plus final carry
 template <int W>
 CHIP_DEV uint32_t recode(uint32_t out[8], const u256& a) {
@@ -264,7 +364,7 @@ __global__ void __launch_bounds__(256) k_ecdsa_verify(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ msg_len,
                                                       const uint32_t* __restrict__ table, uint8_t* __restrict__ status) {
     __shared__ uint32_t gtab[EC_G_ENTRIES * 16];
-    const ec_aff_c* G = (C == CURVE_R1) ? EC_R1_G_TABLE : EC_K1_G_TABLE;
+    const ec_aff_c* G = (EC_CURVE(C) == CURVE_R1) ? EC_R1_G_TABLE : EC_K1_G_TABLE;
     for (int i = threadIdx.x; i < EC_G_ENTRIES * 16; i += blockDim.x) {
         const ec_aff_c& e = G[i >> 4];
         gtab[i] = (i & 15) < 8 ? e.x[i & 7] : e.y[i & 7];
@@ -274,27 +374,12 @@ __global__ void __launch_bounds__(256) k_ecdsa_verify(const uint32_t* __restrict
     if (gid >= *count) return;
     const uint32_t i = list[gid];
     const ec_curve_c& cv = curve<C>();
-    u256 r, s;
-    bool roor, soor;
-    if (!der_decode(sig_data + sig_off[i], sig_len[i], r, roor, s, soor)) {
-        status[i] = CHIP_SIG_DECODE;
-        return;
-    }
-    // r, s in [1, n-1]
-    if (roor || soor || u256_is_zero(r) || u256_is_zero(s) || u256_ge(r, cv.n) || u256_ge(s, cv.n)) {
-        status[i] = CHIP_INVALID;
-        return;
-    }
-    // e = SHA-256(M), big-endian integer; reduce once mod n (e < 2^256 < 2n)
+    u256 r, s, e;
     const uint32_t mi = msg_idx[i];
-    uint32_t H[8];
-    sha256_bytes(H, msg_data + msg_off[mi], msg_len[mi]);
-    u256 e;
-#pragma unroll
-    for (int k = 0; k < 8; k++) e.w[k] = H[7 - k];
-    {
-        u256 t;
-        if (!u256_sub(t, e, cv.n)) e = t;
+    const uint32_t st0 = ecdsa_front<C>(r, s, e, sig_data + sig_off[i], sig_len[i], msg_data + msg_off[mi], msg_len[mi]);
+    if (st0 != 0xffu) {
+        status[i] = (uint8_t)st0;
+        return;
     }
     // w = s^-1 mod n (Fermat, Montgomery domain); u1 = e w, u2 = r w
     u256 r2n, sm, wm, u1, u2;
@@ -309,8 +394,7 @@ __global__ void __launch_bounds__(256) k_ecdsa_verify(const uint32_t* __restrict
     const uint32_t cg = recode<8>(dg, u1);
     const uint32_t* qt = table + (uint64_t)key_idx[i] * EC_TAB_STRIDE;
     jpt acc;
-#pragma unroll
-    for (int k = 0; k < 8; k++) acc.X.w[k] = acc.Y.w[k] = acc.Z.w[k] = 0;
+    jpt_inf(acc);
     apt ent;
     // top window (position 64): the recodings' final carries
     if (cq) {
@@ -321,6 +405,7 @@ __global__ void __launch_bounds__(256) k_ecdsa_verify(const uint32_t* __restrict
         load_apt(ent, gtab + 16);
         add_digit<C>(acc, ent, 1);
     }
+#pragma unroll 1
     for (int w = 63; w >= 0; w--) {
         jdbl<C>(acc, acc);
         jdbl<C>(acc, acc);
@@ -344,24 +429,7 @@ __global__ void __launch_bounds__(256) k_ecdsa_verify(const uint32_t* __restrict
             add_digit<C>(acc, ent, g);
         }
     }
-    if (u256_is_zero(acc.Z)) {
-        status[i] = CHIP_INVALID;
-        return;
-    }
-    // x(R) mod n == r  <=>  X == r Z^2  or  (r + n < p and X == (r + n) Z^2)
-    u256 z2, t;
-    fp_sqr<C>(z2, acc.Z);
-    fp_mul<C>(t, r, z2);
-    bool ok = u256_eq(t, acc.X);
-    if (!ok) {
-        u256 rn;
-        const uint32_t c = u256_add(rn, r, cv.n);
-        if (!c && !u256_ge(rn, cv.p)) {
-            fp_mul<C>(t, rn, z2);
-            ok = u256_eq(t, acc.X);
-        }
-    }
-    status[i] = ok ? CHIP_VALID : CHIP_INVALID;
+    status[i] = ecdsa_check<C>(acc, r) ? CHIP_VALID : CHIP_INVALID;
 }
 
 void launch_ecdsa_key_prep(hipStream_t st, uint64_t n_keys, const uint8_t* key_data, const uint64_t* key_off,
@@ -370,6 +438,10 @@ void launch_ecdsa_key_prep(hipStream_t st, uint64_t n_keys, const uint8_t* key_d
     const uint32_t blocks = (uint32_t)((n_keys + 255) / 256);
     hipLaunchKernelGGL(k_ecdsa_key_prep, dim3(blocks), dim3(256), 0, st, n_keys, key_data, key_off, key_len, meta,
                        ectab);
+}
+void launch_ecdsa_key_table(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, uint32_t* ectab) {
+    if (!n_keys) return;
+    hipLaunchKernelGGL(k_ecdsa_key_table, dim3((uint32_t)((n_keys + 63) / 64)), dim3(64), 0, st, n_keys, meta, ectab);
 }
 
 void launch_ecdsa_verify(hipStream_t st, int scheme, uint64_t n, const uint32_t* list, const uint32_t* count,
@@ -387,118 +459,80 @@ void launch_ecdsa_verify(hipStream_t st, int scheme, uint64_t n, const uint32_t*
 }
 
 // ---------------------------------------------------------------------------------------
-// K2c: per-key comb path (keys that sign many signatures of a batch).  R = u1 G + u2 Q with no
-// doublings: u2 in signed radix-16 digits over 65 windows from a per-key table of 2^(4w) {1..8} Q
-// (built for the batch by k_ecdsa_comb_chain / k_ecdsa_comb_fill on the second stream, normalised to
-// affine so every addition is a mixed one), u1 in signed radix-256 digits over 33 windows from the
-// fixed tables EC_<C>_G_COMB.  s^-1 is one Fermat inversion per EC_INV_BATCH signatures (Montgomery's
-// trick, k_ecdsa_comb_inv).  96 mixed additions instead of 256 doublings + 96 mixed additions; the same
-// BC 1.57 semantics as k_ecdsa_verify (identical DER / range / x(R) mod n checks).
-#include "comb_tables.hpp"
+// Fixed-base G comb: entry (w, j) = j 2^(EC_GW w) G for windows w < EC_GWIN, j = 1..2^(EC_GW-1),
+// affine, 16 words each.  u1 < n < 2^256 in signed radix-2^EC_GW digits: EC_GWIN digits cover
+// EC_GW * EC_GWIN >= 257 bits, so the recoding never leaves a final carry.  Built once per context
+// (k_ecdsa_gcomb_build: one lane per entry, 2^(EC_GW w) G by doublings, the multiple by
+// double-and-add, one inversion to affine).
+#ifndef EC_GW
+#define EC_GW 12
+#endif
+#define EC_GWIN ((256 + EC_GW) / EC_GW)
+#define EC_GENT (1u << (EC_GW - 1))
+#define EC_GCOMB_WORDS ((uint64_t)EC_GWIN * EC_GENT * 16)
 
+template <int C>
+__global__ void __launch_bounds__(64) k_ecdsa_gcomb_build(uint32_t* __restrict__ out) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= EC_GWIN * EC_GENT) return;
+    const uint32_t w = g / EC_GENT, j = g % EC_GENT + 1;
+    const ec_aff_c& G = (EC_CURVE(C) == CURVE_R1) ? EC_R1_G_TABLE[1] : EC_K1_G_TABLE[1];
+    jpt P;
+    u256_from_c(P.X, G.x);
+    u256_from_c(P.Y, G.y);
+    u256_set_word(P.Z, 1);
+#pragma unroll 1
+    for (uint32_t b = 0; b < EC_GW * w; b++) jdbl<C>(P, P);
+    u256 zi;
+    apt base;
+    fp_inv_vt<C>(zi, P.Z);
+    jpt_to_aff<C>(base, P, zi);
+    jpt acc;
+    jpt_inf(acc);
+#pragma unroll 1
+    for (int bit = EC_GW - 1; bit >= 0; bit--) {
+        jdbl<C>(acc, acc);
+        if ((j >> bit) & 1u) jmadd<C>(acc, acc, base);
+    }
+    fp_inv_vt<C>(zi, acc.Z);
+    apt a;
+    jpt_to_aff<C>(a, acc, zi);
+    fp_canon<C>(a.x, a.x);
+    fp_canon<C>(a.y, a.y);
+    store_apt(out + ((uint64_t)w * EC_GENT + (j - 1)) * 16, a);
+}
+
+uint64_t ecdsa_gcomb_words() { return 2 * EC_GCOMB_WORDS; }
+void launch_ecdsa_gcomb_build(hipStream_t st, uint32_t* gcomb) {
+    const uint32_t lanes = EC_GWIN * EC_GENT;
+    hipLaunchKernelGGL(k_ecdsa_gcomb_build<CURVE_R1>, dim3((lanes + 63) / 64), dim3(64), 0, st, gcomb);
+    hipLaunchKernelGGL(k_ecdsa_gcomb_build<CURVE_K1>, dim3((lanes + 63) / 64), dim3(64), 0, st, gcomb + EC_GCOMB_WORDS);
+}
+
+// ---------------------------------------------------------------------------------------
+// Per-key comb tables: window w (0..64) holds j 2^(4w) Q for j = 1..8, affine (16 words each).
 #define EC_COMB_QWIN 65
 #define EC_COMB_QENT 8
 #define EC_COMB_JW 24
 // affine table per key, then (after all keys) the Jacobian scratch it is normalised from
 #define EC_COMB_KEY_WORDS (EC_COMB_QWIN * EC_COMB_QENT * 16)
 #define EC_COMB_JAC_WORDS (EC_COMB_QWIN * EC_COMB_QENT * EC_COMB_JW)
-#define EC_INV_BATCH 16
-
-CHIP_DEV void store_jpt(uint32_t* d, const jpt& p) {
-    uint4* d4 = reinterpret_cast<uint4*>(d);
-    d4[0] = make_uint4(p.X.w[0], p.X.w[1], p.X.w[2], p.X.w[3]);
-    d4[1] = make_uint4(p.X.w[4], p.X.w[5], p.X.w[6], p.X.w[7]);
-    d4[2] = make_uint4(p.Y.w[0], p.Y.w[1], p.Y.w[2], p.Y.w[3]);
-    d4[3] = make_uint4(p.Y.w[4], p.Y.w[5], p.Y.w[6], p.Y.w[7]);
-    d4[4] = make_uint4(p.Z.w[0], p.Z.w[1], p.Z.w[2], p.Z.w[3]);
-    d4[5] = make_uint4(p.Z.w[4], p.Z.w[5], p.Z.w[6], p.Z.w[7]);
-}
-CHIP_DEV void store_u256(uint32_t* d, const u256& v) {
-    uint4* d4 = reinterpret_cast<uint4*>(d);
-    d4[0] = make_uint4(v.w[0], v.w[1], v.w[2], v.w[3]);
-    d4[1] = make_uint4(v.w[4], v.w[5], v.w[6], v.w[7]);
-}
-CHIP_DEV void load_u256(u256& v, const uint32_t* s) {
-    const uint4* s4 = reinterpret_cast<const uint4*>(s);
-    const uint4 a = s4[0], b = s4[1];
-    v.w[0] = a.x; v.w[1] = a.y; v.w[2] = a.z; v.w[3] = a.w;
-    v.w[4] = b.x; v.w[5] = b.y; v.w[6] = b.z; v.w[7] = b.w;
-}
-CHIP_DEV void load_jpt(jpt& p, const uint32_t* s) {
-    const uint4* s4 = reinterpret_cast<const uint4*>(s);
-    uint4 v;
-    v = s4[0]; p.X.w[0] = v.x; p.X.w[1] = v.y; p.X.w[2] = v.z; p.X.w[3] = v.w;
-    v = s4[1]; p.X.w[4] = v.x; p.X.w[5] = v.y; p.X.w[6] = v.z; p.X.w[7] = v.w;
-    v = s4[2]; p.Y.w[0] = v.x; p.Y.w[1] = v.y; p.Y.w[2] = v.z; p.Y.w[3] = v.w;
-    v = s4[3]; p.Y.w[4] = v.x; p.Y.w[5] = v.y; p.Y.w[6] = v.z; p.Y.w[7] = v.w;
-    v = s4[4]; p.Z.w[0] = v.x; p.Z.w[1] = v.y; p.Z.w[2] = v.z; p.Z.w[3] = v.w;
-    v = s4[5]; p.Z.w[4] = v.x; p.Z.w[5] = v.y; p.Z.w[6] = v.z; p.Z.w[7] = v.w;
-}
-
-// r = p + q, both Jacobian (add-2007-bl); exact for infinity, p == q and p == -q.  r may alias p.
-template <int C> CHIP_DEV void jadd(jpt& r, const jpt& p, const jpt& q) {
-    if (u256_is_zero(p.Z)) { r = q; return; }
-    if (u256_is_zero(q.Z)) { r = p; return; }
-    u256 Z1Z1, Z2Z2, U1, U2, S1, S2, H, I, J, rr, V, t;
-    fp_sqr<C>(Z1Z1, p.Z);
-    fp_sqr<C>(Z2Z2, q.Z);
-    fp_mul<C>(U1, p.X, Z2Z2);
-    fp_mul<C>(U2, q.X, Z1Z1);
-    fp_mul<C>(S1, p.Y, q.Z);
-    fp_mul<C>(S1, S1, Z2Z2);
-    fp_mul<C>(S2, q.Y, p.Z);
-    fp_mul<C>(S2, S2, Z1Z1);
-    fp_sub<C>(H, U2, U1);
-    fp_sub<C>(rr, S2, S1);
-    if (u256_is_zero(H)) {
-        if (u256_is_zero(rr)) {
-            jdbl<C>(r, p);
-        } else {
-#pragma unroll
-            for (int i = 0; i < 8; i++) r.X.w[i] = r.Y.w[i] = r.Z.w[i] = 0;
-        }
-        return;
-    }
-    fp_add<C>(rr, rr, rr);
-    fp_add<C>(I, H, H);
-    fp_sqr<C>(I, I);
-    fp_mul<C>(J, H, I);
-    fp_mul<C>(V, U1, I);
-    jpt o;
-    fp_sqr<C>(o.X, rr);
-    fp_sub<C>(o.X, o.X, J);
-    fp_sub<C>(o.X, o.X, V);
-    fp_sub<C>(o.X, o.X, V);
-    fp_sub<C>(t, V, o.X);
-    fp_mul<C>(o.Y, rr, t);
-    fp_mul<C>(t, S1, J);
-    fp_add<C>(t, t, t);
-    fp_sub<C>(o.Y, o.Y, t);
-    fp_add<C>(t, p.Z, q.Z);
-    fp_sqr<C>(t, t);
-    fp_sub<C>(t, t, Z1Z1);
-    fp_sub<C>(t, t, Z2Z2);
-    fp_mul<C>(o.Z, t, H);
-    r = o;
-}
 
 CHIP_DEV bool ec_key_ok(const KeyMeta* meta, uint64_t k, int scheme) {
     const KeyMeta m = meta[k];
     return m.scheme == scheme && m.ok;
 }
 
-// chain: P_w = 2^(4w) Q for w = 0..64 into entry 1 of every window of the Jacobian scratch
-// (256 serial doublings per key)
+// chain: P_w = 2^(4w) Q (Jacobian) for w = 0..64 into entry 0 of every window of the scratch
+// (256 serial doublings per key: the latency of this kernel is the per-key table's critical path)
 template <int C>
 CHIP_DEV void ec_comb_chain(const uint32_t* __restrict__ ectab, uint32_t* __restrict__ jac, uint64_t k) {
     apt q;
     load_apt(q, ectab + k * EC_TAB_STRIDE + 16);
     jpt P;
-    P.X = q.x;
-    P.Y = q.y;
-#pragma unroll
-    for (int i = 0; i < 8; i++) P.Z.w[i] = (i == 0);
+    jpt_from_aff(P, q);
     uint32_t* tab = jac + k * EC_COMB_JAC_WORDS;
+#pragma unroll 1
     for (int w = 0; w < EC_COMB_QWIN; w++) {
         store_jpt(tab + (uint32_t)w * EC_COMB_QENT * EC_COMB_JW, P);
         if (w + 1 == EC_COMB_QWIN) break;
@@ -506,54 +540,74 @@ CHIP_DEV void ec_comb_chain(const uint32_t* __restrict__ ectab, uint32_t* __rest
         for (int b = 0; b < 4; b++) jdbl<C>(P, P);
     }
 }
-// fill: entries j = 2..8 of window w = j P_w (Jacobian scratch), then to affine.  A lane takes
-// EC_FILL_GROUP windows so that one Fermat inversion serves 8 EC_FILL_GROUP entries (Montgomery's
-// trick; the prefix products are parked in the x slots of the affine entries)
-#define EC_FILL_GROUP 8
+// fill, for windows [w0, w1) of one key:
+//   1. P_w to affine with one inversion for the group (Montgomery's trick; prefix products parked in
+//      the x slots of the output entries)
+//   2. j P_w for j = 2..8: one doubling and six mixed additions, Jacobian into the scratch
+//   3. those 7 (w1 - w0) entries to affine with one more shared inversion
+#define EC_FILL_GROUP 2
 #define EC_FILL_LANES ((EC_COMB_QWIN - 1) / EC_FILL_GROUP)
 template <int C>
 CHIP_DEV void ec_comb_fill(uint32_t* __restrict__ jac, uint32_t* __restrict__ out, uint32_t w0, uint32_t w1) {
-    u256 acc, z, t;
-#pragma unroll
-    for (int i = 0; i < 8; i++) acc.w[i] = (i == 0);
+    u256 acc, z, inv;
+    // 1.
+    u256_set_word(acc, 1);
+#pragma unroll 1
+    for (uint32_t w = w0; w < w1; w++) {
+        store_u256(out + w * EC_COMB_QENT * 16, acc);
+        load_u256(z, jac + w * EC_COMB_QENT * EC_COMB_JW + 16);
+        fp_mul<C>(acc, acc, z);
+    }
+    fp_inv_vt<C>(inv, acc);   // entries are 2^(4w) Q, never infinity for a valid key
+#pragma unroll 1
+    for (uint32_t w = w1; w-- > w0;) {
+        uint32_t* o = out + w * EC_COMB_QENT * 16;
+        jpt P;
+        u256 pre, zi;
+        load_jpt(P, jac + w * EC_COMB_QENT * EC_COMB_JW);
+        load_u256(pre, o);
+        fp_mul<C>(zi, inv, pre);
+        fp_mul<C>(inv, inv, P.Z);
+        apt a;
+        jpt_to_aff<C>(a, P, zi);
+        store_apt(o, a);
+    }
+    // 2.
+    u256_set_word(acc, 1);
+#pragma unroll 1
     for (uint32_t w = w0; w < w1; w++) {
         uint32_t* e = jac + w * EC_COMB_QENT * EC_COMB_JW;
         uint32_t* o = out + w * EC_COMB_QENT * 16;
-        jpt P, A;
-        load_jpt(P, e);
-        store_u256(o, acc);
-        fp_mul<C>(acc, acc, P.Z);
-        jdbl<C>(A, P);
-        store_jpt(e + EC_COMB_JW, A);
-        store_u256(o + 16, acc);
-        fp_mul<C>(acc, acc, A.Z);
+        apt a;
+        load_apt(a, o);
+        jpt A;
+        jpt_from_aff(A, a);
+        jdbl<C>(A, A);
 #pragma unroll 1
-        for (int j = 3; j <= EC_COMB_QENT; j++) {
-            jadd<C>(A, A, P);
+        for (int j = 2; j <= EC_COMB_QENT; j++) {
+            if (j > 2) jmadd<C>(A, A, a);
             store_jpt(e + (uint32_t)(j - 1) * EC_COMB_JW, A);
             store_u256(o + (uint32_t)(j - 1) * 16, acc);
             fp_mul<C>(acc, acc, A.Z);
         }
     }
-    fp_inv<C>(acc, acc);   // entries are j 2^(4w) Q, never infinity for a valid key
+    // 3.
+    fp_inv_vt<C>(inv, acc);
+#pragma unroll 1
     for (uint32_t w = w1; w-- > w0;) {
         const uint32_t* e = jac + w * EC_COMB_QENT * EC_COMB_JW;
         uint32_t* o = out + w * EC_COMB_QENT * 16;
 #pragma unroll 1
-        for (int j = EC_COMB_QENT - 1; j >= 0; j--) {
-            u256 zi, zi2, pre, x, y;
+        for (int j = EC_COMB_QENT - 1; j >= 1; j--) {
+            jpt A;
+            u256 pre, zi;
+            load_jpt(A, e + (uint32_t)j * EC_COMB_JW);
             load_u256(pre, o + (uint32_t)j * 16);
-            load_u256(z, e + (uint32_t)j * EC_COMB_JW + 16);
-            fp_mul<C>(zi, acc, pre);
-            fp_mul<C>(acc, acc, z);
-            fp_sqr<C>(zi2, zi);
-            load_u256(x, e + (uint32_t)j * EC_COMB_JW);
-            load_u256(y, e + (uint32_t)j * EC_COMB_JW + 8);
-            fp_mul<C>(x, x, zi2);
-            fp_mul<C>(t, zi2, zi);
-            fp_mul<C>(y, y, t);
-            store_u256(o + (uint32_t)j * 16, x);
-            store_u256(o + (uint32_t)j * 16 + 8, y);
+            fp_mul<C>(zi, inv, pre);
+            fp_mul<C>(inv, inv, A.Z);
+            apt a;
+            jpt_to_aff<C>(a, A, zi);
+            store_apt(o + (uint32_t)j * 16, a);
         }
     }
 }
@@ -562,8 +616,8 @@ __global__ void __launch_bounds__(64) k_ecdsa_comb_chain(uint64_t n_keys, const 
                                                          const uint32_t* __restrict__ ectab, uint32_t* __restrict__ jac) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_keys) return;
-    if (ec_key_ok(meta, k, CHIP_SCHEME_R1)) ec_comb_chain<CURVE_R1>(ectab, jac, k);
-    else if (ec_key_ok(meta, k, CHIP_SCHEME_K1)) ec_comb_chain<CURVE_K1>(ectab, jac, k);
+    if (ec_key_ok(meta, k, CHIP_SCHEME_R1)) ec_comb_chain<CURVE_R1 | CURVE_ILP>(ectab, jac, k);
+    else if (ec_key_ok(meta, k, CHIP_SCHEME_K1)) ec_comb_chain<CURVE_K1 | CURVE_ILP>(ectab, jac, k);
 }
 // lane per key x group of windows (the last group also takes window 64)
 __global__ void __launch_bounds__(256) k_ecdsa_comb_fill(uint64_t n_keys, const KeyMeta* __restrict__ meta,
@@ -580,8 +634,52 @@ __global__ void __launch_bounds__(256) k_ecdsa_comb_fill(uint64_t n_keys, const 
     else if (ec_key_ok(meta, k, CHIP_SCHEME_K1)) ec_comb_fill<CURVE_K1>(e, out, w0, w1);
 }
 
-// hand-off between the kernels, SoA by list position: acc X/Y/Z (24 words), u2 (8), r (8), state (1).
-// Before k_ecdsa_comb_g the X slots hold e, the Y slots s R and the Z slots s^-1 R.
+// ---- work lists grouped by key (counting sort), so the lanes of a wave read one key's table ----
+// key_count[k] = signatures of key k in its curve's list (k_classify's histogram); a key's
+// signatures occupy [key_base[k], key_base[k] + key_count[k]) of the grouped list of its curve.
+__global__ void __launch_bounds__(256) k_ec_group_base(uint64_t n_keys, const KeyMeta* __restrict__ meta,
+                                                       const uint32_t* __restrict__ key_count,
+                                                       uint32_t* __restrict__ key_base, uint32_t* __restrict__ ctr) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= n_keys) return;
+    const KeyMeta m = meta[k];
+    const uint32_t c = key_count[k];
+    if (!m.ok || !c || (m.scheme != CHIP_SCHEME_R1 && m.scheme != CHIP_SCHEME_K1)) return;
+    key_base[k] = atomicAdd(&ctr[m.scheme == CHIP_SCHEME_R1 ? 0 : 1], c);
+}
+// one lane per (curve list, position): grid covers 2 n lanes, [0, n) r1 and [n, 2n) k1
+__global__ void __launch_bounds__(256) k_ec_group_scatter(uint64_t n, const uint32_t* __restrict__ lists,
+                                                          const uint32_t* __restrict__ counts,
+                                                          const uint32_t* __restrict__ key_idx,
+                                                          const uint32_t* __restrict__ key_base,
+                                                          uint32_t* __restrict__ key_cur, uint32_t* __restrict__ out) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t lane = threadIdx.x & 63;
+    const int L = g < n ? 0 : 1;
+    const uint64_t pos = g - (uint64_t)L * n;
+    const uint32_t cnt = counts[L == 0 ? LIST_R1 : LIST_K1];
+    const bool v = pos < cnt;
+    uint32_t i = 0, k = 0;
+    if (v) {
+        i = lists[(uint64_t)(L == 0 ? LIST_R1 : LIST_K1) * n + pos];
+        k = key_idx[i];
+    }
+    uint32_t leader, c, rank;
+    wave_group(v, k, leader, c, rank);
+    uint32_t cur = 0;
+    if (v && lane == leader) cur = atomicAdd(&key_cur[k], c);
+    cur = __shfl(cur, (int)leader);
+    if (v) out[(uint64_t)L * n + key_base[k] + cur + rank] = i;
+}
+
+// ---- signature kernels, SoA hand-off by list position (`cap` = list capacity) ----
+//   pre (A): DER, range, e = SHA-256(M), s R; wave prefix / suffix products of s R
+//            slots 0-7 e, 8-15 exclusive prefix, 16-23 exclusive suffix, 32-39 r, 40 state;
+//            wave product -> wp[wave]
+//   inv (B): wp[wave] -> wp[wave]^-1 (one Fermat inversion per wave of signatures)
+//   g   (C): s^-1 = wp^-1 * prefix * suffix, u1 = e s^-1, u2 = r s^-1, u1 G;
+//            slots 0-23 u1 G (X, Y, Z), 24-31 u2
+//   q   (D): + u2 Q from the key's table, x(R) mod n == r
 #define EC_MID_WORDS 41
 
 CHIP_DEV void mid_store(uint32_t* mid, uint64_t cap, uint32_t gid, int slot, const u256& v) {
@@ -593,7 +691,28 @@ CHIP_DEV void mid_load(u256& v, const uint32_t* mid, uint64_t cap, uint32_t gid,
     for (int k = 0; k < 8; k++) v.w[k] = mid[(uint64_t)(slot + k) * cap + gid];
 }
 
-// DER, range checks, e = SHA-256(M), s R (Montgomery form mod n)
+CHIP_DEV void wave_shfl_up(u256& o, const u256& v, int d) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) o.w[k] = (uint32_t)__shfl_up((int)v.w[k], d, 64);
+}
+CHIP_DEV void wave_shfl_down(u256& o, const u256& v, int d) {
+#pragma unroll
+    for (int k = 0; k < 8; k++) o.w[k] = (uint32_t)__shfl_down((int)v.w[k], d, 64);
+}
+
+// blocks b, b+8, b+16, ... are dispatched to one XCD: give them consecutive work.  `used` = blocks
+// that hold list positions (the list count is known on the device only; the grid covers the
+// capacity): each XCD takes ceil(used / 8) consecutive blocks, so the work stays spread over all 8
+// XCDs however short the list is.  Returns a block index >= used for blocks without work.
+CHIP_DEV uint32_t ec_xcd_block(uint32_t b, uint32_t used) {
+    const uint32_t share = (used + 7) >> 3;
+    return (b & 7u) * share + (b >> 3);
+}
+
+// A.  The wave-level part of the batched inversion: inclusive prefix and suffix products of s R
+// across the 64 lanes (Hillis-Steele scans over shuffles); the exclusive products stay with the
+// lane, the wave's total goes to k_ecdsa_comb_inv.  Lanes without an arithmetic signature pass the
+// Montgomery one.  Every lane of a live wave takes part.
 template <int C>
 __global__ void __launch_bounds__(256) k_ecdsa_comb_pre(const uint32_t* __restrict__ list,
                                                         const uint32_t* __restrict__ count,
@@ -604,110 +723,110 @@ __global__ void __launch_bounds__(256) k_ecdsa_comb_pre(const uint32_t* __restri
                                                         const uint8_t* __restrict__ msg_data,
                                                         const uint64_t* __restrict__ msg_off,
                                                         const uint32_t* __restrict__ msg_len, uint32_t* __restrict__ mid,
-                                                        uint64_t cap, uint8_t* __restrict__ status) {
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= *count) return;
-    const uint32_t i = list[gid];
-    const ec_curve_c& cv = curve<C>();
-    uint32_t* st_word = mid + (uint64_t)40 * cap + gid;
-    u256 r, s;
-    bool roor, soor;
-    if (!der_decode(sig_data + sig_off[i], sig_len[i], r, roor, s, soor)) {
-        status[i] = CHIP_SIG_DECODE;
-        *st_word = 0;
-        return;
-    }
-    if (roor || soor || u256_is_zero(r) || u256_is_zero(s) || u256_ge(r, cv.n) || u256_ge(s, cv.n)) {
-        status[i] = CHIP_INVALID;
-        *st_word = 0;
-        return;
-    }
-    const uint32_t mi = msg_idx[i];
-    uint32_t H[8];
-    sha256_bytes(H, msg_data + msg_off[mi], msg_len[mi]);
-    u256 e;
-#pragma unroll
-    for (int k = 0; k < 8; k++) e.w[k] = H[7 - k];
-    {
-        u256 t;
-        if (!u256_sub(t, e, cv.n)) e = t;
-    }
-    u256 r2n, sm;
-    u256_from_c(r2n, cv.r2_n);
-    mn_mul<C>(sm, s, r2n);
-    mid_store(mid, cap, gid, 0, e);
-    mid_store(mid, cap, gid, 8, sm);
-    mid_store(mid, cap, gid, 32, r);
-    *st_word = 1;
-}
-
-// s^-1 R for EC_INV_BATCH signatures per lane: prefix products of s R (parked in the Z slots), one
-// Fermat inversion of the product, then back to front.  Rejected signatures count as 1.  Lane l of a
-// wave takes positions base + j 64 + l, so every step is a coalesced row.
-template <int C>
-__global__ void __launch_bounds__(64) k_ecdsa_comb_inv(const uint32_t* __restrict__ count, uint32_t* __restrict__ mid,
-                                                       uint64_t cap) {
+                                                        uint32_t* __restrict__ wp, uint64_t cap,
+                                                        uint8_t* __restrict__ status) {
     const uint32_t n = *count;
-    const uint32_t base = blockIdx.x * 64u * EC_INV_BATCH + threadIdx.x;
-    if (base >= n) return;
+    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+    if ((gid & ~63u) >= n) return;   // whole wave past the list: wave-uniform exit
     const ec_curve_c& cv = curve<C>();
-    u256 acc, sm;
-    u256_from_c(acc, cv.one_n);
-    for (int j = 0; j < EC_INV_BATCH; j++) {
-        const uint32_t gid = base + 64u * j;
-        if (gid >= n) break;
-        if (!mid[(uint64_t)40 * cap + gid]) continue;
-        mid_store(mid, cap, gid, 16, acc);
-        mid_load(sm, mid, cap, gid, 8);
-        mn_mul<C>(acc, acc, sm);
+    const int lane = (int)__lane_id();
+    const bool live = gid < n;
+    u256 r, s, e, sm;
+    bool go = false;
+    if (live) {
+        const uint32_t i = list[gid];
+        const uint32_t mi = msg_idx[i];
+        const uint32_t st0 = ecdsa_front<C>(r, s, e, sig_data + sig_off[i], sig_len[i], msg_data + msg_off[mi], msg_len[mi]);
+        if (st0 != 0xffu) status[i] = (uint8_t)st0;
+        go = st0 == 0xffu;
     }
-    mn_pow<C>(acc, acc, cv.n_minus_2);
-    for (int j = EC_INV_BATCH - 1; j >= 0; j--) {
-        const uint32_t gid = base + 64u * j;
-        if (gid >= n || !mid[(uint64_t)40 * cap + gid]) continue;
-        u256 pre, w;
-        mid_load(pre, mid, cap, gid, 16);
-        mid_load(sm, mid, cap, gid, 8);
-        mn_mul<C>(w, acc, pre);
-        mn_mul<C>(acc, acc, sm);
-        mid_store(mid, cap, gid, 16, w);
+    if (go) {
+        u256 r2n;
+        u256_from_c(r2n, cv.r2_n);
+        mn_mul<C>(sm, s, r2n);
+    } else {
+        u256_from_c(sm, cv.one_n);
     }
+    u256 pre = sm, suf = sm, o, t;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        wave_shfl_up(o, pre, d);
+        mn_mul<C>(t, pre, o);
+        if (lane >= d) pre = t;
+        wave_shfl_down(o, suf, d);
+        mn_mul<C>(t, suf, o);
+        if (lane + d < 64) suf = t;
+    }
+    if (lane == 63) store_u256(wp + (uint64_t)(gid >> 6) * 8, pre);
+    u256 ep, es;
+    wave_shfl_up(ep, pre, 1);
+    wave_shfl_down(es, suf, 1);
+    if (lane == 0) u256_from_c(ep, cv.one_n);
+    if (lane == 63) u256_from_c(es, cv.one_n);
+    if (!live) return;
+    mid[(uint64_t)40 * cap + gid] = go ? 1u : 0u;
+    if (!go) return;
+    mid_store(mid, cap, gid, 0, e);
+    mid_store(mid, cap, gid, 8, ep);
+    mid_store(mid, cap, gid, 16, es);
+    mid_store(mid, cap, gid, 32, r);
 }
 
-// u1 = e s^-1, u2 = r s^-1 and u1 G from the fixed comb
+// B.  One inversion per wave product (binary extended Euclid, mn_inv), both curves in one launch: lanes [0, nw) r1 waves,
+// [nw, 2 nw) k1 waves (nw = the wave capacity of one list).
+__global__ void __launch_bounds__(64) k_ecdsa_comb_inv(const uint32_t* __restrict__ counts, uint32_t* __restrict__ wp_r1,
+                                                       uint32_t* __restrict__ wp_k1, uint32_t nw) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const bool k1 = g >= nw;
+    const uint32_t w = k1 ? g - nw : g;
+    const uint32_t n = counts[k1 ? LIST_K1 : LIST_R1];
+    if (w >= (n + 63) / 64) return;
+    uint32_t* p = (k1 ? wp_k1 : wp_r1) + (uint64_t)w * 8;
+    u256 v, inv;
+    load_u256(v, p);
+    if (k1) mn_inv<CURVE_K1 | CURVE_ILP>(inv, v);
+    else mn_inv<CURVE_R1 | CURVE_ILP>(inv, v);
+    store_u256(p, inv);
+}
+
+// C.  s^-1, u1, u2 and u1 G from the fixed comb.
 template <int C>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k_ecdsa_comb_g(const uint32_t* __restrict__ count, uint32_t* __restrict__ mid,
-                                                      uint64_t cap) {
+__global__ void __launch_bounds__(256) k_ecdsa_comb_g(const uint32_t* __restrict__ count,
+                                                      const uint32_t* __restrict__ gcomb, uint32_t* __restrict__ mid,
+                                                      const uint32_t* __restrict__ wp, uint64_t cap) {
     const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
     if (gid >= *count || !mid[(uint64_t)40 * cap + gid]) return;
-    u256 e, r, wm, u1, u2;
+    u256 e, r, ep, es, winv, wm, u1, u2;
+    mid_load(ep, mid, cap, gid, 8);
+    mid_load(es, mid, cap, gid, 16);
+    load_u256(winv, wp + (uint64_t)(gid >> 6) * 8);
+    mn_mul<C>(wm, winv, ep);
+    mn_mul<C>(wm, wm, es);
     mid_load(e, mid, cap, gid, 0);
-    mid_load(wm, mid, cap, gid, 16);
     mid_load(r, mid, cap, gid, 32);
     mn_mul<C>(u1, e, wm);
     mn_mul<C>(u2, r, wm);
-    uint32_t dg[8];
-    const uint32_t cg = recode<8>(dg, u1);
     jpt acc;
-#pragma unroll
-    for (int k = 0; k < 8; k++) acc.X.w[k] = acc.Y.w[k] = acc.Z.w[k] = 0;
-    const uint32_t* G = (C == CURVE_R1) ? EC_R1_G_COMB : EC_K1_G_COMB;
+    jpt_inf(acc);
+    const uint32_t* G = gcomb + (EC_CURVE(C) == CURVE_R1 ? 0 : EC_GCOMB_WORDS);
+    int carry = 0;
     apt ga;
-#pragma unroll 1
-    for (int wd = 0; wd < 8; wd++) {
-        const uint32_t cur = dg[wd];
-#pragma unroll 1
-        for (int q = 0; q < 4; q++) {
-            const int d = (int)((cur >> (8 * q)) & 255u) - 128;
-            if (!d) continue;
-            const uint32_t w = (uint32_t)(wd * 4 + q);
-            load_apt(ga, G + (w * EC_COMB_GENT + (uint32_t)(d < 0 ? -d : d)) * 16);
-            add_digit<C>(acc, ga, d);
+#pragma unroll
+    for (int w = 0; w < EC_GWIN; w++) {
+        const int b = w * EC_GW;   // bits [b, b + EC_GW) of u1
+        uint32_t bits;
+        if (b >= 256) bits = 0;
+        else if ((b & 31) + EC_GW <= 32 || (b >> 5) == 7) bits = u1.w[b >> 5] >> (b & 31);
+        else bits = __builtin_amdgcn_alignbit(u1.w[(b >> 5) + 1], u1.w[b >> 5], b & 31);
+        int v = (int)(bits & ((1u << EC_GW) - 1)) + carry;
+        carry = (v + (1 << (EC_GW - 1)) - 1) >> EC_GW;   // digits in [-2^(W-1) + 1, 2^(W-1)]
+        v -= carry << EC_GW;
+        if (v != 0) {
+            const uint32_t av = (uint32_t)(v < 0 ? -v : v);
+            load_apt(ga, G + ((uint64_t)w * EC_GENT + av - 1) * 16);
+            if (v < 0) fp_neg<C>(ga.y, ga.y);
+            jmadd<C>(acc, acc, ga);
         }
-    }
-    if (cg) {
-        load_apt(ga, G + (32u * EC_COMB_GENT + 1u) * 16);
-        add_digit<C>(acc, ga, 1);
     }
     mid_store(mid, cap, gid, 0, acc.X);
     mid_store(mid, cap, gid, 8, acc.Y);
@@ -715,28 +834,26 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k
     mid_store(mid, cap, gid, 24, u2);
 }
 
-// u2 Q half: one mixed addition per non-zero radix-16 digit from the key's affine table, then
-// x(R) mod n == r exactly as k_ecdsa_verify checks it
+// D.  u2 Q half: one mixed addition per non-zero radix-16 digit from the key's affine table, then
+// x(R) mod n == r exactly as k_ecdsa_verify checks it.  The list is grouped by key and consecutive
+// blocks run on one XCD, so a key's 33 KB table is read from one L2.
 template <int C>
 __global__ void __launch_bounds__(256) k_ecdsa_comb_q(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
                                                       const uint32_t* __restrict__ key_idx,
                                                       const uint32_t* __restrict__ ctab, const uint32_t* __restrict__ mid,
-                                                      uint64_t cap, uint8_t* __restrict__ status) {
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
-    if (gid >= *count || !mid[(uint64_t)40 * cap + gid]) return;
+                                                      uint64_t cap, uint8_t* __restrict__ status, uint32_t remap) {
+    const uint32_t n = *count;
+    const uint32_t gid = (remap ? ec_xcd_block(blockIdx.x, (n + 255) / 256) : blockIdx.x) * blockDim.x + threadIdx.x;
+    if (gid >= n || !mid[(uint64_t)40 * cap + gid]) return;
     const uint32_t i = list[gid];
-    const ec_curve_c& cv = curve<C>();
     jpt acc;
     apt ent;
     u256 u2, r;
-#pragma unroll
-    for (int k = 0; k < 8; k++) {
-        acc.X.w[k] = mid[(uint64_t)k * cap + gid];
-        acc.Y.w[k] = mid[(uint64_t)(8 + k) * cap + gid];
-        acc.Z.w[k] = mid[(uint64_t)(16 + k) * cap + gid];
-        u2.w[k] = mid[(uint64_t)(24 + k) * cap + gid];
-        r.w[k] = mid[(uint64_t)(32 + k) * cap + gid];
-    }
+    mid_load(acc.X, mid, cap, gid, 0);
+    mid_load(acc.Y, mid, cap, gid, 8);
+    mid_load(acc.Z, mid, cap, gid, 16);
+    mid_load(u2, mid, cap, gid, 24);
+    mid_load(r, mid, cap, gid, 32);
     uint32_t dq[8];
     const uint32_t cq = recode<4>(dq, u2);
     const uint32_t* qt = ctab + (uint64_t)key_idx[i] * EC_COMB_KEY_WORDS;
@@ -756,23 +873,7 @@ __global__ void __launch_bounds__(256) k_ecdsa_comb_q(const uint32_t* __restrict
         load_apt(ent, qt + (64u * EC_COMB_QENT) * 16);
         add_digit<C>(acc, ent, 1);
     }
-    if (u256_is_zero(acc.Z)) {
-        status[i] = CHIP_INVALID;
-        return;
-    }
-    u256 z2, t;
-    fp_sqr<C>(z2, acc.Z);
-    fp_mul<C>(t, r, z2);
-    bool ok = u256_eq(t, acc.X);
-    if (!ok) {
-        u256 rn;
-        const uint32_t c = u256_add(rn, r, cv.n);
-        if (!c && !u256_ge(rn, cv.p)) {
-            fp_mul<C>(t, rn, z2);
-            ok = u256_eq(t, acc.X);
-        }
-    }
-    status[i] = ok ? CHIP_VALID : CHIP_INVALID;
+    status[i] = ecdsa_check<C>(acc, r) ? CHIP_VALID : CHIP_INVALID;
 }
 
 uint64_t ecdsa_comb_key_words() { return EC_COMB_KEY_WORDS + EC_COMB_JAC_WORDS; }
@@ -787,33 +888,56 @@ void launch_ecdsa_comb_build(hipStream_t st, uint64_t n_keys, const KeyMeta* met
                        meta, ctab, jac);
 }
 
+// words of the hand-off area per list position, and of the wave products per list
 uint64_t ecdsa_comb_mid_words() { return EC_MID_WORDS; }
+uint64_t ecdsa_comb_wp_words(uint64_t n) { return ((n + 63) / 64) * 8; }
 
-template <int C>
-static void comb_pre(hipStream_t st, uint64_t n, const uint32_t* list, const uint32_t* count, const chip_sig_batch* b,
-                     uint32_t* mid, uint8_t* status) {
-    hipLaunchKernelGGL(k_ecdsa_comb_pre<C>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, list, count,
-                       b->msg_idx, b->sig_data, b->sig_off, b->sig_len, b->msg_data, b->msg_off, b->msg_len, mid,
-                       (uint64_t)n, status);
-    hipLaunchKernelGGL(k_ecdsa_comb_inv<C>, dim3((uint32_t)((n + 64 * EC_INV_BATCH - 1) / (64 * EC_INV_BATCH))), dim3(64),
-                       0, st, count, mid, (uint64_t)n);
-    hipLaunchKernelGGL(k_ecdsa_comb_g<C>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, count, mid, (uint64_t)n);
+void launch_ecdsa_group(hipStream_t st, uint64_t n, uint64_t n_keys, const KeyMeta* meta, const uint32_t* key_count,
+                        uint32_t* key_base, uint32_t* key_cur, uint32_t* ctr, const uint32_t* lists,
+                        const uint32_t* counts, const uint32_t* key_idx, uint32_t* grouped) {
+    if (!n || !n_keys) return;
+    hipLaunchKernelGGL(k_ec_group_base, dim3((uint32_t)((n_keys + 255) / 256)), dim3(256), 0, st, n_keys, meta, key_count,
+                       key_base, ctr);
+    hipLaunchKernelGGL(k_ec_group_scatter, dim3((uint32_t)((2 * n + 255) / 256)), dim3(256), 0, st, n, lists, counts,
+                       key_idx, key_base, key_cur, grouped);
 }
 
+template <int C>
+static void comb_sig(hipStream_t st, uint64_t n, const uint32_t* list, const uint32_t* count, const chip_sig_batch* b,
+                     uint32_t* mid, uint32_t* wp, uint8_t* status) {
+    hipLaunchKernelGGL(k_ecdsa_comb_pre<C>, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, list, count, b->msg_idx,
+                       b->sig_data, b->sig_off, b->sig_len, b->msg_data, b->msg_off, b->msg_len, mid, wp, (uint64_t)n,
+                       status);
+}
 void launch_ecdsa_comb_pre(hipStream_t st, int scheme, uint64_t n, const uint32_t* list, const uint32_t* count,
-                           const chip_sig_batch* b, uint32_t* mid, uint8_t* status) {
+                           const chip_sig_batch* b, uint32_t* mid, uint32_t* wp, uint8_t* status) {
     if (!n) return;
-    if (scheme == CHIP_SCHEME_R1) comb_pre<CURVE_R1>(st, n, list, count, b, mid, status);
-    else comb_pre<CURVE_K1>(st, n, list, count, b, mid, status);
+    if (scheme == CHIP_SCHEME_R1) comb_sig<CURVE_R1>(st, n, list, count, b, mid, wp, status);
+    else comb_sig<CURVE_K1>(st, n, list, count, b, mid, wp, status);
+}
+void launch_ecdsa_comb_inv(hipStream_t st, uint64_t n, const uint32_t* counts, uint32_t* wp_r1, uint32_t* wp_k1) {
+    if (!n) return;
+    const uint32_t nw = (uint32_t)((n + 63) / 64);
+    hipLaunchKernelGGL(k_ecdsa_comb_inv, dim3((2 * nw + 63) / 64), dim3(64), 0, st, counts, wp_r1, wp_k1, nw);
+}
+void launch_ecdsa_comb_g(hipStream_t st, int scheme, uint64_t n, const uint32_t* count, const uint32_t* gcomb,
+                         uint32_t* mid, const uint32_t* wp) {
+    if (!n) return;
+    const uint32_t blocks = (uint32_t)((n + 255) / 256);
+    if (scheme == CHIP_SCHEME_R1)
+        hipLaunchKernelGGL(k_ecdsa_comb_g<CURVE_R1>, dim3(blocks), dim3(256), 0, st, count, gcomb, mid, wp, (uint64_t)n);
+    else
+        hipLaunchKernelGGL(k_ecdsa_comb_g<CURVE_K1>, dim3(blocks), dim3(256), 0, st, count, gcomb, mid, wp, (uint64_t)n);
 }
 void launch_ecdsa_comb_q(hipStream_t st, int scheme, uint64_t n, const uint32_t* list, const uint32_t* count,
                          const chip_sig_batch* b, const uint32_t* ctab, const uint32_t* mid, uint8_t* status) {
     if (!n) return;
-    const uint32_t blocks = (uint32_t)((n + 255) / 256);
+    const uint32_t blocks = ((uint32_t)((n + 255) / 256) + 7) & ~7u;   // multiple of 8 for the XCD remap
+    static const uint32_t remap = getenv("CHIP_EC_XCD") ? (getenv("CHIP_EC_XCD")[0] == '1') : 0u;   // measured slower on cfg3
     if (scheme == CHIP_SCHEME_R1)
         hipLaunchKernelGGL(k_ecdsa_comb_q<CURVE_R1>, dim3(blocks), dim3(256), 0, st, list, count, b->key_idx, ctab, mid,
-                           (uint64_t)n, status);
+                           (uint64_t)n, status, remap);
     else
         hipLaunchKernelGGL(k_ecdsa_comb_q<CURVE_K1>, dim3(blocks), dim3(256), 0, st, list, count, b->key_idx, ctab, mid,
-                           (uint64_t)n, status);
+                           (uint64_t)n, status, remap);
 }

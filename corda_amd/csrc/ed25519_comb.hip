@@ -186,8 +186,13 @@ __global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict
 }
 
 // ---- verify: one lane per comb-list position ----
-// blocks b, b+8, b+16, ... are dispatched to one XCD: give them consecutive work (grid % 8 == 0)
-CHIP_DEV uint32_t xcd_block(uint32_t b, uint32_t nb) { return (b & 7u) * (nb >> 3) + (b >> 3); }
+// blocks b, b+8, b+16, ... are dispatched to one XCD: give them consecutive work.  `used` = blocks
+// that hold list positions (the comb count is on the device; the grid covers the whole batch):
+// each XCD takes ceil(used / 8) consecutive blocks, so a short list still spreads over all 8 XCDs.
+CHIP_DEV uint32_t xcd_block(uint32_t b, uint32_t used) {
+    const uint32_t share = (used + 7) >> 3;
+    return (b & 7u) * share + (b >> 3);
+}
 
 __global__ void __launch_bounds__(256) k_ed_comb_verify(const uint32_t* __restrict__ list, const uint32_t* __restrict__ ctr,
                                                         const uint32_t* __restrict__ key_idx,
@@ -201,8 +206,9 @@ __global__ void __launch_bounds__(256) k_ed_comb_verify(const uint32_t* __restri
                                                         const int32_t* __restrict__ key_slot,
                                                         const uint32_t* __restrict__ ctab, uint32_t* __restrict__ xyz,
                                                         uint64_t cap) {
-    const uint32_t p = xcd_block(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
-    if (p >= ctr[1]) return;
+    const uint32_t ncomb = ctr[1];
+    const uint32_t p = xcd_block(blockIdx.x, (ncomb + 255) / 256) * blockDim.x + threadIdx.x;
+    if (p >= ncomb) return;
     const uint32_t i = list[p];
     const uint32_t k = key_idx[i];
     const uint32_t mi = msg_idx[i];

@@ -40,6 +40,7 @@ struct chip_ctx {
     int device = 0;
     uint32_t flags = 0;
     uint32_t comb_min_sigs = 4;                   // Ed25519 comb threshold (signatures per key)
+    bool ec_group = true;                         // ECDSA comb lists grouped by key (CHIP_EC_GROUP=0 off)
     uint64_t comb_budget = 8ull << 30;            // bytes of per-key comb tables
     hipStream_t stream = nullptr;
     hipStream_t aux = nullptr;                    // second stream: per-key comb tables
@@ -50,7 +51,7 @@ struct chip_ctx {
     DevBuf meta, abytes, edtab, ectab, lists, counts;
     // Ed25519 comb path
     DevBuf c_key_count, c_key_slot, c_key_base, c_key_cur, c_slot_key, c_ctr, c_comb_list, c_straus_list, c_ctab,
-        c_xyz, c_zpre, c_nega, e_ctab, e_mid;
+        c_xyz, c_zpre, c_nega, e_ctab, e_mid, e_gcomb, e_wp, e_glist;
     // host-path mirrors of the caller's buffers
     DevBuf h_key_idx, h_msg_idx, h_sig_data, h_sig_off, h_sig_len, h_key_data, h_key_off, h_key_len, h_msg_data,
         h_msg_off, h_msg_len, h_status, h_bitmap;
@@ -148,11 +149,11 @@ __global__ void __launch_bounds__(256) k_classify(uint64_t n, const uint32_t* __
         if (list < 0) status[i] = st;
     }
     const uint32_t lane = threadIdx.x & 63;
-    if (key_count) {   // comb-path histogram: signatures per Ed25519 key, one atomic per key per wave
+    if (key_count) {   // comb-path histogram: signatures per key (one scheme per key), one atomic per key per wave
         uint32_t leader, cnt, rank;
-        const bool ed = list == LIST_ED25519;
-        wave_group(ed, k, leader, cnt, rank);
-        if (ed && lane == leader) atomicAdd(&key_count[k], cnt);
+        const bool arith = list >= 0;
+        wave_group(arith, k, leader, cnt, rank);
+        if (arith && lane == leader) atomicAdd(&key_count[k], cnt);
     }
 #pragma unroll
     for (int L = 0; L < N_LISTS; L++) {
@@ -241,6 +242,16 @@ int chip_device_count(void) {
     return n;
 }
 
+// The second stream builds the per-key tables that the last kernels of a batch wait for; its
+// kernels go first when both streams have work queued (greatest priority, CHIP_AUX_PRIORITY=0 off).
+static int aux_priority() {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return 0;
+    if (const char* e = getenv("CHIP_AUX_PRIORITY"))
+        if (e[0] == '0') return lo;
+    return hi;
+}
+
 int chip_init(const chip_config* cfg, chip_ctx** out) {
     if (!out) return CHIP_E_ARG;
     *out = nullptr;
@@ -253,7 +264,7 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
     if (hipSetDevice(dev) != hipSuccess || hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess ||
         hipEventCreate(&c->tev0) != hipSuccess || hipEventCreate(&c->tev1) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->aux, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, aux_priority()) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork2, hipEventDisableTiming) != hipSuccess ||
@@ -262,7 +273,18 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
         return CHIP_E_DEVICE;
     }
     if (cfg) c->flags = cfg->flags;
+    // fixed-base G combs for the ECDSA comb schedule: built once, on the device
+    if (c->e_gcomb.ensure(ecdsa_gcomb_words() * 4) != hipSuccess) {
+        chip_shutdown(c);
+        return CHIP_E_NOMEM;
+    }
+    launch_ecdsa_gcomb_build(c->stream, c->e_gcomb.as<uint32_t>());
+    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
+        chip_shutdown(c);
+        return CHIP_E_DEVICE;
+    }
     if (c->flags & CHIP_FLAG_FORCE_COMB) c->comb_min_sigs = 1;
+    if (const char* e = getenv("CHIP_EC_GROUP")) c->ec_group = e[0] != '0';
     if (const char* e = getenv("CHIP_COMB_MIN_SIGS")) c->comb_min_sigs = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("CHIP_COMB_BUDGET_MB")) c->comb_budget = (uint64_t)strtoull(e, nullptr, 10) << 20;
     if (cfg && cfg->reserve_sigs) {
@@ -278,7 +300,7 @@ void chip_shutdown(chip_ctx* c) {
     hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->meta, &c->abytes, &c->edtab, &c->ectab, &c->lists, &c->counts, &c->c_key_count,
                       &c->c_key_slot, &c->c_key_base, &c->c_key_cur, &c->c_slot_key, &c->c_ctr, &c->c_comb_list,
-                      &c->c_straus_list, &c->c_ctab, &c->c_xyz, &c->c_zpre, &c->c_nega, &c->e_ctab, &c->e_mid, &c->h_key_idx, &c->h_msg_idx,
+                      &c->c_straus_list, &c->c_ctab, &c->c_xyz, &c->c_zpre, &c->c_nega, &c->e_ctab, &c->e_mid, &c->e_gcomb, &c->e_wp, &c->e_glist, &c->h_key_idx, &c->h_msg_idx,
                       &c->h_sig_data, &c->h_sig_off, &c->h_sig_len, &c->h_key_data, &c->h_key_off, &c->h_key_len,
                       &c->h_msg_data, &c->h_msg_off, &c->h_msg_len, &c->h_status, &c->h_bitmap, &c->t_salts,
                       &c->t_start, &c->t_group, &c->t_internal, &c->t_data, &c->t_off, &c->t_len, &c->t_ids,
@@ -364,6 +386,8 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     if (ec_comb) {
         HIPCHK(c, c->e_ctab.ensure(nk * ec_key_bytes + 16));
         HIPCHK(c, c->e_mid.ensure(2 * n * ecdsa_comb_mid_words() * 4 + 16));
+        HIPCHK(c, c->e_wp.ensure(2 * ecdsa_comb_wp_words(n) * 4 + 16));
+        HIPCHK(c, c->e_glist.ensure(2 * n * 4 + 16));
     }
     HIPCHK(c, hipEventRecord(c->ev0, st));
     HIPCHK(c, hipMemsetAsync(c->counts.p, 0, 64, st));
@@ -388,6 +412,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
     }
     launch_ecdsa_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->ectab.as<uint32_t>());
+    if (!ec_comb) launch_ecdsa_key_table(st, nk, meta, c->ectab.as<uint32_t>());
     if (ec_comb) {
         HIPCHK(c, hipEventRecord(c->ev_fork2, st));
         HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork2, 0));
@@ -430,22 +455,35 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         launch_ed25519_verify(st, n, ed_list, ed_count, b, c->abytes.as<uint32_t>(), c->edtab.as<uint32_t>(), status);
         c->kend(ke, st);
         if (ec_comb) {
-            // table-free halves first (overlap the per-key table build on the aux stream), then the
-            // u2 Q halves once the tables are there
+            // key-grouped work lists, then the table-free kernels (overlapping the per-key table build on
+            // the aux stream), then the u2 Q kernels once the tables are there
+            const uint64_t mw = ecdsa_comb_mid_words();
             uint32_t* mid_r1 = c->e_mid.as<uint32_t>();
-            uint32_t* mid_k1 = mid_r1 + n * ecdsa_comb_mid_words();
+            uint32_t* mid_k1 = mid_r1 + n * mw;
+            uint32_t* wp_r1 = c->e_wp.as<uint32_t>();
+            uint32_t* wp_k1 = wp_r1 + ecdsa_comb_wp_words(n);
+            uint32_t* gl_r1 = c->e_glist.as<uint32_t>();
+            uint32_t* gl_k1 = gl_r1 + n;
             ke = c->kbegin(CHIP_K_ECDSA_R1, st);
-            launch_ecdsa_comb_pre(st, CHIP_SCHEME_R1, n, lists + (uint64_t)LIST_R1 * n, counts + LIST_R1, b, mid_r1,
-                                  status);
-            launch_ecdsa_comb_pre(st, CHIP_SCHEME_K1, n, lists + (uint64_t)LIST_K1 * n, counts + LIST_K1, b, mid_k1,
-                                  status);
+            if (c->ec_group) {
+                launch_ecdsa_group(st, n, nk, meta, w.key_count, w.key_base, w.key_cur, w.ctr + 4, lists, counts,
+                                   b->key_idx, gl_r1);
+            } else {
+                gl_r1 = lists + (uint64_t)LIST_R1 * n;
+                gl_k1 = lists + (uint64_t)LIST_K1 * n;
+            }
+            launch_ecdsa_comb_pre(st, CHIP_SCHEME_R1, n, gl_r1, counts + LIST_R1, b, mid_r1, wp_r1, status);
+            launch_ecdsa_comb_pre(st, CHIP_SCHEME_K1, n, gl_k1, counts + LIST_K1, b, mid_k1, wp_k1, status);
+            launch_ecdsa_comb_inv(st, n, counts, wp_r1, wp_k1);
+            launch_ecdsa_comb_g(st, CHIP_SCHEME_R1, n, counts + LIST_R1, c->e_gcomb.as<uint32_t>(), mid_r1, wp_r1);
+            launch_ecdsa_comb_g(st, CHIP_SCHEME_K1, n, counts + LIST_K1, c->e_gcomb.as<uint32_t>(), mid_k1, wp_k1);
             HIPCHK(c, hipStreamWaitEvent(st, c->ev_join2, 0));
-            launch_ecdsa_comb_q(st, CHIP_SCHEME_R1, n, lists + (uint64_t)LIST_R1 * n, counts + LIST_R1, b,
-                                c->e_ctab.as<uint32_t>(), mid_r1, status);
+            launch_ecdsa_comb_q(st, CHIP_SCHEME_R1, n, gl_r1, counts + LIST_R1, b, c->e_ctab.as<uint32_t>(), mid_r1,
+                                status);
             c->kend(ke, st);
             ke = c->kbegin(CHIP_K_ECDSA_K1, st);
-            launch_ecdsa_comb_q(st, CHIP_SCHEME_K1, n, lists + (uint64_t)LIST_K1 * n, counts + LIST_K1, b,
-                                c->e_ctab.as<uint32_t>(), mid_k1, status);
+            launch_ecdsa_comb_q(st, CHIP_SCHEME_K1, n, gl_k1, counts + LIST_K1, b, c->e_ctab.as<uint32_t>(), mid_k1,
+                                status);
             c->kend(ke, st);
         } else {
             ke = c->kbegin(CHIP_K_ECDSA_R1, st);

@@ -14,6 +14,8 @@ void launch_ed25519_verify(hipStream_t st, uint64_t n, const uint32_t* list, con
 
 void launch_ecdsa_key_prep(hipStream_t st, uint64_t n_keys, const uint8_t* key_data, const uint64_t* key_off,
                            const uint32_t* key_len, KeyMeta* meta, uint32_t* ectab);
+// {1..8}Q per key for the windowed schedule (k_ecdsa_verify); the comb schedule does not need it
+void launch_ecdsa_key_table(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, uint32_t* ectab);
 void launch_ecdsa_verify(hipStream_t st, int scheme, uint64_t n, const uint32_t* list, const uint32_t* count,
                          const chip_sig_batch* b, const uint32_t* ectab, uint8_t* status);
 
@@ -22,9 +24,20 @@ uint64_t ecdsa_comb_key_words();
 void launch_ecdsa_comb_build(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, const uint32_t* ectab,
                              uint32_t* ctab);
 uint64_t ecdsa_comb_mid_words();
-// table-free half (DER, SHA-256, s^-1, u1 G) and the u2 Q half of the comb verify
+// fixed-base G combs of both curves (built once per context)
+uint64_t ecdsa_gcomb_words();
+void launch_ecdsa_gcomb_build(hipStream_t st, uint32_t* gcomb);
+// comb signature kernels: pre (DER, SHA-256, s R, wave prefix/suffix products), inv (one inversion
+// per wave product, both curves), g (s^-1, u1, u2, u1 G); then q (u2 Q + check) once the tables exist
+uint64_t ecdsa_comb_wp_words(uint64_t n);
+void launch_ecdsa_group(hipStream_t st, uint64_t n, uint64_t n_keys, const KeyMeta* meta, const uint32_t* key_count,
+                        uint32_t* key_base, uint32_t* key_cur, uint32_t* ctr, const uint32_t* lists,
+                        const uint32_t* counts, const uint32_t* key_idx, uint32_t* grouped);
 void launch_ecdsa_comb_pre(hipStream_t st, int scheme, uint64_t n, const uint32_t* list, const uint32_t* count,
-                           const chip_sig_batch* b, uint32_t* mid, uint8_t* status);
+                           const chip_sig_batch* b, uint32_t* mid, uint32_t* wp, uint8_t* status);
+void launch_ecdsa_comb_inv(hipStream_t st, uint64_t n, const uint32_t* counts, uint32_t* wp_r1, uint32_t* wp_k1);
+void launch_ecdsa_comb_g(hipStream_t st, int scheme, uint64_t n, const uint32_t* count, const uint32_t* gcomb,
+                         uint32_t* mid, const uint32_t* wp);
 void launch_ecdsa_comb_q(hipStream_t st, int scheme, uint64_t n, const uint32_t* list, const uint32_t* count,
                          const chip_sig_batch* b, const uint32_t* ctab, const uint32_t* mid, uint8_t* status);
 

@@ -272,8 +272,9 @@ EC_KINDS = ["valid", "r_flip", "s_flip", "msg_flip", "wrong_key", "wrong_curve",
 
 
 def ecdsa_batch(n: int, n_keys: int = 4096, msg_len: int = 200, corrupt: float = 0.10,
-                seed: int = 0x5EED0003, threads: int = 8) -> SigBatch:
-    """cfg3: n ECDSA signatures, r1/k1 interleaved (even index r1, odd k1), one message per tx of 2."""
+                seed: int = 0x5EED0003, threads: int = 8, schemes=(SCHEME_R1, SCHEME_K1)) -> SigBatch:
+    """cfg3: n ECDSA signatures, r1/k1 interleaved (even index r1, odd k1), one message per tx of 2.
+    schemes=(SCHEME_R1,) gives a P-256-only batch (the same keys, messages and corruption mix)."""
     rng = np.random.Generator(np.random.PCG64(seed))
     nk = n_keys
     privs = {}
@@ -299,7 +300,10 @@ def ecdsa_batch(n: int, n_keys: int = 4096, msg_len: int = 200, corrupt: float =
     msg_off = np.arange(ntx, dtype=np.uint64) * msg_len
     msg_lenv = np.full(ntx, msg_len, dtype=np.uint32)
     msg_idx = (np.arange(n, dtype=np.uint32) // 2)
-    scheme = np.where(np.arange(n) % 2 == 0, SCHEME_R1, SCHEME_K1).astype(np.uint8)
+    if len(schemes) == 1:
+        scheme = np.full(n, schemes[0], dtype=np.uint8)
+    else:
+        scheme = np.where(np.arange(n) % 2 == 0, SCHEME_R1, SCHEME_K1).astype(np.uint8)
     key_local = rng.integers(0, nk, size=n, dtype=np.uint32)
     kind = np.zeros(n, dtype=np.uint8)
     ncor = int(n * corrupt)
