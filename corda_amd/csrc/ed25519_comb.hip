@@ -194,21 +194,29 @@ CHIP_DEV uint32_t xcd_block(uint32_t b, uint32_t used) {
     return (b & 7u) * share + (b >> 3);
 }
 
-__global__ void __launch_bounds__(256) k_ed_comb_verify(const uint32_t* __restrict__ list, const uint32_t* __restrict__ ctr,
-                                                        const uint32_t* __restrict__ key_idx,
-                                                        const uint32_t* __restrict__ msg_idx,
-                                                        const uint8_t* __restrict__ sig_data,
-                                                        const uint64_t* __restrict__ sig_off,
-                                                        const uint8_t* __restrict__ msg_data,
-                                                        const uint64_t* __restrict__ msg_off,
-                                                        const uint32_t* __restrict__ msg_len,
-                                                        const uint32_t* __restrict__ abytes,
-                                                        const int32_t* __restrict__ key_slot,
-                                                        const uint32_t* __restrict__ ctab, uint32_t* __restrict__ xyz,
-                                                        uint64_t cap) {
-    const uint32_t ncomb = ctr[1];
-    const uint32_t p = xcd_block(blockIdx.x, (ncomb + 255) / 256) * blockDim.x + threadIdx.x;
-    if (p >= ncomb) return;
+// The verify runs in two kernels so that the part that needs no per-key table overlaps the table
+// build on the second stream:
+//   k_ed_comb_bhalf  h = SHA-512(R || Abyte || M) mod L and [S]B from the fixed comb (32 madds);
+//                    hands over [S]B (extended, 40 words) and h (8 words) SoA in bmid
+//   k_ed_comb_ahalf  + [h](-A) from the key's table (64 cached additions), projective R' to xyz
+// hand-off: [S]B (40 words) + the ED_COMB_ADW words of h's recoded digits, read one word per 4
+// windows by the table half (keeping all 16 live would cost the occupancy step to 3 waves/SIMD)
+#define ED_BMID_WORDS (40 + ED_COMB_ADW)
+#ifndef ED_AHALF_WAVES
+#define ED_AHALF_WAVES
+#endif
+__global__ void __launch_bounds__(256) k_ed_comb_bhalf(const uint32_t* __restrict__ list, const uint32_t* __restrict__ ctr,
+                                                       const uint32_t* __restrict__ key_idx,
+                                                       const uint32_t* __restrict__ msg_idx,
+                                                       const uint8_t* __restrict__ sig_data,
+                                                       const uint64_t* __restrict__ sig_off,
+                                                       const uint8_t* __restrict__ msg_data,
+                                                       const uint64_t* __restrict__ msg_off,
+                                                       const uint32_t* __restrict__ msg_len,
+                                                       const uint32_t* __restrict__ abytes, uint32_t* __restrict__ bmid,
+                                                       uint64_t cap) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= ctr[1]) return;
     const uint32_t i = list[p];
     const uint32_t k = key_idx[i];
     const uint32_t mi = msg_idx[i];
@@ -224,38 +232,15 @@ __global__ void __launch_bounds__(256) k_ed_comb_verify(const uint32_t* __restri
     ed_challenge(hx, R, Ab, msg_data + msg_off[mi], msg_len[mi]);
     sc_reduce512(h, hx);
     ed_effective_s(s, S);
-    uint32_t da[ED_COMB_ADW], db[8];
-    recode_bytes<ED_COMB_W, ED_COMB_AWIN>(da, h);
+    uint32_t db[8];
     recode_bytes<8, 32>(db, s);
-    const uint32_t* tab = ctab + (uint64_t)key_slot[k] * ED_COMB_KEY_WORDS;
-
-    // [h](-A): one cached addition per window (extended coordinates, unified = complete formulas)
+    // [S]B: one mixed (affine Niels) addition per window from the identity; the accumulator carries 2Z
     ge_p3 u;
     ge_p3_0(u);
-    ge_p1p1 t;
-    ge_cached ca;
-    for (int wd = 0; wd < ED_COMB_ADW; wd++) {
-        const uint32_t cur = da[0];
-#pragma unroll
-        for (int q = 0; q < ED_COMB_ADW - 1; q++) da[q] = da[q + 1];
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-            const int w = wd * 4 + e;
-            if (w < ED_COMB_AWIN) {
-                const int d = (int)((cur >> (8 * e)) & 0xffu) - ED_COMB_ABIAS;
-                const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
-                ed_load_cached(ca, tab + ((uint32_t)w * ED_COMB_AENT + ad) * 40);
-                if (w > 0) ge_p1p1_to_p3(u, t);
-                ge_add_cached(t, u, ca, d < 0);
-            }
-        }
-    }
-    // [S]B: one mixed (affine Niels) addition per window; the accumulator carries 2Z for madd
     fe z2;
-    fe_mul(u.X, t.X, t.T);
-    fe_mul(u.Y, t.Z, t.Y);
-    fe_mul2(z2, t.Z, t.T);
-    fe_mul(u.T, t.X, t.Y);
+    fe_0(z2);
+    z2.v[0] = 2;
+    ge_p1p1 t;
     ge_niels nb;
     for (int wd = 0; wd < 8; wd++) {
         const uint32_t cur = db[0];
@@ -274,6 +259,57 @@ __global__ void __launch_bounds__(256) k_ed_comb_verify(const uint32_t* __restri
                 fe_mul(u.T, t.X, t.Y);
             }
             ge_madd(t, u, z2, nb, d < 0);
+        }
+    }
+    ge_p1p1_to_p3(u, t);
+#pragma unroll
+    for (int q = 0; q < 10; q++) {
+        bmid[(uint64_t)q * cap + p] = u.X.v[q];
+        bmid[(uint64_t)(10 + q) * cap + p] = u.Y.v[q];
+        bmid[(uint64_t)(20 + q) * cap + p] = u.Z.v[q];
+        bmid[(uint64_t)(30 + q) * cap + p] = u.T.v[q];
+    }
+    uint32_t da[ED_COMB_ADW];
+    recode_bytes<ED_COMB_W, ED_COMB_AWIN>(da, h);
+#pragma unroll
+    for (int q = 0; q < ED_COMB_ADW; q++) bmid[(uint64_t)(40 + q) * cap + p] = da[q];
+}
+
+__global__ void __launch_bounds__(256, 2) ED_AHALF_WAVES k_ed_comb_ahalf(const uint32_t* __restrict__ list,
+                                                                      const uint32_t* __restrict__ ctr,
+                                                       const uint32_t* __restrict__ key_idx,
+                                                       const int32_t* __restrict__ key_slot,
+                                                       const uint32_t* __restrict__ ctab,
+                                                       const uint32_t* __restrict__ bmid, uint32_t* __restrict__ xyz,
+                                                       uint64_t cap) {
+    const uint32_t ncomb = ctr[1];
+    const uint32_t p = xcd_block(blockIdx.x, (ncomb + 255) / 256) * blockDim.x + threadIdx.x;
+    if (p >= ncomb) return;
+    const uint32_t k = key_idx[list[p]];
+    const uint32_t* tab = ctab + (uint64_t)key_slot[k] * ED_COMB_KEY_WORDS;
+    ge_p3 u;
+#pragma unroll
+    for (int q = 0; q < 10; q++) {
+        u.X.v[q] = bmid[(uint64_t)q * cap + p];
+        u.Y.v[q] = bmid[(uint64_t)(10 + q) * cap + p];
+        u.Z.v[q] = bmid[(uint64_t)(20 + q) * cap + p];
+        u.T.v[q] = bmid[(uint64_t)(30 + q) * cap + p];
+    }
+    // + [h](-A): one cached addition per window (extended coordinates, unified = complete formulas)
+    ge_p1p1 t;
+    ge_cached ca;
+    for (int wd = 0; wd < ED_COMB_ADW; wd++) {
+        const uint32_t cur = bmid[(uint64_t)(40 + wd) * cap + p];
+#pragma unroll
+        for (int e = 0; e < 4; e++) {
+            const int w = wd * 4 + e;
+            if (w < ED_COMB_AWIN) {
+                const int d = (int)((cur >> (8 * e)) & 0xffu) - ED_COMB_ABIAS;
+                const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+                ed_load_cached(ca, tab + ((uint32_t)w * ED_COMB_AENT + ad) * 40);
+                if (w > 0) ge_p1p1_to_p3(u, t);
+                ge_add_cached(t, u, ca, d < 0);
+            }
         }
     }
     // projective R' = (X : Y : Z), stored structure-of-arrays for the finish kernel
@@ -371,13 +407,19 @@ void launch_ed_comb_build(hipStream_t st, uint64_t n, uint64_t n_keys, const Key
                        w.max_slots, w.eager, meta, w.ctab);
 }
 
-void launch_ed_comb_verify(hipStream_t st, uint64_t n, const chip_sig_batch* b, const uint32_t* abytes,
-                           const EdCombWs& w) {
+uint64_t ed_comb_bmid_words() { return ED_BMID_WORDS; }
+
+void launch_ed_comb_bhalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, const uint32_t* abytes,
+                          const EdCombWs& w) {
+    if (!n || !w.max_slots) return;
+    hipLaunchKernelGGL(k_ed_comb_bhalf, dim3(nblk(n, 256)), dim3(256), 0, st, w.comb_list, w.ctr, b->key_idx, b->msg_idx,
+                       b->sig_data, b->sig_off, b->msg_data, b->msg_off, b->msg_len, abytes, w.bmid, (uint64_t)n);
+}
+void launch_ed_comb_ahalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w) {
     if (!n || !w.max_slots) return;
     const uint32_t blocks = (nblk(n, 256) + 7) & ~7u;   // multiple of 8 for the XCD remap
-    hipLaunchKernelGGL(k_ed_comb_verify, dim3(blocks), dim3(256), 0, st, w.comb_list, w.ctr, b->key_idx, b->msg_idx,
-                       b->sig_data, b->sig_off, b->msg_data, b->msg_off, b->msg_len, abytes, w.key_slot, w.ctab, w.xyz,
-                       (uint64_t)n);
+    hipLaunchKernelGGL(k_ed_comb_ahalf, dim3(blocks), dim3(256), 0, st, w.comb_list, w.ctr, b->key_idx, w.key_slot,
+                       w.ctab, w.bmid, w.xyz, (uint64_t)n);
 }
 
 void launch_ed_comb_finish(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w, uint8_t* status) {

@@ -51,7 +51,7 @@ struct chip_ctx {
     DevBuf meta, abytes, edtab, ectab, lists, counts;
     // Ed25519 comb path
     DevBuf c_key_count, c_key_slot, c_key_base, c_key_cur, c_slot_key, c_ctr, c_comb_list, c_straus_list, c_ctab,
-        c_xyz, c_zpre, c_nega, e_ctab, e_mid, e_gcomb, e_wp, e_glist;
+        c_xyz, c_zpre, c_nega, c_bmid, e_ctab, e_mid, e_gcomb, e_wp, e_glist;
     // host-path mirrors of the caller's buffers
     DevBuf h_key_idx, h_msg_idx, h_sig_data, h_sig_off, h_sig_len, h_key_data, h_key_off, h_key_len, h_msg_data,
         h_msg_off, h_msg_len, h_status, h_bitmap;
@@ -120,13 +120,16 @@ static int fail(chip_ctx* c, int code, const std::string& msg) {
 // ---------------------------------------------------------------------------------------
 // classify: status precedence of Crypto.doVerify (Crypto.kt:522-536 + engine order) and
 // wave-aggregated compaction of the signatures that need arithmetic into per-scheme lists.
+// is_valid = 1: Crypto.isValid (Crypto.kt:615-625) has no empty checks: an empty signature falls
+// through to the engine's decode error, empty clear data is verified as an empty message.
 __global__ void __launch_bounds__(256) k_classify(uint64_t n, const uint32_t* __restrict__ key_idx,
                                                   const uint32_t* __restrict__ msg_idx,
                                                   const uint32_t* __restrict__ sig_len,
                                                   const uint32_t* __restrict__ msg_len, uint64_t n_keys,
                                                   uint64_t n_msgs, const KeyMeta* __restrict__ meta,
                                                   uint8_t* __restrict__ status, uint32_t* __restrict__ lists,
-                                                  uint32_t* __restrict__ counts, uint32_t* __restrict__ key_count) {
+                                                  uint32_t* __restrict__ counts, uint32_t* __restrict__ key_count,
+                                                  uint32_t is_valid) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     int list = -1;
     uint32_t k = 0;
@@ -140,8 +143,8 @@ __global__ void __launch_bounds__(256) k_classify(uint64_t n, const uint32_t* __
             const KeyMeta km = meta[k];
             const uint32_t sl = sig_len[i];
             if (km.scheme == 0) st = CHIP_UNSUPPORTED;          // findSignatureScheme / require(supported)
-            else if (sl == 0) st = CHIP_EMPTY_SIG;              // Crypto.kt:528
-            else if (msg_len[m] == 0) st = CHIP_EMPTY_CLEAR;    // Crypto.kt:529
+            else if (sl == 0 && !is_valid) st = CHIP_EMPTY_SIG;              // Crypto.kt:528
+            else if (msg_len[m] == 0 && !is_valid) st = CHIP_EMPTY_CLEAR;    // Crypto.kt:529
             else if (!km.ok) st = CHIP_KEY_INVALID;             // key never constructible
             else if (km.scheme == CHIP_SCHEME_ED25519 && sl != 64) st = CHIP_SIG_DECODE;  // length is wrong
             else list = km.scheme == CHIP_SCHEME_ED25519 ? LIST_ED25519 : (km.scheme == CHIP_SCHEME_R1 ? LIST_R1 : LIST_K1);
@@ -300,7 +303,7 @@ void chip_shutdown(chip_ctx* c) {
     hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->meta, &c->abytes, &c->edtab, &c->ectab, &c->lists, &c->counts, &c->c_key_count,
                       &c->c_key_slot, &c->c_key_base, &c->c_key_cur, &c->c_slot_key, &c->c_ctr, &c->c_comb_list,
-                      &c->c_straus_list, &c->c_ctab, &c->c_xyz, &c->c_zpre, &c->c_nega, &c->e_ctab, &c->e_mid, &c->e_gcomb, &c->e_wp, &c->e_glist, &c->h_key_idx, &c->h_msg_idx,
+                      &c->c_straus_list, &c->c_ctab, &c->c_xyz, &c->c_zpre, &c->c_nega, &c->c_bmid, &c->e_ctab, &c->e_mid, &c->e_gcomb, &c->e_wp, &c->e_glist, &c->h_key_idx, &c->h_msg_idx,
                       &c->h_sig_data, &c->h_sig_off, &c->h_sig_len, &c->h_key_data, &c->h_key_off, &c->h_key_len,
                       &c->h_msg_data, &c->h_msg_off, &c->h_msg_len, &c->h_status, &c->h_bitmap, &c->t_salts,
                       &c->t_start, &c->t_group, &c->t_internal, &c->t_data, &c->t_off, &c->t_len, &c->t_ids,
@@ -329,9 +332,16 @@ void chip_shutdown(chip_ctx* c) {
 
 const char* chip_last_error(const chip_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
-static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap, hipStream_t st) {
+// One stream-ordered pipeline per batch.  Main stream: key prep -> classify -> every kernel that
+// needs no per-key table (Ed25519 plan + challenge/[S]B half, ECDSA grouping/DER/SHA/s^-1/u1 G)
+// -> the table halves (Ed25519 [h](-A), ECDSA u2 Q) once the aux stream has built the tables ->
+// finish / bitmap.  Aux stream: the per-key comb tables (serial doubling chains + fills), forked
+// right after key prep so they overlap everything table-free.
+static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap, hipStream_t st,
+                                bool is_valid) {
     const uint64_t n = b->n, nk = b->n_keys;
     if (n > 0xffffffffull) return fail(c, CHIP_E_ARG, "batch too large (n >= 2^32)");
+    const uint32_t schemes = b->schemes ? b->schemes : CHIP_SCHEMES_ALL;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, c->meta.ensure(nk * sizeof(KeyMeta) + 16));
     HIPCHK(c, c->abytes.ensure(nk * 32 + 16));
@@ -339,9 +349,24 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     HIPCHK(c, c->ectab.ensure(nk * EC_KEY_TABLE_WORDS * 4 + 16));
     HIPCHK(c, c->lists.ensure(n * 4 * N_LISTS + 16));
     HIPCHK(c, c->counts.ensure(64));
+    const bool comb_ok = !(c->flags & CHIP_FLAG_NO_COMB) && n && nk;
     // Ed25519 comb workspaces: slots <= min(keys, signatures / threshold, table budget)
-    const bool comb = !(c->flags & CHIP_FLAG_NO_COMB) && n && nk;
+    const bool comb = comb_ok && (schemes & (1u << CHIP_SCHEME_ED25519));
+    // ECDSA per-key comb tables for every EC key when keys sign many signatures (slot = key index)
+    const uint64_t ec_key_bytes = ecdsa_comb_key_words() * 4;
+    const bool ec_comb = comb_ok && (schemes & CHIP_SCHEMES_EC) && nk * ec_key_bytes <= c->comb_budget &&
+                         (n >= 16 * nk || (c->flags & CHIP_FLAG_FORCE_COMB));
     EdCombWs w{};
+    if (comb || ec_comb) {   // per-key histogram / grouping workspace shared by both comb paths
+        HIPCHK(c, c->c_key_count.ensure(nk * 4 + 16));
+        HIPCHK(c, c->c_key_base.ensure(nk * 4 + 16));
+        HIPCHK(c, c->c_key_cur.ensure(nk * 4 + 16));
+        HIPCHK(c, c->c_ctr.ensure(64));
+        w.key_count = c->c_key_count.as<uint32_t>();
+        w.key_base = c->c_key_base.as<uint32_t>();
+        w.key_cur = c->c_key_cur.as<uint32_t>();
+        w.ctr = c->c_ctr.as<uint32_t>();
+    }
     if (comb) {
         const uint64_t key_bytes = (uint64_t)ED_COMB_KEY_WORDS * 4;
         // eager: many signatures per key and every key's table fits the budget -> build all tables
@@ -352,37 +377,27 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
             slots = std::min<uint64_t>(slots, n / std::max<uint32_t>(1u, c->comb_min_sigs));
             slots = std::min<uint64_t>(slots, c->comb_budget / key_bytes);
         }
-        HIPCHK(c, c->c_key_count.ensure(nk * 4 + 16));
         HIPCHK(c, c->c_key_slot.ensure(nk * 4 + 16));
-        HIPCHK(c, c->c_key_base.ensure(nk * 4 + 16));
-        HIPCHK(c, c->c_key_cur.ensure(nk * 4 + 16));
         HIPCHK(c, c->c_slot_key.ensure(slots * 4 + 16));
-        HIPCHK(c, c->c_ctr.ensure(64));
         HIPCHK(c, c->c_comb_list.ensure(n * 4 + 16));
         HIPCHK(c, c->c_straus_list.ensure(n * 4 + 16));
         HIPCHK(c, c->c_ctab.ensure(slots * key_bytes + 16));
         HIPCHK(c, c->c_xyz.ensure(n * 30 * 4 + 16));
         HIPCHK(c, c->c_zpre.ensure(n * 10 * 4 + 16));
         HIPCHK(c, c->c_nega.ensure(nk * 40 * 4 + 16));
-        w.key_count = c->c_key_count.as<uint32_t>();
+        HIPCHK(c, c->c_bmid.ensure(n * ed_comb_bmid_words() * 4 + 16));
         w.key_slot = c->c_key_slot.as<int32_t>();
-        w.key_base = c->c_key_base.as<uint32_t>();
-        w.key_cur = c->c_key_cur.as<uint32_t>();
         w.slot_key = c->c_slot_key.as<uint32_t>();
-        w.ctr = c->c_ctr.as<uint32_t>();
         w.comb_list = c->c_comb_list.as<uint32_t>();
         w.straus_list = c->c_straus_list.as<uint32_t>();
         w.ctab = c->c_ctab.as<uint32_t>();
         w.xyz = c->c_xyz.as<uint32_t>();
         w.zpre = c->c_zpre.as<uint32_t>();
         w.nega = c->c_nega.as<uint32_t>();
+        w.bmid = c->c_bmid.as<uint32_t>();
         w.max_slots = (uint32_t)slots;
         w.min_sigs = c->comb_min_sigs;
     }
-    // ECDSA per-key comb tables for every EC key when keys sign many signatures (slot = key index)
-    const uint64_t ec_key_bytes = ecdsa_comb_key_words() * 4;
-    const bool ec_comb = !(c->flags & CHIP_FLAG_NO_COMB) && n && nk && nk * ec_key_bytes <= c->comb_budget &&
-                         (n >= 16 * nk || (c->flags & CHIP_FLAG_FORCE_COMB));
     if (ec_comb) {
         HIPCHK(c, c->e_ctab.ensure(nk * ec_key_bytes + 16));
         HIPCHK(c, c->e_mid.ensure(2 * n * ecdsa_comb_mid_words() * 4 + 16));
@@ -392,7 +407,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     HIPCHK(c, hipEventRecord(c->ev0, st));
     HIPCHK(c, hipMemsetAsync(c->counts.p, 0, 64, st));
     if (nk) HIPCHK(c, hipMemsetAsync(c->meta.p, 0, nk * sizeof(KeyMeta), st));
-    if (comb) {
+    if (comb || ec_comb) {
         HIPCHK(c, hipMemsetAsync(w.ctr, 0, 64, st));
         HIPCHK(c, hipMemsetAsync(w.key_count, 0, nk * 4, st));
         HIPCHK(c, hipMemsetAsync(w.key_cur, 0, nk * 4, st));
@@ -403,7 +418,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
                             c->edtab.as<uint32_t>(), comb ? w.nega : nullptr);
     if (comb && w.eager && n) {
         // fork: per-key comb tables on the aux stream, concurrent with ECDSA key prep, classify and
-        // the work-list partition on the main stream (the chain is a serial 252-doubling latency)
+        // every table-free kernel on the main stream (the chain is a serial 252-doubling latency)
         HIPCHK(c, hipEventRecord(c->ev_fork, st));
         HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
         const int kt = c->kbegin(CHIP_K_ED_TABLES, c->aux);
@@ -427,44 +442,31 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         uint32_t* lists = c->lists.as<uint32_t>();
         uint32_t* counts = c->counts.as<uint32_t>();
         hipLaunchKernelGGL(k_classify, dim3(blocks), dim3(256), 0, st, n, b->key_idx, b->msg_idx, b->sig_len, b->msg_len,
-                           nk, b->n_msgs, meta, status, lists, counts, comb ? w.key_count : nullptr);
+                           nk, b->n_msgs, meta, status, lists, counts, (comb || ec_comb) ? w.key_count : nullptr,
+                           is_valid ? 1u : 0u);
         const uint32_t* ed_list = lists + (uint64_t)LIST_ED25519 * n;
         const uint32_t* ed_count = counts + LIST_ED25519;
+        // ---- table-free kernels ----
         if (comb) {
             ke = c->kbegin(CHIP_K_ED_PLAN, st);
             launch_ed_comb_plan(st, n, nk, ed_list, ed_count, b, meta, w, false);
             launch_ed_comb_plan(st, n, nk, ed_list, ed_count, b, meta, w, true);
             c->kend(ke, st);
-            if (w.eager) {
-                HIPCHK(c, hipStreamWaitEvent(st, c->ev_join, 0));
-            } else {
-                ke = c->kbegin(CHIP_K_ED_TABLES, st);
-                launch_ed_comb_build(st, n, nk, meta, w);
-                c->kend(ke, st);
-            }
-            ke = c->kbegin(CHIP_K_ED_COMB, st);
-            launch_ed_comb_verify(st, n, b, c->abytes.as<uint32_t>(), w);
+            ke = c->kbegin(CHIP_K_ED_COMB_B, st);
+            launch_ed_comb_bhalf(st, n, b, c->abytes.as<uint32_t>(), w);
             c->kend(ke, st);
-            ke = c->kbegin(CHIP_K_ED_FINISH, st);
-            launch_ed_comb_finish(st, n, b, w, status);
-            c->kend(ke, st);
-            ed_list = w.straus_list;
-            ed_count = w.ctr + 2;
         }
-        ke = c->kbegin(CHIP_K_ED25519, st);
-        launch_ed25519_verify(st, n, ed_list, ed_count, b, c->abytes.as<uint32_t>(), c->edtab.as<uint32_t>(), status);
-        c->kend(ke, st);
+        const uint64_t mw = ecdsa_comb_mid_words();
+        uint32_t* mid_r1 = c->e_mid.as<uint32_t>();
+        uint32_t* mid_k1 = mid_r1 + n * mw;
+        uint32_t* gl_r1 = c->e_glist.as<uint32_t>();
+        uint32_t* gl_k1 = gl_r1 + n;
         if (ec_comb) {
-            // key-grouped work lists, then the table-free kernels (overlapping the per-key table build on
-            // the aux stream), then the u2 Q kernels once the tables are there
-            const uint64_t mw = ecdsa_comb_mid_words();
-            uint32_t* mid_r1 = c->e_mid.as<uint32_t>();
-            uint32_t* mid_k1 = mid_r1 + n * mw;
+            // key-grouped work lists, DER/SHA-256/s R + wave prefix products, one inversion per wave,
+            // s^-1 / u1 / u2 / u1 G
             uint32_t* wp_r1 = c->e_wp.as<uint32_t>();
             uint32_t* wp_k1 = wp_r1 + ecdsa_comb_wp_words(n);
-            uint32_t* gl_r1 = c->e_glist.as<uint32_t>();
-            uint32_t* gl_k1 = gl_r1 + n;
-            ke = c->kbegin(CHIP_K_ECDSA_R1, st);
+            ke = c->kbegin(CHIP_K_EC_FRONT, st);
             if (c->ec_group) {
                 launch_ecdsa_group(st, n, nk, meta, w.key_count, w.key_base, w.key_cur, w.ctr + 4, lists, counts,
                                    b->key_idx, gl_r1);
@@ -477,7 +479,32 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
             launch_ecdsa_comb_inv(st, n, counts, wp_r1, wp_k1);
             launch_ecdsa_comb_g(st, CHIP_SCHEME_R1, n, counts + LIST_R1, c->e_gcomb.as<uint32_t>(), mid_r1, wp_r1);
             launch_ecdsa_comb_g(st, CHIP_SCHEME_K1, n, counts + LIST_K1, c->e_gcomb.as<uint32_t>(), mid_k1, wp_k1);
+            c->kend(ke, st);
+        }
+        // ---- kernels that read the per-key tables ----
+        if (comb) {
+            if (w.eager) {
+                HIPCHK(c, hipStreamWaitEvent(st, c->ev_join, 0));
+            } else {
+                ke = c->kbegin(CHIP_K_ED_TABLES, st);
+                launch_ed_comb_build(st, n, nk, meta, w);
+                c->kend(ke, st);
+            }
+            ke = c->kbegin(CHIP_K_ED_COMB, st);
+            launch_ed_comb_ahalf(st, n, b, w);
+            c->kend(ke, st);
+            ke = c->kbegin(CHIP_K_ED_FINISH, st);
+            launch_ed_comb_finish(st, n, b, w, status);
+            c->kend(ke, st);
+            ed_list = w.straus_list;
+            ed_count = w.ctr + 2;
+        }
+        ke = c->kbegin(CHIP_K_ED25519, st);
+        launch_ed25519_verify(st, n, ed_list, ed_count, b, c->abytes.as<uint32_t>(), c->edtab.as<uint32_t>(), status);
+        c->kend(ke, st);
+        if (ec_comb) {
             HIPCHK(c, hipStreamWaitEvent(st, c->ev_join2, 0));
+            ke = c->kbegin(CHIP_K_ECDSA_R1, st);
             launch_ecdsa_comb_q(st, CHIP_SCHEME_R1, n, gl_r1, counts + LIST_R1, b, c->e_ctab.as<uint32_t>(), mid_r1,
                                 status);
             c->kend(ke, st);
@@ -506,14 +533,33 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     return CHIP_OK;
 }
 
-int chip_verify_batch_device(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap, void* stream) {
+// scheme hint of a host key pool: SPKI lengths of Ed25519 (44), secp256r1 (91 / 59), secp256k1 (88 / 56)
+static uint32_t host_scheme_hint(const chip_sig_batch* b) {
+    uint32_t m = 0;
+    for (uint64_t k = 0; k < b->n_keys && m != CHIP_SCHEMES_ALL; k++) {
+        const uint32_t L = b->key_len[k];
+        if (L == 44) m |= 1u << CHIP_SCHEME_ED25519;
+        else if (L == 91 || L == 59) m |= 1u << CHIP_SCHEME_R1;
+        else if (L == 88 || L == 56) m |= 1u << CHIP_SCHEME_K1;
+    }
+    return m ? m : CHIP_SCHEMES_ALL;
+}
+
+static int verify_device_entry(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap, void* stream,
+                               bool is_valid) {
     if (!c || !b || !status) return fail(c, CHIP_E_ARG, "null argument");
     std::lock_guard<std::mutex> g(c->mu);
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
-    return verify_device_locked(c, b, status, bitmap, st);
+    return verify_device_locked(c, b, status, bitmap, st, is_valid);
+}
+int chip_verify_batch_device(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap, void* stream) {
+    return verify_device_entry(c, b, status, bitmap, stream, false);
+}
+int chip_is_valid_batch_device(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap, void* stream) {
+    return verify_device_entry(c, b, status, bitmap, stream, true);
 }
 
-int chip_verify_batch(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap) {
+static int verify_host_entry(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap, bool is_valid) {
     if (!c || !b) return fail(c, CHIP_E_ARG, "null argument");
     const uint64_t n = b->n, nk = b->n_keys, nm = b->n_msgs;
     if ((n && (!b->key_idx || !b->msg_idx || !b->sig_off || !b->sig_len)) ||
@@ -554,7 +600,9 @@ int chip_verify_batch(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uin
     d.msg_data = c->h_msg_data.as<uint8_t>();
     d.msg_off = c->h_msg_off.as<uint64_t>();
     d.msg_len = c->h_msg_len.as<uint32_t>();
-    if ((r = verify_device_locked(c, &d, c->h_status.as<uint8_t>(), c->h_bitmap.as<uint64_t>(), st))) return r;
+    if (!d.schemes) d.schemes = host_scheme_hint(b);
+    if ((r = verify_device_locked(c, &d, c->h_status.as<uint8_t>(), c->h_bitmap.as<uint64_t>(), st, is_valid)))
+        return r;
     if (status && n) HIPCHK(c, hipMemcpyAsync(status, c->h_status.p, n, hipMemcpyDeviceToHost, st));
     if (bitmap && nw) HIPCHK(c, hipMemcpyAsync(bitmap, c->h_bitmap.p, nw * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
@@ -564,6 +612,22 @@ int chip_verify_batch(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uin
     if (status)
         for (uint64_t i = 0; i < n; i++) c->stats.status_count[status[i] & 7]++;
     return CHIP_OK;
+}
+int chip_verify_batch(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap) {
+    return verify_host_entry(c, b, status, bitmap, false);
+}
+int chip_is_valid_batch(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap) {
+    return verify_host_entry(c, b, status, bitmap, true);
+}
+
+int chip_alloc_pinned(uint64_t bytes, void** out) {
+    if (!out) return CHIP_E_ARG;
+    *out = nullptr;
+    if (!bytes) return CHIP_OK;
+    return hipHostMalloc(out, bytes, hipHostMallocDefault) == hipSuccess ? CHIP_OK : CHIP_E_NOMEM;
+}
+void chip_free_pinned(void* p) {
+    if (p) (void)hipHostFree(p);
 }
 
 int chip_get_stats(const chip_ctx* cc, chip_stats* out) {
@@ -700,7 +764,7 @@ static int verify_tx_device_locked(chip_ctx* c, const chip_tx_batch* tb, const c
     d.sig_bytes = sb->sig_bytes;
     d.key_bytes = sb->key_bytes;
     d.msg_bytes = nm * stride;
-    return verify_device_locked(c, &d, status, bitmap, st);
+    return verify_device_locked(c, &d, status, bitmap, st, false);
 }
 
 int chip_verify_tx_batch_device(chip_ctx* c, const chip_tx_batch* tb, const chip_msg_templates* tm,

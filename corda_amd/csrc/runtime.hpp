@@ -72,6 +72,7 @@ struct EdCombWs {
     uint32_t* xyz;          // [30][n] projective R' (SoA), comb path
     uint32_t* zpre;         // [10][n] prefix products of the batched inversion
     uint32_t* nega;         // [n_keys][40] -A in extended coordinates (key prep)
+    uint32_t* bmid;         // [48][n] [S]B (extended) + h, from the table-free half to the table half
     uint32_t max_slots, min_sigs;
     uint32_t eager;         // tables for every Ed25519 key at slot = key index, built during classify
 };
@@ -82,6 +83,10 @@ void launch_ed_comb_plan(hipStream_t st, uint64_t n, uint64_t n_keys, const uint
                          bool partition);
 // per-key comb tables (chain + fill); in eager mode independent of the signatures (second stream)
 void launch_ed_comb_build(hipStream_t st, uint64_t n, uint64_t n_keys, const KeyMeta* meta, const EdCombWs& w);
-void launch_ed_comb_verify(hipStream_t st, uint64_t n, const chip_sig_batch* b, const uint32_t* abytes,
-                           const EdCombWs& w);
+// the comb verify in two halves: bhalf (SHA-512 challenge + [S]B, no per-key table: runs while the
+// tables are built on the second stream) and ahalf (+ [h](-A) from the key's table)
+uint64_t ed_comb_bmid_words();
+void launch_ed_comb_bhalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, const uint32_t* abytes,
+                          const EdCombWs& w);
+void launch_ed_comb_ahalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w);
 void launch_ed_comb_finish(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w, uint8_t* status);

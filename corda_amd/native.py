@@ -31,7 +31,8 @@ SCHEME_K1, SCHEME_R1, SCHEME_ED25519 = 2, 3, 4
 
 # exported symbols declared in include/cordahip.h
 EXPORTS = ["chip_abi_version", "chip_device_count", "chip_init", "chip_shutdown", "chip_last_error",
-           "chip_verify_batch", "chip_verify_batch_device", "chip_txid_batch", "chip_txid_batch_device",
+           "chip_verify_batch", "chip_verify_batch_device", "chip_is_valid_batch", "chip_is_valid_batch_device",
+           "chip_alloc_pinned", "chip_free_pinned", "chip_txid_batch", "chip_txid_batch_device",
            "chip_uniq_open", "chip_uniq_close", "chip_uniq_size", "chip_uniq_rebuild", "chip_uniq_commit_batch",
            "chip_uniq_commit_batch_device", "chip_uniq_last_error", "chip_uniq_shard_begin", "chip_uniq_shard_vote",
            "chip_uniq_shard_apply", "chip_uniq_shard_classify", "chip_uniq_shard_finish",
@@ -54,7 +55,8 @@ class ChipSigBatch(ctypes.Structure):
                 ("n_keys", ctypes.c_uint64), ("key_data", ctypes.c_void_p), ("key_off", ctypes.c_void_p),
                 ("key_len", ctypes.c_void_p), ("n_msgs", ctypes.c_uint64), ("msg_data", ctypes.c_void_p),
                 ("msg_off", ctypes.c_void_p), ("msg_len", ctypes.c_void_p), ("sig_bytes", ctypes.c_uint64),
-                ("key_bytes", ctypes.c_uint64), ("msg_bytes", ctypes.c_uint64)]
+                ("key_bytes", ctypes.c_uint64), ("msg_bytes", ctypes.c_uint64), ("schemes", ctypes.c_uint32),
+                ("pad", ctypes.c_uint32)]
 
 
 class ChipTxBatch(ctypes.Structure):
@@ -113,8 +115,8 @@ class ChipConflict(ctypes.Structure):
 
 
 (K_ED25519, K_ECDSA_R1, K_ECDSA_K1, K_TXID, K_KEYPREP, K_UNIQ, K_ED_COMB, K_ED_FINISH, K_ED_TABLES, K_EC_TABLES,
- K_ED_PLAN) = range(11)
-N_KERNELS = 11
+ K_ED_PLAN, K_ED_COMB_B, K_EC_FRONT) = range(13)
+N_KERNELS = 16
 FLAG_NO_COMB, FLAG_FORCE_COMB = 0x1, 0x2
 
 
@@ -155,6 +157,10 @@ def load(build_if_missing: bool = False):
     lib.chip_verify_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipSigBatch), ctypes.c_void_p, ctypes.c_void_p]
     lib.chip_verify_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipSigBatch), ctypes.c_void_p,
                                              ctypes.c_void_p, ctypes.c_void_p]
+    lib.chip_is_valid_batch.argtypes = lib.chip_verify_batch.argtypes
+    lib.chip_is_valid_batch_device.argtypes = lib.chip_verify_batch_device.argtypes
+    lib.chip_alloc_pinned.argtypes = [ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]
+    lib.chip_free_pinned.argtypes = [ctypes.c_void_p]
     lib.chip_txid_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipTxBatch), ctypes.c_void_p]
     lib.chip_txid_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipTxBatch), ctypes.c_void_p,
                                            ctypes.c_void_p]
@@ -222,6 +228,7 @@ def make_sig_batch(b) -> ChipSigBatch:
     s.n_msgs = len(b.msg_off)
     s.msg_data, s.msg_off, s.msg_len = _ptr(b.msg_data), _ptr(b.msg_off), _ptr(b.msg_len)
     s.sig_bytes, s.key_bytes, s.msg_bytes = nbytes(b.sig_data), nbytes(b.key_data), nbytes(b.msg_data)
+    s.schemes = int(getattr(b, "schemes_hint", 0) or 0)
     return s
 
 
@@ -298,19 +305,22 @@ class Context:
             raise ChipError(rc, self.lib.chip_last_error(self.h).decode(errors="replace"))
 
     # ---- signatures ----
-    def verify_batch(self, b):
-        """Host SoA batch -> (status u8[n], bitmap u64[ceil(n/64)])."""
+    def verify_batch(self, b, is_valid: bool = False):
+        """Host SoA batch -> (status u8[n], bitmap u64[ceil(n/64)]).  is_valid=True gives
+        Crypto.isValid semantics (no empty-input checks) instead of Crypto.doVerify's."""
         s = make_sig_batch(b)
         status = np.zeros(s.n, dtype=np.uint8)
         bitmap = np.zeros((s.n + 63) // 64, dtype=np.uint64)
-        self._check(self.lib.chip_verify_batch(self.h, ctypes.byref(s), _ptr(status), _ptr(bitmap)))
+        fn = self.lib.chip_is_valid_batch if is_valid else self.lib.chip_verify_batch
+        self._check(fn(self.h, ctypes.byref(s), _ptr(status), _ptr(bitmap)))
         return status, bitmap
 
-    def verify_batch_device(self, dev_batch, status, bitmap, stream=None):
-        """Device-resident batch (torch tensors on this GPU); enqueued on `stream` (int handle)."""
+    def verify_batch_device(self, dev_batch, status, bitmap, stream=None, is_valid: bool = False):
+        """Device-resident batch (torch tensors on this GPU); enqueued on `stream` (int handle).
+        An optional `schemes_hint` attribute (bit 1 << scheme per scheme present) is passed through."""
         s = make_sig_batch(dev_batch)
-        self._check(self.lib.chip_verify_batch_device(self.h, ctypes.byref(s), _ptr(status), _ptr(bitmap),
-                                                      stream or None))
+        fn = self.lib.chip_is_valid_batch_device if is_valid else self.lib.chip_verify_batch_device
+        self._check(fn(self.h, ctypes.byref(s), _ptr(status), _ptr(bitmap), stream or None))
 
     # ---- tx ids ----
     def txid_batch(self, t) -> np.ndarray:

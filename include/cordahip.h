@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define CHIP_ABI_VERSION 3
+#define CHIP_ABI_VERSION 4
 
 enum chip_sig_status {
     CHIP_VALID = 0,
@@ -113,7 +113,16 @@ typedef struct {
     const uint64_t* msg_off;   /* [n_msgs]     */
     const uint32_t* msg_len;   /* [n_msgs]     */
     uint64_t sig_bytes, key_bytes, msg_bytes;  /* pool sizes in bytes */
+    /* optional hint: bit (1u << CHIP_SCHEME_*) set for every scheme whose keys may occur in the key
+     * pool; 0 = unknown.  Lets the device entry skip per-key table builds for absent schemes (the
+     * host entry derives it from the key pool itself).  Results never depend on it: a key of a
+     * scheme missing from the hint is still verified, on the windowed schedule. */
+    uint32_t schemes;
+    uint32_t pad;
 } chip_sig_batch;
+
+#define CHIP_SCHEMES_EC ((1u << CHIP_SCHEME_K1) | (1u << CHIP_SCHEME_R1))
+#define CHIP_SCHEMES_ALL (CHIP_SCHEMES_EC | (1u << CHIP_SCHEME_ED25519))
 
 /* Host buffers in, host buffers out (staged through pinned memory; blocking).
  * status: [n] bytes (may be NULL); bitmap: [ceil(n/64)] words (may be NULL). */
@@ -123,6 +132,19 @@ int chip_verify_batch(chip_ctx* ctx, const chip_sig_batch* batch, uint8_t* statu
  * Enqueued on `stream` (a hipStream_t; NULL = the context's stream); returns without waiting. */
 int chip_verify_batch_device(chip_ctx* ctx, const chip_sig_batch* batch, uint8_t* status,
                              uint64_t* bitmap, void* stream);
+
+/* Crypto.isValid(scheme, key, sig, clearData) semantics (Crypto.kt:615-625): no empty-input checks
+ * (those belong to doVerify, Crypto.kt:528-529).  An empty signature is the engine's decode error
+ * (CHIP_SIG_DECODE: Ed25519 "signature length is wrong", ECDSA DER decode); empty clear data is
+ * verified as an empty message.  Status codes otherwise as chip_verify_batch. */
+int chip_is_valid_batch(chip_ctx* ctx, const chip_sig_batch* batch, uint8_t* status, uint64_t* bitmap);
+int chip_is_valid_batch_device(chip_ctx* ctx, const chip_sig_batch* batch, uint8_t* status, uint64_t* bitmap,
+                               void* stream);
+
+/* Page-locked host memory for batch staging (the JNI layer's DirectByteBuffers); freed with
+ * chip_free_pinned.  Returns CHIP_E_NOMEM when the allocation fails. */
+int chip_alloc_pinned(uint64_t bytes, void** out);
+void chip_free_pinned(void* p);
 
 /* ---------------------------------------------------------------------------------------
  * Transaction-id batch (WireTransaction.id).  Components of transaction t are
@@ -316,12 +338,16 @@ int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_st
 
 /* ---------------------------------------------------------------------------------------
  * Counters (observability; OutOfProcessTransactionVerifierService.kt:35-46 analogue). */
-/* CHIP_K_ED_COMB = k_ed_comb_verify, CHIP_K_ED_TABLES / CHIP_K_EC_TABLES = per-key comb table builds
- * (on the context's second stream when every key gets a table), CHIP_K_ED_PLAN = slot assignment +
- * key-grouped work list; CHIP_K_ECDSA_R1/K1 time whichever ECDSA kernel ran (comb or windowed) */
+/* CHIP_K_ED_COMB = k_ed_comb_ahalf (+[h](-A) from the per-key table), CHIP_K_ED_COMB_B =
+ * k_ed_comb_bhalf (challenge hash + [S]B, no table), CHIP_K_ED_TABLES / CHIP_K_EC_TABLES = per-key comb
+ * table builds (on the context's second stream when every key gets a table), CHIP_K_ED_PLAN = slot
+ * assignment + key-grouped work list; CHIP_K_ECDSA_R1/K1 = the per-curve kernel that needs the key's
+ * table (k_ecdsa_comb_q, or k_ecdsa_verify on the windowed schedule), CHIP_K_EC_FRONT = the ECDSA comb
+ * kernels that need none (key grouping, DER/SHA-256/s R, batched s^-1, u1 G; both curves) */
 enum chip_kernel { CHIP_K_ED25519 = 0, CHIP_K_ECDSA_R1 = 1, CHIP_K_ECDSA_K1 = 2, CHIP_K_TXID = 3,
                    CHIP_K_KEYPREP = 4, CHIP_K_UNIQ = 5, CHIP_K_ED_COMB = 6, CHIP_K_ED_FINISH = 7,
-                   CHIP_K_ED_TABLES = 8, CHIP_K_EC_TABLES = 9, CHIP_K_ED_PLAN = 10, CHIP_N_KERNELS = 11 };
+                   CHIP_K_ED_TABLES = 8, CHIP_K_EC_TABLES = 9, CHIP_K_ED_PLAN = 10, CHIP_K_ED_COMB_B = 11,
+                   CHIP_K_EC_FRONT = 12, CHIP_N_KERNELS = 16 };
 typedef struct {
     uint64_t batches, sigs, keys_prepared;
     uint64_t status_count[8];

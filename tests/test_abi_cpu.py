@@ -33,7 +33,7 @@ def test_library_exports_every_header_function():
 
 def test_abi_version_and_device_count():
     lib = corda_amd.load()
-    assert lib.chip_abi_version() == 3
+    assert lib.chip_abi_version() == 4
     assert lib.chip_device_count() >= 0
 
 
@@ -63,7 +63,7 @@ def test_cpp_mirror_compiles(tmp_path):
 
 def test_struct_layouts_match_header():
     # ctypes mirrors of the ABI structs (offsets the C compiler would produce)
-    assert ctypes.sizeof(native.ChipSigBatch) == 8 * 17
+    assert ctypes.sizeof(native.ChipSigBatch) == 8 * 18   # 17 words + schemes hint / pad
     assert ctypes.sizeof(native.ChipTxBatch) == 8 * 10
     assert ctypes.sizeof(native.ChipConflict) == 8 + 4 + 4 + 32 + 4 + 4
     src = r'''

@@ -211,6 +211,63 @@ int gen_sign_many(int scheme, uint64_t n, const uint8_t* privs, const uint32_t* 
     return err ? -1 : 0;
 }
 
+/* ---------------- CPU baseline: OpenSSL EVP_DigestVerify over a SoA signature batch ----------------
+ * BASELINE.md / SURVEY §8d substitute (2): the reference JVM path cannot run here.  Keys are decoded
+ * once per thread and key (the JVM holds decoded PublicKey objects), every signature is one
+ * EVP_DigestVerifyInit + EVP_DigestVerify.  ok[i] = 1 valid, 0 otherwise. */
+typedef struct {
+    uint64_t lo, hi;
+    const uint32_t* key_idx; const uint32_t* msg_idx;
+    const uint8_t* sig_data; const uint64_t* sig_off; const uint32_t* sig_len;
+    uint64_t n_keys; const uint8_t* key_data; const uint64_t* key_off; const uint32_t* key_len;
+    const uint8_t* msg_data; const uint64_t* msg_off; const uint32_t* msg_len;
+    uint8_t* ok;
+} vjob;
+
+static void* vworker(void* p) {
+    vjob* j = (vjob*)p;
+    EVP_PKEY** keys = (EVP_PKEY**)calloc(j->n_keys ? j->n_keys : 1, sizeof(EVP_PKEY*));
+    EVP_MD_CTX* c = EVP_MD_CTX_new();
+    for (uint64_t i = j->lo; i < j->hi; i++) {
+        const uint32_t k = j->key_idx[i], m = j->msg_idx[i];
+        if (!keys[k]) {
+            const uint8_t* kp = j->key_data + j->key_off[k];
+            keys[k] = d2i_PUBKEY(NULL, &kp, (long)j->key_len[k]);
+        }
+        int v = 0;
+        if (keys[k]) {
+            const EVP_MD* md = EVP_PKEY_get_base_id(keys[k]) == EVP_PKEY_ED25519 ? NULL : EVP_sha256();
+            EVP_MD_CTX_reset(c);
+            if (EVP_DigestVerifyInit(c, NULL, md, NULL, keys[k]) == 1)
+                v = EVP_DigestVerify(c, j->sig_data + j->sig_off[i], j->sig_len[i], j->msg_data + j->msg_off[m],
+                                     j->msg_len[m]) == 1;
+        }
+        j->ok[i] = (uint8_t)v;
+    }
+    EVP_MD_CTX_free(c);
+    for (uint64_t k = 0; k < j->n_keys; k++)
+        if (keys[k]) EVP_PKEY_free(keys[k]);
+    free(keys);
+    return NULL;
+}
+
+int ossl_verify_many(uint64_t n, const uint32_t* key_idx, const uint32_t* msg_idx, const uint8_t* sig_data,
+                     const uint64_t* sig_off, const uint32_t* sig_len, uint64_t n_keys, const uint8_t* key_data,
+                     const uint64_t* key_off, const uint32_t* key_len, const uint8_t* msg_data, const uint64_t* msg_off,
+                     const uint32_t* msg_len, uint8_t* ok, int threads) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t th[256];
+    vjob jobs[256];
+    for (int t = 0; t < threads; t++) {
+        jobs[t] = (vjob){n * t / threads, n * (t + 1) / threads, key_idx, msg_idx, sig_data, sig_off, sig_len, n_keys,
+                         key_data, key_off, key_len, msg_data, msg_off, msg_len, ok};
+        pthread_create(&th[t], NULL, vworker, &jobs[t]);
+    }
+    for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+    return 0;
+}
+
 /* pubs for many keys: Ed25519 -> 32 B each, EC -> 65 B each */
 int gen_pubs_many(int scheme, uint64_t n, const uint8_t* privs, uint8_t* out) {
     for (uint64_t i = 0; i < n; i++) {

@@ -87,6 +87,16 @@ def ossl_verify(spki: bytes, sig: bytes, msg: bytes) -> int:
                                   msg, ctypes.c_size_t(len(msg)))
 
 
+def ossl_verify_batch(b, threads: int = 8) -> np.ndarray:
+    """OpenSSL EVP_DigestVerify over a SigBatch (CPU baseline): uint8[n], 1 = valid."""
+    n = len(b.key_idx)
+    ok = np.zeros(n, dtype=np.uint8)
+    lib().ossl_verify_many(ctypes.c_uint64(n), _p(b.key_idx), _p(b.msg_idx), _p(b.sig_data), _p(b.sig_off),
+                           _p(b.sig_len), ctypes.c_uint64(len(b.key_off)), _p(b.key_data), _p(b.key_off),
+                           _p(b.key_len), _p(b.msg_data), _p(b.msg_off), _p(b.msg_len), _p(ok), int(threads))
+    return ok
+
+
 def spki_ed25519(a: bytes) -> bytes:
     return SPKI_ED25519 + a
 
