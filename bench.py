@@ -450,6 +450,10 @@ def main():
         t2 = time.perf_counter()
         ok = G.ossl_verify_batch(subo, threads=threads)
         oel = time.perf_counter() - t2
+        s1 = sub_batch(G, batch, min(8192, n))
+        t2 = time.perf_counter()
+        G.ossl_verify_batch(s1, threads=1)
+        one_thread = len(s1.key_idx) / (time.perf_counter() - t2)
         eb = G.ecdsa_batch(8192, n_keys=256, seed=0x5EED0023, threads=gen_threads)
         ec_rates = {}
         for name, sch in (("p256", G.SCHEME_R1), ("secp256k1", G.SCHEME_K1)):
@@ -467,6 +471,8 @@ def main():
         cpu_ossl = {"value": mo / oel, "unit": "verified Ed25519 sigs/s", "cores": threads, "kind": "openssl",
                     "sample": "first %d signatures of the cfg2 batch, OpenSSL %s EVP_DigestVerify; %s"
                               % (mo, "3.x", share_note),
+                    "single_thread_sigs_per_s": one_thread,
+                    "thread_scaling": (mo / oel) / one_thread,
                     "ecdsa_p256_sigs_per_s": ec_rates["p256"], "ecdsa_secp256k1_sigs_per_s": ec_rates["secp256k1"],
                     "note": "OpenSSL rejects the i2p-specific reference-valid classes (S+L, small-order forgeries): "
                             "%d of %d accepted vs %d reference-valid" % (int(ok.sum()), mo,

@@ -25,7 +25,8 @@ from typing import Callable, Dict, Iterable, List, Optional, Sequence, Set, Tupl
 import numpy as np
 
 from .native import (VALID, INVALID, SIG_DECODE, EMPTY_SIG, EMPTY_CLEAR, UNSUPPORTED, KEY_INVALID)
-from .composite import CompositeKey, as_key, is_fulfilled_by
+from .composite import CompositeKey, IllegalArgumentException, as_key, is_fulfilled_by
+from . import kryo
 
 
 # ---- exceptions (java.security / IllegalArgumentException / Corda exceptions) ----
@@ -34,10 +35,6 @@ class SignatureException(Exception):
 
 
 class InvalidKeyException(Exception):
-    pass
-
-
-class IllegalArgumentException(ValueError):
     pass
 
 
@@ -60,6 +57,11 @@ class UniquenessException(Exception):
     def __init__(self, conflict: "Conflict"):
         super().__init__("UniquenessException")
         self.error = conflict
+
+
+class CommitLogFailure(RuntimeError):
+    """The commit log could not be made durable: the provider stops accepting commits (fail-stop)
+    and must be reopened, which rebuilds the table from the rows that did reach the log."""
 
 
 class NotaryException(Exception):
@@ -157,11 +159,15 @@ def _pool(items: List[bytes]):
     return data, off, lens
 
 
-def verify_statuses(engine, items: Sequence[Tuple[bytes, bytes, bytes]]) -> np.ndarray:
-    """CHIP_* status of every (key, signature, clear data) triple, one engine call."""
+def verify_statuses(engine, items: Sequence[Tuple[bytes, bytes, bytes]], is_valid: bool = False) -> np.ndarray:
+    """CHIP_* status of every (key, signature, clear data) triple, one engine call.  is_valid=True:
+    Crypto.isValid semantics (chip_is_valid_batch: no empty-input checks, Crypto.kt:615-625)."""
     if not items:
         return np.zeros(0, dtype=np.uint8)
-    status, _ = engine.verify_batch(SigBatch(items))
+    if is_valid:
+        status, _ = engine.verify_batch(SigBatch(items), is_valid=True)
+    else:
+        status, _ = engine.verify_batch(SigBatch(items))
     return status
 
 
@@ -182,8 +188,10 @@ class Crypto:
 
     @staticmethod
     def is_valid(engine, public_key: bytes, signature_data: bytes, clear_data: bytes) -> bool:
-        """False on a bad signature; engine decode errors still throw (Crypto.kt:600-625)."""
-        st = int(verify_statuses(engine, [(public_key, signature_data, clear_data)])[0])
+        """False on a bad signature; engine decode errors still throw (Crypto.kt:600-625).  No empty
+        checks: an empty signature is the engine's decode SignatureException, empty clear data is
+        verified as the empty message."""
+        st = int(verify_statuses(engine, [(public_key, signature_data, clear_data)], is_valid=True)[0])
         if st == VALID:
             return True
         if st == INVALID:
@@ -198,21 +206,17 @@ class SignatureMetadata:
     scheme_number_id: int = 4
 
 
-_SIGNABLE_HEAD = (b"corda\x00\x00\x01" + b"\x01\x00net.corda.core.crypto.SignableData\x01\x01"
-                  b"net.corda.core.crypto.SecureHash$SHA256\x01\x02net.corda.core.crypto.SignatureMetadata")
-
-
-def signable_template(meta: SignatureMetadata, total: int = 200) -> Tuple[bytes, int]:
-    """(template bytes without the id, id offset) of the SignableData bytes for `meta`: Kryo's exact
-    bytes are unpinned without a JVM; for one metadata value they are a fixed byte
-    string with the 32-byte id at a fixed offset, which is what chip_verify_tx_batch relies on."""
-    head = (_SIGNABLE_HEAD + bytes(200))[:total - 32 - 8]
-    return head + struct.pack(">ii", meta.platform_version, meta.scheme_number_id), len(head)
+def signable_template(meta: SignatureMetadata) -> Tuple[bytes, int]:
+    """(template bytes without the id, id offset) of SignableData(txId, meta).serialize() — the Kryo
+    4.0.0 P2P-context bytes restated in corda_amd.kryo (parity unpinned: no JVM, no reference-held
+    bytes).  For one metadata value the message is a fixed byte string with the 32-byte id at a fixed
+    offset, which is what chip_verify_tx_batch relies on."""
+    return kryo.signable_data_template(meta.platform_version, meta.scheme_number_id)
 
 
 def signable_data_bytes(tx_id: bytes, meta: SignatureMetadata) -> bytes:
-    t, at = signable_template(meta)
-    return t[:at] + tx_id + t[at:]
+    """SignableData(txId, meta).serialize().bytes (Crypto.kt:550-578, SignableData.kt:12-13)."""
+    return kryo.signable_data(tx_id, meta.platform_version, meta.scheme_number_id)
 
 
 Serializer = Callable[[bytes, SignatureMetadata], bytes]
@@ -278,19 +282,23 @@ def _short(k) -> str:
 
 def composite_signature_verify(engine, verify_key, sigs: Sequence[TransactionSignature], clear_data: bytes,
                                serializer: Serializer = signable_data_bytes) -> bool:
-    """CompositeSignature.State.engineVerify (CompositeSignature.kt:78-86): the composite key must be
-    fulfilled by the signers, then every component signature must be valid over SHA256(clear_data) as
-    a transaction id (TransactionSignature.isValid) — all of them in one engine call."""
-    import hashlib
+    """CompositeSignature.State.engineVerify (CompositeSignature.kt:77-86): the composite key must be
+    fulfilled by the signers; then the buffered clear data IS the transaction id —
+    SecureHash.SHA256(bytes) wraps the 32 bytes without hashing and requires size == 32
+    (SecureHash.kt:16-19) — and every component signature must pass TransactionSignature.isValid(id)
+    (Crypto.isValid semantics), all of them in one engine call.  `sigs.all {}` stops at the first
+    false, so a decode failure after an invalid signature does not throw."""
     key = as_key(verify_key)
     if not isinstance(key, CompositeKey):
         raise IllegalArgumentException("verify key is not a CompositeKey")
     if not key.is_fulfilled_by([s.by for s in sigs]):
         return False
-    tx_id = hashlib.sha256(clear_data).digest()
+    if len(clear_data) != 32:
+        raise IllegalArgumentException("Provided bytes are not 32 bytes long")
+    tx_id = bytes(clear_data)
     items = [(s.by, s.bytes, serializer(tx_id, s.signature_metadata)) for s in sigs]
-    for st, s in zip(verify_statuses(engine, items), sigs):
-        if st == INVALID:      # isValid: false; decode / argument failures throw as Crypto.isValid does
+    for st, s in zip(verify_statuses(engine, items, is_valid=True), sigs):
+        if st == INVALID:
             return False
         if st != VALID:
             _raise_for(int(st), s.by)
@@ -441,9 +449,11 @@ class CommitLog:
     """Append-only on-disk commit log of the notary (the role of the `notary_commit_log` table behind
     AppendOnlyPersistentMap, PersistentUniquenessProvider.kt:50-89): fixed 76-byte rows, appended in
     commit order after each batch; `load()` memory-maps the file for the table rebuild at open
-    (AppendOnlyPersistentMap.allPersisted).  A torn final row (crash mid-append) is ignored."""
+    (AppendOnlyPersistentMap.allPersisted).  A torn final row (crash mid-append) is ignored.
+    `append` returns only once the rows are durable (fsync, the role of the reference's database
+    transaction commit); fsync=False trades that for speed in benchmarks and tests only."""
 
-    def __init__(self, path: str, fsync: bool = False):
+    def __init__(self, path: str, fsync: bool = True):
         self.path = path
         self.fsync = fsync
         self._f = open(path, "ab")
@@ -479,9 +489,10 @@ class PersistentUniquenessProvider:
     are also appended to an on-disk CommitLog and the table is rebuilt from it at open, so a restarted
     notary rejects double spends of states committed before the restart."""
 
-    def __init__(self, engine, capacity: int = 1 << 20, log_path: Optional[str] = None, fsync: bool = False):
+    def __init__(self, engine, capacity: int = 1 << 20, log_path: Optional[str] = None, fsync: bool = True):
         self.table = engine.uniq_open(capacity)
         self.log = None
+        self._failed: Optional[BaseException] = None
         if log_path is not None:
             self.log = CommitLog(log_path, fsync)
             rows = self.log.load()
@@ -516,7 +527,13 @@ class PersistentUniquenessProvider:
 
     def commit_batch(self, requests: Sequence[Tuple[List[StateRef], bytes, int]]):
         """[(states, txId, callerIdentity)] applied in order -> [(status, Conflict)]; status 0 committed,
-        1 re-notarisation of the same tx (commitInputStates accepts it), 2 conflict."""
+        1 re-notarisation of the same tx (commitInputStates accepts it), 2 conflict.  With a commit
+        log, results are returned only after the committed rows are durable; if the append fails
+        the provider fails stop (CommitLogFailure now and on every later call): the device table is
+        then ahead of the log, and only a reopen — which rebuilds it from the log — may serve again.
+        No result of the failed batch was reported, so its transactions were never acknowledged."""
+        if self._failed is not None:
+            raise CommitLogFailure("commit log append failed earlier; reopen the provider") from self._failed
         start = [0]
         refs, ids, callers = [], [], []
         for states, tx_id, caller in requests:
@@ -532,7 +549,11 @@ class PersistentUniquenessProvider:
         for tx, i, ci, cid, cc in recs:
             out[tx][1].state_history.append((requests[tx][0][i], ConsumingTx(cid, ci, cc)))
         if self.log is not None:
-            self._log_committed(requests, [o[0] for o in out])
+            try:
+                self._log_committed(requests, [o[0] for o in out])
+            except BaseException as e:
+                self._failed = e
+                raise CommitLogFailure("commit log append failed: %s" % e) from e
         return out
 
     def commit(self, states: List[StateRef], tx_id: bytes, caller_identity: int):

@@ -89,21 +89,33 @@ __global__ void __launch_bounds__(256) k_ed_comb_slots(uint64_t n_keys, const Ke
     key_slot[k] = slot;
 }
 
+// The comb path only pays when enough signatures take it: its table chain is a fixed serial latency
+// (~0.5 ms) that a few thousand hot-key signatures do not amortise, so below `min_total` comb-bound
+// signatures the whole list goes to the Straus kernel.  The gated counts (ctr[ED_CTR_NCOMB],
+// ctr[ED_CTR_NSLOTS]) are what every later comb kernel reads; ctr[0..1] stay the raw assignment.
+#define ED_CTR_NCOMB 8
+#define ED_CTR_NSLOTS 9
 __global__ void __launch_bounds__(256) k_ed_comb_partition(const uint32_t* __restrict__ ed_list,
                                                            const uint32_t* __restrict__ ed_count,
                                                            const uint32_t* __restrict__ key_idx,
                                                            const int32_t* __restrict__ key_slot,
                                                            const uint32_t* __restrict__ key_base,
                                                            uint32_t* __restrict__ key_cur, uint32_t* __restrict__ comb_list,
-                                                           uint32_t* __restrict__ straus_list, uint32_t* __restrict__ ctr) {
+                                                           uint32_t* __restrict__ straus_list, uint32_t* __restrict__ ctr,
+                                                           uint32_t min_total, uint32_t max_slots) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t lane = threadIdx.x & 63;
+    const bool on = ctr[1] >= min_total;
+    if (g == 0) {
+        ctr[ED_CTR_NCOMB] = on ? ctr[1] : 0u;
+        ctr[ED_CTR_NSLOTS] = on ? min(ctr[0], max_slots) : 0u;
+    }
     bool straus = false, comb = false;
     uint32_t i = 0, k = 0;
     if (g < *ed_count) {
         i = ed_list[g];
         k = key_idx[i];
-        comb = key_slot[k] >= 0;
+        comb = on && key_slot[k] >= 0;
         straus = !comb;
     }
     // one fill-cursor atomic per key per wave (a single-key batch must not serialize on key_cur)
@@ -133,7 +145,7 @@ __global__ void __launch_bounds__(64) k_ed_comb_chain(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ slot_key,
                                                       const uint32_t* __restrict__ nega, uint32_t* __restrict__ ctab) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t nslots = eager ? max_slots : min(ctr[0], max_slots);
+    const uint32_t nslots = eager ? max_slots : ctr[ED_CTR_NSLOTS];
     if (s >= nslots) return;
     if (eager && !ed_key_ok(meta, s)) return;
     const uint32_t k = eager ? s : slot_key[s];
@@ -162,7 +174,7 @@ __global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict
                                                       uint32_t* __restrict__ ctab) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t s = g / ED_COMB_AWIN, w = g % ED_COMB_AWIN;
-    if (s >= (eager ? max_slots : min(ctr[0], max_slots))) return;
+    if (s >= (eager ? max_slots : ctr[ED_CTR_NSLOTS])) return;
     if (eager && !ed_key_ok(meta, s)) return;
     uint32_t* e = ctab + (uint64_t)s * ED_COMB_KEY_WORDS + (uint64_t)w * ED_COMB_AENT * 40;
     ge_p3 P;
@@ -216,7 +228,7 @@ __global__ void __launch_bounds__(256) k_ed_comb_bhalf(const uint32_t* __restric
                                                        const uint32_t* __restrict__ abytes, uint32_t* __restrict__ bmid,
                                                        uint64_t cap) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= ctr[1]) return;
+    if (p >= ctr[ED_CTR_NCOMB]) return;
     const uint32_t i = list[p];
     const uint32_t k = key_idx[i];
     const uint32_t mi = msg_idx[i];
@@ -282,7 +294,7 @@ __global__ void __launch_bounds__(256, 2) ED_AHALF_WAVES k_ed_comb_ahalf(const u
                                                        const uint32_t* __restrict__ ctab,
                                                        const uint32_t* __restrict__ bmid, uint32_t* __restrict__ xyz,
                                                        uint64_t cap) {
-    const uint32_t ncomb = ctr[1];
+    const uint32_t ncomb = ctr[ED_CTR_NCOMB];
     const uint32_t p = xcd_block(blockIdx.x, (ncomb + 255) / 256) * blockDim.x + threadIdx.x;
     if (p >= ncomb) return;
     const uint32_t k = key_idx[list[p]];
@@ -337,7 +349,7 @@ __global__ void __launch_bounds__(256) k_ed_comb_finish(const uint32_t* __restri
                                                         const uint64_t* __restrict__ sig_off,
                                                         const uint32_t* __restrict__ xyz, uint32_t* __restrict__ zpre,
                                                         uint64_t cap, uint8_t* __restrict__ status) {
-    const uint32_t n = ctr[1];
+    const uint32_t n = ctr[ED_CTR_NCOMB];
     const uint32_t lanes = (n + ED_FIN_G - 1) / ED_FIN_G;
     const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= lanes) return;
@@ -396,7 +408,8 @@ void launch_ed_comb_plan(hipStream_t st, uint64_t n, uint64_t n_keys, const uint
         return;
     }
     hipLaunchKernelGGL(k_ed_comb_partition, dim3(nblk(n, 256)), dim3(256), 0, st, ed_list, ed_count, b->key_idx,
-                       w.key_slot, w.key_base, w.key_cur, w.comb_list, w.straus_list, w.ctr);
+                       w.key_slot, w.key_base, w.key_cur, w.comb_list, w.straus_list, w.ctr,
+                       w.eager ? 0u : w.min_total, w.max_slots);
 }
 
 void launch_ed_comb_build(hipStream_t st, uint64_t n, uint64_t n_keys, const KeyMeta* meta, const EdCombWs& w) {

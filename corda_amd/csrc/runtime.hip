@@ -40,6 +40,9 @@ struct chip_ctx {
     int device = 0;
     uint32_t flags = 0;
     uint32_t comb_min_sigs = 4;                   // Ed25519 comb threshold (signatures per key)
+    // comb paths only for batches with at least this many table-bound signatures: below it the serial
+    // table chains (Ed25519 ~0.5 ms, ECDSA ~2.4 ms) cost more than the Straus / windowed kernels save
+    uint32_t comb_min_total = 65536;
     bool ec_group = true;                         // ECDSA comb lists grouped by key (CHIP_EC_GROUP=0 off)
     uint64_t comb_budget = 8ull << 30;            // bytes of per-key comb tables
     hipStream_t stream = nullptr;
@@ -286,9 +289,10 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
         chip_shutdown(c);
         return CHIP_E_DEVICE;
     }
-    if (c->flags & CHIP_FLAG_FORCE_COMB) c->comb_min_sigs = 1;
+    if (c->flags & CHIP_FLAG_FORCE_COMB) c->comb_min_sigs = 1, c->comb_min_total = 0;
     if (const char* e = getenv("CHIP_EC_GROUP")) c->ec_group = e[0] != '0';
     if (const char* e = getenv("CHIP_COMB_MIN_SIGS")) c->comb_min_sigs = (uint32_t)strtoul(e, nullptr, 10);
+    if (const char* e = getenv("CHIP_COMB_MIN_TOTAL")) c->comb_min_total = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("CHIP_COMB_BUDGET_MB")) c->comb_budget = (uint64_t)strtoull(e, nullptr, 10) << 20;
     if (cfg && cfg->reserve_sigs) {
         (void)c->lists.ensure(cfg->reserve_sigs * 4 * N_LISTS);
@@ -355,7 +359,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     // ECDSA per-key comb tables for every EC key when keys sign many signatures (slot = key index)
     const uint64_t ec_key_bytes = ecdsa_comb_key_words() * 4;
     const bool ec_comb = comb_ok && (schemes & CHIP_SCHEMES_EC) && nk * ec_key_bytes <= c->comb_budget &&
-                         (n >= 16 * nk || (c->flags & CHIP_FLAG_FORCE_COMB));
+                         ((n >= 16 * nk && n >= c->comb_min_total) || (c->flags & CHIP_FLAG_FORCE_COMB));
     EdCombWs w{};
     if (comb || ec_comb) {   // per-key histogram / grouping workspace shared by both comb paths
         HIPCHK(c, c->c_key_count.ensure(nk * 4 + 16));
@@ -371,7 +375,8 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         const uint64_t key_bytes = (uint64_t)ED_COMB_KEY_WORDS * 4;
         // eager: many signatures per key and every key's table fits the budget -> build all tables
         // (slot = key index) on the aux stream while classify runs; else tables for hot keys only
-        w.eager = (n >= 16 * nk && nk * key_bytes <= c->comb_budget && !(c->flags & CHIP_FLAG_FORCE_COMB)) ? 1u : 0u;
+        w.eager = (n >= 16 * nk && n >= c->comb_min_total && nk * key_bytes <= c->comb_budget &&
+                   !(c->flags & CHIP_FLAG_FORCE_COMB)) ? 1u : 0u;
         uint64_t slots = nk;
         if (!w.eager) {
             slots = std::min<uint64_t>(slots, n / std::max<uint32_t>(1u, c->comb_min_sigs));
@@ -397,6 +402,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         w.bmid = c->c_bmid.as<uint32_t>();
         w.max_slots = (uint32_t)slots;
         w.min_sigs = c->comb_min_sigs;
+        w.min_total = c->comb_min_total;
     }
     if (ec_comb) {
         HIPCHK(c, c->e_ctab.ensure(nk * ec_key_bytes + 16));

@@ -65,7 +65,8 @@ struct EdCombWs {
     uint32_t* key_base;     // [n_keys] first position of the key's signatures in comb_list
     uint32_t* key_cur;      // [n_keys] fill cursor (zeroed per batch)
     uint32_t* slot_key;     // [max_slots]
-    uint32_t* ctr;          // [0] slots claimed, [1] comb signatures, [2] Straus signatures
+    uint32_t* ctr;          // [0] slots claimed, [1] comb signatures, [2] Straus signatures, [4..5] ECDSA
+                            // grouping, [8] / [9] comb signatures / slots after the min_total gate
     uint32_t* comb_list;    // [n] signature indices grouped by key
     uint32_t* straus_list;  // [n]
     uint32_t* ctab;         // [max_slots][ED_COMB_KEY_WORDS]
@@ -74,7 +75,8 @@ struct EdCombWs {
     uint32_t* nega;         // [n_keys][40] -A in extended coordinates (key prep)
     uint32_t* bmid;         // [48][n] [S]B (extended) + h, from the table-free half to the table half
     uint32_t max_slots, min_sigs;
-    uint32_t eager;         // tables for every Ed25519 key at slot = key index, built during classify
+    uint32_t min_total;     // fewer comb-bound signatures than this: all go to Straus (non-eager)
+    uint32_t eager;        // tables for every Ed25519 key at slot = key index, built during classify
 };
 
 // slots (partition = false) or the key-grouped work list (partition = true)

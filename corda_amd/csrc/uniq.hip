@@ -14,9 +14,13 @@
 // the key space one GPU owns (all of it on a single GPU).  A shard sees every transaction of the
 // batch but only its own inputs ("local refs", grouped by tx, each carrying its position in the
 // tx's input list):
-//   begin     lookup every local input in the table (pre-committed?)               k_uniq_lookup
-//             intern the distinct states of the batch in a scratch table            k_uniq_intern
+//   begin     lookup every local input in the table (pre-committed?) and intern the distinct
+//             states of the batch in a scratch table, one kernel                    k_uniq_lookup
+//             states referenced more than once in the batch ("dup" states, found by the intern)
+//             are the only ones the rounds and the records need: a state with one referencer is
+//             never contended inside the batch (per-ref flag rdup, set by the intern)
 //   rounds    vote: first(s) = min tx among the live (not failed) referencers of s; k_uniq_round_min
+//                   (over the dup states' refs only)
 //                   for every undecided tx t: 2 (fail) when a local input is pre-committed or
 //                   first(s) is an earlier COMMITTED tx, else 1 (wait) when first(s) is an earlier
 //                   undecided tx, else 0 (commit as far as this shard knows)          k_uniq_vote
@@ -31,6 +35,14 @@
 //   finish    Conflict.stateHistory records (one per consumed distinct input, ordered by
 //             (tx, input index) through a prefix sum), inserts of committed txs (first index of a
 //             repeated input wins), final status bytes       k_uniq_flag / k_uniq_emit / k_uniq_insert
+//
+// Atomics on MI355X execute at the memory side, one 64-B request per lane for scattered addresses,
+// so none touches the 128-B-slot table: slots are claimed in an occupancy bitmap (1 bit per slot,
+// cap/8 bytes, Infinity-Cache resident) and the slot is then written with plain stores.  An insert
+// starts its claim at the first empty slot its lookup met on the probe path (usually the slot it
+// gets); the round / commit scratch (bmin, bcommit) is written only for dup states, bcommit with
+// plain stores (at most one committed tx consumes a state: a later referencer of a committed state
+// fails, an earlier one's commit makes it fail).
 #include <mutex>
 #include <string>
 #include <vector>
@@ -78,6 +90,7 @@ struct chip_uniq {
     hipStream_t stream = nullptr;
     uint64_t cap = 0, size = 0;
     uint32_t* tab = nullptr;   // [cap][SLOT_W]
+    uint32_t* bits = nullptr;  // [cap / 32] occupancy bitmap (slot claims)
     std::string err;
     // batch in flight (between shard_begin and shard_finish)
     bool open = false;
@@ -89,7 +102,8 @@ struct chip_uniq {
     const uint8_t* ids = nullptr;
     const uint32_t* callers = nullptr;
     // scratch
-    UBuf reftx, pre, bslot, bowner, bmin, bcommit, st, flag, scan, cub, ctr, refpos;
+    UBuf reftx, pre, empty, bslot, bowner, rdup, bmin, bcommit, st, flag, scan, cub, ctr, spread, refpos;
+    unsigned long long* h_spread = nullptr;   // pinned host copy of the SPREAD counters
     // staging of the host entry points
     UBuf h_start, h_refs, h_ids, h_call, h_st, h_vote, h_out;
 };
@@ -119,15 +133,19 @@ CHIP_DEV bool key_eq(const uint32_t* a, const uint32_t k[KW]) {
     return d == 0;
 }
 
-// probe: slot index of k or NO_SLOT.  A slot's first 40 bytes (key + used) are read as 2x16 B + 8 B.
-CHIP_DEV uint32_t tab_find(const uint32_t* __restrict__ tab, uint64_t cap, const uint32_t k[KW]) {
+// probe: slot index of k or NO_SLOT (then *empty = the empty slot that ended the probe, where an
+// insert of k starts its claim).  A slot's first 40 bytes (key + used) are read as 2x16 B + 8 B.
+CHIP_DEV uint32_t tab_find(const uint32_t* __restrict__ tab, uint64_t cap, const uint32_t k[KW], uint32_t* empty) {
     uint64_t i = key_hash(k) & (cap - 1);
     for (uint64_t n = 0; n < cap; n++) {
         const uint32_t* s = tab + i * SLOT_W;
         const uint4 a = *reinterpret_cast<const uint4*>(s);
         const uint4 b = *reinterpret_cast<const uint4*>(s + 4);
         const uint2 c = *reinterpret_cast<const uint2*>(s + 8);
-        if (!c.y) return NO_SLOT;
+        if (!c.y) {
+            *empty = (uint32_t)i;
+            return NO_SLOT;
+        }
         const uint32_t d = (a.x ^ k[0]) | (a.y ^ k[1]) | (a.z ^ k[2]) | (a.w ^ k[3]) | (b.x ^ k[4]) | (b.y ^ k[5]) |
                            (b.z ^ k[6]) | (b.w ^ k[7]) | (c.x ^ k[8]);
         if (!d) return (uint32_t)i;
@@ -136,42 +154,46 @@ CHIP_DEV uint32_t tab_find(const uint32_t* __restrict__ tab, uint64_t cap, const
     return NO_SLOT;
 }
 
-// claim an empty slot for k (k absent from the table and distinct among concurrent inserters)
-CHIP_DEV void tab_put(uint32_t* tab, uint64_t cap, const uint32_t k[KW], const uint32_t v[10]) {
-    uint64_t i = key_hash(k) & (cap - 1);
+// claim an empty slot for k at or after slot i0 (k absent from the table and distinct among
+// concurrent inserters): the claim is one atomicOr on the occupancy bitmap (a plain read skips
+// slots already known to be taken), the slot is then written with plain stores
+CHIP_DEV void tab_put(uint32_t* tab, uint32_t* bits, uint64_t cap, uint64_t i0, const uint32_t k[KW],
+                      const uint32_t v[10]) {
+    uint64_t i = i0 & (cap - 1);
     for (uint64_t n = 0; n < cap; n++) {
-        uint32_t* s = tab + i * SLOT_W;
-        if (atomicCAS(&s[S_USED], 0u, 1u) == 0u) {
-            *reinterpret_cast<uint4*>(s) = make_uint4(k[0], k[1], k[2], k[3]);
-            *reinterpret_cast<uint4*>(s + 4) = make_uint4(k[4], k[5], k[6], k[7]);
-            s[8] = k[8];
-            *reinterpret_cast<uint2*>(s + 10) = make_uint2(v[0], v[1]);
-            *reinterpret_cast<uint4*>(s + 12) = make_uint4(v[2], v[3], v[4], v[5]);
-            *reinterpret_cast<uint4*>(s + 16) = make_uint4(v[6], v[7], v[8], v[9]);
+        const uint32_t m = 1u << (i & 31);
+        if (!(__builtin_nontemporal_load(&bits[i >> 5]) & m) && !(atomicOr(&bits[i >> 5], m) & m)) {
+            // the whole 128-B line (zero tail): a partial line would cost a read-modify-write in HBM
+            uint4* s = reinterpret_cast<uint4*>(tab + i * SLOT_W);
+            s[0] = make_uint4(k[0], k[1], k[2], k[3]);
+            s[1] = make_uint4(k[4], k[5], k[6], k[7]);
+            s[2] = make_uint4(k[8], 1u, v[0], v[1]);
+            s[3] = make_uint4(v[2], v[3], v[4], v[5]);
+            s[4] = make_uint4(v[6], v[7], v[8], v[9]);
+            s[5] = s[6] = s[7] = make_uint4(0u, 0u, 0u, 0u);
             return;
         }
         i = (i + 1) & (cap - 1);
     }
 }
 
+// lookup (pre-committed slot or NO_SLOT, and where an insert would start) fused with the batch
+// intern of the distinct states: bowner[s] = 1 + ref index of the first inserter.  A ref that finds
+// its state already interned marks itself and the first inserter in rdup (per ref, so every later
+// pass reads the flag coalesced instead of gathering a per-state flag)
 __global__ void __launch_bounds__(256) k_uniq_lookup(uint64_t nref, const uint8_t* __restrict__ refs,
                                                      const uint32_t* __restrict__ tab, uint64_t cap,
-                                                     uint32_t* __restrict__ pre) {
+                                                     uint32_t* __restrict__ pre, uint32_t* __restrict__ empty,
+                                                     uint32_t* bowner, uint8_t* __restrict__ rdup, uint64_t bcap,
+                                                     uint32_t* __restrict__ bslot) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nref) return;
     uint32_t k[KW];
     load_key(k, refs, r);
-    pre[r] = tab_find(tab, cap, k);
-}
-
-// batch scratch table of the distinct states: bowner[s] = 1 + ref index of the first inserter
-__global__ void __launch_bounds__(256) k_uniq_intern(uint64_t nref, const uint8_t* __restrict__ refs, uint32_t* bowner,
-                                                     uint64_t bcap, uint32_t* __restrict__ bslot) {
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nref) return;
-    uint32_t k[KW];
-    load_key(k, refs, r);
-    uint64_t i = key_hash(k) & (bcap - 1);
+    uint32_t e = NO_SLOT;
+    pre[r] = tab_find(tab, cap, k, &e);
+    if (empty) empty[r] = e;
+    uint64_t i = key_hash(k) >> 32 & (bcap - 1);
     for (uint64_t n = 0; n < bcap; n++) {
         const uint32_t prev = atomicCAS(&bowner[i], 0u, (uint32_t)(r + 1));
         if (prev == 0u) {
@@ -182,10 +204,26 @@ __global__ void __launch_bounds__(256) k_uniq_intern(uint64_t nref, const uint8_
         load_key(ok, refs, prev - 1);
         if (key_eq(ok, k)) {
             bslot[r] = (uint32_t)i;
+            rdup[r] = 1;
+            rdup[prev - 1] = 1;
             return;
         }
         i = (i + 1) & (bcap - 1);
     }
+}
+
+// Same-address atomics serialize at the memory side (~13 ns each): a per-wave count into ONE
+// counter costs ~2 ms over a 10M-lane grid.  Counts go to SPREAD counters 64 B apart instead; the
+// host sums them.
+#define SPREAD 256
+CHIP_DEV void spread_add(unsigned long long* spread, uint32_t v) {
+    const uint64_t m = __ballot(v != 0);
+    if (!m) return;
+    uint32_t sum = v;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    if ((threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m))
+        atomicAdd(&spread[((blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) & (SPREAD - 1)) * 8], (unsigned long long)sum);
 }
 
 __global__ void __launch_bounds__(256) k_ref_tx(uint64_t ntx, const uint64_t* __restrict__ start,
@@ -198,11 +236,13 @@ __global__ void __launch_bounds__(256) k_ref_tx(uint64_t ntx, const uint64_t* __
     }
 }
 
-__global__ void __launch_bounds__(256) k_uniq_round_min(uint64_t nref, const uint32_t* __restrict__ ref_tx,
+// over the refs of dup states only (a state with one referencer needs no minimum)
+__global__ void __launch_bounds__(256) k_uniq_round_min(uint64_t nref, const uint8_t* __restrict__ rdup,
+                                                        const uint32_t* __restrict__ ref_tx,
                                                         const uint32_t* __restrict__ bslot,
                                                         const uint8_t* __restrict__ st, uint32_t* __restrict__ bmin) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nref) return;
+    if (r >= nref || !rdup[r]) return;
     const uint32_t t = ref_tx[r];
     if (st[t] != ST_FAILED) atomicMin(&bmin[bslot[r]], t);
 }
@@ -211,6 +251,7 @@ __global__ void __launch_bounds__(256) k_uniq_round_min(uint64_t nref, const uin
 // round's outcome does not depend on thread scheduling
 __global__ void __launch_bounds__(256) k_uniq_vote(uint64_t ntx, const uint64_t* __restrict__ start,
                                                    const uint32_t* __restrict__ pre, const uint32_t* __restrict__ bslot,
+                                                   const uint8_t* __restrict__ rdup,
                                                    const uint32_t* __restrict__ bmin, const uint8_t* __restrict__ st,
                                                    uint8_t* __restrict__ vote) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -219,6 +260,7 @@ __global__ void __launch_bounds__(256) k_uniq_vote(uint64_t ntx, const uint64_t*
     if (st[t] == ST_UNDECIDED) {
         for (uint64_t r = start[t], e = start[t + 1]; r < e; r++) {
             if (pre[r] != NO_SLOT) { v = 2; break; }
+            if (!rdup[r]) continue;   // t is the state's only referencer
             const uint32_t m = bmin[bslot[r]];
             if (m < t) {
                 if (st[m] == ST_COMMITTED) { v = 2; break; }
@@ -229,19 +271,29 @@ __global__ void __launch_bounds__(256) k_uniq_vote(uint64_t ntx, const uint64_t*
     vote[t] = v;
 }
 
-// bcommit[s] = (t << 32) | input index of s in the committing tx t (first occurrence wins via min)
+CHIP_DEV bool first_in_tx(const uint32_t* __restrict__ bslot, uint64_t a, uint64_t r) {
+    for (uint64_t r2 = a; r2 < r; r2++)
+        if (bslot[r2] == bslot[r]) return false;
+    return true;
+}
+
+// bcommit[s] = (t << 32) | input index of s in the committing tx t, dup states only (the first
+// occurrence of s inside t; no other tx commits s, so plain stores)
 __global__ void __launch_bounds__(256) k_uniq_apply(uint64_t ntx, const uint64_t* __restrict__ start,
                                                     const uint32_t* __restrict__ bslot, const uint32_t* __restrict__ pos,
+                                                    const uint8_t* __restrict__ rdup,
                                                     const uint8_t* __restrict__ decision, uint8_t* __restrict__ st,
                                                     unsigned long long* __restrict__ bcommit,
-                                                    unsigned int* __restrict__ undecided) {
+                                                    unsigned long long* __restrict__ undecided) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool wait = false;
     if (t < ntx && st[t] == ST_UNDECIDED) {
         const uint8_t d = decision[t];
         if (d == 0) {
-            for (uint64_t r = start[t], e = start[t + 1]; r < e; r++)
-                atomicMin(&bcommit[bslot[r]], ((unsigned long long)t << 32) | (unsigned long long)pos[r]);
+            const uint64_t a = start[t];
+            for (uint64_t r = a, e = start[t + 1]; r < e; r++)
+                if (rdup[r] && first_in_tx(bslot, a, r))
+                    bcommit[bslot[r]] = ((unsigned long long)t << 32) | (unsigned long long)pos[r];
             st[t] = ST_COMMITTED;
         } else if (d >= 2) {
             st[t] = ST_FAILED;
@@ -249,8 +301,7 @@ __global__ void __launch_bounds__(256) k_uniq_apply(uint64_t ntx, const uint64_t
             wait = true;
         }
     }
-    const uint64_t m = __ballot(wait);
-    if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(undecided, (unsigned int)__popcll(m));
+    spread_add(undecided, wait ? 1u : 0u);
 }
 
 // the ConsumingTx that consumed local input r before tx t, if any
@@ -260,7 +311,8 @@ struct Consumer {
 };
 CHIP_DEV bool consumed_before(uint64_t r, uint32_t t, const uint32_t* __restrict__ pre, const uint32_t* __restrict__ tab,
                               const unsigned long long* __restrict__ bcommit, const uint32_t* __restrict__ bslot,
-                              const uint8_t* __restrict__ tx_ids, const uint32_t* __restrict__ callers, Consumer& c) {
+                              const uint8_t* __restrict__ rdup, const uint8_t* __restrict__ tx_ids,
+                              const uint32_t* __restrict__ callers, Consumer& c) {
     if (pre[r] != NO_SLOT) {
         const uint32_t* v = tab + (uint64_t)pre[r] * SLOT_W + S_VAL;
         c.id = v;
@@ -268,6 +320,7 @@ CHIP_DEV bool consumed_before(uint64_t r, uint32_t t, const uint32_t* __restrict
         c.caller = v[9];
         return true;
     }
+    if (!rdup[r]) return false;
     const unsigned long long bc = bcommit[bslot[r]];
     const uint32_t ct = (uint32_t)(bc >> 32);
     if (bc == ~0ull || ct >= t) return false;
@@ -282,6 +335,7 @@ CHIP_DEV bool consumed_before(uint64_t r, uint32_t t, const uint32_t* __restrict
 __global__ void __launch_bounds__(256) k_uniq_classify(uint64_t ntx, const uint64_t* __restrict__ start,
                                                        const uint32_t* __restrict__ pos, const uint32_t* __restrict__ pre,
                                                        const uint32_t* __restrict__ bslot,
+                                                       const uint8_t* __restrict__ rdup,
                                                        const unsigned long long* __restrict__ bcommit,
                                                        const uint8_t* __restrict__ tx_ids,
                                                        const uint32_t* __restrict__ callers,
@@ -294,7 +348,7 @@ __global__ void __launch_bounds__(256) k_uniq_classify(uint64_t ntx, const uint6
         const uint32_t* myid = reinterpret_cast<const uint32_t*>(tx_ids + 32ull * t);
         for (uint64_t r = start[t], e = start[t + 1]; r < e; r++) {
             Consumer c;
-            if (!consumed_before(r, (uint32_t)t, pre, tab, bcommit, bslot, tx_ids, callers, c)) continue;
+            if (!consumed_before(r, (uint32_t)t, pre, tab, bcommit, bslot, rdup, tx_ids, callers, c)) continue;
             bool same = (c.idx == pos[r]) && (c.caller == callers[t]);
 #pragma unroll
             for (int q = 0; q < 8; q++) same = same && (c.id[q] == myid[q]);
@@ -304,16 +358,10 @@ __global__ void __launch_bounds__(256) k_uniq_classify(uint64_t ntx, const uint6
     vote[t] = v;
 }
 
-CHIP_DEV bool first_in_tx(const uint32_t* __restrict__ bslot, uint64_t a, uint64_t r) {
-    for (uint64_t r2 = a; r2 < r; r2++)
-        if (bslot[r2] == bslot[r]) return false;
-    return true;
-}
-
 // flag[r] = 1 when local input r yields a Conflict.stateHistory record
 __global__ void __launch_bounds__(256) k_uniq_flag(uint64_t nref, const uint32_t* __restrict__ ref_tx,
                                                    const uint64_t* __restrict__ start, const uint32_t* __restrict__ pre,
-                                                   const uint32_t* __restrict__ bslot,
+                                                   const uint32_t* __restrict__ bslot, const uint8_t* __restrict__ rdup,
                                                    const unsigned long long* __restrict__ bcommit,
                                                    const uint8_t* __restrict__ st, uint32_t* __restrict__ flag) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -322,7 +370,7 @@ __global__ void __launch_bounds__(256) k_uniq_flag(uint64_t nref, const uint32_t
     uint32_t f = 0;
     if (st[t] == ST_FAILED) {
         bool consumed = pre[r] != NO_SLOT;
-        if (!consumed) {
+        if (!consumed && rdup[r]) {
             const unsigned long long bc = bcommit[bslot[r]];
             consumed = bc != ~0ull && (uint32_t)(bc >> 32) < t;
         }
@@ -333,7 +381,7 @@ __global__ void __launch_bounds__(256) k_uniq_flag(uint64_t nref, const uint32_t
 
 __global__ void __launch_bounds__(256) k_uniq_emit(uint64_t nref, const uint32_t* __restrict__ ref_tx,
                                                    const uint32_t* __restrict__ pos, const uint32_t* __restrict__ pre,
-                                                   const uint32_t* __restrict__ bslot,
+                                                   const uint32_t* __restrict__ bslot, const uint8_t* __restrict__ rdup,
                                                    const unsigned long long* __restrict__ bcommit,
                                                    const uint8_t* __restrict__ tx_ids,
                                                    const uint32_t* __restrict__ callers,
@@ -344,7 +392,7 @@ __global__ void __launch_bounds__(256) k_uniq_emit(uint64_t nref, const uint32_t
     if (r >= nref || !flag[r] || at[r] >= cap) return;
     const uint32_t t = ref_tx[r];
     Consumer c;
-    consumed_before(r, t, pre, tab, bcommit, bslot, tx_ids, callers, c);
+    consumed_before(r, t, pre, tab, bcommit, bslot, rdup, tx_ids, callers, c);
     chip_conflict cf;
     cf.tx = t;
     cf.input_index = pos[r];
@@ -362,14 +410,17 @@ __global__ void __launch_bounds__(256) k_uniq_insert(uint64_t nref, const uint8_
                                                      const uint32_t* __restrict__ ref_tx,
                                                      const uint32_t* __restrict__ pos, const uint64_t* __restrict__ start,
                                                      const uint8_t* __restrict__ st, const uint32_t* __restrict__ bslot,
+                                                     const uint8_t* __restrict__ rdup,
+                                                     const uint32_t* __restrict__ empty,
                                                      const uint8_t* __restrict__ tx_ids,
-                                                     const uint32_t* __restrict__ callers, uint32_t* tab, uint64_t cap,
+                                                     const uint32_t* __restrict__ callers, uint32_t* tab,
+                                                     uint32_t* bits, uint64_t cap,
                                                      unsigned long long* __restrict__ inserted) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool ins = false;
     if (r < nref) {
         const uint32_t t = ref_tx[r];
-        if (st[t] == ST_COMMITTED && first_in_tx(bslot, start[t], r)) {
+        if (st[t] == ST_COMMITTED && (!rdup[r] || first_in_tx(bslot, start[t], r))) {
             uint32_t k[KW], v[10];
             load_key(k, refs, r);
             const uint32_t* id = reinterpret_cast<const uint32_t*>(tx_ids + 32ull * t);
@@ -377,12 +428,11 @@ __global__ void __launch_bounds__(256) k_uniq_insert(uint64_t nref, const uint8_
             for (int q = 0; q < 8; q++) v[q] = id[q];
             v[8] = pos[r];
             v[9] = callers[t];
-            tab_put(tab, cap, k, v);
+            tab_put(tab, bits, cap, empty[r], k, v);
             ins = true;
         }
     }
-    const uint64_t m = __ballot(ins);
-    if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(inserted, (unsigned long long)__popcll(m));
+    spread_add(inserted, ins ? 1u : 0u);
 }
 
 __global__ void __launch_bounds__(256) k_uniq_status(uint64_t ntx, const uint8_t* __restrict__ st,
@@ -397,8 +447,8 @@ __global__ void __launch_bounds__(256) k_uniq_rebuild(uint64_t n, const uint8_t*
                                                       const uint8_t* __restrict__ tx32, const uint32_t* __restrict__ idx,
                                                       const uint32_t* __restrict__ caller, const uint32_t* __restrict__ pre,
                                                       const uint32_t* __restrict__ bslot,
-                                                      const uint32_t* __restrict__ bowner, uint32_t* tab, uint64_t cap,
-                                                      unsigned long long* __restrict__ inserted) {
+                                                      const uint32_t* __restrict__ bowner, uint32_t* tab, uint32_t* bits,
+                                                      uint64_t cap, unsigned long long* __restrict__ inserted) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool ins = false;
     if (r < n && pre[r] == NO_SLOT && bowner[bslot[r]] == (uint32_t)(r + 1)) {
@@ -409,16 +459,15 @@ __global__ void __launch_bounds__(256) k_uniq_rebuild(uint64_t n, const uint8_t*
         for (int q = 0; q < 8; q++) v[q] = id[q];
         v[8] = idx[r];
         v[9] = caller[r];
-        tab_put(tab, cap, k, v);
+        tab_put(tab, bits, cap, key_hash(k), k, v);
         ins = true;
     }
-    const uint64_t m = __ballot(ins);
-    if (m && (threadIdx.x & 63) == (uint32_t)__builtin_ctzll(m)) atomicAdd(inserted, (unsigned long long)__popcll(m));
+    spread_add(inserted, ins ? 1u : 0u);
 }
 
 // rehash every used slot of an old table into a new one
 __global__ void __launch_bounds__(256) k_uniq_rehash(uint64_t ocap, const uint32_t* __restrict__ old, uint32_t* tab,
-                                                     uint64_t cap) {
+                                                     uint32_t* bits, uint64_t cap) {
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= ocap) return;
     const uint32_t* o = old + s * SLOT_W;
@@ -428,7 +477,7 @@ __global__ void __launch_bounds__(256) k_uniq_rehash(uint64_t ocap, const uint32
     for (int q = 0; q < KW; q++) k[q] = o[q];
 #pragma unroll
     for (int q = 0; q < 10; q++) v[q] = o[S_VAL + q];
-    tab_put(tab, cap, k, v);
+    tab_put(tab, bits, cap, key_hash(k), k, v);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -450,20 +499,43 @@ static uint64_t pow2_at_least(uint64_t x) {
 }
 static inline uint32_t blocks_for(uint64_t n) { return (uint32_t)((n + 255) / 256); }
 
+// SPREAD counters: zero on the device / copy to the pinned host mirror (sum after the stream syncs)
+static int spread_zero(chip_uniq* u, hipStream_t st) {
+    UCHK(u, hipMemsetAsync(u->spread.p, 0, SPREAD * 64, st));
+    return CHIP_OK;
+}
+static int spread_fetch(chip_uniq* u, hipStream_t st) {
+    UCHK(u, hipMemcpyAsync(u->h_spread, u->spread.p, SPREAD * 64, hipMemcpyDeviceToHost, st));
+    return CHIP_OK;
+}
+static unsigned long long spread_total(const chip_uniq* u) {
+    unsigned long long t = 0;
+    for (int i = 0; i < SPREAD; i++) t += u->h_spread[i * 8];
+    return t;
+}
+
 // make room for `extra` more entries at load factor <= 1/2
 static int ensure_capacity(chip_uniq* u, uint64_t extra, hipStream_t st) {
     if (2 * (u->size + extra) <= u->cap) return CHIP_OK;
     const uint64_t ncap = pow2_at_least(2 * (u->size + extra));
     uint32_t* t = nullptr;
+    uint32_t* bits = nullptr;
     UCHK(u, hipMalloc(&t, ncap * SLOT_W * 4));
+    if (hipMalloc(&bits, ncap / 8) != hipSuccess) {
+        hipFree(t);
+        return ufail(u, CHIP_E_NOMEM, "occupancy bitmap");
+    }
     UCHK(u, hipMemsetAsync(t, 0, ncap * SLOT_W * 4, st));
+    UCHK(u, hipMemsetAsync(bits, 0, ncap / 8, st));
     if (u->cap) {
-        hipLaunchKernelGGL(k_uniq_rehash, dim3(blocks_for(u->cap)), dim3(256), 0, st, u->cap, u->tab, t, ncap);
+        hipLaunchKernelGGL(k_uniq_rehash, dim3(blocks_for(u->cap)), dim3(256), 0, st, u->cap, u->tab, t, bits, ncap);
         UCHK(u, hipGetLastError());
         UCHK(u, hipStreamSynchronize(st));
         hipFree(u->tab);
+        hipFree(u->bits);
     }
     u->tab = t;
+    u->bits = bits;
     u->cap = ncap;
     return CHIP_OK;
 }
@@ -476,6 +548,8 @@ static int batch_scratch(chip_uniq* u, uint64_t ntx, uint64_t nref) {
     const uint64_t bcap = pow2_at_least(2 * (nref + 1));
     UCHK(u, u->reftx.ensure(nref * 4 + 16));
     UCHK(u, u->pre.ensure(nref * 4 + 16));
+    UCHK(u, u->empty.ensure(nref * 4 + 16));
+    UCHK(u, u->rdup.ensure(nref + 16));
     UCHK(u, u->bslot.ensure(nref * 4 + 16));
     UCHK(u, u->flag.ensure(nref * 4 + 16));
     UCHK(u, u->scan.ensure(nref * 4 + 16));
@@ -484,6 +558,7 @@ static int batch_scratch(chip_uniq* u, uint64_t ntx, uint64_t nref) {
     UCHK(u, u->bcommit.ensure(bcap * 8));
     UCHK(u, u->st.ensure(ntx + 16));
     UCHK(u, u->ctr.ensure(64));
+    UCHK(u, u->spread.ensure(SPREAD * 64));
     u->bcap = bcap;
     return CHIP_OK;
 }
@@ -501,8 +576,11 @@ int chip_uniq_open(chip_ctx* ctx, uint64_t capacity, chip_uniq** out) {
         return CHIP_E_DEVICE;
     }
     int r = ensure_capacity(u, capacity ? capacity : 1024, u->stream);
+    if (!r && hipHostMalloc((void**)&u->h_spread, SPREAD * 64, hipHostMallocDefault) != hipSuccess) r = CHIP_E_NOMEM;
     if (r || hipStreamSynchronize(u->stream) != hipSuccess) {
         if (u->tab) hipFree(u->tab);
+        if (u->bits) hipFree(u->bits);
+        if (u->h_spread) hipHostFree(u->h_spread);
         hipStreamDestroy(u->stream);
         delete u;
         return r ? r : CHIP_E_DEVICE;
@@ -516,9 +594,12 @@ void chip_uniq_close(chip_uniq* u) {
     hipSetDevice(u->device);
     hipStreamSynchronize(u->stream);
     if (u->tab) hipFree(u->tab);
-    UBuf* bufs[] = {&u->reftx, &u->pre,    &u->bslot, &u->bowner, &u->bmin,   &u->bcommit, &u->st,
-                    &u->flag,  &u->scan,   &u->cub,   &u->ctr,    &u->refpos, &u->h_start, &u->h_refs,
-                    &u->h_ids, &u->h_call, &u->h_st,  &u->h_vote, &u->h_out};
+    if (u->bits) hipFree(u->bits);
+    if (u->h_spread) hipHostFree(u->h_spread);
+    UBuf* bufs[] = {&u->reftx,  &u->pre,    &u->empty,  &u->bslot, &u->bowner, &u->rdup,   &u->spread,
+                    &u->bmin,   &u->bcommit, &u->st,    &u->flag,  &u->scan,   &u->cub,    &u->ctr,
+                    &u->refpos, &u->h_start, &u->h_refs, &u->h_ids, &u->h_call, &u->h_st,  &u->h_vote,
+                    &u->h_out};
     for (UBuf* b : bufs) b->release();
     hipStreamDestroy(u->stream);
     delete u;
@@ -547,20 +628,19 @@ int chip_uniq_rebuild(chip_uniq* u, uint64_t n, const uint8_t* refs36, const uin
     UCHK(u, hipMemcpyAsync(u->refpos.p, idx, n * 4, hipMemcpyHostToDevice, st));
     UCHK(u, hipMemcpyAsync(u->h_call.p, caller, n * 4, hipMemcpyHostToDevice, st));
     UCHK(u, hipMemsetAsync(u->bowner.p, 0, u->bcap * 4, st));
-    UCHK(u, hipMemsetAsync(u->ctr.p, 0, 64, st));
+    UCHK(u, hipMemsetAsync(u->rdup.p, 0, n, st));
+    if ((r = spread_zero(u, st))) return r;
     const uint8_t* d_refs = u->h_refs.as<uint8_t>();
     hipLaunchKernelGGL(k_uniq_lookup, dim3(blocks_for(n)), dim3(256), 0, st, n, d_refs, u->tab, u->cap,
-                       u->pre.as<uint32_t>());
-    hipLaunchKernelGGL(k_uniq_intern, dim3(blocks_for(n)), dim3(256), 0, st, n, d_refs, u->bowner.as<uint32_t>(), u->bcap,
-                       u->bslot.as<uint32_t>());
+                       u->pre.as<uint32_t>(), (uint32_t*)nullptr, u->bowner.as<uint32_t>(), u->rdup.as<uint8_t>(),
+                       u->bcap, u->bslot.as<uint32_t>());
     hipLaunchKernelGGL(k_uniq_rebuild, dim3(blocks_for(n)), dim3(256), 0, st, n, d_refs, u->h_ids.as<uint8_t>(),
                        u->refpos.as<uint32_t>(), u->h_call.as<uint32_t>(), u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(),
-                       u->bowner.as<uint32_t>(), u->tab, u->cap, u->ctr.as<unsigned long long>());
+                       u->bowner.as<uint32_t>(), u->tab, u->bits, u->cap, u->spread.as<unsigned long long>());
     UCHK(u, hipGetLastError());
-    unsigned long long ins = 0;
-    UCHK(u, hipMemcpyAsync(&ins, u->ctr.p, 8, hipMemcpyDeviceToHost, st));
+    if ((r = spread_fetch(u, st))) return r;
     UCHK(u, hipStreamSynchronize(st));
-    u->size += ins;
+    u->size += spread_total(u);
     return CHIP_OK;
 }
 
@@ -585,6 +665,7 @@ int chip_uniq_shard_begin(chip_uniq* u, const chip_uniq_shard_batch* b, void* st
     u->ids = b->tx_ids;
     u->callers = b->callers;
     UCHK(u, hipMemsetAsync(u->bowner.p, 0, u->bcap * 4, st));
+    if (nref) UCHK(u, hipMemsetAsync(u->rdup.p, 0, nref, st));
     UCHK(u, hipMemsetAsync(u->bcommit.p, 0xff, u->bcap * 8, st));
     if (ntx) UCHK(u, hipMemsetAsync(u->st.p, ST_UNDECIDED, ntx, st));
     UCHK(u, hipMemsetAsync(u->ctr.p, 0, 64, st));
@@ -593,9 +674,8 @@ int chip_uniq_shard_begin(chip_uniq* u, const chip_uniq_shard_batch* b, void* st
                            (uint32_t*)nullptr);
     if (nref) {
         hipLaunchKernelGGL(k_uniq_lookup, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->refs, u->tab, u->cap,
-                           u->pre.as<uint32_t>());
-        hipLaunchKernelGGL(k_uniq_intern, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->refs,
-                           u->bowner.as<uint32_t>(), u->bcap, u->bslot.as<uint32_t>());
+                           u->pre.as<uint32_t>(), u->empty.as<uint32_t>(), u->bowner.as<uint32_t>(),
+                           u->rdup.as<uint8_t>(), u->bcap, u->bslot.as<uint32_t>());
     }
     UCHK(u, hipGetLastError());
     u->open = true;
@@ -608,12 +688,12 @@ int chip_uniq_shard_vote(chip_uniq* u, uint8_t* vote) {
     hipStream_t st = u->bst;
     UCHK(u, hipMemsetAsync(u->bmin.p, 0xff, u->bcap * 4, st));
     if (u->nref)
-        hipLaunchKernelGGL(k_uniq_round_min, dim3(blocks_for(u->nref)), dim3(256), 0, st, u->nref,
+        hipLaunchKernelGGL(k_uniq_round_min, dim3(blocks_for(u->nref)), dim3(256), 0, st, u->nref, u->rdup.as<uint8_t>(),
                            u->reftx.as<uint32_t>(), u->bslot.as<uint32_t>(), u->st.as<uint8_t>(), u->bmin.as<uint32_t>());
     if (u->ntx)
         hipLaunchKernelGGL(k_uniq_vote, dim3(blocks_for(u->ntx)), dim3(256), 0, st, u->ntx, u->start,
-                           u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->bmin.as<uint32_t>(), u->st.as<uint8_t>(),
-                           vote);
+                           u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->rdup.as<uint8_t>(), u->bmin.as<uint32_t>(),
+                           u->st.as<uint8_t>(), vote);
     UCHK(u, hipGetLastError());
     return CHIP_OK;
 }
@@ -622,17 +702,16 @@ int chip_uniq_shard_apply(chip_uniq* u, const uint8_t* decision, uint64_t* undec
     if (!u) return CHIP_E_ARG;
     if (!u->open || !undecided || (u->ntx && !decision)) return ufail(u, CHIP_E_ARG, "no batch in flight / null argument");
     hipStream_t st = u->bst;
-    unsigned int* d_und = u->ctr.as<unsigned int>();
-    UCHK(u, hipMemsetAsync(d_und, 0, 4, st));
+    int r = spread_zero(u, st);
+    if (r) return r;
     if (u->ntx)
         hipLaunchKernelGGL(k_uniq_apply, dim3(blocks_for(u->ntx)), dim3(256), 0, st, u->ntx, u->start,
-                           u->bslot.as<uint32_t>(), u->pos, decision, u->st.as<uint8_t>(),
-                           u->bcommit.as<unsigned long long>(), d_und);
+                           u->bslot.as<uint32_t>(), u->pos, u->rdup.as<uint8_t>(), decision, u->st.as<uint8_t>(),
+                           u->bcommit.as<unsigned long long>(), u->spread.as<unsigned long long>());
     UCHK(u, hipGetLastError());
-    unsigned int und = 0;
-    UCHK(u, hipMemcpyAsync(&und, d_und, 4, hipMemcpyDeviceToHost, st));
+    if ((r = spread_fetch(u, st))) return r;
     UCHK(u, hipStreamSynchronize(st));
-    *undecided = und;
+    *undecided = spread_total(u);
     return CHIP_OK;
 }
 
@@ -641,7 +720,8 @@ int chip_uniq_shard_classify(chip_uniq* u, uint8_t* vote) {
     if (!u->open || (u->ntx && !vote)) return ufail(u, CHIP_E_ARG, "no batch in flight / null vote");
     if (u->ntx)
         hipLaunchKernelGGL(k_uniq_classify, dim3(blocks_for(u->ntx)), dim3(256), 0, u->bst, u->ntx, u->start, u->pos,
-                           u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->bcommit.as<unsigned long long>(), u->ids,
+                           u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->rdup.as<uint8_t>(),
+                           u->bcommit.as<unsigned long long>(), u->ids,
                            u->callers, u->tab, u->st.as<uint8_t>(), vote);
     UCHK(u, hipGetLastError());
     return CHIP_OK;
@@ -657,28 +737,30 @@ int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_st
     u->open = false;
     uint32_t* flag = u->flag.as<uint32_t>();
     uint32_t* at = u->scan.as<uint32_t>();
-    unsigned long long* d_ins = u->ctr.as<unsigned long long>() + 1;
-    UCHK(u, hipMemsetAsync(d_ins, 0, 8, st));
+    int rc = spread_zero(u, st);
+    if (rc) return rc;
     uint32_t last[2] = {0, 0};
-    unsigned long long ins = 0;
     if (nref) {
         hipLaunchKernelGGL(k_uniq_flag, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->reftx.as<uint32_t>(), u->start,
-                           u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->bcommit.as<unsigned long long>(),
+                           u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->rdup.as<uint8_t>(),
+                           u->bcommit.as<unsigned long long>(),
                            u->st.as<uint8_t>(), flag);
         size_t tmp = 0;
         UCHK(u, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, flag, at, (int)nref, st));
         UCHK(u, u->cub.ensure(tmp + 16));
         UCHK(u, hipcub::DeviceScan::ExclusiveSum(u->cub.p, tmp, flag, at, (int)nref, st));
         hipLaunchKernelGGL(k_uniq_emit, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->reftx.as<uint32_t>(), u->pos,
-                           u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->bcommit.as<unsigned long long>(), u->ids,
+                           u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->rdup.as<uint8_t>(),
+                           u->bcommit.as<unsigned long long>(), u->ids,
                            u->callers, u->tab, flag, at, out, cap);
         // inserts after the records: emit reads pre-committed slots, inserts only fill empty ones
         hipLaunchKernelGGL(k_uniq_insert, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->refs, u->reftx.as<uint32_t>(),
-                           u->pos, u->start, u->st.as<uint8_t>(), u->bslot.as<uint32_t>(), u->ids, u->callers, u->tab,
-                           u->cap, d_ins);
+                           u->pos, u->start, u->st.as<uint8_t>(), u->bslot.as<uint32_t>(), u->rdup.as<uint8_t>(),
+                           u->empty.as<uint32_t>(), u->ids, u->callers, u->tab, u->bits, u->cap,
+                           u->spread.as<unsigned long long>());
         UCHK(u, hipMemcpyAsync(&last[0], at + nref - 1, 4, hipMemcpyDeviceToHost, st));
         UCHK(u, hipMemcpyAsync(&last[1], flag + nref - 1, 4, hipMemcpyDeviceToHost, st));
-        UCHK(u, hipMemcpyAsync(&ins, d_ins, 8, hipMemcpyDeviceToHost, st));
+        if ((rc = spread_fetch(u, st))) return rc;
     }
     if (ntx)
         hipLaunchKernelGGL(k_uniq_status, dim3(blocks_for(ntx)), dim3(256), 0, st, ntx, u->st.as<uint8_t>(), decision,
@@ -686,7 +768,7 @@ int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_st
     UCHK(u, hipGetLastError());
     UCHK(u, hipStreamSynchronize(st));
     const uint64_t nout = (uint64_t)last[0] + last[1];
-    u->size += ins;
+    if (nref) u->size += spread_total(u);
     *n_out = nout;
     return nout > cap ? ufail(u, CHIP_E_CAPACITY, "more conflict records than capacity") : CHIP_OK;
 }

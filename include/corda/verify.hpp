@@ -16,8 +16,8 @@
 // Batching is the point: a list of signatures (one transaction, or many transactions gathered by a
 // caller such as ResolveTransactionsFlow) is verified by one chip_verify_batch call; the exception
 // a caller sees is the one the reference's sequential loop would have thrown first.
-// Kryo serialization of SignableData is out of scope: a TransactionSignature carries the bytes the
-// JVM's SignableData(txId, metadata).serialize() produced (or a serializer callback builds them).
+// The signed message SignableData(txId, metadata).serialize() is built by kryo::signableData (the
+// Kryo 4.0.0 restatement, parity unpinned), by a serializer callback, or carried precomputed.
 #pragma once
 #include <algorithm>
 #include <cstdint>
@@ -32,6 +32,8 @@
 #include <string>
 #include <utility>
 #include <vector>
+
+#include <unistd.h>
 
 #include "../cordahip.h"
 
@@ -305,6 +307,63 @@ struct SignatureMetadata {
     int schemeNumberID = 4;
 };
 
+// SignableData(txId, metadata).serialize().bytes under the Kryo P2P context (Kryo 4.0.0,
+// CompatibleFieldSerializer with EXTENDED field names, references on, classes by name) — the same
+// restatement as corda_amd/kryo.py, which documents every rule with its reference line.  PARITY
+// UNPINNED: no JVM and no reference-held serialized bytes.
+namespace kryo {
+inline void varint(Bytes& o, uint32_t v) {
+    while (v >= 0x80) {
+        o.push_back((uint8_t)(v | 0x80));
+        v >>= 7;
+    }
+    o.push_back((uint8_t)v);
+}
+inline uint32_t zigzag(int32_t v) { return ((uint32_t)v << 1) ^ (uint32_t)(v >> 31); }
+inline void ascii(Bytes& o, const char* s) {   // Output.writeString, 1 < length < 64, ASCII
+    const size_t n = std::strlen(s);
+    for (size_t i = 0; i < n; i++) o.push_back((uint8_t)s[i] | (i + 1 == n ? 0x80 : 0));
+}
+inline void chunk(Bytes& o, const Bytes& d) {   // OutputChunked(1024) + endChunks
+    for (size_t i = 0; i < d.size(); i += 1024) {
+        const size_t m = std::min<size_t>(1024, d.size() - i);
+        varint(o, (uint32_t)m);
+        o.insert(o.end(), d.begin() + (long)i, d.begin() + (long)(i + m));
+    }
+    o.push_back(0);
+}
+inline Bytes signableData(const uint8_t txId[32], const SignatureMetadata& m) {
+    Bytes o = {'c', 'o', 'r', 'd', 'a', 0, 0, 1};
+    o.push_back(1);   // class by name (NAME + 2), name id 0
+    o.push_back(0);
+    ascii(o, "net.corda.core.crypto.SignableData");
+    o.push_back(1);   // NOT_NULL (first-seen reference)
+    o.push_back(2);
+    ascii(o, "SignableData.signatureMetadata");
+    ascii(o, "SignableData.txId");
+    Bytes meta = {1, 2};
+    ascii(meta, "SignatureMetadata.platformVersion");
+    ascii(meta, "SignatureMetadata.schemeNumberID");
+    Bytes f;
+    varint(f, zigzag(m.platformVersion));
+    chunk(meta, f);
+    f.clear();
+    varint(f, zigzag(m.schemeNumberID));
+    chunk(meta, f);
+    chunk(o, meta);
+    Bytes h = {1, 1};   // class by name, name id 1
+    ascii(h, "net.corda.core.crypto.SecureHash$SHA256");
+    h.push_back(1);
+    h.push_back(1);
+    ascii(h, "OpaqueBytes.bytes");
+    Bytes arr = {1, 33};   // NOT_NULL, length + 1
+    arr.insert(arr.end(), txId, txId + 32);
+    chunk(h, arr);
+    chunk(o, h);
+    return o;
+}
+}  // namespace kryo
+
 // One libcordahip context (one GPU).
 class Engine {
   public:
@@ -342,8 +401,9 @@ struct Item {
     const Bytes* msg;
 };
 
-// status of every item, one batch call (keys and messages de-duplicated)
-inline std::vector<uint8_t> verify_items(Engine& e, const std::vector<Item>& items) {
+// status of every item, one batch call (keys and messages de-duplicated); is_valid: Crypto.isValid
+// semantics (chip_is_valid_batch: no empty-input checks)
+inline std::vector<uint8_t> verify_items(Engine& e, const std::vector<Item>& items, bool is_valid = false) {
     std::map<Bytes, uint32_t> kid, mid;
     std::vector<const Bytes*> keys, msgs;
     std::vector<uint32_t> key_idx, msg_idx, sig_len;
@@ -393,7 +453,8 @@ inline std::vector<uint8_t> verify_items(Engine& e, const std::vector<Item>& ite
     b.key_bytes = key_pool.size();
     b.msg_bytes = msg_pool.size();
     std::vector<uint8_t> status(items.size());
-    if (!items.empty()) e.check(chip_verify_batch(e.get(), &b, status.data(), nullptr));
+    if (!items.empty())
+        e.check((is_valid ? chip_is_valid_batch : chip_verify_batch)(e.get(), &b, status.data(), nullptr));
     return status;
 }
 
@@ -431,15 +492,15 @@ struct Crypto {
     // Crypto.isValid(PublicKey, ByteArray, ByteArray): false on a bad signature; engine decode
     // errors still throw SignatureException   Crypto.kt:600-625
     static bool isValid(Engine& e, const PublicKey& key, const Bytes& signatureData, const Bytes& clearData) {
-        const uint8_t st = detail::verify_items(e, {{&key.encoded, &signatureData, &clearData}})[0];
+        const uint8_t st = detail::verify_items(e, {{&key.encoded, &signatureData, &clearData}}, true)[0];
         if (st == CHIP_VALID) return true;
         if (st == CHIP_INVALID) return false;
         detail::throw_for(st, key.encoded);
     }
 };
 
-// SignableData(txId, metadata).serialize().bytes is produced by the JVM (Kryo); a deployment plugs
-// its serializer here, TransactionSignature may also carry the bytes directly.
+// SignableData(txId, metadata).serialize().bytes: kryo::signableData by default; a deployment may
+// plug the JVM's serializer here, and TransactionSignature may also carry the bytes directly.
 using SignableDataSerializer = std::function<Bytes(const SecureHash&, const SignatureMetadata&)>;
 
 struct TransactionSignature {
@@ -449,8 +510,8 @@ struct TransactionSignature {
     Bytes signableBytes;   // precomputed SignableData bytes (optional)
 
     Bytes signable(const SecureHash& txId, const SignableDataSerializer& ser) const {
-        if (!signableBytes.empty() || !ser) return signableBytes;
-        return ser(txId, signatureMetadata);
+        if (!signableBytes.empty()) return signableBytes;
+        return ser ? ser(txId, signatureMetadata) : kryo::signableData(txId.bytes, signatureMetadata);
     }
     // TransactionSignature.verify(txId) = Crypto.doVerify(txId, this)
     bool verify(Engine& e, const SecureHash& txId, const SignableDataSerializer& ser = nullptr) const {
@@ -627,6 +688,9 @@ struct UniquenessException : std::runtime_error {
     Conflict error;
     explicit UniquenessException(Conflict c) : std::runtime_error("UniquenessException"), error(std::move(c)) {}
 };
+struct CommitLogFailure : std::runtime_error {   // the commit log could not be made durable (fail-stop)
+    using std::runtime_error::runtime_error;
+};
 struct NotaryException : std::runtime_error {   // NotaryError.Conflict(txId, conflict)
     SecureHash txId;
     Conflict conflict;
@@ -653,8 +717,13 @@ class PersistentUniquenessProvider {
     // rows are appended after each batch.  Rows are 76 bytes — StateRef key (32-B txhash, LE u32
     // index), consuming tx id, LE u32 input index, LE u32 caller — the same file format as
     // corda_amd.crypto.CommitLog; a torn final row is ignored.
-    PersistentUniquenessProvider(Engine& e, uint64_t capacity, const std::string& logPath)
+    // commitBatch returns only once the committed rows are durable (fflush + fsync: the role of the
+    // reference's database commit); fsync = false is for benchmarks and tests.  A failed append
+    // makes the provider fail stop: CommitLogFailure now and on every later call, since the device
+    // table is ahead of the log until a reopen rebuilds it from the log.
+    PersistentUniquenessProvider(Engine& e, uint64_t capacity, const std::string& logPath, bool fsync = true)
         : PersistentUniquenessProvider(e, capacity) {
+        fsync_ = fsync;
         std::vector<uint8_t> raw;
         if (FILE* f = std::fopen(logPath.c_str(), "rb")) {
             uint8_t buf[1 << 16];
@@ -691,6 +760,7 @@ class PersistentUniquenessProvider {
 
     // batch of commits applied in order (the notary's batching layer)
     std::vector<Outcome> commitBatch(const std::vector<Request>& reqs) {
+        if (failed_) throw CommitLogFailure("commit log append failed earlier; reopen the provider");
         std::vector<uint64_t> start{0};
         std::vector<uint8_t> refs, ids;
         std::vector<uint32_t> callers;
@@ -757,13 +827,18 @@ class PersistentUniquenessProvider {
             }
         }
         if (!rows.empty()) {
-            if (std::fwrite(rows.data(), 1, rows.size(), log_) != rows.size() || std::fflush(log_) != 0)
-                throw std::runtime_error("commit log write failed");
+            if (std::fwrite(rows.data(), 1, rows.size(), log_) != rows.size() || std::fflush(log_) != 0 ||
+                (fsync_ && ::fsync(::fileno(log_)) != 0)) {
+                failed_ = true;
+                throw CommitLogFailure("commit log write failed");
+            }
         }
     }
     Engine& e_;
     chip_uniq* u_ = nullptr;
     FILE* log_ = nullptr;
+    bool fsync_ = true;
+    bool failed_ = false;
 };
 
 // TrustedAuthorityNotaryService.commitInputStates (NotaryService.kt:61-75)

@@ -1,0 +1,88 @@
+package net.corda.core.internal.gpu
+
+import java.nio.ByteBuffer
+import java.nio.ByteOrder
+
+/**
+ * JNI entry points of libcordahip (include/cordahip.h) — the natives of jni/cordahip_jni.c.
+ * Arrays are direct little-endian ByteBuffers in the chip_* structure-of-arrays layouts; handles are
+ * the library's chip_ctx / chip_uniq pointers.  Return codes: 0 or a negative CHIP_E* value.
+ *
+ * Status bytes per signature (chip_status) and the exception Crypto.doVerify throws for each:
+ *   0 VALID, 1 INVALID -> SignatureException, 2 SIG_DECODE -> SignatureException (engine decode),
+ *   3 EMPTY_SIG / 4 EMPTY_CLEAR -> IllegalArgumentException, 5 UNSUPPORTED -> keep the JCA path
+ *   (RSA, SPHINCS, composite keys), 6 KEY_INVALID -> InvalidKeyException.
+ */
+object CordaHip {
+    init {
+        System.loadLibrary("cordahip_jni")
+    }
+
+    const val VALID = 0
+    const val INVALID = 1
+    const val SIG_DECODE = 2
+    const val EMPTY_SIG = 3
+    const val EMPTY_CLEAR = 4
+    const val UNSUPPORTED = 5
+    const val KEY_INVALID = 6
+    const val E_CAPACITY = -4
+    /** sizeof(chip_conflict): tx u64, input_index u32, consumed_index u32, consuming_tx 32 B, caller u32, pad u32 */
+    const val CONFLICT_BYTES = 56
+
+    @JvmStatic external fun open(device: Int, flags: Int): Long
+    @JvmStatic external fun close(ctx: Long)
+    @JvmStatic external fun lastError(ctx: Long): String
+    @JvmStatic external fun allocPinned(bytes: Long): ByteBuffer?
+    @JvmStatic external fun freePinned(buffer: ByteBuffer)
+
+    @JvmStatic external fun verifyBatch(ctx: Long, isValid: Boolean, n: Int,
+                                        keyIdx: ByteBuffer, msgIdx: ByteBuffer,
+                                        sigData: ByteBuffer, sigOff: ByteBuffer, sigLen: ByteBuffer,
+                                        nKeys: Int, keyData: ByteBuffer, keyOff: ByteBuffer, keyLen: ByteBuffer,
+                                        nMsgs: Int, msgData: ByteBuffer, msgOff: ByteBuffer, msgLen: ByteBuffer,
+                                        status: ByteBuffer): Int
+
+    @JvmStatic external fun txIds(ctx: Long, ntx: Int, salts: ByteBuffer, txCompStart: ByteBuffer, nComp: Int,
+                                  compGroup: ByteBuffer, compInternal: ByteBuffer, data: ByteBuffer,
+                                  compOff: ByteBuffer, compLen: ByteBuffer, ids: ByteBuffer): Int
+
+    @JvmStatic external fun uniqOpen(ctx: Long, capacity: Long): Long
+    @JvmStatic external fun uniqClose(uniq: Long)
+    @JvmStatic external fun uniqSize(uniq: Long): Long
+    @JvmStatic external fun uniqLastError(uniq: Long): String
+    @JvmStatic external fun uniqRebuild(uniq: Long, n: Int, refs: ByteBuffer, txIds: ByteBuffer,
+                                        inputIndex: ByteBuffer, caller: ByteBuffer): Int
+    @JvmStatic external fun uniqCommitBatch(uniq: Long, ntx: Int, txRefStart: ByteBuffer, refs: ByteBuffer,
+                                            txIds: ByteBuffer, callers: ByteBuffer, status: ByteBuffer,
+                                            out: ByteBuffer, cap: Int, nOut: LongArray): Int
+}
+
+/** A growable direct buffer in pinned memory (falls back to an ordinary direct buffer). */
+class PinnedBuffer(initial: Int = 1 shl 16) : AutoCloseable {
+    private var pinned = false
+    var buffer: ByteBuffer = alloc(initial)
+        private set
+
+    private fun alloc(bytes: Int): ByteBuffer {
+        val p = CordaHip.allocPinned(bytes.toLong())
+        pinned = p != null
+        return (p ?: ByteBuffer.allocateDirect(bytes)).order(ByteOrder.LITTLE_ENDIAN)
+    }
+
+    /** Cleared buffer of at least `bytes` capacity. */
+    fun reserve(bytes: Int): ByteBuffer {
+        if (buffer.capacity() < bytes) {
+            release()
+            buffer = alloc(maxOf(bytes, buffer.capacity() * 2))
+        }
+        buffer.clear()
+        return buffer
+    }
+
+    private fun release() {
+        if (pinned) CordaHip.freePinned(buffer)
+        pinned = false
+    }
+
+    override fun close() = release()
+}

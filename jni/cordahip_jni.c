@@ -1,0 +1,166 @@
+/* cordahip_jni.c — JNI glue between the Kotlin classes in this directory and libcordahip's C ABI
+ * (include/cordahip.h).  Built only where a JDK exists (none in this container):
+ *
+ *   cc -O2 -shared -fPIC -I$JAVA_HOME/include -I$JAVA_HOME/include/linux -I../include \
+ *      -o libcordahip_jni.so cordahip_jni.c -L../corda_amd -lcordahip -Wl,-rpath,'$ORIGIN'
+ *
+ * Every array crosses as a direct java.nio.ByteBuffer (little-endian for integer arrays): no copies
+ * in the glue, and buffers from CordaHip.allocPinned are page-locked so the library's host entry
+ * points stage them over PCIe without a bounce.  Handles (chip_ctx*, chip_uniq*) travel as jlong.
+ *
+ * Replaces (reference, /root/reference):
+ *   verifyBatch      TransactionWithSignatures.checkSignaturesAreValid (TransactionWithSignatures.kt:62-66)
+ *                    -> Crypto.doVerify / Crypto.isValid (Crypto.kt:502-536, 615-625)
+ *   txIds            WireTransaction.id / merkleTree (WireTransaction.kt:63,139-189)
+ *   uniq*            UniquenessProvider.commit (UniquenessProvider.kt:15-17),
+ *                    PersistentUniquenessProvider.commit (PersistentUniquenessProvider.kt:92-113) */
+#include <jni.h>
+#include <stdint.h>
+#include <string.h>
+
+#include "cordahip.h"
+
+#define CLS(name) Java_net_corda_core_internal_gpu_CordaHip_##name
+
+static void* addr(JNIEnv* env, jobject buf) { return buf ? (*env)->GetDirectBufferAddress(env, buf) : NULL; }
+static uint64_t cap_of(JNIEnv* env, jobject buf) {
+    return buf ? (uint64_t)(*env)->GetDirectBufferCapacity(env, buf) : 0;
+}
+
+/* ---- context ---- */
+JNIEXPORT jlong JNICALL CLS(open)(JNIEnv* env, jclass cls, jint device, jint flags) {
+    (void)env; (void)cls;
+    chip_config cfg = {device, (uint32_t)flags, 0};
+    chip_ctx* c = NULL;
+    return chip_init(&cfg, &c) == CHIP_OK ? (jlong)(intptr_t)c : 0;
+}
+
+JNIEXPORT void JNICALL CLS(close)(JNIEnv* env, jclass cls, jlong ctx) {
+    (void)env; (void)cls;
+    chip_shutdown((chip_ctx*)(intptr_t)ctx);
+}
+
+JNIEXPORT jstring JNICALL CLS(lastError)(JNIEnv* env, jclass cls, jlong ctx) {
+    (void)cls;
+    return (*env)->NewStringUTF(env, chip_last_error((chip_ctx*)(intptr_t)ctx));
+}
+
+/* Page-locked host memory as a direct ByteBuffer (chip_alloc_pinned); null when it fails. */
+JNIEXPORT jobject JNICALL CLS(allocPinned)(JNIEnv* env, jclass cls, jlong bytes) {
+    (void)cls;
+    void* p = NULL;
+    if (bytes <= 0 || chip_alloc_pinned((uint64_t)bytes, &p) != CHIP_OK) return NULL;
+    return (*env)->NewDirectByteBuffer(env, p, bytes);
+}
+
+JNIEXPORT void JNICALL CLS(freePinned)(JNIEnv* env, jclass cls, jobject buf) {
+    (void)cls;
+    chip_free_pinned(addr(env, buf));
+}
+
+/* ---- signatures (chip_sig_batch SoA) ----
+ * status: n bytes out (CHIP_* per signature).  isValid selects Crypto.isValid semantics
+ * (chip_is_valid_batch: no empty-input checks) over Crypto.doVerify's. */
+JNIEXPORT jint JNICALL CLS(verifyBatch)(JNIEnv* env, jclass cls, jlong ctx, jboolean isValid, jint n,
+                                        jobject keyIdx, jobject msgIdx, jobject sigData, jobject sigOff,
+                                        jobject sigLen, jint nKeys, jobject keyData, jobject keyOff, jobject keyLen,
+                                        jint nMsgs, jobject msgData, jobject msgOff, jobject msgLen,
+                                        jobject status) {
+    (void)cls;
+    chip_sig_batch b;
+    memset(&b, 0, sizeof b);
+    b.n = (uint64_t)n;
+    b.key_idx = (const uint32_t*)addr(env, keyIdx);
+    b.msg_idx = (const uint32_t*)addr(env, msgIdx);
+    b.sig_data = (const uint8_t*)addr(env, sigData);
+    b.sig_off = (const uint64_t*)addr(env, sigOff);
+    b.sig_len = (const uint32_t*)addr(env, sigLen);
+    b.n_keys = (uint64_t)nKeys;
+    b.key_data = (const uint8_t*)addr(env, keyData);
+    b.key_off = (const uint64_t*)addr(env, keyOff);
+    b.key_len = (const uint32_t*)addr(env, keyLen);
+    b.n_msgs = (uint64_t)nMsgs;
+    b.msg_data = (const uint8_t*)addr(env, msgData);
+    b.msg_off = (const uint64_t*)addr(env, msgOff);
+    b.msg_len = (const uint32_t*)addr(env, msgLen);
+    b.sig_bytes = cap_of(env, sigData);
+    b.key_bytes = cap_of(env, keyData);
+    b.msg_bytes = cap_of(env, msgData);
+    uint8_t* st = (uint8_t*)addr(env, status);
+    if (n < 0 || (n > 0 && (!st || cap_of(env, status) < (uint64_t)n))) return CHIP_E_ARG;
+    chip_ctx* c = (chip_ctx*)(intptr_t)ctx;
+    return isValid ? chip_is_valid_batch(c, &b, st, NULL) : chip_verify_batch(c, &b, st, NULL);
+}
+
+/* ---- tx ids (chip_tx_batch SoA); ids: ntx * 32 bytes out ---- */
+JNIEXPORT jint JNICALL CLS(txIds)(JNIEnv* env, jclass cls, jlong ctx, jint ntx, jobject salts, jobject txCompStart,
+                                  jint nComp, jobject compGroup, jobject compInternal, jobject data,
+                                  jobject compOff, jobject compLen, jobject ids) {
+    (void)cls;
+    chip_tx_batch b;
+    memset(&b, 0, sizeof b);
+    b.ntx = (uint64_t)ntx;
+    b.salts = (const uint8_t*)addr(env, salts);
+    b.tx_comp_start = (const uint64_t*)addr(env, txCompStart);
+    b.ncomp = (uint64_t)nComp;
+    b.comp_group = (const uint32_t*)addr(env, compGroup);
+    b.comp_internal = (const uint32_t*)addr(env, compInternal);
+    b.data = (const uint8_t*)addr(env, data);
+    b.comp_off = (const uint64_t*)addr(env, compOff);
+    b.comp_len = (const uint32_t*)addr(env, compLen);
+    b.data_bytes = cap_of(env, data);
+    uint8_t* out = (uint8_t*)addr(env, ids);
+    if (ntx < 0 || (ntx > 0 && (!out || cap_of(env, ids) < 32ull * (uint64_t)ntx))) return CHIP_E_ARG;
+    return chip_txid_batch((chip_ctx*)(intptr_t)ctx, &b, out);
+}
+
+/* ---- notary uniqueness ---- */
+JNIEXPORT jlong JNICALL CLS(uniqOpen)(JNIEnv* env, jclass cls, jlong ctx, jlong capacity) {
+    (void)env; (void)cls;
+    chip_uniq* u = NULL;
+    return chip_uniq_open((chip_ctx*)(intptr_t)ctx, (uint64_t)capacity, &u) == CHIP_OK ? (jlong)(intptr_t)u : 0;
+}
+
+JNIEXPORT void JNICALL CLS(uniqClose)(JNIEnv* env, jclass cls, jlong u) {
+    (void)env; (void)cls;
+    chip_uniq_close((chip_uniq*)(intptr_t)u);
+}
+
+JNIEXPORT jlong JNICALL CLS(uniqSize)(JNIEnv* env, jclass cls, jlong u) {
+    (void)env; (void)cls;
+    return (jlong)chip_uniq_size((const chip_uniq*)(intptr_t)u);
+}
+
+JNIEXPORT jstring JNICALL CLS(uniqLastError)(JNIEnv* env, jclass cls, jlong u) {
+    (void)cls;
+    return (*env)->NewStringUTF(env, chip_uniq_last_error((const chip_uniq*)(intptr_t)u));
+}
+
+/* rows of the commit log: refs 36 B, tx ids 32 B, input index and caller u32 each */
+JNIEXPORT jint JNICALL CLS(uniqRebuild)(JNIEnv* env, jclass cls, jlong u, jint n, jobject refs, jobject txIds,
+                                        jobject inputIndex, jobject caller) {
+    (void)cls;
+    if (n < 0) return CHIP_E_ARG;
+    return chip_uniq_rebuild((chip_uniq*)(intptr_t)u, (uint64_t)n, (const uint8_t*)addr(env, refs),
+                             (const uint8_t*)addr(env, txIds), (const uint32_t*)addr(env, inputIndex),
+                             (const uint32_t*)addr(env, caller));
+}
+
+/* status: ntx bytes out (0 committed, 1 idempotent, 2 conflict); out: cap chip_conflict records
+ * (56 B each); nOut[0] receives the full record count (CHIP_E_CAPACITY when it exceeds cap). */
+JNIEXPORT jint JNICALL CLS(uniqCommitBatch)(JNIEnv* env, jclass cls, jlong u, jint ntx, jobject txRefStart,
+                                            jobject refs, jobject txIds, jobject callers, jobject status,
+                                            jobject out, jint cap, jlongArray nOut) {
+    (void)cls;
+    if (ntx < 0 || cap < 0 || !nOut) return CHIP_E_ARG;
+    if (cap_of(env, out) < (uint64_t)cap * sizeof(chip_conflict) || cap_of(env, status) < (uint64_t)ntx)
+        return CHIP_E_ARG;
+    uint64_t n = 0;
+    const int r = chip_uniq_commit_batch((chip_uniq*)(intptr_t)u, (uint64_t)ntx, (const uint64_t*)addr(env, txRefStart),
+                                         (const uint8_t*)addr(env, refs), (const uint8_t*)addr(env, txIds),
+                                         (const uint32_t*)addr(env, callers), (uint8_t*)addr(env, status),
+                                         (chip_conflict*)addr(env, out), (uint64_t)cap, &n);
+    const jlong nv = (jlong)n;
+    (*env)->SetLongArrayRegion(env, nOut, 0, 1, &nv);
+    return r;
+}

@@ -79,6 +79,12 @@ void orc_verify_batch(uint64_t n, const uint32_t* key_idx, const uint32_t* msg_i
                       const uint8_t* key_data, const uint64_t* key_off, const uint32_t* key_len,
                       const uint8_t* msg_data, const uint64_t* msg_off, const uint32_t* msg_len,
                       uint8_t* status, int threads);
+/* is_valid = 1: Crypto.isValid semantics (Crypto.kt:615-625, no empty-input checks) */
+void orc_verify_batch_mode(uint64_t n, const uint32_t* key_idx, const uint32_t* msg_idx,
+                           const uint8_t* sig_data, const uint64_t* sig_off, const uint32_t* sig_len,
+                           const uint8_t* key_data, const uint64_t* key_off, const uint32_t* key_len,
+                           const uint8_t* msg_data, const uint64_t* msg_off, const uint32_t* msg_len,
+                           uint8_t* status, int threads, int is_valid);
 
 /* ---- tx id: WireTransaction.id / MerkleTree (WireTransaction.kt:139-189, MerkleTree.kt:27-66,
  *      CryptoUtils.kt:216-233, SecureHash.kt:25) ---- */

@@ -35,18 +35,26 @@ int orc_spki_scheme(const uint8_t* k, size_t len, const uint8_t** raw, size_t* r
     return 0;
 }
 
-int orc_do_verify(const uint8_t* spki, size_t spki_len, const uint8_t* sig, size_t siglen,
-                  const uint8_t* msg, size_t msglen) {
+/* is_valid = 1: Crypto.isValid(scheme, key, sig, clear) (Crypto.kt:615-625) — initVerify, update,
+ * verify with no empty-input checks: an empty signature reaches the engine's decode (SIG_DECODE),
+ * empty clear data is verified as the empty message. */
+static int do_verify_mode(const uint8_t* spki, size_t spki_len, const uint8_t* sig, size_t siglen,
+                          const uint8_t* msg, size_t msglen, int is_valid) {
     const uint8_t* raw;
     size_t rl;
     int scheme = orc_spki_scheme(spki, spki_len, &raw, &rl);
     if (!scheme) return ORC_UNSUPPORTED;
-    if (siglen == 0) return ORC_EMPTY_SIG;
-    if (msglen == 0) return ORC_EMPTY_CLEAR;
+    if (siglen == 0 && !is_valid) return ORC_EMPTY_SIG;
+    if (msglen == 0 && !is_valid) return ORC_EMPTY_CLEAR;
     if (scheme == ORC_SCHEME_ED25519) return orc_ed25519_verify(raw, sig, siglen, msg, msglen);
     uint8_t xy[64];
     if (orc_ecdsa_decode_key(scheme, raw, rl, xy)) return ORC_KEY_INVALID;
     return orc_ecdsa_verify(scheme, xy, sig, siglen, msg, msglen);
+}
+
+int orc_do_verify(const uint8_t* spki, size_t spki_len, const uint8_t* sig, size_t siglen,
+                  const uint8_t* msg, size_t msglen) {
+    return do_verify_mode(spki, spki_len, sig, siglen, msg, msglen, 0);
 }
 
 typedef struct {
@@ -56,24 +64,25 @@ typedef struct {
     const uint8_t* key_data; const uint64_t* key_off; const uint32_t* key_len;
     const uint8_t* msg_data; const uint64_t* msg_off; const uint32_t* msg_len;
     uint8_t* status;
+    int is_valid;
 } vjob;
 
 static void* vworker(void* p) {
     vjob* j = (vjob*)p;
     for (uint64_t i = j->lo; i < j->hi; i++) {
         uint32_t k = j->key_idx[i], m = j->msg_idx[i];
-        j->status[i] = (uint8_t)orc_do_verify(j->key_data + j->key_off[k], j->key_len[k],
-                                              j->sig_data + j->sig_off[i], j->sig_len[i],
-                                              j->msg_data + j->msg_off[m], j->msg_len[m]);
+        j->status[i] = (uint8_t)do_verify_mode(j->key_data + j->key_off[k], j->key_len[k],
+                                               j->sig_data + j->sig_off[i], j->sig_len[i],
+                                               j->msg_data + j->msg_off[m], j->msg_len[m], j->is_valid);
     }
     return NULL;
 }
 
-void orc_verify_batch(uint64_t n, const uint32_t* key_idx, const uint32_t* msg_idx,
-                      const uint8_t* sig_data, const uint64_t* sig_off, const uint32_t* sig_len,
-                      const uint8_t* key_data, const uint64_t* key_off, const uint32_t* key_len,
-                      const uint8_t* msg_data, const uint64_t* msg_off, const uint32_t* msg_len,
-                      uint8_t* status, int threads) {
+void orc_verify_batch_mode(uint64_t n, const uint32_t* key_idx, const uint32_t* msg_idx,
+                           const uint8_t* sig_data, const uint64_t* sig_off, const uint32_t* sig_len,
+                           const uint8_t* key_data, const uint64_t* key_off, const uint32_t* key_len,
+                           const uint8_t* msg_data, const uint64_t* msg_off, const uint32_t* msg_len,
+                           uint8_t* status, int threads, int is_valid) {
     orc_ed_init();
     orc_ec_init();
     if (threads < 1) threads = 1;
@@ -82,8 +91,17 @@ void orc_verify_batch(uint64_t n, const uint32_t* key_idx, const uint32_t* msg_i
     vjob jobs[256];
     for (int t = 0; t < threads; t++) {
         jobs[t] = (vjob){n * t / threads, n * (t + 1) / threads, key_idx, msg_idx, sig_data, sig_off, sig_len,
-                         key_data, key_off, key_len, msg_data, msg_off, msg_len, status};
+                         key_data, key_off, key_len, msg_data, msg_off, msg_len, status, is_valid};
         pthread_create(&th[t], NULL, vworker, &jobs[t]);
     }
     for (int t = 0; t < threads; t++) pthread_join(th[t], NULL);
+}
+
+void orc_verify_batch(uint64_t n, const uint32_t* key_idx, const uint32_t* msg_idx,
+                      const uint8_t* sig_data, const uint64_t* sig_off, const uint32_t* sig_len,
+                      const uint8_t* key_data, const uint64_t* key_off, const uint32_t* key_len,
+                      const uint8_t* msg_data, const uint64_t* msg_off, const uint32_t* msg_len,
+                      uint8_t* status, int threads) {
+    orc_verify_batch_mode(n, key_idx, msg_idx, sig_data, sig_off, sig_len, key_data, key_off, key_len, msg_data,
+                          msg_off, msg_len, status, threads, 0);
 }

@@ -52,3 +52,32 @@ def run(engine, tmpdir):
     assert len(rows) == live.size()
     assert os.path.getsize(path) % C.COMMIT_LOG_DTYPE.itemsize == 0
     return len(rows)
+
+
+def run_fail_stop(engine, tmpdir):
+    """An append that fails leaves the device table ahead of the log: the provider must refuse that
+    batch's results and every later commit (CommitLogFailure); a reopen rebuilds the table from the
+    log, so the unacknowledged batch's states are free again and a retry commits them (status 0)."""
+    import pytest
+    path = os.path.join(str(tmpdir), "notary_commit_log_fs.bin")
+    bs = batches(seed=11, n_batches=3)
+    p = C.PersistentUniquenessProvider(engine, 1 << 14, log_path=path)
+    first = p.commit_batch(bs[0])
+    good_rows = os.path.getsize(path)
+
+    def broken(rows):
+        raise OSError(28, "No space left on device")
+
+    p.log.append = broken
+    with pytest.raises(C.CommitLogFailure):
+        p.commit_batch(bs[1])
+    with pytest.raises(C.CommitLogFailure):          # fail-stop: no later commit is served
+        p.commit_batch(bs[2])
+    p.close()
+    assert os.path.getsize(path) == good_rows
+    reopened = C.PersistentUniquenessProvider(engine, 1 << 14, log_path=path)
+    ref = C.PersistentUniquenessProvider(engine, 1 << 14)
+    assert ref.commit_batch(bs[0]) == first
+    assert reopened.commit_batch(bs[1]) == ref.commit_batch(bs[1])
+    reopened.close()
+    return len(first)

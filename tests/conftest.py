@@ -32,11 +32,18 @@ def oracle():
 @pytest.fixture(scope="session")
 def ctx_modes():
     """Contexts for each Ed25519 schedule: default policy, every key on the per-key comb, every key
-    on the windowed Straus kernel.  Results must be identical (bit-exact status bytes)."""
+    on the windowed Straus kernel, and the default policy with the batch-size gate of the comb paths
+    off (CHIP_COMB_MIN_TOTAL=0: test-sized batches then take the eager-table schedules the bench
+    sizes take).  Results must be identical (bit-exact status bytes)."""
     import corda_amd
     from corda_amd import native
+    os.environ["CHIP_COMB_MIN_TOTAL"] = "0"
+    try:
+        ungated = corda_amd.Context(0)
+    finally:
+        del os.environ["CHIP_COMB_MIN_TOTAL"]
     cs = {"default": corda_amd.Context(0), "comb": corda_amd.Context(0, flags=native.FLAG_FORCE_COMB),
-          "straus": corda_amd.Context(0, flags=native.FLAG_NO_COMB)}
+          "straus": corda_amd.Context(0, flags=native.FLAG_NO_COMB), "ungated": ungated}
     yield cs
     for c in cs.values():
         c.close()

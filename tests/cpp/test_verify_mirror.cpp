@@ -78,6 +78,19 @@ int main() {
     CHECK(throws<IllegalArgumentException>([&] { Crypto::doVerify(e, alice.pub, sig, Bytes{}); }));
     CHECK(throws<SignatureException>([&] { Crypto::doVerify(e, alice.pub, Bytes(sig.begin(), sig.end() - 1), msg); }));
     CHECK(throws<SignatureException>([&] { Crypto::doVerify(e, bob.pub, sig, msg); }));
+    // Crypto.isValid has no empty-input checks (Crypto.kt:615-625)
+    Bytes sig0 = ed_sign(alice, Bytes{});
+    CHECK(Crypto::isValid(e, alice.pub, sig0, Bytes{}));
+    CHECK(!Crypto::isValid(e, alice.pub, sig0, msg));
+    CHECK(throws<SignatureException>([&] { Crypto::isValid(e, alice.pub, Bytes{}, msg); }));
+    // --- TransactionSignature.verify over the default Kryo SignableData bytes ---
+    {
+        SecureHash id = sha("tx-kryo");
+        SignatureMetadata m{1, 4};
+        TransactionSignature tk{ed_sign(alice, kryo::signableData(id.bytes, m)), alice.pub, m, {}};
+        CHECK(tk.verify(e, id));
+        CHECK(throws<SignatureException>([&] { tk.verify(e, sha("tx-other")); }));
+    }
     // --- TransactionSignature.verify with the tx id (TransactionSignatureTest) ---
     SecureHash txId = sha("tx-1");
     SignatureMetadata meta{1, 4};

@@ -113,11 +113,12 @@ def ecdsa_decode_key(scheme: int, pt: bytes):
     return out.raw if r == 0 else None
 
 
-def verify_batch(b, threads: int = 1) -> np.ndarray:
+def verify_batch(b, threads: int = 1, is_valid: bool = False) -> np.ndarray:
+    """Crypto.doVerify statuses (is_valid=False) or Crypto.isValid statuses (no empty-input checks)."""
     st = np.zeros(b.n, dtype=np.uint8)
-    lib().orc_verify_batch(ctypes.c_uint64(b.n), _p(b.key_idx), _p(b.msg_idx), _p(b.sig_data), _p(b.sig_off),
-                           _p(b.sig_len), _p(b.key_data), _p(b.key_off), _p(b.key_len), _p(b.msg_data),
-                           _p(b.msg_off), _p(b.msg_len), _p(st), threads)
+    lib().orc_verify_batch_mode(ctypes.c_uint64(b.n), _p(b.key_idx), _p(b.msg_idx), _p(b.sig_data), _p(b.sig_off),
+                                _p(b.sig_len), _p(b.key_data), _p(b.key_off), _p(b.key_len), _p(b.msg_data),
+                                _p(b.msg_off), _p(b.msg_len), _p(st), threads, int(is_valid))
     return st
 
 

@@ -25,9 +25,9 @@ class OracleEngine:
         self.threads = threads
         self.calls = 0
 
-    def verify_batch(self, b):
+    def verify_batch(self, b, is_valid: bool = False):
         self.calls += 1
-        st = O.verify_batch(b, threads=self.threads)
+        st = O.verify_batch(b, threads=self.threads, is_valid=is_valid)
         bits = np.zeros(((len(st) + 63) // 64) * 64, dtype=np.uint64)
         bits[:len(st)] = (st == 0)
         bm = np.bitwise_or.reduce(bits.reshape(-1, 64) << np.arange(64, dtype=np.uint64), axis=1) if len(st) else bits

@@ -165,16 +165,41 @@ def test_signed_transaction_with_composite_required_key(eng):
 
 
 def test_composite_signature_engine_verify(eng):
-    """CompositeKeyTests.kt:156-174 (CompositeSignature over SHA256(clear) as the tx id)."""
+    """CompositeKeyTests.kt:156-174: the engine is fed the 32 id bytes (engine.update(SHA256(message)
+    .bytes)); CompositeSignature wraps them as the tx id without hashing (SecureHash.SHA256(bytes),
+    CompositeSignature.kt:81, SecureHash.kt:16-19)."""
     import hashlib
-    clear = b"composite clear data"
-    tx_id = hashlib.sha256(clear).digest()
+    tx_id = hashlib.sha256(b"composite clear data").digest()
     two_of_three = B().add_keys(ALICE, BOB, CHARLIE).build(threshold=2)
     a, b, c = _sig(0, ALICE, tx_id), _sig(1, BOB, tx_id), _sig(2, CHARLIE, tx_id)
-    v = lambda sigs: C.composite_signature_verify(eng, two_of_three, sigs, clear)   # noqa: E731
+    v = lambda sigs, clear=tx_id: C.composite_signature_verify(eng, two_of_three, sigs, clear)   # noqa: E731
     assert not v([a]) and not v([b]) and not v([c])
     assert v([a, b]) and v([a, c]) and v([b, c]) and v([a, b, c])
     broken_bob = C.TransactionSignature(a.bytes, BOB, C.SignatureMetadata(1, 4))
     assert not v([a, broken_bob])
     # composite given as its encoded SPKI bytes
-    assert C.composite_signature_verify(eng, two_of_three.encoded, [a, c], clear)
+    assert C.composite_signature_verify(eng, two_of_three.encoded, [a, c], tx_id)
+    # the buffer is the id, not a message to hash: SHA256(id) as clear data fails every signature
+    assert not v([a, b], hashlib.sha256(tx_id).digest())
+    # not 32 bytes: SecureHash.SHA256's require(size == 32) -> IllegalArgumentException, but only
+    # once the key is fulfilled (engineVerify checks fulfilment first)
+    with pytest.raises(C.IllegalArgumentException):
+        v([a, b], b"composite clear data")
+    assert not v([a], b"composite clear data")
+
+
+def test_is_valid_has_no_empty_checks(eng):
+    """Crypto.isValid (Crypto.kt:615-625) has no empty-input checks, unlike doVerify (:528-529): an
+    empty Ed25519 signature is the engine's SignatureException("signature length is wrong"), empty
+    clear data is verified as the empty message."""
+    import cordagen as G
+    seed = SEEDS[0]
+    sig_empty_msg = G.ed25519_sign(seed, b"")
+    assert C.Crypto.is_valid(eng, ALICE, sig_empty_msg, b"")
+    assert not C.Crypto.is_valid(eng, ALICE, sig_empty_msg, b"x")
+    with pytest.raises(C.IllegalArgumentException):
+        C.Crypto.do_verify(eng, ALICE, sig_empty_msg, b"")
+    with pytest.raises(C.SignatureException, match="signature length is wrong"):
+        C.Crypto.is_valid(eng, ALICE, b"", b"x")
+    with pytest.raises(C.IllegalArgumentException):
+        C.Crypto.do_verify(eng, ALICE, b"", b"x")

@@ -63,8 +63,14 @@ def test_composite_keys_on_gpu(ctx):
     cases = [[sigs[0]], [sigs[0], sigs[1]], [sigs[1], sigs[2]], [sigs[0], broken], sigs]
     oracle = OracleEngine()
     for cs in cases:
-        assert (C.composite_signature_verify(ctx, k, cs, clear)
-                == C.composite_signature_verify(oracle, k, cs, clear))
+        assert (C.composite_signature_verify(ctx, k, cs, tx_id)
+                == C.composite_signature_verify(oracle, k, cs, tx_id))
+    assert C.composite_signature_verify(ctx, k, sigs, tx_id)
+    # Crypto.isValid semantics on the device: empty clear data is an ordinary message
+    s0 = G.ed25519_sign(seeds[0], b"")
+    assert C.Crypto.is_valid(ctx, keys[0], s0, b"") and not C.Crypto.is_valid(ctx, keys[0], s0, b"\x00")
+    with pytest.raises(C.SignatureException):
+        C.Crypto.is_valid(ctx, keys[0], b"", b"\x00")
     stxs = [C.SignedTransaction(tx_id, cs, [k]) for cs in cases]
     got = [outcome(e) for e in C.verify_signatures_except_batch(ctx, stxs)]
     ref = [outcome(e) for e in C.verify_signatures_except_batch(oracle, stxs)]

@@ -20,7 +20,7 @@ def bitmap_of(status):
     return words
 
 
-MODES = ["default", "comb", "straus"]
+MODES = ["default", "comb", "straus", "ungated"]
 
 
 @pytest.mark.parametrize("mode", MODES)
@@ -84,9 +84,10 @@ def test_ed25519_mixed_policy_large(ctx_modes):
 
 
 def test_ed25519_comb_stats(ctx_modes):
-    """The default policy routes repeated keys through the comb kernels (native path observable)."""
+    """The default policy (size gate off) routes repeated keys through the comb kernels (native path
+    observable)."""
     from corda_amd import native
-    c = ctx_modes["default"]
+    c = ctx_modes["ungated"]
     c.reset_stats()
     b = G.ed25519_batch(4096, n_keys=16, corrupt=0.1, seed=5)
     st, _ = c.verify_batch(b)

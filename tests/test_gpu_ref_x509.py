@@ -10,7 +10,7 @@ import golden_cases
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("mode", ["default", "comb", "straus"])
+@pytest.mark.parametrize("mode", ["default", "comb", "straus", "ungated"])
 def test_reference_x509_links_on_gpu(ctx_modes, oracle, mode):
     cases = golden_cases.ref_x509_cases(corrupt=True)
     b = golden_cases.sig_batch_from_cases([dict(c, expected=c["expected"] or 0) for c in cases])
@@ -26,8 +26,9 @@ def test_reference_x509_links_on_gpu(ctx_modes, oracle, mode):
 
 
 def test_reference_x509_links_repeated_on_comb_path(ctx_modes, oracle):
-    """The six links repeated 64x (hot keys -> per-key comb tables by the default policy)."""
+    """The six links repeated 64x (hot keys -> per-key comb tables by the default policy with the
+    batch-size gate off)."""
     cases = golden_cases.ref_x509_cases(corrupt=False) * 64
     b = golden_cases.sig_batch_from_cases(cases)
-    st, _ = ctx_modes["default"].verify_batch(b)
+    st, _ = ctx_modes["ungated"].verify_batch(b)
     assert (st == 0).all()

@@ -131,3 +131,10 @@ def test_commit_log_restart_on_gpu(ctx, tmp_path):
     restarted (tests/commit_log_case.py)."""
     from commit_log_case import run
     assert run(ctx, tmp_path) > 0
+
+
+def test_commit_log_failure_is_fail_stop_on_gpu(ctx, tmp_path):
+    """A failed append stops the GPU-backed provider; the reopened table (rebuilt from the log)
+    serves the unacknowledged batch again (tests/commit_log_case.py)."""
+    from commit_log_case import run_fail_stop
+    assert run_fail_stop(ctx, tmp_path) > 0

@@ -226,27 +226,38 @@ typedef struct {
 
 static void* vworker(void* p) {
     vjob* j = (vjob*)p;
+    /* one initialised EVP_MD_CTX per (thread, key), copied per signature: OpenSSL 3.0's
+     * EVP_DigestVerifyInit fetches the algorithm under global locks, which a per-signature init pays
+     * on every call and which stops the baseline from scaling with threads */
     EVP_PKEY** keys = (EVP_PKEY**)calloc(j->n_keys ? j->n_keys : 1, sizeof(EVP_PKEY*));
+    EVP_MD_CTX** tmpl = (EVP_MD_CTX**)calloc(j->n_keys ? j->n_keys : 1, sizeof(EVP_MD_CTX*));
     EVP_MD_CTX* c = EVP_MD_CTX_new();
     for (uint64_t i = j->lo; i < j->hi; i++) {
         const uint32_t k = j->key_idx[i], m = j->msg_idx[i];
         if (!keys[k]) {
             const uint8_t* kp = j->key_data + j->key_off[k];
             keys[k] = d2i_PUBKEY(NULL, &kp, (long)j->key_len[k]);
+            if (keys[k]) {
+                const EVP_MD* md = EVP_PKEY_get_base_id(keys[k]) == EVP_PKEY_ED25519 ? NULL : EVP_sha256();
+                tmpl[k] = EVP_MD_CTX_new();
+                if (EVP_DigestVerifyInit(tmpl[k], NULL, md, NULL, keys[k]) != 1) {
+                    EVP_MD_CTX_free(tmpl[k]);
+                    tmpl[k] = NULL;
+                }
+            }
         }
         int v = 0;
-        if (keys[k]) {
-            const EVP_MD* md = EVP_PKEY_get_base_id(keys[k]) == EVP_PKEY_ED25519 ? NULL : EVP_sha256();
-            EVP_MD_CTX_reset(c);
-            if (EVP_DigestVerifyInit(c, NULL, md, NULL, keys[k]) == 1)
-                v = EVP_DigestVerify(c, j->sig_data + j->sig_off[i], j->sig_len[i], j->msg_data + j->msg_off[m],
-                                     j->msg_len[m]) == 1;
-        }
+        if (tmpl[k] && EVP_MD_CTX_copy_ex(c, tmpl[k]) == 1)
+            v = EVP_DigestVerify(c, j->sig_data + j->sig_off[i], j->sig_len[i], j->msg_data + j->msg_off[m],
+                                 j->msg_len[m]) == 1;
         j->ok[i] = (uint8_t)v;
     }
     EVP_MD_CTX_free(c);
-    for (uint64_t k = 0; k < j->n_keys; k++)
+    for (uint64_t k = 0; k < j->n_keys; k++) {
+        if (tmpl[k]) EVP_MD_CTX_free(tmpl[k]);
         if (keys[k]) EVP_PKEY_free(keys[k]);
+    }
+    free(tmpl);
     free(keys);
     return NULL;
 }

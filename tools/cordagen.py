@@ -570,9 +570,9 @@ def txids(tb: TxBatch, threads: int = 8) -> np.ndarray:
     return ids.reshape(tb.ntx, 32)
 
 
-# Stand-in for SignableData(txId, SignatureMetadata(platformVersion, schemeNumberID)).serialize():
-# Kryo's bytes are unpinned without a JVM, but for one metadata value they are a
-# fixed byte string with the 32-byte id at a fixed offset — which is all the engine relies on.
+# SignableData(txId, SignatureMetadata(platformVersion, schemeNumberID)).serialize(): the Kryo 4.0.0
+# restatement of corda_amd.kryo (parity unpinned without a JVM).  `total` gives a synthetic
+# SignableData-shaped template of another length instead (template-length coverage only).
 _SIGNABLE_HEAD = (b"corda\x00\x00\x01" + b"\x01\x00net.corda.core.crypto.SignableData\x01\x01"
                   b"net.corda.core.crypto.SecureHash$SHA256\x01\x02net.corda.core.crypto.SignatureMetadata")
 
@@ -583,8 +583,12 @@ class Templates:
     max_len = 0
 
 
-def signable_template(scheme_id: int, platform_version: int = 1, total: int = 200):
-    """(template bytes without the id, id offset): a `total`-byte SignableData-shaped message."""
+def signable_template(scheme_id: int, platform_version: int = 1, total: int = None):
+    """(template bytes without the id, id offset): the Kryo SignableData bytes, or a `total`-byte
+    SignableData-shaped message when `total` is given."""
+    if total is None:
+        from corda_amd import kryo
+        return kryo.signable_data_template(platform_version, scheme_id)
     head = (_SIGNABLE_HEAD + bytes(200))[:total - 32 - 8]
     return head + struct.pack(">ii", platform_version, scheme_id), len(head)
 
