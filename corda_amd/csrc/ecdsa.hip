@@ -640,12 +640,25 @@ __global__ void __launch_bounds__(256) k_ecdsa_comb_fill(uint64_t n_keys, const 
 __global__ void __launch_bounds__(256) k_ec_group_base(uint64_t n_keys, const KeyMeta* __restrict__ meta,
                                                        const uint32_t* __restrict__ key_count,
                                                        uint32_t* __restrict__ key_base, uint32_t* __restrict__ ctr) {
+    // one atomic per workgroup per curve (block prefix sums)
+    __shared__ uint32_t s_wave[4], s_base[2];
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n_keys) return;
-    const KeyMeta m = meta[k];
-    const uint32_t c = key_count[k];
-    if (!m.ok || !c || (m.scheme != CHIP_SCHEME_R1 && m.scheme != CHIP_SCHEME_K1)) return;
-    key_base[k] = atomicAdd(&ctr[m.scheme == CHIP_SCHEME_R1 ? 0 : 1], c);
+    uint32_t c = 0;
+    int curve = -1;
+    if (k < n_keys) {
+        const KeyMeta m = meta[k];
+        c = key_count[k];
+        if (m.ok && c && (m.scheme == CHIP_SCHEME_R1 || m.scheme == CHIP_SCHEME_K1)) curve = m.scheme == CHIP_SCHEME_R1 ? 0 : 1;
+    }
+    uint32_t tot0, tot1;
+    const uint32_t ex0 = block_scan_excl(curve == 0 ? c : 0u, s_wave, tot0);
+    const uint32_t ex1 = block_scan_excl(curve == 1 ? c : 0u, s_wave, tot1);
+    if (threadIdx.x == 0) {
+        s_base[0] = tot0 ? atomicAdd(&ctr[0], tot0) : 0u;
+        s_base[1] = tot1 ? atomicAdd(&ctr[1], tot1) : 0u;
+    }
+    __syncthreads();
+    if (curve >= 0) key_base[k] = s_base[curve] + (curve == 0 ? ex0 : ex1);
 }
 // one lane per (curve list, position): grid covers 2 n lanes, [0, n) r1 and [n, 2n) k1
 __global__ void __launch_bounds__(256) k_ec_group_scatter(uint64_t n, const uint32_t* __restrict__ lists,

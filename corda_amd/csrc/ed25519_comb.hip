@@ -74,19 +74,26 @@ __global__ void __launch_bounds__(256) k_ed_comb_slots(uint64_t n_keys, const Ke
                                                        uint32_t max_slots, uint32_t eager, int32_t* __restrict__ key_slot,
                                                        uint32_t* __restrict__ key_base, uint32_t* __restrict__ slot_key,
                                                        uint32_t* __restrict__ ctr) {
+    // slot and list-range claims: one atomic per workgroup on each counter (block prefix sums)
+    __shared__ uint32_t s_wave[4], s_base[2];
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t c = k < n_keys ? key_count[k] : 0u;
+    const bool want = k < n_keys && ed_key_ok(meta, (uint32_t)k) && c > 0 && c >= min_sigs;
+    uint32_t tot;
+    const uint32_t ex0 = block_scan_excl(want && !eager ? 1u : 0u, s_wave, tot);
+    if (threadIdx.x == 0) s_base[0] = tot ? atomicAdd(&ctr[0], tot) : 0u;
+    __syncthreads();
+    const uint32_t s = eager ? (uint32_t)k : s_base[0] + ex0;
+    const bool got = want && s < max_slots;
+    const uint32_t ex1 = block_scan_excl(got ? c : 0u, s_wave, tot);
+    if (threadIdx.x == 0) s_base[1] = tot ? atomicAdd(&ctr[1], tot) : 0u;
+    __syncthreads();
     if (k >= n_keys) return;
-    int32_t slot = -1;
-    const uint32_t c = key_count[k];
-    if (ed_key_ok(meta, (uint32_t)k) && c > 0 && c >= min_sigs) {
-        const uint32_t s = eager ? (uint32_t)k : atomicAdd(&ctr[0], 1u);
-        if (s < max_slots) {
-            slot = (int32_t)s;
-            slot_key[s] = (uint32_t)k;
-            key_base[k] = atomicAdd(&ctr[1], c);
-        }
+    if (got) {
+        slot_key[s] = (uint32_t)k;
+        key_base[k] = s_base[1] + ex1;
     }
-    key_slot[k] = slot;
+    key_slot[k] = got ? (int32_t)s : -1;
 }
 
 // The comb path only pays when enough signatures take it: its table chain is a fixed serial latency
@@ -125,16 +132,14 @@ __global__ void __launch_bounds__(256) k_ed_comb_partition(const uint32_t* __res
     if (comb && lane == leader) cur = atomicAdd(&key_cur[k], cnt);
     cur = __shfl(cur, (int)leader);
     if (comb) comb_list[key_base[k] + cur + rank] = i;
-    const uint64_t mask = __ballot(straus);
-    if (!mask) return;
-    const uint32_t sl = (uint32_t)__builtin_ctzll(mask);
-    uint32_t base = 0;
-    if (lane == sl) base = atomicAdd(&ctr[2], (uint32_t)__popcll(mask));
-    base = __shfl(base, sl);
-    if (straus) {
-        const uint32_t sr = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
-        straus_list[base + sr] = i;
-    }
+    // Straus list: one atomic per workgroup (block prefix sum)
+    __shared__ uint32_t s_wave[4], s_base;
+    uint32_t tot;
+    const uint32_t ex = block_scan_excl(straus ? 1u : 0u, s_wave, tot);
+    if (!tot) return;   // workgroup-uniform
+    if (threadIdx.x == 0) s_base = atomicAdd(&ctr[2], tot);
+    __syncthreads();
+    if (straus) straus_list[s_base + ex] = i;
 }
 
 // ---- per-key tables ----

@@ -125,7 +125,8 @@ static int fail(chip_ctx* c, int code, const std::string& msg) {
 // wave-aggregated compaction of the signatures that need arithmetic into per-scheme lists.
 // is_valid = 1: Crypto.isValid (Crypto.kt:615-625) has no empty checks: an empty signature falls
 // through to the engine's decode error, empty clear data is verified as an empty message.
-__global__ void __launch_bounds__(256) k_classify(uint64_t n, const uint32_t* __restrict__ key_idx,
+#define CLASSIFY_BLOCK 1024
+__global__ void __launch_bounds__(CLASSIFY_BLOCK) k_classify(uint64_t n, const uint32_t* __restrict__ key_idx,
                                                   const uint32_t* __restrict__ msg_idx,
                                                   const uint32_t* __restrict__ sig_len,
                                                   const uint32_t* __restrict__ msg_len, uint64_t n_keys,
@@ -161,17 +162,32 @@ __global__ void __launch_bounds__(256) k_classify(uint64_t n, const uint32_t* __
         wave_group(arith, k, leader, cnt, rank);
         if (arith && lane == leader) atomicAdd(&key_count[k], cnt);
     }
+    // list slots: one atomic per list per workgroup (per-wave offsets from an LDS prefix)
+    __shared__ uint32_t s_cnt[CLASSIFY_BLOCK / 64][N_LISTS];
+    __shared__ uint32_t s_base[N_LISTS];
+    const uint32_t w = threadIdx.x >> 6;
+    uint64_t mine = 0;
 #pragma unroll
     for (int L = 0; L < N_LISTS; L++) {
         const uint64_t mask = __ballot(list == L);
-        if (!mask) continue;
-        uint32_t base = 0;
-        if (lane == (uint32_t)__builtin_ctzll(mask)) base = atomicAdd(&counts[L], (uint32_t)__popcll(mask));
-        base = __shfl(base, __builtin_ctzll(mask));
-        if (list == L) {
-            const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mask >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mask, 0));
-            lists[(uint64_t)L * n + base + rank] = (uint32_t)i;
+        if (list == L) mine = mask;
+        if (lane == 0) s_cnt[w][L] = (uint32_t)__popcll(mask);
+    }
+    __syncthreads();
+    if (threadIdx.x < N_LISTS) {
+        const uint32_t L = threadIdx.x;
+        uint32_t tot = 0;
+        for (uint32_t j = 0; j < CLASSIFY_BLOCK / 64; j++) {
+            const uint32_t c = s_cnt[j][L];
+            s_cnt[j][L] = tot;
+            tot += c;
         }
+        s_base[L] = tot ? atomicAdd(&counts[L], tot) : 0u;
+    }
+    __syncthreads();
+    if (list >= 0) {
+        const uint32_t rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(mine >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)mine, 0));
+        lists[(uint64_t)list * n + s_base[list] + s_cnt[w][list] + rank] = (uint32_t)i;
     }
 }
 
@@ -444,10 +460,10 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     }
     c->kend(ke, st);
     if (n) {
-        const uint32_t blocks = (uint32_t)((n + 255) / 256);
+        const uint32_t blocks = (uint32_t)((n + CLASSIFY_BLOCK - 1) / CLASSIFY_BLOCK);
         uint32_t* lists = c->lists.as<uint32_t>();
         uint32_t* counts = c->counts.as<uint32_t>();
-        hipLaunchKernelGGL(k_classify, dim3(blocks), dim3(256), 0, st, n, b->key_idx, b->msg_idx, b->sig_len, b->msg_len,
+        hipLaunchKernelGGL(k_classify, dim3(blocks), dim3(CLASSIFY_BLOCK), 0, st, n, b->key_idx, b->msg_idx, b->sig_len, b->msg_len,
                            nk, b->n_msgs, meta, status, lists, counts, (comb || ec_comb) ? w.key_count : nullptr,
                            is_valid ? 1u : 0u);
         const uint32_t* ed_list = lists + (uint64_t)LIST_ED25519 * n;
@@ -528,7 +544,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
                                 c->ectab.as<uint32_t>(), status);
             c->kend(ke, st);
         }
-        if (bitmap) hipLaunchKernelGGL(k_bitmap, dim3(blocks), dim3(256), 0, st, n, status, bitmap);
+        if (bitmap) hipLaunchKernelGGL(k_bitmap, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, n, status, bitmap);
     }
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev1, st));

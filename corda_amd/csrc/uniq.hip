@@ -155,14 +155,15 @@ CHIP_DEV uint32_t tab_find(const uint32_t* __restrict__ tab, uint64_t cap, const
 }
 
 // claim an empty slot for k at or after slot i0 (k absent from the table and distinct among
-// concurrent inserters): the claim is one atomicOr on the occupancy bitmap (a plain read skips
-// slots already known to be taken), the slot is then written with plain stores
+// concurrent inserters): the claim is one atomicOr on the occupancy bitmap, the slot is then
+// written with plain stores.  A plain read first skips slots already known to be taken — except
+// at i0 when the caller's lookup saw it empty (`fresh`): then the atomic alone decides.
 CHIP_DEV void tab_put(uint32_t* tab, uint32_t* bits, uint64_t cap, uint64_t i0, const uint32_t k[KW],
-                      const uint32_t v[10]) {
+                      const uint32_t v[10], bool fresh) {
     uint64_t i = i0 & (cap - 1);
     for (uint64_t n = 0; n < cap; n++) {
         const uint32_t m = 1u << (i & 31);
-        if (!(__builtin_nontemporal_load(&bits[i >> 5]) & m) && !(atomicOr(&bits[i >> 5], m) & m)) {
+        if (((n == 0 && fresh) || !(__builtin_nontemporal_load(&bits[i >> 5]) & m)) && !(atomicOr(&bits[i >> 5], m) & m)) {
             // the whole 128-B line (zero tail): a partial line would cost a read-modify-write in HBM
             uint4* s = reinterpret_cast<uint4*>(tab + i * SLOT_W);
             s[0] = make_uint4(k[0], k[1], k[2], k[3]);
@@ -428,7 +429,7 @@ __global__ void __launch_bounds__(256) k_uniq_insert(uint64_t nref, const uint8_
             for (int q = 0; q < 8; q++) v[q] = id[q];
             v[8] = pos[r];
             v[9] = callers[t];
-            tab_put(tab, bits, cap, empty[r], k, v);
+            tab_put(tab, bits, cap, empty[r], k, v, true);
             ins = true;
         }
     }
@@ -459,7 +460,7 @@ __global__ void __launch_bounds__(256) k_uniq_rebuild(uint64_t n, const uint8_t*
         for (int q = 0; q < 8; q++) v[q] = id[q];
         v[8] = idx[r];
         v[9] = caller[r];
-        tab_put(tab, bits, cap, key_hash(k), k, v);
+        tab_put(tab, bits, cap, key_hash(k), k, v, false);
         ins = true;
     }
     spread_add(inserted, ins ? 1u : 0u);
@@ -477,7 +478,7 @@ __global__ void __launch_bounds__(256) k_uniq_rehash(uint64_t ocap, const uint32
     for (int q = 0; q < KW; q++) k[q] = o[q];
 #pragma unroll
     for (int q = 0; q < 10; q++) v[q] = o[S_VAL + q];
-    tab_put(tab, bits, cap, key_hash(k), k, v);
+    tab_put(tab, bits, cap, key_hash(k), k, v, false);
 }
 
 // ---------------------------------------------------------------------------------------
