@@ -10,9 +10,9 @@
 //             table of ED_COMB_AWIN windows x (2^(W-1)+1) cached multiples built for the batch by
 //             k_ed_comb_chain (the W-fold doubling chain, one lane per key) and k_ed_comb_fill
 //             (the multiples, one lane per key x window);
-//   [S]B    = sum_w e_w (256^w B),       e_w the signed radix-256 digits of S, read from the fixed
-//             table ED_B_COMB (32 x 129 affine Niels rows, 528 KB, L2-resident).
-// 64 + 32 additions per signature (736 field multiplications) instead of 252 doublings + 96
+//   [S]B    = sum_w e_w (2^(16 w) B),    e_w the signed radix-2^16 digits of S, read from the fixed
+//             table built per context by k_ed_bcomb16_build (16 x 32,769 affine Niels rows, 67 MB).
+// 51 + 16 additions per signature (~520 field multiplications) instead of 252 doublings + 96
 // additions (2,766).  The projective R' is inverted in batches of ED_FIN_G by k_ed_comb_finish
 // (Montgomery's trick: ~21 instead of 265 multiplications per signature).
 //
@@ -211,6 +211,130 @@ CHIP_DEV uint32_t xcd_block(uint32_t b, uint32_t used) {
     return (b & 7u) * share + (b >> 3);
 }
 
+// ---- fixed-base comb of B, radix 2^16 (built once per context, 67 MB, Infinity-Cache resident) ----
+// ED_B16[w][j] = j * 2^(16 w) * B for w < 16, j = 0..2^15 (+ padding to whole 64-entry chunks),
+// affine Niels rows of 30 limbs padded to 32 words (one 128-B line per entry).  [S]B then takes 16
+// mixed additions from signed radix-2^16 digits of s instead of 32 from the L2-resident radix-256
+// table: 112 fewer field multiplications per signature for one 128-B gather per window.
+// Build: one lane per (window, chunk of 64 consecutive multiples): j0 * P by double-and-add, then 63
+// additions, the 64 Z inverted together (Montgomery's trick; prefix products in `scratch`).
+CHIP_DEV void ed_niels_to_p3(ge_p3& r, const uint32_t* __restrict__ e) {
+    ge_niels q;
+    ed_load_niels(q, e);
+    fe two, inv2, s, d;
+    fe_0(two);
+    two.v[0] = 2;
+    fe_invert(inv2, two);
+    fe_sub(d, q.ypx, q.ymx);
+    fe_carry(d);
+    fe_add(s, q.ypx, q.ymx);
+    fe_carry(s);
+    fe_mul(r.X, d, inv2);
+    fe_mul(r.Y, s, inv2);
+    fe_1(r.Z);
+    fe_mul(r.T, r.X, r.Y);
+}
+
+__global__ void __launch_bounds__(64) k_ed_bcomb16_build(uint32_t* __restrict__ tab, uint32_t* __restrict__ scratch) {
+    const uint32_t* b8 = ED_B_COMB;   // device symbol (its host-side name is not a device address)
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= ED_B16_WIN * ED_B16_CHUNKS) return;
+    const uint32_t w = g / ED_B16_CHUNKS, chunk = g % ED_B16_CHUNKS, j0 = chunk * 64;
+    // P = 2^(16 w) B = 256^(2w) B: entry 1 of window 2w of the radix-256 table
+    ge_p3 P, Q;
+    ed_niels_to_p3(P, b8 + ((2 * w) * ED_COMB_BENT + 1) * ED_COMB_BSTRIDE);
+    ge_cached pc;
+    ge_p3_to_cached(pc, P);
+    ge_p3_0(Q);
+    ge_p1p1 t;
+    for (int b = 15; b >= 0; b--) {   // Q = j0 * P
+        ge_p3_dbl(t, Q);
+        ge_p1p1_to_p3(Q, t);
+        if ((j0 >> b) & 1u) {
+            ge_add_cached(t, Q, pc, false);
+            ge_p1p1_to_p3(Q, t);
+        }
+    }
+    uint32_t* out = tab + ((uint64_t)w * ED_B16_ENT + j0) * 32;
+    uint32_t* zp = scratch + (uint64_t)g * 64 * 10;
+    fe acc;
+    for (int j = 0; j < 64; j++) {   // X, Y, Z of (j0 + j) P into the entry, prefix products of Z
+        uint32_t* e = out + j * 32;
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            e[q] = Q.X.v[q];
+            e[10 + q] = Q.Y.v[q];
+            e[20 + q] = Q.Z.v[q];
+        }
+        if (j == 0) acc = Q.Z;
+        else fe_mul(acc, acc, Q.Z);
+#pragma unroll
+        for (int q = 0; q < 10; q++) zp[j * 10 + q] = acc.v[q];
+        ge_add_cached(t, Q, pc, false);
+        ge_p1p1_to_p3(Q, t);
+    }
+    fe inv, d2;
+    fe_invert(inv, acc);
+    fe_from_c(d2, ED_D2);
+    for (int j = 63; j >= 0; j--) {
+        uint32_t* e = out + j * 32;
+        fe X, Y, Z, zi, x, y;
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            X.v[q] = e[q];
+            Y.v[q] = e[10 + q];
+            Z.v[q] = e[20 + q];
+        }
+        if (j > 0) {
+            fe prev;
+#pragma unroll
+            for (int q = 0; q < 10; q++) prev.v[q] = zp[(j - 1) * 10 + q];
+            fe_mul(zi, inv, prev);
+            fe_mul(inv, inv, Z);
+        } else {
+            zi = inv;
+        }
+        fe_mul(x, X, zi);
+        fe_mul(y, Y, zi);
+        ge_niels n;
+        fe_add(n.ypx, y, x);
+        fe_carry(n.ypx);
+        fe_sub(n.ymx, y, x);
+        fe_carry(n.ymx);
+        fe xy;
+        fe_mul(xy, x, y);
+        fe_mul(n.xy2d, xy, d2);
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            e[q] = n.ypx.v[q];
+            e[10 + q] = n.ymx.v[q];
+            e[20 + q] = n.xy2d.v[q];
+        }
+        e[30] = 0;
+        e[31] = 0;
+    }
+}
+
+void launch_ed_bcomb16_build(hipStream_t st, uint32_t* tab, uint32_t* scratch) {
+    const uint32_t lanes = ED_B16_WIN * ED_B16_CHUNKS;
+    hipLaunchKernelGGL(k_ed_bcomb16_build, dim3((lanes + 63) / 64), dim3(64), 0, st, tab, scratch);
+}
+uint64_t ed_bcomb16_words() { return (uint64_t)ED_B16_WIN * ED_B16_ENT * 32; }
+uint64_t ed_bcomb16_scratch_words() { return (uint64_t)ED_B16_WIN * ED_B16_CHUNKS * 64 * 10; }
+
+// signed radix-2^16 digits of a (< 2^253), two per word as int16
+CHIP_DEV void recode16(uint32_t out[8], const uint32_t a[8]) {
+    int carry = 0;
+#pragma unroll
+    for (int d = 0; d < 16; d++) {
+        int v = (int)((a[d >> 1] >> (16 * (d & 1))) & 0xffffu) + carry;
+        carry = (v + 0x8000) >> 16;
+        v -= carry << 16;
+        if (d & 1) out[d >> 1] |= (uint32_t)(v & 0xffff) << 16;
+        else out[d >> 1] = (uint32_t)(v & 0xffff);
+    }
+}
+
 // The verify runs in two kernels so that the part that needs no per-key table overlaps the table
 // build on the second stream:
 //   k_ed_comb_bhalf  h = SHA-512(R || Abyte || M) mod L and [S]B from the fixed comb (32 madds);
@@ -230,7 +354,8 @@ __global__ void __launch_bounds__(256) k_ed_comb_bhalf(const uint32_t* __restric
                                                        const uint8_t* __restrict__ msg_data,
                                                        const uint64_t* __restrict__ msg_off,
                                                        const uint32_t* __restrict__ msg_len,
-                                                       const uint32_t* __restrict__ abytes, uint32_t* __restrict__ bmid,
+                                                       const uint32_t* __restrict__ abytes,
+                                                       const uint32_t* __restrict__ b16, uint32_t* __restrict__ bmid,
                                                        uint64_t cap) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= ctr[ED_CTR_NCOMB]) return;
@@ -250,8 +375,9 @@ __global__ void __launch_bounds__(256) k_ed_comb_bhalf(const uint32_t* __restric
     sc_reduce512(h, hx);
     ed_effective_s(s, S);
     uint32_t db[8];
-    recode_bytes<8, 32>(db, s);
-    // [S]B: one mixed (affine Niels) addition per window from the identity; the accumulator carries 2Z
+    recode16(db, s);
+    // [S]B: one mixed (affine Niels) addition per radix-2^16 window from the identity; the
+    // accumulator carries 2Z
     ge_p3 u;
     ge_p3_0(u);
     fe z2;
@@ -264,11 +390,11 @@ __global__ void __launch_bounds__(256) k_ed_comb_bhalf(const uint32_t* __restric
 #pragma unroll
         for (int q = 0; q < 7; q++) db[q] = db[q + 1];
 #pragma unroll
-        for (int e = 0; e < 4; e++) {
-            const int w = wd * 4 + e;
-            const int d = (int)((cur >> (8 * e)) & 0xffu) - 128;
+        for (int e = 0; e < 2; e++) {
+            const int w = wd * 2 + e;
+            const int d = (int)(int16_t)(cur >> (16 * e));
             const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
-            ed_load_niels(nb, ED_B_COMB + ((uint32_t)w * ED_COMB_BENT + ad) * ED_COMB_BSTRIDE);
+            ed_load_niels(nb, b16 + ((uint64_t)w * ED_B16_ENT + ad) * 32);
             if (w > 0) {
                 fe_mul(u.X, t.X, t.T);
                 fe_mul(u.Y, t.Z, t.Y);
@@ -431,7 +557,8 @@ void launch_ed_comb_bhalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, c
                           const EdCombWs& w) {
     if (!n || !w.max_slots) return;
     hipLaunchKernelGGL(k_ed_comb_bhalf, dim3(nblk(n, 256)), dim3(256), 0, st, w.comb_list, w.ctr, b->key_idx, b->msg_idx,
-                       b->sig_data, b->sig_off, b->msg_data, b->msg_off, b->msg_len, abytes, w.bmid, (uint64_t)n);
+                       b->sig_data, b->sig_off, b->msg_data, b->msg_off, b->msg_len, abytes, w.bcomb16, w.bmid,
+                       (uint64_t)n);
 }
 void launch_ed_comb_ahalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w) {
     if (!n || !w.max_slots) return;

@@ -54,7 +54,7 @@ struct chip_ctx {
     DevBuf meta, abytes, edtab, ectab, lists, counts;
     // Ed25519 comb path
     DevBuf c_key_count, c_key_slot, c_key_base, c_key_cur, c_slot_key, c_ctr, c_comb_list, c_straus_list, c_ctab,
-        c_xyz, c_zpre, c_nega, c_bmid, e_ctab, e_mid, e_gcomb, e_wp, e_glist;
+        c_xyz, c_zpre, c_nega, c_bmid, e_ctab, e_mid, e_gcomb, e_bcomb16, e_wp, e_glist;
     // host-path mirrors of the caller's buffers
     DevBuf h_key_idx, h_msg_idx, h_sig_data, h_sig_off, h_sig_len, h_key_data, h_key_off, h_key_len, h_msg_data,
         h_msg_off, h_msg_len, h_status, h_bitmap;
@@ -301,7 +301,17 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
         return CHIP_E_NOMEM;
     }
     launch_ecdsa_gcomb_build(c->stream, c->e_gcomb.as<uint32_t>());
-    if (hipGetLastError() != hipSuccess || hipStreamSynchronize(c->stream) != hipSuccess) {
+    // fixed-base radix-2^16 comb of B for the Ed25519 comb schedule (scratch: batched-inversion prefixes)
+    DevBuf bscratch;
+    if (c->e_bcomb16.ensure(ed_bcomb16_words() * 4) != hipSuccess ||
+        bscratch.ensure(ed_bcomb16_scratch_words() * 4) != hipSuccess) {
+        chip_shutdown(c);
+        return CHIP_E_NOMEM;
+    }
+    launch_ed_bcomb16_build(c->stream, c->e_bcomb16.as<uint32_t>(), bscratch.as<uint32_t>());
+    const bool built = hipGetLastError() == hipSuccess && hipStreamSynchronize(c->stream) == hipSuccess;
+    bscratch.release();
+    if (!built) {
         chip_shutdown(c);
         return CHIP_E_DEVICE;
     }
@@ -323,7 +333,7 @@ void chip_shutdown(chip_ctx* c) {
     hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->meta, &c->abytes, &c->edtab, &c->ectab, &c->lists, &c->counts, &c->c_key_count,
                       &c->c_key_slot, &c->c_key_base, &c->c_key_cur, &c->c_slot_key, &c->c_ctr, &c->c_comb_list,
-                      &c->c_straus_list, &c->c_ctab, &c->c_xyz, &c->c_zpre, &c->c_nega, &c->c_bmid, &c->e_ctab, &c->e_mid, &c->e_gcomb, &c->e_wp, &c->e_glist, &c->h_key_idx, &c->h_msg_idx,
+                      &c->c_straus_list, &c->c_ctab, &c->c_xyz, &c->c_zpre, &c->c_nega, &c->c_bmid, &c->e_ctab, &c->e_mid, &c->e_gcomb, &c->e_bcomb16, &c->e_wp, &c->e_glist, &c->h_key_idx, &c->h_msg_idx,
                       &c->h_sig_data, &c->h_sig_off, &c->h_sig_len, &c->h_key_data, &c->h_key_off, &c->h_key_len,
                       &c->h_msg_data, &c->h_msg_off, &c->h_msg_len, &c->h_status, &c->h_bitmap, &c->t_salts,
                       &c->t_start, &c->t_group, &c->t_internal, &c->t_data, &c->t_off, &c->t_len, &c->t_ids,
@@ -416,6 +426,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         w.zpre = c->c_zpre.as<uint32_t>();
         w.nega = c->c_nega.as<uint32_t>();
         w.bmid = c->c_bmid.as<uint32_t>();
+        w.bcomb16 = c->e_bcomb16.as<uint32_t>();
         w.max_slots = (uint32_t)slots;
         w.min_sigs = c->comb_min_sigs;
         w.min_total = c->comb_min_total;

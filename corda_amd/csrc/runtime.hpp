@@ -52,12 +52,15 @@ void launch_ftx_verify(hipStream_t st, const chip_ftx_batch* b, uint8_t* status,
 // ---- Ed25519 per-key comb path (ed25519_comb.hip) ----
 // A comb geometry: signed radix-2^ED_COMB_W digits of h (< L < 2^253), one table window per digit
 #ifndef ED_COMB_W
-#define ED_COMB_W 4
+#define ED_COMB_W 5
 #endif
-#define ED_COMB_AWIN ((253 + ED_COMB_W - 1) / ED_COMB_W)   // W=4: 64 windows (top digit <= 2)
+#define ED_COMB_AWIN ((253 + ED_COMB_W - 1) / ED_COMB_W)   // W=5: 51 windows (top digit <= 8)
 #define ED_COMB_AENT ((1 << (ED_COMB_W - 1)) + 1)          // multiples 0..2^(W-1)
 #define ED_COMB_KEY_WORDS (ED_COMB_AWIN * ED_COMB_AENT * 40)
 #define ED_FIN_G 16                                        // signatures per batched inversion
+#define ED_B16_WIN 16                                      // radix-2^16 fixed-base comb of B
+#define ED_B16_CHUNKS 513                                  // 64-entry chunks per window (0..2^15)
+#define ED_B16_ENT (ED_B16_CHUNKS * 64)
 
 struct EdCombWs {
     uint32_t* key_count;    // [n_keys] Ed25519 signatures per key needing arithmetic (k_classify)
@@ -73,7 +76,8 @@ struct EdCombWs {
     uint32_t* xyz;          // [30][n] projective R' (SoA), comb path
     uint32_t* zpre;         // [10][n] prefix products of the batched inversion
     uint32_t* nega;         // [n_keys][40] -A in extended coordinates (key prep)
-    uint32_t* bmid;         // [48][n] [S]B (extended) + h, from the table-free half to the table half
+    uint32_t* bmid;         // [40 + ED_COMB_ADW][n] [S]B (extended) + h's digits, bhalf -> ahalf
+    const uint32_t* bcomb16;  // fixed-base comb of B (per context)
     uint32_t max_slots, min_sigs;
     uint32_t min_total;     // fewer comb-bound signatures than this: all go to Straus (non-eager)
     uint32_t eager;        // tables for every Ed25519 key at slot = key index, built during classify
@@ -88,6 +92,10 @@ void launch_ed_comb_build(hipStream_t st, uint64_t n, uint64_t n_keys, const Key
 // the comb verify in two halves: bhalf (SHA-512 challenge + [S]B, no per-key table: runs while the
 // tables are built on the second stream) and ahalf (+ [h](-A) from the key's table)
 uint64_t ed_comb_bmid_words();
+// fixed-base radix-2^16 comb of B (built once per context; scratch freed after the build)
+uint64_t ed_bcomb16_words();
+uint64_t ed_bcomb16_scratch_words();
+void launch_ed_bcomb16_build(hipStream_t st, uint32_t* tab, uint32_t* scratch);
 void launch_ed_comb_bhalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, const uint32_t* abytes,
                           const EdCombWs& w);
 void launch_ed_comb_ahalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w);
