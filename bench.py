@@ -38,14 +38,23 @@ for _p in (ROOT, os.path.join(ROOT, "tools"), os.path.join(ROOT, "tests")):
 
 import numpy as np  # noqa: E402
 
+_T0 = time.time()
+
+
+def progress(msg):
+    """One stderr line per finished leg (long profiler passes keep writing while they run)."""
+    print("[bench %7.1fs] %s" % (time.time() - _T0, msg), file=sys.stderr, flush=True)
+
 # Fixed algorithmic work per unit (DESIGN.md §4-5; pinned from the algorithm each kernel runs).
 # 32x32->64 multiply-accumulates (v_mad_u64_u32) per signature:
 #   Ed25519 comb, radix 2^25.5 (100 limb products per GF(2^255-19) multiplication):
-#     k_ed_comb_bhalf: 32 Niels adds (3 mults) + 31 conversions (4) + 1 final conversion (4) = 224 mults
-#     k_ed_comb_ahalf: 64 cached adds (4 mults) + 63 conversions (4) + 3 final = 511 mults
-ED_COMB_MACS_B = 22_400
-ED_COMB_MACS_A = 51_100
-ED_COMB_MACS_PER_VERIFY = ED_COMB_MACS_A + ED_COMB_MACS_B          # 73,500
+#     k_ed_comb_bhalf: [S]B from the radix-2^16 fixed-base comb: 16 Niels adds (3 mults) + 15
+#                      conversions (4) + 1 final conversion (4) = 112 mults (+ SHA-512, not counted)
+#     k_ed_comb_ahalf: [h](-A) from the per-key radix-32 comb: 51 cached adds (4 mults) + 50
+#                      conversions (4) + 3 final = 407 mults
+ED_COMB_MACS_B = 11_200
+ED_COMB_MACS_A = 40_700
+ED_COMB_MACS_PER_VERIFY = ED_COMB_MACS_A + ED_COMB_MACS_B          # 51,900
 #   Ed25519 windowed Straus (k_ed25519_verify): 252 doublings (4 squarings each) + the encode
 #   inversion (254 squarings) = 1,262 squarings x 55 limb products, and 1,504 multiplications x 100
 #   (doubling-chain conversions 819, 64 cached A-adds 256 + conversions 192, 32 B-madds 224, 11 + 2
@@ -318,6 +327,7 @@ def main():
     del db, status, bitmap, gathered
 
     secondary = {}
+    progress("cfg2 headline done")
     # ---- cfg2 through the host-buffer entry (staging H2D + pipeline + D2H, blocking) ----
     if not args.no_host_path:
         ctx.verify_batch(batch)
@@ -335,6 +345,7 @@ def main():
             "cfg2_host_path_correct": bool(np.array_equal(hst, batch.expected)),
         })
 
+    progress("cfg2 host path done")
     # ---- cold keys: every signature its own key (windowed Straus kernel) ----
     if args.cold_n:
         cb = G.ed25519_batch(args.cold_n, n_keys=args.cold_n, seed=0x5EED0012 + rank, threads=gen_threads)
@@ -364,6 +375,7 @@ def main():
         })
         del dc, cst, cbm, cb
 
+    progress("cold-key leg done")
     # ---- cfg4: tx ids alone, then ids + required signers fused (1M tx, 2M Ed25519 signers) ----
     if not args.no_txid:
         tb, tm, sb, ids_ref, _msgs = G.cfg4_workload(args.txid_n, n_keys=args.keys, seed=0x5EED0004 + rank,
@@ -420,14 +432,17 @@ def main():
         })
         del dt, ids, dm, ds, fst, fbm, tb, tm, sb
 
+    progress("cfg4 legs done")
     # ---- cfg3: mixed ECDSA r1/k1, one global batch sharded by transaction, RCCL bitmap all-gather ----
     if not args.no_ecdsa:
         secondary.update(ecdsa_leg(args, ctx, world, rank, torch, dev, dist, D, G, native, gen_threads, stream))
 
+    progress("cfg3 legs done")
     # ---- cfg5: notary batch (uniqueness against a 10M-row log + one notary signature per tx) ----
     if not args.no_notary:
         secondary.update(notary_leg(args, ctx, world, rank, torch, dev, dist, D, G, native, gen_threads, stream))
 
+    progress("cfg5 leg done")
     # ---- CPU baselines (rank 0, N = 1 only): the oracle restatement and OpenSSL on host cores ----
     cpu = cpu_ossl = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -559,7 +574,7 @@ def ecdsa_leg(args, ctx, world, rank, torch, dev, dist, D, G, native, threads, s
         "ecdsa_correct_vs_labels": ecorrect,
         "ecdsa_ms_per_step": step_ms,
         "ecdsa_front_ms": front_ms, "ecdsa_tables_aux_ms": tab_ms,
-        "ecdsa_q_r1_kernel_ms": r1_ms, "ecdsa_q_k1_kernel_ms": k1_ms,
+        "ecdsa_q_kernel_ms": r1_ms + k1_ms,   # k_ecdsa_comb_q, both curves in one launch
         "ecdsa_roofline_frac": ECDSA_COMB_MACS_PER_VERIFY * n_arith / (step_ms * 1e-3) / 1e12 / MAC_PEAK_T,
         "ecdsa_q_roofline_frac": ECDSA_Q_MACS_PER_VERIFY * n_arith / ((r1_ms + k1_ms) * 1e-3) / 1e12 / MAC_PEAK_T,
         "ecdsa_roofline_note": "%d MACs/signature (87 mixed additions x 592 + scalar work) over the whole step; "

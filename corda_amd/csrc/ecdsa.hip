@@ -613,9 +613,13 @@ CHIP_DEV void ec_comb_fill(uint32_t* __restrict__ jac, uint32_t* __restrict__ ou
 }
 // one launch for both curves: r1 and k1 keys build concurrently (lane per key)
 __global__ void __launch_bounds__(64) k_ecdsa_comb_chain(uint64_t n_keys, const KeyMeta* __restrict__ meta,
-                                                         const uint32_t* __restrict__ ectab, uint32_t* __restrict__ jac) {
+                                                         const uint32_t* __restrict__ ectab, uint32_t* __restrict__ jac,
+                                                         uint32_t prio) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_keys) return;
+    // the chain is the latency-bound critical path of the step: win VALU arbitration against the
+    // throughput kernels of the main stream that share its SIMDs
+    if (prio) __builtin_amdgcn_s_setprio(3);
     if (ec_key_ok(meta, k, CHIP_SCHEME_R1)) ec_comb_chain<CURVE_R1 | CURVE_ILP>(ectab, jac, k);
     else if (ec_key_ok(meta, k, CHIP_SCHEME_K1)) ec_comb_chain<CURVE_K1 | CURVE_ILP>(ectab, jac, k);
 }
@@ -713,15 +717,6 @@ CHIP_DEV void wave_shfl_down(u256& o, const u256& v, int d) {
     for (int k = 0; k < 8; k++) o.w[k] = (uint32_t)__shfl_down((int)v.w[k], d, 64);
 }
 
-// blocks b, b+8, b+16, ... are dispatched to one XCD: give them consecutive work.  `used` = blocks
-// that hold list positions (the list count is known on the device only; the grid covers the
-// capacity): each XCD takes ceil(used / 8) consecutive blocks, so the work stays spread over all 8
-// XCDs however short the list is.  Returns a block index >= used for blocks without work.
-CHIP_DEV uint32_t ec_xcd_block(uint32_t b, uint32_t used) {
-    const uint32_t share = (used + 7) >> 3;
-    return (b & 7u) * share + (b >> 3);
-}
-
 // A.  The wave-level part of the batched inversion: inclusive prefix and suffix products of s R
 // across the 64 lanes (Hillis-Steele scans over shuffles); the exclusive products stay with the
 // lane, the wave's total goes to k_ecdsa_comb_inv.  Lanes without an arithmetic signature pass the
@@ -804,10 +799,9 @@ __global__ void __launch_bounds__(64) k_ecdsa_comb_inv(const uint32_t* __restric
 
 // C.  s^-1, u1, u2 and u1 G from the fixed comb.
 template <int C>
-__global__ void __launch_bounds__(256) k_ecdsa_comb_g(const uint32_t* __restrict__ count,
-                                                      const uint32_t* __restrict__ gcomb, uint32_t* __restrict__ mid,
-                                                      const uint32_t* __restrict__ wp, uint64_t cap) {
-    const uint32_t gid = blockIdx.x * blockDim.x + threadIdx.x;
+CHIP_DEV void comb_g_body(uint32_t blk, const uint32_t* __restrict__ count, const uint32_t* __restrict__ gcomb,
+                          uint32_t* __restrict__ mid, const uint32_t* __restrict__ wp, uint64_t cap) {
+    const uint32_t gid = blk * blockDim.x + threadIdx.x;
     if (gid >= *count || !mid[(uint64_t)40 * cap + gid]) return;
     u256 e, r, ep, es, winv, wm, u1, u2;
     mid_load(ep, mid, cap, gid, 8);
@@ -846,17 +840,25 @@ __global__ void __launch_bounds__(256) k_ecdsa_comb_g(const uint32_t* __restrict
     mid_store(mid, cap, gid, 16, acc.Z);
     mid_store(mid, cap, gid, 24, u2);
 }
+// both curves in one grid (blocks [0, half) P-256, the rest secp256k1): the secp256k1 blocks fill
+// the chip while the last P-256 waves drain instead of waiting for a second launch
+__global__ void __launch_bounds__(256) k_ecdsa_comb_g(const uint32_t* __restrict__ counts,
+                                                      const uint32_t* __restrict__ gcomb, uint32_t* __restrict__ mid_r1,
+                                                      uint32_t* __restrict__ mid_k1, const uint32_t* __restrict__ wp_r1,
+                                                      const uint32_t* __restrict__ wp_k1, uint64_t cap, uint32_t half) {
+    if (blockIdx.x < half) comb_g_body<CURVE_R1>(blockIdx.x, counts + LIST_R1, gcomb, mid_r1, wp_r1, cap);
+    else comb_g_body<CURVE_K1>(blockIdx.x - half, counts + LIST_K1, gcomb, mid_k1, wp_k1, cap);
+}
 
 // D.  u2 Q half: one mixed addition per non-zero radix-16 digit from the key's affine table, then
 // x(R) mod n == r exactly as k_ecdsa_verify checks it.  The list is grouped by key and consecutive
 // blocks run on one XCD, so a key's 33 KB table is read from one L2.
 template <int C>
-__global__ void __launch_bounds__(256) k_ecdsa_comb_q(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
-                                                      const uint32_t* __restrict__ key_idx,
-                                                      const uint32_t* __restrict__ ctab, const uint32_t* __restrict__ mid,
-                                                      uint64_t cap, uint8_t* __restrict__ status, uint32_t remap) {
+CHIP_DEV void comb_q_body(uint32_t blk, const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
+                          const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ ctab,
+                          const uint32_t* __restrict__ mid, uint64_t cap, uint8_t* __restrict__ status) {
     const uint32_t n = *count;
-    const uint32_t gid = (remap ? ec_xcd_block(blockIdx.x, (n + 255) / 256) : blockIdx.x) * blockDim.x + threadIdx.x;
+    const uint32_t gid = blk * blockDim.x + threadIdx.x;
     if (gid >= n || !mid[(uint64_t)40 * cap + gid]) return;
     const uint32_t i = list[gid];
     jpt acc;
@@ -888,6 +890,18 @@ __global__ void __launch_bounds__(256) k_ecdsa_comb_q(const uint32_t* __restrict
     }
     status[i] = ecdsa_check<C>(acc, r) ? CHIP_VALID : CHIP_INVALID;
 }
+// both curves in one grid, as k_ecdsa_comb_g
+__global__ void __launch_bounds__(256) k_ecdsa_comb_q(const uint32_t* __restrict__ list_r1,
+                                                      const uint32_t* __restrict__ list_k1,
+                                                      const uint32_t* __restrict__ counts,
+                                                      const uint32_t* __restrict__ key_idx,
+                                                      const uint32_t* __restrict__ ctab,
+                                                      const uint32_t* __restrict__ mid_r1,
+                                                      const uint32_t* __restrict__ mid_k1, uint64_t cap,
+                                                      uint8_t* __restrict__ status, uint32_t half) {
+    if (blockIdx.x < half) comb_q_body<CURVE_R1>(blockIdx.x, list_r1, counts + LIST_R1, key_idx, ctab, mid_r1, cap, status);
+    else comb_q_body<CURVE_K1>(blockIdx.x - half, list_k1, counts + LIST_K1, key_idx, ctab, mid_k1, cap, status);
+}
 
 uint64_t ecdsa_comb_key_words() { return EC_COMB_KEY_WORDS + EC_COMB_JAC_WORDS; }
 
@@ -895,8 +909,12 @@ void launch_ecdsa_comb_build(hipStream_t st, uint64_t n_keys, const KeyMeta* met
                              uint32_t* ctab) {
     if (!n_keys) return;
     uint32_t* jac = ctab + n_keys * EC_COMB_KEY_WORDS;
+    static const uint32_t prio = [] {
+        const char* e = getenv("CHIP_CHAIN_PRIO");
+        return e ? (uint32_t)(e[0] != '0') : 1u;
+    }();
     hipLaunchKernelGGL(k_ecdsa_comb_chain, dim3((uint32_t)((n_keys + 63) / 64)), dim3(64), 0, st, n_keys, meta, ectab,
-                       jac);
+                       jac, prio);
     hipLaunchKernelGGL(k_ecdsa_comb_fill, dim3((uint32_t)((n_keys * EC_FILL_LANES + 255) / 256)), dim3(256), 0, st, n_keys,
                        meta, ctab, jac);
 }
@@ -933,24 +951,18 @@ void launch_ecdsa_comb_inv(hipStream_t st, uint64_t n, const uint32_t* counts, u
     const uint32_t nw = (uint32_t)((n + 63) / 64);
     hipLaunchKernelGGL(k_ecdsa_comb_inv, dim3((2 * nw + 63) / 64), dim3(64), 0, st, counts, wp_r1, wp_k1, nw);
 }
-void launch_ecdsa_comb_g(hipStream_t st, int scheme, uint64_t n, const uint32_t* count, const uint32_t* gcomb,
-                         uint32_t* mid, const uint32_t* wp) {
+void launch_ecdsa_comb_g(hipStream_t st, uint64_t n, const uint32_t* counts, const uint32_t* gcomb, uint32_t* mid_r1,
+                         uint32_t* mid_k1, const uint32_t* wp_r1, const uint32_t* wp_k1) {
     if (!n) return;
-    const uint32_t blocks = (uint32_t)((n + 255) / 256);
-    if (scheme == CHIP_SCHEME_R1)
-        hipLaunchKernelGGL(k_ecdsa_comb_g<CURVE_R1>, dim3(blocks), dim3(256), 0, st, count, gcomb, mid, wp, (uint64_t)n);
-    else
-        hipLaunchKernelGGL(k_ecdsa_comb_g<CURVE_K1>, dim3(blocks), dim3(256), 0, st, count, gcomb, mid, wp, (uint64_t)n);
+    const uint32_t half = (uint32_t)((n + 255) / 256);
+    hipLaunchKernelGGL(k_ecdsa_comb_g, dim3(2 * half), dim3(256), 0, st, counts, gcomb, mid_r1, mid_k1, wp_r1, wp_k1,
+                       (uint64_t)n, half);
 }
-void launch_ecdsa_comb_q(hipStream_t st, int scheme, uint64_t n, const uint32_t* list, const uint32_t* count,
-                         const chip_sig_batch* b, const uint32_t* ctab, const uint32_t* mid, uint8_t* status) {
+void launch_ecdsa_comb_q(hipStream_t st, uint64_t n, const uint32_t* list_r1, const uint32_t* list_k1,
+                         const uint32_t* counts, const chip_sig_batch* b, const uint32_t* ctab, const uint32_t* mid_r1,
+                         const uint32_t* mid_k1, uint8_t* status) {
     if (!n) return;
-    const uint32_t blocks = ((uint32_t)((n + 255) / 256) + 7) & ~7u;   // multiple of 8 for the XCD remap
-    static const uint32_t remap = getenv("CHIP_EC_XCD") ? (getenv("CHIP_EC_XCD")[0] == '1') : 0u;   // measured slower on cfg3
-    if (scheme == CHIP_SCHEME_R1)
-        hipLaunchKernelGGL(k_ecdsa_comb_q<CURVE_R1>, dim3(blocks), dim3(256), 0, st, list, count, b->key_idx, ctab, mid,
-                           (uint64_t)n, status, remap);
-    else
-        hipLaunchKernelGGL(k_ecdsa_comb_q<CURVE_K1>, dim3(blocks), dim3(256), 0, st, list, count, b->key_idx, ctab, mid,
-                           (uint64_t)n, status, remap);
+    const uint32_t half = (uint32_t)((n + 255) / 256);
+    hipLaunchKernelGGL(k_ecdsa_comb_q, dim3(2 * half), dim3(256), 0, st, list_r1, list_k1, counts, b->key_idx, ctab,
+                       mid_r1, mid_k1, (uint64_t)n, status, half);
 }

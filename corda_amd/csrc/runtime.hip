@@ -510,8 +510,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
             launch_ecdsa_comb_pre(st, CHIP_SCHEME_R1, n, gl_r1, counts + LIST_R1, b, mid_r1, wp_r1, status);
             launch_ecdsa_comb_pre(st, CHIP_SCHEME_K1, n, gl_k1, counts + LIST_K1, b, mid_k1, wp_k1, status);
             launch_ecdsa_comb_inv(st, n, counts, wp_r1, wp_k1);
-            launch_ecdsa_comb_g(st, CHIP_SCHEME_R1, n, counts + LIST_R1, c->e_gcomb.as<uint32_t>(), mid_r1, wp_r1);
-            launch_ecdsa_comb_g(st, CHIP_SCHEME_K1, n, counts + LIST_K1, c->e_gcomb.as<uint32_t>(), mid_k1, wp_k1);
+            launch_ecdsa_comb_g(st, n, counts, c->e_gcomb.as<uint32_t>(), mid_r1, mid_k1, wp_r1, wp_k1);
             c->kend(ke, st);
         }
         // ---- kernels that read the per-key tables ----
@@ -537,13 +536,8 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         c->kend(ke, st);
         if (ec_comb) {
             HIPCHK(c, hipStreamWaitEvent(st, c->ev_join2, 0));
-            ke = c->kbegin(CHIP_K_ECDSA_R1, st);
-            launch_ecdsa_comb_q(st, CHIP_SCHEME_R1, n, gl_r1, counts + LIST_R1, b, c->e_ctab.as<uint32_t>(), mid_r1,
-                                status);
-            c->kend(ke, st);
-            ke = c->kbegin(CHIP_K_ECDSA_K1, st);
-            launch_ecdsa_comb_q(st, CHIP_SCHEME_K1, n, gl_k1, counts + LIST_K1, b, c->e_ctab.as<uint32_t>(), mid_k1,
-                                status);
+            ke = c->kbegin(CHIP_K_ECDSA_R1, st);   // both curves' table halves (one launch)
+            launch_ecdsa_comb_q(st, n, gl_r1, gl_k1, counts, b, c->e_ctab.as<uint32_t>(), mid_r1, mid_k1, status);
             c->kend(ke, st);
         } else {
             ke = c->kbegin(CHIP_K_ECDSA_R1, st);

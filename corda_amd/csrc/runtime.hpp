@@ -36,10 +36,12 @@ void launch_ecdsa_group(hipStream_t st, uint64_t n, uint64_t n_keys, const KeyMe
 void launch_ecdsa_comb_pre(hipStream_t st, int scheme, uint64_t n, const uint32_t* list, const uint32_t* count,
                            const chip_sig_batch* b, uint32_t* mid, uint32_t* wp, uint8_t* status);
 void launch_ecdsa_comb_inv(hipStream_t st, uint64_t n, const uint32_t* counts, uint32_t* wp_r1, uint32_t* wp_k1);
-void launch_ecdsa_comb_g(hipStream_t st, int scheme, uint64_t n, const uint32_t* count, const uint32_t* gcomb,
-                         uint32_t* mid, const uint32_t* wp);
-void launch_ecdsa_comb_q(hipStream_t st, int scheme, uint64_t n, const uint32_t* list, const uint32_t* count,
-                         const chip_sig_batch* b, const uint32_t* ctab, const uint32_t* mid, uint8_t* status);
+// g and q run both curves in one grid (P-256 blocks first)
+void launch_ecdsa_comb_g(hipStream_t st, uint64_t n, const uint32_t* counts, const uint32_t* gcomb, uint32_t* mid_r1,
+                         uint32_t* mid_k1, const uint32_t* wp_r1, const uint32_t* wp_k1);
+void launch_ecdsa_comb_q(hipStream_t st, uint64_t n, const uint32_t* list_r1, const uint32_t* list_k1,
+                         const uint32_t* counts, const chip_sig_batch* b, const uint32_t* ctab, const uint32_t* mid_r1,
+                         const uint32_t* mid_k1, uint8_t* status);
 
 void launch_txid(hipStream_t st, const chip_tx_batch* b, uint8_t* ids, uint32_t* scratch, uint64_t scratch_words);
 uint64_t ftx_scratch_words(uint64_t ntx);

@@ -341,8 +341,9 @@ int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_st
 /* CHIP_K_ED_COMB = k_ed_comb_ahalf (+[h](-A) from the per-key table), CHIP_K_ED_COMB_B =
  * k_ed_comb_bhalf (challenge hash + [S]B, no table), CHIP_K_ED_TABLES / CHIP_K_EC_TABLES = per-key comb
  * table builds (on the context's second stream when every key gets a table), CHIP_K_ED_PLAN = slot
- * assignment + key-grouped work list; CHIP_K_ECDSA_R1/K1 = the per-curve kernel that needs the key's
- * table (k_ecdsa_comb_q, or k_ecdsa_verify on the windowed schedule), CHIP_K_EC_FRONT = the ECDSA comb
+ * assignment + key-grouped work list; CHIP_K_ECDSA_R1/K1 = the ECDSA kernels that need the key's
+ * table: k_ecdsa_verify per curve on the windowed schedule; on the comb schedule k_ecdsa_comb_q runs
+ * both curves in one launch, counted under CHIP_K_ECDSA_R1; CHIP_K_EC_FRONT = the ECDSA comb
  * kernels that need none (key grouping, DER/SHA-256/s R, batched s^-1, u1 G; both curves) */
 enum chip_kernel { CHIP_K_ED25519 = 0, CHIP_K_ECDSA_R1 = 1, CHIP_K_ECDSA_K1 = 2, CHIP_K_TXID = 3,
                    CHIP_K_KEYPREP = 4, CHIP_K_UNIQ = 5, CHIP_K_ED_COMB = 6, CHIP_K_ED_FINISH = 7,

@@ -6,7 +6,7 @@ TAG=${1:-ab}
 OUT=$REPO/gpurun_out/$TAG
 mkdir -p $OUT
 cd $REPO
-VARS=("" "CHIP_EC_GROUP=0")
+VARS=("")
 for v in "${VARS[@]}"; do
   env $v timeout -k 10 120 python3 tools/bench_ecdsa.py --steps 5 >> $OUT/ab.jsonl 2>>$OUT/ab.err || { echo "variant '$v' failed"; tail -5 $OUT/ab.err; exit 1; }
 done

@@ -1,7 +1,8 @@
 #!/bin/bash
 # rocprofv3 passes for the judged profiles (run on the GPU box through gpurun):
-#   1. kernel trace + stats over the default bench command
-#   2-4. PMC passes (one counter group per run, kernel-trace only) over a reduced bench
+#   1. kernel trace + stats over the default bench command (every leg, full sizes)
+#   2-5. PMC passes, one counter group per run (kernel trace only, no other trace domains), over
+#        every leg at full size but fewer steps: SQ issue counters, FETCH_SIZE, WRITE_SIZE, L2 hits
 # Outputs under gpurun_out/prof_<tag>/; copy the summaries into profiles/<round>/.
 set -euo pipefail
 TAG=${1:-run}
@@ -10,13 +11,16 @@ OUT=$REPO/gpurun_out/prof_$TAG
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 cd /tmp
-BENCH_SMALL="$REPO/bench.py --steps 2 --warmup 1 --no-ecdsa --no-notary --no-cpu-baseline"
+BENCH_PMC="$REPO/bench.py --steps 2 --warmup 1 --no-cpu-baseline --no-host-path --no-notary-check"
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$OUT/kt" -o kt --output-format csv -- \
     python3 "$REPO/bench.py" --steps 5 --warmup 2 > "$OUT/bench_kt.json" 2> "$OUT/bench_kt.err"
-timeout -s KILL 240 rocprofv3 --kernel-trace --pmc SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_WAVE_CYCLES \
-    SQ_BUSY_CYCLES -d "$OUT/sq" -o sq --output-format csv -- python3 $BENCH_SMALL > "$OUT/bench_sq.json" 2> "$OUT/bench_sq.err"
-timeout -s KILL 240 rocprofv3 --kernel-trace --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv -- \
-    python3 $BENCH_SMALL > "$OUT/bench_fetch.json" 2> "$OUT/bench_fetch.err"
-timeout -s KILL 240 rocprofv3 --kernel-trace --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv -- \
-    python3 $BENCH_SMALL > "$OUT/bench_write.json" 2> "$OUT/bench_write.err"
-find "$OUT" -name "*.csv" | head -50
+pass() {   # pass <name> <counters...>
+    local name=$1; shift
+    timeout -s KILL 400 rocprofv3 --kernel-trace --pmc "$@" -d "$OUT/$name" -o "$name" --output-format csv -- \
+        python3 $BENCH_PMC > "$OUT/bench_$name.json" 2> "$OUT/bench_$name.err"
+}
+pass sq SQ_INSTS_VALU SQ_WAVES SQ_INSTS_SALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES
+pass fetch FETCH_SIZE
+pass write WRITE_SIZE
+pass tcc TCC_HIT_sum TCC_MISS_sum
+find "$OUT" -name "*counter_collection.csv" -o -name "kt_kernel_stats.csv" | head -20
