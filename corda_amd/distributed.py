@@ -65,12 +65,14 @@ def status_to_bitmap(status):
     return np.bitwise_or.reduce(b << np.arange(64, dtype=np.uint64), axis=1).astype(np.uint64)
 
 
-def verify_sharded(verify_fn, batch, group=None):
+def verify_sharded(verify_fn, batch, group=None, msg_idx=None):
     """Shard `batch` by transaction over the process group, verify the local shard with
-    verify_fn(sub_batch) -> status (torch uint8 tensor), and all-gather the statuses."""
+    verify_fn(sub_batch) -> status (torch uint8 tensor), and all-gather the statuses.  `batch` may be
+    device-resident (torch tensors: the shard is a view, verified by chip_verify_batch_device); the
+    transaction boundaries then come from the host copy `msg_idx`."""
     import torch.distributed as dist
     world, rank = dist.get_world_size(group), dist.get_rank(group)
-    ranges = tx_ranges(np.asarray(batch.msg_idx), world)
+    ranges = tx_ranges(np.asarray(batch.msg_idx if msg_idx is None else msg_idx), world)
     lo, hi = ranges[rank]
     local = verify_fn(sub_batch(batch, lo, hi))
     return gather_status(local, ranges, group)
@@ -145,6 +147,33 @@ def route_rows(refs36, world: int):
     return [np.nonzero(own == r)[0] for r in range(world)]
 
 
+REC_BYTES = 56   # sizeof(chip_conflict)
+
+
+def gather_records(local, group=None):
+    """All-gather every rank's Conflict.stateHistory records as raw chip_conflict bytes (a u8 tensor
+    of n * 56 bytes, on the GPU with RCCL) — one count all-gather and one padded record all-gather,
+    no pickled host objects — and merge them in (tx, input_index) order."""
+    import torch
+    import torch.distributed as dist
+    from .native import records_from_bytes
+    world = dist.get_world_size(group)
+    host = dist.get_backend(group) != "nccl"
+    dev = torch.device("cpu") if host else local.device
+    loc = local.to(dev)
+    n = torch.tensor([loc.numel() // REC_BYTES], dtype=torch.int64, device=dev)
+    counts = torch.empty(world, dtype=torch.int64, device=dev)
+    dist.all_gather_into_tensor(counts, n, group=group)
+    width = max(1, int(counts.max().item())) * REC_BYTES
+    buf = torch.zeros(width, dtype=torch.uint8, device=dev)
+    buf[:loc.numel()] = loc
+    out = torch.empty(world * width, dtype=torch.uint8, device=dev)
+    dist.all_gather_into_tensor(out, buf, group=group)
+    raw = out.cpu().numpy()
+    per = [records_from_bytes(raw[r * width:r * width + int(counts[r]) * REC_BYTES].tobytes()) for r in range(world)]
+    return merge_records(per)
+
+
 def merge_records(per_shard):
     """Union of the shards' Conflict.stateHistory records in (tx, input_index) order."""
     out = [rec for recs in per_shard for rec in recs]
@@ -208,7 +237,13 @@ def commit_sharded(engine, batch, group=None, shard=None):
         if engine.apply(v) == 0:
             break
     v = reduce_max(engine.classify())
-    status, recs = engine.finish(v)
-    gathered = [None] * world
-    dist.all_gather_object(gathered, recs, group=group)
-    return status, merge_records(gathered), rounds
+    if hasattr(engine, "finish_device"):
+        st, local = engine.finish_device(v)
+        status = st.cpu().numpy()
+    else:   # host-side shard engines (CPU tests): the same byte records, through the same collective
+        import torch
+        from .native import records_to_bytes
+        status, recs = engine.finish(v)
+        local = torch.frombuffer(bytearray(records_to_bytes(recs)) or bytearray(1), dtype=torch.uint8)
+        local = local[:len(recs) * REC_BYTES]
+    return status, gather_records(local, group), rounds

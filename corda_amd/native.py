@@ -434,8 +434,17 @@ class UniqTable:
         return st, recs
 
 
+def records_to_bytes(recs) -> bytes:
+    """[(tx, input_index, consumed_index, consuming_tx, caller)] -> ChipConflict records (56 B each)."""
+    arr = (ChipConflict * len(recs))()
+    for a, (tx, i, ci, cid, cc) in zip(arr, recs):
+        a.tx, a.input_index, a.consumed_index, a.consuming_caller, a.pad = tx, i, ci, cc, 0
+        ctypes.memmove(a.consuming_tx, bytes(cid), 32)
+    return bytes(arr)
+
+
 def records_from_bytes(raw: bytes):
-    """ChipConflict records (48 bytes each) -> [(tx, input_index, consumed_index, consuming_tx, caller)]."""
+    """ChipConflict records (56 bytes each) -> [(tx, input_index, consumed_index, consuming_tx, caller)]."""
     n = len(raw) // ctypes.sizeof(ChipConflict)
     arr = (ChipConflict * n).from_buffer_copy(raw[:n * ctypes.sizeof(ChipConflict)])
     return [(c.tx, c.input_index, c.consumed_index, bytes(c.consuming_tx), c.consuming_caller) for c in arr]
@@ -512,8 +521,9 @@ class UniqShardEngine:
         self._to_torch()
         return self.vote_buf[:self.ntx]
 
-    def finish(self, decision):
-        """-> (status u8[ntx] numpy, this shard's conflict records)."""
+    def finish_device(self, decision):
+        """-> (status u8[ntx] device tensor, this shard's ChipConflict records as a device u8 tensor of
+        n * 56 bytes, ordered by (tx, input_index)); nothing leaves the GPU."""
         import torch
         cap = int(self._keep["nref"]) + 1
         out = torch.empty(cap * ctypes.sizeof(ChipConflict), dtype=torch.uint8,
@@ -522,7 +532,12 @@ class UniqShardEngine:
         nout = ctypes.c_uint64()
         self.table._check(self.lib.chip_uniq_shard_finish(self.table.h, decision.data_ptr(), self.status.data_ptr(),
                                                           out.data_ptr(), ctypes.c_uint64(cap), ctypes.byref(nout)))
+        self._to_torch()
         n = min(nout.value, cap)
-        raw = out[:n * ctypes.sizeof(ChipConflict)].cpu().numpy().tobytes()
         self._keep = None
-        return self.status[:self.ntx].cpu().numpy(), records_from_bytes(raw)
+        return self.status[:self.ntx], out[:n * ctypes.sizeof(ChipConflict)]
+
+    def finish(self, decision):
+        """-> (status u8[ntx] numpy, this shard's conflict records)."""
+        st, raw = self.finish_device(decision)
+        return st.cpu().numpy(), records_from_bytes(raw.cpu().numpy().tobytes())

@@ -12,7 +12,8 @@ import numpy as np
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE_DIR = os.path.join(ROOT, "oracle")
-LIB_PATH = os.path.join(ORACLE_DIR, "liboracle.so")
+# CORDA_ORACLE_LIB: an alternative build of the same sources (the sanitizer build, oracle/_asan/)
+LIB_PATH = os.environ.get("CORDA_ORACLE_LIB") or os.path.join(ORACLE_DIR, "liboracle.so")
 _lib = None
 
 VALID, INVALID, SIG_DECODE, EMPTY_SIG, EMPTY_CLEAR, UNSUPPORTED, KEY_INVALID = range(7)
