@@ -316,8 +316,11 @@ class Context:
         return status, bitmap
 
     def verify_batch_device(self, dev_batch, status, bitmap, stream=None, is_valid: bool = False):
-        """Device-resident batch (torch tensors on this GPU); enqueued on `stream` (int handle).
-        An optional `schemes_hint` attribute (bit 1 << scheme per scheme present) is passed through."""
+        """Device-resident batch (torch tensors on this GPU); enqueued on `stream` (int handle) and
+        returns without waiting.  A 0 / None handle means the context's own stream (NOT torch's legacy
+        default stream, whose handle is also 0): pass a torch.cuda.Stream's handle and order it
+        against the consumer.  An optional `schemes_hint` attribute (bit 1 << scheme per scheme
+        present) is passed through."""
         s = make_sig_batch(dev_batch)
         fn = self.lib.chip_is_valid_batch_device if is_valid else self.lib.chip_verify_batch_device
         self._check(fn(self.h, ctypes.byref(s), _ptr(status), _ptr(bitmap), stream or None))

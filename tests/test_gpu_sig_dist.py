@@ -54,8 +54,13 @@ def _worker(rank, world, port, q):
                                                   (np.int32 if a.dtype == np.uint32 else np.uint8))).to(dev))
 
         def verify(sub):
+            # the library's stream, ordered against torch's on both sides (torch's default stream is
+            # handle 0, which the C-ABI reads as "the context's own stream")
             st = torch.empty(max(1, sub.key_idx.numel()), dtype=torch.uint8, device=dev)
-            ctx.verify_batch_device(sub, st, None, stream=torch.cuda.current_stream(dev).cuda_stream)
+            s = torch.cuda.Stream(dev)
+            s.wait_stream(torch.cuda.current_stream(dev))
+            ctx.verify_batch_device(sub, st, None, stream=s.cuda_stream)
+            torch.cuda.current_stream(dev).wait_stream(s)
             return st[:sub.key_idx.numel()]
         full = D.verify_sharded(verify, d, msg_idx=b.msg_idx)
         results.append(full.cpu().numpy().tolist())
