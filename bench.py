@@ -408,28 +408,46 @@ def main():
             "txid_traffic": profile_traffic("k_txid", (tb.ntx + 255) // 256 * 256),
             "txid_algorithmic_bytes": int(tb.data.nbytes + tb.salts.nbytes + 32 * tb.ntx + 20 * len(tb.comp_len)),
         })
-        # fused: ids -> SignableData messages -> 2 signers per tx
+        # fused: ids -> SignableData messages -> 2 signers per tx -> required signers (verifySignaturesExcept)
+        q = G.cfg4_required(sb, tb.ntx, args.keys, seed=0x5EED0006 + rank)
         dm = upload(tm, ("data", "off", "len", "id_at"), torch, dev)
         dm.max_len = tm.max_len
         ds = upload(sb, ("tx_idx", "tmpl_idx", "key_idx", "sig_data", "sig_off", "sig_len", "key_data", "key_off",
                          "key_len"), torch, dev)
+        dq = upload(q, ("sig_start", "req_start", "node_start", "node_val", "node_nkids", "node_weight"), torch, dev)
+        dq.ntx = q.ntx
         fst = torch.empty(sb.n, dtype=torch.uint8, device=dev)
-        fbm = torch.empty((sb.n + 63) // 64, dtype=torch.int64, device=dev)
+        fv = torch.empty(tb.ntx, dtype=torch.uint8, device=dev)
+        fa = torch.empty(tb.ntx, dtype=torch.int32, device=dev)
+        fm = torch.empty(len(q.node_start) - 1, dtype=torch.uint8, device=dev)
+
+        def fused():
+            ctx.verify_signed_tx_batch_device(dt, dm, ds, dq, ids, fst, fv, fa, fm, stream=stream.cuda_stream)
         for _ in range(2):
-            ctx.verify_tx_batch_device(dt, dm, ds, ids, fst, fbm, stream=stream.cuda_stream)
+            fused()
         torch.cuda.synchronize(dev)
         fused_ok = bool(np.array_equal(fst.cpu().numpy(), sb.expected)) and \
-            bool(np.array_equal(ids.cpu().numpy().reshape(-1, 32), ids_ref))
-        fel = timed_steps(lambda: ctx.verify_tx_batch_device(dt, dm, ds, ids, fst, fbm, stream=stream.cuda_stream), ts,
-                          world, torch, dev, dist)
+            bool(np.array_equal(ids.cpu().numpy().reshape(-1, 32), ids_ref)) and \
+            bool(np.array_equal(fv.cpu().numpy(), q.expected_verdict)) and \
+            bool(np.array_equal(fa.cpu().numpy().view(np.uint32), q.expected_arg))
+        vcounts = np.bincount(fv.cpu().numpy(), minlength=4)
+        ctx.reset_stats()
+        fel = timed_steps(fused, ts, world, torch, dev, dist)
+        s3 = ctx.stats()
         secondary.update({
             "cfg4_verified_tx_per_s": world * tb.ntx * ts / fel,
             "cfg4_signers_per_s": world * sb.n * ts / fel,
             "cfg4_ms_per_batch": fel / ts * 1e3,
-            "cfg4_workload": "%d WireTransactions: id recomputed + %d Ed25519 required signers (owner of %d keys + "
-                             "notary) verified against it, 1%% corrupted" % (tb.ntx, sb.n, args.keys),
+            "cfg4_required_kernel_ms": kms(s3, native.K_REQ),
+            "cfg4_workload": "%d SignedTransactions, verifySignaturesExcept: id recomputed + %d Ed25519 signatures "
+                             "(owner of %d keys + notary) verified against it (1%% corrupted) + requiredSigningKeys "
+                             "check on the device (2%% CompositeKey 1-of-2, 1%% with a party that did not sign)"
+                             % (tb.ntx, sb.n, args.keys),
+            "cfg4_verdicts": {"ok": int(vcounts[0]), "signature_exception": int(vcounts[1]),
+                              "signatures_missing": int(vcounts[2]), "malformed": int(vcounts[3])},
             "cfg4_correct": fused_ok,
         })
+        del dq, fv, fa, fm, q
         del dt, ids, dm, ds, fst, fbm, tb, tm, sb
 
     progress("cfg4 legs done")

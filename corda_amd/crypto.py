@@ -137,6 +137,7 @@ class SigBatch:
             key_idx.append(kid[k])
             msg_idx.append(mid[m])
             sigs.append(s)
+        self.key_index = kid                  # SPKI bytes -> key pool index
         self.key_idx = np.array(key_idx, dtype=np.uint32)
         self.msg_idx = np.array(msg_idx, dtype=np.uint32)
         self.sig_data, self.sig_off, self.sig_len = _pool(sigs)
@@ -305,36 +306,165 @@ def composite_signature_verify(engine, verify_key, sigs: Sequence[TransactionSig
     return True
 
 
+REQ_NO_SIGNER = 0xFFFFFFFF
+REQ_MAX_PENDING = 64      # CHIP_REQ_MAX_PENDING: pending subtrees of one key tree on the device
+TXV_OK, TXV_SIGNATURE, TXV_MISSING, TXV_MALFORMED = range(4)
+
+
+class ReqBatch:
+    """chip_req_batch layout: every transaction's required signing keys as post-order key trees over
+    the key pool of the signature batch `sigs` (a SigBatch over the same transactions' signatures,
+    in order), plus the allowedToBeMissing flags.  A CompositeKey is validated here
+    (CompositeKey.checkValidity, which isFulfilledBy runs first, CompositeKey.kt:192-198); a transaction
+    whose required key fails validation gets no required keys and its exception in `errors[t]`."""
+
+    def __init__(self, txs: Sequence["SignedTransaction"], sigs: "SigBatch", allowed_to_be_missing: Iterable = ()):
+        allowed = {as_key(k) for k in allowed_to_be_missing}
+        sig_start, req_start, node_start = [0], [0], [0]
+        val, nk, w, allow = [], [], [], []
+        self.required: List[List] = []
+        self.errors: List[Optional[Exception]] = []
+        pos = 0
+        for tx in txs:
+            pos += len(tx.sigs)
+            sig_start.append(pos)
+            keys = [as_key(k) for k in tx.required_signing_keys]
+            err = None
+            try:
+                for k in keys:
+                    if isinstance(k, CompositeKey):
+                        k.check_validity()
+            except (IllegalArgumentException, ArithmeticError) as e:
+                err, keys = e, []
+            self.errors.append(err)
+            self.required.append(keys)
+            for k in keys:
+                self._flatten(k, 1, sigs.key_index, val, nk, w)
+                node_start.append(len(val))
+                allow.append(1 if k in allowed else 0)
+            req_start.append(len(allow))
+        self.ntx = len(txs)
+        self.sig_start = np.array(sig_start, dtype=np.uint64)
+        self.req_start = np.array(req_start, dtype=np.uint64)
+        self.node_start = np.array(node_start, dtype=np.uint64)
+        self.allowed = np.array(allow or [0], dtype=np.uint8)
+        self.node_val = np.array(val or [0], dtype=np.uint32)
+        self.node_nkids = np.array(nk or [0], dtype=np.uint32)
+        self.node_weight = np.array(w or [0], dtype=np.uint32)
+        if not val:       # keep array lengths = node counts (n_nodes is taken from node_val)
+            self.node_val, self.node_nkids, self.node_weight = (np.zeros(0, np.uint32),) * 3
+        if not allow:
+            self.allowed = np.zeros(0, np.uint8)
+
+    @staticmethod
+    def _flatten(key, weight, kid, val, nk, w, depth=0):
+        """Post-order: children (each with its weight in this node), then the node itself."""
+        if isinstance(key, CompositeKey):
+            for child, cw in key.children:
+                ReqBatch._flatten(child, cw, kid, val, nk, w, depth + 1)
+            val.append(key.threshold)
+            nk.append(len(key.children))
+        else:
+            val.append(kid.get(bytes(key), REQ_NO_SIGNER))
+            nk.append(0)
+        w.append(weight)
+
+    def check_limits(self):
+        """The device evaluates a key tree with at most REQ_MAX_PENDING pending subtrees (a CompositeKey
+        node with that many children, or that deep a left spine): wider trees are refused up front."""
+        sp, starts = 0, set(self.node_start.tolist())
+        for j, n in enumerate(self.node_nkids.tolist()):
+            if j in starts:
+                sp = 0
+            sp = sp - n + 1
+            if sp > REQ_MAX_PENDING:
+                raise IllegalArgumentException("key tree needs more than %d pending subtrees" % REQ_MAX_PENDING)
+
+
 def verify_signatures_except_batch(engine, txs: Sequence[SignedTransaction],
                                    allowed_to_be_missing: Iterable[bytes] = ()) -> List[Optional[Exception]]:
     """Batch site (ResolveTransactionsFlow.kt:91-98 style): every transaction's signatures in ONE
-    engine call.  result[i] is None when transaction i passes verifySignaturesExcept, else the exception
-    its own sequential call would have raised first."""
-    items, owner = [], []
-    for t, tx in enumerate(txs):
-        for k, it in enumerate(tx._items()):
-            items.append(it)
-            owner.append((t, k))
-    st = verify_statuses(engine, items)
+    engine call, then the required-signer check of every transaction in one more (chip_required_signers:
+    first failing signature, getMissingSigners with CompositeKey thresholds, minus allowedToBeMissing,
+    TransactionWithSignatures.kt:44-50,62-66,79-85).  result[i] is None when transaction i passes
+    verifySignaturesExcept, else the exception its own sequential call would have raised first."""
+    items = [it for tx in txs for it in tx._items()]
     res: List[Optional[Exception]] = [None] * len(txs)
-    allowed = tuple(allowed_to_be_missing)
-    pos = 0
+    if not txs:
+        return res
+    sb = SigBatch(items)
+    st, _ = engine.verify_batch(sb) if items else (np.zeros(0, np.uint8), None)
+    q = ReqBatch(txs, sb, allowed_to_be_missing)
+    q.check_limits()
+    verdict, arg, missing = engine.required_signers(q, sb, st)
+    sig_base = q.sig_start
     for t, tx in enumerate(txs):
-        n = len(tx.sigs)
-        for k in range(n):
-            if st[pos + k] != VALID:
-                try:
-                    _raise_for(int(st[pos + k]), tx.sigs[k].by)
-                except Exception as e:   # noqa: BLE001 - the reference exception is the result
-                    res[t] = e
-                break
-        pos += n
-        if res[t] is None:
+        v = int(verdict[t])
+        if v == TXV_SIGNATURE:
+            j = int(arg[t])
             try:
-                tx._check_missing(allowed)
-            except SignaturesMissingException as e:
+                _raise_for(int(st[j]), tx.sigs[j - int(sig_base[t])].by)
+            except Exception as e:   # noqa: BLE001 - the reference exception is the result
                 res[t] = e
+        elif q.errors[t] is not None:
+            res[t] = q.errors[t]     # CompositeKey.checkValidity inside isFulfilledBy
+        elif v == TXV_MISSING:
+            r0 = int(q.req_start[t])
+            needed = {k for i, k in enumerate(q.required[t]) if missing[r0 + i]}
+            desc = sorted(tx.key_descriptions.get(k, _short(k)) for k in needed)
+            res[t] = SignaturesMissingException(needed, desc, tx.id)
+        elif v != TXV_OK:
+            raise RuntimeError("required-signer batch malformed at transaction %d" % t)
     return res
+
+
+def resolve_transactions_verify(engine, txs: Sequence[SignedTransaction],
+                                inputs_of: Callable[[SignedTransaction], Iterable[bytes]]):
+    """ResolveTransactionsFlow's verification loop (ResolveTransactionsFlow.kt:83-99) as one batch:
+    topologicalSort (:37-62, dependencies before dependers, deterministic for a given input order), then
+    verifySignaturesExcept() of every transaction through verify_signatures_except_batch.  Returns
+    (sorted transactions, the first failure in that order as (index, exception) or None) — the sequential
+    loop would stop at that transaction, having verified the ones before it."""
+    order = topological_sort(txs, inputs_of)
+    res = verify_signatures_except_batch(engine, order)
+    for i, e in enumerate(res):
+        if e is not None:
+            return order, (i, e)
+    return order, None
+
+
+def topological_sort(txs: Sequence[SignedTransaction], inputs_of) -> List[SignedTransaction]:
+    """ResolveTransactionsFlow.topologicalSort (ResolveTransactionsFlow.kt:37-62)."""
+    forward: Dict[bytes, List[SignedTransaction]] = {}
+    for stx in txs:
+        for txhash in inputs_of(stx):
+            lst = forward.setdefault(bytes(txhash), [])
+            if all(x is not stx for x in lst):       # LinkedHashSet
+                lst.append(stx)
+    visited: Set[bytes] = set()
+    result: List[SignedTransaction] = []
+
+    def visit(stx):          # the reference's recursive visit(), with an explicit stack
+        if stx.id in visited:
+            return
+        visited.add(stx.id)
+        stack = [(stx, iter(forward.get(stx.id, [])))]
+        while stack:
+            node, it = stack[-1]
+            nxt = next(it, None)
+            if nxt is None:
+                stack.pop()
+                result.append(node)
+            elif nxt.id not in visited:
+                visited.add(nxt.id)
+                stack.append((nxt, iter(forward.get(nxt.id, []))))
+
+    for stx in txs:
+        visit(stx)
+    result.reverse()
+    if len(result) != len(txs):
+        raise IllegalArgumentException("Failed requirement.")
+    return result
 
 
 # ---- WireTransaction ----

@@ -62,6 +62,8 @@ struct chip_ctx {
     DevBuf t_salts, t_start, t_group, t_internal, t_data, t_off, t_len, t_ids, t_scratch;
     // fused tx verification: device-built SignableData messages + staging of the host entry
     DevBuf f_pool, f_moff, f_mlen, f_midx, f_htx, f_htm, f_tdata, f_toff, f_tlen, f_tid;
+    // required signers: staging of the host entries
+    DevBuf q_sigs, q_reqs, q_nodes, q_allowed, q_val, q_nk, q_w, q_st, q_verdict, q_arg, q_missing;
     // filtered transactions: kernel scratch + staging of the host entry
     DevBuf x_scratch, x_ids, x_ghs, x_gh, x_fgs, x_fgi, x_cs, x_cd, x_co, x_cl, x_nonce, x_pts, x_ptt, x_pth, x_cv,
         x_st, x_rs;
@@ -802,8 +804,126 @@ int chip_verify_tx_batch_device(chip_ctx* c, const chip_tx_batch* tb, const chip
     return verify_tx_device_locked(c, tb, tm, sb, ids, status, bitmap, stream ? (hipStream_t)stream : c->stream);
 }
 
-int chip_verify_tx_batch(chip_ctx* c, const chip_tx_batch* b, const chip_msg_templates* tm, const chip_signer_batch* sb,
-                         uint8_t* ids, uint8_t* status, uint64_t* bitmap) {
+// ---------------------------------------------------------------------------------------
+// required signers (signers.hip)
+static int req_args_ok(chip_ctx* c, const chip_req_batch* q) {
+    if (!q) return fail(c, CHIP_E_ARG, "null required-signer batch");
+    if (q->ntx && (!q->sig_start || !q->req_start)) return fail(c, CHIP_E_ARG, "null sig_start / req_start");
+    if (q->nreq && !q->node_start) return fail(c, CHIP_E_ARG, "null node_start");
+    if (q->n_nodes && (!q->node_val || !q->node_nkids || !q->node_weight)) return fail(c, CHIP_E_ARG, "null node array");
+    if (q->ntx >= 0xffffffffull) return fail(c, CHIP_E_ARG, "batch too large");
+    return CHIP_OK;
+}
+
+static int required_device_locked(chip_ctx* c, const chip_req_batch* q, uint64_t nsig, const uint32_t* key_idx,
+                                  const uint32_t* tx_idx, uint64_t n_keys, const uint8_t* key_data,
+                                  const uint64_t* key_off, const uint32_t* key_len, uint64_t key_bytes,
+                                  const uint8_t* status, uint8_t* verdict, uint32_t* arg, uint8_t* missing,
+                                  hipStream_t st) {
+    if (nsig >= 0xffffffffull) return fail(c, CHIP_E_ARG, "batch too large");
+    HIPCHK(c, hipSetDevice(c->device));
+    const int ke = c->kbegin(CHIP_K_REQ, st);
+    launch_required_signers(st, q, nsig, key_idx, tx_idx, n_keys, key_data, key_off, key_len, key_bytes, status,
+                            verdict, arg, missing);
+    c->kend(ke, st);
+    HIPCHK(c, hipGetLastError());
+    return CHIP_OK;
+}
+
+int chip_required_signers_device(chip_ctx* c, const chip_req_batch* q, const chip_sig_batch* b, const uint8_t* status,
+                                 uint8_t* verdict, uint32_t* arg, uint8_t* missing, void* stream) {
+    if (!c || !b) return fail(c, CHIP_E_ARG, "null argument");
+    int r = req_args_ok(c, q);
+    if (r) return r;
+    if (q->ntx && (!verdict || !arg)) return fail(c, CHIP_E_ARG, "null verdict / arg");
+    if (b->n && (!b->key_idx || !status)) return fail(c, CHIP_E_ARG, "null key_idx / status");
+    std::lock_guard<std::mutex> g(c->mu);
+    return required_device_locked(c, q, b->n, b->key_idx, nullptr, b->n_keys, b->key_data, b->key_off, b->key_len,
+                                  b->key_bytes, status, verdict, arg, missing, stream ? (hipStream_t)stream : c->stream);
+}
+
+// stage a required-signer batch's arrays (host -> device) into `d`
+static int stage_req(chip_ctx* c, const chip_req_batch* q, chip_req_batch* d, hipStream_t st) {
+    const uint64_t ntx = q->ntx;
+    int r;
+    if ((r = stage(c, c->q_sigs, q->sig_start, ntx ? ntx + 1 : 0, st)) ||
+        (r = stage(c, c->q_reqs, q->req_start, ntx ? ntx + 1 : 0, st)) ||
+        (r = stage(c, c->q_nodes, q->node_start, q->nreq ? q->nreq + 1 : 0, st)) ||
+        (r = stage(c, c->q_val, q->node_val, q->n_nodes, st)) || (r = stage(c, c->q_nk, q->node_nkids, q->n_nodes, st)) ||
+        (r = stage(c, c->q_w, q->node_weight, q->n_nodes, st)))
+        return r;
+    if (q->allowed && (r = stage(c, c->q_allowed, q->allowed, q->nreq, st))) return r;
+    HIPCHK(c, c->q_verdict.ensure(ntx + 16));
+    HIPCHK(c, c->q_arg.ensure(ntx * 4 + 16));
+    HIPCHK(c, c->q_missing.ensure(q->nreq + 16));
+    *d = *q;
+    d->sig_start = c->q_sigs.as<uint64_t>();
+    d->req_start = c->q_reqs.as<uint64_t>();
+    d->node_start = c->q_nodes.as<uint64_t>();
+    d->allowed = q->allowed ? c->q_allowed.as<uint8_t>() : nullptr;
+    d->node_val = c->q_val.as<uint32_t>();
+    d->node_nkids = c->q_nk.as<uint32_t>();
+    d->node_weight = c->q_w.as<uint32_t>();
+    return CHIP_OK;
+}
+
+static int fetch_req(chip_ctx* c, const chip_req_batch* q, uint8_t* verdict, uint32_t* arg, uint8_t* missing,
+                     hipStream_t st) {
+    if (q->ntx) {
+        HIPCHK(c, hipMemcpyAsync(verdict, c->q_verdict.p, q->ntx, hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipMemcpyAsync(arg, c->q_arg.p, q->ntx * 4, hipMemcpyDeviceToHost, st));
+    }
+    if (missing && q->nreq) HIPCHK(c, hipMemcpyAsync(missing, c->q_missing.p, q->nreq, hipMemcpyDeviceToHost, st));
+    return CHIP_OK;
+}
+
+int chip_required_signers(chip_ctx* c, const chip_req_batch* q, const chip_sig_batch* b, const uint8_t* status,
+                          uint8_t* verdict, uint32_t* arg, uint8_t* missing) {
+    if (!c || !b) return fail(c, CHIP_E_ARG, "null argument");
+    int r = req_args_ok(c, q);
+    if (r) return r;
+    const uint64_t n = b->n, nk = b->n_keys;
+    if (q->ntx && (!verdict || !arg)) return fail(c, CHIP_E_ARG, "null verdict / arg");
+    if (n && (!b->key_idx || !status)) return fail(c, CHIP_E_ARG, "null key_idx / status");
+    if (nk && (!b->key_data || !b->key_off || !b->key_len)) return fail(c, CHIP_E_ARG, "null key array");
+    std::lock_guard<std::mutex> g(c->mu);
+    hipStream_t st = c->stream;
+    HIPCHK(c, hipSetDevice(c->device));
+    chip_req_batch d;
+    if ((r = stage_req(c, q, &d, st)) || (r = stage(c, c->h_key_idx, b->key_idx, n, st)) ||
+        (r = stage(c, c->q_st, status, n, st)) || (r = stage(c, c->h_key_data, b->key_data, b->key_bytes, st)) ||
+        (r = stage(c, c->h_key_off, b->key_off, nk, st)) || (r = stage(c, c->h_key_len, b->key_len, nk, st)))
+        return r;
+    if ((r = required_device_locked(c, &d, n, c->h_key_idx.as<uint32_t>(), nullptr, nk, c->h_key_data.as<uint8_t>(),
+                                    c->h_key_off.as<uint64_t>(), c->h_key_len.as<uint32_t>(), b->key_bytes,
+                                    c->q_st.as<uint8_t>(), c->q_verdict.as<uint8_t>(), c->q_arg.as<uint32_t>(),
+                                    missing ? c->q_missing.as<uint8_t>() : nullptr, st)) ||
+        (r = fetch_req(c, q, verdict, arg, missing, st)))
+        return r;
+    HIPCHK(c, hipStreamSynchronize(st));
+    return CHIP_OK;
+}
+
+int chip_verify_signed_tx_batch_device(chip_ctx* c, const chip_tx_batch* tb, const chip_msg_templates* tm,
+                                       const chip_signer_batch* sb, const chip_req_batch* q, uint8_t* ids,
+                                       uint8_t* status, uint8_t* verdict, uint32_t* arg, uint8_t* missing,
+                                       void* stream) {
+    if (!c || !tb || !tm || !sb || !status || (tb->ntx && !ids)) return fail(c, CHIP_E_ARG, "null argument");
+    int r = req_args_ok(c, q);
+    if (r) return r;
+    if (q->ntx != tb->ntx) return fail(c, CHIP_E_ARG, "required-signer batch and tx batch differ in ntx");
+    if (q->ntx && (!verdict || !arg)) return fail(c, CHIP_E_ARG, "null verdict / arg");
+    std::lock_guard<std::mutex> g(c->mu);
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    if ((r = verify_tx_device_locked(c, tb, tm, sb, ids, status, nullptr, st))) return r;
+    return required_device_locked(c, q, sb->n, sb->key_idx, sb->tx_idx, sb->n_keys, sb->key_data, sb->key_off,
+                                  sb->key_len, sb->key_bytes, status, verdict, arg, missing, st);
+}
+
+// host entry of the fused path, with (q != NULL) or without the required-signer stage
+static int verify_tx_host(chip_ctx* c, const chip_tx_batch* b, const chip_msg_templates* tm, const chip_signer_batch* sb,
+                          const chip_req_batch* q, uint8_t* ids, uint8_t* status, uint64_t* bitmap, uint8_t* verdict,
+                          uint32_t* arg, uint8_t* missing) {
     if (!c || !b || !tm || !sb) return fail(c, CHIP_E_ARG, "null argument");
     const uint64_t ntx = b->ntx, nc = b->ncomp, n = sb->n, nk = sb->n_keys, nt = tm->n;
     if (ntx && (!b->salts || !b->tx_comp_start || !ids)) return fail(c, CHIP_E_ARG, "null tx array");
@@ -870,8 +990,15 @@ int chip_verify_tx_batch(chip_ctx* c, const chip_tx_batch* b, const chip_msg_tem
     ds.key_data = c->h_key_data.as<uint8_t>();
     ds.key_off = c->h_key_off.as<uint64_t>();
     ds.key_len = c->h_key_len.as<uint32_t>();
+    chip_req_batch dq{};
+    if (q && (r = stage_req(c, q, &dq, st))) return r;
     if ((r = verify_tx_device_locked(c, &dt, &dm, &ds, c->t_ids.as<uint8_t>(), c->h_status.as<uint8_t>(),
                                      c->h_bitmap.as<uint64_t>(), st)))
+        return r;
+    if (q && ((r = required_device_locked(c, &dq, n, ds.key_idx, ds.tx_idx, nk, ds.key_data, ds.key_off, ds.key_len,
+                                          sb->key_bytes, c->h_status.as<uint8_t>(), c->q_verdict.as<uint8_t>(),
+                                          c->q_arg.as<uint32_t>(), missing ? c->q_missing.as<uint8_t>() : nullptr, st)) ||
+              (r = fetch_req(c, q, verdict, arg, missing, st))))
         return r;
     if (ntx) HIPCHK(c, hipMemcpyAsync(ids, c->t_ids.p, ntx * 32, hipMemcpyDeviceToHost, st));
     if (status && n) HIPCHK(c, hipMemcpyAsync(status, c->h_status.p, n, hipMemcpyDeviceToHost, st));
@@ -880,6 +1007,23 @@ int chip_verify_tx_batch(chip_ctx* c, const chip_tx_batch* b, const chip_msg_tem
     c->ev_pending = false;
     c->tev_pending = false;
     return CHIP_OK;
+}
+
+int chip_verify_tx_batch(chip_ctx* c, const chip_tx_batch* b, const chip_msg_templates* tm, const chip_signer_batch* sb,
+                         uint8_t* ids, uint8_t* status, uint64_t* bitmap) {
+    return verify_tx_host(c, b, tm, sb, nullptr, ids, status, bitmap, nullptr, nullptr, nullptr);
+}
+
+int chip_verify_signed_tx_batch(chip_ctx* c, const chip_tx_batch* b, const chip_msg_templates* tm,
+                                const chip_signer_batch* sb, const chip_req_batch* q, uint8_t* ids, uint8_t* status,
+                                uint8_t* verdict, uint32_t* arg, uint8_t* missing) {
+    if (!c) return CHIP_E_ARG;
+    int r = req_args_ok(c, q);
+    if (r) return r;
+    if (!b || q->ntx != b->ntx) return fail(c, CHIP_E_ARG, "required-signer batch and tx batch differ in ntx");
+    if (q->ntx && (!verdict || !arg)) return fail(c, CHIP_E_ARG, "null verdict / arg");
+    if (!status && sb && sb->n) return fail(c, CHIP_E_ARG, "null status");
+    return verify_tx_host(c, b, tm, sb, q, ids, status, nullptr, verdict, arg, missing);
 }
 
 // ---------------------------------------------------------------------------------------

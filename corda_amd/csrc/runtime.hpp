@@ -47,6 +47,12 @@ void launch_txid(hipStream_t st, const chip_tx_batch* b, uint8_t* ids, uint32_t*
 uint64_t ftx_scratch_words(uint64_t ntx);
 void launch_ftx_verify(hipStream_t st, const chip_ftx_batch* b, uint8_t* status, uint8_t* reason, uint32_t* scratch);
 
+// required signers (signers.hip); tx_idx may be NULL (no per-signature owner check)
+void launch_required_signers(hipStream_t st, const chip_req_batch* q, uint64_t nsig, const uint32_t* key_idx,
+                             const uint32_t* tx_idx, uint64_t n_keys, const uint8_t* key_data, const uint64_t* key_off,
+                             const uint32_t* key_len, uint64_t key_bytes, const uint8_t* status, uint8_t* verdict,
+                             uint32_t* arg, uint8_t* missing);
+
 // sizes of the per-key device tables (words per key)
 #define ED_KEY_TABLE_WORDS (9 * 40)
 #define EC_KEY_TABLE_WORDS (9 * 16 + 16)

@@ -37,7 +37,8 @@ EXPORTS = ["chip_abi_version", "chip_device_count", "chip_init", "chip_shutdown"
            "chip_uniq_commit_batch_device", "chip_uniq_last_error", "chip_uniq_shard_begin", "chip_uniq_shard_vote",
            "chip_uniq_shard_apply", "chip_uniq_shard_classify", "chip_uniq_shard_finish",
            "chip_verify_tx_batch", "chip_verify_tx_batch_device", "chip_ftx_verify_batch",
-           "chip_ftx_verify_batch_device",
+           "chip_ftx_verify_batch_device", "chip_required_signers", "chip_required_signers_device",
+           "chip_verify_signed_tx_batch", "chip_verify_signed_tx_batch_device",
            "chip_get_stats", "chip_reset_stats"]
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
@@ -102,6 +103,32 @@ def make_ftx_batch(f) -> ChipFtxBatch:
     return s
 
 
+class ChipReqBatch(ctypes.Structure):
+    _fields_ = [("ntx", ctypes.c_uint64), ("sig_start", ctypes.c_void_p), ("req_start", ctypes.c_void_p),
+                ("nreq", ctypes.c_uint64), ("node_start", ctypes.c_void_p), ("allowed", ctypes.c_void_p),
+                ("n_nodes", ctypes.c_uint64), ("node_val", ctypes.c_void_p), ("node_nkids", ctypes.c_void_p),
+                ("node_weight", ctypes.c_void_p)]
+
+
+# required-signer verdicts (chip_tx_verdict) and the key-tree leaf of a key that signed nothing
+TXV_OK, TXV_SIGNATURE, TXV_MISSING, TXV_MALFORMED = range(4)
+REQ_NO_SIGNER = 0xFFFFFFFF
+REQ_MAX_PENDING = 64
+
+
+def make_req_batch(q) -> ChipReqBatch:
+    """chip_req_batch from an object with fields ntx, sig_start, req_start, node_start, allowed (or None),
+    node_val, node_nkids, node_weight (numpy arrays or torch tensors)."""
+    s = ChipReqBatch()
+    s.ntx = int(q.ntx)
+    s.sig_start, s.req_start = _ptr(q.sig_start), _ptr(q.req_start)
+    s.nreq = max(len(q.node_start) - 1, 0)
+    s.node_start, s.allowed = _ptr(q.node_start), _ptr(getattr(q, "allowed", None))
+    s.n_nodes = len(q.node_val)
+    s.node_val, s.node_nkids, s.node_weight = _ptr(q.node_val), _ptr(q.node_nkids), _ptr(q.node_weight)
+    return s
+
+
 class ChipUniqShardBatch(ctypes.Structure):
     _fields_ = [("ntx", ctypes.c_uint64), ("ref_start", ctypes.c_void_p), ("nref", ctypes.c_uint64),
                 ("refs36", ctypes.c_void_p), ("ref_pos", ctypes.c_void_p), ("tx_ids", ctypes.c_void_p),
@@ -115,7 +142,7 @@ class ChipConflict(ctypes.Structure):
 
 
 (K_ED25519, K_ECDSA_R1, K_ECDSA_K1, K_TXID, K_KEYPREP, K_UNIQ, K_ED_COMB, K_ED_FINISH, K_ED_TABLES, K_EC_TABLES,
- K_ED_PLAN, K_ED_COMB_B, K_EC_FRONT) = range(13)
+ K_ED_PLAN, K_ED_COMB_B, K_EC_FRONT, K_REQ) = range(14)
 N_KERNELS = 16
 FLAG_NO_COMB, FLAG_FORCE_COMB = 0x1, 0x2
 
@@ -174,6 +201,14 @@ def load(build_if_missing: bool = False):
                                           ctypes.c_void_p]
     lib.chip_ftx_verify_batch_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipFtxBatch), ctypes.c_void_p,
                                                  ctypes.c_void_p, ctypes.c_void_p]
+    lib.chip_required_signers.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipReqBatch), ctypes.POINTER(ChipSigBatch),
+                                          ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.chip_required_signers_device.argtypes = lib.chip_required_signers.argtypes + [ctypes.c_void_p]
+    lib.chip_verify_signed_tx_batch.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipTxBatch),
+                                                ctypes.POINTER(ChipMsgTemplates), ctypes.POINTER(ChipSignerBatch),
+                                                ctypes.POINTER(ChipReqBatch), ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
+    lib.chip_verify_signed_tx_batch_device.argtypes = lib.chip_verify_signed_tx_batch.argtypes + [ctypes.c_void_p]
     lib.chip_uniq_open.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]
     lib.chip_uniq_close.argtypes = [ctypes.c_void_p]
     lib.chip_uniq_size.argtypes = [ctypes.c_void_p]
@@ -352,6 +387,46 @@ class Context:
         self._check(self.lib.chip_verify_tx_batch_device(self.h, ctypes.byref(tb), ctypes.byref(tm),
                                                          ctypes.byref(sb), _ptr(ids), _ptr(status), _ptr(bitmap),
                                                          stream or None))
+
+    # ---- required signers (verifySignaturesExcept after the statuses) ----
+    def required_signers(self, q, b, status):
+        """Host arrays: chip_req_batch `q` over the signatures of SoA batch `b` with statuses `status`
+        -> (verdict u8[ntx], arg u32[ntx], missing u8[nreq])."""
+        rq, sb = make_req_batch(q), make_sig_batch(b)
+        verdict = np.zeros(rq.ntx, dtype=np.uint8)
+        arg = np.zeros(rq.ntx, dtype=np.uint32)
+        missing = np.zeros(max(rq.nreq, 1), dtype=np.uint8)
+        self._check(self.lib.chip_required_signers(self.h, ctypes.byref(rq), ctypes.byref(sb),
+                                                   _ptr(np.ascontiguousarray(status, dtype=np.uint8)),
+                                                   _ptr(verdict), _ptr(arg), _ptr(missing)))
+        return verdict, arg, missing[:rq.nreq]
+
+    def required_signers_device(self, dev_q, dev_b, status, verdict, arg, missing=None, stream=None):
+        rq, sb = make_req_batch(dev_q), make_sig_batch(dev_b)
+        self._check(self.lib.chip_required_signers_device(self.h, ctypes.byref(rq), ctypes.byref(sb), _ptr(status),
+                                                          _ptr(verdict), _ptr(arg), _ptr(missing), stream or None))
+
+    def verify_signed_tx_batch(self, t, templates, signers, q):
+        """Host arrays -> (ids u8[ntx,32], status u8[n], verdict u8[ntx], arg u32[ntx], missing u8[nreq])."""
+        tb, tm, sb, rq = make_tx_batch(t), make_templates(templates), make_signers(signers), make_req_batch(q)
+        ids = np.zeros(tb.ntx * 32, dtype=np.uint8)
+        status = np.zeros(max(sb.n, 1), dtype=np.uint8)
+        verdict = np.zeros(rq.ntx, dtype=np.uint8)
+        arg = np.zeros(rq.ntx, dtype=np.uint32)
+        missing = np.zeros(max(rq.nreq, 1), dtype=np.uint8)
+        self._check(self.lib.chip_verify_signed_tx_batch(self.h, ctypes.byref(tb), ctypes.byref(tm), ctypes.byref(sb),
+                                                         ctypes.byref(rq), _ptr(ids), _ptr(status), _ptr(verdict),
+                                                         _ptr(arg), _ptr(missing)))
+        return ids.reshape(tb.ntx, 32), status[:sb.n], verdict, arg, missing[:rq.nreq]
+
+    def verify_signed_tx_batch_device(self, dev_tx, dev_templates, dev_signers, dev_q, ids, status, verdict, arg,
+                                      missing=None, stream=None):
+        tb, tm, sb = make_tx_batch(dev_tx), make_templates(dev_templates), make_signers(dev_signers)
+        rq = make_req_batch(dev_q)
+        self._check(self.lib.chip_verify_signed_tx_batch_device(self.h, ctypes.byref(tb), ctypes.byref(tm),
+                                                                ctypes.byref(sb), ctypes.byref(rq), _ptr(ids),
+                                                                _ptr(status), _ptr(verdict), _ptr(arg), _ptr(missing),
+                                                                stream or None))
 
     # ---- FilteredTransaction.verify + checkAllComponentsVisible ----
     def ftx_verify_batch(self, f):

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define CHIP_ABI_VERSION 4
+#define CHIP_ABI_VERSION 5
 
 enum chip_sig_status {
     CHIP_VALID = 0,
@@ -262,6 +262,69 @@ int chip_verify_tx_batch_device(chip_ctx* ctx, const chip_tx_batch* txs, const c
                                 void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Required signers: the rest of TransactionWithSignatures.verifySignaturesExcept (:44-50) for a batch
+ * of transactions, on the device, once their signatures' statuses are known:
+ *   checkSignaturesAreValid (:62-66)  the first non-VALID signature in list order throws;
+ *   getMissingSigners (:79-85)        requiredSigningKeys.filter { !it.isFulfilledBy(sigKeys) }, where
+ *                                     sigKeys = the keys of the transaction's signatures;
+ *   needed = missing - allowedToBeMissing; SignaturesMissingException when not empty.
+ * isFulfilledBy: a plain key is fulfilled when it equals (same SPKI bytes) a signer's key
+ * (CryptoUtils.kt:103-105); a CompositeKey when the weights of its fulfilled children reach its
+ * threshold, recursively (CompositeKey.checkFulfilledBy, CompositeKey.kt:175-185).
+ *
+ * Transaction t owns signatures sig_start[t] .. sig_start[t+1] of the signature batch (list order) and
+ * required keys req_start[t] .. req_start[t+1] (a set: no duplicates).  Required key r is a key tree
+ * in post-order, nodes node_start[r] .. node_start[r+1], its root last.  Node j: node_nkids[j] == 0 is
+ * a leaf whose node_val[j] indexes the key pool of the signature batch (or is CHIP_REQ_NO_SIGNER: a
+ * key that signs none of the batch's signatures, so it need not be in the pool); otherwise a CompositeKey node
+ * with threshold node_val[j] over the node_nkids[j] subtrees that precede it; node_weight[j] is the
+ * node's weight in its parent (ignored for a root).  Composite keys are validated by the caller
+ * (CompositeKey.checkValidity, CompositeKey.kt:99-111) before they are flattened.
+ * allowed[r] = 1 when required key r is in allowedToBeMissing (NULL: none is).
+ * Per transaction:
+ *   verdict[t]  CHIP_TXV_OK, CHIP_TXV_SIGNATURE (arg[t] = index of the first non-VALID signature),
+ *               CHIP_TXV_MISSING (arg[t] = number of needed keys; missing[r] = 1 for each of them),
+ *               CHIP_TXV_MALFORMED (a range, key index or tree encoding is invalid, a tree needs more
+ *               than CHIP_REQ_MAX_PENDING pending subtrees, or — in the fused entry — a signature
+ *               of the range belongs to another transaction; nothing else is decided for t)
+ *   missing[r]  (may be NULL) 0 unless t's verdict is CHIP_TXV_MISSING. */
+enum chip_tx_verdict { CHIP_TXV_OK = 0, CHIP_TXV_SIGNATURE = 1, CHIP_TXV_MISSING = 2, CHIP_TXV_MALFORMED = 3 };
+#define CHIP_REQ_MAX_PENDING 64
+#define CHIP_REQ_NO_SIGNER 0xffffffffu
+typedef struct {
+    uint64_t ntx;
+    const uint64_t* sig_start;     /* [ntx + 1] */
+    const uint64_t* req_start;     /* [ntx + 1] */
+    uint64_t nreq;
+    const uint64_t* node_start;    /* [nreq + 1] */
+    const uint8_t* allowed;        /* [nreq] or NULL */
+    uint64_t n_nodes;
+    const uint32_t* node_val;      /* [n_nodes] leaf: key pool index; composite: threshold   */
+    const uint32_t* node_nkids;    /* [n_nodes] 0 = leaf; else the number of children        */
+    const uint32_t* node_weight;   /* [n_nodes] weight in the parent                          */
+} chip_req_batch;
+
+/* After chip_verify_batch(_device) on `sigs` (its key_idx and key pool; messages are not read) with
+ * statuses `status`.  Host buffers / device buffers respectively. */
+int chip_required_signers(chip_ctx* ctx, const chip_req_batch* req, const chip_sig_batch* sigs,
+                          const uint8_t* status, uint8_t* verdict, uint32_t* arg, uint8_t* missing);
+int chip_required_signers_device(chip_ctx* ctx, const chip_req_batch* req, const chip_sig_batch* sigs,
+                                 const uint8_t* status, uint8_t* verdict, uint32_t* arg, uint8_t* missing,
+                                 void* stream);
+
+/* The whole SignedTransaction.verifySignaturesExcept for a batch, fused on one stream: ids
+ * (chip_txid_batch), SignableData messages and signatures (chip_verify_tx_batch), then the
+ * required-signer check above.  The signatures of tx t are sig_start[t] .. sig_start[t+1] of `sigs`
+ * and each must carry tx_idx == t (else CHIP_TXV_MALFORMED for t); req->ntx == txs->ntx. */
+int chip_verify_signed_tx_batch(chip_ctx* ctx, const chip_tx_batch* txs, const chip_msg_templates* tmpl,
+                                const chip_signer_batch* sigs, const chip_req_batch* req, uint8_t* ids,
+                                uint8_t* status, uint8_t* verdict, uint32_t* arg, uint8_t* missing);
+int chip_verify_signed_tx_batch_device(chip_ctx* ctx, const chip_tx_batch* txs, const chip_msg_templates* tmpl,
+                                       const chip_signer_batch* sigs, const chip_req_batch* req, uint8_t* ids,
+                                       uint8_t* status, uint8_t* verdict, uint32_t* arg, uint8_t* missing,
+                                       void* stream);
+
+/* ---------------------------------------------------------------------------------------
  * Notary uniqueness (GPU-resident StateRef -> ConsumingTx table).
  * StateRef key = 32-byte txhash || little-endian u32 index (36 bytes).
  * ConsumingTx  = (32-byte consuming tx id, u32 inputIndex, u32 caller) where caller is the
@@ -344,11 +407,12 @@ int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_st
  * assignment + key-grouped work list; CHIP_K_ECDSA_R1/K1 = the ECDSA kernels that need the key's
  * table: k_ecdsa_verify per curve on the windowed schedule; on the comb schedule k_ecdsa_comb_q runs
  * both curves in one launch, counted under CHIP_K_ECDSA_R1; CHIP_K_EC_FRONT = the ECDSA comb
- * kernels that need none (key grouping, DER/SHA-256/s R, batched s^-1, u1 G; both curves) */
+ * kernels that need none (key grouping, DER/SHA-256/s R, batched s^-1, u1 G; both curves);
+ * CHIP_K_REQ = k_required_signers */
 enum chip_kernel { CHIP_K_ED25519 = 0, CHIP_K_ECDSA_R1 = 1, CHIP_K_ECDSA_K1 = 2, CHIP_K_TXID = 3,
                    CHIP_K_KEYPREP = 4, CHIP_K_UNIQ = 5, CHIP_K_ED_COMB = 6, CHIP_K_ED_FINISH = 7,
                    CHIP_K_ED_TABLES = 8, CHIP_K_EC_TABLES = 9, CHIP_K_ED_PLAN = 10, CHIP_K_ED_COMB_B = 11,
-                   CHIP_K_EC_FRONT = 12, CHIP_N_KERNELS = 16 };
+                   CHIP_K_EC_FRONT = 12, CHIP_K_REQ = 13, CHIP_N_KERNELS = 16 };
 typedef struct {
     uint64_t batches, sigs, keys_prepared;
     uint64_t status_count[8];

@@ -139,6 +139,17 @@ void orc_ftx_verify_batch(uint64_t ntx, const uint8_t* ids, const uint64_t* gh_s
                           const uint8_t* nonces, const uint64_t* pt_start, const uint8_t* pt_tag,
                           const uint8_t* pt_hash, const int32_t* check_visible, uint8_t* status, uint8_t* reason);
 
+/* ---- required signers: TransactionWithSignatures.verifySignaturesExcept after the statuses
+ *      (:44-50,62-66,79-85), CompositeKey.checkFulfilledBy (CompositeKey.kt:175-185);
+ *      chip_req_batch layout, verdicts CHIP_TXV_* ---- */
+void orc_required_signers(uint64_t ntx, const uint64_t* sig_start, const uint64_t* req_start, uint64_t nreq,
+                          const uint64_t* node_start, const uint8_t* allowed, uint64_t n_nodes,
+                          const uint32_t* node_val, const uint32_t* node_nkids, const uint32_t* node_weight,
+                          uint64_t nsig, const uint32_t* key_idx, const uint32_t* tx_idx, uint64_t n_keys,
+                          const uint8_t* key_data, const uint64_t* key_off, const uint32_t* key_len,
+                          uint64_t key_bytes, const uint8_t* status, uint8_t* verdict, uint32_t* arg,
+                          uint8_t* missing);
+
 #ifdef __cplusplus
 }
 #endif

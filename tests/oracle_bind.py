@@ -190,3 +190,21 @@ def ftx_verify_batch(f):
                                _p(f.nonces), _p(f.pt_start), _p(f.pt_tag), _p(f.pt_hash), _p(f.check_visible),
                                _p(st), _p(rs))
     return st, rs
+
+
+def required_signers(q, b, status, tx_idx=None):
+    """TransactionWithSignatures.verifySignaturesExcept after the statuses (chip_req_batch layout over
+    the signatures / key pool of `b`) -> (verdict u8[ntx], arg u32[ntx], missing u8[nreq])."""
+    ntx = int(q.ntx)
+    nreq = max(len(q.node_start) - 1, 0)
+    verdict = np.zeros(ntx, dtype=np.uint8)
+    arg = np.zeros(ntx, dtype=np.uint32)
+    missing = np.zeros(max(nreq, 1), dtype=np.uint8)
+    allowed = getattr(q, "allowed", None)
+    lib().orc_required_signers(
+        ctypes.c_uint64(ntx), _p(q.sig_start), _p(q.req_start), ctypes.c_uint64(nreq), _p(q.node_start),
+        _p(allowed), ctypes.c_uint64(len(q.node_val)), _p(q.node_val), _p(q.node_nkids), _p(q.node_weight),
+        ctypes.c_uint64(len(b.key_idx)), _p(b.key_idx), _p(tx_idx), ctypes.c_uint64(len(b.key_off)), _p(b.key_data),
+        _p(b.key_off), _p(b.key_len), ctypes.c_uint64(int(b.key_data.nbytes)),
+        _p(np.ascontiguousarray(status, dtype=np.uint8)), _p(verdict), _p(arg), _p(missing))
+    return verdict, arg, missing[:nreq]

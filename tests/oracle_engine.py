@@ -37,5 +37,9 @@ class OracleEngine:
         self.calls += 1
         return O.txid_batch(tb, threads=self.threads)
 
+    def required_signers(self, q, b, status):
+        self.calls += 1
+        return O.required_signers(q, b, status)
+
     def uniq_open(self, cap):
         return _Table(cap)

@@ -702,3 +702,76 @@ def signer_sig_batch(sb: SignerBatch, msgs: np.ndarray) -> SigBatch:
     b.msg_len = np.full(ntx, ml, dtype=np.uint32)
     b.expected = sb.expected
     return b
+
+
+REQ_NO_SIGNER = 0xFFFFFFFF
+
+
+class ReqBatch:
+    """chip_req_batch layout (+ expected verdicts)."""
+    ntx = 0
+    sig_start = req_start = node_start = allowed = None
+    node_val = node_nkids = node_weight = None
+    expected_verdict = expected_arg = None
+
+
+def cfg4_required(sb: SignerBatch, ntx: int, n_keys: int, seed: int = 0x5EED0006, p_composite: float = 0.02,
+                  p_missing: float = 0.01) -> ReqBatch:
+    """requiredSigningKeys of the cfg4 transactions (SURVEY.md §8d cfg4 "all required-signer
+    verification"), over the signer batch of cfg4_workload (2 signatures per tx: owner, notary):
+    {owner, notary} for most; {CompositeKey(1 of owner, another party), notary} for p_composite
+    (fulfilled by the owner's signature); {owner, notary, a party that did not sign} for p_missing
+    (-> SignaturesMissingException).  Expected verdicts follow the signature labels (a corrupted
+    signature throws first) — TransactionWithSignatures.kt:44-50."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    kind = rng.random(ntx)
+    comp = kind < p_composite
+    miss = (kind >= p_composite) & (kind < p_composite + p_missing)
+    owner = sb.key_idx[0::2].astype(np.int64)
+    notary = sb.key_idx[1::2].astype(np.int64)
+    other = (owner + 1 + rng.integers(0, n_keys - 1, size=ntx)) % n_keys
+    nreq = np.where(miss, 3, 2)
+    nnodes = np.where(comp, 4, np.where(miss, 3, 2))
+    req_start = np.zeros(ntx + 1, dtype=np.uint64)
+    req_start[1:] = np.cumsum(nreq)
+    node_base = np.zeros(ntx + 1, dtype=np.int64)
+    node_base[1:] = np.cumsum(nnodes)
+    nn = int(node_base[-1])
+    val = np.zeros(nn, dtype=np.uint32)
+    nk = np.zeros(nn, dtype=np.uint32)
+    w = np.ones(nn, dtype=np.uint32)
+    b = node_base[:-1]
+    # plain txs: [owner] [notary]; missing: + [other]; composite: [owner other C(1,2)] [notary]
+    val[b] = owner
+    plain = ~comp
+    val[b[plain] + 1] = notary[plain]
+    val[b[miss] + 2] = other[miss]
+    cb = b[comp]
+    val[cb + 1] = other[comp]
+    val[cb + 2] = 1
+    nk[cb + 2] = 2
+    val[cb + 3] = notary[comp]
+    # node_start per required key
+    ns = []
+    starts = np.zeros(int(req_start[-1]) + 1, dtype=np.uint64)
+    r = req_start[:-1].astype(np.int64)
+    starts[r[plain]] = b[plain]
+    starts[r[plain] + 1] = b[plain] + 1
+    starts[r[miss] + 2] = b[miss] + 2
+    starts[r[comp]] = cb
+    starts[r[comp] + 1] = cb + 3
+    starts[-1] = nn
+    del ns
+    q = ReqBatch()
+    q.ntx = ntx
+    q.sig_start = (np.arange(ntx + 1, dtype=np.uint64) * 2)
+    q.req_start = req_start
+    q.node_start = starts
+    q.allowed = None
+    q.node_val, q.node_nkids, q.node_weight = val, nk, w
+    bad = sb.expected.reshape(ntx, 2) != 0
+    first_bad = np.where(bad[:, 0], 0, 1) + np.arange(ntx) * 2
+    any_bad = bad.any(axis=1)
+    q.expected_verdict = np.where(any_bad, 1, np.where(miss, 2, 0)).astype(np.uint8)
+    q.expected_arg = np.where(any_bad, first_bad, np.where(miss, 1, 0)).astype(np.uint32)
+    return q
