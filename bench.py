@@ -448,7 +448,7 @@ def main():
             "cfg4_correct": fused_ok,
         })
         del dq, fv, fa, fm, q
-        del dt, ids, dm, ds, fst, fbm, tb, tm, sb
+        del dt, ids, dm, ds, fst, tb, tm, sb
 
     progress("cfg4 legs done")
     # ---- cfg3: mixed ECDSA r1/k1, one global batch sharded by transaction, RCCL bitmap all-gather ----

@@ -102,8 +102,10 @@ struct chip_uniq {
     const uint8_t* ids = nullptr;
     const uint32_t* callers = nullptr;
     // scratch
-    UBuf reftx, pre, empty, bslot, bowner, rdup, bmin, bcommit, st, flag, scan, cub, ctr, spread, refpos;
+    UBuf reftx, pre, empty, bslot, bowner, rdup, bmin, bcommit, st, flag, scan, cub, ctr, spread, refpos, gate;
     unsigned long long* h_spread = nullptr;   // pinned host copy of the SPREAD counters
+    uint32_t* h_gate = nullptr;               // pinned host copy of the round gate
+    uint32_t round = 0;                       // ordered-commit rounds of the batch in flight
     // staging of the host entry points
     UBuf h_start, h_refs, h_ids, h_call, h_st, h_vote, h_out;
 };
@@ -221,7 +223,8 @@ __global__ void __launch_bounds__(256) k_uniq_lookup(uint64_t nref, const uint8_
                                                      const uint32_t* __restrict__ tab, uint64_t cap,
                                                      uint32_t* __restrict__ pre, uint32_t* __restrict__ empty,
                                                      uint32_t* bowner, uint8_t* __restrict__ rdup, uint64_t bcap,
-                                                     uint32_t* __restrict__ bslot) {
+                                                     uint32_t* __restrict__ bslot, unsigned long long* __restrict__ bmin,
+                                                     unsigned long long* __restrict__ bcommit) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nref) return;
     uint32_t k[KW];
@@ -242,6 +245,10 @@ __global__ void __launch_bounds__(256) k_uniq_lookup(uint64_t nref, const uint8_
             bslot[r] = (uint32_t)i;
             rdup[r] = 1;
             rdup[prev - 1] = 1;
+            // the round / commit scratch of a dup state starts "empty" (every referencer writes the
+            // same values): no memset of the whole scratch per batch or per round
+            bmin[i] = ~0ull;
+            bcommit[i] = ~0ull;
             return;
         }
         i = (i + 1) & (bcap - 1);
@@ -272,15 +279,25 @@ __global__ void __launch_bounds__(256) k_ref_tx(uint64_t ntx, const uint64_t* __
     }
 }
 
-// over the refs of dup states only (a state with one referencer needs no minimum)
+// Rounds run back to back on the device: `gate` (NULL on the sharded path, whose host decides per
+// round) holds the previous round's undecided count; a round that starts with none left exits at once.
+CHIP_DEV bool round_closed(const uint32_t* gate) { return gate && __builtin_nontemporal_load(gate) == 0u; }
+
+// over the refs of dup states only (a state with one referencer needs no minimum).  bmin[s] =
+// (tag << 32) | t with tag = ~round: a later round's entries are smaller than any stale entry of an
+// earlier round, so the minimum needs no reset between rounds, and a reader (itself a live
+// referencer of s, so a writer in this round) always sees this round's minimum.
 __global__ void __launch_bounds__(256) k_uniq_round_min(uint64_t nref, const uint8_t* __restrict__ rdup,
                                                         const uint32_t* __restrict__ ref_tx,
                                                         const uint32_t* __restrict__ bslot,
-                                                        const uint8_t* __restrict__ st, uint32_t* __restrict__ bmin) {
+                                                        const uint8_t* __restrict__ st,
+                                                        unsigned long long* __restrict__ bmin, uint32_t tag,
+                                                        const uint32_t* gate) {
+    if (round_closed(gate)) return;
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nref || !rdup[r]) return;
     const uint32_t t = ref_tx[r];
-    if (st[t] != ST_FAILED) atomicMin(&bmin[bslot[r]], t);
+    if (st[t] != ST_FAILED) atomicMin(&bmin[bslot[r]], ((unsigned long long)tag << 32) | t);
 }
 
 // votes read only the previous round's status bytes (st is written by k_uniq_apply alone), so a
@@ -288,8 +305,10 @@ __global__ void __launch_bounds__(256) k_uniq_round_min(uint64_t nref, const uin
 __global__ void __launch_bounds__(256) k_uniq_vote(uint64_t ntx, const uint64_t* __restrict__ start,
                                                    const uint32_t* __restrict__ pre, const uint32_t* __restrict__ bslot,
                                                    const uint8_t* __restrict__ rdup,
-                                                   const uint32_t* __restrict__ bmin, const uint8_t* __restrict__ st,
-                                                   uint8_t* __restrict__ vote) {
+                                                   const unsigned long long* __restrict__ bmin,
+                                                   const uint8_t* __restrict__ st, uint8_t* __restrict__ vote,
+                                                   const uint32_t* gate) {
+    if (round_closed(gate)) return;
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntx) return;
     uint8_t v = 0;
@@ -297,7 +316,7 @@ __global__ void __launch_bounds__(256) k_uniq_vote(uint64_t ntx, const uint64_t*
         for (uint64_t r = start[t], e = start[t + 1]; r < e; r++) {
             if (pre[r] != NO_SLOT) { v = 2; break; }
             if (!rdup[r]) continue;   // t is the state's only referencer
-            const uint32_t m = bmin[bslot[r]];
+            const uint32_t m = (uint32_t)bmin[bslot[r]];
             if (m < t) {
                 if (st[m] == ST_COMMITTED) { v = 2; break; }
                 v = 1;
@@ -320,7 +339,8 @@ __global__ void __launch_bounds__(256) k_uniq_apply(uint64_t ntx, const uint64_t
                                                     const uint8_t* __restrict__ rdup,
                                                     const uint8_t* __restrict__ decision, uint8_t* __restrict__ st,
                                                     unsigned long long* __restrict__ bcommit,
-                                                    unsigned long long* __restrict__ undecided) {
+                                                    unsigned long long* __restrict__ undecided, const uint32_t* gate) {
+    if (round_closed(gate)) return;
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool wait = false;
     if (t < ntx && st[t] == ST_UNDECIDED) {
@@ -338,6 +358,21 @@ __global__ void __launch_bounds__(256) k_uniq_apply(uint64_t ntx, const uint64_t
         }
     }
     spread_add(undecided, wait ? 1u : 0u);
+}
+
+// one wave: the round's undecided count (sum of the SPREAD counters) -> *gate, counters zeroed for
+// the next round
+__global__ void __launch_bounds__(64) k_uniq_gate(unsigned long long* __restrict__ spread, uint32_t* __restrict__ gate) {
+    if (round_closed(gate)) return;
+    const uint32_t lane = threadIdx.x;
+    unsigned long long sum = 0;
+    for (uint32_t i = lane; i < SPREAD; i += 64) {
+        sum += spread[i * 8];
+        spread[i * 8] = 0;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
+    if (lane == 0) *gate = sum ? (uint32_t)(sum > 0xffffffffull ? 0xffffffffull : sum) : 0u;
 }
 
 // the ConsumingTx that consumed local input r before tx t, if any
@@ -367,7 +402,9 @@ CHIP_DEV bool consumed_before(uint64_t r, uint32_t t, const uint32_t* __restrict
 }
 
 // failed tx: 1 IDEMPOTENT (every consumed local input was consumed by (txId, i, caller) itself),
-// 2 CONFLICT; 0 for committed txs and for failed txs with no consumed input on this shard
+// 2 CONFLICT; 0 for committed txs and for failed txs with no consumed input on this shard.
+// nrec[t] = the tx's Conflict.stateHistory records on this shard: its consumed local inputs, the
+// first occurrence of a repeated state only.
 __global__ void __launch_bounds__(256) k_uniq_classify(uint64_t ntx, const uint64_t* __restrict__ start,
                                                        const uint32_t* __restrict__ pos, const uint32_t* __restrict__ pre,
                                                        const uint32_t* __restrict__ bslot,
@@ -376,69 +413,59 @@ __global__ void __launch_bounds__(256) k_uniq_classify(uint64_t ntx, const uint6
                                                        const uint8_t* __restrict__ tx_ids,
                                                        const uint32_t* __restrict__ callers,
                                                        const uint32_t* __restrict__ tab, const uint8_t* __restrict__ st,
-                                                       uint8_t* __restrict__ vote) {
+                                                       uint8_t* __restrict__ vote, uint32_t* __restrict__ nrec) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntx) return;
     uint8_t v = 0;
+    uint32_t n = 0;
     if (st[t] == ST_FAILED) {
         const uint32_t* myid = reinterpret_cast<const uint32_t*>(tx_ids + 32ull * t);
-        for (uint64_t r = start[t], e = start[t + 1]; r < e; r++) {
+        const uint64_t a = start[t];
+        for (uint64_t r = a, e = start[t + 1]; r < e; r++) {
             Consumer c;
             if (!consumed_before(r, (uint32_t)t, pre, tab, bcommit, bslot, rdup, tx_ids, callers, c)) continue;
             bool same = (c.idx == pos[r]) && (c.caller == callers[t]);
 #pragma unroll
             for (int q = 0; q < 8; q++) same = same && (c.id[q] == myid[q]);
             v = same ? (v > 1 ? v : 1) : 2;
+            n += first_in_tx(bslot, a, r);
         }
     }
     vote[t] = v;
+    nrec[t] = n;
 }
 
-// flag[r] = 1 when local input r yields a Conflict.stateHistory record
-__global__ void __launch_bounds__(256) k_uniq_flag(uint64_t nref, const uint32_t* __restrict__ ref_tx,
-                                                   const uint64_t* __restrict__ start, const uint32_t* __restrict__ pre,
-                                                   const uint32_t* __restrict__ bslot, const uint8_t* __restrict__ rdup,
-                                                   const unsigned long long* __restrict__ bcommit,
-                                                   const uint8_t* __restrict__ st, uint32_t* __restrict__ flag) {
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nref) return;
-    const uint32_t t = ref_tx[r];
-    uint32_t f = 0;
-    if (st[t] == ST_FAILED) {
-        bool consumed = pre[r] != NO_SLOT;
-        if (!consumed && rdup[r]) {
-            const unsigned long long bc = bcommit[bslot[r]];
-            consumed = bc != ~0ull && (uint32_t)(bc >> 32) < t;
-        }
-        f = consumed && first_in_tx(bslot, start[t], r);
-    }
-    flag[r] = f;
-}
-
-__global__ void __launch_bounds__(256) k_uniq_emit(uint64_t nref, const uint32_t* __restrict__ ref_tx,
+// records of failed tx t at at[t] ...: its consumed local inputs in input order (first occurrence of
+// a repeated state), so the whole array is ordered by (tx, input index)
+__global__ void __launch_bounds__(256) k_uniq_emit(uint64_t ntx, const uint64_t* __restrict__ start,
                                                    const uint32_t* __restrict__ pos, const uint32_t* __restrict__ pre,
                                                    const uint32_t* __restrict__ bslot, const uint8_t* __restrict__ rdup,
                                                    const unsigned long long* __restrict__ bcommit,
                                                    const uint8_t* __restrict__ tx_ids,
                                                    const uint32_t* __restrict__ callers,
-                                                   const uint32_t* __restrict__ tab, const uint32_t* __restrict__ flag,
+                                                   const uint32_t* __restrict__ tab, const uint32_t* __restrict__ nrec,
                                                    const uint32_t* __restrict__ at, chip_conflict* __restrict__ out,
                                                    uint64_t cap) {
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nref || !flag[r] || at[r] >= cap) return;
-    const uint32_t t = ref_tx[r];
-    Consumer c;
-    consumed_before(r, t, pre, tab, bcommit, bslot, rdup, tx_ids, callers, c);
-    chip_conflict cf;
-    cf.tx = t;
-    cf.input_index = pos[r];
-    cf.consumed_index = c.idx;
-    uint32_t* d = reinterpret_cast<uint32_t*>(cf.consuming_tx);
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= ntx || !nrec[t]) return;
+    uint64_t o = at[t];
+    const uint64_t a = start[t];
+    for (uint64_t r = a, e = start[t + 1]; r < e && o < cap; r++) {
+        Consumer c;
+        if (!consumed_before(r, (uint32_t)t, pre, tab, bcommit, bslot, rdup, tx_ids, callers, c) ||
+            !first_in_tx(bslot, a, r))
+            continue;
+        chip_conflict cf;
+        cf.tx = t;
+        cf.input_index = pos[r];
+        cf.consumed_index = c.idx;
+        uint32_t* d = reinterpret_cast<uint32_t*>(cf.consuming_tx);
 #pragma unroll
-    for (int q = 0; q < 8; q++) d[q] = c.id[q];
-    cf.consuming_caller = c.caller;
-    cf.pad = 0;
-    out[at[r]] = cf;
+        for (int q = 0; q < 8; q++) d[q] = c.id[q];
+        cf.consuming_caller = c.caller;
+        cf.pad = 0;
+        out[o++] = cf;
+    }
 }
 
 // inserts: inputs of COMMITTED txs, first occurrence of a state inside its tx
@@ -591,10 +618,11 @@ static int batch_scratch(chip_uniq* u, uint64_t ntx, uint64_t nref) {
     UCHK(u, u->empty.ensure(nref * 4 + 16));
     UCHK(u, u->rdup.ensure(nref + 16));
     UCHK(u, u->bslot.ensure(nref * 4 + 16));
-    UCHK(u, u->flag.ensure(nref * 4 + 16));
-    UCHK(u, u->scan.ensure(nref * 4 + 16));
+    UCHK(u, u->flag.ensure(std::max(nref, ntx) * 4 + 16));   // per-tx record counts
+    UCHK(u, u->scan.ensure(std::max(nref, ntx) * 4 + 16));
     UCHK(u, u->bowner.ensure(bcap * 4));
-    UCHK(u, u->bmin.ensure(bcap * 4));
+    UCHK(u, u->bmin.ensure(bcap * 8));
+    UCHK(u, u->gate.ensure(64));
     UCHK(u, u->bcommit.ensure(bcap * 8));
     UCHK(u, u->st.ensure(ntx + 16));
     UCHK(u, u->ctr.ensure(64));
@@ -617,10 +645,12 @@ int chip_uniq_open(chip_ctx* ctx, uint64_t capacity, chip_uniq** out) {
     }
     int r = ensure_capacity(u, capacity ? capacity : 1024, u->stream);
     if (!r && hipHostMalloc((void**)&u->h_spread, SPREAD * 64, hipHostMallocDefault) != hipSuccess) r = CHIP_E_NOMEM;
+    if (!r && hipHostMalloc((void**)&u->h_gate, 64, hipHostMallocDefault) != hipSuccess) r = CHIP_E_NOMEM;
     if (r || hipStreamSynchronize(u->stream) != hipSuccess) {
         if (u->tab) hipFree(u->tab);
         if (u->bits) hipFree(u->bits);
         if (u->h_spread) hipHostFree(u->h_spread);
+        if (u->h_gate) hipHostFree(u->h_gate);
         hipStreamDestroy(u->stream);
         delete u;
         return r ? r : CHIP_E_DEVICE;
@@ -636,10 +666,11 @@ void chip_uniq_close(chip_uniq* u) {
     if (u->tab) hipFree(u->tab);
     if (u->bits) hipFree(u->bits);
     if (u->h_spread) hipHostFree(u->h_spread);
+    if (u->h_gate) hipHostFree(u->h_gate);
     UBuf* bufs[] = {&u->reftx,  &u->pre,    &u->empty,  &u->bslot, &u->bowner, &u->rdup,   &u->spread,
                     &u->bmin,   &u->bcommit, &u->st,    &u->flag,  &u->scan,   &u->cub,    &u->ctr,
                     &u->refpos, &u->h_start, &u->h_refs, &u->h_ids, &u->h_call, &u->h_st,  &u->h_vote,
-                    &u->h_out};
+                    &u->h_out,  &u->gate};
     for (UBuf* b : bufs) b->release();
     hipStreamDestroy(u->stream);
     delete u;
@@ -673,7 +704,8 @@ int chip_uniq_rebuild(chip_uniq* u, uint64_t n, const uint8_t* refs36, const uin
     const uint8_t* d_refs = u->h_refs.as<uint8_t>();
     hipLaunchKernelGGL(k_uniq_lookup, dim3(blocks_for(n)), dim3(256), 0, st, n, d_refs, u->tab, u->cap,
                        u->pre.as<uint32_t>(), (uint32_t*)nullptr, u->bowner.as<uint32_t>(), u->rdup.as<uint8_t>(),
-                       u->bcap, u->bslot.as<uint32_t>());
+                       u->bcap, u->bslot.as<uint32_t>(), u->bmin.as<unsigned long long>(),
+                       u->bcommit.as<unsigned long long>());
     hipLaunchKernelGGL(k_uniq_rebuild, dim3(blocks_for(n)), dim3(256), 0, st, n, d_refs, u->h_ids.as<uint8_t>(),
                        u->refpos.as<uint32_t>(), u->h_call.as<uint32_t>(), u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(),
                        u->bowner.as<uint32_t>(), u->tab, u->bits, u->cap, u->spread.as<unsigned long long>());
@@ -706,7 +738,7 @@ int chip_uniq_shard_begin(chip_uniq* u, const chip_uniq_shard_batch* b, void* st
     u->callers = b->callers;
     UCHK(u, hipMemsetAsync(u->bowner.p, 0, u->bcap * 4, st));
     if (nref) UCHK(u, hipMemsetAsync(u->rdup.p, 0, nref, st));
-    UCHK(u, hipMemsetAsync(u->bcommit.p, 0xff, u->bcap * 8, st));
+    u->round = 0;
     if (ntx) UCHK(u, hipMemsetAsync(u->st.p, ST_UNDECIDED, ntx, st));
     UCHK(u, hipMemsetAsync(u->ctr.p, 0, 64, st));
     if (ntx)
@@ -715,25 +747,39 @@ int chip_uniq_shard_begin(chip_uniq* u, const chip_uniq_shard_batch* b, void* st
     if (nref) {
         hipLaunchKernelGGL(k_uniq_lookup, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->refs, u->tab, u->cap,
                            u->pre.as<uint32_t>(), u->empty.as<uint32_t>(), u->bowner.as<uint32_t>(),
-                           u->rdup.as<uint8_t>(), u->bcap, u->bslot.as<uint32_t>());
+                           u->rdup.as<uint8_t>(), u->bcap, u->bslot.as<uint32_t>(), u->bmin.as<unsigned long long>(),
+                           u->bcommit.as<unsigned long long>());
     }
     UCHK(u, hipGetLastError());
     u->open = true;
     return CHIP_OK;
 }
 
+// one ordered-commit round: round minimum, vote (gate: NULL = always run)
+static void launch_round_vote(chip_uniq* u, uint8_t* vote, const uint32_t* gate) {
+    hipStream_t st = u->bst;
+    u->round++;
+    const uint32_t tag = ~u->round;
+    if (u->nref)
+        hipLaunchKernelGGL(k_uniq_round_min, dim3(blocks_for(u->nref)), dim3(256), 0, st, u->nref, u->rdup.as<uint8_t>(),
+                           u->reftx.as<uint32_t>(), u->bslot.as<uint32_t>(), u->st.as<uint8_t>(),
+                           u->bmin.as<unsigned long long>(), tag, gate);
+    if (u->ntx)
+        hipLaunchKernelGGL(k_uniq_vote, dim3(blocks_for(u->ntx)), dim3(256), 0, st, u->ntx, u->start,
+                           u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->rdup.as<uint8_t>(),
+                           u->bmin.as<unsigned long long>(), u->st.as<uint8_t>(), vote, gate);
+}
+static void launch_apply(chip_uniq* u, const uint8_t* decision, const uint32_t* gate) {
+    if (u->ntx)
+        hipLaunchKernelGGL(k_uniq_apply, dim3(blocks_for(u->ntx)), dim3(256), 0, u->bst, u->ntx, u->start,
+                           u->bslot.as<uint32_t>(), u->pos, u->rdup.as<uint8_t>(), decision, u->st.as<uint8_t>(),
+                           u->bcommit.as<unsigned long long>(), u->spread.as<unsigned long long>(), gate);
+}
+
 int chip_uniq_shard_vote(chip_uniq* u, uint8_t* vote) {
     if (!u) return CHIP_E_ARG;
     if (!u->open || (u->ntx && !vote)) return ufail(u, CHIP_E_ARG, "no batch in flight / null vote");
-    hipStream_t st = u->bst;
-    UCHK(u, hipMemsetAsync(u->bmin.p, 0xff, u->bcap * 4, st));
-    if (u->nref)
-        hipLaunchKernelGGL(k_uniq_round_min, dim3(blocks_for(u->nref)), dim3(256), 0, st, u->nref, u->rdup.as<uint8_t>(),
-                           u->reftx.as<uint32_t>(), u->bslot.as<uint32_t>(), u->st.as<uint8_t>(), u->bmin.as<uint32_t>());
-    if (u->ntx)
-        hipLaunchKernelGGL(k_uniq_vote, dim3(blocks_for(u->ntx)), dim3(256), 0, st, u->ntx, u->start,
-                           u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->rdup.as<uint8_t>(), u->bmin.as<uint32_t>(),
-                           u->st.as<uint8_t>(), vote);
+    launch_round_vote(u, vote, nullptr);
     UCHK(u, hipGetLastError());
     return CHIP_OK;
 }
@@ -744,10 +790,7 @@ int chip_uniq_shard_apply(chip_uniq* u, const uint8_t* decision, uint64_t* undec
     hipStream_t st = u->bst;
     int r = spread_zero(u, st);
     if (r) return r;
-    if (u->ntx)
-        hipLaunchKernelGGL(k_uniq_apply, dim3(blocks_for(u->ntx)), dim3(256), 0, st, u->ntx, u->start,
-                           u->bslot.as<uint32_t>(), u->pos, u->rdup.as<uint8_t>(), decision, u->st.as<uint8_t>(),
-                           u->bcommit.as<unsigned long long>(), u->spread.as<unsigned long long>());
+    launch_apply(u, decision, nullptr);
     UCHK(u, hipGetLastError());
     if ((r = spread_fetch(u, st))) return r;
     UCHK(u, hipStreamSynchronize(st));
@@ -762,7 +805,7 @@ int chip_uniq_shard_classify(chip_uniq* u, uint8_t* vote) {
         hipLaunchKernelGGL(k_uniq_classify, dim3(blocks_for(u->ntx)), dim3(256), 0, u->bst, u->ntx, u->start, u->pos,
                            u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->rdup.as<uint8_t>(),
                            u->bcommit.as<unsigned long long>(), u->ids,
-                           u->callers, u->tab, u->st.as<uint8_t>(), vote);
+                           u->callers, u->tab, u->st.as<uint8_t>(), vote, u->flag.as<uint32_t>());
     UCHK(u, hipGetLastError());
     return CHIP_OK;
 }
@@ -775,31 +818,26 @@ int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_st
     hipStream_t st = u->bst;
     const uint64_t nref = u->nref, ntx = u->ntx;
     u->open = false;
-    uint32_t* flag = u->flag.as<uint32_t>();
+    uint32_t* nrec = u->flag.as<uint32_t>();   // per-tx record counts (k_uniq_classify)
     uint32_t* at = u->scan.as<uint32_t>();
     int rc = spread_zero(u, st);
     if (rc) return rc;
     uint32_t last[2] = {0, 0};
-    if (nref) {
-        hipLaunchKernelGGL(k_uniq_flag, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->reftx.as<uint32_t>(), u->start,
-                           u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->rdup.as<uint8_t>(),
-                           u->bcommit.as<unsigned long long>(),
-                           u->st.as<uint8_t>(), flag);
+    if (nref && ntx) {
         size_t tmp = 0;
-        UCHK(u, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, flag, at, (int)nref, st));
+        UCHK(u, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, nrec, at, (int)ntx, st));
         UCHK(u, u->cub.ensure(tmp + 16));
-        UCHK(u, hipcub::DeviceScan::ExclusiveSum(u->cub.p, tmp, flag, at, (int)nref, st));
-        hipLaunchKernelGGL(k_uniq_emit, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->reftx.as<uint32_t>(), u->pos,
+        UCHK(u, hipcub::DeviceScan::ExclusiveSum(u->cub.p, tmp, nrec, at, (int)ntx, st));
+        hipLaunchKernelGGL(k_uniq_emit, dim3(blocks_for(ntx)), dim3(256), 0, st, ntx, u->start, u->pos,
                            u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->rdup.as<uint8_t>(),
-                           u->bcommit.as<unsigned long long>(), u->ids,
-                           u->callers, u->tab, flag, at, out, cap);
+                           u->bcommit.as<unsigned long long>(), u->ids, u->callers, u->tab, nrec, at, out, cap);
         // inserts after the records: emit reads pre-committed slots, inserts only fill empty ones
         hipLaunchKernelGGL(k_uniq_insert, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->refs, u->reftx.as<uint32_t>(),
                            u->pos, u->start, u->st.as<uint8_t>(), u->bslot.as<uint32_t>(), u->rdup.as<uint8_t>(),
                            u->empty.as<uint32_t>(), u->ids, u->callers, u->tab, u->bits, u->cap,
                            u->spread.as<unsigned long long>());
-        UCHK(u, hipMemcpyAsync(&last[0], at + nref - 1, 4, hipMemcpyDeviceToHost, st));
-        UCHK(u, hipMemcpyAsync(&last[1], flag + nref - 1, 4, hipMemcpyDeviceToHost, st));
+        UCHK(u, hipMemcpyAsync(&last[0], at + ntx - 1, 4, hipMemcpyDeviceToHost, st));
+        UCHK(u, hipMemcpyAsync(&last[1], nrec + ntx - 1, 4, hipMemcpyDeviceToHost, st));
         if ((rc = spread_fetch(u, st))) return rc;
     }
     if (ntx)
@@ -813,7 +851,9 @@ int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_st
     return nout > cap ? ufail(u, CHIP_E_CAPACITY, "more conflict records than capacity") : CHIP_OK;
 }
 
-// one shard owning the whole key space: rounds with decision = vote
+// one shard owning the whole key space: decision = vote, and the rounds run back to back on the
+// device in chunks (each round gated by the previous one's undecided count, k_uniq_gate); the host
+// reads the gate once per chunk instead of once per round
 static int commit_device(chip_uniq* u, const chip_uniq_shard_batch* b, uint8_t* tx_status, chip_conflict* out,
                          uint64_t cap, uint64_t* n_out, hipStream_t st) {
     int r = chip_uniq_shard_begin(u, b, st);
@@ -823,13 +863,29 @@ static int commit_device(chip_uniq* u, const chip_uniq_shard_batch* b, uint8_t* 
         return ufail(u, CHIP_E_NOMEM, "vote buffer");
     }
     uint8_t* vote = u->h_vote.as<uint8_t>();
-    for (uint64_t round = 0; round <= b->ntx; round++) {
-        uint64_t und = 0;
-        if ((r = chip_uniq_shard_vote(u, vote)) || (r = chip_uniq_shard_apply(u, vote, &und))) {
-            u->open = false;
-            return r;
+    uint32_t* gate = u->gate.as<uint32_t>();
+    if ((r = spread_zero(u, st))) {
+        u->open = false;
+        return r;
+    }
+    if (hipMemsetD32Async((hipDeviceptr_t)gate, 1u, 1, st) != hipSuccess) {
+        u->open = false;
+        return ufail(u, CHIP_E_DEVICE, "gate init");
+    }
+    uint64_t rounds = 0;
+    for (uint32_t chunk = 4; rounds <= b->ntx; chunk = 8) {
+        for (uint32_t i = 0; i < chunk; i++) {
+            launch_round_vote(u, vote, gate);
+            launch_apply(u, vote, gate);
+            hipLaunchKernelGGL(k_uniq_gate, dim3(1), dim3(64), 0, st, u->spread.as<unsigned long long>(), gate);
         }
-        if (!und) break;
+        rounds += chunk;
+        if (hipGetLastError() != hipSuccess || hipMemcpyAsync(u->h_gate, gate, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+            hipStreamSynchronize(st) != hipSuccess) {
+            u->open = false;
+            return ufail(u, CHIP_E_DEVICE, "ordered-commit rounds");
+        }
+        if (!*u->h_gate) break;
     }
     if ((r = chip_uniq_shard_classify(u, vote))) {
         u->open = false;
