@@ -523,21 +523,31 @@ CHIP_DEV bool ec_key_ok(const KeyMeta* meta, uint64_t k, int scheme) {
     return m.scheme == scheme && m.ok;
 }
 
-// chain: P_w = 2^(4w) Q (Jacobian) for w = 0..64 into entry 0 of every window of the scratch
-// (256 serial doublings per key: the latency of this kernel is the per-key table's critical path)
+// chain: P_w = 2^(4w) Q (Jacobian) for windows [wa, wb) into entry 0 of each window of the scratch
+// (4 serial doublings per window, 256 per key: the latency of this kernel is the per-key table's
+// critical path).  Run in two launches (windows 0..31, then 32..64 continuing from P_31) so the low
+// half of the table is filled — and the signatures' low-window additions run — while the chain
+// still doubles towards the high half.
 template <int C>
-CHIP_DEV void ec_comb_chain(const uint32_t* __restrict__ ectab, uint32_t* __restrict__ jac, uint64_t k) {
-    apt q;
-    load_apt(q, ectab + k * EC_TAB_STRIDE + 16);
-    jpt P;
-    jpt_from_aff(P, q);
+CHIP_DEV void ec_comb_chain(const uint32_t* __restrict__ ectab, uint32_t* __restrict__ jac, uint64_t k, uint32_t wa,
+                            uint32_t wb) {
     uint32_t* tab = jac + k * EC_COMB_JAC_WORDS;
+    jpt P;
+    uint32_t w = wa;
+    if (wa == 0) {
+        apt q;
+        load_apt(q, ectab + k * EC_TAB_STRIDE + 16);
+        jpt_from_aff(P, q);
+        store_jpt(tab, P);
+        w = 1;
+    } else {
+        load_jpt(P, tab + (wa - 1) * EC_COMB_QENT * EC_COMB_JW);
+    }
 #pragma unroll 1
-    for (int w = 0; w < EC_COMB_QWIN; w++) {
-        store_jpt(tab + (uint32_t)w * EC_COMB_QENT * EC_COMB_JW, P);
-        if (w + 1 == EC_COMB_QWIN) break;
+    for (; w < wb; w++) {
 #pragma unroll 1
         for (int b = 0; b < 4; b++) jdbl<C>(P, P);
+        store_jpt(tab + w * EC_COMB_QENT * EC_COMB_JW, P);
     }
 }
 // fill, for windows [w0, w1) of one key:
@@ -545,8 +555,7 @@ CHIP_DEV void ec_comb_chain(const uint32_t* __restrict__ ectab, uint32_t* __rest
 //      the x slots of the output entries)
 //   2. j P_w for j = 2..8: one doubling and six mixed additions, Jacobian into the scratch
 //   3. those 7 (w1 - w0) entries to affine with one more shared inversion
-#define EC_FILL_GROUP 2
-#define EC_FILL_LANES ((EC_COMB_QWIN - 1) / EC_FILL_GROUP)
+#define EC_FILL_GROUP 4   // measured: 1 -> 68.9M, 2 -> 73.4M, 4 -> 75.3M, 8 -> 74.6M, 16 -> 59.7M cfg3 sigs/s
 template <int C>
 CHIP_DEV void ec_comb_fill(uint32_t* __restrict__ jac, uint32_t* __restrict__ out, uint32_t w0, uint32_t w1) {
     u256 acc, z, inv;
@@ -614,24 +623,27 @@ CHIP_DEV void ec_comb_fill(uint32_t* __restrict__ jac, uint32_t* __restrict__ ou
 // one launch for both curves: r1 and k1 keys build concurrently (lane per key)
 __global__ void __launch_bounds__(64) k_ecdsa_comb_chain(uint64_t n_keys, const KeyMeta* __restrict__ meta,
                                                          const uint32_t* __restrict__ ectab, uint32_t* __restrict__ jac,
-                                                         uint32_t prio) {
+                                                         uint32_t prio, uint32_t wa, uint32_t wb) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_keys) return;
     // the chain is the latency-bound critical path of the step: win VALU arbitration against the
     // throughput kernels of the main stream that share its SIMDs
     if (prio) __builtin_amdgcn_s_setprio(3);
-    if (ec_key_ok(meta, k, CHIP_SCHEME_R1)) ec_comb_chain<CURVE_R1 | CURVE_ILP>(ectab, jac, k);
-    else if (ec_key_ok(meta, k, CHIP_SCHEME_K1)) ec_comb_chain<CURVE_K1 | CURVE_ILP>(ectab, jac, k);
+    if (ec_key_ok(meta, k, CHIP_SCHEME_R1)) ec_comb_chain<CURVE_R1 | CURVE_ILP>(ectab, jac, k, wa, wb);
+    else if (ec_key_ok(meta, k, CHIP_SCHEME_K1)) ec_comb_chain<CURVE_K1 | CURVE_ILP>(ectab, jac, k, wa, wb);
 }
-// lane per key x group of windows (the last group also takes window 64)
+// lane per key x group of `gw` windows of [wa, wb) (the fill is latency-bound: fewer windows per
+// lane = more lanes, at one shared inversion pair per lane)
 __global__ void __launch_bounds__(256) k_ecdsa_comb_fill(uint64_t n_keys, const KeyMeta* __restrict__ meta,
-                                                         uint32_t* __restrict__ ctab, uint32_t* __restrict__ jac) {
+                                                         uint32_t* __restrict__ ctab, uint32_t* __restrict__ jac,
+                                                         uint32_t wa, uint32_t wb, uint32_t gw) {
+    const uint32_t ng = (wb - wa + gw - 1) / gw;
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint64_t k = g / EC_FILL_LANES;
-    const uint32_t grp = (uint32_t)(g % EC_FILL_LANES);
+    const uint64_t k = g / ng;
+    const uint32_t grp = (uint32_t)(g % ng);
     if (k >= n_keys) return;
-    const uint32_t w0 = grp * EC_FILL_GROUP;
-    const uint32_t w1 = (grp + 1 == EC_FILL_LANES) ? EC_COMB_QWIN : w0 + EC_FILL_GROUP;
+    const uint32_t w0 = wa + grp * gw;
+    const uint32_t w1 = w0 + gw < wb ? w0 + gw : wb;
     uint32_t* e = jac + k * EC_COMB_JAC_WORDS;
     uint32_t* out = ctab + k * EC_COMB_KEY_WORDS;
     if (ec_key_ok(meta, k, CHIP_SCHEME_R1)) ec_comb_fill<CURVE_R1>(e, out, w0, w1);
@@ -853,10 +865,12 @@ __global__ void __launch_bounds__(256) k_ecdsa_comb_g(const uint32_t* __restrict
 // D.  u2 Q half: one mixed addition per non-zero radix-16 digit from the key's affine table, then
 // x(R) mod n == r exactly as k_ecdsa_verify checks it.  The list is grouped by key and consecutive
 // blocks run on one XCD, so a key's 33 KB table is read from one L2.
-template <int C>
+// Two launches: HALF 0 adds the digits of windows 0..31 (the low half of the table, filled first)
+// and parks the Jacobian sum in the hand-off area; HALF 1 adds windows 32..64 and checks x(R).
+template <int C, int HALF>
 CHIP_DEV void comb_q_body(uint32_t blk, const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
                           const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ ctab,
-                          const uint32_t* __restrict__ mid, uint64_t cap, uint8_t* __restrict__ status) {
+                          uint32_t* __restrict__ mid, uint64_t cap, uint8_t* __restrict__ status) {
     const uint32_t n = *count;
     const uint32_t gid = blk * blockDim.x + threadIdx.x;
     if (gid >= n || !mid[(uint64_t)40 * cap + gid]) return;
@@ -873,7 +887,7 @@ CHIP_DEV void comb_q_body(uint32_t blk, const uint32_t* __restrict__ list, const
     const uint32_t cq = recode<4>(dq, u2);
     const uint32_t* qt = ctab + (uint64_t)key_idx[i] * EC_COMB_KEY_WORDS;
 #pragma unroll 1
-    for (int wd = 0; wd < 8; wd++) {
+    for (int wd = HALF * 4; wd < HALF * 4 + 4; wd++) {
         const uint32_t cur = dq[wd];
 #pragma unroll 1
         for (int q = 0; q < 8; q++) {
@@ -884,6 +898,12 @@ CHIP_DEV void comb_q_body(uint32_t blk, const uint32_t* __restrict__ list, const
             add_digit<C>(acc, ent, d);
         }
     }
+    if (HALF == 0) {
+        mid_store(mid, cap, gid, 0, acc.X);
+        mid_store(mid, cap, gid, 8, acc.Y);
+        mid_store(mid, cap, gid, 16, acc.Z);
+        return;
+    }
     if (cq) {
         load_apt(ent, qt + (64u * EC_COMB_QENT) * 16);
         add_digit<C>(acc, ent, 1);
@@ -891,32 +911,49 @@ CHIP_DEV void comb_q_body(uint32_t blk, const uint32_t* __restrict__ list, const
     status[i] = ecdsa_check<C>(acc, r) ? CHIP_VALID : CHIP_INVALID;
 }
 // both curves in one grid, as k_ecdsa_comb_g
+template <int HALF>
 __global__ void __launch_bounds__(256) k_ecdsa_comb_q(const uint32_t* __restrict__ list_r1,
                                                       const uint32_t* __restrict__ list_k1,
                                                       const uint32_t* __restrict__ counts,
                                                       const uint32_t* __restrict__ key_idx,
                                                       const uint32_t* __restrict__ ctab,
-                                                      const uint32_t* __restrict__ mid_r1,
-                                                      const uint32_t* __restrict__ mid_k1, uint64_t cap,
+                                                      uint32_t* __restrict__ mid_r1,
+                                                      uint32_t* __restrict__ mid_k1, uint64_t cap,
                                                       uint8_t* __restrict__ status, uint32_t half) {
-    if (blockIdx.x < half) comb_q_body<CURVE_R1>(blockIdx.x, list_r1, counts + LIST_R1, key_idx, ctab, mid_r1, cap, status);
-    else comb_q_body<CURVE_K1>(blockIdx.x - half, list_k1, counts + LIST_K1, key_idx, ctab, mid_k1, cap, status);
+    if (blockIdx.x < half)
+        comb_q_body<CURVE_R1, HALF>(blockIdx.x, list_r1, counts + LIST_R1, key_idx, ctab, mid_r1, cap, status);
+    else
+        comb_q_body<CURVE_K1, HALF>(blockIdx.x - half, list_k1, counts + LIST_K1, key_idx, ctab, mid_k1, cap, status);
 }
 
 uint64_t ecdsa_comb_key_words() { return EC_COMB_KEY_WORDS + EC_COMB_JAC_WORDS; }
 
-void launch_ecdsa_comb_build(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, const uint32_t* ectab,
-                             uint32_t* ctab) {
+// table halves: windows [0, EC_LO_WIN) and [EC_LO_WIN, 65); fill groups cover EC_FILL_GROUP windows each
+#define EC_LO_WIN 32
+void launch_ecdsa_comb_chain(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, const uint32_t* ectab,
+                             uint32_t* ctab, int half) {
     if (!n_keys) return;
     uint32_t* jac = ctab + n_keys * EC_COMB_KEY_WORDS;
     static const uint32_t prio = [] {
         const char* e = getenv("CHIP_CHAIN_PRIO");
         return e ? (uint32_t)(e[0] != '0') : 1u;
     }();
+    const uint32_t wa = half ? EC_LO_WIN : 0, wb = half ? EC_COMB_QWIN : EC_LO_WIN;
     hipLaunchKernelGGL(k_ecdsa_comb_chain, dim3((uint32_t)((n_keys + 63) / 64)), dim3(64), 0, st, n_keys, meta, ectab,
-                       jac, prio);
-    hipLaunchKernelGGL(k_ecdsa_comb_fill, dim3((uint32_t)((n_keys * EC_FILL_LANES + 255) / 256)), dim3(256), 0, st, n_keys,
-                       meta, ctab, jac);
+                       jac, prio, wa, wb);
+}
+void launch_ecdsa_comb_fill(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, uint32_t* ctab, int half) {
+    if (!n_keys) return;
+    uint32_t* jac = ctab + n_keys * EC_COMB_KEY_WORDS;
+    static const uint32_t gw = [] {
+        const char* e = getenv("CHIP_EC_FILL_GROUP");
+        const uint32_t v = e ? (uint32_t)strtoul(e, nullptr, 10) : EC_FILL_GROUP;
+        return v ? v : 1u;
+    }();
+    const uint32_t wa = half ? EC_LO_WIN : 0, wb = half ? EC_COMB_QWIN : EC_LO_WIN;
+    const uint32_t ng = (wb - wa + gw - 1) / gw;
+    hipLaunchKernelGGL(k_ecdsa_comb_fill, dim3((uint32_t)((n_keys * ng + 255) / 256)), dim3(256), 0, st, n_keys, meta,
+                       ctab, jac, wa, wb, gw);
 }
 
 // words of the hand-off area per list position, and of the wave products per list
@@ -959,10 +996,14 @@ void launch_ecdsa_comb_g(hipStream_t st, uint64_t n, const uint32_t* counts, con
                        (uint64_t)n, half);
 }
 void launch_ecdsa_comb_q(hipStream_t st, uint64_t n, const uint32_t* list_r1, const uint32_t* list_k1,
-                         const uint32_t* counts, const chip_sig_batch* b, const uint32_t* ctab, const uint32_t* mid_r1,
-                         const uint32_t* mid_k1, uint8_t* status) {
+                         const uint32_t* counts, const chip_sig_batch* b, const uint32_t* ctab, uint32_t* mid_r1,
+                         uint32_t* mid_k1, uint8_t* status, int table_half) {
     if (!n) return;
     const uint32_t half = (uint32_t)((n + 255) / 256);
-    hipLaunchKernelGGL(k_ecdsa_comb_q, dim3(2 * half), dim3(256), 0, st, list_r1, list_k1, counts, b->key_idx, ctab,
-                       mid_r1, mid_k1, (uint64_t)n, status, half);
+    if (table_half)
+        hipLaunchKernelGGL(k_ecdsa_comb_q<1>, dim3(2 * half), dim3(256), 0, st, list_r1, list_k1, counts, b->key_idx, ctab,
+                           mid_r1, mid_k1, (uint64_t)n, status, half);
+    else
+        hipLaunchKernelGGL(k_ecdsa_comb_q<0>, dim3(2 * half), dim3(256), 0, st, list_r1, list_k1, counts, b->key_idx, ctab,
+                           mid_r1, mid_k1, (uint64_t)n, status, half);
 }

@@ -44,10 +44,13 @@ struct chip_ctx {
     // table chains (Ed25519 ~0.5 ms, ECDSA ~2.4 ms) cost more than the Straus / windowed kernels save
     uint32_t comb_min_total = 65536;
     bool ec_group = true;                         // ECDSA comb lists grouped by key (CHIP_EC_GROUP=0 off)
+    bool ec_split = true;                         // ECDSA table halves filled on a third stream (CHIP_EC_SPLIT)
     uint64_t comb_budget = 8ull << 30;            // bytes of per-key comb tables
     hipStream_t stream = nullptr;
     hipStream_t aux = nullptr;                    // second stream: per-key comb tables
+    hipStream_t aux2 = nullptr;                   // third stream: ECDSA table fills (while aux doubles on)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fork2 = nullptr, ev_join2 = nullptr;
+    hipEvent_t ev_ec_chain_lo = nullptr, ev_ec_chain_hi = nullptr, ev_ec_lo = nullptr;
     std::mutex mu;
     std::string err;
     // verify workspaces
@@ -292,7 +295,11 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork2, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->aux2, hipStreamNonBlocking, aux_priority()) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_ec_chain_lo, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_ec_chain_hi, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_ec_lo, hipEventDisableTiming) != hipSuccess) {
         delete c;
         return CHIP_E_DEVICE;
     }
@@ -319,6 +326,7 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
     }
     if (c->flags & CHIP_FLAG_FORCE_COMB) c->comb_min_sigs = 1, c->comb_min_total = 0;
     if (const char* e = getenv("CHIP_EC_GROUP")) c->ec_group = e[0] != '0';
+    if (const char* e = getenv("CHIP_EC_SPLIT")) c->ec_split = e[0] != '0';
     if (const char* e = getenv("CHIP_COMB_MIN_SIGS")) c->comb_min_sigs = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("CHIP_COMB_MIN_TOTAL")) c->comb_min_total = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("CHIP_COMB_BUDGET_MB")) c->comb_budget = (uint64_t)strtoull(e, nullptr, 10) << 20;
@@ -357,6 +365,11 @@ void chip_shutdown(chip_ctx* c) {
     hipEventDestroy(c->ev_join);
     hipEventDestroy(c->ev_fork2);
     hipEventDestroy(c->ev_join2);
+    hipStreamSynchronize(c->aux2);
+    hipEventDestroy(c->ev_ec_chain_lo);
+    hipEventDestroy(c->ev_ec_chain_hi);
+    hipEventDestroy(c->ev_ec_lo);
+    hipStreamDestroy(c->aux2);
     hipStreamDestroy(c->aux);
     hipStreamDestroy(c->stream);
     delete c;
@@ -464,12 +477,27 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     launch_ecdsa_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->ectab.as<uint32_t>());
     if (!ec_comb) launch_ecdsa_key_table(st, nk, meta, c->ectab.as<uint32_t>());
     if (ec_comb) {
+        // aux: the doubling chain, low windows then high windows; aux2: the fill of each half as soon
+        // as its chain half is done (the low fill overlaps the high chain); main waits for the low
+        // half (ev_ec_lo) before the low-window additions and for the whole table (ev_join2) after
         HIPCHK(c, hipEventRecord(c->ev_fork2, st));
         HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork2, 0));
         const int kt = c->kbegin(CHIP_K_EC_TABLES, c->aux);
-        launch_ecdsa_comb_build(c->aux, nk, meta, c->ectab.as<uint32_t>(), c->e_ctab.as<uint32_t>());
-        c->kend(kt, c->aux);
-        HIPCHK(c, hipEventRecord(c->ev_join2, c->aux));
+        uint32_t* ctab = c->e_ctab.as<uint32_t>();
+        launch_ecdsa_comb_chain(c->aux, nk, meta, c->ectab.as<uint32_t>(), ctab, 0);
+        HIPCHK(c, hipEventRecord(c->ev_ec_chain_lo, c->aux));
+        launch_ecdsa_comb_chain(c->aux, nk, meta, c->ectab.as<uint32_t>(), ctab, 1);
+        HIPCHK(c, hipEventRecord(c->ev_ec_chain_hi, c->aux));
+        // CHIP_EC_SPLIT=0: both fills after the whole chain on aux (the round-1 order)
+        hipStream_t fs = c->ec_split ? c->aux2 : c->aux;
+        if (c->ec_split) HIPCHK(c, hipStreamWaitEvent(fs, c->ev_ec_chain_lo, 0));
+        else HIPCHK(c, hipStreamWaitEvent(fs, c->ev_ec_chain_hi, 0));
+        launch_ecdsa_comb_fill(fs, nk, meta, ctab, 0);
+        HIPCHK(c, hipEventRecord(c->ev_ec_lo, fs));
+        HIPCHK(c, hipStreamWaitEvent(fs, c->ev_ec_chain_hi, 0));
+        launch_ecdsa_comb_fill(fs, nk, meta, ctab, 1);
+        c->kend(kt, fs);
+        HIPCHK(c, hipEventRecord(c->ev_join2, fs));
     }
     c->kend(ke, st);
     if (n) {
@@ -537,9 +565,14 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         launch_ed25519_verify(st, n, ed_list, ed_count, b, c->abytes.as<uint32_t>(), c->edtab.as<uint32_t>(), status);
         c->kend(ke, st);
         if (ec_comb) {
+            // u2 Q, both curves per launch: windows 0..31 once the low table half exists, 32..64 after
+            HIPCHK(c, hipStreamWaitEvent(st, c->ev_ec_lo, 0));
+            ke = c->kbegin(CHIP_K_ECDSA_R1, st);
+            launch_ecdsa_comb_q(st, n, gl_r1, gl_k1, counts, b, c->e_ctab.as<uint32_t>(), mid_r1, mid_k1, status, 0);
+            c->kend(ke, st);
             HIPCHK(c, hipStreamWaitEvent(st, c->ev_join2, 0));
-            ke = c->kbegin(CHIP_K_ECDSA_R1, st);   // both curves' table halves (one launch)
-            launch_ecdsa_comb_q(st, n, gl_r1, gl_k1, counts, b, c->e_ctab.as<uint32_t>(), mid_r1, mid_k1, status);
+            ke = c->kbegin(CHIP_K_ECDSA_K1, st);
+            launch_ecdsa_comb_q(st, n, gl_r1, gl_k1, counts, b, c->e_ctab.as<uint32_t>(), mid_r1, mid_k1, status, 1);
             c->kend(ke, st);
         } else {
             ke = c->kbegin(CHIP_K_ECDSA_R1, st);

@@ -21,8 +21,10 @@ void launch_ecdsa_verify(hipStream_t st, int scheme, uint64_t n, const uint32_t*
 
 // ECDSA per-key comb path (ecdsa.hip): tables of 2^(4w) {1..8} Q per key (slot = key index)
 uint64_t ecdsa_comb_key_words();
-void launch_ecdsa_comb_build(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, const uint32_t* ectab,
-                             uint32_t* ctab);
+// in two halves each (half 0: windows 0..31, half 1: windows 32..64): chain (serial doublings), fill
+void launch_ecdsa_comb_chain(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, const uint32_t* ectab,
+                             uint32_t* ctab, int half);
+void launch_ecdsa_comb_fill(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, uint32_t* ctab, int half);
 uint64_t ecdsa_comb_mid_words();
 // fixed-base G combs of both curves (built once per context)
 uint64_t ecdsa_gcomb_words();
@@ -39,9 +41,10 @@ void launch_ecdsa_comb_inv(hipStream_t st, uint64_t n, const uint32_t* counts, u
 // g and q run both curves in one grid (P-256 blocks first)
 void launch_ecdsa_comb_g(hipStream_t st, uint64_t n, const uint32_t* counts, const uint32_t* gcomb, uint32_t* mid_r1,
                          uint32_t* mid_k1, const uint32_t* wp_r1, const uint32_t* wp_k1);
+// table_half 0: windows 0..31 of u2 (partial sum parked in mid); 1: windows 32..64 + the x(R) check
 void launch_ecdsa_comb_q(hipStream_t st, uint64_t n, const uint32_t* list_r1, const uint32_t* list_k1,
-                         const uint32_t* counts, const chip_sig_batch* b, const uint32_t* ctab, const uint32_t* mid_r1,
-                         const uint32_t* mid_k1, uint8_t* status);
+                         const uint32_t* counts, const chip_sig_batch* b, const uint32_t* ctab, uint32_t* mid_r1,
+                         uint32_t* mid_k1, uint8_t* status, int table_half);
 
 void launch_txid(hipStream_t st, const chip_tx_batch* b, uint8_t* ids, uint32_t* scratch, uint64_t scratch_words);
 uint64_t ftx_scratch_words(uint64_t ntx);

@@ -406,7 +406,8 @@ int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_st
  * table builds (on the context's second stream when every key gets a table), CHIP_K_ED_PLAN = slot
  * assignment + key-grouped work list; CHIP_K_ECDSA_R1/K1 = the ECDSA kernels that need the key's
  * table: k_ecdsa_verify per curve on the windowed schedule; on the comb schedule k_ecdsa_comb_q runs
- * both curves in one launch, counted under CHIP_K_ECDSA_R1; CHIP_K_EC_FRONT = the ECDSA comb
+ * both curves per launch in two launches, the low table half (windows 0..31) counted under
+ * CHIP_K_ECDSA_R1 and the high half (+ the x(R) check) under CHIP_K_ECDSA_K1; CHIP_K_EC_FRONT = the ECDSA comb
  * kernels that need none (key grouping, DER/SHA-256/s R, batched s^-1, u1 G; both curves);
  * CHIP_K_REQ = k_required_signers */
 enum chip_kernel { CHIP_K_ED25519 = 0, CHIP_K_ECDSA_R1 = 1, CHIP_K_ECDSA_K1 = 2, CHIP_K_TXID = 3,
