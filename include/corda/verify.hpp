@@ -401,57 +401,66 @@ struct Item {
     const Bytes* msg;
 };
 
+// chip_sig_batch pools of a list of items (keys and messages de-duplicated by bytes)
+struct SigPack {
+    std::map<Bytes, uint32_t> kid, mid;
+    std::vector<uint32_t> key_idx, msg_idx, sig_len, key_len, msg_len;
+    std::vector<uint64_t> sig_off, key_off, msg_off;
+    Bytes sig_pool, key_pool, msg_pool;
+    explicit SigPack(const std::vector<Item>& items) {
+        std::vector<const Bytes*> keys, msgs;
+        for (const Item& it : items) {
+            auto k = kid.emplace(*it.key, (uint32_t)keys.size());
+            if (k.second) keys.push_back(it.key);
+            auto m = mid.emplace(*it.msg, (uint32_t)msgs.size());
+            if (m.second) msgs.push_back(it.msg);
+            key_idx.push_back(k.first->second);
+            msg_idx.push_back(m.first->second);
+            sig_off.push_back(sig_pool.size());
+            sig_len.push_back((uint32_t)it.sig->size());
+            sig_pool.insert(sig_pool.end(), it.sig->begin(), it.sig->end());
+        }
+        auto pack = [](const std::vector<const Bytes*>& v, Bytes& pool, std::vector<uint64_t>& off,
+                       std::vector<uint32_t>& len) {
+            for (const Bytes* b : v) {
+                off.push_back(pool.size());
+                len.push_back((uint32_t)b->size());
+                pool.insert(pool.end(), b->begin(), b->end());
+            }
+            if (pool.empty()) pool.push_back(0);
+        };
+        pack(keys, key_pool, key_off, key_len);
+        pack(msgs, msg_pool, msg_off, msg_len);
+        if (sig_pool.empty()) sig_pool.push_back(0);
+    }
+    chip_sig_batch batch() const {
+        chip_sig_batch b{};
+        b.n = key_idx.size();
+        b.key_idx = key_idx.data();
+        b.msg_idx = msg_idx.data();
+        b.sig_data = sig_pool.data();
+        b.sig_off = sig_off.data();
+        b.sig_len = sig_len.data();
+        b.n_keys = key_off.size();
+        b.key_data = key_pool.data();
+        b.key_off = key_off.data();
+        b.key_len = key_len.data();
+        b.n_msgs = msg_off.size();
+        b.msg_data = msg_pool.data();
+        b.msg_off = msg_off.data();
+        b.msg_len = msg_len.data();
+        b.sig_bytes = sig_pool.size();
+        b.key_bytes = key_pool.size();
+        b.msg_bytes = msg_pool.size();
+        return b;
+    }
+};
+
 // status of every item, one batch call (keys and messages de-duplicated); is_valid: Crypto.isValid
 // semantics (chip_is_valid_batch: no empty-input checks)
 inline std::vector<uint8_t> verify_items(Engine& e, const std::vector<Item>& items, bool is_valid = false) {
-    std::map<Bytes, uint32_t> kid, mid;
-    std::vector<const Bytes*> keys, msgs;
-    std::vector<uint32_t> key_idx, msg_idx, sig_len;
-    std::vector<uint64_t> sig_off;
-    Bytes sig_pool;
-    for (const Item& it : items) {
-        auto k = kid.emplace(*it.key, (uint32_t)keys.size());
-        if (k.second) keys.push_back(it.key);
-        auto m = mid.emplace(*it.msg, (uint32_t)msgs.size());
-        if (m.second) msgs.push_back(it.msg);
-        key_idx.push_back(k.first->second);
-        msg_idx.push_back(m.first->second);
-        sig_off.push_back(sig_pool.size());
-        sig_len.push_back((uint32_t)it.sig->size());
-        sig_pool.insert(sig_pool.end(), it.sig->begin(), it.sig->end());
-    }
-    auto pack = [](const std::vector<const Bytes*>& v, Bytes& pool, std::vector<uint64_t>& off, std::vector<uint32_t>& len) {
-        for (const Bytes* b : v) {
-            off.push_back(pool.size());
-            len.push_back((uint32_t)b->size());
-            pool.insert(pool.end(), b->begin(), b->end());
-        }
-        if (pool.empty()) pool.push_back(0);
-    };
-    Bytes key_pool, msg_pool;
-    std::vector<uint64_t> key_off, msg_off;
-    std::vector<uint32_t> key_len, msg_len;
-    pack(keys, key_pool, key_off, key_len);
-    pack(msgs, msg_pool, msg_off, msg_len);
-    if (sig_pool.empty()) sig_pool.push_back(0);
-    chip_sig_batch b{};
-    b.n = items.size();
-    b.key_idx = key_idx.data();
-    b.msg_idx = msg_idx.data();
-    b.sig_data = sig_pool.data();
-    b.sig_off = sig_off.data();
-    b.sig_len = sig_len.data();
-    b.n_keys = keys.size();
-    b.key_data = key_pool.data();
-    b.key_off = key_off.data();
-    b.key_len = key_len.data();
-    b.n_msgs = msgs.size();
-    b.msg_data = msg_pool.data();
-    b.msg_off = msg_off.data();
-    b.msg_len = msg_len.data();
-    b.sig_bytes = sig_pool.size();
-    b.key_bytes = key_pool.size();
-    b.msg_bytes = msg_pool.size();
+    const SigPack p(items);
+    const chip_sig_batch b = p.batch();
     std::vector<uint8_t> status(items.size());
     if (!items.empty())
         e.check((is_valid ? chip_is_valid_batch : chip_verify_batch)(e.get(), &b, status.data(), nullptr));
@@ -599,6 +608,112 @@ inline std::vector<std::exception_ptr> checkSignaturesAreValidBatch(Engine& e,
             } catch (...) {
                 res[t] = std::current_exception();
             }
+        }
+    }
+    return res;
+}
+
+// Batch verifySignaturesExcept (TransactionWithSignatures.kt:44-50) for many transactions: the
+// signatures in one chip_verify_batch call, then every transaction's required-signer check on the
+// device in one chip_required_signers call (first failing signature, getMissingSigners with
+// CompositeKey thresholds flattened to post-order key trees, minus allowedToBeMissing).  result[i] is
+// null when transaction i passes, else the exception its own sequential call would have thrown first.
+inline std::vector<std::exception_ptr> verifySignaturesExceptBatch(Engine& e,
+                                                                   const std::vector<const SignedTransaction*>& txs,
+                                                                   const std::vector<PublicKey>& allowedToBeMissing = {}) {
+    std::vector<Bytes> msgs;
+    for (const auto* t : txs)
+        for (const auto& s : t->sigs) msgs.push_back(s.signable(t->id, t->serializer));
+    std::vector<detail::Item> items;
+    std::vector<uint64_t> sig_start{0};
+    size_t m = 0;
+    for (const auto* t : txs) {
+        for (const auto& s : t->sigs) items.push_back({&s.by.encoded, &s.bytes, &msgs[m++]});
+        sig_start.push_back(items.size());
+    }
+    detail::SigPack pack(items);
+    std::vector<uint8_t> status(items.size());
+    chip_sig_batch b = pack.batch();
+    if (!items.empty()) e.check(chip_verify_batch(e.get(), &b, status.data(), nullptr));
+    // required keys as post-order key trees over the pack's key pool
+    const std::set<PublicKey> allowed(allowedToBeMissing.begin(), allowedToBeMissing.end());
+    std::vector<uint64_t> req_start{0}, node_start{0};
+    std::vector<uint32_t> val, nkids, weight;
+    std::vector<uint8_t> allow;
+    std::vector<std::vector<PublicKey>> req(txs.size());
+    struct Tree { std::vector<uint32_t> val, nkids, weight; };
+    std::function<void(const PublicKey&, int, Tree&)> flatten = [&](const PublicKey& k, int w, Tree& o) {
+        if (CompositeKey::isComposite(k)) {
+            const CompositeKey ck = CompositeKey::decode(k);   // validates (checkConstraints)
+            for (const auto& c : ck.children) flatten(c.key, c.weight, o);
+            o.val.push_back((uint32_t)ck.threshold);
+            o.nkids.push_back((uint32_t)ck.children.size());
+        } else {
+            auto it = pack.kid.find(k.encoded);
+            o.val.push_back(it == pack.kid.end() ? CHIP_REQ_NO_SIGNER : it->second);
+            o.nkids.push_back(0);
+        }
+        o.weight.push_back((uint32_t)w);
+    };
+    std::vector<std::exception_ptr> res(txs.size()), invalid(txs.size());
+    for (size_t t = 0; t < txs.size(); t++) {
+        // CompositeKey validation (isFulfilledBy's checkValidity) may throw: for this tx only, and
+        // only reported once its signatures passed
+        std::vector<Tree> trees;
+        try {
+            for (const auto& k : txs[t]->requiredSigningKeys) {
+                trees.emplace_back();
+                flatten(k, 1, trees.back());
+            }
+        } catch (...) {
+            invalid[t] = std::current_exception();
+            trees.clear();
+        }
+        if (!invalid[t]) {
+            size_t i = 0;
+            for (const auto& k : txs[t]->requiredSigningKeys) {
+                const Tree& tr = trees[i++];
+                val.insert(val.end(), tr.val.begin(), tr.val.end());
+                nkids.insert(nkids.end(), tr.nkids.begin(), tr.nkids.end());
+                weight.insert(weight.end(), tr.weight.begin(), tr.weight.end());
+                node_start.push_back(val.size());
+                allow.push_back(allowed.count(k) ? 1 : 0);
+                req[t].push_back(k);
+            }
+        }
+        req_start.push_back(allow.size());
+    }
+    chip_req_batch q{};
+    q.ntx = txs.size();
+    q.sig_start = sig_start.data();
+    q.req_start = req_start.data();
+    q.nreq = allow.size();
+    q.node_start = node_start.data();
+    q.allowed = allow.data();
+    q.n_nodes = val.size();
+    q.node_val = val.data();
+    q.node_nkids = nkids.data();
+    q.node_weight = weight.data();
+    std::vector<uint8_t> verdict(txs.size());
+    std::vector<uint32_t> arg(txs.size());
+    std::vector<uint8_t> missing(allow.size() + 1);
+    if (!txs.empty())
+        e.check(chip_required_signers(e.get(), &q, &b, status.data(), verdict.data(), arg.data(), missing.data()));
+    for (size_t t = 0; t < txs.size(); t++) {
+        try {
+            if (verdict[t] == CHIP_TXV_SIGNATURE) detail::throw_for(status[arg[t]], items[arg[t]].key[0]);
+            if (invalid[t]) std::rethrow_exception(invalid[t]);
+            if (verdict[t] == CHIP_TXV_MISSING) {
+                std::set<PublicKey> needed;
+                for (size_t i = 0; i < req[t].size(); i++)
+                    if (missing[req_start[t] + i]) needed.insert(req[t][i]);
+                throw SignaturesMissingException(needed, {}, txs[t]->id);
+            }
+            if (verdict[t] != CHIP_TXV_OK) throw EngineException("required-signer batch malformed");
+        } catch (const EngineException&) {
+            throw;
+        } catch (...) {
+            res[t] = std::current_exception();
         }
     }
     return res;

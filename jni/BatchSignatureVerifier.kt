@@ -1,5 +1,6 @@
 package net.corda.core.internal.gpu
 
+import net.corda.core.crypto.CompositeKey
 import net.corda.core.crypto.Crypto
 import net.corda.core.crypto.SecureHash
 import net.corda.core.crypto.SignableData
@@ -7,9 +8,11 @@ import net.corda.core.crypto.SignatureMetadata
 import net.corda.core.crypto.TransactionSignature
 import net.corda.core.serialization.serialize
 import net.corda.core.transactions.SignedTransaction
+import net.corda.core.transactions.SignedTransaction.SignaturesMissingException
 import java.nio.ByteBuffer
 import java.nio.ByteOrder
 import java.security.PublicKey
+import net.corda.core.utilities.toNonEmptySet
 
 /**
  * Batched signature verification on an MI355X (libcordahip through CordaHip).
@@ -123,6 +126,97 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0) : AutoCloseable {
                 p++
             }
             err
+        }
+    }
+
+    /**
+     * SignedTransaction.verifySignaturesExcept for many transactions (TransactionWithSignatures.kt:44-50):
+     * the signatures in one device batch, then getMissingSigners - allowedToBeMissing of every
+     * transaction in one more (chip_required_signers: CompositeKey trees flattened in post-order over
+     * the batch's key pool).  result[i] is null when transaction i passes, else its exception.
+     */
+    fun verifySignaturesExcept(txs: List<SignedTransaction>, allowedToBeMissing: Set<PublicKey> = emptySet()): List<Exception?> {
+        val sigErr = checkSignaturesAreValid(txs)
+        val keyIds = HashMap<ByteBuffer, Int>()
+        val keys = ArrayList<ByteArray>()
+        val keyIdx = ArrayList<Int>()
+        val sigStart = LongArray(txs.size + 1)
+        for ((t, tx) in txs.withIndex()) {
+            for (s in tx.sigs) {
+                val enc = s.by.encoded
+                keyIdx.add(keyIds.getOrPut(ByteBuffer.wrap(enc)) { keys.add(enc); keys.size - 1 })
+            }
+            sigStart[t + 1] = keyIdx.size.toLong()
+        }
+        val vals = ArrayList<Int>(); val nkids = ArrayList<Int>(); val weights = ArrayList<Int>()
+        fun flatten(k: PublicKey, w: Int) {
+            if (k is CompositeKey) {
+                for (c in k.children) flatten(c.node, c.weight)
+                vals.add(k.threshold); nkids.add(k.children.size)
+            } else {
+                vals.add(keyIds[ByteBuffer.wrap(k.encoded)] ?: -1)   // -1 = CHIP_REQ_NO_SIGNER
+                nkids.add(0)
+            }
+            weights.add(w)
+        }
+        val reqStart = LongArray(txs.size + 1)
+        val nodeStart = ArrayList<Long>().apply { add(0L) }
+        val allowed = ArrayList<Byte>()
+        val required = ArrayList<List<PublicKey>>()
+        val invalid = arrayOfNulls<Exception>(txs.size)
+        for ((t, tx) in txs.withIndex()) {
+            val req = tx.tx.requiredSigningKeys.toList()
+            try {
+                req.forEach { if (it is CompositeKey) it.checkValidity() }   // isFulfilledBy validates first
+                for (k in req) {
+                    flatten(k, 1)
+                    nodeStart.add(vals.size.toLong())
+                    allowed.add(if (k in allowedToBeMissing) 1 else 0)
+                }
+                required.add(req)
+            } catch (e: IllegalArgumentException) {
+                invalid[t] = e
+                required.add(emptyList())
+            }
+            reqStart[t + 1] = allowed.size.toLong()
+        }
+        val b = arena.reserve(64 + 8 * (2 * txs.size + nodeStart.size + keys.size) + 4 * (keyIdx.size + keys.size +
+                3 * vals.size) + keys.sumOf { it.size } + allowed.size + 16 * txs.size + allowed.size + 1024)
+        fun take(bytes: Int): ByteBuffer {
+            val s = b.slice().order(ByteOrder.LITTLE_ENDIAN)
+            s.limit(maxOf(bytes, 1))
+            b.position(b.position() + ((bytes + 7) and 7.inv()).coerceAtLeast(8))
+            return s
+        }
+        val bKeyIdx = take(4 * keyIdx.size).apply { keyIdx.forEach { putInt(it) } }
+        val bKeyOff = take(8 * keys.size); val bKeyLen = take(4 * keys.size)
+        val bKeys = take(keys.sumOf { it.size })
+        var o = 0L
+        for (k in keys) { bKeyOff.putLong(o); bKeyLen.putInt(k.size); bKeys.put(k); o += k.size }
+        // statuses: all VALID (a transaction with a failing signature already has its exception, sigErr)
+        val bStatus = take(keyIdx.size).apply { repeat(keyIdx.size) { put(0) } }
+        val bSigStart = take(8 * sigStart.size).apply { sigStart.forEach { putLong(it) } }
+        val bReqStart = take(8 * reqStart.size).apply { reqStart.forEach { putLong(it) } }
+        val bNodeStart = take(8 * nodeStart.size).apply { nodeStart.forEach { putLong(it) } }
+        val bAllowed = take(allowed.size).apply { allowed.forEach { put(it) } }
+        val bVal = take(4 * vals.size).apply { vals.forEach { putInt(it) } }
+        val bNk = take(4 * nkids.size).apply { nkids.forEach { putInt(it) } }
+        val bW = take(4 * weights.size).apply { weights.forEach { putInt(it) } }
+        val bVerdict = take(txs.size); val bArg = take(4 * txs.size); val bMissing = take(allowed.size)
+        val rc = CordaHip.requiredSigners(ctx, keyIdx.size, bKeyIdx, keys.size, bKeys, bKeyOff, bKeyLen, bStatus,
+                txs.size, bSigStart, bReqStart, allowed.size, bNodeStart, bAllowed, vals.size, bVal, bNk, bW,
+                bVerdict, bArg, bMissing)
+        check(rc == 0) { "libcordahip requiredSigners failed ($rc): ${CordaHip.lastError(ctx)}" }
+        return txs.mapIndexed { t, tx ->
+            sigErr[t] ?: invalid[t] ?: when (bVerdict.get(t).toInt()) {
+                0 -> null
+                2 -> {
+                    val r0 = reqStart[t].toInt()
+                    val needed = required[t].filterIndexed { i, _ -> bMissing.get(r0 + i).toInt() != 0 }.toSet()
+                    SignaturesMissingException(needed.toNonEmptySet(), tx.getKeyDescriptions(needed), tx.id)
+                }
+                else -> IllegalStateException("required-signer batch malformed at transaction $t")
+            }
         }
     }
 

@@ -42,6 +42,13 @@ object CordaHip {
                                         nMsgs: Int, msgData: ByteBuffer, msgOff: ByteBuffer, msgLen: ByteBuffer,
                                         status: ByteBuffer): Int
 
+    @JvmStatic external fun requiredSigners(ctx: Long, n: Int, keyIdx: ByteBuffer, nKeys: Int, keyData: ByteBuffer,
+                                            keyOff: ByteBuffer, keyLen: ByteBuffer, status: ByteBuffer, ntx: Int,
+                                            sigStart: ByteBuffer, reqStart: ByteBuffer, nreq: Int,
+                                            nodeStart: ByteBuffer, allowed: ByteBuffer?, nNodes: Int,
+                                            nodeVal: ByteBuffer, nodeNkids: ByteBuffer, nodeWeight: ByteBuffer,
+                                            verdict: ByteBuffer, arg: ByteBuffer, missing: ByteBuffer?): Int
+
     @JvmStatic external fun txIds(ctx: Long, ntx: Int, salts: ByteBuffer, txCompStart: ByteBuffer, nComp: Int,
                                   compGroup: ByteBuffer, compInternal: ByteBuffer, data: ByteBuffer,
                                   compOff: ByteBuffer, compLen: ByteBuffer, ids: ByteBuffer): Int

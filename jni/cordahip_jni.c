@@ -92,6 +92,45 @@ JNIEXPORT jint JNICALL CLS(verifyBatch)(JNIEnv* env, jclass cls, jlong ctx, jboo
     return isValid ? chip_is_valid_batch(c, &b, st, NULL) : chip_verify_batch(c, &b, st, NULL);
 }
 
+/* ---- required signers (chip_req_batch over the key pool / statuses of a verified batch) ----
+ * verdict: ntx bytes out (CHIP_TXV_*); arg: ntx u32 out; missing: nreq bytes out (may be null). */
+JNIEXPORT jint JNICALL CLS(requiredSigners)(JNIEnv* env, jclass cls, jlong ctx, jint n, jobject keyIdx, jint nKeys,
+                                            jobject keyData, jobject keyOff, jobject keyLen, jobject status,
+                                            jint ntx, jobject sigStart, jobject reqStart, jint nreq,
+                                            jobject nodeStart, jobject allowed, jint nNodes, jobject nodeVal,
+                                            jobject nodeNkids, jobject nodeWeight, jobject verdict, jobject arg,
+                                            jobject missing) {
+    (void)cls;
+    if (n < 0 || ntx < 0 || nreq < 0 || nNodes < 0) return CHIP_E_ARG;
+    chip_sig_batch b;
+    memset(&b, 0, sizeof b);
+    b.n = (uint64_t)n;
+    b.key_idx = (const uint32_t*)addr(env, keyIdx);
+    b.n_keys = (uint64_t)nKeys;
+    b.key_data = (const uint8_t*)addr(env, keyData);
+    b.key_off = (const uint64_t*)addr(env, keyOff);
+    b.key_len = (const uint32_t*)addr(env, keyLen);
+    b.key_bytes = cap_of(env, keyData);
+    chip_req_batch q;
+    memset(&q, 0, sizeof q);
+    q.ntx = (uint64_t)ntx;
+    q.sig_start = (const uint64_t*)addr(env, sigStart);
+    q.req_start = (const uint64_t*)addr(env, reqStart);
+    q.nreq = (uint64_t)nreq;
+    q.node_start = (const uint64_t*)addr(env, nodeStart);
+    q.allowed = (const uint8_t*)addr(env, allowed);
+    q.n_nodes = (uint64_t)nNodes;
+    q.node_val = (const uint32_t*)addr(env, nodeVal);
+    q.node_nkids = (const uint32_t*)addr(env, nodeNkids);
+    q.node_weight = (const uint32_t*)addr(env, nodeWeight);
+    uint8_t* v = (uint8_t*)addr(env, verdict);
+    uint32_t* a = (uint32_t*)addr(env, arg);
+    if (ntx > 0 && (!v || !a || cap_of(env, verdict) < (uint64_t)ntx || cap_of(env, arg) < 4ull * (uint64_t)ntx))
+        return CHIP_E_ARG;
+    return chip_required_signers((chip_ctx*)(intptr_t)ctx, &q, &b, (const uint8_t*)addr(env, status), v, a,
+                                 (uint8_t*)addr(env, missing));
+}
+
 /* ---- tx ids (chip_tx_batch SoA); ids: ntx * 32 bytes out ---- */
 JNIEXPORT jint JNICALL CLS(txIds)(JNIEnv* env, jclass cls, jlong ctx, jint ntx, jobject salts, jobject txCompStart,
                                   jint nComp, jobject compGroup, jobject compInternal, jobject data,

@@ -117,6 +117,38 @@ int main() {
     CHECK(throws<IllegalArgumentException>([&] { bad2.checkSignaturesAreValid(e); }));
     auto res = checkSignaturesAreValidBatch(e, {&stx, &bad2});
     CHECK(!res[0] && res[1]);
+    // --- batch verifySignaturesExcept: required signers on the device (chip_required_signers) ---
+    {
+        const PublicKey twoOfThree = CompositeKey::build({{alice.pub, 1}, {bob.pub, 1}, {notary.pub, 1}}, 2);
+        SignedTransaction c1(txId, {ts, tb}, {twoOfThree});          // alice + bob: fulfilled
+        SignedTransaction c2(txId, {ts}, {twoOfThree, bob.pub});    // only alice: both missing
+        SignedTransaction c3(txId, {ts}, {alice.pub, notary.pub});  // notary missing but allowed
+        for (auto* x : {&c1, &c2, &c3}) x->serializer = signable;
+        auto r = verifySignaturesExceptBatch(e, {&stx, &bad2, &c1, &c2, &c3}, {notary.pub});
+        CHECK(!r[0] && r[1] && !r[2] && r[3] && !r[4]);
+        bool both = false;
+        try {
+            std::rethrow_exception(r[3]);
+        } catch (const SignaturesMissingException& m) {
+            both = m.missing.size() == 2 && m.missing.count(twoOfThree) && m.missing.count(bob.pub);
+        } catch (...) {
+        }
+        CHECK(both);
+        bool iae = false;
+        try {
+            std::rethrow_exception(r[1]);
+        } catch (const IllegalArgumentException&) {
+            iae = true;
+        } catch (...) {
+        }
+        CHECK(iae);
+        // the sequential path agrees for every transaction
+        const SignedTransaction* all[] = {&stx, &bad2, &c1, &c2, &c3};
+        for (int i = 0; i < 5; i++) {
+            const bool threw = throws<std::exception>([&] { all[i]->verifySignaturesExcept(e, {notary.pub}); });
+            CHECK(threw == (bool)r[i]);
+        }
+    }
     // --- WireTransaction.id vs an independent SHA-256 restatement ---
     WireTransaction wtx;
     wtx.componentGroups = {{1, {Bytes(640, 7)}}, {0, {Bytes(96, 1), Bytes(96, 2)}}, {4, {Bytes(384, 9)}}};
