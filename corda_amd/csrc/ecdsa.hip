@@ -676,29 +676,20 @@ __global__ void __launch_bounds__(256) k_ec_group_base(uint64_t n_keys, const Ke
     __syncthreads();
     if (curve >= 0) key_base[k] = s_base[curve] + (curve == 0 ? ex0 : ex1);
 }
-// one lane per (curve list, position): grid covers 2 n lanes, [0, n) r1 and [n, 2n) k1
+// one lane per (curve list, position): grid covers 2 n lanes, [0, n) r1 and [n, 2n) k1; the slot
+// inside the key's range is the signature's key rank from k_classify (no atomics)
 __global__ void __launch_bounds__(256) k_ec_group_scatter(uint64_t n, const uint32_t* __restrict__ lists,
                                                           const uint32_t* __restrict__ counts,
                                                           const uint32_t* __restrict__ key_idx,
                                                           const uint32_t* __restrict__ key_base,
-                                                          uint32_t* __restrict__ key_cur, uint32_t* __restrict__ out) {
+                                                          const uint32_t* __restrict__ key_rank, uint32_t* __restrict__ out) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t lane = threadIdx.x & 63;
     const int L = g < n ? 0 : 1;
     const uint64_t pos = g - (uint64_t)L * n;
     const uint32_t cnt = counts[L == 0 ? LIST_R1 : LIST_K1];
-    const bool v = pos < cnt;
-    uint32_t i = 0, k = 0;
-    if (v) {
-        i = lists[(uint64_t)(L == 0 ? LIST_R1 : LIST_K1) * n + pos];
-        k = key_idx[i];
-    }
-    uint32_t leader, c, rank;
-    wave_group(v, k, leader, c, rank);
-    uint32_t cur = 0;
-    if (v && lane == leader) cur = atomicAdd(&key_cur[k], c);
-    cur = __shfl(cur, (int)leader);
-    if (v) out[(uint64_t)L * n + key_base[k] + cur + rank] = i;
+    if (pos >= cnt) return;
+    const uint32_t i = lists[(uint64_t)(L == 0 ? LIST_R1 : LIST_K1) * n + pos];
+    out[(uint64_t)L * n + key_base[key_idx[i]] + key_rank[i]] = i;
 }
 
 // ---- signature kernels, SoA hand-off by list position (`cap` = list capacity) ----
@@ -961,13 +952,13 @@ uint64_t ecdsa_comb_mid_words() { return EC_MID_WORDS; }
 uint64_t ecdsa_comb_wp_words(uint64_t n) { return ((n + 63) / 64) * 8; }
 
 void launch_ecdsa_group(hipStream_t st, uint64_t n, uint64_t n_keys, const KeyMeta* meta, const uint32_t* key_count,
-                        uint32_t* key_base, uint32_t* key_cur, uint32_t* ctr, const uint32_t* lists,
+                        uint32_t* key_base, const uint32_t* key_rank, uint32_t* ctr, const uint32_t* lists,
                         const uint32_t* counts, const uint32_t* key_idx, uint32_t* grouped) {
     if (!n || !n_keys) return;
     hipLaunchKernelGGL(k_ec_group_base, dim3((uint32_t)((n_keys + 255) / 256)), dim3(256), 0, st, n_keys, meta, key_count,
                        key_base, ctr);
     hipLaunchKernelGGL(k_ec_group_scatter, dim3((uint32_t)((2 * n + 255) / 256)), dim3(256), 0, st, n, lists, counts,
-                       key_idx, key_base, key_cur, grouped);
+                       key_idx, key_base, key_rank, grouped);
 }
 
 template <int C>

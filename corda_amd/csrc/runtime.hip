@@ -56,7 +56,7 @@ struct chip_ctx {
     // verify workspaces
     DevBuf meta, abytes, edtab, ectab, lists, counts;
     // Ed25519 comb path
-    DevBuf c_key_count, c_key_slot, c_key_base, c_key_cur, c_slot_key, c_ctr, c_comb_list, c_straus_list, c_ctab,
+    DevBuf c_key_count, c_key_rank, c_key_slot, c_key_base, c_key_cur, c_slot_key, c_ctr, c_comb_list, c_straus_list, c_ctab,
         c_xyz, c_zpre, c_nega, c_bmid, e_ctab, e_mid, e_gcomb, e_bcomb16, e_wp, e_glist;
     // host-path mirrors of the caller's buffers
     DevBuf h_key_idx, h_msg_idx, h_sig_data, h_sig_off, h_sig_len, h_key_data, h_key_off, h_key_len, h_msg_data,
@@ -138,7 +138,7 @@ __global__ void __launch_bounds__(CLASSIFY_BLOCK) k_classify(uint64_t n, const u
                                                   uint64_t n_msgs, const KeyMeta* __restrict__ meta,
                                                   uint8_t* __restrict__ status, uint32_t* __restrict__ lists,
                                                   uint32_t* __restrict__ counts, uint32_t* __restrict__ key_count,
-                                                  uint32_t is_valid) {
+                                                  uint32_t* __restrict__ key_rank, uint32_t is_valid) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     int list = -1;
     uint32_t k = 0;
@@ -161,11 +161,16 @@ __global__ void __launch_bounds__(CLASSIFY_BLOCK) k_classify(uint64_t n, const u
         if (list < 0) status[i] = st;
     }
     const uint32_t lane = threadIdx.x & 63;
-    if (key_count) {   // comb-path histogram: signatures per key (one scheme per key), one atomic per key per wave
+    if (key_count) {   // comb-path histogram: signatures per key (one scheme per key), one atomic per key per
+                       // wave; key_rank[i] = the signature's rank among its key's (the counting sort's slot,
+                       // so the work-list scatters need no atomics of their own)
         uint32_t leader, cnt, rank;
         const bool arith = list >= 0;
         wave_group(arith, k, leader, cnt, rank);
-        if (arith && lane == leader) atomicAdd(&key_count[k], cnt);
+        uint32_t base = 0;
+        if (arith && lane == leader) base = atomicAdd(&key_count[k], cnt);
+        base = (uint32_t)__shfl((int)base, (int)leader);
+        if (arith) key_rank[i] = base + rank;
     }
     // list slots: one atomic per list per workgroup (per-wave offsets from an LDS prefix)
     __shared__ uint32_t s_cnt[CLASSIFY_BLOCK / 64][N_LISTS];
@@ -341,7 +346,7 @@ void chip_shutdown(chip_ctx* c) {
     if (!c) return;
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
-    DevBuf* bufs[] = {&c->meta, &c->abytes, &c->edtab, &c->ectab, &c->lists, &c->counts, &c->c_key_count,
+    DevBuf* bufs[] = {&c->meta, &c->abytes, &c->edtab, &c->ectab, &c->lists, &c->counts, &c->c_key_count, &c->c_key_rank,
                       &c->c_key_slot, &c->c_key_base, &c->c_key_cur, &c->c_slot_key, &c->c_ctr, &c->c_comb_list,
                       &c->c_straus_list, &c->c_ctab, &c->c_xyz, &c->c_zpre, &c->c_nega, &c->c_bmid, &c->e_ctab, &c->e_mid, &c->e_gcomb, &c->e_bcomb16, &c->e_wp, &c->e_glist, &c->h_key_idx, &c->h_msg_idx,
                       &c->h_sig_data, &c->h_sig_off, &c->h_sig_len, &c->h_key_data, &c->h_key_off, &c->h_key_len,
@@ -406,10 +411,12 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         HIPCHK(c, c->c_key_count.ensure(nk * 4 + 16));
         HIPCHK(c, c->c_key_base.ensure(nk * 4 + 16));
         HIPCHK(c, c->c_key_cur.ensure(nk * 4 + 16));
+        HIPCHK(c, c->c_key_rank.ensure(n * 4 + 16));
         HIPCHK(c, c->c_ctr.ensure(64));
         w.key_count = c->c_key_count.as<uint32_t>();
         w.key_base = c->c_key_base.as<uint32_t>();
         w.key_cur = c->c_key_cur.as<uint32_t>();
+        w.key_rank = c->c_key_rank.as<uint32_t>();
         w.ctr = c->c_ctr.as<uint32_t>();
     }
     if (comb) {
@@ -506,7 +513,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         uint32_t* counts = c->counts.as<uint32_t>();
         hipLaunchKernelGGL(k_classify, dim3(blocks), dim3(CLASSIFY_BLOCK), 0, st, n, b->key_idx, b->msg_idx, b->sig_len, b->msg_len,
                            nk, b->n_msgs, meta, status, lists, counts, (comb || ec_comb) ? w.key_count : nullptr,
-                           is_valid ? 1u : 0u);
+                           w.key_rank, is_valid ? 1u : 0u);
         const uint32_t* ed_list = lists + (uint64_t)LIST_ED25519 * n;
         const uint32_t* ed_count = counts + LIST_ED25519;
         // ---- table-free kernels ----
@@ -531,7 +538,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
             uint32_t* wp_k1 = wp_r1 + ecdsa_comb_wp_words(n);
             ke = c->kbegin(CHIP_K_EC_FRONT, st);
             if (c->ec_group) {
-                launch_ecdsa_group(st, n, nk, meta, w.key_count, w.key_base, w.key_cur, w.ctr + 4, lists, counts,
+                launch_ecdsa_group(st, n, nk, meta, w.key_count, w.key_base, w.key_rank, w.ctr + 4, lists, counts,
                                    b->key_idx, gl_r1);
             } else {
                 gl_r1 = lists + (uint64_t)LIST_R1 * n;

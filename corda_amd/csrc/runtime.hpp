@@ -32,8 +32,9 @@ void launch_ecdsa_gcomb_build(hipStream_t st, uint32_t* gcomb);
 // comb signature kernels: pre (DER, SHA-256, s R, wave prefix/suffix products), inv (one inversion
 // per wave product, both curves), g (s^-1, u1, u2, u1 G); then q (u2 Q + check) once the tables exist
 uint64_t ecdsa_comb_wp_words(uint64_t n);
+// key_rank: each signature's rank among its key's (k_classify), so the scatter needs no atomics
 void launch_ecdsa_group(hipStream_t st, uint64_t n, uint64_t n_keys, const KeyMeta* meta, const uint32_t* key_count,
-                        uint32_t* key_base, uint32_t* key_cur, uint32_t* ctr, const uint32_t* lists,
+                        uint32_t* key_base, const uint32_t* key_rank, uint32_t* ctr, const uint32_t* lists,
                         const uint32_t* counts, const uint32_t* key_idx, uint32_t* grouped);
 void launch_ecdsa_comb_pre(hipStream_t st, int scheme, uint64_t n, const uint32_t* list, const uint32_t* count,
                            const chip_sig_batch* b, uint32_t* mid, uint32_t* wp, uint8_t* status);
@@ -78,6 +79,7 @@ struct EdCombWs {
     int32_t* key_slot;      // [n_keys] comb-table slot or -1 (Straus path)
     uint32_t* key_base;     // [n_keys] first position of the key's signatures in comb_list
     uint32_t* key_cur;      // [n_keys] fill cursor (zeroed per batch)
+    uint32_t* key_rank;     // [n] a signature's rank among its key's signatures (k_classify)
     uint32_t* slot_key;     // [max_slots]
     uint32_t* ctr;          // [0] slots claimed, [1] comb signatures, [2] Straus signatures, [4..5] ECDSA
                             // grouping, [8] / [9] comb signatures / slots after the min_total gate

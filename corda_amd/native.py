@@ -155,7 +155,8 @@ class ChipStats(ctypes.Structure):
 
 
 def lib_path() -> str:
-    return _build.LIB
+    # CORDAHIP_LIB: an alternative in-tree build of the same sources (A/B experiments, tools/)
+    return os.environ.get("CORDAHIP_LIB") or _build.LIB
 
 
 def load(build_if_missing: bool = False):
