@@ -364,6 +364,7 @@ __global__ void __launch_bounds__(256) k_ecdsa_verify(const uint32_t* __restrict
                                                       const uint32_t* __restrict__ msg_len,
                                                       const uint32_t* __restrict__ table, uint8_t* __restrict__ status) {
     __shared__ uint32_t gtab[EC_G_ENTRIES * 16];
+    if (blockIdx.x * blockDim.x >= *count) return;   // whole block past the list: skip the table load
     const ec_aff_c* G = (EC_CURVE(C) == CURVE_R1) ? EC_R1_G_TABLE : EC_K1_G_TABLE;
     for (int i = threadIdx.x; i < EC_G_ENTRIES * 16; i += blockDim.x) {
         const ec_aff_c& e = G[i >> 4];

@@ -94,6 +94,7 @@ __global__ void __launch_bounds__(256) k_ed25519_verify(const uint32_t* __restri
                                                         const uint32_t* __restrict__ abytes,
                                                         const uint32_t* __restrict__ table, uint8_t* __restrict__ status) {
     __shared__ uint32_t btab[ED_B_ENTRIES * 30];
+    if (blockIdx.x * blockDim.x >= *count) return;   // whole block past the list: skip the table load
     for (int i = threadIdx.x; i < ED_B_ENTRIES * 30; i += blockDim.x) {
         const niels_c& e = ED_B_TABLE[i / 30];
         const int f = (i % 30) / 10, l = i % 10;

@@ -56,7 +56,7 @@ struct chip_ctx {
     // verify workspaces
     DevBuf meta, abytes, edtab, ectab, lists, counts;
     // Ed25519 comb path
-    DevBuf c_key_count, c_key_rank, c_key_slot, c_key_base, c_key_cur, c_slot_key, c_ctr, c_comb_list, c_straus_list, c_ctab,
+    DevBuf c_key_count, c_key_rank, c_key_slot, c_key_base, c_slot_key, c_ctr, c_comb_list, c_straus_list, c_ctab,
         c_xyz, c_zpre, c_nega, c_bmid, e_ctab, e_mid, e_gcomb, e_bcomb16, e_wp, e_glist;
     // host-path mirrors of the caller's buffers
     DevBuf h_key_idx, h_msg_idx, h_sig_data, h_sig_off, h_sig_len, h_key_data, h_key_off, h_key_len, h_msg_data,
@@ -347,7 +347,7 @@ void chip_shutdown(chip_ctx* c) {
     hipSetDevice(c->device);
     hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->meta, &c->abytes, &c->edtab, &c->ectab, &c->lists, &c->counts, &c->c_key_count, &c->c_key_rank,
-                      &c->c_key_slot, &c->c_key_base, &c->c_key_cur, &c->c_slot_key, &c->c_ctr, &c->c_comb_list,
+                      &c->c_key_slot, &c->c_key_base, &c->c_slot_key, &c->c_ctr, &c->c_comb_list,
                       &c->c_straus_list, &c->c_ctab, &c->c_xyz, &c->c_zpre, &c->c_nega, &c->c_bmid, &c->e_ctab, &c->e_mid, &c->e_gcomb, &c->e_bcomb16, &c->e_wp, &c->e_glist, &c->h_key_idx, &c->h_msg_idx,
                       &c->h_sig_data, &c->h_sig_off, &c->h_sig_len, &c->h_key_data, &c->h_key_off, &c->h_key_len,
                       &c->h_msg_data, &c->h_msg_off, &c->h_msg_len, &c->h_status, &c->h_bitmap, &c->t_salts,
@@ -410,12 +410,10 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     if (comb || ec_comb) {   // per-key histogram / grouping workspace shared by both comb paths
         HIPCHK(c, c->c_key_count.ensure(nk * 4 + 16));
         HIPCHK(c, c->c_key_base.ensure(nk * 4 + 16));
-        HIPCHK(c, c->c_key_cur.ensure(nk * 4 + 16));
         HIPCHK(c, c->c_key_rank.ensure(n * 4 + 16));
         HIPCHK(c, c->c_ctr.ensure(64));
         w.key_count = c->c_key_count.as<uint32_t>();
         w.key_base = c->c_key_base.as<uint32_t>();
-        w.key_cur = c->c_key_cur.as<uint32_t>();
         w.key_rank = c->c_key_rank.as<uint32_t>();
         w.ctr = c->c_ctr.as<uint32_t>();
     }
@@ -465,7 +463,6 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     if (comb || ec_comb) {
         HIPCHK(c, hipMemsetAsync(w.ctr, 0, 64, st));
         HIPCHK(c, hipMemsetAsync(w.key_count, 0, nk * 4, st));
-        HIPCHK(c, hipMemsetAsync(w.key_cur, 0, nk * 4, st));
     }
     KeyMeta* meta = c->meta.as<KeyMeta>();
     int ke = c->kbegin(CHIP_K_KEYPREP, st);

@@ -69,7 +69,9 @@ void launch_required_signers(hipStream_t st, const chip_req_batch* q, uint64_t n
 #define ED_COMB_AWIN ((253 + ED_COMB_W - 1) / ED_COMB_W)   // W=5: 51 windows (top digit <= 8)
 #define ED_COMB_AENT ((1 << (ED_COMB_W - 1)) + 1)          // multiples 0..2^(W-1)
 #define ED_COMB_KEY_WORDS (ED_COMB_AWIN * ED_COMB_AENT * 40)
+#ifndef ED_FIN_G
 #define ED_FIN_G 16                                        // signatures per batched inversion
+#endif
 #define ED_B16_WIN 16                                      // radix-2^16 fixed-base comb of B
 #define ED_B16_CHUNKS 513                                  // 64-entry chunks per window (0..2^15)
 #define ED_B16_ENT (ED_B16_CHUNKS * 64)
@@ -78,7 +80,6 @@ struct EdCombWs {
     uint32_t* key_count;    // [n_keys] Ed25519 signatures per key needing arithmetic (k_classify)
     int32_t* key_slot;      // [n_keys] comb-table slot or -1 (Straus path)
     uint32_t* key_base;     // [n_keys] first position of the key's signatures in comb_list
-    uint32_t* key_cur;      // [n_keys] fill cursor (zeroed per batch)
     uint32_t* key_rank;     // [n] a signature's rank among its key's signatures (k_classify)
     uint32_t* slot_key;     // [max_slots]
     uint32_t* ctr;          // [0] slots claimed, [1] comb signatures, [2] Straus signatures, [4..5] ECDSA
