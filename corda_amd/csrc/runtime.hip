@@ -131,6 +131,9 @@ static int fail(chip_ctx* c, int code, const std::string& msg) {
 // is_valid = 1: Crypto.isValid (Crypto.kt:615-625) has no empty checks: an empty signature falls
 // through to the engine's decode error, empty clear data is verified as an empty message.
 #define CLASSIFY_BLOCK 1024
+#ifndef CLASSIFY_LDS_KEYS
+#define CLASSIFY_LDS_KEYS 8192   // key pools up to this size get the LDS histogram (32 KB)
+#endif
 __global__ void __launch_bounds__(CLASSIFY_BLOCK) k_classify(uint64_t n, const uint32_t* __restrict__ key_idx,
                                                   const uint32_t* __restrict__ msg_idx,
                                                   const uint32_t* __restrict__ sig_len,
@@ -161,11 +164,22 @@ __global__ void __launch_bounds__(CLASSIFY_BLOCK) k_classify(uint64_t n, const u
         if (list < 0) status[i] = st;
     }
     const uint32_t lane = threadIdx.x & 63;
-    if (key_count) {   // comb-path histogram: signatures per key (one scheme per key), one atomic per key per
-                       // wave; key_rank[i] = the signature's rank among its key's (the counting sort's slot,
-                       // so the work-list scatters need no atomics of their own)
+    // comb-path histogram: signatures per key (one scheme per key); key_rank[i] = the signature's rank
+    // among its key's (the counting sort's slot, so the work-list scatters need no atomics of their own)
+    __shared__ uint32_t s_hist[CLASSIFY_LDS_KEYS > 0 ? CLASSIFY_LDS_KEYS : 1];
+    const bool arith = list >= 0;
+    if (key_count && n_keys <= CLASSIFY_LDS_KEYS) {
+        // block-private histogram in LDS (the rank inside the block from the LDS atomic), then one
+        // global atomic per key present in the block, by the key's first signature in it
+        for (uint32_t j = threadIdx.x; j < (uint32_t)n_keys; j += blockDim.x) s_hist[j] = 0;
+        __syncthreads();
+        const uint32_t lr = arith ? atomicAdd(&s_hist[k], 1u) : 0u;
+        __syncthreads();
+        if (arith && lr == 0) s_hist[k] = atomicAdd(&key_count[k], s_hist[k]);
+        __syncthreads();
+        if (arith) key_rank[i] = s_hist[k] + lr;
+    } else if (key_count) {   // many keys: one atomic per key per wave
         uint32_t leader, cnt, rank;
-        const bool arith = list >= 0;
         wave_group(arith, k, leader, cnt, rank);
         uint32_t base = 0;
         if (arith && lane == leader) base = atomicAdd(&key_count[k], cnt);
