@@ -61,9 +61,9 @@ ED_COMB_MACS_PER_VERIFY = ED_COMB_MACS_A + ED_COMB_MACS_B          # 51,900
 #   inversion/encode)
 ED_STRAUS_MACS_PER_VERIFY = 1_262 * 55 + 1_504 * 100                # 219,810
 #   ECDSA comb (P-256 / secp256k1, 8 x 32-bit limbs): a mixed addition = 7 mults (64 products) +
-#   4 squarings (36) = 592; 22 G windows (radix 2^12) + 65 Q windows (radix 16) = 87 additions;
+#   4 squarings (36) = 592; 17 G windows (radix 2^16) + 65 Q windows (radix 16) = 82 additions;
 #   17 scalar Montgomery mults (128 each: s R, 12 wave-scan, 2 finalize, u1, u2) + the x(R) check (100)
-ECDSA_COMB_MACS_PER_VERIFY = 87 * 592 + 17 * 128 + 100              # 53,780
+ECDSA_COMB_MACS_PER_VERIFY = 82 * 592 + 17 * 128 + 100              # 50,820
 ECDSA_Q_MACS_PER_VERIFY = 65 * 592 + 100                            # k_ecdsa_comb_q: 38,580
 # SHA-256 compression, canonical 32-bit operations (rotates as one funnel shift): 64 rounds x 24
 # (Sigma1 5, Ch 3, T1 adds 4, Sigma0 5, Maj 4, 3 state adds) + 48 schedule words x 13 + 8 = 2,168
@@ -595,7 +595,7 @@ def ecdsa_leg(args, ctx, world, rank, torch, dev, dist, D, G, native, threads, s
         "ecdsa_q_kernel_ms": r1_ms + k1_ms,   # k_ecdsa_comb_q: low + high table half, both curves per launch
         "ecdsa_roofline_frac": ECDSA_COMB_MACS_PER_VERIFY * n_arith / (step_ms * 1e-3) / 1e12 / MAC_PEAK_T,
         "ecdsa_q_roofline_frac": ECDSA_Q_MACS_PER_VERIFY * n_arith / ((r1_ms + k1_ms) * 1e-3) / 1e12 / MAC_PEAK_T,
-        "ecdsa_roofline_note": "%d MACs/signature (87 mixed additions x 592 + scalar work) over the whole step; "
+        "ecdsa_roofline_note": "%d MACs/signature (82 mixed additions x 592 + scalar work) over the whole step; "
                                "q kernels %d MACs/signature over their own time" % (ECDSA_COMB_MACS_PER_VERIFY,
                                                                                     ECDSA_Q_MACS_PER_VERIFY),
     }
