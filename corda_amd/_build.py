@@ -9,7 +9,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libcordahip.so")
-SOURCES = ["runtime.hip", "ed25519.hip", "ed25519_comb.hip", "ecdsa.hip", "txid.hip", "uniq.hip", "signers.hip"]
+SOURCES = ["runtime.hip", "ed25519.hip", "ed25519_comb.hip", "ecdsa.hip", "txid.hip", "uniq.hip", "signers.hip", "kryo.hip"]
 HEADERS = ["common.hpp", "fe25519_dev.hpp", "scalar_dev.hpp", "sha2_dev.hpp", "runtime.hpp", "curve_consts.hpp",
            "ec_dev.hpp", "ed_common_dev.hpp", "comb_tables.hpp"]
 GEN = os.path.join(ROOT, "tools", "gen_constants.py")

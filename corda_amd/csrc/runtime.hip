@@ -70,6 +70,10 @@ struct chip_ctx {
     // filtered transactions: kernel scratch + staging of the host entry
     DevBuf x_scratch, x_ids, x_ghs, x_gh, x_fgs, x_fgi, x_cs, x_cd, x_co, x_cl, x_nonce, x_pts, x_ptt, x_pth, x_cv,
         x_st, x_rs;
+    // Kryo front end (kryo.hip): counts, ranges, pool, batches, key interning, scan scratch
+    DevBuf s_ncomp, s_nsig, s_nbytes, s_cstart, s_sstart, s_pstart, s_pool, s_salts, s_cgroup, s_cint, s_coff, s_clen,
+        s_txidx, s_tmpl, s_soff, s_slen, s_skoff, s_sklen, s_meta, s_tab, s_tabmin, s_kslot, s_krep, s_kflag, s_kincl,
+        s_kidx, s_koff, s_klen, s_temp;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, tev0 = nullptr, tev1 = nullptr;
     bool ev_pending = false, tev_pending = false;
     chip_stats stats{};
@@ -369,7 +373,12 @@ void chip_shutdown(chip_ctx* c) {
                       &c->t_scratch, &c->f_pool, &c->f_moff, &c->f_mlen, &c->f_midx, &c->f_htx, &c->f_htm,
                       &c->f_tdata, &c->f_toff, &c->f_tlen, &c->f_tid, &c->x_scratch, &c->x_ids, &c->x_ghs,
                       &c->x_gh, &c->x_fgs, &c->x_fgi, &c->x_cs, &c->x_cd, &c->x_co, &c->x_cl, &c->x_nonce,
-                      &c->x_pts, &c->x_ptt, &c->x_pth, &c->x_cv, &c->x_st, &c->x_rs};
+                      &c->x_pts, &c->x_ptt, &c->x_pth, &c->x_cv, &c->x_st, &c->x_rs,
+                      &c->s_ncomp, &c->s_nsig, &c->s_nbytes, &c->s_cstart, &c->s_sstart, &c->s_pstart, &c->s_pool,
+                      &c->s_salts, &c->s_cgroup, &c->s_cint, &c->s_coff, &c->s_clen, &c->s_txidx, &c->s_tmpl,
+                      &c->s_soff, &c->s_slen, &c->s_skoff, &c->s_sklen, &c->s_meta, &c->s_tab, &c->s_tabmin,
+                      &c->s_kslot, &c->s_krep, &c->s_kflag, &c->s_kincl, &c->s_kidx, &c->s_koff, &c->s_klen,
+                      &c->s_temp};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < chip_ctx::KRING; i++) {
         if (c->kring[i].a) hipEventDestroy(c->kring[i].a);
@@ -708,6 +717,144 @@ int chip_alloc_pinned(uint64_t bytes, void** out) {
 }
 void chip_free_pinned(void* p) {
     if (p) (void)hipHostFree(p);
+}
+
+// ---------------------------------------------------------------------------------------
+// Kryo front end (cordahip.h chip_stx_parse_device; kernels in kryo.hip)
+int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_status, chip_stx_parsed* out,
+                          void* stream) {
+    if (!c || !in || !out) return fail(c, CHIP_E_ARG, "null argument");
+    const uint64_t n = in->n;
+    if (n && (!in->data || !in->off || !in->len || !tx_status)) return fail(c, CHIP_E_ARG, "null blob array");
+    if (in->n_meta && !in->meta) return fail(c, CHIP_E_ARG, "null meta");
+    if (n >= (1ull << 31)) return fail(c, CHIP_E_ARG, "too many blobs");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
+    std::memset(out, 0, sizeof(*out));
+    const uint64_t n1 = n + 1;
+    HIPCHK(c, c->s_ncomp.ensure(n1 * 8));
+    HIPCHK(c, c->s_nsig.ensure(n1 * 8));
+    HIPCHK(c, c->s_nbytes.ensure(n1 * 8));
+    HIPCHK(c, c->s_cstart.ensure(n1 * 8));
+    HIPCHK(c, c->s_sstart.ensure(n1 * 8));
+    HIPCHK(c, c->s_pstart.ensure(n1 * 8));
+    HIPCHK(c, c->s_salts.ensure(n * 32 + 16));
+    const size_t temp = stx_scan_temp_bytes(n1 > 2 ? n1 : 2);
+    HIPCHK(c, c->s_temp.ensure(temp));
+    // pass 1: validate + count; ranges = inclusive scans written one past a zero
+    const int kc = c->kbegin(CHIP_K_STX, st);
+    launch_stx_count(st, in, tx_status, c->s_ncomp.as<uint64_t>(), c->s_nsig.as<uint64_t>(), c->s_nbytes.as<uint64_t>());
+    HIPCHK(c, hipGetLastError());
+    DevBuf* cnt[3] = {&c->s_ncomp, &c->s_nsig, &c->s_nbytes};
+    DevBuf* rng[3] = {&c->s_cstart, &c->s_sstart, &c->s_pstart};
+    for (int k = 0; k < 3; k++) {
+        HIPCHK(c, hipMemsetAsync(rng[k]->p, 0, 8, st));
+        if (n) HIPCHK(c, stx_scan_u64(st, c->s_temp.p, c->s_temp.cap, cnt[k]->as<uint64_t>(), rng[k]->as<uint64_t>() + 1, n));
+    }
+    uint64_t tot[3] = {0, 0, 0};
+    for (int k = 0; k < 3; k++)
+        HIPCHK(c, hipMemcpyAsync(&tot[k], rng[k]->as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    const uint64_t ncomp = tot[0], nsig = tot[1], pool = tot[2];
+    if (nsig >= (1ull << 31)) return fail(c, CHIP_E_ARG, "too many signatures");
+    HIPCHK(c, c->s_pool.ensure(pool + 16));
+    HIPCHK(c, c->s_cgroup.ensure(ncomp * 4 + 16));
+    HIPCHK(c, c->s_cint.ensure(ncomp * 4 + 16));
+    HIPCHK(c, c->s_coff.ensure(ncomp * 8 + 16));
+    HIPCHK(c, c->s_clen.ensure(ncomp * 4 + 16));
+    HIPCHK(c, c->s_txidx.ensure(nsig * 4 + 16));
+    HIPCHK(c, c->s_tmpl.ensure(nsig * 4 + 16));
+    HIPCHK(c, c->s_soff.ensure(nsig * 8 + 16));
+    HIPCHK(c, c->s_slen.ensure(nsig * 4 + 16));
+    HIPCHK(c, c->s_skoff.ensure(nsig * 8 + 16));
+    HIPCHK(c, c->s_sklen.ensure(nsig * 4 + 16));
+    HIPCHK(c, c->s_meta.ensure((uint64_t)in->n_meta * 8 + 16));
+    uint64_t cap = 1024;
+    while (cap < 2 * nsig) cap <<= 1;
+    HIPCHK(c, c->s_tab.ensure(cap * 8));
+    HIPCHK(c, c->s_tabmin.ensure(cap * 4));
+    for (DevBuf* b : {&c->s_kslot, &c->s_krep, &c->s_kflag, &c->s_kincl, &c->s_kidx, &c->s_klen})
+        HIPCHK(c, b->ensure(nsig * 4 + 16));
+    HIPCHK(c, c->s_koff.ensure(nsig * 8 + 16));
+    if (stx_scan_temp_bytes(nsig > 2 ? nsig : 2) > c->s_temp.cap)
+        HIPCHK(c, c->s_temp.ensure(stx_scan_temp_bytes(nsig > 2 ? nsig : 2)));
+    if (in->n_meta)
+        HIPCHK(c, hipMemcpyAsync(c->s_meta.p, in->meta, (uint64_t)in->n_meta * 8, hipMemcpyHostToDevice, st));
+    StxOut d{};
+    d.pool = c->s_pool.as<uint8_t>();
+    d.pool_start = c->s_pstart.as<uint64_t>();
+    d.salts = c->s_salts.as<uint8_t>();
+    d.comp_start = c->s_cstart.as<uint64_t>();
+    d.comp_group = c->s_cgroup.as<uint32_t>();
+    d.comp_internal = c->s_cint.as<uint32_t>();
+    d.comp_len = c->s_clen.as<uint32_t>();
+    d.comp_off = c->s_coff.as<uint64_t>();
+    d.sig_start = c->s_sstart.as<uint64_t>();
+    d.tx_idx = c->s_txidx.as<uint32_t>();
+    d.tmpl_idx = c->s_tmpl.as<uint32_t>();
+    d.sig_len = c->s_slen.as<uint32_t>();
+    d.skey_len = c->s_sklen.as<uint32_t>();
+    d.sig_off = c->s_soff.as<uint64_t>();
+    d.skey_off = c->s_skoff.as<uint64_t>();
+    d.meta = c->s_meta.as<int32_t>();
+    d.n_meta = in->n_meta;
+    d.tab = c->s_tab.as<uint64_t>();
+    d.tab_min = c->s_tabmin.as<uint32_t>();
+    d.kslot = c->s_kslot.as<uint32_t>();
+    d.krep = c->s_krep.as<uint32_t>();
+    d.kflag = c->s_kflag.as<uint32_t>();
+    d.kincl = c->s_kincl.as<uint32_t>();
+    d.key_idx = c->s_kidx.as<uint32_t>();
+    d.key_off = c->s_koff.as<uint64_t>();
+    d.key_len = c->s_klen.as<uint32_t>();
+    // pass 2: the batches; then the signer keys interned
+    launch_stx_emit(st, in, tx_status, d);
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemsetAsync(c->s_tab.p, 0, cap * 8, st));
+    HIPCHK(c, hipMemsetAsync(c->s_tabmin.p, 0xff, cap * 4, st));
+    launch_stx_keys(st, nsig, d, cap - 1, c->s_temp.p, c->s_temp.cap);
+    HIPCHK(c, hipGetLastError());
+    uint32_t nkeys = 0;
+    if (nsig) HIPCHK(c, hipMemcpyAsync(&nkeys, c->s_kincl.as<uint32_t>() + nsig - 1, 4, hipMemcpyDeviceToHost, st));
+    c->kend(kc, st);
+    HIPCHK(c, hipStreamSynchronize(st));
+    chip_tx_batch& t = out->txs;
+    t.ntx = n;
+    t.salts = d.salts;
+    t.tx_comp_start = d.comp_start;
+    t.ncomp = ncomp;
+    t.comp_group = d.comp_group;
+    t.comp_internal = d.comp_internal;
+    t.data = d.pool;
+    t.comp_off = d.comp_off;
+    t.comp_len = d.comp_len;
+    t.data_bytes = pool;
+    chip_signer_batch& s = out->sigs;
+    s.n = nsig;
+    s.tx_idx = d.tx_idx;
+    s.tmpl_idx = d.tmpl_idx;
+    s.key_idx = d.key_idx;
+    s.sig_data = d.pool;
+    s.sig_off = d.sig_off;
+    s.sig_len = d.sig_len;
+    s.n_keys = nkeys;
+    s.key_data = d.pool;
+    s.key_off = d.key_off;
+    s.key_len = d.key_len;
+    s.sig_bytes = pool;
+    s.key_bytes = pool;
+    out->sig_start = d.sig_start;
+    return CHIP_OK;
+}
+
+int chip_copy_to_host(chip_ctx* c, void* dst, const void* src, uint64_t bytes) {
+    if (!c || (bytes && (!dst || !src))) return fail(c, CHIP_E_ARG, "null argument");
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, hipStreamSynchronize(c->stream));
+    if (bytes) HIPCHK(c, hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return CHIP_OK;
 }
 
 int chip_get_stats(const chip_ctx* cc, chip_stats* out) {

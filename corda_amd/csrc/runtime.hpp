@@ -57,6 +57,33 @@ void launch_required_signers(hipStream_t st, const chip_req_batch* q, uint64_t n
                              const uint32_t* key_len, uint64_t key_bytes, const uint8_t* status, uint8_t* verdict,
                              uint32_t* arg, uint8_t* missing);
 
+// Kryo front end (kryo.hip): SignedTransaction bytes -> tx / signer batches in the context's buffers
+struct StxOut {
+    uint8_t* pool;                 // de-chunked payload: components, signature bytes, signer keys
+    const uint64_t* pool_start;    // [n + 1] region of blob t in the pool
+    uint8_t* salts;                // [n * 32]
+    const uint64_t* comp_start;    // [n + 1]
+    uint32_t *comp_group, *comp_internal, *comp_len;
+    uint64_t* comp_off;
+    const uint64_t* sig_start;     // [n + 1]
+    uint32_t *tx_idx, *tmpl_idx, *sig_len, *skey_len;
+    uint64_t *sig_off, *skey_off;  // per signature: its bytes and its signer's key bytes in the pool
+    const int32_t* meta;           // [2 * n_meta] (platformVersion, schemeNumberID) per template
+    uint32_t n_meta;
+    // key interning
+    uint64_t* tab;
+    uint32_t *tab_min, *kslot, *krep, *kflag, *kincl;
+    uint32_t* key_idx;             // [nsig] into the de-duplicated key pool
+    uint64_t* key_off;             // [n_keys]
+    uint32_t* key_len;
+};
+void launch_stx_count(hipStream_t st, const chip_stx_blobs* in, uint8_t* status, uint64_t* ncomp, uint64_t* nsig,
+                      uint64_t* nbytes);
+void launch_stx_emit(hipStream_t st, const chip_stx_blobs* in, uint8_t* status, const StxOut& d);
+size_t stx_scan_temp_bytes(uint64_t n);
+hipError_t stx_scan_u64(hipStream_t st, void* temp, size_t temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n);
+void launch_stx_keys(hipStream_t st, uint64_t nsig, const StxOut& d, uint64_t mask, void* temp, size_t temp_bytes);
+
 // sizes of the per-key device tables (words per key)
 #define ED_KEY_TABLE_WORDS (9 * 40)
 #define EC_KEY_TABLE_WORDS (9 * 16 + 16)

@@ -1,55 +1,92 @@
-"""Kryo 4.0.0 wire format, restated for the bytes the signature path signs.
+"""Kryo 4.0.0 wire format, restated for the bytes on the signature path.
 
-The signed message of every transaction signature is `SignableData(txId, signatureMetadata)
-.serialize().bytes` (Crypto.kt:550-578 -> SerializationAPI.kt:193), produced on a node by the Kryo
-P2P context (Node.kt:372: SerializationDefaults.P2P_CONTEXT = KRYO_P2P_CONTEXT).  This module writes
-and reads those bytes without a JVM, from the published Kryo 4.0.0 algorithms as Corda configures
-them (node-api/build.gradle:25 pins Kryo 4.0.0):
+Two uses:
+  * the signed message of every transaction signature, `SignableData(txId, signatureMetadata)
+    .serialize().bytes` (Crypto.kt:550-578 -> SerializationAPI.kt:193);
+  * the front end of a batch: `SignedTransaction` / `WireTransaction` bytes as nodes store and send
+    them (Kryo.kt:236-280 serializers), parsed into component groups and signatures.  The product
+    parser is the device kernel (corda_amd/csrc/kryo.hip, chip_stx_parse_device); the reader here is
+    its host mirror and the writer builds the test and bench inputs.
+
+Both are produced on a node by the Kryo P2P context (Node.kt:372: SerializationDefaults.P2P_CONTEXT =
+KRYO_P2P_CONTEXT, references on) from the published Kryo 4.0.0 algorithms as Corda configures them
+(node-api/build.gradle:25 pins Kryo 4.0.0):
 
   header      "corda" 00 00 01                                    SerializationScheme.kt:251 (KryoHeaderV0_1)
   object      kryo.writeClassAndObject(output, obj)               SerializationScheme.kt:218-239
-  class       unregistered @CordaSerializable classes are registered implicitly by NAME
-              (CordaClassResolver.registerImplicit, CordaClassResolver.kt:76-99):
-              varint(NAME + 2 = 1), varint(name id), name string the first time per graph, just the
-              id afterwards (Kryo DefaultClassResolver.writeName; ids restart every graph)
-  reference   references on (KRYO_P2P_CONTEXT objectReferencesEnabled = true; MapReferenceResolver):
-              a first-seen object is preceded by varint(NOT_NULL = 1)
-  serializer  default CompatibleFieldSerializer with CachedFieldNameStrategy.EXTENDED
+  class       registered classes as varint(id + 2).  The Kryo constructor registers 10 primitives
+              (ids 0-9); DefaultKryoCustomizer.kt:76-79 then registers Arrays$ArrayList (10),
+              SignedTransaction (11), WireTransaction (12), SerializedBytes (13).  Later
+              registrations (PrivacySalt, the PublicKey classes, DefaultKryoCustomizer.kt:86-112)
+              follow a library-dependent number of javakaffee / Guava registrations (:80-85), so
+              their ids are NOT pinned here: readers accept any registered id >= 14 where the
+              position fixes the meaning; writers take the ids as parameters.
+              Unregistered @CordaSerializable / whitelisted classes are registered implicitly by
+              NAME (CordaClassResolver.registerImplicit, CordaClassResolver.kt:76-99): varint(1),
+              varint(name id), the name string the first time per graph (ids restart every graph)
+  reference   references on (MapReferenceResolver): a first-seen object written through
+              writeClassAndObject / writeObject(OrNull) is preceded by varint(NOT_NULL = 1).
+              WireTransaction's serializer runs with references off (noReferencesWithin,
+              DefaultKryoCustomizer.kt:88, Kryo.kt:425-437): no markers inside it
+  serializer  default CompatibleFieldSerializer, CachedFieldNameStrategy.EXTENDED
               (DefaultKryoCustomizer.kt:59-62): the first time a class is written in a graph,
               varint(field count) + every cached field name ("DeclaringSimpleName.field", sorted);
-              then each field's bytes through one OutputChunked(1024): varint(chunk length), bytes,
-              and a 0 end marker per field
-  fields      int: zig-zag varint (CachedField.varIntsEnabled); byte[]: varint(length + 1) + bytes
-              (DefaultArraySerializers.ByteArraySerializer); a field of a final class (Kotlin
-              classes are final) writes reference + object; of an abstract type (SecureHash is
-              sealed) writes the concrete class first
+              then each field through ONE OutputChunked(output, 1024) and endChunks() per field
+  chunks      OutputChunked flushes a chunk (varint size + bytes, size > 0) when its 1024-byte buffer
+              cannot take the next primitive (Output.require: a varint / byte never straddles a
+              chunk, writeBytes fills the buffer first), and at endChunks, then writes the 0 end
+              marker.  Output.flush also flushes the stream it writes to, so a nested
+              CompatibleFieldSerializer (a field value with its own chunked fields) makes the
+              enclosing field emit a chunk at every inner chunk: the writer below simulates the
+              Output / OutputChunked buffers exactly instead of chunking flat byte strings
+  fields      int: zig-zag varint (varIntsEnabled); byte[] field (final type): reference marker +
+              varint(length + 1) + bytes (ByteArraySerializer); a field of a final class writes the
+              reference marker + object; of an abstract / interface type (SecureHash, PublicKey,
+              List) the concrete class first
   strings     Output.writeString: ASCII with 1 < length < 64 -> the bytes with bit 7 set on the last;
               otherwise varint(UTF-16 length + 1) with bit 7 of the first byte set, then UTF-8
+  lists       ArrayList: CollectionSerializer, varint(size) + writeClassAndObject per element;
+              Collections$SingletonList: writeClassAndObject(element); Arrays$ArrayList (id 10,
+              javakaffee ArraysAsListSerializer): varint(size), the component class, elements
 
-SignableData (SignableData.kt:12-13) has fields signatureMetadata (SignatureMetadata.kt:14-15: two
-ints) and txId (SecureHash.SHA256 -> OpaqueBytes.bytes, ByteArrays.kt:121).  For one metadata value
-the serialized form is a fixed byte string with the 32-byte id at a fixed offset, which is what the
-fused tx-verify kernel (chip_verify_tx_batch templates) relies on.
-
-PARITY UNPINNED: the reference holds no serialized SignableData bytes and no JVM runs here, so these
-bytes follow the Kryo 4.0.0 source semantics as restated above; tests pin only self-consistency
-(write -> read round trips, template offsets, field order).
+PARITY UNPINNED: the reference holds no serialized bytes and no JVM runs here, so these bytes follow
+the Kryo 4.0.0 source semantics as restated above; tests pin self-consistency (write -> read round
+trips, Python == C++ == the device parser, template offsets, chunk placement rules).
 """
 from __future__ import annotations
 
-from typing import Dict, List, Tuple
+from typing import Callable, Dict, List, Optional, Sequence, Tuple
 
 KRYO_HEADER_V0_1 = b"corda\x00\x00\x01"
 NULL, NOT_NULL, NAME = 0, 1, -1
 CHUNK = 1024
 
+# registration ids pinned by DefaultKryoCustomizer.kt:76-79 (after the Kryo constructor's 0-9)
+REG_ARRAYS_ASLIST, REG_SIGNED_TX, REG_WIRE_TX, REG_SERIALIZED_BYTES = 10, 11, 12, 13
+FIRST_UNPINNED_ID = 14
+# NOT pinned (library-dependent): placeholders the writers use by default; readers accept any id >= 14
+DEFAULT_IDS = {"privacy_salt": 47, "eddsa_public_key": 31, "bcec_public_key": 42, "composite_key": 33}
+
 SIGNABLE_DATA = "net.corda.core.crypto.SignableData"
 SECURE_HASH_SHA256 = "net.corda.core.crypto.SecureHash$SHA256"
 SIGNATURE_METADATA = "net.corda.core.crypto.SignatureMetadata"
+TRANSACTION_SIGNATURE = "net.corda.core.crypto.TransactionSignature"
+COMPONENT_GROUP = "net.corda.core.transactions.ComponentGroup"
+ARRAY_LIST = "java.util.ArrayList"
+SINGLETON_LIST = "java.util.Collections$SingletonList"
+
+TXSIG_FIELDS = ["OpaqueBytes.bytes", "TransactionSignature.by", "TransactionSignature.signatureMetadata"]
+META_FIELDS = ["SignatureMetadata.platformVersion", "SignatureMetadata.schemeNumberID"]
+GROUP_FIELDS = ["ComponentGroup.components", "ComponentGroup.groupIndex"]
 
 
 class KryoException(Exception):
     pass
+
+
+class KryoUnsupported(KryoException):
+    """Well-formed input outside the front end's grammar (device status CHIP_STX_UNSUPPORTED): the
+    caller verifies that transaction on the JVM path."""
 
 
 # ---- primitives (com.esotericsoftware.kryo.io.Output) ----
@@ -93,70 +130,162 @@ def string(s: str) -> bytes:
     return bytes(head) + s.encode("utf-8")
 
 
-class Graph:
-    """Per-graph state of one writeClassAndObject call: class-name ids and the classes whose
-    CompatibleFieldSerializer field-name header is already out (both reset per graph)."""
+def chunked(data: bytes) -> bytes:
+    """One OutputChunked(1024) field holding `data` written with writeBytes, then endChunks(), over a
+    plain (non-chunked) output: chunks of 1024 bytes, the rest, the 0 end marker."""
+    o = Out()
+    c = Out(o)
+    c.write_bytes(data)
+    c.end_chunks()
+    return o.getvalue()
 
-    def __init__(self):
+
+class Out:
+    """Kryo 4.0.0 Output / OutputChunked.  parent None = the top-level Output (its 64 KB buffer and
+    ByteArrayOutputStream never change the bytes: modelled as unbounded); otherwise an
+    OutputChunked(parent, 1024) whose OutputStream is the parent Output."""
+
+    def __init__(self, parent: Optional["Out"] = None):
+        self.parent = parent
+        self.cap = CHUNK if parent is not None else None
+        self.buf = bytearray()
+
+    def getvalue(self) -> bytes:
+        return bytes(self.buf)
+
+    def _require(self, n: int):       # Output.require: flush when the buffer cannot take n more
+        if self.cap is not None and self.cap - len(self.buf) < n:
+            self.flush()
+
+    def write_byte(self, b: int):      # Output.write(int) / writeByte
+        if self.cap is not None and len(self.buf) == self.cap:
+            self._require(1)
+        self.buf.append(b & 0xFF)
+
+    def write_varint(self, v: int, optimize_positive: bool = True):
+        enc = varint(v, optimize_positive)
+        self._require(len(enc))
+        self.buf += enc
+
+    def write_bytes(self, data: bytes):   # Output.writeBytes: fill the buffer, then whole buffers
+        data = bytes(data)
+        if self.cap is None:
+            self.buf += data
+            return
+        i, n = 0, len(data)
+        k = min(self.cap - len(self.buf), n)
+        while True:
+            self.buf += data[i:i + k]
+            i += k
+            if i == n:
+                return
+            k = min(self.cap, n - i)
+            self._require(k)
+
+    def write_string(self, s: str):
+        enc = string(s)
+        if len(enc) == len(s) and len(s) > 1:   # ASCII path: bytes (slow path = writeBytes), flag last
+            self.write_bytes(enc[:-1] + bytes([enc[-1] & 0x7F]))
+            self.buf[-1] |= 0x80
+        else:
+            for b in enc:
+                self.write_byte(b)
+
+    def flush(self):                   # OutputChunked.flush -> Output.flush -> parent.flush
+        if self.parent is None:
+            return
+        if self.buf:
+            for b in varint(len(self.buf)):   # writeChunkSize: outputStream.write(int) per byte
+                self.parent.write_byte(b)
+            self.parent.write_bytes(bytes(self.buf))
+            self.buf.clear()
+        self.parent.flush()
+
+    def end_chunks(self):
+        self.flush()
+        self.parent.write_byte(0)
+
+
+class Graph:
+    """Per-graph state of one top-level writeClassAndObject: class-name ids, the classes whose
+    CompatibleFieldSerializer field-name header is already out, and whether references are on."""
+
+    def __init__(self, references: bool = True):
         self.name_ids: Dict[str, int] = {}
         self.headers: set = set()
+        self.references = references
 
-    def write_class(self, name: str) -> bytes:
-        if name in self.name_ids:
-            return varint(NAME + 2) + varint(self.name_ids[name])
+    def write_class(self, o: Out, cls) -> None:
+        """DefaultClassResolver.writeClass: int = registered id, str = written by NAME."""
+        if isinstance(cls, int):
+            o.write_varint(cls + 2)
+            return
+        o.write_varint(NAME + 2)
+        if cls in self.name_ids:
+            o.write_varint(self.name_ids[cls])
+            return
         nid = len(self.name_ids)
-        self.name_ids[name] = nid
-        return varint(NAME + 2) + varint(nid) + string(name)
+        self.name_ids[cls] = nid
+        o.write_varint(nid)
+        o.write_string(cls)
 
-    def compatible(self, cls: str, fields: List[Tuple[str, bytes]]) -> bytes:
-        """CompatibleFieldSerializer.write: fields = [(cached name, field bytes)], sorted here by
-        cached name (FieldSerializer orders its CachedFields by name)."""
+    def marker(self, o: Out) -> None:
+        """writeReferenceOrNull for a first-seen object (references on only)."""
+        if self.references:
+            o.write_varint(NOT_NULL)
+
+    def compatible(self, o: Out, cls: str, fields: List[Tuple[str, Callable[[Out], None]]]) -> None:
+        """CompatibleFieldSerializer.write: fields = [(cached name, writer)], in cached-name order."""
         fields = sorted(fields, key=lambda f: f[0])
-        out = bytearray()
         if cls not in self.headers:
             self.headers.add(cls)
-            out += varint(len(fields))
+            o.write_varint(len(fields))
             for name, _ in fields:
-                out += string(name)
-        for _, data in fields:
-            out += chunked(data)
-        return bytes(out)
-
-
-def chunked(data: bytes) -> bytes:
-    """OutputChunked(output, 1024) for one field then endChunks(): chunks of at most 1024 bytes,
-    each prefixed by its varint length, then a 0 end marker."""
-    out = bytearray()
-    for i in range(0, len(data), CHUNK):
-        part = data[i:i + CHUNK]
-        out += varint(len(part)) + part
-    out.append(0)
-    return bytes(out)
+                o.write_string(name)
+        c = Out(o)
+        for _, fn in fields:
+            fn(c)
+            c.end_chunks()
 
 
 # ---- SignableData ----
-def _sha256_object(g: Graph, tx_id: bytes) -> bytes:
-    if len(tx_id) != 32:   # SecureHash.SHA256 init { require(bytes.size == 32) }
-        raise KryoException("SecureHash.SHA256 needs 32 bytes")
-    arr = varint(NOT_NULL) + varint(len(tx_id) + 1) + bytes(tx_id)
-    return (g.write_class(SECURE_HASH_SHA256) + varint(NOT_NULL)
-            + g.compatible(SECURE_HASH_SHA256, [("OpaqueBytes.bytes", arr)]))
+def _bytes_field(g: Graph, data: bytes) -> Callable[[Out], None]:
+    def w(o: Out):
+        g.marker(o)                              # writeObjectOrNull of a final byte[] field
+        o.write_varint(len(data) + 1)            # ByteArraySerializer: length + 1 (0 = null)
+        o.write_bytes(data)
+    return w
 
 
-def _metadata_object(g: Graph, platform_version: int, scheme_number_id: int) -> bytes:
-    return varint(NOT_NULL) + g.compatible(SIGNATURE_METADATA, [
-        ("SignatureMetadata.platformVersion", varint(platform_version, False)),
-        ("SignatureMetadata.schemeNumberID", varint(scheme_number_id, False))])
+def _metadata_field(g: Graph, platform_version: int, scheme_number_id: int) -> Callable[[Out], None]:
+    def w(o: Out):
+        g.marker(o)                              # SignatureMetadata is final: marker + object
+        g.compatible(o, SIGNATURE_METADATA, [
+            ("SignatureMetadata.platformVersion", lambda c: c.write_varint(platform_version, False)),
+            ("SignatureMetadata.schemeNumberID", lambda c: c.write_varint(scheme_number_id, False))])
+    return w
 
 
 def signable_data(tx_id: bytes, platform_version: int, scheme_number_id: int) -> bytes:
     """SignableData(SecureHash.SHA256(tx_id), SignatureMetadata(platformVersion, schemeNumberID))
     .serialize().bytes under the Kryo P2P context."""
+    if len(tx_id) != 32:   # SecureHash.SHA256 init { require(bytes.size == 32) }
+        raise KryoException("SecureHash.SHA256 needs 32 bytes")
     g = Graph()
-    body = g.write_class(SIGNABLE_DATA) + varint(NOT_NULL) + g.compatible(SIGNABLE_DATA, [
-        ("SignableData.signatureMetadata", _metadata_object(g, platform_version, scheme_number_id)),
-        ("SignableData.txId", _sha256_object(g, tx_id))])
-    return KRYO_HEADER_V0_1 + body
+    o = Out()
+    o.write_bytes(KRYO_HEADER_V0_1)
+    g.write_class(o, SIGNABLE_DATA)
+    g.marker(o)
+
+    def tx_field(c: Out):                        # SecureHash is sealed (abstract): class first
+        g.write_class(c, SECURE_HASH_SHA256)
+        g.marker(c)
+        g.compatible(c, SECURE_HASH_SHA256, [("OpaqueBytes.bytes", _bytes_field(g, tx_id))])
+
+    g.compatible(o, SIGNABLE_DATA, [
+        ("SignableData.signatureMetadata", _metadata_field(g, platform_version, scheme_number_id)),
+        ("SignableData.txId", tx_field)])
+    return o.getvalue()
 
 
 def signable_data_template(platform_version: int, scheme_number_id: int) -> Tuple[bytes, int]:
@@ -170,20 +299,141 @@ def signable_data_template(platform_version: int, scheme_number_id: int) -> Tupl
     return a[:at] + a[at + 32:], at
 
 
-# ---- reader (front end: SignableData bytes -> (txId, platformVersion, schemeNumberID)) ----
+# ---- WireTransaction / SignedTransaction (Kryo.kt:236-280) ----
+def _list(g: Graph, o: Out, items: Sequence, write_item: Callable[[Out, object], None], kind: str = "auto"):
+    """writeClassAndObject(list): kind 'array' = ArrayList, 'single' = Collections$SingletonList,
+    ('aslist', component class) = Arrays$ArrayList (listOf(a, b)); 'auto': singleton for one element
+    (listOf(x)), else ArrayList (mutableListOf / map / plus)."""
+    if kind == "auto":
+        kind = "single" if len(items) == 1 else "array"
+    if kind == "single":
+        assert len(items) == 1
+        g.write_class(o, SINGLETON_LIST)
+        g.marker(o)
+        write_item(o, items[0])                  # CollectionsSingletonListSerializer
+    elif isinstance(kind, tuple) and kind[0] == "aslist":
+        g.write_class(o, REG_ARRAYS_ASLIST)      # ArraysAsListSerializer: size, component class, elements
+        g.marker(o)
+        o.write_varint(len(items))
+        g.write_class(o, kind[1])
+        for it in items:
+            write_item(o, it)
+    else:
+        g.write_class(o, ARRAY_LIST)
+        g.marker(o)
+        o.write_varint(len(items))               # CollectionSerializer: size, then class + object
+        for it in items:
+            write_item(o, it)
+
+
+def wire_transaction(groups: Sequence[Tuple[int, Sequence[bytes]]], salt: bytes,
+                     privacy_salt_id: int = DEFAULT_IDS["privacy_salt"], list_kinds: Optional[Dict] = None) -> bytes:
+    """WireTransaction(componentGroups, privacySalt).serialize().bytes: groups = [(groupIndex,
+    [component bytes = SerializedBytes of the component]), ...] in list order (createComponentGroups,
+    WireTransaction.kt:207-221).  list_kinds optionally forces the list class per group index
+    ('array' / 'single'); -1 = the componentGroups list itself."""
+    kinds = list_kinds or {}
+    g = Graph()
+    o = Out()
+    o.write_bytes(KRYO_HEADER_V0_1)
+    g.write_class(o, REG_WIRE_TX)
+    g.marker(o)                                  # references are still on for the top object
+    g.references = False                         # NoReferencesSerializer (Kryo.kt:429-437)
+
+    def ser_bytes(c: Out, b):                    # element: SerializedBytes, SerializedBytesSerializer
+        g.write_class(c, REG_SERIALIZED_BYTES)
+        g.marker(c)
+        c.write_varint(len(b))
+        c.write_bytes(b)
+
+    def group(c: Out, gi_comps):
+        gi, comps = gi_comps
+        g.write_class(c, COMPONENT_GROUP)
+        g.marker(c)
+        g.compatible(c, COMPONENT_GROUP, [
+            ("ComponentGroup.components", lambda f: _list(g, f, list(comps), ser_bytes, kinds.get(gi, "auto"))),
+            ("ComponentGroup.groupIndex", lambda f: f.write_varint(gi, False))])
+
+    _list(g, o, list(groups), group, kinds.get(-1, "array"))
+    if len(salt) != 32:
+        raise KryoException("Privacy salt should be 32 bytes.")
+    g.write_class(o, privacy_salt_id)            # PrivacySaltSerializer: writeBytesWithLength
+    o.write_varint(32)
+    o.write_bytes(salt)
+    return o.getvalue()
+
+
+class Sig:
+    """A TransactionSignature as the front end sees it."""
+
+    def __init__(self, sig: bytes, key: bytes, platform_version: int = 1, scheme_number_id: int = 4,
+                 key_class_id: Optional[int] = None):
+        self.sig, self.key = bytes(sig), bytes(key)
+        self.platform_version, self.scheme_number_id = platform_version, scheme_number_id
+        self.key_class_id = key_class_id
+
+    def tuple(self):
+        return (self.sig, self.key, self.platform_version, self.scheme_number_id)
+
+
+def signed_transaction(tx_bits: bytes, sigs: Sequence[Sig], list_kind: str = "auto") -> bytes:
+    """SignedTransaction(txBits, sigs).serialize().bytes (SignedTransactionSerializer, Kryo.kt:266-280)."""
+    g = Graph()
+    o = Out()
+    o.write_bytes(KRYO_HEADER_V0_1)
+    g.write_class(o, REG_SIGNED_TX)
+    g.marker(o)
+    g.write_class(o, REG_SERIALIZED_BYTES)       # txBits
+    g.marker(o)
+    o.write_varint(len(tx_bits))
+    o.write_bytes(tx_bits)
+
+    def txsig(c: Out, s: Sig):
+        g.write_class(c, TRANSACTION_SIGNATURE)
+        g.marker(c)
+
+        def by(f: Out):                          # PublicKey (interface): class, marker, PublicKeySerializer
+            kid = s.key_class_id if s.key_class_id is not None else DEFAULT_IDS["eddsa_public_key"]
+            g.write_class(f, kid)
+            g.marker(f)
+            f.write_varint(len(s.key))
+            f.write_bytes(s.key)
+
+        g.compatible(c, TRANSACTION_SIGNATURE, [
+            ("OpaqueBytes.bytes", _bytes_field(g, s.sig)),
+            ("TransactionSignature.by", by),
+            ("TransactionSignature.signatureMetadata", _metadata_field(g, s.platform_version, s.scheme_number_id))])
+
+    _list(g, o, list(sigs), txsig, list_kind)
+    return o.getvalue()
+
+
+# ---- reader (host mirror of the device front end) ----
 class Reader:
-    def __init__(self, buf: bytes, pos: int = 0):
+    """Input / InputChunked over one graph: chunk() returns the de-chunked bytes of one field as a
+    reader sharing the graph's name ids and headers (InputChunked.nextChunks semantics: unread
+    bytes of a field are skipped)."""
+
+    def __init__(self, buf: bytes, pos: int = 0, end: Optional[int] = None):
         self.buf = buf
         self.pos = pos
+        self.end = len(buf) if end is None else end
         self.names: Dict[int, str] = {}
         self.headers: Dict[str, List[str]] = {}
 
     def byte(self) -> int:
-        if self.pos >= len(self.buf):
+        if self.pos >= self.end:
             raise KryoException("buffer underflow")
         b = self.buf[self.pos]
         self.pos += 1
         return b
+
+    def take(self, n: int) -> bytes:
+        if n < 0 or self.pos + n > self.end:
+            raise KryoException("buffer underflow")
+        b = self.buf[self.pos:self.pos + n]
+        self.pos += n
+        return bytes(b)
 
     def varint(self, optimize_positive: bool = True) -> int:
         v, shift = 0, 0
@@ -193,8 +443,10 @@ class Reader:
             shift += 7
             if not b & 0x80:
                 break
-            if shift > 35:
-                raise KryoException("malformed varint")
+            if shift > 28:
+                b = self.byte()
+                v |= (b & 0x7F) << shift
+                break
         v &= 0xFFFFFFFF
         if not optimize_positive:
             v = (v >> 1) ^ -(v & 1)
@@ -222,22 +474,27 @@ class Reader:
         if v == 0:
             raise KryoException("null string")
         n = v - 1
-        s = self.buf[self.pos:].decode("utf-8", errors="strict")[:n]
+        s = bytes(self.buf[self.pos:self.end]).decode("utf-8", errors="strict")[:n]
         self.pos += len(s.encode("utf-8"))
         return s
 
-    def read_class(self) -> str:
+    def read_class(self):
+        """-> registered id (int) or class name (str); None for a null."""
         tag = self.varint()
+        if tag == NULL:
+            return None
         if tag != NAME + 2:
-            raise KryoException("expected a class written by name, got registration id %d" % (tag - 2))
+            return tag - 2
         nid = self.varint()
         if nid not in self.names:
+            if nid != len(self.names) or nid >= 8:     # the device keeps 8 name ids per graph
+                raise KryoUnsupported("class name id %d" % nid)
             self.names[nid] = self.string()
         return self.names[nid]
 
     def not_null(self):
         if self.varint() != NOT_NULL:
-            raise KryoException("expected a first-seen object")
+            raise KryoUnsupported("expected a first-seen object (back-references / null unsupported)")
 
     def field_names(self, cls: str) -> List[str]:
         if cls not in self.headers:
@@ -250,45 +507,199 @@ class Reader:
             n = self.varint()
             if n == 0:
                 break
-            data += self.buf[self.pos:self.pos + n]
-            if self.pos + n > len(self.buf):
-                raise KryoException("truncated chunk")
-            self.pos += n
+            data += self.take(n)
         r = Reader(bytes(data))
         r.names, r.headers = self.names, self.headers   # one graph
         return r
 
 
+def _header(buf: bytes) -> Reader:
+    if bytes(buf[:8]) != KRYO_HEADER_V0_1:
+        raise KryoException("Serialized bytes header does not match expected format.")
+    return Reader(buf, 8)
+
+
+def _expect_fields(r: Reader, cls: str, names: List[str]):
+    if cls not in r.headers:
+        n = r.varint()
+        if n != len(names):
+            raise KryoUnsupported("unexpected %s field count %d" % (cls, n))
+        got = []
+        for want in names:
+            got.append(r.string())
+            if got[-1] != want:
+                raise KryoUnsupported("unexpected %s field %r" % (cls, got[-1]))
+        r.headers[cls] = got
+
+
+def _read_metadata(r: Reader) -> Tuple[int, int]:
+    r.not_null()
+    _expect_fields(r, SIGNATURE_METADATA, META_FIELDS)
+    pv = r.chunk().varint(False)
+    sch = r.chunk().varint(False)
+    return pv, sch
+
+
+def _read_list(r: Reader, references: bool, read_item: Callable[[Reader], object]) -> list:
+    cls = r.read_class()
+    if references:
+        r.not_null()
+    if cls == SINGLETON_LIST:
+        return [read_item(r)]
+    if cls == ARRAY_LIST:
+        return [read_item(r) for _ in range(r.varint())]
+    if cls == REG_ARRAYS_ASLIST:
+        n = r.varint()
+        r.read_class()                           # the array's component class
+        return [read_item(r) for _ in range(n)]
+    raise KryoUnsupported("unsupported list class %r" % (cls,))
+
+
 def parse_signable_data(buf: bytes) -> Tuple[bytes, int, int]:
     """Inverse of signable_data: (txId, platformVersion, schemeNumberID); KryoException on any
     other layout (trailing bytes included)."""
-    if buf[:8] != KRYO_HEADER_V0_1:
-        raise KryoException("Serialized bytes header does not match expected format.")
-    r = Reader(buf, 8)
+    r = _header(buf)
     if r.read_class() != SIGNABLE_DATA:
         raise KryoException("not a SignableData")
     r.not_null()
-    names = r.field_names(SIGNABLE_DATA)
-    if names != ["SignableData.signatureMetadata", "SignableData.txId"]:
-        raise KryoException("unexpected SignableData fields %r" % names)
-    m = r.chunk()
-    m.not_null()
-    if m.field_names(SIGNATURE_METADATA) != ["SignatureMetadata.platformVersion", "SignatureMetadata.schemeNumberID"]:
-        raise KryoException("unexpected SignatureMetadata fields")
-    pv = m.chunk().varint(False)
-    sch = m.chunk().varint(False)
+    _expect_fields(r, SIGNABLE_DATA, ["SignableData.signatureMetadata", "SignableData.txId"])
+    pv, sch = _read_metadata(r.chunk())
     t = r.chunk()
     if t.read_class() != SECURE_HASH_SHA256:
         raise KryoException("txId is not a SecureHash.SHA256")
     t.not_null()
-    if t.field_names(SECURE_HASH_SHA256) != ["OpaqueBytes.bytes"]:
-        raise KryoException("unexpected SecureHash fields")
+    _expect_fields(t, SECURE_HASH_SHA256, ["OpaqueBytes.bytes"])
     a = t.chunk()
     a.not_null()
     n = a.varint() - 1
-    tx_id = a.buf[a.pos:a.pos + n]
-    if n != 32 or len(tx_id) != 32:
+    if n != 32:
         raise KryoException("txId is not 32 bytes")
+    tx_id = a.take(32)
     if r.pos != len(buf):
         raise KryoException("trailing bytes")
-    return bytes(tx_id), pv, sch
+    return tx_id, pv, sch
+
+
+def parse_wire_transaction(buf: bytes) -> Tuple[List[Tuple[int, List[bytes]]], bytes]:
+    """WireTransactionSerializer.read (Kryo.kt:242-246): ([(groupIndex, [component bytes])], salt)."""
+    r = _header(buf)
+    if r.read_class() != REG_WIRE_TX:
+        raise KryoUnsupported("not a WireTransaction")
+    r.not_null()
+
+    def comp(c: Reader) -> bytes:
+        if c.read_class() != REG_SERIALIZED_BYTES:
+            raise KryoUnsupported("component is not SerializedBytes")
+        return c.take(c.varint())
+
+    def group(c: Reader):
+        if c.read_class() != COMPONENT_GROUP:
+            raise KryoUnsupported("not a ComponentGroup")
+        _expect_fields(c, COMPONENT_GROUP, GROUP_FIELDS)
+        comps = _read_list(c.chunk(), False, comp)
+        gi = c.chunk().varint(False)
+        if not 0 <= gi < 64:                     # the device tracks group presence in 64 bits
+            raise KryoUnsupported("group index %d" % gi)
+        return gi, comps
+
+    groups = _read_list(r, False, group)
+    sid = r.read_class()
+    if not isinstance(sid, int) or sid < FIRST_UNPINNED_ID:
+        raise KryoUnsupported("privacySalt is not a registered class")
+    if r.varint() != 32:                         # PrivacySalt.init require: left to the JVM path
+        raise KryoUnsupported("Privacy salt should be 32 bytes.")
+    salt = r.take(32)
+    return groups, salt
+
+
+def parse_signed_transaction(buf: bytes) -> Tuple[bytes, List[Tuple[bytes, bytes, int, int]]]:
+    """SignedTransactionSerializer.read (Kryo.kt:273-278): (txBits, [(sig, key SPKI, pv, scheme)])."""
+    r = _header(buf)
+    if r.read_class() != REG_SIGNED_TX:
+        raise KryoUnsupported("not a SignedTransaction")
+    r.not_null()
+    if r.read_class() != REG_SERIALIZED_BYTES:
+        raise KryoUnsupported("txBits is not SerializedBytes")
+    r.not_null()
+    tx_bits = r.take(r.varint())
+
+    def txsig(c: Reader):
+        if c.read_class() != TRANSACTION_SIGNATURE:
+            raise KryoUnsupported("not a TransactionSignature")
+        c.not_null()
+        _expect_fields(c, TRANSACTION_SIGNATURE, TXSIG_FIELDS)
+        f = c.chunk()
+        f.not_null()
+        n = f.varint()
+        if n == 0:
+            raise KryoUnsupported("null signature bytes")
+        sig = f.take(n - 1)
+        f = c.chunk()
+        kid = f.read_class()
+        if not isinstance(kid, int) or kid < FIRST_UNPINNED_ID:
+            raise KryoUnsupported("key class is not a registered PublicKey class")
+        f.not_null()
+        key = f.take(f.varint())
+        pv, sch = _read_metadata(c.chunk())
+        return sig, key, pv, sch
+
+    sigs = _read_list(r, True, txsig)
+    return tx_bits, sigs
+
+
+# ---- WireTransaction.init / SignedTransaction.init checks the device front end applies ----
+GROUP_INPUTS, GROUP_OUTPUTS, GROUP_COMMANDS, GROUP_ATTACHMENTS, GROUP_NOTARY, GROUP_TIMEWINDOW = range(6)
+
+
+def wire_invariant_error(groups: Sequence[Tuple[int, Sequence[bytes]]], check_duplicates: bool = True) -> Optional[str]:
+    """The structural part of WireTransaction.init (WireTransaction.kt:53-60, BaseTransaction.kt:30-33):
+    the message of the IllegalStateException it throws, or None."""
+    if not all(len(c) for _, c in groups):
+        return "Empty component groups are not allowed"
+    idx = [gi for gi, _ in groups]
+    if len(set(idx)) != len(idx):
+        return "Duplicated component groups detected"
+    present = set(idx)
+    if GROUP_INPUTS in present and GROUP_NOTARY not in present:
+        return "The notary must be specified explicitly for any transaction that has inputs"
+    inputs = [bytes(c) for gi, comps in groups if gi == GROUP_INPUTS for c in comps]
+    if check_duplicates and len(set(inputs)) != len(inputs):      # StateRef equality = equality of its serialized bytes
+        return "Duplicate input states detected"
+    if GROUP_INPUTS not in present and GROUP_OUTPUTS not in present:
+        return "A transaction must contain at least one input or output state"
+    if GROUP_COMMANDS not in present:
+        return "A transaction must contain at least one command"
+    if GROUP_TIMEWINDOW in present and GROUP_NOTARY not in present:
+        return "Transactions with time-windows must be notarised"
+    return None
+
+
+# ---- the front end's verdict per SignedTransaction (host mirror of chip_stx_parse_device) ----
+STX_OK, STX_KRYO, STX_NO_SIGS, STX_INVARIANT, STX_UNSUPPORTED = range(5)
+
+
+def stx_parse(buf: bytes):
+    """-> (status, groups, salt, sigs): what SignedTransaction deserialisation, the lazy WireTransaction
+    deserialisation and their init checks make of `buf`, in the order the JVM meets them (cordahip.h
+    chip_stx_status).  groups / salt / sigs are None unless status is STX_OK."""
+    try:
+        tx_bits, sigs = parse_signed_transaction(buf)
+    except KryoUnsupported:
+        return STX_UNSUPPORTED, None, None, None
+    except KryoException:
+        return STX_KRYO, None, None, None
+    if not sigs:                                 # SignedTransaction.init require(sigs.isNotEmpty())
+        return STX_NO_SIGS, None, None, None
+    try:
+        groups, salt = parse_wire_transaction(tx_bits)
+    except KryoUnsupported:
+        return STX_UNSUPPORTED, None, None, None
+    except KryoException:
+        return STX_KRYO, None, None, None
+    if wire_invariant_error(groups, check_duplicates=False) is not None:
+        return STX_INVARIANT, None, None, None
+    if sum(len(c) for gi, c in groups if gi == GROUP_INPUTS) > 64:
+        return STX_UNSUPPORTED, None, None, None  # the device's duplicate-input check covers <= 64 inputs
+    if wire_invariant_error(groups) is not None:
+        return STX_INVARIANT, None, None, None
+    return STX_OK, groups, salt, sigs

@@ -39,7 +39,7 @@ EXPORTS = ["chip_abi_version", "chip_device_count", "chip_init", "chip_shutdown"
            "chip_verify_tx_batch", "chip_verify_tx_batch_device", "chip_ftx_verify_batch",
            "chip_ftx_verify_batch_device", "chip_required_signers", "chip_required_signers_device",
            "chip_verify_signed_tx_batch", "chip_verify_signed_tx_batch_device",
-           "chip_get_stats", "chip_reset_stats"]
+           "chip_stx_parse_device", "chip_copy_to_host", "chip_get_stats", "chip_reset_stats"]
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
 u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -79,6 +79,16 @@ class ChipSignerBatch(ctypes.Structure):
                 ("sig_len", ctypes.c_void_p), ("n_keys", ctypes.c_uint64), ("key_data", ctypes.c_void_p),
                 ("key_off", ctypes.c_void_p), ("key_len", ctypes.c_void_p), ("sig_bytes", ctypes.c_uint64),
                 ("key_bytes", ctypes.c_uint64)]
+
+
+class ChipStxBlobs(ctypes.Structure):
+    _fields_ = [("n", ctypes.c_uint64), ("data", ctypes.c_void_p), ("off", ctypes.c_void_p), ("len", ctypes.c_void_p),
+                ("data_bytes", ctypes.c_uint64), ("meta", ctypes.c_void_p), ("n_meta", ctypes.c_uint32),
+                ("pad", ctypes.c_uint32)]
+
+
+class ChipStxParsed(ctypes.Structure):
+    _fields_ = [("txs", ChipTxBatch), ("sigs", ChipSignerBatch), ("sig_start", ctypes.c_void_p)]
 
 
 class ChipFtxBatch(ctypes.Structure):
@@ -142,7 +152,8 @@ class ChipConflict(ctypes.Structure):
 
 
 (K_ED25519, K_ECDSA_R1, K_ECDSA_K1, K_TXID, K_KEYPREP, K_UNIQ, K_ED_COMB, K_ED_FINISH, K_ED_TABLES, K_EC_TABLES,
- K_ED_PLAN, K_ED_COMB_B, K_EC_FRONT, K_REQ) = range(14)
+ K_ED_PLAN, K_ED_COMB_B, K_EC_FRONT, K_REQ, K_STX) = range(15)
+(STX_OK, STX_KRYO, STX_NO_SIGS, STX_INVARIANT, STX_UNSUPPORTED) = range(5)
 N_KERNELS = 16
 FLAG_NO_COMB, FLAG_FORCE_COMB = 0x1, 0x2
 
@@ -231,6 +242,9 @@ def load(build_if_missing: bool = False):
     lib.chip_uniq_shard_classify.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     lib.chip_uniq_shard_finish.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
+    lib.chip_stx_parse_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipStxBlobs), ctypes.c_void_p,
+                                          ctypes.POINTER(ChipStxParsed), ctypes.c_void_p]
+    lib.chip_copy_to_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
     lib.chip_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipStats)]
     lib.chip_reset_stats.argtypes = [ctypes.c_void_p]
     _lib = lib
@@ -426,6 +440,35 @@ class Context:
         rq = make_req_batch(dev_q)
         self._check(self.lib.chip_verify_signed_tx_batch_device(self.h, ctypes.byref(tb), ctypes.byref(tm),
                                                                 ctypes.byref(sb), ctypes.byref(rq), _ptr(ids),
+                                                                _ptr(status), _ptr(verdict), _ptr(arg), _ptr(missing),
+                                                                stream or None))
+
+    # ---- Kryo front end: SignedTransaction bytes -> batches (device) ----
+    def stx_parse_device(self, data, off, lens, data_bytes, meta, tx_status, stream=None) -> ChipStxParsed:
+        """data / off / lens / tx_status: device tensors; meta: host int32 [n_meta, 2] (platformVersion,
+        schemeNumberID) per message template.  Returns the chip_stx_parsed of device pointers (valid
+        until the next call on this context)."""
+        meta = np.ascontiguousarray(np.asarray(meta, dtype=np.int32).reshape(-1, 2))
+        b = ChipStxBlobs(n=int(off.numel() if hasattr(off, "numel") else len(off)), data=_ptr(data), off=_ptr(off),
+                         len=_ptr(lens), data_bytes=int(data_bytes), meta=meta.ctypes.data, n_meta=len(meta), pad=0)
+        out = ChipStxParsed()
+        self._check(self.lib.chip_stx_parse_device(self.h, ctypes.byref(b), _ptr(tx_status), ctypes.byref(out),
+                                                   stream or None))
+        out._meta = meta
+        return out
+
+    def copy_to_host(self, ptr, count: int, dtype) -> np.ndarray:
+        """A library-owned device array (e.g. a chip_stx_parsed field) -> host numpy array."""
+        out = np.zeros(max(count, 1), dtype=dtype)
+        self._check(self.lib.chip_copy_to_host(self.h, out.ctypes.data, ptr, count * out.itemsize))
+        return out[:count]
+
+    def verify_signed_tx_parsed_device(self, parsed: ChipStxParsed, dev_templates, dev_q, ids, status, verdict, arg,
+                                       missing=None, stream=None):
+        """chip_verify_signed_tx_batch_device over a parsed batch (its sig_start must be dev_q's)."""
+        tm, rq = make_templates(dev_templates), make_req_batch(dev_q)
+        self._check(self.lib.chip_verify_signed_tx_batch_device(self.h, ctypes.byref(parsed.txs), ctypes.byref(tm),
+                                                                ctypes.byref(parsed.sigs), ctypes.byref(rq), _ptr(ids),
                                                                 _ptr(status), _ptr(verdict), _ptr(arg), _ptr(missing),
                                                                 stream or None))
 

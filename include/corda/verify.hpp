@@ -320,47 +320,100 @@ inline void varint(Bytes& o, uint32_t v) {
     o.push_back((uint8_t)v);
 }
 inline uint32_t zigzag(int32_t v) { return ((uint32_t)v << 1) ^ (uint32_t)(v >> 31); }
-inline void ascii(Bytes& o, const char* s) {   // Output.writeString, 1 < length < 64, ASCII
-    const size_t n = std::strlen(s);
-    for (size_t i = 0; i < n; i++) o.push_back((uint8_t)s[i] | (i + 1 == n ? 0x80 : 0));
-}
-inline void chunk(Bytes& o, const Bytes& d) {   // OutputChunked(1024) + endChunks
-    for (size_t i = 0; i < d.size(); i += 1024) {
-        const size_t m = std::min<size_t>(1024, d.size() - i);
-        varint(o, (uint32_t)m);
-        o.insert(o.end(), d.begin() + (long)i, d.begin() + (long)(i + m));
+// Kryo 4.0.0 Output (parent == nullptr: the top-level output, unbounded) / OutputChunked(parent, 1024):
+// a chunk is flushed when the buffer cannot take the next primitive and at endChunks; Output.flush
+// also flushes the parent, so nested chunked fields split the enclosing field's chunks (kryo.py).
+struct Out {
+    Out* parent = nullptr;
+    Bytes buf;
+    explicit Out(Out* p = nullptr) : parent(p) {}
+    void require(size_t n) {
+        if (parent && 1024 - buf.size() < n) flush();
     }
-    o.push_back(0);
-}
+    void byte(uint8_t b) {
+        if (parent && buf.size() == 1024) require(1);
+        buf.push_back(b);
+    }
+    void var(uint32_t v) {
+        Bytes e;
+        varint(e, v);
+        require(e.size());
+        buf.insert(buf.end(), e.begin(), e.end());
+    }
+    void bytes(const uint8_t* p, size_t n) {
+        if (!parent) {
+            buf.insert(buf.end(), p, p + n);
+            return;
+        }
+        size_t k = std::min(1024 - buf.size(), n);
+        for (;;) {
+            buf.insert(buf.end(), p, p + k);
+            p += k;
+            n -= k;
+            if (n == 0) return;
+            k = std::min<size_t>(1024, n);
+            require(k);
+        }
+    }
+    void str(const char* s) {   // Output.writeString, 1 < length < 64, ASCII
+        bytes((const uint8_t*)s, std::strlen(s));
+        buf.back() |= 0x80;
+    }
+    void flush() {
+        if (!parent) return;
+        if (!buf.empty()) {
+            Bytes e;
+            varint(e, (uint32_t)buf.size());
+            for (uint8_t b : e) parent->byte(b);
+            parent->bytes(buf.data(), buf.size());
+            buf.clear();
+        }
+        parent->flush();
+    }
+    void endChunks() {
+        flush();
+        parent->byte(0);
+    }
+};
 inline Bytes signableData(const uint8_t txId[32], const SignatureMetadata& m) {
-    Bytes o = {'c', 'o', 'r', 'd', 'a', 0, 0, 1};
-    o.push_back(1);   // class by name (NAME + 2), name id 0
-    o.push_back(0);
-    ascii(o, "net.corda.core.crypto.SignableData");
-    o.push_back(1);   // NOT_NULL (first-seen reference)
-    o.push_back(2);
-    ascii(o, "SignableData.signatureMetadata");
-    ascii(o, "SignableData.txId");
-    Bytes meta = {1, 2};
-    ascii(meta, "SignatureMetadata.platformVersion");
-    ascii(meta, "SignatureMetadata.schemeNumberID");
-    Bytes f;
-    varint(f, zigzag(m.platformVersion));
-    chunk(meta, f);
-    f.clear();
-    varint(f, zigzag(m.schemeNumberID));
-    chunk(meta, f);
-    chunk(o, meta);
-    Bytes h = {1, 1};   // class by name, name id 1
-    ascii(h, "net.corda.core.crypto.SecureHash$SHA256");
-    h.push_back(1);
-    h.push_back(1);
-    ascii(h, "OpaqueBytes.bytes");
-    Bytes arr = {1, 33};   // NOT_NULL, length + 1
-    arr.insert(arr.end(), txId, txId + 32);
-    chunk(h, arr);
-    chunk(o, h);
-    return o;
+    Out o;
+    static const uint8_t header[8] = {'c', 'o', 'r', 'd', 'a', 0, 0, 1};
+    o.bytes(header, 8);
+    o.var(1);   // class by name (NAME + 2), name id 0
+    o.var(0);
+    o.str("net.corda.core.crypto.SignableData");
+    o.var(1);   // NOT_NULL (first-seen reference)
+    o.var(2);
+    o.str("SignableData.signatureMetadata");
+    o.str("SignableData.txId");
+    Out c(&o);   // one OutputChunked for SignableData's fields
+    c.var(1);    // signatureMetadata: NOT_NULL, header, two chunked int fields
+    c.var(2);
+    c.str("SignatureMetadata.platformVersion");
+    c.str("SignatureMetadata.schemeNumberID");
+    {
+        Out f(&c);
+        f.var(zigzag(m.platformVersion));
+        f.endChunks();
+        f.var(zigzag(m.schemeNumberID));
+        f.endChunks();
+    }
+    c.endChunks();
+    c.var(1);   // txId: class by name (name id 1), NOT_NULL, header, one chunked byte[] field
+    c.var(1);
+    c.str("net.corda.core.crypto.SecureHash$SHA256");
+    c.var(1);
+    c.var(1);
+    c.str("OpaqueBytes.bytes");
+    {
+        Out f(&c);
+        f.var(1);    // NOT_NULL
+        f.var(33);   // length + 1
+        f.bytes(txId, 32);
+        f.endChunks();
+    }
+    c.endChunks();
+    return o.buf;
 }
 }  // namespace kryo
 

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define CHIP_ABI_VERSION 5
+#define CHIP_ABI_VERSION 6
 
 enum chip_sig_status {
     CHIP_VALID = 0,
@@ -325,6 +325,59 @@ int chip_verify_signed_tx_batch_device(chip_ctx* ctx, const chip_tx_batch* txs, 
                                        void* stream);
 
 /* ---------------------------------------------------------------------------------------
+ * Kryo front end: SignedTransaction bytes -> the batches above, on the device.
+ * Blob t = SignedTransaction.serialize().bytes under the Kryo P2P context (SignedTransactionSerializer
+ * + WireTransactionSerializer, node-api/.../serialization/Kryo.kt:236-280; layout restated in
+ * corda_amd/kryo.py, parity unpinned: no JVM output exists here).  The parse is what
+ * SignedTransaction deserialisation + the lazy WireTransaction deserialisation + their init checks do
+ * before SignedTransaction.verifySignaturesExcept reads tx.id and sigs:
+ *   tx_status[t]  CHIP_STX_OK
+ *                 CHIP_STX_KRYO         KryoException (header mismatch, truncated input)
+ *                 CHIP_STX_NO_SIGS      SignedTransaction.init: "...without any signatures"
+ *                 CHIP_STX_INVARIANT    WireTransaction.init IllegalStateException (empty / duplicated
+ *                                       component groups, notary with inputs, duplicate inputs, no input
+ *                                       or output, no command, time-window without notary)
+ *                 CHIP_STX_UNSUPPORTED  well-formed bytes outside the device grammar (object back-references,
+ *                                       other list / key classes, group index >= 64, ...): verify that
+ *                                       transaction on the JVM path
+ * A transaction that is not OK contributes no components and no signatures, except one whose only fault is
+ * a duplicate input (found by the second pass, which compares the de-chunked inputs): its ranges stay
+ * filled and its status says CHIP_STX_INVARIANT.  The outputs live in the
+ * context's buffers until its next chip_stx_parse_device call (device pointers, this context's GPU):
+ *   out->txs    chip_tx_batch of every blob (salts, component ranges, groups, internal indices; the
+ *               component bytes de-chunked into the context's pool)
+ *   out->sigs   chip_signer_batch: tx_idx = blob index, tmpl_idx = the index i of the first template whose
+ *               (meta[2i], meta[2i+1]) = (platformVersion, schemeNumberID) of the signature's
+ *               SignatureMetadata (0xffffffff when none matches: the fused verify then reports
+ *               CHIP_UNSUPPORTED for it), key_idx into a de-duplicated key pool numbered in order of first
+ *               occurrence in the signature list (equal SPKI bytes = one key)
+ *   out->sig_start  [n + 1] each transaction's signature range (list order), for chip_req_batch
+ * so that chip_verify_signed_tx_batch_device(ctx, &out->txs, tmpl, &out->sigs, req, ...) verifies the batch.
+ * Synchronises with `stream` twice (the totals size the outputs). */
+enum chip_stx_status { CHIP_STX_OK = 0, CHIP_STX_KRYO = 1, CHIP_STX_NO_SIGS = 2, CHIP_STX_INVARIANT = 3,
+                       CHIP_STX_UNSUPPORTED = 4 };
+typedef struct {
+    uint64_t n;
+    const uint8_t* data;       /* pool (device)                                               */
+    const uint64_t* off;       /* [n] (device)                                                */
+    const uint32_t* len;       /* [n] (device)                                                */
+    uint64_t data_bytes;
+    const int32_t* meta;       /* [2 * n_meta] HOST memory: SignatureMetadata of template i   */
+    uint32_t n_meta;
+    uint32_t pad;
+} chip_stx_blobs;
+typedef struct {
+    chip_tx_batch txs;
+    chip_signer_batch sigs;
+    const uint64_t* sig_start;
+} chip_stx_parsed;
+int chip_stx_parse_device(chip_ctx* ctx, const chip_stx_blobs* in, uint8_t* tx_status, chip_stx_parsed* out,
+                          void* stream);
+/* Copies `bytes` from device memory of this context's GPU (e.g. a chip_stx_parsed array) to host memory
+ * (blocking; after the context's stream has drained). */
+int chip_copy_to_host(chip_ctx* ctx, void* dst, const void* src_device, uint64_t bytes);
+
+/* ---------------------------------------------------------------------------------------
  * Notary uniqueness (GPU-resident StateRef -> ConsumingTx table).
  * StateRef key = 32-byte txhash || little-endian u32 index (36 bytes).
  * ConsumingTx  = (32-byte consuming tx id, u32 inputIndex, u32 caller) where caller is the
@@ -409,11 +462,12 @@ int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_st
  * both curves per launch in two launches, the low table half (windows 0..31) counted under
  * CHIP_K_ECDSA_R1 and the high half (+ the x(R) check) under CHIP_K_ECDSA_K1; CHIP_K_EC_FRONT = the ECDSA comb
  * kernels that need none (key grouping, DER/SHA-256/s R, batched s^-1, u1 G; both curves);
- * CHIP_K_REQ = k_required_signers */
+ * CHIP_K_REQ = k_required_signers, CHIP_K_STX = the Kryo front end (both parse passes, scans, key interning
+ * of one chip_stx_parse_device call) */
 enum chip_kernel { CHIP_K_ED25519 = 0, CHIP_K_ECDSA_R1 = 1, CHIP_K_ECDSA_K1 = 2, CHIP_K_TXID = 3,
                    CHIP_K_KEYPREP = 4, CHIP_K_UNIQ = 5, CHIP_K_ED_COMB = 6, CHIP_K_ED_FINISH = 7,
                    CHIP_K_ED_TABLES = 8, CHIP_K_EC_TABLES = 9, CHIP_K_ED_PLAN = 10, CHIP_K_ED_COMB_B = 11,
-                   CHIP_K_EC_FRONT = 12, CHIP_K_REQ = 13, CHIP_N_KERNELS = 16 };
+                   CHIP_K_EC_FRONT = 12, CHIP_K_REQ = 13, CHIP_K_STX = 14, CHIP_N_KERNELS = 16 };
 typedef struct {
     uint64_t batches, sigs, keys_prepared;
     uint64_t status_count[8];

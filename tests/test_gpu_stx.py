@@ -1,0 +1,157 @@
+"""GPU: the Kryo front end (chip_stx_parse_device, kryo.hip) against its host mirror (corda_amd/kryo.py).
+
+PARITY UNPINNED for the bytes themselves (no JVM output exists here: kryo.py restates Kryo 4.0.0); what
+these tests pin is that the device parse of every SignedTransaction equals the host mirror's — statuses
+for each failure class, components (group, internal index, bytes), salts, signatures, signer keys,
+metadata -> template mapping, the first-occurrence key numbering — and that verifying a batch from its
+bytes gives the same ids, signature statuses and required-signer verdicts as the structured batch."""
+import numpy as np
+import pytest
+import torch
+
+import cordagen as G
+import stx_build as S
+from corda_amd import kryo as K
+from corda_amd import native
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+METAS = np.array(S.METAS[:3], dtype=np.int32)     # (2, 4) maps to no template
+
+
+def _dev(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def parse(ctx, blobs):
+    data, off, ln = G.stx_blobs_from_lists(blobs)
+    if len(data) == 0:
+        data = np.zeros(1, np.uint8)
+    dd, doff, dlen = _dev(data), _dev(off), _dev(ln)
+    st = torch.zeros(len(blobs), dtype=torch.uint8, device=DEV)
+    p = ctx.stx_parse_device(dd, doff, dlen, len(data), METAS, st)
+    torch.cuda.synchronize()
+    return p, st.cpu().numpy(), (dd, doff, dlen)
+
+
+def host(ctx, p, n):
+    t, s = p.txs, p.sigs
+    r = {"cstart": ctx.copy_to_host(t.tx_comp_start, n + 1, np.uint64),
+         "sstart": ctx.copy_to_host(p.sig_start, n + 1, np.uint64),
+         "salts": ctx.copy_to_host(t.salts, 32 * n, np.uint8).reshape(n, 32),
+         "group": ctx.copy_to_host(t.comp_group, t.ncomp, np.uint32),
+         "internal": ctx.copy_to_host(t.comp_internal, t.ncomp, np.uint32),
+         "coff": ctx.copy_to_host(t.comp_off, t.ncomp, np.uint64),
+         "clen": ctx.copy_to_host(t.comp_len, t.ncomp, np.uint32),
+         "pool": ctx.copy_to_host(t.data, t.data_bytes, np.uint8),
+         "tx_idx": ctx.copy_to_host(s.tx_idx, s.n, np.uint32),
+         "tmpl": ctx.copy_to_host(s.tmpl_idx, s.n, np.uint32),
+         "kidx": ctx.copy_to_host(s.key_idx, s.n, np.uint32),
+         "soff": ctx.copy_to_host(s.sig_off, s.n, np.uint64),
+         "slen": ctx.copy_to_host(s.sig_len, s.n, np.uint32),
+         "koff": ctx.copy_to_host(s.key_off, s.n_keys, np.uint64),
+         "klen": ctx.copy_to_host(s.key_len, s.n_keys, np.uint32)}
+    return r
+
+
+def test_parse_equals_host_mirror(ctx):
+    blobs = S.cases(seed=7, n_valid=300)
+    p, st, _keep = parse(ctx, blobs)
+    n = len(blobs)
+    want = [K.stx_parse(b) for b in blobs]
+    assert list(st) == [w[0] for w in want]
+    assert set(st) == {0, 1, 2, 3, 4}                   # every status class is exercised
+    h = host(ctx, p, n)
+    pool = h["pool"]
+    keys_seen = {}
+    for t, (status, groups, salt, sigs) in enumerate(want):
+        c0, c1 = int(h["cstart"][t]), int(h["cstart"][t + 1])
+        s0, s1 = int(h["sstart"][t]), int(h["sstart"][t + 1])
+        if status != K.STX_OK:
+            dup_only = status == K.STX_INVARIANT and K.wire_invariant_error(
+                K.parse_wire_transaction(K.parse_signed_transaction(blobs[t])[0])[0], check_duplicates=False) is None
+            assert dup_only or (c0 == c1 and s0 == s1), t
+            continue
+        comps = [(gi, i, c) for gi, cs in groups for i, c in enumerate(cs)]
+        assert c1 - c0 == len(comps), t
+        for k, (gi, i, c) in enumerate(comps):
+            o, ln = int(h["coff"][c0 + k]), int(h["clen"][c0 + k])
+            assert (int(h["group"][c0 + k]), int(h["internal"][c0 + k])) == (gi, i), (t, k)
+            assert pool[o:o + ln].tobytes() == c, (t, k)
+        assert h["salts"][t].tobytes() == salt
+        assert s1 - s0 == len(sigs), t
+        for j, (sig, key, pv, sch) in enumerate(sigs):
+            i = s0 + j
+            o, ln = int(h["soff"][i]), int(h["slen"][i])
+            assert pool[o:o + ln].tobytes() == sig, (t, j)
+            assert int(h["tx_idx"][i]) == t
+            m = [k for k in range(len(METAS)) if tuple(METAS[k]) == (pv, sch)]
+            assert int(h["tmpl"][i]) == (m[0] if m else 0xFFFFFFFF)
+            kid = keys_seen.setdefault(key, len(keys_seen))          # first-occurrence numbering
+            assert int(h["kidx"][i]) == kid, (t, j)
+            ko, kl = int(h["koff"][kid]), int(h["klen"][kid])
+            assert pool[ko:ko + kl].tobytes() == key
+    assert p.sigs.n_keys == len(keys_seen)
+
+
+def test_empty_and_single_blob(ctx):
+    p, st, _ = parse(ctx, [])
+    assert p.txs.ntx == 0 and p.sigs.n == 0
+    blobs = S.cases(seed=3, n_valid=1)[:1]
+    p, st, _ = parse(ctx, blobs)
+    assert list(st) == [K.stx_parse(blobs[0])[0]] == [0]
+
+
+def test_verify_from_bytes_equals_structured_path(ctx):
+    """cfg4-shaped batch: ids, signature statuses and required-signer verdicts from the parsed bytes
+    equal those of the structured batch (chip_verify_signed_tx_batch_device on host-built arrays)."""
+    ntx = 2000
+    tb, tm, sb, ids_ref, _ = G.cfg4_workload(ntx, n_keys=64, seed=0x5EED0104, threads=8)
+    q = G.cfg4_required(sb, ntx, 64, seed=0x5EED0106)
+    data, off, ln = G.stx_uniform(tb, sb, 2)
+    dd, doff, dlen = _dev(data), _dev(off), _dev(ln)
+    st = torch.zeros(ntx, dtype=torch.uint8, device=DEV)
+    p = ctx.stx_parse_device(dd, doff, dlen, len(data), np.array([[1, 4]], np.int32), st)
+    assert int((st != 0).sum()) == 0
+    # required keys: the structured batch's key-pool indices -> the parser's first-occurrence numbering
+    first = {}
+    for k in sb.key_idx:
+        first.setdefault(int(k), len(first))
+    remap = np.array([first.get(k, native_no_signer()) for k in range(len(sb.key_off))] + [native_no_signer()],
+                     dtype=np.uint64)
+    q2 = G.ReqBatch()
+    for f in ("ntx", "sig_start", "req_start", "node_start", "allowed", "node_val", "node_nkids", "node_weight"):
+        setattr(q2, f, getattr(q, f))
+    leaf = q.node_nkids == 0
+    nv = q.node_val.astype(np.uint64).copy()
+    nv[leaf] = remap[np.minimum(nv[leaf], len(remap) - 1)]
+    q2.node_val = nv.astype(np.uint32)
+    # structured reference
+    ids, status, verdict, arg, missing = ctx.verify_signed_tx_batch(tb, tm, sb, q)
+    dev = {k: _dev(getattr(q2, k)) for k in ("sig_start", "req_start", "node_start", "allowed", "node_val",
+                                               "node_nkids", "node_weight") if getattr(q2, k) is not None}
+    dq2 = G.ReqBatch()
+    dq2.ntx = ntx
+    for k in ("sig_start", "req_start", "node_start", "allowed", "node_val", "node_nkids", "node_weight"):
+        setattr(dq2, k, dev.get(k))
+    dq2.nreq, dq2.n_nodes = len(q.node_start) - 1, len(q.node_val)
+    dtm = G.Templates()
+    dtm.data, dtm.off, dtm.len, dtm.id_at, dtm.max_len = _dev(tm.data), _dev(tm.off), _dev(tm.len), _dev(tm.id_at), tm.max_len
+    d_ids = torch.zeros(ntx * 32, dtype=torch.uint8, device=DEV)
+    d_status = torch.zeros(sb.n, dtype=torch.uint8, device=DEV)
+    d_verdict = torch.zeros(ntx, dtype=torch.uint8, device=DEV)
+    d_arg = torch.zeros(ntx, dtype=torch.int32, device=DEV)
+    d_missing = torch.zeros(max(dq2.nreq, 1), dtype=torch.uint8, device=DEV)
+    ctx.verify_signed_tx_parsed_device(p, dtm, dq2, d_ids, d_status, d_verdict, d_arg, d_missing)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_ids.cpu().numpy().reshape(ntx, 32), ids)
+    assert np.array_equal(ids, ids_ref)
+    assert np.array_equal(d_status.cpu().numpy(), status)
+    assert np.array_equal(d_verdict.cpu().numpy(), verdict)
+    assert np.array_equal(d_arg.cpu().numpy().view(np.uint32), arg)
+    assert np.array_equal(d_missing.cpu().numpy()[:dq2.nreq], missing)
+    assert int((status == 0).sum()) > 0 and int((verdict != 0).sum()) > 0
+
+
+def native_no_signer():
+    return G.REQ_NO_SIGNER

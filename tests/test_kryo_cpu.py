@@ -35,11 +35,14 @@ def test_layout_of_signable_data():
                  b"SignatureMetadata.platformVersio\xeeSignatureMetadata.schemeNumberI\xc4",
                  b"\x01\x01net.corda.core.crypto.SecureHash$SHA25\xb6\x01\x01OpaqueBytes.byte\xf3"):
         assert name in b
-    # metadata ints are zig-zag varints inside their own chunks: 01 02 00 | 01 08 00
-    assert b"\x01\x02\x00\x01\x08\x00" in b
-    # the id: NOT_NULL, length + 1, 32 bytes, then the two chunk end markers
-    assert b.endswith(b"\x01\x21" + tx + b"\x00\x00")
-    assert len(b) == 266
+    # metadata ints are zig-zag varints inside their own chunked fields; every inner flush also flushes
+    # the enclosing field's OutputChunked (Output.flush -> parent.flush): the signatureMetadata field
+    # is chunk(NOT_NULL, header, 01 02) chunk(00 01 08) chunk(00) 00
+    assert b"\x45\x01\x02SignatureMetadata." in b
+    assert b"\x01\x02\x03\x00\x01\x08\x01\x00\x00" in b
+    # the id: NOT_NULL, length + 1, 32 bytes, then the inner end marker as its own chunk and the outer
+    assert b.endswith(b"\x01\x21" + tx + b"\x01\x00\x00")
+    assert len(b) == 269
 
 
 @pytest.mark.parametrize("pv,sch", METAS)

@@ -1,0 +1,81 @@
+"""CPU: the Kryo SignedTransaction / WireTransaction restatement (corda_amd/kryo.py) — the host mirror of
+the device front end (chip_stx_parse_device) and the writer of its test and bench inputs.
+
+PARITY UNPINNED: no JVM output exists here.  These tests pin the restatement's own rules: write -> read
+round trips for every list class and chunk-spanning component, the OutputChunked placement rules
+(1024-byte chunks, a primitive never straddles a chunk, nested fields flush the enclosing chunk), the
+status each failure class gets, and the uniform-batch filler against the per-transaction writer."""
+import numpy as np
+import pytest
+
+import cordagen as G
+import stx_build as S
+from corda_amd import kryo as K
+
+
+def test_round_trip_of_random_transactions():
+    rng = np.random.default_rng(11)
+    pool = [S._key(rng, S.ED_KEY) for _ in range(5)] + [S._key(rng, 91)]
+    for _ in range(150):
+        groups, salt, sigs, kinds, skind = S.random_valid(rng, pool)
+        b = S.blob(groups, salt, sigs, kinds, skind)
+        st, g, s, sg = K.stx_parse(b)
+        assert st == K.STX_OK
+        assert g == [(gi, list(c)) for gi, c in groups]
+        assert s == salt
+        assert sg == [x.tuple() for x in sigs]
+
+
+def test_status_classes():
+    blobs = S.cases(seed=7, n_valid=20)
+    st = [K.stx_parse(b)[0] for b in blobs]
+    assert st[:20] == [K.STX_OK] * 20
+    tail = st[20:]
+    assert tail[:12] == [K.STX_KRYO] * 12                 # truncations, damaged headers, truncated txBits
+    assert tail[12] == K.STX_NO_SIGS
+    assert tail[13:20] == [K.STX_INVARIANT] * 7           # each WireTransaction.init check
+    assert tail[20:] == [K.STX_UNSUPPORTED] * 6           # outside the device grammar
+
+
+@pytest.mark.parametrize("groups,msg", [
+    ([(1, [b"a"]), (2, [])], "Empty component groups are not allowed"),
+    ([(1, [b"a"]), (1, [b"b"]), (2, [b"c"])], "Duplicated component groups detected"),
+    ([(0, [b"a"]), (1, [b"b"]), (2, [b"c"])], "The notary must be specified explicitly for any transaction that has inputs"),
+    ([(0, [b"a", b"a"]), (2, [b"c"]), (4, [b"n"])], "Duplicate input states detected"),
+    ([(2, [b"c"]), (4, [b"n"])], "A transaction must contain at least one input or output state"),
+    ([(1, [b"o"]), (4, [b"n"])], "A transaction must contain at least one command"),
+    ([(1, [b"o"]), (2, [b"c"]), (5, [b"t"])], "Transactions with time-windows must be notarised"),
+    ([(0, [b"a"]), (1, [b"o"]), (2, [b"c"]), (4, [b"n"]), (5, [b"t"])], None),
+])
+def test_wire_transaction_invariants(groups, msg):
+    assert K.wire_invariant_error(groups) == msg
+
+
+def test_chunk_placement():
+    # a 1500-byte component: ComponentGroup.components is one chunked field; the first chunk is full
+    w = K.wire_transaction([(1, [bytes(1500)]), (2, [b"c"])], bytes(32))
+    assert b"\x80\x08" in w                                  # varint(1024)
+    groups, salt = K.parse_wire_transaction(w)
+    assert groups[0][1][0] == bytes(1500)
+    # a varint never straddles a chunk: 1023 payload bytes then a 2-byte varint -> flush at 1023
+    o = K.Out()
+    c = K.Out(o)
+    c.write_bytes(bytes(1023))
+    c.write_varint(300)
+    c.end_chunks()
+    assert o.getvalue() == b"\xff\x07" + bytes(1023) + b"\x02\xac\x02\x00"
+    # nested CompatibleFieldSerializer: every inner chunk flushes the enclosing field's chunk
+    s = K.signed_transaction(K.wire_transaction([(1, [b"o"]), (2, [b"c"])], bytes(32)),
+                             [K.Sig(bytes(64), bytes(44), 1, 4, 31)])
+    assert b"\x01\x02\x03\x00\x01\x08\x01\x00\x00" in s       # ...01 02 | 00 01 08 | 00 | end
+
+
+def test_uniform_filler_equals_writer():
+    tb, tm, sb, ids, _ = G.cfg4_workload(24, n_keys=8, seed=0x5EED0204, threads=4)
+    data, off, ln = G.stx_uniform(tb, sb, 2)
+    for t in range(24):
+        b = data[int(off[t]):int(off[t]) + int(ln[t])].tobytes()
+        assert b == G.stx_signed_tx(tb, sb, t, range(2 * t, 2 * t + 2))
+        st, groups, salt, sigs = K.stx_parse(b)
+        assert st == K.STX_OK and salt == tb.salts[32 * t:32 * t + 32].tobytes()
+        assert [len(c) for _, cs in groups for c in cs] == [96, 96, 640, 640, 320, 96, 384, 96]

@@ -775,3 +775,89 @@ def cfg4_required(sb: SignerBatch, ntx: int, n_keys: int, seed: int = 0x5EED0006
     q.expected_verdict = np.where(any_bad, 1, np.where(miss, 2, 0)).astype(np.uint8)
     q.expected_arg = np.where(any_bad, first_bad, np.where(miss, 1, 0)).astype(np.uint32)
     return q
+
+
+# ---- Kryo SignedTransaction blobs (the §8f-2 front end's input; corda_amd/kryo.py writer) ----
+def _tx_groups(tb, t):
+    """[(groupIndex, [component bytes])] of transaction t of a TxBatch, in component order."""
+    groups = []
+    for k in range(int(tb.tx_comp_start[t]), int(tb.tx_comp_start[t + 1])):
+        g = int(tb.comp_group[k])
+        c = tb.data[int(tb.comp_off[k]):int(tb.comp_off[k]) + int(tb.comp_len[k])].tobytes()
+        if groups and groups[-1][0] == g:
+            groups[-1][1].append(c)
+        else:
+            groups.append((g, [c]))
+    return groups
+
+
+def stx_blobs_from_lists(blobs):
+    """list of bytes -> (data u8, off u64, len u32)."""
+    return pools_from_list(list(blobs))
+
+
+def stx_signed_tx(tb, sb, t, sig_range, metas=((1, 4),), key_class_id=None):
+    """SignedTransaction bytes of transaction t of (TxBatch, SignerBatch): its components, salt and the
+    signatures sig_range (SignableData metadata of template sb.tmpl_idx[i] from `metas`)."""
+    from corda_amd import kryo as K
+    wtx = K.wire_transaction(_tx_groups(tb, t), tb.salts[32 * t:32 * t + 32].tobytes())
+    sigs = []
+    for i in sig_range:
+        k = int(sb.key_idx[i])
+        key = sb.key_data[int(sb.key_off[k]):int(sb.key_off[k]) + int(sb.key_len[k])].tobytes()
+        sig = sb.sig_data[int(sb.sig_off[i]):int(sb.sig_off[i]) + int(sb.sig_len[i])].tobytes()
+        pv, sch = metas[int(sb.tmpl_idx[i])]
+        sigs.append(K.Sig(sig, key, pv, sch, key_class_id))
+    return K.signed_transaction(wtx, sigs)
+
+
+def stx_uniform(tb, sb, sigs_per_tx: int, meta=(1, 4)):
+    """The SignedTransaction blobs of a uniform batch (every tx the same component lengths, sigs_per_tx
+    signatures of equal lengths with equal-length keys, one metadata): the Kryo layout is then the same
+    for every tx, so one template is written with corda_amd/kryo.py and each payload field's byte
+    positions found by writing it all-0x00 vs all-0xFF; the batch is filled with numpy scatters.
+    -> (data u8 [ntx * L], off u64, len u32)."""
+    from corda_amd import kryo as K
+    ntx = int(tb.ntx)
+    per = int(tb.tx_comp_start[1] - tb.tx_comp_start[0])
+    glist = [int(g) for g in tb.comp_group[:per]]
+    clens = [int(x) for x in tb.comp_len[:per]]
+    slen = int(sb.sig_len[0])
+    klen = int(sb.key_len[int(sb.key_idx[0])])
+    fields = [("c", k, clens[k]) for k in range(per)] + [("salt", 0, 32)] + \
+             [(f, j, slen if f == "s" else klen) for j in range(sigs_per_tx) for f in ("s", "k")]
+
+    def write(fill):
+        comps = [bytes([fill.get(("c", k), 0)]) * clens[k] for k in range(per)]
+        groups = []
+        for k in range(per):
+            if groups and groups[-1][0] == glist[k]:
+                groups[-1][1].append(comps[k])
+            else:
+                groups.append((glist[k], [comps[k]]))
+        wtx = K.wire_transaction(groups, bytes([fill.get(("salt", 0), 0)]) * 32)
+        sigs = [K.Sig(bytes([fill.get(("s", j), 0)]) * slen, bytes([fill.get(("k", j), 0)]) * klen, meta[0], meta[1])
+                for j in range(sigs_per_tx)]
+        return np.frombuffer(K.signed_transaction(wtx, sigs), dtype=np.uint8)
+
+    base = write({})
+    pos = {}
+    for f, j, n in fields:
+        d = np.nonzero(base != write({(f, j): 0xFF}))[0]
+        assert len(d) == n, (f, j, len(d), n)
+        pos[(f, j)] = d
+    L = len(base)
+    out = np.tile(base, (ntx, 1))
+    cdat = tb.data[:ntx * sum(clens)].reshape(ntx, sum(clens))
+    at = 0
+    for k in range(per):
+        out[:, pos[("c", k)]] = cdat[:, at:at + clens[k]]
+        at += clens[k]
+    out[:, pos[("salt", 0)]] = tb.salts.reshape(ntx, 32)
+    sig = sb.sig_data.reshape(-1, slen).reshape(ntx, sigs_per_tx, slen)
+    kpool = np.stack([sb.key_data[int(o):int(o) + klen] for o in sb.key_off])
+    keys = kpool[sb.key_idx.astype(np.int64)].reshape(ntx, sigs_per_tx, klen)
+    for j in range(sigs_per_tx):
+        out[:, pos[("s", j)]] = sig[:, j]
+        out[:, pos[("k", j)]] = keys[:, j]
+    return out.reshape(-1), np.arange(ntx, dtype=np.uint64) * L, np.full(ntx, L, dtype=np.uint32)
