@@ -23,8 +23,9 @@
 //
 // Passes: k_stx_parse<false> validates and counts (components skipped chunk by chunk), an inclusive scan
 // gives the ranges, k_stx_parse<true> parses again and writes the batches: component / signature /
-// key bytes de-chunked into the context's pool (a 4-byte-aligned region per blob from a scan of the
-// payload sizes, dword stores), then the
+// key bytes located in the context's pool — a copy of the blobs at their input offsets, so a run that lies
+// in one chunk keeps its offset and only chunk-spanning runs are de-chunked into a per-blob extra region
+// (sized by a scan, dword stores) — then the
 // signers' keys are interned on the device (hash table, byte compare, first occurrence wins) into a
 // de-duplicated key pool in first-occurrence order.
 #include <hipcub/hipcub.hpp>
@@ -51,7 +52,7 @@ struct Sink {   // dword-accumulating byte writer into the output pool
     uint8_t* base;
     uint64_t pos;
     uint32_t acc;
-    __device__ void put(uint8_t b) {
+    __device__ __forceinline__ void put(uint8_t b) {
         acc |= (uint32_t)b << (8 * (pos & 3));
         pos++;
         if ((pos & 3) == 0) {
@@ -59,7 +60,7 @@ struct Sink {   // dword-accumulating byte writer into the output pool
             acc = 0;
         }
     }
-    __device__ void flush() {
+    __device__ __forceinline__ void flush() {
         if (pos & 3) *reinterpret_cast<uint32_t*>(base + (pos & ~3ull)) = acc;
     }
 };
@@ -69,7 +70,7 @@ struct Cur {
     const uint8_t* pool;
     uint64_t pool_bytes, pos, end;
     uint64_t widx;
-    uint32_t w;
+    uint4 w;
     uint32_t rem1, rem2;
     int err;
     // class-name ids of this graph (4 bits each) and the CompatibleFieldSerializer headers already read
@@ -77,40 +78,42 @@ struct Cur {
     uint32_t nnames;
     uint32_t headers;
 
-    __device__ void init(const uint8_t* p, uint64_t pb, uint64_t a, uint64_t b) {
+    __device__ __forceinline__ void init(const uint8_t* p, uint64_t pb, uint64_t a, uint64_t b) {
         pool = p;
         pool_bytes = pb;
         pos = a;
         end = b;
         widx = ~0ull;
-        w = 0;
+        w = make_uint4(0, 0, 0, 0);
         rem1 = rem2 = 0;
         err = E_OK;
         names = nnames = headers = 0;
     }
-    __device__ void fail(int e) {
+    __device__ __forceinline__ void fail(int e) {
         if (err == E_OK) err = e;
     }
-    __device__ uint8_t raw() {
+    __device__ __forceinline__ uint8_t raw() {
         if (pos >= end) {
             fail(E_KRYO);
             return 0;
         }
-        const uint64_t wi = pos >> 2;
+        const uint64_t wi = pos >> 4;   // a 16-byte window per lane: one global_load_dwordx4 per 16 bytes
         if (wi != widx) {
-            if ((wi << 2) + 4 <= pool_bytes) {
-                w = *reinterpret_cast<const uint32_t*>(pool + (wi << 2));
+            if ((wi << 4) + 16 <= pool_bytes) {
+                w = *reinterpret_cast<const uint4*>(pool + (wi << 4));
                 widx = wi;
             } else {
                 return pool[pos++];
             }
         }
-        const uint8_t b = (uint8_t)(w >> (8 * (pos & 3)));
+        const uint32_t q = (pos >> 2) & 3;
+        const uint32_t d = q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w;
+        const uint8_t b = (uint8_t)(d >> (8 * (pos & 3)));
         pos++;
         return b;
     }
-    template <int L> __device__ uint8_t byte();
-    template <int L> __device__ uint32_t varint() {
+    template <int L> __device__ __forceinline__ uint8_t byte();
+    template <int L> __device__ __forceinline__ uint32_t varint() {
         uint32_t v = 0;
         for (int s = 0; s < 35; s += 7) {
             const uint8_t b = byte<L>();
@@ -119,12 +122,12 @@ struct Cur {
         }
         return v;
     }
-    template <int L> __device__ int32_t zigzag() {
+    template <int L> __device__ __forceinline__ int32_t zigzag() {
         const uint32_t v = varint<L>();
         return (int32_t)(v >> 1) ^ -(int32_t)(v & 1);
     }
     // skip n bytes at level L (L <= 1 without reading their contents at level 0)
-    template <int L> __device__ void skip(uint32_t n) {
+    template <int L> __device__ __forceinline__ void skip(uint32_t n) {
         if constexpr (L == 0) {
             if (end - pos < n) {
                 pos = end;
@@ -151,7 +154,7 @@ struct Cur {
         }
     }
     // InputChunked.nextChunks at the end of a field: skip what is left of it, through the 0 marker
-    template <int L> __device__ void end_field() {
+    template <int L> __device__ __forceinline__ void end_field() {
         if constexpr (L == 1) {
             skip<0>(rem1);
             rem1 = 0;
@@ -171,7 +174,7 @@ struct Cur {
         }
     }
     // Input.readString compared against one expected ASCII string (field names)
-    template <int L> __device__ bool string_is(const char* s, uint32_t len) {
+    template <int L> __device__ __forceinline__ bool string_is(const char* s, uint32_t len) {
         bool ok = true;
         for (uint32_t i = 0;; i++) {
             const uint8_t b = byte<L>();
@@ -190,7 +193,7 @@ struct Cur {
         }
     }
     // a class name read as a string: one of k_names (C_ARRAYLIST ..) or C_OTHER
-    template <int L> __device__ int class_name() {
+    template <int L> __device__ __forceinline__ int class_name() {
         uint32_t cand = 0xf;
         for (uint32_t i = 0;; i++) {
             const uint8_t b = byte<L>();
@@ -214,7 +217,7 @@ struct Cur {
         }
     }
     // DefaultClassResolver.readClass: >= 0 registered id, -(code) for a class by name, -100 null
-    template <int L> __device__ int read_class() {
+    template <int L> __device__ __forceinline__ int read_class() {
         const uint32_t tag = varint<L>();
         if (err) return -100;
         if (tag == 0) return -100;
@@ -231,11 +234,11 @@ struct Cur {
         nnames++;
         return -code;
     }
-    template <int L> __device__ void not_null() {
+    template <int L> __device__ __forceinline__ void not_null() {
         if (varint<L>() != 1) fail(E_UNSUP);   // null or a back-reference
     }
     // CompatibleFieldSerializer field-name header, the first time per graph
-    template <int L> __device__ void header(uint32_t flag, int first, int count) {
+    template <int L> __device__ __forceinline__ void header(uint32_t flag, int first, int count) {
         if (headers & flag) return;
         headers |= flag;
         if (varint<L>() != (uint32_t)count) {
@@ -246,7 +249,7 @@ struct Cur {
             if (!string_is<L>(k_fields[first + f], k_field_len[first + f])) fail(E_UNSUP);
     }
     // a list class + size: ArrayList / SingletonList / Arrays$ArrayList (with its component class)
-    template <int L> __device__ uint32_t list(bool refs) {
+    template <int L> __device__ __forceinline__ uint32_t list(bool refs) {
         const int c = read_class<L>();
         if (err) return 0;
         if (refs) not_null<L>();
@@ -262,8 +265,8 @@ struct Cur {
     }
 };
 
-template <> __device__ uint8_t Cur::byte<0>() { return raw(); }
-template <> __device__ uint8_t Cur::byte<1>() {
+template <> __device__ __forceinline__ uint8_t Cur::byte<0>() { return raw(); }
+template <> __device__ __forceinline__ uint8_t Cur::byte<1>() {
     while (rem1 == 0) {
         rem1 = varint<0>();
         if (err) return 0;
@@ -275,7 +278,7 @@ template <> __device__ uint8_t Cur::byte<1>() {
     rem1--;
     return raw();
 }
-template <> __device__ uint8_t Cur::byte<2>() {
+template <> __device__ __forceinline__ uint8_t Cur::byte<2>() {
     while (rem2 == 0) {
         rem2 = varint<1>();
         if (err) return 0;
@@ -288,7 +291,98 @@ template <> __device__ uint8_t Cur::byte<2>() {
     return byte<1>();
 }
 
-__device__ bool header_ok(Cur& c) {
+// 4 bytes at any offset of the pool (two aligned loads + byte funnel; the pool has >= 8 bytes of slack)
+__device__ __forceinline__ uint32_t ld32u(const uint8_t* pool, uint64_t off) {
+    const uint64_t a = off & ~3ull;
+    const uint32_t lo = *reinterpret_cast<const uint32_t*>(pool + a);
+    const uint32_t hi = *reinterpret_cast<const uint32_t*>(pool + a + 4);
+    return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(off & 3));
+}
+__device__ __forceinline__ uint32_t tail_mask(uint32_t left) { return left >= 4 ? ~0u : (1u << (8 * left)) - 1; }
+__device__ __forceinline__ bool key_eq(const uint8_t* pool, uint64_t a, uint32_t la, uint64_t b, uint32_t lb) {
+    if (la != lb) return false;
+    for (uint32_t i = 0; i < la; i += 4)
+        if ((ld32u(pool, a + i) ^ ld32u(pool, b + i)) & tail_mask(la - i)) return false;
+    return true;
+}
+
+// A payload run of n bytes inside a level-1 field: where it starts in the blob pool when it lies in one
+// chunk (the context's pool holds a copy of the blobs at their input offsets, so the offset is reused),
+// else it is de-chunked into the blob's extra region (4-byte aligned); `extra` counts those bytes.
+template <bool EMIT> __device__ __forceinline__ uint64_t run1(Cur& c, uint32_t n, Sink& sink, uint64_t& extra) {
+    if (n == 0) return c.pos;
+    if (c.rem1 == 0) {
+        c.rem1 = c.varint<0>();
+        if (c.err) return 0;
+        if (c.rem1 == 0) {
+            c.fail(E_KRYO);
+            return 0;
+        }
+    }
+    if (n <= c.rem1) {
+        const uint64_t at = c.pos;
+        c.skip<0>(n);
+        c.rem1 -= n;
+        return at;
+    }
+    extra += (n + 3) & ~3u;
+    if (!EMIT) {
+        c.skip<1>(n);
+        return 0;
+    }
+    // de-chunk piece by piece: bytes until the sink is dword aligned, then dword copies (unaligned
+    // source loads from the pool copy), then the tail
+    const uint64_t at = sink.pos;
+    uint32_t left = n;
+    while (left && !c.err) {
+        if (c.rem1 == 0) {
+            c.rem1 = c.varint<0>();
+            if (c.err) break;
+            if (c.rem1 == 0) {
+                c.fail(E_KRYO);
+                break;
+            }
+        }
+        uint32_t k = left < c.rem1 ? left : c.rem1;
+        if (c.end - c.pos < k) {
+            c.fail(E_KRYO);
+            break;
+        }
+        uint64_t src = c.pos;
+        c.pos += k;
+        c.rem1 -= k;
+        left -= k;
+        for (; k && (sink.pos & 3); k--) sink.put(sink.base[src++]);
+        // 16 bytes per step: five independent aligned loads, funnelled (source and sink share the pool, so
+        // the loads are issued before the stores explicitly)
+        for (; k >= 16; k -= 16, src += 16, sink.pos += 16) {
+            const uint32_t* a = reinterpret_cast<const uint32_t*>(sink.base + (src & ~3ull));
+            const uint32_t sh = (uint32_t)(src & 3);
+            const uint32_t w0 = a[0], w1 = a[1], w2 = a[2], w3 = a[3], w4 = a[4];
+            uint4 v;
+            v.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
+            v.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
+            v.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
+            v.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
+            if ((sink.pos & 15) == 0) {
+                *reinterpret_cast<uint4*>(sink.base + sink.pos) = v;
+            } else {
+                uint32_t* d = reinterpret_cast<uint32_t*>(sink.base + sink.pos);
+                d[0] = v.x;
+                d[1] = v.y;
+                d[2] = v.z;
+                d[3] = v.w;
+            }
+        }
+        for (; k >= 4; k -= 4, src += 4, sink.pos += 4)
+            *reinterpret_cast<uint32_t*>(sink.base + sink.pos) = ld32u(sink.base, src);
+        for (; k; k--) sink.put(sink.base[src++]);
+    }
+    while (sink.pos & 3) sink.put(0);
+    return at;
+}
+
+__device__ __forceinline__ bool header_ok(Cur& c) {
     const uint8_t h[8] = {'c', 'o', 'r', 'd', 'a', 0, 0, 1};
     for (int i = 0; i < 8; i++)
         if (c.byte<0>() != h[i]) return false;
@@ -297,7 +391,8 @@ __device__ bool header_ok(Cur& c) {
 
 struct Outs {   // pass-2 destinations (NULL in pass 1)
     uint8_t* pool;
-    const uint64_t* pool_start;
+    const uint64_t* extra_start;   // [n + 1] extra region of blob t, relative to extra_base
+    uint64_t extra_base;
     uint8_t* salts;
     const uint64_t* comp_start;
     uint32_t* comp_group;
@@ -320,13 +415,13 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
                                                    const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
                                                    uint64_t data_bytes, uint8_t* __restrict__ status,
                                                    uint64_t* __restrict__ ncomp, uint64_t* __restrict__ nsig,
-                                                   uint64_t* __restrict__ nbytes, Outs o) {
+                                                   uint64_t* __restrict__ nextra, Outs o) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     if (EMIT && status[t] != CHIP_STX_OK) return;
     const uint64_t a = off[t], b = a + len[t];
-    uint64_t comps = 0, sigs = 0, payload = 0;
-    Sink sink{o.pool, EMIT ? o.pool_start[t] : 0, 0};
+    uint64_t comps = 0, sigs = 0, extra = 0;
+    Sink sink{o.pool, EMIT ? o.extra_base + o.extra_start[t] : 0, 0};
     uint64_t cbase = EMIT ? o.comp_start[t] : 0, sbase = EMIT ? o.sig_start[t] : 0;
     int st = CHIP_STX_OK;
     Cur c;
@@ -362,27 +457,25 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
             uint32_t sl = c.varint<1>();
             if (sl == 0) c.fail(E_UNSUP);
             sl -= 1;
-            if (EMIT) {
-                o.sig_off[sbase + sigs] = sink.pos;
-                o.sig_len[sbase + sigs] = sl;
-                for (uint32_t k = 0; k < sl && !c.err; k++) sink.put(c.byte<1>());
-            } else {
-                c.skip<1>(sl);
+            {
+                const uint64_t at = run1<EMIT>(c, sl, sink, extra);
+                if (EMIT) {
+                    o.sig_off[sbase + sigs] = at;
+                    o.sig_len[sbase + sigs] = sl;
+                }
             }
-            payload += sl;
             c.end_field<1>();
             // TransactionSignature.by: a registered PublicKey class, NOT_NULL, varint length, SPKI bytes
             if (c.read_class<1>() < 14) c.fail(E_UNSUP);
             c.not_null<1>();
             const uint32_t kl = c.varint<1>();
-            if (EMIT) {
-                o.key_off[sbase + sigs] = sink.pos;
-                o.key_len[sbase + sigs] = kl;
-                for (uint32_t k = 0; k < kl && !c.err; k++) sink.put(c.byte<1>());
-            } else {
-                c.skip<1>(kl);
+            {
+                const uint64_t at = run1<EMIT>(c, kl, sink, extra);
+                if (EMIT) {
+                    o.key_off[sbase + sigs] = at;
+                    o.key_len[sbase + sigs] = kl;
+                }
             }
-            payload += kl;
             c.end_field<1>();
             // TransactionSignature.signatureMetadata: NOT_NULL, header, two chunked ints (level 2)
             c.not_null<1>();
@@ -416,7 +509,7 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
     }
     // ---- WireTransaction (txBits; references off inside) ----
     {
-        Cur w;
+        Cur& w = c;                               // the outer graph is done: reuse the cursor
         w.init(data, data_bytes, tx_a, tx_b);
         if (!header_ok(w)) {
             st = CHIP_STX_KRYO;
@@ -443,15 +536,12 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
                     break;
                 }
                 const uint32_t cl = w.varint<1>();
+                const uint64_t at = run1<EMIT>(w, cl, sink, extra);
                 if (EMIT) {
-                    o.comp_off[cbase + comps] = sink.pos;
+                    o.comp_off[cbase + comps] = at;
                     o.comp_len[cbase + comps] = cl;
                     o.comp_internal[cbase + comps] = k;
-                    for (uint32_t q = 0; q < cl && !w.err; q++) sink.put(w.byte<1>());
-                } else {
-                    w.skip<1>(cl);
                 }
-                payload += cl;
                 comps++;
             }
             w.end_field<1>();
@@ -475,10 +565,11 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
         if (!w.err) {
             if (w.read_class<0>() < 14) w.fail(E_UNSUP);
             if (w.varint<0>() != 32) w.fail(E_UNSUP);
-            for (int k = 0; k < 32 && !w.err; k++) {
-                const uint8_t s = w.byte<0>();
-                if (EMIT) o.salts[t * 32 + k] = s;
+            if (EMIT && !w.err && w.end - w.pos >= 32) {
+                uint32_t* dst = reinterpret_cast<uint32_t*>(o.salts + t * 32);
+                for (int k = 0; k < 8; k++) dst[k] = ld32u(o.pool, w.pos + 4 * k);
             }
+            w.skip<0>(32);
         }
         if (w.err) {
             st = w.err == E_KRYO ? CHIP_STX_KRYO : CHIP_STX_UNSUPPORTED;
@@ -495,13 +586,8 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
             sink.flush();
             for (uint64_t i = 0; i < in_count && st == CHIP_STX_OK; i++)
                 for (uint64_t j = i + 1; j < in_count; j++) {
-                    const uint32_t li = o.comp_len[in_first + i];
-                    if (li != o.comp_len[in_first + j]) continue;
-                    const uint8_t* pi = o.pool + o.comp_off[in_first + i];
-                    const uint8_t* pj = o.pool + o.comp_off[in_first + j];
-                    bool eq = true;
-                    for (uint32_t q = 0; q < li && eq; q++) eq = pi[q] == pj[q];
-                    if (eq) {
+                    if (key_eq(o.pool, o.comp_off[in_first + i], o.comp_len[in_first + i], o.comp_off[in_first + j],
+                               o.comp_len[in_first + j])) {
                         st = CHIP_STX_INVARIANT;
                         break;
                     }
@@ -516,32 +602,28 @@ done:
         status[t] = (uint8_t)st;
         ncomp[t] = st == CHIP_STX_OK ? comps : 0;
         nsig[t] = st == CHIP_STX_OK ? sigs : 0;
-        nbytes[t] = st == CHIP_STX_OK ? (payload + 3) & ~3ull : 0;   // 4-byte-aligned region per blob
+        nextra[t] = st == CHIP_STX_OK ? extra : 0;   // de-chunked (chunk-spanning) payload, 4-byte units
     }
 }
 
 // ---- signer key interning: distinct SPKI byte strings in first-occurrence order ----
-__device__ uint32_t key_hash(const uint8_t* p, uint32_t n) {
+__device__ uint32_t key_hash(const uint8_t* pool, uint64_t off, uint32_t n) {
     uint32_t h = 2166136261u ^ n;
-    for (uint32_t i = 0; i < n; i++) h = (h ^ p[i]) * 16777619u;
+    for (uint32_t i = 0; i < n; i += 4) h = (h ^ (ld32u(pool, off + i) & tail_mask(n - i))) * 16777619u;
+    h ^= h >> 15;
+    h *= 0x2c1b3c6du;
+    h ^= h >> 12;
     return h | 1u;   // never 0 (0 = empty slot)
 }
-__device__ bool key_eq(const uint8_t* a, uint32_t la, const uint8_t* b, uint32_t lb) {
-    if (la != lb) return false;
-    for (uint32_t i = 0; i < la; i++)
-        if (a[i] != b[i]) return false;
-    return true;
-}
-
 __global__ void __launch_bounds__(256) k_stx_key_insert(uint64_t nsig, const uint8_t* __restrict__ pool,
                                                         const uint64_t* __restrict__ koff, const uint32_t* __restrict__ klen,
                                                         unsigned long long* tab, uint32_t* tab_min, uint64_t mask,
                                                         uint32_t* __restrict__ slot) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= nsig) return;
-    const uint8_t* k = pool + koff[i];
+    const uint64_t k = koff[i];
     const uint32_t kl = klen[i];
-    const uint32_t h = key_hash(k, kl);
+    const uint32_t h = key_hash(pool, k, kl);
     const unsigned long long mine = ((unsigned long long)h << 32) | (unsigned long long)i;
     uint64_t s = h & mask;
     for (uint64_t probe = 0; probe <= mask; probe++, s = (s + 1) & mask) {
@@ -553,11 +635,14 @@ __global__ void __launch_bounds__(256) k_stx_key_insert(uint64_t nsig, const uin
         }
         if ((uint32_t)(e >> 32) == h) {
             const uint64_t j = e & 0xffffffffull;
-            if (key_eq(k, kl, pool + koff[j], klen[j])) break;
+            if (key_eq(pool, k, kl, koff[j], klen[j])) break;
         }
     }
     slot[i] = (uint32_t)s;
-    atomicMin(&tab_min[s], (uint32_t)i);
+    // the key's first occurrence: most lanes see a smaller index already and skip the atomic (a hot
+    // key's slot would otherwise serialise every one of its signatures)
+    if (__hip_atomic_load(&tab_min[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > (uint32_t)i)
+        atomicMin(&tab_min[s], (uint32_t)i);
 }
 
 __global__ void __launch_bounds__(256) k_stx_key_flag(uint64_t nsig, const uint32_t* __restrict__ slot,
@@ -590,16 +675,16 @@ inline dim3 grid_of(uint64_t n) { return dim3((uint32_t)((n + 255) / 256)); }
 }  // namespace
 
 void launch_stx_count(hipStream_t st, const chip_stx_blobs* in, uint8_t* status, uint64_t* ncomp, uint64_t* nsig,
-                      uint64_t* nbytes) {
+                      uint64_t* nextra) {
     if (!in->n) return;
     Outs o{};
     hipLaunchKernelGGL(k_stx_parse<false>, grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->off, in->len,
-                       in->data_bytes, status, ncomp, nsig, nbytes, o);
+                       in->data_bytes, status, ncomp, nsig, nextra, o);
 }
 
 void launch_stx_emit(hipStream_t st, const chip_stx_blobs* in, uint8_t* status, const StxOut& d) {
     if (!in->n) return;
-    Outs o{d.pool, d.pool_start, d.salts, d.comp_start, d.comp_group, d.comp_internal, d.comp_off, d.comp_len, d.sig_start,
+    Outs o{d.pool, d.extra_start, d.extra_base, d.salts, d.comp_start, d.comp_group, d.comp_internal, d.comp_off, d.comp_len, d.sig_start,
            d.tx_idx, d.tmpl_idx, d.sig_off, d.sig_len, d.skey_off, d.skey_len, d.meta, d.n_meta};
     hipLaunchKernelGGL(k_stx_parse<true>, grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->off, in->len,
                        in->data_bytes, status, nullptr, nullptr, nullptr, o);

@@ -756,9 +756,14 @@ int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_sta
     for (int k = 0; k < 3; k++)
         HIPCHK(c, hipMemcpyAsync(&tot[k], rng[k]->as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
-    const uint64_t ncomp = tot[0], nsig = tot[1], pool = tot[2];
+    const uint64_t ncomp = tot[0], nsig = tot[1];
     if (nsig >= (1ull << 31)) return fail(c, CHIP_E_ARG, "too many signatures");
-    HIPCHK(c, c->s_pool.ensure(pool + 16));
+    // pool = a copy of the blobs (payload runs inside one chunk keep their offsets) + the extra region
+    const uint64_t extra_base = (in->data_bytes + 15) & ~15ull;
+    const uint64_t pool = extra_base + tot[2];
+    HIPCHK(c, c->s_pool.ensure(pool + 64));
+    if (in->data_bytes)
+        HIPCHK(c, hipMemcpyAsync(c->s_pool.p, in->data, in->data_bytes, hipMemcpyDeviceToDevice, st));
     HIPCHK(c, c->s_cgroup.ensure(ncomp * 4 + 16));
     HIPCHK(c, c->s_cint.ensure(ncomp * 4 + 16));
     HIPCHK(c, c->s_coff.ensure(ncomp * 8 + 16));
@@ -783,7 +788,8 @@ int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_sta
         HIPCHK(c, hipMemcpyAsync(c->s_meta.p, in->meta, (uint64_t)in->n_meta * 8, hipMemcpyHostToDevice, st));
     StxOut d{};
     d.pool = c->s_pool.as<uint8_t>();
-    d.pool_start = c->s_pstart.as<uint64_t>();
+    d.extra_start = c->s_pstart.as<uint64_t>();
+    d.extra_base = extra_base;
     d.salts = c->s_salts.as<uint8_t>();
     d.comp_start = c->s_cstart.as<uint64_t>();
     d.comp_group = c->s_cgroup.as<uint32_t>();

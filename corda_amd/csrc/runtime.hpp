@@ -59,8 +59,9 @@ void launch_required_signers(hipStream_t st, const chip_req_batch* q, uint64_t n
 
 // Kryo front end (kryo.hip): SignedTransaction bytes -> tx / signer batches in the context's buffers
 struct StxOut {
-    uint8_t* pool;                 // de-chunked payload: components, signature bytes, signer keys
-    const uint64_t* pool_start;    // [n + 1] region of blob t in the pool
+    uint8_t* pool;                 // copy of the blobs + the extra region (de-chunked spanning runs)
+    const uint64_t* extra_start;   // [n + 1] extra region of blob t, relative to extra_base
+    uint64_t extra_base;
     uint8_t* salts;                // [n * 32]
     const uint64_t* comp_start;    // [n + 1]
     uint32_t *comp_group, *comp_internal, *comp_len;
@@ -78,7 +79,7 @@ struct StxOut {
     uint32_t* key_len;
 };
 void launch_stx_count(hipStream_t st, const chip_stx_blobs* in, uint8_t* status, uint64_t* ncomp, uint64_t* nsig,
-                      uint64_t* nbytes);
+                      uint64_t* nextra);
 void launch_stx_emit(hipStream_t st, const chip_stx_blobs* in, uint8_t* status, const StxOut& d);
 size_t stx_scan_temp_bytes(uint64_t n);
 hipError_t stx_scan_u64(hipStream_t st, void* temp, size_t temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n);

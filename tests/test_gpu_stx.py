@@ -113,19 +113,7 @@ def test_verify_from_bytes_equals_structured_path(ctx):
     st = torch.zeros(ntx, dtype=torch.uint8, device=DEV)
     p = ctx.stx_parse_device(dd, doff, dlen, len(data), np.array([[1, 4]], np.int32), st)
     assert int((st != 0).sum()) == 0
-    # required keys: the structured batch's key-pool indices -> the parser's first-occurrence numbering
-    first = {}
-    for k in sb.key_idx:
-        first.setdefault(int(k), len(first))
-    remap = np.array([first.get(k, native_no_signer()) for k in range(len(sb.key_off))] + [native_no_signer()],
-                     dtype=np.uint64)
-    q2 = G.ReqBatch()
-    for f in ("ntx", "sig_start", "req_start", "node_start", "allowed", "node_val", "node_nkids", "node_weight"):
-        setattr(q2, f, getattr(q, f))
-    leaf = q.node_nkids == 0
-    nv = q.node_val.astype(np.uint64).copy()
-    nv[leaf] = remap[np.minimum(nv[leaf], len(remap) - 1)]
-    q2.node_val = nv.astype(np.uint32)
+    q2 = G.required_for_parsed(q, sb)
     # structured reference
     ids, status, verdict, arg, missing = ctx.verify_signed_tx_batch(tb, tm, sb, q)
     dev = {k: _dev(getattr(q2, k)) for k in ("sig_start", "req_start", "node_start", "allowed", "node_val",
@@ -152,6 +140,3 @@ def test_verify_from_bytes_equals_structured_path(ctx):
     assert np.array_equal(d_missing.cpu().numpy()[:dq2.nreq], missing)
     assert int((status == 0).sum()) > 0 and int((verdict != 0).sum()) > 0
 
-
-def native_no_signer():
-    return G.REQ_NO_SIGNER

@@ -848,16 +848,42 @@ def stx_uniform(tb, sb, sigs_per_tx: int, meta=(1, 4)):
         pos[(f, j)] = d
     L = len(base)
     out = np.tile(base, (ntx, 1))
+
+    def put(key, src):                           # positions -> contiguous runs: slice copies, not gathers
+        d = pos[key]
+        cut = np.nonzero(np.diff(d) != 1)[0] + 1
+        for a, b in zip(np.concatenate([[0], cut]), np.concatenate([cut, [len(d)]])):
+            out[:, d[a]:d[a] + (b - a)] = src[:, a:b]
     cdat = tb.data[:ntx * sum(clens)].reshape(ntx, sum(clens))
     at = 0
     for k in range(per):
-        out[:, pos[("c", k)]] = cdat[:, at:at + clens[k]]
+        put(("c", k), cdat[:, at:at + clens[k]])
         at += clens[k]
-    out[:, pos[("salt", 0)]] = tb.salts.reshape(ntx, 32)
+    put(("salt", 0), tb.salts.reshape(ntx, 32))
     sig = sb.sig_data.reshape(-1, slen).reshape(ntx, sigs_per_tx, slen)
     kpool = np.stack([sb.key_data[int(o):int(o) + klen] for o in sb.key_off])
     keys = kpool[sb.key_idx.astype(np.int64)].reshape(ntx, sigs_per_tx, klen)
     for j in range(sigs_per_tx):
-        out[:, pos[("s", j)]] = sig[:, j]
-        out[:, pos[("k", j)]] = keys[:, j]
+        put(("s", j), sig[:, j])
+        put(("k", j), keys[:, j])
     return out.reshape(-1), np.arange(ntx, dtype=np.uint64) * L, np.full(ntx, L, dtype=np.uint32)
+
+
+def required_for_parsed(q, sb):
+    """A ReqBatch whose leaves index the structured key pool -> the same batch over the key pool of
+    chip_stx_parse_device (distinct signer keys numbered by first occurrence in the signature list;
+    a key that signs nothing becomes REQ_NO_SIGNER)."""
+    first = {}
+    for k in sb.key_idx:
+        first.setdefault(int(k), len(first))
+    remap = np.array([first.get(k, REQ_NO_SIGNER) for k in range(len(sb.key_off))] + [REQ_NO_SIGNER],
+                     dtype=np.uint64)
+    q2 = ReqBatch()
+    for f in ("ntx", "sig_start", "req_start", "node_start", "allowed", "node_nkids", "node_weight",
+              "expected_verdict", "expected_arg"):
+        setattr(q2, f, getattr(q, f, None))
+    leaf = q.node_nkids == 0
+    nv = q.node_val.astype(np.uint64).copy()
+    nv[leaf] = remap[np.minimum(nv[leaf], len(remap) - 1)]
+    q2.node_val = nv.astype(np.uint32)
+    return q2
