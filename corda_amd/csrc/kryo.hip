@@ -34,19 +34,25 @@
 namespace {
 
 enum { E_OK = 0, E_KRYO = 1, E_UNSUP = 2 };
-enum { C_NONE = 0, C_ARRAYLIST = 1, C_SINGLETON = 2, C_TXSIG = 3, C_GROUP = 4, C_OTHER = 5 };
-enum { H_TXSIG = 1, H_META = 2, H_GROUP = 4 };
+enum { C_NONE = 0, C_ARRAYLIST = 1, C_SINGLETON = 2, C_TXSIG = 3, C_GROUP = 4, C_COMMAND = 5, C_PARTY = 6, C_OTHER = 7 };
+enum { H_TXSIG = 1, H_META = 2, H_GROUP = 4, H_CMD = 8, H_PARTY = 16 };
+#define N_NAMES 6
 
 // class names the grammar knows (C_ARRAYLIST .. C_GROUP) and the field names of the three headers
-__constant__ char k_names[4][48] = {"java.util.ArrayList", "java.util.Collections$SingletonList",
-                                    "net.corda.core.crypto.TransactionSignature",
-                                    "net.corda.core.transactions.ComponentGroup"};
-__constant__ uint8_t k_name_len[4] = {19, 35, 42, 42};
-__constant__ char k_fields[7][48] = {"OpaqueBytes.bytes", "TransactionSignature.by",
-                                     "TransactionSignature.signatureMetadata", "SignatureMetadata.platformVersion",
-                                     "SignatureMetadata.schemeNumberID", "ComponentGroup.components",
-                                     "ComponentGroup.groupIndex"};
-__constant__ uint8_t k_field_len[7] = {17, 23, 38, 33, 32, 25, 25};
+__constant__ char k_names[N_NAMES][48] = {"java.util.ArrayList", "java.util.Collections$SingletonList",
+                                          "net.corda.core.crypto.TransactionSignature",
+                                          "net.corda.core.transactions.ComponentGroup",
+                                          "net.corda.core.contracts.Command", "net.corda.core.identity.Party"};
+__constant__ uint8_t k_name_len[N_NAMES] = {19, 35, 42, 42, 32, 29};
+__constant__ char k_fields[11][48] = {"OpaqueBytes.bytes", "TransactionSignature.by",
+                                      "TransactionSignature.signatureMetadata", "SignatureMetadata.platformVersion",
+                                      "SignatureMetadata.schemeNumberID", "ComponentGroup.components",
+                                      "ComponentGroup.groupIndex", "Command.signers", "Command.value",
+                                      "AbstractParty.owningKey", "Party.name"};
+__constant__ uint8_t k_field_len[11] = {17, 23, 38, 33, 32, 25, 25, 15, 13, 23, 10};
+// DER of the CompositeKey algorithm OID 2.25.30086077608615255153862931087626791002 (CompositeKey.kt)
+__constant__ uint8_t k_composite_oid[21] = {0x06, 0x13, 0x69, 0xad, 0xa2, 0xaf, 0x89, 0xd5, 0xb8, 0xe2, 0xaf,
+                                            0xf3, 0x8d, 0x93, 0xac, 0x9d, 0xe6, 0x96, 0x9b, 0xd0, 0x5a};
 
 struct Sink {   // dword-accumulating byte writer into the output pool
     uint8_t* base;
@@ -194,7 +200,7 @@ struct Cur {
     }
     // a class name read as a string: one of k_names (C_ARRAYLIST ..) or C_OTHER
     template <int L> __device__ __forceinline__ int class_name() {
-        uint32_t cand = 0xf;
+        uint32_t cand = (1u << N_NAMES) - 1;
         for (uint32_t i = 0;; i++) {
             const uint8_t b = byte<L>();
             if (err) return C_NONE;
@@ -203,10 +209,10 @@ struct Cur {
                 return C_NONE;
             }
             const uint8_t ch = b & 0x7f;
-            for (int c = 0; c < 4; c++)
+            for (int c = 0; c < N_NAMES; c++)
                 if (i >= k_name_len[c] || (uint8_t)k_names[c][i] != ch) cand &= ~(1u << c);
             if (b & 0x80) {
-                for (int c = 0; c < 4; c++)
+                for (int c = 0; c < N_NAMES; c++)
                     if ((cand >> c & 1) && k_name_len[c] == i + 1) return C_ARRAYLIST + c;
                 return C_OTHER;
             }
@@ -670,6 +676,159 @@ __global__ void __launch_bounds__(256) k_stx_key_assign(uint64_t nsig, const uin
     }
 }
 
+// ---- requiredSigningKeys from the components (WireTransaction.kt:66-75) ----
+__device__ __forceinline__ uint8_t pool_byte(const uint8_t* pool, uint64_t off) { return pool[off]; }
+
+// SubjectPublicKeyInfo whose AlgorithmIdentifier OID is the CompositeKey OID
+__device__ __forceinline__ bool is_composite_spki(const uint8_t* pool, uint64_t off, uint32_t len) {
+    if (len < 27 || pool_byte(pool, off) != 0x30) return false;
+    uint32_t p = 1;
+    const uint8_t l1 = pool_byte(pool, off + 1);
+    p += l1 < 0x80 ? 1 : l1 == 0x81 ? 2 : l1 == 0x82 ? 3 : 99;
+    if (p + 2 + 21 > len || pool_byte(pool, off + p) != 0x30) return false;
+    const uint8_t l2 = pool_byte(pool, off + p + 1);
+    p += l2 < 0x80 ? 2 : l2 == 0x81 ? 3 : 99;
+    if (p + 21 > len) return false;
+    for (int i = 0; i < 21; i++)
+        if (pool_byte(pool, off + p + i) != k_composite_oid[i]) return false;
+    return true;
+}
+
+struct ReqCtx {
+    const uint8_t* pool;
+    const unsigned long long* tab;
+    const uint32_t* tab_min;
+    uint64_t mask;
+    const uint64_t* skey_off;
+    const uint32_t* skey_len;
+    const uint32_t* kincl;
+};
+
+// the key index of a signer key equal to (off, len), or CHIP_REQ_NO_SIGNER
+__device__ __forceinline__ uint32_t lookup_kid(const ReqCtx& r, uint64_t off, uint32_t len) {
+    const uint32_t h = key_hash(r.pool, off, len);
+    uint64_t s = h & r.mask;
+    for (uint64_t probe = 0; probe <= r.mask; probe++, s = (s + 1) & r.mask) {
+        const unsigned long long e = r.tab[s];
+        if (e == 0) return CHIP_REQ_NO_SIGNER;
+        if ((uint32_t)(e >> 32) == h) {
+            const uint64_t j = e & 0xffffffffull;
+            if (key_eq(r.pool, off, len, r.skey_off[j], r.skey_len[j])) return r.kincl[r.tab_min[s]] - 1;
+        }
+    }
+    return CHIP_REQ_NO_SIGNER;
+}
+
+// pass R1 counts the signer entries (commands' signers, then the notary key) of every OK transaction;
+// R2 writes them with their key index and a duplicate flag (an earlier entry of the same transaction
+// with the same key: requiredSigningKeys is a set).  A command or notary component outside the grammar,
+// a chunk-spanning key or a CompositeKey (its tree is not in the signer pool) -> CHIP_STX_UNSUPPORTED.
+template <bool EMIT>
+__global__ void __launch_bounds__(256) k_stx_required(uint64_t n, uint8_t* __restrict__ status,
+                                                      const uint64_t* __restrict__ comp_start,
+                                                      const uint32_t* __restrict__ comp_group,
+                                                      const uint64_t* __restrict__ comp_off,
+                                                      const uint32_t* __restrict__ comp_len, uint64_t pool_bytes,
+                                                      ReqCtx r, uint64_t* __restrict__ nraw,
+                                                      const uint64_t* __restrict__ raw_start, uint32_t* __restrict__ raw_kid,
+                                                      uint64_t* __restrict__ raw_off, uint32_t* __restrict__ raw_len,
+                                                      uint32_t* __restrict__ raw_keep, uint64_t* __restrict__ nreq) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    if (status[t] != CHIP_STX_OK) {
+        if (!EMIT) nraw[t] = 0;
+        else nreq[t] = 0;
+        return;
+    }
+    const uint64_t c0 = comp_start[t], c1 = comp_start[t + 1];
+    uint64_t present = 0;
+    int64_t notary = -1;
+    for (uint64_t k = c0; k < c1; k++) {
+        const uint32_t g = comp_group[k];
+        present |= 1ull << g;
+        if (g == 4 && notary < 0) notary = (int64_t)k;
+    }
+    const bool want_notary = notary >= 0 && ((present & 1) || (present >> 5 & 1));
+    uint64_t cnt = 0, kept = 0;
+    const uint64_t base = EMIT ? raw_start[t] : 0;
+    bool bad = false;
+    Sink none{nullptr, 0, 0};
+    uint64_t spill = 0;
+    auto take = [&](uint64_t off, uint32_t len) {
+        const uint32_t kid = lookup_kid(r, off, len);
+        if (kid == CHIP_REQ_NO_SIGNER && is_composite_spki(r.pool, off, len)) bad = true;
+        if (EMIT && !bad) {
+            bool dup = false;
+            for (uint64_t j = base; j < base + cnt && !dup; j++) {
+                if (kid != CHIP_REQ_NO_SIGNER) dup = raw_kid[j] == kid;
+                else dup = raw_kid[j] == CHIP_REQ_NO_SIGNER && key_eq(r.pool, off, len, raw_off[j], raw_len[j]);
+            }
+            raw_kid[base + cnt] = kid;
+            raw_off[base + cnt] = off;
+            raw_len[base + cnt] = len;
+            raw_keep[base + cnt] = dup ? 0u : 1u;
+            kept += dup ? 0 : 1;
+        }
+        cnt++;
+    };
+    Cur c;
+    for (uint64_t k = c0; k <= c1 && !bad; k++) {
+        // every command component in order, then the notary component
+        int64_t kk;
+        if (k < c1) {
+            if (comp_group[k] != 2) continue;
+            kk = (int64_t)k;
+        } else {
+            if (!want_notary) break;
+            kk = notary;
+        }
+        const uint64_t a = comp_off[kk];
+        c.init(r.pool, pool_bytes, a, a + comp_len[kk]);
+        if (!header_ok(c)) {
+            bad = true;
+            break;
+        }
+        const bool is_cmd = k < c1;
+        if (c.read_class<0>() != (is_cmd ? -C_COMMAND : -C_PARTY)) c.fail(E_UNSUP);
+        c.not_null<0>();
+        if (is_cmd) c.header<0>(H_CMD, 7, 2);
+        else c.header<0>(H_PARTY, 9, 2);
+        c.rem1 = 0;
+        const uint32_t nk = is_cmd ? c.list<1>(true) : 1;
+        for (uint32_t i = 0; i < nk && !c.err; i++) {
+            if (c.read_class<1>() < 14) c.fail(E_UNSUP);
+            c.not_null<1>();
+            const uint32_t kl = c.varint<1>();
+            const uint64_t at = run1<false>(c, kl, none, spill);
+            if (c.err || spill) break;
+            take(at, kl);
+        }
+        if (c.err || spill) bad = true;
+    }
+    if (!EMIT) {
+        if (bad) status[t] = CHIP_STX_UNSUPPORTED;
+        nraw[t] = bad ? 0 : cnt;
+    } else {
+        nreq[t] = kept;
+    }
+}
+
+// required key r = the kept entries in order: one leaf node each (node r, key index or NO_SIGNER)
+__global__ void __launch_bounds__(256) k_stx_req_compact(uint64_t nraw, const uint32_t* __restrict__ raw_kid,
+                                                         const uint32_t* __restrict__ raw_keep,
+                                                         const uint32_t* __restrict__ keep_incl,
+                                                         uint64_t* __restrict__ node_start, uint32_t* __restrict__ node_val,
+                                                         uint32_t* __restrict__ node_nkids,
+                                                         uint32_t* __restrict__ node_weight) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nraw || !raw_keep[i]) return;
+    const uint32_t q = keep_incl[i] - 1;
+    node_val[q] = raw_kid[i];
+    node_nkids[q] = 0;
+    node_weight[q] = 1;
+    node_start[q + 1] = q + 1;
+}
+
 inline dim3 grid_of(uint64_t n) { return dim3((uint32_t)((n + 255) / 256)); }
 
 }  // namespace
@@ -709,4 +868,28 @@ void launch_stx_keys(hipStream_t st, uint64_t nsig, const StxOut& d, uint64_t ma
     hipcub::DeviceScan::InclusiveSum(temp, temp_bytes, d.kflag, d.kincl, (int)nsig, st);
     hipLaunchKernelGGL(k_stx_key_assign, grid_of(nsig), dim3(256), 0, st, nsig, d.krep, d.kflag, d.kincl, d.skey_off,
                        d.skey_len, d.key_idx, d.key_off, d.key_len);
+}
+
+void launch_stx_required(hipStream_t st, bool emit, uint64_t n, uint8_t* status, const StxOut& d, uint64_t pool_bytes,
+                         uint64_t mask, const StxReq& q) {
+    if (!n) return;
+    ReqCtx r{d.pool, reinterpret_cast<const unsigned long long*>(d.tab), d.tab_min, mask, d.skey_off, d.skey_len, d.kincl};
+    if (!emit)
+        hipLaunchKernelGGL(k_stx_required<false>, grid_of(n), dim3(256), 0, st, n, status, d.comp_start, d.comp_group,
+                           d.comp_off, d.comp_len, pool_bytes, r, q.nraw, nullptr, nullptr, nullptr, nullptr, nullptr,
+                           nullptr);
+    else
+        hipLaunchKernelGGL(k_stx_required<true>, grid_of(n), dim3(256), 0, st, n, status, d.comp_start, d.comp_group,
+                           d.comp_off, d.comp_len, pool_bytes, r, nullptr, q.raw_start, q.raw_kid, q.raw_off, q.raw_len,
+                           q.raw_keep, q.nreq);
+}
+
+hipError_t stx_scan_u32(hipStream_t st, void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, uint64_t n) {
+    return hipcub::DeviceScan::InclusiveSum(temp, temp_bytes, in, out, (int)n, st);
+}
+
+void launch_stx_req_compact(hipStream_t st, uint64_t nraw, const StxReq& q) {
+    if (!nraw) return;
+    hipLaunchKernelGGL(k_stx_req_compact, grid_of(nraw), dim3(256), 0, st, nraw, q.raw_kid, q.raw_keep, q.keep_incl,
+                       q.node_start, q.node_val, q.node_nkids, q.node_weight);
 }

@@ -73,7 +73,8 @@ struct chip_ctx {
     // Kryo front end (kryo.hip): counts, ranges, pool, batches, key interning, scan scratch
     DevBuf s_ncomp, s_nsig, s_nbytes, s_cstart, s_sstart, s_pstart, s_pool, s_salts, s_cgroup, s_cint, s_coff, s_clen,
         s_txidx, s_tmpl, s_soff, s_slen, s_skoff, s_sklen, s_meta, s_tab, s_tabmin, s_kslot, s_krep, s_kflag, s_kincl,
-        s_kidx, s_koff, s_klen, s_temp;
+        s_kidx, s_koff, s_klen, s_temp, r_nraw, r_rstart, r_kid, r_len, r_keep, r_kincl, r_off, r_nreq, r_qstart,
+        r_nstart, r_val, r_nk, r_w;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, tev0 = nullptr, tev1 = nullptr;
     bool ev_pending = false, tev_pending = false;
     chip_stats stats{};
@@ -378,7 +379,8 @@ void chip_shutdown(chip_ctx* c) {
                       &c->s_salts, &c->s_cgroup, &c->s_cint, &c->s_coff, &c->s_clen, &c->s_txidx, &c->s_tmpl,
                       &c->s_soff, &c->s_slen, &c->s_skoff, &c->s_sklen, &c->s_meta, &c->s_tab, &c->s_tabmin,
                       &c->s_kslot, &c->s_krep, &c->s_kflag, &c->s_kincl, &c->s_kidx, &c->s_koff, &c->s_klen,
-                      &c->s_temp};
+                      &c->s_temp, &c->r_nraw, &c->r_rstart, &c->r_kid, &c->r_len, &c->r_keep, &c->r_kincl,
+                      &c->r_off, &c->r_nreq, &c->r_qstart, &c->r_nstart, &c->r_val, &c->r_nk, &c->r_w};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < chip_ctx::KRING; i++) {
         if (c->kring[i].a) hipEventDestroy(c->kring[i].a);
@@ -823,8 +825,67 @@ int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_sta
     HIPCHK(c, hipGetLastError());
     uint32_t nkeys = 0;
     if (nsig) HIPCHK(c, hipMemcpyAsync(&nkeys, c->s_kincl.as<uint32_t>() + nsig - 1, 4, hipMemcpyDeviceToHost, st));
-    c->kend(kc, st);
-    HIPCHK(c, hipStreamSynchronize(st));
+    if (in->flags & CHIP_STX_REQUIRED) {
+        // requiredSigningKeys: R1 counts signer entries, scan, R2 writes them + duplicate flags, scans,
+        // compaction into one leaf per distinct required key
+        StxReq q{};
+        HIPCHK(c, c->r_nraw.ensure(n1 * 8));
+        HIPCHK(c, c->r_rstart.ensure(n1 * 8));
+        HIPCHK(c, c->r_nreq.ensure(n1 * 8));
+        HIPCHK(c, c->r_qstart.ensure(n1 * 8));
+        q.nraw = c->r_nraw.as<uint64_t>();
+        q.raw_start = c->r_rstart.as<uint64_t>();
+        q.nreq = c->r_nreq.as<uint64_t>();
+        launch_stx_required(st, false, n, tx_status, d, pool, cap - 1, q);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemsetAsync(q.raw_start, 0, 8, st));
+        if (n) HIPCHK(c, stx_scan_u64(st, c->s_temp.p, c->s_temp.cap, q.nraw, q.raw_start + 1, n));
+        uint64_t nraw = 0;
+        HIPCHK(c, hipMemcpyAsync(&nraw, q.raw_start + n, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        if (nraw >= (1ull << 31)) return fail(c, CHIP_E_ARG, "too many required keys");
+        for (DevBuf* b : {&c->r_kid, &c->r_len, &c->r_keep, &c->r_kincl, &c->r_val, &c->r_nk, &c->r_w})
+            HIPCHK(c, b->ensure(nraw * 4 + 16));
+        HIPCHK(c, c->r_off.ensure(nraw * 8 + 16));
+        HIPCHK(c, c->r_nstart.ensure(nraw * 8 + 16));
+        if (stx_scan_temp_bytes(nraw > 2 ? nraw : 2) > c->s_temp.cap)
+            HIPCHK(c, c->s_temp.ensure(stx_scan_temp_bytes(nraw > 2 ? nraw : 2)));
+        q.raw_kid = c->r_kid.as<uint32_t>();
+        q.raw_len = c->r_len.as<uint32_t>();
+        q.raw_keep = c->r_keep.as<uint32_t>();
+        q.keep_incl = c->r_kincl.as<uint32_t>();
+        q.raw_off = c->r_off.as<uint64_t>();
+        q.node_start = c->r_nstart.as<uint64_t>();
+        q.node_val = c->r_val.as<uint32_t>();
+        q.node_nkids = c->r_nk.as<uint32_t>();
+        q.node_weight = c->r_w.as<uint32_t>();
+        launch_stx_required(st, true, n, tx_status, d, pool, cap - 1, q);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemsetAsync(c->r_qstart.p, 0, 8, st));
+        if (n) HIPCHK(c, stx_scan_u64(st, c->s_temp.p, c->s_temp.cap, q.nreq, c->r_qstart.as<uint64_t>() + 1, n));
+        HIPCHK(c, hipMemsetAsync(q.node_start, 0, 8, st));
+        if (nraw) HIPCHK(c, stx_scan_u32(st, c->s_temp.p, c->s_temp.cap, q.raw_keep, q.keep_incl, nraw));
+        launch_stx_req_compact(st, nraw, q);
+        HIPCHK(c, hipGetLastError());
+        uint64_t nreq = 0;
+        HIPCHK(c, hipMemcpyAsync(&nreq, c->r_qstart.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
+        c->kend(kc, st);
+        HIPCHK(c, hipStreamSynchronize(st));
+        chip_req_batch& rq = out->req;
+        rq.ntx = n;
+        rq.sig_start = d.sig_start;
+        rq.req_start = c->r_qstart.as<uint64_t>();
+        rq.nreq = nreq;
+        rq.node_start = q.node_start;
+        rq.allowed = nullptr;
+        rq.n_nodes = nreq;
+        rq.node_val = q.node_val;
+        rq.node_nkids = q.node_nkids;
+        rq.node_weight = q.node_weight;
+    } else {
+        c->kend(kc, st);
+        HIPCHK(c, hipStreamSynchronize(st));
+    }
     chip_tx_batch& t = out->txs;
     t.ntx = n;
     t.salts = d.salts;

@@ -84,6 +84,20 @@ void launch_stx_emit(hipStream_t st, const chip_stx_blobs* in, uint8_t* status, 
 size_t stx_scan_temp_bytes(uint64_t n);
 hipError_t stx_scan_u64(hipStream_t st, void* temp, size_t temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n);
 void launch_stx_keys(hipStream_t st, uint64_t nsig, const StxOut& d, uint64_t mask, void* temp, size_t temp_bytes);
+// requiredSigningKeys from the command / notary components (after launch_stx_keys)
+struct StxReq {
+    uint64_t* nraw;         // [n] signer entries per tx (R1)
+    uint64_t* raw_start;    // [n + 1]
+    uint32_t *raw_kid, *raw_len, *raw_keep, *keep_incl;
+    uint64_t* raw_off;
+    uint64_t* nreq;         // [n] distinct required keys per tx (R2)
+    uint64_t* node_start;   // [nreq_total + 1]
+    uint32_t *node_val, *node_nkids, *node_weight;
+};
+void launch_stx_required(hipStream_t st, bool emit, uint64_t n, uint8_t* status, const StxOut& d, uint64_t pool_bytes,
+                         uint64_t mask, const StxReq& q);
+hipError_t stx_scan_u32(hipStream_t st, void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, uint64_t n);
+void launch_stx_req_compact(hipStream_t st, uint64_t nraw, const StxReq& q);
 
 // sizes of the per-key device tables (words per key)
 #define ED_KEY_TABLE_WORDS (9 * 40)

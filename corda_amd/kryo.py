@@ -703,3 +703,127 @@ def stx_parse(buf: bytes):
     if wire_invariant_error(groups) is not None:
         return STX_INVARIANT, None, None, None
     return STX_OK, groups, salt, sigs
+
+
+# ---- component contents the front end reads: Command.signers, the notary Party's owningKey ----
+COMMAND = "net.corda.core.contracts.Command"
+PARTY = "net.corda.core.identity.Party"
+CORDA_X500_NAME = "net.corda.core.identity.CordaX500Name"
+COMMAND_FIELDS = ["Command.signers", "Command.value"]
+PARTY_FIELDS = ["AbstractParty.owningKey", "Party.name"]
+
+
+def _key_object(g: Graph, o: Out, key: bytes, key_class_id) -> None:
+    """A PublicKey through an interface-typed slot: class, marker, PublicKeySerializer
+    (writeBytesWithLength of the X.509 encoding, Kryo.kt:299-310)."""
+    g.write_class(o, key_class_id)
+    g.marker(o)
+    o.write_varint(len(key))
+    o.write_bytes(key)
+
+
+def command(signers: Sequence[bytes], value_class: str = "net.corda.finance.contracts.asset.Cash$Commands$Move",
+            key_class_id=DEFAULT_IDS["eddsa_public_key"], list_kind="auto") -> bytes:
+    """Command(value, signers).serialize().bytes (Structures.kt:179-185): a CompatibleFieldSerializer
+    object whose fields sort as Command.signers, Command.value; the value here is an object of
+    `value_class` with no fields (the front end reads only the signers)."""
+    g = Graph()
+    o = Out()
+    o.write_bytes(KRYO_HEADER_V0_1)
+    g.write_class(o, COMMAND)
+    g.marker(o)
+
+    def value(c: Out):
+        g.write_class(c, value_class)
+        g.marker(c)
+        g.compatible(c, value_class, [])
+
+    g.compatible(o, COMMAND, [
+        ("Command.signers", lambda c: _list(g, c, list(signers), lambda f, k: _key_object(g, f, k, key_class_id),
+                                            list_kind)),
+        ("Command.value", value)])
+    return o.getvalue()
+
+
+def party(owning_key: bytes, name: str = "O=Notary Service,L=Zurich,C=CH",
+          key_class_id=DEFAULT_IDS["eddsa_public_key"]) -> bytes:
+    """Party(name, owningKey).serialize().bytes (Party.kt:29, AbstractParty.kt:13): fields sort as
+    AbstractParty.owningKey, Party.name; the name is a CordaX500Name with its string fields."""
+    g = Graph()
+    o = Out()
+    o.write_bytes(KRYO_HEADER_V0_1)
+    g.write_class(o, PARTY)
+    g.marker(o)
+
+    def name_field(c: Out):
+        g.marker(c)                              # CordaX500Name is final: marker + object
+        parts = dict(p.split("=", 1) for p in name.split(","))
+
+        def s(v):
+            def w(f: Out):
+                if v is None:
+                    f.write_byte(0x80)           # writeString(null)
+                else:
+                    f.write_string(v)
+            return w
+        g.compatible(c, CORDA_X500_NAME, [
+            ("CordaX500Name.commonName", s(parts.get("CN"))), ("CordaX500Name.country", s(parts.get("C"))),
+            ("CordaX500Name.locality", s(parts.get("L"))), ("CordaX500Name.organisation", s(parts.get("O"))),
+            ("CordaX500Name.organisationUnit", s(parts.get("OU"))), ("CordaX500Name.state", s(parts.get("ST")))])
+
+    g.compatible(o, PARTY, [
+        ("AbstractParty.owningKey", lambda c: _key_object(g, c, owning_key, key_class_id)),
+        ("Party.name", name_field)])
+    return o.getvalue()
+
+
+def _read_key_object(r: Reader) -> bytes:
+    kid = r.read_class()
+    if not isinstance(kid, int) or kid < FIRST_UNPINNED_ID:
+        raise KryoUnsupported("key class is not a registered PublicKey class")
+    r.not_null()
+    return r.take(r.varint())
+
+
+def command_signers(buf: bytes) -> List[bytes]:
+    """Command.signers of a command component (the value is not read)."""
+    r = _header(buf)
+    if r.read_class() != COMMAND:
+        raise KryoUnsupported("not a Command")
+    r.not_null()
+    _expect_fields(r, COMMAND, COMMAND_FIELDS)
+    return _read_list(r.chunk(), True, _read_key_object)
+
+
+def party_owning_key(buf: bytes) -> bytes:
+    """AbstractParty.owningKey of a notary component."""
+    r = _header(buf)
+    if r.read_class() != PARTY:
+        raise KryoUnsupported("not a Party")
+    r.not_null()
+    _expect_fields(r, PARTY, PARTY_FIELDS)
+    return _read_key_object(r.chunk())
+
+
+def required_signing_keys(groups: Sequence[Tuple[int, Sequence[bytes]]]) -> List[bytes]:
+    """WireTransaction.requiredSigningKeys (WireTransaction.kt:66-75): commands.flatMap { signers }
+    .toSet() + notary.owningKey when the transaction has inputs or a time-window, in first-appearance
+    order (the order of the device's required-key ranges).  Keys compare by their encoding."""
+    out: List[bytes] = []
+    seen = set()
+    present = {gi for gi, _ in groups}
+    for gi, comps in groups:
+        if gi == GROUP_COMMANDS:
+            for c in comps:
+                for k in command_signers(c):
+                    if k not in seen:
+                        seen.add(k)
+                        out.append(k)
+    if GROUP_NOTARY in present and (GROUP_INPUTS in present or GROUP_TIMEWINDOW in present):
+        for gi, comps in groups:
+            if gi == GROUP_NOTARY:
+                k = party_owning_key(comps[0])
+                if k not in seen:
+                    seen.add(k)
+                    out.append(k)
+    return out

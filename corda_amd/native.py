@@ -84,11 +84,7 @@ class ChipSignerBatch(ctypes.Structure):
 class ChipStxBlobs(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint64), ("data", ctypes.c_void_p), ("off", ctypes.c_void_p), ("len", ctypes.c_void_p),
                 ("data_bytes", ctypes.c_uint64), ("meta", ctypes.c_void_p), ("n_meta", ctypes.c_uint32),
-                ("pad", ctypes.c_uint32)]
-
-
-class ChipStxParsed(ctypes.Structure):
-    _fields_ = [("txs", ChipTxBatch), ("sigs", ChipSignerBatch), ("sig_start", ctypes.c_void_p)]
+                ("flags", ctypes.c_uint32)]
 
 
 class ChipFtxBatch(ctypes.Structure):
@@ -137,6 +133,14 @@ def make_req_batch(q) -> ChipReqBatch:
     s.n_nodes = len(q.node_val)
     s.node_val, s.node_nkids, s.node_weight = _ptr(q.node_val), _ptr(q.node_nkids), _ptr(q.node_weight)
     return s
+
+
+STX_REQUIRED = 0x1
+
+
+class ChipStxParsed(ctypes.Structure):
+    _fields_ = [("txs", ChipTxBatch), ("sigs", ChipSignerBatch), ("sig_start", ctypes.c_void_p),
+                ("req", ChipReqBatch)]
 
 
 class ChipUniqShardBatch(ctypes.Structure):
@@ -444,13 +448,15 @@ class Context:
                                                                 stream or None))
 
     # ---- Kryo front end: SignedTransaction bytes -> batches (device) ----
-    def stx_parse_device(self, data, off, lens, data_bytes, meta, tx_status, stream=None) -> ChipStxParsed:
+    def stx_parse_device(self, data, off, lens, data_bytes, meta, tx_status, stream=None,
+                         required: bool = False) -> ChipStxParsed:
         """data / off / lens / tx_status: device tensors; meta: host int32 [n_meta, 2] (platformVersion,
         schemeNumberID) per message template.  Returns the chip_stx_parsed of device pointers (valid
         until the next call on this context)."""
         meta = np.ascontiguousarray(np.asarray(meta, dtype=np.int32).reshape(-1, 2))
         b = ChipStxBlobs(n=int(off.numel() if hasattr(off, "numel") else len(off)), data=_ptr(data), off=_ptr(off),
-                         len=_ptr(lens), data_bytes=int(data_bytes), meta=meta.ctypes.data, n_meta=len(meta), pad=0)
+                         len=_ptr(lens), data_bytes=int(data_bytes), meta=meta.ctypes.data, n_meta=len(meta),
+                         flags=STX_REQUIRED if required else 0)
         out = ChipStxParsed()
         self._check(self.lib.chip_stx_parse_device(self.h, ctypes.byref(b), _ptr(tx_status), ctypes.byref(out),
                                                    stream or None))
@@ -465,8 +471,10 @@ class Context:
 
     def verify_signed_tx_parsed_device(self, parsed: ChipStxParsed, dev_templates, dev_q, ids, status, verdict, arg,
                                        missing=None, stream=None):
-        """chip_verify_signed_tx_batch_device over a parsed batch (its sig_start must be dev_q's)."""
-        tm, rq = make_templates(dev_templates), make_req_batch(dev_q)
+        """chip_verify_signed_tx_batch_device over a parsed batch (its sig_start must be dev_q's); dev_q None =
+        the required keys the parse derived (required=True)."""
+        tm = make_templates(dev_templates)
+        rq = parsed.req if dev_q is None else make_req_batch(dev_q)
         self._check(self.lib.chip_verify_signed_tx_batch_device(self.h, ctypes.byref(parsed.txs), ctypes.byref(tm),
                                                                 ctypes.byref(parsed.sigs), ctypes.byref(rq), _ptr(ids),
                                                                 _ptr(status), _ptr(verdict), _ptr(arg), _ptr(missing),

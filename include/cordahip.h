@@ -353,7 +353,14 @@ int chip_verify_signed_tx_batch_device(chip_ctx* ctx, const chip_tx_batch* txs, 
  *               occurrence in the signature list (equal SPKI bytes = one key)
  *   out->sig_start  [n + 1] each transaction's signature range (list order), for chip_req_batch
  * so that chip_verify_signed_tx_batch_device(ctx, &out->txs, tmpl, &out->sigs, req, ...) verifies the batch.
- * Synchronises with `stream` twice (the totals size the outputs). */
+ * With CHIP_STX_REQUIRED the library also derives `req` on the device: WireTransaction.requiredSigningKeys
+ * (WireTransaction.kt:66-75) = the signers of every Command component (Command.signers, read without the
+ * command value) in first-appearance order, then the notary Party's owningKey when the transaction has
+ * inputs or a time-window, without duplicates; each required key is one leaf (its index in out->sigs' key
+ * pool, or CHIP_REQ_NO_SIGNER), req.sig_start = out->sig_start, allowed = NULL.  A command / notary
+ * component outside the device grammar, a chunk-spanning key or a CompositeKey among the required keys
+ * (its tree is not in the signer pool) turns the transaction's status into CHIP_STX_UNSUPPORTED.
+ * Synchronises with `stream` twice (four times with CHIP_STX_REQUIRED): the totals size the outputs. */
 enum chip_stx_status { CHIP_STX_OK = 0, CHIP_STX_KRYO = 1, CHIP_STX_NO_SIGS = 2, CHIP_STX_INVARIANT = 3,
                        CHIP_STX_UNSUPPORTED = 4 };
 typedef struct {
@@ -364,12 +371,14 @@ typedef struct {
     uint64_t data_bytes;
     const int32_t* meta;       /* [2 * n_meta] HOST memory: SignatureMetadata of template i   */
     uint32_t n_meta;
-    uint32_t pad;
+    uint32_t flags;            /* CHIP_STX_REQUIRED: also derive out->req from the components */
 } chip_stx_blobs;
+#define CHIP_STX_REQUIRED 0x1u
 typedef struct {
     chip_tx_batch txs;
     chip_signer_batch sigs;
     const uint64_t* sig_start;
+    chip_req_batch req;        /* with CHIP_STX_REQUIRED; else zeroed */
 } chip_stx_parsed;
 int chip_stx_parse_device(chip_ctx* ctx, const chip_stx_blobs* in, uint8_t* tx_status, chip_stx_parsed* out,
                           void* stream);

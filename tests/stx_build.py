@@ -112,3 +112,74 @@ def cases(seed: int = 7, n_valid: int = 200):
                if b"java.util.ArrayLis\xf4" in ok else ok.replace(b"java.util.Collections$SingletonLis\xf4",
                                                                      b"java.util.Collections$SingletonSe\xf4", 1))
     return out
+
+
+def cases_required(seed: int = 13, n: int = 240):
+    """SignedTransactions whose command / notary components are real Kryo Command / Party objects:
+    requiredSigningKeys = commands' signers (several commands, repeated and non-signing keys, every list
+    class) + the notary when there are inputs or a time-window; plus a CompositeKey signer, a malformed
+    command and a command of another class (-> UNSUPPORTED)."""
+    from corda_amd import composite as CK
+    rng = np.random.default_rng(seed)
+    pool = [_key(rng, ED_KEY) for _ in range(10)] + [_key(rng, 91), _key(rng, 88)]
+    comp = CK.CompositeKey.Builder().add_keys(pool[0], pool[1]).build(1).encoded \
+        if hasattr(CK.CompositeKey, "Builder") else None
+    out = []
+    for i in range(n):
+        signers_of_cmds = [[pool[int(rng.integers(0, len(pool)))] for _ in range(int(rng.integers(1, 4)))]
+                           for _ in range(int(rng.integers(1, 3)))]
+        notary_key = pool[int(rng.integers(0, len(pool)))]
+        kind = rng.random()
+        groups = []
+        has_in = rng.random() < 0.6
+        if has_in:
+            groups.append((0, [rng.bytes(40) + bytes([j]) for j in range(int(rng.integers(1, 3)))]))
+        groups.append((1, [rng.bytes(int(rng.integers(20, 900)))]))
+        cmds = []
+        for ss in signers_of_cmds:
+            lk = "auto" if len(ss) == 1 else ("aslist", 31) if rng.random() < 0.3 else "array"
+            cmds.append(K.command(ss, list_kind=lk if lk[0] != "aslist" else ("aslist", K.DEFAULT_IDS["eddsa_public_key"])))
+        if kind < 0.03 and comp is not None:
+            cmds.append(K.command([comp]))                                 # CompositeKey signer
+        elif kind < 0.06:
+            cmds.append(K.command(signers_of_cmds[0])[:40])                 # truncated inside the signers
+        elif kind < 0.08:
+            cmds[0] = cmds[0].replace(b"net.corda.core.contracts.Comman\xe4", b"net.corda.core.contracts.Commanx\xe4", 1)
+        groups.append((2, cmds))
+        if has_in or rng.random() < 0.5:
+            groups.append((4, [K.party(notary_key)]))
+            if rng.random() < 0.3:
+                groups.append((5, [rng.bytes(40)]))
+        req_all = [k for ss in signers_of_cmds for k in ss] + [notary_key]
+        sig_keys = [req_all[int(rng.integers(0, len(req_all)))] for _ in range(int(rng.integers(1, 4)))]
+        sigs = [K.Sig(rng.bytes(64) if len(k) == ED_KEY else rng.bytes(71), k, 1, 4, 31) for k in sig_keys]
+        out.append(blob(groups, rng.bytes(32), sigs))
+    return out
+
+
+def expected_required(blobs):
+    """Host mirror of chip_stx_parse_device(..., CHIP_STX_REQUIRED): per blob (status, [required key
+    bytes]) and the signer key numbering (first occurrence over the signatures of the transactions the
+    parse passes accepted, before the required-key stage)."""
+    from corda_amd import composite as CK
+    parsed = [K.stx_parse(b) for b in blobs]
+    kid = {}
+    for st, g, salt, sigs in parsed:
+        if st == K.STX_OK:
+            for sig, key, pv, sch in sigs:
+                kid.setdefault(key, len(kid))
+    out = []
+    for st, g, salt, sigs in parsed:
+        if st != K.STX_OK:
+            out.append((st, None))
+            continue
+        try:
+            req = K.required_signing_keys(g)
+        except K.KryoException:
+            out.append((K.STX_UNSUPPORTED, None))
+            continue
+        if any(k not in kid and CK._spki_oid(k) == CK._COMPOSITE_OID_TLV for k in req):
+            out.append((K.STX_UNSUPPORTED, None))
+            continue
+        out.append((K.STX_OK, req))
+    return out, kid

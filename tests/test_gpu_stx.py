@@ -140,3 +140,64 @@ def test_verify_from_bytes_equals_structured_path(ctx):
     assert np.array_equal(d_missing.cpu().numpy()[:dq2.nreq], missing)
     assert int((status == 0).sum()) > 0 and int((verdict != 0).sum()) > 0
 
+
+
+def test_required_keys_derived_on_device(ctx):
+    """CHIP_STX_REQUIRED: requiredSigningKeys read from the Command / notary Party components on the
+    device equal the host mirror (kryo.required_signing_keys): per transaction the distinct keys in
+    first-appearance order as leaves of the signer key pool (or NO_SIGNER), UNSUPPORTED for a
+    CompositeKey signer or a damaged command."""
+    blobs = S.cases_required(seed=13, n=300) + S.cases(seed=5, n_valid=40)
+    want, kid = S.expected_required(blobs)
+    data, off, ln = G.stx_blobs_from_lists(blobs)
+    dd, doff, dlen = _dev(data), _dev(off), _dev(ln)
+    st = torch.zeros(len(blobs), dtype=torch.uint8, device=DEV)
+    p = ctx.stx_parse_device(dd, doff, dlen, len(data), METAS, st, required=True)
+    torch.cuda.synchronize()
+    got = st.cpu().numpy()
+    n = len(blobs)
+    assert list(got) == [w[0] for w in want]
+    assert int((got == K.STX_UNSUPPORTED).sum()) >= 5 and int((got == K.STX_OK).sum()) > 250
+    q = p.req
+    assert q.ntx == n and q.n_nodes == q.nreq and not q.allowed
+    rstart = ctx.copy_to_host(q.req_start, n + 1, np.uint64)
+    nstart = ctx.copy_to_host(q.node_start, q.nreq + 1, np.uint64)
+    val = ctx.copy_to_host(q.node_val, q.nreq, np.uint32)
+    nk = ctx.copy_to_host(q.node_nkids, q.nreq, np.uint32)
+    assert np.array_equal(nstart, np.arange(q.nreq + 1)) and not nk.any()
+    assert q.sig_start == p.sig_start
+    for t, (status, req) in enumerate(want):
+        r0, r1 = int(rstart[t]), int(rstart[t + 1])
+        if status != K.STX_OK:
+            assert r0 == r1, t
+            continue
+        exp = [kid.get(k, G.REQ_NO_SIGNER) for k in req]
+        assert list(val[r0:r1]) == exp, t
+
+
+def test_verify_from_bytes_with_derived_required_keys(ctx):
+    """cfg4 with real Command / Party components: the whole verifySignaturesExcept from the bytes alone
+    (ids, SignableData messages, signatures, requiredSigningKeys on the device) gives the labelled
+    verdicts: OK, SignatureException at the first corrupted signature, SignaturesMissingException
+    when the command names a party that did not sign."""
+    ntx = 3000
+    tb, tm, sb, ids_ref, verdict, arg = G.cfg4_workload_commands(ntx, n_keys=64, seed=0x5EED0304, threads=8)
+    data, off, ln = G.stx_uniform(tb, sb, 2)
+    dd, doff, dlen = _dev(data), _dev(off), _dev(ln)
+    st = torch.zeros(ntx, dtype=torch.uint8, device=DEV)
+    p = ctx.stx_parse_device(dd, doff, dlen, len(data), np.array([[1, 4]], np.int32), st, required=True)
+    assert int((st != 0).sum()) == 0
+    dtm = G.Templates()
+    dtm.data, dtm.off, dtm.len, dtm.id_at, dtm.max_len = _dev(tm.data), _dev(tm.off), _dev(tm.len), _dev(tm.id_at), tm.max_len
+    d_ids = torch.zeros(ntx * 32, dtype=torch.uint8, device=DEV)
+    d_status = torch.zeros(sb.n, dtype=torch.uint8, device=DEV)
+    d_verdict = torch.zeros(ntx, dtype=torch.uint8, device=DEV)
+    d_arg = torch.zeros(ntx, dtype=torch.int32, device=DEV)
+    d_missing = torch.zeros(max(p.req.nreq, 1), dtype=torch.uint8, device=DEV)
+    ctx.verify_signed_tx_parsed_device(p, dtm, None, d_ids, d_status, d_verdict, d_arg, d_missing)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_ids.cpu().numpy().reshape(ntx, 32), ids_ref)
+    assert np.array_equal(d_status.cpu().numpy(), sb.expected)
+    assert np.array_equal(d_verdict.cpu().numpy(), verdict)
+    assert np.array_equal(d_arg.cpu().numpy().view(np.uint32), arg)
+    assert set(np.unique(verdict)) == {0, 1, 2}

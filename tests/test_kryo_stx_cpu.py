@@ -79,3 +79,25 @@ def test_uniform_filler_equals_writer():
         st, groups, salt, sigs = K.stx_parse(b)
         assert st == K.STX_OK and salt == tb.salts[32 * t:32 * t + 32].tobytes()
         assert [len(c) for _, cs in groups for c in cs] == [96, 96, 640, 640, 320, 96, 384, 96]
+
+
+def test_device_name_tables_match_the_restatement():
+    """The class / field names and lengths the device grammar compares against (kryo.hip constant tables)
+    are the restatement's (kryo.py)."""
+    import os
+    import re
+    src = open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                            "corda_amd", "csrc", "kryo.hip")).read()
+
+    def table(arr, lens):
+        body = src[src.index("__constant__ char %s" % arr):]
+        names = re.findall(r'"([^"]*)"', body[:body.index("};")])
+        lb = src[src.index("__constant__ uint8_t %s" % lens):]
+        return names, [int(x) for x in lb[lb.index("{") + 1:lb.index("}")].split(",")]
+
+    names, lens = table("k_names", "k_name_len")
+    assert names == [K.ARRAY_LIST, K.SINGLETON_LIST, K.TRANSACTION_SIGNATURE, K.COMPONENT_GROUP, K.COMMAND, K.PARTY]
+    assert lens == [len(x) for x in names]
+    fields, flens = table("k_fields", "k_field_len")
+    assert fields == K.TXSIG_FIELDS + K.META_FIELDS + K.GROUP_FIELDS + K.COMMAND_FIELDS + K.PARTY_FIELDS
+    assert flens == [len(x) for x in fields]

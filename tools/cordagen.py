@@ -887,3 +887,62 @@ def required_for_parsed(q, sb):
     nv[leaf] = remap[np.minimum(nv[leaf], len(remap) - 1)]
     q2.node_val = nv.astype(np.uint32)
     return q2
+
+
+def ed25519_spkis(n_keys: int, extra_key_seeds=()) -> list:
+    """SPKI encodings of key_seed(0..n_keys-1) followed by extra_key_seeds (ed25519_signers' key pool)."""
+    seeds = b"".join(key_seed(i) for i in range(n_keys)) + b"".join(extra_key_seeds)
+    seeds_np = np.frombuffer(seeds, dtype=np.uint8).copy()
+    nk = len(seeds_np) // 32
+    pubs = np.zeros(nk * 32, dtype=np.uint8)
+    if lib().gen_pubs_many(SCHEME_ED25519, ctypes.c_uint64(nk), _p(seeds_np), _p(pubs)) != 0:
+        raise RuntimeError("keygen failed")
+    return [spki_ed25519(pubs[32 * i:32 * i + 32].tobytes()) for i in range(nk)]
+
+
+def cfg4_workload_commands(ntx: int, n_keys: int = 4096, seed: int = 0x5EED0004, corrupt: float = 0.01,
+                           p_missing: float = 0.01, threads: int = 8):
+    """cfg4 with real Kryo contents where requiredSigningKeys come from: the command component is
+    Command(Cash.Commands.Move, [signer]) and the notary component Party(notary name, notary key)
+    (corda_amd/kryo.py), so WireTransaction.requiredSigningKeys = {signer, notary}.  The owner of
+    each tx signs, and so does the notary; for p_missing of the transactions the command names another
+    party as its signer, which does not sign (-> SignaturesMissingException, 1 needed key).
+    -> (tb, tm, sb, ids, expected_verdict, expected_arg)."""
+    from corda_amd import kryo as K
+    rng = np.random.Generator(np.random.PCG64(seed + 7))
+    spkis = ed25519_spkis(n_keys, (NOTARY_SEED,))
+    owner = rng.integers(0, n_keys, size=ntx)
+    miss = rng.random(ntx) < p_missing
+    other = (owner + 1 + rng.integers(0, n_keys - 1, size=ntx)) % n_keys
+    signer = np.where(miss, other, owner)
+    cmd0 = np.frombuffer(K.command([bytes(44)]), dtype=np.uint8)
+    cmd1 = np.frombuffer(K.command([b"\xff" * 44]), dtype=np.uint8)
+    kpos = np.nonzero(cmd0 != cmd1)[0]
+    assert len(kpos) == 44 and np.all(np.diff(kpos) == 1)
+    party = np.frombuffer(K.party(spkis[n_keys]), dtype=np.uint8)
+    profile = [(g, [len(cmd0)] if g == 2 else [len(party)] if g == 4 else ss) for g, ss in CFG4_PROFILE]
+    tb = tx_batch(ntx, profile=profile, seed=seed)
+    per = sum(len(ss) for _, ss in profile)
+    sizes = [s for _, ss in profile for s in ss]
+    groups = [g for g, ss in profile for _ in ss]
+    per_bytes = sum(sizes)
+    view = tb.data[:ntx * per_bytes].reshape(ntx, per_bytes)
+    at = 0
+    kp = np.stack([np.frombuffer(k, dtype=np.uint8) for k in spkis])
+    for g, sz in zip(groups, sizes):
+        if g == 2:
+            view[:, at:at + sz] = cmd0
+            view[:, at + kpos[0]:at + kpos[0] + 44] = kp[signer]
+        elif g == 4:
+            view[:, at:at + sz] = party
+        at += sz
+    assert per == len(sizes)
+    ids = txids(tb, threads)
+    keys = np.stack([owner, np.full(ntx, n_keys)], axis=1)
+    sb, tm, _msgs = ed25519_signers(ids, keys, n_keys, corrupt=corrupt, seed=seed + 2, threads=threads,
+                                    extra_key_seeds=(NOTARY_SEED,))
+    bad = sb.expected.reshape(ntx, 2) != 0
+    verdict = np.where(bad.any(axis=1), 1, np.where(miss, 2, 0)).astype(np.uint8)
+    first_bad = np.where(bad[:, 0], 0, 1) + np.arange(ntx) * 2          # global index of the first failing sig
+    arg = np.where(bad.any(axis=1), first_bad, np.where(miss, 1, 0)).astype(np.uint32)
+    return tb, tm, sb, ids, verdict, arg
