@@ -73,7 +73,8 @@ struct chip_ctx {
     // Kryo front end (kryo.hip): counts, ranges, pool, batches, key interning, scan scratch
     DevBuf s_ncomp, s_nsig, s_nbytes, s_cstart, s_sstart, s_pstart, s_pool, s_salts, s_cgroup, s_cint, s_coff, s_clen,
         s_txidx, s_tmpl, s_soff, s_slen, s_skoff, s_sklen, s_meta, s_tab, s_tabmin, s_kslot, s_krep, s_kflag, s_kincl,
-        s_kidx, s_koff, s_klen, s_temp, r_nraw, r_rstart, r_kid, r_len, r_keep, r_kincl, r_off, r_nreq, r_qstart,
+        s_kidx, s_koff, s_klen, s_temp, h2_data, h2_off, h2_len, h2_st, h2_ids, h2_v, h2_a, h2_sigst, h2_miss,
+        h2_td, h2_to, h2_tl, h2_ta, r_nraw, r_rstart, r_kid, r_len, r_keep, r_kincl, r_off, r_nreq, r_qstart,
         r_nstart, r_val, r_nk, r_w;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, tev0 = nullptr, tev1 = nullptr;
     bool ev_pending = false, tev_pending = false;
@@ -379,7 +380,8 @@ void chip_shutdown(chip_ctx* c) {
                       &c->s_salts, &c->s_cgroup, &c->s_cint, &c->s_coff, &c->s_clen, &c->s_txidx, &c->s_tmpl,
                       &c->s_soff, &c->s_slen, &c->s_skoff, &c->s_sklen, &c->s_meta, &c->s_tab, &c->s_tabmin,
                       &c->s_kslot, &c->s_krep, &c->s_kflag, &c->s_kincl, &c->s_kidx, &c->s_koff, &c->s_klen,
-                      &c->s_temp, &c->r_nraw, &c->r_rstart, &c->r_kid, &c->r_len, &c->r_keep, &c->r_kincl,
+                      &c->s_temp, &c->h2_data, &c->h2_off, &c->h2_len, &c->h2_st, &c->h2_ids, &c->h2_v,
+                      &c->h2_a, &c->h2_sigst, &c->h2_miss, &c->h2_td, &c->h2_to, &c->h2_tl, &c->h2_ta, &c->r_nraw, &c->r_rstart, &c->r_kid, &c->r_len, &c->r_keep, &c->r_kincl,
                       &c->r_off, &c->r_nreq, &c->r_qstart, &c->r_nstart, &c->r_val, &c->r_nk, &c->r_w};
     for (DevBuf* b : bufs) b->release();
     for (int i = 0; i < chip_ctx::KRING; i++) {
@@ -912,6 +914,60 @@ int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_sta
     s.sig_bytes = pool;
     s.key_bytes = pool;
     out->sig_start = d.sig_start;
+    return CHIP_OK;
+}
+
+int chip_stx_verify(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t* off, const uint32_t* len,
+                    uint64_t data_bytes, const chip_msg_templates* tmpl, const int32_t* meta, uint32_t n_meta,
+                    uint8_t* tx_status, uint8_t* verdict, uint32_t* arg, uint8_t* ids) {
+    if (!c || !tmpl) return fail(c, CHIP_E_ARG, "null argument");
+    if (!n) return CHIP_OK;
+    if (!data || !off || !len || !tx_status || !verdict || !arg) return fail(c, CHIP_E_ARG, "null array");
+    if (n_meta != tmpl->n) return fail(c, CHIP_E_ARG, "one SignatureMetadata per template");
+    for (uint64_t t = 0; t < n; t++)
+        if (off[t] + len[t] > data_bytes || off[t] + len[t] < off[t]) return fail(c, CHIP_E_ARG, "blob outside pool");
+    for (uint64_t i = 0; i < tmpl->n; i++)
+        if (tmpl->off[i] + tmpl->len[i] > tmpl->data_bytes || tmpl->id_at[i] > tmpl->len[i])
+            return fail(c, CHIP_E_ARG, "template outside pool");
+    hipStream_t st = c->stream;
+    chip_msg_templates dtm = *tmpl;
+    int r;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        HIPCHK(c, hipSetDevice(c->device));
+        if ((r = stage(c, c->h2_data, data, data_bytes, st)) || (r = stage(c, c->h2_off, off, n, st)) ||
+            (r = stage(c, c->h2_len, len, n, st)) || (r = stage(c, c->h2_td, tmpl->data, tmpl->data_bytes, st)) ||
+            (r = stage(c, c->h2_to, tmpl->off, tmpl->n, st)) || (r = stage(c, c->h2_tl, tmpl->len, tmpl->n, st)) ||
+            (r = stage(c, c->h2_ta, tmpl->id_at, tmpl->n, st)))
+            return r;
+        HIPCHK(c, c->h2_st.ensure(n + 16));
+        HIPCHK(c, c->h2_ids.ensure(n * 32 + 16));
+        HIPCHK(c, c->h2_v.ensure(n + 16));
+        HIPCHK(c, c->h2_a.ensure(n * 4 + 16));
+        dtm.data = c->h2_td.as<uint8_t>();
+        dtm.off = c->h2_to.as<uint64_t>();
+        dtm.len = c->h2_tl.as<uint32_t>();
+        dtm.id_at = c->h2_ta.as<uint32_t>();
+    }
+    chip_stx_blobs in{n, c->h2_data.as<uint8_t>(), c->h2_off.as<uint64_t>(), c->h2_len.as<uint32_t>(), data_bytes,
+                      meta, n_meta, CHIP_STX_REQUIRED};
+    chip_stx_parsed p;
+    if ((r = chip_stx_parse_device(c, &in, c->h2_st.as<uint8_t>(), &p, st))) return r;
+    {
+        std::lock_guard<std::mutex> g(c->mu);
+        HIPCHK(c, c->h2_sigst.ensure(p.sigs.n + 16));
+        HIPCHK(c, c->h2_miss.ensure(p.req.nreq + 16));
+    }
+    if ((r = chip_verify_signed_tx_batch_device(c, &p.txs, &dtm, &p.sigs, &p.req, c->h2_ids.as<uint8_t>(),
+                                                c->h2_sigst.as<uint8_t>(), c->h2_v.as<uint8_t>(),
+                                                c->h2_a.as<uint32_t>(), c->h2_miss.as<uint8_t>(), st)))
+        return r;
+    std::lock_guard<std::mutex> g(c->mu);
+    HIPCHK(c, hipMemcpyAsync(tx_status, c->h2_st.p, n, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(verdict, c->h2_v.p, n, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(arg, c->h2_a.p, n * 4, hipMemcpyDeviceToHost, st));
+    if (ids) HIPCHK(c, hipMemcpyAsync(ids, c->h2_ids.p, n * 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
     return CHIP_OK;
 }
 

@@ -39,7 +39,7 @@ EXPORTS = ["chip_abi_version", "chip_device_count", "chip_init", "chip_shutdown"
            "chip_verify_tx_batch", "chip_verify_tx_batch_device", "chip_ftx_verify_batch",
            "chip_ftx_verify_batch_device", "chip_required_signers", "chip_required_signers_device",
            "chip_verify_signed_tx_batch", "chip_verify_signed_tx_batch_device",
-           "chip_stx_parse_device", "chip_copy_to_host", "chip_get_stats", "chip_reset_stats"]
+           "chip_stx_parse_device", "chip_stx_verify", "chip_copy_to_host", "chip_get_stats", "chip_reset_stats"]
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
 u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -248,6 +248,10 @@ def load(build_if_missing: bool = False):
                                            ctypes.c_uint64, ctypes.POINTER(ctypes.c_uint64)]
     lib.chip_stx_parse_device.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipStxBlobs), ctypes.c_void_p,
                                           ctypes.POINTER(ChipStxParsed), ctypes.c_void_p]
+    lib.chip_stx_verify.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ChipMsgTemplates),
+                                    ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_void_p]
     lib.chip_copy_to_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
     lib.chip_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipStats)]
     lib.chip_reset_stats.argtypes = [ctypes.c_void_p]
@@ -462,6 +466,23 @@ class Context:
                                                    stream or None))
         out._meta = meta
         return out
+
+    def stx_verify(self, data, off, lens, templates, meta, want_ids: bool = False):
+        """Host arrays: SignedTransaction blobs -> (tx_status u8[n], verdict u8[n], arg u32[n], ids or None)
+        through chip_stx_verify (parse + requiredSigningKeys + the fused verify, on the device)."""
+        n = len(off)
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        meta = np.ascontiguousarray(np.asarray(meta, dtype=np.int32).reshape(-1, 2))
+        tm = make_templates(templates)
+        st = np.zeros(max(n, 1), dtype=np.uint8)
+        v = np.zeros(max(n, 1), dtype=np.uint8)
+        a = np.zeros(max(n, 1), dtype=np.uint32)
+        ids = np.zeros(max(n, 1) * 32, dtype=np.uint8) if want_ids else None
+        self._check(self.lib.chip_stx_verify(self.h, n, _ptr(data), _ptr(off), _ptr(lens), len(data), ctypes.byref(tm),
+                                             meta.ctypes.data, len(meta), _ptr(st), _ptr(v), _ptr(a), _ptr(ids)))
+        return st[:n], v[:n], a[:n], (ids[:32 * n].reshape(n, 32) if want_ids else None)
 
     def copy_to_host(self, ptr, count: int, dtype) -> np.ndarray:
         """A library-owned device array (e.g. a chip_stx_parsed field) -> host numpy array."""

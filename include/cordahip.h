@@ -382,6 +382,16 @@ typedef struct {
 } chip_stx_parsed;
 int chip_stx_parse_device(chip_ctx* ctx, const chip_stx_blobs* in, uint8_t* tx_status, chip_stx_parsed* out,
                           void* stream);
+/* Host entry of the whole path from bytes: n SignedTransaction blobs in host memory (pool + off/len) ->
+ * chip_stx_parse_device with CHIP_STX_REQUIRED -> chip_verify_signed_tx_batch_device, blocking.  `tmpl`
+ * (host) are the SignableData templates and meta[2i], meta[2i+1] the SignatureMetadata of template i.
+ * Out (host): tx_status[n] (chip_stx_status; only CHIP_STX_OK transactions have a verdict), verdict[n] /
+ * arg[n] (chip_tx_verdict as chip_verify_signed_tx_batch), ids[n * 32] (may be NULL).  This is what a JVM
+ * binding calls with the SerializedBytes<SignedTransaction> of a batch (jni/BatchSignatureVerifier.kt). */
+int chip_stx_verify(chip_ctx* ctx, uint64_t n, const uint8_t* data, const uint64_t* off, const uint32_t* len,
+                    uint64_t data_bytes, const chip_msg_templates* tmpl, const int32_t* meta, uint32_t n_meta,
+                    uint8_t* tx_status, uint8_t* verdict, uint32_t* arg, uint8_t* ids);
+
 /* Copies `bytes` from device memory of this context's GPU (e.g. a chip_stx_parsed array) to host memory
  * (blocking; after the context's stream has drained). */
 int chip_copy_to_host(chip_ctx* ctx, void* dst, const void* src_device, uint64_t bytes);

@@ -6,6 +6,8 @@ import net.corda.core.crypto.SecureHash
 import net.corda.core.crypto.SignableData
 import net.corda.core.crypto.SignatureMetadata
 import net.corda.core.crypto.TransactionSignature
+import net.corda.core.serialization.SerializedBytes
+import net.corda.core.serialization.deserialize
 import net.corda.core.serialization.serialize
 import net.corda.core.transactions.SignedTransaction
 import net.corda.core.transactions.SignedTransaction.SignaturesMissingException
@@ -221,6 +223,54 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0) : AutoCloseable {
     }
 
     /** Crypto.isValid(PublicKey, ByteArray, ByteArray) on the device; decode errors still throw. */
+    /**
+     * verifySignaturesExcept for transactions still in their serialized form (vault rows, P2P payloads,
+     * ResolveTransactionsFlow downloads): the bytes go to the device, which parses them (Kryo front end),
+     * derives requiredSigningKeys, recomputes the ids and verifies every signature (chip_stx_verify).
+     * Transactions the device passes return null; any other outcome (a failing signature, missing signers,
+     * CHIP_STX_UNSUPPORTED bytes, a malformed transaction) is re-run on the JVM, which throws the exact
+     * exception the reference would.
+     */
+    fun verifySerialized(txs: List<SerializedBytes<SignedTransaction>>): List<Exception?> {
+        if (txs.isEmpty()) return emptyList()
+        // SignableData templates for the metadata values this node signs with (platform version 1)
+        val metas = listOf(SignatureMetadata(1, Crypto.EDDSA_ED25519_SHA512.schemeNumberID),
+                SignatureMetadata(1, Crypto.ECDSA_SECP256R1_SHA256.schemeNumberID),
+                SignatureMetadata(1, Crypto.ECDSA_SECP256K1_SHA256.schemeNumberID))
+        val tmpls = metas.map { m ->
+            val a = SignableData(SecureHash.zeroHash, m).serialize().bytes
+            val b = SignableData(SecureHash.allOnesHash, m).serialize().bytes
+            val at = a.indices.first { a[it] != b[it] }
+            Pair(a.copyOfRange(0, at) + a.copyOfRange(at + 32, a.size), at)
+        }
+        val total = txs.sumOf { it.size }
+        val b = arena.reserve(total + 64 * txs.size + tmpls.sumOf { it.first.size } + 64 * tmpls.size + 1024)
+        fun take(bytes: Int): ByteBuffer {
+            val s = b.slice().order(ByteOrder.LITTLE_ENDIAN)
+            s.limit(maxOf(bytes, 1))
+            b.position(b.position() + ((bytes + 7) and 7.inv()).coerceAtLeast(8))
+            return s
+        }
+        val bData = take(total); val bOff = take(8 * txs.size); val bLen = take(4 * txs.size)
+        var o = 0L
+        for (t in txs) { bOff.putLong(o); bLen.putInt(t.size); bData.put(t.bytes, t.offset, t.size); o += t.size }
+        val bTd = take(tmpls.sumOf { it.first.size }); val bTo = take(8 * tmpls.size); val bTl = take(4 * tmpls.size)
+        val bTa = take(4 * tmpls.size); val bMeta = take(8 * metas.size)
+        o = 0L
+        for ((bytes, at) in tmpls) { bTo.putLong(o); bTl.putInt(bytes.size); bTa.putInt(at); bTd.put(bytes); o += bytes.size }
+        for (m in metas) { bMeta.putInt(m.platformVersion); bMeta.putInt(m.schemeNumberID) }
+        val bStatus = take(txs.size); val bVerdict = take(txs.size); val bArg = take(4 * txs.size)
+        val rc = CordaHip.stxVerify(ctx, txs.size, bData, bOff, bLen, tmpls.size, bTd, bTo, bTl, bTa, bMeta,
+                bStatus, bVerdict, bArg, null)
+        check(rc == 0) { "libcordahip stxVerify failed ($rc): ${CordaHip.lastError(ctx)}" }
+        return txs.mapIndexed { t, bytes ->
+            if (bStatus.get(t).toInt() == 0 && bVerdict.get(t).toInt() == 0) null
+            else try {
+                bytes.deserialize().verifySignaturesExcept(); null
+            } catch (e: Exception) { e }
+        }
+    }
+
     fun isValid(key: PublicKey, signature: ByteArray, clearData: ByteArray): Boolean =
             when (statuses(listOf(Item(key, signature, clearData)), isValid = true)[0].toInt()) {
                 CordaHip.VALID -> true

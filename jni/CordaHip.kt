@@ -53,6 +53,12 @@ object CordaHip {
                                   compGroup: ByteBuffer, compInternal: ByteBuffer, data: ByteBuffer,
                                   compOff: ByteBuffer, compLen: ByteBuffer, ids: ByteBuffer): Int
 
+    /** chip_stx_verify: SignedTransaction.serialize().bytes of n transactions -> status / verdict / arg (ids optional). */
+    @JvmStatic external fun stxVerify(ctx: Long, n: Int, data: ByteBuffer, off: ByteBuffer, len: ByteBuffer,
+                                      nTmpl: Int, tmplData: ByteBuffer, tmplOff: ByteBuffer, tmplLen: ByteBuffer,
+                                      tmplIdAt: ByteBuffer, meta: ByteBuffer, status: ByteBuffer, verdict: ByteBuffer,
+                                      arg: ByteBuffer, ids: ByteBuffer?): Int
+
     @JvmStatic external fun uniqOpen(ctx: Long, capacity: Long): Long
     @JvmStatic external fun uniqClose(uniq: Long)
     @JvmStatic external fun uniqSize(uniq: Long): Long

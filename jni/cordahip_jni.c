@@ -153,6 +153,33 @@ JNIEXPORT jint JNICALL CLS(txIds)(JNIEnv* env, jclass cls, jlong ctx, jint ntx, 
     return chip_txid_batch((chip_ctx*)(intptr_t)ctx, &b, out);
 }
 
+/* ---- the whole path from bytes: SignedTransaction blobs -> tx status + verdict (chip_stx_verify) ---- */
+JNIEXPORT jint JNICALL CLS(stxVerify)(JNIEnv* env, jclass cls, jlong ctx, jint n, jobject data, jobject off,
+                                      jobject len, jint nTmpl, jobject tmplData, jobject tmplOff, jobject tmplLen,
+                                      jobject tmplIdAt, jobject meta, jobject status, jobject verdict, jobject arg,
+                                      jobject ids) {
+    (void)cls;
+    chip_msg_templates t;
+    memset(&t, 0, sizeof t);
+    t.n = (uint64_t)nTmpl;
+    t.data = (const uint8_t*)addr(env, tmplData);
+    t.off = (const uint64_t*)addr(env, tmplOff);
+    t.len = (const uint32_t*)addr(env, tmplLen);
+    t.id_at = (const uint32_t*)addr(env, tmplIdAt);
+    t.data_bytes = cap_of(env, tmplData);
+    for (jint i = 0; i < nTmpl; i++)
+        if (t.len[i] > t.max_len) t.max_len = t.len[i];
+    uint8_t* st = (uint8_t*)addr(env, status);
+    uint8_t* v = (uint8_t*)addr(env, verdict);
+    uint32_t* a = (uint32_t*)addr(env, arg);
+    if (n < 0 || nTmpl < 0 || (n > 0 && (!st || !v || !a || cap_of(env, status) < (uint64_t)n ||
+                                         cap_of(env, verdict) < (uint64_t)n || cap_of(env, arg) < 4ull * (uint64_t)n)))
+        return CHIP_E_ARG;
+    return chip_stx_verify((chip_ctx*)(intptr_t)ctx, (uint64_t)n, (const uint8_t*)addr(env, data),
+                           (const uint64_t*)addr(env, off), (const uint32_t*)addr(env, len), cap_of(env, data), &t,
+                           (const int32_t*)addr(env, meta), (uint32_t)nTmpl, st, v, a, (uint8_t*)addr(env, ids));
+}
+
 /* ---- notary uniqueness ---- */
 JNIEXPORT jlong JNICALL CLS(uniqOpen)(JNIEnv* env, jclass cls, jlong ctx, jlong capacity) {
     (void)env; (void)cls;

@@ -201,3 +201,21 @@ def test_verify_from_bytes_with_derived_required_keys(ctx):
     assert np.array_equal(d_verdict.cpu().numpy(), verdict)
     assert np.array_equal(d_arg.cpu().numpy().view(np.uint32), arg)
     assert set(np.unique(verdict)) == {0, 1, 2}
+
+
+def test_host_entry_from_bytes(ctx):
+    """chip_stx_verify (what the JNI binding calls): host blobs in, per-tx status / verdict / arg / ids out."""
+    ntx = 1500
+    tb, tm, sb, ids_ref, verdict, arg = G.cfg4_workload_commands(ntx, n_keys=32, seed=0x5EED0404, threads=8)
+    data, off, ln = G.stx_uniform(tb, sb, 2)
+    st, v, a, ids = ctx.stx_verify(data, off, ln, tm, [[1, 4]], want_ids=True)
+    assert not st.any()
+    assert np.array_equal(ids, ids_ref) and np.array_equal(v, verdict) and np.array_equal(a, arg)
+    # a damaged blob and an empty batch
+    blobs = [data[int(off[t]):int(off[t]) + int(ln[t])].tobytes() for t in range(3)]
+    blobs[1] = blobs[1][:100]
+    d2, o2, l2 = G.stx_blobs_from_lists(blobs)
+    st, v, a, _ = ctx.stx_verify(d2, o2, l2, tm, [[1, 4]])
+    assert list(st) == [0, K.STX_KRYO, 0] and v[0] == verdict[0] and v[2] == verdict[2]
+    st, v, a, _ = ctx.stx_verify(np.zeros(1, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32), tm, [[1, 4]])
+    assert len(st) == 0
