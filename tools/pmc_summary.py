@@ -9,8 +9,11 @@ import sys
 
 
 def base(name):
-    name = name.split("(", 1)[0].strip()
-    return name[5:] if name.startswith("void ") else name
+    name = name.strip()
+    if name.startswith("void "):
+        name = name[5:]
+    name = name.replace("(anonymous namespace)::", "")
+    return name.split("(", 1)[0].strip()
 
 
 def main():
