@@ -200,6 +200,16 @@ def profile_traffic(kernel, grid):
     return tot
 
 
+def stx_traffic(grid_tx, grid_sig):
+    """FETCH_SIZE + WRITE_SIZE of one Kryo front-end call (both parse passes, the key interning and the
+    required-key passes; the pool copy is a DMA, not counted) from the committed PMC profile, or None."""
+    parts = [profile_traffic(k, grid_tx) for k in ("k_stx_parse<false>", "k_stx_parse<true>", "k_stx_required<false>",
+                                                    "k_stx_required<true>")]
+    parts += [profile_traffic(k, grid_sig) for k in ("k_stx_key_insert", "k_stx_key_flag", "k_stx_key_assign",
+                                                      "k_stx_req_compact")]
+    return None if any(p is None for p in parts) else sum(parts)
+
+
 def sha256_compressions(tb):
     """Exact SHA-256 compressions WireTransaction.id costs for each tx of a TxBatch (the kernel's
     all-zero padding subtrees Z_k are counted as the reference computes them, i.e. hashed)."""
@@ -509,6 +519,7 @@ def main():
             "stx_parse_roofline": {"bound": "hbm", "achieved": alg / (parse_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                                    "unit": "GB/s", "frac": alg / (parse_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                    "algorithmic_bytes": alg,
+                                   "traffic": stx_traffic((tb.ntx + 255) // 256 * 256, (sb.n + 255) // 256 * 256),
                                    "note": "one launch = both parse passes, the pool copy, scans, key interning "
                                            "and the required-key passes with their 4 host syncs"},
         })
