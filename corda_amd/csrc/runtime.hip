@@ -36,6 +36,15 @@ struct DevBuf {
     template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+// buffers of one Kryo front-end call (chip_stx_parse_device): counts, ranges, pool, batches, key
+// interning, required keys, scan scratch
+struct StxBufs {
+    DevBuf s_ncomp, s_nsig, s_nbytes, s_cstart, s_sstart, s_pstart, s_pool, s_salts, s_cgroup, s_cint, s_coff, s_clen, s_txidx, s_tmpl, s_soff, s_slen, s_skoff, s_sklen, s_meta, s_tab, s_tabmin, s_kslot, s_krep, s_kflag, s_kincl, s_kidx, s_koff, s_klen, s_temp, r_nraw, r_rstart, r_kid, r_len, r_keep, r_kincl, r_off, r_nreq, r_qstart, r_nstart, r_val, r_nk, r_w;
+    void release() {
+        for (DevBuf* b : {&s_ncomp, &s_nsig, &s_nbytes, &s_cstart, &s_sstart, &s_pstart, &s_pool, &s_salts, &s_cgroup, &s_cint, &s_coff, &s_clen, &s_txidx, &s_tmpl, &s_soff, &s_slen, &s_skoff, &s_sklen, &s_meta, &s_tab, &s_tabmin, &s_kslot, &s_krep, &s_kflag, &s_kincl, &s_kidx, &s_koff, &s_klen, &s_temp, &r_nraw, &r_rstart, &r_kid, &r_len, &r_keep, &r_kincl, &r_off, &r_nreq, &r_qstart, &r_nstart, &r_val, &r_nk, &r_w}) b->release();
+    }
+};
+
 struct chip_ctx {
     int device = 0;
     uint32_t flags = 0;
@@ -70,12 +79,12 @@ struct chip_ctx {
     // filtered transactions: kernel scratch + staging of the host entry
     DevBuf x_scratch, x_ids, x_ghs, x_gh, x_fgs, x_fgi, x_cs, x_cd, x_co, x_cl, x_nonce, x_pts, x_ptt, x_pth, x_cv,
         x_st, x_rs;
-    // Kryo front end (kryo.hip): counts, ranges, pool, batches, key interning, scan scratch
-    DevBuf s_ncomp, s_nsig, s_nbytes, s_cstart, s_sstart, s_pstart, s_pool, s_salts, s_cgroup, s_cint, s_coff, s_clen,
-        s_txidx, s_tmpl, s_soff, s_slen, s_skoff, s_sklen, s_meta, s_tab, s_tabmin, s_kslot, s_krep, s_kflag, s_kincl,
-        s_kidx, s_koff, s_klen, s_temp, h2_data, h2_off, h2_len, h2_st, h2_ids, h2_v, h2_a, h2_sigst, h2_miss,
-        h2_td, h2_to, h2_tl, h2_ta, r_nraw, r_rstart, r_kid, r_len, r_keep, r_kincl, r_off, r_nreq, r_qstart,
-        r_nstart, r_val, r_nk, r_w;
+    // Kryo front end (kryo.hip): two buffer sets used alternately, so batch k + 1 can be parsed (one
+    // stream) while batch k is verified from the other set (another stream)
+    StxBufs stx[2];
+    int stx_next = 0;
+    // chip_stx_verify staging
+    DevBuf h2_data, h2_off, h2_len, h2_st, h2_ids, h2_v, h2_a, h2_sigst, h2_miss, h2_td, h2_to, h2_tl, h2_ta;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, tev0 = nullptr, tev1 = nullptr;
     bool ev_pending = false, tev_pending = false;
     chip_stats stats{};
@@ -376,14 +385,11 @@ void chip_shutdown(chip_ctx* c) {
                       &c->f_tdata, &c->f_toff, &c->f_tlen, &c->f_tid, &c->x_scratch, &c->x_ids, &c->x_ghs,
                       &c->x_gh, &c->x_fgs, &c->x_fgi, &c->x_cs, &c->x_cd, &c->x_co, &c->x_cl, &c->x_nonce,
                       &c->x_pts, &c->x_ptt, &c->x_pth, &c->x_cv, &c->x_st, &c->x_rs,
-                      &c->s_ncomp, &c->s_nsig, &c->s_nbytes, &c->s_cstart, &c->s_sstart, &c->s_pstart, &c->s_pool,
-                      &c->s_salts, &c->s_cgroup, &c->s_cint, &c->s_coff, &c->s_clen, &c->s_txidx, &c->s_tmpl,
-                      &c->s_soff, &c->s_slen, &c->s_skoff, &c->s_sklen, &c->s_meta, &c->s_tab, &c->s_tabmin,
-                      &c->s_kslot, &c->s_krep, &c->s_kflag, &c->s_kincl, &c->s_kidx, &c->s_koff, &c->s_klen,
-                      &c->s_temp, &c->h2_data, &c->h2_off, &c->h2_len, &c->h2_st, &c->h2_ids, &c->h2_v,
-                      &c->h2_a, &c->h2_sigst, &c->h2_miss, &c->h2_td, &c->h2_to, &c->h2_tl, &c->h2_ta, &c->r_nraw, &c->r_rstart, &c->r_kid, &c->r_len, &c->r_keep, &c->r_kincl,
-                      &c->r_off, &c->r_nreq, &c->r_qstart, &c->r_nstart, &c->r_val, &c->r_nk, &c->r_w};
+                      &c->h2_data, &c->h2_off, &c->h2_len, &c->h2_st, &c->h2_ids, &c->h2_v,
+                      &c->h2_a, &c->h2_sigst, &c->h2_miss, &c->h2_td, &c->h2_to, &c->h2_tl, &c->h2_ta};
     for (DevBuf* b : bufs) b->release();
+    c->stx[0].release();
+    c->stx[1].release();
     for (int i = 0; i < chip_ctx::KRING; i++) {
         if (c->kring[i].a) hipEventDestroy(c->kring[i].a);
         if (c->kring[i].b) hipEventDestroy(c->kring[i].b);
@@ -736,25 +742,27 @@ int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_sta
     HIPCHK(c, hipSetDevice(c->device));
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     std::memset(out, 0, sizeof(*out));
+    StxBufs& B = c->stx[c->stx_next];
+    c->stx_next ^= 1;
     const uint64_t n1 = n + 1;
-    HIPCHK(c, c->s_ncomp.ensure(n1 * 8));
-    HIPCHK(c, c->s_nsig.ensure(n1 * 8));
-    HIPCHK(c, c->s_nbytes.ensure(n1 * 8));
-    HIPCHK(c, c->s_cstart.ensure(n1 * 8));
-    HIPCHK(c, c->s_sstart.ensure(n1 * 8));
-    HIPCHK(c, c->s_pstart.ensure(n1 * 8));
-    HIPCHK(c, c->s_salts.ensure(n * 32 + 16));
+    HIPCHK(c, B.s_ncomp.ensure(n1 * 8));
+    HIPCHK(c, B.s_nsig.ensure(n1 * 8));
+    HIPCHK(c, B.s_nbytes.ensure(n1 * 8));
+    HIPCHK(c, B.s_cstart.ensure(n1 * 8));
+    HIPCHK(c, B.s_sstart.ensure(n1 * 8));
+    HIPCHK(c, B.s_pstart.ensure(n1 * 8));
+    HIPCHK(c, B.s_salts.ensure(n * 32 + 16));
     const size_t temp = stx_scan_temp_bytes(n1 > 2 ? n1 : 2);
-    HIPCHK(c, c->s_temp.ensure(temp));
+    HIPCHK(c, B.s_temp.ensure(temp));
     // pass 1: validate + count; ranges = inclusive scans written one past a zero
     const int kc = c->kbegin(CHIP_K_STX, st);
-    launch_stx_count(st, in, tx_status, c->s_ncomp.as<uint64_t>(), c->s_nsig.as<uint64_t>(), c->s_nbytes.as<uint64_t>());
+    launch_stx_count(st, in, tx_status, B.s_ncomp.as<uint64_t>(), B.s_nsig.as<uint64_t>(), B.s_nbytes.as<uint64_t>());
     HIPCHK(c, hipGetLastError());
-    DevBuf* cnt[3] = {&c->s_ncomp, &c->s_nsig, &c->s_nbytes};
-    DevBuf* rng[3] = {&c->s_cstart, &c->s_sstart, &c->s_pstart};
+    DevBuf* cnt[3] = {&B.s_ncomp, &B.s_nsig, &B.s_nbytes};
+    DevBuf* rng[3] = {&B.s_cstart, &B.s_sstart, &B.s_pstart};
     for (int k = 0; k < 3; k++) {
         HIPCHK(c, hipMemsetAsync(rng[k]->p, 0, 8, st));
-        if (n) HIPCHK(c, stx_scan_u64(st, c->s_temp.p, c->s_temp.cap, cnt[k]->as<uint64_t>(), rng[k]->as<uint64_t>() + 1, n));
+        if (n) HIPCHK(c, stx_scan_u64(st, B.s_temp.p, B.s_temp.cap, cnt[k]->as<uint64_t>(), rng[k]->as<uint64_t>() + 1, n));
     }
     uint64_t tot[3] = {0, 0, 0};
     for (int k = 0; k < 3; k++)
@@ -765,118 +773,118 @@ int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_sta
     // pool = a copy of the blobs (payload runs inside one chunk keep their offsets) + the extra region
     const uint64_t extra_base = (in->data_bytes + 15) & ~15ull;
     const uint64_t pool = extra_base + tot[2];
-    HIPCHK(c, c->s_pool.ensure(pool + 64));
+    HIPCHK(c, B.s_pool.ensure(pool + 64));
     if (in->data_bytes)
-        HIPCHK(c, hipMemcpyAsync(c->s_pool.p, in->data, in->data_bytes, hipMemcpyDeviceToDevice, st));
-    HIPCHK(c, c->s_cgroup.ensure(ncomp * 4 + 16));
-    HIPCHK(c, c->s_cint.ensure(ncomp * 4 + 16));
-    HIPCHK(c, c->s_coff.ensure(ncomp * 8 + 16));
-    HIPCHK(c, c->s_clen.ensure(ncomp * 4 + 16));
-    HIPCHK(c, c->s_txidx.ensure(nsig * 4 + 16));
-    HIPCHK(c, c->s_tmpl.ensure(nsig * 4 + 16));
-    HIPCHK(c, c->s_soff.ensure(nsig * 8 + 16));
-    HIPCHK(c, c->s_slen.ensure(nsig * 4 + 16));
-    HIPCHK(c, c->s_skoff.ensure(nsig * 8 + 16));
-    HIPCHK(c, c->s_sklen.ensure(nsig * 4 + 16));
-    HIPCHK(c, c->s_meta.ensure((uint64_t)in->n_meta * 8 + 16));
+        HIPCHK(c, hipMemcpyAsync(B.s_pool.p, in->data, in->data_bytes, hipMemcpyDeviceToDevice, st));
+    HIPCHK(c, B.s_cgroup.ensure(ncomp * 4 + 16));
+    HIPCHK(c, B.s_cint.ensure(ncomp * 4 + 16));
+    HIPCHK(c, B.s_coff.ensure(ncomp * 8 + 16));
+    HIPCHK(c, B.s_clen.ensure(ncomp * 4 + 16));
+    HIPCHK(c, B.s_txidx.ensure(nsig * 4 + 16));
+    HIPCHK(c, B.s_tmpl.ensure(nsig * 4 + 16));
+    HIPCHK(c, B.s_soff.ensure(nsig * 8 + 16));
+    HIPCHK(c, B.s_slen.ensure(nsig * 4 + 16));
+    HIPCHK(c, B.s_skoff.ensure(nsig * 8 + 16));
+    HIPCHK(c, B.s_sklen.ensure(nsig * 4 + 16));
+    HIPCHK(c, B.s_meta.ensure((uint64_t)in->n_meta * 8 + 16));
     uint64_t cap = 1024;
     while (cap < 2 * nsig) cap <<= 1;
-    HIPCHK(c, c->s_tab.ensure(cap * 8));
-    HIPCHK(c, c->s_tabmin.ensure(cap * 4));
-    for (DevBuf* b : {&c->s_kslot, &c->s_krep, &c->s_kflag, &c->s_kincl, &c->s_kidx, &c->s_klen})
+    HIPCHK(c, B.s_tab.ensure(cap * 8));
+    HIPCHK(c, B.s_tabmin.ensure(cap * 4));
+    for (DevBuf* b : {&B.s_kslot, &B.s_krep, &B.s_kflag, &B.s_kincl, &B.s_kidx, &B.s_klen})
         HIPCHK(c, b->ensure(nsig * 4 + 16));
-    HIPCHK(c, c->s_koff.ensure(nsig * 8 + 16));
-    if (stx_scan_temp_bytes(nsig > 2 ? nsig : 2) > c->s_temp.cap)
-        HIPCHK(c, c->s_temp.ensure(stx_scan_temp_bytes(nsig > 2 ? nsig : 2)));
+    HIPCHK(c, B.s_koff.ensure(nsig * 8 + 16));
+    if (stx_scan_temp_bytes(nsig > 2 ? nsig : 2) > B.s_temp.cap)
+        HIPCHK(c, B.s_temp.ensure(stx_scan_temp_bytes(nsig > 2 ? nsig : 2)));
     if (in->n_meta)
-        HIPCHK(c, hipMemcpyAsync(c->s_meta.p, in->meta, (uint64_t)in->n_meta * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(c, hipMemcpyAsync(B.s_meta.p, in->meta, (uint64_t)in->n_meta * 8, hipMemcpyHostToDevice, st));
     StxOut d{};
-    d.pool = c->s_pool.as<uint8_t>();
-    d.extra_start = c->s_pstart.as<uint64_t>();
+    d.pool = B.s_pool.as<uint8_t>();
+    d.extra_start = B.s_pstart.as<uint64_t>();
     d.extra_base = extra_base;
-    d.salts = c->s_salts.as<uint8_t>();
-    d.comp_start = c->s_cstart.as<uint64_t>();
-    d.comp_group = c->s_cgroup.as<uint32_t>();
-    d.comp_internal = c->s_cint.as<uint32_t>();
-    d.comp_len = c->s_clen.as<uint32_t>();
-    d.comp_off = c->s_coff.as<uint64_t>();
-    d.sig_start = c->s_sstart.as<uint64_t>();
-    d.tx_idx = c->s_txidx.as<uint32_t>();
-    d.tmpl_idx = c->s_tmpl.as<uint32_t>();
-    d.sig_len = c->s_slen.as<uint32_t>();
-    d.skey_len = c->s_sklen.as<uint32_t>();
-    d.sig_off = c->s_soff.as<uint64_t>();
-    d.skey_off = c->s_skoff.as<uint64_t>();
-    d.meta = c->s_meta.as<int32_t>();
+    d.salts = B.s_salts.as<uint8_t>();
+    d.comp_start = B.s_cstart.as<uint64_t>();
+    d.comp_group = B.s_cgroup.as<uint32_t>();
+    d.comp_internal = B.s_cint.as<uint32_t>();
+    d.comp_len = B.s_clen.as<uint32_t>();
+    d.comp_off = B.s_coff.as<uint64_t>();
+    d.sig_start = B.s_sstart.as<uint64_t>();
+    d.tx_idx = B.s_txidx.as<uint32_t>();
+    d.tmpl_idx = B.s_tmpl.as<uint32_t>();
+    d.sig_len = B.s_slen.as<uint32_t>();
+    d.skey_len = B.s_sklen.as<uint32_t>();
+    d.sig_off = B.s_soff.as<uint64_t>();
+    d.skey_off = B.s_skoff.as<uint64_t>();
+    d.meta = B.s_meta.as<int32_t>();
     d.n_meta = in->n_meta;
-    d.tab = c->s_tab.as<uint64_t>();
-    d.tab_min = c->s_tabmin.as<uint32_t>();
-    d.kslot = c->s_kslot.as<uint32_t>();
-    d.krep = c->s_krep.as<uint32_t>();
-    d.kflag = c->s_kflag.as<uint32_t>();
-    d.kincl = c->s_kincl.as<uint32_t>();
-    d.key_idx = c->s_kidx.as<uint32_t>();
-    d.key_off = c->s_koff.as<uint64_t>();
-    d.key_len = c->s_klen.as<uint32_t>();
+    d.tab = B.s_tab.as<uint64_t>();
+    d.tab_min = B.s_tabmin.as<uint32_t>();
+    d.kslot = B.s_kslot.as<uint32_t>();
+    d.krep = B.s_krep.as<uint32_t>();
+    d.kflag = B.s_kflag.as<uint32_t>();
+    d.kincl = B.s_kincl.as<uint32_t>();
+    d.key_idx = B.s_kidx.as<uint32_t>();
+    d.key_off = B.s_koff.as<uint64_t>();
+    d.key_len = B.s_klen.as<uint32_t>();
     // pass 2: the batches; then the signer keys interned
     launch_stx_emit(st, in, tx_status, d);
     HIPCHK(c, hipGetLastError());
-    HIPCHK(c, hipMemsetAsync(c->s_tab.p, 0, cap * 8, st));
-    HIPCHK(c, hipMemsetAsync(c->s_tabmin.p, 0xff, cap * 4, st));
-    launch_stx_keys(st, nsig, d, cap - 1, c->s_temp.p, c->s_temp.cap);
+    HIPCHK(c, hipMemsetAsync(B.s_tab.p, 0, cap * 8, st));
+    HIPCHK(c, hipMemsetAsync(B.s_tabmin.p, 0xff, cap * 4, st));
+    launch_stx_keys(st, nsig, d, cap - 1, B.s_temp.p, B.s_temp.cap);
     HIPCHK(c, hipGetLastError());
     uint32_t nkeys = 0;
-    if (nsig) HIPCHK(c, hipMemcpyAsync(&nkeys, c->s_kincl.as<uint32_t>() + nsig - 1, 4, hipMemcpyDeviceToHost, st));
+    if (nsig) HIPCHK(c, hipMemcpyAsync(&nkeys, B.s_kincl.as<uint32_t>() + nsig - 1, 4, hipMemcpyDeviceToHost, st));
     if (in->flags & CHIP_STX_REQUIRED) {
         // requiredSigningKeys: R1 counts signer entries, scan, R2 writes them + duplicate flags, scans,
         // compaction into one leaf per distinct required key
         StxReq q{};
-        HIPCHK(c, c->r_nraw.ensure(n1 * 8));
-        HIPCHK(c, c->r_rstart.ensure(n1 * 8));
-        HIPCHK(c, c->r_nreq.ensure(n1 * 8));
-        HIPCHK(c, c->r_qstart.ensure(n1 * 8));
-        q.nraw = c->r_nraw.as<uint64_t>();
-        q.raw_start = c->r_rstart.as<uint64_t>();
-        q.nreq = c->r_nreq.as<uint64_t>();
+        HIPCHK(c, B.r_nraw.ensure(n1 * 8));
+        HIPCHK(c, B.r_rstart.ensure(n1 * 8));
+        HIPCHK(c, B.r_nreq.ensure(n1 * 8));
+        HIPCHK(c, B.r_qstart.ensure(n1 * 8));
+        q.nraw = B.r_nraw.as<uint64_t>();
+        q.raw_start = B.r_rstart.as<uint64_t>();
+        q.nreq = B.r_nreq.as<uint64_t>();
         launch_stx_required(st, false, n, tx_status, d, pool, cap - 1, q);
         HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemsetAsync(q.raw_start, 0, 8, st));
-        if (n) HIPCHK(c, stx_scan_u64(st, c->s_temp.p, c->s_temp.cap, q.nraw, q.raw_start + 1, n));
+        if (n) HIPCHK(c, stx_scan_u64(st, B.s_temp.p, B.s_temp.cap, q.nraw, q.raw_start + 1, n));
         uint64_t nraw = 0;
         HIPCHK(c, hipMemcpyAsync(&nraw, q.raw_start + n, 8, hipMemcpyDeviceToHost, st));
         HIPCHK(c, hipStreamSynchronize(st));
         if (nraw >= (1ull << 31)) return fail(c, CHIP_E_ARG, "too many required keys");
-        for (DevBuf* b : {&c->r_kid, &c->r_len, &c->r_keep, &c->r_kincl, &c->r_val, &c->r_nk, &c->r_w})
+        for (DevBuf* b : {&B.r_kid, &B.r_len, &B.r_keep, &B.r_kincl, &B.r_val, &B.r_nk, &B.r_w})
             HIPCHK(c, b->ensure(nraw * 4 + 16));
-        HIPCHK(c, c->r_off.ensure(nraw * 8 + 16));
-        HIPCHK(c, c->r_nstart.ensure(nraw * 8 + 16));
-        if (stx_scan_temp_bytes(nraw > 2 ? nraw : 2) > c->s_temp.cap)
-            HIPCHK(c, c->s_temp.ensure(stx_scan_temp_bytes(nraw > 2 ? nraw : 2)));
-        q.raw_kid = c->r_kid.as<uint32_t>();
-        q.raw_len = c->r_len.as<uint32_t>();
-        q.raw_keep = c->r_keep.as<uint32_t>();
-        q.keep_incl = c->r_kincl.as<uint32_t>();
-        q.raw_off = c->r_off.as<uint64_t>();
-        q.node_start = c->r_nstart.as<uint64_t>();
-        q.node_val = c->r_val.as<uint32_t>();
-        q.node_nkids = c->r_nk.as<uint32_t>();
-        q.node_weight = c->r_w.as<uint32_t>();
+        HIPCHK(c, B.r_off.ensure(nraw * 8 + 16));
+        HIPCHK(c, B.r_nstart.ensure(nraw * 8 + 16));
+        if (stx_scan_temp_bytes(nraw > 2 ? nraw : 2) > B.s_temp.cap)
+            HIPCHK(c, B.s_temp.ensure(stx_scan_temp_bytes(nraw > 2 ? nraw : 2)));
+        q.raw_kid = B.r_kid.as<uint32_t>();
+        q.raw_len = B.r_len.as<uint32_t>();
+        q.raw_keep = B.r_keep.as<uint32_t>();
+        q.keep_incl = B.r_kincl.as<uint32_t>();
+        q.raw_off = B.r_off.as<uint64_t>();
+        q.node_start = B.r_nstart.as<uint64_t>();
+        q.node_val = B.r_val.as<uint32_t>();
+        q.node_nkids = B.r_nk.as<uint32_t>();
+        q.node_weight = B.r_w.as<uint32_t>();
         launch_stx_required(st, true, n, tx_status, d, pool, cap - 1, q);
         HIPCHK(c, hipGetLastError());
-        HIPCHK(c, hipMemsetAsync(c->r_qstart.p, 0, 8, st));
-        if (n) HIPCHK(c, stx_scan_u64(st, c->s_temp.p, c->s_temp.cap, q.nreq, c->r_qstart.as<uint64_t>() + 1, n));
+        HIPCHK(c, hipMemsetAsync(B.r_qstart.p, 0, 8, st));
+        if (n) HIPCHK(c, stx_scan_u64(st, B.s_temp.p, B.s_temp.cap, q.nreq, B.r_qstart.as<uint64_t>() + 1, n));
         HIPCHK(c, hipMemsetAsync(q.node_start, 0, 8, st));
-        if (nraw) HIPCHK(c, stx_scan_u32(st, c->s_temp.p, c->s_temp.cap, q.raw_keep, q.keep_incl, nraw));
+        if (nraw) HIPCHK(c, stx_scan_u32(st, B.s_temp.p, B.s_temp.cap, q.raw_keep, q.keep_incl, nraw));
         launch_stx_req_compact(st, nraw, q);
         HIPCHK(c, hipGetLastError());
         uint64_t nreq = 0;
-        HIPCHK(c, hipMemcpyAsync(&nreq, c->r_qstart.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipMemcpyAsync(&nreq, B.r_qstart.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
         c->kend(kc, st);
         HIPCHK(c, hipStreamSynchronize(st));
         chip_req_batch& rq = out->req;
         rq.ntx = n;
         rq.sig_start = d.sig_start;
-        rq.req_start = c->r_qstart.as<uint64_t>();
+        rq.req_start = B.r_qstart.as<uint64_t>();
         rq.nreq = nreq;
         rq.node_start = q.node_start;
         rq.allowed = nullptr;

@@ -343,7 +343,9 @@ int chip_verify_signed_tx_batch_device(chip_ctx* ctx, const chip_tx_batch* txs, 
  * A transaction that is not OK contributes no components and no signatures, except one whose only fault is
  * a duplicate input (found by the second pass, which compares the de-chunked inputs): its ranges stay
  * filled and its status says CHIP_STX_INVARIANT.  The outputs live in the
- * context's buffers until its next chip_stx_parse_device call (device pointers, this context's GPU):
+ * context's buffers until the second chip_stx_parse_device call after it (two buffer sets alternate, so
+ * batch k + 1 can be parsed on one stream while batch k is verified on another; the caller orders the
+ * parse of batch k + 2 after the verification of batch k) — device pointers, this context's GPU:
  *   out->txs    chip_tx_batch of every blob (salts, component ranges, groups, internal indices; the
  *               component bytes de-chunked into the context's pool)
  *   out->sigs   chip_signer_batch: tx_idx = blob index, tmpl_idx = the index i of the first template whose

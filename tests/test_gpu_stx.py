@@ -219,3 +219,34 @@ def test_host_entry_from_bytes(ctx):
     assert list(st) == [0, K.STX_KRYO, 0] and v[0] == verdict[0] and v[2] == verdict[2]
     st, v, a, _ = ctx.stx_verify(np.zeros(1, np.uint8), np.zeros(0, np.uint64), np.zeros(0, np.uint32), tm, [[1, 4]])
     assert len(st) == 0
+
+
+def test_two_buffer_sets_alternate(ctx):
+    """The outputs of a parse stay valid across the next parse (two buffer sets): batch A is parsed,
+    then batch B (on another stream), and A's parsed batch still verifies to A's labels."""
+    ta = G.cfg4_workload_commands(700, n_keys=16, seed=0x5EED0504, threads=8)
+    tb_ = G.cfg4_workload_commands(900, n_keys=16, seed=0x5EED0604, threads=8)
+    parsed = []
+    keep = []
+    other = torch.cuda.Stream(DEV)
+    for i, (tbx, tmx, sbx, idsx, vx, ax) in enumerate((ta, tb_)):
+        data, off, ln = G.stx_uniform(tbx, sbx, 2)
+        dd, doff, dlen = _dev(data), _dev(off), _dev(ln)
+        st = torch.zeros(tbx.ntx, dtype=torch.uint8, device=DEV)
+        p = ctx.stx_parse_device(dd, doff, dlen, len(data), np.array([[1, 4]], np.int32), st, required=True,
+                                 stream=other.cuda_stream if i else None)
+        parsed.append(p)
+        keep.append((dd, doff, dlen, st))
+    tbx, tmx, sbx, idsx, vx, ax = ta
+    p = parsed[0]
+    dtm = G.Templates()
+    dtm.data, dtm.off, dtm.len, dtm.id_at, dtm.max_len = _dev(tmx.data), _dev(tmx.off), _dev(tmx.len), _dev(tmx.id_at), tmx.max_len
+    d_ids = torch.zeros(tbx.ntx * 32, dtype=torch.uint8, device=DEV)
+    d_status = torch.zeros(sbx.n, dtype=torch.uint8, device=DEV)
+    d_verdict = torch.zeros(tbx.ntx, dtype=torch.uint8, device=DEV)
+    d_arg = torch.zeros(tbx.ntx, dtype=torch.int32, device=DEV)
+    d_missing = torch.zeros(max(p.req.nreq, 1), dtype=torch.uint8, device=DEV)
+    ctx.verify_signed_tx_parsed_device(p, dtm, None, d_ids, d_status, d_verdict, d_arg, d_missing)
+    torch.cuda.synchronize()
+    assert np.array_equal(d_ids.cpu().numpy().reshape(-1, 32), idsx)
+    assert np.array_equal(d_verdict.cpu().numpy(), vx) and np.array_equal(d_arg.cpu().numpy().view(np.uint32), ax)
