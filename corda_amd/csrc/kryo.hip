@@ -722,7 +722,8 @@ __device__ __forceinline__ uint32_t lookup_kid(const ReqCtx& r, uint64_t off, ui
 // pass R1 counts the signer entries (commands' signers, then the notary key) of every OK transaction;
 // R2 writes them with their key index and a duplicate flag (an earlier entry of the same transaction
 // with the same key: requiredSigningKeys is a set).  A command or notary component outside the grammar,
-// a chunk-spanning key or a CompositeKey (its tree is not in the signer pool) -> CHIP_STX_UNSUPPORTED.
+// a chunk-spanning key, more than 64 signer entries or a CompositeKey (its tree is not in the signer
+// pool) -> CHIP_STX_UNSUPPORTED.
 template <bool EMIT>
 __global__ void __launch_bounds__(256) k_stx_required(uint64_t n, uint8_t* __restrict__ status,
                                                       const uint64_t* __restrict__ comp_start,
@@ -755,6 +756,10 @@ __global__ void __launch_bounds__(256) k_stx_required(uint64_t n, uint8_t* __res
     Sink none{nullptr, 0, 0};
     uint64_t spill = 0;
     auto take = [&](uint64_t off, uint32_t len) {
+        if (cnt >= 64) {   // the duplicate check is quadratic: more signer entries go to the JVM path
+            bad = true;
+            return;
+        }
         const uint32_t kid = lookup_kid(r, off, len);
         if (kid == CHIP_REQ_NO_SIGNER && is_composite_spki(r.pool, off, len)) bad = true;
         if (EMIT && !bad) {

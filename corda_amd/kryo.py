@@ -806,7 +806,8 @@ def party_owning_key(buf: bytes) -> bytes:
 
 
 def required_signing_keys(groups: Sequence[Tuple[int, Sequence[bytes]]]) -> List[bytes]:
-    """WireTransaction.requiredSigningKeys (WireTransaction.kt:66-75): commands.flatMap { signers }
+    """WireTransaction.requiredSigningKeys (WireTransaction.kt:66-75) — the device additionally hands a
+    transaction with more than 64 signer entries to the JVM path: commands.flatMap { signers }
     .toSet() + notary.owningKey when the transaction has inputs or a time-window, in first-appearance
     order (the order of the device's required-key ranges).  Keys compare by their encoding."""
     out: List[bytes] = []

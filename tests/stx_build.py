@@ -150,6 +150,8 @@ def cases_required(seed: int = 13, n: int = 240):
             groups.append((4, [K.party(notary_key)]))
             if rng.random() < 0.3:
                 groups.append((5, [rng.bytes(40)]))
+        if i % 97 == 5:                                                     # > 64 signer entries
+            cmds.append(K.command([pool[j % len(pool)] for j in range(70)], list_kind="array"))
         req_all = [k for ss in signers_of_cmds for k in ss] + [notary_key]
         sig_keys = [req_all[int(rng.integers(0, len(req_all)))] for _ in range(int(rng.integers(1, 4)))]
         sigs = [K.Sig(rng.bytes(64) if len(k) == ED_KEY else rng.bytes(71), k, 1, 4, 31) for k in sig_keys]
@@ -175,7 +177,13 @@ def expected_required(blobs):
             continue
         try:
             req = K.required_signing_keys(g)
+            present = {gi for gi, _ in g}
+            entries = sum(len(K.command_signers(c)) for gi, cs in g if gi == K.GROUP_COMMANDS for c in cs) + \
+                (1 if K.GROUP_NOTARY in present and (K.GROUP_INPUTS in present or K.GROUP_TIMEWINDOW in present) else 0)
         except K.KryoException:
+            out.append((K.STX_UNSUPPORTED, None))
+            continue
+        if entries > 64:                         # the device's duplicate check covers <= 64 signer entries
             out.append((K.STX_UNSUPPORTED, None))
             continue
         if any(k not in kid and CK._spki_oid(k) == CK._COMPOSITE_OID_TLV for k in req):
