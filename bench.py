@@ -70,7 +70,7 @@ ECDSA_Q_MACS_PER_VERIFY = 65 * 592 + 100                            # k_ecdsa_co
 SHA256_OPS_PER_COMPRESSION = 2_168
 # HBM traffic per launch comes from the committed PMC passes of the same command (tools/profile.sh):
 # FETCH_SIZE + WRITE_SIZE (KiB) of the launch with the same grid
-PROFILE_DIR = os.path.join(ROOT, "profiles", os.environ.get("CORDA_PROFILE_DIR", "r02d"))
+PROFILE_DIR = os.path.join(ROOT, "profiles", os.environ.get("CORDA_PROFILE_DIR", "r02e"))
 # VALU issue peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6e12 lane-ops/s (a wave64 VALU
 # instruction issues over 2 cycles, MI355X_MICROARCH.md).  v_mad_u64_u32 issues at a quarter of
 # that: 19.66e12 MACs/s (tools/microbench_mul.hip measures 18.0e12).
