@@ -340,9 +340,10 @@ int chip_verify_signed_tx_batch_device(chip_ctx* ctx, const chip_tx_batch* txs, 
  *                 CHIP_STX_UNSUPPORTED  well-formed bytes outside the device grammar (object back-references,
  *                                       other list / key classes, group index >= 64, ...): verify that
  *                                       transaction on the JVM path
- * A transaction that is not OK contributes no components and no signatures, except one whose only fault is
- * a duplicate input (found by the second pass, which compares the de-chunked inputs): its ranges stay
- * filled and its status says CHIP_STX_INVARIANT.  The outputs live in the
+ * A transaction that is not OK contributes no components and no signatures, except one whose fault is
+ * found after its ranges were filled — a duplicate input (the second pass compares the de-chunked inputs:
+ * CHIP_STX_INVARIANT) or, with CHIP_STX_REQUIRED, its required keys (CHIP_STX_UNSUPPORTED): its ranges
+ * stay filled and are to be ignored.  The outputs live in the
  * context's buffers until the second chip_stx_parse_device call after it (two buffer sets alternate, so
  * batch k + 1 can be parsed on one stream while batch k is verified on another; the caller orders the
  * parse of batch k + 2 after the verification of batch k) — device pointers, this context's GPU:
