@@ -26,6 +26,7 @@ launch stream; `cpu_baseline` times the oracle (oracle/, the C restatement) on t
 `cpu_baseline_openssl` OpenSSL EVP_DigestVerify on the same sample.
 """
 import argparse
+import copy
 import json
 import os
 import sys
@@ -356,6 +357,22 @@ def main():
                                    "the same pipeline, D2H of status + bitmap",
             "cfg2_host_path_correct": bool(np.array_equal(hst, batch.expected)),
         })
+        # the same from page-locked host buffers (chip_alloc_pinned: the JNI layer's direct ByteBuffers)
+        pb = copy.copy(batch)
+        for f in SIG_FIELDS:
+            setattr(pb, f, ctx.pinned_copy(getattr(batch, f)))
+        ctx.verify_batch(pb)
+        t1 = time.perf_counter()
+        for _ in range(2):
+            pst, _bm = ctx.verify_batch(pb)
+        pel = max_over_ranks((time.perf_counter() - t1) / 2, world, torch, dev, dist)
+        secondary.update({
+            "cfg2_host_path_pinned_sigs_per_s": world * n / pel,
+            "cfg2_host_path_pinned_ms": pel * 1e3,
+            "cfg2_host_path_pinned_correct": bool(np.array_equal(pst, batch.expected)),
+        })
+        del pb
+        ctx.free_pinned()
 
     progress("cfg2 host path done")
     # ---- cold keys: every signature its own key (windowed Straus kernel) ----

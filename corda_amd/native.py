@@ -484,6 +484,26 @@ class Context:
                                              meta.ctypes.data, len(meta), _ptr(st), _ptr(v), _ptr(a), _ptr(ids)))
         return st[:n], v[:n], a[:n], (ids[:32 * n].reshape(n, 32) if want_ids else None)
 
+    def pinned_copy(self, arr: np.ndarray) -> np.ndarray:
+        """A copy of `arr` in page-locked host memory from chip_alloc_pinned (freed with the context);
+        host entries then stage it by DMA instead of through a pageable bounce."""
+        arr = np.ascontiguousarray(arr)
+        nbytes = max(arr.nbytes, 1)
+        p = ctypes.c_void_p()
+        self._check(self.lib.chip_alloc_pinned(nbytes, ctypes.byref(p)))
+        if not hasattr(self, "_pinned"):
+            self._pinned = []
+        self._pinned.append(p.value)
+        buf = (ctypes.c_uint8 * nbytes).from_address(p.value)
+        out = np.frombuffer(buf, dtype=np.uint8, count=arr.nbytes).view(arr.dtype).reshape(arr.shape)
+        out[...] = arr
+        return out
+
+    def free_pinned(self):
+        for p in getattr(self, "_pinned", []):
+            self.lib.chip_free_pinned(p)
+        self._pinned = []
+
     def copy_to_host(self, ptr, count: int, dtype) -> np.ndarray:
         """A library-owned device array (e.g. a chip_stx_parsed field) -> host numpy array."""
         out = np.zeros(max(count, 1), dtype=dtype)
