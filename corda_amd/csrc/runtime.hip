@@ -69,7 +69,7 @@ struct chip_ctx {
         c_xyz, c_zpre, c_nega, c_bmid, e_ctab, e_mid, e_gcomb, e_bcomb16, e_wp, e_glist;
     // host-path mirrors of the caller's buffers
     DevBuf h_key_idx, h_msg_idx, h_sig_data, h_sig_off, h_sig_len, h_key_data, h_key_off, h_key_len, h_msg_data,
-        h_msg_off, h_msg_len, h_status, h_bitmap;
+        h_msg_off, h_msg_len, h_status, h_bitmap, h_check;
     // txid
     DevBuf t_salts, t_start, t_group, t_internal, t_data, t_off, t_len, t_ids, t_scratch;
     // fused tx verification: device-built SignableData messages + staging of the host entry
@@ -379,7 +379,7 @@ void chip_shutdown(chip_ctx* c) {
                       &c->c_key_slot, &c->c_key_base, &c->c_slot_key, &c->c_ctr, &c->c_comb_list,
                       &c->c_straus_list, &c->c_ctab, &c->c_xyz, &c->c_zpre, &c->c_nega, &c->c_bmid, &c->e_ctab, &c->e_mid, &c->e_gcomb, &c->e_bcomb16, &c->e_wp, &c->e_glist, &c->h_key_idx, &c->h_msg_idx,
                       &c->h_sig_data, &c->h_sig_off, &c->h_sig_len, &c->h_key_data, &c->h_key_off, &c->h_key_len,
-                      &c->h_msg_data, &c->h_msg_off, &c->h_msg_len, &c->h_status, &c->h_bitmap, &c->t_salts,
+                      &c->h_msg_data, &c->h_msg_off, &c->h_msg_len, &c->h_status, &c->h_bitmap, &c->h_check, &c->t_salts,
                       &c->t_start, &c->t_group, &c->t_internal, &c->t_data, &c->t_off, &c->t_len, &c->t_ids,
                       &c->t_scratch, &c->f_pool, &c->f_moff, &c->f_mlen, &c->f_midx, &c->f_htx, &c->f_htm,
                       &c->f_tdata, &c->f_toff, &c->f_tlen, &c->f_tid, &c->x_scratch, &c->x_ids, &c->x_ghs,
@@ -658,21 +658,52 @@ int chip_is_valid_batch_device(chip_ctx* c, const chip_sig_batch* b, uint8_t* st
     return verify_device_entry(c, b, status, bitmap, stream, true);
 }
 
+// host entry: the argument bounds checks of a staged batch on the device (one flag word; every index and
+// (offset, length) range of the caller's arrays), so no out-of-range index reaches a verify kernel and the
+// host does not walk 1M entries; and the per-status counters of chip_stats
+__global__ void __launch_bounds__(256) k_check_batch(uint64_t n, uint64_t nk, uint64_t nm, const uint32_t* __restrict__ key_idx,
+                                                     const uint32_t* __restrict__ msg_idx, const uint64_t* __restrict__ sig_off,
+                                                     const uint32_t* __restrict__ sig_len, uint64_t sig_bytes,
+                                                     const uint64_t* __restrict__ key_off, const uint32_t* __restrict__ key_len,
+                                                     uint64_t key_bytes, const uint64_t* __restrict__ msg_off,
+                                                     const uint32_t* __restrict__ msg_len, uint64_t msg_bytes,
+                                                     uint32_t* __restrict__ bad) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t f = 0;
+    if (i < n) {
+        if (key_idx[i] >= nk || msg_idx[i] >= nm) f |= 1;
+        const uint64_t e = sig_off[i] + sig_len[i];
+        if (e > sig_bytes || e < sig_off[i]) f |= 2;
+    }
+    if (i < nk) {
+        const uint64_t e = key_off[i] + key_len[i];
+        if (e > key_bytes || e < key_off[i]) f |= 4;
+    }
+    if (i < nm) {
+        const uint64_t e = msg_off[i] + msg_len[i];
+        if (e > msg_bytes || e < msg_off[i]) f |= 8;
+    }
+    if (f) atomicOr(bad, f);
+}
+
+__global__ void __launch_bounds__(256) k_status_count(uint64_t n, const uint8_t* __restrict__ status,
+                                                      unsigned long long* __restrict__ counts) {
+    __shared__ uint32_t h[8];
+    if (threadIdx.x < 8) h[threadIdx.x] = 0;
+    __syncthreads();
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) atomicAdd(&h[status[i] & 7], 1u);
+    __syncthreads();
+    if (threadIdx.x < 8 && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], (unsigned long long)h[threadIdx.x]);
+}
+
 static int verify_host_entry(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap, bool is_valid) {
     if (!c || !b) return fail(c, CHIP_E_ARG, "null argument");
     const uint64_t n = b->n, nk = b->n_keys, nm = b->n_msgs;
     if ((n && (!b->key_idx || !b->msg_idx || !b->sig_off || !b->sig_len)) ||
         (nk && (!b->key_data || !b->key_off || !b->key_len)) || (nm && (!b->msg_data || !b->msg_off || !b->msg_len)))
         return fail(c, CHIP_E_ARG, "null batch array");
-    // bounds: pools must contain every (offset, length) range and indices must be in range
-    for (uint64_t i = 0; i < n; i++) {
-        if (b->key_idx[i] >= nk || b->msg_idx[i] >= nm) return fail(c, CHIP_E_ARG, "key_idx/msg_idx out of range");
-        if (b->sig_off[i] + b->sig_len[i] > b->sig_bytes) return fail(c, CHIP_E_ARG, "signature outside sig pool");
-    }
-    for (uint64_t k = 0; k < nk; k++)
-        if (b->key_off[k] + b->key_len[k] > b->key_bytes) return fail(c, CHIP_E_ARG, "key outside key pool");
-    for (uint64_t m = 0; m < nm; m++)
-        if (b->msg_off[m] + b->msg_len[m] > b->msg_bytes) return fail(c, CHIP_E_ARG, "message outside msg pool");
+    // bounds: checked on the device after staging (k_check_batch), before any verify kernel runs
     std::lock_guard<std::mutex> g(c->mu);
     hipStream_t st = c->stream;
     HIPCHK(c, hipSetDevice(c->device));
@@ -687,6 +718,25 @@ static int verify_host_entry(chip_ctx* c, const chip_sig_batch* b, uint8_t* stat
     HIPCHK(c, c->h_status.ensure(n + 16));
     const uint64_t nw = (n + 63) / 64;
     HIPCHK(c, c->h_bitmap.ensure(nw * 8 + 16));
+    HIPCHK(c, c->h_check.ensure(128));
+    {   // pools must contain every (offset, length) range and indices must be in range
+        const uint64_t m = std::max(n, std::max(nk, nm));
+        HIPCHK(c, hipMemsetAsync(c->h_check.p, 0, 128, st));
+        if (m)
+            hipLaunchKernelGGL(k_check_batch, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, st, n, nk, nm,
+                               c->h_key_idx.as<uint32_t>(), c->h_msg_idx.as<uint32_t>(), c->h_sig_off.as<uint64_t>(),
+                               c->h_sig_len.as<uint32_t>(), b->sig_bytes, c->h_key_off.as<uint64_t>(),
+                               c->h_key_len.as<uint32_t>(), b->key_bytes, c->h_msg_off.as<uint64_t>(),
+                               c->h_msg_len.as<uint32_t>(), b->msg_bytes, c->h_check.as<uint32_t>());
+        HIPCHK(c, hipGetLastError());
+        uint32_t bad = 0;
+        HIPCHK(c, hipMemcpyAsync(&bad, c->h_check.p, 4, hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        if (bad & 1) return fail(c, CHIP_E_ARG, "key_idx/msg_idx out of range");
+        if (bad & 2) return fail(c, CHIP_E_ARG, "signature outside sig pool");
+        if (bad & 4) return fail(c, CHIP_E_ARG, "key outside key pool");
+        if (bad & 8) return fail(c, CHIP_E_ARG, "message outside msg pool");
+    }
     chip_sig_batch d = *b;
     d.key_idx = c->h_key_idx.as<uint32_t>();
     d.msg_idx = c->h_msg_idx.as<uint32_t>();
@@ -702,14 +752,21 @@ static int verify_host_entry(chip_ctx* c, const chip_sig_batch* b, uint8_t* stat
     if (!d.schemes) d.schemes = host_scheme_hint(b);
     if ((r = verify_device_locked(c, &d, c->h_status.as<uint8_t>(), c->h_bitmap.as<uint64_t>(), st, is_valid)))
         return r;
+    unsigned long long counts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (n) {
+        HIPCHK(c, hipMemsetAsync(c->h_check.p, 0, 64, st));
+        hipLaunchKernelGGL(k_status_count, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, n,
+                           c->h_status.as<uint8_t>(), c->h_check.as<unsigned long long>());
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(counts, c->h_check.p, 64, hipMemcpyDeviceToHost, st));
+    }
     if (status && n) HIPCHK(c, hipMemcpyAsync(status, c->h_status.p, n, hipMemcpyDeviceToHost, st));
     if (bitmap && nw) HIPCHK(c, hipMemcpyAsync(bitmap, c->h_bitmap.p, nw * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
     float ms = 0;
     if (hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) c->stats.last_verify_kernel_ms = ms;
     c->ev_pending = false;
-    if (status)
-        for (uint64_t i = 0; i < n; i++) c->stats.status_count[status[i] & 7]++;
+    for (int k = 0; k < 8; k++) c->stats.status_count[k] += counts[k];
     return CHIP_OK;
 }
 int chip_verify_batch(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap) {
