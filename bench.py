@@ -564,7 +564,7 @@ def main():
                                    "algorithmic_bytes": alg,
                                    "traffic": stx_traffic((tb.ntx + 255) // 256 * 256, (sb.n + 255) // 256 * 256),
                                    "note": "one launch = both parse passes, the pool copy, scans, key interning "
-                                           "and the required-key passes with their 4 host syncs"},
+                                           "and the required-key pass with their 3 host syncs"},
         })
         del bb, bo, bl, bst, holder, p, dm, ids, fst, fv, fa, fm, tb, tm, sb, evs, s_parse
     progress("cfg4 legs done")

@@ -395,8 +395,59 @@ __device__ __forceinline__ bool header_ok(Cur& c) {
     return !c.err;
 }
 
+// requiredSigningKeys walk (WireTransaction.kt:66-75) over one transaction's components in the pool:
+// take(off, len) for each signer key of every Command component in order, then for the notary Party's
+// owningKey when the transaction has inputs or a time-window.  False when a command / notary component
+// is outside the grammar or a key spans a chunk (the caller marks the transaction UNSUPPORTED).
+template <class F>
+__device__ __forceinline__ bool req_walk(Cur& c, const uint8_t* pool, uint64_t pool_bytes, uint64_t c0, uint64_t c1,
+                                         const uint32_t* comp_group, const uint64_t* comp_off,
+                                         const uint32_t* comp_len, F&& take) {
+    uint64_t present = 0;
+    int64_t notary = -1;
+    for (uint64_t k = c0; k < c1; k++) {
+        const uint32_t g = comp_group[k];
+        present |= 1ull << g;
+        if (g == 4 && notary < 0) notary = (int64_t)k;
+    }
+    const bool want_notary = notary >= 0 && ((present & 1) || (present >> 5 & 1));
+    Sink none{nullptr, 0, 0};
+    uint64_t spill = 0;
+    for (uint64_t k = c0; k <= c1; k++) {
+        int64_t kk;
+        if (k < c1) {
+            if (comp_group[k] != 2) continue;
+            kk = (int64_t)k;
+        } else {
+            if (!want_notary) break;
+            kk = notary;
+        }
+        const uint64_t a = comp_off[kk];
+        c.init(pool, pool_bytes, a, a + comp_len[kk]);
+        if (!header_ok(c)) return false;
+        const bool is_cmd = k < c1;
+        if (c.read_class<0>() != (is_cmd ? -C_COMMAND : -C_PARTY)) c.fail(E_UNSUP);
+        c.not_null<0>();
+        if (is_cmd) c.header<0>(H_CMD, 7, 2);
+        else c.header<0>(H_PARTY, 9, 2);
+        c.rem1 = 0;
+        const uint32_t nk = is_cmd ? c.list<1>(true) : 1;
+        for (uint32_t i = 0; i < nk && !c.err; i++) {
+            if (c.read_class<1>() < 14) c.fail(E_UNSUP);
+            c.not_null<1>();
+            const uint32_t kl = c.varint<1>();
+            const uint64_t at = run1<false>(c, kl, none, spill);
+            if (c.err || spill) break;
+            take(at, kl);
+        }
+        if (c.err || spill) return false;
+    }
+    return true;
+}
+
 struct Outs {   // pass-2 destinations (NULL in pass 1)
     uint8_t* pool;
+    uint64_t pool_bytes;
     const uint64_t* extra_start;   // [n + 1] extra region of blob t, relative to extra_base
     uint64_t extra_base;
     uint8_t* salts;
@@ -414,6 +465,7 @@ struct Outs {   // pass-2 destinations (NULL in pass 1)
     uint32_t* key_len;
     const int32_t* meta;
     uint32_t n_meta;
+    uint64_t* nraw;                // CHIP_STX_REQUIRED: signer entries per tx (counted here), else NULL
 };
 
 template <bool EMIT>
@@ -424,7 +476,10 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
                                                    uint64_t* __restrict__ nextra, Outs o) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
-    if (EMIT && status[t] != CHIP_STX_OK) return;
+    if (EMIT && status[t] != CHIP_STX_OK) {
+        if (o.nraw) o.nraw[t] = 0;
+        return;
+    }
     const uint64_t a = off[t], b = a + len[t];
     uint64_t comps = 0, sigs = 0, extra = 0;
     Sink sink{o.pool, EMIT ? o.extra_base + o.extra_start[t] : 0, 0};
@@ -603,7 +658,17 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
 done:
     if (EMIT) {
         sink.flush();
-        if (st != CHIP_STX_OK) status[t] = (uint8_t)st;   // only the duplicate-input check can fail here
+        if (o.nraw) {   // the required-key walk's count, fused here (the components are in the pool now)
+            uint64_t cnt = 0;
+            bool over = false;
+            if (st == CHIP_STX_OK &&
+                !req_walk(c, o.pool, o.pool_bytes, cbase, cbase + comps, o.comp_group, o.comp_off, o.comp_len,
+                          [&](uint64_t, uint32_t) { over |= cnt >= 64; cnt++; }))
+                st = CHIP_STX_UNSUPPORTED;
+            if (over) st = CHIP_STX_UNSUPPORTED;   // more than 64 signer entries: JVM path
+            o.nraw[t] = st == CHIP_STX_OK ? cnt : 0;
+        }
+        if (st != CHIP_STX_OK) status[t] = (uint8_t)st;
     } else {
         status[t] = (uint8_t)st;
         ncomp[t] = st == CHIP_STX_OK ? comps : 0;
@@ -741,20 +806,9 @@ __global__ void __launch_bounds__(256) k_stx_required(uint64_t n, uint8_t* __res
         else nreq[t] = 0;
         return;
     }
-    const uint64_t c0 = comp_start[t], c1 = comp_start[t + 1];
-    uint64_t present = 0;
-    int64_t notary = -1;
-    for (uint64_t k = c0; k < c1; k++) {
-        const uint32_t g = comp_group[k];
-        present |= 1ull << g;
-        if (g == 4 && notary < 0) notary = (int64_t)k;
-    }
-    const bool want_notary = notary >= 0 && ((present & 1) || (present >> 5 & 1));
     uint64_t cnt = 0, kept = 0;
     const uint64_t base = EMIT ? raw_start[t] : 0;
     bool bad = false;
-    Sink none{nullptr, 0, 0};
-    uint64_t spill = 0;
     auto take = [&](uint64_t off, uint32_t len) {
         if (cnt >= 64) {   // the duplicate check is quadratic: more signer entries go to the JVM path
             bad = true;
@@ -777,44 +831,19 @@ __global__ void __launch_bounds__(256) k_stx_required(uint64_t n, uint8_t* __res
         cnt++;
     };
     Cur c;
-    for (uint64_t k = c0; k <= c1 && !bad; k++) {
-        // every command component in order, then the notary component
-        int64_t kk;
-        if (k < c1) {
-            if (comp_group[k] != 2) continue;
-            kk = (int64_t)k;
-        } else {
-            if (!want_notary) break;
-            kk = notary;
-        }
-        const uint64_t a = comp_off[kk];
-        c.init(r.pool, pool_bytes, a, a + comp_len[kk]);
-        if (!header_ok(c)) {
-            bad = true;
-            break;
-        }
-        const bool is_cmd = k < c1;
-        if (c.read_class<0>() != (is_cmd ? -C_COMMAND : -C_PARTY)) c.fail(E_UNSUP);
-        c.not_null<0>();
-        if (is_cmd) c.header<0>(H_CMD, 7, 2);
-        else c.header<0>(H_PARTY, 9, 2);
-        c.rem1 = 0;
-        const uint32_t nk = is_cmd ? c.list<1>(true) : 1;
-        for (uint32_t i = 0; i < nk && !c.err; i++) {
-            if (c.read_class<1>() < 14) c.fail(E_UNSUP);
-            c.not_null<1>();
-            const uint32_t kl = c.varint<1>();
-            const uint64_t at = run1<false>(c, kl, none, spill);
-            if (c.err || spill) break;
-            take(at, kl);
-        }
-        if (c.err || spill) bad = true;
-    }
+    if (!req_walk(c, r.pool, pool_bytes, comp_start[t], comp_start[t + 1], comp_group, comp_off, comp_len, take))
+        bad = true;
     if (!EMIT) {
         if (bad) status[t] = CHIP_STX_UNSUPPORTED;
         nraw[t] = bad ? 0 : cnt;
     } else {
-        nreq[t] = kept;
+        // (after the fused count in the emit pass, the only new failure here is a CompositeKey signer): a
+        // failed transaction keeps none of its counted entries, so the compaction stays aligned
+        if (bad) {
+            status[t] = CHIP_STX_UNSUPPORTED;
+            for (uint64_t j = base; j < raw_start[t + 1]; j++) raw_keep[j] = 0;
+        }
+        nreq[t] = bad ? 0 : kept;
     }
 }
 
@@ -848,8 +877,8 @@ void launch_stx_count(hipStream_t st, const chip_stx_blobs* in, uint8_t* status,
 
 void launch_stx_emit(hipStream_t st, const chip_stx_blobs* in, uint8_t* status, const StxOut& d) {
     if (!in->n) return;
-    Outs o{d.pool, d.extra_start, d.extra_base, d.salts, d.comp_start, d.comp_group, d.comp_internal, d.comp_off, d.comp_len, d.sig_start,
-           d.tx_idx, d.tmpl_idx, d.sig_off, d.sig_len, d.skey_off, d.skey_len, d.meta, d.n_meta};
+    Outs o{d.pool, d.pool_bytes, d.extra_start, d.extra_base, d.salts, d.comp_start, d.comp_group, d.comp_internal, d.comp_off, d.comp_len, d.sig_start,
+           d.tx_idx, d.tmpl_idx, d.sig_off, d.sig_len, d.skey_off, d.skey_len, d.meta, d.n_meta, d.nraw};
     hipLaunchKernelGGL(k_stx_parse<true>, grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->off, in->len,
                        in->data_bytes, status, nullptr, nullptr, nullptr, o);
 }

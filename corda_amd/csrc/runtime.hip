@@ -857,6 +857,10 @@ int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_sta
         HIPCHK(c, hipMemcpyAsync(B.s_meta.p, in->meta, (uint64_t)in->n_meta * 8, hipMemcpyHostToDevice, st));
     StxOut d{};
     d.pool = B.s_pool.as<uint8_t>();
+    d.pool_bytes = pool;
+    const bool want_req = in->flags & CHIP_STX_REQUIRED;
+    if (want_req) HIPCHK(c, B.r_nraw.ensure(n1 * 8));
+    d.nraw = want_req ? B.r_nraw.as<uint64_t>() : nullptr;
     d.extra_start = B.s_pstart.as<uint64_t>();
     d.extra_base = extra_base;
     d.salts = B.s_salts.as<uint8_t>();
@@ -892,19 +896,16 @@ int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_sta
     HIPCHK(c, hipGetLastError());
     uint32_t nkeys = 0;
     if (nsig) HIPCHK(c, hipMemcpyAsync(&nkeys, B.s_kincl.as<uint32_t>() + nsig - 1, 4, hipMemcpyDeviceToHost, st));
-    if (in->flags & CHIP_STX_REQUIRED) {
-        // requiredSigningKeys: R1 counts signer entries, scan, R2 writes them + duplicate flags, scans,
-        // compaction into one leaf per distinct required key
+    if (want_req) {
+        // requiredSigningKeys: the emit pass counted the signer entries; scan, R2 writes them with key
+        // indices + duplicate flags, scans, compaction into one leaf per distinct required key
         StxReq q{};
-        HIPCHK(c, B.r_nraw.ensure(n1 * 8));
         HIPCHK(c, B.r_rstart.ensure(n1 * 8));
         HIPCHK(c, B.r_nreq.ensure(n1 * 8));
         HIPCHK(c, B.r_qstart.ensure(n1 * 8));
         q.nraw = B.r_nraw.as<uint64_t>();
         q.raw_start = B.r_rstart.as<uint64_t>();
         q.nreq = B.r_nreq.as<uint64_t>();
-        launch_stx_required(st, false, n, tx_status, d, pool, cap - 1, q);
-        HIPCHK(c, hipGetLastError());
         HIPCHK(c, hipMemsetAsync(q.raw_start, 0, 8, st));
         if (n) HIPCHK(c, stx_scan_u64(st, B.s_temp.p, B.s_temp.cap, q.nraw, q.raw_start + 1, n));
         uint64_t nraw = 0;

@@ -60,6 +60,8 @@ void launch_required_signers(hipStream_t st, const chip_req_batch* q, uint64_t n
 // Kryo front end (kryo.hip): SignedTransaction bytes -> tx / signer batches in the context's buffers
 struct StxOut {
     uint8_t* pool;                 // copy of the blobs + the extra region (de-chunked spanning runs)
+    uint64_t pool_bytes;
+    uint64_t* nraw;                // CHIP_STX_REQUIRED: signer entries per tx, counted by the emit pass
     const uint64_t* extra_start;   // [n + 1] extra region of blob t, relative to extra_base
     uint64_t extra_base;
     uint8_t* salts;                // [n * 32]

@@ -364,7 +364,7 @@ int chip_verify_signed_tx_batch_device(chip_ctx* ctx, const chip_tx_batch* txs, 
  * component outside the device grammar, a chunk-spanning key, more than 64 signer entries (commands' signers
  * + notary, before de-duplication) or a CompositeKey among the required keys
  * (its tree is not in the signer pool) turns the transaction's status into CHIP_STX_UNSUPPORTED.
- * Synchronises with `stream` twice (four times with CHIP_STX_REQUIRED): the totals size the outputs. */
+ * Synchronises with `stream` twice (three times with CHIP_STX_REQUIRED): the totals size the outputs. */
 enum chip_stx_status { CHIP_STX_OK = 0, CHIP_STX_KRYO = 1, CHIP_STX_NO_SIGS = 2, CHIP_STX_INVARIANT = 3,
                        CHIP_STX_UNSUPPORTED = 4 };
 typedef struct {
