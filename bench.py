@@ -71,7 +71,7 @@ ECDSA_Q_MACS_PER_VERIFY = 65 * 592 + 100                            # k_ecdsa_co
 SHA256_OPS_PER_COMPRESSION = 2_168
 # HBM traffic per launch comes from the committed PMC passes of the same command (tools/profile.sh):
 # FETCH_SIZE + WRITE_SIZE (KiB) of the launch with the same grid
-PROFILE_DIR = os.path.join(ROOT, "profiles", os.environ.get("CORDA_PROFILE_DIR", "r02e"))
+PROFILE_DIR = os.path.join(ROOT, "profiles", os.environ.get("CORDA_PROFILE_DIR", "r02f"))
 # VALU issue peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6e12 lane-ops/s (a wave64 VALU
 # instruction issues over 2 cycles, MI355X_MICROARCH.md).  v_mad_u64_u32 issues at a quarter of
 # that: 19.66e12 MACs/s (tools/microbench_mul.hip measures 18.0e12).
@@ -204,8 +204,7 @@ def profile_traffic(kernel, grid):
 def stx_traffic(grid_tx, grid_sig):
     """FETCH_SIZE + WRITE_SIZE of one Kryo front-end call (both parse passes, the key interning and the
     required-key passes; the pool copy is a DMA, not counted) from the committed PMC profile, or None."""
-    parts = [profile_traffic(k, grid_tx) for k in ("k_stx_parse<false>", "k_stx_parse<true>", "k_stx_required<false>",
-                                                    "k_stx_required<true>")]
+    parts = [profile_traffic(k, grid_tx) for k in ("k_stx_parse<false>", "k_stx_parse<true>", "k_stx_required<true>")]
     parts += [profile_traffic(k, grid_sig) for k in ("k_stx_key_insert", "k_stx_key_flag", "k_stx_key_assign",
                                                       "k_stx_req_compact")]
     return None if any(p is None for p in parts) else sum(parts)
