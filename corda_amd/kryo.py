@@ -15,12 +15,17 @@ KRYO_P2P_CONTEXT, references on) from the published Kryo 4.0.0 algorithms as Cor
   header      "corda" 00 00 01                                    SerializationScheme.kt:251 (KryoHeaderV0_1)
   object      kryo.writeClassAndObject(output, obj)               SerializationScheme.kt:218-239
   class       registered classes as varint(id + 2).  The Kryo constructor registers 10 primitives
-              (ids 0-9); DefaultKryoCustomizer.kt:76-79 then registers Arrays$ArrayList (10),
-              SignedTransaction (11), WireTransaction (12), SerializedBytes (13).  Later
-              registrations (PrivacySalt, the PublicKey classes, DefaultKryoCustomizer.kt:86-112)
-              follow a library-dependent number of javakaffee / Guava registrations (:80-85), so
-              their ids are NOT pinned here: readers accept any registered id >= 14 where the
-              position fixes the meaning; writers take the ids as parameters.
+              (ids 0-9); DefaultKryoCustomizer.kt:77-80 then registers Arrays$ArrayList (10),
+              SignedTransaction (11), WireTransaction (12), SerializedBytes (13).  Every later id
+              follows from the registration ORDER of DefaultKryoCustomizer.kt:81-122 (REGISTRATION_ORDER
+              below: Kryo.register gives a new class the next free id, a class registered twice keeps
+              its first id).  The javakaffee / Guava blocks (:81-86) register library-dependent class
+              sets (kryo-serializers 0.41, Guava 21.0 — neither jar is under /root/reference): their
+              counts are restated from those versions' published sources, so the ids from PrivacySalt
+              and the PublicKey classes on are UNPINNED defaults.  They live in a Registry that a
+              deployment overwrites with its JVM's own ids (chip_set_kryo_registry, INTEGRATION.md);
+              readers accept exactly the registry's id where the position fixes the class and fail
+              closed (KryoUnsupported -> the JVM path) on any other id.
               Unregistered @CordaSerializable / whitelisted classes are registered implicitly by
               NAME (CordaClassResolver.registerImplicit, CordaClassResolver.kt:76-99): varint(1),
               varint(name id), the name string the first time per graph (ids restart every graph)
@@ -61,11 +66,146 @@ KRYO_HEADER_V0_1 = b"corda\x00\x00\x01"
 NULL, NOT_NULL, NAME = 0, 1, -1
 CHUNK = 1024
 
-# registration ids pinned by DefaultKryoCustomizer.kt:76-79 (after the Kryo constructor's 0-9)
-REG_ARRAYS_ASLIST, REG_SIGNED_TX, REG_WIRE_TX, REG_SERIALIZED_BYTES = 10, 11, 12, 13
-FIRST_UNPINNED_ID = 14
-# NOT pinned (library-dependent): placeholders the writers use by default; readers accept any id >= 14
-DEFAULT_IDS = {"privacy_salt": 47, "eddsa_public_key": 31, "bcec_public_key": 42, "composite_key": 33}
+# ---- class registrations (DefaultKryoCustomizer.kt:56-136) ----
+# The Kryo constructor registers int, String, float, boolean, byte, char, short, long, double, void
+# (ids 0-9); customize() then registers, in this order (file:line of the register call), one id per NEW
+# class.  The javakaffee blocks list the classes their registerSerializers(kryo) registers under
+# kryo-serializers 0.41 with Guava 21.0 (node-api/build.gradle:26, constants.properties:3), already
+# reduced to distinct classes: e.g. ImmutableList.of() and .of().reverse() are both RegularImmutableList
+# in Guava 21, .subList(1, 2) of a 3-list is a SingletonImmutableList.  Those two libraries are not
+# under /root/reference, so from :81 on the ids are restated, not pinned (see the module docstring).
+REGISTRATION_ORDER = [
+    ("java.util.Arrays$ArrayList", "DefaultKryoCustomizer.kt:77"),
+    ("net.corda.core.transactions.SignedTransaction", ":78"),
+    ("net.corda.core.transactions.WireTransaction", ":79"),
+    ("net.corda.core.serialization.SerializedBytes", ":80"),
+    # :81 UnmodifiableCollectionsSerializer: one class per UnmodifiableCollection constant
+    ("java.util.Collections$UnmodifiableCollection", ":81"),
+    ("java.util.Collections$UnmodifiableRandomAccessList", ":81"),
+    ("java.util.Collections$UnmodifiableList", ":81"),
+    ("java.util.Collections$UnmodifiableSet", ":81"),
+    ("java.util.Collections$UnmodifiableSortedSet", ":81"),
+    ("java.util.Collections$UnmodifiableMap", ":81"),
+    ("java.util.Collections$UnmodifiableSortedMap", ":81"),
+    # :82 ImmutableListSerializer: ImmutableList, of(), of(1), of(1,2,3).subList(1,2), of().reverse(),
+    # Lists.charactersOf(..), ImmutableTable.copyOf(..).values()
+    ("com.google.common.collect.ImmutableList", ":82"),
+    ("com.google.common.collect.RegularImmutableList", ":82"),
+    ("com.google.common.collect.SingletonImmutableList", ":82"),
+    ("com.google.common.collect.Lists$StringAsImmutableList", ":82"),
+    ("com.google.common.collect.RegularImmutableTable$Values", ":82"),
+    # :83 ImmutableSetSerializer: ImmutableSet, of(), of(1), of(1,2,3), Sets.immutableEnumSet(..)
+    ("com.google.common.collect.ImmutableSet", ":83"),
+    ("com.google.common.collect.RegularImmutableSet", ":83"),
+    ("com.google.common.collect.SingletonImmutableSet", ":83"),
+    ("com.google.common.collect.ImmutableEnumSet", ":83"),
+    # :84 ImmutableSortedSetSerializer: ImmutableSortedSet, of(), of(""), of().descendingSet()
+    ("com.google.common.collect.ImmutableSortedSet", ":84"),
+    ("com.google.common.collect.RegularImmutableSortedSet", ":84"),
+    # :85 ImmutableMapSerializer: ImmutableMap, of(), of(k, v), of(k, v, k, v), copyOf(EnumMap)
+    ("com.google.common.collect.ImmutableMap", ":85"),
+    ("com.google.common.collect.RegularImmutableBiMap", ":85"),
+    ("com.google.common.collect.SingletonImmutableBiMap", ":85"),
+    ("com.google.common.collect.RegularImmutableMap", ":85"),
+    ("com.google.common.collect.ImmutableEnumMap", ":85"),
+    # :86 ImmutableMultimapSerializer: ImmutableMultimap, ImmutableListMultimap.of() / .of(a, b),
+    # ImmutableSetMultimap.of() / .of(a, b)
+    ("com.google.common.collect.ImmutableMultimap", ":86"),
+    ("com.google.common.collect.EmptyImmutableListMultimap", ":86"),
+    ("com.google.common.collect.ImmutableListMultimap", ":86"),
+    ("com.google.common.collect.EmptyImmutableSetMultimap", ":86"),
+    ("com.google.common.collect.ImmutableSetMultimap", ":86"),
+    ("java.io.BufferedInputStream", ":88"),
+    ("sun.net.www.protocol.jar.JarURLConnection$JarURLInputStream", ":89"),
+    ("sun.security.ec.ECPublicKeyImpl", ":91"),
+    ("net.i2p.crypto.eddsa.EdDSAPublicKey", ":92"),
+    ("net.i2p.crypto.eddsa.EdDSAPrivateKey", ":93"),
+    ("net.corda.core.crypto.CompositeKey", ":94"),
+    ("[Ljava.lang.StackTraceElement;", ":96"),
+    ("net.corda.core.utilities.NonEmptySet", ":98"),
+    ("java.util.BitSet", ":99"),
+    ("java.lang.Class", ":100"),
+    ("java.io.FileInputStream", ":101"),
+    ("java.security.cert.CertPath", ":102"),
+    ("sun.security.provider.certpath.X509CertPath", ":103"),
+    ("org.bouncycastle.asn1.x500.X500Name", ":104"),
+    ("org.bouncycastle.cert.X509CertificateHolder", ":105"),
+    ("org.bouncycastle.jcajce.provider.asymmetric.ec.BCECPrivateKey", ":106"),
+    ("org.bouncycastle.jcajce.provider.asymmetric.ec.BCECPublicKey", ":107"),
+    ("org.bouncycastle.jcajce.provider.asymmetric.rsa.BCRSAPrivateCrtKey", ":108"),
+    ("org.bouncycastle.jcajce.provider.asymmetric.rsa.BCRSAPublicKey", ":109"),
+    ("org.bouncycastle.pqc.jcajce.provider.sphincs.BCSphincs256PrivateKey", ":110"),
+    ("org.bouncycastle.pqc.jcajce.provider.sphincs.BCSphincs256PublicKey", ":111"),
+    ("net.corda.core.transactions.NotaryChangeWireTransaction", ":112"),
+    ("net.corda.core.identity.PartyAndCertificate", ":113"),
+    ("net.corda.core.contracts.PrivacySalt", ":116"),
+    ("net.corda.core.contracts.ContractAttachment", ":119"),
+    ("java.lang.invoke.SerializedLambda", ":121"),
+    ("com.esotericsoftware.kryo.serializers.ClosureSerializer$Closure", ":122"),
+]
+FIRST_CUSTOM_ID = 10
+
+
+def registration_ids(order=REGISTRATION_ORDER) -> Dict[str, int]:
+    """class name -> id: Kryo.register assigns the next free id to a class not registered yet."""
+    ids: Dict[str, int] = {}
+    for name, _ in order:
+        ids.setdefault(name, FIRST_CUSTOM_ID + len(ids))
+    return ids
+
+
+# the classes registered with PublicKeySerializer (DefaultKryoCustomizer.kt:91,92,94,107,109,111): whichever
+# of them a key slot names, the JVM reads writeBytesWithLength(encoded) -> Crypto.decodePublicKey (Kryo.kt:302-311)
+PUBLIC_KEY_CLASSES = ["sun.security.ec.ECPublicKeyImpl", "net.i2p.crypto.eddsa.EdDSAPublicKey",
+                      "net.corda.core.crypto.CompositeKey",
+                      "org.bouncycastle.jcajce.provider.asymmetric.ec.BCECPublicKey",
+                      "org.bouncycastle.jcajce.provider.asymmetric.rsa.BCRSAPublicKey",
+                      "org.bouncycastle.pqc.jcajce.provider.sphincs.BCSphincs256PublicKey"]
+MAX_PUBLIC_KEY_IDS = 8   # chip_kryo_registry.public_key[]
+
+
+class Registry:
+    """The registration ids the front end depends on (the C-ABI's chip_kryo_registry): the four pinned
+    ones, PrivacySalt's, and every id whose serializer is PublicKeySerializer.  Defaults: the restated
+    REGISTRATION_ORDER; a deployment passes its JVM's Kryo ids (kryo.getRegistration(cls).id)."""
+
+    def __init__(self, ids: Optional[Dict[str, int]] = None):
+        ids = registration_ids() if ids is None else ids
+        self.arrays_aslist = ids["java.util.Arrays$ArrayList"]
+        self.signed_tx = ids["net.corda.core.transactions.SignedTransaction"]
+        self.wire_tx = ids["net.corda.core.transactions.WireTransaction"]
+        self.serialized_bytes = ids["net.corda.core.serialization.SerializedBytes"]
+        self.privacy_salt = ids["net.corda.core.contracts.PrivacySalt"]
+        self.eddsa_public_key = ids["net.i2p.crypto.eddsa.EdDSAPublicKey"]
+        self.bcec_public_key = ids["org.bouncycastle.jcajce.provider.asymmetric.ec.BCECPublicKey"]
+        self.composite_key = ids["net.corda.core.crypto.CompositeKey"]
+        self.public_key = [ids[c] for c in PUBLIC_KEY_CLASSES if c in ids][:MAX_PUBLIC_KEY_IDS]
+
+    def as_tuple(self):
+        return (self.arrays_aslist, self.signed_tx, self.wire_tx, self.serialized_bytes, self.privacy_salt,
+                tuple(self.public_key))
+
+    def key_class_for(self, spki: bytes) -> int:
+        """The class a JVM writes for a key with this encoding (EdDSAPublicKey / BCECPublicKey / CompositeKey)."""
+        if len(spki) == 44:
+            return self.eddsa_public_key
+        if _spki_oid_is_composite(spki):
+            return self.composite_key
+        return self.bcec_public_key
+
+
+DEFAULT_REGISTRY = Registry()
+REG_ARRAYS_ASLIST = DEFAULT_REGISTRY.arrays_aslist       # 10: pinned by DefaultKryoCustomizer.kt:77-80
+REG_SIGNED_TX = DEFAULT_REGISTRY.signed_tx               # 11
+REG_WIRE_TX = DEFAULT_REGISTRY.wire_tx                   # 12
+REG_SERIALIZED_BYTES = DEFAULT_REGISTRY.serialized_bytes # 13
+DEFAULT_IDS = {"privacy_salt": DEFAULT_REGISTRY.privacy_salt, "eddsa_public_key": DEFAULT_REGISTRY.eddsa_public_key,
+               "bcec_public_key": DEFAULT_REGISTRY.bcec_public_key, "composite_key": DEFAULT_REGISTRY.composite_key}
+
+
+def _spki_oid_is_composite(spki: bytes) -> bool:
+    from corda_amd import composite as CK
+    return CK._spki_oid(bytes(spki)) == CK._COMPOSITE_OID_TLV
 
 SIGNABLE_DATA = "net.corda.core.crypto.SignableData"
 SECURE_HASH_SHA256 = "net.corda.core.crypto.SecureHash$SHA256"
@@ -393,7 +533,7 @@ def signed_transaction(tx_bits: bytes, sigs: Sequence[Sig], list_kind: str = "au
         g.marker(c)
 
         def by(f: Out):                          # PublicKey (interface): class, marker, PublicKeySerializer
-            kid = s.key_class_id if s.key_class_id is not None else DEFAULT_IDS["eddsa_public_key"]
+            kid = s.key_class_id if s.key_class_id is not None else DEFAULT_REGISTRY.key_class_for(s.key)
             g.write_class(f, kid)
             g.marker(f)
             f.write_varint(len(s.key))
@@ -414,12 +554,13 @@ class Reader:
     reader sharing the graph's name ids and headers (InputChunked.nextChunks semantics: unread
     bytes of a field are skipped)."""
 
-    def __init__(self, buf: bytes, pos: int = 0, end: Optional[int] = None):
+    def __init__(self, buf: bytes, pos: int = 0, end: Optional[int] = None, reg: Registry = DEFAULT_REGISTRY):
         self.buf = buf
         self.pos = pos
         self.end = len(buf) if end is None else end
         self.names: Dict[int, str] = {}
         self.headers: Dict[str, List[str]] = {}
+        self.reg = reg
 
     def byte(self) -> int:
         if self.pos >= self.end:
@@ -436,47 +577,31 @@ class Reader:
         return bytes(b)
 
     def varint(self, optimize_positive: bool = True) -> int:
-        v, shift = 0, 0
-        while True:
+        """Input.readVarInt: at most 5 bytes; the 5th byte's 7 bits all shift in (bits >= 32 drop)."""
+        v = 0
+        for i in range(5):
             b = self.byte()
-            v |= (b & 0x7F) << shift
-            shift += 7
+            v |= (b & 0x7F) << (7 * i)
             if not b & 0x80:
-                break
-            if shift > 28:
-                b = self.byte()
-                v |= (b & 0x7F) << shift
                 break
         v &= 0xFFFFFFFF
         if not optimize_positive:
             v = (v >> 1) ^ -(v & 1)
         return v
 
-    def string(self) -> str:
-        b = self.byte()
-        if b & 0x80 == 0:                  # ASCII run, last byte flagged
-            out = bytearray([b])
-            while True:
-                c = self.byte()
-                if c & 0x80:
-                    out.append(c & 0x7F)
-                    return out.decode("ascii")
-                out.append(c)
-        v = b & 0x3F
-        if b & 0x40:
-            shift = 6
-            while True:
-                c = self.byte()
-                v |= (c & 0x7F) << shift
-                shift += 7
-                if not c & 0x80:
-                    break
-        if v == 0:
-            raise KryoException("null string")
-        n = v - 1
-        s = bytes(self.buf[self.pos:self.end]).decode("utf-8", errors="strict")[:n]
-        self.pos += len(s.encode("utf-8"))
-        return s
+    def string(self, max_chars: int = 64) -> str:
+        """Input.readString restricted to the form the grammar's names take (Output.writeString's ASCII
+        form: bit 7 on the last byte): a UTF-8-form string, or one running past max_chars + 1 characters
+        without its last byte, is outside the device grammar (KryoUnsupported)."""
+        out = bytearray()
+        for i in range(max_chars + 2):
+            c = self.byte()
+            if i == 0 and c & 0x80:
+                raise KryoUnsupported("UTF-8 form string")
+            out.append(c & 0x7F)
+            if c & 0x80:
+                return out.decode("ascii")
+        raise KryoUnsupported("string longer than %d characters" % (max_chars + 1))
 
     def read_class(self):
         """-> registered id (int) or class name (str); None for a null."""
@@ -489,17 +614,12 @@ class Reader:
         if nid not in self.names:
             if nid != len(self.names) or nid >= 8:     # the device keeps 8 name ids per graph
                 raise KryoUnsupported("class name id %d" % nid)
-            self.names[nid] = self.string()
+            self.names[nid] = self.string(200)
         return self.names[nid]
 
     def not_null(self):
         if self.varint() != NOT_NULL:
             raise KryoUnsupported("expected a first-seen object (back-references / null unsupported)")
-
-    def field_names(self, cls: str) -> List[str]:
-        if cls not in self.headers:
-            self.headers[cls] = [self.string() for _ in range(self.varint())]
-        return self.headers[cls]
 
     def chunk(self) -> "Reader":
         data = bytearray()
@@ -508,15 +628,15 @@ class Reader:
             if n == 0:
                 break
             data += self.take(n)
-        r = Reader(bytes(data))
+        r = Reader(bytes(data), reg=self.reg)
         r.names, r.headers = self.names, self.headers   # one graph
         return r
 
 
-def _header(buf: bytes) -> Reader:
+def _header(buf: bytes, reg: Registry = DEFAULT_REGISTRY) -> Reader:
     if bytes(buf[:8]) != KRYO_HEADER_V0_1:
         raise KryoException("Serialized bytes header does not match expected format.")
-    return Reader(buf, 8)
+    return Reader(buf, 8, reg=reg)
 
 
 def _expect_fields(r: Reader, cls: str, names: List[str]):
@@ -548,7 +668,7 @@ def _read_list(r: Reader, references: bool, read_item: Callable[[Reader], object
         return [read_item(r)]
     if cls == ARRAY_LIST:
         return [read_item(r) for _ in range(r.varint())]
-    if cls == REG_ARRAYS_ASLIST:
+    if cls == r.reg.arrays_aslist:
         n = r.varint()
         r.read_class()                           # the array's component class
         return [read_item(r) for _ in range(n)]
@@ -580,15 +700,15 @@ def parse_signable_data(buf: bytes) -> Tuple[bytes, int, int]:
     return tx_id, pv, sch
 
 
-def parse_wire_transaction(buf: bytes) -> Tuple[List[Tuple[int, List[bytes]]], bytes]:
+def parse_wire_transaction(buf: bytes, reg: Registry = DEFAULT_REGISTRY) -> Tuple[List[Tuple[int, List[bytes]]], bytes]:
     """WireTransactionSerializer.read (Kryo.kt:242-246): ([(groupIndex, [component bytes])], salt)."""
-    r = _header(buf)
-    if r.read_class() != REG_WIRE_TX:
+    r = _header(buf, reg)
+    if r.read_class() != reg.wire_tx:
         raise KryoUnsupported("not a WireTransaction")
     r.not_null()
 
     def comp(c: Reader) -> bytes:
-        if c.read_class() != REG_SERIALIZED_BYTES:
+        if c.read_class() != reg.serialized_bytes:
             raise KryoUnsupported("component is not SerializedBytes")
         return c.take(c.varint())
 
@@ -603,22 +723,26 @@ def parse_wire_transaction(buf: bytes) -> Tuple[List[Tuple[int, List[bytes]]], b
         return gi, comps
 
     groups = _read_list(r, False, group)
-    sid = r.read_class()
-    if not isinstance(sid, int) or sid < FIRST_UNPINNED_ID:
-        raise KryoUnsupported("privacySalt is not a registered class")
+    if r.read_class() != reg.privacy_salt:       # another registered class: another serializer
+        raise KryoUnsupported("privacySalt is not the registered PrivacySalt class")
     if r.varint() != 32:                         # PrivacySalt.init require: left to the JVM path
         raise KryoUnsupported("Privacy salt should be 32 bytes.")
     salt = r.take(32)
     return groups, salt
 
 
-def parse_signed_transaction(buf: bytes) -> Tuple[bytes, List[Tuple[bytes, bytes, int, int]]]:
+def _key_class_ok(reg: Registry, kid) -> bool:
+    """A key slot names a class registered with PublicKeySerializer (the same decode for all of them)."""
+    return isinstance(kid, int) and kid in reg.public_key
+
+
+def parse_signed_transaction(buf: bytes, reg: Registry = DEFAULT_REGISTRY) -> Tuple[bytes, List[Tuple[bytes, bytes, int, int]]]:
     """SignedTransactionSerializer.read (Kryo.kt:273-278): (txBits, [(sig, key SPKI, pv, scheme)])."""
-    r = _header(buf)
-    if r.read_class() != REG_SIGNED_TX:
+    r = _header(buf, reg)
+    if r.read_class() != reg.signed_tx:
         raise KryoUnsupported("not a SignedTransaction")
     r.not_null()
-    if r.read_class() != REG_SERIALIZED_BYTES:
+    if r.read_class() != reg.serialized_bytes:
         raise KryoUnsupported("txBits is not SerializedBytes")
     r.not_null()
     tx_bits = r.take(r.varint())
@@ -635,9 +759,8 @@ def parse_signed_transaction(buf: bytes) -> Tuple[bytes, List[Tuple[bytes, bytes
             raise KryoUnsupported("null signature bytes")
         sig = f.take(n - 1)
         f = c.chunk()
-        kid = f.read_class()
-        if not isinstance(kid, int) or kid < FIRST_UNPINNED_ID:
-            raise KryoUnsupported("key class is not a registered PublicKey class")
+        if not _key_class_ok(reg, f.read_class()):
+            raise KryoUnsupported("key class is not registered with PublicKeySerializer")
         f.not_null()
         key = f.take(f.varint())
         pv, sch = _read_metadata(c.chunk())
@@ -647,13 +770,74 @@ def parse_signed_transaction(buf: bytes) -> Tuple[bytes, List[Tuple[bytes, bytes
     return tx_bits, sigs
 
 
+# ---- StateRef components (the inputs group: SerializedBytes<StateRef>, MerkleTransaction.kt:23) ----
+STATE_REF = "net.corda.core.contracts.StateRef"
+STATEREF_FIELDS = ["StateRef.index", "StateRef.txhash"]
+
+
+def state_ref(txhash: bytes, index: int) -> bytes:
+    """StateRef(SecureHash.SHA256(txhash), index).serialize().bytes (Structures.kt:143-145): fields sort as
+    StateRef.index (zig-zag int), StateRef.txhash (SecureHash is sealed: class, marker, OpaqueBytes.bytes)."""
+    if len(txhash) != 32:
+        raise KryoException("SecureHash.SHA256 needs 32 bytes")
+    g = Graph()
+    o = Out()
+    o.write_bytes(KRYO_HEADER_V0_1)
+    g.write_class(o, STATE_REF)
+    g.marker(o)
+
+    def txh(c: Out):
+        g.write_class(c, SECURE_HASH_SHA256)
+        g.marker(c)
+        g.compatible(c, SECURE_HASH_SHA256, [("OpaqueBytes.bytes", _bytes_field(g, txhash))])
+
+    g.compatible(o, STATE_REF, [("StateRef.index", lambda c: c.write_varint(index, False)), ("StateRef.txhash", txh)])
+    return o.getvalue()
+
+
+def state_ref_of(comp: bytes) -> Optional[Tuple[bytes, int]]:
+    """(txhash, index) when `comp` is the canonical encoding of a StateRef (what a JVM writes for it), else
+    None.  checkNoDuplicateInputs compares decoded StateRefs (BaseTransaction.kt:37); requiring the
+    canonical encoding makes byte equality of two inputs the same as StateRef equality, so the device
+    compares bytes and hands anything else to the JVM path."""
+    try:
+        r = _header(comp)
+        if r.read_class() != STATE_REF:
+            return None
+        r.not_null()
+        _expect_fields(r, STATE_REF, STATEREF_FIELDS)
+        index = r.chunk().varint(False)
+        t = r.chunk()
+        if t.read_class() != SECURE_HASH_SHA256:
+            return None
+        t.not_null()
+        _expect_fields(t, SECURE_HASH_SHA256, ["OpaqueBytes.bytes"])
+        a = t.chunk()
+        a.not_null()
+        if a.varint() != 33:
+            return None
+        h = a.take(32)
+    except KryoException:
+        return None
+    return (h, index) if bytes(comp) == state_ref(h, index) else None
+
+
 # ---- WireTransaction.init / SignedTransaction.init checks the device front end applies ----
 GROUP_INPUTS, GROUP_OUTPUTS, GROUP_COMMANDS, GROUP_ATTACHMENTS, GROUP_NOTARY, GROUP_TIMEWINDOW = range(6)
 
 
 def wire_invariant_error(groups: Sequence[Tuple[int, Sequence[bytes]]], check_duplicates: bool = True) -> Optional[str]:
-    """The structural part of WireTransaction.init (WireTransaction.kt:53-60, BaseTransaction.kt:30-33):
-    the message of the IllegalStateException it throws, or None."""
+    """The structural checks of WireTransaction deserialisation in the order the JVM meets them:
+    TraversableTransaction's notary / time-window initialisers (MerkleTransaction.kt:30-40, the first group
+    of each index), then WireTransaction.init (WireTransaction.kt:53-60, BaseTransaction.kt:30-37): the
+    message of the IllegalStateException, or None."""
+    first = {}
+    for gi, comps in groups:
+        first.setdefault(gi, comps)
+    if len(first.get(GROUP_NOTARY, ())) > 1:
+        return "Invalid Transaction. More than 1 notary party detected."
+    if len(first.get(GROUP_TIMEWINDOW, ())) > 1:
+        return "Invalid Transaction. More than 1 time-window detected."
     if not all(len(c) for _, c in groups):
         return "Empty component groups are not allowed"
     idx = [gi for gi, _ in groups]
@@ -663,7 +847,7 @@ def wire_invariant_error(groups: Sequence[Tuple[int, Sequence[bytes]]], check_du
     if GROUP_INPUTS in present and GROUP_NOTARY not in present:
         return "The notary must be specified explicitly for any transaction that has inputs"
     inputs = [bytes(c) for gi, comps in groups if gi == GROUP_INPUTS for c in comps]
-    if check_duplicates and len(set(inputs)) != len(inputs):      # StateRef equality = equality of its serialized bytes
+    if check_duplicates and len(set(inputs)) != len(inputs):      # canonical StateRefs: bytes = value
         return "Duplicate input states detected"
     if GROUP_INPUTS not in present and GROUP_OUTPUTS not in present:
         return "A transaction must contain at least one input or output state"
@@ -676,14 +860,18 @@ def wire_invariant_error(groups: Sequence[Tuple[int, Sequence[bytes]]], check_du
 
 # ---- the front end's verdict per SignedTransaction (host mirror of chip_stx_parse_device) ----
 STX_OK, STX_KRYO, STX_NO_SIGS, STX_INVARIANT, STX_UNSUPPORTED = range(5)
+MAX_INPUTS = 64          # the device's duplicate-input check covers <= 64 inputs
+MAX_SIGNER_ENTRIES = 64  # commands' signers + the notary, before de-duplication
 
 
-def stx_parse(buf: bytes):
+def stx_parse(buf: bytes, reg: Registry = DEFAULT_REGISTRY):
     """-> (status, groups, salt, sigs): what SignedTransaction deserialisation, the lazy WireTransaction
     deserialisation and their init checks make of `buf`, in the order the JVM meets them (cordahip.h
-    chip_stx_status).  groups / salt / sigs are None unless status is STX_OK."""
+    chip_stx_status).  groups / salt / sigs are None unless status is STX_OK.  After the structural
+    checks: an input that is not a canonical StateRef, or more than 64 inputs -> STX_UNSUPPORTED; then
+    duplicate inputs -> STX_INVARIANT."""
     try:
-        tx_bits, sigs = parse_signed_transaction(buf)
+        tx_bits, sigs = parse_signed_transaction(buf, reg)
     except KryoUnsupported:
         return STX_UNSUPPORTED, None, None, None
     except KryoException:
@@ -691,15 +879,16 @@ def stx_parse(buf: bytes):
     if not sigs:                                 # SignedTransaction.init require(sigs.isNotEmpty())
         return STX_NO_SIGS, None, None, None
     try:
-        groups, salt = parse_wire_transaction(tx_bits)
+        groups, salt = parse_wire_transaction(tx_bits, reg)
     except KryoUnsupported:
         return STX_UNSUPPORTED, None, None, None
     except KryoException:
         return STX_KRYO, None, None, None
     if wire_invariant_error(groups, check_duplicates=False) is not None:
         return STX_INVARIANT, None, None, None
-    if sum(len(c) for gi, c in groups if gi == GROUP_INPUTS) > 64:
-        return STX_UNSUPPORTED, None, None, None  # the device's duplicate-input check covers <= 64 inputs
+    inputs = [c for gi, cs in groups if gi == GROUP_INPUTS for c in cs]
+    if any(state_ref_of(c) is None for c in inputs) or len(inputs) > MAX_INPUTS:
+        return STX_UNSUPPORTED, None, None, None
     if wire_invariant_error(groups) is not None:
         return STX_INVARIANT, None, None, None
     return STX_OK, groups, salt, sigs
@@ -723,10 +912,11 @@ def _key_object(g: Graph, o: Out, key: bytes, key_class_id) -> None:
 
 
 def command(signers: Sequence[bytes], value_class: str = "net.corda.finance.contracts.asset.Cash$Commands$Move",
-            key_class_id=DEFAULT_IDS["eddsa_public_key"], list_kind="auto") -> bytes:
+            key_class_id=None, list_kind="auto") -> bytes:
     """Command(value, signers).serialize().bytes (Structures.kt:179-185): a CompatibleFieldSerializer
     object whose fields sort as Command.signers, Command.value; the value here is an object of
-    `value_class` with no fields (the front end reads only the signers)."""
+    `value_class` with no fields (the front end reads only the signers).  key_class_id None = the class
+    a JVM writes for each key (EdDSAPublicKey / BCECPublicKey / CompositeKey)."""
     g = Graph()
     o = Out()
     o.write_bytes(KRYO_HEADER_V0_1)
@@ -739,14 +929,13 @@ def command(signers: Sequence[bytes], value_class: str = "net.corda.finance.cont
         g.compatible(c, value_class, [])
 
     g.compatible(o, COMMAND, [
-        ("Command.signers", lambda c: _list(g, c, list(signers), lambda f, k: _key_object(g, f, k, key_class_id),
-                                            list_kind)),
+        ("Command.signers", lambda c: _list(g, c, list(signers), lambda f, k: _key_object(
+            g, f, k, DEFAULT_REGISTRY.key_class_for(k) if key_class_id is None else key_class_id), list_kind)),
         ("Command.value", value)])
     return o.getvalue()
 
 
-def party(owning_key: bytes, name: str = "O=Notary Service,L=Zurich,C=CH",
-          key_class_id=DEFAULT_IDS["eddsa_public_key"]) -> bytes:
+def party(owning_key: bytes, name: str = "O=Notary Service,L=Zurich,C=CH", key_class_id=None) -> bytes:
     """Party(name, owningKey).serialize().bytes (Party.kt:29, AbstractParty.kt:13): fields sort as
     AbstractParty.owningKey, Party.name; the name is a CordaX500Name with its string fields."""
     g = Graph()
@@ -772,32 +961,36 @@ def party(owning_key: bytes, name: str = "O=Notary Service,L=Zurich,C=CH",
             ("CordaX500Name.organisationUnit", s(parts.get("OU"))), ("CordaX500Name.state", s(parts.get("ST")))])
 
     g.compatible(o, PARTY, [
-        ("AbstractParty.owningKey", lambda c: _key_object(g, c, owning_key, key_class_id)),
+        ("AbstractParty.owningKey", lambda c: _key_object(
+            g, c, owning_key, DEFAULT_REGISTRY.key_class_for(owning_key) if key_class_id is None else key_class_id)),
         ("Party.name", name_field)])
     return o.getvalue()
 
 
 def _read_key_object(r: Reader) -> bytes:
-    kid = r.read_class()
-    if not isinstance(kid, int) or kid < FIRST_UNPINNED_ID:
-        raise KryoUnsupported("key class is not a registered PublicKey class")
+    if not _key_class_ok(r.reg, r.read_class()):
+        raise KryoUnsupported("key class is not registered with PublicKeySerializer")
     r.not_null()
     return r.take(r.varint())
 
 
-def command_signers(buf: bytes) -> List[bytes]:
-    """Command.signers of a command component (the value is not read)."""
-    r = _header(buf)
+def command_signers(buf: bytes, reg: Registry = DEFAULT_REGISTRY) -> List[bytes]:
+    """Command.signers of a command component (the value is not read).  An empty list is what Command.init
+    rejects (require(signers.isNotEmpty()), Structures.kt:183): the JVM path decides that transaction."""
+    r = _header(buf, reg)
     if r.read_class() != COMMAND:
         raise KryoUnsupported("not a Command")
     r.not_null()
     _expect_fields(r, COMMAND, COMMAND_FIELDS)
-    return _read_list(r.chunk(), True, _read_key_object)
+    out = _read_list(r.chunk(), True, _read_key_object)
+    if not out:
+        raise KryoUnsupported("Command with no signers")
+    return out
 
 
-def party_owning_key(buf: bytes) -> bytes:
+def party_owning_key(buf: bytes, reg: Registry = DEFAULT_REGISTRY) -> bytes:
     """AbstractParty.owningKey of a notary component."""
-    r = _header(buf)
+    r = _header(buf, reg)
     if r.read_class() != PARTY:
         raise KryoUnsupported("not a Party")
     r.not_null()
@@ -805,26 +998,68 @@ def party_owning_key(buf: bytes) -> bytes:
     return _read_key_object(r.chunk())
 
 
-def required_signing_keys(groups: Sequence[Tuple[int, Sequence[bytes]]]) -> List[bytes]:
-    """WireTransaction.requiredSigningKeys (WireTransaction.kt:66-75) — the device additionally hands a
-    transaction with more than 64 signer entries to the JVM path: commands.flatMap { signers }
-    .toSet() + notary.owningKey when the transaction has inputs or a time-window, in first-appearance
-    order (the order of the device's required-key ranges).  Keys compare by their encoding."""
+def required_signing_keys(groups: Sequence[Tuple[int, Sequence[bytes]]], reg: Registry = DEFAULT_REGISTRY) -> List[bytes]:
+    """WireTransaction.requiredSigningKeys (WireTransaction.kt:66-75): commands.flatMap { signers }.toSet()
+    + notary.owningKey when the transaction has inputs or a time-window, in first-appearance order (the
+    order of the device's required-key ranges).  Keys compare by their encoding."""
     out: List[bytes] = []
     seen = set()
+    for k in _signer_entries(groups, reg)[0]:
+        if k not in seen:
+            seen.add(k)
+            out.append(k)
+    return out
+
+
+def _signer_entries(groups, reg):
+    """(commands' signers then the notary when required, the notary key or None)."""
+    entries: List[bytes] = []
     present = {gi for gi, _ in groups}
     for gi, comps in groups:
         if gi == GROUP_COMMANDS:
             for c in comps:
-                for k in command_signers(c):
-                    if k not in seen:
-                        seen.add(k)
-                        out.append(k)
-    if GROUP_NOTARY in present and (GROUP_INPUTS in present or GROUP_TIMEWINDOW in present):
-        for gi, comps in groups:
-            if gi == GROUP_NOTARY:
-                k = party_owning_key(comps[0])
-                if k not in seen:
-                    seen.add(k)
-                    out.append(k)
-    return out
+                entries += command_signers(c, reg)
+    notary = None
+    for gi, comps in groups:
+        if gi == GROUP_NOTARY:
+            notary = party_owning_key(comps[0], reg)
+            break
+    if notary is not None and (GROUP_INPUTS in present or GROUP_TIMEWINDOW in present):
+        entries.append(notary)
+    return entries, notary
+
+
+def required_key_trees(groups, sig_keys, reg: Registry = DEFAULT_REGISTRY):
+    """requiredSigningKeys as the device derives them (CHIP_STX_REQUIRED): per distinct key its tree of
+    post-order nodes (keys.Node: a plain key is one leaf, a CompositeKey its canonical tree).  Raises
+    KryoUnsupported for what the device hands to the JVM path: a command / notary component outside the
+    grammar, an empty signers list, more than 64 signer entries, a key that is neither a decodable
+    Ed25519 / ECDSA key nor a canonical CompositeKey (keys.py).  A plain key that signs none of this
+    transaction's signatures (`sig_keys`: its signatures' key bytes) is decoded here — the verify path
+    decodes the others — and so is the notary's key when the notary is not required."""
+    from corda_amd import keys as KS
+
+    def tree_of(k: bytes):
+        if KS.is_composite(k):
+            return KS.composite_tree(k)
+        if KS.spki_scheme(k)[0]:
+            if k not in sig_keys and not KS.plain_key_ok(k):
+                raise KryoUnsupported("undecodable key")
+            return [(k, 0, 0, 1)]
+        raise KryoUnsupported("key type")
+
+    try:
+        entries, notary = _signer_entries(groups, reg)
+        if len(entries) > MAX_SIGNER_ENTRIES:
+            raise KryoUnsupported("more than %d signer entries" % MAX_SIGNER_ENTRIES)
+        if notary is not None:
+            tree_of(notary)                      # deserialised whether or not it must sign
+        trees, seen = [], set()
+        for k in entries:
+            t = tree_of(k)
+            if k not in seen:
+                seen.add(k)
+                trees.append(t)
+        return trees
+    except KS.KeyUnsupported as e:
+        raise KryoUnsupported(str(e))

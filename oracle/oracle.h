@@ -150,6 +150,25 @@ void orc_required_signers(uint64_t ntx, const uint64_t* sig_start, const uint64_
                           uint64_t key_bytes, const uint8_t* status, uint8_t* verdict, uint32_t* arg,
                           uint8_t* missing);
 
+/* ---- Kryo front end: SignedTransaction bytes (kryo_ref.c; chip_stx_parse_device's restatement) ---- */
+typedef struct {
+    int32_t arrays_aslist, signed_tx, wire_tx, serialized_bytes;   /* DefaultKryoCustomizer.kt:77-80 */
+    int32_t privacy_salt;                                            /* :116 */
+    uint32_t n_public_key;
+    int32_t public_key[8];        /* every id registered with PublicKeySerializer (:91-111) */
+} orc_kryo_registry;
+/* One blob -> a record: u8 parse status, u8 final status (CHIP_STX_*; with want_required the required
+ * stage may turn OK into UNSUPPORTED); when the parse status is OK: u32 ncomp + (u32 group, u32 internal,
+ * u32 len, bytes) each, 32-byte salt, u32 nsig + (i32 platformVersion, i32 schemeNumberID, u32 len, sig,
+ * u32 len, key SPKI) each; when want_required and the final status is OK: u32 nreq + per required key
+ * u32 nnodes + (u32 nkids, u32 weight, u32 threshold, u32 leaf length, leaf SPKI) per post-order node.
+ * Returns the record length, (size_t)-1 when cap is too small. */
+size_t orc_stx_parse(const uint8_t* blob, size_t len, const orc_kryo_registry* reg, int want_required,
+                     uint8_t* out, size_t cap);
+int orc_stx_parse_batch(uint64_t n, const uint8_t* data, const uint64_t* off, const uint32_t* len,
+                        const orc_kryo_registry* reg, int want_required, uint8_t* out, uint64_t cap,
+                        uint64_t* rec_off);
+
 #ifdef __cplusplus
 }
 #endif

@@ -208,3 +208,91 @@ def required_signers(q, b, status, tx_idx=None):
         _p(b.key_off), _p(b.key_len), ctypes.c_uint64(int(b.key_data.nbytes)),
         _p(np.ascontiguousarray(status, dtype=np.uint8)), _p(verdict), _p(arg), _p(missing))
     return verdict, arg, missing[:nreq]
+
+
+# ---- Kryo front end (oracle/kryo_ref.c) ----
+class KryoRegistry(ctypes.Structure):
+    _fields_ = [("arrays_aslist", ctypes.c_int32), ("signed_tx", ctypes.c_int32), ("wire_tx", ctypes.c_int32),
+                ("serialized_bytes", ctypes.c_int32), ("privacy_salt", ctypes.c_int32),
+                ("n_public_key", ctypes.c_uint32), ("public_key", ctypes.c_int32 * 8)]
+
+
+def kryo_registry(reg) -> KryoRegistry:
+    """orc_kryo_registry of a corda_amd.kryo.Registry."""
+    r = KryoRegistry(reg.arrays_aslist, reg.signed_tx, reg.wire_tx, reg.serialized_bytes, reg.privacy_salt,
+                     len(reg.public_key))
+    for i, v in enumerate(reg.public_key):
+        r.public_key[i] = v
+    return r
+
+
+def _decode_stx_record(b: bytes, want_required: bool):
+    """One orc_stx_parse record -> (parse status, final status, groups, salt, sigs, trees) in the shapes of
+    corda_amd.kryo.stx_parse / required_key_trees (None where absent)."""
+    import struct
+    pst, fst = b[0], b[1]
+    if pst != 0:
+        return pst, fst, None, None, None, None
+    at = 2
+
+    def u32():
+        nonlocal at
+        v = struct.unpack_from("<I", b, at)[0]
+        at += 4
+        return v
+
+    def raw(n):
+        nonlocal at
+        v = bytes(b[at:at + n])
+        at += n
+        return v
+
+    groups = []
+    for _ in range(u32()):
+        g, i, n = u32(), u32(), u32()
+        c = raw(n)
+        if i == 0:
+            groups.append((g, [c]))
+        else:
+            groups[-1][1].append(c)
+    salt = raw(32)
+    sigs = []
+    for _ in range(u32()):
+        pv, sch = struct.unpack("<ii", raw(8))
+        s = raw(u32())
+        k = raw(u32())
+        sigs.append((s, k, pv, sch))
+    trees = None
+    if want_required and fst == 0:
+        trees = []
+        for _ in range(u32()):
+            nodes = []
+            for _ in range(u32()):
+                nk, w, thr, ln = u32(), u32(), u32(), u32()
+                nodes.append((raw(ln) if nk == 0 else None, thr, nk, w))
+            trees.append(nodes)
+    return pst, fst, groups, salt, sigs, trees
+
+
+def stx_parse(blobs, reg, want_required: bool = False):
+    """oracle/kryo_ref.c over a list of SignedTransaction blobs -> one decoded record per blob."""
+    data, off, ln = _pools(blobs)
+    r = kryo_registry(reg)
+    cap = 4 * int(data.nbytes) + 4096 * len(blobs) + 4096
+    out = np.zeros(cap, dtype=np.uint8)
+    rec_off = np.zeros(len(blobs) + 1, dtype=np.uint64)
+    rc = lib().orc_stx_parse_batch(ctypes.c_uint64(len(blobs)), _p(data), _p(off), _p(ln), ctypes.byref(r),
+                                   int(want_required), _p(out), ctypes.c_uint64(cap), _p(rec_off))
+    if rc != 0:
+        raise RuntimeError("orc_stx_parse_batch: output too small")
+    return [_decode_stx_record(out[int(rec_off[t]):int(rec_off[t + 1])].tobytes(), want_required)
+            for t in range(len(blobs))]
+
+
+def _pools(blobs):
+    ln = np.array([len(b) for b in blobs], dtype=np.uint32)
+    off = np.zeros(len(blobs), dtype=np.uint64)
+    if len(blobs) > 1:
+        off[1:] = np.cumsum(ln[:-1].astype(np.uint64))
+    data = np.frombuffer(b"".join(bytes(b) for b in blobs) or b"\0", dtype=np.uint8).copy()
+    return data, off, ln

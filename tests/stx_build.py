@@ -1,30 +1,74 @@
-"""SignedTransaction blobs for the Kryo front-end tests (chip_stx_parse_device vs corda_amd/kryo.py).
+"""SignedTransaction blobs for the Kryo front-end tests (chip_stx_parse_device vs oracle/kryo_ref.c and the
+host mirror corda_amd/kryo.py).
 
 Every case is built with the kryo.py writer (the Kryo 4.0.0 restatement, parity unpinned) and labelled
 with the status the host mirror kryo.stx_parse gives; the cases cover each status class the device
 reports: valid transactions of random shapes (chunk-spanning components, unknown group ordinals 20 /
-63, every list class, several key classes and metadata values), truncations and header damage
-(KryoException), empty signature lists, each WireTransaction.init invariant, and well-formed bytes
-outside the device grammar (class names for keys, object back-references, group index 64, > 64 inputs,
-renamed fields)."""
+63, every list class, every PublicKeySerializer class id, several metadata values), truncations and
+header damage (KryoException), empty signature lists, each WireTransaction deserialisation invariant
+(incl. two notaries / two time-windows), and well-formed bytes outside the device grammar (a class id
+other than the registry's in the PrivacySalt and key slots, class names for keys, object
+back-references, group index 64, > 64 inputs, inputs that are not canonical StateRefs, renamed
+fields).  Keys are real Ed25519 / ECDSA keys; inputs are canonical StateRef encodings."""
 import numpy as np
 
+import cordagen as G
+from corda_amd import composite as CK
+from corda_amd import keys as KS
 from corda_amd import kryo as K
 
 ED_KEY = 44
-EC_KEYS = (91, 88)
 METAS = [(1, 4), (1, 3), (1, 2), (2, 4)]
+REG = K.DEFAULT_REGISTRY
 
 
-def _key(rng, n):
-    return bytes([0x30]) + rng.bytes(n - 1)
+def ed_key(rng) -> bytes:
+    return G.spki_ed25519(G.ed25519_pub(rng.bytes(32)))
 
 
-def random_valid(rng, key_pool):
-    """(groups, salt, sigs, list kinds) of one structurally valid transaction."""
+def ec_key(rng, scheme: int = 3, compressed: bool = False) -> bytes:
+    pub = G.ec_pub(scheme, (b"\x01" + rng.bytes(31)))
+    if not compressed:
+        return G.spki_ec(scheme, pub)
+    pre = KS.SPKI_R1_C if scheme == 3 else KS.SPKI_K1_C
+    return pre + bytes([2 | (pub[64] & 1)]) + pub[1:33]
+
+
+def bad_ed_key(rng) -> bytes:
+    """An Ed25519 SPKI whose A does not decode (i2p: no square root)."""
+    while True:
+        a = bytearray(rng.bytes(32))
+        a[31] &= 0x7F
+        if not KS.ed25519_point_ok(bytes(a)):
+            return KS.SPKI_ED25519 + bytes(a)
+
+
+def bad_ec_key(rng) -> bytes:
+    k = bytearray(ec_key(rng))
+    k[-1] ^= 1                                   # y + 1: off the curve
+    return bytes(k)
+
+
+def key_pool(rng):
+    return [ed_key(rng) for _ in range(10)] + [ec_key(rng, 3), ec_key(rng, 3), ec_key(rng, 2)]
+
+
+def stateref(rng) -> bytes:
+    return K.state_ref(rng.bytes(32), int(rng.integers(0, 5)))
+
+
+def key_class(rng, key: bytes) -> int:
+    """The class id a JVM writes for this key, or (1 in 4) another PublicKeySerializer class."""
+    if rng.random() < 0.25:
+        return int(rng.choice(REG.public_key))
+    return REG.key_class_for(key)
+
+
+def random_valid(rng, keys):
+    """(groups, salt, sigs, list kinds, sig list kind) of one structurally valid transaction."""
     groups = []
     if rng.random() < 0.8:
-        groups.append((0, [rng.bytes(int(rng.integers(36, 120))) for _ in range(int(rng.integers(1, 4)))]))
+        groups.append((0, [stateref(rng) for _ in range(int(rng.integers(1, 4)))]))
     if rng.random() < 0.8 or not groups:
         groups.append((1, [rng.bytes(int(rng.integers(0, 1600))) for _ in range(int(rng.integers(1, 4)))]))
     groups.append((2, [rng.bytes(int(rng.integers(20, 300))) for _ in range(int(rng.integers(1, 3)))]))
@@ -42,13 +86,12 @@ def random_valid(rng, key_pool):
     groups = [groups[i] for i in order]
     sigs = []
     for _ in range(int(rng.integers(1, 5))):
-        key = key_pool[int(rng.integers(0, len(key_pool)))]
+        key = keys[int(rng.integers(0, len(keys)))]
         sl = 64 if len(key) == ED_KEY else int(rng.integers(70, 73))
         pv, sch = METAS[int(rng.integers(0, len(METAS)))]
-        sigs.append(K.Sig(rng.bytes(sl), key, pv, sch, int(rng.integers(14, 60))))
+        sigs.append(K.Sig(rng.bytes(sl), key, pv, sch, key_class(rng, key)))
     kinds = {}
-    r = rng.random()
-    if r < 0.2:
+    if rng.random() < 0.2:
         kinds[-1] = ("aslist", K.COMPONENT_GROUP)
     for gi, comps in groups:
         if rng.random() < 0.2:
@@ -62,8 +105,9 @@ def random_valid(rng, key_pool):
     return groups, rng.bytes(32), sigs, kinds, skind
 
 
-def blob(groups, salt, sigs, kinds=None, skind="auto"):
-    return K.signed_transaction(K.wire_transaction(groups, salt, K.DEFAULT_IDS["privacy_salt"], kinds), sigs, skind)
+def blob(groups, salt, sigs, kinds=None, skind="auto", salt_id=None):
+    return K.signed_transaction(K.wire_transaction(groups, salt, REG.privacy_salt if salt_id is None else salt_id,
+                                                   kinds), sigs, skind)
 
 
 def _replace_once(b: bytes, old: bytes, new: bytes) -> bytes:
@@ -71,12 +115,22 @@ def _replace_once(b: bytes, old: bytes, new: bytes) -> bytes:
     return b[:i] + new + b[i + len(old):]
 
 
+def overlong_stateref(rng) -> bytes:
+    """A StateRef whose index varint is overlong (0x81 0x00 = 1 written in 2 bytes): Kryo reads it, but it
+    is not the encoding a JVM writes, so byte equality would no longer be StateRef equality."""
+    h = rng.bytes(32)
+    good = K.state_ref(h, 1)
+    i = good.index(b"\x01\x02\x00", 40)          # the index field: chunk(1) = zz(1) = 2, end marker
+    return good[:i] + b"\x02\x82\x00\x00" + good[i + 3:]
+
+
 def cases(seed: int = 7, n_valid: int = 200):
-    """-> list of blobs (bytes); labels come from K.stx_parse."""
+    """-> list of blobs (bytes); labels come from K.stx_parse.  Layout of the list: n_valid OK, 12 KRYO,
+    1 NO_SIGS, 9 INVARIANT, then UNSUPPORTED cases."""
     rng = np.random.default_rng(seed)
-    key_pool = [_key(rng, ED_KEY) for _ in range(12)] + [_key(rng, n) for n in EC_KEYS for _ in range(3)]
+    keys = key_pool(rng)
     out = []
-    valid = [random_valid(rng, key_pool) for _ in range(n_valid)]
+    valid = [random_valid(rng, keys) for _ in range(n_valid)]
     out += [blob(*v) for v in valid]
     g0, s0, sg0, _, _ = valid[0]
     ok = blob(g0, s0, sg0)
@@ -90,20 +144,23 @@ def cases(seed: int = 7, n_valid: int = 200):
     out.append(K.signed_transaction(w[:-1], sg0))
     # SignedTransaction.init: no signatures
     out.append(K.signed_transaction(w, [], "array"))
-    # WireTransaction.init invariants
+    # WireTransaction deserialisation invariants
     c = lambda n=40: rng.bytes(n)
+    sr = stateref(rng)
     inv = [
         [(1, [c()]), (2, []), (4, [c()])],                                   # empty group
         [(1, [c()]), (2, [c()]), (1, [c()])],                                # duplicated group
-        [(0, [c()]), (1, [c()]), (2, [c()])],                                # inputs without notary
+        [(0, [stateref(rng)]), (1, [c()]), (2, [c()])],                      # inputs without notary
         [(2, [c()]), (4, [c()])],                                            # no input or output
         [(1, [c()]), (4, [c()])],                                            # no command
         [(1, [c()]), (2, [c()]), (5, [c()])],                                # time-window without notary
-        [(0, [b"x" * 36, b"y" * 36, b"x" * 36]), (1, [c()]), (2, [c()]), (4, [c()])],   # duplicate inputs
+        [(0, [sr, stateref(rng), sr]), (1, [c()]), (2, [c()]), (4, [c()])],  # duplicate inputs
+        [(1, [c()]), (2, [c()]), (4, [c(), c()])],                           # two notaries
+        [(1, [c()]), (2, [c()]), (4, [c()]), (5, [c(), c()])],               # two time-windows
     ]
     out += [blob(g, c(32), sg0) for g in inv]
     # outside the device grammar (UNSUPPORTED: the JVM path decides)
-    out.append(blob([(0, [c(36 + i % 3) for i in range(65)]), (2, [c()]), (4, [c()])], c(32), sg0))   # > 64 inputs
+    out.append(blob([(0, [stateref(rng) for i in range(65)]), (2, [c()]), (4, [c()])], c(32), sg0))   # > 64 inputs
     out.append(blob([(1, [c()]), (2, [c()]), (64, [c()])], c(32), sg0))                                # group 64
     out.append(blob(g0, s0, [K.Sig(sg0[0].sig, sg0[0].key, 1, 4, "net.i2p.crypto.eddsa.EdDSAPublicKey")]))  # by name
     out.append(_replace_once(ok, b"\x0f\x01", b"\x0f\x02"))                 # txBits as a back-reference
@@ -111,19 +168,55 @@ def cases(seed: int = 7, n_valid: int = 200):
     out.append(ok.replace(b"java.util.ArrayLis\xf4", b"java.util.LinkedLis\xf4", 1)
                if b"java.util.ArrayLis\xf4" in ok else ok.replace(b"java.util.Collections$SingletonLis\xf4",
                                                                      b"java.util.Collections$SingletonSe\xf4", 1))
+    # a registered class other than the registry's: PrivacySalt slot, key slots
+    ids = K.registration_ids()
+    for sid in (REG.eddsa_public_key, 14, ids["java.util.BitSet"]):
+        out.append(blob(g0, s0, sg0, salt_id=sid))
+    for kid in (REG.privacy_salt, ids["net.i2p.crypto.eddsa.EdDSAPrivateKey"], 14, ids["java.lang.Class"]):
+        out.append(blob(g0, s0, [K.Sig(sg0[0].sig, sg0[0].key, 1, 4, kid)]))
+    # inputs that are not canonical StateRefs
+    out.append(blob([(0, [overlong_stateref(rng)]), (1, [c()]), (2, [c()]), (4, [c()])], c(32), sg0))
+    out.append(blob([(0, [c(36)]), (1, [c()]), (2, [c()]), (4, [c()])], c(32), sg0))
     return out
+
+
+N_KRYO, N_NO_SIGS, N_INVARIANT = 12, 1, 9
+
+
+# ---- requiredSigningKeys cases ----
+def composite(children, threshold) -> bytes:
+    """A canonical CompositeKey SPKI (composite.py re-encodes sorted, minimal DER)."""
+    b = CK.CompositeKey.Builder()
+    for k, w in children:
+        b.add_key(CK.as_key(k), w)
+    return b.build(threshold).encoded
+
+
+def composite_raw(children, threshold) -> bytes:
+    """A CompositeKey SPKI with the children in the given order (not re-sorted)."""
+    kids = b"".join(CK._tlv(0x30, CK._tlv(0x03, b"\x00" + k) + CK._der_int(w)) for k, w in children)
+    body = CK._der_int(threshold) + CK._tlv(0x30, kids)
+    return CK._tlv(0x30, CK._tlv(0x30, CK._COMPOSITE_OID_TLV) + CK._tlv(0x03, b"\x00" + CK._tlv(0x30, body)))
 
 
 def cases_required(seed: int = 13, n: int = 240):
     """SignedTransactions whose command / notary components are real Kryo Command / Party objects:
     requiredSigningKeys = commands' signers (several commands, repeated and non-signing keys, every list
-    class) + the notary when there are inputs or a time-window; plus a CompositeKey signer, a malformed
-    command and a command of another class (-> UNSUPPORTED)."""
-    from corda_amd import composite as CK
+    class, ECDSA keys incl. a compressed encoding) + the notary when there are inputs or a time-window;
+    CompositeKey signers (flat, weighted, nested) decoded on the device; and what goes to the JVM path:
+    a non-canonical / invalid composite, an undecodable key that signs nothing (also as the notary of a
+    transaction that does not need it), an empty signers list, a damaged command, > 64 signer entries."""
     rng = np.random.default_rng(seed)
-    pool = [_key(rng, ED_KEY) for _ in range(10)] + [_key(rng, 91), _key(rng, 88)]
-    comp = CK.CompositeKey.Builder().add_keys(pool[0], pool[1]).build(1).encoded \
-        if hasattr(CK.CompositeKey, "Builder") else None
+    pool = [ed_key(rng) for _ in range(10)] + [ec_key(rng, 3), ec_key(rng, 2), ec_key(rng, 3, compressed=True)]
+    comps = [composite([(pool[0], 1), (pool[1], 1)], 1),
+             composite([(pool[2], 1), (pool[3], 1)], 2),
+             composite([(pool[4], 2), (pool[5], 1), (pool[10], 1)], 3),
+             composite([(composite([(pool[6], 1), (pool[7], 1)], 2), 1), (pool[8], 1)], 1)]
+    bad_comps = [composite_raw(sorted([(pool[1], 1), (pool[0], 1)], key=lambda kw: kw[0], reverse=True), 1),
+                 composite_raw([(pool[0], 1), (pool[1], 1)], 3),                       # threshold > total
+                 composite_raw([(pool[0], 1)], 1),                                     # one child
+                 composite_raw([(bad_ed_key(rng), 1), (pool[1], 1)], 1),               # undecodable leaf
+                 composite_raw([(ec_key(rng, 3, compressed=True), 1), (pool[1], 1)], 1)]   # non-canonical leaf
     out = []
     for i in range(n):
         signers_of_cmds = [[pool[int(rng.integers(0, len(pool)))] for _ in range(int(rng.integers(1, 4)))]
@@ -133,37 +226,46 @@ def cases_required(seed: int = 13, n: int = 240):
         groups = []
         has_in = rng.random() < 0.6
         if has_in:
-            groups.append((0, [rng.bytes(40) + bytes([j]) for j in range(int(rng.integers(1, 3)))]))
+            groups.append((0, [stateref(rng) for _ in range(int(rng.integers(1, 3)))]))
         groups.append((1, [rng.bytes(int(rng.integers(20, 900)))]))
+        if kind < 0.10:
+            signers_of_cmds[0].append(comps[int(rng.integers(0, len(comps)))])
+        elif kind < 0.13:
+            signers_of_cmds[0].append(bad_comps[int(rng.integers(0, len(bad_comps)))])
+        elif kind < 0.15:
+            signers_of_cmds[0].append(bad_ed_key(rng) if rng.random() < 0.5 else bad_ec_key(rng))
         cmds = []
         for ss in signers_of_cmds:
-            lk = "auto" if len(ss) == 1 else ("aslist", 31) if rng.random() < 0.3 else "array"
-            cmds.append(K.command(ss, list_kind=lk if lk[0] != "aslist" else ("aslist", K.DEFAULT_IDS["eddsa_public_key"])))
-        if kind < 0.03 and comp is not None:
-            cmds.append(K.command([comp]))                                 # CompositeKey signer
-        elif kind < 0.06:
+            lk = "auto" if len(ss) == 1 else ("aslist", REG.eddsa_public_key) if rng.random() < 0.3 else "array"
+            cmds.append(K.command(ss, list_kind=lk))
+        if 0.15 <= kind < 0.17:
             cmds.append(K.command(signers_of_cmds[0])[:40])                 # truncated inside the signers
-        elif kind < 0.08:
+        elif 0.17 <= kind < 0.19:
             cmds[0] = cmds[0].replace(b"net.corda.core.contracts.Comman\xe4", b"net.corda.core.contracts.Commanx\xe4", 1)
+        elif 0.19 <= kind < 0.21:
+            cmds.append(K.command([], list_kind="array"))                  # Command.init: no signers
         groups.append((2, cmds))
         if has_in or rng.random() < 0.5:
-            groups.append((4, [K.party(notary_key)]))
+            nk = bad_ed_key(rng) if (0.21 <= kind < 0.23 and not has_in) else notary_key
+            groups.append((4, [K.party(nk)]))
             if rng.random() < 0.3:
                 groups.append((5, [rng.bytes(40)]))
         if i % 97 == 5:                                                     # > 64 signer entries
             cmds.append(K.command([pool[j % len(pool)] for j in range(70)], list_kind="array"))
-        req_all = [k for ss in signers_of_cmds for k in ss] + [notary_key]
+        req_all = [k for ss in signers_of_cmds for k in ss if not KS.is_composite(k)] + [notary_key]
         sig_keys = [req_all[int(rng.integers(0, len(req_all)))] for _ in range(int(rng.integers(1, 4)))]
-        sigs = [K.Sig(rng.bytes(64) if len(k) == ED_KEY else rng.bytes(71), k, 1, 4, 31) for k in sig_keys]
+        if kind < 0.10:                                                     # sign for a composite leaf
+            sig_keys.append(pool[int(rng.choice([0, 2, 3, 4, 6, 7, 8]))])
+        sigs = [K.Sig(rng.bytes(64) if len(k) == ED_KEY else rng.bytes(71), k, 1, 4) for k in sig_keys]
         out.append(blob(groups, rng.bytes(32), sigs))
     return out
 
 
 def expected_required(blobs):
-    """Host mirror of chip_stx_parse_device(..., CHIP_STX_REQUIRED): per blob (status, [required key
-    bytes]) and the signer key numbering (first occurrence over the signatures of the transactions the
-    parse passes accepted, before the required-key stage)."""
-    from corda_amd import composite as CK
+    """Host mirror of chip_stx_parse_device(..., CHIP_STX_REQUIRED): per blob (status, [required key trees
+    as (leaf key bytes or None, threshold, nkids, weight) nodes]) and the signer key numbering (first
+    occurrence over the signatures of the transactions the parse passes accepted, before the required-key
+    stage)."""
     parsed = [K.stx_parse(b) for b in blobs]
     kid = {}
     for st, g, salt, sigs in parsed:
@@ -176,18 +278,44 @@ def expected_required(blobs):
             out.append((st, None))
             continue
         try:
-            req = K.required_signing_keys(g)
-            present = {gi for gi, _ in g}
-            entries = sum(len(K.command_signers(c)) for gi, cs in g if gi == K.GROUP_COMMANDS for c in cs) + \
-                (1 if K.GROUP_NOTARY in present and (K.GROUP_INPUTS in present or K.GROUP_TIMEWINDOW in present) else 0)
+            trees = K.required_key_trees(g, {key for _, key, _, _ in sigs})
         except K.KryoException:
             out.append((K.STX_UNSUPPORTED, None))
             continue
-        if entries > 64:                         # the device's duplicate check covers <= 64 signer entries
-            out.append((K.STX_UNSUPPORTED, None))
-            continue
-        if any(k not in kid and CK._spki_oid(k) == CK._COMPOSITE_OID_TLV for k in req):
-            out.append((K.STX_UNSUPPORTED, None))
-            continue
-        out.append((K.STX_OK, req))
+        out.append((K.STX_OK, trees))
     return out, kid
+
+
+def flat_nodes(trees, kid):
+    """[(val, nkids, weight)] of a transaction's required keys in the chip_req_batch node layout."""
+    nodes = []
+    for tree in trees:
+        for leaf, thr, nk, w in tree:
+            nodes.append((kid.get(leaf, G.REQ_NO_SIGNER) if nk == 0 else thr, nk, w))
+    return nodes
+
+
+def mutants(blobs, seed: int = 99, n: int = 2000):
+    """Random damage to valid blobs (bit flips, byte changes, deletions, insertions, truncations): every
+    status class and the grammar's edges, for the oracle == mirror == device comparisons."""
+    rng = np.random.default_rng(seed)
+    out = []
+    for _ in range(n):
+        b = bytearray(blobs[int(rng.integers(0, len(blobs)))])
+        for _ in range(int(rng.integers(1, 4))):
+            kind = rng.random()
+            i = int(rng.integers(0, len(b)))
+            if kind < 0.4:
+                b[i] ^= 1 << int(rng.integers(0, 8))
+            elif kind < 0.6:
+                b[i] = int(rng.integers(0, 256))
+            elif kind < 0.75:
+                del b[i]
+            elif kind < 0.9:
+                b.insert(i, int(rng.integers(0, 256)))
+            else:
+                b = b[:i]
+            if not b:
+                break
+        out.append(bytes(b))
+    return out

@@ -15,7 +15,7 @@ from corda_amd import kryo as K
 
 def test_round_trip_of_random_transactions():
     rng = np.random.default_rng(11)
-    pool = [S._key(rng, S.ED_KEY) for _ in range(5)] + [S._key(rng, 91)]
+    pool = S.key_pool(rng)
     for _ in range(150):
         groups, salt, sigs, kinds, skind = S.random_valid(rng, pool)
         b = S.blob(groups, salt, sigs, kinds, skind)
@@ -31,10 +31,60 @@ def test_status_classes():
     st = [K.stx_parse(b)[0] for b in blobs]
     assert st[:20] == [K.STX_OK] * 20
     tail = st[20:]
-    assert tail[:12] == [K.STX_KRYO] * 12                 # truncations, damaged headers, truncated txBits
-    assert tail[12] == K.STX_NO_SIGS
-    assert tail[13:20] == [K.STX_INVARIANT] * 7           # each WireTransaction.init check
-    assert tail[20:] == [K.STX_UNSUPPORTED] * 6           # outside the device grammar
+    k, i = S.N_KRYO, S.N_KRYO + S.N_NO_SIGS
+    assert tail[:k] == [K.STX_KRYO] * k                   # truncations, damaged headers, truncated txBits
+    assert tail[k:i] == [K.STX_NO_SIGS]
+    assert tail[i:i + S.N_INVARIANT] == [K.STX_INVARIANT] * S.N_INVARIANT   # each deserialisation check
+    assert tail[i + S.N_INVARIANT:] == [K.STX_UNSUPPORTED] * (len(tail) - i - S.N_INVARIANT)
+    assert len(tail) - i - S.N_INVARIANT >= 15            # outside the grammar, incl. 7 rejected class ids
+
+
+def test_registry_restates_the_registration_order():
+    """DefaultKryoCustomizer.kt:77-80 pins 10-13; every later id is the position of a new class in the
+    registration order; PublicKeySerializer's classes are the key slots' accepted ids."""
+    ids = K.registration_ids()
+    reg = K.DEFAULT_REGISTRY
+    assert (reg.arrays_aslist, reg.signed_tx, reg.wire_tx, reg.serialized_bytes) == (10, 11, 12, 13)
+    assert sorted(ids.values()) == list(range(10, 10 + len(ids)))
+    assert reg.public_key == [ids[c] for c in K.PUBLIC_KEY_CLASSES]
+    assert ids["net.i2p.crypto.eddsa.EdDSAPublicKey"] == ids["sun.security.ec.ECPublicKeyImpl"] + 1
+    assert reg.privacy_salt == ids["net.corda.core.contracts.PrivacySalt"] > max(reg.public_key)
+    # a re-registered class keeps its id (Kryo.register on a known class replaces the serializer only)
+    again = K.registration_ids(K.REGISTRATION_ORDER + [("java.util.BitSet", "")])
+    assert again == ids
+    # a deployment's own ids (e.g. one more Guava class) shift every later id; the Registry follows
+    shifted = K.Registry(K.registration_ids(K.REGISTRATION_ORDER[:20] + [("x.Extra", "")] + K.REGISTRATION_ORDER[20:]))
+    assert shifted.privacy_salt == reg.privacy_salt + 1 and shifted.public_key == [k + 1 for k in reg.public_key]
+
+
+def test_rejected_class_ids_fail_closed():
+    """A class id other than the registry's in the PrivacySalt slot or a key slot: a different serializer
+    on the JVM, so the front end hands the transaction to the JVM path."""
+    rng = np.random.default_rng(3)
+    keys = S.key_pool(rng)
+    groups, salt, sigs, _, _ = S.random_valid(rng, keys)
+    assert K.stx_parse(S.blob(groups, salt, sigs))[0] == K.STX_OK
+    ids = K.registration_ids()
+    for sid in (K.DEFAULT_REGISTRY.eddsa_public_key, 14, ids["java.util.BitSet"], K.DEFAULT_REGISTRY.privacy_salt + 1):
+        assert K.stx_parse(S.blob(groups, salt, sigs, salt_id=sid))[0] == K.STX_UNSUPPORTED
+    for kid in K.DEFAULT_REGISTRY.public_key:
+        assert K.stx_parse(S.blob(groups, salt, [K.Sig(sigs[0].sig, sigs[0].key, 1, 4, kid)]))[0] == K.STX_OK
+    for kid in (K.DEFAULT_REGISTRY.privacy_salt, ids["net.i2p.crypto.eddsa.EdDSAPrivateKey"], 13, 14):
+        assert K.stx_parse(S.blob(groups, salt, [K.Sig(sigs[0].sig, sigs[0].key, 1, 4, kid)]))[0] == K.STX_UNSUPPORTED
+    other = K.Registry(K.registration_ids(K.REGISTRATION_ORDER[:20] + [("x.Extra", "")] + K.REGISTRATION_ORDER[20:]))
+    assert K.stx_parse(S.blob(groups, salt, sigs), other)[0] == K.STX_UNSUPPORTED
+
+
+def test_state_ref_inputs_are_canonical():
+    rng = np.random.default_rng(5)
+    for idx in (0, 1, 63, 64, 8191, 2**31 - 1, -1, -2**31):
+        h = rng.bytes(32)
+        b = K.state_ref(h, idx)
+        assert K.state_ref_of(b) == (h, idx)
+    assert K.state_ref_of(S.overlong_stateref(rng)) is None
+    good = K.state_ref(rng.bytes(32), 2)
+    assert K.state_ref_of(good + b"\0") is None and K.state_ref_of(good[:-1]) is None
+    assert K.state_ref_of(rng.bytes(176)) is None
 
 
 @pytest.mark.parametrize("groups,msg", [
@@ -46,6 +96,9 @@ def test_status_classes():
     ([(1, [b"o"]), (4, [b"n"])], "A transaction must contain at least one command"),
     ([(1, [b"o"]), (2, [b"c"]), (5, [b"t"])], "Transactions with time-windows must be notarised"),
     ([(0, [b"a"]), (1, [b"o"]), (2, [b"c"]), (4, [b"n"]), (5, [b"t"])], None),
+    ([(1, [b"o"]), (2, [b"c"]), (4, [b"n", b"m"])], "Invalid Transaction. More than 1 notary party detected."),
+    ([(1, [b"o"]), (2, [b"c"]), (4, [b"n"]), (5, [b"t", b"u"])], "Invalid Transaction. More than 1 time-window detected."),
+    ([(1, [b"o"]), (2, []), (4, [b"n", b"m"])], "Invalid Transaction. More than 1 notary party detected."),
 ])
 def test_wire_transaction_invariants(groups, msg):
     assert K.wire_invariant_error(groups) == msg
@@ -71,14 +124,15 @@ def test_chunk_placement():
 
 
 def test_uniform_filler_equals_writer():
-    tb, tm, sb, ids, _ = G.cfg4_workload(24, n_keys=8, seed=0x5EED0204, threads=4)
+    tb, tm, sb, ids, _v, _a = G.cfg4_workload_commands(24, n_keys=8, seed=0x5EED0204, threads=4)
     data, off, ln = G.stx_uniform(tb, sb, 2)
     for t in range(24):
         b = data[int(off[t]):int(off[t]) + int(ln[t])].tobytes()
         assert b == G.stx_signed_tx(tb, sb, t, range(2 * t, 2 * t + 2))
         st, groups, salt, sigs = K.stx_parse(b)
         assert st == K.STX_OK and salt == tb.salts[32 * t:32 * t + 32].tobytes()
-        assert [len(c) for _, cs in groups for c in cs] == [96, 96, 640, 640, 320, 96, 384, 96]
+        assert [len(c) for _, cs in groups for c in cs][:2] == [176, 176]
+        assert all(K.state_ref_of(c) for gi, cs in groups if gi == 0 for c in cs)
 
 
 def test_device_name_tables_match_the_restatement():

@@ -31,7 +31,7 @@ def test_oracle_under_asan_ubsan():
     env["CORDA_ORACLE_LIB"] = os.path.join(ROOT, "oracle", "_asan", "liboracle.so")
     env["LD_PRELOAD"] = libasan + ((":" + os.environ["LD_PRELOAD"]) if os.environ.get("LD_PRELOAD") else "")
     files = ["test_oracle_golden.py", "test_ref_x509_cpu.py", "test_ftx_cpu.py", "test_commit_log_cpu.py",
-             "test_uniq_sharded_cpu.py", "test_cfg1_cash_cpu.py"]
+             "test_uniq_sharded_cpu.py", "test_cfg1_cash_cpu.py", "test_kryo_oracle_cpu.py"]
     r = subprocess.run([sys.executable, "-m", "pytest", "-q", "-x", "-p", "no:cacheprovider", "-m", "not gpu"]
                        + [os.path.join(ROOT, "tests", f) for f in files],
                        cwd=ROOT, env=env, capture_output=True, text=True, timeout=900)

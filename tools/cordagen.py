@@ -902,9 +902,10 @@ def ed25519_spkis(n_keys: int, extra_key_seeds=()) -> list:
 
 def cfg4_workload_commands(ntx: int, n_keys: int = 4096, seed: int = 0x5EED0004, corrupt: float = 0.01,
                            p_missing: float = 0.01, threads: int = 8):
-    """cfg4 with real Kryo contents where requiredSigningKeys come from: the command component is
-    Command(Cash.Commands.Move, [signer]) and the notary component Party(notary name, notary key)
-    (corda_amd/kryo.py), so WireTransaction.requiredSigningKeys = {signer, notary}.  The owner of
+    """cfg4 with real Kryo contents where the front end reads them: the inputs are StateRef(random hash, 0 / 1)
+    (176 bytes each instead of the profile's 96), the command component is Command(Cash.Commands.Move,
+    [signer]) and the notary component Party(notary name, notary key) (corda_amd/kryo.py), so
+    WireTransaction.requiredSigningKeys = {signer, notary}.  The owner of
     each tx signs, and so does the notary; for p_missing of the transactions the command names another
     party as its signer, which does not sign (-> SignaturesMissingException, 1 needed key).
     -> (tb, tm, sb, ids, expected_verdict, expected_arg)."""
@@ -915,12 +916,18 @@ def cfg4_workload_commands(ntx: int, n_keys: int = 4096, seed: int = 0x5EED0004,
     miss = rng.random(ntx) < p_missing
     other = (owner + 1 + rng.integers(0, n_keys - 1, size=ntx)) % n_keys
     signer = np.where(miss, other, owner)
+    # inputs: canonical StateRef encodings (the front end accepts no other input bytes); index 0 and 1
+    sr0 = np.frombuffer(K.state_ref(bytes(32), 0), dtype=np.uint8)
+    sr1 = np.frombuffer(K.state_ref(bytes(32), 1), dtype=np.uint8)
+    hpos = np.nonzero(sr0 != np.frombuffer(K.state_ref(b"\xff" * 32, 0), dtype=np.uint8))[0]
+    assert len(hpos) == 32 and np.all(np.diff(hpos) == 1) and len(sr0) == len(sr1)
     cmd0 = np.frombuffer(K.command([bytes(44)]), dtype=np.uint8)
     cmd1 = np.frombuffer(K.command([b"\xff" * 44]), dtype=np.uint8)
     kpos = np.nonzero(cmd0 != cmd1)[0]
     assert len(kpos) == 44 and np.all(np.diff(kpos) == 1)
     party = np.frombuffer(K.party(spkis[n_keys]), dtype=np.uint8)
-    profile = [(g, [len(cmd0)] if g == 2 else [len(party)] if g == 4 else ss) for g, ss in CFG4_PROFILE]
+    profile = [(g, [len(cmd0)] if g == 2 else [len(party)] if g == 4 else [len(sr0)] * len(ss) if g == 0 else ss)
+               for g, ss in CFG4_PROFILE]
     tb = tx_batch(ntx, profile=profile, seed=seed)
     per = sum(len(ss) for _, ss in profile)
     sizes = [s for _, ss in profile for s in ss]
@@ -929,8 +936,14 @@ def cfg4_workload_commands(ntx: int, n_keys: int = 4096, seed: int = 0x5EED0004,
     view = tb.data[:ntx * per_bytes].reshape(ntx, per_bytes)
     at = 0
     kp = np.stack([np.frombuffer(k, dtype=np.uint8) for k in spkis])
+    hashes = PRNG(seed, b"inputs").np_bytes(ntx * 32 * 2).reshape(ntx, 2, 32)
+    nin = 0
     for g, sz in zip(groups, sizes):
-        if g == 2:
+        if g == 0:
+            view[:, at:at + sz] = sr0 if nin == 0 else sr1
+            view[:, at + hpos[0]:at + hpos[0] + 32] = hashes[:, nin % 2]
+            nin += 1
+        elif g == 2:
             view[:, at:at + sz] = cmd0
             view[:, at + kpos[0]:at + kpos[0] + 44] = kp[signer]
         elif g == 4:
