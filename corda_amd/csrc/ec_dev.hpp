@@ -711,13 +711,12 @@ template <int C> CHIP_DEV void jdbl(jpt& r, const jpt& p) {
         fp_sub<C>(r.Y, t, Cc);
     }
 }
-// the doubling reached from an addition's exceptional case (P == Q): kept out of line so the hot
-// addition code stays small
-// the rare P + P case of a mixed addition, out of line: inlining it into every mixed addition
-// measured slower (k_ecdsa_comb_q 2.80 -> 3.18 ms; more registers, larger code) although it removes
-// the kernels' private segment
-template <int C> __device__ __attribute__((noinline)) void jdbl_slow(jpt& r, const jpt& p) { jdbl<C>(r, p); }
-template <int C> CHIP_DEV void jmadd(jpt& r, const jpt& p, const apt& q) {
+// Mixed addition r = p + q (q affine) for the comb kernels.  The exceptional case P == Q (H = 0 and r = 0:
+// the running sum equals the table point, never for honest signatures, reachable by crafted ones) is not
+// computed here: `exc` is set and r is left unspecified; the kernel parks the lane for k_ecdsa_comb_retry.
+// Having no doubling call on this path keeps the accumulator in registers (an out-of-line call taking it by
+// reference had put it in scratch memory across every addition).
+template <int C> CHIP_DEV void jmadd_x(jpt& r, const jpt& p, const apt& q, bool& exc) {
     if (u256_is_zero(p.Z)) {
         r.X = q.x;
         r.Y = q.y;
@@ -733,7 +732,8 @@ template <int C> CHIP_DEV void jmadd(jpt& r, const jpt& p, const apt& q) {
     fp_sub<C>(rr, S2, p.Y);
     if (fp_is_zero<C>(H)) {
         if (fp_is_zero<C>(rr)) {
-            jdbl_slow<C>(r, p);
+            exc = true;
+            r = p;
         } else {
             u256_set_word(r.X, 0);
             u256_set_word(r.Y, 0);
@@ -761,5 +761,23 @@ template <int C> CHIP_DEV void jmadd(jpt& r, const jpt& p, const apt& q) {
     fp_sqr<C>(t, t);
     fp_sub<C>(t, t, Z1Z1);
     fp_sub<C>(o.Z, t, HH);
+    r = o;
+}
+// the complete mixed addition of the cold kernels (windowed verify, fixed-base table build, retries): the
+// P == Q case doubles, out of line so the common path stays small
+template <int C> __device__ __attribute__((noinline)) void jdbl_slow(jpt& r, const jpt& p) { jdbl<C>(r, p); }
+template <int C> CHIP_DEV void jmadd(jpt& r, const jpt& p, const apt& q) {
+    bool exc = false;
+    jpt o;
+    jmadd_x<C>(o, p, q, exc);
+    if (exc) jdbl_slow<C>(r, p);
+    else r = o;
+}
+// complete, with the doubling inline (a kernel that runs only for the rare exceptional lanes)
+template <int C> CHIP_DEV void jmadd_full(jpt& r, const jpt& p, const apt& q) {
+    bool exc = false;
+    jpt o;
+    jmadd_x<C>(o, p, q, exc);
+    if (exc) jdbl<C>(o, p);
     r = o;
 }

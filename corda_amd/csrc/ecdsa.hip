@@ -31,6 +31,17 @@
 
 #define EC_TAB_STRIDE EC_KEY_TABLE_WORDS
 
+// the signature-batch pointers a retry lane reads (kernel argument)
+struct chip_sig_batch_dev {
+    const uint32_t *key_idx, *msg_idx;
+    const uint8_t* sig_data;
+    const uint64_t* sig_off;
+    const uint32_t* sig_len;
+    const uint8_t* msg_data;
+    const uint64_t* msg_off;
+    const uint32_t* msg_len;
+};
+
 __device__ __constant__ const uint8_t SPKI_R1_PFX[26] = {0x30, 0x59, 0x30, 0x13, 0x06, 0x07, 0x2a, 0x86, 0x48,
                                                         0xce, 0x3d, 0x02, 0x01, 0x06, 0x08, 0x2a, 0x86, 0x48,
                                                         0xce, 0x3d, 0x03, 0x01, 0x07, 0x03, 0x42, 0x00};
@@ -351,6 +362,14 @@ CHIP_DEV void add_digit(jpt& acc, const apt& e, int d) {
     if (d < 0) fp_neg<C>(a.y, a.y);
     jmadd<C>(acc, acc, a);
 }
+// the comb kernels' digit addition: the exceptional case sets `exc` (jmadd_x)
+template <int C>
+CHIP_DEV void add_digit_x(jpt& acc, const apt& e, int d, bool& exc) {
+    if (d == 0) return;
+    apt a = e;
+    if (d < 0) fp_neg<C>(a.y, a.y);
+    jmadd_x<C>(acc, acc, a, exc);
+}
 
 template <int C>
 __global__ void __launch_bounds__(256) k_ecdsa_verify(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
@@ -431,6 +450,36 @@ __global__ void __launch_bounds__(256) k_ecdsa_verify(const uint32_t* __restrict
         }
     }
     status[i] = ecdsa_check<C>(acc, r) ? CHIP_VALID : CHIP_INVALID;
+}
+
+// ---- Crypto.decodePublicKey of an ECDSA r1 / k1 SPKI (BC decodePoint) for the Kryo front end: ok = the point
+// decodes; kind 1 also requires the uncompressed encoding BCECPublicKey re-encodes
+__global__ void __launch_bounds__(256) k_ecdsa_key_check(uint64_t n, const uint8_t* __restrict__ pool,
+                                                         const uint64_t* __restrict__ off,
+                                                         const uint32_t* __restrict__ len,
+                                                         const uint8_t* __restrict__ kind, uint8_t* __restrict__ ok) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint8_t* p = pool + off[i];
+    const uint32_t l = len[i];
+    int scheme = 0;
+    const uint8_t* pt = nullptr;
+    uint32_t ptlen = 0;
+    if (l == 91 && match_prefix(p, SPKI_R1_PFX, 26, 0x59, 0x42)) { scheme = CHIP_SCHEME_R1; pt = p + 26; ptlen = 65; }
+    else if (l == 59 && match_prefix(p, SPKI_R1_PFX, 26, 0x39, 0x22)) { scheme = CHIP_SCHEME_R1; pt = p + 26; ptlen = 33; }
+    else if (l == 88 && match_prefix(p, SPKI_K1_PFX, 23, 0x56, 0x42)) { scheme = CHIP_SCHEME_K1; pt = p + 23; ptlen = 65; }
+    else if (l == 56 && match_prefix(p, SPKI_K1_PFX, 23, 0x36, 0x22)) { scheme = CHIP_SCHEME_K1; pt = p + 23; ptlen = 33; }
+    if (!scheme) return;
+    apt q;
+    bool good = scheme == CHIP_SCHEME_R1 ? ec_decode_point<CURVE_R1>(q, pt, ptlen) : ec_decode_point<CURVE_K1>(q, pt, ptlen);
+    if (kind[i]) good = good && ptlen == 65;
+    ok[i] = good ? 1 : 0;
+}
+
+void launch_ecdsa_key_check(hipStream_t st, uint64_t n, const uint8_t* pool, const uint64_t* off, const uint32_t* len,
+                            const uint8_t* kind, uint8_t* ok) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_ecdsa_key_check, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, n, pool, off, len, kind, ok);
 }
 
 void launch_ecdsa_key_prep(hipStream_t st, uint64_t n_keys, const uint8_t* key_data, const uint64_t* key_off,
@@ -593,9 +642,10 @@ CHIP_DEV void ec_comb_fill(uint32_t* __restrict__ jac, uint32_t* __restrict__ ou
         jpt A;
         jpt_from_aff(A, a);
         jdbl<C>(A, A);
+        bool exc = false;   // j a + a with 2 <= j <= 7 is never P == Q (prime order n > 8)
 #pragma unroll 1
         for (int j = 2; j <= EC_COMB_QENT; j++) {
-            if (j > 2) jmadd<C>(A, A, a);
+            if (j > 2) jmadd_x<C>(A, A, a, exc);
             store_jpt(e + (uint32_t)(j - 1) * EC_COMB_JW, A);
             store_u256(o + (uint32_t)(j - 1) * 16, acc);
             fp_mul<C>(acc, acc, A.Z);
@@ -804,9 +854,9 @@ __global__ void __launch_bounds__(64) k_ecdsa_comb_inv(const uint32_t* __restric
 // C.  s^-1, u1, u2 and u1 G from the fixed comb.
 template <int C>
 CHIP_DEV void comb_g_body(uint32_t blk, const uint32_t* __restrict__ count, const uint32_t* __restrict__ gcomb,
-                          uint32_t* __restrict__ mid, const uint32_t* __restrict__ wp, uint64_t cap) {
+                          uint32_t* __restrict__ mid, const uint32_t* __restrict__ wp, uint64_t cap, uint32_t park_all) {
     const uint32_t gid = blk * blockDim.x + threadIdx.x;
-    if (gid >= *count || !mid[(uint64_t)40 * cap + gid]) return;
+    if (gid >= *count || mid[(uint64_t)40 * cap + gid] != 1u) return;
     u256 e, r, ep, es, winv, wm, u1, u2;
     mid_load(ep, mid, cap, gid, 8);
     mid_load(es, mid, cap, gid, 16);
@@ -822,6 +872,7 @@ CHIP_DEV void comb_g_body(uint32_t blk, const uint32_t* __restrict__ count, cons
     const uint32_t* G = gcomb + (EC_CURVE(C) == CURVE_R1 ? 0 : EC_GCOMB_WORDS);
     int carry = 0;
     apt ga;
+    bool exc = false;
 #pragma unroll
     for (int w = 0; w < EC_GWIN; w++) {
         const int b = w * EC_GW;   // bits [b, b + EC_GW) of u1
@@ -836,8 +887,12 @@ CHIP_DEV void comb_g_body(uint32_t blk, const uint32_t* __restrict__ count, cons
             const uint32_t av = (uint32_t)(v < 0 ? -v : v);
             load_apt(ga, G + ((uint64_t)w * EC_GENT + av - 1) * 16);
             if (v < 0) fp_neg<C>(ga.y, ga.y);
-            jmadd<C>(acc, acc, ga);
+            jmadd_x<C>(acc, acc, ga, exc);
         }
+    }
+    if (exc || park_all) {   // finished by k_ecdsa_comb_retry (park_all: CHIP_FLAG_EC_RETRY_ALL, tests)
+        mid[(uint64_t)40 * cap + gid] = 2u;
+        return;
     }
     mid_store(mid, cap, gid, 0, acc.X);
     mid_store(mid, cap, gid, 8, acc.Y);
@@ -849,9 +904,10 @@ CHIP_DEV void comb_g_body(uint32_t blk, const uint32_t* __restrict__ count, cons
 __global__ void __launch_bounds__(256) k_ecdsa_comb_g(const uint32_t* __restrict__ counts,
                                                       const uint32_t* __restrict__ gcomb, uint32_t* __restrict__ mid_r1,
                                                       uint32_t* __restrict__ mid_k1, const uint32_t* __restrict__ wp_r1,
-                                                      const uint32_t* __restrict__ wp_k1, uint64_t cap, uint32_t half) {
-    if (blockIdx.x < half) comb_g_body<CURVE_R1>(blockIdx.x, counts + LIST_R1, gcomb, mid_r1, wp_r1, cap);
-    else comb_g_body<CURVE_K1>(blockIdx.x - half, counts + LIST_K1, gcomb, mid_k1, wp_k1, cap);
+                                                      const uint32_t* __restrict__ wp_k1, uint64_t cap, uint32_t half,
+                                                      uint32_t park_all) {
+    if (blockIdx.x < half) comb_g_body<CURVE_R1>(blockIdx.x, counts + LIST_R1, gcomb, mid_r1, wp_r1, cap, park_all);
+    else comb_g_body<CURVE_K1>(blockIdx.x - half, counts + LIST_K1, gcomb, mid_k1, wp_k1, cap, park_all);
 }
 
 // D.  u2 Q half: one mixed addition per non-zero radix-16 digit from the key's affine table, then
@@ -865,8 +921,9 @@ CHIP_DEV void comb_q_body(uint32_t blk, const uint32_t* __restrict__ list, const
                           uint32_t* __restrict__ mid, uint64_t cap, uint8_t* __restrict__ status) {
     const uint32_t n = *count;
     const uint32_t gid = blk * blockDim.x + threadIdx.x;
-    if (gid >= n || !mid[(uint64_t)40 * cap + gid]) return;
+    if (gid >= n || mid[(uint64_t)40 * cap + gid] != 1u) return;
     const uint32_t i = list[gid];
+    bool exc = false;
     jpt acc;
     apt ent;
     u256 u2, r;
@@ -887,10 +944,14 @@ CHIP_DEV void comb_q_body(uint32_t blk, const uint32_t* __restrict__ list, const
             if (!d) continue;
             const uint32_t w = (uint32_t)(wd * 8 + q);
             load_apt(ent, qt + (w * EC_COMB_QENT + (uint32_t)(d < 0 ? -d : d) - 1) * 16);
-            add_digit<C>(acc, ent, d);
+            add_digit_x<C>(acc, ent, d, exc);
         }
     }
     if (HALF == 0) {
+        if (exc) {
+            mid[(uint64_t)40 * cap + gid] = 2u;
+            return;
+        }
         mid_store(mid, cap, gid, 0, acc.X);
         mid_store(mid, cap, gid, 8, acc.Y);
         mid_store(mid, cap, gid, 16, acc.Z);
@@ -898,7 +959,11 @@ CHIP_DEV void comb_q_body(uint32_t blk, const uint32_t* __restrict__ list, const
     }
     if (cq) {
         load_apt(ent, qt + (64u * EC_COMB_QENT) * 16);
-        add_digit<C>(acc, ent, 1);
+        add_digit_x<C>(acc, ent, 1, exc);
+    }
+    if (exc) {
+        mid[(uint64_t)40 * cap + gid] = 2u;
+        return;
     }
     status[i] = ecdsa_check<C>(acc, r) ? CHIP_VALID : CHIP_INVALID;
 }
@@ -916,6 +981,60 @@ __global__ void __launch_bounds__(256) k_ecdsa_comb_q(const uint32_t* __restrict
         comb_q_body<CURVE_R1, HALF>(blockIdx.x, list_r1, counts + LIST_R1, key_idx, ctab, mid_r1, cap, status);
     else
         comb_q_body<CURVE_K1, HALF>(blockIdx.x - half, list_k1, counts + LIST_K1, key_idx, ctab, mid_k1, cap, status);
+}
+
+// E.  Lanes parked by an exceptional addition (mid state 2) verified again from their bytes with complete
+// additions: e, s^-1, u1, u2, then u1 G + u2 Q by one double-and-add over both scalars (Shamir).  Runs for
+// every batch; for honest inputs no lane is parked and every wave exits at its first load.
+template <int C>
+CHIP_DEV void comb_retry_body(uint32_t blk, const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
+                              const chip_sig_batch_dev& b, const uint32_t* __restrict__ ectab,
+                              const uint32_t* __restrict__ mid, uint64_t cap, uint8_t* __restrict__ status) {
+    const uint32_t gid = blk * blockDim.x + threadIdx.x;
+    if (gid >= *count || mid[(uint64_t)40 * cap + gid] != 2u) return;
+    const ec_curve_c& cv = curve<C>();
+    const uint32_t i = list[gid];
+    const uint32_t mi = b.msg_idx[i];
+    u256 r, s, e;
+    const uint32_t st0 = ecdsa_front<C>(r, s, e, b.sig_data + b.sig_off[i], b.sig_len[i], b.msg_data + b.msg_off[mi],
+                                        b.msg_len[mi]);
+    if (st0 != 0xffu) {
+        status[i] = (uint8_t)st0;
+        return;
+    }
+    u256 r2n, sm, inv, u1, u2;
+    u256_from_c(r2n, cv.r2_n);
+    mn_mul<C>(sm, s, r2n);
+    mn_inv<C>(inv, sm);   // s^-1 R
+    mn_mul<C>(u1, e, inv);
+    mn_mul<C>(u2, r, inv);
+    const ec_aff_c& g = (EC_CURVE(C) == CURVE_R1) ? EC_R1_G_TABLE[1] : EC_K1_G_TABLE[1];
+    apt G, Q;
+#pragma unroll
+    for (int k = 0; k < 8; k++) {
+        G.x.w[k] = g.x[k];
+        G.y.w[k] = g.y[k];
+    }
+    load_apt(Q, ectab + (uint64_t)b.key_idx[i] * EC_TAB_STRIDE + 16);
+    jpt acc;
+    jpt_inf(acc);
+#pragma unroll 1
+    for (int bit = 255; bit >= 0; bit--) {
+        if (!u256_is_zero(acc.Z)) jdbl<C>(acc, acc);
+        if ((u1.w[bit >> 5] >> (bit & 31)) & 1u) jmadd_full<C>(acc, acc, G);
+        if ((u2.w[bit >> 5] >> (bit & 31)) & 1u) jmadd_full<C>(acc, acc, Q);
+    }
+    status[i] = ecdsa_check<C>(acc, r) ? CHIP_VALID : CHIP_INVALID;
+}
+__global__ void __launch_bounds__(256) k_ecdsa_comb_retry(const uint32_t* __restrict__ list_r1,
+                                                          const uint32_t* __restrict__ list_k1,
+                                                          const uint32_t* __restrict__ counts, chip_sig_batch_dev b,
+                                                          const uint32_t* __restrict__ ectab,
+                                                          const uint32_t* __restrict__ mid_r1,
+                                                          const uint32_t* __restrict__ mid_k1, uint64_t cap,
+                                                          uint8_t* __restrict__ status, uint32_t half) {
+    if (blockIdx.x < half) comb_retry_body<CURVE_R1>(blockIdx.x, list_r1, counts + LIST_R1, b, ectab, mid_r1, cap, status);
+    else comb_retry_body<CURVE_K1>(blockIdx.x - half, list_k1, counts + LIST_K1, b, ectab, mid_k1, cap, status);
 }
 
 uint64_t ecdsa_comb_key_words() { return EC_COMB_KEY_WORDS + EC_COMB_JAC_WORDS; }
@@ -981,11 +1100,20 @@ void launch_ecdsa_comb_inv(hipStream_t st, uint64_t n, const uint32_t* counts, u
     hipLaunchKernelGGL(k_ecdsa_comb_inv, dim3((2 * nw + 63) / 64), dim3(64), 0, st, counts, wp_r1, wp_k1, nw);
 }
 void launch_ecdsa_comb_g(hipStream_t st, uint64_t n, const uint32_t* counts, const uint32_t* gcomb, uint32_t* mid_r1,
-                         uint32_t* mid_k1, const uint32_t* wp_r1, const uint32_t* wp_k1) {
+                         uint32_t* mid_k1, const uint32_t* wp_r1, const uint32_t* wp_k1, bool park_all) {
     if (!n) return;
     const uint32_t half = (uint32_t)((n + 255) / 256);
     hipLaunchKernelGGL(k_ecdsa_comb_g, dim3(2 * half), dim3(256), 0, st, counts, gcomb, mid_r1, mid_k1, wp_r1, wp_k1,
-                       (uint64_t)n, half);
+                       (uint64_t)n, half, park_all ? 1u : 0u);
+}
+void launch_ecdsa_comb_retry(hipStream_t st, uint64_t n, const uint32_t* list_r1, const uint32_t* list_k1,
+                             const uint32_t* counts, const chip_sig_batch* b, const uint32_t* ectab,
+                             const uint32_t* mid_r1, const uint32_t* mid_k1, uint8_t* status) {
+    if (!n) return;
+    const uint32_t half = (uint32_t)((n + 255) / 256);
+    chip_sig_batch_dev d{b->key_idx, b->msg_idx, b->sig_data, b->sig_off, b->sig_len, b->msg_data, b->msg_off, b->msg_len};
+    hipLaunchKernelGGL(k_ecdsa_comb_retry, dim3(2 * half), dim3(256), 0, st, list_r1, list_k1, counts, d, ectab, mid_r1,
+                       mid_k1, (uint64_t)n, status, half);
 }
 void launch_ecdsa_comb_q(hipStream_t st, uint64_t n, const uint32_t* list_r1, const uint32_t* list_k1,
                          const uint32_t* counts, const chip_sig_batch* b, const uint32_t* ctab, uint32_t* mid_r1,

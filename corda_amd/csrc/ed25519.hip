@@ -179,6 +179,42 @@ __global__ void __launch_bounds__(256) k_ed25519_verify(const uint32_t* __restri
     status[i] = eq ? CHIP_VALID : CHIP_INVALID;
 }
 
+// ---- Crypto.decodePublicKey of an Ed25519 SPKI (i2p GroupElement(curve, bytes)) for the Kryo front end:
+// ok = the point decodes; kind 1 also requires the canonical encoding EdDSAPublicKey re-encodes (A.toByteArray:
+// y < p, the sign bit = parity of x)
+__global__ void __launch_bounds__(256) k_ed25519_key_check(uint64_t n, const uint8_t* __restrict__ pool,
+                                                           const uint64_t* __restrict__ off,
+                                                           const uint32_t* __restrict__ len,
+                                                           const uint8_t* __restrict__ kind, uint8_t* __restrict__ ok) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n || len[i] != 44) return;
+    const uint8_t* p = pool + off[i];
+    bool is_ed = true;
+#pragma unroll
+    for (int j = 0; j < 12; j++) is_ed = is_ed && (p[j] == SPKI_ED[j]);
+    if (!is_ed) return;
+    uint32_t w[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) w[j] = ld_le32(p + 12 + 4 * j);
+    ge_p3 A;
+    bool good = ge_frombytes(A, w);
+    if (good && kind[i]) {
+        uint32_t ab[8];
+        fe_tobytes(ab, A.Y);
+        ab[7] |= fe_isnegative(A.X) << 31;
+#pragma unroll
+        for (int j = 0; j < 8; j++) good = good && ab[j] == w[j];
+    }
+    ok[i] = good ? 1 : 0;
+}
+
+void launch_ed25519_key_check(hipStream_t st, uint64_t n, const uint8_t* pool, const uint64_t* off, const uint32_t* len,
+                              const uint8_t* kind, uint8_t* ok) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_ed25519_key_check, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, n, pool, off, len, kind,
+                       ok);
+}
+
 // ---------------------------------------------------------------------------------------
 void launch_ed25519_key_prep(hipStream_t st, uint64_t n_keys, const uint8_t* key_data, const uint64_t* key_off,
                              const uint32_t* key_len, KeyMeta* meta, uint32_t* abytes, uint32_t* table,

@@ -9,17 +9,21 @@
 //                        OpaqueBytes.bytes / TransactionSignature.by / TransactionSignature.signatureMetadata,
 //                        each through OutputChunked(1024); metadata = two chunked zig-zag ints (nested chunks)
 //   WireTransaction    = header, class 12, NOT_NULL, then references OFF: list of ComponentGroup
-//                        (fields components = list of SerializedBytes, groupIndex), PrivacySalt (class id >= 14,
-//                        varint 32, 32 bytes)                                            Kryo.kt:236-247
-// Classes registered after SerializedBytes (PrivacySalt, the PublicKey classes) have library-dependent
-// ids: any registered id >= 14 is accepted where the position fixes the meaning.
+//                        (fields components = list of SerializedBytes, groupIndex), PrivacySalt (the
+//                        registry's id, varint 32, 32 bytes)                             Kryo.kt:236-247
+// Class ids come from the context's chip_kryo_registry (DefaultKryoCustomizer.kt:56-136; ids 10-13 pinned,
+// PrivacySalt and the PublicKeySerializer classes per deployment): any other registered id where the
+// position fixes the class is outside the grammar (fail closed -> CHIP_STX_UNSUPPORTED).
+// Inputs must be the canonical StateRef encoding (checked in pass 1), so pass 2's duplicate-input check
+// compares bytes (checkNoDuplicateInputs compares decoded StateRefs, BaseTransaction.kt:37).
 //
 // Statuses, in the order the JVM meets them: CHIP_STX_KRYO (header mismatch, truncation: the
 // KryoException of SignedTransaction deserialisation, then of the lazy WireTransaction one),
 // CHIP_STX_NO_SIGS (SignedTransaction.init require), CHIP_STX_INVARIANT (WireTransaction.init checks,
 // WireTransaction.kt:53-60 + BaseTransaction.kt:30-37), CHIP_STX_UNSUPPORTED (well-formed input outside
 // this grammar: back-references, other classes, > 8 class names per graph, group index >= 64, > 64 inputs
-// for the duplicate check — the caller hands such a transaction to the JVM path).
+// for the duplicate check, inputs that are not canonical StateRefs — the caller hands such a transaction to
+// the JVM path).
 //
 // Passes: k_stx_parse<false> validates and counts (components skipped chunk by chunk), an inclusive scan
 // gives the ranges, k_stx_parse<true> parses again and writes the batches: component / signature /
@@ -159,6 +163,20 @@ struct Cur {
             for (uint32_t i = 0; i < n && !err; i++) (void)byte<L>();
         }
     }
+    // A level-1 field begins here.  With `check`, its whole chunk chain is validated first (every chunk inside
+    // the input, the 0 end marker present): a truncated field is a KryoException before anything inside it
+    // is interpreted, the order in which the oracle (which de-chunks a field before reading it) meets them.
+    __device__ __forceinline__ void open1(bool check) {
+        rem1 = 0;
+        if (!check || err) return;
+        const uint64_t p = pos;
+        for (int guard = 0; guard < (1 << 20) && !err; guard++) {
+            const uint32_t n = varint<0>();
+            if (err || n == 0) break;
+            skip<0>(n);
+        }
+        if (!err) pos = p;
+    }
     // InputChunked.nextChunks at the end of a field: skip what is left of it, through the 0 marker
     template <int L> __device__ __forceinline__ void end_field() {
         if constexpr (L == 1) {
@@ -255,13 +273,13 @@ struct Cur {
             if (!string_is<L>(k_fields[first + f], k_field_len[first + f])) fail(E_UNSUP);
     }
     // a list class + size: ArrayList / SingletonList / Arrays$ArrayList (with its component class)
-    template <int L> __device__ __forceinline__ uint32_t list(bool refs) {
+    template <int L> __device__ __forceinline__ uint32_t list(bool refs, int32_t aslist) {
         const int c = read_class<L>();
         if (err) return 0;
         if (refs) not_null<L>();
         if (c == -C_SINGLETON) return 1;
         if (c == -C_ARRAYLIST) return varint<L>();
-        if (c == 10) {
+        if (c == aslist) {
             const uint32_t n = varint<L>();
             (void)read_class<L>();
             return n;
@@ -296,6 +314,26 @@ template <> __device__ __forceinline__ uint8_t Cur::byte<2>() {
     rem2--;
     return byte<1>();
 }
+
+// a class id registered with PublicKeySerializer (Kryo.kt:302-311: every such class reads the same bytes)
+__device__ __forceinline__ bool key_class_ok(const chip_kryo_registry& reg, int c) {
+    bool ok = false;
+    for (uint32_t i = 0; i < CHIP_KRYO_MAX_KEY_CLASSES; i++) ok |= i < reg.n_public_key && reg.public_key[i] == c;
+    return ok && c >= 0;
+}
+
+// The canonical StateRef encoding (kryo.state_ref, oracle stateref_enc): 74 fixed bytes, varint(zn), the
+// zig-zag index in zn minimal varint bytes, 65 fixed bytes, the 32-byte txhash, 01 00 00; 175 + zn bytes.
+__constant__ uint8_t k_sr_pre[74] = {
+    0x63, 0x6f, 0x72, 0x64, 0x61, 0x00, 0x00, 0x01, 0x01, 0x00, 0x6e, 0x65, 0x74, 0x2e, 0x63, 0x6f, 0x72, 0x64, 0x61,
+    0x2e, 0x63, 0x6f, 0x72, 0x65, 0x2e, 0x63, 0x6f, 0x6e, 0x74, 0x72, 0x61, 0x63, 0x74, 0x73, 0x2e, 0x53, 0x74, 0x61,
+    0x74, 0x65, 0x52, 0x65, 0xe6, 0x01, 0x02, 0x53, 0x74, 0x61, 0x74, 0x65, 0x52, 0x65, 0x66, 0x2e, 0x69, 0x6e, 0x64,
+    0x65, 0xf8, 0x53, 0x74, 0x61, 0x74, 0x65, 0x52, 0x65, 0x66, 0x2e, 0x74, 0x78, 0x68, 0x61, 0x73, 0xe8};
+__constant__ uint8_t k_sr_mid[65] = {
+    0x00, 0x5f, 0x01, 0x01, 0x6e, 0x65, 0x74, 0x2e, 0x63, 0x6f, 0x72, 0x64, 0x61, 0x2e, 0x63, 0x6f, 0x72, 0x65, 0x2e,
+    0x63, 0x72, 0x79, 0x70, 0x74, 0x6f, 0x2e, 0x53, 0x65, 0x63, 0x75, 0x72, 0x65, 0x48, 0x61, 0x73, 0x68, 0x24, 0x53,
+    0x48, 0x41, 0x32, 0x35, 0xb6, 0x01, 0x01, 0x4f, 0x70, 0x61, 0x71, 0x75, 0x65, 0x42, 0x79, 0x74, 0x65, 0x73, 0x2e,
+    0x62, 0x79, 0x74, 0x65, 0xf3, 0x22, 0x01, 0x21};
 
 // 4 bytes at any offset of the pool (two aligned loads + byte funnel; the pool has >= 8 bytes of slack)
 __device__ __forceinline__ uint32_t ld32u(const uint8_t* pool, uint64_t off) {
@@ -388,6 +426,36 @@ template <bool EMIT> __device__ __forceinline__ uint64_t run1(Cur& c, uint32_t n
     return at;
 }
 
+// A component of n bytes read at level 1 (consumed whole): is it the canonical StateRef encoding?
+__device__ __forceinline__ bool stateref_canonical(Cur& c, uint32_t n) {
+    if (n < 176 || n > 180) {
+        c.skip<1>(n);
+        return false;
+    }
+    const uint32_t zn = n - 175;
+    bool ok = true;
+    uint32_t last = 0;
+    for (uint32_t i = 0; i < n && !c.err; i++) {
+        const uint8_t b = c.byte<1>();
+        if (i < 74) {
+            ok &= b == k_sr_pre[i];
+        } else if (i == 74) {
+            ok &= b == zn;
+        } else if (i < 75 + zn) {                 // the index varint: minimal, at most 32 bits
+            const bool lastb = i == 74 + zn;
+            ok &= lastb ? !(b & 0x80) : (b & 0x80) != 0;
+            last = b;
+        } else if (i < 140 + zn) {
+            ok &= b == k_sr_mid[i - 75 - zn];
+        } else if (i >= 172 + zn) {
+            ok &= b == (i == 172 + zn ? 1 : 0);
+        }
+    }
+    if (zn > 1) ok &= last != 0;
+    if (zn == 5) ok &= last <= 0x0f;
+    return ok;
+}
+
 __device__ __forceinline__ bool header_ok(Cur& c) {
     const uint8_t h[8] = {'c', 'o', 'r', 'd', 'a', 0, 0, 1};
     for (int i = 0; i < 8; i++)
@@ -396,13 +464,15 @@ __device__ __forceinline__ bool header_ok(Cur& c) {
 }
 
 // requiredSigningKeys walk (WireTransaction.kt:66-75) over one transaction's components in the pool:
-// take(off, len) for each signer key of every Command component in order, then for the notary Party's
-// owningKey when the transaction has inputs or a time-window.  False when a command / notary component
-// is outside the grammar or a key spans a chunk (the caller marks the transaction UNSUPPORTED).
+// take(off, len, required) for each signer key of every Command component in order, then for the notary
+// Party's owningKey — required when the transaction has inputs or a time-window; otherwise taken with
+// required = false (the JVM decodes it while deserialising the notary, so it is validated, not kept).  False
+// when a command / notary component is outside the grammar, a Command has no signers (Command.init,
+// Structures.kt:183) or a key spans a chunk (the caller marks the transaction UNSUPPORTED).
 template <class F>
 __device__ __forceinline__ bool req_walk(Cur& c, const uint8_t* pool, uint64_t pool_bytes, uint64_t c0, uint64_t c1,
                                          const uint32_t* comp_group, const uint64_t* comp_off,
-                                         const uint32_t* comp_len, F&& take) {
+                                         const uint32_t* comp_len, const chip_kryo_registry& reg, F&& take) {
     uint64_t present = 0;
     int64_t notary = -1;
     for (uint64_t k = c0; k < c1; k++) {
@@ -419,7 +489,7 @@ __device__ __forceinline__ bool req_walk(Cur& c, const uint8_t* pool, uint64_t p
             if (comp_group[k] != 2) continue;
             kk = (int64_t)k;
         } else {
-            if (!want_notary) break;
+            if (notary < 0) break;
             kk = notary;
         }
         const uint64_t a = comp_off[kk];
@@ -430,15 +500,16 @@ __device__ __forceinline__ bool req_walk(Cur& c, const uint8_t* pool, uint64_t p
         c.not_null<0>();
         if (is_cmd) c.header<0>(H_CMD, 7, 2);
         else c.header<0>(H_PARTY, 9, 2);
-        c.rem1 = 0;
-        const uint32_t nk = is_cmd ? c.list<1>(true) : 1;
+        c.open1(true);   // the signers / owningKey field: a truncated chunk chain is a KryoException
+        const uint32_t nk = is_cmd ? c.list<1>(true, reg.arrays_aslist) : 1;
+        if (nk == 0) c.fail(E_UNSUP);
         for (uint32_t i = 0; i < nk && !c.err; i++) {
-            if (c.read_class<1>() < 14) c.fail(E_UNSUP);
+            if (!key_class_ok(reg, c.read_class<1>())) c.fail(E_UNSUP);
             c.not_null<1>();
             const uint32_t kl = c.varint<1>();
             const uint64_t at = run1<false>(c, kl, none, spill);
             if (c.err || spill) break;
-            take(at, kl);
+            take(at, kl, is_cmd || want_notary);
         }
         if (c.err || spill) return false;
     }
@@ -466,6 +537,7 @@ struct Outs {   // pass-2 destinations (NULL in pass 1)
     const int32_t* meta;
     uint32_t n_meta;
     uint64_t* nraw;                // CHIP_STX_REQUIRED: signer entries per tx (counted here), else NULL
+    chip_kryo_registry reg;
 };
 
 template <bool EMIT>
@@ -493,9 +565,9 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
         st = CHIP_STX_KRYO;
         goto done;
     }
-    if (c.read_class<0>() != 11) c.fail(E_UNSUP);
+    if (c.read_class<0>() != o.reg.signed_tx) c.fail(E_UNSUP);
     c.not_null<0>();
-    if (c.read_class<0>() != 13) c.fail(E_UNSUP);
+    if (c.read_class<0>() != o.reg.serialized_bytes) c.fail(E_UNSUP);
     c.not_null<0>();
     {
         const uint32_t m = c.varint<0>();
@@ -504,7 +576,7 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
         tx_b = c.pos;
     }
     {
-        const uint32_t ns = c.list<0>(true);
+        const uint32_t ns = c.list<0>(true, o.reg.arrays_aslist);
         for (uint32_t i = 0; i < ns && !c.err; i++) {
             if (c.read_class<0>() != -C_TXSIG) {
                 c.fail(E_UNSUP);
@@ -513,7 +585,7 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
             c.not_null<0>();
             c.header<0>(H_TXSIG, 0, 3);
             // OpaqueBytes.bytes: NOT_NULL, varint(length + 1), bytes
-            c.rem1 = 0;
+            c.open1(!EMIT);
             c.not_null<1>();
             uint32_t sl = c.varint<1>();
             if (sl == 0) c.fail(E_UNSUP);
@@ -526,8 +598,9 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
                 }
             }
             c.end_field<1>();
-            // TransactionSignature.by: a registered PublicKey class, NOT_NULL, varint length, SPKI bytes
-            if (c.read_class<1>() < 14) c.fail(E_UNSUP);
+            // TransactionSignature.by: a PublicKeySerializer class, NOT_NULL, varint length, SPKI bytes
+            c.open1(!EMIT);
+            if (!key_class_ok(o.reg, c.read_class<1>())) c.fail(E_UNSUP);
             c.not_null<1>();
             const uint32_t kl = c.varint<1>();
             {
@@ -539,6 +612,7 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
             }
             c.end_field<1>();
             // TransactionSignature.signatureMetadata: NOT_NULL, header, two chunked ints (level 2)
+            c.open1(!EMIT);
             c.not_null<1>();
             c.header<1>(H_META, 3, 2);
             c.rem2 = 0;
@@ -576,11 +650,11 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
             st = CHIP_STX_KRYO;
             goto done;
         }
-        if (w.read_class<0>() != 12) w.fail(E_UNSUP);
+        if (w.read_class<0>() != o.reg.wire_tx) w.fail(E_UNSUP);
         w.not_null<0>();
-        const uint32_t ng = w.list<0>(false);
+        const uint32_t ng = w.list<0>(false, o.reg.arrays_aslist);
         uint64_t present = 0;
-        bool empty_group = false, dup_group = false;
+        bool empty_group = false, dup_group = false, multi = false, noncanon = false;
         uint64_t in_first = 0, in_count = 0;
         for (uint32_t g = 0; g < ng && !w.err; g++) {
             if (w.read_class<0>() != -C_GROUP) {
@@ -588,24 +662,34 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
                 break;
             }
             w.header<0>(H_GROUP, 5, 2);
-            w.rem1 = 0;
-            const uint32_t nc = w.list<1>(false);
+            w.open1(!EMIT);
+            const uint32_t nc = w.list<1>(false, o.reg.arrays_aslist);
             const uint64_t first = cbase + comps;
+            bool canon = true;   // pass 1: every component of the group is a canonical StateRef (matters for 0)
             for (uint32_t k = 0; k < nc && !w.err; k++) {
-                if (w.read_class<1>() != 13) {
+                if (w.read_class<1>() != o.reg.serialized_bytes) {
                     w.fail(E_UNSUP);
                     break;
                 }
                 const uint32_t cl = w.varint<1>();
-                const uint64_t at = run1<EMIT>(w, cl, sink, extra);
                 if (EMIT) {
+                    const uint64_t at = run1<EMIT>(w, cl, sink, extra);
                     o.comp_off[cbase + comps] = at;
                     o.comp_len[cbase + comps] = cl;
                     o.comp_internal[cbase + comps] = k;
+                } else {
+                    // the extra region is sized by run1's rule: a run not inside the current chunk
+                    if (w.rem1 == 0 && cl) {
+                        w.rem1 = w.varint<0>();
+                        if (!w.err && w.rem1 == 0) w.fail(E_KRYO);
+                    }
+                    if (cl > w.rem1) extra += (cl + 3) & ~3u;
+                    canon &= stateref_canonical(w, cl);
                 }
                 comps++;
             }
             w.end_field<1>();
+            w.open1(!EMIT);
             const int32_t gi = w.zigzag<1>();
             w.end_field<1>();
             if (gi < 0 || gi >= 64) {
@@ -614,6 +698,8 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
             }
             if (nc == 0) empty_group = true;
             if (present >> gi & 1) dup_group = true;
+            else if ((gi == 4 || gi == 5) && nc > 1) multi = true;   // MerkleTransaction.kt:32,38 (first group)
+            if (gi == 0 && !canon) noncanon = true;
             present |= 1ull << gi;
             if (gi == 0) {
                 in_first = first;
@@ -622,9 +708,9 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
             if (EMIT)
                 for (uint64_t k = first; k < cbase + comps; k++) o.comp_group[k] = (uint32_t)gi;
         }
-        // PrivacySalt: registered class (id >= 14), writeBytesWithLength(32 bytes)
+        // PrivacySalt: the registry's id, writeBytesWithLength(32 bytes)
         if (!w.err) {
-            if (w.read_class<0>() < 14) w.fail(E_UNSUP);
+            if (w.read_class<0>() != o.reg.privacy_salt) w.fail(E_UNSUP);
             if (w.varint<0>() != 32) w.fail(E_UNSUP);
             if (EMIT && !w.err && w.end - w.pos >= 32) {
                 uint32_t* dst = reinterpret_cast<uint32_t*>(o.salts + t * 32);
@@ -639,10 +725,10 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
         // WireTransaction.init (WireTransaction.kt:53-60), checkBaseInvariants (BaseTransaction.kt:30-37)
         const bool has_in = present & 1, has_out = present >> 1 & 1, has_cmd = present >> 2 & 1;
         const bool has_notary = present >> 4 & 1, has_tw = present >> 5 & 1;
-        if (empty_group || dup_group || (has_in && !has_notary) || (!has_in && !has_out) || !has_cmd ||
+        if (multi || empty_group || dup_group || (has_in && !has_notary) || (!has_in && !has_out) || !has_cmd ||
             (has_tw && !has_notary))
             st = CHIP_STX_INVARIANT;
-        if (in_count > 64) st = st == CHIP_STX_OK ? CHIP_STX_UNSUPPORTED : st;
+        if (in_count > 64 || noncanon) st = st == CHIP_STX_OK ? CHIP_STX_UNSUPPORTED : st;
         if (EMIT && st == CHIP_STX_OK && in_count > 1) {   // checkNoDuplicateInputs: equal serialized StateRefs
             sink.flush();
             for (uint64_t i = 0; i < in_count && st == CHIP_STX_OK; i++)
@@ -659,14 +745,20 @@ done:
     if (EMIT) {
         sink.flush();
         if (o.nraw) {   // the required-key walk's count, fused here (the components are in the pool now)
-            uint64_t cnt = 0;
+            uint64_t cnt = 0, all = 0;
             bool over = false;
             if (st == CHIP_STX_OK &&
-                !req_walk(c, o.pool, o.pool_bytes, cbase, cbase + comps, o.comp_group, o.comp_off, o.comp_len,
-                          [&](uint64_t, uint32_t) { over |= cnt >= 64; cnt++; }))
+                !req_walk(c, o.pool, o.pool_bytes, cbase, cbase + comps, o.comp_group, o.comp_off, o.comp_len, o.reg,
+                          [&](uint64_t, uint32_t, bool req) {
+                              if (req) {
+                                  over |= cnt >= 64;
+                                  cnt++;
+                              }
+                              all++;
+                          }))
                 st = CHIP_STX_UNSUPPORTED;
             if (over) st = CHIP_STX_UNSUPPORTED;   // more than 64 signer entries: JVM path
-            o.nraw[t] = st == CHIP_STX_OK ? cnt : 0;
+            o.nraw[t] = st == CHIP_STX_OK ? all : 0;
         }
         if (st != CHIP_STX_OK) status[t] = (uint8_t)st;
     } else {
@@ -744,19 +836,71 @@ __global__ void __launch_bounds__(256) k_stx_key_assign(uint64_t nsig, const uin
 // ---- requiredSigningKeys from the components (WireTransaction.kt:66-75) ----
 __device__ __forceinline__ uint8_t pool_byte(const uint8_t* pool, uint64_t off) { return pool[off]; }
 
-// SubjectPublicKeyInfo whose AlgorithmIdentifier OID is the CompositeKey OID
-__device__ __forceinline__ bool is_composite_spki(const uint8_t* pool, uint64_t off, uint32_t len) {
-    if (len < 27 || pool_byte(pool, off) != 0x30) return false;
-    uint32_t p = 1;
-    const uint8_t l1 = pool_byte(pool, off + 1);
-    p += l1 < 0x80 ? 1 : l1 == 0x81 ? 2 : l1 == 0x82 ? 3 : 99;
-    if (p + 2 + 21 > len || pool_byte(pool, off + p) != 0x30) return false;
-    const uint8_t l2 = pool_byte(pool, off + p + 1);
-    p += l2 < 0x80 ? 2 : l2 == 0x81 ? 3 : 99;
-    if (p + 21 > len) return false;
-    for (int i = 0; i < 21; i++)
-        if (pool_byte(pool, off + p + i) != k_composite_oid[i]) return false;
+// A DER TLV with a minimal definite length (short form, 0x81 >= 128, 0x82 >= 256) inside [pos, end) of the
+// key at `base` (CompositeKey.encoded is DER: what the JVM re-encodes is the only accepted form).
+__device__ __forceinline__ bool der_tlv(const uint8_t* pool, uint64_t base, uint32_t pos, uint32_t end, uint32_t& tag,
+                                        uint32_t& c0, uint32_t& c1) {
+    if (pos + 2 > end) return false;
+    tag = pool_byte(pool, base + pos);
+    const uint32_t l = pool_byte(pool, base + pos + 1);
+    uint32_t n, h;
+    if (l < 0x80) {
+        n = l;
+        h = 2;
+    } else if (l == 0x81) {
+        if (pos + 3 > end) return false;
+        n = pool_byte(pool, base + pos + 2);
+        if (n < 0x80) return false;
+        h = 3;
+    } else if (l == 0x82) {
+        if (pos + 4 > end) return false;
+        n = (uint32_t)pool_byte(pool, base + pos + 2) << 8 | pool_byte(pool, base + pos + 3);
+        if (n < 0x100) return false;
+        h = 4;
+    } else {
+        return false;
+    }
+    if (pos + h + n > end) return false;
+    c0 = pos + h;
+    c1 = pos + h + n;
     return true;
+}
+
+
+// SubjectPublicKeyInfo whose AlgorithmIdentifier is exactly SEQUENCE { the CompositeKey OID } (keys.is_composite)
+__device__ __forceinline__ bool is_composite_spki(const uint8_t* pool, uint64_t off, uint32_t len) {
+    uint32_t tag, c0, c1, a0, a1;
+    if (!der_tlv(pool, off, 0, len, tag, c0, c1) || tag != 0x30 || c1 != len) return false;
+    if (!der_tlv(pool, off, c0, c1, tag, a0, a1) || tag != 0x30 || a1 - a0 != 21) return false;
+    for (int i = 0; i < 21; i++)
+        if (pool_byte(pool, off + a0 + i) != k_composite_oid[i]) return false;
+    return true;
+}
+
+// the SubjectPublicKeyInfo prefixes of the keys the verify path reads (keys.spki_scheme, oracle orc_spki_scheme)
+__constant__ uint8_t k_spki_ed[12] = {0x30, 0x2a, 0x30, 0x05, 0x06, 0x03, 0x2b, 0x65, 0x70, 0x03, 0x21, 0x00};
+__constant__ uint8_t k_spki_r1[26] = {0x30, 0x59, 0x30, 0x13, 0x06, 0x07, 0x2a, 0x86, 0x48, 0xce, 0x3d, 0x02, 0x01,
+                                      0x06, 0x08, 0x2a, 0x86, 0x48, 0xce, 0x3d, 0x03, 0x01, 0x07, 0x03, 0x42, 0x00};
+__constant__ uint8_t k_spki_k1[23] = {0x30, 0x56, 0x30, 0x10, 0x06, 0x07, 0x2a, 0x86, 0x48, 0xce, 0x3d, 0x02,
+                                      0x01, 0x06, 0x05, 0x2b, 0x81, 0x04, 0x00, 0x0a, 0x03, 0x42, 0x00};
+enum { KS_NONE = 0, KS_ED = 1, KS_EC_U = 2, KS_EC_C = 3 };
+// 0, or the form of a plain key: Ed25519 (44 bytes), ECDSA r1 / k1 uncompressed (91 / 88) or compressed (59 / 56;
+// the two length bytes of the prefix differ: 0x39 / 0x22 and 0x36 / 0x22)
+__device__ __forceinline__ int spki_form(const uint8_t* pool, uint64_t off, uint32_t len) {
+    const uint8_t* k;
+    int n, form;
+    uint8_t l1, l2;
+    if (len == 44) { k = k_spki_ed; n = 12; form = KS_ED; l1 = 0x2a; l2 = 0x21; }
+    else if (len == 91) { k = k_spki_r1; n = 26; form = KS_EC_U; l1 = 0x59; l2 = 0x42; }
+    else if (len == 59) { k = k_spki_r1; n = 26; form = KS_EC_C; l1 = 0x39; l2 = 0x22; }
+    else if (len == 88) { k = k_spki_k1; n = 23; form = KS_EC_U; l1 = 0x56; l2 = 0x42; }
+    else if (len == 56) { k = k_spki_k1; n = 23; form = KS_EC_C; l1 = 0x36; l2 = 0x22; }
+    else return KS_NONE;
+    for (int i = 0; i < n; i++) {
+        const uint8_t want = i == 1 ? l1 : i == n - 2 ? l2 : k[i];
+        if (pool_byte(pool, off + i) != want) return KS_NONE;
+    }
+    return form;
 }
 
 struct ReqCtx {
@@ -784,101 +928,297 @@ __device__ __forceinline__ uint32_t lookup_kid(const ReqCtx& r, uint64_t off, ui
     return CHIP_REQ_NO_SIGNER;
 }
 
-// pass R1 counts the signer entries (commands' signers, then the notary key) of every OK transaction;
-// R2 writes them with their key index and a duplicate flag (an earlier entry of the same transaction
-// with the same key: requiredSigningKeys is a set).  A command or notary component outside the grammar,
-// a chunk-spanning key, more than 64 signer entries or a CompositeKey (its tree is not in the signer
-// pool) -> CHIP_STX_UNSUPPORTED.
-template <bool EMIT>
+// raw entry flags (k_stx_required -> k_stx_req_entry)
+enum { RF_KEEP = 1, RF_VALIDATE = 2, RF_COMPOSITE = 4, RF_DECODE = 8 };
+
+// k_stx_required<true>: per OK transaction, its signer entries (commands' signers, then the notary) with
+// their key index, a duplicate flag against the transaction's earlier required entries (requiredSigningKeys
+// is a set: equal encodings are one key), what has to be validated — a kept entry, and the notary when it is
+// not required — and whether a plain key has to be decoded (it signs none of this transaction's signatures:
+// the verify path decodes the others).  A key that is neither an Ed25519 / ECDSA key nor a CompositeKey
+// -> CHIP_STX_UNSUPPORTED.  (The emit pass counted the entries.)
 __global__ void __launch_bounds__(256) k_stx_required(uint64_t n, uint8_t* __restrict__ status,
                                                       const uint64_t* __restrict__ comp_start,
                                                       const uint32_t* __restrict__ comp_group,
                                                       const uint64_t* __restrict__ comp_off,
                                                       const uint32_t* __restrict__ comp_len, uint64_t pool_bytes,
-                                                      ReqCtx r, uint64_t* __restrict__ nraw,
+                                                      ReqCtx r, chip_kryo_registry reg,
+                                                      const uint64_t* __restrict__ sig_start,
+                                                      const uint32_t* __restrict__ key_idx,
                                                       const uint64_t* __restrict__ raw_start, uint32_t* __restrict__ raw_kid,
                                                       uint64_t* __restrict__ raw_off, uint32_t* __restrict__ raw_len,
-                                                      uint32_t* __restrict__ raw_keep, uint64_t* __restrict__ nreq) {
+                                                      uint32_t* __restrict__ raw_keep, uint32_t* __restrict__ raw_flag,
+                                                      uint32_t* __restrict__ raw_tx, uint64_t* __restrict__ nreq) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     if (status[t] != CHIP_STX_OK) {
-        if (!EMIT) nraw[t] = 0;
-        else nreq[t] = 0;
+        nreq[t] = 0;
         return;
     }
     uint64_t cnt = 0, kept = 0;
-    const uint64_t base = EMIT ? raw_start[t] : 0;
+    const uint64_t base = raw_start[t], lim = raw_start[t + 1];
+    const uint64_t s0 = sig_start[t], s1 = sig_start[t + 1];
     bool bad = false;
-    auto take = [&](uint64_t off, uint32_t len) {
-        if (cnt >= 64) {   // the duplicate check is quadratic: more signer entries go to the JVM path
+    auto take = [&](uint64_t off, uint32_t len, bool required) {
+        if (base + cnt >= lim) {   // the emit pass counted fewer entries: cannot happen for an OK transaction
             bad = true;
             return;
         }
-        const uint32_t kid = lookup_kid(r, off, len);
-        if (kid == CHIP_REQ_NO_SIGNER && is_composite_spki(r.pool, off, len)) bad = true;
-        if (EMIT && !bad) {
-            bool dup = false;
+        uint32_t kid = CHIP_REQ_NO_SIGNER, flag = RF_VALIDATE;
+        if (is_composite_spki(r.pool, off, len)) {
+            flag |= RF_COMPOSITE;
+        } else if (spki_form(r.pool, off, len) == KS_NONE) {
+            bad = true;   // RSA, SPHINCS, other encodings: Crypto.decodePublicKey is the JVM's
+        } else {
+            kid = lookup_kid(r, off, len);
+            bool signs = false;
+            if (kid != CHIP_REQ_NO_SIGNER)
+                for (uint64_t s = s0; s < s1 && !signs; s++) signs = key_idx[s] == kid;
+            if (!signs) flag |= RF_DECODE;
+        }
+        bool dup = false;
+        if (required) {
             for (uint64_t j = base; j < base + cnt && !dup; j++) {
+                if (!(raw_keep[j])) continue;
                 if (kid != CHIP_REQ_NO_SIGNER) dup = raw_kid[j] == kid;
                 else dup = raw_kid[j] == CHIP_REQ_NO_SIGNER && key_eq(r.pool, off, len, raw_off[j], raw_len[j]);
             }
-            raw_kid[base + cnt] = kid;
-            raw_off[base + cnt] = off;
-            raw_len[base + cnt] = len;
-            raw_keep[base + cnt] = dup ? 0u : 1u;
-            kept += dup ? 0 : 1;
         }
+        const bool keep = required && !dup;
+        if (!keep && required) flag &= ~RF_VALIDATE;   // an equal key is validated once
+        if (keep) flag |= RF_KEEP;
+        raw_kid[base + cnt] = kid;
+        raw_off[base + cnt] = off;
+        raw_len[base + cnt] = len;
+        raw_keep[base + cnt] = keep ? 1u : 0u;
+        raw_flag[base + cnt] = flag;
+        raw_tx[base + cnt] = (uint32_t)t;
+        kept += keep ? 1 : 0;
         cnt++;
     };
     Cur c;
-    if (!req_walk(c, r.pool, pool_bytes, comp_start[t], comp_start[t + 1], comp_group, comp_off, comp_len, take))
+    if (!req_walk(c, r.pool, pool_bytes, comp_start[t], comp_start[t + 1], comp_group, comp_off, comp_len, reg, take))
         bad = true;
-    if (!EMIT) {
-        if (bad) status[t] = CHIP_STX_UNSUPPORTED;
-        nraw[t] = bad ? 0 : cnt;
-    } else {
-        // (after the fused count in the emit pass, the only new failure here is a CompositeKey signer): a
-        // failed transaction keeps none of its counted entries, so the compaction stays aligned
-        if (bad) {
-            status[t] = CHIP_STX_UNSUPPORTED;
-            for (uint64_t j = base; j < raw_start[t + 1]; j++) raw_keep[j] = 0;
-        }
-        nreq[t] = bad ? 0 : kept;
+    if (bad) status[t] = CHIP_STX_UNSUPPORTED;
+    // a failed transaction keeps none of its entries, so the compaction stays aligned
+    for (uint64_t j = base + (bad ? 0 : cnt); j < lim; j++) {
+        raw_keep[j] = 0;
+        raw_flag[j] = 0;
+        raw_tx[j] = (uint32_t)t;
     }
+    nreq[t] = bad ? 0 : kept;
 }
 
-// required key r = the kept entries in order: one leaf node each (node r, key index or NO_SIGNER)
-__global__ void __launch_bounds__(256) k_stx_req_compact(uint64_t nraw, const uint32_t* __restrict__ raw_kid,
-                                                         const uint32_t* __restrict__ raw_keep,
-                                                         const uint32_t* __restrict__ keep_incl,
-                                                         uint64_t* __restrict__ node_start, uint32_t* __restrict__ node_val,
-                                                         uint32_t* __restrict__ node_nkids,
-                                                         uint32_t* __restrict__ node_weight) {
+// A CompositeKey SPKI (CompositeKey.kt:37-55 decode, :99-111 checkValidity / checkConstraints, :133-161 the
+// NodeAndWeight order) walked iteratively in post-order: leaf(off, len, weight) for every leaf, node(threshold,
+// kids, weight) for every composite node (root last, weight 1).  False when it is not the canonical encoding
+// of a valid key within the device's limits (<= 64 nodes, nesting < 8): keys.composite_tree's rules.
+struct CFrame {
+    uint32_t c1, pos, kids, threshold, weight, prev_off, prev_len, prev_w;
+    uint64_t total;
+};
+__device__ __forceinline__ bool der_pos_int(const uint8_t* pool, uint64_t base, uint32_t c0, uint32_t c1, uint32_t& v) {
+    const uint32_t n = c1 - c0;
+    if (n < 1 || n > 4) return false;
+    const uint32_t b0 = pool_byte(pool, base + c0);
+    if (b0 >= 0x80 || (n > 1 && b0 == 0 && pool_byte(pool, base + c0 + 1) < 0x80)) return false;
+    uint32_t x = 0;
+    for (uint32_t i = c0; i < c1; i++) x = x << 8 | pool_byte(pool, base + i);
+    v = x;
+    return x >= 1;
+}
+// ByteSequence.compareTo: unsigned lexicographic, then the shorter first
+__device__ __forceinline__ int bytes_cmp(const uint8_t* pool, uint64_t a, uint32_t na, uint64_t b, uint32_t nb) {
+    const uint32_t m = na < nb ? na : nb;
+    for (uint32_t i = 0; i < m; i++) {
+        const int x = pool_byte(pool, a + i), y = pool_byte(pool, b + i);
+        if (x != y) return x < y ? -1 : 1;
+    }
+    return na < nb ? -1 : na > nb ? 1 : 0;
+}
+// open the composite at [s, s + n) of the key (offsets relative to `off`): its children range and threshold
+__device__ __forceinline__ bool composite_open(const uint8_t* pool, uint64_t off, uint32_t s, uint32_t n, uint32_t weight,
+                                               CFrame& f) {
+    uint32_t tag, s0, s1, a0, a1, b0, b1, q0, q1, t0, t1, c0, c1;
+    if (!der_tlv(pool, off, s, s + n, tag, s0, s1) || tag != 0x30 || s1 != s + n) return false;
+    if (!der_tlv(pool, off, s0, s1, tag, a0, a1) || tag != 0x30 || a1 - a0 != 21) return false;
+    for (int i = 0; i < 21; i++)
+        if (pool_byte(pool, off + a0 + i) != k_composite_oid[i]) return false;
+    if (!der_tlv(pool, off, a1, s1, tag, b0, b1) || tag != 0x03 || b1 != s1 || b0 >= b1 || pool_byte(pool, off + b0) != 0)
+        return false;
+    if (!der_tlv(pool, off, b0 + 1, b1, tag, q0, q1) || tag != 0x30 || q1 != b1) return false;
+    uint32_t thr;
+    if (!der_tlv(pool, off, q0, q1, tag, t0, t1) || tag != 0x02 || !der_pos_int(pool, off, t0, t1, thr)) return false;
+    if (!der_tlv(pool, off, t1, q1, tag, c0, c1) || tag != 0x30 || c1 != q1) return false;
+    f.c1 = c1;
+    f.pos = c0;
+    f.kids = 0;
+    f.threshold = thr;
+    f.weight = weight;
+    f.prev_off = f.prev_len = f.prev_w = 0;
+    f.total = 0;
+    return true;
+}
+template <class Leaf, class Node>
+__device__ bool composite_walk(const uint8_t* pool, uint64_t off, uint32_t len, Leaf&& leaf, Node&& node) {
+    CFrame st[8];
+    int depth = 0, nn = 0;
+    if (!composite_open(pool, off, 0, len, 1, st[0])) return false;
+    for (int guard = 0; guard < 4096; guard++) {
+        CFrame& f = st[depth];
+        if (f.pos < f.c1) {
+            uint32_t tag, k0, k1, e0, e1, w0, w1, w;
+            if (!der_tlv(pool, off, f.pos, f.c1, tag, k0, k1) || tag != 0x30) return false;
+            if (!der_tlv(pool, off, k0, k1, tag, e0, e1) || tag != 0x03 || e0 >= e1 || pool_byte(pool, off + e0) != 0)
+                return false;
+            if (!der_tlv(pool, off, e1, k1, tag, w0, w1) || tag != 0x02 || w1 != k1 || !der_pos_int(pool, off, w0, w1, w))
+                return false;
+            const uint32_t co = e0 + 1, cn = e1 - e0 - 1;
+            if (f.kids && !(f.prev_w < w || (f.prev_w == w && bytes_cmp(pool, off + f.prev_off, f.prev_len, off + co, cn) < 0)))
+                return false;   // NodeAndWeight order, strictly (no duplicate children)
+            f.prev_off = co;
+            f.prev_len = cn;
+            f.prev_w = w;
+            f.kids++;
+            f.total += w;
+            if (f.total > 0x7fffffffull) return false;   // Math.addExact in checkConstraints
+            f.pos = k1;
+            if (is_composite_spki(pool, off + co, cn)) {
+                if (depth + 1 >= 8) return false;
+                if (!composite_open(pool, off, co, cn, w, st[depth + 1])) return false;
+                depth++;
+            } else {
+                const int form = spki_form(pool, off + co, cn);
+                if (form != KS_ED && form != KS_EC_U) return false;   // the encoding its key class re-encodes
+                if (++nn > 64) return false;
+                leaf(off + co, cn, w);
+            }
+        } else {
+            if (f.kids < 2 || (uint64_t)f.threshold > f.total) return false;
+            if (++nn > 64) return false;
+            node(f.threshold, f.kids, f.weight);
+            if (depth == 0) return true;
+            depth--;
+        }
+    }
+    return false;
+}
+
+// per raw entry: <false> counts the nodes of a kept required key (1 for a plain key, the tree for a
+// CompositeKey) and the key decodes it needs (a plain key that signs nothing here; every composite leaf,
+// whose encoding must also be canonical); an invalid CompositeKey -> CHIP_STX_UNSUPPORTED.  <true> writes
+// them: nodes at node_incl - nnodes (key index or NO_SIGNER for leaves, the threshold for composite nodes),
+// node_start of its required key, and the decode requests.
+template <bool EMIT>
+__global__ void __launch_bounds__(256) k_stx_req_entry(uint64_t nraw, uint8_t* __restrict__ status, ReqCtx r,
+                                                       const uint32_t* __restrict__ raw_kid,
+                                                       const uint64_t* __restrict__ raw_off,
+                                                       const uint32_t* __restrict__ raw_len,
+                                                       const uint32_t* __restrict__ raw_flag,
+                                                       const uint32_t* __restrict__ raw_tx,
+                                                       uint32_t* __restrict__ raw_nnodes, uint32_t* __restrict__ raw_ncheck,
+                                                       const uint32_t* __restrict__ keep_incl,
+                                                       const uint32_t* __restrict__ node_incl,
+                                                       const uint32_t* __restrict__ check_incl,
+                                                       uint64_t* __restrict__ node_start, uint32_t* __restrict__ node_val,
+                                                       uint32_t* __restrict__ node_nkids, uint32_t* __restrict__ node_weight,
+                                                       uint64_t* __restrict__ chk_off, uint32_t* __restrict__ chk_len,
+                                                       uint8_t* __restrict__ chk_kind, uint32_t* __restrict__ chk_tx) {
     const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= nraw || !raw_keep[i]) return;
-    const uint32_t q = keep_incl[i] - 1;
-    node_val[q] = raw_kid[i];
-    node_nkids[q] = 0;
-    node_weight[q] = 1;
-    node_start[q + 1] = q + 1;
+    if (i >= nraw) return;
+    const uint32_t flag = raw_flag[i];
+    if (!EMIT) {
+        uint32_t nodes = 0, checks = 0;
+        if (flag & RF_VALIDATE) {
+            if (flag & RF_COMPOSITE) {
+                uint32_t nl = 0, nc = 0;
+                if (composite_walk(r.pool, raw_off[i], raw_len[i], [&](uint64_t, uint32_t, uint32_t) { nl++; },
+                                   [&](uint32_t, uint32_t, uint32_t) { nc++; })) {
+                    nodes = nl + nc;
+                    checks = nl;
+                } else {
+                    status[raw_tx[i]] = CHIP_STX_UNSUPPORTED;
+                }
+            } else {
+                nodes = 1;
+                checks = (flag & RF_DECODE) ? 1 : 0;
+            }
+        }
+        raw_nnodes[i] = (flag & RF_KEEP) ? nodes : 0;
+        raw_ncheck[i] = checks;
+        return;
+    }
+    if (!(flag & RF_VALIDATE)) return;
+    uint64_t q = node_incl[i] - raw_nnodes[i];
+    uint64_t k = check_incl[i] - raw_ncheck[i];
+    const bool keep = flag & RF_KEEP;
+    if (keep) node_start[keep_incl[i]] = node_incl[i];
+    if (!(flag & RF_COMPOSITE)) {
+        if (keep) {
+            node_val[q] = raw_kid[i];
+            node_nkids[q] = 0;
+            node_weight[q] = 1;
+        }
+        if (raw_ncheck[i]) {
+            chk_off[k] = raw_off[i];
+            chk_len[k] = raw_len[i];
+            chk_kind[k] = 0;
+            chk_tx[k] = raw_tx[i];
+        }
+        return;
+    }
+    if (!raw_ncheck[i]) return;   // invalid (counted nothing)
+    composite_walk(
+        r.pool, raw_off[i], raw_len[i],
+        [&](uint64_t lo, uint32_t ln, uint32_t w) {
+            if (keep) {
+                node_val[q] = lookup_kid(r, lo, ln);
+                node_nkids[q] = 0;
+                node_weight[q] = w;
+                q++;
+            }
+            chk_off[k] = lo;
+            chk_len[k] = ln;
+            chk_kind[k] = 1;
+            chk_tx[k] = raw_tx[i];
+            k++;
+        },
+        [&](uint32_t thr, uint32_t kids, uint32_t w) {
+            if (keep) {
+                node_val[q] = thr;
+                node_nkids[q] = kids;
+                node_weight[q] = w;
+                q++;
+            }
+        });
+}
+
+// a failed key decode -> the transaction goes to the JVM path
+__global__ void __launch_bounds__(256) k_stx_check_apply(uint64_t nchk, const uint8_t* __restrict__ ok,
+                                                         const uint32_t* __restrict__ chk_tx, uint8_t* __restrict__ status) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= nchk) return;
+    if (!ok[i]) status[chk_tx[i]] = CHIP_STX_UNSUPPORTED;
 }
 
 inline dim3 grid_of(uint64_t n) { return dim3((uint32_t)((n + 255) / 256)); }
 
 }  // namespace
 
-void launch_stx_count(hipStream_t st, const chip_stx_blobs* in, uint8_t* status, uint64_t* ncomp, uint64_t* nsig,
-                      uint64_t* nextra) {
+void launch_stx_count(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_registry& reg, uint8_t* status,
+                      uint64_t* ncomp, uint64_t* nsig, uint64_t* nextra) {
     if (!in->n) return;
     Outs o{};
+    o.reg = reg;
     hipLaunchKernelGGL(k_stx_parse<false>, grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->off, in->len,
                        in->data_bytes, status, ncomp, nsig, nextra, o);
 }
 
-void launch_stx_emit(hipStream_t st, const chip_stx_blobs* in, uint8_t* status, const StxOut& d) {
+void launch_stx_emit(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_registry& reg, uint8_t* status,
+                     const StxOut& d) {
     if (!in->n) return;
     Outs o{d.pool, d.pool_bytes, d.extra_start, d.extra_base, d.salts, d.comp_start, d.comp_group, d.comp_internal, d.comp_off, d.comp_len, d.sig_start,
-           d.tx_idx, d.tmpl_idx, d.sig_off, d.sig_len, d.skey_off, d.skey_len, d.meta, d.n_meta, d.nraw};
+           d.tx_idx, d.tmpl_idx, d.sig_off, d.sig_len, d.skey_off, d.skey_len, d.meta, d.n_meta, d.nraw, reg};
     hipLaunchKernelGGL(k_stx_parse<true>, grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->off, in->len,
                        in->data_bytes, status, nullptr, nullptr, nullptr, o);
 }
@@ -904,26 +1244,38 @@ void launch_stx_keys(hipStream_t st, uint64_t nsig, const StxOut& d, uint64_t ma
                        d.skey_len, d.key_idx, d.key_off, d.key_len);
 }
 
-void launch_stx_required(hipStream_t st, bool emit, uint64_t n, uint8_t* status, const StxOut& d, uint64_t pool_bytes,
-                         uint64_t mask, const StxReq& q) {
+static ReqCtx req_ctx(const StxOut& d, uint64_t mask) {
+    return ReqCtx{d.pool, reinterpret_cast<const unsigned long long*>(d.tab), d.tab_min, mask, d.skey_off, d.skey_len,
+                  d.kincl};
+}
+
+void launch_stx_required(hipStream_t st, uint64_t n, uint8_t* status, const StxOut& d, uint64_t pool_bytes, uint64_t mask,
+                         const chip_kryo_registry& reg, const StxReq& q) {
     if (!n) return;
-    ReqCtx r{d.pool, reinterpret_cast<const unsigned long long*>(d.tab), d.tab_min, mask, d.skey_off, d.skey_len, d.kincl};
+    hipLaunchKernelGGL(k_stx_required, grid_of(n), dim3(256), 0, st, n, status, d.comp_start, d.comp_group,
+                       d.comp_off, d.comp_len, pool_bytes, req_ctx(d, mask), reg, d.sig_start, d.key_idx, q.raw_start,
+                       q.raw_kid, q.raw_off, q.raw_len, q.raw_keep, q.raw_flag, q.raw_tx, q.nreq);
+}
+
+void launch_stx_req_entries(hipStream_t st, bool emit, uint64_t nraw, uint8_t* status, const StxOut& d, uint64_t mask,
+                            const StxReq& q) {
+    if (!nraw) return;
     if (!emit)
-        hipLaunchKernelGGL(k_stx_required<false>, grid_of(n), dim3(256), 0, st, n, status, d.comp_start, d.comp_group,
-                           d.comp_off, d.comp_len, pool_bytes, r, q.nraw, nullptr, nullptr, nullptr, nullptr, nullptr,
-                           nullptr);
+        hipLaunchKernelGGL(k_stx_req_entry<false>, grid_of(nraw), dim3(256), 0, st, nraw, status, req_ctx(d, mask),
+                           q.raw_kid, q.raw_off, q.raw_len, q.raw_flag, q.raw_tx, q.raw_nnodes, q.raw_ncheck, nullptr,
+                           nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr);
     else
-        hipLaunchKernelGGL(k_stx_required<true>, grid_of(n), dim3(256), 0, st, n, status, d.comp_start, d.comp_group,
-                           d.comp_off, d.comp_len, pool_bytes, r, nullptr, q.raw_start, q.raw_kid, q.raw_off, q.raw_len,
-                           q.raw_keep, q.nreq);
+        hipLaunchKernelGGL(k_stx_req_entry<true>, grid_of(nraw), dim3(256), 0, st, nraw, status, req_ctx(d, mask),
+                           q.raw_kid, q.raw_off, q.raw_len, q.raw_flag, q.raw_tx, q.raw_nnodes, q.raw_ncheck,
+                           q.keep_incl, q.node_incl, q.check_incl, q.node_start, q.node_val, q.node_nkids,
+                           q.node_weight, q.chk_off, q.chk_len, q.chk_kind, q.chk_tx);
+}
+
+void launch_stx_check_apply(hipStream_t st, uint64_t nchk, const uint8_t* ok, const uint32_t* chk_tx, uint8_t* status) {
+    if (!nchk) return;
+    hipLaunchKernelGGL(k_stx_check_apply, grid_of(nchk), dim3(256), 0, st, nchk, ok, chk_tx, status);
 }
 
 hipError_t stx_scan_u32(hipStream_t st, void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, uint64_t n) {
     return hipcub::DeviceScan::InclusiveSum(temp, temp_bytes, in, out, (int)n, st);
-}
-
-void launch_stx_req_compact(hipStream_t st, uint64_t nraw, const StxReq& q) {
-    if (!nraw) return;
-    hipLaunchKernelGGL(k_stx_req_compact, grid_of(nraw), dim3(256), 0, st, nraw, q.raw_kid, q.raw_keep, q.keep_incl,
-                       q.node_start, q.node_val, q.node_nkids, q.node_weight);
 }

@@ -39,9 +39,9 @@ struct DevBuf {
 // buffers of one Kryo front-end call (chip_stx_parse_device): counts, ranges, pool, batches, key
 // interning, required keys, scan scratch
 struct StxBufs {
-    DevBuf s_ncomp, s_nsig, s_nbytes, s_cstart, s_sstart, s_pstart, s_pool, s_salts, s_cgroup, s_cint, s_coff, s_clen, s_txidx, s_tmpl, s_soff, s_slen, s_skoff, s_sklen, s_meta, s_tab, s_tabmin, s_kslot, s_krep, s_kflag, s_kincl, s_kidx, s_koff, s_klen, s_temp, r_nraw, r_rstart, r_kid, r_len, r_keep, r_kincl, r_off, r_nreq, r_qstart, r_nstart, r_val, r_nk, r_w;
+    DevBuf s_ncomp, s_nsig, s_nbytes, s_cstart, s_sstart, s_pstart, s_pool, s_salts, s_cgroup, s_cint, s_coff, s_clen, s_txidx, s_tmpl, s_soff, s_slen, s_skoff, s_sklen, s_meta, s_tab, s_tabmin, s_kslot, s_krep, s_kflag, s_kincl, s_kidx, s_koff, s_klen, s_temp, r_nraw, r_rstart, r_kid, r_len, r_keep, r_kincl, r_off, r_nreq, r_qstart, r_nstart, r_val, r_nk, r_w, r_flag, r_tx, r_nn, r_nc, r_ninc, r_cinc, k_off, k_len, k_kind, k_ok, k_tx, r_tot;
     void release() {
-        for (DevBuf* b : {&s_ncomp, &s_nsig, &s_nbytes, &s_cstart, &s_sstart, &s_pstart, &s_pool, &s_salts, &s_cgroup, &s_cint, &s_coff, &s_clen, &s_txidx, &s_tmpl, &s_soff, &s_slen, &s_skoff, &s_sklen, &s_meta, &s_tab, &s_tabmin, &s_kslot, &s_krep, &s_kflag, &s_kincl, &s_kidx, &s_koff, &s_klen, &s_temp, &r_nraw, &r_rstart, &r_kid, &r_len, &r_keep, &r_kincl, &r_off, &r_nreq, &r_qstart, &r_nstart, &r_val, &r_nk, &r_w}) b->release();
+        for (DevBuf* b : {&s_ncomp, &s_nsig, &s_nbytes, &s_cstart, &s_sstart, &s_pstart, &s_pool, &s_salts, &s_cgroup, &s_cint, &s_coff, &s_clen, &s_txidx, &s_tmpl, &s_soff, &s_slen, &s_skoff, &s_sklen, &s_meta, &s_tab, &s_tabmin, &s_kslot, &s_krep, &s_kflag, &s_kincl, &s_kidx, &s_koff, &s_klen, &s_temp, &r_nraw, &r_rstart, &r_kid, &r_len, &r_keep, &r_kincl, &r_off, &r_nreq, &r_qstart, &r_nstart, &r_val, &r_nk, &r_w, &r_flag, &r_tx, &r_nn, &r_nc, &r_ninc, &r_cinc, &k_off, &k_len, &k_kind, &k_ok, &k_tx, &r_tot}) b->release();
     }
 };
 
@@ -60,7 +60,7 @@ struct chip_ctx {
     hipStream_t aux2 = nullptr;                   // third stream: ECDSA table fills (while aux doubles on)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fork2 = nullptr, ev_join2 = nullptr;
     hipEvent_t ev_ec_chain_lo = nullptr, ev_ec_chain_hi = nullptr, ev_ec_lo = nullptr;
-    std::mutex mu;
+    std::recursive_mutex mu;   // recursive: chip_stx_verify holds it across the entries it calls
     std::string err;
     // verify workspaces
     DevBuf meta, abytes, edtab, ectab, lists, counts;
@@ -81,8 +81,9 @@ struct chip_ctx {
         x_st, x_rs;
     // Kryo front end (kryo.hip): two buffer sets used alternately, so batch k + 1 can be parsed (one
     // stream) while batch k is verified from the other set (another stream)
-    StxBufs stx[2];
+    StxBufs stx[3];   // [2]: chip_stx_verify's own set
     int stx_next = 0;
+    chip_kryo_registry kreg{10, 11, 12, 13, 65, 6, {44, 45, 47, 58, 60, 62, 0, 0}};   // cordahip.h defaults
     // chip_stx_verify staging
     DevBuf h2_data, h2_off, h2_len, h2_st, h2_ids, h2_v, h2_a, h2_sigst, h2_miss, h2_td, h2_to, h2_tl, h2_ta;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, tev0 = nullptr, tev1 = nullptr;
@@ -388,8 +389,7 @@ void chip_shutdown(chip_ctx* c) {
                       &c->h2_data, &c->h2_off, &c->h2_len, &c->h2_st, &c->h2_ids, &c->h2_v,
                       &c->h2_a, &c->h2_sigst, &c->h2_miss, &c->h2_td, &c->h2_to, &c->h2_tl, &c->h2_ta};
     for (DevBuf* b : bufs) b->release();
-    c->stx[0].release();
-    c->stx[1].release();
+    for (StxBufs& b : c->stx) b.release();
     for (int i = 0; i < chip_ctx::KRING; i++) {
         if (c->kring[i].a) hipEventDestroy(c->kring[i].a);
         if (c->kring[i].b) hipEventDestroy(c->kring[i].b);
@@ -577,7 +577,8 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
             launch_ecdsa_comb_pre(st, CHIP_SCHEME_R1, n, gl_r1, counts + LIST_R1, b, mid_r1, wp_r1, status);
             launch_ecdsa_comb_pre(st, CHIP_SCHEME_K1, n, gl_k1, counts + LIST_K1, b, mid_k1, wp_k1, status);
             launch_ecdsa_comb_inv(st, n, counts, wp_r1, wp_k1);
-            launch_ecdsa_comb_g(st, n, counts, c->e_gcomb.as<uint32_t>(), mid_r1, mid_k1, wp_r1, wp_k1);
+            launch_ecdsa_comb_g(st, n, counts, c->e_gcomb.as<uint32_t>(), mid_r1, mid_k1, wp_r1, wp_k1,
+                                (c->flags & CHIP_FLAG_EC_RETRY_ALL) != 0);
             c->kend(ke, st);
         }
         // ---- kernels that read the per-key tables ----
@@ -610,6 +611,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
             HIPCHK(c, hipStreamWaitEvent(st, c->ev_join2, 0));
             ke = c->kbegin(CHIP_K_ECDSA_K1, st);
             launch_ecdsa_comb_q(st, n, gl_r1, gl_k1, counts, b, c->e_ctab.as<uint32_t>(), mid_r1, mid_k1, status, 1);
+            launch_ecdsa_comb_retry(st, n, gl_r1, gl_k1, counts, b, c->ectab.as<uint32_t>(), mid_r1, mid_k1, status);
             c->kend(ke, st);
         } else {
             ke = c->kbegin(CHIP_K_ECDSA_R1, st);
@@ -647,7 +649,7 @@ static uint32_t host_scheme_hint(const chip_sig_batch* b) {
 static int verify_device_entry(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap, void* stream,
                                bool is_valid) {
     if (!c || !b || !status) return fail(c, CHIP_E_ARG, "null argument");
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     return verify_device_locked(c, b, status, bitmap, st, is_valid);
 }
@@ -704,7 +706,7 @@ static int verify_host_entry(chip_ctx* c, const chip_sig_batch* b, uint8_t* stat
         (nk && (!b->key_data || !b->key_off || !b->key_len)) || (nm && (!b->msg_data || !b->msg_off || !b->msg_len)))
         return fail(c, CHIP_E_ARG, "null batch array");
     // bounds: checked on the device after staging (k_check_batch), before any verify kernel runs
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     hipStream_t st = c->stream;
     HIPCHK(c, hipSetDevice(c->device));
     int r;
@@ -788,19 +790,28 @@ void chip_free_pinned(void* p) {
 
 // ---------------------------------------------------------------------------------------
 // Kryo front end (cordahip.h chip_stx_parse_device; kernels in kryo.hip)
-int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_status, chip_stx_parsed* out,
-                          void* stream) {
-    if (!c || !in || !out) return fail(c, CHIP_E_ARG, "null argument");
+int chip_set_kryo_registry(chip_ctx* c, const chip_kryo_registry* reg) {
+    if (!c || !reg) return fail(c, CHIP_E_ARG, "null argument");
+    if (reg->n_public_key > CHIP_KRYO_MAX_KEY_CLASSES) return fail(c, CHIP_E_ARG, "too many key classes");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    c->kreg = *reg;
+    return CHIP_OK;
+}
+
+int chip_get_kryo_registry(chip_ctx* c, chip_kryo_registry* reg) {
+    if (!c || !reg) return fail(c, CHIP_E_ARG, "null argument");
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    *reg = c->kreg;
+    return CHIP_OK;
+}
+
+// one parse into buffer set B (the caller holds c->mu)
+static int stx_parse(chip_ctx* c, StxBufs& B, const chip_stx_blobs* in, uint8_t* tx_status, chip_stx_parsed* out,
+                     hipStream_t st) {
     const uint64_t n = in->n;
-    if (n && (!in->data || !in->off || !in->len || !tx_status)) return fail(c, CHIP_E_ARG, "null blob array");
-    if (in->n_meta && !in->meta) return fail(c, CHIP_E_ARG, "null meta");
-    if (n >= (1ull << 31)) return fail(c, CHIP_E_ARG, "too many blobs");
-    std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(c, hipSetDevice(c->device));
-    hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     std::memset(out, 0, sizeof(*out));
-    StxBufs& B = c->stx[c->stx_next];
-    c->stx_next ^= 1;
+    const chip_kryo_registry reg = c->kreg;
     const uint64_t n1 = n + 1;
     HIPCHK(c, B.s_ncomp.ensure(n1 * 8));
     HIPCHK(c, B.s_nsig.ensure(n1 * 8));
@@ -813,7 +824,7 @@ int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_sta
     HIPCHK(c, B.s_temp.ensure(temp));
     // pass 1: validate + count; ranges = inclusive scans written one past a zero
     const int kc = c->kbegin(CHIP_K_STX, st);
-    launch_stx_count(st, in, tx_status, B.s_ncomp.as<uint64_t>(), B.s_nsig.as<uint64_t>(), B.s_nbytes.as<uint64_t>());
+    launch_stx_count(st, in, reg, tx_status, B.s_ncomp.as<uint64_t>(), B.s_nsig.as<uint64_t>(), B.s_nbytes.as<uint64_t>());
     HIPCHK(c, hipGetLastError());
     DevBuf* cnt[3] = {&B.s_ncomp, &B.s_nsig, &B.s_nbytes};
     DevBuf* rng[3] = {&B.s_cstart, &B.s_sstart, &B.s_pstart};
@@ -888,7 +899,7 @@ int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_sta
     d.key_off = B.s_koff.as<uint64_t>();
     d.key_len = B.s_klen.as<uint32_t>();
     // pass 2: the batches; then the signer keys interned
-    launch_stx_emit(st, in, tx_status, d);
+    launch_stx_emit(st, in, reg, tx_status, d);
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipMemsetAsync(B.s_tab.p, 0, cap * 8, st));
     HIPCHK(c, hipMemsetAsync(B.s_tabmin.p, 0xff, cap * 4, st));
@@ -897,12 +908,16 @@ int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_sta
     uint32_t nkeys = 0;
     if (nsig) HIPCHK(c, hipMemcpyAsync(&nkeys, B.s_kincl.as<uint32_t>() + nsig - 1, 4, hipMemcpyDeviceToHost, st));
     if (want_req) {
-        // requiredSigningKeys: the emit pass counted the signer entries; scan, R2 writes them with key
-        // indices + duplicate flags, scans, compaction into one leaf per distinct required key
+        // requiredSigningKeys: the emit pass counted the signer entries (commands' signers + the notary); scan;
+        // k_stx_required writes them with key indices, duplicate flags and what each needs validated;
+        // k_stx_req_entry counts every kept key's nodes (composite trees decoded) and key decodes; scans ->
+        // totals (one sync); then the nodes and decode requests are written, the keys decoded, failures
+        // applied to the statuses
         StxReq q{};
         HIPCHK(c, B.r_rstart.ensure(n1 * 8));
         HIPCHK(c, B.r_nreq.ensure(n1 * 8));
         HIPCHK(c, B.r_qstart.ensure(n1 * 8));
+        HIPCHK(c, B.r_tot.ensure(64));
         q.nraw = B.r_nraw.as<uint64_t>();
         q.raw_start = B.r_rstart.as<uint64_t>();
         q.nreq = B.r_nreq.as<uint64_t>();
@@ -912,10 +927,10 @@ int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_sta
         HIPCHK(c, hipMemcpyAsync(&nraw, q.raw_start + n, 8, hipMemcpyDeviceToHost, st));
         HIPCHK(c, hipStreamSynchronize(st));
         if (nraw >= (1ull << 31)) return fail(c, CHIP_E_ARG, "too many required keys");
-        for (DevBuf* b : {&B.r_kid, &B.r_len, &B.r_keep, &B.r_kincl, &B.r_val, &B.r_nk, &B.r_w})
+        for (DevBuf* b : {&B.r_kid, &B.r_len, &B.r_keep, &B.r_kincl, &B.r_flag, &B.r_tx, &B.r_nn, &B.r_nc, &B.r_ninc,
+                          &B.r_cinc})
             HIPCHK(c, b->ensure(nraw * 4 + 16));
         HIPCHK(c, B.r_off.ensure(nraw * 8 + 16));
-        HIPCHK(c, B.r_nstart.ensure(nraw * 8 + 16));
         if (stx_scan_temp_bytes(nraw > 2 ? nraw : 2) > B.s_temp.cap)
             HIPCHK(c, B.s_temp.ensure(stx_scan_temp_bytes(nraw > 2 ? nraw : 2)));
         q.raw_kid = B.r_kid.as<uint32_t>();
@@ -923,20 +938,59 @@ int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_sta
         q.raw_keep = B.r_keep.as<uint32_t>();
         q.keep_incl = B.r_kincl.as<uint32_t>();
         q.raw_off = B.r_off.as<uint64_t>();
+        q.raw_flag = B.r_flag.as<uint32_t>();
+        q.raw_tx = B.r_tx.as<uint32_t>();
+        q.raw_nnodes = B.r_nn.as<uint32_t>();
+        q.raw_ncheck = B.r_nc.as<uint32_t>();
+        q.node_incl = B.r_ninc.as<uint32_t>();
+        q.check_incl = B.r_cinc.as<uint32_t>();
+        launch_stx_required(st, n, tx_status, d, pool, cap - 1, reg, q);
+        HIPCHK(c, hipGetLastError());
+        launch_stx_req_entries(st, false, nraw, tx_status, d, cap - 1, q);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemsetAsync(B.r_qstart.p, 0, 8, st));
+        if (n) HIPCHK(c, stx_scan_u64(st, B.s_temp.p, B.s_temp.cap, q.nreq, B.r_qstart.as<uint64_t>() + 1, n));
+        uint32_t* tot32 = B.r_tot.as<uint32_t>();
+        HIPCHK(c, hipMemsetAsync(tot32, 0, 16, st));
+        if (nraw) {
+            HIPCHK(c, stx_scan_u32(st, B.s_temp.p, B.s_temp.cap, q.raw_keep, q.keep_incl, nraw));
+            HIPCHK(c, stx_scan_u32(st, B.s_temp.p, B.s_temp.cap, q.raw_nnodes, q.node_incl, nraw));
+            HIPCHK(c, stx_scan_u32(st, B.s_temp.p, B.s_temp.cap, q.raw_ncheck, q.check_incl, nraw));
+            HIPCHK(c, hipMemcpyAsync(tot32, q.node_incl + nraw - 1, 4, hipMemcpyDeviceToDevice, st));
+            HIPCHK(c, hipMemcpyAsync(tot32 + 1, q.check_incl + nraw - 1, 4, hipMemcpyDeviceToDevice, st));
+        }
+        uint64_t tot2[3] = {0, 0, 0};
+        HIPCHK(c, hipMemcpyAsync(&tot2[0], B.r_qstart.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipMemcpyAsync(&tot2[1], tot32, 8, hipMemcpyDeviceToHost, st));
+        HIPCHK(c, hipStreamSynchronize(st));
+        const uint64_t nreq = tot2[0];
+        const uint64_t nnodes = (uint32_t)tot2[1], nchk = tot2[1] >> 32;
+        HIPCHK(c, B.r_nstart.ensure(nreq * 8 + 16));
+        for (DevBuf* b : {&B.r_val, &B.r_nk, &B.r_w}) HIPCHK(c, b->ensure(nnodes * 4 + 16));
+        HIPCHK(c, B.k_off.ensure(nchk * 8 + 16));
+        HIPCHK(c, B.k_len.ensure(nchk * 4 + 16));
+        HIPCHK(c, B.k_tx.ensure(nchk * 4 + 16));
+        HIPCHK(c, B.k_kind.ensure(nchk + 16));
+        HIPCHK(c, B.k_ok.ensure(nchk + 16));
         q.node_start = B.r_nstart.as<uint64_t>();
         q.node_val = B.r_val.as<uint32_t>();
         q.node_nkids = B.r_nk.as<uint32_t>();
         q.node_weight = B.r_w.as<uint32_t>();
-        launch_stx_required(st, true, n, tx_status, d, pool, cap - 1, q);
-        HIPCHK(c, hipGetLastError());
-        HIPCHK(c, hipMemsetAsync(B.r_qstart.p, 0, 8, st));
-        if (n) HIPCHK(c, stx_scan_u64(st, B.s_temp.p, B.s_temp.cap, q.nreq, B.r_qstart.as<uint64_t>() + 1, n));
+        q.chk_off = B.k_off.as<uint64_t>();
+        q.chk_len = B.k_len.as<uint32_t>();
+        q.chk_tx = B.k_tx.as<uint32_t>();
+        q.chk_kind = B.k_kind.as<uint8_t>();
+        q.chk_ok = B.k_ok.as<uint8_t>();
         HIPCHK(c, hipMemsetAsync(q.node_start, 0, 8, st));
-        if (nraw) HIPCHK(c, stx_scan_u32(st, B.s_temp.p, B.s_temp.cap, q.raw_keep, q.keep_incl, nraw));
-        launch_stx_req_compact(st, nraw, q);
+        launch_stx_req_entries(st, true, nraw, tx_status, d, cap - 1, q);
         HIPCHK(c, hipGetLastError());
-        uint64_t nreq = 0;
-        HIPCHK(c, hipMemcpyAsync(&nreq, B.r_qstart.as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
+        if (nchk) {
+            HIPCHK(c, hipMemsetAsync(q.chk_ok, 0, nchk, st));
+            launch_ed25519_key_check(st, nchk, d.pool, q.chk_off, q.chk_len, q.chk_kind, q.chk_ok);
+            launch_ecdsa_key_check(st, nchk, d.pool, q.chk_off, q.chk_len, q.chk_kind, q.chk_ok);
+            launch_stx_check_apply(st, nchk, q.chk_ok, q.chk_tx, tx_status);
+            HIPCHK(c, hipGetLastError());
+        }
         c->kend(kc, st);
         HIPCHK(c, hipStreamSynchronize(st));
         chip_req_batch& rq = out->req;
@@ -946,7 +1000,7 @@ int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_sta
         rq.nreq = nreq;
         rq.node_start = q.node_start;
         rq.allowed = nullptr;
-        rq.n_nodes = nreq;
+        rq.n_nodes = nnodes;
         rq.node_val = q.node_val;
         rq.node_nkids = q.node_nkids;
         rq.node_weight = q.node_weight;
@@ -983,6 +1037,24 @@ int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_sta
     return CHIP_OK;
 }
 
+static int stx_args(chip_ctx* c, const chip_stx_blobs* in, const uint8_t* tx_status, const chip_stx_parsed* out) {
+    if (!c || !in || !out) return fail(c, CHIP_E_ARG, "null argument");
+    if (in->n && (!in->data || !in->off || !in->len || !tx_status)) return fail(c, CHIP_E_ARG, "null blob array");
+    if (in->n_meta && !in->meta) return fail(c, CHIP_E_ARG, "null meta");
+    if (in->n >= (1ull << 31)) return fail(c, CHIP_E_ARG, "too many blobs");
+    return CHIP_OK;
+}
+
+int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_status, chip_stx_parsed* out,
+                          void* stream) {
+    int r;
+    if ((r = stx_args(c, in, tx_status, out))) return r;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    StxBufs& B = c->stx[c->stx_next];
+    c->stx_next ^= 1;
+    return stx_parse(c, B, in, tx_status, out, stream ? (hipStream_t)stream : c->stream);
+}
+
 int chip_stx_verify(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t* off, const uint32_t* len,
                     uint64_t data_bytes, const chip_msg_templates* tmpl, const int32_t* meta, uint32_t n_meta,
                     uint8_t* tx_status, uint8_t* verdict, uint32_t* arg, uint8_t* ids) {
@@ -990,45 +1062,42 @@ int chip_stx_verify(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t
     if (!n) return CHIP_OK;
     if (!data || !off || !len || !tx_status || !verdict || !arg) return fail(c, CHIP_E_ARG, "null array");
     if (n_meta != tmpl->n) return fail(c, CHIP_E_ARG, "one SignatureMetadata per template");
+    if (n_meta && !meta) return fail(c, CHIP_E_ARG, "null meta");
     for (uint64_t t = 0; t < n; t++)
         if (off[t] + len[t] > data_bytes || off[t] + len[t] < off[t]) return fail(c, CHIP_E_ARG, "blob outside pool");
     for (uint64_t i = 0; i < tmpl->n; i++)
-        if (tmpl->off[i] + tmpl->len[i] > tmpl->data_bytes || tmpl->id_at[i] > tmpl->len[i])
-            return fail(c, CHIP_E_ARG, "template outside pool");
+        if (tmpl->off[i] + tmpl->len[i] > tmpl->data_bytes || tmpl->id_at[i] > tmpl->len[i] ||
+            tmpl->len[i] > tmpl->max_len)
+            return fail(c, CHIP_E_ARG, "template outside pool or longer than max_len");
     hipStream_t st = c->stream;
     chip_msg_templates dtm = *tmpl;
     int r;
-    {
-        std::lock_guard<std::mutex> g(c->mu);
-        HIPCHK(c, hipSetDevice(c->device));
-        if ((r = stage(c, c->h2_data, data, data_bytes, st)) || (r = stage(c, c->h2_off, off, n, st)) ||
-            (r = stage(c, c->h2_len, len, n, st)) || (r = stage(c, c->h2_td, tmpl->data, tmpl->data_bytes, st)) ||
-            (r = stage(c, c->h2_to, tmpl->off, tmpl->n, st)) || (r = stage(c, c->h2_tl, tmpl->len, tmpl->n, st)) ||
-            (r = stage(c, c->h2_ta, tmpl->id_at, tmpl->n, st)))
-            return r;
-        HIPCHK(c, c->h2_st.ensure(n + 16));
-        HIPCHK(c, c->h2_ids.ensure(n * 32 + 16));
-        HIPCHK(c, c->h2_v.ensure(n + 16));
-        HIPCHK(c, c->h2_a.ensure(n * 4 + 16));
-        dtm.data = c->h2_td.as<uint8_t>();
-        dtm.off = c->h2_to.as<uint64_t>();
-        dtm.len = c->h2_tl.as<uint32_t>();
-        dtm.id_at = c->h2_ta.as<uint32_t>();
-    }
+    // the whole call under the context lock (the entries it calls re-enter it), in a buffer set of its own
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    if ((r = stage(c, c->h2_data, data, data_bytes, st)) || (r = stage(c, c->h2_off, off, n, st)) ||
+        (r = stage(c, c->h2_len, len, n, st)) || (r = stage(c, c->h2_td, tmpl->data, tmpl->data_bytes, st)) ||
+        (r = stage(c, c->h2_to, tmpl->off, tmpl->n, st)) || (r = stage(c, c->h2_tl, tmpl->len, tmpl->n, st)) ||
+        (r = stage(c, c->h2_ta, tmpl->id_at, tmpl->n, st)))
+        return r;
+    HIPCHK(c, c->h2_st.ensure(n + 16));
+    HIPCHK(c, c->h2_ids.ensure(n * 32 + 16));
+    HIPCHK(c, c->h2_v.ensure(n + 16));
+    HIPCHK(c, c->h2_a.ensure(n * 4 + 16));
+    dtm.data = c->h2_td.as<uint8_t>();
+    dtm.off = c->h2_to.as<uint64_t>();
+    dtm.len = c->h2_tl.as<uint32_t>();
+    dtm.id_at = c->h2_ta.as<uint32_t>();
     chip_stx_blobs in{n, c->h2_data.as<uint8_t>(), c->h2_off.as<uint64_t>(), c->h2_len.as<uint32_t>(), data_bytes,
                       meta, n_meta, CHIP_STX_REQUIRED};
     chip_stx_parsed p;
-    if ((r = chip_stx_parse_device(c, &in, c->h2_st.as<uint8_t>(), &p, st))) return r;
-    {
-        std::lock_guard<std::mutex> g(c->mu);
-        HIPCHK(c, c->h2_sigst.ensure(p.sigs.n + 16));
-        HIPCHK(c, c->h2_miss.ensure(p.req.nreq + 16));
-    }
+    if ((r = stx_parse(c, c->stx[2], &in, c->h2_st.as<uint8_t>(), &p, st))) return r;
+    HIPCHK(c, c->h2_sigst.ensure(p.sigs.n + 16));
+    HIPCHK(c, c->h2_miss.ensure(p.req.nreq + 16));
     if ((r = chip_verify_signed_tx_batch_device(c, &p.txs, &dtm, &p.sigs, &p.req, c->h2_ids.as<uint8_t>(),
                                                 c->h2_sigst.as<uint8_t>(), c->h2_v.as<uint8_t>(),
                                                 c->h2_a.as<uint32_t>(), c->h2_miss.as<uint8_t>(), st)))
         return r;
-    std::lock_guard<std::mutex> g(c->mu);
     HIPCHK(c, hipMemcpyAsync(tx_status, c->h2_st.p, n, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipMemcpyAsync(verdict, c->h2_v.p, n, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipMemcpyAsync(arg, c->h2_a.p, n * 4, hipMemcpyDeviceToHost, st));
@@ -1039,7 +1108,7 @@ int chip_stx_verify(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t
 
 int chip_copy_to_host(chip_ctx* c, void* dst, const void* src, uint64_t bytes) {
     if (!c || (bytes && (!dst || !src))) return fail(c, CHIP_E_ARG, "null argument");
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, hipStreamSynchronize(c->stream));
     if (bytes) HIPCHK(c, hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
@@ -1049,7 +1118,7 @@ int chip_copy_to_host(chip_ctx* c, void* dst, const void* src, uint64_t bytes) {
 int chip_get_stats(const chip_ctx* cc, chip_stats* out) {
     if (!cc || !out) return CHIP_E_ARG;
     chip_ctx* c = const_cast<chip_ctx*>(cc);
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     float ms;
     if (c->ev_pending && hipEventQuery(c->ev1) == hipSuccess && hipEventElapsedTime(&ms, c->ev0, c->ev1) == hipSuccess) {
         c->stats.last_verify_kernel_ms = ms;
@@ -1066,7 +1135,7 @@ int chip_get_stats(const chip_ctx* cc, chip_stats* out) {
 
 int chip_reset_stats(chip_ctx* c) {
     if (!c) return CHIP_E_ARG;
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     c->kresolve_all();
     c->stats = chip_stats{};
     return CHIP_OK;
@@ -1091,7 +1160,7 @@ static int txid_device_locked(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids,
 
 int chip_txid_batch_device(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids, void* stream) {
     if (!c || !b || (!ids && b->ntx)) return fail(c, CHIP_E_ARG, "null argument");
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     return txid_device_locked(c, b, ids, stream ? (hipStream_t)stream : c->stream);
 }
 
@@ -1109,7 +1178,7 @@ int chip_txid_batch(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids) {
     hipStream_t st = c->stream;
     int r;
     {
-        std::lock_guard<std::mutex> g(c->mu);
+        std::lock_guard<std::recursive_mutex> g(c->mu);
         HIPCHK(c, hipSetDevice(c->device));
         if ((r = stage(c, c->t_salts, b->salts, ntx * 32, st)) ||
             (r = stage(c, c->t_start, b->tx_comp_start, ntx ? ntx + 1 : 0, st)) ||
@@ -1128,7 +1197,7 @@ int chip_txid_batch(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids) {
     d.comp_off = c->t_off.as<uint64_t>();
     d.comp_len = c->t_len.as<uint32_t>();
     if ((r = chip_txid_batch_device(c, &d, c->t_ids.as<uint8_t>(), st))) return r;
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     if (ntx) HIPCHK(c, hipMemcpyAsync(ids, c->t_ids.p, ntx * 32, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
     float ms = 0;
@@ -1187,7 +1256,7 @@ int chip_verify_tx_batch_device(chip_ctx* c, const chip_tx_batch* tb, const chip
                                 const chip_signer_batch* sb, uint8_t* ids, uint8_t* status, uint64_t* bitmap,
                                 void* stream) {
     if (!c || !tb || !tm || !sb || !status || (tb->ntx && !ids)) return fail(c, CHIP_E_ARG, "null argument");
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     return verify_tx_device_locked(c, tb, tm, sb, ids, status, bitmap, stream ? (hipStream_t)stream : c->stream);
 }
 
@@ -1224,7 +1293,7 @@ int chip_required_signers_device(chip_ctx* c, const chip_req_batch* q, const chi
     if (r) return r;
     if (q->ntx && (!verdict || !arg)) return fail(c, CHIP_E_ARG, "null verdict / arg");
     if (b->n && (!b->key_idx || !status)) return fail(c, CHIP_E_ARG, "null key_idx / status");
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     return required_device_locked(c, q, b->n, b->key_idx, nullptr, b->n_keys, b->key_data, b->key_off, b->key_len,
                                   b->key_bytes, status, verdict, arg, missing, stream ? (hipStream_t)stream : c->stream);
 }
@@ -1273,7 +1342,7 @@ int chip_required_signers(chip_ctx* c, const chip_req_batch* q, const chip_sig_b
     if (q->ntx && (!verdict || !arg)) return fail(c, CHIP_E_ARG, "null verdict / arg");
     if (n && (!b->key_idx || !status)) return fail(c, CHIP_E_ARG, "null key_idx / status");
     if (nk && (!b->key_data || !b->key_off || !b->key_len)) return fail(c, CHIP_E_ARG, "null key array");
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     hipStream_t st = c->stream;
     HIPCHK(c, hipSetDevice(c->device));
     chip_req_batch d;
@@ -1300,7 +1369,7 @@ int chip_verify_signed_tx_batch_device(chip_ctx* c, const chip_tx_batch* tb, con
     if (r) return r;
     if (q->ntx != tb->ntx) return fail(c, CHIP_E_ARG, "required-signer batch and tx batch differ in ntx");
     if (q->ntx && (!verdict || !arg)) return fail(c, CHIP_E_ARG, "null verdict / arg");
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     if ((r = verify_tx_device_locked(c, tb, tm, sb, ids, status, nullptr, st))) return r;
     return required_device_locked(c, q, sb->n, sb->key_idx, sb->tx_idx, sb->n_keys, sb->key_data, sb->key_off,
@@ -1334,7 +1403,7 @@ static int verify_tx_host(chip_ctx* c, const chip_tx_batch* b, const chip_msg_te
     }
     for (uint64_t k = 0; k < nk; k++)
         if (sb->key_off[k] + sb->key_len[k] > sb->key_bytes) return fail(c, CHIP_E_ARG, "key outside key pool");
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     hipStream_t st = c->stream;
     HIPCHK(c, hipSetDevice(c->device));
     int r;
@@ -1418,7 +1487,7 @@ int chip_verify_signed_tx_batch(chip_ctx* c, const chip_tx_batch* b, const chip_
 int chip_ftx_verify_batch_device(chip_ctx* c, const chip_ftx_batch* b, uint8_t* status, uint8_t* reason,
                                  void* stream) {
     if (!c || !b || (b->ntx && !status)) return fail(c, CHIP_E_ARG, "null argument");
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     hipStream_t st = stream ? (hipStream_t)stream : c->stream;
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, c->x_scratch.ensure(ftx_scratch_words(b->ntx) * 4 + 16));
@@ -1457,7 +1526,7 @@ int chip_ftx_verify_batch(chip_ctx* c, const chip_ftx_batch* b, uint8_t* status,
     hipStream_t st = c->stream;
     int r;
     {
-        std::lock_guard<std::mutex> g(c->mu);
+        std::lock_guard<std::recursive_mutex> g(c->mu);
         HIPCHK(c, hipSetDevice(c->device));
         if ((r = stage(c, c->x_ids, b->ids, ntx * 32, st)) || (r = stage(c, c->x_ghs, b->gh_start, ntx + 1, st)) ||
             (r = stage(c, c->x_gh, b->group_hashes, ngh * 32, st)) || (r = stage(c, c->x_fgs, b->fg_start, ntx + 1, st)) ||
@@ -1488,7 +1557,7 @@ int chip_ftx_verify_batch(chip_ctx* c, const chip_ftx_batch* b, uint8_t* status,
     d.pt_hash = c->x_pth.as<uint8_t>();
     d.check_visible = b->check_visible ? c->x_cv.as<int32_t>() : nullptr;
     if ((r = chip_ftx_verify_batch_device(c, &d, c->x_st.as<uint8_t>(), c->x_rs.as<uint8_t>(), st))) return r;
-    std::lock_guard<std::mutex> g(c->mu);
+    std::lock_guard<std::recursive_mutex> g(c->mu);
     HIPCHK(c, hipMemcpyAsync(status, c->x_st.p, ntx, hipMemcpyDeviceToHost, st));
     if (reason) HIPCHK(c, hipMemcpyAsync(reason, c->x_rs.p, ntx, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));

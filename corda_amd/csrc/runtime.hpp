@@ -41,11 +41,15 @@ void launch_ecdsa_comb_pre(hipStream_t st, int scheme, uint64_t n, const uint32_
 void launch_ecdsa_comb_inv(hipStream_t st, uint64_t n, const uint32_t* counts, uint32_t* wp_r1, uint32_t* wp_k1);
 // g and q run both curves in one grid (P-256 blocks first)
 void launch_ecdsa_comb_g(hipStream_t st, uint64_t n, const uint32_t* counts, const uint32_t* gcomb, uint32_t* mid_r1,
-                         uint32_t* mid_k1, const uint32_t* wp_r1, const uint32_t* wp_k1);
+                         uint32_t* mid_k1, const uint32_t* wp_r1, const uint32_t* wp_k1, bool park_all);
 // table_half 0: windows 0..31 of u2 (partial sum parked in mid); 1: windows 32..64 + the x(R) check
 void launch_ecdsa_comb_q(hipStream_t st, uint64_t n, const uint32_t* list_r1, const uint32_t* list_k1,
                          const uint32_t* counts, const chip_sig_batch* b, const uint32_t* ctab, uint32_t* mid_r1,
                          uint32_t* mid_k1, uint8_t* status, int table_half);
+// the lanes an exceptional addition (P == Q) parked in g / q: complete re-verification (both curves)
+void launch_ecdsa_comb_retry(hipStream_t st, uint64_t n, const uint32_t* list_r1, const uint32_t* list_k1,
+                             const uint32_t* counts, const chip_sig_batch* b, const uint32_t* ectab,
+                             const uint32_t* mid_r1, const uint32_t* mid_k1, uint8_t* status);
 
 void launch_txid(hipStream_t st, const chip_tx_batch* b, uint8_t* ids, uint32_t* scratch, uint64_t scratch_words);
 uint64_t ftx_scratch_words(uint64_t ntx);
@@ -80,26 +84,41 @@ struct StxOut {
     uint64_t* key_off;             // [n_keys]
     uint32_t* key_len;
 };
-void launch_stx_count(hipStream_t st, const chip_stx_blobs* in, uint8_t* status, uint64_t* ncomp, uint64_t* nsig,
-                      uint64_t* nextra);
-void launch_stx_emit(hipStream_t st, const chip_stx_blobs* in, uint8_t* status, const StxOut& d);
+void launch_stx_count(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_registry& reg, uint8_t* status,
+                      uint64_t* ncomp, uint64_t* nsig, uint64_t* nextra);
+void launch_stx_emit(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_registry& reg, uint8_t* status,
+                     const StxOut& d);
 size_t stx_scan_temp_bytes(uint64_t n);
 hipError_t stx_scan_u64(hipStream_t st, void* temp, size_t temp_bytes, const uint64_t* in, uint64_t* out, uint64_t n);
 void launch_stx_keys(hipStream_t st, uint64_t nsig, const StxOut& d, uint64_t mask, void* temp, size_t temp_bytes);
 // requiredSigningKeys from the command / notary components (after launch_stx_keys)
 struct StxReq {
-    uint64_t* nraw;         // [n] signer entries per tx (R1)
+    uint64_t* nraw;         // [n] signer entries per tx (counted by the emit pass)
     uint64_t* raw_start;    // [n + 1]
-    uint32_t *raw_kid, *raw_len, *raw_keep, *keep_incl;
+    uint32_t *raw_kid, *raw_len, *raw_keep, *raw_flag, *raw_tx, *keep_incl;
     uint64_t* raw_off;
-    uint64_t* nreq;         // [n] distinct required keys per tx (R2)
+    uint32_t *raw_nnodes, *raw_ncheck, *node_incl, *check_incl;   // per entry: nodes / key decodes (+ scans)
+    uint64_t* nreq;         // [n] distinct required keys per tx
     uint64_t* node_start;   // [nreq_total + 1]
     uint32_t *node_val, *node_nkids, *node_weight;
+    uint64_t* chk_off;      // key decode requests
+    uint32_t *chk_len, *chk_tx;
+    uint8_t *chk_kind, *chk_ok;
 };
-void launch_stx_required(hipStream_t st, bool emit, uint64_t n, uint8_t* status, const StxOut& d, uint64_t pool_bytes,
-                         uint64_t mask, const StxReq& q);
+void launch_stx_required(hipStream_t st, uint64_t n, uint8_t* status, const StxOut& d, uint64_t pool_bytes, uint64_t mask,
+                         const chip_kryo_registry& reg, const StxReq& q);
+void launch_stx_req_entries(hipStream_t st, bool emit, uint64_t nraw, uint8_t* status, const StxOut& d, uint64_t mask,
+                            const StxReq& q);
+void launch_stx_check_apply(hipStream_t st, uint64_t nchk, const uint8_t* ok, const uint32_t* chk_tx, uint8_t* status);
 hipError_t stx_scan_u32(hipStream_t st, void* temp, size_t temp_bytes, const uint32_t* in, uint32_t* out, uint64_t n);
-void launch_stx_req_compact(hipStream_t st, uint64_t nraw, const StxReq& q);
+// Crypto.decodePublicKey of SubjectPublicKeyInfo keys on the device: ok[i] = 1 when key i is an Ed25519
+// (ed25519.hip) / ECDSA r1 or k1 (ecdsa.hip) key whose point decodes — and, with kind[i] = 1, is in the
+// encoding its JVM key class re-encodes (Ed25519: canonical A; ECDSA: uncompressed); keys of the other
+// file's scheme are left as they are (ok zeroed by the caller)
+void launch_ed25519_key_check(hipStream_t st, uint64_t n, const uint8_t* pool, const uint64_t* off, const uint32_t* len,
+                              const uint8_t* kind, uint8_t* ok);
+void launch_ecdsa_key_check(hipStream_t st, uint64_t n, const uint8_t* pool, const uint64_t* off, const uint32_t* len,
+                            const uint8_t* kind, uint8_t* ok);
 
 // sizes of the per-key device tables (words per key)
 #define ED_KEY_TABLE_WORDS (9 * 40)

@@ -561,6 +561,7 @@ class Reader:
         self.names: Dict[int, str] = {}
         self.headers: Dict[str, List[str]] = {}
         self.reg = reg
+        self.bounds: List[int] = []      # a de-chunked field: where its chunks end
 
     def byte(self) -> int:
         if self.pos >= self.end:
@@ -623,14 +624,21 @@ class Reader:
 
     def chunk(self) -> "Reader":
         data = bytearray()
+        bounds = []
         while True:
             n = self.varint()
             if n == 0:
                 break
             data += self.take(n)
+            bounds.append(len(data))
         r = Reader(bytes(data), reg=self.reg)
         r.names, r.headers = self.names, self.headers   # one graph
+        r.bounds = bounds
         return r
+
+    def spans(self, n: int) -> bool:
+        """The next n bytes cross a chunk boundary of this (de-chunked) field."""
+        return any(self.pos < b < self.pos + n for b in self.bounds)
 
 
 def _header(buf: bytes, reg: Registry = DEFAULT_REGISTRY) -> Reader:
@@ -968,10 +976,15 @@ def party(owning_key: bytes, name: str = "O=Notary Service,L=Zurich,C=CH", key_c
 
 
 def _read_key_object(r: Reader) -> bytes:
+    """A command signer / the notary's owningKey.  The device reads these keys in place in the component:
+    one whose bytes cross a chunk boundary of their field is outside its grammar (the JVM path decides)."""
     if not _key_class_ok(r.reg, r.read_class()):
         raise KryoUnsupported("key class is not registered with PublicKeySerializer")
     r.not_null()
-    return r.take(r.varint())
+    n = r.varint()
+    if r.spans(n):
+        raise KryoUnsupported("key spans a chunk boundary")
+    return r.take(n)
 
 
 def command_signers(buf: bytes, reg: Registry = DEFAULT_REGISTRY) -> List[bytes]:

@@ -39,11 +39,25 @@ EXPORTS = ["chip_abi_version", "chip_device_count", "chip_init", "chip_shutdown"
            "chip_verify_tx_batch", "chip_verify_tx_batch_device", "chip_ftx_verify_batch",
            "chip_ftx_verify_batch_device", "chip_required_signers", "chip_required_signers_device",
            "chip_verify_signed_tx_batch", "chip_verify_signed_tx_batch_device",
-           "chip_stx_parse_device", "chip_stx_verify", "chip_copy_to_host", "chip_get_stats", "chip_reset_stats"]
+           "chip_stx_parse_device", "chip_stx_verify", "chip_set_kryo_registry", "chip_get_kryo_registry",
+           "chip_copy_to_host", "chip_get_stats", "chip_reset_stats"]
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
 u32p = ctypes.POINTER(ctypes.c_uint32)
 u64p = ctypes.POINTER(ctypes.c_uint64)
+
+
+class ChipKryoRegistry(ctypes.Structure):
+    """chip_kryo_registry: the Kryo class ids the front end depends on (corda_amd/kryo.py Registry)."""
+    _fields_ = [("arrays_aslist", ctypes.c_int32), ("signed_tx", ctypes.c_int32), ("wire_tx", ctypes.c_int32),
+                ("serialized_bytes", ctypes.c_int32), ("privacy_salt", ctypes.c_int32),
+                ("n_public_key", ctypes.c_uint32), ("public_key", ctypes.c_int32 * 8)]
+
+    @classmethod
+    def of(cls, reg) -> "ChipKryoRegistry":
+        ks = list(reg.public_key)[:8]
+        return cls(reg.arrays_aslist, reg.signed_tx, reg.wire_tx, reg.serialized_bytes, reg.privacy_salt, len(ks),
+                   (ctypes.c_int32 * 8)(*(ks + [0] * (8 - len(ks)))))
 
 
 class ChipConfig(ctypes.Structure):
@@ -159,7 +173,7 @@ class ChipConflict(ctypes.Structure):
  K_ED_PLAN, K_ED_COMB_B, K_EC_FRONT, K_REQ, K_STX) = range(15)
 (STX_OK, STX_KRYO, STX_NO_SIGS, STX_INVARIANT, STX_UNSUPPORTED) = range(5)
 N_KERNELS = 16
-FLAG_NO_COMB, FLAG_FORCE_COMB = 0x1, 0x2
+FLAG_NO_COMB, FLAG_FORCE_COMB, FLAG_EC_RETRY_ALL = 0x1, 0x2, 0x4
 
 
 class ChipStats(ctypes.Structure):
@@ -252,6 +266,8 @@ def load(build_if_missing: bool = False):
                                     ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ChipMsgTemplates),
                                     ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p, ctypes.c_void_p,
                                     ctypes.c_void_p, ctypes.c_void_p]
+    lib.chip_set_kryo_registry.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipKryoRegistry)]
+    lib.chip_get_kryo_registry.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipKryoRegistry)]
     lib.chip_copy_to_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
     lib.chip_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipStats)]
     lib.chip_reset_stats.argtypes = [ctypes.c_void_p]
@@ -466,6 +482,16 @@ class Context:
                                                    stream or None))
         out._meta = meta
         return out
+
+    def set_kryo_registry(self, reg) -> None:
+        """chip_set_kryo_registry from a corda_amd.kryo.Registry."""
+        r = ChipKryoRegistry.of(reg)
+        self._check(self.lib.chip_set_kryo_registry(self.h, ctypes.byref(r)))
+
+    def kryo_registry(self) -> ChipKryoRegistry:
+        r = ChipKryoRegistry()
+        self._check(self.lib.chip_get_kryo_registry(self.h, ctypes.byref(r)))
+        return r
 
     def stx_verify(self, data, off, lens, templates, meta, want_ids: bool = False):
         """Host arrays: SignedTransaction blobs -> (tx_status u8[n], verdict u8[n], arg u32[n], ids or None)

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define CHIP_ABI_VERSION 6
+#define CHIP_ABI_VERSION 7
 
 enum chip_sig_status {
     CHIP_VALID = 0,
@@ -81,6 +81,7 @@ typedef struct {
  * windowed Straus kernel.  Results are identical either way; the flags exist for tests/benchmarks. */
 #define CHIP_FLAG_NO_COMB 0x1u      /* every key on the Straus kernel                  */
 #define CHIP_FLAG_FORCE_COMB 0x2u   /* every key on the comb kernel (threshold 1)      */
+#define CHIP_FLAG_EC_RETRY_ALL 0x4u /* test: every ECDSA comb lane takes the exceptional-addition retry path */
 
 int chip_abi_version(void);
 int chip_device_count(void);
@@ -359,12 +360,23 @@ int chip_verify_signed_tx_batch_device(chip_ctx* ctx, const chip_tx_batch* txs, 
  * With CHIP_STX_REQUIRED the library also derives `req` on the device: WireTransaction.requiredSigningKeys
  * (WireTransaction.kt:66-75) = the signers of every Command component (Command.signers, read without the
  * command value) in first-appearance order, then the notary Party's owningKey when the transaction has
- * inputs or a time-window, without duplicates; each required key is one leaf (its index in out->sigs' key
- * pool, or CHIP_REQ_NO_SIGNER), req.sig_start = out->sig_start, allowed = NULL.  A command / notary
- * component outside the device grammar, a chunk-spanning key, more than 64 signer entries (commands' signers
- * + notary, before de-duplication) or a CompositeKey among the required keys
- * (its tree is not in the signer pool) turns the transaction's status into CHIP_STX_UNSUPPORTED.
- * Synchronises with `stream` twice (three times with CHIP_STX_REQUIRED): the totals size the outputs. */
+ * inputs or a time-window, without duplicates (equal encodings); req.sig_start = out->sig_start, allowed =
+ * NULL.  A plain key is one leaf (its index in out->sigs' key pool, or CHIP_REQ_NO_SIGNER); a CompositeKey
+ * is decoded on the device into its post-order tree (CompositeKey.kt:37-81,133-161: canonical DER only —
+ * minimal lengths and INTEGERs, children strictly ordered by (weight, encoding), >= 2 children, weights > 0
+ * with an Int sum, 0 < threshold <= total; leaves are canonical Ed25519 / ECDSA keys; <= 64 nodes, nesting
+ * < 8).  Every key the JVM would decode while deserialising (PublicKeySerializer -> Crypto.decodePublicKey,
+ * Kryo.kt:302-311) and the verify path does not decode anyway — a required key that signs none of the
+ * transaction's signatures, the notary's owningKey, composite leaves — is decoded on the device.  A command
+ * / notary component outside the device grammar, a Command with no signers (Structures.kt:183), a key
+ * spanning a chunk of its field, more than 64 signer entries (commands' signers + the required notary,
+ * before de-duplication), a key that is not an Ed25519 / ECDSA r1 / k1 key or a canonical CompositeKey, or
+ * one that does not decode turns the transaction's status into CHIP_STX_UNSUPPORTED (the JVM path decides).
+ * Class ids are those of the context's Kryo registry (chip_set_kryo_registry): a registered id other than
+ * the registry's where the position fixes the class is CHIP_STX_UNSUPPORTED (fail closed).  Inputs must be
+ * the canonical StateRef encoding (what a JVM writes; else CHIP_STX_UNSUPPORTED), so the duplicate-input
+ * check compares bytes.
+ * Synchronises with `stream` twice (four times with CHIP_STX_REQUIRED): the totals size the outputs. */
 enum chip_stx_status { CHIP_STX_OK = 0, CHIP_STX_KRYO = 1, CHIP_STX_NO_SIGS = 2, CHIP_STX_INVARIANT = 3,
                        CHIP_STX_UNSUPPORTED = 4 };
 typedef struct {
@@ -386,12 +398,30 @@ typedef struct {
 } chip_stx_parsed;
 int chip_stx_parse_device(chip_ctx* ctx, const chip_stx_blobs* in, uint8_t* tx_status, chip_stx_parsed* out,
                           void* stream);
+/* The Kryo class registrations the front end depends on (DefaultKryoCustomizer.kt:56-136): ids 10-13 are
+ * fixed by :77-80; PrivacySalt's and the PublicKeySerializer classes' ids follow the registration order of
+ * the deployment's Kryo / kryo-serializers / Guava versions, so a JVM binding passes its own
+ * (kryo.getRegistration(cls).id).  Defaults (chip_init): the restatement in corda_amd/kryo.py for
+ * kryo-serializers 0.41 + Guava 21.0 — arrays_aslist 10, signed_tx 11, wire_tx 12, serialized_bytes 13,
+ * privacy_salt 65, public_key {44 ECPublicKeyImpl, 45 EdDSAPublicKey, 47 CompositeKey, 58 BCECPublicKey,
+ * 60 BCRSAPublicKey, 62 BCSphincs256PublicKey}.  Applies to later chip_stx_* calls. */
+#define CHIP_KRYO_MAX_KEY_CLASSES 8
+typedef struct {
+    int32_t arrays_aslist, signed_tx, wire_tx, serialized_bytes;
+    int32_t privacy_salt;
+    uint32_t n_public_key;                          /* <= CHIP_KRYO_MAX_KEY_CLASSES */
+    int32_t public_key[CHIP_KRYO_MAX_KEY_CLASSES];  /* every id registered with PublicKeySerializer */
+} chip_kryo_registry;
+int chip_set_kryo_registry(chip_ctx* ctx, const chip_kryo_registry* reg);
+int chip_get_kryo_registry(chip_ctx* ctx, chip_kryo_registry* reg);
 /* Host entry of the whole path from bytes: n SignedTransaction blobs in host memory (pool + off/len) ->
  * chip_stx_parse_device with CHIP_STX_REQUIRED -> chip_verify_signed_tx_batch_device, blocking.  `tmpl`
  * (host) are the SignableData templates and meta[2i], meta[2i+1] the SignatureMetadata of template i.
  * Out (host): tx_status[n] (chip_stx_status; only CHIP_STX_OK transactions have a verdict), verdict[n] /
  * arg[n] (chip_tx_verdict as chip_verify_signed_tx_batch), ids[n * 32] (may be NULL).  This is what a JVM
- * binding calls with the SerializedBytes<SignedTransaction> of a batch (jni/BatchSignatureVerifier.kt). */
+ * binding calls with the SerializedBytes<SignedTransaction> of a batch (jni/BatchSignatureVerifier.kt).
+ * Holds the context for the whole call and parses into a buffer set of its own: it never invalidates the
+ * outputs of a chip_stx_parse_device call. */
 int chip_stx_verify(chip_ctx* ctx, uint64_t n, const uint8_t* data, const uint64_t* off, const uint32_t* len,
                     uint64_t data_bytes, const chip_msg_templates* tmpl, const int32_t* meta, uint32_t n_meta,
                     uint8_t* tx_status, uint8_t* verdict, uint32_t* arg, uint8_t* ids);

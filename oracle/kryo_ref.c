@@ -29,7 +29,8 @@
  * path decides it): back-references, > 8 class names per graph, other list / component classes, group
  * index >= 64, > 64 inputs, inputs that are not the canonical StateRef encoding, > 64 signer entries, keys
  * that are neither decodable Ed25519 / ECDSA keys nor canonical CompositeKeys (<= 64 nodes, nesting < 8),
- * non-ASCII class / field names, field names over 66 and class names over 202 characters.
+ * non-ASCII class / field names, field names over 66 and class names over 202 characters, a command signer
+ * or notary key whose bytes cross a chunk boundary of their field (the device reads those keys in place).
  *
  * PARITY UNPINNED for the bytes themselves (no JVM output exists in the reference or here); the grammar is
  * the restatement of corda_amd/kryo.py, pinned to this file and to the device by the tests.
@@ -69,6 +70,8 @@ typedef struct {
     int* err;
     graph* g;
     arena* a;
+    uint32_t bnd[64];   /* a de-chunked field: where its chunks end (nb > 64: more chunks than recorded) */
+    int nb;
 } rd;
 
 static void fail(rd* r, int e) {
@@ -170,6 +173,8 @@ static void not_null(rd* r) {
 static int chunk(rd* r, rd* out) {
     size_t start = r->a->used;
     size_t total = 0;
+    uint32_t bnd[64];
+    int nb = 0;
     for (;;) {
         uint32_t n = varint(r);
         if (*r->err) return 0;
@@ -183,12 +188,25 @@ static int chunk(rd* r, rd* out) {
         }
         memcpy(d, p, n);
         total += n;
+        if (nb < 64) bnd[nb] = (uint32_t)total;
+        nb++;
     }
     *out = *r;
     out->b = r->a->base + start;
     out->pos = 0;
     out->end = total;
+    out->nb = nb;
+    memcpy(out->bnd, bnd, sizeof bnd);
     return 1;
+}
+
+/* the n bytes at the reader's position cross a chunk boundary of its field (the device reads keys in place
+ * and hands such a key to the JVM path) */
+static int spans(const rd* f, uint32_t n) {
+    if (f->nb > 64) return 1;
+    for (int i = 0; i < f->nb; i++)
+        if (f->pos < f->bnd[i] && f->bnd[i] < f->pos + n) return 1;
+    return 0;
 }
 
 /* the field-name header, the first time the class is met in the graph */
@@ -451,7 +469,7 @@ static int stateref_canonical(const uint8_t* c, uint32_t len) {
     memset(&g, 0, sizeof g);
     uint8_t buf[512];
     arena a = {buf, 0, sizeof buf};
-    rd r = {c, 0, len, &err, &g, &a};
+    rd r = {c, 0, len, &err, &g, &a, {0}, 0};
     if (!header_ok(&r) || !is_name(&r, "net.corda.core.contracts.StateRef")) return 0;
     not_null(&r);
     fields(&r, "net.corda.core.contracts.StateRef", 2, STATEREF_F);
@@ -628,7 +646,7 @@ static int command_signers(const uint8_t* c, uint32_t len, const orc_kryo_regist
     size_t cap = 2 * (size_t)len + 64;
     uint8_t* buf = malloc(cap);
     arena a = {buf, 0, cap};
-    rd r = {c, 0, len, &err, &g, &a};
+    rd r = {c, 0, len, &err, &g, &a, {0}, 0};
     int ok = 0;
     if (header_ok(&r) && is_name(&r, "net.corda.core.contracts.Command")) {
         not_null(&r);
@@ -642,6 +660,7 @@ static int command_signers(const uint8_t* c, uint32_t len, const orc_kryo_regist
                 if (!err && !key_class_ok(reg, kc)) err = KU;
                 not_null(&f);
                 uint32_t kl = varint(&f);
+                if (!err && spans(&f, kl)) err = KU;
                 const uint8_t* kp = take(&f, kl);
                 if (err) break;
                 if (*ne >= 65) break;     /* more than 64 entries: counted, not kept */
@@ -664,7 +683,7 @@ static int party_key(const uint8_t* c, uint32_t len, const orc_kryo_registry* re
     size_t cap = 2 * (size_t)len + 64;
     uint8_t* buf = malloc(cap);
     arena a = {buf, 0, cap};
-    rd r = {c, 0, len, &err, &g, &a};
+    rd r = {c, 0, len, &err, &g, &a, {0}, 0};
     int ok = 0;
     if (header_ok(&r) && is_name(&r, "net.corda.core.identity.Party")) {
         not_null(&r);
@@ -675,6 +694,7 @@ static int party_key(const uint8_t* c, uint32_t len, const orc_kryo_registry* re
             if (!err && !key_class_ok(reg, kc)) err = KU;
             not_null(&f);
             uint32_t kl = varint(&f);
+            if (!err && spans(&f, kl)) err = KU;
             const uint8_t* kp = take(&f, kl);
             if (!err) {
                 uint8_t* keep = malloc(kl ? kl : 1);
@@ -815,7 +835,7 @@ size_t orc_stx_parse(const uint8_t* blob, size_t len, const orc_kryo_registry* r
     graph g;
     memset(&g, 0, sizeof g);
     g.refs = 1;
-    rd r = {blob, 0, len, &err, &g, &a};
+    rd r = {blob, 0, len, &err, &g, &a, {0}, 0};
     const uint8_t* txb = NULL;
     uint32_t txlen = 0;
     int st = S_OK;
@@ -828,7 +848,7 @@ size_t orc_stx_parse(const uint8_t* blob, size_t len, const orc_kryo_registry* r
         graph g2;
         memset(&g2, 0, sizeof g2);
         g2.refs = 1;
-        rd w = {txb, 0, txlen, &err2, &g2, &a};
+        rd w = {txb, 0, txlen, &err2, &g2, &a, {0}, 0};
         if (!wire_tx(&w, reg, &P)) {
             st = err2 == KE ? S_KRYO : S_UNSUP;
         } else if (invariant(&P, 0)) {

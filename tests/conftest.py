@@ -43,7 +43,9 @@ def ctx_modes():
     finally:
         del os.environ["CHIP_COMB_MIN_TOTAL"]
     cs = {"default": corda_amd.Context(0), "comb": corda_amd.Context(0, flags=native.FLAG_FORCE_COMB),
-          "straus": corda_amd.Context(0, flags=native.FLAG_NO_COMB), "ungated": ungated}
+          "straus": corda_amd.Context(0, flags=native.FLAG_NO_COMB), "ungated": ungated,
+          # every ECDSA comb lane finished by the exceptional-addition retry kernel (k_ecdsa_comb_retry)
+          "ec_retry": corda_amd.Context(0, flags=native.FLAG_FORCE_COMB | native.FLAG_EC_RETRY_ALL)}
     yield cs
     for c in cs.values():
         c.close()

@@ -205,7 +205,8 @@ def cases_required(seed: int = 13, n: int = 240):
     class, ECDSA keys incl. a compressed encoding) + the notary when there are inputs or a time-window;
     CompositeKey signers (flat, weighted, nested) decoded on the device; and what goes to the JVM path:
     a non-canonical / invalid composite, an undecodable key that signs nothing (also as the notary of a
-    transaction that does not need it), an empty signers list, a damaged command, > 64 signer entries."""
+    transaction that does not need it), an empty signers list, a damaged command, > 64 signer entries, a
+    signer key whose bytes cross a chunk boundary of the signers field."""
     rng = np.random.default_rng(seed)
     pool = [ed_key(rng) for _ in range(10)] + [ec_key(rng, 3), ec_key(rng, 2), ec_key(rng, 3, compressed=True)]
     comps = [composite([(pool[0], 1), (pool[1], 1)], 1),
@@ -252,6 +253,8 @@ def cases_required(seed: int = 13, n: int = 240):
                 groups.append((5, [rng.bytes(40)]))
         if i % 97 == 5:                                                     # > 64 signer entries
             cmds.append(K.command([pool[j % len(pool)] for j in range(70)], list_kind="array"))
+        if i % 89 == 7:                                                     # a signer key across a chunk boundary
+            cmds.append(K.command([pool[10]] * 14, list_kind="array"))
         req_all = [k for ss in signers_of_cmds for k in ss if not KS.is_composite(k)] + [notary_key]
         sig_keys = [req_all[int(rng.integers(0, len(req_all)))] for _ in range(int(rng.integers(1, 4)))]
         if kind < 0.10:                                                     # sign for a composite leaf

@@ -33,7 +33,7 @@ def test_library_exports_every_header_function():
 
 def test_abi_version_and_device_count():
     lib = corda_amd.load()
-    assert lib.chip_abi_version() == 6
+    assert lib.chip_abi_version() == 7
     assert lib.chip_device_count() >= 0
 
 
@@ -87,3 +87,17 @@ int main(void) {
     assert vals[2] == ctypes.sizeof(native.ChipConflict)
     assert vals[3] == ctypes.sizeof(native.ChipStats)
     assert vals[4] == native.ChipStats.kernel_ms_total.offset
+
+
+def test_kryo_registry_defaults_match_the_restatement():
+    """The registry defaults of cordahip.h / runtime.hip are the ids corda_amd/kryo.py derives from
+    DefaultKryoCustomizer.kt's registration order."""
+    from corda_amd import kryo as K
+    src = open(os.path.join(ROOT, "corda_amd", "csrc", "runtime.hip")).read()
+    m = re.search(r"chip_kryo_registry kreg\{(\d+), (\d+), (\d+), (\d+), (\d+), (\d+), \{([\d, ]+)\}\}", src)
+    vals = [int(x) for x in m.groups()[:6]]
+    keys = [int(x) for x in m.group(7).split(",")][:vals[5]]
+    r = K.DEFAULT_REGISTRY
+    assert vals[:5] == [r.arrays_aslist, r.signed_tx, r.wire_tx, r.serialized_bytes, r.privacy_salt]
+    assert keys == list(r.public_key)
+    assert ctypes.sizeof(native.ChipKryoRegistry) == 4 * 14

@@ -9,7 +9,7 @@ import golden_cases
 pytestmark = pytest.mark.gpu
 
 
-MODES = ["default", "comb", "straus", "ungated"]
+MODES = ["default", "comb", "straus", "ungated", "ec_retry"]
 
 
 @pytest.mark.parametrize("mode", MODES)

@@ -10,7 +10,7 @@ import golden_cases
 pytestmark = pytest.mark.gpu
 
 
-@pytest.mark.parametrize("mode", ["default", "comb", "straus", "ungated"])
+@pytest.mark.parametrize("mode", ["default", "comb", "straus", "ungated", "ec_retry"])
 def test_reference_x509_links_on_gpu(ctx_modes, oracle, mode):
     cases = golden_cases.ref_x509_cases(corrupt=True)
     b = golden_cases.sig_batch_from_cases([dict(c, expected=c["expected"] or 0) for c in cases])

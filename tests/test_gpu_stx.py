@@ -1,7 +1,8 @@
-"""GPU: the Kryo front end (chip_stx_parse_device, kryo.hip) against its host mirror (corda_amd/kryo.py).
+"""GPU: the Kryo front end (chip_stx_parse_device, kryo.hip) against the oracle (oracle/kryo_ref.c, an
+independent de-chunking restatement) and the host mirror (corda_amd/kryo.py).
 
 PARITY UNPINNED for the bytes themselves (no JVM output exists here: kryo.py restates Kryo 4.0.0); what
-these tests pin is that the device parse of every SignedTransaction equals the host mirror's — statuses
+these tests pin is that the device parse of every SignedTransaction equals the oracle's — statuses
 for each failure class, components (group, internal index, bytes), salts, signatures, signer keys,
 metadata -> template mapping, the first-occurrence key numbering — and that verifying a batch from its
 bytes gives the same ids, signature statuses and required-signer verdicts as the structured batch."""
@@ -10,6 +11,7 @@ import pytest
 import torch
 
 import cordagen as G
+import oracle_bind as O
 import stx_build as S
 from corda_amd import kryo as K
 from corda_amd import native
@@ -106,7 +108,8 @@ def test_verify_from_bytes_equals_structured_path(ctx):
     """cfg4-shaped batch: ids, signature statuses and required-signer verdicts from the parsed bytes
     equal those of the structured batch (chip_verify_signed_tx_batch_device on host-built arrays)."""
     ntx = 2000
-    tb, tm, sb, ids_ref, _ = G.cfg4_workload(ntx, n_keys=64, seed=0x5EED0104, threads=8)
+    # inputs must be canonical StateRefs for the front end: the Command / Party variant of the cfg4 shape
+    tb, tm, sb, ids_ref, _v, _a = G.cfg4_workload_commands(ntx, n_keys=64, seed=0x5EED0104, threads=8)
     q = G.cfg4_required(sb, ntx, 64, seed=0x5EED0106)
     data, off, ln = G.stx_uniform(tb, sb, 2)
     dd, doff, dlen = _dev(data), _dev(off), _dev(ln)
@@ -142,37 +145,142 @@ def test_verify_from_bytes_equals_structured_path(ctx):
 
 
 
-def test_required_keys_derived_on_device(ctx):
-    """CHIP_STX_REQUIRED: requiredSigningKeys read from the Command / notary Party components on the
-    device equal the host mirror (kryo.required_signing_keys): per transaction the distinct keys in
-    first-appearance order as leaves of the signer key pool (or NO_SIGNER), UNSUPPORTED for a
-    CompositeKey signer or a damaged command."""
-    blobs = S.cases_required(seed=13, n=300) + S.cases(seed=5, n_valid=40)
-    want, kid = S.expected_required(blobs)
+def device_records(ctx, blobs, required=False, metas=METAS):
+    """chip_stx_parse_device over `blobs` -> one record per blob in the shape of oracle_bind.stx_parse:
+    (status, groups, salt, [(sig, key, template index)], required key trees).  A leaf of a tree is its key's
+    bytes when the device gave it a signer-pool index (else None: CHIP_REQ_NO_SIGNER)."""
     data, off, ln = G.stx_blobs_from_lists(blobs)
+    if len(data) == 0:
+        data = np.zeros(1, np.uint8)
     dd, doff, dlen = _dev(data), _dev(off), _dev(ln)
-    st = torch.zeros(len(blobs), dtype=torch.uint8, device=DEV)
-    p = ctx.stx_parse_device(dd, doff, dlen, len(data), METAS, st, required=True)
+    st = torch.zeros(max(len(blobs), 1), dtype=torch.uint8, device=DEV)
+    p = ctx.stx_parse_device(dd, doff, dlen, len(data), metas, st[:len(blobs)], required=required)
     torch.cuda.synchronize()
-    got = st.cpu().numpy()
     n = len(blobs)
-    assert list(got) == [w[0] for w in want]
-    assert int((got == K.STX_UNSUPPORTED).sum()) >= 5 and int((got == K.STX_OK).sum()) > 250
+    st = st.cpu().numpy()[:n]
+    h = host(ctx, p, n)
+    pool = h["pool"]
+    keys = [pool[int(h["koff"][k]):int(h["koff"][k]) + int(h["klen"][k])].tobytes() for k in range(p.sigs.n_keys)]
     q = p.req
-    assert q.ntx == n and q.n_nodes == q.nreq and not q.allowed
-    rstart = ctx.copy_to_host(q.req_start, n + 1, np.uint64)
-    nstart = ctx.copy_to_host(q.node_start, q.nreq + 1, np.uint64)
-    val = ctx.copy_to_host(q.node_val, q.nreq, np.uint32)
-    nk = ctx.copy_to_host(q.node_nkids, q.nreq, np.uint32)
-    assert np.array_equal(nstart, np.arange(q.nreq + 1)) and not nk.any()
-    assert q.sig_start == p.sig_start
-    for t, (status, req) in enumerate(want):
-        r0, r1 = int(rstart[t]), int(rstart[t + 1])
-        if status != K.STX_OK:
-            assert r0 == r1, t
+    if required:
+        rstart = ctx.copy_to_host(q.req_start, n + 1, np.uint64)
+        nstart = ctx.copy_to_host(q.node_start, q.nreq + 1, np.uint64)
+        val = ctx.copy_to_host(q.node_val, q.n_nodes, np.uint32)
+        nk = ctx.copy_to_host(q.node_nkids, q.n_nodes, np.uint32)
+        w = ctx.copy_to_host(q.node_weight, q.n_nodes, np.uint32)
+    out = []
+    for t in range(n):
+        if st[t] != K.STX_OK:
+            out.append((int(st[t]), None, None, None, None))
             continue
-        exp = [kid.get(k, G.REQ_NO_SIGNER) for k in req]
-        assert list(val[r0:r1]) == exp, t
+        c0, c1 = int(h["cstart"][t]), int(h["cstart"][t + 1])
+        groups = []
+        for k in range(c0, c1):
+            o, l = int(h["coff"][k]), int(h["clen"][k])
+            c = pool[o:o + l].tobytes()
+            if int(h["internal"][k]) == 0:
+                groups.append((int(h["group"][k]), [c]))
+            else:
+                groups[-1][1].append(c)
+        s0, s1 = int(h["sstart"][t]), int(h["sstart"][t + 1])
+        sigs = []
+        for i in range(s0, s1):
+            o, l = int(h["soff"][i]), int(h["slen"][i])
+            assert int(h["tx_idx"][i]) == t
+            sigs.append((pool[o:o + l].tobytes(), keys[int(h["kidx"][i])], int(h["tmpl"][i])))
+        trees = None
+        if required:
+            trees = []
+            for r in range(int(rstart[t]), int(rstart[t + 1])):
+                tree = []
+                for j in range(int(nstart[r]), int(nstart[r + 1])):
+                    if nk[j] == 0:
+                        tree.append((None if val[j] == G.REQ_NO_SIGNER else keys[int(val[j])], 0, 0, int(w[j])))
+                    else:
+                        tree.append((None, int(val[j]), int(nk[j]), int(w[j])))
+                trees.append(tree)
+        out.append((int(st[t]), groups, h["salts"][t].tobytes(), sigs, trees))
+    return out, keys
+
+
+def assert_device_equals_oracle(ctx, blobs, required, reg=K.DEFAULT_REGISTRY):
+    """Device records == oracle/kryo_ref.c records for every blob (statuses, components, salts, signatures with
+    their template mapping, required-key trees with leaves resolved against the device's signer key pool)."""
+    dev, keys = device_records(ctx, blobs, required)
+    orc = O.stx_parse(blobs, reg, want_required=required)
+    pool_keys = set(keys)
+    metas = [tuple(m) for m in METAS]
+    for t, (d, o) in enumerate(zip(dev, orc)):
+        pst, fst, groups, salt, sigs, trees = o
+        want = fst if required else pst
+        assert d[0] == want, (t, d[0], want)
+        if want != K.STX_OK:
+            continue
+        assert d[1] == groups, t
+        assert d[2] == salt, t
+        exp_sigs = [(s, k, metas.index((pv, sch)) if (pv, sch) in metas else 0xFFFFFFFF) for s, k, pv, sch in sigs]
+        assert d[3] == exp_sigs, t
+        if required:
+            exp = [[((leaf if leaf in pool_keys else None) if nk == 0 else None, thr, nk, w) for leaf, thr, nk, w in tree]
+                   for tree in trees]
+            assert d[4] == exp, t
+    return dev, orc
+
+
+def test_required_keys_derived_on_device(ctx):
+    """CHIP_STX_REQUIRED: requiredSigningKeys read from the Command / notary Party components on the device
+    equal the oracle's (and the host mirror's): per transaction the distinct keys in first-appearance order,
+    plain keys as leaves of the signer key pool (or NO_SIGNER), CompositeKeys as their post-order trees;
+    UNSUPPORTED for an invalid / non-canonical composite, an undecodable key, a damaged command, an empty
+    signers list, > 64 signer entries."""
+    blobs = S.cases_required(seed=13, n=300) + S.cases(seed=5, n_valid=40)
+    dev, orc = assert_device_equals_oracle(ctx, blobs, required=True)
+    want, _ = S.expected_required(blobs)
+    assert [d[0] for d in dev] == [w[0] for w in want]
+    got = np.array([d[0] for d in dev])
+    assert int((got == K.STX_UNSUPPORTED).sum()) >= 20 and int((got == K.STX_OK).sum()) > 250
+    assert sum(1 for d in dev if d[0] == 0 and any(len(t) > 1 for t in d[4])) >= 20   # composite trees on device
+
+
+@pytest.mark.parametrize("required", [False, True])
+def test_device_equals_oracle_on_cases(ctx, required):
+    blobs = S.cases(seed=7, n_valid=200) + S.cases_required(seed=21, n=200)
+    dev, _ = assert_device_equals_oracle(ctx, blobs, required)
+    assert {d[0] for d in dev} == {0, 1, 2, 3, 4}
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_device_equals_oracle_on_damaged_blobs(ctx, seed):
+    """Fuzzed blobs (bit flips, byte changes, insertions, deletions, truncations of valid ones): the device's
+    status and outputs equal the oracle's for every one, with and without the required-key stage."""
+    base = S.cases(seed=7 + seed, n_valid=40)[:40] + S.cases_required(seed=13 + seed, n=80)
+    blobs = S.mutants(base, seed=seed, n=4000)
+    for required in (False, True):
+        assert_device_equals_oracle(ctx, blobs, required)
+
+
+def test_registry_is_applied(ctx):
+    """chip_set_kryo_registry: blobs written with another deployment's ids parse under that registry and fail
+    closed (UNSUPPORTED) under the defaults, on the device as in the oracle."""
+    ids = K.registration_ids(K.REGISTRATION_ORDER[:20] + [("x.Extra", "")] + K.REGISTRATION_ORDER[20:])
+    other = K.Registry(ids)
+    rng = np.random.default_rng(4)
+    keys = S.key_pool(rng)
+    blobs = []
+    for _ in range(30):
+        groups, salt, sigs, kinds, skind = S.random_valid(rng, keys)
+        sigs = [K.Sig(s.sig, s.key, s.platform_version, s.scheme_number_id,
+                      other.eddsa_public_key if len(s.key) == 44 else other.bcec_public_key) for s in sigs]
+        blobs.append(K.signed_transaction(K.wire_transaction(groups, salt, other.privacy_salt, kinds), sigs, skind))
+    assert [d[0] for d in device_records(ctx, blobs)[0]] == [4] * 30
+    ctx.set_kryo_registry(other)
+    try:
+        assert tuple(ctx.kryo_registry().public_key)[:6] == tuple(other.public_key)[:6]
+        assert_device_equals_oracle(ctx, blobs, required=False, reg=other)
+        assert [d[0] for d in device_records(ctx, blobs)[0]] == [0] * 30
+    finally:
+        ctx.set_kryo_registry(K.DEFAULT_REGISTRY)
+    assert ctx.kryo_registry().privacy_salt == K.DEFAULT_REGISTRY.privacy_salt
 
 
 def test_verify_from_bytes_with_derived_required_keys(ctx):
