@@ -54,9 +54,55 @@ __constant__ char k_fields[11][48] = {"OpaqueBytes.bytes", "TransactionSignature
                                       "ComponentGroup.groupIndex", "Command.signers", "Command.value",
                                       "AbstractParty.owningKey", "Party.name"};
 __constant__ uint8_t k_field_len[11] = {17, 23, 38, 33, 32, 25, 25, 15, 13, 23, 10};
+// the same strings as Output.writeString writes them (ASCII form: bit 7 set on the last character), packed in
+// little-endian dwords for the cursor's fast compare (a name that lies inside one chunk is compared 4 bytes at a
+// time instead of through the byte path)
+struct Enc {
+    uint32_t w[12];
+    uint32_t n;
+};
+constexpr Enc enc(const char* s) {
+    Enc e{};
+    uint32_t n = 0;
+    while (s[n]) n++;
+    for (uint32_t i = 0; i < n; i++) {
+        const uint32_t c = (uint8_t)s[i] | (i + 1 == n ? 0x80u : 0u);
+        e.w[i / 4] |= c << (8 * (i % 4));
+    }
+    e.n = n;
+    return e;
+}
+__constant__ Enc k_name_enc[N_NAMES] = {enc("java.util.ArrayList"), enc("java.util.Collections$SingletonList"),
+                                        enc("net.corda.core.crypto.TransactionSignature"),
+                                        enc("net.corda.core.transactions.ComponentGroup"),
+                                        enc("net.corda.core.contracts.Command"), enc("net.corda.core.identity.Party")};
+__constant__ Enc k_field_enc[11] = {enc("OpaqueBytes.bytes"), enc("TransactionSignature.by"),
+                                    enc("TransactionSignature.signatureMetadata"),
+                                    enc("SignatureMetadata.platformVersion"), enc("SignatureMetadata.schemeNumberID"),
+                                    enc("ComponentGroup.components"), enc("ComponentGroup.groupIndex"),
+                                    enc("Command.signers"), enc("Command.value"), enc("AbstractParty.owningKey"),
+                                    enc("Party.name")};
+#define M_LIST ((1u << (C_ARRAYLIST - 1)) | (1u << (C_SINGLETON - 1)))
+#define M_OF(code) (1u << ((code) - 1))
+
 // DER of the CompositeKey algorithm OID 2.25.30086077608615255153862931087626791002 (CompositeKey.kt)
 __constant__ uint8_t k_composite_oid[21] = {0x06, 0x13, 0x69, 0xad, 0xa2, 0xaf, 0x89, 0xd5, 0xb8, 0xe2, 0xaf,
                                             0xf3, 0x8d, 0x93, 0xac, 0x9d, 0xe6, 0x96, 0x9b, 0xd0, 0x5a};
+
+// 4 bytes at any offset of the pool (two aligned loads + byte funnel; the pool has >= 8 bytes of slack)
+__device__ __forceinline__ uint32_t ld32u(const uint8_t* pool, uint64_t off) {
+    const uint64_t a = off & ~3ull;
+    const uint32_t lo = *reinterpret_cast<const uint32_t*>(pool + a);
+    const uint32_t hi = *reinterpret_cast<const uint32_t*>(pool + a + 4);
+    return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(off & 3));
+}
+__device__ __forceinline__ uint32_t tail_mask(uint32_t left) { return left >= 4 ? ~0u : (1u << (8 * left)) - 1; }
+// pool[at, at + n) == the packed bytes w (n <= 4 * words of w)
+__device__ __forceinline__ bool eq_packed(const uint8_t* pool, uint64_t at, const uint32_t* w, uint32_t n) {
+    bool ok = true;
+    for (uint32_t i = 0; i < n; i += 4) ok &= ((ld32u(pool, at + i) ^ w[i >> 2]) & tail_mask(n - i)) == 0;
+    return ok;
+}
 
 struct Sink {   // dword-accumulating byte writer into the output pool
     uint8_t* base;
@@ -75,12 +121,23 @@ struct Sink {   // dword-accumulating byte writer into the output pool
     }
 };
 
+// A lane's read windows: 16 bytes in registers (the byte extraction is a 4-way select), refilled from a
+// KRYO_WIN-byte window in LDS (one ds_read_b128), refilled from the pool with KRYO_WIN / 16 independent 16-byte
+// loads.  The parse is a chain of dependent loads per lane: a KRYO_WIN window is one global round trip where
+// 16-byte windows took KRYO_WIN / 16, and fetches its lines once (a lane's next 16 bytes were rarely still in
+// L1 / L2: every lane streams its own blob).  LDS layout: row k of lane t at win[k * KRYO_BLOCK + t].
+#ifndef KRYO_WIN
+#define KRYO_WIN 128
+#endif
+#define KRYO_BLOCK 256
+#define KRYO_ROWS (KRYO_WIN / 16)
 // Input over one graph's bytes [pos, end) of the pool with up to two levels of InputChunked on top.
 struct Cur {
     const uint8_t* pool;
     uint64_t pool_bytes, pos, end;
-    uint64_t widx;
+    uint64_t widx, lidx;
     uint4 w;
+    uint4* lw;   // this lane's LDS window (rows KRYO_BLOCK apart)
     uint32_t rem1, rem2;
     int err;
     // class-name ids of this graph (4 bits each) and the CompatibleFieldSerializer headers already read
@@ -93,8 +150,7 @@ struct Cur {
         pool_bytes = pb;
         pos = a;
         end = b;
-        widx = ~0ull;
-        w = make_uint4(0, 0, 0, 0);
+        widx = lidx = ~0ull;
         rem1 = rem2 = 0;
         err = E_OK;
         names = nnames = headers = 0;
@@ -102,19 +158,34 @@ struct Cur {
     __device__ __forceinline__ void fail(int e) {
         if (err == E_OK) err = e;
     }
+    __device__ __forceinline__ void window(uint4* lds_lane) {
+        lw = lds_lane;
+        lidx = ~0ull;
+    }
     __device__ __forceinline__ uint8_t raw() {
         if (pos >= end) {
             fail(E_KRYO);
             return 0;
         }
-        const uint64_t wi = pos >> 4;   // a 16-byte window per lane: one global_load_dwordx4 per 16 bytes
+        const uint64_t wi = pos >> 4;
         if (wi != widx) {
-            if ((wi << 4) + 16 <= pool_bytes) {
-                w = *reinterpret_cast<const uint4*>(pool + (wi << 4));
-                widx = wi;
-            } else {
-                return pool[pos++];
+            const uint64_t li = pos / KRYO_WIN;
+            if (li != lidx) {
+                if ((li + 1) * KRYO_WIN > pool_bytes) return pool[pos++];   // the pool's tail: byte loads
+                // LDS-DMA (global_load_lds_dwordx4): no VGPR destinations; row k of the wave's lanes lands at
+                // the wave-uniform base + lane * 16, i.e. at lw[k * KRYO_BLOCK] for every lane
+                const uint4* src = reinterpret_cast<const uint4*>(pool + li * KRYO_WIN);
+                uint4* wave_base = lw - (threadIdx.x & 63);
+#pragma unroll
+                for (int k = 0; k < KRYO_ROWS; k++)
+                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + k),
+                                                     (__attribute__((address_space(3))) void*)(wave_base + k * KRYO_BLOCK),
+                                                     16, 0, 0);
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                lidx = li;
             }
+            w = lw[((uint32_t)(pos % KRYO_WIN) >> 4) * KRYO_BLOCK];
+            widx = wi;
         }
         const uint32_t q = (pos >> 2) & 3;
         const uint32_t d = q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w;
@@ -197,8 +268,37 @@ struct Cur {
             }
         }
     }
+    // The next n bytes at level L as one run of the pool, not consumed: true (with `at`) when they lie inside the
+    // current chunk and 8 bytes before the end of the pool (the dword compares read up to 7 bytes ahead); a
+    // level-1 chunk header due first is read, exactly as byte<1>() would.  False: take the byte path.
+    template <int L> __device__ __forceinline__ bool contig(uint32_t n, uint64_t& at) {
+        if (err || L > 1) return false;
+        if (L == 1 && rem1 == 0 && n) {
+            rem1 = varint<0>();
+            if (err) return false;
+            if (rem1 == 0) {
+                fail(E_KRYO);
+                return false;
+            }
+        }
+        if ((L == 1 && n > rem1) || end - pos < n || pos + n + 8 > pool_bytes) return false;
+        at = pos;
+        return true;
+    }
+    template <int L> __device__ __forceinline__ void advance(uint32_t n) {
+        pos += n;
+        if (L == 1) rem1 -= n;
+    }
+    // the next bytes are exactly the encoded string e (consumed); false: nothing consumed
+    template <int L> __device__ __forceinline__ bool take_enc(const Enc& e) {
+        uint64_t at;
+        if (!contig<L>(e.n, at) || !eq_packed(pool, at, e.w, e.n)) return false;
+        advance<L>(e.n);
+        return true;
+    }
     // Input.readString compared against one expected ASCII string (field names)
-    template <int L> __device__ __forceinline__ bool string_is(const char* s, uint32_t len) {
+    template <int L> __device__ __forceinline__ bool string_is(const char* s, uint32_t len, const Enc& e) {
+        if (take_enc<L>(e)) return true;
         bool ok = true;
         for (uint32_t i = 0;; i++) {
             const uint8_t b = byte<L>();
@@ -216,8 +316,11 @@ struct Cur {
             }
         }
     }
-    // a class name read as a string: one of k_names (C_ARRAYLIST ..) or C_OTHER
-    template <int L> __device__ __forceinline__ int class_name() {
+    // a class name read as a string: one of k_names (C_ARRAYLIST ..) or C_OTHER; the names in `expect` (bit
+    // code - 1) are tried first with the fast compare
+    template <int L> __device__ __forceinline__ int class_name(uint32_t expect) {
+        for (int c = 0; c < N_NAMES; c++)
+            if ((expect >> c & 1) && take_enc<L>(k_name_enc[c])) return C_ARRAYLIST + c;
         uint32_t cand = (1u << N_NAMES) - 1;
         for (uint32_t i = 0;; i++) {
             const uint8_t b = byte<L>();
@@ -241,7 +344,7 @@ struct Cur {
         }
     }
     // DefaultClassResolver.readClass: >= 0 registered id, -(code) for a class by name, -100 null
-    template <int L> __device__ __forceinline__ int read_class() {
+    template <int L> __device__ __forceinline__ int read_class(uint32_t expect = 0) {
         const uint32_t tag = varint<L>();
         if (err) return -100;
         if (tag == 0) return -100;
@@ -253,7 +356,7 @@ struct Cur {
             fail(E_UNSUP);
             return -100;
         }
-        const int code = class_name<L>();
+        const int code = class_name<L>(expect);
         names |= (uint32_t)code << (4 * nid);
         nnames++;
         return -code;
@@ -270,11 +373,11 @@ struct Cur {
             return;
         }
         for (int f = 0; f < count && !err; f++)
-            if (!string_is<L>(k_fields[first + f], k_field_len[first + f])) fail(E_UNSUP);
+            if (!string_is<L>(k_fields[first + f], k_field_len[first + f], k_field_enc[first + f])) fail(E_UNSUP);
     }
     // a list class + size: ArrayList / SingletonList / Arrays$ArrayList (with its component class)
     template <int L> __device__ __forceinline__ uint32_t list(bool refs, int32_t aslist) {
-        const int c = read_class<L>();
+        const int c = read_class<L>(M_LIST);
         if (err) return 0;
         if (refs) not_null<L>();
         if (c == -C_SINGLETON) return 1;
@@ -324,25 +427,37 @@ __device__ __forceinline__ bool key_class_ok(const chip_kryo_registry& reg, int 
 
 // The canonical StateRef encoding (kryo.state_ref, oracle stateref_enc): 74 fixed bytes, varint(zn), the
 // zig-zag index in zn minimal varint bytes, 65 fixed bytes, the 32-byte txhash, 01 00 00; 175 + zn bytes.
-__constant__ uint8_t k_sr_pre[74] = {
+constexpr uint8_t SR_PRE[74] = {
     0x63, 0x6f, 0x72, 0x64, 0x61, 0x00, 0x00, 0x01, 0x01, 0x00, 0x6e, 0x65, 0x74, 0x2e, 0x63, 0x6f, 0x72, 0x64, 0x61,
     0x2e, 0x63, 0x6f, 0x72, 0x65, 0x2e, 0x63, 0x6f, 0x6e, 0x74, 0x72, 0x61, 0x63, 0x74, 0x73, 0x2e, 0x53, 0x74, 0x61,
     0x74, 0x65, 0x52, 0x65, 0xe6, 0x01, 0x02, 0x53, 0x74, 0x61, 0x74, 0x65, 0x52, 0x65, 0x66, 0x2e, 0x69, 0x6e, 0x64,
     0x65, 0xf8, 0x53, 0x74, 0x61, 0x74, 0x65, 0x52, 0x65, 0x66, 0x2e, 0x74, 0x78, 0x68, 0x61, 0x73, 0xe8};
-__constant__ uint8_t k_sr_mid[65] = {
+constexpr uint8_t SR_MID[65] = {
     0x00, 0x5f, 0x01, 0x01, 0x6e, 0x65, 0x74, 0x2e, 0x63, 0x6f, 0x72, 0x64, 0x61, 0x2e, 0x63, 0x6f, 0x72, 0x65, 0x2e,
     0x63, 0x72, 0x79, 0x70, 0x74, 0x6f, 0x2e, 0x53, 0x65, 0x63, 0x75, 0x72, 0x65, 0x48, 0x61, 0x73, 0x68, 0x24, 0x53,
     0x48, 0x41, 0x32, 0x35, 0xb6, 0x01, 0x01, 0x4f, 0x70, 0x61, 0x71, 0x75, 0x65, 0x42, 0x79, 0x74, 0x65, 0x73, 0x2e,
     0x62, 0x79, 0x74, 0x65, 0xf3, 0x22, 0x01, 0x21};
-
-// 4 bytes at any offset of the pool (two aligned loads + byte funnel; the pool has >= 8 bytes of slack)
-__device__ __forceinline__ uint32_t ld32u(const uint8_t* pool, uint64_t off) {
-    const uint64_t a = off & ~3ull;
-    const uint32_t lo = *reinterpret_cast<const uint32_t*>(pool + a);
-    const uint32_t hi = *reinterpret_cast<const uint32_t*>(pool + a + 4);
-    return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(off & 3));
+struct Packed80 {
+    uint32_t w[20];
+};
+template <uint32_t N> constexpr Packed80 pack(const uint8_t (&b)[N]) {
+    Packed80 p{};
+    for (uint32_t i = 0; i < N; i++) p.w[i / 4] |= (uint32_t)b[i] << (8 * (i % 4));
+    return p;
 }
-__device__ __forceinline__ uint32_t tail_mask(uint32_t left) { return left >= 4 ? ~0u : (1u << (8 * left)) - 1; }
+__constant__ Packed80 k_sr_pre_w = pack(SR_PRE);
+__constant__ Packed80 k_sr_mid_w = pack(SR_MID);
+template <uint32_t N> struct Bytes {
+    uint8_t b[N];
+};
+template <uint32_t N> constexpr Bytes<N> bytes_of(const uint8_t (&a)[N]) {
+    Bytes<N> r{};
+    for (uint32_t i = 0; i < N; i++) r.b[i] = a[i];
+    return r;
+}
+__constant__ Bytes<74> k_sr_pre = bytes_of(SR_PRE);
+__constant__ Bytes<65> k_sr_mid = bytes_of(SR_MID);
+
 __device__ __forceinline__ bool key_eq(const uint8_t* pool, uint64_t a, uint32_t la, uint64_t b, uint32_t lb) {
     if (la != lb) return false;
     for (uint32_t i = 0; i < la; i += 4)
@@ -433,12 +548,27 @@ __device__ __forceinline__ bool stateref_canonical(Cur& c, uint32_t n) {
         return false;
     }
     const uint32_t zn = n - 175;
+    uint64_t at;
+    if (c.contig<1>(n, at)) {   // inside one chunk: dword compares
+        bool ok = eq_packed(c.pool, at, k_sr_pre_w.w, 74) && c.pool[at + 74] == zn &&
+                  eq_packed(c.pool, at + 75 + zn, k_sr_mid_w.w, 65) && (ld32u(c.pool, at + n - 3) & 0xffffffu) == 1u;
+        uint32_t last = 0;
+        for (uint32_t i = 0; i < zn; i++) {   // the index varint: minimal, at most 32 bits
+            const uint32_t b = c.pool[at + 75 + i];
+            ok &= i + 1 == zn ? !(b & 0x80) : (b & 0x80) != 0;
+            last = b;
+        }
+        if (zn > 1) ok &= last != 0;
+        if (zn == 5) ok &= last <= 0x0f;
+        c.advance<1>(n);
+        return ok;
+    }
     bool ok = true;
     uint32_t last = 0;
     for (uint32_t i = 0; i < n && !c.err; i++) {
         const uint8_t b = c.byte<1>();
         if (i < 74) {
-            ok &= b == k_sr_pre[i];
+            ok &= b == k_sr_pre.b[i];
         } else if (i == 74) {
             ok &= b == zn;
         } else if (i < 75 + zn) {                 // the index varint: minimal, at most 32 bits
@@ -446,7 +576,7 @@ __device__ __forceinline__ bool stateref_canonical(Cur& c, uint32_t n) {
             ok &= lastb ? !(b & 0x80) : (b & 0x80) != 0;
             last = b;
         } else if (i < 140 + zn) {
-            ok &= b == k_sr_mid[i - 75 - zn];
+            ok &= b == k_sr_mid.b[i - 75 - zn];
         } else if (i >= 172 + zn) {
             ok &= b == (i == 172 + zn ? 1 : 0);
         }
@@ -457,6 +587,12 @@ __device__ __forceinline__ bool stateref_canonical(Cur& c, uint32_t n) {
 }
 
 __device__ __forceinline__ bool header_ok(Cur& c) {
+    uint64_t at;
+    if (c.contig<0>(8, at)) {   // "corda" 00 00 01
+        const bool ok = ld32u(c.pool, at) == 0x64726f63u && ld32u(c.pool, at + 4) == 0x01000061u;
+        c.advance<0>(8);
+        return ok;
+    }
     const uint8_t h[8] = {'c', 'o', 'r', 'd', 'a', 0, 0, 1};
     for (int i = 0; i < 8; i++)
         if (c.byte<0>() != h[i]) return false;
@@ -496,7 +632,8 @@ __device__ __forceinline__ bool req_walk(Cur& c, const uint8_t* pool, uint64_t p
         c.init(pool, pool_bytes, a, a + comp_len[kk]);
         if (!header_ok(c)) return false;
         const bool is_cmd = k < c1;
-        if (c.read_class<0>() != (is_cmd ? -C_COMMAND : -C_PARTY)) c.fail(E_UNSUP);
+        if (c.read_class<0>(is_cmd ? M_OF(C_COMMAND) : M_OF(C_PARTY)) != (is_cmd ? -C_COMMAND : -C_PARTY))
+            c.fail(E_UNSUP);
         c.not_null<0>();
         if (is_cmd) c.header<0>(H_CMD, 7, 2);
         else c.header<0>(H_PARTY, 9, 2);
@@ -541,7 +678,7 @@ struct Outs {   // pass-2 destinations (NULL in pass 1)
 };
 
 template <bool EMIT>
-__global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __restrict__ data,
+__global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint8_t* __restrict__ data,
                                                    const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
                                                    uint64_t data_bytes, uint8_t* __restrict__ status,
                                                    uint64_t* __restrict__ ncomp, uint64_t* __restrict__ nsig,
@@ -557,7 +694,9 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
     Sink sink{o.pool, EMIT ? o.extra_base + o.extra_start[t] : 0, 0};
     uint64_t cbase = EMIT ? o.comp_start[t] : 0, sbase = EMIT ? o.sig_start[t] : 0;
     int st = CHIP_STX_OK;
+    __shared__ uint4 s_win[KRYO_ROWS * KRYO_BLOCK];
     Cur c;
+    c.window(s_win + threadIdx.x);
     c.init(data, data_bytes, a, b);
     uint64_t tx_a = 0, tx_b = 0;
     // ---- SignedTransaction (references on) ----
@@ -578,7 +717,7 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
     {
         const uint32_t ns = c.list<0>(true, o.reg.arrays_aslist);
         for (uint32_t i = 0; i < ns && !c.err; i++) {
-            if (c.read_class<0>() != -C_TXSIG) {
+            if (c.read_class<0>(M_OF(C_TXSIG)) != -C_TXSIG) {
                 c.fail(E_UNSUP);
                 break;
             }
@@ -657,7 +796,7 @@ __global__ void __launch_bounds__(256) k_stx_parse(uint64_t n, const uint8_t* __
         bool empty_group = false, dup_group = false, multi = false, noncanon = false;
         uint64_t in_first = 0, in_count = 0;
         for (uint32_t g = 0; g < ng && !w.err; g++) {
-            if (w.read_class<0>() != -C_GROUP) {
+            if (w.read_class<0>(M_OF(C_GROUP)) != -C_GROUP) {
                 w.fail(E_UNSUP);
                 break;
             }
@@ -937,7 +1076,7 @@ enum { RF_KEEP = 1, RF_VALIDATE = 2, RF_COMPOSITE = 4, RF_DECODE = 8 };
 // not required — and whether a plain key has to be decoded (it signs none of this transaction's signatures:
 // the verify path decodes the others).  A key that is neither an Ed25519 / ECDSA key nor a CompositeKey
 // -> CHIP_STX_UNSUPPORTED.  (The emit pass counted the entries.)
-__global__ void __launch_bounds__(256) k_stx_required(uint64_t n, uint8_t* __restrict__ status,
+__global__ void __launch_bounds__(KRYO_BLOCK) k_stx_required(uint64_t n, uint8_t* __restrict__ status,
                                                       const uint64_t* __restrict__ comp_start,
                                                       const uint32_t* __restrict__ comp_group,
                                                       const uint64_t* __restrict__ comp_off,
@@ -996,7 +1135,9 @@ __global__ void __launch_bounds__(256) k_stx_required(uint64_t n, uint8_t* __res
         kept += keep ? 1 : 0;
         cnt++;
     };
+    __shared__ uint4 s_win[KRYO_ROWS * KRYO_BLOCK];
     Cur c;
+    c.window(s_win + threadIdx.x);
     if (!req_walk(c, r.pool, pool_bytes, comp_start[t], comp_start[t + 1], comp_group, comp_off, comp_len, reg, take))
         bad = true;
     if (bad) status[t] = CHIP_STX_UNSUPPORTED;

@@ -40,7 +40,14 @@ struct DevBuf {
 // interning, required keys, scan scratch
 struct StxBufs {
     DevBuf s_ncomp, s_nsig, s_nbytes, s_cstart, s_sstart, s_pstart, s_pool, s_salts, s_cgroup, s_cint, s_coff, s_clen, s_txidx, s_tmpl, s_soff, s_slen, s_skoff, s_sklen, s_meta, s_tab, s_tabmin, s_kslot, s_krep, s_kflag, s_kincl, s_kidx, s_koff, s_klen, s_temp, r_nraw, r_rstart, r_kid, r_len, r_keep, r_kincl, r_off, r_nreq, r_qstart, r_nstart, r_val, r_nk, r_w, r_flag, r_tx, r_nn, r_nc, r_ninc, r_cinc, k_off, k_len, k_kind, k_ok, k_tx, r_tot;
+    hipStream_t cs = nullptr;                     // the blob copy into s_pool, overlapping pass 1
+    hipEvent_t ce0 = nullptr, ce1 = nullptr;
     void release() {
+        if (cs) (void)hipStreamDestroy(cs);
+        if (ce0) (void)hipEventDestroy(ce0);
+        if (ce1) (void)hipEventDestroy(ce1);
+        cs = nullptr;
+        ce0 = ce1 = nullptr;
         for (DevBuf* b : {&s_ncomp, &s_nsig, &s_nbytes, &s_cstart, &s_sstart, &s_pstart, &s_pool, &s_salts, &s_cgroup, &s_cint, &s_coff, &s_clen, &s_txidx, &s_tmpl, &s_soff, &s_slen, &s_skoff, &s_sklen, &s_meta, &s_tab, &s_tabmin, &s_kslot, &s_krep, &s_kflag, &s_kincl, &s_kidx, &s_koff, &s_klen, &s_temp, &r_nraw, &r_rstart, &r_kid, &r_len, &r_keep, &r_kincl, &r_off, &r_nreq, &r_qstart, &r_nstart, &r_val, &r_nk, &r_w, &r_flag, &r_tx, &r_nn, &r_nc, &r_ninc, &r_cinc, &k_off, &k_len, &k_kind, &k_ok, &k_tx, &r_tot}) b->release();
     }
 };
@@ -822,8 +829,26 @@ static int stx_parse(chip_ctx* c, StxBufs& B, const chip_stx_blobs* in, uint8_t*
     HIPCHK(c, B.s_salts.ensure(n * 32 + 16));
     const size_t temp = stx_scan_temp_bytes(n1 > 2 ? n1 : 2);
     HIPCHK(c, B.s_temp.ensure(temp));
-    // pass 1: validate + count; ranges = inclusive scans written one past a zero
+    // the pool = a copy of the blobs (payload runs inside one chunk keep their offsets) + the extra region of
+    // de-chunked runs, sized by pass 1.  The copy runs on a stream of its own while pass 1 runs, into a pool
+    // sized for an extra region of up to half the blob bytes; a larger one (rare) is copied again below.
+    const uint64_t extra_base = (in->data_bytes + 15) & ~15ull;
+    if (!B.cs) {
+        HIPCHK(c, hipStreamCreateWithFlags(&B.cs, hipStreamNonBlocking));
+        HIPCHK(c, hipEventCreateWithFlags(&B.ce0, hipEventDisableTiming));
+        HIPCHK(c, hipEventCreateWithFlags(&B.ce1, hipEventDisableTiming));
+    }
+    HIPCHK(c, B.s_pool.ensure(extra_base + in->data_bytes / 2 + 4096 + 64));
     const int kc = c->kbegin(CHIP_K_STX, st);
+    bool copied = false;
+    if (in->data_bytes) {
+        HIPCHK(c, hipEventRecord(B.ce0, st));
+        HIPCHK(c, hipStreamWaitEvent(B.cs, B.ce0, 0));
+        HIPCHK(c, hipMemcpyAsync(B.s_pool.p, in->data, in->data_bytes, hipMemcpyDeviceToDevice, B.cs));
+        HIPCHK(c, hipEventRecord(B.ce1, B.cs));
+        copied = true;
+    }
+    // pass 1: validate + count; ranges = inclusive scans written one past a zero
     launch_stx_count(st, in, reg, tx_status, B.s_ncomp.as<uint64_t>(), B.s_nsig.as<uint64_t>(), B.s_nbytes.as<uint64_t>());
     HIPCHK(c, hipGetLastError());
     DevBuf* cnt[3] = {&B.s_ncomp, &B.s_nsig, &B.s_nbytes};
@@ -838,12 +863,15 @@ static int stx_parse(chip_ctx* c, StxBufs& B, const chip_stx_blobs* in, uint8_t*
     HIPCHK(c, hipStreamSynchronize(st));
     const uint64_t ncomp = tot[0], nsig = tot[1];
     if (nsig >= (1ull << 31)) return fail(c, CHIP_E_ARG, "too many signatures");
-    // pool = a copy of the blobs (payload runs inside one chunk keep their offsets) + the extra region
-    const uint64_t extra_base = (in->data_bytes + 15) & ~15ull;
     const uint64_t pool = extra_base + tot[2];
-    HIPCHK(c, B.s_pool.ensure(pool + 64));
-    if (in->data_bytes)
-        HIPCHK(c, hipMemcpyAsync(B.s_pool.p, in->data, in->data_bytes, hipMemcpyDeviceToDevice, st));
+    if (pool + 64 > B.s_pool.cap) {   // the extra region outgrew the guess: a larger pool, copied again
+        HIPCHK(c, hipStreamSynchronize(B.cs));
+        HIPCHK(c, B.s_pool.ensure(pool + 64));
+        if (in->data_bytes)
+            HIPCHK(c, hipMemcpyAsync(B.s_pool.p, in->data, in->data_bytes, hipMemcpyDeviceToDevice, st));
+    } else if (copied) {
+        HIPCHK(c, hipStreamWaitEvent(st, B.ce1, 0));
+    }
     HIPCHK(c, B.s_cgroup.ensure(ncomp * 4 + 16));
     HIPCHK(c, B.s_cint.ensure(ncomp * 4 + 16));
     HIPCHK(c, B.s_coff.ensure(ncomp * 8 + 16));

@@ -7,8 +7,11 @@
 //   MerkleRoot  = pad with zeroHash to 2^k; 1 leaf -> the leaf; nodes SHA256(l || r)  MerkleTree.kt:27-66
 //
 // One lane per transaction (the unit the caller batches; no cross-lane divergence for
-// same-shaped transactions).  Leaf and group-root levels are reduced in place in a per-tx
-// scratch slab in HBM (64 slots x 32 B; group ordinals must be < 64).
+// same-shaped transactions).  Fast path (groups in ascending ordinal order, <= 8 components each: what
+// createComponentGroups produces for ordinary transactions): every tree is reduced in registers as its
+// leaves arrive (a binary-counter stack per tree, padding subtrees from the constant zero-hash chain), so
+// nothing but the id is written.  Otherwise the leaf and group-root levels are reduced in place in a
+// per-tx scratch slab in HBM (64 slots x 32 B; group ordinals must be < 64).
 #include <algorithm>
 #include "sha2_dev.hpp"
 #include "runtime.hpp"
@@ -182,7 +185,107 @@ CHIP_DEV void merkle_inplace(uint32_t root[8], uint32_t* slots, uint32_t n, uint
     ld8(root, slots);
 }
 
-__global__ void __launch_bounds__(256) k_txid(uint64_t ntx, const uint8_t* __restrict__ salts,
+// Z_k: the root of a subtree of 2^k zeroHash padding leaves (Z_0 = zeroHash, Z_{k+1} = SHA256(Z_k || Z_k))
+__constant__ uint32_t k_zhash[8][8] = {
+    {0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u, 0x00000000u},
+    {0xf5a5fd42u, 0xd16a2030u, 0x2798ef6eu, 0xd309979bu, 0x43003d23u, 0x20d9f0e8u, 0xea9831a9u, 0x2759fb4bu},
+    {0xdb56114eu, 0x00fdd4c1u, 0xf85c892bu, 0xf35ac9a8u, 0x9289aaecu, 0xb1ebd0a9u, 0x6cde606au, 0x748b5d71u},
+    {0xc78009fdu, 0xf07fc56au, 0x11f12237u, 0x0658a353u, 0xaaa542edu, 0x63e44c4bu, 0xc15ff4cdu, 0x105ab33cu},
+    {0x536d9883u, 0x7f2dd165u, 0xa55d5eeau, 0xe9148595u, 0x4472d56fu, 0x246df256u, 0xbf3cae19u, 0x352a123cu},
+    {0x9efde052u, 0xaa15429fu, 0xae05bad4u, 0xd0b1d7c6u, 0x4da64d03u, 0xd7a1854au, 0x588c2cb8u, 0x430c0d30u},
+    {0xd88ddfeeu, 0xd400a875u, 0x5596b219u, 0x42c1497eu, 0x114c302eu, 0x6118290fu, 0x91e67729u, 0x76041fa1u},
+    {0x87eb0ddbu, 0xa57e35f6u, 0xd2866738u, 0x02a4af59u, 0x75e22506u, 0xc7cf4c64u, 0xbb6be5eeu, 0x11527f2cu}};
+
+// A Merkle tree built as its leaves arrive (MerkleTree.getMerkleTree over leaves padded with zeroHash to a
+// power of two): stack level l holds the root of a complete subtree of 2^l leaves when bit l of `count` is
+// set.  The stack lives in LDS, word q of level l at s[(8 l + q) * TX_BLOCK] (this lane's column: no bank
+// conflicts), so one hash call site serves every level and nothing but the id reaches HBM.
+#define TX_BLOCK 64   // k_txid's block: one wave (the LDS stacks below are per lane)
+#define TX_LEVELS 4   // fast path: <= 16 components per group, group ordinals < 16 (stacks of 5 levels)
+struct MerkleLds {
+    uint32_t* s;
+    uint32_t count;
+    CHIP_DEV void init(uint32_t* base) {
+        s = base;
+        count = 0;
+    }
+    CHIP_DEV void ld(uint32_t v[8], uint32_t l) const {
+#pragma unroll
+        for (int q = 0; q < 8; q++) v[q] = s[(8 * l + q) * TX_BLOCK];
+    }
+    CHIP_DEV void st(uint32_t l, const uint32_t v[8]) {
+#pragma unroll
+        for (int q = 0; q < 8; q++) s[(8 * l + q) * TX_BLOCK] = v[q];
+    }
+    CHIP_DEV void push(const uint32_t leaf[8]) {
+        uint32_t node[8], left[8];
+#pragma unroll
+        for (int q = 0; q < 8; q++) node[q] = leaf[q];
+        uint32_t l = 0;
+        while ((count >> l) & 1u) {
+            ld(left, l);
+            hash_concat(node, left, node);
+            l++;
+        }
+        st(l, node);
+        count++;
+    }
+    // the root (count >= 1): a single leaf is the root itself; otherwise the partial subtrees are closed with
+    // padding subtrees of zeroHash leaves (Z_l from the constant chain)
+    CHIP_DEV void root(uint32_t out[8]) const {
+        const uint32_t n = count;
+        uint32_t d = 0;
+        while ((1u << d) < n) d++;
+        if (n == (1u << d)) {
+            ld(out, d);
+            return;
+        }
+        bool have = false;
+        uint32_t left[8], right[8];
+        for (uint32_t l = 0; l < d; l++) {
+            const bool bit = (n >> l) & 1u;
+            if (!have && !bit) continue;
+            if (bit) {
+                ld(left, l);
+                if (!have) {
+#pragma unroll
+                    for (int q = 0; q < 8; q++) right[q] = k_zhash[l][q];
+                } else {
+#pragma unroll
+                    for (int q = 0; q < 8; q++) right[q] = out[q];
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < 8; q++) {
+                    left[q] = out[q];
+                    right[q] = k_zhash[l][q];
+                }
+            }
+            hash_concat(out, left, right);
+            have = true;
+        }
+    }
+};
+#define TX_FAST_GROUP_LEAVES (1u << TX_LEVELS)
+#define TX_FAST_TOP (1u << TX_LEVELS)
+
+// the fast path's precondition: groups in strictly ascending ordinal order, each of <= 8 components
+CHIP_DEV bool txid_fast_ok(const uint32_t* __restrict__ grp, uint64_t a, uint64_t e) {
+    uint32_t prev = 0xffffffffu, run = 0;
+    for (uint64_t k = a; k < e; k++) {
+        const uint32_t g = grp[k];
+        if (g == prev) {
+            if (++run > TX_FAST_GROUP_LEAVES) return false;
+        } else {
+            if ((prev != 0xffffffffu && g <= prev) || g >= TX_FAST_TOP) return false;
+            prev = g;
+            run = 1;
+        }
+    }
+    return true;
+}
+
+__global__ void __launch_bounds__(TX_BLOCK) k_txid(uint64_t ntx, const uint8_t* __restrict__ salts,
                                               const uint64_t* __restrict__ start, const uint32_t* __restrict__ grp,
                                               const uint32_t* __restrict__ internal, const uint8_t* __restrict__ data,
                                               const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
@@ -201,6 +304,33 @@ __global__ void __launch_bounds__(256) k_txid(uint64_t ntx, const uint8_t* __res
         const uint8_t* sp = salts + 32 * t;
 #pragma unroll
         for (int j = 0; j < 8; j++) salt[j] = ld_be32(sp + 4 * j);
+        if (txid_fast_ok(grp, a, e)) {
+            __shared__ uint32_t lds[2 * (TX_LEVELS + 1) * 8 * TX_BLOCK];   // two stacks per lane, 20 KB per block
+            MerkleLds top, grp_tree;
+            top.init(lds + threadIdx.x);
+            uint64_t k = a;
+            while (k < e) {
+                const uint32_t g = grp[k];
+                while (top.count < g) {   // absent ordinals below g: allOnesHash
+                    uint32_t ones[8];
+#pragma unroll
+                    for (int q = 0; q < 8; q++) ones[q] = 0xffffffffu;
+                    top.push(ones);
+                }
+                grp_tree.init(lds + (TX_LEVELS + 1) * 8 * TX_BLOCK + threadIdx.x);
+                for (; k < e && grp[k] == g; k++) {
+                    uint32_t nonce[8], leaf[8];
+                    compute_nonce(nonce, salt, g, internal[k]);
+                    sha256d_prefixed(leaf, nonce, data + off[k], len[k]);
+                    grp_tree.push(leaf);
+                }
+                uint32_t root[8];
+                grp_tree.root(root);
+                top.push(root);
+            }
+            top.root(id);
+            goto out;
+        }
         uint32_t pm_lo = 0, pm_hi = 0, maxg = 0;
         uint64_t k = a;
         while (k < e) {
@@ -224,6 +354,7 @@ __global__ void __launch_bounds__(256) k_txid(uint64_t ntx, const uint8_t* __res
         }
         merkle_inplace(id, slots, maxg + 1, pm_lo, pm_hi, true);
     }
+out:
 #pragma unroll
     for (int j = 0; j < 8; j++) {
         const uint32_t v = id[j];
@@ -240,8 +371,8 @@ void launch_txid(hipStream_t st, const chip_tx_batch* b, uint8_t* ids, uint32_t*
     // scratch layout: [ntx][64 slots][8 words] group roots, then [ncomp][8 words] leaves
     uint32_t* slots = scratch;
     uint32_t* leaves = scratch + b->ntx * TX_MAX_GROUPS * 8;
-    const uint32_t blocks = (uint32_t)((b->ntx + 255) / 256);
-    hipLaunchKernelGGL(k_txid, dim3(blocks), dim3(256), 0, st, b->ntx, b->salts, b->tx_comp_start, b->comp_group,
+    const uint32_t blocks = (uint32_t)((b->ntx + TX_BLOCK - 1) / TX_BLOCK);
+    hipLaunchKernelGGL(k_txid, dim3(blocks), dim3(TX_BLOCK), 0, st, b->ntx, b->salts, b->tx_comp_start, b->comp_group,
                        b->comp_internal, b->data, b->comp_off, b->comp_len, ids, leaves, slots);
 }
 

@@ -29,8 +29,21 @@ import net.corda.core.utilities.toNonEmptySet
  * Packing (the SoA layout of chip_sig_batch, include/cordahip.h): keys are de-duplicated by their
  * encoded SubjectPublicKeyInfo, messages by (txId, SignatureMetadata) — every signer of one
  * transaction with the same metadata signs the same SignableData bytes (Crypto.kt:552-555).
+ *
+ * Small batches stay on the CPU (SURVEY.md §8(b): single calls through Crypto.isValid, Crypto.kt:615-625,
+ * keep the JCA path below a batch-size threshold): a call with fewer than `minBatch` signatures runs the
+ * reference loop itself (`sig.verify(id)` per signature, TransactionWithSignatures.kt:62-66) — a GPU round
+ * trip (staging, launch, synchronisation: ~0.1 ms) costs more than a few JCA verifications.  The default
+ * comes from the system property `corda.gpu.minBatch` (else DEFAULT_MIN_BATCH); 0 sends everything to the
+ * device.
  */
-class BatchSignatureVerifier(device: Int = 0, flags: Int = 0) : AutoCloseable {
+class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
+                             val minBatch: Int = Integer.getInteger("corda.gpu.minBatch", DEFAULT_MIN_BATCH)) : AutoCloseable {
+    companion object {
+        /** Signatures below which a call stays on the JCA engines (one i2p Ed25519 verify ≈ 60-100 µs on a
+         *  host core; one device round trip of a small batch ≈ 100-150 µs, docs in INTEGRATION.md). */
+        const val DEFAULT_MIN_BATCH = 16
+    }
     private val ctx: Long = CordaHip.open(device, flags).also {
         check(it != 0L) { "libcordahip: no usable GPU for device $device" }
     }
@@ -101,8 +114,13 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0) : AutoCloseable {
     /** SignableData(txId, metadata).serialize().bytes — the message a TransactionSignature signs. */
     private fun signable(id: SecureHash, meta: SignatureMetadata): ByteArray = SignableData(id, meta).serialize().bytes
 
-    /** TransactionWithSignatures.checkSignaturesAreValid for one transaction, batched. */
+    /** TransactionWithSignatures.checkSignaturesAreValid for one transaction, batched (below minBatch: the
+     *  reference loop on the JCA engines). */
     fun checkSignaturesAreValid(id: SecureHash, sigs: List<TransactionSignature>) {
+        if (sigs.size < minBatch) {
+            for (sig in sigs) sig.verify(id)
+            return
+        }
         val st = statuses(sigs.map { Item(it.by, it.bytes, signable(id, it.signatureMetadata)) })
         for ((i, s) in st.withIndex()) if (s.toInt() != CordaHip.VALID) sigs[i].verify(id)   // throws as the JCA path does
     }
@@ -113,6 +131,8 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0) : AutoCloseable {
      * sequential call would have thrown first.
      */
     fun checkSignaturesAreValid(txs: List<SignedTransaction>): List<Exception?> {
+        if (txs.sumOf { it.sigs.size } < minBatch)   // small batch: each transaction's own sequential check
+            return txs.map { tx -> try { tx.sigs.forEach { it.verify(tx.id) }; null } catch (e: Exception) { e } }
         val items = ArrayList<Item>()
         val messages = HashMap<Pair<SecureHash, SignatureMetadata>, ByteArray>()
         for (tx in txs) for (s in tx.sigs)
@@ -233,6 +253,8 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0) : AutoCloseable {
      */
     fun verifySerialized(txs: List<SerializedBytes<SignedTransaction>>): List<Exception?> {
         if (txs.isEmpty()) return emptyList()
+        if (2 * txs.size < minBatch)   // small batch (~2 signatures per transaction): the JVM path as today
+            return txs.map { try { it.deserialize().verifySignaturesExcept(); null } catch (e: Exception) { e } }
         // SignableData templates for the metadata values this node signs with (platform version 1)
         val metas = listOf(SignatureMetadata(1, Crypto.EDDSA_ED25519_SHA512.schemeNumberID),
                 SignatureMetadata(1, Crypto.ECDSA_SECP256R1_SHA256.schemeNumberID),

@@ -35,3 +35,23 @@ def test_txid_mixed_shapes_matches_oracle(ctx, oracle):
         txs.append((rng.bytes(32), groups))
     tb = G.tx_batch_from_lists(txs)
     assert np.array_equal(ctx.txid_batch(tb), oracle.txid_batch(tb))
+
+
+def test_txid_fast_path_edges_match_oracle(ctx, oracle):
+    """Both k_txid schedules against the oracle: the register / LDS tree path (groups ascending, <= 16
+    components, ordinals < 16) at its limits — 1, 2, 15, 16 components per group, ordinal 15, every power-of-two
+    boundary of the top tree — and the HBM-slab fallback just past them (17 components, ordinal 16, 20, 63,
+    groups out of ordinal order)."""
+    rng = np.random.Generator(np.random.PCG64(11))
+    txs = []
+    shapes = [[(0, 1)], [(0, 2)], [(3, 15)], [(1, 16)], [(15, 1)], [(0, 1), (1, 1)], [(0, 3), (2, 5), (7, 16)],
+              [(0, 17)], [(16, 1)], [(20, 2)], [(63, 1)], [(2, 2), (0, 1)], [(0, 1), (4, 1), (8, 1), (9, 3)]]
+    for shape in shapes * 6:
+        groups = [(g, [rng.bytes(int(rng.integers(0, 200))) for _ in range(k)]) for g, k in shape]
+        txs.append((rng.bytes(32), groups))
+    for _ in range(300):
+        gs = sorted(rng.choice(18, size=int(rng.integers(1, 9)), replace=False))
+        groups = [(int(g), [rng.bytes(int(rng.integers(0, 120))) for _ in range(int(rng.integers(1, 19)))]) for g in gs]
+        txs.append((rng.bytes(32), groups))
+    tb = G.tx_batch_from_lists(txs)
+    assert np.array_equal(ctx.txid_batch(tb), oracle.txid_batch(tb))
