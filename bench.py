@@ -627,6 +627,55 @@ def main():
                             "%d of %d accepted vs %d reference-valid" % (int(ok.sum()), mo,
                                                                         int((batch.expected[:mo] == 0).sum()))}
 
+    # CPU baselines of the secondary legs (rank 0, N = 1): the reference-semantics restatement (oracle/) on
+    # bounded samples of each workload shape, threads = this process's CPU share (north_star: the
+    # reference path timed beside each run; the JVM path itself cannot run here)
+    cpu_legs = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle_bind as O
+        share_note = "%d threads = this process's CPU share (nproc %d; %s)" % (threads, nproc, cpu_model())
+        cpu_legs = {}
+        if not args.no_ecdsa:
+            m3 = 4096
+            eb3 = G.ecdsa_batch(m3, n_keys=4096, corrupt=0.10, seed=0x5EED0033, threads=gen_threads)
+            t2 = time.perf_counter()
+            ref3 = O.verify_batch(eb3, threads=threads)
+            el3 = time.perf_counter() - t2
+            t2 = time.perf_counter()
+            G.ossl_verify_batch(eb3, threads=threads)
+            elo3 = time.perf_counter() - t2
+            cpu_legs["cfg3"] = {"value": m3 / el3, "unit": "verified ECDSA sigs/s (r1/k1 mixed)", "cores": threads,
+                                "kind": "port", "openssl_sigs_per_s": m3 / elo3,
+                                "agrees_with_labels": bool(np.array_equal(ref3, eb3.expected)),
+                                "sample": "%d signatures of the cfg3 shape (4,096 keys per curve, 10%% corrupted) "
+                                          "through oracle/ (BC 1.57 semantics) and OpenSSL EVP_DigestVerify; %s"
+                                          % (m3, share_note)}
+        if not args.no_txid:
+            m4 = 4096
+            tb4, tm4, sb4, ids4, msgs4 = G.cfg4_workload(m4, n_keys=args.keys, seed=0x5EED0034, threads=gen_threads)
+            q4 = G.cfg4_required(sb4, m4, args.keys, seed=0x5EED0036)
+            b4 = G.signer_sig_batch(sb4, msgs4)
+            t2 = time.perf_counter()
+            oid = O.txid_batch(tb4, threads=threads)
+            st4 = O.verify_batch(b4, threads=threads)
+            v4, a4, _m4 = O.required_signers(q4, b4, st4)
+            el4 = time.perf_counter() - t2
+            cpu_legs["cfg4"] = {"value": m4 / el4, "unit": "fully verified tx/s (verifySignaturesExcept)",
+                                "cores": threads, "kind": "port",
+                                "agrees": bool(np.array_equal(oid, ids4)) and
+                                          bool(np.array_equal(v4, q4.expected_verdict)),
+                                "sample": "%d cfg4 transactions: tx id (oracle/txid_ref.c) + 2 Ed25519 signatures "
+                                          "(oracle/ed25519_ref.c) + required signers (oracle/required_ref.c); %s"
+                                          % (m4, share_note)}
+        chk = secondary.get("notary_oracle_check")
+        if chk and chk.get("oracle_commit_s"):
+            cpu_legs["cfg5"] = {"value": chk["nref"] / chk["oracle_commit_s"], "unit": "input StateRefs/s",
+                                "cores": 1, "kind": "port",
+                                "sample": "the whole cfg5 batch (%d input StateRefs against the 10M-row log) through "
+                                          "oracle/uniq_ref.c's ordered commit, one thread: the reference commits "
+                                          "under one global lock (PersistentUniquenessProvider.kt:56-60), so its "
+                                          "parallelism is one" % chk["nref"]}
+
     if rank == 0:
         out = {
             "metric": "verified sigs/sec (Ed25519, ECDSA P-256) at 1/2/4/8 MI355X; tx ids/sec",
@@ -661,6 +710,7 @@ def main():
                                          "straus_verify": straus_ms}},
             "cpu_baseline": cpu,
             "cpu_baseline_openssl": cpu_ossl,
+            "cpu_baselines_secondary": cpu_legs,
             "secondary": secondary,
             "gen_s": gen_s,
         }
@@ -816,13 +866,15 @@ def notary_leg(args, ctx, world, rank, torch, dev, dist, D, G, native, threads, 
         ocap = nref + 1
         obuf = (O.OrcConflict * ocap)()
         onout = O.ctypes.c_uint64()
+        t_commit = time.perf_counter()
         O.lib().orc_uniq_commit_batch(u.h, O.ctypes.c_uint64(ntx), O._p(ub.tx_ref_start), O._p(ub.refs),
                                       O._p(ub.tx_ids), O._p(ub.callers), O._p(ost), obuf, O.ctypes.c_uint64(ocap),
                                       O.ctypes.byref(onout))
+        commit_s = time.perf_counter() - t_commit
         orecs = np.frombuffer(obuf, dtype=np.uint8, count=int(onout.value) * 56)
         check = {"statuses_equal": bool(np.array_equal(st, ost)), "records_gpu": int(nout),
                  "records_oracle": int(onout.value), "records_equal": bool(np.array_equal(recs_gpu, orecs)),
-                 "oracle_s": time.time() - t_chk}
+                 "oracle_s": time.time() - t_chk, "oracle_commit_s": commit_s, "nref": int(nref)}
         del u, obuf, orecs
     # notary signature over every tx id (one key: the per-key comb path)
     lo, hi = ntx * rank // world, ntx * (rank + 1) // world
