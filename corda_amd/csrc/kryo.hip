@@ -129,6 +129,9 @@ struct Sink {   // dword-accumulating byte writer into the output pool
 #ifndef KRYO_WIN
 #define KRYO_WIN 128
 #endif
+#ifndef KRYO_NO_STORES
+#define KRYO_NO_STORES 0   // timing experiments only: pass 2 without its index stores (wrong outputs)
+#endif
 #define KRYO_BLOCK 256
 #define KRYO_ROWS (KRYO_WIN / 16)
 // Input over one graph's bytes [pos, end) of the pool with up to two levels of InputChunked on top.
@@ -731,7 +734,7 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
             sl -= 1;
             {
                 const uint64_t at = run1<EMIT>(c, sl, sink, extra);
-                if (EMIT) {
+                if (EMIT && !KRYO_NO_STORES) {
                     o.sig_off[sbase + sigs] = at;
                     o.sig_len[sbase + sigs] = sl;
                 }
@@ -744,7 +747,7 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
             const uint32_t kl = c.varint<1>();
             {
                 const uint64_t at = run1<EMIT>(c, kl, sink, extra);
-                if (EMIT) {
+                if (EMIT) {   // (kept in the KRYO_NO_STORES experiment: the key interning reads them)
                     o.key_off[sbase + sigs] = at;
                     o.key_len[sbase + sigs] = kl;
                 }
@@ -767,8 +770,10 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
                         ti = m;
                         break;
                     }
-                o.tmpl_idx[sbase + sigs] = ti;
-                o.tx_idx[sbase + sigs] = (uint32_t)t;
+                if (!KRYO_NO_STORES) {
+                    o.tmpl_idx[sbase + sigs] = ti;
+                    o.tx_idx[sbase + sigs] = (uint32_t)t;
+                }
             }
             sigs++;
         }
@@ -813,9 +818,11 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
                 const uint32_t cl = w.varint<1>();
                 if (EMIT) {
                     const uint64_t at = run1<EMIT>(w, cl, sink, extra);
-                    o.comp_off[cbase + comps] = at;
-                    o.comp_len[cbase + comps] = cl;
-                    o.comp_internal[cbase + comps] = k;
+                    if (!KRYO_NO_STORES) {
+                        o.comp_off[cbase + comps] = at;
+                        o.comp_len[cbase + comps] = cl;
+                        o.comp_internal[cbase + comps] = k;
+                    }
                 } else {
                     // the extra region is sized by run1's rule: a run not inside the current chunk
                     if (w.rem1 == 0 && cl) {
@@ -845,7 +852,7 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
                 in_count = nc;
             }
             if (EMIT)
-                for (uint64_t k = first; k < cbase + comps; k++) o.comp_group[k] = (uint32_t)gi;
+                for (uint64_t k = first; k < cbase + comps && !KRYO_NO_STORES; k++) o.comp_group[k] = (uint32_t)gi;
         }
         // PrivacySalt: the registry's id, writeBytesWithLength(32 bytes)
         if (!w.err) {
@@ -868,7 +875,7 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
             (has_tw && !has_notary))
             st = CHIP_STX_INVARIANT;
         if (in_count > 64 || noncanon) st = st == CHIP_STX_OK ? CHIP_STX_UNSUPPORTED : st;
-        if (EMIT && st == CHIP_STX_OK && in_count > 1) {   // checkNoDuplicateInputs: equal serialized StateRefs
+        if (EMIT && st == CHIP_STX_OK && in_count > 1 && !KRYO_NO_STORES) {   // checkNoDuplicateInputs: equal serialized StateRefs
             sink.flush();
             for (uint64_t i = 0; i < in_count && st == CHIP_STX_OK; i++)
                 for (uint64_t j = i + 1; j < in_count; j++) {
