@@ -484,7 +484,16 @@ def main():
         tb, tm, sb, ids_ref, want_v, want_a = G.cfg4_workload_commands(args.txid_n, n_keys=args.keys,
                                                                        seed=0x5EED0014 + rank, threads=gen_threads)
         bdata, boff, blen = G.stx_uniform(tb, sb, 2)
-        bb = torch.from_numpy(bdata).to(dev)
+        # two blob buffers (the pipelined leg alternates them), each with room for the de-chunked runs behind
+        # the blobs: chip_stx_parse_device parses in place (data_capacity), no copy of the 3 GB of blobs
+        nbytes = int(bdata.nbytes)
+        bcap = nbytes + nbytes // 2 + (1 << 20)
+        bbs = []
+        for _ in range(2):
+            x = torch.empty(bcap, dtype=torch.uint8, device=dev)
+            x[:nbytes].copy_(torch.from_numpy(bdata))
+            bbs.append(x)
+        bb = bbs[0]
         bo, bl = torch.from_numpy(boff).to(dev), torch.from_numpy(blen).to(dev)
         del bdata
         dm = upload(tm, ("data", "off", "len", "id_at"), torch, dev)
@@ -499,8 +508,8 @@ def main():
         holder = {}
 
         def from_bytes():
-            holder["p"] = ctx.stx_parse_device(bb, bo, bl, bb.numel(), meta, bst, stream=stream.cuda_stream,
-                                               required=True)
+            holder["p"] = ctx.stx_parse_device(bb, bo, bl, nbytes, meta, bst, stream=stream.cuda_stream,
+                                               required=True, data_capacity=bcap)
             ctx.verify_signed_tx_parsed_device(holder["p"], dm, None, ids, fst, fv, fa, fm, stream=stream.cuda_stream)
         for _ in range(2):
             from_bytes()
@@ -523,8 +532,8 @@ def main():
             k = holder.get("k", 0)
             if evs[k % 2] is not None:
                 s_parse.wait_event(evs[k % 2])
-            holder["p"] = ctx.stx_parse_device(bb, bo, bl, bb.numel(), meta, bst, stream=s_parse.cuda_stream,
-                                               required=True)
+            holder["p"] = ctx.stx_parse_device(bbs[k % 2], bo, bl, nbytes, meta, bst, stream=s_parse.cuda_stream,
+                                               required=True, data_capacity=bcap)
             ctx.verify_signed_tx_parsed_device(holder["p"], dm, None, ids, fst, fv, fa, fm, stream=stream.cuda_stream)
             ev = torch.cuda.Event()
             ev.record(stream)
@@ -537,7 +546,7 @@ def main():
             bool(np.array_equal(fst.cpu().numpy(), sb.expected))
         bel = timed_steps(from_bytes_pipelined, ts, world, torch, dev, dist)
         p = holder["p"]
-        blob_bytes = int(bb.numel())
+        blob_bytes = nbytes
         # algorithmic bytes of one parse: the blobs read once, the index arrays written (components 20 B,
         # signatures 40 B incl. the key interning, required keys 16 B, tx 56 B)
         alg = blob_bytes + 20 * int(p.txs.ncomp) + 40 * int(p.sigs.n) + 16 * int(p.req.nreq) + 56 * tb.ntx
@@ -565,7 +574,7 @@ def main():
                                    "note": "one launch = both parse passes, the pool copy, scans, key interning "
                                            "and the required-key pass with their 3 host syncs"},
         })
-        del bb, bo, bl, bst, holder, p, dm, ids, fst, fv, fa, fm, tb, tm, sb, evs, s_parse
+        del bb, bbs, bo, bl, bst, holder, p, dm, ids, fst, fv, fa, fm, tb, tm, sb, evs, s_parse
     progress("cfg4 legs done")
     # ---- cfg3: mixed ECDSA r1/k1, one global batch sharded by transaction, RCCL bitmap all-gather ----
     if not args.no_ecdsa:

@@ -97,12 +97,44 @@ __device__ __forceinline__ uint32_t ld32u(const uint8_t* pool, uint64_t off) {
     return __builtin_amdgcn_alignbyte(hi, lo, (uint32_t)(off & 3));
 }
 __device__ __forceinline__ uint32_t tail_mask(uint32_t left) { return left >= 4 ? ~0u : (1u << (8 * left)) - 1; }
-// pool[at, at + n) == the packed bytes w (n <= 4 * words of w)
+// Consecutive dwords from any byte offset of the pool, 16 bytes per request: 4-byte-aligned dwordx4 loads
+// (global_load_dwordx4 needs dword alignment only) funnelled by the byte shift.  take4 yields the next 16 bytes
+// as 4 dwords; it reads up to 32 bytes past them (callers keep 40 bytes of slack before the pool's end).
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+struct DStream {
+    const uint8_t* p;
+    uint32_t s;
+    u32x4a4 cur;
+    __device__ __forceinline__ void open(const uint8_t* pool, uint64_t at) {
+        p = pool + (at & ~3ull);
+        s = (uint32_t)(at & 3);
+        cur = *reinterpret_cast<const u32x4a4*>(p);
+    }
+    __device__ __forceinline__ void take4(uint32_t o[4]) {
+        p += 16;
+        const u32x4a4 nx = *reinterpret_cast<const u32x4a4*>(p);
+        o[0] = __builtin_amdgcn_alignbyte(cur.y, cur.x, s);
+        o[1] = __builtin_amdgcn_alignbyte(cur.z, cur.y, s);
+        o[2] = __builtin_amdgcn_alignbyte(cur.w, cur.z, s);
+        o[3] = __builtin_amdgcn_alignbyte(nx.x, cur.w, s);
+        cur = nx;
+    }
+};
+// pool[at, at + n) == the packed bytes w (n <= 4 * words of w): n / 16 + 2 requests
 __device__ __forceinline__ bool eq_packed(const uint8_t* pool, uint64_t at, const uint32_t* w, uint32_t n) {
     bool ok = true;
-    for (uint32_t i = 0; i < n; i += 4) ok &= ((ld32u(pool, at + i) ^ w[i >> 2]) & tail_mask(n - i)) == 0;
+    DStream d;
+    d.open(pool, at);
+    for (uint32_t i = 0; i < n; i += 16) {
+        uint32_t o[4];
+        d.take4(o);
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (i + 4 * q < n) ok &= ((o[q] ^ w[(i >> 2) + q]) & tail_mask(n - i - 4 * q)) == 0;
+    }
     return ok;
 }
+#define KRYO_SLACK 40   // bytes a DStream may read past what it returns
 
 struct Sink {   // dword-accumulating byte writer into the output pool
     uint8_t* base;
@@ -121,26 +153,21 @@ struct Sink {   // dword-accumulating byte writer into the output pool
     }
 };
 
-// A lane's read windows: 16 bytes in registers (the byte extraction is a 4-way select), refilled from a
-// KRYO_WIN-byte window in LDS (one ds_read_b128), refilled from the pool with KRYO_WIN / 16 independent 16-byte
-// loads.  The parse is a chain of dependent loads per lane: a KRYO_WIN window is one global round trip where
-// 16-byte windows took KRYO_WIN / 16, and fetches its lines once (a lane's next 16 bytes were rarely still in
-// L1 / L2: every lane streams its own blob).  LDS layout: row k of lane t at win[k * KRYO_BLOCK + t].
-#ifndef KRYO_WIN
-#define KRYO_WIN 128
-#endif
+// Memory requests, not round trips, bound the walk: every lane reads its own blob, so a wave-instruction's
+// 64 lanes touch 64 different lines and each 16-byte lane piece is a request of its own (measured: pass time
+// linear in the batch from 125k blobs on; 16- / 64- / 128-byte read windows all the same).  So the cursor
+// reads the structure through a 16-byte register window and every bulk compare loads 16 bytes per request
+// (ld_dwords below), never a dword at a time.
+#define KRYO_BLOCK 256
 #ifndef KRYO_NO_STORES
 #define KRYO_NO_STORES 0   // timing experiments only: pass 2 without its index stores (wrong outputs)
 #endif
-#define KRYO_BLOCK 256
-#define KRYO_ROWS (KRYO_WIN / 16)
 // Input over one graph's bytes [pos, end) of the pool with up to two levels of InputChunked on top.
 struct Cur {
     const uint8_t* pool;
     uint64_t pool_bytes, pos, end;
-    uint64_t widx, lidx;
+    uint64_t widx;
     uint4 w;
-    uint4* lw;   // this lane's LDS window (rows KRYO_BLOCK apart)
     uint32_t rem1, rem2;
     int err;
     // class-name ids of this graph (4 bits each) and the CompatibleFieldSerializer headers already read
@@ -153,7 +180,7 @@ struct Cur {
         pool_bytes = pb;
         pos = a;
         end = b;
-        widx = lidx = ~0ull;
+        widx = ~0ull;
         rem1 = rem2 = 0;
         err = E_OK;
         names = nnames = headers = 0;
@@ -161,34 +188,20 @@ struct Cur {
     __device__ __forceinline__ void fail(int e) {
         if (err == E_OK) err = e;
     }
-    __device__ __forceinline__ void window(uint4* lds_lane) {
-        lw = lds_lane;
-        lidx = ~0ull;
-    }
+
     __device__ __forceinline__ uint8_t raw() {
         if (pos >= end) {
             fail(E_KRYO);
             return 0;
         }
-        const uint64_t wi = pos >> 4;
+        const uint64_t wi = pos >> 4;   // a 16-byte window per lane: one global_load_dwordx4 per 16 bytes
         if (wi != widx) {
-            const uint64_t li = pos / KRYO_WIN;
-            if (li != lidx) {
-                if ((li + 1) * KRYO_WIN > pool_bytes) return pool[pos++];   // the pool's tail: byte loads
-                // LDS-DMA (global_load_lds_dwordx4): no VGPR destinations; row k of the wave's lanes lands at
-                // the wave-uniform base + lane * 16, i.e. at lw[k * KRYO_BLOCK] for every lane
-                const uint4* src = reinterpret_cast<const uint4*>(pool + li * KRYO_WIN);
-                uint4* wave_base = lw - (threadIdx.x & 63);
-#pragma unroll
-                for (int k = 0; k < KRYO_ROWS; k++)
-                    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + k),
-                                                     (__attribute__((address_space(3))) void*)(wave_base + k * KRYO_BLOCK),
-                                                     16, 0, 0);
-                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                lidx = li;
+            if ((wi << 4) + 16 <= pool_bytes) {
+                w = *reinterpret_cast<const uint4*>(pool + (wi << 4));
+                widx = wi;
+            } else {
+                return pool[pos++];
             }
-            w = lw[((uint32_t)(pos % KRYO_WIN) >> 4) * KRYO_BLOCK];
-            widx = wi;
         }
         const uint32_t q = (pos >> 2) & 3;
         const uint32_t d = q == 0 ? w.x : q == 1 ? w.y : q == 2 ? w.z : w.w;
@@ -284,7 +297,7 @@ struct Cur {
                 return false;
             }
         }
-        if ((L == 1 && n > rem1) || end - pos < n || pos + n + 8 > pool_bytes) return false;
+        if ((L == 1 && n > rem1) || end - pos < n || pos + n + KRYO_SLACK > pool_bytes) return false;
         at = pos;
         return true;
     }
@@ -463,9 +476,19 @@ __constant__ Bytes<65> k_sr_mid = bytes_of(SR_MID);
 
 __device__ __forceinline__ bool key_eq(const uint8_t* pool, uint64_t a, uint32_t la, uint64_t b, uint32_t lb) {
     if (la != lb) return false;
-    for (uint32_t i = 0; i < la; i += 4)
-        if ((ld32u(pool, a + i) ^ ld32u(pool, b + i)) & tail_mask(la - i)) return false;
-    return true;
+    DStream x, y;
+    x.open(pool, a);
+    y.open(pool, b);
+    bool ok = true;
+    for (uint32_t i = 0; i < la && ok; i += 16) {
+        uint32_t u[4], v[4];
+        x.take4(u);
+        y.take4(v);
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (i + 4 * q < la) ok &= ((u[q] ^ v[q]) & tail_mask(la - i - 4 * q)) == 0;
+    }
+    return ok;
 }
 
 // A payload run of n bytes inside a level-1 field: where it starts in the blob pool when it lies in one
@@ -515,25 +538,19 @@ template <bool EMIT> __device__ __forceinline__ uint64_t run1(Cur& c, uint32_t n
         c.rem1 -= k;
         left -= k;
         for (; k && (sink.pos & 3); k--) sink.put(sink.base[src++]);
-        // 16 bytes per step: five independent aligned loads, funnelled (source and sink share the pool, so
-        // the loads are issued before the stores explicitly)
-        for (; k >= 16; k -= 16, src += 16, sink.pos += 16) {
-            const uint32_t* a = reinterpret_cast<const uint32_t*>(sink.base + (src & ~3ull));
-            const uint32_t sh = (uint32_t)(src & 3);
-            const uint32_t w0 = a[0], w1 = a[1], w2 = a[2], w3 = a[3], w4 = a[4];
-            uint4 v;
-            v.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
-            v.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
-            v.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
-            v.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
-            if ((sink.pos & 15) == 0) {
-                *reinterpret_cast<uint4*>(sink.base + sink.pos) = v;
-            } else {
-                uint32_t* d = reinterpret_cast<uint32_t*>(sink.base + sink.pos);
-                d[0] = v.x;
-                d[1] = v.y;
-                d[2] = v.z;
-                d[3] = v.w;
+        // 16 bytes per step: one 16-byte request in (a DStream), one out (the sink is 4-byte aligned here)
+        if (k >= 16) {
+            DStream d;
+            d.open(sink.base, src);
+            for (; k >= 16; k -= 16, src += 16, sink.pos += 16) {
+                uint32_t v[4];
+                d.take4(v);
+                u32x4a4 o;
+                o.x = v[0];
+                o.y = v[1];
+                o.z = v[2];
+                o.w = v[3];
+                *reinterpret_cast<u32x4a4*>(sink.base + sink.pos) = o;
             }
         }
         for (; k >= 4; k -= 4, src += 4, sink.pos += 4)
@@ -553,11 +570,19 @@ __device__ __forceinline__ bool stateref_canonical(Cur& c, uint32_t n) {
     const uint32_t zn = n - 175;
     uint64_t at;
     if (c.contig<1>(n, at)) {   // inside one chunk: dword compares
-        bool ok = eq_packed(c.pool, at, k_sr_pre_w.w, 74) && c.pool[at + 74] == zn &&
-                  eq_packed(c.pool, at + 75 + zn, k_sr_mid_w.w, 65) && (ld32u(c.pool, at + n - 3) & 0xffffffu) == 1u;
+        bool ok = eq_packed(c.pool, at, k_sr_pre_w.w, 74) && eq_packed(c.pool, at + 75 + zn, k_sr_mid_w.w, 65);
+        DStream d;   // bytes 74 .. 81 (zn and the index varint) and the 3-byte suffix
+        d.open(c.pool, at + 72);
+        uint32_t v[4];
+        d.take4(v);
+        const uint64_t zb = ((uint64_t)v[1] << 32 | v[0]) >> 16;   // byte 74 first
+        ok &= (uint32_t)(zb & 0xff) == zn;
+        d.open(c.pool, at + n - 3);
+        d.take4(v);
+        ok &= (v[0] & 0xffffffu) == 1u;
         uint32_t last = 0;
         for (uint32_t i = 0; i < zn; i++) {   // the index varint: minimal, at most 32 bits
-            const uint32_t b = c.pool[at + 75 + i];
+            const uint32_t b = (uint32_t)(zb >> (8 * (i + 1))) & 0xff;
             ok &= i + 1 == zn ? !(b & 0x80) : (b & 0x80) != 0;
             last = b;
         }
@@ -592,7 +617,11 @@ __device__ __forceinline__ bool stateref_canonical(Cur& c, uint32_t n) {
 __device__ __forceinline__ bool header_ok(Cur& c) {
     uint64_t at;
     if (c.contig<0>(8, at)) {   // "corda" 00 00 01
-        const bool ok = ld32u(c.pool, at) == 0x64726f63u && ld32u(c.pool, at + 4) == 0x01000061u;
+        DStream d;
+        d.open(c.pool, at);
+        uint32_t v[4];
+        d.take4(v);
+        const bool ok = v[0] == 0x64726f63u && v[1] == 0x01000061u;
         c.advance<0>(8);
         return ok;
     }
@@ -656,6 +685,7 @@ __device__ __forceinline__ bool req_walk(Cur& c, const uint8_t* pool, uint64_t p
     return true;
 }
 
+#define STX_REC 4   // signer entries per transaction recorded by the emit pass (more: k_stx_required walks again)
 struct Outs {   // pass-2 destinations (NULL in pass 1)
     uint8_t* pool;
     uint64_t pool_bytes;
@@ -678,6 +708,8 @@ struct Outs {   // pass-2 destinations (NULL in pass 1)
     uint32_t n_meta;
     uint64_t* nraw;                // CHIP_STX_REQUIRED: signer entries per tx (counted here), else NULL
     chip_kryo_registry reg;
+    uint64_t* rec_off;             // [n * STX_REC] the first STX_REC signer entries of each tx (with nraw)
+    uint32_t* rec_len;             //   length | required << 31
 };
 
 template <bool EMIT>
@@ -697,9 +729,7 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
     Sink sink{o.pool, EMIT ? o.extra_base + o.extra_start[t] : 0, 0};
     uint64_t cbase = EMIT ? o.comp_start[t] : 0, sbase = EMIT ? o.sig_start[t] : 0;
     int st = CHIP_STX_OK;
-    __shared__ uint4 s_win[KRYO_ROWS * KRYO_BLOCK];
     Cur c;
-    c.window(s_win + threadIdx.x);
     c.init(data, data_bytes, a, b);
     uint64_t tx_a = 0, tx_b = 0;
     // ---- SignedTransaction (references on) ----
@@ -860,7 +890,13 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
             if (w.varint<0>() != 32) w.fail(E_UNSUP);
             if (EMIT && !w.err && w.end - w.pos >= 32) {
                 uint32_t* dst = reinterpret_cast<uint32_t*>(o.salts + t * 32);
-                for (int k = 0; k < 8; k++) dst[k] = ld32u(o.pool, w.pos + 4 * k);
+                DStream d;
+                d.open(o.pool, w.pos);
+                uint32_t v[4];
+                d.take4(v);
+                for (int k = 0; k < 4; k++) dst[k] = v[k];
+                d.take4(v);
+                for (int k = 0; k < 4; k++) dst[4 + k] = v[k];
             }
             w.skip<0>(32);
         }
@@ -895,10 +931,14 @@ done:
             bool over = false;
             if (st == CHIP_STX_OK &&
                 !req_walk(c, o.pool, o.pool_bytes, cbase, cbase + comps, o.comp_group, o.comp_off, o.comp_len, o.reg,
-                          [&](uint64_t, uint32_t, bool req) {
+                          [&](uint64_t at, uint32_t len, bool req) {
                               if (req) {
                                   over |= cnt >= 64;
                                   cnt++;
+                              }
+                              if (all < STX_REC) {   // recorded: k_stx_required then needs no third walk
+                                  o.rec_off[t * STX_REC + all] = at;
+                                  o.rec_len[t * STX_REC + all] = len | (req ? 0x80000000u : 0u);
                               }
                               all++;
                           }))
@@ -918,7 +958,15 @@ done:
 // ---- signer key interning: distinct SPKI byte strings in first-occurrence order ----
 __device__ uint32_t key_hash(const uint8_t* pool, uint64_t off, uint32_t n) {
     uint32_t h = 2166136261u ^ n;
-    for (uint32_t i = 0; i < n; i += 4) h = (h ^ (ld32u(pool, off + i) & tail_mask(n - i))) * 16777619u;
+    DStream d;
+    d.open(pool, off);
+    for (uint32_t i = 0; i < n; i += 16) {
+        uint32_t v[4];
+        d.take4(v);
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            if (i + 4 * q < n) h = (h ^ (v[q] & tail_mask(n - i - 4 * q))) * 16777619u;
+    }
     h ^= h >> 15;
     h *= 0x2c1b3c6du;
     h ^= h >> 12;
@@ -1094,7 +1142,9 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_required(uint64_t n, uint8_t
                                                       const uint64_t* __restrict__ raw_start, uint32_t* __restrict__ raw_kid,
                                                       uint64_t* __restrict__ raw_off, uint32_t* __restrict__ raw_len,
                                                       uint32_t* __restrict__ raw_keep, uint32_t* __restrict__ raw_flag,
-                                                      uint32_t* __restrict__ raw_tx, uint64_t* __restrict__ nreq) {
+                                                      uint32_t* __restrict__ raw_tx, uint64_t* __restrict__ nreq,
+                                                      const uint64_t* __restrict__ rec_off,
+                                                      const uint32_t* __restrict__ rec_len) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     if (status[t] != CHIP_STX_OK) {
@@ -1142,11 +1192,17 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_required(uint64_t n, uint8_t
         kept += keep ? 1 : 0;
         cnt++;
     };
-    __shared__ uint4 s_win[KRYO_ROWS * KRYO_BLOCK];
-    Cur c;
-    c.window(s_win + threadIdx.x);
-    if (!req_walk(c, r.pool, pool_bytes, comp_start[t], comp_start[t + 1], comp_group, comp_off, comp_len, reg, take))
-        bad = true;
+    if (lim - base <= STX_REC) {   // the entries the emit pass recorded (its walk succeeded for an OK tx)
+        for (uint64_t i = 0; i < lim - base; i++) {
+            const uint32_t l = rec_len[t * STX_REC + i];
+            take(rec_off[t * STX_REC + i], l & 0x7fffffffu, (l >> 31) != 0);
+        }
+    } else {
+        Cur c;
+        if (!req_walk(c, r.pool, pool_bytes, comp_start[t], comp_start[t + 1], comp_group, comp_off, comp_len, reg,
+                      take))
+            bad = true;
+    }
     if (bad) status[t] = CHIP_STX_UNSUPPORTED;
     // a failed transaction keeps none of its entries, so the compaction stays aligned
     for (uint64_t j = base + (bad ? 0 : cnt); j < lim; j++) {
@@ -1366,7 +1422,8 @@ void launch_stx_emit(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_r
                      const StxOut& d) {
     if (!in->n) return;
     Outs o{d.pool, d.pool_bytes, d.extra_start, d.extra_base, d.salts, d.comp_start, d.comp_group, d.comp_internal, d.comp_off, d.comp_len, d.sig_start,
-           d.tx_idx, d.tmpl_idx, d.sig_off, d.sig_len, d.skey_off, d.skey_len, d.meta, d.n_meta, d.nraw, reg};
+           d.tx_idx, d.tmpl_idx, d.sig_off, d.sig_len, d.skey_off, d.skey_len, d.meta, d.n_meta, d.nraw, reg,
+           d.rec_off, d.rec_len};
     hipLaunchKernelGGL(k_stx_parse<true>, grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->off, in->len,
                        in->data_bytes, status, nullptr, nullptr, nullptr, o);
 }
@@ -1402,7 +1459,7 @@ void launch_stx_required(hipStream_t st, uint64_t n, uint8_t* status, const StxO
     if (!n) return;
     hipLaunchKernelGGL(k_stx_required, grid_of(n), dim3(256), 0, st, n, status, d.comp_start, d.comp_group,
                        d.comp_off, d.comp_len, pool_bytes, req_ctx(d, mask), reg, d.sig_start, d.key_idx, q.raw_start,
-                       q.raw_kid, q.raw_off, q.raw_len, q.raw_keep, q.raw_flag, q.raw_tx, q.nreq);
+                       q.raw_kid, q.raw_off, q.raw_len, q.raw_keep, q.raw_flag, q.raw_tx, q.nreq, d.rec_off, d.rec_len);
 }
 
 void launch_stx_req_entries(hipStream_t st, bool emit, uint64_t nraw, uint8_t* status, const StxOut& d, uint64_t mask,

@@ -39,7 +39,7 @@ struct DevBuf {
 // buffers of one Kryo front-end call (chip_stx_parse_device): counts, ranges, pool, batches, key
 // interning, required keys, scan scratch
 struct StxBufs {
-    DevBuf s_ncomp, s_nsig, s_nbytes, s_cstart, s_sstart, s_pstart, s_pool, s_salts, s_cgroup, s_cint, s_coff, s_clen, s_txidx, s_tmpl, s_soff, s_slen, s_skoff, s_sklen, s_meta, s_tab, s_tabmin, s_kslot, s_krep, s_kflag, s_kincl, s_kidx, s_koff, s_klen, s_temp, r_nraw, r_rstart, r_kid, r_len, r_keep, r_kincl, r_off, r_nreq, r_qstart, r_nstart, r_val, r_nk, r_w, r_flag, r_tx, r_nn, r_nc, r_ninc, r_cinc, k_off, k_len, k_kind, k_ok, k_tx, r_tot;
+    DevBuf s_ncomp, s_nsig, s_nbytes, s_cstart, s_sstart, s_pstart, s_pool, s_salts, s_cgroup, s_cint, s_coff, s_clen, s_txidx, s_tmpl, s_soff, s_slen, s_skoff, s_sklen, s_meta, s_tab, s_tabmin, s_kslot, s_krep, s_kflag, s_kincl, s_kidx, s_koff, s_klen, s_temp, r_nraw, r_rstart, r_kid, r_len, r_keep, r_kincl, r_off, r_nreq, r_qstart, r_nstart, r_val, r_nk, r_w, r_flag, r_tx, r_nn, r_nc, r_ninc, r_cinc, k_off, k_len, k_kind, k_ok, k_tx, r_tot, r_roff, r_rlen;
     hipStream_t cs = nullptr;                     // the blob copy into s_pool, overlapping pass 1
     hipEvent_t ce0 = nullptr, ce1 = nullptr;
     void release() {
@@ -48,7 +48,7 @@ struct StxBufs {
         if (ce1) (void)hipEventDestroy(ce1);
         cs = nullptr;
         ce0 = ce1 = nullptr;
-        for (DevBuf* b : {&s_ncomp, &s_nsig, &s_nbytes, &s_cstart, &s_sstart, &s_pstart, &s_pool, &s_salts, &s_cgroup, &s_cint, &s_coff, &s_clen, &s_txidx, &s_tmpl, &s_soff, &s_slen, &s_skoff, &s_sklen, &s_meta, &s_tab, &s_tabmin, &s_kslot, &s_krep, &s_kflag, &s_kincl, &s_kidx, &s_koff, &s_klen, &s_temp, &r_nraw, &r_rstart, &r_kid, &r_len, &r_keep, &r_kincl, &r_off, &r_nreq, &r_qstart, &r_nstart, &r_val, &r_nk, &r_w, &r_flag, &r_tx, &r_nn, &r_nc, &r_ninc, &r_cinc, &k_off, &k_len, &k_kind, &k_ok, &k_tx, &r_tot}) b->release();
+        for (DevBuf* b : {&s_ncomp, &s_nsig, &s_nbytes, &s_cstart, &s_sstart, &s_pstart, &s_pool, &s_salts, &s_cgroup, &s_cint, &s_coff, &s_clen, &s_txidx, &s_tmpl, &s_soff, &s_slen, &s_skoff, &s_sklen, &s_meta, &s_tab, &s_tabmin, &s_kslot, &s_krep, &s_kflag, &s_kincl, &s_kidx, &s_koff, &s_klen, &s_temp, &r_nraw, &r_rstart, &r_kid, &r_len, &r_keep, &r_kincl, &r_off, &r_nreq, &r_qstart, &r_nstart, &r_val, &r_nk, &r_w, &r_flag, &r_tx, &r_nn, &r_nc, &r_ninc, &r_cinc, &k_off, &k_len, &k_kind, &k_ok, &k_tx, &r_tot, &r_roff, &r_rlen}) b->release();
     }
 };
 
@@ -829,24 +829,28 @@ static int stx_parse(chip_ctx* c, StxBufs& B, const chip_stx_blobs* in, uint8_t*
     HIPCHK(c, B.s_salts.ensure(n * 32 + 16));
     const size_t temp = stx_scan_temp_bytes(n1 > 2 ? n1 : 2);
     HIPCHK(c, B.s_temp.ensure(temp));
-    // the pool = a copy of the blobs (payload runs inside one chunk keep their offsets) + the extra region of
-    // de-chunked runs, sized by pass 1.  The copy runs on a stream of its own while pass 1 runs, into a pool
-    // sized for an extra region of up to half the blob bytes; a larger one (rare) is copied again below.
+    // the pool = the blobs (payload runs inside one chunk keep their offsets) + the extra region of de-chunked
+    // runs, sized by pass 1.  In place (data_capacity) when the extra region fits behind the caller's blobs; else
+    // a copy in the context's pool, made on a stream of its own while pass 1 runs, into a pool sized for an
+    // extra region of up to half the blob bytes (a larger one, rare, is copied again below).
     const uint64_t extra_base = (in->data_bytes + 15) & ~15ull;
+    const bool may_in_place = in->data_capacity > extra_base + 64;
     if (!B.cs) {
         HIPCHK(c, hipStreamCreateWithFlags(&B.cs, hipStreamNonBlocking));
         HIPCHK(c, hipEventCreateWithFlags(&B.ce0, hipEventDisableTiming));
         HIPCHK(c, hipEventCreateWithFlags(&B.ce1, hipEventDisableTiming));
     }
-    HIPCHK(c, B.s_pool.ensure(extra_base + in->data_bytes / 2 + 4096 + 64));
     const int kc = c->kbegin(CHIP_K_STX, st);
     bool copied = false;
-    if (in->data_bytes) {
-        HIPCHK(c, hipEventRecord(B.ce0, st));
-        HIPCHK(c, hipStreamWaitEvent(B.cs, B.ce0, 0));
-        HIPCHK(c, hipMemcpyAsync(B.s_pool.p, in->data, in->data_bytes, hipMemcpyDeviceToDevice, B.cs));
-        HIPCHK(c, hipEventRecord(B.ce1, B.cs));
-        copied = true;
+    if (!may_in_place) {
+        HIPCHK(c, B.s_pool.ensure(extra_base + in->data_bytes / 2 + 4096 + 64));
+        if (in->data_bytes) {
+            HIPCHK(c, hipEventRecord(B.ce0, st));
+            HIPCHK(c, hipStreamWaitEvent(B.cs, B.ce0, 0));
+            HIPCHK(c, hipMemcpyAsync(B.s_pool.p, in->data, in->data_bytes, hipMemcpyDeviceToDevice, B.cs));
+            HIPCHK(c, hipEventRecord(B.ce1, B.cs));
+            copied = true;
+        }
     }
     // pass 1: validate + count; ranges = inclusive scans written one past a zero
     launch_stx_count(st, in, reg, tx_status, B.s_ncomp.as<uint64_t>(), B.s_nsig.as<uint64_t>(), B.s_nbytes.as<uint64_t>());
@@ -864,13 +868,18 @@ static int stx_parse(chip_ctx* c, StxBufs& B, const chip_stx_blobs* in, uint8_t*
     const uint64_t ncomp = tot[0], nsig = tot[1];
     if (nsig >= (1ull << 31)) return fail(c, CHIP_E_ARG, "too many signatures");
     const uint64_t pool = extra_base + tot[2];
-    if (pool + 64 > B.s_pool.cap) {   // the extra region outgrew the guess: a larger pool, copied again
-        HIPCHK(c, hipStreamSynchronize(B.cs));
-        HIPCHK(c, B.s_pool.ensure(pool + 64));
-        if (in->data_bytes)
-            HIPCHK(c, hipMemcpyAsync(B.s_pool.p, in->data, in->data_bytes, hipMemcpyDeviceToDevice, st));
-    } else if (copied) {
-        HIPCHK(c, hipStreamWaitEvent(st, B.ce1, 0));
+    const bool in_place = may_in_place && pool + 64 <= in->data_capacity;
+    uint8_t* pool_p = in_place ? const_cast<uint8_t*>(in->data) : nullptr;
+    if (!in_place) {
+        if (pool + 64 > B.s_pool.cap || !copied) {   // no copy yet, or the extra region outgrew the guess
+            if (copied) HIPCHK(c, hipStreamSynchronize(B.cs));
+            HIPCHK(c, B.s_pool.ensure(pool + 64));
+            if (in->data_bytes)
+                HIPCHK(c, hipMemcpyAsync(B.s_pool.p, in->data, in->data_bytes, hipMemcpyDeviceToDevice, st));
+        } else {
+            HIPCHK(c, hipStreamWaitEvent(st, B.ce1, 0));
+        }
+        pool_p = B.s_pool.as<uint8_t>();
     }
     HIPCHK(c, B.s_cgroup.ensure(ncomp * 4 + 16));
     HIPCHK(c, B.s_cint.ensure(ncomp * 4 + 16));
@@ -895,11 +904,17 @@ static int stx_parse(chip_ctx* c, StxBufs& B, const chip_stx_blobs* in, uint8_t*
     if (in->n_meta)
         HIPCHK(c, hipMemcpyAsync(B.s_meta.p, in->meta, (uint64_t)in->n_meta * 8, hipMemcpyHostToDevice, st));
     StxOut d{};
-    d.pool = B.s_pool.as<uint8_t>();
+    d.pool = pool_p;
     d.pool_bytes = pool;
     const bool want_req = in->flags & CHIP_STX_REQUIRED;
-    if (want_req) HIPCHK(c, B.r_nraw.ensure(n1 * 8));
+    if (want_req) {
+        HIPCHK(c, B.r_nraw.ensure(n1 * 8));
+        HIPCHK(c, B.r_roff.ensure(n1 * 4 * 8));   // STX_REC (4) recorded signer entries per tx
+        HIPCHK(c, B.r_rlen.ensure(n1 * 4 * 4));
+    }
     d.nraw = want_req ? B.r_nraw.as<uint64_t>() : nullptr;
+    d.rec_off = want_req ? B.r_roff.as<uint64_t>() : nullptr;
+    d.rec_len = want_req ? B.r_rlen.as<uint32_t>() : nullptr;
     d.extra_start = B.s_pstart.as<uint64_t>();
     d.extra_base = extra_base;
     d.salts = B.s_salts.as<uint8_t>();
@@ -1103,6 +1118,8 @@ int chip_stx_verify(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t
     // the whole call under the context lock (the entries it calls re-enter it), in a buffer set of its own
     std::lock_guard<std::recursive_mutex> g(c->mu);
     HIPCHK(c, hipSetDevice(c->device));
+    // the staged blobs get room for the de-chunked runs behind them (in-place parse, no copy of the blobs)
+    HIPCHK(c, c->h2_data.ensure(((data_bytes + 15) & ~15ull) + data_bytes / 2 + 4096 + 64));
     if ((r = stage(c, c->h2_data, data, data_bytes, st)) || (r = stage(c, c->h2_off, off, n, st)) ||
         (r = stage(c, c->h2_len, len, n, st)) || (r = stage(c, c->h2_td, tmpl->data, tmpl->data_bytes, st)) ||
         (r = stage(c, c->h2_to, tmpl->off, tmpl->n, st)) || (r = stage(c, c->h2_tl, tmpl->len, tmpl->n, st)) ||
@@ -1117,7 +1134,7 @@ int chip_stx_verify(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t
     dtm.len = c->h2_tl.as<uint32_t>();
     dtm.id_at = c->h2_ta.as<uint32_t>();
     chip_stx_blobs in{n, c->h2_data.as<uint8_t>(), c->h2_off.as<uint64_t>(), c->h2_len.as<uint32_t>(), data_bytes,
-                      meta, n_meta, CHIP_STX_REQUIRED};
+                      meta, n_meta, CHIP_STX_REQUIRED, c->h2_data.cap};
     chip_stx_parsed p;
     if ((r = stx_parse(c, c->stx[2], &in, c->h2_st.as<uint8_t>(), &p, st))) return r;
     HIPCHK(c, c->h2_sigst.ensure(p.sigs.n + 16));

@@ -66,6 +66,8 @@ struct StxOut {
     uint8_t* pool;                 // copy of the blobs + the extra region (de-chunked spanning runs)
     uint64_t pool_bytes;
     uint64_t* nraw;                // CHIP_STX_REQUIRED: signer entries per tx, counted by the emit pass
+    uint64_t* rec_off;             //   and the first few of them recorded ([n * STX_REC], kryo.hip)
+    uint32_t* rec_len;
     const uint64_t* extra_start;   // [n + 1] extra region of blob t, relative to extra_base
     uint64_t extra_base;
     uint8_t* salts;                // [n * 32]

@@ -4,11 +4,15 @@
 //   TrustedAuthorityNotaryService.commitInputStates   core/.../node/services/NotaryService.kt:61-75
 // applied to a batch of transactions as if they were committed one after another in batch order.
 //
-// Table: open addressing (linear probing) in HBM, load factor <= 1/2, one 128-byte slot per
-// StateRef (= one L2 line; a probe touches one line and compares in registers):
+// Table: open addressing (linear probing) in HBM, load factor <= 1/2, one 64-byte slot per StateRef
+// (= one HBM / L2 request; a probe touches one line and compares in registers):
 //   words [0..8]   key  = 36-byte StateRef (32-byte txhash || LE u32 index)
-//   word  [9]      used flag (claimed with one CAS)
-//   words [10..17] ConsumingTx.id, [18] ConsumingTx.inputIndex, [19] requestingParty (interned)
+//   word  [9]      used flag
+//   words [10..11] ConsumingTx.id as a row of the id side table (u64), [12] ConsumingTx.inputIndex,
+//   [13] requestingParty (interned), [14..15] zero
+// The ConsumingTx ids live once per transaction in an append-only side table (`txrows`, 32 B a row): every
+// commit appends its batch's ids (one coalesced copy) and a slot names its consumer by row, where the
+// 128-byte slot of the round-2 layout repeated the 32-byte id for every input of the transaction.
 //
 // Batch algorithm ("ordered-commit rounds", exact sequential semantics).  One shard = the slice of
 // the key space one GPU owns (all of it on a single GPU).  A shard sees every transaction of the
@@ -37,7 +41,7 @@
 //             repeated input wins), final status bytes       k_uniq_flag / k_uniq_emit / k_uniq_insert
 //
 // Atomics on MI355X execute at the memory side, one 64-B request per lane for scattered addresses,
-// so none touches the 128-B-slot table: slots are claimed in an occupancy bitmap (1 bit per slot,
+// so none touches the slot table: slots are claimed in an occupancy bitmap (1 bit per slot,
 // cap/8 bytes, Infinity-Cache resident) and the slot is then written with plain stores.  An insert
 // starts its claim at the first empty slot its lookup met on the probe path (usually the slot it
 // gets); the round / commit scratch (bmin, bcommit) is written only for dup states, bcommit with
@@ -51,9 +55,11 @@
 #include "runtime.hpp"
 
 #define KW 9          // key words
-#define SLOT_W 32     // words per slot (128 B)
+#define SLOT_W 16     // words per slot (64 B)
 #define S_USED 9
-#define S_VAL 10      // tx id (8 words), inputIndex, caller
+#define S_ROW 10      // ConsumingTx id row (u64, words 10-11), then inputIndex, caller
+#define S_IDX 12
+#define S_CALLER 13
 #define ST_UNDECIDED 0xffu
 #define ST_COMMITTED 0x10u
 #define ST_FAILED 0x20u
@@ -91,6 +97,8 @@ struct chip_uniq {
     uint64_t cap = 0, size = 0;
     uint32_t* tab = nullptr;   // [cap][SLOT_W]
     uint32_t* bits = nullptr;  // [cap / 32] occupancy bitmap (slot claims)
+    uint8_t* txrows = nullptr; // ConsumingTx id side table: [rows_cap][32]
+    uint64_t rows = 0, rows_cap = 0;
     std::string err;
     // batch in flight (between shard_begin and shard_finish)
     bool open = false;
@@ -171,24 +179,25 @@ CHIP_DEV uint32_t tab_claim(uint32_t* bits, uint64_t cap, uint64_t i0, bool fres
     return NO_SLOT;
 }
 
-// Slot writes of one wave, cooperatively: a lane's random 128-B line written by its own eight 16-B
-// stores costs one partial-line request per store (64 lines per wave-instruction); staged through
-// LDS, every store instruction writes eight whole lines (eight lanes x 16 B each).  Measured: the
-// lane-private form spent 0.9 ms of a 10M-insert commit on the stores alone.  Every lane of the
-// wave calls this (slot = NO_SLOT: nothing to write); `stage` = this wave's 64 x 33 words of LDS.
+// Slot writes of one wave, cooperatively: a lane's random 64-B line written by its own four 16-B stores
+// costs one partial-line request per store (64 lines per wave-instruction); staged through LDS, every store
+// instruction writes sixteen whole lines (four lanes x 16 B each).  Every lane of the wave calls this
+// (slot = NO_SLOT: nothing to write); `stage` = this wave's 64 x (SLOT_W + 1) words of LDS.
+#define STAGE_W (SLOT_W + 1)
 CHIP_DEV void wave_store_slots(uint32_t* tab, uint32_t slot, const uint32_t row[SLOT_W], uint32_t* stage) {
     const uint32_t lane = threadIdx.x & 63;
 #pragma unroll
-    for (int w = 0; w < SLOT_W; w++) stage[lane * 33 + w] = row[w];
+    for (int w = 0; w < SLOT_W; w++) stage[lane * STAGE_W + w] = row[w];
     __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): the wave's LDS writes are done
     __builtin_amdgcn_wave_barrier();
-    const uint32_t chunk = lane & 7;
+    constexpr uint32_t CH = SLOT_W / 4;   // 16-B chunks per slot
+    const uint32_t chunk = lane % CH;
 #pragma unroll
-    for (int j = 0; j < 8; j++) {
-        const uint32_t o = (uint32_t)j * 8 + (lane >> 3);   // owner lane of the slot this lane helps write
+    for (int j = 0; j < (int)CH; j++) {
+        const uint32_t o = (uint32_t)j * (64 / CH) + lane / CH;   // owner lane of the slot this lane helps write
         const uint32_t so = (uint32_t)__shfl((int)slot, (int)o);
         if (so != NO_SLOT) {
-            const uint32_t* src = stage + o * 33 + 4 * chunk;
+            const uint32_t* src = stage + o * STAGE_W + 4 * chunk;
             *reinterpret_cast<uint4*>(tab + (uint64_t)so * SLOT_W + 4 * chunk) = make_uint4(src[0], src[1], src[2], src[3]);
         }
     }
@@ -196,19 +205,17 @@ CHIP_DEV void wave_store_slots(uint32_t* tab, uint32_t slot, const uint32_t row[
 
 // lane-private slot write (rebuild / rehash, where claims mostly probe)
 CHIP_DEV void tab_put(uint32_t* tab, uint32_t* bits, uint64_t cap, uint64_t i0, const uint32_t k[KW],
-                      const uint32_t v[10], bool fresh) {
+                      const uint32_t v[4], bool fresh) {
     uint64_t i = i0 & (cap - 1);
     for (uint64_t n = 0; n < cap; n++) {
         const uint32_t m = 1u << (i & 31);
         if (((n == 0 && fresh) || !(__builtin_nontemporal_load(&bits[i >> 5]) & m)) && !(atomicOr(&bits[i >> 5], m) & m)) {
-            // the whole 128-B line (zero tail): a partial line would cost a read-modify-write in HBM
+            // the whole 64-B line (zero tail): a partial line would cost a read-modify-write in HBM
             uint4* s = reinterpret_cast<uint4*>(tab + i * SLOT_W);
             s[0] = make_uint4(k[0], k[1], k[2], k[3]);
             s[1] = make_uint4(k[4], k[5], k[6], k[7]);
             s[2] = make_uint4(k[8], 1u, v[0], v[1]);
-            s[3] = make_uint4(v[2], v[3], v[4], v[5]);
-            s[4] = make_uint4(v[6], v[7], v[8], v[9]);
-            s[5] = s[6] = s[7] = make_uint4(0u, 0u, 0u, 0u);
+            s[3] = make_uint4(v[2], v[3], 0u, 0u);
             return;
         }
         i = (i + 1) & (cap - 1);
@@ -381,14 +388,15 @@ struct Consumer {
     uint32_t idx, caller;
 };
 CHIP_DEV bool consumed_before(uint64_t r, uint32_t t, const uint32_t* __restrict__ pre, const uint32_t* __restrict__ tab,
-                              const unsigned long long* __restrict__ bcommit, const uint32_t* __restrict__ bslot,
-                              const uint8_t* __restrict__ rdup, const uint8_t* __restrict__ tx_ids,
-                              const uint32_t* __restrict__ callers, Consumer& c) {
+                              const uint8_t* __restrict__ txrows, const unsigned long long* __restrict__ bcommit,
+                              const uint32_t* __restrict__ bslot, const uint8_t* __restrict__ rdup,
+                              const uint8_t* __restrict__ tx_ids, const uint32_t* __restrict__ callers, Consumer& c) {
     if (pre[r] != NO_SLOT) {
-        const uint32_t* v = tab + (uint64_t)pre[r] * SLOT_W + S_VAL;
-        c.id = v;
-        c.idx = v[8];
-        c.caller = v[9];
+        const uint32_t* v = tab + (uint64_t)pre[r] * SLOT_W;
+        const uint64_t row = (uint64_t)v[S_ROW] | (uint64_t)v[S_ROW + 1] << 32;
+        c.id = reinterpret_cast<const uint32_t*>(txrows + 32ull * row);
+        c.idx = v[S_IDX];
+        c.caller = v[S_CALLER];
         return true;
     }
     if (!rdup[r]) return false;
@@ -412,8 +420,9 @@ __global__ void __launch_bounds__(256) k_uniq_classify(uint64_t ntx, const uint6
                                                        const unsigned long long* __restrict__ bcommit,
                                                        const uint8_t* __restrict__ tx_ids,
                                                        const uint32_t* __restrict__ callers,
-                                                       const uint32_t* __restrict__ tab, const uint8_t* __restrict__ st,
-                                                       uint8_t* __restrict__ vote, uint32_t* __restrict__ nrec) {
+                                                       const uint32_t* __restrict__ tab, const uint8_t* __restrict__ txrows,
+                                                       const uint8_t* __restrict__ st, uint8_t* __restrict__ vote,
+                                                       uint32_t* __restrict__ nrec) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntx) return;
     uint8_t v = 0;
@@ -423,7 +432,7 @@ __global__ void __launch_bounds__(256) k_uniq_classify(uint64_t ntx, const uint6
         const uint64_t a = start[t];
         for (uint64_t r = a, e = start[t + 1]; r < e; r++) {
             Consumer c;
-            if (!consumed_before(r, (uint32_t)t, pre, tab, bcommit, bslot, rdup, tx_ids, callers, c)) continue;
+            if (!consumed_before(r, (uint32_t)t, pre, tab, txrows, bcommit, bslot, rdup, tx_ids, callers, c)) continue;
             bool same = (c.idx == pos[r]) && (c.caller == callers[t]);
 #pragma unroll
             for (int q = 0; q < 8; q++) same = same && (c.id[q] == myid[q]);
@@ -443,16 +452,16 @@ __global__ void __launch_bounds__(256) k_uniq_emit(uint64_t ntx, const uint64_t*
                                                    const unsigned long long* __restrict__ bcommit,
                                                    const uint8_t* __restrict__ tx_ids,
                                                    const uint32_t* __restrict__ callers,
-                                                   const uint32_t* __restrict__ tab, const uint32_t* __restrict__ nrec,
-                                                   const uint32_t* __restrict__ at, chip_conflict* __restrict__ out,
-                                                   uint64_t cap) {
+                                                   const uint32_t* __restrict__ tab, const uint8_t* __restrict__ txrows,
+                                                   const uint32_t* __restrict__ nrec, const uint32_t* __restrict__ at,
+                                                   chip_conflict* __restrict__ out, uint64_t cap) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntx || !nrec[t]) return;
     uint64_t o = at[t];
     const uint64_t a = start[t];
     for (uint64_t r = a, e = start[t + 1]; r < e && o < cap; r++) {
         Consumer c;
-        if (!consumed_before(r, (uint32_t)t, pre, tab, bcommit, bslot, rdup, tx_ids, callers, c) ||
+        if (!consumed_before(r, (uint32_t)t, pre, tab, txrows, bcommit, bslot, rdup, tx_ids, callers, c) ||
             !first_in_tx(bslot, a, r))
             continue;
         chip_conflict cf;
@@ -474,12 +483,11 @@ __global__ void __launch_bounds__(256) k_uniq_insert(uint64_t nref, const uint8_
                                                      const uint32_t* __restrict__ pos, const uint64_t* __restrict__ start,
                                                      const uint8_t* __restrict__ st, const uint32_t* __restrict__ bslot,
                                                      const uint8_t* __restrict__ rdup,
-                                                     const uint32_t* __restrict__ empty,
-                                                     const uint8_t* __restrict__ tx_ids,
+                                                     const uint32_t* __restrict__ empty, uint64_t row_base,
                                                      const uint32_t* __restrict__ callers, uint32_t* tab,
                                                      uint32_t* bits, uint64_t cap,
                                                      unsigned long long* __restrict__ inserted) {
-    __shared__ uint32_t stage[4][64 * 33];
+    __shared__ uint32_t stage[4][64 * STAGE_W];
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t slot = NO_SLOT;
     uint32_t row[SLOT_W];
@@ -490,11 +498,11 @@ __global__ void __launch_bounds__(256) k_uniq_insert(uint64_t nref, const uint8_
         if (st[t] == ST_COMMITTED && (!rdup[r] || first_in_tx(bslot, start[t], r))) {
             load_key(row, refs, r);
             row[S_USED] = 1;
-            const uint32_t* id = reinterpret_cast<const uint32_t*>(tx_ids + 32ull * t);
-#pragma unroll
-            for (int q = 0; q < 8; q++) row[S_VAL + q] = id[q];
-            row[S_VAL + 8] = pos[r];
-            row[S_VAL + 9] = callers[t];
+            const uint64_t txrow = row_base + t;   // this batch's ids were appended to the side table at row_base
+            row[S_ROW] = (uint32_t)txrow;
+            row[S_ROW + 1] = (uint32_t)(txrow >> 32);
+            row[S_IDX] = pos[r];
+            row[S_CALLER] = callers[t];
             slot = tab_claim(bits, cap, empty[r], true);
         }
     }
@@ -511,7 +519,7 @@ __global__ void __launch_bounds__(256) k_uniq_status(uint64_t ntx, const uint8_t
 
 // rebuild (AppendOnlyPersistentMap.allPersisted): rows absent from the table, first of equal keys
 __global__ void __launch_bounds__(256) k_uniq_rebuild(uint64_t n, const uint8_t* __restrict__ refs,
-                                                      const uint8_t* __restrict__ tx32, const uint32_t* __restrict__ idx,
+                                                      uint64_t row_base, const uint32_t* __restrict__ idx,
                                                       const uint32_t* __restrict__ caller, const uint32_t* __restrict__ pre,
                                                       const uint32_t* __restrict__ bslot,
                                                       const uint32_t* __restrict__ bowner, uint32_t* tab, uint32_t* bits,
@@ -519,13 +527,13 @@ __global__ void __launch_bounds__(256) k_uniq_rebuild(uint64_t n, const uint8_t*
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     bool ins = false;
     if (r < n && pre[r] == NO_SLOT && bowner[bslot[r]] == (uint32_t)(r + 1)) {
-        uint32_t k[KW], v[10];
+        uint32_t k[KW], v[4];
         load_key(k, refs, r);
-        const uint32_t* id = reinterpret_cast<const uint32_t*>(tx32 + 32ull * r);
-#pragma unroll
-        for (int q = 0; q < 8; q++) v[q] = id[q];
-        v[8] = idx[r];
-        v[9] = caller[r];
+        const uint64_t txrow = row_base + r;   // the rebuild's ids were appended to the side table at row_base
+        v[0] = (uint32_t)txrow;
+        v[1] = (uint32_t)(txrow >> 32);
+        v[2] = idx[r];
+        v[3] = caller[r];
         tab_put(tab, bits, cap, key_hash(k), k, v, false);
         ins = true;
     }
@@ -539,11 +547,11 @@ __global__ void __launch_bounds__(256) k_uniq_rehash(uint64_t ocap, const uint32
     if (s >= ocap) return;
     const uint32_t* o = old + s * SLOT_W;
     if (!o[S_USED]) return;
-    uint32_t k[KW], v[10];
+    uint32_t k[KW], v[4];
 #pragma unroll
     for (int q = 0; q < KW; q++) k[q] = o[q];
 #pragma unroll
-    for (int q = 0; q < 10; q++) v[q] = o[S_VAL + q];
+    for (int q = 0; q < 4; q++) v[q] = o[S_ROW + q];
     tab_put(tab, bits, cap, key_hash(k), k, v, false);
 }
 
@@ -607,6 +615,21 @@ static int ensure_capacity(chip_uniq* u, uint64_t extra, hipStream_t st) {
     return CHIP_OK;
 }
 
+// room for `extra` more rows in the ConsumingTx id side table (grown by doubling, old rows copied)
+static int ensure_rows(chip_uniq* u, uint64_t extra, hipStream_t st) {
+    if (u->rows + extra <= u->rows_cap) return CHIP_OK;
+    uint64_t ncap = u->rows_cap ? u->rows_cap : 1024;
+    while (ncap < u->rows + extra) ncap <<= 1;
+    uint8_t* t = nullptr;
+    UCHK(u, hipMalloc(&t, ncap * 32));
+    if (u->rows) UCHK(u, hipMemcpyAsync(t, u->txrows, u->rows * 32, hipMemcpyDeviceToDevice, st));
+    UCHK(u, hipStreamSynchronize(st));
+    if (u->txrows) hipFree(u->txrows);
+    u->txrows = t;
+    u->rows_cap = ncap;
+    return CHIP_OK;
+}
+
 struct chip_ctx;
 extern "C" int chip_ctx_device(const chip_ctx* c);
 
@@ -665,6 +688,7 @@ void chip_uniq_close(chip_uniq* u) {
     hipStreamSynchronize(u->stream);
     if (u->tab) hipFree(u->tab);
     if (u->bits) hipFree(u->bits);
+    if (u->txrows) hipFree(u->txrows);
     if (u->h_spread) hipHostFree(u->h_spread);
     if (u->h_gate) hipHostFree(u->h_gate);
     UBuf* bufs[] = {&u->reftx,  &u->pre,    &u->empty,  &u->bslot, &u->bowner, &u->rdup,   &u->spread,
@@ -706,13 +730,16 @@ int chip_uniq_rebuild(chip_uniq* u, uint64_t n, const uint8_t* refs36, const uin
                        u->pre.as<uint32_t>(), (uint32_t*)nullptr, u->bowner.as<uint32_t>(), u->rdup.as<uint8_t>(),
                        u->bcap, u->bslot.as<uint32_t>(), u->bmin.as<unsigned long long>(),
                        u->bcommit.as<unsigned long long>());
-    hipLaunchKernelGGL(k_uniq_rebuild, dim3(blocks_for(n)), dim3(256), 0, st, n, d_refs, u->h_ids.as<uint8_t>(),
+    if ((r = ensure_rows(u, n, st))) return r;
+    UCHK(u, hipMemcpyAsync(u->txrows + u->rows * 32, u->h_ids.p, n * 32, hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(k_uniq_rebuild, dim3(blocks_for(n)), dim3(256), 0, st, n, d_refs, u->rows,
                        u->refpos.as<uint32_t>(), u->h_call.as<uint32_t>(), u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(),
                        u->bowner.as<uint32_t>(), u->tab, u->bits, u->cap, u->spread.as<unsigned long long>());
     UCHK(u, hipGetLastError());
     if ((r = spread_fetch(u, st))) return r;
     UCHK(u, hipStreamSynchronize(st));
     u->size += spread_total(u);
+    u->rows += n;
     return CHIP_OK;
 }
 
@@ -805,7 +832,7 @@ int chip_uniq_shard_classify(chip_uniq* u, uint8_t* vote) {
         hipLaunchKernelGGL(k_uniq_classify, dim3(blocks_for(u->ntx)), dim3(256), 0, u->bst, u->ntx, u->start, u->pos,
                            u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->rdup.as<uint8_t>(),
                            u->bcommit.as<unsigned long long>(), u->ids,
-                           u->callers, u->tab, u->st.as<uint8_t>(), vote, u->flag.as<uint32_t>());
+                           u->callers, u->tab, u->txrows, u->st.as<uint8_t>(), vote, u->flag.as<uint32_t>());
     UCHK(u, hipGetLastError());
     return CHIP_OK;
 }
@@ -823,19 +850,26 @@ int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_st
     int rc = spread_zero(u, st);
     if (rc) return rc;
     uint32_t last[2] = {0, 0};
+    uint64_t row_base = u->rows;
     if (nref && ntx) {
+        // the batch's ConsumingTx ids into the side table (one coalesced copy); inserted slots name rows
+        if ((rc = ensure_rows(u, ntx, st))) return rc;
+        row_base = u->rows;
+        UCHK(u, hipMemcpyAsync(u->txrows + row_base * 32, u->ids, ntx * 32, hipMemcpyDeviceToDevice, st));
         size_t tmp = 0;
         UCHK(u, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, nrec, at, (int)ntx, st));
         UCHK(u, u->cub.ensure(tmp + 16));
         UCHK(u, hipcub::DeviceScan::ExclusiveSum(u->cub.p, tmp, nrec, at, (int)ntx, st));
         hipLaunchKernelGGL(k_uniq_emit, dim3(blocks_for(ntx)), dim3(256), 0, st, ntx, u->start, u->pos,
                            u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->rdup.as<uint8_t>(),
-                           u->bcommit.as<unsigned long long>(), u->ids, u->callers, u->tab, nrec, at, out, cap);
+                           u->bcommit.as<unsigned long long>(), u->ids, u->callers, u->tab, u->txrows, nrec, at, out,
+                           cap);
         // inserts after the records: emit reads pre-committed slots, inserts only fill empty ones
         hipLaunchKernelGGL(k_uniq_insert, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->refs, u->reftx.as<uint32_t>(),
                            u->pos, u->start, u->st.as<uint8_t>(), u->bslot.as<uint32_t>(), u->rdup.as<uint8_t>(),
-                           u->empty.as<uint32_t>(), u->ids, u->callers, u->tab, u->bits, u->cap,
+                           u->empty.as<uint32_t>(), row_base, u->callers, u->tab, u->bits, u->cap,
                            u->spread.as<unsigned long long>());
+        u->rows += ntx;
         UCHK(u, hipMemcpyAsync(&last[0], at + ntx - 1, 4, hipMemcpyDeviceToHost, st));
         UCHK(u, hipMemcpyAsync(&last[1], nrec + ntx - 1, 4, hipMemcpyDeviceToHost, st));
         if ((rc = spread_fetch(u, st))) return rc;

@@ -98,7 +98,7 @@ class ChipSignerBatch(ctypes.Structure):
 class ChipStxBlobs(ctypes.Structure):
     _fields_ = [("n", ctypes.c_uint64), ("data", ctypes.c_void_p), ("off", ctypes.c_void_p), ("len", ctypes.c_void_p),
                 ("data_bytes", ctypes.c_uint64), ("meta", ctypes.c_void_p), ("n_meta", ctypes.c_uint32),
-                ("flags", ctypes.c_uint32)]
+                ("flags", ctypes.c_uint32), ("data_capacity", ctypes.c_uint64)]
 
 
 class ChipFtxBatch(ctypes.Structure):
@@ -469,14 +469,14 @@ class Context:
 
     # ---- Kryo front end: SignedTransaction bytes -> batches (device) ----
     def stx_parse_device(self, data, off, lens, data_bytes, meta, tx_status, stream=None,
-                         required: bool = False) -> ChipStxParsed:
+                         required: bool = False, data_capacity: int = 0) -> ChipStxParsed:
         """data / off / lens / tx_status: device tensors; meta: host int32 [n_meta, 2] (platformVersion,
         schemeNumberID) per message template.  Returns the chip_stx_parsed of device pointers (valid
         until the next call on this context)."""
         meta = np.ascontiguousarray(np.asarray(meta, dtype=np.int32).reshape(-1, 2))
         b = ChipStxBlobs(n=int(off.numel() if hasattr(off, "numel") else len(off)), data=_ptr(data), off=_ptr(off),
                          len=_ptr(lens), data_bytes=int(data_bytes), meta=meta.ctypes.data, n_meta=len(meta),
-                         flags=STX_REQUIRED if required else 0)
+                         flags=STX_REQUIRED if required else 0, data_capacity=int(data_capacity))
         out = ChipStxParsed()
         self._check(self.lib.chip_stx_parse_device(self.h, ctypes.byref(b), _ptr(tx_status), ctypes.byref(out),
                                                    stream or None))

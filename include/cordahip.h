@@ -388,6 +388,11 @@ typedef struct {
     const int32_t* meta;       /* [2 * n_meta] HOST memory: SignatureMetadata of template i   */
     uint32_t n_meta;
     uint32_t flags;            /* CHIP_STX_REQUIRED: also derive out->req from the components */
+    /* 0, or the writable size of the `data` allocation: when the de-chunked runs fit behind the blobs
+     * (round16(data_bytes) + their bytes + 64 <= data_capacity) the library writes them there and the outputs
+     * address `data` itself (no copy of the blobs; `data` must then stay unchanged while they are used);
+     * otherwise the blobs are copied into the context's pool as without it. */
+    uint64_t data_capacity;
 } chip_stx_blobs;
 #define CHIP_STX_REQUIRED 0x1u
 typedef struct {

@@ -145,16 +145,24 @@ def test_verify_from_bytes_equals_structured_path(ctx):
 
 
 
-def device_records(ctx, blobs, required=False, metas=METAS):
+def device_records(ctx, blobs, required=False, metas=METAS, in_place=False):
     """chip_stx_parse_device over `blobs` -> one record per blob in the shape of oracle_bind.stx_parse:
     (status, groups, salt, [(sig, key, template index)], required key trees).  A leaf of a tree is its key's
     bytes when the device gave it a signer-pool index (else None: CHIP_REQ_NO_SIGNER)."""
     data, off, ln = G.stx_blobs_from_lists(blobs)
     if len(data) == 0:
         data = np.zeros(1, np.uint8)
-    dd, doff, dlen = _dev(data), _dev(off), _dev(ln)
+    cap = 0
+    if in_place:   # room for the de-chunked runs behind the blobs: parsed in place (data_capacity)
+        cap = 2 * len(data) + 4096
+        dd = torch.zeros(cap, dtype=torch.uint8, device=DEV)
+        dd[:len(data)].copy_(torch.from_numpy(np.ascontiguousarray(data)))
+    else:
+        dd = _dev(data)
+    doff, dlen = _dev(off), _dev(ln)
     st = torch.zeros(max(len(blobs), 1), dtype=torch.uint8, device=DEV)
-    p = ctx.stx_parse_device(dd, doff, dlen, len(data), metas, st[:len(blobs)], required=required)
+    p = ctx.stx_parse_device(dd, doff, dlen, len(data), metas, st[:len(blobs)], required=required,
+                             data_capacity=cap)
     torch.cuda.synchronize()
     n = len(blobs)
     st = st.cpu().numpy()[:n]
@@ -203,10 +211,10 @@ def device_records(ctx, blobs, required=False, metas=METAS):
     return out, keys
 
 
-def assert_device_equals_oracle(ctx, blobs, required, reg=K.DEFAULT_REGISTRY):
+def assert_device_equals_oracle(ctx, blobs, required, reg=K.DEFAULT_REGISTRY, in_place=False):
     """Device records == oracle/kryo_ref.c records for every blob (statuses, components, salts, signatures with
     their template mapping, required-key trees with leaves resolved against the device's signer key pool)."""
-    dev, keys = device_records(ctx, blobs, required)
+    dev, keys = device_records(ctx, blobs, required, in_place=in_place)
     orc = O.stx_parse(blobs, reg, want_required=required)
     pool_keys = set(keys)
     metas = [tuple(m) for m in METAS]
@@ -242,10 +250,11 @@ def test_required_keys_derived_on_device(ctx):
     assert sum(1 for d in dev if d[0] == 0 and any(len(t) > 1 for t in d[4])) >= 20   # composite trees on device
 
 
-@pytest.mark.parametrize("required", [False, True])
-def test_device_equals_oracle_on_cases(ctx, required):
+@pytest.mark.parametrize("required,in_place", [(False, False), (True, False), (True, True)])
+def test_device_equals_oracle_on_cases(ctx, required, in_place):
+    """in_place: the blobs parsed where they lie (data_capacity), the de-chunked runs written behind them."""
     blobs = S.cases(seed=7, n_valid=200) + S.cases_required(seed=21, n=200)
-    dev, _ = assert_device_equals_oracle(ctx, blobs, required)
+    dev, _ = assert_device_equals_oracle(ctx, blobs, required, in_place=in_place)
     assert {d[0] for d in dev} == {0, 1, 2, 3, 4}
 
 

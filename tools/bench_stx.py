@@ -27,6 +27,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--verify", action="store_true")
     ap.add_argument("--no-required", action="store_true", help="parse without CHIP_STX_REQUIRED")
+    ap.add_argument("--copy", action="store_true", help="no data_capacity: the blobs are copied into the context")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     ctx = corda_amd.Context(0)
@@ -34,24 +35,30 @@ def main():
     tb, tm, sb, ids_ref, want_v, want_a = G.cfg4_workload_commands(a.n, n_keys=4096, seed=0x5EED0014, threads=16)
     bdata, boff, blen = G.stx_uniform(tb, sb, 2)
     gen_s = time.time() - t0
-    bb = torch.from_numpy(bdata).to(dev)
+    # the blobs in a buffer with room for the de-chunked runs behind them: the parse runs in place
+    cap = bdata.nbytes + bdata.nbytes // 2 + (1 << 20)
+    bb = torch.empty(cap, dtype=torch.uint8, device=dev)
+    bb[:bdata.nbytes].copy_(torch.from_numpy(bdata))
+    nbytes = int(bdata.nbytes)
+    if a.copy:
+        cap = 0
     bo, bl = torch.from_numpy(boff).to(dev), torch.from_numpy(blen).to(dev)
     bst = torch.empty(a.n, dtype=torch.uint8, device=dev)
     meta = np.array([[1, 4]], dtype=np.int32)
     stream = torch.cuda.current_stream(dev)
     for _ in range(2):
-        p = ctx.stx_parse_device(bb, bo, bl, bb.numel(), meta, bst, stream=stream.cuda_stream, required=not a.no_required)
+        p = ctx.stx_parse_device(bb, bo, bl, nbytes, meta, bst, stream=stream.cuda_stream, required=not a.no_required, data_capacity=cap)
     torch.cuda.synchronize(dev)
     ok = int((bst != 0).sum()) == 0
     ctx.reset_stats()
     torch.cuda.synchronize(dev)
     t = time.perf_counter()
     for _ in range(a.steps):
-        p = ctx.stx_parse_device(bb, bo, bl, bb.numel(), meta, bst, stream=stream.cuda_stream, required=not a.no_required)
+        p = ctx.stx_parse_device(bb, bo, bl, nbytes, meta, bst, stream=stream.cuda_stream, required=not a.no_required, data_capacity=cap)
     torch.cuda.synchronize(dev)
     host_ms = (time.perf_counter() - t) / a.steps * 1e3
     s = ctx.stats()
-    out = {"n": a.n, "blob_bytes": int(bb.numel()), "parse_host_ms": host_ms,
+    out = {"n": a.n, "blob_bytes": nbytes, "in_place": cap > 0, "parse_host_ms": host_ms,
            "parse_kernel_ms": s.kernel_ms_total[native.K_STX] / max(s.kernel_launches[native.K_STX], 1),
            "ncomp": int(p.txs.ncomp), "nsig": int(p.sigs.n), "n_keys": int(p.sigs.n_keys), "nreq": int(p.req.nreq),
            "status_ok": ok, "gen_s": gen_s}
