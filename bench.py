@@ -821,7 +821,7 @@ def notary_leg(args, ctx, world, rank, torch, dev, dist, D, G, native, threads, 
         pre = (refs.reshape(-1, 36)[rows].reshape(-1).copy(), txs.reshape(-1, 32)[rows].reshape(-1).copy(),
                idx[rows].copy(), caller[rows].copy())
     n_pre_local = len(pre[2])
-    table = ctx.uniq_open(2 * (n_pre_local + nref // world) + 1024)
+    table = ctx.uniq_open(n_pre_local + nref // world + 1024)
     ts = 2
     times, rounds, st_sum = [], 0, None
     recs_gpu = None
@@ -833,7 +833,7 @@ def notary_leg(args, ctx, world, rank, torch, dev, dist, D, G, native, threads, 
         d_out = torch.empty(cap * 56, dtype=torch.uint8, device=dev)
         for _ in range(ts + 1):
             table.close()
-            table = ctx.uniq_open(2 * (n_pre_local + nref) + 1024)
+            table = ctx.uniq_open(n_pre_local + nref + 1024)   # entries; the table keeps load <= 1/2
             table.rebuild(*pre)
             torch.cuda.synchronize(dev)
             t1 = time.perf_counter()
@@ -850,7 +850,7 @@ def notary_leg(args, ctx, world, rank, torch, dev, dist, D, G, native, threads, 
         dshard = eng.upload(shard, ub.tx_ids, ub.callers)
         for _ in range(ts + 1):
             table.close()
-            table = ctx.uniq_open(2 * (n_pre_local + shard.nref) + 1024)
+            table = ctx.uniq_open(n_pre_local + shard.nref + 1024)
             table.rebuild(*pre)
             eng = native.UniqShardEngine(table)
             torch.cuda.synchronize(dev)

@@ -95,6 +95,12 @@ struct chip_ctx {
     DevBuf h2_data, h2_off, h2_len, h2_st, h2_ids, h2_v, h2_a, h2_sigst, h2_miss, h2_td, h2_to, h2_tl, h2_ta;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, tev0 = nullptr, tev1 = nullptr;
     bool ev_pending = false, tev_pending = false;
+    // chip_verify_batch's chunk pipeline: H2D (and the chunk's bounds / pool-range check) on hcs ahead of the
+    // verify kernels on the main stream; the checks' results land in pinned h_rng
+    hipStream_t hcs = nullptr;
+    hipEvent_t hev_c = nullptr, hev_p = nullptr;
+    unsigned long long* h_rng = nullptr;
+    DevBuf h_rngd;
     chip_stats stats{};
     // per-kernel timing: a ring of event pairs recorded on the launch stream
     struct KEv {
@@ -341,7 +347,11 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
         hipStreamCreateWithPriority(&c->aux2, hipStreamNonBlocking, aux_priority()) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_ec_chain_lo, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_ec_chain_hi, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&c->ev_ec_lo, hipEventDisableTiming) != hipSuccess) {
+        hipEventCreateWithFlags(&c->ev_ec_lo, hipEventDisableTiming) != hipSuccess ||
+        hipStreamCreateWithFlags(&c->hcs, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&c->hev_c, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->hev_p, hipEventDisableTiming) != hipSuccess ||
+        hipHostMalloc((void**)&c->h_rng, 64 * 8, hipHostMallocDefault) != hipSuccess) {
         delete c;
         return CHIP_E_DEVICE;
     }
@@ -414,6 +424,12 @@ void chip_shutdown(chip_ctx* c) {
     hipEventDestroy(c->ev_ec_chain_lo);
     hipEventDestroy(c->ev_ec_chain_hi);
     hipEventDestroy(c->ev_ec_lo);
+    hipStreamSynchronize(c->hcs);
+    hipEventDestroy(c->hev_c);
+    hipEventDestroy(c->hev_p);
+    hipStreamDestroy(c->hcs);
+    c->h_rngd.release();
+    if (c->h_rng) hipHostFree(c->h_rng);
     hipStreamDestroy(c->aux2);
     hipStreamDestroy(c->aux);
     hipStreamDestroy(c->stream);
@@ -427,9 +443,19 @@ const char* chip_last_error(const chip_ctx* c) { return c ? c->err.c_str() : "nu
 // -> the table halves (Ed25519 [h](-A), ECDSA u2 Q) once the aux stream has built the tables ->
 // finish / bitmap.  Aux stream: the per-key comb tables (serial doubling chains + fills), forked
 // right after key prep so they overlap everything table-free.
+// Chunks of one host batch (verify_host_pipelined): the path decisions are taken for the whole batch
+// (n_decide signatures), and chunks after the first reuse the key prep and the eager per-key tables the
+// first chunk built (same key pool, same device buffers).
+struct VerifyChunk {
+    uint64_t n_decide;
+    bool reuse_keys;
+};
+
 static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap, hipStream_t st,
-                                bool is_valid) {
+                                bool is_valid, const VerifyChunk* vc = nullptr) {
     const uint64_t n = b->n, nk = b->n_keys;
+    const uint64_t nd = vc ? vc->n_decide : n;   // the batch size the path decisions are taken for
+    const bool reuse = vc && vc->reuse_keys;
     if (n > 0xffffffffull) return fail(c, CHIP_E_ARG, "batch too large (n >= 2^32)");
     const uint32_t schemes = b->schemes ? b->schemes : CHIP_SCHEMES_ALL;
     HIPCHK(c, hipSetDevice(c->device));
@@ -445,7 +471,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     // ECDSA per-key comb tables for every EC key when keys sign many signatures (slot = key index)
     const uint64_t ec_key_bytes = ecdsa_comb_key_words() * 4;
     const bool ec_comb = comb_ok && (schemes & CHIP_SCHEMES_EC) && nk * ec_key_bytes <= c->comb_budget &&
-                         ((n >= 16 * nk && n >= c->comb_min_total) || (c->flags & CHIP_FLAG_FORCE_COMB));
+                         ((nd >= 16 * nk && nd >= c->comb_min_total) || (c->flags & CHIP_FLAG_FORCE_COMB));
     EdCombWs w{};
     if (comb || ec_comb) {   // per-key histogram / grouping workspace shared by both comb paths
         HIPCHK(c, c->c_key_count.ensure(nk * 4 + 16));
@@ -461,7 +487,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         const uint64_t key_bytes = (uint64_t)ED_COMB_KEY_WORDS * 4;
         // eager: many signatures per key and every key's table fits the budget -> build all tables
         // (slot = key index) on the aux stream while classify runs; else tables for hot keys only
-        w.eager = (n >= 16 * nk && n >= c->comb_min_total && nk * key_bytes <= c->comb_budget &&
+        w.eager = (nd >= 16 * nk && nd >= c->comb_min_total && nk * key_bytes <= c->comb_budget &&
                    !(c->flags & CHIP_FLAG_FORCE_COMB)) ? 1u : 0u;
         uint64_t slots = nk;
         if (!w.eager) {
@@ -499,16 +525,17 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     }
     HIPCHK(c, hipEventRecord(c->ev0, st));
     HIPCHK(c, hipMemsetAsync(c->counts.p, 0, 64, st));
-    if (nk) HIPCHK(c, hipMemsetAsync(c->meta.p, 0, nk * sizeof(KeyMeta), st));
+    if (nk && !reuse) HIPCHK(c, hipMemsetAsync(c->meta.p, 0, nk * sizeof(KeyMeta), st));
     if (comb || ec_comb) {
         HIPCHK(c, hipMemsetAsync(w.ctr, 0, 64, st));
         HIPCHK(c, hipMemsetAsync(w.key_count, 0, nk * 4, st));
     }
     KeyMeta* meta = c->meta.as<KeyMeta>();
     int ke = c->kbegin(CHIP_K_KEYPREP, st);
-    launch_ed25519_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->abytes.as<uint32_t>(),
-                            c->edtab.as<uint32_t>(), comb ? w.nega : nullptr);
-    if (comb && w.eager && n) {
+    if (!reuse)
+        launch_ed25519_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->abytes.as<uint32_t>(),
+                                c->edtab.as<uint32_t>(), comb ? w.nega : nullptr);
+    if (comb && w.eager && n && !reuse) {
         // fork: per-key comb tables on the aux stream, concurrent with ECDSA key prep, classify and
         // every table-free kernel on the main stream (the chain is a serial 252-doubling latency)
         HIPCHK(c, hipEventRecord(c->ev_fork, st));
@@ -518,9 +545,9 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         c->kend(kt, c->aux);
         HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
     }
-    launch_ecdsa_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->ectab.as<uint32_t>());
-    if (!ec_comb) launch_ecdsa_key_table(st, nk, meta, c->ectab.as<uint32_t>());
-    if (ec_comb) {
+    if (!reuse) launch_ecdsa_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->ectab.as<uint32_t>());
+    if (!ec_comb && !reuse) launch_ecdsa_key_table(st, nk, meta, c->ectab.as<uint32_t>());
+    if (ec_comb && !reuse) {
         // aux: the doubling chain, low windows then high windows; aux2: the fill of each half as soon
         // as its chain half is done (the low fill overlaps the high chain); main waits for the low
         // half (ev_ec_lo) before the low-window additions and for the whole table (ev_join2) after
@@ -637,7 +664,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     c->ev_pending = true;
     c->stats.batches++;
     c->stats.sigs += n;
-    c->stats.keys_prepared += nk;
+    if (!reuse) c->stats.keys_prepared += nk;
     return CHIP_OK;
 }
 
@@ -706,6 +733,209 @@ __global__ void __launch_bounds__(256) k_status_count(uint64_t n, const uint8_t*
     if (threadIdx.x < 8 && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], (unsigned long long)h[threadIdx.x]);
 }
 
+// One chunk of a host batch: the bounds checks of its signatures (and, in the first chunk, of every key and
+// message range) and the byte ranges of the sig / msg pools it reads.  out: [0] flags (k_check_batch's bits),
+// [1] / [2] min / max over its valid sigs of sig_off / sig_off + sig_len, [3] / [4] the same over their
+// messages; init by k_chunk_init.  One atomic per workgroup and word.
+__global__ void k_chunk_init(unsigned long long* out) {
+    if (threadIdx.x < 8) out[threadIdx.x] = (threadIdx.x == 1 || threadIdx.x == 3) ? ~0ull : 0ull;
+}
+__global__ void __launch_bounds__(256) k_check_chunk(uint64_t n, uint64_t nk, uint64_t nm, bool pools,
+                                                     const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ msg_idx,
+                                                     const uint64_t* __restrict__ sig_off, const uint32_t* __restrict__ sig_len,
+                                                     uint64_t sig_bytes, const uint64_t* __restrict__ key_off,
+                                                     const uint32_t* __restrict__ key_len, uint64_t key_bytes,
+                                                     const uint64_t* __restrict__ msg_off, const uint32_t* __restrict__ msg_len,
+                                                     uint64_t msg_bytes, unsigned long long* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t f = 0;
+    unsigned long long v[4] = {~0ull, 0ull, ~0ull, 0ull};
+    if (i < n) {
+        const uint32_t k = key_idx[i], m = msg_idx[i];
+        if (k >= nk || m >= nm) f |= 1;
+        const uint64_t so = sig_off[i], se = so + sig_len[i];
+        if (se > sig_bytes || se < so) f |= 2;
+        else v[0] = so, v[1] = se;
+        if (m < nm) {
+            const uint64_t mo = msg_off[m], me = mo + msg_len[m];
+            if (me <= msg_bytes && me >= mo) v[2] = mo, v[3] = me;   // out-of-pool messages: the pools check below
+        }
+    }
+    if (pools && i < nk) {
+        const uint64_t e = key_off[i] + key_len[i];
+        if (e > key_bytes || e < key_off[i]) f |= 4;
+    }
+    if (pools && i < nm) {
+        const uint64_t e = msg_off[i] + msg_len[i];
+        if (e > msg_bytes || e < msg_off[i]) f |= 8;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        f |= (uint32_t)__shfl_xor((int)f, o);
+        v[0] = min(v[0], (unsigned long long)__shfl_xor((long long)v[0], o));
+        v[1] = max(v[1], (unsigned long long)__shfl_xor((long long)v[1], o));
+        v[2] = min(v[2], (unsigned long long)__shfl_xor((long long)v[2], o));
+        v[3] = max(v[3], (unsigned long long)__shfl_xor((long long)v[3], o));
+    }
+    __shared__ unsigned long long sv[4][4];
+    __shared__ uint32_t sf[4];
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
+        sf[w] = f;
+        for (int q = 0; q < 4; q++) sv[w][q] = v[q];
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        for (uint32_t x = 1; x < (blockDim.x >> 6); x++) {
+            f |= sf[x];
+            v[0] = min(v[0], sv[x][0]);
+            v[1] = max(v[1], sv[x][1]);
+            v[2] = min(v[2], sv[x][2]);
+            v[3] = max(v[3], sv[x][3]);
+        }
+        if (f) atomicOr(&out[0], (unsigned long long)f);
+        if (v[0] != ~0ull) atomicMin(&out[1], v[0]);
+        if (v[1]) atomicMax(&out[2], v[1]);
+        if (v[2] != ~0ull) atomicMin(&out[3], v[2]);
+        if (v[3]) atomicMax(&out[4], v[3]);
+    }
+}
+
+static int check_flags(chip_ctx* c, uint64_t bad) {
+    if (bad & 1) return fail(c, CHIP_E_ARG, "key_idx/msg_idx out of range");
+    if (bad & 2) return fail(c, CHIP_E_ARG, "signature outside sig pool");
+    if (bad & 4) return fail(c, CHIP_E_ARG, "key outside key pool");
+    if (bad & 8) return fail(c, CHIP_E_ARG, "message outside msg pool");
+    return CHIP_OK;
+}
+
+// host batch in chunks (signature ranges, multiples of 64): chunk j+1's index arrays, its device check and the
+// parts of the sig / msg pools it reads that earlier chunks did not copy go over PCIe on hcs while chunk j
+// is verified on the main stream; the key tables are built once (chunk 0) and reused.  The pools are copied
+// to their own offsets (each pool's copied part is one interval, grown on either side), so every offset
+// of the caller's arrays stays valid on the device.
+static int verify_host_pipelined(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap, bool is_valid,
+                                 uint64_t chunks) {
+    const uint64_t n = b->n, nk = b->n_keys, nm = b->n_msgs;
+    hipStream_t st = c->stream, cs = c->hcs;
+    HIPCHK(c, hipSetDevice(c->device));
+    HIPCHK(c, c->h_key_idx.ensure(n * 4 + 16));
+    HIPCHK(c, c->h_msg_idx.ensure(n * 4 + 16));
+    HIPCHK(c, c->h_sig_off.ensure(n * 8 + 16));
+    HIPCHK(c, c->h_sig_len.ensure(n * 4 + 16));
+    HIPCHK(c, c->h_sig_data.ensure(b->sig_bytes + 16));
+    HIPCHK(c, c->h_msg_data.ensure(b->msg_bytes + 16));
+    HIPCHK(c, c->h_status.ensure(n + 16));
+    const uint64_t nw = (n + 63) / 64;
+    HIPCHK(c, c->h_bitmap.ensure(nw * 8 + 16));
+    HIPCHK(c, c->h_check.ensure(128));
+    HIPCHK(c, c->h_rngd.ensure(64));
+    // the main stream's previous work (an earlier batch reading these buffers) before any copy into them
+    HIPCHK(c, hipEventRecord(c->hev_p, st));
+    HIPCHK(c, hipStreamWaitEvent(cs, c->hev_p, 0));
+    int r;
+    if ((r = stage(c, c->h_key_data, b->key_data, b->key_bytes, cs)) || (r = stage(c, c->h_key_off, b->key_off, nk, cs)) ||
+        (r = stage(c, c->h_key_len, b->key_len, nk, cs)) || (r = stage(c, c->h_msg_off, b->msg_off, nm, cs)) ||
+        (r = stage(c, c->h_msg_len, b->msg_len, nm, cs)))
+        return r;
+    const uint64_t csz = ((n + chunks - 1) / chunks + 63) & ~63ull;
+    uint64_t sig_lo = 0, sig_hi = 0, msg_lo = 0, msg_hi = 0;   // copied intervals (empty: lo == hi == 0, none yet)
+    bool sig_any = false, msg_any = false;
+    // copies [lo, hi) of a pool that the interval [*clo, *chi) does not cover yet, and grows it
+    auto grow = [&](DevBuf& d, const uint8_t* src, uint64_t lo, uint64_t hi, uint64_t& clo, uint64_t& chi, bool& any) -> int {
+        if (lo >= hi) return CHIP_OK;
+        if (!any) {
+            HIPCHK(c, hipMemcpyAsync(d.as<uint8_t>() + lo, src + lo, hi - lo, hipMemcpyHostToDevice, cs));
+            clo = lo, chi = hi, any = true;
+            return CHIP_OK;
+        }
+        if (lo < clo) {
+            HIPCHK(c, hipMemcpyAsync(d.as<uint8_t>() + lo, src + lo, clo - lo, hipMemcpyHostToDevice, cs));
+            clo = lo;
+        }
+        if (hi > chi) {
+            HIPCHK(c, hipMemcpyAsync(d.as<uint8_t>() + chi, src + chi, hi - chi, hipMemcpyHostToDevice, cs));
+            chi = hi;
+        }
+        return CHIP_OK;
+    };
+    // stage chunk j: index slices, check, ranges -> host, then the pool parts; hev_p = chunk j's bytes are on the device
+    auto stage_chunk = [&](uint64_t j) -> int {
+        const uint64_t a = j * csz, e = std::min(n, a + csz), m = e - a;
+        HIPCHK(c, hipMemcpyAsync(c->h_key_idx.as<uint32_t>() + a, b->key_idx + a, m * 4, hipMemcpyHostToDevice, cs));
+        HIPCHK(c, hipMemcpyAsync(c->h_msg_idx.as<uint32_t>() + a, b->msg_idx + a, m * 4, hipMemcpyHostToDevice, cs));
+        HIPCHK(c, hipMemcpyAsync(c->h_sig_off.as<uint64_t>() + a, b->sig_off + a, m * 8, hipMemcpyHostToDevice, cs));
+        HIPCHK(c, hipMemcpyAsync(c->h_sig_len.as<uint32_t>() + a, b->sig_len + a, m * 4, hipMemcpyHostToDevice, cs));
+        unsigned long long* out = c->h_rngd.as<unsigned long long>();
+        hipLaunchKernelGGL(k_chunk_init, dim3(1), dim3(64), 0, cs, out);
+        const uint64_t g = j == 0 ? std::max(m, std::max(nk, nm)) : m;
+        hipLaunchKernelGGL(k_check_chunk, dim3((uint32_t)((g + 255) / 256)), dim3(256), 0, cs, m, nk, nm, j == 0,
+                           c->h_key_idx.as<uint32_t>() + a, c->h_msg_idx.as<uint32_t>() + a, c->h_sig_off.as<uint64_t>() + a,
+                           c->h_sig_len.as<uint32_t>() + a, b->sig_bytes, c->h_key_off.as<uint64_t>(),
+                           c->h_key_len.as<uint32_t>(), b->key_bytes, c->h_msg_off.as<uint64_t>(),
+                           c->h_msg_len.as<uint32_t>(), b->msg_bytes, out);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(c->h_rng, out, 64, hipMemcpyDeviceToHost, cs));
+        HIPCHK(c, hipEventRecord(c->hev_c, cs));
+        HIPCHK(c, hipEventSynchronize(c->hev_c));
+        const unsigned long long* q = c->h_rng;
+        if (int rc = check_flags(c, q[0])) return rc;
+        if (int rc = grow(c->h_sig_data, b->sig_data, q[1] == ~0ull ? 0 : q[1], q[2], sig_lo, sig_hi, sig_any)) return rc;
+        if (int rc = grow(c->h_msg_data, b->msg_data, q[3] == ~0ull ? 0 : q[3], q[4], msg_lo, msg_hi, msg_any)) return rc;
+        HIPCHK(c, hipEventRecord(c->hev_p, cs));
+        return CHIP_OK;
+    };
+    chip_sig_batch d = *b;
+    d.key_data = c->h_key_data.as<uint8_t>();
+    d.key_off = c->h_key_off.as<uint64_t>();
+    d.key_len = c->h_key_len.as<uint32_t>();
+    d.sig_data = c->h_sig_data.as<uint8_t>();
+    d.msg_data = c->h_msg_data.as<uint8_t>();
+    d.msg_off = c->h_msg_off.as<uint64_t>();
+    d.msg_len = c->h_msg_len.as<uint32_t>();
+    if (!d.schemes) d.schemes = host_scheme_hint(b);
+    if ((r = stage_chunk(0))) return r;
+    for (uint64_t j = 0; j * csz < n; j++) {
+        const uint64_t a = j * csz, m = std::min(n, a + csz) - a;
+        HIPCHK(c, hipStreamWaitEvent(st, c->hev_p, 0));
+        d.n = m;
+        d.key_idx = c->h_key_idx.as<uint32_t>() + a;
+        d.msg_idx = c->h_msg_idx.as<uint32_t>() + a;
+        d.sig_off = c->h_sig_off.as<uint64_t>() + a;
+        d.sig_len = c->h_sig_len.as<uint32_t>() + a;
+        const VerifyChunk vc{n, j > 0};
+        if ((r = verify_device_locked(c, &d, c->h_status.as<uint8_t>() + a, c->h_bitmap.as<uint64_t>() + a / 64, st,
+                                      is_valid, &vc))) {
+            hipStreamSynchronize(st);
+            return r;
+        }
+        if ((j + 1) * csz < n && (r = stage_chunk(j + 1))) {
+            hipStreamSynchronize(st);
+            return r;
+        }
+    }
+    unsigned long long counts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    HIPCHK(c, hipMemsetAsync(c->h_check.p, 0, 64, st));
+    hipLaunchKernelGGL(k_status_count, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, n, c->h_status.as<uint8_t>(),
+                       c->h_check.as<unsigned long long>());
+    HIPCHK(c, hipGetLastError());
+    HIPCHK(c, hipMemcpyAsync(counts, c->h_check.p, 64, hipMemcpyDeviceToHost, st));
+    if (status) HIPCHK(c, hipMemcpyAsync(status, c->h_status.p, n, hipMemcpyDeviceToHost, st));
+    if (bitmap) HIPCHK(c, hipMemcpyAsync(bitmap, c->h_bitmap.p, nw * 8, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    c->ev_pending = false;
+    for (int k = 0; k < 8; k++) c->stats.status_count[k] += counts[k];
+    return CHIP_OK;
+}
+
+// chunks of a host batch: 1 (no pipeline) below 2^19 signatures, else about 2^18 signatures a chunk, at most
+// 8 (CHIP_HOST_CHUNKS overrides)
+static uint64_t host_chunks(uint64_t n) {
+    uint64_t k = n >= (1ull << 19) ? std::min<uint64_t>(8, n >> 18) : 1;
+    if (const char* e = getenv("CHIP_HOST_CHUNKS")) k = std::max<uint64_t>(1, std::min<uint64_t>(64, strtoull(e, nullptr, 10)));
+    return std::min<uint64_t>(k, std::max<uint64_t>(1, n / 64));
+}
+
 static int verify_host_entry(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap, bool is_valid) {
     if (!c || !b) return fail(c, CHIP_E_ARG, "null argument");
     const uint64_t n = b->n, nk = b->n_keys, nm = b->n_msgs;
@@ -714,6 +944,7 @@ static int verify_host_entry(chip_ctx* c, const chip_sig_batch* b, uint8_t* stat
         return fail(c, CHIP_E_ARG, "null batch array");
     // bounds: checked on the device after staging (k_check_batch), before any verify kernel runs
     std::lock_guard<std::recursive_mutex> g(c->mu);
+    if (const uint64_t k = host_chunks(n); k > 1) return verify_host_pipelined(c, b, status, bitmap, is_valid, k);
     hipStream_t st = c->stream;
     HIPCHK(c, hipSetDevice(c->device));
     int r;

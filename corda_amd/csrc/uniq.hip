@@ -7,9 +7,9 @@
 // Table: open addressing (linear probing) in HBM, load factor <= 1/2, one 64-byte slot per StateRef
 // (= one HBM / L2 request; a probe touches one line and compares in registers):
 //   words [0..8]   key  = 36-byte StateRef (32-byte txhash || LE u32 index)
-//   word  [9]      used flag
+//   word  [9]      used: 0 empty, 1 live (consumed), 2 dead (claimed, never consumed; see below)
 //   words [10..11] ConsumingTx.id as a row of the id side table (u64), [12] ConsumingTx.inputIndex,
-//   [13] requestingParty (interned), [14..15] zero
+//   [13] requestingParty (interned), [14..15] claim word (epoch, claiming ref) of the lookup pass
 // The ConsumingTx ids live once per transaction in an append-only side table (`txrows`, 32 B a row): every
 // commit appends its batch's ids (one coalesced copy) and a slot names its consumer by row, where the
 // 128-byte slot of the round-2 layout repeated the 32-byte id for every input of the transaction.
@@ -18,11 +18,12 @@
 // the key space one GPU owns (all of it on a single GPU).  A shard sees every transaction of the
 // batch but only its own inputs ("local refs", grouped by tx, each carrying its position in the
 // tx's input list):
-//   begin     lookup every local input in the table (pre-committed?) and intern the distinct
-//             states of the batch in a scratch table, one kernel                    k_uniq_lookup
-//             states referenced more than once in the batch ("dup" states, found by the intern)
-//             are the only ones the rounds and the records need: a state with one referencer is
-//             never contended inside the batch (per-ref flag rdup, set by the intern)
+//   begin     one probe walk per local input: pre-committed (live slot), else the first referencer
+//             of the state claims its table slot with one CAS on the slot's claim word, which is at
+//             once the batch intern (later referencers meet the claim and compare keys: "dup"
+//             states, per-ref flag rdup) and the insert position                   k_uniq_lookup
+//             states referenced more than once in the batch are the only ones the rounds and the
+//             records need: a state with one referencer is never contended inside the batch
 //   rounds    vote: first(s) = min tx among the live (not failed) referencers of s; k_uniq_round_min
 //                   (over the dup states' refs only)
 //                   for every undecided tx t: 2 (fail) when a local input is pre-committed or
@@ -38,15 +39,19 @@
 //             (txId, i, caller), else 1 (IDEMPOTENT); decision = max over shards  k_uniq_classify
 //   finish    Conflict.stateHistory records (one per consumed distinct input, ordered by
 //             (tx, input index) through a prefix sum), inserts of committed txs (first index of a
-//             repeated input wins), final status bytes       k_uniq_flag / k_uniq_emit / k_uniq_insert
+//             repeated input wins) into their claimed slots, final status bytes
+//                                                            k_uniq_emit / k_uniq_insert / k_uniq_status
 //
-// Atomics on MI355X execute at the memory side, one 64-B request per lane for scattered addresses,
-// so none touches the slot table: slots are claimed in an occupancy bitmap (1 bit per slot,
-// cap/8 bytes, Infinity-Cache resident) and the slot is then written with plain stores.  An insert
-// starts its claim at the first empty slot its lookup met on the probe path (usually the slot it
-// gets); the round / commit scratch (bmin, bcommit) is written only for dup states, bcommit with
-// plain stores (at most one committed tx consumes a state: a later referencer of a committed state
-// fails, an earlier one's commit makes it fail).
+// Atomics on MI355X execute at the memory side, one 64-B request per lane for scattered addresses:
+// the commit issues one per first referencer of a new state (the claim CAS, on the line its probe
+// just read) and none in the insert pass, which writes claimed slots with plain whole-line stores.
+// The round / commit scratch (bmin, bcommit) lives per state at its owner ref's index and is written
+// only for dup states, bcommit with plain stores (at most one committed tx consumes a state: a later
+// referencer of a committed state fails, an earlier one's commit makes it fail).
+// A claimed slot whose state nothing committed is left empty, unless another key's probe walked past
+// the claim in the same batch: then it is written back "dead" (key, used 2), so that key stays
+// findable; a later batch that consumes the state claims its dead slot again.  chip_uniq_size counts
+// live slots only (the reference's row count); the load factor counts dead ones too.
 #include <mutex>
 #include <string>
 #include <vector>
@@ -94,24 +99,28 @@ struct chip_uniq {
     chip_ctx* ctx = nullptr;
     int device = 0;
     hipStream_t stream = nullptr;
-    uint64_t cap = 0, size = 0;
+    uint64_t cap = 0, size = 0, slots = 0;   // size: live states (consumed); slots: used slots (live or dead)
+    uint32_t epoch = 0;                        // claim epoch of the last lookup / rehash launch
     uint32_t* tab = nullptr;   // [cap][SLOT_W]
-    uint32_t* bits = nullptr;  // [cap / 32] occupancy bitmap (slot claims)
     uint8_t* txrows = nullptr; // ConsumingTx id side table: [rows_cap][32]
     uint64_t rows = 0, rows_cap = 0;
     std::string err;
     // batch in flight (between shard_begin and shard_finish)
     bool open = false;
-    uint64_t ntx = 0, nref = 0, bcap = 0;
+    uint64_t ntx = 0, nref = 0;
     hipStream_t bst = nullptr;
+    hipStream_t ist = nullptr;                // inserts, beside the records (commit_device)
+    hipEvent_t iev0 = nullptr, iev1 = nullptr;
+    bool inserted = false;                    // the batch's inserts were launched (launch_insert)
     const uint64_t* start = nullptr;
     const uint8_t* refs = nullptr;
     const uint32_t* pos = nullptr;
     const uint8_t* ids = nullptr;
     const uint32_t* callers = nullptr;
     // scratch
-    UBuf reftx, pre, empty, bslot, bowner, rdup, bmin, bcommit, st, flag, scan, cub, ctr, spread, refpos, gate;
+    UBuf reftx, pre, tslot, sid, own, passed, rdup, bmin, bcommit, st, flag, scan, cub, ctr, spread, icount, refpos, gate;
     unsigned long long* h_spread = nullptr;   // pinned host copy of the SPREAD counters
+    unsigned long long* h_icount = nullptr;   // pinned host copy of the insert counters
     uint32_t* h_gate = nullptr;               // pinned host copy of the round gate
     uint32_t round = 0;                       // ordered-commit rounds of the batch in flight
     // staging of the host entry points
@@ -143,40 +152,24 @@ CHIP_DEV bool key_eq(const uint32_t* a, const uint32_t k[KW]) {
     return d == 0;
 }
 
-// probe: slot index of k or NO_SLOT (then *empty = the empty slot that ended the probe, where an
-// insert of k starts its claim).  A slot's first 40 bytes (key + used) are read as 2x16 B + 8 B.
-CHIP_DEV uint32_t tab_find(const uint32_t* __restrict__ tab, uint64_t cap, const uint32_t k[KW], uint32_t* empty) {
-    uint64_t i = key_hash(k) & (cap - 1);
-    for (uint64_t n = 0; n < cap; n++) {
-        const uint32_t* s = tab + i * SLOT_W;
-        const uint4 a = *reinterpret_cast<const uint4*>(s);
-        const uint4 b = *reinterpret_cast<const uint4*>(s + 4);
-        const uint2 c = *reinterpret_cast<const uint2*>(s + 8);
-        if (!c.y) {
-            *empty = (uint32_t)i;
-            return NO_SLOT;
-        }
-        const uint32_t d = (a.x ^ k[0]) | (a.y ^ k[1]) | (a.z ^ k[2]) | (a.w ^ k[3]) | (b.x ^ k[4]) | (b.y ^ k[5]) |
-                           (b.z ^ k[6]) | (b.w ^ k[7]) | (c.x ^ k[8]);
-        if (!d) return (uint32_t)i;
-        i = (i + 1) & (cap - 1);
-    }
-    return NO_SLOT;
-}
+// Slot claims.  Words [14..15] of a slot are its claim word: (epoch << 32) | (1 + ref index) of the
+// ref that claimed the slot in the lookup pass of batch `epoch` (one per lookup launch, never reused).
+// A claim is the batch intern and the insert position at once: the first referencer of a state that
+// is not live in the table claims the first claimable slot on its probe path with one 64-bit CAS; a
+// later referencer of the same state walks the same path, meets the claim, and compares keys.  The
+// insert pass then writes claimed slots with plain stores and no atomics.
+//   used 0  empty                  claimable by any key
+//   used 1  live (consumed state)  a match is a pre-committed input
+//   used 2  dead                   a state claimed by a batch in which nothing committed it, written
+//                                  back only when another key probed past its claim (the probe chain
+//                                  must not break); claimable by that key alone
+// Plain loads of a line may return a stale claim word (atomics execute at the memory side); a claim
+// word is written once per epoch, so the CAS settles any stale read.
+#define S_CLAIM 14
 
-// claim an empty slot at or after slot i0 for a key absent from the table and distinct among
-// concurrent inserters: one atomicOr on the occupancy bitmap.  A plain read first skips slots
-// already known to be taken — except at i0 when the caller's lookup saw it empty (`fresh`): then the
-// atomic alone decides.  Returns the slot.
-CHIP_DEV uint32_t tab_claim(uint32_t* bits, uint64_t cap, uint64_t i0, bool fresh) {
-    uint64_t i = i0 & (cap - 1);
-    for (uint64_t n = 0; n < cap; n++) {
-        const uint32_t m = 1u << (i & 31);
-        if (((n == 0 && fresh) || !(__builtin_nontemporal_load(&bits[i >> 5]) & m)) && !(atomicOr(&bits[i >> 5], m) & m))
-            return (uint32_t)i;
-        i = (i + 1) & (cap - 1);
-    }
-    return NO_SLOT;
+CHIP_DEV bool line_key_eq(const uint4& a, const uint4& b, uint32_t c, const uint32_t k[KW]) {
+    return ((a.x ^ k[0]) | (a.y ^ k[1]) | (a.z ^ k[2]) | (a.w ^ k[3]) | (b.x ^ k[4]) | (b.y ^ k[5]) | (b.z ^ k[6]) |
+            (b.w ^ k[7]) | (c ^ k[8])) == 0u;
 }
 
 // Slot writes of one wave, cooperatively: a lane's random 64-B line written by its own four 16-B stores
@@ -203,62 +196,100 @@ CHIP_DEV void wave_store_slots(uint32_t* tab, uint32_t slot, const uint32_t row[
     }
 }
 
-// lane-private slot write (rebuild / rehash, where claims mostly probe)
-CHIP_DEV void tab_put(uint32_t* tab, uint32_t* bits, uint64_t cap, uint64_t i0, const uint32_t k[KW],
-                      const uint32_t v[4], bool fresh) {
+// rehash: lane-private put of a distinct key (live or dead slot `v` = words 9..13) into a zeroed table.
+// The claim word is written back with the line, so a concurrent prober that read the slot before the
+// line landed still fails its CAS.
+CHIP_DEV void tab_put(uint32_t* tab, uint64_t cap, uint64_t i0, const uint32_t k[KW], const uint32_t v[5],
+                      unsigned long long claim) {
     uint64_t i = i0 & (cap - 1);
     for (uint64_t n = 0; n < cap; n++) {
-        const uint32_t m = 1u << (i & 31);
-        if (((n == 0 && fresh) || !(__builtin_nontemporal_load(&bits[i >> 5]) & m)) && !(atomicOr(&bits[i >> 5], m) & m)) {
-            // the whole 64-B line (zero tail): a partial line would cost a read-modify-write in HBM
-            uint4* s = reinterpret_cast<uint4*>(tab + i * SLOT_W);
-            s[0] = make_uint4(k[0], k[1], k[2], k[3]);
-            s[1] = make_uint4(k[4], k[5], k[6], k[7]);
-            s[2] = make_uint4(k[8], 1u, v[0], v[1]);
-            s[3] = make_uint4(v[2], v[3], 0u, 0u);
+        uint32_t* s = tab + i * SLOT_W;
+        if (!__builtin_nontemporal_load(s + S_USED) &&
+            atomicCAS(reinterpret_cast<unsigned long long*>(s + S_CLAIM), 0ull, claim) == 0ull) {
+            uint4* q = reinterpret_cast<uint4*>(s);   // the whole 64-B line
+            q[0] = make_uint4(k[0], k[1], k[2], k[3]);
+            q[1] = make_uint4(k[4], k[5], k[6], k[7]);
+            q[2] = make_uint4(k[8], v[0], v[1], v[2]);
+            q[3] = make_uint4(v[3], v[4], (uint32_t)claim, (uint32_t)(claim >> 32));
             return;
         }
         i = (i + 1) & (cap - 1);
     }
 }
 
-// lookup (pre-committed slot or NO_SLOT, and where an insert would start) fused with the batch
-// intern of the distinct states: bowner[s] = 1 + ref index of the first inserter.  A ref that finds
-// its state already interned marks itself and the first inserter in rdup (per ref, so every later
-// pass reads the flag coalesced instead of gathering a per-state flag)
+// own[r] bits: the ref claimed its slot (owner of the state in this batch), the slot was empty (a
+// write adds a slot), another key probed past the claim (the slot must be written back)
+#define OWN_CLAIM 1u
+#define OWN_FRESH 2u
+
+// lookup + intern + claim, one probe walk per ref:
+//   live slot of k       pre[r] = slot; sid[r] = 0x80000000 | slot (pre-committed; no claim)
+//   claimable slot       CAS the claim word: won -> sid[r] = r (r owns the state in this batch)
+//   claimed this epoch   key of the claimer equal -> sid[r] = claimer; both marked rdup (the state has
+//                        more than one referencer); else mark the claimer passed and walk on
+// sid[] ("state id") is what the rounds, records and inserts compare and index: equal for the refs of
+// one state, distinct across states; tslot[r] = the table slot of a non-pre-committed ref's state.
 __global__ void __launch_bounds__(256) k_uniq_lookup(uint64_t nref, const uint8_t* __restrict__ refs,
-                                                     const uint32_t* __restrict__ tab, uint64_t cap,
-                                                     uint32_t* __restrict__ pre, uint32_t* __restrict__ empty,
-                                                     uint32_t* bowner, uint8_t* __restrict__ rdup, uint64_t bcap,
-                                                     uint32_t* __restrict__ bslot, unsigned long long* __restrict__ bmin,
+                                                     uint32_t* tab, uint64_t cap, uint32_t epoch,
+                                                     uint32_t* __restrict__ pre, uint32_t* __restrict__ tslot,
+                                                     uint32_t* __restrict__ sid, uint8_t* __restrict__ rdup,
+                                                     uint8_t* __restrict__ own, uint8_t* __restrict__ passed,
+                                                     unsigned long long* __restrict__ bmin,
                                                      unsigned long long* __restrict__ bcommit) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nref) return;
     uint32_t k[KW];
     load_key(k, refs, r);
-    uint32_t e = NO_SLOT;
-    pre[r] = tab_find(tab, cap, k, &e);
-    if (empty) empty[r] = e;
-    uint64_t i = key_hash(k) >> 32 & (bcap - 1);
-    for (uint64_t n = 0; n < bcap; n++) {
-        const uint32_t prev = atomicCAS(&bowner[i], 0u, (uint32_t)(r + 1));
-        if (prev == 0u) {
-            bslot[r] = (uint32_t)i;
+    const unsigned long long mine = ((unsigned long long)epoch << 32) | (unsigned long long)(r + 1);
+    uint64_t i = key_hash(k) & (cap - 1);
+    for (uint64_t n = 0; n < cap; n++) {
+        uint32_t* s = tab + i * SLOT_W;
+        const uint4 a = *reinterpret_cast<const uint4*>(s);
+        const uint4 b = *reinterpret_cast<const uint4*>(s + 4);
+        const uint4 c = *reinterpret_cast<const uint4*>(s + 8);
+        const uint4 d = *reinterpret_cast<const uint4*>(s + 12);
+        const uint32_t used = c.y;
+        const bool eq = line_key_eq(a, b, c.x, k);
+        if (used == 1u && eq) {
+            pre[r] = (uint32_t)i;
+            sid[r] = 0x80000000u | (uint32_t)i;
+            tslot[r] = NO_SLOT;
             return;
         }
-        uint32_t ok[KW];
-        load_key(ok, refs, prev - 1);
-        if (key_eq(ok, k)) {
-            bslot[r] = (uint32_t)i;
-            rdup[r] = 1;
-            rdup[prev - 1] = 1;
-            // the round / commit scratch of a dup state starts "empty" (every referencer writes the
-            // same values): no memset of the whole scratch per batch or per round
-            bmin[i] = ~0ull;
-            bcommit[i] = ~0ull;
-            return;
+        if (used == 0u || (used == 2u && eq)) {
+            unsigned long long cw = ((unsigned long long)d.w << 32) | d.z;
+            for (;;) {
+                if ((uint32_t)(cw >> 32) == epoch) {
+                    const uint32_t o = (uint32_t)cw - 1u;
+                    uint32_t ok[KW];
+                    load_key(ok, refs, o);
+                    if (key_eq(ok, k)) {
+                        pre[r] = NO_SLOT;
+                        sid[r] = o;
+                        tslot[r] = (uint32_t)i;
+                        rdup[r] = 1;
+                        rdup[o] = 1;
+                        // the round / commit scratch of a dup state starts "empty" (every referencer
+                        // writes the same values): no memset of the scratch per batch or per round
+                        bmin[o] = ~0ull;
+                        bcommit[o] = ~0ull;
+                        return;
+                    }
+                    passed[o] = 1;
+                    break;
+                }
+                const unsigned long long prev = atomicCAS(reinterpret_cast<unsigned long long*>(s + S_CLAIM), cw, mine);
+                if (prev == cw) {
+                    pre[r] = NO_SLOT;
+                    sid[r] = (uint32_t)r;
+                    tslot[r] = (uint32_t)i;
+                    own[r] = (uint8_t)(OWN_CLAIM | (used == 0u ? OWN_FRESH : 0u));
+                    return;
+                }
+                cw = prev;
+            }
         }
-        i = (i + 1) & (bcap - 1);
+        i = (i + 1) & (cap - 1);
     }
 }
 
@@ -296,7 +327,7 @@ CHIP_DEV bool round_closed(const uint32_t* gate) { return gate && __builtin_nont
 // referencer of s, so a writer in this round) always sees this round's minimum.
 __global__ void __launch_bounds__(256) k_uniq_round_min(uint64_t nref, const uint8_t* __restrict__ rdup,
                                                         const uint32_t* __restrict__ ref_tx,
-                                                        const uint32_t* __restrict__ bslot,
+                                                        const uint32_t* __restrict__ sid,
                                                         const uint8_t* __restrict__ st,
                                                         unsigned long long* __restrict__ bmin, uint32_t tag,
                                                         const uint32_t* gate) {
@@ -304,13 +335,13 @@ __global__ void __launch_bounds__(256) k_uniq_round_min(uint64_t nref, const uin
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nref || !rdup[r]) return;
     const uint32_t t = ref_tx[r];
-    if (st[t] != ST_FAILED) atomicMin(&bmin[bslot[r]], ((unsigned long long)tag << 32) | t);
+    if (st[t] != ST_FAILED) atomicMin(&bmin[sid[r]], ((unsigned long long)tag << 32) | t);
 }
 
 // votes read only the previous round's status bytes (st is written by k_uniq_apply alone), so a
 // round's outcome does not depend on thread scheduling
 __global__ void __launch_bounds__(256) k_uniq_vote(uint64_t ntx, const uint64_t* __restrict__ start,
-                                                   const uint32_t* __restrict__ pre, const uint32_t* __restrict__ bslot,
+                                                   const uint32_t* __restrict__ pre, const uint32_t* __restrict__ sid,
                                                    const uint8_t* __restrict__ rdup,
                                                    const unsigned long long* __restrict__ bmin,
                                                    const uint8_t* __restrict__ st, uint8_t* __restrict__ vote,
@@ -323,7 +354,7 @@ __global__ void __launch_bounds__(256) k_uniq_vote(uint64_t ntx, const uint64_t*
         for (uint64_t r = start[t], e = start[t + 1]; r < e; r++) {
             if (pre[r] != NO_SLOT) { v = 2; break; }
             if (!rdup[r]) continue;   // t is the state's only referencer
-            const uint32_t m = (uint32_t)bmin[bslot[r]];
+            const uint32_t m = (uint32_t)bmin[sid[r]];
             if (m < t) {
                 if (st[m] == ST_COMMITTED) { v = 2; break; }
                 v = 1;
@@ -333,16 +364,16 @@ __global__ void __launch_bounds__(256) k_uniq_vote(uint64_t ntx, const uint64_t*
     vote[t] = v;
 }
 
-CHIP_DEV bool first_in_tx(const uint32_t* __restrict__ bslot, uint64_t a, uint64_t r) {
+CHIP_DEV bool first_in_tx(const uint32_t* __restrict__ sid, uint64_t a, uint64_t r) {
     for (uint64_t r2 = a; r2 < r; r2++)
-        if (bslot[r2] == bslot[r]) return false;
+        if (sid[r2] == sid[r]) return false;
     return true;
 }
 
 // bcommit[s] = (t << 32) | input index of s in the committing tx t, dup states only (the first
 // occurrence of s inside t; no other tx commits s, so plain stores)
 __global__ void __launch_bounds__(256) k_uniq_apply(uint64_t ntx, const uint64_t* __restrict__ start,
-                                                    const uint32_t* __restrict__ bslot, const uint32_t* __restrict__ pos,
+                                                    const uint32_t* __restrict__ sid, const uint32_t* __restrict__ pos,
                                                     const uint8_t* __restrict__ rdup,
                                                     const uint8_t* __restrict__ decision, uint8_t* __restrict__ st,
                                                     unsigned long long* __restrict__ bcommit,
@@ -355,8 +386,8 @@ __global__ void __launch_bounds__(256) k_uniq_apply(uint64_t ntx, const uint64_t
         if (d == 0) {
             const uint64_t a = start[t];
             for (uint64_t r = a, e = start[t + 1]; r < e; r++)
-                if (rdup[r] && first_in_tx(bslot, a, r))
-                    bcommit[bslot[r]] = ((unsigned long long)t << 32) | (unsigned long long)pos[r];
+                if (rdup[r] && first_in_tx(sid, a, r))
+                    bcommit[sid[r]] = ((unsigned long long)t << 32) | (unsigned long long)pos[r];
             st[t] = ST_COMMITTED;
         } else if (d >= 2) {
             st[t] = ST_FAILED;
@@ -389,7 +420,7 @@ struct Consumer {
 };
 CHIP_DEV bool consumed_before(uint64_t r, uint32_t t, const uint32_t* __restrict__ pre, const uint32_t* __restrict__ tab,
                               const uint8_t* __restrict__ txrows, const unsigned long long* __restrict__ bcommit,
-                              const uint32_t* __restrict__ bslot, const uint8_t* __restrict__ rdup,
+                              const uint32_t* __restrict__ sid, const uint8_t* __restrict__ rdup,
                               const uint8_t* __restrict__ tx_ids, const uint32_t* __restrict__ callers, Consumer& c) {
     if (pre[r] != NO_SLOT) {
         const uint32_t* v = tab + (uint64_t)pre[r] * SLOT_W;
@@ -400,7 +431,7 @@ CHIP_DEV bool consumed_before(uint64_t r, uint32_t t, const uint32_t* __restrict
         return true;
     }
     if (!rdup[r]) return false;
-    const unsigned long long bc = bcommit[bslot[r]];
+    const unsigned long long bc = bcommit[sid[r]];
     const uint32_t ct = (uint32_t)(bc >> 32);
     if (bc == ~0ull || ct >= t) return false;
     c.id = reinterpret_cast<const uint32_t*>(tx_ids + 32ull * ct);
@@ -415,7 +446,7 @@ CHIP_DEV bool consumed_before(uint64_t r, uint32_t t, const uint32_t* __restrict
 // first occurrence of a repeated state only.
 __global__ void __launch_bounds__(256) k_uniq_classify(uint64_t ntx, const uint64_t* __restrict__ start,
                                                        const uint32_t* __restrict__ pos, const uint32_t* __restrict__ pre,
-                                                       const uint32_t* __restrict__ bslot,
+                                                       const uint32_t* __restrict__ sid,
                                                        const uint8_t* __restrict__ rdup,
                                                        const unsigned long long* __restrict__ bcommit,
                                                        const uint8_t* __restrict__ tx_ids,
@@ -432,12 +463,12 @@ __global__ void __launch_bounds__(256) k_uniq_classify(uint64_t ntx, const uint6
         const uint64_t a = start[t];
         for (uint64_t r = a, e = start[t + 1]; r < e; r++) {
             Consumer c;
-            if (!consumed_before(r, (uint32_t)t, pre, tab, txrows, bcommit, bslot, rdup, tx_ids, callers, c)) continue;
+            if (!consumed_before(r, (uint32_t)t, pre, tab, txrows, bcommit, sid, rdup, tx_ids, callers, c)) continue;
             bool same = (c.idx == pos[r]) && (c.caller == callers[t]);
 #pragma unroll
             for (int q = 0; q < 8; q++) same = same && (c.id[q] == myid[q]);
             v = same ? (v > 1 ? v : 1) : 2;
-            n += first_in_tx(bslot, a, r);
+            n += first_in_tx(sid, a, r);
         }
     }
     vote[t] = v;
@@ -448,7 +479,7 @@ __global__ void __launch_bounds__(256) k_uniq_classify(uint64_t ntx, const uint6
 // a repeated state), so the whole array is ordered by (tx, input index)
 __global__ void __launch_bounds__(256) k_uniq_emit(uint64_t ntx, const uint64_t* __restrict__ start,
                                                    const uint32_t* __restrict__ pos, const uint32_t* __restrict__ pre,
-                                                   const uint32_t* __restrict__ bslot, const uint8_t* __restrict__ rdup,
+                                                   const uint32_t* __restrict__ sid, const uint8_t* __restrict__ rdup,
                                                    const unsigned long long* __restrict__ bcommit,
                                                    const uint8_t* __restrict__ tx_ids,
                                                    const uint32_t* __restrict__ callers,
@@ -461,8 +492,8 @@ __global__ void __launch_bounds__(256) k_uniq_emit(uint64_t ntx, const uint64_t*
     const uint64_t a = start[t];
     for (uint64_t r = a, e = start[t + 1]; r < e && o < cap; r++) {
         Consumer c;
-        if (!consumed_before(r, (uint32_t)t, pre, tab, txrows, bcommit, bslot, rdup, tx_ids, callers, c) ||
-            !first_in_tx(bslot, a, r))
+        if (!consumed_before(r, (uint32_t)t, pre, tab, txrows, bcommit, sid, rdup, tx_ids, callers, c) ||
+            !first_in_tx(sid, a, r))
             continue;
         chip_conflict cf;
         cf.tx = t;
@@ -477,37 +508,53 @@ __global__ void __launch_bounds__(256) k_uniq_emit(uint64_t ntx, const uint64_t*
     }
 }
 
-// inserts: inputs of COMMITTED txs, first occurrence of a state inside its tx
+// inserts, one writer per claimed slot and no atomics: the committing referencer of a state (first
+// occurrence inside the committed tx) writes it live; a state nothing committed is written back dead by
+// its owner when another key probed past the claim.  count[0] += live writes (the table's size),
+// count[1] += writes into empty slots (its occupancy)
 __global__ void __launch_bounds__(256) k_uniq_insert(uint64_t nref, const uint8_t* __restrict__ refs,
                                                      const uint32_t* __restrict__ ref_tx,
                                                      const uint32_t* __restrict__ pos, const uint64_t* __restrict__ start,
-                                                     const uint8_t* __restrict__ st, const uint32_t* __restrict__ bslot,
-                                                     const uint8_t* __restrict__ rdup,
-                                                     const uint32_t* __restrict__ empty, uint64_t row_base,
+                                                     const uint8_t* __restrict__ st, const uint32_t* __restrict__ sid,
+                                                     const uint8_t* __restrict__ rdup, const uint32_t* __restrict__ pre,
+                                                     const uint32_t* __restrict__ tslot, const uint8_t* __restrict__ own,
+                                                     const uint8_t* __restrict__ passed,
+                                                     const unsigned long long* __restrict__ bcommit, uint64_t row_base,
                                                      const uint32_t* __restrict__ callers, uint32_t* tab,
-                                                     uint32_t* bits, uint64_t cap,
-                                                     unsigned long long* __restrict__ inserted) {
+                                                     unsigned long long* __restrict__ count) {
     __shared__ uint32_t stage[4][64 * STAGE_W];
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint32_t slot = NO_SLOT;
+    uint32_t slot = NO_SLOT, live = 0, fresh = 0;
     uint32_t row[SLOT_W];
 #pragma unroll
     for (int w = 0; w < SLOT_W; w++) row[w] = 0;
-    if (r < nref) {
+    if (r < nref && pre[r] == NO_SLOT) {
         const uint32_t t = ref_tx[r];
-        if (st[t] == ST_COMMITTED && (!rdup[r] || first_in_tx(bslot, start[t], r))) {
+        const uint32_t o = sid[r];
+        bool write = false;
+        if (st[t] == ST_COMMITTED && (!rdup[r] || first_in_tx(sid, start[t], r))) {
+            write = true;
+            live = 1;
+        } else if (o == (uint32_t)r && (own[r] & OWN_FRESH)) {
+            write = passed[r] && (!rdup[r] || bcommit[o] == ~0ull);
+        }
+        if (write) {
             load_key(row, refs, r);
-            row[S_USED] = 1;
-            const uint64_t txrow = row_base + t;   // this batch's ids were appended to the side table at row_base
-            row[S_ROW] = (uint32_t)txrow;
-            row[S_ROW + 1] = (uint32_t)(txrow >> 32);
-            row[S_IDX] = pos[r];
-            row[S_CALLER] = callers[t];
-            slot = tab_claim(bits, cap, empty[r], true);
+            row[S_USED] = live ? 1u : 2u;
+            if (live) {
+                const uint64_t txrow = row_base + t;   // this batch's ids were appended to the side table at row_base
+                row[S_ROW] = (uint32_t)txrow;
+                row[S_ROW + 1] = (uint32_t)(txrow >> 32);
+                row[S_IDX] = pos[r];
+                row[S_CALLER] = callers[t];
+            }
+            fresh = (own[o] & OWN_FRESH) ? 1u : 0u;
+            slot = tslot[r];
         }
     }
     wave_store_slots(tab, slot, row, stage[threadIdx.x >> 6]);
-    spread_add(inserted, slot != NO_SLOT ? 1u : 0u);
+    spread_add(count, live);
+    spread_add(count + 1, fresh);
 }
 
 __global__ void __launch_bounds__(256) k_uniq_status(uint64_t ntx, const uint8_t* __restrict__ st,
@@ -517,42 +564,48 @@ __global__ void __launch_bounds__(256) k_uniq_status(uint64_t ntx, const uint8_t
     out[t] = st[t] == ST_COMMITTED ? 0 : (decision[t] >= 2 ? 2 : 1);
 }
 
-// rebuild (AppendOnlyPersistentMap.allPersisted): rows absent from the table, first of equal keys
+// rebuild (AppendOnlyPersistentMap.allPersisted): rows absent from the table, the owner of equal keys
 __global__ void __launch_bounds__(256) k_uniq_rebuild(uint64_t n, const uint8_t* __restrict__ refs,
                                                       uint64_t row_base, const uint32_t* __restrict__ idx,
                                                       const uint32_t* __restrict__ caller, const uint32_t* __restrict__ pre,
-                                                      const uint32_t* __restrict__ bslot,
-                                                      const uint32_t* __restrict__ bowner, uint32_t* tab, uint32_t* bits,
-                                                      uint64_t cap, unsigned long long* __restrict__ inserted) {
+                                                      const uint32_t* __restrict__ tslot, const uint8_t* __restrict__ own,
+                                                      uint32_t* tab, unsigned long long* __restrict__ count) {
+    __shared__ uint32_t stage[4][64 * STAGE_W];
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    bool ins = false;
-    if (r < n && pre[r] == NO_SLOT && bowner[bslot[r]] == (uint32_t)(r + 1)) {
-        uint32_t k[KW], v[4];
-        load_key(k, refs, r);
+    uint32_t slot = NO_SLOT, live = 0, fresh = 0;
+    uint32_t row[SLOT_W];
+#pragma unroll
+    for (int w = 0; w < SLOT_W; w++) row[w] = 0;
+    if (r < n && pre[r] == NO_SLOT && (own[r] & OWN_CLAIM)) {
+        load_key(row, refs, r);
+        row[S_USED] = 1;
         const uint64_t txrow = row_base + r;   // the rebuild's ids were appended to the side table at row_base
-        v[0] = (uint32_t)txrow;
-        v[1] = (uint32_t)(txrow >> 32);
-        v[2] = idx[r];
-        v[3] = caller[r];
-        tab_put(tab, bits, cap, key_hash(k), k, v, false);
-        ins = true;
+        row[S_ROW] = (uint32_t)txrow;
+        row[S_ROW + 1] = (uint32_t)(txrow >> 32);
+        row[S_IDX] = idx[r];
+        row[S_CALLER] = caller[r];
+        slot = tslot[r];
+        live = 1;
+        fresh = (own[r] & OWN_FRESH) ? 1u : 0u;
     }
-    spread_add(inserted, ins ? 1u : 0u);
+    wave_store_slots(tab, slot, row, stage[threadIdx.x >> 6]);
+    spread_add(count, live);
+    spread_add(count + 1, fresh);
 }
 
-// rehash every used slot of an old table into a new one
+// rehash every used slot (live or dead) of an old table into a new one
 __global__ void __launch_bounds__(256) k_uniq_rehash(uint64_t ocap, const uint32_t* __restrict__ old, uint32_t* tab,
-                                                     uint32_t* bits, uint64_t cap) {
+                                                     uint64_t cap, unsigned long long claim) {
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= ocap) return;
     const uint32_t* o = old + s * SLOT_W;
     if (!o[S_USED]) return;
-    uint32_t k[KW], v[4];
+    uint32_t k[KW], v[5];
 #pragma unroll
     for (int q = 0; q < KW; q++) k[q] = o[q];
 #pragma unroll
-    for (int q = 0; q < 4; q++) v[q] = o[S_ROW + q];
-    tab_put(tab, bits, cap, key_hash(k), k, v, false);
+    for (int q = 0; q < 5; q++) v[q] = o[S_USED + q];
+    tab_put(tab, cap, key_hash(k), k, v, claim);
 }
 
 // ---------------------------------------------------------------------------------------
@@ -583,34 +636,33 @@ static int spread_fetch(chip_uniq* u, hipStream_t st) {
     UCHK(u, hipMemcpyAsync(u->h_spread, u->spread.p, SPREAD * 64, hipMemcpyDeviceToHost, st));
     return CHIP_OK;
 }
-static unsigned long long spread_total(const chip_uniq* u) {
+static unsigned long long spread_total(const unsigned long long* h, int which = 0) {
     unsigned long long t = 0;
-    for (int i = 0; i < SPREAD; i++) t += u->h_spread[i * 8];
+    for (int i = 0; i < SPREAD; i++) t += h[i * 8 + which];
     return t;
 }
+static unsigned long long spread_total(const chip_uniq* u, int which = 0) { return spread_total(u->h_spread, which); }
+static uint32_t next_epoch(chip_uniq* u) {
+    if (++u->epoch == 0) u->epoch = 1;   // 2^32 launches: an epoch is reused only after that many
+    return u->epoch;
+}
 
-// make room for `extra` more entries at load factor <= 1/2
+// make room for `extra` more used slots at load factor <= 1/2
 static int ensure_capacity(chip_uniq* u, uint64_t extra, hipStream_t st) {
-    if (2 * (u->size + extra) <= u->cap) return CHIP_OK;
-    const uint64_t ncap = pow2_at_least(2 * (u->size + extra));
+    if (2 * (u->slots + extra) <= u->cap) return CHIP_OK;
+    const uint64_t ncap = pow2_at_least(2 * (u->slots + extra));
+    if (ncap > (1ull << 31)) return ufail(u, CHIP_E_CAPACITY, "table above 2^31 slots");
     uint32_t* t = nullptr;
-    uint32_t* bits = nullptr;
     UCHK(u, hipMalloc(&t, ncap * SLOT_W * 4));
-    if (hipMalloc(&bits, ncap / 8) != hipSuccess) {
-        hipFree(t);
-        return ufail(u, CHIP_E_NOMEM, "occupancy bitmap");
-    }
     UCHK(u, hipMemsetAsync(t, 0, ncap * SLOT_W * 4, st));
-    UCHK(u, hipMemsetAsync(bits, 0, ncap / 8, st));
     if (u->cap) {
-        hipLaunchKernelGGL(k_uniq_rehash, dim3(blocks_for(u->cap)), dim3(256), 0, st, u->cap, u->tab, t, bits, ncap);
+        const unsigned long long claim = ((unsigned long long)next_epoch(u) << 32) | 1ull;
+        hipLaunchKernelGGL(k_uniq_rehash, dim3(blocks_for(u->cap)), dim3(256), 0, st, u->cap, u->tab, t, ncap, claim);
         UCHK(u, hipGetLastError());
         UCHK(u, hipStreamSynchronize(st));
         hipFree(u->tab);
-        hipFree(u->bits);
     }
     u->tab = t;
-    u->bits = bits;
     u->cap = ncap;
     return CHIP_OK;
 }
@@ -635,22 +687,34 @@ extern "C" int chip_ctx_device(const chip_ctx* c);
 
 // batch scratch for nref local inputs and ntx transactions
 static int batch_scratch(chip_uniq* u, uint64_t ntx, uint64_t nref) {
-    const uint64_t bcap = pow2_at_least(2 * (nref + 1));
     UCHK(u, u->reftx.ensure(nref * 4 + 16));
     UCHK(u, u->pre.ensure(nref * 4 + 16));
-    UCHK(u, u->empty.ensure(nref * 4 + 16));
+    UCHK(u, u->tslot.ensure(nref * 4 + 16));
+    UCHK(u, u->sid.ensure(nref * 4 + 16));
     UCHK(u, u->rdup.ensure(nref + 16));
-    UCHK(u, u->bslot.ensure(nref * 4 + 16));
+    UCHK(u, u->own.ensure(nref + 16));
+    UCHK(u, u->passed.ensure(nref + 16));
     UCHK(u, u->flag.ensure(std::max(nref, ntx) * 4 + 16));   // per-tx record counts
     UCHK(u, u->scan.ensure(std::max(nref, ntx) * 4 + 16));
-    UCHK(u, u->bowner.ensure(bcap * 4));
-    UCHK(u, u->bmin.ensure(bcap * 8));
+    UCHK(u, u->bmin.ensure(nref * 8 + 16));                  // per state, indexed by its owner ref
     UCHK(u, u->gate.ensure(64));
-    UCHK(u, u->bcommit.ensure(bcap * 8));
+    UCHK(u, u->bcommit.ensure(nref * 8 + 16));
     UCHK(u, u->st.ensure(ntx + 16));
     UCHK(u, u->ctr.ensure(64));
     UCHK(u, u->spread.ensure(SPREAD * 64));
-    u->bcap = bcap;
+    UCHK(u, u->icount.ensure(SPREAD * 64));
+    return CHIP_OK;
+}
+
+// the lookup / intern / claim pass over n refs (per-batch flags cleared first)
+static int launch_lookup(chip_uniq* u, uint64_t n, const uint8_t* refs, hipStream_t st) {
+    UCHK(u, hipMemsetAsync(u->rdup.p, 0, n, st));
+    UCHK(u, hipMemsetAsync(u->passed.p, 0, n, st));
+    hipLaunchKernelGGL(k_uniq_lookup, dim3(blocks_for(n)), dim3(256), 0, st, n, refs, u->tab, u->cap, next_epoch(u),
+                       u->pre.as<uint32_t>(), u->tslot.as<uint32_t>(), u->sid.as<uint32_t>(), u->rdup.as<uint8_t>(),
+                       u->own.as<uint8_t>(), u->passed.as<uint8_t>(), u->bmin.as<unsigned long long>(),
+                       u->bcommit.as<unsigned long long>());
+    UCHK(u, hipGetLastError());
     return CHIP_OK;
 }
 
@@ -669,11 +733,19 @@ int chip_uniq_open(chip_ctx* ctx, uint64_t capacity, chip_uniq** out) {
     int r = ensure_capacity(u, capacity ? capacity : 1024, u->stream);
     if (!r && hipHostMalloc((void**)&u->h_spread, SPREAD * 64, hipHostMallocDefault) != hipSuccess) r = CHIP_E_NOMEM;
     if (!r && hipHostMalloc((void**)&u->h_gate, 64, hipHostMallocDefault) != hipSuccess) r = CHIP_E_NOMEM;
+    if (!r && hipHostMalloc((void**)&u->h_icount, SPREAD * 64, hipHostMallocDefault) != hipSuccess) r = CHIP_E_NOMEM;
+    if (!r && (hipStreamCreateWithFlags(&u->ist, hipStreamNonBlocking) != hipSuccess ||
+               hipEventCreateWithFlags(&u->iev0, hipEventDisableTiming) != hipSuccess ||
+               hipEventCreateWithFlags(&u->iev1, hipEventDisableTiming) != hipSuccess))
+        r = CHIP_E_DEVICE;
     if (r || hipStreamSynchronize(u->stream) != hipSuccess) {
         if (u->tab) hipFree(u->tab);
-        if (u->bits) hipFree(u->bits);
         if (u->h_spread) hipHostFree(u->h_spread);
         if (u->h_gate) hipHostFree(u->h_gate);
+        if (u->h_icount) hipHostFree(u->h_icount);
+        if (u->ist) hipStreamDestroy(u->ist);
+        if (u->iev0) hipEventDestroy(u->iev0);
+        if (u->iev1) hipEventDestroy(u->iev1);
         hipStreamDestroy(u->stream);
         delete u;
         return r ? r : CHIP_E_DEVICE;
@@ -687,14 +759,18 @@ void chip_uniq_close(chip_uniq* u) {
     hipSetDevice(u->device);
     hipStreamSynchronize(u->stream);
     if (u->tab) hipFree(u->tab);
-    if (u->bits) hipFree(u->bits);
     if (u->txrows) hipFree(u->txrows);
     if (u->h_spread) hipHostFree(u->h_spread);
     if (u->h_gate) hipHostFree(u->h_gate);
-    UBuf* bufs[] = {&u->reftx,  &u->pre,    &u->empty,  &u->bslot, &u->bowner, &u->rdup,   &u->spread,
+    if (u->h_icount) hipHostFree(u->h_icount);
+    hipStreamSynchronize(u->ist);
+    hipStreamDestroy(u->ist);
+    hipEventDestroy(u->iev0);
+    hipEventDestroy(u->iev1);
+    UBuf* bufs[] = {&u->reftx,  &u->pre,    &u->tslot,  &u->sid, &u->own, &u->passed, &u->rdup, &u->spread,
                     &u->bmin,   &u->bcommit, &u->st,    &u->flag,  &u->scan,   &u->cub,    &u->ctr,
                     &u->refpos, &u->h_start, &u->h_refs, &u->h_ids, &u->h_call, &u->h_st,  &u->h_vote,
-                    &u->h_out,  &u->gate};
+                    &u->h_out,  &u->gate, &u->icount};
     for (UBuf* b : bufs) b->release();
     hipStreamDestroy(u->stream);
     delete u;
@@ -722,23 +798,19 @@ int chip_uniq_rebuild(chip_uniq* u, uint64_t n, const uint8_t* refs36, const uin
     UCHK(u, hipMemcpyAsync(u->h_ids.p, tx32, n * 32, hipMemcpyHostToDevice, st));
     UCHK(u, hipMemcpyAsync(u->refpos.p, idx, n * 4, hipMemcpyHostToDevice, st));
     UCHK(u, hipMemcpyAsync(u->h_call.p, caller, n * 4, hipMemcpyHostToDevice, st));
-    UCHK(u, hipMemsetAsync(u->bowner.p, 0, u->bcap * 4, st));
-    UCHK(u, hipMemsetAsync(u->rdup.p, 0, n, st));
     if ((r = spread_zero(u, st))) return r;
     const uint8_t* d_refs = u->h_refs.as<uint8_t>();
-    hipLaunchKernelGGL(k_uniq_lookup, dim3(blocks_for(n)), dim3(256), 0, st, n, d_refs, u->tab, u->cap,
-                       u->pre.as<uint32_t>(), (uint32_t*)nullptr, u->bowner.as<uint32_t>(), u->rdup.as<uint8_t>(),
-                       u->bcap, u->bslot.as<uint32_t>(), u->bmin.as<unsigned long long>(),
-                       u->bcommit.as<unsigned long long>());
+    if ((r = launch_lookup(u, n, d_refs, st))) return r;
     if ((r = ensure_rows(u, n, st))) return r;
     UCHK(u, hipMemcpyAsync(u->txrows + u->rows * 32, u->h_ids.p, n * 32, hipMemcpyDeviceToDevice, st));
     hipLaunchKernelGGL(k_uniq_rebuild, dim3(blocks_for(n)), dim3(256), 0, st, n, d_refs, u->rows,
-                       u->refpos.as<uint32_t>(), u->h_call.as<uint32_t>(), u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(),
-                       u->bowner.as<uint32_t>(), u->tab, u->bits, u->cap, u->spread.as<unsigned long long>());
+                       u->refpos.as<uint32_t>(), u->h_call.as<uint32_t>(), u->pre.as<uint32_t>(),
+                       u->tslot.as<uint32_t>(), u->own.as<uint8_t>(), u->tab, u->spread.as<unsigned long long>());
     UCHK(u, hipGetLastError());
     if ((r = spread_fetch(u, st))) return r;
     UCHK(u, hipStreamSynchronize(st));
-    u->size += spread_total(u);
+    u->size += spread_total(u, 0);
+    u->slots += spread_total(u, 1);
     u->rows += n;
     return CHIP_OK;
 }
@@ -758,25 +830,19 @@ int chip_uniq_shard_begin(chip_uniq* u, const chip_uniq_shard_batch* b, void* st
     u->ntx = ntx;
     u->nref = nref;
     u->bst = st;
+    u->inserted = false;
     u->start = b->ref_start;
     u->refs = b->refs36;
     u->pos = b->ref_pos;
     u->ids = b->tx_ids;
     u->callers = b->callers;
-    UCHK(u, hipMemsetAsync(u->bowner.p, 0, u->bcap * 4, st));
-    if (nref) UCHK(u, hipMemsetAsync(u->rdup.p, 0, nref, st));
     u->round = 0;
     if (ntx) UCHK(u, hipMemsetAsync(u->st.p, ST_UNDECIDED, ntx, st));
     UCHK(u, hipMemsetAsync(u->ctr.p, 0, 64, st));
     if (ntx)
         hipLaunchKernelGGL(k_ref_tx, dim3(blocks_for(ntx)), dim3(256), 0, st, ntx, u->start, u->reftx.as<uint32_t>(),
                            (uint32_t*)nullptr);
-    if (nref) {
-        hipLaunchKernelGGL(k_uniq_lookup, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->refs, u->tab, u->cap,
-                           u->pre.as<uint32_t>(), u->empty.as<uint32_t>(), u->bowner.as<uint32_t>(),
-                           u->rdup.as<uint8_t>(), u->bcap, u->bslot.as<uint32_t>(), u->bmin.as<unsigned long long>(),
-                           u->bcommit.as<unsigned long long>());
-    }
+    if (nref && (r = launch_lookup(u, nref, u->refs, st))) return r;
     UCHK(u, hipGetLastError());
     u->open = true;
     return CHIP_OK;
@@ -789,17 +855,17 @@ static void launch_round_vote(chip_uniq* u, uint8_t* vote, const uint32_t* gate)
     const uint32_t tag = ~u->round;
     if (u->nref)
         hipLaunchKernelGGL(k_uniq_round_min, dim3(blocks_for(u->nref)), dim3(256), 0, st, u->nref, u->rdup.as<uint8_t>(),
-                           u->reftx.as<uint32_t>(), u->bslot.as<uint32_t>(), u->st.as<uint8_t>(),
+                           u->reftx.as<uint32_t>(), u->sid.as<uint32_t>(), u->st.as<uint8_t>(),
                            u->bmin.as<unsigned long long>(), tag, gate);
     if (u->ntx)
         hipLaunchKernelGGL(k_uniq_vote, dim3(blocks_for(u->ntx)), dim3(256), 0, st, u->ntx, u->start,
-                           u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->rdup.as<uint8_t>(),
+                           u->pre.as<uint32_t>(), u->sid.as<uint32_t>(), u->rdup.as<uint8_t>(),
                            u->bmin.as<unsigned long long>(), u->st.as<uint8_t>(), vote, gate);
 }
 static void launch_apply(chip_uniq* u, const uint8_t* decision, const uint32_t* gate) {
     if (u->ntx)
         hipLaunchKernelGGL(k_uniq_apply, dim3(blocks_for(u->ntx)), dim3(256), 0, u->bst, u->ntx, u->start,
-                           u->bslot.as<uint32_t>(), u->pos, u->rdup.as<uint8_t>(), decision, u->st.as<uint8_t>(),
+                           u->sid.as<uint32_t>(), u->pos, u->rdup.as<uint8_t>(), decision, u->st.as<uint8_t>(),
                            u->bcommit.as<unsigned long long>(), u->spread.as<unsigned long long>(), gate);
 }
 
@@ -830,10 +896,44 @@ int chip_uniq_shard_classify(chip_uniq* u, uint8_t* vote) {
     if (!u->open || (u->ntx && !vote)) return ufail(u, CHIP_E_ARG, "no batch in flight / null vote");
     if (u->ntx)
         hipLaunchKernelGGL(k_uniq_classify, dim3(blocks_for(u->ntx)), dim3(256), 0, u->bst, u->ntx, u->start, u->pos,
-                           u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->rdup.as<uint8_t>(),
+                           u->pre.as<uint32_t>(), u->sid.as<uint32_t>(), u->rdup.as<uint8_t>(),
                            u->bcommit.as<unsigned long long>(), u->ids,
                            u->callers, u->tab, u->txrows, u->st.as<uint8_t>(), vote, u->flag.as<uint32_t>());
     UCHK(u, hipGetLastError());
+    return CHIP_OK;
+}
+
+// the batch's ConsumingTx ids appended to the side table and the inserts of its committed inputs (after the
+// last round: they read the final statuses and bcommit).  On `ist` (forked from the batch stream) when
+// `side`, so that they overlap the records: those read pre-committed (live) slots and the side table's
+// older rows only, the inserts write claimed (not live) slots and the new rows.  Joined in finish.
+static int launch_insert(chip_uniq* u, bool side) {
+    const uint64_t nref = u->nref, ntx = u->ntx;
+    u->inserted = true;
+    if (!nref || !ntx) return CHIP_OK;
+    hipStream_t st = u->bst;
+    int rc = ensure_rows(u, ntx, st);   // may reallocate the side table: before any kernel that reads it
+    if (rc) return rc;
+    const uint64_t row_base = u->rows;
+    if (side) {
+        UCHK(u, hipEventRecord(u->iev0, st));
+        UCHK(u, hipStreamWaitEvent(u->ist, u->iev0, 0));
+        st = u->ist;
+    }
+    UCHK(u, hipMemsetAsync(u->icount.p, 0, SPREAD * 64, st));
+    UCHK(u, hipMemcpyAsync(u->txrows + row_base * 32, u->ids, ntx * 32, hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(k_uniq_insert, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->refs, u->reftx.as<uint32_t>(),
+                       u->pos, u->start, u->st.as<uint8_t>(), u->sid.as<uint32_t>(), u->rdup.as<uint8_t>(),
+                       u->pre.as<uint32_t>(), u->tslot.as<uint32_t>(), u->own.as<uint8_t>(), u->passed.as<uint8_t>(),
+                       u->bcommit.as<unsigned long long>(), row_base, u->callers, u->tab,
+                       u->icount.as<unsigned long long>());
+    UCHK(u, hipGetLastError());
+    UCHK(u, hipMemcpyAsync(u->h_icount, u->icount.p, SPREAD * 64, hipMemcpyDeviceToHost, st));
+    if (side) {
+        UCHK(u, hipEventRecord(u->iev1, st));
+        UCHK(u, hipStreamWaitEvent(u->bst, u->iev1, 0));
+    }
+    u->rows += ntx;
     return CHIP_OK;
 }
 
@@ -847,40 +947,32 @@ int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_st
     u->open = false;
     uint32_t* nrec = u->flag.as<uint32_t>();   // per-tx record counts (k_uniq_classify)
     uint32_t* at = u->scan.as<uint32_t>();
-    int rc = spread_zero(u, st);
-    if (rc) return rc;
+    int rc;
+    if (!u->inserted && (rc = launch_insert(u, false))) return rc;   // the phase API: in order on the batch stream
     uint32_t last[2] = {0, 0};
-    uint64_t row_base = u->rows;
     if (nref && ntx) {
-        // the batch's ConsumingTx ids into the side table (one coalesced copy); inserted slots name rows
-        if ((rc = ensure_rows(u, ntx, st))) return rc;
-        row_base = u->rows;
-        UCHK(u, hipMemcpyAsync(u->txrows + row_base * 32, u->ids, ntx * 32, hipMemcpyDeviceToDevice, st));
         size_t tmp = 0;
         UCHK(u, hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, nrec, at, (int)ntx, st));
         UCHK(u, u->cub.ensure(tmp + 16));
         UCHK(u, hipcub::DeviceScan::ExclusiveSum(u->cub.p, tmp, nrec, at, (int)ntx, st));
         hipLaunchKernelGGL(k_uniq_emit, dim3(blocks_for(ntx)), dim3(256), 0, st, ntx, u->start, u->pos,
-                           u->pre.as<uint32_t>(), u->bslot.as<uint32_t>(), u->rdup.as<uint8_t>(),
+                           u->pre.as<uint32_t>(), u->sid.as<uint32_t>(), u->rdup.as<uint8_t>(),
                            u->bcommit.as<unsigned long long>(), u->ids, u->callers, u->tab, u->txrows, nrec, at, out,
                            cap);
-        // inserts after the records: emit reads pre-committed slots, inserts only fill empty ones
-        hipLaunchKernelGGL(k_uniq_insert, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->refs, u->reftx.as<uint32_t>(),
-                           u->pos, u->start, u->st.as<uint8_t>(), u->bslot.as<uint32_t>(), u->rdup.as<uint8_t>(),
-                           u->empty.as<uint32_t>(), row_base, u->callers, u->tab, u->bits, u->cap,
-                           u->spread.as<unsigned long long>());
-        u->rows += ntx;
         UCHK(u, hipMemcpyAsync(&last[0], at + ntx - 1, 4, hipMemcpyDeviceToHost, st));
         UCHK(u, hipMemcpyAsync(&last[1], nrec + ntx - 1, 4, hipMemcpyDeviceToHost, st));
-        if ((rc = spread_fetch(u, st))) return rc;
     }
     if (ntx)
         hipLaunchKernelGGL(k_uniq_status, dim3(blocks_for(ntx)), dim3(256), 0, st, ntx, u->st.as<uint8_t>(), decision,
                            tx_status);
     UCHK(u, hipGetLastError());
     UCHK(u, hipStreamSynchronize(st));
+    UCHK(u, hipStreamSynchronize(u->ist));
     const uint64_t nout = (uint64_t)last[0] + last[1];
-    if (nref) u->size += spread_total(u);
+    if (nref && ntx) {
+        u->size += spread_total(u->h_icount, 0);
+        u->slots += spread_total(u->h_icount, 1);
+    }
     *n_out = nout;
     return nout > cap ? ufail(u, CHIP_E_CAPACITY, "more conflict records than capacity") : CHIP_OK;
 }
@@ -920,6 +1012,10 @@ static int commit_device(chip_uniq* u, const chip_uniq_shard_batch* b, uint8_t* 
             return ufail(u, CHIP_E_DEVICE, "ordered-commit rounds");
         }
         if (!*u->h_gate) break;
+    }
+    if ((r = launch_insert(u, true))) {
+        u->open = false;
+        return r;
     }
     if ((r = chip_uniq_shard_classify(u, vote))) {
         u->open = false;

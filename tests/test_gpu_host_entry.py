@@ -44,3 +44,58 @@ def test_bad_arguments_rejected_then_valid_call(ctx):
     assert np.array_equal(st, b.expected)
     s = ctx.stats()
     assert [int(s.status_count[k]) for k in range(8)] == list(np.bincount(st, minlength=8))
+
+
+def _permuted(b, seed):
+    """The same signatures in a shuffled order: sig offsets and message indices no longer ascend, so
+    every chunk's pool ranges overlap the others' (the copied intervals grow on both sides)."""
+    p = np.random.Generator(np.random.PCG64(seed)).permutation(len(b.key_idx))
+    x = copy.copy(b)
+    for f in ("key_idx", "msg_idx", "sig_off", "sig_len", "expected"):
+        setattr(x, f, np.ascontiguousarray(getattr(b, f)[p]))
+    return x
+
+
+def _chunked(ctx, b, chunks, monkeypatch):
+    monkeypatch.setenv("CHIP_HOST_CHUNKS", str(chunks))
+    return ctx.verify_batch(b)
+
+
+@pytest.mark.parametrize("permute", [False, True])
+def test_host_chunk_pipeline_equals_one_chunk(ctx, monkeypatch, permute):
+    """chip_verify_batch in chunks (H2D of chunk j+1 beside the kernels of chunk j; key tables built by
+    the first chunk and reused): statuses and bitmap equal the one-chunk call and the labels, on a batch
+    that takes the eager per-key comb tables (80k signatures over 64 keys)."""
+    b = G.ed25519_batch(80000, n_keys=64, corrupt=0.1, seed=0x5EED0501)
+    if permute:
+        b = _permuted(b, 5)
+    st1, bm1 = _chunked(ctx, b, 1, monkeypatch)
+    assert np.array_equal(st1, b.expected)
+    for k in (3, 7):
+        st, bm = _chunked(ctx, b, k, monkeypatch)
+        assert np.array_equal(st, st1), k
+        assert np.array_equal(bm, bm1), k
+
+
+def test_host_chunk_pipeline_ecdsa_tables_reused(ctx, monkeypatch):
+    """ECDSA (P-256 + secp256k1) in 4 chunks: the per-key comb tables of the first chunk serve the rest."""
+    b = G.ecdsa_batch(72000, n_keys=32, corrupt=0.1, seed=0x5EED0502)
+    st1, bm1 = _chunked(ctx, b, 1, monkeypatch)
+    assert np.array_equal(st1, b.expected)
+    st, bm = _chunked(ctx, b, 4, monkeypatch)
+    assert np.array_equal(st, st1)
+    assert np.array_equal(bm, bm1)
+
+
+def test_host_chunk_pipeline_rejects_bad_index_in_a_later_chunk(ctx, monkeypatch):
+    """A bad index in the last chunk is found by that chunk's device check: CHIP_E_ARG, and the next
+    call is unaffected."""
+    b = G.ed25519_batch(20000, n_keys=16, corrupt=0.1, seed=0x5EED0503)
+    x = copy.copy(b)
+    x.msg_idx = b.msg_idx.copy()
+    x.msg_idx[-3] = len(b.msg_off) + 1
+    with pytest.raises(native.ChipError) as e:
+        _chunked(ctx, x, 5, monkeypatch)
+    assert "range" in str(e.value)
+    st, _ = _chunked(ctx, b, 5, monkeypatch)
+    assert np.array_equal(st, b.expected)

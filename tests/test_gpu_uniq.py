@@ -68,6 +68,25 @@ def test_uniq_multi_batch_and_growth(ctx, oracle):
         assert g[1] == r[1]
 
 
+def test_uniq_failed_inputs_then_consumed(ctx, oracle):
+    """Inputs of failed txs are claimed in the batch but never consumed: their slots stay empty or are
+    written back dead (when another key's probe walked past the claim).  Later batches consume those
+    states, and new keys probe through the dead slots, at a load factor kept near 1/2: statuses,
+    records and the live size equal the oracle after every batch."""
+    pre, b0 = G.uniq_workload(6000, 3000, seed=21, pre_hit=0.3, dbl=0.05, resubmit=0.01)
+    batches = [b0]
+    for s in range(22, 26):
+        _, bs = G.uniq_workload(6000, 0, seed=s, pre_hit=0.0, dbl=0.05)
+        k = 3000
+        bs.refs[:36 * k] = b0.refs[36 * (s - 22) * 500:36 * ((s - 22) * 500 + k)]
+        batches.append(bs)
+    outs = run_both(ctx, oracle, pre, batches, cap=1 << 13)
+    for g, r in outs:
+        assert np.array_equal(g[0], r[0])
+        assert g[1] == r[1]
+    assert (outs[0][0][0] == CONFLICT).sum() > 1000
+
+
 def test_uniq_device_entry_matches_host_entry(ctx, oracle):
     """chip_uniq_commit_batch_device (inputs resident in HBM) == the host entry == the oracle."""
     import torch
