@@ -352,8 +352,9 @@ def main():
             "cfg2_host_path_ms": hel * 1e3,
             "cfg2_host_path_bytes_in": int(batch.sig_data.nbytes + batch.msg_data.nbytes + batch.key_data.nbytes +
                                            16 * n),
-            "cfg2_host_path_note": "chip_verify_batch from pageable host buffers: H2D of every pool + index array, "
-                                   "the same pipeline, D2H of status + bitmap",
+            "cfg2_host_path_note": "chip_verify_batch from pageable host buffers: H2D of every pool + index array "
+                                   "in signature chunks, each chunk's copy beside the previous chunk's kernels "
+                                   "(key tables built once), D2H of status + bitmap",
             "cfg2_host_path_correct": bool(np.array_equal(hst, batch.expected)),
         })
         # the same from page-locked host buffers (chip_alloc_pinned: the JNI layer's direct ByteBuffers)

@@ -449,6 +449,7 @@ const char* chip_last_error(const chip_ctx* c) { return c ? c->err.c_str() : "nu
 struct VerifyChunk {
     uint64_t n_decide;
     bool reuse_keys;
+    hipEvent_t data_ready;   // the chunk's signatures / pools are on the device (waited for after the key prep)
 };
 
 static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap, hipStream_t st,
@@ -571,6 +572,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         HIPCHK(c, hipEventRecord(c->ev_join2, fs));
     }
     c->kend(ke, st);
+    if (vc && vc->data_ready) HIPCHK(c, hipStreamWaitEvent(st, vc->data_ready, 0));
     if (n) {
         const uint32_t blocks = (uint32_t)((n + CLASSIFY_BLOCK - 1) / CLASSIFY_BLOCK);
         uint32_t* lists = c->lists.as<uint32_t>();
@@ -835,10 +837,23 @@ static int verify_host_pipelined(chip_ctx* c, const chip_sig_batch* b, uint8_t* 
     HIPCHK(c, hipStreamWaitEvent(cs, c->hev_p, 0));
     int r;
     if ((r = stage(c, c->h_key_data, b->key_data, b->key_bytes, cs)) || (r = stage(c, c->h_key_off, b->key_off, nk, cs)) ||
-        (r = stage(c, c->h_key_len, b->key_len, nk, cs)) || (r = stage(c, c->h_msg_off, b->msg_off, nm, cs)) ||
-        (r = stage(c, c->h_msg_len, b->msg_len, nm, cs)))
+        (r = stage(c, c->h_key_len, b->key_len, nk, cs)))
         return r;
-    const uint64_t csz = ((n + chunks - 1) / chunks + 63) & ~63ull;
+    HIPCHK(c, hipEventRecord(c->hev_c, cs));
+    HIPCHK(c, hipStreamWaitEvent(st, c->hev_c, 0));   // the key prep and the table chains start on the keys alone
+    if ((r = stage(c, c->h_msg_off, b->msg_off, nm, cs)) || (r = stage(c, c->h_msg_len, b->msg_len, nm, cs))) return r;
+    // chunk boundaries (multiples of 64): a first chunk of ~1/(2 chunks) of the batch, so that the kernels start
+    // early, then equal chunks
+    std::vector<uint64_t> at{0};
+    {
+        const uint64_t first = std::max<uint64_t>(64, (n / (2 * chunks) + 63) & ~63ull);
+        const uint64_t rest = ((n - std::min(n, first)) + (chunks - 1) - 1) / std::max<uint64_t>(1, chunks - 1);
+        const uint64_t rsz = std::max<uint64_t>(64, (rest + 63) & ~63ull);
+        for (uint64_t x = std::min(n, first); ; x = std::min(n, x + rsz)) {
+            at.push_back(x);
+            if (x == n) break;
+        }
+    }
     uint64_t sig_lo = 0, sig_hi = 0, msg_lo = 0, msg_hi = 0;   // copied intervals (empty: lo == hi == 0, none yet)
     bool sig_any = false, msg_any = false;
     // copies [lo, hi) of a pool that the interval [*clo, *chi) does not cover yet, and grows it
@@ -861,7 +876,7 @@ static int verify_host_pipelined(chip_ctx* c, const chip_sig_batch* b, uint8_t* 
     };
     // stage chunk j: index slices, check, ranges -> host, then the pool parts; hev_p = chunk j's bytes are on the device
     auto stage_chunk = [&](uint64_t j) -> int {
-        const uint64_t a = j * csz, e = std::min(n, a + csz), m = e - a;
+        const uint64_t a = at[j], e = at[j + 1], m = e - a;
         HIPCHK(c, hipMemcpyAsync(c->h_key_idx.as<uint32_t>() + a, b->key_idx + a, m * 4, hipMemcpyHostToDevice, cs));
         HIPCHK(c, hipMemcpyAsync(c->h_msg_idx.as<uint32_t>() + a, b->msg_idx + a, m * 4, hipMemcpyHostToDevice, cs));
         HIPCHK(c, hipMemcpyAsync(c->h_sig_off.as<uint64_t>() + a, b->sig_off + a, m * 8, hipMemcpyHostToDevice, cs));
@@ -895,21 +910,20 @@ static int verify_host_pipelined(chip_ctx* c, const chip_sig_batch* b, uint8_t* 
     d.msg_len = c->h_msg_len.as<uint32_t>();
     if (!d.schemes) d.schemes = host_scheme_hint(b);
     if ((r = stage_chunk(0))) return r;
-    for (uint64_t j = 0; j * csz < n; j++) {
-        const uint64_t a = j * csz, m = std::min(n, a + csz) - a;
-        HIPCHK(c, hipStreamWaitEvent(st, c->hev_p, 0));
+    for (uint64_t j = 0; j + 1 < at.size(); j++) {
+        const uint64_t a = at[j], m = at[j + 1] - a;
         d.n = m;
         d.key_idx = c->h_key_idx.as<uint32_t>() + a;
         d.msg_idx = c->h_msg_idx.as<uint32_t>() + a;
         d.sig_off = c->h_sig_off.as<uint64_t>() + a;
         d.sig_len = c->h_sig_len.as<uint32_t>() + a;
-        const VerifyChunk vc{n, j > 0};
+        const VerifyChunk vc{n, j > 0, c->hev_p};
         if ((r = verify_device_locked(c, &d, c->h_status.as<uint8_t>() + a, c->h_bitmap.as<uint64_t>() + a / 64, st,
                                       is_valid, &vc))) {
             hipStreamSynchronize(st);
             return r;
         }
-        if ((j + 1) * csz < n && (r = stage_chunk(j + 1))) {
+        if (j + 2 < at.size() && (r = stage_chunk(j + 1))) {
             hipStreamSynchronize(st);
             return r;
         }
@@ -929,9 +943,9 @@ static int verify_host_pipelined(chip_ctx* c, const chip_sig_batch* b, uint8_t* 
 }
 
 // chunks of a host batch: 1 (no pipeline) below 2^19 signatures, else about 2^18 signatures a chunk, at most
-// 8 (CHIP_HOST_CHUNKS overrides)
+// 8 (CHIP_HOST_CHUNKS overrides; cfg2's 1M: 4 chunks 6.3 ms pinned, 3: 6.4, 6: 6.9, 1: 8.4; tools/host_sweep.py)
 static uint64_t host_chunks(uint64_t n) {
-    uint64_t k = n >= (1ull << 19) ? std::min<uint64_t>(8, n >> 18) : 1;
+    uint64_t k = n >= (1ull << 19) ? std::min<uint64_t>(8, (n + (1ull << 17)) >> 18) : 1;
     if (const char* e = getenv("CHIP_HOST_CHUNKS")) k = std::max<uint64_t>(1, std::min<uint64_t>(64, strtoull(e, nullptr, 10)));
     return std::min<uint64_t>(k, std::max<uint64_t>(1, n / 64));
 }
