@@ -304,6 +304,65 @@ static int stage(chip_ctx* c, DevBuf& d, const T* src, uint64_t count, hipStream
 }
 
 // ---------------------------------------------------------------------------------------
+// Argument checks of the host entries, on the device after staging: the arrays are checked where they were
+// copied to anyway, so the host does not walk them (k_check_batch / k_check_chunk for chip_verify_batch; this
+// table-driven one for the tx-id, fused, FilteredTransaction, chip_stx_verify and uniqueness entries).
+__global__ void __launch_bounds__(256) k_dev_check(DevCheckSet set, uint32_t* __restrict__ bad) {
+    const DevCheck& d = set.c[blockIdx.y];
+    uint32_t f = 0;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < d.n; i += (uint64_t)gridDim.x * blockDim.x) {
+        bool ok = true;
+        switch (d.kind) {
+            case DEV_CHECK_MONOTONE: {   // u64 starts [n + 1]: nondecreasing, the first = lim2 (~0: any), the last <= lim
+                const uint64_t* a = static_cast<const uint64_t*>(d.a);
+                ok = a[i] <= a[i + 1] && (i || d.lim2 == ~0ull || a[0] == d.lim2) && (i + 1 < d.n || a[d.n] <= d.lim);
+                break;
+            }
+            case DEV_CHECK_RANGE: {      // (u64 off, u32 len) inside a pool of lim bytes; len <= lim2 (0: any)
+                const uint64_t o = static_cast<const uint64_t*>(d.a)[i];
+                const uint32_t l = static_cast<const uint32_t*>(d.b)[i];
+                ok = o + l <= d.lim && o + l >= o && (!d.lim2 || l <= d.lim2);
+                if (ok && d.c) ok = static_cast<const uint32_t*>(d.c)[i] <= l;   // template id offset inside it
+                break;
+            }
+            case DEV_CHECK_INDEX:        // u32 index < lim
+                ok = static_cast<const uint32_t*>(d.a)[i] < d.lim;
+                break;
+        }
+        if (!ok) f |= d.bit;
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) f |= (uint32_t)__shfl_xor((int)f, o);
+    if (f && (threadIdx.x & 63) == 0) atomicOr(bad, f);
+}
+
+int dev_check(chip_ctx* c, const DevCheck* chk, int nchk, hipStream_t st, uint32_t* bad_out) {
+    *bad_out = 0;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    DevCheckSet set{};
+    uint64_t nmax = 0;
+    int k = 0;
+    for (int i = 0; i < nchk; i++)
+        if (chk[i].n) {
+            if (k == DEV_CHECK_MAX) return fail(c, CHIP_E_ARG, "too many device checks");
+            set.c[k++] = chk[i];
+            nmax = std::max(nmax, chk[i].n);
+        }
+    if (!k) return CHIP_OK;
+    HIPCHK(c, c->h_check.ensure(128));
+    HIPCHK(c, hipMemsetAsync(c->h_check.p, 0, 4, st));
+    const uint32_t blocks = (uint32_t)std::min<uint64_t>(2048, (nmax + 255) / 256);
+    hipLaunchKernelGGL(k_dev_check, dim3(blocks, (uint32_t)k), dim3(256), 0, st, set, c->h_check.as<uint32_t>());
+    HIPCHK(c, hipGetLastError());
+    uint32_t* h = c->h_rng ? reinterpret_cast<uint32_t*>(c->h_rng) + 32 : nullptr;   // pinned scratch word
+    if (!h) return fail(c, CHIP_E_DEVICE, "no pinned scratch");
+    HIPCHK(c, hipMemcpyAsync(h, c->h_check.p, 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    *bad_out = *h;
+    return CHIP_OK;
+}
+
+// ---------------------------------------------------------------------------------------
 extern "C" {
 
 int chip_abi_version(void) { return CHIP_ABI_VERSION; }
@@ -1351,12 +1410,7 @@ int chip_stx_verify(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t
     if (!data || !off || !len || !tx_status || !verdict || !arg) return fail(c, CHIP_E_ARG, "null array");
     if (n_meta != tmpl->n) return fail(c, CHIP_E_ARG, "one SignatureMetadata per template");
     if (n_meta && !meta) return fail(c, CHIP_E_ARG, "null meta");
-    for (uint64_t t = 0; t < n; t++)
-        if (off[t] + len[t] > data_bytes || off[t] + len[t] < off[t]) return fail(c, CHIP_E_ARG, "blob outside pool");
-    for (uint64_t i = 0; i < tmpl->n; i++)
-        if (tmpl->off[i] + tmpl->len[i] > tmpl->data_bytes || tmpl->id_at[i] > tmpl->len[i] ||
-            tmpl->len[i] > tmpl->max_len)
-            return fail(c, CHIP_E_ARG, "template outside pool or longer than max_len");
+    if (tmpl->n && (!tmpl->data || !tmpl->off || !tmpl->len || !tmpl->id_at)) return fail(c, CHIP_E_ARG, "null template array");
     hipStream_t st = c->stream;
     chip_msg_templates dtm = *tmpl;
     int r;
@@ -1370,6 +1424,16 @@ int chip_stx_verify(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t
         (r = stage(c, c->h2_to, tmpl->off, tmpl->n, st)) || (r = stage(c, c->h2_tl, tmpl->len, tmpl->n, st)) ||
         (r = stage(c, c->h2_ta, tmpl->id_at, tmpl->n, st)))
         return r;
+    {   // blob ranges inside the pool; templates inside theirs, id offset inside, len <= max_len
+        const DevCheck chk[] = {
+            {DEV_CHECK_RANGE, 1, c->h2_off.p, c->h2_len.p, nullptr, n, data_bytes, 0},
+            {DEV_CHECK_RANGE, 2, c->h2_to.p, c->h2_tl.p, c->h2_ta.p, tmpl->n, tmpl->data_bytes,
+             tmpl->max_len ? tmpl->max_len : 0xffffffffull}};
+        uint32_t bad = 0;
+        if ((r = dev_check(c, chk, 2, st, &bad))) return r;
+        if (bad & 1) return fail(c, CHIP_E_ARG, "blob outside pool");
+        if (bad & 2) return fail(c, CHIP_E_ARG, "template outside pool or longer than max_len");
+    }
     HIPCHK(c, c->h2_st.ensure(n + 16));
     HIPCHK(c, c->h2_ids.ensure(n * 32 + 16));
     HIPCHK(c, c->h2_v.ensure(n + 16));
@@ -1454,17 +1518,25 @@ int chip_txid_batch_device(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids, vo
     return txid_device_locked(c, b, ids, stream ? (hipStream_t)stream : c->stream);
 }
 
+// a staged chip_tx_batch (t_start, t_off, t_len): tx_comp_start from 0, nondecreasing, within ncomp; every
+// component inside the data pool
+static int check_tx_batch(chip_ctx* c, const chip_tx_batch* b, hipStream_t st) {
+    const DevCheck chk[] = {
+        {DEV_CHECK_MONOTONE, 1, c->t_start.p, nullptr, nullptr, b->ntx, b->ncomp, ~0ull},
+        {DEV_CHECK_RANGE, 2, c->t_off.p, c->t_len.p, nullptr, b->ncomp, b->data_bytes, 0}};
+    uint32_t bad = 0;
+    if (int r = dev_check(c, chk, 2, st, &bad)) return r;
+    if (bad & 1) return fail(c, CHIP_E_ARG, "tx_comp_start not monotone / out of range");
+    if (bad & 2) return fail(c, CHIP_E_ARG, "component outside data pool");
+    return CHIP_OK;
+}
+
 int chip_txid_batch(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids) {
     if (!c || !b) return fail(c, CHIP_E_ARG, "null argument");
     const uint64_t ntx = b->ntx, nc = b->ncomp;
     if (ntx && (!b->salts || !b->tx_comp_start || !ids)) return fail(c, CHIP_E_ARG, "null tx array");
     if (nc && (!b->comp_group || !b->comp_internal || !b->comp_off || !b->comp_len || !b->data))
         return fail(c, CHIP_E_ARG, "null component array");
-    if (ntx && b->tx_comp_start[ntx] > nc) return fail(c, CHIP_E_ARG, "tx_comp_start out of range");
-    for (uint64_t t = 0; t < ntx; t++)
-        if (b->tx_comp_start[t] > b->tx_comp_start[t + 1]) return fail(c, CHIP_E_ARG, "tx_comp_start not monotone");
-    for (uint64_t k = 0; k < nc; k++)
-        if (b->comp_off[k] + b->comp_len[k] > b->data_bytes) return fail(c, CHIP_E_ARG, "component outside data pool");
     hipStream_t st = c->stream;
     int r;
     {
@@ -1477,6 +1549,7 @@ int chip_txid_batch(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids) {
             (r = stage(c, c->t_len, b->comp_len, nc, st)))
             return r;
         HIPCHK(c, c->t_ids.ensure(ntx * 32 + 16));
+        if ((r = check_tx_batch(c, b, st))) return r;
     }
     chip_tx_batch d = *b;
     d.salts = c->t_salts.as<uint8_t>();
@@ -1675,24 +1748,10 @@ static int verify_tx_host(chip_ctx* c, const chip_tx_batch* b, const chip_msg_te
     if (ntx && (!b->salts || !b->tx_comp_start || !ids)) return fail(c, CHIP_E_ARG, "null tx array");
     if (nc && (!b->comp_group || !b->comp_internal || !b->comp_off || !b->comp_len || !b->data))
         return fail(c, CHIP_E_ARG, "null component array");
-    if (ntx && b->tx_comp_start[ntx] > nc) return fail(c, CHIP_E_ARG, "tx_comp_start out of range");
-    for (uint64_t t = 0; t < ntx; t++)
-        if (b->tx_comp_start[t] > b->tx_comp_start[t + 1]) return fail(c, CHIP_E_ARG, "tx_comp_start not monotone");
-    for (uint64_t k = 0; k < nc; k++)
-        if (b->comp_off[k] + b->comp_len[k] > b->data_bytes) return fail(c, CHIP_E_ARG, "component outside data pool");
     if (nt && (!tm->data || !tm->off || !tm->len || !tm->id_at)) return fail(c, CHIP_E_ARG, "null template array");
-    for (uint64_t t = 0; t < nt; t++)
-        if (tm->off[t] + tm->len[t] > tm->data_bytes || tm->id_at[t] > tm->len[t] || tm->len[t] > tm->max_len)
-            return fail(c, CHIP_E_ARG, "template outside pool / id offset past its end / len > max_len");
     if (n && (!sb->tx_idx || !sb->tmpl_idx || !sb->key_idx || !sb->sig_off || !sb->sig_len || !status))
         return fail(c, CHIP_E_ARG, "null signer array");
     if (nk && (!sb->key_data || !sb->key_off || !sb->key_len)) return fail(c, CHIP_E_ARG, "null key array");
-    for (uint64_t i = 0; i < n; i++) {
-        if (sb->key_idx[i] >= nk) return fail(c, CHIP_E_ARG, "key_idx out of range");
-        if (sb->sig_off[i] + sb->sig_len[i] > sb->sig_bytes) return fail(c, CHIP_E_ARG, "signature outside sig pool");
-    }
-    for (uint64_t k = 0; k < nk; k++)
-        if (sb->key_off[k] + sb->key_len[k] > sb->key_bytes) return fail(c, CHIP_E_ARG, "key outside key pool");
     std::lock_guard<std::recursive_mutex> g(c->mu);
     hipStream_t st = c->stream;
     HIPCHK(c, hipSetDevice(c->device));
@@ -1713,6 +1772,21 @@ static int verify_tx_host(chip_ctx* c, const chip_tx_batch* b, const chip_msg_te
     HIPCHK(c, c->h_status.ensure(n + 16));
     const uint64_t nw = (n + 63) / 64;
     HIPCHK(c, c->h_bitmap.ensure(nw * 8 + 16));
+    if ((r = check_tx_batch(c, b, st))) return r;
+    {   // templates; signers' keys and signatures inside their pools
+        const DevCheck chk[] = {
+            {DEV_CHECK_RANGE, 1, c->f_toff.p, c->f_tlen.p, c->f_tid.p, nt, tm->data_bytes,
+             tm->max_len ? tm->max_len : 0xffffffffull},
+            {DEV_CHECK_INDEX, 2, c->h_key_idx.p, nullptr, nullptr, n, nk, 0},
+            {DEV_CHECK_RANGE, 4, c->h_sig_off.p, c->h_sig_len.p, nullptr, n, sb->sig_bytes, 0},
+            {DEV_CHECK_RANGE, 8, c->h_key_off.p, c->h_key_len.p, nullptr, nk, sb->key_bytes, 0}};
+        uint32_t bad = 0;
+        if ((r = dev_check(c, chk, 4, st, &bad))) return r;
+        if (bad & 1) return fail(c, CHIP_E_ARG, "template outside pool / id offset past its end / len > max_len");
+        if (bad & 2) return fail(c, CHIP_E_ARG, "key_idx out of range");
+        if (bad & 4) return fail(c, CHIP_E_ARG, "signature outside sig pool");
+        if (bad & 8) return fail(c, CHIP_E_ARG, "key outside key pool");
+    }
     chip_tx_batch dt = *b;
     dt.salts = c->t_salts.as<uint8_t>();
     dt.tx_comp_start = c->t_start.as<uint64_t>();
@@ -1793,26 +1867,16 @@ int chip_ftx_verify_batch(chip_ctx* c, const chip_ftx_batch* b, uint8_t* status,
     const uint64_t ntx = b->ntx;
     if (!ntx) return CHIP_OK;
     if (!b->ids || !b->gh_start || !b->fg_start || !status) return fail(c, CHIP_E_ARG, "null tx array");
-    if (b->gh_start[0] != 0 || b->fg_start[0] != 0) return fail(c, CHIP_E_ARG, "start arrays must begin at 0");
-    for (uint64_t t = 0; t < ntx; t++)
-        if (b->gh_start[t] > b->gh_start[t + 1] || b->fg_start[t] > b->fg_start[t + 1])
-            return fail(c, CHIP_E_ARG, "gh_start / fg_start not monotone");
-    const uint64_t ngh = b->gh_start[ntx], nfg = b->fg_start[ntx];
+    const uint64_t ngh = b->gh_start[ntx], nfg = b->fg_start[ntx];   // sizes; the arrays are checked on the device
     if ((ngh && !b->group_hashes) || (nfg && (!b->fg_index || !b->comp_start || !b->pt_start)))
         return fail(c, CHIP_E_ARG, "null group array");
     uint64_t ncomp = 0, nnodes = 0;
     if (nfg) {
-        if (b->comp_start[0] != 0 || b->pt_start[0] != 0) return fail(c, CHIP_E_ARG, "start arrays must begin at 0");
-        for (uint64_t g = 0; g < nfg; g++)
-            if (b->comp_start[g] > b->comp_start[g + 1] || b->pt_start[g] > b->pt_start[g + 1])
-                return fail(c, CHIP_E_ARG, "comp_start / pt_start not monotone");
         ncomp = b->comp_start[nfg];
         nnodes = b->pt_start[nfg];
     }
     if ((ncomp && (!b->comp_data || !b->comp_off || !b->comp_len || !b->nonces)) || (nnodes && (!b->pt_tag || !b->pt_hash)))
         return fail(c, CHIP_E_ARG, "null component / tree array");
-    for (uint64_t k = 0; k < ncomp; k++)
-        if (b->comp_off[k] + b->comp_len[k] > b->comp_bytes) return fail(c, CHIP_E_ARG, "component outside pool");
     hipStream_t st = c->stream;
     int r;
     {
@@ -1830,6 +1894,17 @@ int chip_ftx_verify_batch(chip_ctx* c, const chip_ftx_batch* b, uint8_t* status,
             return r;
         HIPCHK(c, c->x_st.ensure(ntx + 16));
         HIPCHK(c, c->x_rs.ensure(ntx + 16));
+        // the four start arrays from 0, nondecreasing, ending at the sizes read above; components in the pool
+        const DevCheck chk[] = {
+            {DEV_CHECK_MONOTONE, 1, c->x_ghs.p, nullptr, nullptr, ntx, ngh, 0},
+            {DEV_CHECK_MONOTONE, 1, c->x_fgs.p, nullptr, nullptr, ntx, nfg, 0},
+            {DEV_CHECK_MONOTONE, 1, c->x_cs.p, nullptr, nullptr, nfg, ncomp, 0},
+            {DEV_CHECK_MONOTONE, 1, c->x_pts.p, nullptr, nullptr, nfg, nnodes, 0},
+            {DEV_CHECK_RANGE, 2, c->x_co.p, c->x_cl.p, nullptr, ncomp, b->comp_bytes, 0}};
+        uint32_t bad = 0;
+        if ((r = dev_check(c, chk, 5, st, &bad))) return r;
+        if (bad & 1) return fail(c, CHIP_E_ARG, "start arrays must begin at 0 and be nondecreasing");
+        if (bad & 2) return fail(c, CHIP_E_ARG, "component outside pool");
     }
     chip_ftx_batch d = *b;
     d.ids = c->x_ids.as<uint8_t>();

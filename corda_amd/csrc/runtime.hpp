@@ -179,3 +179,19 @@ void launch_ed_comb_bhalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, c
                           const EdCombWs& w);
 void launch_ed_comb_ahalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w);
 void launch_ed_comb_finish(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w, uint8_t* status);
+
+// ---- host-entry argument checks on the device (runtime.hip dev_check) ----
+enum { DEV_CHECK_MONOTONE = 0, DEV_CHECK_RANGE = 1, DEV_CHECK_INDEX = 2 };
+struct DevCheck {
+    uint32_t kind, bit;
+    const void* a;   // MONOTONE: u64 starts[n + 1]; RANGE: u64 offsets[n]; INDEX: u32 indices[n]
+    const void* b;   // RANGE: u32 lengths[n]
+    const void* c;   // RANGE: optional u32 [n], each <= its length (template id offsets)
+    uint64_t n, lim, lim2;   // MONOTONE: last <= lim, first == lim2 (~0: any); RANGE: pool bytes, max length (0 any); INDEX: bound
+};
+#define DEV_CHECK_MAX 8
+struct DevCheckSet {
+    DevCheck c[DEV_CHECK_MAX];
+};
+// runs the checks (empty ones skipped) on `st`, waits, and returns the OR of the failed checks' bits
+int dev_check(chip_ctx* c, const DevCheck* chk, int nchk, hipStream_t st, uint32_t* bad_out);

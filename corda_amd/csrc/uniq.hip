@@ -1051,9 +1051,6 @@ int chip_uniq_commit_batch(chip_uniq* u, uint64_t ntx, const uint64_t* start, co
     if (!ntx) return CHIP_OK;
     const uint64_t nref = start[ntx];
     if (nref && !refs36) return CHIP_E_ARG;
-    if (start[0] != 0) return ufail(u, CHIP_E_ARG, "tx_ref_start[0] != 0");
-    for (uint64_t t = 0; t < ntx; t++)
-        if (start[t] > start[t + 1]) return ufail(u, CHIP_E_ARG, "tx_ref_start not monotone");
     if (ntx >= 0xffffffffull || nref >= 0x7fffffffull) return ufail(u, CHIP_E_ARG, "batch too large");
     if (u->open) return ufail(u, CHIP_E_ARG, "a shard batch is in flight");
     UCHK(u, hipSetDevice(u->device));
@@ -1068,6 +1065,12 @@ int chip_uniq_commit_batch(chip_uniq* u, uint64_t ntx, const uint64_t* start, co
     UCHK(u, hipMemcpyAsync(u->h_start.p, start, (ntx + 1) * 8, hipMemcpyHostToDevice, st));
     UCHK(u, hipMemcpyAsync(u->h_ids.p, tx_ids, ntx * 32, hipMemcpyHostToDevice, st));
     UCHK(u, hipMemcpyAsync(u->h_call.p, callers, ntx * 4, hipMemcpyHostToDevice, st));
+    {   // tx_ref_start from 0, nondecreasing, ending at nref: checked on the device where it was staged
+        const DevCheck chk[] = {{DEV_CHECK_MONOTONE, 1, u->h_start.p, nullptr, nullptr, ntx, nref, 0}};
+        uint32_t bad = 0;
+        if (dev_check(u->ctx, chk, 1, st, &bad) != CHIP_OK) return ufail(u, CHIP_E_DEVICE, "argument check");
+        if (bad) return ufail(u, CHIP_E_ARG, "tx_ref_start must begin at 0 and be nondecreasing");
+    }
     uint64_t nout = 0;
     int r = chip_uniq_commit_batch_device(u, ntx, u->h_start.as<uint64_t>(), nref, u->h_refs.as<uint8_t>(),
                                           u->h_ids.as<uint8_t>(), u->h_call.as<uint32_t>(), u->h_st.as<uint8_t>(),

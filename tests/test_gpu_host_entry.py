@@ -99,3 +99,70 @@ def test_host_chunk_pipeline_rejects_bad_index_in_a_later_chunk(ctx, monkeypatch
     assert "range" in str(e.value)
     st, _ = _chunked(ctx, b, 5, monkeypatch)
     assert np.array_equal(st, b.expected)
+
+
+def test_other_host_entries_check_arguments_on_the_device(ctx):
+    """The tx-id, fused, FilteredTransaction, chip_stx_verify and uniqueness host entries check their
+    arrays on the device after staging (no host walk): each bad argument is CHIP_E_ARG with its message,
+    and the same call with good arguments afterwards is correct."""
+    import sys
+    sys.path.insert(0, __import__("os").path.dirname(__file__))
+    from ftx_build import FtxBatch, notary_workload
+
+    def bad(fn, *a, want):
+        with pytest.raises(native.ChipError) as e:
+            fn(*a)
+        assert want in str(e.value), (want, str(e.value))
+
+    tb, tm, sb, ids, _msgs = G.cfg4_workload(300, n_keys=8, corrupt=0.05, seed=0x5EED0504, threads=8)
+    # tx ids: a non-monotone start array, a component outside the pool
+    x = copy.copy(tb)
+    x.tx_comp_start = tb.tx_comp_start.copy()
+    x.tx_comp_start[5], x.tx_comp_start[6] = x.tx_comp_start[6], x.tx_comp_start[5] - 1
+    bad(ctx.txid_batch, x, want="tx_comp_start")
+    x = copy.copy(tb)
+    x.comp_off = tb.comp_off.copy()
+    x.comp_off[-1] = len(tb.data)
+    bad(ctx.txid_batch, x, want="component outside")
+    assert np.array_equal(ctx.txid_batch(tb), ids)
+    # fused: key index, signature range, template range
+    y = copy.copy(sb)
+    y.key_idx = sb.key_idx.copy()
+    y.key_idx[7] = 10 ** 6
+    bad(ctx.verify_tx_batch, tb, tm, y, want="key_idx")
+    y = copy.copy(sb)
+    y.sig_off = sb.sig_off.copy()
+    y.sig_off[-1] = len(sb.sig_data)
+    bad(ctx.verify_tx_batch, tb, tm, y, want="signature outside")
+    z = copy.copy(tm)
+    z.id_at = tm.id_at.copy()
+    z.id_at[0] = int(tm.len[0]) + 1
+    bad(ctx.verify_tx_batch, tb, z, sb, want="template")
+    gids, st, _ = ctx.verify_tx_batch(tb, tm, sb)
+    assert np.array_equal(gids, ids) and np.array_equal(st, sb.expected)
+    # FilteredTransaction: a component outside the pool
+    ftxs, want = notary_workload(200, seed=4)
+    fb = FtxBatch(ftxs)
+    f2 = copy.copy(fb)
+    f2.comp_off = fb.comp_off.copy()
+    f2.comp_off[0] = len(fb.comp_data) + 3
+    bad(ctx.ftx_verify_batch, f2, want="component outside")
+    st, rs = ctx.ftx_verify_batch(fb)
+    assert list(zip(st.tolist(), rs.tolist())) == want
+    # chip_stx_verify: a blob outside the pool
+    tb2, tm2, sb2, ids2, verdict, arg = G.cfg4_workload_commands(200, n_keys=8, seed=0x5EED0505, threads=8)
+    data, off, ln = G.stx_uniform(tb2, sb2, 2)
+    o2 = off.copy()
+    o2[3] = len(data)
+    bad(ctx.stx_verify, data, o2, ln, tm2, [[1, 4]], want="blob outside")
+    st, v, a, _ = ctx.stx_verify(data, off, ln, tm2, [[1, 4]])
+    assert not st.any() and np.array_equal(v, verdict)
+    # uniqueness: tx_ref_start not starting at 0
+    pre, ub = G.uniq_workload(500, 100, seed=31)
+    t = ctx.uniq_open(4096)
+    s2 = ub.tx_ref_start.copy()
+    s2[0] = 1
+    bad(t.commit_batch, s2, ub.refs, ub.tx_ids, ub.callers, want="tx_ref_start")
+    st, _recs = t.commit_batch(ub.tx_ref_start, ub.refs, ub.tx_ids, ub.callers)
+    assert (st == 0).sum() > 400
+    t.close()
