@@ -72,11 +72,19 @@ SHA256_OPS_PER_COMPRESSION = 2_168
 # HBM traffic per launch comes from the committed PMC passes of the same command (tools/profile.sh):
 # FETCH_SIZE + WRITE_SIZE (KiB) of the launch with the same grid
 PROFILE_DIR = os.path.join(ROOT, "profiles", os.environ.get("CORDA_PROFILE_DIR", "r02f"))
-# VALU issue peak: 256 CU x 4 SIMD x 32 lanes x 2.4 GHz = 78.6e12 lane-ops/s (a wave64 VALU
-# instruction issues over 2 cycles, MI355X_MICROARCH.md).  v_mad_u64_u32 issues at a quarter of
-# that: 19.66e12 MACs/s (tools/microbench_mul.hip measures 18.0e12).
+# VALU issue peak (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2 cycles): 256 CU x 4 SIMD x
+# 32 lanes x 2.4 GHz = 78.6e12 lane-instructions/s.  The 32x32->64 MAC (v_mad_u64_u32) has no guide figure:
+# profiles/r03/microbench_mac.txt measures it at 34.0e12 MACs/s chip-wide (8 independent chains per lane, full
+# occupancy; 31-34 T with 1-8 chains), plain 32-bit VALU (add / xor / add3) at 40-45e12 lane-ops/s, and MACs
+# mixed with plain VALU take the SUM of their issue times (no co-issue: mac_alu<K> rows).  MAC-bound rooflines
+# use the measured MAC rate; the round-2 figure (78.6 / 4 = 19.65 T, "quarter rate") was a guess below what the
+# hardware does, so round-2 fractions overstated by 1.73x.
 INT32_PEAK_TOPS = 78.6
-MAC_PEAK_T = 78.6 / 4
+MAC_PEAK_T = 34.0
+VALU_MEASURED_T = 45.0
+# k_ed_comb_ahalf's VALU instructions per lane besides its MACs (SQ_INSTS_VALU per wave, profiles/r02f/pmc_sq.csv:
+# 74.1k per wave - 40.7k MACs): the issue model prices them at VALU_MEASURED_T
+ED_COMB_OTHER_VALU_A = 33_400
 HBM_PEAK_GBS = 8000.0
 # uniqueness: 36 B key read + 64 B slot probe + 64 B slot write per input StateRef
 UNIQ_BYTES_PER_REF = 164
@@ -711,6 +719,15 @@ def main():
                          "traffic_note": "FETCH_SIZE+WRITE_SIZE bytes per launch, %s (same grid); vs ~%d B/sig "
                                          "algorithmic (h 32 + [S]B 160 in, key table entries read from L2, R' 120 out)"
                                          % (os.path.relpath(PROFILE_DIR, ROOT), 312),
+                         "peak_note": "v_mad_u64_u32 issue rate measured by tools/microbench_mac.hip "
+                                      "(profiles/r03/microbench_mac.txt); no co-issue with other VALU",
+                         "issue_model": {"macs_per_unit": ED_COMB_MACS_A, "other_valu_per_unit": ED_COMB_OTHER_VALU_A,
+                                         "predicted_ms": n_comb * (ED_COMB_MACS_A / (MAC_PEAK_T * 1e12) +
+                                                                   ED_COMB_OTHER_VALU_A / (VALU_MEASURED_T * 1e12)) * 1e3,
+                                         "frac": n_comb * (ED_COMB_MACS_A / (MAC_PEAK_T * 1e12) +
+                                                           ED_COMB_OTHER_VALU_A / (VALU_MEASURED_T * 1e12)) * 1e3 / a_ms,
+                                         "note": "the MACs and the other VALU instructions issue from one port: "
+                                                 "time >= MACs / 34 T + other / 45 T (measured rates)"},
                          "kernel": "k_ed_comb_ahalf", "kernel_ms": a_ms,
                          "units_per_launch": n_comb, "macs_per_unit": ED_COMB_MACS_A,
                          "both_halves_frac": ED_COMB_MACS_PER_VERIFY * n_comb / ((a_ms + b_ms) * 1e-3) / 1e12 / MAC_PEAK_T,

@@ -13,7 +13,7 @@
 #include <cstdio>
 #include <cstdint>
 
-#define ITERS 2048
+#define ITERS 16384
 
 template <int C>
 __global__ void __launch_bounds__(256) k_mac(uint64_t* out, uint32_t seed) {
