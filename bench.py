@@ -71,7 +71,7 @@ ECDSA_Q_MACS_PER_VERIFY = 65 * 592 + 100                            # k_ecdsa_co
 SHA256_OPS_PER_COMPRESSION = 2_168
 # HBM traffic per launch comes from the committed PMC passes of the same command (tools/profile.sh):
 # FETCH_SIZE + WRITE_SIZE (KiB) of the launch with the same grid
-PROFILE_DIR = os.path.join(ROOT, "profiles", os.environ.get("CORDA_PROFILE_DIR", "r02f"))
+PROFILE_DIR = os.path.join(ROOT, "profiles", os.environ.get("CORDA_PROFILE_DIR", "r03"))
 # VALU issue peak (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2 cycles): 256 CU x 4 SIMD x
 # 32 lanes x 2.4 GHz = 78.6e12 lane-instructions/s.  The 32x32->64 MAC (v_mad_u64_u32) has no guide figure:
 # profiles/r03/microbench_mac.txt measures it at 34.0e12 MACs/s chip-wide (8 independent chains per lane, full
@@ -212,9 +212,9 @@ def profile_traffic(kernel, grid):
 def stx_traffic(grid_tx, grid_sig):
     """FETCH_SIZE + WRITE_SIZE of one Kryo front-end call (both parse passes, the key interning and the
     required-key passes; the pool copy is a DMA, not counted) from the committed PMC profile, or None."""
-    parts = [profile_traffic(k, grid_tx) for k in ("k_stx_parse<false>", "k_stx_parse<true>", "k_stx_required<true>")]
+    parts = [profile_traffic(k, grid_tx) for k in ("k_stx_parse<false>", "k_stx_parse<true>", "k_stx_required")]
     parts += [profile_traffic(k, grid_sig) for k in ("k_stx_key_insert", "k_stx_key_flag", "k_stx_key_assign",
-                                                      "k_stx_req_compact")]
+                                                      "k_stx_req_entry<false>", "k_stx_req_entry<true>")]
     return None if any(p is None for p in parts) else sum(parts)
 
 
@@ -442,7 +442,7 @@ def main():
                                   / INT32_PEAK_TOPS,
             "txid_roofline_note": "canonical %d int32 ops per SHA-256 compression x %d compressions/tx vs the %.1f T "
                                   "VALU lane-op peak" % (SHA256_OPS_PER_COMPRESSION, comp_per_tx, INT32_PEAK_TOPS),
-            "txid_traffic": profile_traffic("k_txid", (tb.ntx + 255) // 256 * 256),
+            "txid_traffic": profile_traffic("k_txid", (tb.ntx + 63) // 64 * 64),   # TX_BLOCK 64
             "txid_algorithmic_bytes": int(tb.data.nbytes + tb.salts.nbytes + 32 * tb.ntx + 20 * len(tb.comp_len)),
         })
         # fused: ids -> SignableData messages -> 2 signers per tx -> required signers (verifySignaturesExcept)
