@@ -209,6 +209,17 @@ def profile_traffic(kernel, grid):
     return tot
 
 
+def profile_valu_lane_instrs(kernel, grid):
+    """VALU lane-instructions of one launch (SQ_INSTS_VALU x 64) from the committed SQ pass, or None."""
+    import csv
+    path = os.path.join(PROFILE_DIR, "pmc_sq.csv")
+    if not os.path.exists(path):
+        return None
+    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
+            if kernel_base(r["Kernel_Name"]) == kernel and int(r["Grid_Size"]) == grid and r["Counter_Name"] == "SQ_INSTS_VALU"]
+    return sum(vals) / len(vals) * 64.0 if vals else None
+
+
 def stx_traffic(grid_tx, grid_sig):
     """FETCH_SIZE + WRITE_SIZE of one Kryo front-end call (both parse passes, the key interning and the
     required-key passes; the pool copy is a DMA, not counted) from the committed PMC profile, or None."""
@@ -443,6 +454,10 @@ def main():
             "txid_roofline_note": "canonical %d int32 ops per SHA-256 compression x %d compressions/tx vs the %.1f T "
                                   "VALU lane-op peak" % (SHA256_OPS_PER_COMPRESSION, comp_per_tx, INT32_PEAK_TOPS),
             "txid_traffic": profile_traffic("k_txid", (tb.ntx + 63) // 64 * 64),   # TX_BLOCK 64
+            # the instructions it issues (SQ_INSTS_VALU of the committed profile; fused add3 / lshl_add
+            # instructions do two canonical ops) against the measured 32-bit VALU issue rate
+            "txid_issue_frac": (lambda vi: vi / (tx_ms * 1e-3) / 1e12 / VALU_MEASURED_T if vi else None)(
+                profile_valu_lane_instrs("k_txid", (tb.ntx + 63) // 64 * 64)),
             "txid_algorithmic_bytes": int(tb.data.nbytes + tb.salts.nbytes + 32 * tb.ntx + 20 * len(tb.comp_len)),
         })
         # fused: ids -> SignableData messages -> 2 signers per tx -> required signers (verifySignaturesExcept)
