@@ -27,6 +27,9 @@
 #include "ec_dev.hpp"
 #include "sha2_dev.hpp"
 #include "runtime.hpp"
+#ifndef EC_G_PF
+#define EC_G_PF 0   // software-pipelined G-comb gathers in k_ecdsa_comb_g (A/B switch)
+#endif
 #include <cstdlib>
 
 #define EC_TAB_STRIDE EC_KEY_TABLE_WORDS
@@ -873,8 +876,8 @@ CHIP_DEV void comb_g_body(uint32_t blk, const uint32_t* __restrict__ count, cons
     int carry = 0;
     apt ga;
     bool exc = false;
-#pragma unroll
-    for (int w = 0; w < EC_GWIN; w++) {
+    // the signed radix-2^EC_GW digit of window w (windows in order: the carry runs low to high)
+    auto digit = [&](int w) -> int {
         const int b = w * EC_GW;   // bits [b, b + EC_GW) of u1
         uint32_t bits;
         if (b >= 256) bits = 0;
@@ -882,7 +885,31 @@ CHIP_DEV void comb_g_body(uint32_t blk, const uint32_t* __restrict__ count, cons
         else bits = __builtin_amdgcn_alignbit(u1.w[(b >> 5) + 1], u1.w[b >> 5], b & 31);
         int v = (int)(bits & ((1u << EC_GW) - 1)) + carry;
         carry = (v + (1 << (EC_GW - 1)) - 1) >> EC_GW;   // digits in [-2^(W-1) + 1, 2^(W-1)]
-        v -= carry << EC_GW;
+        return v - (carry << EC_GW);
+    };
+#if EC_G_PF
+    // software-pipelined gathers: window w + 1's G entry is loaded while window w's addition runs (a zero
+    // digit loads entry 1 and skips the addition)
+    int vn = digit(0);
+    apt gn;
+    load_apt(gn, G + ((uint32_t)(vn < 0 ? -vn : vn) - (vn != 0)) * 16);
+#pragma unroll
+    for (int w = 0; w < EC_GWIN; w++) {
+        const int v = vn;
+        ga = gn;
+        if (w + 1 < EC_GWIN) {
+            vn = digit(w + 1);
+            load_apt(gn, G + ((uint64_t)(w + 1) * EC_GENT + (uint32_t)(vn < 0 ? -vn : vn) - (vn != 0)) * 16);
+        }
+        if (v != 0) {
+            if (v < 0) fp_neg<C>(ga.y, ga.y);
+            jmadd_x<C>(acc, acc, ga, exc);
+        }
+    }
+#else
+#pragma unroll
+    for (int w = 0; w < EC_GWIN; w++) {
+        const int v = digit(w);
         if (v != 0) {
             const uint32_t av = (uint32_t)(v < 0 ? -v : v);
             load_apt(ga, G + ((uint64_t)w * EC_GENT + av - 1) * 16);
@@ -890,6 +917,7 @@ CHIP_DEV void comb_g_body(uint32_t blk, const uint32_t* __restrict__ count, cons
             jmadd_x<C>(acc, acc, ga, exc);
         }
     }
+#endif
     if (exc || park_all) {   // finished by k_ecdsa_comb_retry (park_all: CHIP_FLAG_EC_RETRY_ALL, tests)
         mid[(uint64_t)40 * cap + gid] = 2u;
         return;

@@ -318,10 +318,10 @@ __global__ void __launch_bounds__(256) k_dev_check(DevCheckSet set, uint32_t* __
                 ok = a[i] <= a[i + 1] && (i || d.lim2 == ~0ull || a[0] == d.lim2) && (i + 1 < d.n || a[d.n] <= d.lim);
                 break;
             }
-            case DEV_CHECK_RANGE: {      // (u64 off, u32 len) inside a pool of lim bytes; len <= lim2 (0: any)
+            case DEV_CHECK_RANGE: {      // (u64 off, u32 len) inside a pool of lim bytes; len <= lim2
                 const uint64_t o = static_cast<const uint64_t*>(d.a)[i];
                 const uint32_t l = static_cast<const uint32_t*>(d.b)[i];
-                ok = o + l <= d.lim && o + l >= o && (!d.lim2 || l <= d.lim2);
+                ok = o + l <= d.lim && o + l >= o && l <= d.lim2;
                 if (ok && d.c) ok = static_cast<const uint32_t*>(d.c)[i] <= l;   // template id offset inside it
                 break;
             }
@@ -1426,9 +1426,9 @@ int chip_stx_verify(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t
         return r;
     {   // blob ranges inside the pool; templates inside theirs, id offset inside, len <= max_len
         const DevCheck chk[] = {
-            {DEV_CHECK_RANGE, 1, c->h2_off.p, c->h2_len.p, nullptr, n, data_bytes, 0},
+            {DEV_CHECK_RANGE, 1, c->h2_off.p, c->h2_len.p, nullptr, n, data_bytes, 0xffffffffull},
             {DEV_CHECK_RANGE, 2, c->h2_to.p, c->h2_tl.p, c->h2_ta.p, tmpl->n, tmpl->data_bytes,
-             tmpl->max_len ? tmpl->max_len : 0xffffffffull}};
+             tmpl->max_len}};
         uint32_t bad = 0;
         if ((r = dev_check(c, chk, 2, st, &bad))) return r;
         if (bad & 1) return fail(c, CHIP_E_ARG, "blob outside pool");
@@ -1523,7 +1523,7 @@ int chip_txid_batch_device(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids, vo
 static int check_tx_batch(chip_ctx* c, const chip_tx_batch* b, hipStream_t st) {
     const DevCheck chk[] = {
         {DEV_CHECK_MONOTONE, 1, c->t_start.p, nullptr, nullptr, b->ntx, b->ncomp, ~0ull},
-        {DEV_CHECK_RANGE, 2, c->t_off.p, c->t_len.p, nullptr, b->ncomp, b->data_bytes, 0}};
+        {DEV_CHECK_RANGE, 2, c->t_off.p, c->t_len.p, nullptr, b->ncomp, b->data_bytes, 0xffffffffull}};
     uint32_t bad = 0;
     if (int r = dev_check(c, chk, 2, st, &bad)) return r;
     if (bad & 1) return fail(c, CHIP_E_ARG, "tx_comp_start not monotone / out of range");
@@ -1776,10 +1776,10 @@ static int verify_tx_host(chip_ctx* c, const chip_tx_batch* b, const chip_msg_te
     {   // templates; signers' keys and signatures inside their pools
         const DevCheck chk[] = {
             {DEV_CHECK_RANGE, 1, c->f_toff.p, c->f_tlen.p, c->f_tid.p, nt, tm->data_bytes,
-             tm->max_len ? tm->max_len : 0xffffffffull},
+             tm->max_len},
             {DEV_CHECK_INDEX, 2, c->h_key_idx.p, nullptr, nullptr, n, nk, 0},
-            {DEV_CHECK_RANGE, 4, c->h_sig_off.p, c->h_sig_len.p, nullptr, n, sb->sig_bytes, 0},
-            {DEV_CHECK_RANGE, 8, c->h_key_off.p, c->h_key_len.p, nullptr, nk, sb->key_bytes, 0}};
+            {DEV_CHECK_RANGE, 4, c->h_sig_off.p, c->h_sig_len.p, nullptr, n, sb->sig_bytes, 0xffffffffull},
+            {DEV_CHECK_RANGE, 8, c->h_key_off.p, c->h_key_len.p, nullptr, nk, sb->key_bytes, 0xffffffffull}};
         uint32_t bad = 0;
         if ((r = dev_check(c, chk, 4, st, &bad))) return r;
         if (bad & 1) return fail(c, CHIP_E_ARG, "template outside pool / id offset past its end / len > max_len");
@@ -1900,7 +1900,7 @@ int chip_ftx_verify_batch(chip_ctx* c, const chip_ftx_batch* b, uint8_t* status,
             {DEV_CHECK_MONOTONE, 1, c->x_fgs.p, nullptr, nullptr, ntx, nfg, 0},
             {DEV_CHECK_MONOTONE, 1, c->x_cs.p, nullptr, nullptr, nfg, ncomp, 0},
             {DEV_CHECK_MONOTONE, 1, c->x_pts.p, nullptr, nullptr, nfg, nnodes, 0},
-            {DEV_CHECK_RANGE, 2, c->x_co.p, c->x_cl.p, nullptr, ncomp, b->comp_bytes, 0}};
+            {DEV_CHECK_RANGE, 2, c->x_co.p, c->x_cl.p, nullptr, ncomp, b->comp_bytes, 0xffffffffull}};
         uint32_t bad = 0;
         if ((r = dev_check(c, chk, 5, st, &bad))) return r;
         if (bad & 1) return fail(c, CHIP_E_ARG, "start arrays must begin at 0 and be nondecreasing");

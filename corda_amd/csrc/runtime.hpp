@@ -187,7 +187,7 @@ struct DevCheck {
     const void* a;   // MONOTONE: u64 starts[n + 1]; RANGE: u64 offsets[n]; INDEX: u32 indices[n]
     const void* b;   // RANGE: u32 lengths[n]
     const void* c;   // RANGE: optional u32 [n], each <= its length (template id offsets)
-    uint64_t n, lim, lim2;   // MONOTONE: last <= lim, first == lim2 (~0: any); RANGE: pool bytes, max length (0 any); INDEX: bound
+    uint64_t n, lim, lim2;   // MONOTONE: last <= lim, first == lim2 (~0: any); RANGE: pool bytes, max length; INDEX: bound
 };
 #define DEV_CHECK_MAX 8
 struct DevCheckSet {

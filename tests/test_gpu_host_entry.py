@@ -138,6 +138,9 @@ def test_other_host_entries_check_arguments_on_the_device(ctx):
     z.id_at = tm.id_at.copy()
     z.id_at[0] = int(tm.len[0]) + 1
     bad(ctx.verify_tx_batch, tb, z, sb, want="template")
+    z = copy.copy(tm)
+    z.max_len = int(tm.len.max()) - 1                # a template longer than the message slots
+    bad(ctx.verify_tx_batch, tb, z, sb, want="template")
     gids, st, _ = ctx.verify_tx_batch(tb, tm, sb)
     assert np.array_equal(gids, ids) and np.array_equal(st, sb.expected)
     # FilteredTransaction: a component outside the pool
@@ -155,6 +158,9 @@ def test_other_host_entries_check_arguments_on_the_device(ctx):
     o2 = off.copy()
     o2[3] = len(data)
     bad(ctx.stx_verify, data, o2, ln, tm2, [[1, 4]], want="blob outside")
+    z2 = copy.copy(tm2)
+    z2.max_len = int(tm2.len.max()) - 1
+    bad(ctx.stx_verify, data, off, ln, z2, [[1, 4]], want="template")
     st, v, a, _ = ctx.stx_verify(data, off, ln, tm2, [[1, 4]])
     assert not st.any() and np.array_equal(v, verdict)
     # uniqueness: tx_ref_start not starting at 0

@@ -1,17 +1,12 @@
 #!/bin/bash
-# A/B runs of the cfg3 leg (tools/bench_ecdsa.py) under environment variants, then one kernel trace.
+# A/B of the cfg3 (ECDSA) leg over library variants ("-" = the in-tree build), one line per variant
 set -uo pipefail
 REPO=${GRAFT_REPO_ROOT:-$(pwd)}
-TAG=${1:-ab}
-OUT=$REPO/gpurun_out/$TAG
+OUT=$REPO/gpurun_out/${TAG:-abec}
 mkdir -p $OUT
 cd $REPO
-VARS=("")
-for v in "${VARS[@]}"; do
-  env $v timeout -k 10 120 python3 tools/bench_ecdsa.py --steps 5 >> $OUT/ab.jsonl 2>>$OUT/ab.err || { echo "variant '$v' failed"; tail -5 $OUT/ab.err; exit 1; }
+for v in "$@"; do
+  lib=""; [ "$v" != "-" ] && lib="$REPO/$v"
+  CORDAHIP_LIB=$lib timeout -k 10 300 python3 bench.py --steps ${STEPS:-5} --cold-n 0 --no-txid --no-notary --no-cpu-baseline --no-host-path > $OUT/b.json 2>>$OUT/err.log || { echo "variant $v failed"; tail -5 $OUT/err.log; exit 1; }
+  python3 -c "import json; s=json.load(open('$OUT/b.json'))['secondary']; print('$v', round(s['ecdsa_mixed_sigs_per_s']/1e6,2), 'M/s', 'front', round(s['ecdsa_front_ms'],3), 'q', round(s['ecdsa_q_kernel_ms'],3), 'ok', s['ecdsa_correct_vs_labels'])" | tee -a $OUT/ab.txt
 done
-timeout -k 10 120 python3 tools/bench_ecdsa.py --steps 5 --p256-only >> $OUT/ab.jsonl 2>>$OUT/ab.err || exit 1
-cat $OUT/ab.jsonl
-export TMPDIR=/tmp
-cd /tmp
-timeout -k 10 200 rocprofv3 --kernel-trace -d $OUT/kt -o kt --output-format csv -- python3 $REPO/tools/bench_ecdsa.py --steps 3 > /dev/null 2>$OUT/kt.err || { echo "trace failed"; exit 1; }
