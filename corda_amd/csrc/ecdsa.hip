@@ -28,7 +28,7 @@
 #include "sha2_dev.hpp"
 #include "runtime.hpp"
 #ifndef EC_G_PF
-#define EC_G_PF 0   // software-pipelined G-comb gathers in k_ecdsa_comb_g (A/B switch)
+#define EC_G_PF 1   // software-pipelined G-comb gathers in k_ecdsa_comb_g (A/B: +0.9-1.0 %, profiles/r03/ab_ecdsa_g_prefetch.txt)
 #endif
 #include <cstdlib>
 

@@ -109,8 +109,6 @@ struct chip_uniq {
     bool open = false;
     uint64_t ntx = 0, nref = 0;
     hipStream_t bst = nullptr;
-    hipStream_t ist = nullptr;                // inserts, beside the records (commit_device)
-    hipEvent_t iev0 = nullptr, iev1 = nullptr;
     bool inserted = false;                    // the batch's inserts were launched (launch_insert)
     const uint64_t* start = nullptr;
     const uint8_t* refs = nullptr;
@@ -325,6 +323,8 @@ CHIP_DEV bool round_closed(const uint32_t* gate) { return gate && __builtin_nont
 // (tag << 32) | t with tag = ~round: a later round's entries are smaller than any stale entry of an
 // earlier round, so the minimum needs no reset between rounds, and a reader (itself a live
 // referencer of s, so a writer in this round) always sees this round's minimum.
+// (A dup-ref list compacted after the lookup cut the four rounds' round_min from 0.108 to 0.031 ms, but the
+// DeviceSelect over 10M flags cost 0.095 ms: measured, not kept.)
 __global__ void __launch_bounds__(256) k_uniq_round_min(uint64_t nref, const uint8_t* __restrict__ rdup,
                                                         const uint32_t* __restrict__ ref_tx,
                                                         const uint32_t* __restrict__ sid,
@@ -444,7 +444,24 @@ CHIP_DEV bool consumed_before(uint64_t r, uint32_t t, const uint32_t* __restrict
 // 2 CONFLICT; 0 for committed txs and for failed txs with no consumed input on this shard.
 // nrec[t] = the tx's Conflict.stateHistory records on this shard: its consumed local inputs, the
 // first occurrence of a repeated state only.
-__global__ void __launch_bounds__(256) k_uniq_classify(uint64_t ntx, const uint64_t* __restrict__ start,
+struct ClassifyArgs {
+    uint64_t ntx;
+    const uint64_t* start;
+    const uint32_t *pos, *pre, *sid;
+    const uint8_t* rdup;
+    const unsigned long long* bcommit;
+    const uint8_t* tx_ids;
+    const uint32_t* callers;
+    const uint32_t* tab;
+    const uint8_t *txrows, *st;
+    uint8_t* vote;
+    uint32_t* nrec;
+};
+CHIP_DEV void classify_body(uint64_t t, const ClassifyArgs& a);
+__global__ void __launch_bounds__(256) k_uniq_classify(ClassifyArgs a) {
+    classify_body((uint64_t)blockIdx.x * blockDim.x + threadIdx.x, a);
+}
+CHIP_DEV void classify_tx(uint64_t t, uint64_t ntx, const uint64_t* __restrict__ start,
                                                        const uint32_t* __restrict__ pos, const uint32_t* __restrict__ pre,
                                                        const uint32_t* __restrict__ sid,
                                                        const uint8_t* __restrict__ rdup,
@@ -454,7 +471,6 @@ __global__ void __launch_bounds__(256) k_uniq_classify(uint64_t ntx, const uint6
                                                        const uint32_t* __restrict__ tab, const uint8_t* __restrict__ txrows,
                                                        const uint8_t* __restrict__ st, uint8_t* __restrict__ vote,
                                                        uint32_t* __restrict__ nrec) {
-    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= ntx) return;
     uint8_t v = 0;
     uint32_t n = 0;
@@ -473,6 +489,11 @@ __global__ void __launch_bounds__(256) k_uniq_classify(uint64_t ntx, const uint6
     }
     vote[t] = v;
     nrec[t] = n;
+}
+
+CHIP_DEV void classify_body(uint64_t t, const ClassifyArgs& a) {
+    classify_tx(t, a.ntx, a.start, a.pos, a.pre, a.sid, a.rdup, a.bcommit, a.tx_ids, a.callers, a.tab, a.txrows, a.st,
+                a.vote, a.nrec);
 }
 
 // records of failed tx t at at[t] ...: its consumed local inputs in input order (first occurrence of
@@ -512,49 +533,67 @@ __global__ void __launch_bounds__(256) k_uniq_emit(uint64_t ntx, const uint64_t*
 // occurrence inside the committed tx) writes it live; a state nothing committed is written back dead by
 // its owner when another key probed past the claim.  count[0] += live writes (the table's size),
 // count[1] += writes into empty slots (its occupancy)
-__global__ void __launch_bounds__(256) k_uniq_insert(uint64_t nref, const uint8_t* __restrict__ refs,
-                                                     const uint32_t* __restrict__ ref_tx,
-                                                     const uint32_t* __restrict__ pos, const uint64_t* __restrict__ start,
-                                                     const uint8_t* __restrict__ st, const uint32_t* __restrict__ sid,
-                                                     const uint8_t* __restrict__ rdup, const uint32_t* __restrict__ pre,
-                                                     const uint32_t* __restrict__ tslot, const uint8_t* __restrict__ own,
-                                                     const uint8_t* __restrict__ passed,
-                                                     const unsigned long long* __restrict__ bcommit, uint64_t row_base,
-                                                     const uint32_t* __restrict__ callers, uint32_t* tab,
-                                                     unsigned long long* __restrict__ count) {
-    __shared__ uint32_t stage[4][64 * STAGE_W];
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+struct InsertArgs {
+    uint64_t nref;
+    const uint8_t* refs;
+    const uint32_t *ref_tx, *pos;
+    const uint64_t* start;
+    const uint8_t* st;
+    const uint32_t* sid;
+    const uint8_t* rdup;
+    const uint32_t *pre, *tslot;
+    const uint8_t *own, *passed;
+    const unsigned long long* bcommit;
+    uint64_t row_base;
+    const uint32_t* callers;
+    uint32_t* tab;
+    unsigned long long* count;
+};
+// every lane of the wave calls this (the slot stores are wave-cooperative)
+CHIP_DEV void insert_body(uint64_t r, const InsertArgs& a, uint32_t* stage) {
     uint32_t slot = NO_SLOT, live = 0, fresh = 0;
     uint32_t row[SLOT_W];
 #pragma unroll
     for (int w = 0; w < SLOT_W; w++) row[w] = 0;
-    if (r < nref && pre[r] == NO_SLOT) {
-        const uint32_t t = ref_tx[r];
-        const uint32_t o = sid[r];
+    if (r < a.nref && a.pre[r] == NO_SLOT) {
+        const uint32_t t = a.ref_tx[r];
+        const uint32_t o = a.sid[r];
         bool write = false;
-        if (st[t] == ST_COMMITTED && (!rdup[r] || first_in_tx(sid, start[t], r))) {
+        if (a.st[t] == ST_COMMITTED && (!a.rdup[r] || first_in_tx(a.sid, a.start[t], r))) {
             write = true;
             live = 1;
-        } else if (o == (uint32_t)r && (own[r] & OWN_FRESH)) {
-            write = passed[r] && (!rdup[r] || bcommit[o] == ~0ull);
+        } else if (o == (uint32_t)r && (a.own[r] & OWN_FRESH)) {
+            write = a.passed[r] && (!a.rdup[r] || a.bcommit[o] == ~0ull);
         }
         if (write) {
-            load_key(row, refs, r);
+            load_key(row, a.refs, r);
             row[S_USED] = live ? 1u : 2u;
             if (live) {
-                const uint64_t txrow = row_base + t;   // this batch's ids were appended to the side table at row_base
+                const uint64_t txrow = a.row_base + t;   // this batch's ids were appended to the side table at row_base
                 row[S_ROW] = (uint32_t)txrow;
                 row[S_ROW + 1] = (uint32_t)(txrow >> 32);
-                row[S_IDX] = pos[r];
-                row[S_CALLER] = callers[t];
+                row[S_IDX] = a.pos[r];
+                row[S_CALLER] = a.callers[t];
             }
-            fresh = (own[o] & OWN_FRESH) ? 1u : 0u;
-            slot = tslot[r];
+            fresh = (a.own[o] & OWN_FRESH) ? 1u : 0u;
+            slot = a.tslot[r];
         }
     }
-    wave_store_slots(tab, slot, row, stage[threadIdx.x >> 6]);
-    spread_add(count, live);
-    spread_add(count + 1, fresh);
+    wave_store_slots(a.tab, slot, row, stage);
+    spread_add(a.count, live);
+    spread_add(a.count + 1, fresh);
+}
+__global__ void __launch_bounds__(256) k_uniq_insert(InsertArgs a) {
+    __shared__ uint32_t stage[4][64 * STAGE_W];
+    insert_body((uint64_t)blockIdx.x * blockDim.x + threadIdx.x, a, stage[threadIdx.x >> 6]);
+}
+// the inserts and the failed transactions' classification in one grid (blocks [0, ins_blocks) insert): they
+// touch disjoint slots (inserts: claimed, not live; classify: live), so they share the chip instead of
+// running one after the other
+__global__ void __launch_bounds__(256) k_uniq_insert_classify(InsertArgs ia, uint32_t ins_blocks, ClassifyArgs ca) {
+    __shared__ uint32_t stage[4][64 * STAGE_W];
+    if (blockIdx.x < ins_blocks) insert_body((uint64_t)blockIdx.x * blockDim.x + threadIdx.x, ia, stage[threadIdx.x >> 6]);
+    else classify_body((uint64_t)(blockIdx.x - ins_blocks) * blockDim.x + threadIdx.x, ca);
 }
 
 __global__ void __launch_bounds__(256) k_uniq_status(uint64_t ntx, const uint8_t* __restrict__ st,
@@ -734,18 +773,11 @@ int chip_uniq_open(chip_ctx* ctx, uint64_t capacity, chip_uniq** out) {
     if (!r && hipHostMalloc((void**)&u->h_spread, SPREAD * 64, hipHostMallocDefault) != hipSuccess) r = CHIP_E_NOMEM;
     if (!r && hipHostMalloc((void**)&u->h_gate, 64, hipHostMallocDefault) != hipSuccess) r = CHIP_E_NOMEM;
     if (!r && hipHostMalloc((void**)&u->h_icount, SPREAD * 64, hipHostMallocDefault) != hipSuccess) r = CHIP_E_NOMEM;
-    if (!r && (hipStreamCreateWithFlags(&u->ist, hipStreamNonBlocking) != hipSuccess ||
-               hipEventCreateWithFlags(&u->iev0, hipEventDisableTiming) != hipSuccess ||
-               hipEventCreateWithFlags(&u->iev1, hipEventDisableTiming) != hipSuccess))
-        r = CHIP_E_DEVICE;
     if (r || hipStreamSynchronize(u->stream) != hipSuccess) {
         if (u->tab) hipFree(u->tab);
         if (u->h_spread) hipHostFree(u->h_spread);
         if (u->h_gate) hipHostFree(u->h_gate);
         if (u->h_icount) hipHostFree(u->h_icount);
-        if (u->ist) hipStreamDestroy(u->ist);
-        if (u->iev0) hipEventDestroy(u->iev0);
-        if (u->iev1) hipEventDestroy(u->iev1);
         hipStreamDestroy(u->stream);
         delete u;
         return r ? r : CHIP_E_DEVICE;
@@ -763,10 +795,6 @@ void chip_uniq_close(chip_uniq* u) {
     if (u->h_spread) hipHostFree(u->h_spread);
     if (u->h_gate) hipHostFree(u->h_gate);
     if (u->h_icount) hipHostFree(u->h_icount);
-    hipStreamSynchronize(u->ist);
-    hipStreamDestroy(u->ist);
-    hipEventDestroy(u->iev0);
-    hipEventDestroy(u->iev1);
     UBuf* bufs[] = {&u->reftx,  &u->pre,    &u->tslot,  &u->sid, &u->own, &u->passed, &u->rdup, &u->spread,
                     &u->bmin,   &u->bcommit, &u->st,    &u->flag,  &u->scan,   &u->cub,    &u->ctr,
                     &u->refpos, &u->h_start, &u->h_refs, &u->h_ids, &u->h_call, &u->h_st,  &u->h_vote,
@@ -891,48 +919,54 @@ int chip_uniq_shard_apply(chip_uniq* u, const uint8_t* decision, uint64_t* undec
     return CHIP_OK;
 }
 
+static ClassifyArgs classify_args(const chip_uniq* u, uint8_t* vote) {
+    return ClassifyArgs{u->ntx, u->start, u->pos, u->pre.as<uint32_t>(), u->sid.as<uint32_t>(), u->rdup.as<uint8_t>(),
+                        u->bcommit.as<unsigned long long>(), u->ids, u->callers, u->tab, u->txrows,
+                        u->st.as<uint8_t>(), vote, u->flag.as<uint32_t>()};
+}
+
 int chip_uniq_shard_classify(chip_uniq* u, uint8_t* vote) {
     if (!u) return CHIP_E_ARG;
     if (!u->open || (u->ntx && !vote)) return ufail(u, CHIP_E_ARG, "no batch in flight / null vote");
     if (u->ntx)
-        hipLaunchKernelGGL(k_uniq_classify, dim3(blocks_for(u->ntx)), dim3(256), 0, u->bst, u->ntx, u->start, u->pos,
-                           u->pre.as<uint32_t>(), u->sid.as<uint32_t>(), u->rdup.as<uint8_t>(),
-                           u->bcommit.as<unsigned long long>(), u->ids,
-                           u->callers, u->tab, u->txrows, u->st.as<uint8_t>(), vote, u->flag.as<uint32_t>());
+        hipLaunchKernelGGL(k_uniq_classify, dim3(blocks_for(u->ntx)), dim3(256), 0, u->bst, classify_args(u, vote));
     UCHK(u, hipGetLastError());
     return CHIP_OK;
 }
 
 // the batch's ConsumingTx ids appended to the side table and the inserts of its committed inputs (after the
-// last round: they read the final statuses and bcommit).  On `ist` (forked from the batch stream) when
-// `side`, so that they overlap the records: those read pre-committed (live) slots and the side table's
-// older rows only, the inserts write claimed (not live) slots and the new rows.  Joined in finish.
-static int launch_insert(chip_uniq* u, bool side) {
+// last round: they read the final statuses and bcommit).  With `classify_vote` (the one-shard path) the
+// failed transactions' classification runs in the same grid (k_uniq_insert_classify): the records read
+// pre-committed (live) slots and the side table's older rows only, the inserts write claimed (not live)
+// slots and the new rows.
+static int launch_insert(chip_uniq* u, uint8_t* classify_vote) {
     const uint64_t nref = u->nref, ntx = u->ntx;
     u->inserted = true;
-    if (!nref || !ntx) return CHIP_OK;
     hipStream_t st = u->bst;
+    if (!nref || !ntx) {
+        if (classify_vote && ntx)
+            hipLaunchKernelGGL(k_uniq_classify, dim3(blocks_for(ntx)), dim3(256), 0, st, classify_args(u, classify_vote));
+        UCHK(u, hipGetLastError());
+        return CHIP_OK;
+    }
     int rc = ensure_rows(u, ntx, st);   // may reallocate the side table: before any kernel that reads it
     if (rc) return rc;
     const uint64_t row_base = u->rows;
-    if (side) {
-        UCHK(u, hipEventRecord(u->iev0, st));
-        UCHK(u, hipStreamWaitEvent(u->ist, u->iev0, 0));
-        st = u->ist;
-    }
     UCHK(u, hipMemsetAsync(u->icount.p, 0, SPREAD * 64, st));
     UCHK(u, hipMemcpyAsync(u->txrows + row_base * 32, u->ids, ntx * 32, hipMemcpyDeviceToDevice, st));
-    hipLaunchKernelGGL(k_uniq_insert, dim3(blocks_for(nref)), dim3(256), 0, st, nref, u->refs, u->reftx.as<uint32_t>(),
-                       u->pos, u->start, u->st.as<uint8_t>(), u->sid.as<uint32_t>(), u->rdup.as<uint8_t>(),
-                       u->pre.as<uint32_t>(), u->tslot.as<uint32_t>(), u->own.as<uint8_t>(), u->passed.as<uint8_t>(),
-                       u->bcommit.as<unsigned long long>(), row_base, u->callers, u->tab,
-                       u->icount.as<unsigned long long>());
+    const InsertArgs ia{nref, u->refs, u->reftx.as<uint32_t>(), u->pos, u->start, u->st.as<uint8_t>(),
+                        u->sid.as<uint32_t>(), u->rdup.as<uint8_t>(), u->pre.as<uint32_t>(), u->tslot.as<uint32_t>(),
+                        u->own.as<uint8_t>(), u->passed.as<uint8_t>(), u->bcommit.as<unsigned long long>(), row_base,
+                        u->callers, u->tab, u->icount.as<unsigned long long>()};
+    if (classify_vote) {
+        const uint32_t ib = blocks_for(nref);
+        hipLaunchKernelGGL(k_uniq_insert_classify, dim3(ib + blocks_for(ntx)), dim3(256), 0, st, ia, ib,
+                           classify_args(u, classify_vote));
+    } else {
+        hipLaunchKernelGGL(k_uniq_insert, dim3(blocks_for(nref)), dim3(256), 0, st, ia);
+    }
     UCHK(u, hipGetLastError());
     UCHK(u, hipMemcpyAsync(u->h_icount, u->icount.p, SPREAD * 64, hipMemcpyDeviceToHost, st));
-    if (side) {
-        UCHK(u, hipEventRecord(u->iev1, st));
-        UCHK(u, hipStreamWaitEvent(u->bst, u->iev1, 0));
-    }
     u->rows += ntx;
     return CHIP_OK;
 }
@@ -948,7 +982,7 @@ int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_st
     uint32_t* nrec = u->flag.as<uint32_t>();   // per-tx record counts (k_uniq_classify)
     uint32_t* at = u->scan.as<uint32_t>();
     int rc;
-    if (!u->inserted && (rc = launch_insert(u, false))) return rc;   // the phase API: in order on the batch stream
+    if (!u->inserted && (rc = launch_insert(u, nullptr))) return rc;   // the phase API: in order on the batch stream
     uint32_t last[2] = {0, 0};
     if (nref && ntx) {
         size_t tmp = 0;
@@ -967,7 +1001,6 @@ int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_st
                            tx_status);
     UCHK(u, hipGetLastError());
     UCHK(u, hipStreamSynchronize(st));
-    UCHK(u, hipStreamSynchronize(u->ist));
     const uint64_t nout = (uint64_t)last[0] + last[1];
     if (nref && ntx) {
         u->size += spread_total(u->h_icount, 0);
@@ -1013,11 +1046,7 @@ static int commit_device(chip_uniq* u, const chip_uniq_shard_batch* b, uint8_t* 
         }
         if (!*u->h_gate) break;
     }
-    if ((r = launch_insert(u, true))) {
-        u->open = false;
-        return r;
-    }
-    if ((r = chip_uniq_shard_classify(u, vote))) {
+    if ((r = launch_insert(u, vote))) {   // inserts + classification, one grid
         u->open = false;
         return r;
     }
