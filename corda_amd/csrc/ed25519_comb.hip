@@ -501,12 +501,12 @@ __global__ void __launch_bounds__(256) k_ed_comb_finish(const uint32_t* __restri
                                                         const uint8_t* __restrict__ sig_data,
                                                         const uint64_t* __restrict__ sig_off,
                                                         const uint32_t* __restrict__ xyz, uint32_t* __restrict__ zpre,
-                                                        uint64_t cap, uint8_t* __restrict__ status) {
+                                                        uint64_t cap, uint8_t* __restrict__ status, uint32_t g) {
     const uint32_t n = ctr[ED_CTR_NCOMB];
-    const uint32_t lanes = (n + ED_FIN_G - 1) / ED_FIN_G;
+    const uint32_t lanes = (n + g - 1) / g;
     const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= lanes) return;
-    const uint32_t ne = min((uint32_t)ED_FIN_G, (n - l + lanes - 1) / lanes);
+    const uint32_t ne = min(g, (n - l + lanes - 1) / lanes);
     const uint32_t* Zs = xyz + 20 * cap;
     fe acc, z;
     for (uint32_t e = 0; e < ne; e++) {
@@ -591,6 +591,11 @@ void launch_ed_comb_ahalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, c
 
 void launch_ed_comb_finish(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w, uint8_t* status) {
     if (!n || !w.max_slots) return;
-    hipLaunchKernelGGL(k_ed_comb_finish, dim3(nblk((n + ED_FIN_G - 1) / ED_FIN_G, 256)), dim3(256), 0, st, w.comb_list,
-                       w.ctr, b->sig_data, b->sig_off, w.xyz, w.zpre, (uint64_t)n, status);
+    // signatures per inversion: ED_FIN_G (16) for 2^20-signature batches; fewer for smaller ones (the chunks of
+    // a host batch), whose lanes would otherwise be too few to fill the chip (each lane's chain is serial):
+    // about 64k lanes, 4 <= g <= ED_FIN_G
+    uint32_t g = ED_FIN_G;
+    while (g > 4 && n / g < 49152) g >>= 1;
+    hipLaunchKernelGGL(k_ed_comb_finish, dim3(nblk((n + g - 1) / g, 256)), dim3(256), 0, st, w.comb_list,
+                       w.ctr, b->sig_data, b->sig_off, w.xyz, w.zpre, (uint64_t)n, status, g);
 }
