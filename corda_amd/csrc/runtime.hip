@@ -509,6 +509,7 @@ struct VerifyChunk {
     uint64_t n_decide;
     bool reuse_keys;
     hipEvent_t data_ready;   // the chunk's signatures / pools are on the device (waited for after the key prep)
+    bool keys_only;          // size the workspaces for b->n, prep the keys, fork the table builds, and stop
 };
 
 static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap, hipStream_t st,
@@ -631,6 +632,10 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         HIPCHK(c, hipEventRecord(c->ev_join2, fs));
     }
     c->kend(ke, st);
+    if (vc && vc->keys_only) {
+        c->stats.keys_prepared += nk;
+        return CHIP_OK;
+    }
     if (vc && vc->data_ready) HIPCHK(c, hipStreamWaitEvent(st, vc->data_ready, 0));
     if (n) {
         const uint32_t blocks = (uint32_t)((n + CLASSIFY_BLOCK - 1) / CLASSIFY_BLOCK);
@@ -968,7 +973,23 @@ static int verify_host_pipelined(chip_ctx* c, const chip_sig_batch* b, uint8_t* 
     d.msg_off = c->h_msg_off.as<uint64_t>();
     d.msg_len = c->h_msg_len.as<uint32_t>();
     if (!d.schemes) d.schemes = host_scheme_hint(b);
-    if ((r = stage_chunk(0))) return r;
+    {   // key prep and the table chains as soon as the keys are staged (before any chunk's pools), with every
+        // workspace sized for the largest chunk: no reallocation (an implicit device sync) between chunks
+        uint64_t mmax = 0;
+        for (size_t j = 0; j + 1 < at.size(); j++) mmax = std::max(mmax, at[j + 1] - at[j]);
+        d.n = mmax;
+        d.key_idx = c->h_key_idx.as<uint32_t>();
+        d.msg_idx = c->h_msg_idx.as<uint32_t>();
+        d.sig_off = c->h_sig_off.as<uint64_t>();
+        d.sig_len = c->h_sig_len.as<uint32_t>();
+        const VerifyChunk kv{n, false, nullptr, true};
+        if ((r = verify_device_locked(c, &d, c->h_status.as<uint8_t>(), c->h_bitmap.as<uint64_t>(), st, is_valid, &kv)))
+            return r;
+    }
+    if ((r = stage_chunk(0))) {
+        hipStreamSynchronize(st);
+        return r;
+    }
     for (uint64_t j = 0; j + 1 < at.size(); j++) {
         const uint64_t a = at[j], m = at[j + 1] - a;
         d.n = m;
@@ -976,7 +997,7 @@ static int verify_host_pipelined(chip_ctx* c, const chip_sig_batch* b, uint8_t* 
         d.msg_idx = c->h_msg_idx.as<uint32_t>() + a;
         d.sig_off = c->h_sig_off.as<uint64_t>() + a;
         d.sig_len = c->h_sig_len.as<uint32_t>() + a;
-        const VerifyChunk vc{n, j > 0, c->hev_p};
+        const VerifyChunk vc{n, true, c->hev_p, false};
         if ((r = verify_device_locked(c, &d, c->h_status.as<uint8_t>() + a, c->h_bitmap.as<uint64_t>() + a / 64, st,
                                       is_valid, &vc))) {
             hipStreamSynchronize(st);
