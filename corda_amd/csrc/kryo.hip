@@ -631,6 +631,23 @@ __device__ __forceinline__ bool header_ok(Cur& c) {
     return !c.err;
 }
 
+// Component k's (group, offset, length): the SoA arrays, or, for the first KRYO_LM_C components of transaction t
+// (first index cbase) while pass 2 runs, its lane-major rows (entry j of tx t at [j * n + t]).
+struct CompAcc {
+    const uint32_t* grp_soa;
+    const uint64_t* off_soa;
+    const uint32_t* len_soa;
+    const uint32_t* lm_grp;   // NULL: the SoA arrays only
+    const uint64_t* lm_off;
+    const uint32_t* lm_len;
+    uint64_t n, t, cbase;
+    __device__ __forceinline__ bool lm(uint64_t k) const { return lm_off && k - cbase < KRYO_LM_C; }
+    __device__ __forceinline__ uint64_t li(uint64_t k) const { return (k - cbase) * n + t; }
+    __device__ __forceinline__ uint32_t grp(uint64_t k) const { return lm(k) ? lm_grp[li(k)] : grp_soa[k]; }
+    __device__ __forceinline__ uint64_t off(uint64_t k) const { return lm(k) ? lm_off[li(k)] : off_soa[k]; }
+    __device__ __forceinline__ uint32_t len(uint64_t k) const { return lm(k) ? lm_len[li(k)] : len_soa[k]; }
+};
+
 // requiredSigningKeys walk (WireTransaction.kt:66-75) over one transaction's components in the pool:
 // take(off, len, required) for each signer key of every Command component in order, then for the notary
 // Party's owningKey — required when the transaction has inputs or a time-window; otherwise taken with
@@ -639,12 +656,11 @@ __device__ __forceinline__ bool header_ok(Cur& c) {
 // Structures.kt:183) or a key spans a chunk (the caller marks the transaction UNSUPPORTED).
 template <class F>
 __device__ __forceinline__ bool req_walk(Cur& c, const uint8_t* pool, uint64_t pool_bytes, uint64_t c0, uint64_t c1,
-                                         const uint32_t* comp_group, const uint64_t* comp_off,
-                                         const uint32_t* comp_len, const chip_kryo_registry& reg, F&& take) {
+                                         const CompAcc& ca, const chip_kryo_registry& reg, F&& take) {
     uint64_t present = 0;
     int64_t notary = -1;
     for (uint64_t k = c0; k < c1; k++) {
-        const uint32_t g = comp_group[k];
+        const uint32_t g = ca.grp(k);
         present |= 1ull << g;
         if (g == 4 && notary < 0) notary = (int64_t)k;
     }
@@ -654,14 +670,14 @@ __device__ __forceinline__ bool req_walk(Cur& c, const uint8_t* pool, uint64_t p
     for (uint64_t k = c0; k <= c1; k++) {
         int64_t kk;
         if (k < c1) {
-            if (comp_group[k] != 2) continue;
+            if (ca.grp(k) != 2) continue;
             kk = (int64_t)k;
         } else {
             if (notary < 0) break;
             kk = notary;
         }
-        const uint64_t a = comp_off[kk];
-        c.init(pool, pool_bytes, a, a + comp_len[kk]);
+        const uint64_t a = ca.off(kk);
+        c.init(pool, pool_bytes, a, a + ca.len(kk));
         if (!header_ok(c)) return false;
         const bool is_cmd = k < c1;
         if (c.read_class<0>(is_cmd ? M_OF(C_COMMAND) : M_OF(C_PARTY)) != (is_cmd ? -C_COMMAND : -C_PARTY))
@@ -710,6 +726,14 @@ struct Outs {   // pass-2 destinations (NULL in pass 1)
     chip_kryo_registry reg;
     uint64_t* rec_off;             // [n * STX_REC] the first STX_REC signer entries of each tx (with nraw)
     uint32_t* rec_len;             //   length | required << 31
+    // lane-major rows of the first KRYO_LM_C components / KRYO_LM_S signatures of each tx (StxOut): a wave's
+    // lanes store entry j of consecutive transactions side by side, whole lines, instead of each lane
+    // writing partial lines of its own range; k_stx_lm_comps / k_stx_lm_sigs transpose them afterwards
+    uint64_t n_lm;
+    uint64_t* lm_off;
+    uint32_t *lm_len, *lm_int, *lm_grp;
+    uint64_t* lm_soff;
+    uint32_t *lm_slen, *lm_tmpl;
 };
 
 template <bool EMIT>
@@ -765,8 +789,13 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
             {
                 const uint64_t at = run1<EMIT>(c, sl, sink, extra);
                 if (EMIT && !KRYO_NO_STORES) {
-                    o.sig_off[sbase + sigs] = at;
-                    o.sig_len[sbase + sigs] = sl;
+                    if (sigs < KRYO_LM_S) {
+                        o.lm_soff[sigs * o.n_lm + t] = at;
+                        o.lm_slen[sigs * o.n_lm + t] = sl;
+                    } else {
+                        o.sig_off[sbase + sigs] = at;
+                        o.sig_len[sbase + sigs] = sl;
+                    }
                 }
             }
             c.end_field<1>();
@@ -801,8 +830,12 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
                         break;
                     }
                 if (!KRYO_NO_STORES) {
-                    o.tmpl_idx[sbase + sigs] = ti;
-                    o.tx_idx[sbase + sigs] = (uint32_t)t;
+                    if (sigs < KRYO_LM_S) {
+                        o.lm_tmpl[sigs * o.n_lm + t] = ti;   // tx_idx = t, written by the transpose
+                    } else {
+                        o.tmpl_idx[sbase + sigs] = ti;
+                        o.tx_idx[sbase + sigs] = (uint32_t)t;
+                    }
                 }
             }
             sigs++;
@@ -849,9 +882,15 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
                 if (EMIT) {
                     const uint64_t at = run1<EMIT>(w, cl, sink, extra);
                     if (!KRYO_NO_STORES) {
-                        o.comp_off[cbase + comps] = at;
-                        o.comp_len[cbase + comps] = cl;
-                        o.comp_internal[cbase + comps] = k;
+                        if (comps < KRYO_LM_C) {
+                            o.lm_off[comps * o.n_lm + t] = at;
+                            o.lm_len[comps * o.n_lm + t] = cl;
+                            o.lm_int[comps * o.n_lm + t] = k;
+                        } else {
+                            o.comp_off[cbase + comps] = at;
+                            o.comp_len[cbase + comps] = cl;
+                            o.comp_internal[cbase + comps] = k;
+                        }
                     }
                 } else {
                     // the extra region is sized by run1's rule: a run not inside the current chunk
@@ -882,7 +921,10 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
                 in_count = nc;
             }
             if (EMIT)
-                for (uint64_t k = first; k < cbase + comps && !KRYO_NO_STORES; k++) o.comp_group[k] = (uint32_t)gi;
+                for (uint64_t k = first; k < cbase + comps && !KRYO_NO_STORES; k++) {
+                    if (k - cbase < KRYO_LM_C) o.lm_grp[(k - cbase) * o.n_lm + t] = (uint32_t)gi;
+                    else o.comp_group[k] = (uint32_t)gi;
+                }
         }
         // PrivacySalt: the registry's id, writeBytesWithLength(32 bytes)
         if (!w.err) {
@@ -913,10 +955,11 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
         if (in_count > 64 || noncanon) st = st == CHIP_STX_OK ? CHIP_STX_UNSUPPORTED : st;
         if (EMIT && st == CHIP_STX_OK && in_count > 1 && !KRYO_NO_STORES) {   // checkNoDuplicateInputs: equal serialized StateRefs
             sink.flush();
+            const CompAcc ca{o.comp_group, o.comp_off, o.comp_len, o.lm_grp, o.lm_off, o.lm_len, o.n_lm, t, cbase};
             for (uint64_t i = 0; i < in_count && st == CHIP_STX_OK; i++)
                 for (uint64_t j = i + 1; j < in_count; j++) {
-                    if (key_eq(o.pool, o.comp_off[in_first + i], o.comp_len[in_first + i], o.comp_off[in_first + j],
-                               o.comp_len[in_first + j])) {
+                    if (key_eq(o.pool, ca.off(in_first + i), ca.len(in_first + i), ca.off(in_first + j),
+                               ca.len(in_first + j))) {
                         st = CHIP_STX_INVARIANT;
                         break;
                     }
@@ -930,7 +973,8 @@ done:
             uint64_t cnt = 0, all = 0;
             bool over = false;
             if (st == CHIP_STX_OK &&
-                !req_walk(c, o.pool, o.pool_bytes, cbase, cbase + comps, o.comp_group, o.comp_off, o.comp_len, o.reg,
+                !req_walk(c, o.pool, o.pool_bytes, cbase, cbase + comps,
+                          CompAcc{o.comp_group, o.comp_off, o.comp_len, o.lm_grp, o.lm_off, o.lm_len, o.n_lm, t, cbase}, o.reg,
                           [&](uint64_t at, uint32_t len, bool req) {
                               if (req) {
                                   over |= cnt >= 64;
@@ -1199,8 +1243,8 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_required(uint64_t n, uint8_t
         }
     } else {
         Cur c;
-        if (!req_walk(c, r.pool, pool_bytes, comp_start[t], comp_start[t + 1], comp_group, comp_off, comp_len, reg,
-                      take))
+        if (!req_walk(c, r.pool, pool_bytes, comp_start[t], comp_start[t + 1],
+                      CompAcc{comp_group, comp_off, comp_len, nullptr, nullptr, nullptr, 0, 0, 0}, reg, take))
             bad = true;
     }
     if (bad) status[t] = CHIP_STX_UNSUPPORTED;
@@ -1418,14 +1462,54 @@ void launch_stx_count(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_
                        in->data_bytes, status, ncomp, nsig, nextra, o);
 }
 
+// the transaction t of entry c of a range array (start[0] = 0, start[n] > c): the last t with start[t] <= c
+__device__ __forceinline__ uint64_t owner_of(const uint64_t* __restrict__ start, uint64_t n, uint64_t c) {
+    uint64_t lo = 0, hi = n;
+    while (hi - lo > 1) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if (start[mid] <= c) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+// pass 2's lane-major rows into the SoA arrays, one lane per entry (coalesced stores)
+__global__ void __launch_bounds__(256) k_stx_lm_comps(uint64_t n, uint64_t ncomp, const uint64_t* __restrict__ start,
+                                                      Outs o) {
+    const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= ncomp) return;
+    const uint64_t t = owner_of(start, n, c), j = c - start[t];
+    if (j >= KRYO_LM_C) return;   // stored in place by pass 2
+    const uint64_t i = j * o.n_lm + t;
+    o.comp_off[c] = o.lm_off[i];
+    o.comp_len[c] = o.lm_len[i];
+    o.comp_internal[c] = o.lm_int[i];
+    o.comp_group[c] = o.lm_grp[i];
+}
+__global__ void __launch_bounds__(256) k_stx_lm_sigs(uint64_t n, uint64_t nsig, const uint64_t* __restrict__ start,
+                                                     Outs o) {
+    const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (s >= nsig) return;
+    const uint64_t t = owner_of(start, n, s), j = s - start[t];
+    if (j >= KRYO_LM_S) return;
+    const uint64_t i = j * o.n_lm + t;
+    o.sig_off[s] = o.lm_soff[i];
+    o.sig_len[s] = o.lm_slen[i];
+    o.tmpl_idx[s] = o.lm_tmpl[i];
+    o.tx_idx[s] = (uint32_t)t;
+}
+
 void launch_stx_emit(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_registry& reg, uint8_t* status,
                      const StxOut& d) {
     if (!in->n) return;
     Outs o{d.pool, d.pool_bytes, d.extra_start, d.extra_base, d.salts, d.comp_start, d.comp_group, d.comp_internal, d.comp_off, d.comp_len, d.sig_start,
            d.tx_idx, d.tmpl_idx, d.sig_off, d.sig_len, d.skey_off, d.skey_len, d.meta, d.n_meta, d.nraw, reg,
-           d.rec_off, d.rec_len};
+           d.rec_off, d.rec_len, in->n, d.lm_off, d.lm_len, d.lm_int, d.lm_grp, d.lm_soff, d.lm_slen, d.lm_tmpl};
     hipLaunchKernelGGL(k_stx_parse<true>, grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->off, in->len,
                        in->data_bytes, status, nullptr, nullptr, nullptr, o);
+    if (d.ncomp)
+        hipLaunchKernelGGL(k_stx_lm_comps, grid_of(d.ncomp), dim3(256), 0, st, in->n, d.ncomp, d.comp_start, o);
+    if (d.nsig)
+        hipLaunchKernelGGL(k_stx_lm_sigs, grid_of(d.nsig), dim3(256), 0, st, in->n, d.nsig, d.sig_start, o);
 }
 
 size_t stx_scan_temp_bytes(uint64_t n) {

@@ -85,7 +85,16 @@ struct StxOut {
     uint32_t* key_idx;             // [nsig] into the de-duplicated key pool
     uint64_t* key_off;             // [n_keys]
     uint32_t* key_len;
+    // pass 2's per-transaction entries lane-major (entry k of tx t at [k * n + t], the first KRYO_LM_C
+    // components and KRYO_LM_S signatures of each tx), transposed into the arrays above after the pass
+    uint64_t ncomp, nsig;
+    uint64_t* lm_off;              // [KRYO_LM_C * n]
+    uint32_t *lm_len, *lm_int, *lm_grp;
+    uint64_t* lm_soff;             // [KRYO_LM_S * n]
+    uint32_t *lm_slen, *lm_tmpl;
 };
+#define KRYO_LM_C 16
+#define KRYO_LM_S 4
 void launch_stx_count(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_registry& reg, uint8_t* status,
                       uint64_t* ncomp, uint64_t* nsig, uint64_t* nextra);
 void launch_stx_emit(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_registry& reg, uint8_t* status,
