@@ -84,7 +84,7 @@ struct chip_ctx {
     // required signers: staging of the host entries
     DevBuf q_sigs, q_reqs, q_nodes, q_allowed, q_val, q_nk, q_w, q_st, q_verdict, q_arg, q_missing;
     // filtered transactions: kernel scratch + staging of the host entry
-    DevBuf x_scratch, x_ids, x_ghs, x_gh, x_fgs, x_fgi, x_cs, x_cd, x_co, x_cl, x_nonce, x_pts, x_ptt, x_pth, x_cv,
+    DevBuf x_scratch, x_ids, x_ghs, x_gh, x_fgs, x_fgi, x_cs, x_cd, x_co, x_cl, x_nonce, x_pts, x_ptt, x_pth, x_cv, x_vm,
         x_st, x_rs;
     // Kryo front end (kryo.hip): two buffer sets used alternately, so batch k + 1 can be parsed (one
     // stream) while batch k is verified from the other set (another stream)
@@ -461,7 +461,7 @@ void chip_shutdown(chip_ctx* c) {
                       &c->t_scratch, &c->f_pool, &c->f_moff, &c->f_mlen, &c->f_midx, &c->f_htx, &c->f_htm,
                       &c->f_tdata, &c->f_toff, &c->f_tlen, &c->f_tid, &c->x_scratch, &c->x_ids, &c->x_ghs,
                       &c->x_gh, &c->x_fgs, &c->x_fgi, &c->x_cs, &c->x_cd, &c->x_co, &c->x_cl, &c->x_nonce,
-                      &c->x_pts, &c->x_ptt, &c->x_pth, &c->x_cv, &c->x_st, &c->x_rs,
+                      &c->x_pts, &c->x_ptt, &c->x_pth, &c->x_cv, &c->x_vm, &c->x_st, &c->x_rs,
                       &c->h2_data, &c->h2_off, &c->h2_len, &c->h2_st, &c->h2_ids, &c->h2_v,
                       &c->h2_a, &c->h2_sigst, &c->h2_miss, &c->h2_td, &c->h2_to, &c->h2_tl, &c->h2_ta};
     for (DevBuf* b : bufs) b->release();
@@ -903,6 +903,17 @@ static int verify_host_pipelined(chip_ctx* c, const chip_sig_batch* b, uint8_t* 
     if ((r = stage(c, c->h_key_data, b->key_data, b->key_bytes, cs)) || (r = stage(c, c->h_key_off, b->key_off, nk, cs)) ||
         (r = stage(c, c->h_key_len, b->key_len, nk, cs)))
         return r;
+    if (nk) {   // the key ranges inside the key pool before the key prep reads through them (no signature, no message)
+        unsigned long long* out = c->h_rngd.as<unsigned long long>();
+        hipLaunchKernelGGL(k_chunk_init, dim3(1), dim3(64), 0, cs, out);
+        hipLaunchKernelGGL(k_check_chunk, dim3((uint32_t)((nk + 255) / 256)), dim3(256), 0, cs, 0ull, nk, 0ull, true,
+                           nullptr, nullptr, nullptr, nullptr, 0ull, c->h_key_off.as<uint64_t>(), c->h_key_len.as<uint32_t>(),
+                           b->key_bytes, nullptr, nullptr, 0ull, out);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(c->h_rng, out, 64, hipMemcpyDeviceToHost, cs));
+        HIPCHK(c, hipStreamSynchronize(cs));
+        if (int rc = check_flags(c, c->h_rng[0])) return rc;
+    }
     HIPCHK(c, hipEventRecord(c->hev_c, cs));
     HIPCHK(c, hipStreamWaitEvent(st, c->hev_c, 0));   // the key prep and the table chains start on the keys alone
     if ((r = stage(c, c->h_msg_off, b->msg_off, nm, cs)) || (r = stage(c, c->h_msg_len, b->msg_len, nm, cs))) return r;
@@ -1927,7 +1938,8 @@ int chip_ftx_verify_batch(chip_ctx* c, const chip_ftx_batch* b, uint8_t* status,
             (r = stage(c, c->x_cl, b->comp_len, ncomp, st)) || (r = stage(c, c->x_nonce, b->nonces, ncomp * 32, st)) ||
             (r = stage(c, c->x_pts, b->pt_start, nfg ? nfg + 1 : 0, st)) || (r = stage(c, c->x_ptt, b->pt_tag, nnodes, st)) ||
             (r = stage(c, c->x_pth, b->pt_hash, nnodes * 32, st)) ||
-            (r = stage(c, c->x_cv, b->check_visible, b->check_visible ? ntx : 0, st)))
+            (r = stage(c, c->x_cv, b->check_visible, b->check_visible ? ntx : 0, st)) ||
+            (r = stage(c, c->x_vm, b->visible_mask, b->visible_mask ? ntx : 0, st)))
             return r;
         HIPCHK(c, c->x_st.ensure(ntx + 16));
         HIPCHK(c, c->x_rs.ensure(ntx + 16));
@@ -1958,6 +1970,7 @@ int chip_ftx_verify_batch(chip_ctx* c, const chip_ftx_batch* b, uint8_t* status,
     d.pt_tag = c->x_ptt.as<uint8_t>();
     d.pt_hash = c->x_pth.as<uint8_t>();
     d.check_visible = b->check_visible ? c->x_cv.as<int32_t>() : nullptr;
+    d.visible_mask = b->visible_mask ? c->x_vm.as<uint32_t>() : nullptr;
     if ((r = chip_ftx_verify_batch_device(c, &d, c->x_st.as<uint8_t>(), c->x_rs.as<uint8_t>(), st))) return r;
     std::lock_guard<std::recursive_mutex> g(c->mu);
     HIPCHK(c, hipMemcpyAsync(status, c->x_st.p, ntx, hipMemcpyDeviceToHost, st));

@@ -7,8 +7,8 @@
 //   MerkleRoot  = pad with zeroHash to 2^k; 1 leaf -> the leaf; nodes SHA256(l || r)  MerkleTree.kt:27-66
 //
 // One lane per transaction (the unit the caller batches; no cross-lane divergence for
-// same-shaped transactions).  Fast path (groups in ascending ordinal order, <= 8 components each: what
-// createComponentGroups produces for ordinary transactions): every tree is reduced in registers as its
+// same-shaped transactions).  Fast path (groups in ascending ordinal order, ordinals < 16, <= 16 components each
+// (TX_LEVELS): what createComponentGroups produces for ordinary transactions): every tree is reduced in LDS stacks as its
 // leaves arrive (a binary-counter stack per tree, padding subtrees from the constant zero-hash chain), so
 // nothing but the id is written.  Otherwise the leaf and group-root levels are reduced in place in a
 // per-tx scratch slab in HBM (64 slots x 32 B; group ordinals must be < 64).
@@ -269,7 +269,8 @@ struct MerkleLds {
 #define TX_FAST_GROUP_LEAVES (1u << TX_LEVELS)
 #define TX_FAST_TOP (1u << TX_LEVELS)
 
-// the fast path's precondition: groups in strictly ascending ordinal order, each of <= 8 components
+// the fast path's precondition: groups in strictly ascending ordinal order, ordinals < 16, each of <= 16 components
+// (TX_FAST_GROUP_LEAVES = TX_FAST_TOP = 2^TX_LEVELS)
 CHIP_DEV bool txid_fast_ok(const uint32_t* __restrict__ grp, uint64_t a, uint64_t e) {
     uint32_t prev = 0xffffffffu, run = 0;
     for (uint64_t k = a; k < e; k++) {
@@ -402,6 +403,39 @@ CHIP_DEV bool eq8(const uint32_t* a, const uint32_t* b) {
     return d == 0;
 }
 
+// FilteredTransaction.checkAllComponentsVisible(ord) (MerkleTransaction.kt:218-234) for filtered tx t
+CHIP_DEV void ftx_visible(const chip_ftx_batch& b, uint64_t t, uint64_t g0, uint64_t ngh, uint32_t ord,
+                          uint32_t* __restrict__ comps, uint32_t (&h)[8], uint8_t& st, uint8_t& rs) {
+    int64_t found = -1;
+    for (uint64_t g = b.fg_start[t]; g < b.fg_start[t + 1]; g++)
+        if (b.fg_index[g] == ord) { found = (int64_t)g; break; }
+    if (found < 0) {
+        bool ok = (uint64_t)ord >= ngh;
+        if (!ok) {
+            ld8_be(h, b.group_hashes + 32 * (g0 + ord));
+            ok = true;
+#pragma unroll
+            for (int j = 0; j < 8; j++) ok = ok && h[j] == 0xffffffffu;
+        }
+        if (!ok) { st = 2; rs = 6; }
+        return;
+    }
+    const uint32_t gi = b.fg_index[found];
+    const uint64_t c0 = b.comp_start[found], nc = b.comp_start[found + 1] - c0;
+    if (gi >= ngh) { st = 2; rs = 7; return; }
+    if (nc == 0 || nc > FTX_MAX_COMPS) { st = 2; rs = 8; return; }
+    for (uint64_t c = 0; c < nc; c++) {
+        uint32_t nonce[8], leaf[8];
+        ld8_be(nonce, b.nonces + 32 * (c0 + c));
+        sha256d_prefixed(leaf, nonce, b.comp_data + b.comp_off[c0 + c], b.comp_len[c0 + c]);
+        st8(comps + 8 * c, leaf);
+    }
+    uint32_t want[8];
+    merkle_inplace(h, comps, (uint32_t)nc, 0xffffffffu, 0xffffffffu, false);
+    ld8_be(want, b.group_hashes + 32 * (g0 + gi));
+    if (!eq8(h, want)) { st = 2; rs = 8; }
+}
+
 __global__ void __launch_bounds__(256) k_ftx_verify(chip_ftx_batch b, uint8_t* __restrict__ status,
                                                     uint8_t* __restrict__ reason, uint32_t* __restrict__ scratch) {
     const uint64_t lane = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -480,38 +514,15 @@ __global__ void __launch_bounds__(256) k_ftx_verify(chip_ftx_batch b, uint8_t* _
             if (!eq8(h, want)) { st = 1; rs = 4; break; }
             if (unmatched || nused != nc) { st = 1; rs = 5; break; }
         }
+        // checkAllComponentsVisible(check_visible[t]), then once per bit of visible_mask[t] in ascending ordinal
+        // (NonValidatingNotaryFlow.kt:27-29: INPUTS_GROUP, then TIMEWINDOW_GROUP); the first failure decides
         const int32_t cv = b.check_visible ? b.check_visible[t] : -1;
-        if (!st && cv >= 0) {
-            int64_t found = -1;
-            for (uint64_t g = b.fg_start[t]; g < b.fg_start[t + 1]; g++)
-                if (b.fg_index[g] == (uint32_t)cv) { found = (int64_t)g; break; }
-            if (found < 0) {
-                bool ok = (uint64_t)cv >= ngh;
-                if (!ok) {
-                    ld8_be(h, b.group_hashes + 32 * (g0 + cv));
-                    ok = true;
-#pragma unroll
-                    for (int j = 0; j < 8; j++) ok = ok && h[j] == 0xffffffffu;
-                }
-                if (!ok) { st = 2; rs = 6; }
-            } else {
-                const uint32_t gi = b.fg_index[found];
-                const uint64_t c0 = b.comp_start[found], nc = b.comp_start[found + 1] - c0;
-                if (gi >= ngh) { st = 2; rs = 7; }
-                else if (nc == 0 || nc > FTX_MAX_COMPS) { st = 2; rs = 8; }
-                else {
-                    for (uint64_t c = 0; c < nc; c++) {
-                        uint32_t nonce[8], leaf[8];
-                        ld8_be(nonce, b.nonces + 32 * (c0 + c));
-                        sha256d_prefixed(leaf, nonce, b.comp_data + b.comp_off[c0 + c], b.comp_len[c0 + c]);
-                        st8(comps + 8 * c, leaf);
-                    }
-                    uint32_t want[8];
-                    merkle_inplace(h, comps, (uint32_t)nc, 0xffffffffu, 0xffffffffu, false);
-                    ld8_be(want, b.group_hashes + 32 * (g0 + gi));
-                    if (!eq8(h, want)) { st = 2; rs = 8; }
-                }
-            }
+        uint64_t vis = (b.visible_mask ? (uint64_t)b.visible_mask[t] << 1 : 0ull) | (cv >= 0 ? 1ull : 0ull);
+        while (!st && vis) {
+            const uint32_t bit = (uint32_t)__builtin_ctzll(vis);
+            vis &= vis - 1;
+            const uint32_t ord = bit == 0 ? (uint32_t)cv : bit - 1;
+            ftx_visible(b, t, g0, ngh, ord, comps, h, st, rs);
         }
         status[t] = st;
         if (reason) reason[t] = rs;

@@ -252,6 +252,7 @@ __global__ void __launch_bounds__(256) k_uniq_lookup(uint64_t nref, const uint8_
             pre[r] = (uint32_t)i;
             sid[r] = 0x80000000u | (uint32_t)i;
             tslot[r] = NO_SLOT;
+            own[r] = 0;   // every exit writes own[r]: the rebuild and the inserts read it unconditionally
             return;
         }
         if (used == 0u || (used == 2u && eq)) {
@@ -265,6 +266,7 @@ __global__ void __launch_bounds__(256) k_uniq_lookup(uint64_t nref, const uint8_
                         pre[r] = NO_SLOT;
                         sid[r] = o;
                         tslot[r] = (uint32_t)i;
+                        own[r] = 0;
                         rdup[r] = 1;
                         rdup[o] = 1;
                         // the round / commit scratch of a dup state starts "empty" (every referencer
@@ -289,6 +291,7 @@ __global__ void __launch_bounds__(256) k_uniq_lookup(uint64_t nref, const uint8_
         }
         i = (i + 1) & (cap - 1);
     }
+    own[r] = 0;   // full table (not reached: load <= 1/2)
 }
 
 // Same-address atomics serialize at the memory side (~13 ns each): a per-wave count into ONE
@@ -603,11 +606,22 @@ __global__ void __launch_bounds__(256) k_uniq_status(uint64_t ntx, const uint8_t
     out[t] = st[t] == ST_COMMITTED ? 0 : (decision[t] >= 2 ? 2 : 1);
 }
 
-// rebuild (AppendOnlyPersistentMap.allPersisted): rows absent from the table, the owner of equal keys
+// rebuild with equal keys among the rows: the lowest row of each key is the one the map keeps
+// (AppendOnlyPersistentMap: the first value wins); bmin[owner] was set to ~0 by the lookup that found the dup
+__global__ void __launch_bounds__(256) k_uniq_rebuild_first(uint64_t n, const uint8_t* __restrict__ rdup,
+                                                            const uint32_t* __restrict__ pre, const uint32_t* __restrict__ sid,
+                                                            unsigned long long* __restrict__ bmin) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < n && rdup[r] && pre[r] == NO_SLOT) atomicMin(&bmin[sid[r]], (unsigned long long)r);
+}
+
+// rebuild (AppendOnlyPersistentMap.allPersisted): rows absent from the table, the first row of equal keys
 __global__ void __launch_bounds__(256) k_uniq_rebuild(uint64_t n, const uint8_t* __restrict__ refs,
                                                       uint64_t row_base, const uint32_t* __restrict__ idx,
                                                       const uint32_t* __restrict__ caller, const uint32_t* __restrict__ pre,
                                                       const uint32_t* __restrict__ tslot, const uint8_t* __restrict__ own,
+                                                      const uint8_t* __restrict__ rdup, const uint32_t* __restrict__ sid,
+                                                      const unsigned long long* __restrict__ bmin,
                                                       uint32_t* tab, unsigned long long* __restrict__ count) {
     __shared__ uint32_t stage[4][64 * STAGE_W];
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -615,7 +629,7 @@ __global__ void __launch_bounds__(256) k_uniq_rebuild(uint64_t n, const uint8_t*
     uint32_t row[SLOT_W];
 #pragma unroll
     for (int w = 0; w < SLOT_W; w++) row[w] = 0;
-    if (r < n && pre[r] == NO_SLOT && (own[r] & OWN_CLAIM)) {
+    if (r < n && pre[r] == NO_SLOT && (rdup[r] ? bmin[sid[r]] == r : (own[r] & OWN_CLAIM) != 0)) {
         load_key(row, refs, r);
         row[S_USED] = 1;
         const uint64_t txrow = row_base + r;   // the rebuild's ids were appended to the side table at row_base
@@ -625,7 +639,7 @@ __global__ void __launch_bounds__(256) k_uniq_rebuild(uint64_t n, const uint8_t*
         row[S_CALLER] = caller[r];
         slot = tslot[r];
         live = 1;
-        fresh = (own[r] & OWN_FRESH) ? 1u : 0u;
+        fresh = (own[sid[r]] & OWN_FRESH) ? 1u : 0u;   // the owner (claim winner) saw whether the slot was empty
     }
     wave_store_slots(tab, slot, row, stage[threadIdx.x >> 6]);
     spread_add(count, live);
@@ -831,9 +845,12 @@ int chip_uniq_rebuild(chip_uniq* u, uint64_t n, const uint8_t* refs36, const uin
     if ((r = launch_lookup(u, n, d_refs, st))) return r;
     if ((r = ensure_rows(u, n, st))) return r;
     UCHK(u, hipMemcpyAsync(u->txrows + u->rows * 32, u->h_ids.p, n * 32, hipMemcpyDeviceToDevice, st));
+    hipLaunchKernelGGL(k_uniq_rebuild_first, dim3(blocks_for(n)), dim3(256), 0, st, n, u->rdup.as<uint8_t>(),
+                       u->pre.as<uint32_t>(), u->sid.as<uint32_t>(), u->bmin.as<unsigned long long>());
     hipLaunchKernelGGL(k_uniq_rebuild, dim3(blocks_for(n)), dim3(256), 0, st, n, d_refs, u->rows,
                        u->refpos.as<uint32_t>(), u->h_call.as<uint32_t>(), u->pre.as<uint32_t>(),
-                       u->tslot.as<uint32_t>(), u->own.as<uint8_t>(), u->tab, u->spread.as<unsigned long long>());
+                       u->tslot.as<uint32_t>(), u->own.as<uint8_t>(), u->rdup.as<uint8_t>(), u->sid.as<uint32_t>(),
+                       u->bmin.as<unsigned long long>(), u->tab, u->spread.as<unsigned long long>());
     UCHK(u, hipGetLastError());
     if ((r = spread_fetch(u, st))) return r;
     UCHK(u, hipStreamSynchronize(st));

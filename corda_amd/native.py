@@ -107,11 +107,11 @@ class ChipFtxBatch(ctypes.Structure):
                 ("comp_start", ctypes.c_void_p), ("comp_data", ctypes.c_void_p), ("comp_off", ctypes.c_void_p),
                 ("comp_len", ctypes.c_void_p), ("nonces", ctypes.c_void_p), ("pt_start", ctypes.c_void_p),
                 ("pt_tag", ctypes.c_void_p), ("pt_hash", ctypes.c_void_p), ("check_visible", ctypes.c_void_p),
-                ("comp_bytes", ctypes.c_uint64)]
+                ("comp_bytes", ctypes.c_uint64), ("visible_mask", ctypes.c_void_p)]
 
 
 FTX_FIELDS = ("ids", "gh_start", "group_hashes", "fg_start", "fg_index", "comp_start", "comp_data", "comp_off",
-              "comp_len", "nonces", "pt_start", "pt_tag", "pt_hash", "check_visible")
+              "comp_len", "nonces", "pt_start", "pt_tag", "pt_hash", "check_visible", "visible_mask")
 
 
 def make_ftx_batch(f) -> ChipFtxBatch:

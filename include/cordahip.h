@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define CHIP_ABI_VERSION 7
+#define CHIP_ABI_VERSION 8
 
 enum chip_sig_status {
     CHIP_VALID = 0,
@@ -175,7 +175,10 @@ int chip_txid_batch_device(chip_ctx* ctx, const chip_tx_batch* batch, uint8_t* i
  * FilteredTransaction verification (the non-validating notary's check before commitInputStates,
  * NonValidatingNotaryFlow.kt:27-29): FilteredTransaction.verify() (MerkleTransaction.kt:175-191,
  * PartialMerkleTree.kt:133-160) followed, when check_visible[t] >= 0, by
- * checkAllComponentsVisible(ComponentGroupEnum ordinal check_visible[t]) (MerkleTransaction.kt:218-234).
+ * checkAllComponentsVisible(ComponentGroupEnum ordinal check_visible[t]) (MerkleTransaction.kt:218-234), then by
+ * checkAllComponentsVisible(g) for every bit g set in visible_mask[t], in ascending g (ABI 8): the
+ * non-validating notary's pair INPUTS_GROUP, TIMEWINDOW_GROUP (NonValidatingNotaryFlow.kt:27-29) is
+ * visible_mask = (1 << 0) | (1 << 5).  The first failing check decides status / reason.
  * Per filtered tx t: id (32 B), groupHashes rows gh_start[t] .. gh_start[t+1] (32 B each), filtered
  * component groups fg_start[t] .. fg_start[t+1]; per filtered group g: groupIndex fg_index[g], its
  * visible components comp_start[g] .. comp_start[g+1] (bytes in the comp pool, one 32-byte nonce each)
@@ -213,6 +216,7 @@ typedef struct {
     const uint8_t* pt_hash;         /* [nnodes * 32]         */
     const int32_t* check_visible;   /* [ntx] or NULL         */
     uint64_t comp_bytes;
+    const uint32_t* visible_mask;   /* [ntx] or NULL (ABI 8) */
 } chip_ftx_batch;
 
 int chip_ftx_verify_batch(chip_ctx* ctx, const chip_ftx_batch* batch, uint8_t* status, uint8_t* reason);

@@ -242,6 +242,129 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
         }
     }
 
+    /**
+     * verifySignaturesExcept for many deserialized transactions in ONE fused device call
+     * (CordaHip.verifySignedTxBatch -> chip_verify_signed_tx_batch): the ids are recomputed on the device from the
+     * component groups and privacy salt (WireTransaction.id, WireTransaction.kt:63,139-189), the SignableData
+     * messages are built there from one template per SignatureMetadata, then every signature and the required
+     * signers are checked (TransactionWithSignatures.kt:44-85).  Unlike verifySignaturesExcept above, the id the
+     * signatures are checked against is the recomputed one, not the deserialized field.  A transaction the
+     * device passes returns null; any other verdict is re-run on the JVM, which throws the reference's exception.
+     */
+    fun verifySignaturesExceptFused(txs: List<SignedTransaction>, allowedToBeMissing: Set<PublicKey> = emptySet()): List<Exception?> {
+        if (txs.isEmpty()) return emptyList()
+        if (txs.sumOf { it.sigs.size } < minBatch)
+            return txs.map { try { it.verifySignaturesExcept(*allowedToBeMissing.toTypedArray()); null } catch (e: Exception) { e } }
+        // templates: SignableData(id, meta) bytes without the id, one per metadata value in the batch
+        val metaIdx = HashMap<SignatureMetadata, Int>()
+        val tmpls = ArrayList<Pair<ByteArray, Int>>()
+        for (tx in txs) for (s in tx.sigs) metaIdx.getOrPut(s.signatureMetadata) {
+            val a = SignableData(SecureHash.zeroHash, s.signatureMetadata).serialize().bytes
+            val b = SignableData(SecureHash.allOnesHash, s.signatureMetadata).serialize().bytes
+            val at = a.indices.first { a[it] != b[it] }
+            tmpls.add(Pair(a.copyOfRange(0, at) + a.copyOfRange(at + 32, a.size), at)); tmpls.size - 1
+        }
+        val keyIds = HashMap<ByteBuffer, Int>()
+        val keys = ArrayList<ByteArray>()
+        fun keyIndex(k: PublicKey): Int { val e = k.encoded; return keyIds.getOrPut(ByteBuffer.wrap(e)) { keys.add(e); keys.size - 1 } }
+        val nSig = txs.sumOf { it.sigs.size }
+        val comps = txs.sumOf { t -> t.tx.componentGroups.sumOf { it.components.size } }
+        val compBytes = txs.sumOf { t -> t.tx.componentGroups.sumOf { g -> g.components.sumOf { it.size.toLong() } } }
+        val sigBytes = txs.sumOf { t -> t.sigs.sumOf { it.bytes.size.toLong() } }
+        // required key trees, flattened as verifySignaturesExcept does
+        val vals = ArrayList<Int>(); val nkids = ArrayList<Int>(); val weights = ArrayList<Int>()
+        val sigKeyIdx = txs.map { tx -> tx.sigs.map { keyIndex(it.by) } }
+        fun flatten(k: PublicKey, w: Int) {
+            if (k is CompositeKey) {
+                for (c in k.children) flatten(c.node, c.weight)
+                vals.add(k.threshold); nkids.add(k.children.size)
+            } else {
+                vals.add(keyIds[ByteBuffer.wrap(k.encoded)] ?: -1)   // -1 = CHIP_REQ_NO_SIGNER
+                nkids.add(0)
+            }
+            weights.add(w)
+        }
+        val reqStart = LongArray(txs.size + 1)
+        val nodeStart = ArrayList<Long>().apply { add(0L) }
+        val allowed = ArrayList<Byte>()
+        val invalid = arrayOfNulls<Exception>(txs.size)
+        for ((t, tx) in txs.withIndex()) {
+            try {
+                val req = tx.tx.requiredSigningKeys.toList()
+                req.forEach { if (it is CompositeKey) it.checkValidity() }
+                for (k in req) {
+                    flatten(k, 1)
+                    nodeStart.add(vals.size.toLong())
+                    allowed.add(if (k in allowedToBeMissing) 1 else 0)
+                }
+            } catch (e: IllegalArgumentException) {
+                invalid[t] = e
+            }
+            reqStart[t + 1] = allowed.size.toLong()
+        }
+        val keyBytes = keys.sumOf { it.size.toLong() }
+        val total = 32L * txs.size + 8L * (txs.size + 1) * 3 + 16L * comps + compBytes + 24L * tmpls.size +
+                tmpls.sumOf { it.first.size.toLong() } + 24L * nSig + sigBytes + 12L * keys.size + keyBytes +
+                8L * nodeStart.size + allowed.size + 12L * vals.size + 38L * txs.size + allowed.size + nSig + 32 * 64
+        require(total < Int.MAX_VALUE) { "batch too large for one call" }
+        val b = arena.reserve(total.toInt())
+        fun take(bytes: Long): ByteBuffer {
+            val s = b.slice().order(ByteOrder.LITTLE_ENDIAN)
+            s.limit(maxOf(bytes, 1L).toInt())
+            b.position(b.position() + ((bytes + 7) and 7L.inv()).toInt().coerceAtLeast(8))
+            return s
+        }
+        val n = txs.size
+        val bSalts = take(32L * n); val bTxCompStart = take(8L * (n + 1)); val bGroup = take(4L * comps)
+        val bInternal = take(4L * comps); val bData = take(compBytes); val bCompOff = take(8L * comps); val bCompLen = take(4L * comps)
+        var c = 0L; var o = 0L
+        bTxCompStart.putLong(0)
+        for (tx in txs) {
+            bSalts.put(tx.tx.privacySalt.bytes)
+            for (g in tx.tx.componentGroups) for ((i, comp) in g.components.withIndex()) {
+                bGroup.putInt(g.groupIndex); bInternal.putInt(i)
+                bCompOff.putLong(o); bCompLen.putInt(comp.size); bData.put(comp.bytes, comp.offset, comp.size)
+                o += comp.size; c++
+            }
+            bTxCompStart.putLong(c)
+        }
+        val bTd = take(tmpls.sumOf { it.first.size.toLong() }); val bTo = take(8L * tmpls.size)
+        val bTl = take(4L * tmpls.size); val bTa = take(4L * tmpls.size)
+        o = 0L
+        for ((bytes, at) in tmpls) { bTo.putLong(o); bTl.putInt(bytes.size); bTa.putInt(at); bTd.put(bytes); o += bytes.size }
+        val bTxIdx = take(4L * nSig); val bTmplIdx = take(4L * nSig); val bKeyIdx = take(4L * nSig)
+        val bSigData = take(sigBytes); val bSigOff = take(8L * nSig); val bSigLen = take(4L * nSig)
+        val bSigStart = take(8L * (n + 1))
+        o = 0L; var p = 0L
+        bSigStart.putLong(0)
+        for ((t, tx) in txs.withIndex()) {
+            for ((j, s) in tx.sigs.withIndex()) {
+                bTxIdx.putInt(t); bTmplIdx.putInt(metaIdx[s.signatureMetadata]!!); bKeyIdx.putInt(sigKeyIdx[t][j])
+                bSigOff.putLong(o); bSigLen.putInt(s.bytes.size); bSigData.put(s.bytes); o += s.bytes.size; p++
+            }
+            bSigStart.putLong(p)
+        }
+        val bKeyOff = take(8L * keys.size); val bKeyLen = take(4L * keys.size); val bKeys = take(keyBytes)
+        o = 0L
+        for (k in keys) { bKeyOff.putLong(o); bKeyLen.putInt(k.size); bKeys.put(k); o += k.size }
+        val bReqStart = take(8L * (n + 1)).apply { reqStart.forEach { putLong(it) } }
+        val bNodeStart = take(8L * nodeStart.size).apply { nodeStart.forEach { putLong(it) } }
+        val bAllowed = take(allowed.size.toLong()).apply { allowed.forEach { put(it) } }
+        val bVal = take(4L * vals.size).apply { vals.forEach { putInt(it) } }
+        val bNk = take(4L * nkids.size).apply { nkids.forEach { putInt(it) } }
+        val bW = take(4L * weights.size).apply { weights.forEach { putInt(it) } }
+        val bStatus = take(nSig.toLong()); val bVerdict = take(n.toLong()); val bArg = take(4L * n)
+        val rc = CordaHip.verifySignedTxBatch(ctx, n, bSalts, bTxCompStart, comps, bGroup, bInternal, bData, bCompOff,
+                bCompLen, tmpls.size, bTd, bTo, bTl, bTa, nSig, bTxIdx, bTmplIdx, bKeyIdx, bSigData, bSigOff, bSigLen,
+                keys.size, bKeys, bKeyOff, bKeyLen, bSigStart, bReqStart, allowed.size, bNodeStart, bAllowed,
+                vals.size, bVal, bNk, bW, null, bStatus, bVerdict, bArg, null)
+        check(rc == 0) { "libcordahip verifySignedTxBatch failed ($rc): ${CordaHip.lastError(ctx)}" }
+        return txs.mapIndexed { t, tx ->
+            if (invalid[t] == null && bVerdict.get(t).toInt() == 0) null
+            else try { tx.verifySignaturesExcept(*allowedToBeMissing.toTypedArray()); null } catch (e: Exception) { e }
+        }
+    }
+
     /** Crypto.isValid(PublicKey, ByteArray, ByteArray) on the device; decode errors still throw. */
     /**
      * verifySignaturesExcept for transactions still in their serialized form (vault rows, P2P payloads,

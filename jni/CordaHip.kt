@@ -59,6 +59,48 @@ object CordaHip {
                                       tmplIdAt: ByteBuffer, meta: ByteBuffer, status: ByteBuffer, verdict: ByteBuffer,
                                       arg: ByteBuffer, ids: ByteBuffer?): Int
 
+    /**
+     * chip_verify_signed_tx_batch: SignedTransaction.verifySignaturesExcept for ntx transactions in one fused call
+     * (ids, SignableData messages built on the device from templates, signatures, required signers).
+     * Per signature: tx / template / key-pool index; per transaction: its signature range (sigStart) and its
+     * required key trees (reqStart, nodeStart, node*: as requiredSigners).  ids (32 B per tx) and missing may be null.
+     */
+    @JvmStatic external fun verifySignedTxBatch(ctx: Long, ntx: Int, salts: ByteBuffer, txCompStart: ByteBuffer, nComp: Int,
+                                                compGroup: ByteBuffer, compInternal: ByteBuffer, data: ByteBuffer,
+                                                compOff: ByteBuffer, compLen: ByteBuffer, nTmpl: Int, tmplData: ByteBuffer,
+                                                tmplOff: ByteBuffer, tmplLen: ByteBuffer, tmplIdAt: ByteBuffer, nSig: Int,
+                                                txIdx: ByteBuffer, tmplIdx: ByteBuffer, keyIdx: ByteBuffer, sigData: ByteBuffer,
+                                                sigOff: ByteBuffer, sigLen: ByteBuffer, nKeys: Int, keyData: ByteBuffer,
+                                                keyOff: ByteBuffer, keyLen: ByteBuffer, sigStart: ByteBuffer,
+                                                reqStart: ByteBuffer, nreq: Int, nodeStart: ByteBuffer, allowed: ByteBuffer?,
+                                                nNodes: Int, nodeVal: ByteBuffer, nodeNkids: ByteBuffer,
+                                                nodeWeight: ByteBuffer, ids: ByteBuffer?, status: ByteBuffer,
+                                                verdict: ByteBuffer, arg: ByteBuffer, missing: ByteBuffer?): Int
+
+    /**
+     * chip_ftx_verify_batch: FilteredTransaction.verify + checkAllComponentsVisible for ntx filtered transactions
+     * (chip_ftx_batch layout: group hashes, filtered groups, visible components with their nonces, each group's
+     * PartialMerkleTree in post-order).  visibleMask bit g = checkAllComponentsVisible(ordinal g), ascending.
+     * status: 0 OK, 1 FilteredTransactionVerificationException, 2 ComponentVisibilityException; reason: FTX_*.
+     */
+    @JvmStatic external fun ftxVerify(ctx: Long, ntx: Int, ids: ByteBuffer, ghStart: ByteBuffer, groupHashes: ByteBuffer,
+                                      fgStart: ByteBuffer, fgIndex: ByteBuffer, compStart: ByteBuffer, compData: ByteBuffer,
+                                      compOff: ByteBuffer, compLen: ByteBuffer, nonces: ByteBuffer, ptStart: ByteBuffer,
+                                      ptTag: ByteBuffer, ptHash: ByteBuffer, checkVisible: ByteBuffer?,
+                                      visibleMask: ByteBuffer?, status: ByteBuffer, reason: ByteBuffer?): Int
+
+    /** chip_ftx_reason (include/cordahip.h) */
+    const val FTX_OK = 0
+    const val FTX_NO_GROUP_HASHES = 1
+    const val FTX_TOP_ROOT = 2
+    const val FTX_GROUP_INDEX = 3
+    const val FTX_PARTIAL_ROOT = 4
+    const val FTX_VISIBLE_LEAVES = 5
+    const val FTX_VIS_ABSENT_GROUP = 6
+    const val FTX_VIS_GROUP_INDEX = 7
+    const val FTX_VIS_FULL_ROOT = 8
+    const val FTX_MALFORMED = 9
+
     @JvmStatic external fun uniqOpen(ctx: Long, capacity: Long): Long
     @JvmStatic external fun uniqClose(uniq: Long)
     @JvmStatic external fun uniqSize(uniq: Long): Long

@@ -12,6 +12,13 @@
  *   verifyBatch      TransactionWithSignatures.checkSignaturesAreValid (TransactionWithSignatures.kt:62-66)
  *                    -> Crypto.doVerify / Crypto.isValid (Crypto.kt:502-536, 615-625)
  *   txIds            WireTransaction.id / merkleTree (WireTransaction.kt:63,139-189)
+ *   verifySignedTxBatch  SignedTransaction.verifySignaturesExcept for a batch, fused: ids, SignableData
+ *                    messages, signatures, required signers (SignedTransaction.kt:46,228,
+ *                    TransactionWithSignatures.kt:44-85) -> chip_verify_signed_tx_batch
+ *   ftxVerify        FilteredTransaction.verify + checkAllComponentsVisible, the non-validating notary's
+ *                    check (NonValidatingNotaryFlow.kt:26-31, MerkleTransaction.kt:175-234)
+ *                    -> chip_ftx_verify_batch
+ *   stxVerify        the same from SerializedBytes<SignedTransaction> (ResolveTransactionsFlow.kt:91-98)
  *   uniq*            UniquenessProvider.commit (UniquenessProvider.kt:15-17),
  *                    PersistentUniquenessProvider.commit (PersistentUniquenessProvider.kt:92-113) */
 #include <jni.h>
@@ -151,6 +158,126 @@ JNIEXPORT jint JNICALL CLS(txIds)(JNIEnv* env, jclass cls, jlong ctx, jint ntx, 
     uint8_t* out = (uint8_t*)addr(env, ids);
     if (ntx < 0 || (ntx > 0 && (!out || cap_of(env, ids) < 32ull * (uint64_t)ntx))) return CHIP_E_ARG;
     return chip_txid_batch((chip_ctx*)(intptr_t)ctx, &b, out);
+}
+
+/* ---- the fused SignedTransaction.verifySignaturesExcept of a batch (chip_verify_signed_tx_batch) ----
+ * transactions as txIds; signatures: tx / template / key index per signature, signature pool; templates: the
+ * SignableData bytes of each SignatureMetadata without the id, and where the id goes; required keys as
+ * requiredSigners.  ids (ntx * 32, may be null), status (nSig), verdict (ntx), arg (4 * ntx), missing (nreq,
+ * may be null) out. */
+JNIEXPORT jint JNICALL CLS(verifySignedTxBatch)(JNIEnv* env, jclass cls, jlong ctx, jint ntx, jobject salts,
+                                                jobject txCompStart, jint nComp, jobject compGroup, jobject compInternal,
+                                                jobject data, jobject compOff, jobject compLen, jint nTmpl,
+                                                jobject tmplData, jobject tmplOff, jobject tmplLen, jobject tmplIdAt,
+                                                jint nSig, jobject txIdx, jobject tmplIdx, jobject keyIdx,
+                                                jobject sigData, jobject sigOff, jobject sigLen, jint nKeys,
+                                                jobject keyData, jobject keyOff, jobject keyLen, jobject sigStart,
+                                                jobject reqStart, jint nreq, jobject nodeStart, jobject allowed,
+                                                jint nNodes, jobject nodeVal, jobject nodeNkids, jobject nodeWeight,
+                                                jobject ids, jobject status, jobject verdict, jobject arg,
+                                                jobject missing) {
+    (void)cls;
+    if (ntx < 0 || nComp < 0 || nTmpl < 0 || nSig < 0 || nKeys < 0 || nreq < 0 || nNodes < 0) return CHIP_E_ARG;
+    chip_tx_batch t;
+    memset(&t, 0, sizeof t);
+    t.ntx = (uint64_t)ntx;
+    t.salts = (const uint8_t*)addr(env, salts);
+    t.tx_comp_start = (const uint64_t*)addr(env, txCompStart);
+    t.ncomp = (uint64_t)nComp;
+    t.comp_group = (const uint32_t*)addr(env, compGroup);
+    t.comp_internal = (const uint32_t*)addr(env, compInternal);
+    t.data = (const uint8_t*)addr(env, data);
+    t.comp_off = (const uint64_t*)addr(env, compOff);
+    t.comp_len = (const uint32_t*)addr(env, compLen);
+    t.data_bytes = cap_of(env, data);
+    chip_msg_templates m;
+    memset(&m, 0, sizeof m);
+    m.n = (uint64_t)nTmpl;
+    m.data = (const uint8_t*)addr(env, tmplData);
+    m.off = (const uint64_t*)addr(env, tmplOff);
+    m.len = (const uint32_t*)addr(env, tmplLen);
+    m.id_at = (const uint32_t*)addr(env, tmplIdAt);
+    m.data_bytes = cap_of(env, tmplData);
+    if (nTmpl > 0 && (!m.len || cap_of(env, tmplLen) < 4ull * (uint64_t)nTmpl)) return CHIP_E_ARG;
+    for (jint i = 0; i < nTmpl; i++)
+        if (m.len[i] > m.max_len) m.max_len = m.len[i];
+    chip_signer_batch s;
+    memset(&s, 0, sizeof s);
+    s.n = (uint64_t)nSig;
+    s.tx_idx = (const uint32_t*)addr(env, txIdx);
+    s.tmpl_idx = (const uint32_t*)addr(env, tmplIdx);
+    s.key_idx = (const uint32_t*)addr(env, keyIdx);
+    s.sig_data = (const uint8_t*)addr(env, sigData);
+    s.sig_off = (const uint64_t*)addr(env, sigOff);
+    s.sig_len = (const uint32_t*)addr(env, sigLen);
+    s.n_keys = (uint64_t)nKeys;
+    s.key_data = (const uint8_t*)addr(env, keyData);
+    s.key_off = (const uint64_t*)addr(env, keyOff);
+    s.key_len = (const uint32_t*)addr(env, keyLen);
+    s.sig_bytes = cap_of(env, sigData);
+    s.key_bytes = cap_of(env, keyData);
+    chip_req_batch q;
+    memset(&q, 0, sizeof q);
+    q.ntx = (uint64_t)ntx;
+    q.sig_start = (const uint64_t*)addr(env, sigStart);
+    q.req_start = (const uint64_t*)addr(env, reqStart);
+    q.nreq = (uint64_t)nreq;
+    q.node_start = (const uint64_t*)addr(env, nodeStart);
+    q.allowed = (const uint8_t*)addr(env, allowed);
+    q.n_nodes = (uint64_t)nNodes;
+    q.node_val = (const uint32_t*)addr(env, nodeVal);
+    q.node_nkids = (const uint32_t*)addr(env, nodeNkids);
+    q.node_weight = (const uint32_t*)addr(env, nodeWeight);
+    uint8_t* idOut = (uint8_t*)addr(env, ids);
+    uint8_t* st = (uint8_t*)addr(env, status);
+    uint8_t* v = (uint8_t*)addr(env, verdict);
+    uint32_t* a = (uint32_t*)addr(env, arg);
+    uint8_t* miss = (uint8_t*)addr(env, missing);
+    if ((idOut && cap_of(env, ids) < 32ull * (uint64_t)ntx) || (nSig > 0 && (!st || cap_of(env, status) < (uint64_t)nSig)) ||
+        (ntx > 0 && (!v || !a || cap_of(env, verdict) < (uint64_t)ntx || cap_of(env, arg) < 4ull * (uint64_t)ntx)) ||
+        (miss && cap_of(env, missing) < (uint64_t)nreq))
+        return CHIP_E_ARG;
+    return chip_verify_signed_tx_batch((chip_ctx*)(intptr_t)ctx, &t, &m, &s, &q, idOut, st, v, a, miss);
+}
+
+/* ---- FilteredTransaction.verify + checkAllComponentsVisible (chip_ftx_verify_batch) ----
+ * chip_ftx_batch arrays; checkVisible (ntx i32, may be null) and visibleMask (ntx u32, may be null: the notary
+ * flow passes INPUTS_GROUP | TIMEWINDOW_GROUP bits) select the visibility checks.  status (ntx: 0 OK,
+ * 1 FilteredTransactionVerificationException, 2 ComponentVisibilityException) and reason (ntx CHIP_FTX_*,
+ * may be null) out. */
+JNIEXPORT jint JNICALL CLS(ftxVerify)(JNIEnv* env, jclass cls, jlong ctx, jint ntx, jobject ids, jobject ghStart,
+                                      jobject groupHashes, jobject fgStart, jobject fgIndex, jobject compStart,
+                                      jobject compData, jobject compOff, jobject compLen, jobject nonces,
+                                      jobject ptStart, jobject ptTag, jobject ptHash, jobject checkVisible,
+                                      jobject visibleMask, jobject status, jobject reason) {
+    (void)cls;
+    if (ntx < 0) return CHIP_E_ARG;
+    chip_ftx_batch b;
+    memset(&b, 0, sizeof b);
+    b.ntx = (uint64_t)ntx;
+    b.ids = (const uint8_t*)addr(env, ids);
+    b.gh_start = (const uint64_t*)addr(env, ghStart);
+    b.group_hashes = (const uint8_t*)addr(env, groupHashes);
+    b.fg_start = (const uint64_t*)addr(env, fgStart);
+    b.fg_index = (const uint32_t*)addr(env, fgIndex);
+    b.comp_start = (const uint64_t*)addr(env, compStart);
+    b.comp_data = (const uint8_t*)addr(env, compData);
+    b.comp_off = (const uint64_t*)addr(env, compOff);
+    b.comp_len = (const uint32_t*)addr(env, compLen);
+    b.nonces = (const uint8_t*)addr(env, nonces);
+    b.pt_start = (const uint64_t*)addr(env, ptStart);
+    b.pt_tag = (const uint8_t*)addr(env, ptTag);
+    b.pt_hash = (const uint8_t*)addr(env, ptHash);
+    b.check_visible = (const int32_t*)addr(env, checkVisible);
+    b.visible_mask = (const uint32_t*)addr(env, visibleMask);
+    b.comp_bytes = cap_of(env, compData);
+    uint8_t* st = (uint8_t*)addr(env, status);
+    uint8_t* rs = (uint8_t*)addr(env, reason);
+    if ((ntx > 0 && (!st || cap_of(env, status) < (uint64_t)ntx)) || (rs && cap_of(env, reason) < (uint64_t)ntx) ||
+        (b.check_visible && cap_of(env, checkVisible) < 4ull * (uint64_t)ntx) ||
+        (b.visible_mask && cap_of(env, visibleMask) < 4ull * (uint64_t)ntx))
+        return CHIP_E_ARG;
+    return chip_ftx_verify_batch((chip_ctx*)(intptr_t)ctx, &b, st, rs);
 }
 
 /* ---- the whole path from bytes: SignedTransaction blobs -> tx status + verdict (chip_stx_verify) ---- */

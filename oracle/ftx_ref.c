@@ -63,12 +63,16 @@ static int rebuild(const uint8_t* tags, const uint8_t* hashes, uint64_t n, pnode
     return root;
 }
 
+static int visible_check(uint64_t ngh, const uint8_t* gh, uint64_t nfg, const uint32_t* fg_index,
+                         const uint64_t* comp_start, const uint8_t* comp_data, const uint64_t* comp_off,
+                         const uint32_t* comp_len, const uint8_t* nonces, uint32_t check_visible, int* reason);
+
 /* Returns status 0 OK, 1 FilteredTransactionVerificationException, 2 ComponentVisibilityException;
  * *reason as documented in include/cordahip.h (CHIP_FTX_*). */
 int orc_ftx_verify(const uint8_t id[32], uint64_t ngh, const uint8_t* gh, uint64_t nfg, const uint32_t* fg_index,
                    const uint64_t* comp_start, const uint8_t* comp_data, const uint64_t* comp_off,
                    const uint32_t* comp_len, const uint8_t* nonces, const uint64_t* pt_start, const uint8_t* pt_tag,
-                   const uint8_t* pt_hash, int32_t check_visible, int* reason) {
+                   const uint8_t* pt_hash, int32_t check_visible, uint32_t visible_mask, int* reason) {
     *reason = 0;
     if (ngh == 0) { *reason = 1; return 1; }
     uint8_t root[32];
@@ -100,7 +104,26 @@ int orc_ftx_verify(const uint8_t id[32], uint64_t ngh, const uint8_t* gh, uint64
         free(want);
         if (!ok) { *reason = 5; return 1; }
     }
-    if (check_visible < 0) return 0;
+    /* checkAllComponentsVisible(check_visible), then one call per bit of visible_mask in ascending ordinal
+     * (NonValidatingNotaryFlow.kt:27-29 calls it for INPUTS_GROUP, then TIMEWINDOW_GROUP) */
+    if (check_visible >= 0) {
+        const int s = visible_check(ngh, gh, nfg, fg_index, comp_start, comp_data, comp_off, comp_len, nonces,
+                                    (uint32_t)check_visible, reason);
+        if (s) return s;
+    }
+    for (uint32_t g = 0; g < 32; g++)
+        if ((visible_mask >> g) & 1u) {
+            const int s = visible_check(ngh, gh, nfg, fg_index, comp_start, comp_data, comp_off, comp_len, nonces, g,
+                                        reason);
+            if (s) return s;
+        }
+    return 0;
+}
+
+/* FilteredTransaction.checkAllComponentsVisible(ordinal) (MerkleTransaction.kt:218-234) */
+static int visible_check(uint64_t ngh, const uint8_t* gh, uint64_t nfg, const uint32_t* fg_index,
+                         const uint64_t* comp_start, const uint8_t* comp_data, const uint64_t* comp_off,
+                         const uint32_t* comp_len, const uint8_t* nonces, uint32_t check_visible, int* reason) {
     int64_t found = -1;
     for (uint64_t g = 0; g < nfg; g++)
         if (fg_index[g] == (uint32_t)check_visible) { found = (int64_t)g; break; }
@@ -127,14 +150,16 @@ void orc_ftx_verify_batch(uint64_t ntx, const uint8_t* ids, const uint64_t* gh_s
                           const uint64_t* fg_start, const uint32_t* fg_index, const uint64_t* comp_start,
                           const uint8_t* comp_data, const uint64_t* comp_off, const uint32_t* comp_len,
                           const uint8_t* nonces, const uint64_t* pt_start, const uint8_t* pt_tag,
-                          const uint8_t* pt_hash, const int32_t* check_visible, uint8_t* status, uint8_t* reason) {
+                          const uint8_t* pt_hash, const int32_t* check_visible, const uint32_t* visible_mask,
+                          uint8_t* status, uint8_t* reason) {
     for (uint64_t t = 0; t < ntx; t++) {
         int r = 0;
         const uint64_t g0 = fg_start[t];
         status[t] = (uint8_t)orc_ftx_verify(ids + 32 * t, gh_start[t + 1] - gh_start[t], gh + 32 * gh_start[t],
                                             fg_start[t + 1] - g0, fg_index + g0, comp_start + g0, comp_data, comp_off,
                                             comp_len, nonces, pt_start + g0, pt_tag, pt_hash,
-                                            check_visible ? check_visible[t] : -1, &r);
+                                            check_visible ? check_visible[t] : -1, visible_mask ? visible_mask[t] : 0u,
+                                            &r);
         if (reason) reason[t] = (uint8_t)r;
     }
 }

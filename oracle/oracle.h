@@ -132,12 +132,13 @@ void orc_uniq_commit_batch(orc_uniq*, uint64_t ntx, const uint64_t* tx_ref_start
 int orc_ftx_verify(const uint8_t id[32], uint64_t ngh, const uint8_t* gh, uint64_t nfg, const uint32_t* fg_index,
                    const uint64_t* comp_start, const uint8_t* comp_data, const uint64_t* comp_off,
                    const uint32_t* comp_len, const uint8_t* nonces, const uint64_t* pt_start, const uint8_t* pt_tag,
-                   const uint8_t* pt_hash, int32_t check_visible, int* reason);
+                   const uint8_t* pt_hash, int32_t check_visible, uint32_t visible_mask, int* reason);
 void orc_ftx_verify_batch(uint64_t ntx, const uint8_t* ids, const uint64_t* gh_start, const uint8_t* gh,
                           const uint64_t* fg_start, const uint32_t* fg_index, const uint64_t* comp_start,
                           const uint8_t* comp_data, const uint64_t* comp_off, const uint32_t* comp_len,
                           const uint8_t* nonces, const uint64_t* pt_start, const uint8_t* pt_tag,
-                          const uint8_t* pt_hash, const int32_t* check_visible, uint8_t* status, uint8_t* reason);
+                          const uint8_t* pt_hash, const int32_t* check_visible, const uint32_t* visible_mask,
+                          uint8_t* status, uint8_t* reason);
 
 /* ---- required signers: TransactionWithSignatures.verifySignaturesExcept after the statuses
  *      (:44-50,62-66,79-85), CompositeKey.checkFulfilledBy (CompositeKey.kt:175-185);

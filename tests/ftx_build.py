@@ -102,11 +102,12 @@ def post_order(pt, out=None):
 class Ftx:
     """One FilteredTransaction: id, groupHashes, filtered groups [(index, comps, nonces, post-order)]."""
 
-    def __init__(self, id, group_hashes, groups, check_visible=-1):
+    def __init__(self, id, group_hashes, groups, check_visible=-1, visible_mask=0):
         self.id = id
         self.group_hashes = group_hashes
         self.groups = groups
         self.check_visible = check_visible
+        self.visible_mask = visible_mask
 
 
 def build_filtered(salt, component_groups, predicate, check_visible=-1):
@@ -166,12 +167,18 @@ class FtxBatch:
         self.pt_tag = np.array(tags or [0], dtype=np.uint8)
         self.pt_hash = np.frombuffer(b"".join(phash) or ZERO, dtype=np.uint8).copy()
         self.check_visible = np.array([f.check_visible for f in ftxs], dtype=np.int32)
+        self.visible_mask = np.array([f.visible_mask for f in ftxs], dtype=np.uint32)
 
 
-def notary_workload(n, seed=0x5EED0006, corrupt=0.2):
+NOTARY_FLOW_MASK = (1 << 0) | (1 << 5)   # NonValidatingNotaryFlow.kt:27-29: INPUTS_GROUP, then TIMEWINDOW_GROUP
+
+
+def notary_workload(n, seed=0x5EED0006, corrupt=0.2, flow=False):
     """Non-validating-notary shaped FilteredTransactions (inputs, notary, time-window visible;
     outputs / commands / attachments hidden) plus corrupted variants, with the expected
-    (status, reason) from the Kotlin semantics.  Returns ([Ftx], [(status, reason)])."""
+    (status, reason) from the Kotlin semantics.  flow=False: checkAllComponentsVisible(INPUTS_GROUP) through
+    check_visible; flow=True: the notary flow's two checks (INPUTS_GROUP, then TIMEWINDOW_GROUP) through
+    visible_mask, with the time-window component hidden in some transactions.  Returns ([Ftx], [(status, reason)])."""
     rng = np.random.Generator(np.random.PCG64(seed))
     ftxs, want = [], []
     for t in range(n):
@@ -185,15 +192,22 @@ def notary_workload(n, seed=0x5EED0006, corrupt=0.2):
             groups.append((3, [rng.bytes(32) for _ in range(int(rng.integers(1, 3)))]))
         if rng.random() < 0.05:
             groups.append((int(rng.integers(6, 30)), [rng.bytes(10)]))    # unknown group ordinal
-        vis = lambda g, i, c: g in (0, 4, 5)                                   # noqa: E731
+        hide_tw = flow and rng.random() < 0.15
+        vis = lambda g, i, c: g in (0, 4) or (g == 5 and not hide_tw)          # noqa: E731
         if rng.random() < 0.1:
-            vis = lambda g, i, c, s=int(rng.integers(0, 1 << 30)): g in (4, 5) or (g == 0 and (i + s) % 2 == 0)  # noqa: E731
-        f = build_filtered(salt, groups, vis, check_visible=0)
+            vis = lambda g, i, c, s=int(rng.integers(0, 1 << 30)): g == 4 or (g == 5 and not hide_tw) or (g == 0 and (i + s) % 2 == 0)  # noqa: E731
+        if flow:
+            f = build_filtered(salt, groups, vis)
+            f.visible_mask = NOTARY_FLOW_MASK
+        else:
+            f = build_filtered(salt, groups, vis, check_visible=0)
         exp = (0, 0)
         n_inputs = len(dict(groups)[0])
         visible_inputs = len(f.groups[0][1]) if f.groups and f.groups[0][0] == 0 else 0
         if visible_inputs != n_inputs:
             exp = (2, 8) if visible_inputs else (2, 6)
+        elif flow and hide_tw and 5 in dict(groups):
+            exp = (2, 6)   # "Did not receive components for group 5 ..." (its group hash is not allOnesHash)
         u = rng.random()
         if u < corrupt:
             kind = int(rng.integers(0, 6))

@@ -188,7 +188,7 @@ def ftx_verify_batch(f):
     lib().orc_ftx_verify_batch(ctypes.c_uint64(f.ntx), _p(f.ids), _p(f.gh_start), _p(f.group_hashes), _p(f.fg_start),
                                _p(f.fg_index), _p(f.comp_start), _p(f.comp_data), _p(f.comp_off), _p(f.comp_len),
                                _p(f.nonces), _p(f.pt_start), _p(f.pt_tag), _p(f.pt_hash), _p(f.check_visible),
-                               _p(st), _p(rs))
+                               _p(getattr(f, "visible_mask", None)), _p(st), _p(rs))
     return st, rs
 
 

@@ -22,6 +22,27 @@ def test_notary_workload_labels():
     assert {r for _, r in got} >= {0, 1, 2, 3, 4, 5, 6, 8, 9}
 
 
+def test_notary_flow_two_visibility_checks():
+    """NonValidatingNotaryFlow.kt:26-31: verify(), then checkAllComponentsVisible(INPUTS_GROUP), then
+    (TIMEWINDOW_GROUP), as visible_mask bits 0 and 5: a hidden time-window component is (2, 6) when the
+    inputs are all visible, and the inputs' failure wins when both fail."""
+    ftxs, want = notary_workload(1500, seed=0x5EED0016, flow=True)
+    got = run(ftxs)
+    assert got == want
+    tw_only = [i for i, f in enumerate(ftxs) if want[i] == (2, 6) and f.groups and f.groups[0][0] == 0
+               and 5 not in [g for g, *_ in f.groups]]
+    assert len(tw_only) > 20
+    # the same filtered transactions through check_visible = INPUTS_GROUP alone pass those
+    for i in tw_only[:5]:
+        f = ftxs[i]
+        f.visible_mask, f.check_visible = 0, 0
+        assert run([f]) == [(0, 0)]
+    # ascending-ordinal order: a mask bit below check_visible still runs after it
+    f = _one_group_ftx(COMPS, [0, 1], check=-1)
+    f.visible_mask = (1 << 1) | (1 << 7)
+    assert run([f]) == [(2, 8)]
+
+
 def _one_group_ftx(comps, include_idx, visible_comps=None, check=-1):
     salt = bytes(range(1, 33))
     nonces = [compute_nonce(salt, 1, i) for i in range(len(comps))]

@@ -19,6 +19,18 @@ def test_ftx_notary_workload_matches_oracle(ctx):
     assert list(zip(st.tolist(), rs.tolist())) == want
 
 
+def test_ftx_notary_flow_mask_matches_oracle(ctx):
+    """The notary flow's two checks (visible_mask = INPUTS_GROUP | TIMEWINDOW_GROUP): device == oracle ==
+    the Kotlin-semantics labels, including hidden time-window components."""
+    ftxs, want = notary_workload(5000, seed=0x5EED0017, flow=True)
+    b = FtxBatch(ftxs)
+    st, rs = ctx.ftx_verify_batch(b)
+    ost, ors = O.ftx_verify_batch(b)
+    assert np.array_equal(st, ost) and np.array_equal(rs, ors)
+    assert list(zip(st.tolist(), rs.tolist())) == want
+    assert sum(1 for w in want if w == (2, 6)) > 100
+
+
 def test_ftx_scenarios(ctx):
     fs = [_one_group_ftx(COMPS, inc, vis, chk) for inc, vis, chk in
           [([3, 5], None, -1), ([], None, -1), ([0, 1, 2, 3, 4, 5], None, 1), ([3, 5], [3, 5, 0], -1),

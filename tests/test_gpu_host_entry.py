@@ -101,6 +101,26 @@ def test_host_chunk_pipeline_rejects_bad_index_in_a_later_chunk(ctx, monkeypatch
     assert np.array_equal(st, b.expected)
 
 
+@pytest.mark.parametrize("field", ["key_off", "key_len"])
+def test_host_chunk_pipeline_rejects_key_outside_pool_before_key_prep(ctx, monkeypatch, field):
+    """In the chunked host entry the key prep and the table chains start on the keys alone: a key range
+    outside the key pool is CHIP_E_ARG before any kernel reads through it (no device fault), and the next
+    call is unaffected."""
+    b = G.ed25519_batch(20000, n_keys=16, corrupt=0.1, seed=0x5EED0504)
+    x = copy.copy(b)
+    arr = getattr(b, field).copy()
+    if field == "key_off":
+        arr[5] = len(b.key_data) + (1 << 30)
+    else:
+        arr[5] = 1 << 31
+    setattr(x, field, arr)
+    with pytest.raises(native.ChipError) as e:
+        _chunked(ctx, x, 4, monkeypatch)
+    assert "key pool" in str(e.value)
+    st, _ = _chunked(ctx, b, 4, monkeypatch)
+    assert np.array_equal(st, b.expected)
+
+
 def test_other_host_entries_check_arguments_on_the_device(ctx):
     """The tx-id, fused, FilteredTransaction, chip_stx_verify and uniqueness host entries check their
     arrays on the device after staging (no host walk): each bad argument is CHIP_E_ARG with its message,

@@ -145,6 +145,47 @@ def test_uniq_sharded_gpu_shards_match_oracle(ctx, oracle, world):
         t.close()
 
 
+def test_uniq_rebuild_with_duplicate_rows_after_a_commit(ctx, oracle):
+    """A rebuild whose rows repeat StateRefs, run after a commit left its per-ref scratch behind: the
+    first row of each key is kept (AppendOnlyPersistentMap, first value wins), whichever lane won the
+    claim; size() and the conflict records of a batch that re-spends those states equal the oracle."""
+    pre, b = G.uniq_workload(8000, 6000, seed=31, pre_hit=0.02, dbl=0.03, resubmit=0.01)
+    refs, tx, idx, caller = pre
+    n = len(idx)
+    r36, t32 = refs.reshape(-1, 36), tx.reshape(-1, 32)
+    rng = np.random.Generator(np.random.PCG64(32))
+    head = np.arange(0, 1500)           # repeated BEFORE their originals: the repeat wins
+    tail = np.arange(1500, 3000)        # repeated AFTER their originals: the original wins
+    alt_tx = rng.integers(0, 256, size=(n, 32), dtype=np.uint8)
+    alt_idx = rng.integers(0, 50, size=n).astype(np.uint32)
+    alt_call = rng.integers(0, 7, size=n).astype(np.uint32)
+    rows_r = np.concatenate([r36[head], r36, r36[tail], r36[tail]])
+    rows_t = np.concatenate([alt_tx[head], t32, alt_tx[tail], t32[tail]])
+    rows_i = np.concatenate([alt_idx[head], idx, alt_idx[tail], idx[tail]])
+    rows_c = np.concatenate([alt_call[head], caller, alt_call[tail], caller[tail]])
+    dup_pre = (np.ascontiguousarray(rows_r).reshape(-1), np.ascontiguousarray(rows_t).reshape(-1),
+               np.ascontiguousarray(rows_i), np.ascontiguousarray(rows_c))
+    t = ctx.uniq_open(1 << 16)
+    o = oracle.Uniq(1 << 16)
+    # a first commit leaves own / sid / tslot scratch over more refs than the rebuild has
+    _, warm = G.uniq_workload(20000, 0, seed=33, pre_hit=0.0, dbl=0.05)
+    g0 = t.commit_batch(warm.tx_ref_start, warm.refs, warm.tx_ids, warm.callers)
+    r0 = o.commit_batch(warm.tx_ref_start, warm.refs, warm.tx_ids, warm.callers)
+    assert np.array_equal(g0[0], r0[0])
+    t.rebuild(*dup_pre)
+    o.preload(*dup_pre)
+    assert t.size() == o.size()
+    # re-spend every rebuilt state: each conflict record names the kept row's tx / index / caller
+    _, again = G.uniq_workload(3000, 0, seed=34, pre_hit=0.0, dbl=0.0)
+    again.refs[:36 * 3000] = np.ascontiguousarray(r36[:3000]).reshape(-1)
+    g = t.commit_batch(again.tx_ref_start, again.refs, again.tx_ids, again.callers)
+    r = o.commit_batch(again.tx_ref_start, again.refs, again.tx_ids, again.callers)
+    assert np.array_equal(g[0], r[0])
+    assert g[1] == r[1] and len(r[1]) >= 3000
+    assert t.size() == o.size()
+    t.close()
+
+
 def test_commit_log_restart_on_gpu(ctx, tmp_path):
     """The notary commit log rebuilt into the GPU table at open answers like a provider that never
     restarted (tests/commit_log_case.py)."""
