@@ -519,6 +519,8 @@ def main():
             bbs.append(x)
         bb = bbs[0]
         bo, bl = torch.from_numpy(boff).to(dev), torch.from_numpy(blen).to(dev)
+        # the host-buffer leg's blobs: page-locked, what the JNI binding hands chip_stx_verify
+        hb = ctx.pinned_copy(bdata) if not args.no_host_path else None
         del bdata
         dm = upload(tm, ("data", "off", "len", "id_at"), torch, dev)
         dm.max_len = tm.max_len
@@ -571,6 +573,39 @@ def main():
         bel = timed_steps(from_bytes_pipelined, ts, world, torch, dev, dist)
         p = holder["p"]
         blob_bytes = nbytes
+        host_bytes = {}
+        if hb is not None:
+            # host-buffer entry (PCIe-inclusive): the blobs in page-locked host memory through chip_stx_verify,
+            # which copies transaction chunks beside the previous chunk's parse and verification
+            hres = {}
+
+            def from_bytes_host():
+                hres["r"] = ctx.stx_verify(hb, boff, blen, tm, meta)
+            from_bytes_host()
+            hst_, hv, ha, _ = hres["r"]
+            host_ok = bool(not hst_.any() and np.array_equal(hv, want_v) and np.array_equal(ha, want_a))
+            hsteps = max(2, ts // 2)
+            hel = timed_steps(from_bytes_host, hsteps, world, torch, dev, dist)
+            # the PCIe bound of this leg: the same bytes copied alone (pinned -> device, one copy)
+            hdst = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+            hsrc = torch.from_numpy(hb)
+            torch.cuda.synchronize(dev)
+            t_h = time.perf_counter()
+            hdst.copy_(hsrc, non_blocking=True)
+            torch.cuda.synchronize(dev)
+            h2d_gbs = nbytes / (time.perf_counter() - t_h) / 1e9
+            del hdst, hsrc
+            host_bytes = {
+                "cfg4_from_bytes_host_tx_per_s": world * tb.ntx * hsteps / hel,
+                "cfg4_from_bytes_host_ms_per_batch": hel / hsteps * 1e3,
+                "cfg4_from_bytes_host_correct": host_ok,
+                "cfg4_from_bytes_host_h2d_GBps": h2d_gbs,
+                "cfg4_from_bytes_host_pcie_bound_tx_per_s": world * tb.ntx / (nbytes / (h2d_gbs * 1e9)),
+                "cfg4_from_bytes_host_note": "chip_stx_verify from page-locked host blobs (PCIe included): transaction "
+                                             "chunks, chunk j+1's blobs copied on a second stream beside chunk j's "
+                                             "parse + verify; the pcie bound is the blob bytes / the measured "
+                                             "pinned H2D rate",
+            }
         # algorithmic bytes of one parse: the blobs read once, the index arrays written (components 20 B,
         # signatures 40 B incl. the key interning, required keys 16 B, tx 56 B)
         alg = blob_bytes + 20 * int(p.txs.ncomp) + 40 * int(p.sigs.n) + 16 * int(p.req.nreq) + 56 * tb.ntx
@@ -582,6 +617,7 @@ def main():
                                     "of batch k (steady state over the timed steps); serial = parse then verify "
                                     "on one stream",
             "cfg4_from_bytes_correct": bytes_ok,
+            **host_bytes,
             "cfg4_from_bytes_verdicts": {"ok": int(bvc[0]), "signature_exception": int(bvc[1]),
                                          "signatures_missing": int(bvc[2]), "malformed": int(bvc[3])},
             "cfg4_from_bytes_workload": "%d SignedTransaction blobs (Kryo, %d B each, %.2f GB resident): parse + "
@@ -598,7 +634,7 @@ def main():
                                    "note": "one launch = both parse passes, the pool copy, scans, key interning "
                                            "and the required-key pass with their 3 host syncs"},
         })
-        del bb, bbs, bo, bl, bst, holder, p, dm, ids, fst, fv, fa, fm, tb, tm, sb, evs, s_parse
+        del bb, bbs, bo, bl, bst, holder, p, dm, ids, fst, fv, fa, fm, tb, tm, sb, evs, s_parse, hb
     progress("cfg4 legs done")
     # ---- cfg3: mixed ECDSA r1/k1, one global batch sharded by transaction, RCCL bitmap all-gather ----
     if not args.no_ecdsa:

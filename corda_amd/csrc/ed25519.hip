@@ -116,7 +116,7 @@ __global__ void __launch_bounds__(256) k_ed25519_verify(const uint32_t* __restri
     }
     // h = SHA-512(R || Abyte || M) mod L
     uint32_t hx[16], h[8], s[8];
-    ed_challenge(hx, R, Ab, msg_data + msg_off[mi], msg_len[mi]);
+    ed_challenge(hx, R, Ab, msg_data + msg_off[mi], msg_len[mi], sig);
     sc_reduce512(h, hx);
     // effective S (slide() carry drop) reduced mod L
     ed_effective_s(s, S);
@@ -125,52 +125,76 @@ __global__ void __launch_bounds__(256) k_ed25519_verify(const uint32_t* __restri
     sc_recode256(eb, s);
     const uint32_t* tab = table + (uint64_t)k * ED_TAB_WORDS;
 
+    // windows w = 63..0 of 4 bits: 4 doublings, + the A digit's row of the key table (signed radix 16), and at
+    // every even w + the B digit's entry of the LDS table (signed radix 256).  Window 63 starts from the
+    // identity (no doubling, no multiplication: identity + q = (q+ - q-, q+ + q-, 2Z, 2Z)); the loop runs the
+    // windows in (even, odd) pairs, so nothing in it is conditional and it carries only the projective r.
     ge_p2 r;
-    ge_p2_0(r);
     ge_p1p1 t;
     ge_p3 u;
     ge_cached ca;
-    ge_niels nb;
-    fe z2;
-    for (int w = 63; w >= 0; w--) {
-        if (w != 63) {
-            ge_p2_dbl(t, r);
-            ge_p1p1_to_p2(r, t);
-            ge_p2_dbl(t, r);
-            ge_p1p1_to_p2(r, t);
-            ge_p2_dbl(t, r);
-            ge_p1p1_to_p2(r, t);
-            ge_p2_dbl(t, r);
-            ge_p1p1_to_p3(u, t);
-        } else {
-            ge_p3_0(u);
-        }
-        // A digit (radix 16)
-        const int da = (int)(ea[7] >> 28) - 8;
+    fe qp, qm, xy2d, z2;
+    auto a_digit = [&]() -> int {
+        const int d = (int)(ea[7] >> 28) - 8;
         shl256(ea, 4);
-        const uint32_t ia = (uint32_t)(da < 0 ? -da : da);
-        ed_load_cached(ca, tab + 40 * ia);
-        ge_add_cached(t, u, ca, da < 0);
-        if ((w & 1) == 0) {
-            // B digit (radix 256) at every even nibble position
-            fe_mul(u.X, t.X, t.T);
-            fe_mul(u.Y, t.Z, t.Y);
-            fe_mul2(z2, t.Z, t.T);
-            fe_mul(u.T, t.X, t.Y);
-            const int db = (int)(eb[7] >> 24) - 128;
-            shl256(eb, 8);
-            const uint32_t ib = (uint32_t)(db < 0 ? -db : db);
-            const uint32_t* e = btab + 30 * ib;
-#pragma unroll
-            for (int l = 0; l < 10; l++) {
-                nb.ypx.v[l] = e[l];
-                nb.ymx.v[l] = e[10 + l];
-                nb.xy2d.v[l] = e[20 + l];
-            }
-            ge_madd(t, u, z2, nb, db < 0);
+        return d;
+    };
+    auto doublings = [&]() {   // r -> u = 16 r
+#pragma unroll 1
+        for (int q = 0; q < 3; q++) {
+            ge_p2_dbl(t, r);
+            ge_p1p1_to_p2(r, t);
         }
+        ge_p2_dbl(t, r);
+        ge_p1p1_to_p3(u, t);
+    };
+    auto a_add = [&]() {       // t = u + d (-A)
+        const int d = a_digit();
+        ed_load_row_signed(ca, tab + 40 * (uint32_t)(d < 0 ? -d : d), d < 0);
+        ge_add_row<false>(t, u, ca, (uint32_t)(d >> 31));
+    };
+    auto b_add = [&]() {       // t = t + e B (affine Niels entry |e| of the LDS table, signed)
+        const int e = (int)(eb[7] >> 24) - 128;
+        shl256(eb, 8);
+        const uint32_t ie = (uint32_t)(e < 0 ? -e : e);
+        const uint32_t* ent = btab + 30 * ie;
+        const uint32_t* pp = ent + (e < 0 ? 10 : 0);
+        const uint32_t* pm = ent + (e < 0 ? 0 : 10);
+#pragma unroll
+        for (int l = 0; l < 10; l++) {
+            qp.v[l] = pp[l];
+            qm.v[l] = pm[l];
+            xy2d.v[l] = ent[20 + l];
+        }
+        fe_mul(u.X, t.X, t.T);
+        fe_mul(u.Y, t.Z, t.Y);
+        fe_mul2(z2, t.Z, t.T);
+        fe_mul(u.T, t.X, t.Y);
+        ge_madd_signed(t, u, z2, qp, qm, xy2d, (uint32_t)(e >> 31));
+    };
+    {   // window 63 (odd: no B digit)
+        const int d = a_digit();
+        ed_load_row_signed(ca, tab + 40 * (uint32_t)(d < 0 ? -d : d), d < 0);
+        fe_sub(t.X, ca.YpX, ca.YmX);
+        fe_add(t.Y, ca.YpX, ca.YmX);
+        fe_add(t.Z, ca.Z, ca.Z);
+        t.T = t.Z;
         ge_p1p1_to_p2(r, t);
     }
+#pragma unroll 1
+    for (int w = 62; w > 0; w -= 2) {
+        doublings();           // window w (even)
+        a_add();
+        b_add();
+        ge_p1p1_to_p2(r, t);
+        doublings();           // window w - 1 (odd)
+        a_add();
+        ge_p1p1_to_p2(r, t);
+    }
+    doublings();               // window 0
+    a_add();
+    b_add();
+    ge_p1p1_to_p2(r, t);
     uint32_t enc[8];
     ge_tobytes(enc, r.X, r.Y, r.Z);
     bool eq = true;

@@ -168,7 +168,20 @@ __global__ void __launch_bounds__(64) k_ed_comb_chain(const uint32_t* __restrict
     }
 }
 
-// fill: rows j = 0..2^(W-1) of window w: j * P_w in cached form (row 0 = identity)
+// fill: rows j = 0..2^(W-1) of window w: j * P_w as [Y+X, Y-X, 2Z, 2dT] (2Z stored, so the addition needs no
+// doubling of its column sums; row 0: the identity [1, 1, 2, 0]).  A negative digit reads the same row with
+// Y+X and Y-X swapped by address (-Q = (-x, y)) and negates the 2dT term.
+CHIP_DEV void ed_store_row(uint32_t* __restrict__ dst, const ge_cached& c) {
+    fe z2;
+    fe_add(z2, c.Z, c.Z);            // loose: even limbs < 2^27, odd < 2^26
+#pragma unroll
+    for (int i = 0; i < 10; i++) {
+        dst[i] = c.YpX.v[i];
+        dst[10 + i] = c.YmX.v[i];
+        dst[20 + i] = z2.v[i];
+        dst[30 + i] = c.T2d.v[i];
+    }
+}
 __global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict__ ctr, uint32_t max_slots,
                                                       uint32_t eager, const KeyMeta* __restrict__ meta,
                                                       uint32_t* __restrict__ ctab) {
@@ -178,22 +191,22 @@ __global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict
     if (eager && !ed_key_ok(meta, s)) return;
     uint32_t* e = ctab + (uint64_t)s * ED_COMB_KEY_WORDS + (uint64_t)w * ED_COMB_AENT * 40;
     ge_p3 P;
-    ed_load_p3(P, e + 40);
+    ed_load_p3(P, e + 40);   // P_w, stashed in row +1 by the chain
     ge_cached c1, c;
     fe_1(c.YpX);
     fe_1(c.YmX);
     fe_1(c.Z);
     fe_0(c.T2d);
-    ed_store_cached(e, c);
+    ed_store_row(e, c);
     ge_p3_to_cached(c1, P);
-    ed_store_cached(e + 40, c1);
+    ed_store_row(e + 40, c1);
     ge_p3 Q = P;
     ge_p1p1 t;
     for (int j = 2; j < ED_COMB_AENT; j++) {
         ge_add_cached(t, Q, c1, false);
         ge_p1p1_to_p3(Q, t);
         ge_p3_to_cached(c, Q);
-        ed_store_cached(e + 40 * j, c);
+        ed_store_row(e + 40 * j, c);
     }
 }
 
@@ -337,27 +350,24 @@ CHIP_DEV void recode16(uint32_t out[8], const uint32_t a[8]) {
 //   k_ed_comb_ahalf  + [h](-A) from the key's table (64 cached additions), projective R' to xyz
 // hand-off: [S]B (40 words) + the ED_COMB_ADW words of h's recoded digits, read one word per 4
 // windows by the table half (keeping all 16 live would cost the occupancy step to 3 waves/SIMD)
-#define ED_BMID_WORDS (40 + ED_COMB_ADW)
-#ifndef ED_BHALF_PF
-#define ED_BHALF_PF 0
+#define ED_BMID_SDIG (40 + ED_COMB_ADW)   // S's radix-2^16 digits, hash -> [S]B
+#define ED_BMID_WORDS (ED_BMID_SDIG + 8)
+#ifndef ED_BHALF_MINW
+#define ED_BHALF_MINW 2   // the [S]B additions allocate 165 VGPRs: 3 waves per SIMD (a bound of 3 spills)
 #endif
-#ifndef ED_BHALF_UNROLL
-#define ED_BHALF_UNROLL 0
+#ifndef ED_AHALF_MINW
+#define ED_AHALF_MINW 4   // waves per SIMD: <= 128 VGPRs (127, no scratch)
 #endif
-#ifndef ED_AHALF_WAVES
-#define ED_AHALF_WAVES
-#endif
-__global__ void __launch_bounds__(256) k_ed_comb_bhalf(const uint32_t* __restrict__ list, const uint32_t* __restrict__ ctr,
-                                                       const uint32_t* __restrict__ key_idx,
-                                                       const uint32_t* __restrict__ msg_idx,
-                                                       const uint8_t* __restrict__ sig_data,
-                                                       const uint64_t* __restrict__ sig_off,
-                                                       const uint8_t* __restrict__ msg_data,
-                                                       const uint64_t* __restrict__ msg_off,
-                                                       const uint32_t* __restrict__ msg_len,
-                                                       const uint32_t* __restrict__ abytes,
-                                                       const uint32_t* __restrict__ b16, uint32_t* __restrict__ bmid,
-                                                       uint64_t cap) {
+__global__ void __launch_bounds__(256) k_ed_comb_hash(const uint32_t* __restrict__ list, const uint32_t* __restrict__ ctr,
+                                                      const uint32_t* __restrict__ key_idx,
+                                                      const uint32_t* __restrict__ msg_idx,
+                                                      const uint8_t* __restrict__ sig_data,
+                                                      const uint64_t* __restrict__ sig_off,
+                                                      const uint8_t* __restrict__ msg_data,
+                                                      const uint64_t* __restrict__ msg_off,
+                                                      const uint32_t* __restrict__ msg_len,
+                                                      const uint32_t* __restrict__ abytes, uint32_t* __restrict__ bmid,
+                                                      uint64_t cap) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     if (p >= ctr[ED_CTR_NCOMB]) return;
     const uint32_t i = list[p];
@@ -372,61 +382,59 @@ __global__ void __launch_bounds__(256) k_ed_comb_bhalf(const uint32_t* __restric
         Ab[q] = abytes[(uint64_t)k * 8 + q];
     }
     uint32_t hx[16], h[8], s[8];
-    ed_challenge(hx, R, Ab, msg_data + msg_off[mi], msg_len[mi]);
+    ed_challenge(hx, R, Ab, msg_data + msg_off[mi], msg_len[mi], sig);
     sc_reduce512(h, hx);
     ed_effective_s(s, S);
-    uint32_t db[8];
+    uint32_t db[8], da[ED_COMB_ADW];
     recode16(db, s);
-    // [S]B: one mixed (affine Niels) addition per radix-2^16 window from the identity; the
-    // accumulator carries 2Z
-    ge_p3 u;
-    ge_p3_0(u);
-    fe z2;
-    fe_0(z2);
-    z2.v[0] = 2;
+    recode_bytes<ED_COMB_W, ED_COMB_AWIN>(da, h);
+#pragma unroll
+    for (int q = 0; q < ED_COMB_ADW; q++) bmid[(uint64_t)(40 + q) * cap + p] = da[q];
+#pragma unroll
+    for (int q = 0; q < 8; q++) bmid[(uint64_t)(ED_BMID_SDIG + q) * cap + p] = db[q];
+}
+
+// k_ed_comb_bhalf: [S]B from the fixed radix-2^16 comb, 16 mixed additions; [S]B (extended) into bmid rows 0..39
+__global__ void __launch_bounds__(256, ED_BHALF_MINW) k_ed_comb_bhalf(const uint32_t* __restrict__ ctr,
+                                                                      const uint32_t* __restrict__ b16,
+                                                                      uint32_t* __restrict__ bmid, uint64_t cap) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= ctr[ED_CTR_NCOMB]) return;
+    const uint32_t* sdig = bmid + (uint64_t)ED_BMID_SDIG * cap + p;   // digit word j at sdig[j * cap]
+    // [S]B: one mixed (affine Niels) addition per radix-2^16 window.  Window 0 from the identity needs no
+    // multiplication: identity + q = (q+ - q-, q+ + q-, 2, 2) in completed form.  The loop carries only t.
     ge_p1p1 t;
-    ge_niels nb;
-#if ED_BHALF_PF
-    // touch the line of the entry ED_BHALF_PF windows ahead (one dword: the 128-B line comes into L2
-    // while this window's addition runs)
-    uint32_t pf = 0;
-#endif
-#if ED_BHALF_UNROLL
-#pragma unroll
-#endif
-    for (int wd = 0; wd < 8; wd++) {
-        const uint32_t cur = db[0];
-#if ED_BHALF_PF
-        const uint32_t nxt = db[ED_BHALF_PF / 2 < 8 ? ED_BHALF_PF / 2 : 7];
-#endif
-#pragma unroll
-        for (int q = 0; q < 7; q++) db[q] = db[q + 1];
-#pragma unroll
-        for (int e = 0; e < 2; e++) {
-            const int w = wd * 2 + e;
-            const int d = (int)(int16_t)(cur >> (16 * e));
-            const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
-#if ED_BHALF_PF
-            if (w + ED_BHALF_PF < ED_B16_WIN) {
-                const int dn = (int)(int16_t)(nxt >> (16 * e));
-                const uint32_t an = (uint32_t)(dn < 0 ? -dn : dn);
-                pf ^= __builtin_nontemporal_load(b16 + ((uint64_t)(w + ED_BHALF_PF) * ED_B16_ENT + an) * 32);
-            }
-#endif
-            ed_load_niels(nb, b16 + ((uint64_t)w * ED_B16_ENT + ad) * 32);
-            if (w > 0) {
-                fe_mul(u.X, t.X, t.T);
-                fe_mul(u.Y, t.Z, t.Y);
-                fe_mul2(z2, t.Z, t.T);
-                fe_mul(u.T, t.X, t.Y);
-            }
-            ge_madd(t, u, z2, nb, d < 0);
-        }
+    fe qp, qm, xy2d, z2;
+    uint32_t cur = sdig[0];
+    {
+        const int d = (int)(int16_t)cur;
+        const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+        ed_load_niels_signed(qp, qm, xy2d, b16 + (uint64_t)ad * 32, d < 0);
+        fe_sub(t.X, qp, qm);
+        fe_add(t.Y, qp, qm);
+        fe_0(t.Z);
+        t.Z.v[0] = 2;
+        t.T = t.Z;
+    }
+    ge_p3 u;
+    // window w: the signed digit d of S, entry |d| of the window's table; the accumulator carries 2Z
+    auto window = [&](uint32_t w, int d) {
+        const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
+        ed_load_niels_signed(qp, qm, xy2d, b16 + ((uint64_t)w * ED_B16_ENT + ad) * 32, d < 0);
+        fe_mul(u.X, t.X, t.T);
+        fe_mul(u.Y, t.Z, t.Y);
+        fe_mul2(z2, t.Z, t.T);
+        fe_mul(u.T, t.X, t.Y);
+        ge_madd_signed(t, u, z2, qp, qm, xy2d, (uint32_t)(d >> 31));
+    };
+    window(1, (int)(int16_t)(cur >> 16));
+#pragma unroll 1
+    for (uint32_t wd = 1; wd < ED_B16_WIN / 2; wd++) {   // two windows per digit word, read as it is needed
+        cur = sdig[(uint64_t)wd * cap];
+        window(2 * wd, (int)(int16_t)cur);
+        window(2 * wd + 1, (int)(int16_t)(cur >> 16));
     }
     ge_p1p1_to_p3(u, t);
-#if ED_BHALF_PF
-    if (pf == 0x9e3779b9u && p == 0xffffffffu) bmid[0] = pf;   // keeps the touches (never true: p < cap)
-#endif
 #pragma unroll
     for (int q = 0; q < 10; q++) {
         bmid[(uint64_t)q * cap + p] = u.X.v[q];
@@ -434,13 +442,9 @@ __global__ void __launch_bounds__(256) k_ed_comb_bhalf(const uint32_t* __restric
         bmid[(uint64_t)(20 + q) * cap + p] = u.Z.v[q];
         bmid[(uint64_t)(30 + q) * cap + p] = u.T.v[q];
     }
-    uint32_t da[ED_COMB_ADW];
-    recode_bytes<ED_COMB_W, ED_COMB_AWIN>(da, h);
-#pragma unroll
-    for (int q = 0; q < ED_COMB_ADW; q++) bmid[(uint64_t)(40 + q) * cap + p] = da[q];
 }
 
-__global__ void __launch_bounds__(256, 2) ED_AHALF_WAVES k_ed_comb_ahalf(const uint32_t* __restrict__ list,
+__global__ void __launch_bounds__(256, ED_AHALF_MINW) k_ed_comb_ahalf(const uint32_t* __restrict__ list,
                                                                       const uint32_t* __restrict__ ctr,
                                                        const uint32_t* __restrict__ key_idx,
                                                        const int32_t* __restrict__ key_slot,
@@ -451,6 +455,7 @@ __global__ void __launch_bounds__(256, 2) ED_AHALF_WAVES k_ed_comb_ahalf(const u
     const uint32_t p = xcd_block(blockIdx.x, (ncomb + 255) / 256) * blockDim.x + threadIdx.x;
     if (p >= ncomb) return;
     const uint32_t k = key_idx[list[p]];
+    // digit d of window w (-16..16) reads row |d| of the window, signed
     const uint32_t* tab = ctab + (uint64_t)key_slot[k] * ED_COMB_KEY_WORDS;
     ge_p3 u;
 #pragma unroll
@@ -460,22 +465,23 @@ __global__ void __launch_bounds__(256, 2) ED_AHALF_WAVES k_ed_comb_ahalf(const u
         u.Z.v[q] = bmid[(uint64_t)(20 + q) * cap + p];
         u.T.v[q] = bmid[(uint64_t)(30 + q) * cap + p];
     }
-    // + [h](-A): one cached addition per window (extended coordinates, unified = complete formulas)
-    ge_p1p1 t;
+    // + [h](-A): one addition per window from the key's signed-multiple rows (extended coordinates, unified =
+    // complete formulas); window 0 peeled so the loop carries only the completed point t
+    uint32_t cur = bmid[(uint64_t)40 * cap + p];
     ge_cached ca;
-    for (int wd = 0; wd < ED_COMB_ADW; wd++) {
-        const uint32_t cur = bmid[(uint64_t)(40 + wd) * cap + p];
-#pragma unroll
-        for (int e = 0; e < 4; e++) {
-            const int w = wd * 4 + e;
-            if (w < ED_COMB_AWIN) {
-                const int d = (int)((cur >> (8 * e)) & 0xffu) - ED_COMB_ABIAS;
-                const uint32_t ad = (uint32_t)(d < 0 ? -d : d);
-                ed_load_cached(ca, tab + ((uint32_t)w * ED_COMB_AENT + ad) * 40);
-                if (w > 0) ge_p1p1_to_p3(u, t);
-                ge_add_cached(t, u, ca, d < 0);
-            }
-        }
+    ge_p1p1 t;
+    {
+        const int d = (int)(cur & 0xffu) - ED_COMB_ABIAS;
+        ed_load_row_signed(ca, tab + (uint32_t)(d < 0 ? -d : d) * 40, d < 0);
+        ge_add_row(t, u, ca, (uint32_t)(d >> 31));
+    }
+#pragma unroll 1
+    for (uint32_t w = 1; w < ED_COMB_AWIN; w++) {
+        if ((w & 3u) == 0) cur = bmid[(uint64_t)(40 + (w >> 2)) * cap + p];
+        const int d = (int)((cur >> (8 * (w & 3u))) & 0xffu) - ED_COMB_ABIAS;
+        ed_load_row_signed(ca, tab + (w * ED_COMB_AENT + (uint32_t)(d < 0 ? -d : d)) * 40, d < 0);
+        ge_p1p1_to_p3(u, t);
+        ge_add_row(t, u, ca, (uint32_t)(d >> 31));
     }
     // projective R' = (X : Y : Z), stored structure-of-arrays for the finish kernel
     fe X, Y, Z;
@@ -578,9 +584,9 @@ uint64_t ed_comb_bmid_words() { return ED_BMID_WORDS; }
 void launch_ed_comb_bhalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, const uint32_t* abytes,
                           const EdCombWs& w) {
     if (!n || !w.max_slots) return;
-    hipLaunchKernelGGL(k_ed_comb_bhalf, dim3(nblk(n, 256)), dim3(256), 0, st, w.comb_list, w.ctr, b->key_idx, b->msg_idx,
-                       b->sig_data, b->sig_off, b->msg_data, b->msg_off, b->msg_len, abytes, w.bcomb16, w.bmid,
-                       (uint64_t)n);
+    hipLaunchKernelGGL(k_ed_comb_hash, dim3(nblk(n, 256)), dim3(256), 0, st, w.comb_list, w.ctr, b->key_idx, b->msg_idx,
+                       b->sig_data, b->sig_off, b->msg_data, b->msg_off, b->msg_len, abytes, w.bmid, (uint64_t)n);
+    hipLaunchKernelGGL(k_ed_comb_bhalf, dim3(nblk(n, 256)), dim3(256), 0, st, w.ctr, w.bcomb16, w.bmid, (uint64_t)n);
 }
 void launch_ed_comb_ahalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w) {
     if (!n || !w.max_slots) return;

@@ -1450,6 +1450,123 @@ int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_sta
     return stx_parse(c, B, in, tx_status, out, stream ? (hipStream_t)stream : c->stream);
 }
 
+// one chunk of a host blob batch: (offset, length) inside the pool (flag), and the byte range [min off,
+// max off + len) the chunk reads; out as k_chunk_init leaves it ([0] flags, [1] min, [2] max)
+__global__ void __launch_bounds__(256) k_blob_range(uint64_t m, const uint64_t* __restrict__ off,
+                                                    const uint32_t* __restrict__ len, uint64_t pool,
+                                                    unsigned long long* __restrict__ out) {
+    const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t f = 0;
+    unsigned long long lo = ~0ull, hi = 0;
+    if (i < m) {
+        const uint64_t o = off[i], e = o + len[i];
+        if (e > pool || e < o) f = 1;
+        else lo = o, hi = e;
+    }
+#pragma unroll
+    for (int s = 32; s > 0; s >>= 1) {
+        f |= (uint32_t)__shfl_xor((int)f, s);
+        lo = min(lo, (unsigned long long)__shfl_xor((long long)lo, s));
+        hi = max(hi, (unsigned long long)__shfl_xor((long long)hi, s));
+    }
+    if ((threadIdx.x & 63) == 0) {
+        if (f) atomicOr(&out[0], (unsigned long long)f);
+        if (lo != ~0ull) atomicMin(&out[1], lo);
+        if (hi) atomicMax(&out[2], hi);
+    }
+}
+
+// chip_stx_verify over a host batch in transaction chunks: chunk j+1's offsets, lengths, range check and blob
+// bytes go over PCIe on hcs while chunk j is parsed and verified on the main stream.  The blobs are copied to
+// their own offsets (the copied part of the pool grows as one interval), so every offset stays valid and the
+// in-place parse's extra region (behind the pool, reused by every chunk in stream order) never meets a copy.
+static int stx_verify_host_pipelined(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t* off,
+                                     const uint32_t* len, uint64_t data_bytes, const chip_msg_templates* dtm,
+                                     const int32_t* meta, uint32_t n_meta, uint8_t* tx_status, uint8_t* verdict,
+                                     uint32_t* arg, uint8_t* ids, uint64_t chunks) {
+    hipStream_t st = c->stream, cs = c->hcs;
+    std::vector<uint64_t> at{0};
+    for (uint64_t k = 1; k <= chunks; k++) at.push_back(std::min(n, (n * k + chunks - 1) / chunks));
+    HIPCHK(c, c->h_rngd.ensure(64));
+    HIPCHK(c, hipEventRecord(c->hev_p, st));   // earlier work on these buffers before any copy into them
+    HIPCHK(c, hipStreamWaitEvent(cs, c->hev_p, 0));
+    uint64_t clo = 0, chi = 0;
+    bool any = false;
+    auto copy = [&](uint64_t lo, uint64_t hi) -> int {
+        if (lo >= hi) return CHIP_OK;
+        if (!any) {
+            HIPCHK(c, hipMemcpyAsync(c->h2_data.as<uint8_t>() + lo, data + lo, hi - lo, hipMemcpyHostToDevice, cs));
+            clo = lo, chi = hi, any = true;
+            return CHIP_OK;
+        }
+        if (lo < clo) {
+            HIPCHK(c, hipMemcpyAsync(c->h2_data.as<uint8_t>() + lo, data + lo, clo - lo, hipMemcpyHostToDevice, cs));
+            clo = lo;
+        }
+        if (hi > chi) {
+            HIPCHK(c, hipMemcpyAsync(c->h2_data.as<uint8_t>() + chi, data + chi, hi - chi, hipMemcpyHostToDevice, cs));
+            chi = hi;
+        }
+        return CHIP_OK;
+    };
+    // stage chunk j on hcs: offsets / lengths, the range check (host waits for hcs only), the blob bytes;
+    // hev_p = the chunk is on the device
+    auto stage_chunk = [&](uint64_t j) -> int {
+        const uint64_t a = at[j], m = at[j + 1] - a;
+        HIPCHK(c, hipMemcpyAsync(c->h2_off.as<uint64_t>() + a, off + a, m * 8, hipMemcpyHostToDevice, cs));
+        HIPCHK(c, hipMemcpyAsync(c->h2_len.as<uint32_t>() + a, len + a, m * 4, hipMemcpyHostToDevice, cs));
+        unsigned long long* out = c->h_rngd.as<unsigned long long>();
+        hipLaunchKernelGGL(k_chunk_init, dim3(1), dim3(64), 0, cs, out);
+        hipLaunchKernelGGL(k_blob_range, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, cs, m,
+                           c->h2_off.as<uint64_t>() + a, c->h2_len.as<uint32_t>() + a, data_bytes, out);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(c->h_rng, out, 64, hipMemcpyDeviceToHost, cs));
+        HIPCHK(c, hipStreamSynchronize(cs));
+        const unsigned long long* q = c->h_rng;
+        if (q[0]) return fail(c, CHIP_E_ARG, "blob outside pool");
+        if (int rc = copy(q[1] == ~0ull ? 0 : q[1], q[2])) return rc;
+        HIPCHK(c, hipEventRecord(c->hev_p, cs));
+        return CHIP_OK;
+    };
+    int r;
+    if ((r = stage_chunk(0))) return r;
+    for (uint64_t j = 0; j + 1 < at.size(); j++) {
+        const uint64_t a = at[j], m = at[j + 1] - a;
+        // the previous chunk's verify is done before this parse may grow (reallocate) a buffer it reads; the
+        // next chunk's copy, issued below, runs beside this chunk's parse and verify
+        if (j) HIPCHK(c, hipStreamSynchronize(st));
+        HIPCHK(c, hipStreamWaitEvent(st, c->hev_p, 0));
+        if (j + 2 < at.size() && (r = stage_chunk(j + 1))) {
+            hipStreamSynchronize(st);
+            return r;
+        }
+        chip_stx_blobs in{m, c->h2_data.as<uint8_t>(), c->h2_off.as<uint64_t>() + a, c->h2_len.as<uint32_t>() + a,
+                          data_bytes, meta, n_meta, CHIP_STX_REQUIRED, c->h2_data.cap};
+        chip_stx_parsed p;
+        if ((r = stx_parse(c, c->stx[2], &in, c->h2_st.as<uint8_t>() + a, &p, st))) return r;
+        HIPCHK(c, c->h2_sigst.ensure(p.sigs.n + 16));
+        HIPCHK(c, c->h2_miss.ensure(p.req.nreq + 16));
+        if ((r = chip_verify_signed_tx_batch_device(c, &p.txs, dtm, &p.sigs, &p.req, c->h2_ids.as<uint8_t>() + 32 * a,
+                                                    c->h2_sigst.as<uint8_t>(), c->h2_v.as<uint8_t>() + a,
+                                                    c->h2_a.as<uint32_t>() + a, c->h2_miss.as<uint8_t>(), st)))
+            return r;
+    }
+    HIPCHK(c, hipMemcpyAsync(tx_status, c->h2_st.p, n, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(verdict, c->h2_v.p, n, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipMemcpyAsync(arg, c->h2_a.p, n * 4, hipMemcpyDeviceToHost, st));
+    if (ids) HIPCHK(c, hipMemcpyAsync(ids, c->h2_ids.p, n * 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    return CHIP_OK;
+}
+
+// transaction chunks of chip_stx_verify: 1 below 2^17 transactions, else about 2^17 a chunk, at most 8
+// (CHIP_STX_CHUNKS overrides)
+static uint64_t stx_host_chunks(uint64_t n) {
+    uint64_t k = n >= (1ull << 17) ? std::min<uint64_t>(8, (n + (1ull << 16)) >> 17) : 1;
+    if (const char* e = getenv("CHIP_STX_CHUNKS")) k = std::max<uint64_t>(1, std::min<uint64_t>(64, strtoull(e, nullptr, 10)));
+    return std::min<uint64_t>(k, std::max<uint64_t>(1, n));
+}
+
 int chip_stx_verify(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t* off, const uint32_t* len,
                     uint64_t data_bytes, const chip_msg_templates* tmpl, const int32_t* meta, uint32_t n_meta,
                     uint8_t* tx_status, uint8_t* verdict, uint32_t* arg, uint8_t* ids) {
@@ -1467,14 +1584,17 @@ int chip_stx_verify(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t
     HIPCHK(c, hipSetDevice(c->device));
     // the staged blobs get room for the de-chunked runs behind them (in-place parse, no copy of the blobs)
     HIPCHK(c, c->h2_data.ensure(((data_bytes + 15) & ~15ull) + data_bytes / 2 + 4096 + 64));
-    if ((r = stage(c, c->h2_data, data, data_bytes, st)) || (r = stage(c, c->h2_off, off, n, st)) ||
-        (r = stage(c, c->h2_len, len, n, st)) || (r = stage(c, c->h2_td, tmpl->data, tmpl->data_bytes, st)) ||
-        (r = stage(c, c->h2_to, tmpl->off, tmpl->n, st)) || (r = stage(c, c->h2_tl, tmpl->len, tmpl->n, st)) ||
-        (r = stage(c, c->h2_ta, tmpl->id_at, tmpl->n, st)))
+    const uint64_t chunks = stx_host_chunks(n);
+    if ((r = stage(c, c->h2_td, tmpl->data, tmpl->data_bytes, st)) || (r = stage(c, c->h2_to, tmpl->off, tmpl->n, st)) ||
+        (r = stage(c, c->h2_tl, tmpl->len, tmpl->n, st)) || (r = stage(c, c->h2_ta, tmpl->id_at, tmpl->n, st)))
         return r;
-    {   // blob ranges inside the pool; templates inside theirs, id offset inside, len <= max_len
+    if (chunks == 1 && ((r = stage(c, c->h2_data, data, data_bytes, st)) || (r = stage(c, c->h2_off, off, n, st)) ||
+                        (r = stage(c, c->h2_len, len, n, st))))
+        return r;
+    {   // blob ranges inside the pool (the chunked path checks each chunk's); templates inside theirs, id offset
+        // inside, len <= max_len
         const DevCheck chk[] = {
-            {DEV_CHECK_RANGE, 1, c->h2_off.p, c->h2_len.p, nullptr, n, data_bytes, 0xffffffffull},
+            {DEV_CHECK_RANGE, 1, c->h2_off.p, c->h2_len.p, nullptr, chunks == 1 ? n : 0, data_bytes, 0xffffffffull},
             {DEV_CHECK_RANGE, 2, c->h2_to.p, c->h2_tl.p, c->h2_ta.p, tmpl->n, tmpl->data_bytes,
              tmpl->max_len}};
         uint32_t bad = 0;
@@ -1490,6 +1610,12 @@ int chip_stx_verify(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t
     dtm.off = c->h2_to.as<uint64_t>();
     dtm.len = c->h2_tl.as<uint32_t>();
     dtm.id_at = c->h2_ta.as<uint32_t>();
+    if (chunks > 1) {
+        HIPCHK(c, c->h2_off.ensure(n * 8 + 16));
+        HIPCHK(c, c->h2_len.ensure(n * 4 + 16));
+        return stx_verify_host_pipelined(c, n, data, off, len, data_bytes, &dtm, meta, n_meta, tx_status, verdict, arg,
+                                         ids, chunks);
+    }
     chip_stx_blobs in{n, c->h2_data.as<uint8_t>(), c->h2_off.as<uint64_t>(), c->h2_len.as<uint32_t>(), data_bytes,
                       meta, n_meta, CHIP_STX_REQUIRED, c->h2_data.cap};
     chip_stx_parsed p;

@@ -142,7 +142,7 @@ void launch_ecdsa_key_check(hipStream_t st, uint64_t n, const uint8_t* pool, con
 #endif
 #define ED_COMB_AWIN ((253 + ED_COMB_W - 1) / ED_COMB_W)   // W=5: 51 windows (top digit <= 8)
 #define ED_COMB_AENT ((1 << (ED_COMB_W - 1)) + 1)          // multiples 0..2^(W-1)
-#define ED_COMB_KEY_WORDS (ED_COMB_AWIN * ED_COMB_AENT * 40)
+#define ED_COMB_KEY_WORDS (ED_COMB_AWIN * ED_COMB_AENT * 40)  // rows [Y+X, Y-X, 2Z, 2dT] of 40 words
 #ifndef ED_FIN_G
 #define ED_FIN_G 16                                        // signatures per batched inversion
 #endif

@@ -106,36 +106,42 @@ CHIP_DEV uint32_t sel8(const uint32_t v[8], uint32_t i) {
 // Only reachable for s >= 2^255 (carries below that never overflow: SURVEY/DESIGN note);
 // exact literal simulation of the recoding over a 256-bit register.
 CHIP_DEV uint32_t slide_drops(const uint32_t s[8]) {
+    // ref10 slide() over the bits of s, word by word: word k (static after unrolling) and its successor hold
+    // every bit a window anchored in word k looks at (<= 6 ahead), so no register is indexed dynamically
     uint32_t v[8];
 #pragma unroll
     for (int k = 0; k < 8; k++) v[k] = s[k];
     uint32_t drops = 0;
-    for (uint32_t i = 0; i < 256; i++) {
-        if (!((sel8(v, i >> 5) >> (i & 31)) & 1u)) continue;
-        int acc = 1;
-        for (uint32_t b = 1; b <= 6 && i + b < 256; b++) {
-            const uint32_t pos = i + b;
-            if (!((sel8(v, pos >> 5) >> (pos & 31)) & 1u)) continue;
-            if (acc + (1 << b) <= 15) {
-                acc += 1 << b;
-                // clear bit pos
 #pragma unroll
-                for (int k = 0; k < 8; k++)
-                    if ((uint32_t)k == (pos >> 5)) v[k] &= ~(1u << (pos & 31));
-            } else if (acc - (1 << b) >= -15) {
-                acc -= 1 << b;
-                // v += 2^pos (binary increment from position pos), overflow = dropped carry
-                uint64_t c = 0;
+    for (int k = 0; k < 8; k++) {
+        for (uint32_t j = 0; j < 32; j++) {
+            const uint32_t i = 32u * k + j;
+            if (!((v[k] >> j) & 1u)) continue;
+            int acc = 1;
+            for (uint32_t b = 1; b <= 6 && i + b < 256; b++) {
+                const uint32_t pos = j + b;   // bit of the 64-bit window (v[k+1] : v[k])
+                const uint64_t win = ((uint64_t)(k < 7 ? v[k < 7 ? k + 1 : 7] : 0u) << 32) | v[k];
+                if (!((win >> pos) & 1u)) continue;
+                if (acc + (1 << b) <= 15) {
+                    acc += 1 << b;
+                    if (pos < 32) v[k] &= ~(1u << pos);
+                    else if (k < 7) v[k < 7 ? k + 1 : 7] &= ~(1u << (pos - 32));
+                } else if (acc - (1 << b) >= -15) {
+                    acc -= 1 << b;
+                    // v += 2^(32k + pos) (binary increment), overflow past bit 255 = the dropped carry
+                    uint64_t c = 0;
 #pragma unroll
-                for (int k = 0; k < 8; k++) {
-                    const uint32_t add = ((uint32_t)k == (pos >> 5)) ? (1u << (pos & 31)) : 0u;
-                    c += (uint64_t)v[k] + add;
-                    v[k] = (uint32_t)c;
-                    c >>= 32;
+                    for (int q = k; q < 8; q++) {
+                        const uint32_t add = (q == k && pos < 32) ? (1u << pos)
+                                             : ((q == k + 1 && pos >= 32) ? (1u << (pos - 32)) : 0u);
+                        c += (uint64_t)v[q] + add;
+                        v[q] = (uint32_t)c;
+                        c >>= 32;
+                    }
+                    drops += (uint32_t)c;
+                } else {
+                    break;
                 }
-                drops += (uint32_t)c;
-            } else {
-                break;
             }
         }
     }

@@ -35,6 +35,19 @@ __device__ __constant__ const uint64_t SHA512_K[80] = {
     0x28db77f523047d84ull, 0x32caab7b40c72493ull, 0x3c9ebe0a15c9bebcull, 0x431d67c49c100d4cull,
     0x4cc5d4becb3e42b6ull, 0x597f299cfc657e2aull, 0x5fcb6fab3ad6faecull, 0x6c44198c4a475817ull};
 
+// LUT index = S0 << 2 | S1 << 1 | S2
+#define BITOP3_XOR3 0x96
+#define BITOP3_CH 0xCA    // S0 ? S1 : S2
+#define BITOP3_MAJ 0xE8
+// 16 rounds (SHA-256 and SHA-512) with the round function's variables rotated by name (8 rounds = one full rotation: no moves), the
+// message schedule in place in w[16] (static indices: the 16 rounds of a group are unrolled, the 5 groups are not)
+#define SHA2_16(BODY)                                                                                          \
+    BODY(0, a, b, c, d, e, f, g, hh) BODY(1, hh, a, b, c, d, e, f, g) BODY(2, g, hh, a, b, c, d, e, f)          \
+    BODY(3, f, g, hh, a, b, c, d, e) BODY(4, e, f, g, hh, a, b, c, d) BODY(5, d, e, f, g, hh, a, b, c)          \
+    BODY(6, c, d, e, f, g, hh, a, b) BODY(7, b, c, d, e, f, g, hh, a) BODY(8, a, b, c, d, e, f, g, hh)          \
+    BODY(9, hh, a, b, c, d, e, f, g) BODY(10, g, hh, a, b, c, d, e, f) BODY(11, f, g, hh, a, b, c, d, e)        \
+    BODY(12, e, f, g, hh, a, b, c, d) BODY(13, d, e, f, g, hh, a, b, c) BODY(14, c, d, e, f, g, hh, a, b)       \
+    BODY(15, b, c, d, e, f, g, hh, a)
 CHIP_DEV uint32_t rotr32(uint32_t x, int n) { return __builtin_amdgcn_alignbit(x, x, n); }
 CHIP_DEV uint64_t rotr64(uint64_t x, int n) { return (x >> n) | (x << (64 - n)); }
 
@@ -42,28 +55,33 @@ CHIP_DEV void sha256_init(uint32_t h[8]) {
     h[0] = 0x6a09e667u; h[1] = 0xbb67ae85u; h[2] = 0x3c6ef372u; h[3] = 0xa54ff53au;
     h[4] = 0x510e527fu; h[5] = 0x9b05688cu; h[6] = 0x1f83d9abu; h[7] = 0x5be0cd19u;
 }
-// w: 16 big-endian message words (clobbered as the schedule ring)
+// w: 16 big-endian message words (clobbered as the schedule ring).  Three-input logic as v_bitop3_b32 (xor3 / ch /
+// maj: dual-issue class on gfx950), rotates as v_alignbit_b32; rounds in unrolled groups of 16 with the state
+// rotated by name (8 rounds = one rotation) and the schedule ring at static indices.
+#define SHA256_ROUND(a, b, c, d, e, f, g, hh, kw)                                                                \
+    do {                                                                                                         \
+        const uint32_t S1_ = __builtin_amdgcn_bitop3_b32(rotr32(e, 6), rotr32(e, 11), rotr32(e, 25), BITOP3_XOR3); \
+        const uint32_t t1_ = hh + S1_ + __builtin_amdgcn_bitop3_b32(e, f, g, BITOP3_CH) + (kw);                   \
+        const uint32_t S0_ = __builtin_amdgcn_bitop3_b32(rotr32(a, 2), rotr32(a, 13), rotr32(a, 22), BITOP3_XOR3); \
+        d += t1_;                                                                                                \
+        hh = t1_ + S0_ + __builtin_amdgcn_bitop3_b32(a, b, c, BITOP3_MAJ);                                      \
+    } while (0)
 CHIP_DEV void sha256_compress(uint32_t h[8], uint32_t w[16]) {
     uint32_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
-#pragma unroll
-    for (int i = 0; i < 64; i++) {
-        uint32_t wi;
-        if (i < 16) {
-            wi = w[i];
-        } else {
-            uint32_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-            uint32_t s0 = rotr32(w15, 7) ^ rotr32(w15, 18) ^ (w15 >> 3);
-            uint32_t s1 = rotr32(w2, 17) ^ rotr32(w2, 19) ^ (w2 >> 10);
-            wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
-            w[i & 15] = wi;
+#define SHA256_R0(j, A, B, C, D, E, F, G, H) SHA256_ROUND(A, B, C, D, E, F, G, H, SHA256_K[j] + w[j]);
+    SHA2_16(SHA256_R0)
+#undef SHA256_R0
+#pragma unroll 1
+    for (int r = 16; r < 64; r += 16) {
+#define SHA256_RS(j, A, B, C, D, E, F, G, H)                                                                   \
+        {                                                                                                      \
+            const uint32_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];                                       \
+            w[j] += __builtin_amdgcn_bitop3_b32(rotr32(w15, 7), rotr32(w15, 18), w15 >> 3, BITOP3_XOR3) +       \
+                    w[(j + 9) & 15] + __builtin_amdgcn_bitop3_b32(rotr32(w2, 17), rotr32(w2, 19), w2 >> 10, BITOP3_XOR3); \
+            SHA256_ROUND(A, B, C, D, E, F, G, H, SHA256_K[r + j] + w[j]);                                      \
         }
-        uint32_t S1 = rotr32(e, 6) ^ rotr32(e, 11) ^ rotr32(e, 25);
-        uint32_t ch = (e & f) ^ (~e & g);
-        uint32_t t1 = hh + S1 + ch + SHA256_K[i] + wi;
-        uint32_t S0 = rotr32(a, 2) ^ rotr32(a, 13) ^ rotr32(a, 22);
-        uint32_t mj = (a & b) ^ (a & c) ^ (b & c);
-        uint32_t t2 = S0 + mj;
-        hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+        SHA2_16(SHA256_RS)
+#undef SHA256_RS
     }
     h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
 }
@@ -73,27 +91,52 @@ CHIP_DEV void sha512_init(uint64_t h[8]) {
     h[3] = 0xa54ff53a5f1d36f1ull; h[4] = 0x510e527fade682d1ull; h[5] = 0x9b05688c2b3e6c1full;
     h[6] = 0x1f83d9abfb41bd6bull; h[7] = 0x5be0cd19137e2179ull;
 }
+// 64-bit rotates / shifts / three-input logic on the 32-bit halves: one v_alignbit_b32 per half for a rotate (the
+// compiler otherwise builds them from two 64-bit shifts and two ORs), one v_bitop3_b32 per half for xor3 / ch / maj
+// (a dual-issue class instruction on gfx950: tools/microbench_valu.hip)
+CHIP_DEV uint64_t u64_of(uint32_t lo, uint32_t hi) { return ((uint64_t)hi << 32) | lo; }
+template <int N>
+CHIP_DEV uint64_t rotr64h(uint64_t x) {
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    if (N < 32) return u64_of(__builtin_amdgcn_alignbit(hi, lo, N), __builtin_amdgcn_alignbit(lo, hi, N));
+    return u64_of(__builtin_amdgcn_alignbit(lo, hi, N - 32), __builtin_amdgcn_alignbit(hi, lo, N - 32));
+}
+template <int N>
+CHIP_DEV uint64_t shr64h(uint64_t x) {   // N < 32
+    const uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+    return u64_of(__builtin_amdgcn_alignbit(hi, lo, N), hi >> N);
+}
+template <uint32_t LUT>
+CHIP_DEV uint64_t bitop3_64(uint64_t a, uint64_t b, uint64_t c) {
+    return u64_of(__builtin_amdgcn_bitop3_b32((uint32_t)a, (uint32_t)b, (uint32_t)c, LUT),
+                  __builtin_amdgcn_bitop3_b32((uint32_t)(a >> 32), (uint32_t)(b >> 32), (uint32_t)(c >> 32), LUT));
+}
+
+// one round of SHA-512 on the rotating state (a..hh renamed by the caller's unrolled sequence)
+#define SHA512_ROUND(a, b, c, d, e, f, g, hh, kw)                                                                \
+    do {                                                                                                         \
+        const uint64_t S1_ = bitop3_64<BITOP3_XOR3>(rotr64h<14>(e), rotr64h<18>(e), rotr64h<41>(e));            \
+        const uint64_t t1_ = hh + S1_ + bitop3_64<BITOP3_CH>(e, f, g) + (kw);                                   \
+        const uint64_t S0_ = bitop3_64<BITOP3_XOR3>(rotr64h<28>(a), rotr64h<34>(a), rotr64h<39>(a));            \
+        d += t1_;                                                                                                \
+        hh = t1_ + S0_ + bitop3_64<BITOP3_MAJ>(a, b, c);                                                        \
+    } while (0)
 CHIP_DEV void sha512_compress(uint64_t h[8], uint64_t w[16]) {
     uint64_t a = h[0], b = h[1], c = h[2], d = h[3], e = h[4], f = h[5], g = h[6], hh = h[7];
-#pragma unroll
-    for (int i = 0; i < 80; i++) {
-        uint64_t wi;
-        if (i < 16) {
-            wi = w[i];
-        } else {
-            uint64_t w15 = w[(i - 15) & 15], w2 = w[(i - 2) & 15];
-            uint64_t s0 = rotr64(w15, 1) ^ rotr64(w15, 8) ^ (w15 >> 7);
-            uint64_t s1 = rotr64(w2, 19) ^ rotr64(w2, 61) ^ (w2 >> 6);
-            wi = w[i & 15] + s0 + w[(i - 7) & 15] + s1;
-            w[i & 15] = wi;
+#define SHA512_R0(j, A, B, C, D, E, F, G, H) SHA512_ROUND(A, B, C, D, E, F, G, H, SHA512_K[j] + w[j]);
+    SHA2_16(SHA512_R0)
+#undef SHA512_R0
+#pragma unroll 1
+    for (int r = 16; r < 80; r += 16) {
+#define SHA512_RS(j, A, B, C, D, E, F, G, H)                                                                   \
+        {                                                                                                      \
+            const uint64_t w15 = w[(j + 1) & 15], w2 = w[(j + 14) & 15];                                       \
+            w[j] += bitop3_64<BITOP3_XOR3>(rotr64h<1>(w15), rotr64h<8>(w15), shr64h<7>(w15)) + w[(j + 9) & 15] + \
+                    bitop3_64<BITOP3_XOR3>(rotr64h<19>(w2), rotr64h<61>(w2), shr64h<6>(w2));                   \
+            SHA512_ROUND(A, B, C, D, E, F, G, H, SHA512_K[r + j] + w[j]);                                      \
         }
-        uint64_t S1 = rotr64(e, 14) ^ rotr64(e, 18) ^ rotr64(e, 41);
-        uint64_t ch = (e & f) ^ (~e & g);
-        uint64_t t1 = hh + S1 + ch + SHA512_K[i] + wi;
-        uint64_t S0 = rotr64(a, 28) ^ rotr64(a, 34) ^ rotr64(a, 39);
-        uint64_t mj = (a & b) ^ (a & c) ^ (b & c);
-        uint64_t t2 = S0 + mj;
-        hh = g; g = f; f = e; e = d + t1; d = c; c = b; b = a; a = t1 + t2;
+        SHA2_16(SHA512_RS)
+#undef SHA512_RS
     }
     h[0] += a; h[1] += b; h[2] += c; h[3] += d; h[4] += e; h[5] += f; h[6] += g; h[7] += hh;
 }
@@ -103,9 +146,8 @@ CHIP_DEV void sha512_compress(uint64_t h[8], uint64_t w[16]) {
 // word lies inside the string.
 CHIP_DEV uint32_t comp_word(const uint8_t* p, uint32_t len, int64_t q) {
     if (q >= 0 && q + 4 <= (int64_t)len) {
-        const uintptr_t a = (uintptr_t)(p + q);
-        const uint32_t sh = (uint32_t)(a & 3u);
-        const uint32_t* ap = (const uint32_t*)(a & ~(uintptr_t)3);
+        const uint32_t sh = (uint32_t)((uintptr_t)(p + q) & 3u);
+        const uint32_t* ap = reinterpret_cast<const uint32_t*>(p + q - sh);   // pointer arithmetic: stays global
         uint32_t lo = ap[0];
         uint32_t v = lo;
         if (sh) {

@@ -338,6 +338,36 @@ def test_host_entry_from_bytes(ctx):
     assert len(st) == 0
 
 
+@pytest.mark.parametrize("permute", [False, True])
+def test_host_entry_chunks_equal_one_chunk(ctx, monkeypatch, permute):
+    """chip_stx_verify in transaction chunks (chunk j+1's blobs over PCIe beside chunk j's parse and verify):
+    status, verdict, arg and ids equal the one-chunk call and the labels, also with the blobs in shuffled
+    pool order (every chunk's byte range then overlaps the others', the copied interval grows both ways);
+    a blob outside the pool in a later chunk is CHIP_E_ARG."""
+    from corda_amd import native
+    ntx = 6000
+    tb, tm, sb, ids_ref, verdict, arg = G.cfg4_workload_commands(ntx, n_keys=32, seed=0x5EED0704, threads=8)
+    data, off, ln = G.stx_uniform(tb, sb, 2)
+    if permute:
+        p = np.random.Generator(np.random.PCG64(7)).permutation(ntx)
+        off, ln, ids_ref, verdict, arg = off[p].copy(), ln[p].copy(), ids_ref[p], verdict[p], arg[p]
+    monkeypatch.setenv("CHIP_STX_CHUNKS", "1")
+    st1, v1, a1, i1 = ctx.stx_verify(data, off, ln, tm, [[1, 4]], want_ids=True)
+    assert not st1.any() and np.array_equal(i1, ids_ref) and np.array_equal(v1, verdict) and np.array_equal(a1, arg)
+    for k in (3, 5):
+        monkeypatch.setenv("CHIP_STX_CHUNKS", str(k))
+        st, v, a, ids = ctx.stx_verify(data, off, ln, tm, [[1, 4]], want_ids=True)
+        assert np.array_equal(st, st1) and np.array_equal(v, v1) and np.array_equal(a, a1) and np.array_equal(ids, i1), k
+    bad = off.copy()
+    bad[-2] = len(data) - 3
+    monkeypatch.setenv("CHIP_STX_CHUNKS", "4")
+    with pytest.raises(native.ChipError) as e:
+        ctx.stx_verify(data, bad, ln, tm, [[1, 4]])
+    assert "outside" in str(e.value)
+    st, v, a, _ = ctx.stx_verify(data, off, ln, tm, [[1, 4]])
+    assert np.array_equal(v, v1)
+
+
 def test_two_buffer_sets_alternate(ctx):
     """The outputs of a parse stay valid across the next parse (two buffer sets): batch A is parsed,
     then batch B (on another stream), and A's parsed batch still verifies to A's labels."""

@@ -69,6 +69,9 @@
 #define F_MAC_ADD2(n) F_MAC(n) F_ADD(n) "v_xor_b32 " HN(n) ", " HN(n) ", %[z]\n\t"
 #define F_MAC_SHR(n) F_MAC(n) "v_lshrrev_b64 " WN(n) ", 1, " WN(n) "\n\t"
 #define F_CNDE(n) "v_cndmask_b32_e64 " XN(n) ", " XN(n) ", %[y], s[40:41]\n\t"
+#define F_CNDE_VCC(n) "v_cndmask_b32_e64 " XN(n) ", " XN(n) ", %[y], vcc\n\t"
+#define F_CND32_MAC(n) "v_cndmask_b32_e32 " XN(n) ", " XN(n) ", %[y], vcc\n\t" F_MAC(n) F_MAC(n) F_MAC(n)
+#define F_BFI(n) "v_bfi_b32 " XN(n) ", %[z], " XN(n) ", %[y]\n\t"
 #define F_BITOP3(n) "v_bitop3_b32 " XN(n) ", " XN(n) ", %[y], %[z] bitop3:0x96\n\t"
 #define F_OR3(n) "v_or3_b32 " XN(n) ", " XN(n) ", %[y], %[z]\n\t"
 #define F_PERM(n) "v_perm_b32 " XN(n) ", " XN(n) ", %[y], %[z]\n\t"
@@ -96,7 +99,7 @@ enum Op {
     OP_MOV_B32, OP_CNDMASK, OP_SUB_U32, OP_MUL_U32_U24, OP_MAD_U32_U24, OP_MUL_LO_U32, OP_MUL_HI_U32,
     OP_MAD_U64_U32, OP_LSHRREV_B64, OP_LSHLREV_B64, OP_LSHL_ADD_U64, OP_MOV_B64, OP_ADD_CO_U32, OP_ADD_ADDC_PAIR,
     OP_FMA_F32, OP_PK_FMA_F32, OP_MAC_ADD_11, OP_MAC_ADD_12, OP_MAC_SHIFT64_11, OP_CND_E64, OP_CND_VCCSET, OP_CMP_CND,
-    OP_BITOP3, OP_OR3, OP_PERM, OP_LSHRREV_B32, OP_MAX_U32, OP_AND_OR, OP_OR_B32, OP_ADD_SHL_11, OP_ADD_XOR_11, OP_COUNT
+    OP_BITOP3, OP_OR3, OP_PERM, OP_LSHRREV_B32, OP_MAX_U32, OP_AND_OR, OP_OR_B32, OP_ADD_SHL_11, OP_ADD_XOR_11, OP_CMP_CND_E32, OP_CND_E64_VCC, OP_CND_E32_MAC, OP_BFI, OP_COUNT
 };
 struct OpInfo {
     const char* name;
@@ -113,6 +116,8 @@ static const OpInfo kOps[OP_COUNT] = {
     {"v_cndmask_b32_e64 s-mask", 1}, {"v_cndmask_b32 vcc (set)", 1}, {"v_cmp + 8 cndmask_e64", 1},
     {"v_bitop3_b32", 1}, {"v_or3_b32", 1}, {"v_perm_b32", 1}, {"v_lshrrev_b32", 1}, {"v_max_u32", 1},
     {"v_and_or_b32", 1}, {"v_or_b32", 1}, {"add_u32 + lshlrev_b32 1:1", 2}, {"add_u32 + xor_b32 1:1", 2},
+    {"v_cmp vcc + 8 cndmask_e32", 1}, {"v_cndmask_b32_e64 vcc", 1}, {"cndmask_e32 vcc + 3 mad 1:3", 4},
+    {"v_bfi_b32", 1},
 };
 
 template <int OP>
@@ -158,6 +163,13 @@ __device__ __forceinline__ void step(uint32_t (&x)[8], uint32_t (&h)[8], uint64_
     else if constexpr (OP == OP_OR_B32) RUN(F_OR);
     else if constexpr (OP == OP_ADD_SHL_11) RUN(F_ADD_SHL);
     else if constexpr (OP == OP_ADD_XOR_11) RUN(F_ADD_XOR);
+    else if constexpr (OP == OP_CMP_CND_E32)
+        asm volatile("v_cmp_gt_u32 vcc, %[y], %[x0]\n\ts_nop 1\n\t" C8(F_CND) : OPS : INS : SCLOB, "vcc");
+    else if constexpr (OP == OP_CND_E64_VCC)
+        asm volatile("v_cmp_gt_u32 vcc, %[y], %[x0]\n\ts_nop 1\n\t" C8(F_CNDE_VCC) : OPS : INS : SCLOB, "vcc");
+    else if constexpr (OP == OP_CND_E32_MAC)
+        asm volatile("v_cmp_gt_u32 vcc, %[y], %[x0]\n\ts_nop 1\n\t" C8(F_CND32_MAC) : OPS : INS : SCLOB, "vcc");
+    else if constexpr (OP == OP_BFI) RUN(F_BFI);
 }
 
 template <int OP>
@@ -280,7 +292,7 @@ static void dep_row(const char* name, uint64_t* d, unsigned long long* st, unsig
 }
 
 int main(int argc, char** argv) {
-    const bool only_new = argc > 1 && !strcmp(argv[1], "new");
+    const bool only_new = argc > 1 && (!strcmp(argv[1], "new") || !strcmp(argv[1], "newest"));
     hipDeviceProp_t p;
     hipGetDeviceProperties(&p, 0);
     const int cus = p.multiProcessorCount;
@@ -337,6 +349,8 @@ int main(int argc, char** argv) {
     row<OP_MAC_ADD_12>(d, st, hst, cus);
     row<OP_MAC_SHIFT64_11>(d, st, hst, cus);
     }
+    const bool only_newest = argc > 1 && !strcmp(argv[1], "newest");
+    if (!only_newest) {
     row<OP_CND_E64>(d, st, hst, cus);
     row<OP_CND_VCCSET>(d, st, hst, cus);
     row<OP_CMP_CND>(d, st, hst, cus);
@@ -349,6 +363,11 @@ int main(int argc, char** argv) {
     row<OP_OR_B32>(d, st, hst, cus);
     row<OP_ADD_SHL_11>(d, st, hst, cus);
     row<OP_ADD_XOR_11>(d, st, hst, cus);
+    }
+    row<OP_CMP_CND_E32>(d, st, hst, cus);
+    row<OP_CND_E64_VCC>(d, st, hst, cus);
+    row<OP_CND_E32_MAC>(d, st, hst, cus);
+    row<OP_BFI>(d, st, hst, cus);
     if (!only_new) {
     dep_row<OP_ADD_U32>("v_add_u32", d, st, hst, cus);
     dep_row<OP_MUL_LO_U32>("v_mul_lo_u32", d, st, hst, cus);
