@@ -71,20 +71,24 @@ ECDSA_Q_MACS_PER_VERIFY = 65 * 592 + 100                            # k_ecdsa_co
 SHA256_OPS_PER_COMPRESSION = 2_168
 # HBM traffic per launch comes from the committed PMC passes of the same command (tools/profile.sh):
 # FETCH_SIZE + WRITE_SIZE (KiB) of the launch with the same grid
-PROFILE_DIR = os.path.join(ROOT, "profiles", os.environ.get("CORDA_PROFILE_DIR", "r03"))
-# VALU issue peak (MI355X_MICROARCH.md: a wave64 VALU instruction issues over 2 cycles): 256 CU x 4 SIMD x
-# 32 lanes x 2.4 GHz = 78.6e12 lane-instructions/s.  The 32x32->64 MAC (v_mad_u64_u32) has no guide figure:
-# profiles/r03/microbench_mac.txt measures it at 34.0e12 MACs/s chip-wide (8 independent chains per lane, full
-# occupancy; 31-34 T with 1-8 chains), plain 32-bit VALU (add / xor / add3) at 40-45e12 lane-ops/s, and MACs
-# mixed with plain VALU take the SUM of their issue times (no co-issue: mac_alu<K> rows).  MAC-bound rooflines
-# use the measured MAC rate; the round-2 figure (78.6 / 4 = 19.65 T, "quarter rate") was a guess below what the
-# hardware does, so round-2 fractions overstated by 1.73x.
+PROFILE_DIR = os.path.join(ROOT, "profiles", os.environ.get("CORDA_PROFILE_DIR", "r04"))
+# VALU rooflines (profiles/r04/microbench_valu*.txt, tools/microbench_valu.hip):
+#   a wave64 VALU instruction issues in 2 cycles per SIMD only for the dual-issue opcodes (v_add/sub/and/or/xor/
+#   mov/lshrrev_b32, v_bitop3_b32, v_fma_f32: 2.3-2.6 cycles measured at 2-8 waves); every other opcode —
+#   v_mad_u64_u32, mul_lo/hi, add3, lshl_add, alignbit, 64-bit shifts, add_co/addc, cndmask_e64, bfi, perm —
+#   issues in ~4.2 cycles, and a MAC does not co-issue with the simple ops.
+#   INT32_PEAK_TOPS  the guide's VALU lane-op peak: 256 CU x 4 SIMD x 64 lanes / 2 cycles x 2.4 GHz = 78.6 T
+#   MAC_SPEC_T       v_mad_u64_u32 at one per 4 cycles per SIMD and 2.4 GHz = 39.3 T (BASELINE.md's figure)
+#   MAC_MEASURED_T   the microbench's v_mad_u64_u32 rate, 8 independent chains x 8 waves per SIMD: 36.5 T at the
+#                    2.38 GHz the in-kernel clock showed; a real kernel runs at the clock its GRBM pass shows
+#                    (~2.0-2.1 GHz under the cfg2 load), so frac_measured rescales the rate to that clock
 INT32_PEAK_TOPS = 78.6
-MAC_PEAK_T = 34.0
-VALU_MEASURED_T = 45.0
-# k_ed_comb_ahalf's VALU instructions per lane besides its MACs (SQ_INSTS_VALU per wave, profiles/r02f/pmc_sq.csv:
-# 74.1k per wave - 40.7k MACs): the issue model prices them at VALU_MEASURED_T
-ED_COMB_OTHER_VALU_A = 33_400
+MAC_SPEC_T = 39.3
+MAC_PEAK_T = MAC_SPEC_T
+MAC_MEASURED_T = 36.5
+MAC_MEASURED_CLOCK_GHZ = 2.38
+VALU_MEASURED_T = 37.3          # the ~4.2-cycle opcodes at 8 waves (add3, lshl_add, alignbit, mul_lo ...)
+VALU_ISSUE_CYCLES = 4.2         # cycles per non-dual-issue VALU wave-instruction per SIMD (issue-bound kernels)
 HBM_PEAK_GBS = 8000.0
 # uniqueness: 36 B key read + 64 B slot probe + 64 B slot write per input StateRef
 UNIQ_BYTES_PER_REF = 164
@@ -209,15 +213,19 @@ def profile_traffic(kernel, grid):
     return tot
 
 
-def profile_valu_lane_instrs(kernel, grid):
-    """VALU lane-instructions of one launch (SQ_INSTS_VALU x 64) from the committed SQ pass, or None."""
+def profile_issue(kernel, grid):
+    """The issue-model row of `kernel` with `grid` threads (tools/issue_summary.py over the committed
+    SQ_INSTS_VALU + GRBM_GUI_ACTIVE pass): duration, VALU wave-instructions per launch, effective clock,
+    cycles per VALU instruction per SIMD; or None."""
     import csv
-    path = os.path.join(PROFILE_DIR, "pmc_sq.csv")
+    path = os.path.join(PROFILE_DIR, "issue_model.csv")
     if not os.path.exists(path):
         return None
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(path))
-            if kernel_base(r["Kernel_Name"]) == kernel and int(r["Grid_Size"]) == grid and r["Counter_Name"] == "SQ_INSTS_VALU"]
-    return sum(vals) / len(vals) * 64.0 if vals else None
+    for r in csv.DictReader(open(path)):
+        if r["Kernel_Name"] == kernel and int(r["Grid_Size"]) == grid:
+            return {"duration_ms": float(r["Duration_ms"]), "valu_per_launch": float(r["VALU_per_launch"]),
+                    "eff_clock_ghz": float(r["Eff_clock_GHz"]), "cyc_per_valu": float(r["Cyc_per_VALU_per_SIMD"])}
+    return None
 
 
 def stx_traffic(grid_tx, grid_sig):
@@ -355,6 +363,7 @@ def main():
     achieved = ED_COMB_MACS_A * n_comb / (a_ms * 1e-3) / 1e12
     comb_grid = (((n + 255) // 256 + 7) & ~7) * 256
     traffic = profile_traffic("k_ed_comb_ahalf", comb_grid)
+    ahalf_issue = profile_issue("k_ed_comb_ahalf", comb_grid)
     del db, status, bitmap, gathered
 
     secondary = {}
@@ -454,10 +463,10 @@ def main():
             "txid_roofline_note": "canonical %d int32 ops per SHA-256 compression x %d compressions/tx vs the %.1f T "
                                   "VALU lane-op peak" % (SHA256_OPS_PER_COMPRESSION, comp_per_tx, INT32_PEAK_TOPS),
             "txid_traffic": profile_traffic("k_txid", (tb.ntx + 63) // 64 * 64),   # TX_BLOCK 64
-            # the instructions it issues (SQ_INSTS_VALU of the committed profile; fused add3 / lshl_add
-            # instructions do two canonical ops) against the measured 32-bit VALU issue rate
-            "txid_issue_frac": (lambda vi: vi / (tx_ms * 1e-3) / 1e12 / VALU_MEASURED_T if vi else None)(
-                profile_valu_lane_instrs("k_txid", (tb.ntx + 63) // 64 * 64)),
+            # the instructions it issues (SQ_INSTS_VALU of the committed profile; fused add3 / bitop3 / alignbit
+            # instructions do two or three canonical ops) and the cycles each took per SIMD at the profiled clock
+            # (2.3-2.6 = dual-issue bound, ~4.2 = single-issue bound, more = waiting on memory / dependencies)
+            "txid_issue": profile_issue("k_txid", (tb.ntx + 63) // 64 * 64),
             "txid_algorithmic_bytes": int(tb.data.nbytes + tb.salts.nbytes + 32 * tb.ntx + 20 * len(tb.comp_len)),
         })
         # fused: ids -> SignableData messages -> 2 signers per tx -> required signers (verifySignaturesExcept)
@@ -764,24 +773,38 @@ def main():
                        "sigs_per_gpu": n, "keys": args.keys, "msg_len": 200, "corrupt": 0.10,
                        "parallelism": "dp%d (batch sharded by transaction, RCCL bitmap all-gather)" % world},
             "correct_vs_labels": correct,
-            "roofline": {"bound": "valu", "achieved": achieved, "peak": MAC_PEAK_T,
-                         "unit": "T MAC/s (v_mad_u64_u32 32x32->64)", "frac": achieved / MAC_PEAK_T,
+            "roofline": {"bound": "valu", "achieved": achieved, "peak": MAC_SPEC_T,
+                         "unit": "T MAC/s (v_mad_u64_u32 32x32->64)", "frac": achieved / MAC_SPEC_T,
                          "traffic": traffic,
                          "traffic_note": "FETCH_SIZE+WRITE_SIZE bytes per launch, %s (same grid); vs ~%d B/sig "
                                          "algorithmic (h 32 + [S]B 160 in, key table entries read from L2, R' 120 out)"
                                          % (os.path.relpath(PROFILE_DIR, ROOT), 312),
-                         "peak_note": "v_mad_u64_u32 issue rate measured by tools/microbench_mac.hip "
-                                      "(profiles/r03/microbench_mac.txt); no co-issue with other VALU",
-                         "issue_model": {"macs_per_unit": ED_COMB_MACS_A, "other_valu_per_unit": ED_COMB_OTHER_VALU_A,
-                                         "predicted_ms": n_comb * (ED_COMB_MACS_A / (MAC_PEAK_T * 1e12) +
-                                                                   ED_COMB_OTHER_VALU_A / (VALU_MEASURED_T * 1e12)) * 1e3,
-                                         "frac": n_comb * (ED_COMB_MACS_A / (MAC_PEAK_T * 1e12) +
-                                                           ED_COMB_OTHER_VALU_A / (VALU_MEASURED_T * 1e12)) * 1e3 / a_ms,
-                                         "note": "the MACs and the other VALU instructions issue from one port: "
-                                                 "time >= MACs / 34 T + other / 45 T (measured rates)"},
+                         "peak_note": "v_mad_u64_u32 issues once per 4 cycles per SIMD: 256 CU x 4 SIMD x 64 lanes "
+                                      "/ 4 x 2.4 GHz = 39.3 T; frac_spec_dual_issue prices against the guide's 78.6 T "
+                                      "VALU lane-op peak (2-cycle issue, which only the simple 32-bit opcodes reach); "
+                                      "frac_measured against the microbench MAC rate (36.5 T at 2.38 GHz) rescaled to "
+                                      "the kernel's own clock from its GRBM_GUI_ACTIVE pass",
+                         "frac_spec_dual_issue": achieved / INT32_PEAK_TOPS,
+                         "frac_measured": (achieved / (MAC_MEASURED_T * ahalf_issue["eff_clock_ghz"] /
+                                                       MAC_MEASURED_CLOCK_GHZ)) if ahalf_issue else None,
+                         "effective_clock_ghz": ahalf_issue["eff_clock_ghz"] if ahalf_issue else None,
+                         "issue_model": ({
+                             "valu_instr_per_sig": ahalf_issue["valu_per_launch"] * 64 / comb_grid,
+                             "macs_per_sig": ED_COMB_MACS_A,
+                             "cyc_per_valu_profiled": ahalf_issue["cyc_per_valu"],
+                             "predicted_ms": ahalf_issue["valu_per_launch"] / 1024 * VALU_ISSUE_CYCLES /
+                                             (ahalf_issue["eff_clock_ghz"] * 1e6),
+                             "frac": ahalf_issue["valu_per_launch"] / 1024 * VALU_ISSUE_CYCLES /
+                                     (ahalf_issue["eff_clock_ghz"] * 1e6) / a_ms,
+                             "note": "time >= VALU wave-instructions / 1024 SIMDs x %.1f cycles / effective clock "
+                                     "(SQ_INSTS_VALU and GRBM_GUI_ACTIVE of the committed pass, tools/"
+                                     "issue_summary.py); the MACs are %.0f%% of the instructions, the rest are "
+                                     "carries, reductions, table selects and loads' address arithmetic"
+                                     % (VALU_ISSUE_CYCLES, 100.0 * ED_COMB_MACS_A * comb_grid / 64 /
+                                        ahalf_issue["valu_per_launch"])} if ahalf_issue else None),
                          "kernel": "k_ed_comb_ahalf", "kernel_ms": a_ms,
                          "units_per_launch": n_comb, "macs_per_unit": ED_COMB_MACS_A,
-                         "both_halves_frac": ED_COMB_MACS_PER_VERIFY * n_comb / ((a_ms + b_ms) * 1e-3) / 1e12 / MAC_PEAK_T,
+                         "both_halves_frac": ED_COMB_MACS_PER_VERIFY * n_comb / ((a_ms + b_ms) * 1e-3) / 1e12 / MAC_SPEC_T,
                          "comb_share_of_step": (a_ms + b_ms) / ms_per_step,
                          "pipeline_ms": {"keyprep": kp_ms, "comb_plan": plan_ms, "comb_tables_aux_stream": tab_ms,
                                          "comb_bhalf": b_ms, "comb_ahalf": a_ms, "comb_finish": fin_ms,

@@ -1,8 +1,9 @@
 // fe25519_dev.hpp — GF(2^255-19) arithmetic and Ed25519 group operations for gfx950.
 //
 // Representation: ten unsigned 32-bit limbs, radix 2^25.5 (even limbs 26 bits, odd 25 bits).
-// Products are 32x32->64 multiply-accumulates (v_mad_u64_u32, quarter rate on MI355X: 18.0e12 MAC/s
-// measured by tools/microbench_mul.hip vs the 78.6e12 VALU lane-op peak), column sums stay below 2^63 under these bounds:
+// Products are 32x32->64 multiply-accumulates (v_mad_u64_u32: one per ~4.2 cycles per SIMD, 36.5e12 MAC/s at
+// 2.38 GHz measured by tools/microbench_valu.hip, profiles/r04/microbench_valu_a.txt; it does not co-issue
+// with the dual-issue 32-bit ops), column sums stay below 2^63 under these bounds:
 //   "carried" limb : even < 2^26, odd < 2^25 (+2^17 on limb 1)   — every mul/sq output
 //   "loose"   limb : even < 3*2^26, odd < 3*2^25                 — carried + carried or
 //                                                                   carried + 2p - carried

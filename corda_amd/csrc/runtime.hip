@@ -1450,6 +1450,14 @@ int chip_stx_parse_device(chip_ctx* c, const chip_stx_blobs* in, uint8_t* tx_sta
     return stx_parse(c, B, in, tx_status, out, stream ? (hipStream_t)stream : c->stream);
 }
 
+// a chunk's CHIP_TXV_SIGNATURE verdicts name a signature of the chunk's own parsed batch: + the signatures of the
+// chunks before it, so the arg is the one-call value (the index in the whole batch's signature list)
+__global__ void __launch_bounds__(256) k_arg_sig_offset(uint64_t m, const uint8_t* __restrict__ verdict,
+                                                        uint32_t* __restrict__ arg, uint32_t off) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < m && verdict[t] == CHIP_TXV_SIGNATURE) arg[t] += off;
+}
+
 // one chunk of a host blob batch: (offset, length) inside the pool (flag), and the byte range [min off,
 // max off + len) the chunk reads; out as k_chunk_init leaves it ([0] flags, [1] min, [2] max)
 __global__ void __launch_bounds__(256) k_blob_range(uint64_t m, const uint64_t* __restrict__ off,
@@ -1529,6 +1537,7 @@ static int stx_verify_host_pipelined(chip_ctx* c, uint64_t n, const uint8_t* dat
         return CHIP_OK;
     };
     int r;
+    uint64_t sig_base = 0;   // signatures of the chunks before this one
     if ((r = stage_chunk(0))) return r;
     for (uint64_t j = 0; j + 1 < at.size(); j++) {
         const uint64_t a = at[j], m = at[j + 1] - a;
@@ -1550,6 +1559,10 @@ static int stx_verify_host_pipelined(chip_ctx* c, uint64_t n, const uint8_t* dat
                                                     c->h2_sigst.as<uint8_t>(), c->h2_v.as<uint8_t>() + a,
                                                     c->h2_a.as<uint32_t>() + a, c->h2_miss.as<uint8_t>(), st)))
             return r;
+        if (sig_base && m)
+            hipLaunchKernelGGL(k_arg_sig_offset, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, st, m,
+                               c->h2_v.as<uint8_t>() + a, c->h2_a.as<uint32_t>() + a, (uint32_t)sig_base);
+        sig_base += p.sigs.n;
     }
     HIPCHK(c, hipMemcpyAsync(tx_status, c->h2_st.p, n, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipMemcpyAsync(verdict, c->h2_v.p, n, hipMemcpyDeviceToHost, st));
@@ -1705,12 +1718,123 @@ static int check_tx_batch(chip_ctx* c, const chip_tx_batch* b, hipStream_t st) {
     return CHIP_OK;
 }
 
+// chip_txid_batch over a host batch in transaction chunks: chunk j+1's salts, start slice, component arrays and
+// component bytes go over PCIe on hcs (each checked there: starts nondecreasing inside the component range, the
+// first chunk from 0, components inside the pool) while chunk j's ids are computed on the main stream.  Every array
+// lands at its own offsets, so the device kernel reads the caller's absolute indices and offsets.
+static int txid_host_pipelined(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids, uint64_t chunks) {
+    const uint64_t ntx = b->ntx, nc = b->ncomp;
+    hipStream_t st = c->stream, cs = c->hcs;
+    HIPCHK(c, c->t_salts.ensure(ntx * 32 + 16));
+    HIPCHK(c, c->t_start.ensure((ntx + 1) * 8 + 16));
+    HIPCHK(c, c->t_group.ensure(nc * 4 + 16));
+    HIPCHK(c, c->t_internal.ensure(nc * 4 + 16));
+    HIPCHK(c, c->t_off.ensure(nc * 8 + 16));
+    HIPCHK(c, c->t_len.ensure(nc * 4 + 16));
+    HIPCHK(c, c->t_data.ensure(b->data_bytes + 16));
+    HIPCHK(c, c->t_ids.ensure(ntx * 32 + 16));
+    HIPCHK(c, c->h_rngd.ensure(64));
+    std::vector<uint64_t> at{0};
+    for (uint64_t k = 1; k <= chunks; k++) at.push_back(std::min(ntx, (ntx * k + chunks - 1) / chunks));
+    HIPCHK(c, hipEventRecord(c->hev_p, st));
+    HIPCHK(c, hipStreamWaitEvent(cs, c->hev_p, 0));
+    uint64_t clo = 0, chi = 0;
+    bool any = false;
+    auto copy = [&](uint64_t lo, uint64_t hi) -> int {   // the copied part of the pool grows as one interval
+        if (lo >= hi) return CHIP_OK;
+        uint8_t* dst = c->t_data.as<uint8_t>();
+        if (!any) {
+            HIPCHK(c, hipMemcpyAsync(dst + lo, b->data + lo, hi - lo, hipMemcpyHostToDevice, cs));
+            clo = lo, chi = hi, any = true;
+            return CHIP_OK;
+        }
+        if (lo < clo) {
+            HIPCHK(c, hipMemcpyAsync(dst + lo, b->data + lo, clo - lo, hipMemcpyHostToDevice, cs));
+            clo = lo;
+        }
+        if (hi > chi) {
+            HIPCHK(c, hipMemcpyAsync(dst + chi, b->data + chi, hi - chi, hipMemcpyHostToDevice, cs));
+            chi = hi;
+        }
+        return CHIP_OK;
+    };
+    auto stage_chunk = [&](uint64_t j) -> int {
+        const uint64_t a = at[j], e = at[j + 1], m = e - a;
+        // the chunk's component range from its first and last start (checked on the host before it slices
+        // anything; the device check below covers the starts in between)
+        const uint64_t c0 = b->tx_comp_start[a], c1 = b->tx_comp_start[e];
+        if (c0 > c1 || c1 > nc || (j == 0 && c0 != 0))
+            return fail(c, CHIP_E_ARG, "tx_comp_start not monotone / out of range");
+        HIPCHK(c, hipMemcpyAsync(c->t_salts.as<uint8_t>() + 32 * a, b->salts + 32 * a, m * 32, hipMemcpyHostToDevice, cs));
+        HIPCHK(c, hipMemcpyAsync(c->t_start.as<uint64_t>() + a, b->tx_comp_start + a, (m + 1) * 8, hipMemcpyHostToDevice, cs));
+        const uint64_t k = c1 - c0;
+        if (k) {
+            HIPCHK(c, hipMemcpyAsync(c->t_group.as<uint32_t>() + c0, b->comp_group + c0, k * 4, hipMemcpyHostToDevice, cs));
+            HIPCHK(c, hipMemcpyAsync(c->t_internal.as<uint32_t>() + c0, b->comp_internal + c0, k * 4, hipMemcpyHostToDevice, cs));
+            HIPCHK(c, hipMemcpyAsync(c->t_off.as<uint64_t>() + c0, b->comp_off + c0, k * 8, hipMemcpyHostToDevice, cs));
+            HIPCHK(c, hipMemcpyAsync(c->t_len.as<uint32_t>() + c0, b->comp_len + c0, k * 4, hipMemcpyHostToDevice, cs));
+        }
+        const DevCheck chk[] = {{DEV_CHECK_MONOTONE, 1, c->t_start.as<uint64_t>() + a, nullptr, nullptr, m, c1, c0}};
+        uint32_t bad = 0;
+        if (int rc = dev_check(c, chk, 1, cs, &bad)) return rc;
+        if (bad & 1) return fail(c, CHIP_E_ARG, "tx_comp_start not monotone / out of range");
+        unsigned long long* out = c->h_rngd.as<unsigned long long>();
+        hipLaunchKernelGGL(k_chunk_init, dim3(1), dim3(64), 0, cs, out);
+        if (k)
+            hipLaunchKernelGGL(k_blob_range, dim3((uint32_t)((k + 255) / 256)), dim3(256), 0, cs, k,
+                               c->t_off.as<uint64_t>() + c0, c->t_len.as<uint32_t>() + c0, b->data_bytes, out);
+        HIPCHK(c, hipGetLastError());
+        HIPCHK(c, hipMemcpyAsync(c->h_rng, out, 64, hipMemcpyDeviceToHost, cs));
+        HIPCHK(c, hipStreamSynchronize(cs));
+        const unsigned long long* q = c->h_rng;
+        if (q[0]) return fail(c, CHIP_E_ARG, "component outside data pool");
+        if (int rc = copy(q[1] == ~0ull ? 0 : q[1], q[2])) return rc;
+        HIPCHK(c, hipEventRecord(c->hev_p, cs));
+        return CHIP_OK;
+    };
+    int r;
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    HIPCHK(c, hipSetDevice(c->device));
+    if ((r = stage_chunk(0))) return r;
+    for (uint64_t j = 0; j + 1 < at.size(); j++) {
+        const uint64_t a = at[j], m = at[j + 1] - a;
+        HIPCHK(c, hipStreamWaitEvent(st, c->hev_p, 0));
+        if (j + 2 < at.size() && (r = stage_chunk(j + 1))) {
+            hipStreamSynchronize(st);
+            return r;
+        }
+        chip_tx_batch d = *b;
+        d.ntx = m;
+        d.salts = c->t_salts.as<uint8_t>() + 32 * a;
+        d.tx_comp_start = c->t_start.as<uint64_t>() + a;
+        d.comp_group = c->t_group.as<uint32_t>();
+        d.comp_internal = c->t_internal.as<uint32_t>();
+        d.data = c->t_data.as<uint8_t>();
+        d.comp_off = c->t_off.as<uint64_t>();
+        d.comp_len = c->t_len.as<uint32_t>();
+        if ((r = txid_device_locked(c, &d, c->t_ids.as<uint8_t>() + 32 * a, st))) return r;
+    }
+    if (ntx) HIPCHK(c, hipMemcpyAsync(ids, c->t_ids.p, ntx * 32, hipMemcpyDeviceToHost, st));
+    HIPCHK(c, hipStreamSynchronize(st));
+    c->tev_pending = false;
+    return CHIP_OK;
+}
+
+// transaction chunks of chip_txid_batch: 1 below 2^18 transactions, else about 2^18 a chunk, at most 8
+// (CHIP_TXID_CHUNKS overrides)
+static uint64_t txid_host_chunks(uint64_t n) {
+    uint64_t k = n >= (1ull << 18) ? std::min<uint64_t>(8, (n + (1ull << 17)) >> 18) : 1;
+    if (const char* e = getenv("CHIP_TXID_CHUNKS")) k = std::max<uint64_t>(1, std::min<uint64_t>(64, strtoull(e, nullptr, 10)));
+    return std::min<uint64_t>(k, std::max<uint64_t>(1, n));
+}
+
 int chip_txid_batch(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids) {
     if (!c || !b) return fail(c, CHIP_E_ARG, "null argument");
     const uint64_t ntx = b->ntx, nc = b->ncomp;
     if (ntx && (!b->salts || !b->tx_comp_start || !ids)) return fail(c, CHIP_E_ARG, "null tx array");
     if (nc && (!b->comp_group || !b->comp_internal || !b->comp_off || !b->comp_len || !b->data))
         return fail(c, CHIP_E_ARG, "null component array");
+    if (const uint64_t k = txid_host_chunks(ntx); k > 1) return txid_host_pipelined(c, b, ids, k);
     hipStream_t st = c->stream;
     int r;
     {
