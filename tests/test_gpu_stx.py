@@ -351,7 +351,14 @@ def test_host_entry_chunks_equal_one_chunk(ctx, monkeypatch, permute):
     data, off, ln = G.stx_uniform(tb, sb, 2)
     if permute:
         p = np.random.Generator(np.random.PCG64(7)).permutation(ntx)
-        off, ln, ids_ref, verdict, arg = off[p].copy(), ln[p].copy(), ids_ref[p], verdict[p], arg[p]
+        # a SIGNATURE verdict's arg indexes the batch's signature list, which the permutation reorders
+        cnt = np.bincount(sb.tx_idx, minlength=ntx).astype(np.int64)
+        base = np.concatenate([[0], np.cumsum(cnt)])[:-1]
+        pbase = np.concatenate([[0], np.cumsum(cnt[p])])[:-1]
+        sig = verdict[p] == native.TXV_SIGNATURE
+        arg = arg[p].astype(np.int64)
+        arg[sig] += pbase[sig] - base[p][sig]
+        off, ln, ids_ref, verdict, arg = off[p].copy(), ln[p].copy(), ids_ref[p], verdict[p], arg.astype(np.uint32)
     monkeypatch.setenv("CHIP_STX_CHUNKS", "1")
     st1, v1, a1, i1 = ctx.stx_verify(data, off, ln, tm, [[1, 4]], want_ids=True)
     assert not st1.any() and np.array_equal(i1, ids_ref) and np.array_equal(v1, verdict) and np.array_equal(a1, arg)
