@@ -51,11 +51,11 @@ def progress(msg):
 #   Ed25519 comb, radix 2^25.5 (100 limb products per GF(2^255-19) multiplication):
 #     k_ed_comb_bhalf: [S]B from the radix-2^16 fixed-base comb: 16 Niels adds (3 mults) + 15
 #                      conversions (4) + 1 final conversion (4) = 112 mults (+ SHA-512, not counted)
-#     k_ed_comb_ahalf: [h](-A) from the per-key radix-32 comb: 51 cached adds (4 mults) + 50
-#                      conversions (4) + 3 final = 407 mults
+#     k_ed_comb_ahalf: [h](-A) from the per-key radix-64 comb (ED_COMB_W = 6): 43 cached adds (4 mults) +
+#                      42 conversions (4) + 3 final = 343 mults
 ED_COMB_MACS_B = 11_200
-ED_COMB_MACS_A = 40_700
-ED_COMB_MACS_PER_VERIFY = ED_COMB_MACS_A + ED_COMB_MACS_B          # 51,900
+ED_COMB_MACS_A = 34_300
+ED_COMB_MACS_PER_VERIFY = ED_COMB_MACS_A + ED_COMB_MACS_B          # 45,500
 #   Ed25519 windowed Straus (k_ed25519_verify): 252 doublings (4 squarings each) + the encode
 #   inversion (254 squarings) = 1,262 squarings x 55 limb products, and 1,504 multiplications x 100
 #   (doubling-chain conversions 819, 64 cached A-adds 256 + conversions 192, 32 B-madds 224, 11 + 2

@@ -12,13 +12,13 @@
 //             (the multiples, one lane per key x window);
 //   [S]B    = sum_w e_w (2^(16 w) B),    e_w the signed radix-2^16 digits of S, read from the fixed
 //             table built per context by k_ed_bcomb16_build (16 x 32,769 affine Niels rows, 67 MB).
-// 51 + 16 additions per signature (~520 field multiplications) instead of 252 doublings + 96
+// 43 + 16 additions per signature (W = 6: ~460 field multiplications) instead of 252 doublings + 96
 // additions (2,766).  The projective R' is inverted in batches of ED_FIN_G by k_ed_comb_finish
 // (Montgomery's trick: ~21 instead of 265 multiplications per signature).
 //
 // Work list: k_ed_comb_partition groups the signatures of one key contiguously (counting sort on
-// the key index), and k_ed_comb_verify maps consecutive blocks of the list onto one XCD, so a key's
-// 92 KB table is read from one XCD's L2.  Keys with fewer than min_sigs signatures (or beyond the
+// the key index), and k_ed_comb_ahalf maps consecutive blocks of the list onto one XCD, so a key's
+// 227 KB table (W = 6) is read through one XCD's L2.  Keys with fewer than min_sigs signatures (or beyond the
 // table budget) keep the Straus kernel.
 #include "ed_common_dev.hpp"
 #include "runtime.hpp"
@@ -153,7 +153,7 @@ __global__ void __launch_bounds__(64) k_ed_comb_chain(const uint32_t* __restrict
     ed_load_p3(P, nega + (uint64_t)k * 40);
     uint32_t* tab = ctab + (uint64_t)s * ED_COMB_KEY_WORDS;
     for (int w = 0; w < ED_COMB_AWIN; w++) {
-        ed_store_p3(tab + ((uint32_t)w * ED_COMB_AENT + 1) * 40, P);
+        ed_store_p3(tab + ((uint32_t)w * ED_COMB_AENT + 1) * ED_COMB_ROW, P);   // 40 words from row 1 on
         if (w + 1 == ED_COMB_AWIN) break;
         ge_p2 r;
         ge_p3_to_p2(r, P);
@@ -182,6 +182,7 @@ CHIP_DEV void ed_store_row(uint32_t* __restrict__ dst, const ge_cached& c) {
         dst[30 + i] = c.T2d.v[i];
     }
 }
+#if !ED_COMB_AFFINE
 __global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict__ ctr, uint32_t max_slots,
                                                       uint32_t eager, const KeyMeta* __restrict__ meta,
                                                       uint32_t* __restrict__ ctab) {
@@ -189,7 +190,7 @@ __global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict
     const uint32_t s = g / ED_COMB_AWIN, w = g % ED_COMB_AWIN;
     if (s >= (eager ? max_slots : ctr[ED_CTR_NSLOTS])) return;
     if (eager && !ed_key_ok(meta, s)) return;
-    uint32_t* e = ctab + (uint64_t)s * ED_COMB_KEY_WORDS + (uint64_t)w * ED_COMB_AENT * 40;
+    uint32_t* e = ctab + (uint64_t)s * ED_COMB_KEY_WORDS + (uint64_t)w * ED_COMB_AENT * ED_COMB_ROW;
     ge_p3 P;
     ed_load_p3(P, e + 40);   // P_w, stashed in row +1 by the chain
     ge_cached c1, c;
@@ -209,6 +210,129 @@ __global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict
         ed_store_row(e + 40 * j, c);
     }
 }
+#else
+// Affine rows in three steps (one lane per key x window in a and b):
+//   a: j P_w for j = 1..2^(W-1) by additions; row j holds (X_j Z_1..Z_{j-1}, Y_j Z_1..Z_{j-1}, Z_j), so that step
+//      b needs no prefix array: with inv = 1 / (Z_1..Z_j), x_j = row.X inv and the next inv = inv Z_j;
+//      fz[lane] = Z_1..Z_{2^(W-1)}
+//   zinv: one lane per ED_COMB_ZG fill lanes inverts their products together (Montgomery's trick again:
+//      one inversion per group instead of per lane; a serial latency on the second stream)
+//   b: rows to affine Niels [y+x, y-x, 2dxy], row 0 the identity [1, 1, 0]
+CHIP_DEV bool ed_fill_lane(uint32_t g, const uint32_t* __restrict__ ctr, uint32_t max_slots, uint32_t eager,
+                           const KeyMeta* __restrict__ meta, uint32_t& s, uint32_t& w, bool& skip) {
+    s = g / ED_COMB_AWIN;
+    w = g % ED_COMB_AWIN;
+    if (s >= (eager ? max_slots : ctr[ED_CTR_NSLOTS])) return false;
+    skip = eager && !ed_key_ok(meta, s);
+    return true;
+}
+CHIP_DEV void ed_store_fe(uint32_t* __restrict__ dst, const fe& f) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) dst[i] = f.v[i];
+}
+CHIP_DEV void ed_load_fe(fe& f, const uint32_t* __restrict__ src) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) f.v[i] = src[i];
+}
+__global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict__ ctr, uint32_t max_slots,
+                                                      uint32_t eager, const KeyMeta* __restrict__ meta,
+                                                      uint32_t* __restrict__ ctab, uint32_t* __restrict__ fz) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t s, w;
+    bool skip = false;
+    if (!ed_fill_lane(g, ctr, max_slots, eager, meta, s, w, skip)) return;
+    fe acc;
+    fe_1(acc);
+    if (!skip) {
+        uint32_t* e = ctab + (uint64_t)s * ED_COMB_KEY_WORDS + (uint64_t)w * ED_COMB_AENT * ED_COMB_ROW;
+        ge_p3 P;
+        ed_load_p3(P, e + ED_COMB_ROW);   // P_w, stashed from row 1 on by the chain
+        ge_cached c1;
+        ge_p3_to_cached(c1, P);
+        ge_p3 Q = P;
+        ge_p1p1 t;
+        for (int j = 1; j < ED_COMB_AENT; j++) {
+            uint32_t* r = e + j * ED_COMB_ROW;
+            if (j == 1) {
+                ed_store_fe(r, Q.X);
+                ed_store_fe(r + 10, Q.Y);
+                acc = Q.Z;
+            } else {
+                fe x, y;
+                fe_mul(x, Q.X, acc);
+                fe_mul(y, Q.Y, acc);
+                ed_store_fe(r, x);
+                ed_store_fe(r + 10, y);
+                fe_mul(acc, acc, Q.Z);
+            }
+            ed_store_fe(r + 20, Q.Z);
+            if (j + 1 < ED_COMB_AENT) {
+                ge_add_cached(t, Q, c1, false);
+                ge_p1p1_to_p3(Q, t);
+            }
+        }
+    }
+    ed_store_fe(fz + (uint64_t)g * 10, acc);   // 1 for a skipped lane
+}
+__global__ void __launch_bounds__(64) k_ed_comb_zinv(const uint32_t* __restrict__ ctr, uint32_t max_slots, uint32_t eager,
+                                                     const uint32_t* __restrict__ zprod, uint32_t* __restrict__ zinv) {
+    const uint32_t nl = (eager ? max_slots : ctr[ED_CTR_NSLOTS]) * ED_COMB_AWIN;
+    const uint32_t g0 = (blockIdx.x * blockDim.x + threadIdx.x) * ED_COMB_ZG;
+    if (g0 >= nl) return;
+    const uint32_t m = min((uint32_t)ED_COMB_ZG, nl - g0);
+    fe acc, z, inv, t;
+    fe_1(acc);
+    for (uint32_t i = 0; i < m; i++) {   // zinv[i] = the product of the group's values before i
+        ed_store_fe(zinv + (uint64_t)(g0 + i) * 10, acc);
+        ed_load_fe(z, zprod + (uint64_t)(g0 + i) * 10);
+        fe_mul(acc, acc, z);
+    }
+    fe_invert(inv, acc);
+    for (uint32_t i = m; i-- > 0;) {
+        ed_load_fe(t, zinv + (uint64_t)(g0 + i) * 10);
+        ed_load_fe(z, zprod + (uint64_t)(g0 + i) * 10);
+        fe_mul(t, inv, t);
+        fe_mul(inv, inv, z);
+        ed_store_fe(zinv + (uint64_t)(g0 + i) * 10, t);
+    }
+}
+__global__ void __launch_bounds__(256) k_ed_comb_fill_b(const uint32_t* __restrict__ ctr, uint32_t max_slots,
+                                                        uint32_t eager, const KeyMeta* __restrict__ meta,
+                                                        uint32_t* __restrict__ ctab, const uint32_t* __restrict__ zinv) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    uint32_t s, w;
+    bool skip = false;
+    if (!ed_fill_lane(g, ctr, max_slots, eager, meta, s, w, skip) || skip) return;
+    uint32_t* e = ctab + (uint64_t)s * ED_COMB_KEY_WORDS + (uint64_t)w * ED_COMB_AENT * ED_COMB_ROW;
+    fe inv, d2;
+    ed_load_fe(inv, zinv + (uint64_t)g * 10);
+    fe_from_c(d2, ED_D2);
+    for (int j = ED_COMB_AENT - 1; j >= 1; j--) {
+        uint32_t* r = e + j * ED_COMB_ROW;
+        fe X, Y, Z, x, y, xy;
+        ed_load_fe(X, r);
+        ed_load_fe(Y, r + 10);
+        ed_load_fe(Z, r + 20);
+        fe_mul(x, X, inv);
+        fe_mul(y, Y, inv);
+        fe_mul(inv, inv, Z);
+        ge_niels n;
+        fe_add(n.ypx, y, x);
+        fe_carry(n.ypx);
+        fe_sub(n.ymx, y, x);
+        fe_carry(n.ymx);
+        fe_mul(xy, x, y);
+        fe_mul(n.xy2d, xy, d2);
+        ed_store_fe(r, n.ypx);
+        ed_store_fe(r + 10, n.ymx);
+        ed_store_fe(r + 20, n.xy2d);
+        r[30] = 0;
+        r[31] = 0;
+    }
+#pragma unroll
+    for (int i = 0; i < ED_COMB_ROW; i++) e[i] = (i == 0 || i == 10) ? 1u : 0u;   // identity
+}
+#endif
 
 // ---- verify: one lane per comb-list position ----
 // blocks b, b+8, b+16, ... are dispatched to one XCD: give them consecutive work.  `used` = blocks
@@ -468,21 +592,44 @@ __global__ void __launch_bounds__(256, ED_AHALF_MINW) k_ed_comb_ahalf(const uint
     // + [h](-A): one addition per window from the key's signed-multiple rows (extended coordinates, unified =
     // complete formulas); window 0 peeled so the loop carries only the completed point t
     uint32_t cur = bmid[(uint64_t)40 * cap + p];
-    ge_cached ca;
     ge_p1p1 t;
+#if ED_COMB_AFFINE
+    // affine Niels rows: a mixed addition (3 multiplications) after a conversion that yields 2Z directly
+    fe qp, qm, xy2d, z2;
     {
         const int d = (int)(cur & 0xffu) - ED_COMB_ABIAS;
-        ed_load_row_signed(ca, tab + (uint32_t)(d < 0 ? -d : d) * 40, d < 0);
+        ed_load_niels_signed(qp, qm, xy2d, tab + (uint32_t)(d < 0 ? -d : d) * ED_COMB_ROW, d < 0);
+        fe_add(z2, u.Z, u.Z);
+        fe_carry(z2);   // the madd's 2Z - C needs a carried 2Z (fe_mul2 yields one in the loop)
+        ge_madd_signed(t, u, z2, qp, qm, xy2d, (uint32_t)(d >> 31));
+    }
+#pragma unroll 1
+    for (uint32_t w = 1; w < ED_COMB_AWIN; w++) {
+        if ((w & 3u) == 0) cur = bmid[(uint64_t)(40 + (w >> 2)) * cap + p];
+        const int d = (int)((cur >> (8 * (w & 3u))) & 0xffu) - ED_COMB_ABIAS;
+        fe_mul(u.X, t.X, t.T);
+        fe_mul(u.Y, t.Z, t.Y);
+        fe_mul2(z2, t.Z, t.T);
+        fe_mul(u.T, t.X, t.Y);
+        ed_load_niels_signed(qp, qm, xy2d, tab + (w * ED_COMB_AENT + (uint32_t)(d < 0 ? -d : d)) * ED_COMB_ROW, d < 0);
+        ge_madd_signed(t, u, z2, qp, qm, xy2d, (uint32_t)(d >> 31));
+    }
+#else
+    ge_cached ca;
+    {
+        const int d = (int)(cur & 0xffu) - ED_COMB_ABIAS;
+        ed_load_row_signed(ca, tab + (uint32_t)(d < 0 ? -d : d) * ED_COMB_ROW, d < 0);
         ge_add_row(t, u, ca, (uint32_t)(d >> 31));
     }
 #pragma unroll 1
     for (uint32_t w = 1; w < ED_COMB_AWIN; w++) {
         if ((w & 3u) == 0) cur = bmid[(uint64_t)(40 + (w >> 2)) * cap + p];
         const int d = (int)((cur >> (8 * (w & 3u))) & 0xffu) - ED_COMB_ABIAS;
-        ed_load_row_signed(ca, tab + (w * ED_COMB_AENT + (uint32_t)(d < 0 ? -d : d)) * 40, d < 0);
+        ed_load_row_signed(ca, tab + (w * ED_COMB_AENT + (uint32_t)(d < 0 ? -d : d)) * ED_COMB_ROW, d < 0);
         ge_p1p1_to_p3(u, t);
         ge_add_row(t, u, ca, (uint32_t)(d >> 31));
     }
+#endif
     // projective R' = (X : Y : Z), stored structure-of-arrays for the finish kernel
     fe X, Y, Z;
     fe_mul(X, t.X, t.T);
@@ -575,8 +722,20 @@ void launch_ed_comb_build(hipStream_t st, uint64_t n, uint64_t n_keys, const Key
     if (!n || !n_keys || !w.max_slots) return;
     hipLaunchKernelGGL(k_ed_comb_chain, dim3(nblk(w.max_slots, 64)), dim3(64), 0, st, w.ctr, w.max_slots, w.eager, meta,
                        w.slot_key, w.nega, w.ctab);
+#if !ED_COMB_AFFINE
     hipLaunchKernelGGL(k_ed_comb_fill, dim3(nblk((uint64_t)w.max_slots * ED_COMB_AWIN, 256)), dim3(256), 0, st, w.ctr,
                        w.max_slots, w.eager, meta, w.ctab);
+#else
+    const uint64_t lanes = (uint64_t)w.max_slots * ED_COMB_AWIN;
+    uint32_t* zprod = w.fz;
+    uint32_t* zinv = w.fz + lanes * 10;
+    hipLaunchKernelGGL(k_ed_comb_fill, dim3(nblk(lanes, 256)), dim3(256), 0, st, w.ctr, w.max_slots, w.eager, meta,
+                       w.ctab, zprod);
+    hipLaunchKernelGGL(k_ed_comb_zinv, dim3(nblk((lanes + ED_COMB_ZG - 1) / ED_COMB_ZG, 64)), dim3(64), 0, st, w.ctr,
+                       w.max_slots, w.eager, zprod, zinv);
+    hipLaunchKernelGGL(k_ed_comb_fill_b, dim3(nblk(lanes, 256)), dim3(256), 0, st, w.ctr, w.max_slots, w.eager, meta,
+                       w.ctab, zinv);
+#endif
 }
 
 uint64_t ed_comb_bmid_words() { return ED_BMID_WORDS; }

@@ -73,7 +73,7 @@ struct chip_ctx {
     DevBuf meta, abytes, edtab, ectab, lists, counts;
     // Ed25519 comb path
     DevBuf c_key_count, c_key_rank, c_key_slot, c_key_base, c_slot_key, c_ctr, c_comb_list, c_straus_list, c_ctab,
-        c_xyz, c_zpre, c_nega, c_bmid, e_ctab, e_mid, e_gcomb, e_bcomb16, e_wp, e_glist;
+        c_xyz, c_zpre, c_nega, c_fz, c_bmid, e_ctab, e_mid, e_gcomb, e_bcomb16, e_wp, e_glist;
     // host-path mirrors of the caller's buffers
     DevBuf h_key_idx, h_msg_idx, h_sig_data, h_sig_off, h_sig_len, h_key_data, h_key_off, h_key_len, h_msg_data,
         h_msg_off, h_msg_len, h_status, h_bitmap, h_check;
@@ -454,7 +454,7 @@ void chip_shutdown(chip_ctx* c) {
     hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->meta, &c->abytes, &c->edtab, &c->ectab, &c->lists, &c->counts, &c->c_key_count, &c->c_key_rank,
                       &c->c_key_slot, &c->c_key_base, &c->c_slot_key, &c->c_ctr, &c->c_comb_list,
-                      &c->c_straus_list, &c->c_ctab, &c->c_xyz, &c->c_zpre, &c->c_nega, &c->c_bmid, &c->e_ctab, &c->e_mid, &c->e_gcomb, &c->e_bcomb16, &c->e_wp, &c->e_glist, &c->h_key_idx, &c->h_msg_idx,
+                      &c->c_straus_list, &c->c_ctab, &c->c_xyz, &c->c_zpre, &c->c_nega, &c->c_fz, &c->c_bmid, &c->e_ctab, &c->e_mid, &c->e_gcomb, &c->e_bcomb16, &c->e_wp, &c->e_glist, &c->h_key_idx, &c->h_msg_idx,
                       &c->h_sig_data, &c->h_sig_off, &c->h_sig_len, &c->h_key_data, &c->h_key_off, &c->h_key_len,
                       &c->h_msg_data, &c->h_msg_off, &c->h_msg_len, &c->h_status, &c->h_bitmap, &c->h_check, &c->t_salts,
                       &c->t_start, &c->t_group, &c->t_internal, &c->t_data, &c->t_off, &c->t_len, &c->t_ids,
@@ -563,6 +563,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         HIPCHK(c, c->c_xyz.ensure(n * 30 * 4 + 16));
         HIPCHK(c, c->c_zpre.ensure(n * 10 * 4 + 16));
         HIPCHK(c, c->c_nega.ensure(nk * 40 * 4 + 16));
+        if (ED_COMB_AFFINE) HIPCHK(c, c->c_fz.ensure(2 * slots * ED_COMB_AWIN * 10 * 4 + 16));
         HIPCHK(c, c->c_bmid.ensure(n * ed_comb_bmid_words() * 4 + 16));
         w.key_slot = c->c_key_slot.as<int32_t>();
         w.slot_key = c->c_slot_key.as<uint32_t>();
@@ -572,6 +573,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         w.xyz = c->c_xyz.as<uint32_t>();
         w.zpre = c->c_zpre.as<uint32_t>();
         w.nega = c->c_nega.as<uint32_t>();
+        w.fz = ED_COMB_AFFINE ? c->c_fz.as<uint32_t>() : nullptr;
         w.bmid = c->c_bmid.as<uint32_t>();
         w.bcomb16 = c->e_bcomb16.as<uint32_t>();
         w.max_slots = (uint32_t)slots;

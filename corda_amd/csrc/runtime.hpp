@@ -136,13 +136,24 @@ void launch_ecdsa_key_check(hipStream_t st, uint64_t n, const uint8_t* pool, con
 #define EC_KEY_TABLE_WORDS (9 * 16 + 16)
 
 // ---- Ed25519 per-key comb path (ed25519_comb.hip) ----
-// A comb geometry: signed radix-2^ED_COMB_W digits of h (< L < 2^253), one table window per digit
+// A comb geometry: signed radix-2^ED_COMB_W digits of h (< L < 2^253), one table window per digit.
+// Measured (profiles/r04/ab_comb_radix.txt, same box): W = 6 (43 windows x 33 rows, 227 KB a key) 256.9-259.9M
+// cfg2 sigs/s vs 249.3-253.8M for W = 5 (51 x 17, 139 KB) and 248.2M for W = 7: the fill's extra rows cost the
+// second stream less than the 8 additions a signature saves
 #ifndef ED_COMB_W
-#define ED_COMB_W 5
+#define ED_COMB_W 6
 #endif
-#define ED_COMB_AWIN ((253 + ED_COMB_W - 1) / ED_COMB_W)   // W=5: 51 windows (top digit <= 8)
+#define ED_COMB_AWIN ((253 + ED_COMB_W - 1) / ED_COMB_W)   // W=6: 43 windows (top digit <= 2)
 #define ED_COMB_AENT ((1 << (ED_COMB_W - 1)) + 1)          // multiples 0..2^(W-1)
-#define ED_COMB_KEY_WORDS (ED_COMB_AWIN * ED_COMB_AENT * 40)  // rows [Y+X, Y-X, 2Z, 2dT] of 40 words
+// table rows: ED_COMB_AFFINE = 0: cached [Y+X, Y-X, 2Z, 2dT] (40 words; 8 multiplications per table addition);
+// 1: affine Niels [y+x, y-x, 2dxy] padded to 32 words (one 128-B line; 7 multiplications per addition, the
+// fill then inverts every row's Z: Montgomery's trick per lane, one inversion per ED_COMB_ZG lanes)
+#ifndef ED_COMB_AFFINE
+#define ED_COMB_AFFINE 0
+#endif
+#define ED_COMB_ROW (ED_COMB_AFFINE ? 32 : 40)
+#define ED_COMB_ZG 32
+#define ED_COMB_KEY_WORDS (ED_COMB_AWIN * ED_COMB_AENT * ED_COMB_ROW)
 #ifndef ED_FIN_G
 #define ED_FIN_G 16                                        // signatures per batched inversion
 #endif
@@ -164,6 +175,7 @@ struct EdCombWs {
     uint32_t* xyz;          // [30][n] projective R' (SoA), comb path
     uint32_t* zpre;         // [10][n] prefix products of the batched inversion
     uint32_t* nega;         // [n_keys][40] -A in extended coordinates (key prep)
+    uint32_t* fz;           // ED_COMB_AFFINE: [2][max_slots * ED_COMB_AWIN][10] each fill lane's Z product, its inverse
     uint32_t* bmid;         // [40 + ED_COMB_ADW][n] [S]B (extended) + h's digits, bhalf -> ahalf
     const uint32_t* bcomb16;  // fixed-base comb of B (per context)
     uint32_t max_slots, min_sigs;
