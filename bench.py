@@ -104,6 +104,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=32768)
     ap.add_argument("--no-host-path", action="store_true", help="skip the host-buffer (PCIe-inclusive) cfg2 leg")
+    ap.add_argument("--no-key-cache", action="store_true", help="skip the CHIP_FLAG_KEY_CACHE legs")
     ap.add_argument("--cold-n", type=int, default=200_000, help="cold-key leg: signatures = keys (0 = skip)")
     ap.add_argument("--no-txid", action="store_true", help="skip the cfg4 legs")
     ap.add_argument("--txid-n", type=int, default=1_000_000)
@@ -364,10 +365,40 @@ def main():
     comb_grid = (((n + 255) // 256 + 7) & ~7) * 256
     traffic = profile_traffic("k_ed_comb_ahalf", comb_grid)
     ahalf_issue = profile_issue("k_ed_comb_ahalf", comb_grid)
-    del db, status, bitmap, gathered
 
     secondary = {}
     progress("cfg2 headline done")
+    # ---- cfg2 with the key state kept across batches (CHIP_FLAG_KEY_CACHE, a context of its own): every step
+    # verifies the whole batch again, but the key pool equals the previous step's, so the key prep and the per-key
+    # comb tables are reused (the headline builds them inside every step) ----
+    if not args.no_key_cache:
+        kctx = corda_amd.Context(local, flags=native.FLAG_KEY_CACHE)
+
+        def kstep():
+            kctx.verify_batch_device(db, status, bitmap, stream=stream.cuda_stream)
+            all_gather_bitmap(gathered, bitmap, world, dist)
+
+        for _ in range(max(2, args.warmup)):   # the first call builds the key state
+            kstep()
+        torch.cuda.synchronize(dev)
+        kst = status.cpu().numpy()
+        kctx.reset_stats()
+        kel = timed_steps(kstep, args.steps, world, torch, dev, dist)
+        ks = kctx.stats()
+        secondary.update({
+            "cfg2_key_cache_sigs_per_s": world * n * args.steps / kel,
+            "cfg2_key_cache_ms_per_step": kel / args.steps * 1e3,
+            "cfg2_key_cache_correct": min_over_ranks_bool(bool(np.array_equal(kst, batch.expected)), world, torch,
+                                                          dev, dist),
+            "cfg2_key_cache_pipeline_ms": {"keyprep": kms(ks, native.K_KEYPREP), "comb_tables_aux_stream":
+                                           kms(ks, native.K_ED_TABLES), "comb_bhalf": kms(ks, native.K_ED_COMB_B),
+                                           "comb_ahalf": kms(ks, native.K_ED_COMB), "comb_finish": kms(ks, native.K_ED_FINISH)},
+            "cfg2_key_cache_note": "the cfg2 batch re-verified with CHIP_FLAG_KEY_CACHE: statuses recomputed every "
+                                   "step; the key pool is compared on the device and the key state reused",
+        })
+        kctx.close()
+        progress("cfg2 key cache done")
+    del db, status, bitmap, gathered
     # ---- cfg2 through the host-buffer entry (staging H2D + pipeline + D2H, blocking) ----
     if not args.no_host_path:
         ctx.verify_batch(batch)
@@ -866,6 +897,24 @@ def ecdsa_leg(args, ctx, world, rank, torch, dev, dist, D, G, native, threads, s
                                "q kernels %d MACs/signature over their own time" % (ECDSA_COMB_MACS_PER_VERIFY,
                                                                                     ECDSA_Q_MACS_PER_VERIFY),
     }
+    # the same batch with the key state kept across batches (CHIP_FLAG_KEY_CACHE, a context of its own): the
+    # per-key comb tables (ecdsa_tables_aux_ms above) are reused from the previous step
+    if not args.no_key_cache:
+        import corda_amd
+        kctx = corda_amd.Context(torch.cuda.current_device(), flags=native.FLAG_KEY_CACHE)
+
+        def kstep():
+            kctx.verify_batch_device(de, est, ebm, stream=stream.cuda_stream)
+            all_gather_bitmap(gath, ebm, world, dist)
+
+        for _ in range(2):
+            kstep()
+        torch.cuda.synchronize(dev)
+        kok = min_over_ranks_bool(bool(np.array_equal(est.cpu().numpy(), eb.expected)), world, torch, dev, dist)
+        kel = timed_steps(kstep, ts, world, torch, dev, dist)
+        out.update({"ecdsa_key_cache_sigs_per_s": world * eb.n * ts / kel, "ecdsa_key_cache_ms_per_step": kel / ts * 1e3,
+                    "ecdsa_key_cache_correct": kok})
+        kctx.close()
     del de, est, ebm, gath, eb
     # P-256 only (ECDSA_SECP256R1_SHA256): the same share size, every signature on secp256r1
     pb = G.ecdsa_batch(share, n_keys=args.keys, seed=0x5EED0013 + rank, threads=threads, schemes=(G.SCHEME_R1,))

@@ -208,9 +208,9 @@ CHIP_DEV void ec_build_table(uint32_t* tab) {
 __global__ void __launch_bounds__(256) k_ecdsa_key_prep(uint64_t n_keys, const uint8_t* __restrict__ key_data,
                                                         const uint64_t* __restrict__ key_off,
                                                         const uint32_t* __restrict__ key_len, KeyMeta* meta,
-                                                        uint32_t* __restrict__ table) {
+                                                        uint32_t* __restrict__ table, const uint32_t* __restrict__ skip) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n_keys) return;
+    if (k >= n_keys || (skip && *skip)) return;
     const uint8_t* p = key_data + key_off[k];
     const uint32_t len = key_len[k];
     int scheme = 0;
@@ -233,9 +233,9 @@ __global__ void __launch_bounds__(256) k_ecdsa_key_prep(uint64_t n_keys, const u
 }
 
 __global__ void __launch_bounds__(64) k_ecdsa_key_table(uint64_t n_keys, const KeyMeta* __restrict__ meta,
-                                                        uint32_t* __restrict__ table) {
+                                                        uint32_t* __restrict__ table, const uint32_t* __restrict__ skip) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n_keys) return;
+    if (k >= n_keys || (skip && *skip)) return;
     const KeyMeta m = meta[k];
     if (!m.ok) return;
     if (m.scheme == CHIP_SCHEME_R1) ec_build_table<CURVE_R1>(table + k * EC_TAB_STRIDE);
@@ -486,15 +486,17 @@ void launch_ecdsa_key_check(hipStream_t st, uint64_t n, const uint8_t* pool, con
 }
 
 void launch_ecdsa_key_prep(hipStream_t st, uint64_t n_keys, const uint8_t* key_data, const uint64_t* key_off,
-                           const uint32_t* key_len, KeyMeta* meta, uint32_t* ectab) {
+                           const uint32_t* key_len, KeyMeta* meta, uint32_t* ectab, const uint32_t* skip) {
     if (!n_keys) return;
     const uint32_t blocks = (uint32_t)((n_keys + 255) / 256);
     hipLaunchKernelGGL(k_ecdsa_key_prep, dim3(blocks), dim3(256), 0, st, n_keys, key_data, key_off, key_len, meta,
-                       ectab);
+                       ectab, skip);
 }
-void launch_ecdsa_key_table(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, uint32_t* ectab) {
+void launch_ecdsa_key_table(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, uint32_t* ectab,
+                            const uint32_t* skip) {
     if (!n_keys) return;
-    hipLaunchKernelGGL(k_ecdsa_key_table, dim3((uint32_t)((n_keys + 63) / 64)), dim3(64), 0, st, n_keys, meta, ectab);
+    hipLaunchKernelGGL(k_ecdsa_key_table, dim3((uint32_t)((n_keys + 63) / 64)), dim3(64), 0, st, n_keys, meta, ectab,
+                       skip);
 }
 
 void launch_ecdsa_verify(hipStream_t st, int scheme, uint64_t n, const uint32_t* list, const uint32_t* count,
@@ -677,9 +679,10 @@ CHIP_DEV void ec_comb_fill(uint32_t* __restrict__ jac, uint32_t* __restrict__ ou
 // one launch for both curves: r1 and k1 keys build concurrently (lane per key)
 __global__ void __launch_bounds__(64) k_ecdsa_comb_chain(uint64_t n_keys, const KeyMeta* __restrict__ meta,
                                                          const uint32_t* __restrict__ ectab, uint32_t* __restrict__ jac,
-                                                         uint32_t prio, uint32_t wa, uint32_t wb) {
+                                                         uint32_t prio, uint32_t wa, uint32_t wb,
+                                                         const uint32_t* __restrict__ skip) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n_keys) return;
+    if (k >= n_keys || (skip && *skip)) return;
     // the chain is the latency-bound critical path of the step: win VALU arbitration against the
     // throughput kernels of the main stream that share its SIMDs
     if (prio) __builtin_amdgcn_s_setprio(3);
@@ -690,12 +693,13 @@ __global__ void __launch_bounds__(64) k_ecdsa_comb_chain(uint64_t n_keys, const 
 // lane = more lanes, at one shared inversion pair per lane)
 __global__ void __launch_bounds__(256) k_ecdsa_comb_fill(uint64_t n_keys, const KeyMeta* __restrict__ meta,
                                                          uint32_t* __restrict__ ctab, uint32_t* __restrict__ jac,
-                                                         uint32_t wa, uint32_t wb, uint32_t gw) {
+                                                         uint32_t wa, uint32_t wb, uint32_t gw,
+                                                         const uint32_t* __restrict__ skip) {
     const uint32_t ng = (wb - wa + gw - 1) / gw;
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t k = g / ng;
     const uint32_t grp = (uint32_t)(g % ng);
-    if (k >= n_keys) return;
+    if (k >= n_keys || (skip && *skip)) return;
     const uint32_t w0 = wa + grp * gw;
     const uint32_t w1 = w0 + gw < wb ? w0 + gw : wb;
     uint32_t* e = jac + k * EC_COMB_JAC_WORDS;
@@ -1070,7 +1074,7 @@ uint64_t ecdsa_comb_key_words() { return EC_COMB_KEY_WORDS + EC_COMB_JAC_WORDS; 
 // table halves: windows [0, EC_LO_WIN) and [EC_LO_WIN, 65); fill groups cover EC_FILL_GROUP windows each
 #define EC_LO_WIN 32
 void launch_ecdsa_comb_chain(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, const uint32_t* ectab,
-                             uint32_t* ctab, int half) {
+                             uint32_t* ctab, int half, const uint32_t* skip) {
     if (!n_keys) return;
     uint32_t* jac = ctab + n_keys * EC_COMB_KEY_WORDS;
     static const uint32_t prio = [] {
@@ -1079,9 +1083,10 @@ void launch_ecdsa_comb_chain(hipStream_t st, uint64_t n_keys, const KeyMeta* met
     }();
     const uint32_t wa = half ? EC_LO_WIN : 0, wb = half ? EC_COMB_QWIN : EC_LO_WIN;
     hipLaunchKernelGGL(k_ecdsa_comb_chain, dim3((uint32_t)((n_keys + 63) / 64)), dim3(64), 0, st, n_keys, meta, ectab,
-                       jac, prio, wa, wb);
+                       jac, prio, wa, wb, skip);
 }
-void launch_ecdsa_comb_fill(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, uint32_t* ctab, int half) {
+void launch_ecdsa_comb_fill(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, uint32_t* ctab, int half,
+                            const uint32_t* skip) {
     if (!n_keys) return;
     uint32_t* jac = ctab + n_keys * EC_COMB_KEY_WORDS;
     static const uint32_t gw = [] {
@@ -1092,7 +1097,7 @@ void launch_ecdsa_comb_fill(hipStream_t st, uint64_t n_keys, const KeyMeta* meta
     const uint32_t wa = half ? EC_LO_WIN : 0, wb = half ? EC_COMB_QWIN : EC_LO_WIN;
     const uint32_t ng = (wb - wa + gw - 1) / gw;
     hipLaunchKernelGGL(k_ecdsa_comb_fill, dim3((uint32_t)((n_keys * ng + 255) / 256)), dim3(256), 0, st, n_keys, meta,
-                       ctab, jac, wa, wb, gw);
+                       ctab, jac, wa, wb, gw, skip);
 }
 
 // words of the hand-off area per list position, and of the wave products per list

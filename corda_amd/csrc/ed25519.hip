@@ -24,9 +24,9 @@ __global__ void __launch_bounds__(256) k_ed25519_key_prep(uint64_t n_keys, const
                                                           const uint64_t* __restrict__ key_off,
                                                           const uint32_t* __restrict__ key_len, KeyMeta* meta,
                                                           uint32_t* __restrict__ abytes, uint32_t* __restrict__ table,
-                                                          uint32_t* __restrict__ nega) {
+                                                          uint32_t* __restrict__ nega, const uint32_t* __restrict__ skip) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= n_keys) return;
+    if (k >= n_keys || (skip && *skip)) return;
     const uint8_t* p = key_data + key_off[k];
     const uint32_t len = key_len[k];
     bool is_ed = (len == 44);
@@ -242,11 +242,11 @@ void launch_ed25519_key_check(hipStream_t st, uint64_t n, const uint8_t* pool, c
 // ---------------------------------------------------------------------------------------
 void launch_ed25519_key_prep(hipStream_t st, uint64_t n_keys, const uint8_t* key_data, const uint64_t* key_off,
                              const uint32_t* key_len, KeyMeta* meta, uint32_t* abytes, uint32_t* table,
-                             uint32_t* nega) {
+                             uint32_t* nega, const uint32_t* skip) {
     if (!n_keys) return;
     const uint32_t blocks = (uint32_t)((n_keys + 255) / 256);
     hipLaunchKernelGGL(k_ed25519_key_prep, dim3(blocks), dim3(256), 0, st, n_keys, key_data, key_off, key_len, meta,
-                       abytes, table, nega);
+                       abytes, table, nega, skip);
 }
 
 void launch_ed25519_verify(hipStream_t st, uint64_t n, const uint32_t* list, const uint32_t* count,

@@ -143,10 +143,11 @@ __global__ void __launch_bounds__(256) k_ed_comb_partition(const uint32_t* __res
 __global__ void __launch_bounds__(64) k_ed_comb_chain(const uint32_t* __restrict__ ctr, uint32_t max_slots,
                                                       uint32_t eager, const KeyMeta* __restrict__ meta,
                                                       const uint32_t* __restrict__ slot_key,
-                                                      const uint32_t* __restrict__ nega, uint32_t* __restrict__ ctab) {
+                                                      const uint32_t* __restrict__ nega, uint32_t* __restrict__ ctab,
+                                                      const uint32_t* __restrict__ skip) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t nslots = eager ? max_slots : ctr[ED_CTR_NSLOTS];
-    if (s >= nslots) return;
+    if (s >= nslots || (skip && *skip)) return;
     if (eager && !ed_key_ok(meta, s)) return;
     const uint32_t k = eager ? s : slot_key[s];
     ge_p3 P;
@@ -185,10 +186,10 @@ CHIP_DEV void ed_store_row(uint32_t* __restrict__ dst, const ge_cached& c) {
 #if !ED_COMB_AFFINE
 __global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict__ ctr, uint32_t max_slots,
                                                       uint32_t eager, const KeyMeta* __restrict__ meta,
-                                                      uint32_t* __restrict__ ctab) {
+                                                      uint32_t* __restrict__ ctab, const uint32_t* __restrict__ skip) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t s = g / ED_COMB_AWIN, w = g % ED_COMB_AWIN;
-    if (s >= (eager ? max_slots : ctr[ED_CTR_NSLOTS])) return;
+    if (s >= (eager ? max_slots : ctr[ED_CTR_NSLOTS]) || (skip && *skip)) return;
     if (eager && !ed_key_ok(meta, s)) return;
     uint32_t* e = ctab + (uint64_t)s * ED_COMB_KEY_WORDS + (uint64_t)w * ED_COMB_AENT * ED_COMB_ROW;
     ge_p3 P;
@@ -236,11 +237,12 @@ CHIP_DEV void ed_load_fe(fe& f, const uint32_t* __restrict__ src) {
 }
 __global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict__ ctr, uint32_t max_slots,
                                                       uint32_t eager, const KeyMeta* __restrict__ meta,
-                                                      uint32_t* __restrict__ ctab, uint32_t* __restrict__ fz) {
+                                                      uint32_t* __restrict__ ctab, uint32_t* __restrict__ fz,
+                                                      const uint32_t* __restrict__ cached) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t s, w;
     bool skip = false;
-    if (!ed_fill_lane(g, ctr, max_slots, eager, meta, s, w, skip)) return;
+    if (!ed_fill_lane(g, ctr, max_slots, eager, meta, s, w, skip) || (cached && *cached)) return;
     fe acc;
     fe_1(acc);
     if (!skip) {
@@ -275,10 +277,11 @@ __global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict
     ed_store_fe(fz + (uint64_t)g * 10, acc);   // 1 for a skipped lane
 }
 __global__ void __launch_bounds__(64) k_ed_comb_zinv(const uint32_t* __restrict__ ctr, uint32_t max_slots, uint32_t eager,
-                                                     const uint32_t* __restrict__ zprod, uint32_t* __restrict__ zinv) {
+                                                     const uint32_t* __restrict__ zprod, uint32_t* __restrict__ zinv,
+                                                     const uint32_t* __restrict__ cached) {
     const uint32_t nl = (eager ? max_slots : ctr[ED_CTR_NSLOTS]) * ED_COMB_AWIN;
     const uint32_t g0 = (blockIdx.x * blockDim.x + threadIdx.x) * ED_COMB_ZG;
-    if (g0 >= nl) return;
+    if (g0 >= nl || (cached && *cached)) return;
     const uint32_t m = min((uint32_t)ED_COMB_ZG, nl - g0);
     fe acc, z, inv, t;
     fe_1(acc);
@@ -298,11 +301,12 @@ __global__ void __launch_bounds__(64) k_ed_comb_zinv(const uint32_t* __restrict_
 }
 __global__ void __launch_bounds__(256) k_ed_comb_fill_b(const uint32_t* __restrict__ ctr, uint32_t max_slots,
                                                         uint32_t eager, const KeyMeta* __restrict__ meta,
-                                                        uint32_t* __restrict__ ctab, const uint32_t* __restrict__ zinv) {
+                                                        uint32_t* __restrict__ ctab, const uint32_t* __restrict__ zinv,
+                                                        const uint32_t* __restrict__ cached) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t s, w;
     bool skip = false;
-    if (!ed_fill_lane(g, ctr, max_slots, eager, meta, s, w, skip) || skip) return;
+    if (!ed_fill_lane(g, ctr, max_slots, eager, meta, s, w, skip) || skip || (cached && *cached)) return;
     uint32_t* e = ctab + (uint64_t)s * ED_COMB_KEY_WORDS + (uint64_t)w * ED_COMB_AENT * ED_COMB_ROW;
     fe inv, d2;
     ed_load_fe(inv, zinv + (uint64_t)g * 10);
@@ -721,20 +725,20 @@ void launch_ed_comb_plan(hipStream_t st, uint64_t n, uint64_t n_keys, const uint
 void launch_ed_comb_build(hipStream_t st, uint64_t n, uint64_t n_keys, const KeyMeta* meta, const EdCombWs& w) {
     if (!n || !n_keys || !w.max_slots) return;
     hipLaunchKernelGGL(k_ed_comb_chain, dim3(nblk(w.max_slots, 64)), dim3(64), 0, st, w.ctr, w.max_slots, w.eager, meta,
-                       w.slot_key, w.nega, w.ctab);
+                       w.slot_key, w.nega, w.ctab, w.skip);
 #if !ED_COMB_AFFINE
     hipLaunchKernelGGL(k_ed_comb_fill, dim3(nblk((uint64_t)w.max_slots * ED_COMB_AWIN, 256)), dim3(256), 0, st, w.ctr,
-                       w.max_slots, w.eager, meta, w.ctab);
+                       w.max_slots, w.eager, meta, w.ctab, w.skip);
 #else
     const uint64_t lanes = (uint64_t)w.max_slots * ED_COMB_AWIN;
     uint32_t* zprod = w.fz;
     uint32_t* zinv = w.fz + lanes * 10;
     hipLaunchKernelGGL(k_ed_comb_fill, dim3(nblk(lanes, 256)), dim3(256), 0, st, w.ctr, w.max_slots, w.eager, meta,
-                       w.ctab, zprod);
+                       w.ctab, zprod, w.skip);
     hipLaunchKernelGGL(k_ed_comb_zinv, dim3(nblk((lanes + ED_COMB_ZG - 1) / ED_COMB_ZG, 64)), dim3(64), 0, st, w.ctr,
-                       w.max_slots, w.eager, zprod, zinv);
+                       w.max_slots, w.eager, zprod, zinv, w.skip);
     hipLaunchKernelGGL(k_ed_comb_fill_b, dim3(nblk(lanes, 256)), dim3(256), 0, st, w.ctr, w.max_slots, w.eager, meta,
-                       w.ctab, zinv);
+                       w.ctab, zinv, w.skip);
 #endif
 }
 

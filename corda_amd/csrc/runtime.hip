@@ -18,11 +18,13 @@
 struct DevBuf {
     void* p = nullptr;
     size_t cap = 0;
+    uint32_t gen = 0;   // bumped by every (re)allocation: the contents of an older generation are gone
     hipError_t ensure(size_t bytes) {
         if (bytes <= cap) return hipSuccess;
         if (p) hipFree(p);
         p = nullptr;
         cap = 0;
+        gen++;
         size_t want = bytes + bytes / 4 + 256;
         hipError_t e = hipMalloc(&p, want);
         if (e == hipSuccess) cap = want;
@@ -32,6 +34,7 @@ struct DevBuf {
         if (p) hipFree(p);
         p = nullptr;
         cap = 0;
+        gen++;
     }
     template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
@@ -95,6 +98,16 @@ struct chip_ctx {
     DevBuf h2_data, h2_off, h2_len, h2_st, h2_ids, h2_v, h2_a, h2_sigst, h2_miss, h2_td, h2_to, h2_tl, h2_ta;
     hipEvent_t ev0 = nullptr, ev1 = nullptr, tev0 = nullptr, tev1 = nullptr;
     bool ev_pending = false, tev_pending = false;
+    // cross-batch key state (CHIP_FLAG_KEY_CACHE): the key pool the context's key state (meta, key tables, comb
+    // tables) was last built from, the path it was built for, and the buffer generations it lives in
+    DevBuf kc_keys, kc_len, kc_flag;
+    bool kc_valid = false;
+    uint32_t kc_path = 0;
+    uint64_t kc_nk = 0, kc_gen = 0;
+    uint64_t key_state_gen() const {
+        return ((uint64_t)meta.gen << 48) ^ ((uint64_t)abytes.gen << 40) ^ ((uint64_t)edtab.gen << 32) ^
+               ((uint64_t)ectab.gen << 24) ^ ((uint64_t)c_ctab.gen << 16) ^ ((uint64_t)e_ctab.gen << 8) ^ c_nega.gen;
+    }
     // chip_verify_batch's chunk pipeline: H2D (and the chunk's bounds / pool-range check) on hcs ahead of the
     // verify kernels on the main stream; the checks' results land in pinned h_rng
     hipStream_t hcs = nullptr;
@@ -497,6 +510,36 @@ void chip_shutdown(chip_ctx* c) {
 
 const char* chip_last_error(const chip_ctx* c) { return c ? c->err.c_str() : "null context"; }
 
+// Key cache (CHIP_FLAG_KEY_CACHE): one lane per key compares the batch's key bytes with the cached copy (when the
+// host found the batch eligible: same key count and path, key state not reallocated since) and overwrites the
+// copy; *same ends 1 only when every key matched.  Keys longer than KC_MAX never match.
+#define KC_MAX 128
+__global__ void __launch_bounds__(256) k_key_cache(uint64_t nk, const uint8_t* __restrict__ key_data,
+                                                   const uint64_t* __restrict__ key_off,
+                                                   const uint32_t* __restrict__ key_len, uint8_t* __restrict__ kc_keys,
+                                                   uint32_t* __restrict__ kc_len, uint32_t compare, uint32_t* same) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nk) return;
+    const uint32_t len = key_len[k];
+    const uint8_t* src = key_data + key_off[k];
+    uint8_t* dst = kc_keys + k * KC_MAX;
+    bool eq = compare && len <= KC_MAX && kc_len[k] == len;
+    const uint32_t m = len < KC_MAX ? len : KC_MAX;
+    for (uint32_t i = 0; i < m; i++) {
+        const uint8_t v = src[i];
+        eq = eq && dst[i] == v;
+        dst[i] = v;
+    }
+    kc_len[k] = len <= KC_MAX ? len : 0xffffffffu;
+    if (!eq) *same = 0;   // every writer stores the same value
+}
+// the batch's key metadata cleared before the key preps write it, unless the cached state is reused
+__global__ void __launch_bounds__(256) k_meta_clear(uint64_t nk, KeyMeta* __restrict__ meta, const uint32_t* __restrict__ skip) {
+    const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= nk || *skip) return;
+    meta[k] = KeyMeta{};
+}
+
 // One stream-ordered pipeline per batch.  Main stream: key prep -> classify -> every kernel that
 // needs no per-key table (Ed25519 plan + challenge/[S]B half, ECDSA grouping/DER/SHA/s^-1/u1 G)
 // -> the table halves (Ed25519 [h](-A), ECDSA u2 Q) once the aux stream has built the tables ->
@@ -588,7 +631,34 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     }
     HIPCHK(c, hipEventRecord(c->ev0, st));
     HIPCHK(c, hipMemsetAsync(c->counts.p, 0, 64, st));
-    if (nk && !reuse) HIPCHK(c, hipMemsetAsync(c->meta.p, 0, nk * sizeof(KeyMeta), st));
+    // cross-batch key state: the key preps and table builds skip on the device when the key pool equals the
+    // cached one.  Not with per-batch Ed25519 comb slots (non-eager: the slots follow the signatures).
+    const uint32_t path = (comb ? (w.eager ? 1u : 3u) : 0u) | (ec_comb ? 4u : 8u);
+    const uint32_t* skip = nullptr;
+    if (!reuse && nk) {
+        if ((c->flags & CHIP_FLAG_KEY_CACHE) && !(path & 2u)) {
+            HIPCHK(c, c->kc_flag.ensure(64));
+            uint32_t* flag = c->kc_flag.as<uint32_t>();
+            const bool may = c->kc_valid && path == c->kc_path && nk == c->kc_nk && c->kc_gen == c->key_state_gen();
+            HIPCHK(c, hipMemsetD32Async(flag, may ? 1u : 0u, 1, st));
+            HIPCHK(c, c->kc_keys.ensure(nk * KC_MAX + 16));
+            HIPCHK(c, c->kc_len.ensure(nk * 4 + 16));
+            hipLaunchKernelGGL(k_key_cache, dim3((uint32_t)((nk + 255) / 256)), dim3(256), 0, st, nk, b->key_data,
+                               b->key_off, b->key_len, c->kc_keys.as<uint8_t>(), c->kc_len.as<uint32_t>(),
+                               may ? 1u : 0u, flag);
+            hipLaunchKernelGGL(k_meta_clear, dim3((uint32_t)((nk + 255) / 256)), dim3(256), 0, st, nk,
+                               c->meta.as<KeyMeta>(), (const uint32_t*)flag);
+            skip = flag;
+            c->kc_valid = true;   // after this batch the state is the cached pool's, rebuilt or reused
+            c->kc_path = path;
+            c->kc_nk = nk;
+            c->kc_gen = c->key_state_gen();
+        } else {
+            HIPCHK(c, hipMemsetAsync(c->meta.p, 0, nk * sizeof(KeyMeta), st));
+            c->kc_valid = false;   // rebuilt for a pool the cache does not describe
+        }
+    }
+    w.skip = skip;
     if (comb || ec_comb) {
         HIPCHK(c, hipMemsetAsync(w.ctr, 0, 64, st));
         HIPCHK(c, hipMemsetAsync(w.key_count, 0, nk * 4, st));
@@ -597,7 +667,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     int ke = c->kbegin(CHIP_K_KEYPREP, st);
     if (!reuse)
         launch_ed25519_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->abytes.as<uint32_t>(),
-                                c->edtab.as<uint32_t>(), comb ? w.nega : nullptr);
+                                c->edtab.as<uint32_t>(), comb ? w.nega : nullptr, skip);
     if (comb && w.eager && n && !reuse) {
         // fork: per-key comb tables on the aux stream, concurrent with ECDSA key prep, classify and
         // every table-free kernel on the main stream (the chain is a serial 252-doubling latency)
@@ -608,8 +678,8 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         c->kend(kt, c->aux);
         HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
     }
-    if (!reuse) launch_ecdsa_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->ectab.as<uint32_t>());
-    if (!ec_comb && !reuse) launch_ecdsa_key_table(st, nk, meta, c->ectab.as<uint32_t>());
+    if (!reuse) launch_ecdsa_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->ectab.as<uint32_t>(), skip);
+    if (!ec_comb && !reuse) launch_ecdsa_key_table(st, nk, meta, c->ectab.as<uint32_t>(), skip);
     if (ec_comb && !reuse) {
         // aux: the doubling chain, low windows then high windows; aux2: the fill of each half as soon
         // as its chain half is done (the low fill overlaps the high chain); main waits for the low
@@ -618,18 +688,18 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork2, 0));
         const int kt = c->kbegin(CHIP_K_EC_TABLES, c->aux);
         uint32_t* ctab = c->e_ctab.as<uint32_t>();
-        launch_ecdsa_comb_chain(c->aux, nk, meta, c->ectab.as<uint32_t>(), ctab, 0);
+        launch_ecdsa_comb_chain(c->aux, nk, meta, c->ectab.as<uint32_t>(), ctab, 0, skip);
         HIPCHK(c, hipEventRecord(c->ev_ec_chain_lo, c->aux));
-        launch_ecdsa_comb_chain(c->aux, nk, meta, c->ectab.as<uint32_t>(), ctab, 1);
+        launch_ecdsa_comb_chain(c->aux, nk, meta, c->ectab.as<uint32_t>(), ctab, 1, skip);
         HIPCHK(c, hipEventRecord(c->ev_ec_chain_hi, c->aux));
         // CHIP_EC_SPLIT=0: both fills after the whole chain on aux (the round-1 order)
         hipStream_t fs = c->ec_split ? c->aux2 : c->aux;
         if (c->ec_split) HIPCHK(c, hipStreamWaitEvent(fs, c->ev_ec_chain_lo, 0));
         else HIPCHK(c, hipStreamWaitEvent(fs, c->ev_ec_chain_hi, 0));
-        launch_ecdsa_comb_fill(fs, nk, meta, ctab, 0);
+        launch_ecdsa_comb_fill(fs, nk, meta, ctab, 0, skip);
         HIPCHK(c, hipEventRecord(c->ev_ec_lo, fs));
         HIPCHK(c, hipStreamWaitEvent(fs, c->ev_ec_chain_hi, 0));
-        launch_ecdsa_comb_fill(fs, nk, meta, ctab, 1);
+        launch_ecdsa_comb_fill(fs, nk, meta, ctab, 1, skip);
         c->kend(kt, fs);
         HIPCHK(c, hipEventRecord(c->ev_join2, fs));
     }

@@ -8,14 +8,17 @@ enum { LIST_ED25519 = 0, LIST_R1 = 1, LIST_K1 = 2, N_LISTS = 3 };
 
 void launch_ed25519_key_prep(hipStream_t st, uint64_t n_keys, const uint8_t* key_data, const uint64_t* key_off,
                              const uint32_t* key_len, KeyMeta* meta, uint32_t* abytes, uint32_t* table,
-                             uint32_t* nega);
+                             uint32_t* nega, const uint32_t* skip = nullptr);
+// skip (every key-state builder): a device word; non-zero = this batch's key pool equals the one the context's
+// key state was built from (CHIP_FLAG_KEY_CACHE), and the kernel returns at once
 void launch_ed25519_verify(hipStream_t st, uint64_t n, const uint32_t* list, const uint32_t* count,
                            const chip_sig_batch* b, const uint32_t* abytes, const uint32_t* table, uint8_t* status);
 
 void launch_ecdsa_key_prep(hipStream_t st, uint64_t n_keys, const uint8_t* key_data, const uint64_t* key_off,
-                           const uint32_t* key_len, KeyMeta* meta, uint32_t* ectab);
+                           const uint32_t* key_len, KeyMeta* meta, uint32_t* ectab, const uint32_t* skip = nullptr);
 // {1..8}Q per key for the windowed schedule (k_ecdsa_verify); the comb schedule does not need it
-void launch_ecdsa_key_table(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, uint32_t* ectab);
+void launch_ecdsa_key_table(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, uint32_t* ectab,
+                            const uint32_t* skip = nullptr);
 void launch_ecdsa_verify(hipStream_t st, int scheme, uint64_t n, const uint32_t* list, const uint32_t* count,
                          const chip_sig_batch* b, const uint32_t* ectab, uint8_t* status);
 
@@ -23,8 +26,9 @@ void launch_ecdsa_verify(hipStream_t st, int scheme, uint64_t n, const uint32_t*
 uint64_t ecdsa_comb_key_words();
 // in two halves each (half 0: windows 0..31, half 1: windows 32..64): chain (serial doublings), fill
 void launch_ecdsa_comb_chain(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, const uint32_t* ectab,
-                             uint32_t* ctab, int half);
-void launch_ecdsa_comb_fill(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, uint32_t* ctab, int half);
+                             uint32_t* ctab, int half, const uint32_t* skip = nullptr);
+void launch_ecdsa_comb_fill(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, uint32_t* ctab, int half,
+                            const uint32_t* skip = nullptr);
 uint64_t ecdsa_comb_mid_words();
 // fixed-base G combs of both curves (built once per context)
 uint64_t ecdsa_gcomb_words();
@@ -176,6 +180,7 @@ struct EdCombWs {
     uint32_t* zpre;         // [10][n] prefix products of the batched inversion
     uint32_t* nega;         // [n_keys][40] -A in extended coordinates (key prep)
     uint32_t* fz;           // ED_COMB_AFFINE: [2][max_slots * ED_COMB_AWIN][10] each fill lane's Z product, its inverse
+    const uint32_t* skip;   // key-state skip word (CHIP_FLAG_KEY_CACHE) or null: the table build returns at once
     uint32_t* bmid;         // [40 + ED_COMB_ADW][n] [S]B (extended) + h's digits, bhalf -> ahalf
     const uint32_t* bcomb16;  // fixed-base comb of B (per context)
     uint32_t max_slots, min_sigs;

@@ -173,7 +173,7 @@ class ChipConflict(ctypes.Structure):
  K_ED_PLAN, K_ED_COMB_B, K_EC_FRONT, K_REQ, K_STX) = range(15)
 (STX_OK, STX_KRYO, STX_NO_SIGS, STX_INVARIANT, STX_UNSUPPORTED) = range(5)
 N_KERNELS = 16
-FLAG_NO_COMB, FLAG_FORCE_COMB, FLAG_EC_RETRY_ALL = 0x1, 0x2, 0x4
+FLAG_NO_COMB, FLAG_FORCE_COMB, FLAG_EC_RETRY_ALL, FLAG_KEY_CACHE = 0x1, 0x2, 0x4, 0x8
 
 
 class ChipStats(ctypes.Structure):

@@ -82,6 +82,11 @@ typedef struct {
 #define CHIP_FLAG_NO_COMB 0x1u      /* every key on the Straus kernel                  */
 #define CHIP_FLAG_FORCE_COMB 0x2u   /* every key on the comb kernel (threshold 1)      */
 #define CHIP_FLAG_EC_RETRY_ALL 0x4u /* test: every ECDSA comb lane takes the exceptional-addition retry path */
+/* Keep the key state (decoded keys, per-key tables, Ed25519 / ECDSA comb tables) across batches: a batch whose
+ * key pool (key count, every key's bytes) equals the previous batch's and that takes the same schedule reuses
+ * it, compared on the device key by key (no host round trip); any difference rebuilds it.  For callers that
+ * verify many batches against one set of party keys (a notary, a node's counterparties). */
+#define CHIP_FLAG_KEY_CACHE 0x8u
 
 int chip_abi_version(void);
 int chip_device_count(void);

@@ -49,6 +49,14 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
     }
     private val arena = PinnedBuffer(1 shl 20)
     private val statusBuf = PinnedBuffer(1 shl 12)
+    /** With CordaHip.FLAG_KEY_CACHE the key pool is kept across calls, append-only in first-seen order (a node
+     *  sees the same parties and notary again and again): batches whose keys are all known send the identical
+     *  pool, and the library reuses its key state (decoded keys, per-key comb tables).  Reset past
+     *  `stableKeyLimit` keys, so a stream of fresh keys does not grow it without bound. */
+    private val stableKeys = (flags and CordaHip.FLAG_KEY_CACHE) != 0
+    private val poolIds = HashMap<ByteBuffer, Int>()
+    private val poolKeys = ArrayList<ByteArray>()
+    var stableKeyLimit = 65536
 
     /** One signature to decide: `by` signed `message`. */
     class Item(val by: PublicKey, val signature: ByteArray, val message: ByteArray)
@@ -58,9 +66,10 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
     fun statuses(items: List<Item>, isValid: Boolean = false): ByteArray {
         val n = items.size
         if (n == 0) return ByteArray(0)
-        val keyIds = HashMap<ByteBuffer, Int>()
+        if (stableKeys && poolKeys.size + n > stableKeyLimit) { poolIds.clear(); poolKeys.clear() }
+        val keyIds = if (stableKeys) poolIds else HashMap<ByteBuffer, Int>()
         val msgIds = HashMap<ByteBuffer, Int>()
-        val keys = ArrayList<ByteArray>()
+        val keys = if (stableKeys) poolKeys else ArrayList<ByteArray>()
         val msgs = ArrayList<ByteArray>()
         val keyIdx = IntArray(n)
         val msgIdx = IntArray(n)

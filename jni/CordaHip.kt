@@ -26,6 +26,8 @@ object CordaHip {
     const val UNSUPPORTED = 5
     const val KEY_INVALID = 6
     const val E_CAPACITY = -4
+    /** chip_config flag CHIP_FLAG_KEY_CACHE: key state kept across batches with the same key pool */
+    const val FLAG_KEY_CACHE = 0x8
     /** sizeof(chip_conflict): tx u64, input_index u32, consumed_index u32, consuming_tx 32 B, caller u32, pad u32 */
     const val CONFLICT_BYTES = 56
 
