@@ -473,41 +473,90 @@ CHIP_DEV void recode16(uint32_t out[8], const uint32_t a[8]) {
 
 // The verify runs in two kernels so that the part that needs no per-key table overlaps the table
 // build on the second stream:
-//   k_ed_comb_bhalf  h = SHA-512(R || Abyte || M) mod L and [S]B from the fixed comb (32 madds);
-//                    hands over [S]B (extended, 40 words) and h (8 words) SoA in bmid
-//   k_ed_comb_ahalf  + [h](-A) from the key's table (64 cached additions), projective R' to xyz
-// hand-off: [S]B (40 words) + the ED_COMB_ADW words of h's recoded digits, read one word per 4
-// windows by the table half (keeping all 16 live would cost the occupancy step to 3 waves/SIMD)
-#define ED_BMID_SDIG (40 + ED_COMB_ADW)   // S's radix-2^16 digits, hash -> [S]B
-#define ED_BMID_WORDS (ED_BMID_SDIG + 8)
+//   k_ed_comb_hash   h = SHA-512(R || Abyte || M) mod L and the effective S, recoded
+//   k_ed_comb_bhalf  [S]B from the fixed comb (16 madds)
+//   k_ed_comb_ahalf  + [h](-A) from the key's table, projective R' to xyz
+// hand-off rows (AoS, ED_BMID_W words per slot): [S]B extended (40) | h's biased digit bytes (ED_COMB_ADW
+// words, read one word per 4 windows by the table half) | S's radix-2^16 digits (8).  A slot is the comb-list
+// position, or with `early` (eager tables, device entry) the signature index: then hash and [S]B run over the
+// whole batch before the key prep has finished (it runs on the second stream with the tables), and the table
+// half reads row list[p] — one 240-B row per lane, 16-byte loads.
+#define ED_BMID_HD 40                                  // h digits
+#define ED_BMID_SD (40 + ED_COMB_ADW)                   // S digits
+#define ED_BMID_W ((ED_BMID_SD + 8 + 3) & ~3)           // W = 6: 60 words (16-byte aligned rows)
 #ifndef ED_BHALF_MINW
 #define ED_BHALF_MINW 2   // the [S]B additions allocate 165 VGPRs: 3 waves per SIMD (a bound of 3 spills)
 #endif
 #ifndef ED_AHALF_MINW
-#define ED_AHALF_MINW 4   // waves per SIMD: <= 128 VGPRs (127, no scratch)
+#define ED_AHALF_MINW 3   // waves per SIMD: 134 VGPRs, no scratch (a bound of 4 spills the table offset into the
+                          // loop; measured 1.81 vs 1.82-1.87 ms, profiles/r04/ab_early_hash.txt)
 #endif
+// i2p's Abyte = A.toByteArray() (k_ed25519_key_prep) from the SPKI bytes alone, for a key that decodes: the
+// canonical y (the low 255 bits mod p) and the encoding's sign bit, cleared for x = 0 (y = +-1), whose negation
+// is itself.  For a key that does not decode the value is never used (its signatures are KEY_INVALID).
+CHIP_DEV void ed_abyte_canonical(uint32_t ab[8], const uint8_t* __restrict__ raw) {
+    uint32_t y[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) y[q] = ld_le32(raw + 4 * q);
+    uint32_t bit = y[7] >> 31;
+    y[7] &= 0x7fffffffu;
+    // y >= p = 2^255 - 19 <=> y[7] = 0x7fffffff, y[1..6] all ones, y[0] >= 0xffffffed: then y - p = y + 19 - 2^255
+    bool ones = y[7] == 0x7fffffffu;
+#pragma unroll
+    for (int q = 1; q < 7; q++) ones = ones && y[q] == 0xffffffffu;
+    if (ones && y[0] >= 0xffffffedu) {
+        y[0] -= 0xffffffedu;
+#pragma unroll
+        for (int q = 1; q < 8; q++) y[q] = 0;
+    }
+    bool pm1 = y[7] == 0x7fffffffu && y[0] == 0xffffffecu;   // p - 1
+#pragma unroll
+    for (int q = 1; q < 7; q++) pm1 = pm1 && y[q] == 0xffffffffu;
+    bool one = y[0] == 1u;
+#pragma unroll
+    for (int q = 1; q < 8; q++) one = one && y[q] == 0u;
+    if (one || pm1) bit = 0;
+#pragma unroll
+    for (int q = 0; q < 8; q++) ab[q] = y[q];
+    ab[7] |= bit << 31;
+}
+template <bool EARLY>
 __global__ void __launch_bounds__(256) k_ed_comb_hash(const uint32_t* __restrict__ list, const uint32_t* __restrict__ ctr,
-                                                      const uint32_t* __restrict__ key_idx,
+                                                      uint64_t n, const uint32_t* __restrict__ key_idx,
                                                       const uint32_t* __restrict__ msg_idx,
                                                       const uint8_t* __restrict__ sig_data,
                                                       const uint64_t* __restrict__ sig_off,
+                                                      const uint32_t* __restrict__ sig_len,
                                                       const uint8_t* __restrict__ msg_data,
                                                       const uint64_t* __restrict__ msg_off,
-                                                      const uint32_t* __restrict__ msg_len,
-                                                      const uint32_t* __restrict__ abytes, uint32_t* __restrict__ bmid,
-                                                      uint64_t cap) {
+                                                      const uint32_t* __restrict__ msg_len, uint64_t n_keys,
+                                                      uint64_t n_msgs, const uint8_t* __restrict__ key_data,
+                                                      const uint64_t* __restrict__ key_off,
+                                                      const uint32_t* __restrict__ key_len,
+                                                      const uint32_t* __restrict__ abytes, uint32_t* __restrict__ bmid) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= ctr[ED_CTR_NCOMB]) return;
-    const uint32_t i = list[p];
-    const uint32_t k = key_idx[i];
+    uint32_t i, Ab[8];
+    if (EARLY) {
+        // every signature that can take the Ed25519 path (the bounds k_classify checks before any of its reads)
+        if (p >= n) return;
+        i = p;
+        const uint32_t k = key_idx[i];
+        if (k >= n_keys || msg_idx[i] >= n_msgs || sig_len[i] != 64 || key_len[k] != 44) return;
+        ed_abyte_canonical(Ab, key_data + key_off[k] + 12);
+    } else {
+        if (p >= ctr[ED_CTR_NCOMB]) return;
+        i = list[p];
+        const uint32_t k = key_idx[i];
+#pragma unroll
+        for (int q = 0; q < 8; q++) Ab[q] = abytes[(uint64_t)k * 8 + q];
+    }
     const uint32_t mi = msg_idx[i];
     const uint8_t* sig = sig_data + sig_off[i];
-    uint32_t R[8], S[8], Ab[8];
+    uint32_t R[8], S[8];
 #pragma unroll
     for (int q = 0; q < 8; q++) {
         R[q] = ld_le32(sig + 4 * q);
         S[q] = ld_le32(sig + 32 + 4 * q);
-        Ab[q] = abytes[(uint64_t)k * 8 + q];
     }
     uint32_t hx[16], h[8], s[8];
     ed_challenge(hx, R, Ab, msg_data + msg_off[mi], msg_len[mi], sig);
@@ -516,19 +565,23 @@ __global__ void __launch_bounds__(256) k_ed_comb_hash(const uint32_t* __restrict
     uint32_t db[8], da[ED_COMB_ADW];
     recode16(db, s);
     recode_bytes<ED_COMB_W, ED_COMB_AWIN>(da, h);
+    uint32_t* row = bmid + (uint64_t)p * ED_BMID_W;
 #pragma unroll
-    for (int q = 0; q < ED_COMB_ADW; q++) bmid[(uint64_t)(40 + q) * cap + p] = da[q];
+    for (int q = 0; q < ED_COMB_ADW; q++) row[ED_BMID_HD + q] = da[q];
 #pragma unroll
-    for (int q = 0; q < 8; q++) bmid[(uint64_t)(ED_BMID_SDIG + q) * cap + p] = db[q];
+    for (int q = 0; q < 8; q++) row[ED_BMID_SD + q] = db[q];
 }
 
-// k_ed_comb_bhalf: [S]B from the fixed radix-2^16 comb, 16 mixed additions; [S]B (extended) into bmid rows 0..39
-__global__ void __launch_bounds__(256, ED_BHALF_MINW) k_ed_comb_bhalf(const uint32_t* __restrict__ ctr,
+// k_ed_comb_bhalf: [S]B from the fixed radix-2^16 comb, 16 mixed additions; [S]B (extended) into the row's words 0..39
+__global__ void __launch_bounds__(256, ED_BHALF_MINW) k_ed_comb_bhalf(const uint32_t* __restrict__ ctr, uint64_t n_early,
                                                                       const uint32_t* __restrict__ b16,
-                                                                      uint32_t* __restrict__ bmid, uint64_t cap) {
+                                                                      uint32_t* __restrict__ bmid) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-    if (p >= ctr[ED_CTR_NCOMB]) return;
-    const uint32_t* sdig = bmid + (uint64_t)ED_BMID_SDIG * cap + p;   // digit word j at sdig[j * cap]
+    // early: every slot of the batch (a slot the hash skipped holds stale digits: any int16 digit stays inside
+    // the radix-2^16 table, and the row is never read back)
+    if (p >= (n_early ? n_early : (uint64_t)ctr[ED_CTR_NCOMB])) return;
+    uint32_t* row = bmid + (uint64_t)p * ED_BMID_W;
+    const uint32_t* sdig = row + ED_BMID_SD;   // digit word j at sdig[j]
     // [S]B: one mixed (affine Niels) addition per radix-2^16 window.  Window 0 from the identity needs no
     // multiplication: identity + q = (q+ - q-, q+ + q-, 2, 2) in completed form.  The loop carries only t.
     ge_p1p1 t;
@@ -558,17 +611,17 @@ __global__ void __launch_bounds__(256, ED_BHALF_MINW) k_ed_comb_bhalf(const uint
     window(1, (int)(int16_t)(cur >> 16));
 #pragma unroll 1
     for (uint32_t wd = 1; wd < ED_B16_WIN / 2; wd++) {   // two windows per digit word, read as it is needed
-        cur = sdig[(uint64_t)wd * cap];
+        cur = sdig[wd];
         window(2 * wd, (int)(int16_t)cur);
         window(2 * wd + 1, (int)(int16_t)(cur >> 16));
     }
-    ge_p1p1_to_p3(u, t);
+    // handed over completed (X, Y, Z, T): the table half's first window converts it like every other
 #pragma unroll
     for (int q = 0; q < 10; q++) {
-        bmid[(uint64_t)q * cap + p] = u.X.v[q];
-        bmid[(uint64_t)(10 + q) * cap + p] = u.Y.v[q];
-        bmid[(uint64_t)(20 + q) * cap + p] = u.Z.v[q];
-        bmid[(uint64_t)(30 + q) * cap + p] = u.T.v[q];
+        row[q] = t.X.v[q];
+        row[10 + q] = t.Y.v[q];
+        row[20 + q] = t.Z.v[q];
+        row[30 + q] = t.T.v[q];
     }
 }
 
@@ -578,59 +631,69 @@ __global__ void __launch_bounds__(256, ED_AHALF_MINW) k_ed_comb_ahalf(const uint
                                                        const int32_t* __restrict__ key_slot,
                                                        const uint32_t* __restrict__ ctab,
                                                        const uint32_t* __restrict__ bmid, uint32_t* __restrict__ xyz,
-                                                       uint64_t cap) {
+                                                       uint64_t cap, uint32_t early) {
     const uint32_t ncomb = ctr[ED_CTR_NCOMB];
     const uint32_t p = xcd_block(blockIdx.x, (ncomb + 255) / 256) * blockDim.x + threadIdx.x;
     if (p >= ncomb) return;
-    const uint32_t k = key_idx[list[p]];
-    // digit d of window w (-16..16) reads row |d| of the window, signed
-    const uint32_t* tab = ctab + (uint64_t)key_slot[k] * ED_COMB_KEY_WORDS;
-    ge_p3 u;
-#pragma unroll
-    for (int q = 0; q < 10; q++) {
-        u.X.v[q] = bmid[(uint64_t)q * cap + p];
-        u.Y.v[q] = bmid[(uint64_t)(10 + q) * cap + p];
-        u.Z.v[q] = bmid[(uint64_t)(20 + q) * cap + p];
-        u.T.v[q] = bmid[(uint64_t)(30 + q) * cap + p];
-    }
+    const uint32_t i = list[p];
+    const uint32_t k = key_idx[i];
+    // digit d of window w reads row |d| of the window, signed
+    // the key's table as a 32-bit word offset from the uniform base (<= 2^32 words of tables): one VGPR, not two
+    const uint32_t toff = (uint32_t)key_slot[k] * (uint32_t)ED_COMB_KEY_WORDS;
+    // the row as a 32-bit word offset from the uniform base (slot * ED_BMID_W < 2^32): one VGPR through the loop;
+    // p itself is rebuilt after the loop from the wave's first position (an SGPR) and the lane id
+    const uint32_t ro = (early ? i : p) * (uint32_t)ED_BMID_W;
+    const uint32_t pwave = __builtin_amdgcn_readfirstlane(p & ~63u);
     // + [h](-A): one addition per window from the key's signed-multiple rows (extended coordinates, unified =
-    // complete formulas); window 0 peeled so the loop carries only the completed point t
-    uint32_t cur = bmid[(uint64_t)40 * cap + p];
+    // complete formulas), starting from [S]B in completed form; the loop carries only the completed point t
     ge_p1p1 t;
+    {
+        const uint32_t* r = bmid + ro;
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            t.X.v[q] = r[q];
+            t.Y.v[q] = r[10 + q];
+            t.Z.v[q] = r[20 + q];
+            t.T.v[q] = r[30 + q];
+        }
+    }
+    // h's digit words parked in LDS ([word][thread]): the loop reads one every 4 windows at an address rebuilt
+    // from the wave's base (an SGPR) and the lane id, so no per-lane offset stays live through the loop
+    __shared__ uint32_t s_hd[ED_COMB_ADW][256];
+    const uint32_t lane = __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    const uint32_t wbase = __builtin_amdgcn_readfirstlane(threadIdx.x & ~63u);
+#pragma unroll
+    for (int q = 0; q < ED_COMB_ADW; q++) s_hd[q][wbase + lane] = bmid[ro + ED_BMID_HD + q];
+    auto hd_word = [&](uint32_t j) {
+        uint32_t l;   // the lane id recomputed at each use (volatile: not hoisted into a register kept live)
+        asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+        return s_hd[j][wbase + l];
+    };
+    ge_p3 u;
+    uint32_t cur = 0;
 #if ED_COMB_AFFINE
     // affine Niels rows: a mixed addition (3 multiplications) after a conversion that yields 2Z directly
     fe qp, qm, xy2d, z2;
-    {
-        const int d = (int)(cur & 0xffu) - ED_COMB_ABIAS;
-        ed_load_niels_signed(qp, qm, xy2d, tab + (uint32_t)(d < 0 ? -d : d) * ED_COMB_ROW, d < 0);
-        fe_add(z2, u.Z, u.Z);
-        fe_carry(z2);   // the madd's 2Z - C needs a carried 2Z (fe_mul2 yields one in the loop)
-        ge_madd_signed(t, u, z2, qp, qm, xy2d, (uint32_t)(d >> 31));
-    }
 #pragma unroll 1
-    for (uint32_t w = 1; w < ED_COMB_AWIN; w++) {
-        if ((w & 3u) == 0) cur = bmid[(uint64_t)(40 + (w >> 2)) * cap + p];
+    for (uint32_t w = 0; w < ED_COMB_AWIN; w++) {
+        if ((w & 3u) == 0) cur = hd_word(w >> 2);
         const int d = (int)((cur >> (8 * (w & 3u))) & 0xffu) - ED_COMB_ABIAS;
         fe_mul(u.X, t.X, t.T);
         fe_mul(u.Y, t.Z, t.Y);
         fe_mul2(z2, t.Z, t.T);
         fe_mul(u.T, t.X, t.Y);
-        ed_load_niels_signed(qp, qm, xy2d, tab + (w * ED_COMB_AENT + (uint32_t)(d < 0 ? -d : d)) * ED_COMB_ROW, d < 0);
+        ed_load_niels_signed(qp, qm, xy2d, ctab + (toff + (w * ED_COMB_AENT + (uint32_t)(d < 0 ? -d : d)) * ED_COMB_ROW),
+                             d < 0);
         ge_madd_signed(t, u, z2, qp, qm, xy2d, (uint32_t)(d >> 31));
     }
 #else
     ge_cached ca;
-    {
-        const int d = (int)(cur & 0xffu) - ED_COMB_ABIAS;
-        ed_load_row_signed(ca, tab + (uint32_t)(d < 0 ? -d : d) * ED_COMB_ROW, d < 0);
-        ge_add_row(t, u, ca, (uint32_t)(d >> 31));
-    }
 #pragma unroll 1
-    for (uint32_t w = 1; w < ED_COMB_AWIN; w++) {
-        if ((w & 3u) == 0) cur = bmid[(uint64_t)(40 + (w >> 2)) * cap + p];
+    for (uint32_t w = 0; w < ED_COMB_AWIN; w++) {
+        if ((w & 3u) == 0) cur = hd_word(w >> 2);
         const int d = (int)((cur >> (8 * (w & 3u))) & 0xffu) - ED_COMB_ABIAS;
-        ed_load_row_signed(ca, tab + (w * ED_COMB_AENT + (uint32_t)(d < 0 ? -d : d)) * ED_COMB_ROW, d < 0);
         ge_p1p1_to_p3(u, t);
+        ed_load_row_signed(ca, ctab + (toff + (w * ED_COMB_AENT + (uint32_t)(d < 0 ? -d : d)) * ED_COMB_ROW), d < 0);
         ge_add_row(t, u, ca, (uint32_t)(d >> 31));
     }
 #endif
@@ -639,11 +702,12 @@ __global__ void __launch_bounds__(256, ED_AHALF_MINW) k_ed_comb_ahalf(const uint
     fe_mul(X, t.X, t.T);
     fe_mul(Y, t.Z, t.Y);
     fe_mul(Z, t.Z, t.T);
+    const uint32_t pe = pwave + __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
 #pragma unroll
     for (int q = 0; q < 10; q++) {
-        xyz[(uint64_t)q * cap + p] = X.v[q];
-        xyz[(uint64_t)(10 + q) * cap + p] = Y.v[q];
-        xyz[(uint64_t)(20 + q) * cap + p] = Z.v[q];
+        xyz[(uint64_t)q * cap + pe] = X.v[q];
+        xyz[(uint64_t)(10 + q) * cap + pe] = Y.v[q];
+        xyz[(uint64_t)(20 + q) * cap + pe] = Z.v[q];
     }
 }
 
@@ -742,20 +806,27 @@ void launch_ed_comb_build(hipStream_t st, uint64_t n, uint64_t n_keys, const Key
 #endif
 }
 
-uint64_t ed_comb_bmid_words() { return ED_BMID_WORDS; }
+uint64_t ed_comb_bmid_words() { return ED_BMID_W; }
 
 void launch_ed_comb_bhalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, const uint32_t* abytes,
                           const EdCombWs& w) {
     if (!n || !w.max_slots) return;
-    hipLaunchKernelGGL(k_ed_comb_hash, dim3(nblk(n, 256)), dim3(256), 0, st, w.comb_list, w.ctr, b->key_idx, b->msg_idx,
-                       b->sig_data, b->sig_off, b->msg_data, b->msg_off, b->msg_len, abytes, w.bmid, (uint64_t)n);
-    hipLaunchKernelGGL(k_ed_comb_bhalf, dim3(nblk(n, 256)), dim3(256), 0, st, w.ctr, w.bcomb16, w.bmid, (uint64_t)n);
+    if (w.early)
+        hipLaunchKernelGGL(k_ed_comb_hash<true>, dim3(nblk(n, 256)), dim3(256), 0, st, w.comb_list, w.ctr, n, b->key_idx,
+                           b->msg_idx, b->sig_data, b->sig_off, b->sig_len, b->msg_data, b->msg_off, b->msg_len,
+                           b->n_keys, b->n_msgs, b->key_data, b->key_off, b->key_len, abytes, w.bmid);
+    else
+        hipLaunchKernelGGL(k_ed_comb_hash<false>, dim3(nblk(n, 256)), dim3(256), 0, st, w.comb_list, w.ctr, n,
+                           b->key_idx, b->msg_idx, b->sig_data, b->sig_off, b->sig_len, b->msg_data, b->msg_off,
+                           b->msg_len, b->n_keys, b->n_msgs, b->key_data, b->key_off, b->key_len, abytes, w.bmid);
+    hipLaunchKernelGGL(k_ed_comb_bhalf, dim3(nblk(n, 256)), dim3(256), 0, st, w.ctr, w.early ? n : 0, w.bcomb16,
+                       w.bmid);
 }
 void launch_ed_comb_ahalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w) {
     if (!n || !w.max_slots) return;
     const uint32_t blocks = (nblk(n, 256) + 7) & ~7u;   // multiple of 8 for the XCD remap
     hipLaunchKernelGGL(k_ed_comb_ahalf, dim3(blocks), dim3(256), 0, st, w.comb_list, w.ctr, b->key_idx, w.key_slot,
-                       w.ctab, w.bmid, w.xyz, (uint64_t)n);
+                       w.ctab, w.bmid, w.xyz, (uint64_t)n, w.early);
 }
 
 void launch_ed_comb_finish(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w, uint8_t* status) {

@@ -68,7 +68,7 @@ struct chip_ctx {
     hipStream_t stream = nullptr;
     hipStream_t aux = nullptr;                    // second stream: per-key comb tables
     hipStream_t aux2 = nullptr;                   // third stream: ECDSA table fills (while aux doubles on)
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fork2 = nullptr, ev_join2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fork2 = nullptr, ev_join2 = nullptr, ev_kp = nullptr;
     hipEvent_t ev_ec_chain_lo = nullptr, ev_ec_chain_hi = nullptr, ev_ec_lo = nullptr;
     std::recursive_mutex mu;   // recursive: chip_stx_verify holds it across the entries it calls
     std::string err;
@@ -413,6 +413,7 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
         hipEventCreate(&c->tev0) != hipSuccess || hipEventCreate(&c->tev1) != hipSuccess ||
         hipStreamCreateWithPriority(&c->aux, hipStreamNonBlocking, aux_priority()) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&c->ev_kp, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_fork2, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_join2, hipEventDisableTiming) != hipSuccess ||
@@ -489,6 +490,7 @@ void chip_shutdown(chip_ctx* c) {
     hipEventDestroy(c->tev1);
     hipStreamSynchronize(c->aux);
     hipEventDestroy(c->ev_fork);
+    hipEventDestroy(c->ev_kp);
     hipEventDestroy(c->ev_join);
     hipEventDestroy(c->ev_fork2);
     hipEventDestroy(c->ev_join2);
@@ -664,11 +666,31 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         HIPCHK(c, hipMemsetAsync(w.key_count, 0, nk * 4, st));
     }
     KeyMeta* meta = c->meta.as<KeyMeta>();
+    // early (eager tables, device entry): the Ed25519 key prep moves to the aux stream ahead of the table build,
+    // and the challenge hash + [S]B start at once on the main stream over the whole batch (slot = signature
+    // index); classify waits for the key prep (ev_kp)
+    w.early = (comb && w.eager && n && !reuse && !vc && !getenv("CHIP_ED_NO_EARLY")) ? 1u : 0u;
+    if (w.early) {
+        HIPCHK(c, hipEventRecord(c->ev_fork, st));
+        HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+        const int kk = c->kbegin(CHIP_K_KEYPREP, c->aux);
+        launch_ed25519_key_prep(c->aux, nk, b->key_data, b->key_off, b->key_len, meta, c->abytes.as<uint32_t>(),
+                                c->edtab.as<uint32_t>(), w.nega, skip);
+        c->kend(kk, c->aux);
+        HIPCHK(c, hipEventRecord(c->ev_kp, c->aux));
+        const int kt = c->kbegin(CHIP_K_ED_TABLES, c->aux);
+        launch_ed_comb_build(c->aux, n, nk, meta, w);
+        c->kend(kt, c->aux);
+        HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
+        const int kb = c->kbegin(CHIP_K_ED_COMB_B, st);
+        launch_ed_comb_bhalf(st, n, b, c->abytes.as<uint32_t>(), w);
+        c->kend(kb, st);
+    }
     int ke = c->kbegin(CHIP_K_KEYPREP, st);
-    if (!reuse)
+    if (!reuse && !w.early)
         launch_ed25519_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->abytes.as<uint32_t>(),
                                 c->edtab.as<uint32_t>(), comb ? w.nega : nullptr, skip);
-    if (comb && w.eager && n && !reuse) {
+    if (comb && w.eager && n && !reuse && !w.early) {
         // fork: per-key comb tables on the aux stream, concurrent with ECDSA key prep, classify and
         // every table-free kernel on the main stream (the chain is a serial 252-doubling latency)
         HIPCHK(c, hipEventRecord(c->ev_fork, st));
@@ -709,6 +731,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         return CHIP_OK;
     }
     if (vc && vc->data_ready) HIPCHK(c, hipStreamWaitEvent(st, vc->data_ready, 0));
+    if (w.early) HIPCHK(c, hipStreamWaitEvent(st, c->ev_kp, 0));
     if (n) {
         const uint32_t blocks = (uint32_t)((n + CLASSIFY_BLOCK - 1) / CLASSIFY_BLOCK);
         uint32_t* lists = c->lists.as<uint32_t>();
@@ -724,9 +747,11 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
             launch_ed_comb_plan(st, n, nk, ed_list, ed_count, b, meta, w, false);
             launch_ed_comb_plan(st, n, nk, ed_list, ed_count, b, meta, w, true);
             c->kend(ke, st);
-            ke = c->kbegin(CHIP_K_ED_COMB_B, st);
-            launch_ed_comb_bhalf(st, n, b, c->abytes.as<uint32_t>(), w);
-            c->kend(ke, st);
+            if (!w.early) {
+                ke = c->kbegin(CHIP_K_ED_COMB_B, st);
+                launch_ed_comb_bhalf(st, n, b, c->abytes.as<uint32_t>(), w);
+                c->kend(ke, st);
+            }
         }
         const uint64_t mw = ecdsa_comb_mid_words();
         uint32_t* mid_r1 = c->e_mid.as<uint32_t>();

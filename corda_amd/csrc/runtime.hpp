@@ -181,11 +181,13 @@ struct EdCombWs {
     uint32_t* nega;         // [n_keys][40] -A in extended coordinates (key prep)
     uint32_t* fz;           // ED_COMB_AFFINE: [2][max_slots * ED_COMB_AWIN][10] each fill lane's Z product, its inverse
     const uint32_t* skip;   // key-state skip word (CHIP_FLAG_KEY_CACHE) or null: the table build returns at once
-    uint32_t* bmid;         // [40 + ED_COMB_ADW][n] [S]B (extended) + h's digits, bhalf -> ahalf
+    uint32_t* bmid;         // [n][ed_comb_bmid_words()] hand-off rows: [S]B (extended), h's and S's digits
     const uint32_t* bcomb16;  // fixed-base comb of B (per context)
     uint32_t max_slots, min_sigs;
     uint32_t min_total;     // fewer comb-bound signatures than this: all go to Straus (non-eager)
     uint32_t eager;        // tables for every Ed25519 key at slot = key index, built during classify
+    uint32_t early;        // eager device-entry batches: hash and [S]B over the whole batch (slot = signature
+                           // index) from the start, while the key prep and the tables run on the second stream
 };
 
 // slots (partition = false) or the key-grouped work list (partition = true)
