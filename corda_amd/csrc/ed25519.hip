@@ -61,6 +61,10 @@ __global__ void __launch_bounds__(256) k_ed25519_key_prep(uint64_t n_keys, const
     fe_neg(nA.T, A.T);
     fe_carry(nA.T);
     if (nega) ed_store_p3(nega + k * 40, nA);   // -A in extended form: base of the per-key comb (ed25519_comb.hip)
+    if (!table) {   // every signature takes the comb (eager tables): no Straus table
+        meta[k] = m;
+        return;
+    }
     uint32_t* tab = table + k * ED_TAB_WORDS;
     ge_cached c, c1;
     fe_1(c.YpX); fe_1(c.YmX); fe_1(c.Z); fe_0(c.T2d);

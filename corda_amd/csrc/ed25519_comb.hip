@@ -78,7 +78,9 @@ __global__ void __launch_bounds__(256) k_ed_comb_slots(uint64_t n_keys, const Ke
     __shared__ uint32_t s_wave[4], s_base[2];
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t c = k < n_keys ? key_count[k] : 0u;
-    const bool want = k < n_keys && ed_key_ok(meta, (uint32_t)k) && c > 0 && c >= min_sigs;
+    // eager: every valid key has its table, so every one of its signatures takes the comb (no Straus table is
+    // built then)
+    const bool want = k < n_keys && ed_key_ok(meta, (uint32_t)k) && c > 0 && (eager || c >= min_sigs);
     uint32_t tot;
     const uint32_t ex0 = block_scan_excl(want && !eager ? 1u : 0u, s_wave, tot);
     if (threadIdx.x == 0) s_base[0] = tot ? atomicAdd(&ctr[0], tot) : 0u;
@@ -138,8 +140,13 @@ __global__ void __launch_bounds__(256) k_ed_comb_partition(const uint32_t* __res
 }
 
 // ---- per-key tables ----
-// chain: P_w = 2^(W w) (-A) for every window, stashed (extended form) in row 1 of window w.
-// One lane per key: 4 (W) doublings per window, the only serial part of the comb path.
+// chain: P_w = 2^(W w) (-A) for every window, stashed (extended form, 40 words) in the window's last row
+// (affine rows: from row 1 on).  One lane per key: W doublings per window, the only serial part of the comb path.
+#if ED_COMB_AFFINE
+#define ED_COMB_STASH 1
+#else
+#define ED_COMB_STASH (ED_COMB_AENT - 1)
+#endif
 __global__ void __launch_bounds__(64) k_ed_comb_chain(const uint32_t* __restrict__ ctr, uint32_t max_slots,
                                                       uint32_t eager, const KeyMeta* __restrict__ meta,
                                                       const uint32_t* __restrict__ slot_key,
@@ -154,7 +161,7 @@ __global__ void __launch_bounds__(64) k_ed_comb_chain(const uint32_t* __restrict
     ed_load_p3(P, nega + (uint64_t)k * 40);
     uint32_t* tab = ctab + (uint64_t)s * ED_COMB_KEY_WORDS;
     for (int w = 0; w < ED_COMB_AWIN; w++) {
-        ed_store_p3(tab + ((uint32_t)w * ED_COMB_AENT + 1) * ED_COMB_ROW, P);   // 40 words from row 1 on
+        ed_store_p3(tab + ((uint32_t)w * ED_COMB_AENT + ED_COMB_STASH) * ED_COMB_ROW, P);
         if (w + 1 == ED_COMB_AWIN) break;
         ge_p2 r;
         ge_p3_to_p2(r, P);
@@ -184,31 +191,54 @@ CHIP_DEV void ed_store_row(uint32_t* __restrict__ dst, const ge_cached& c) {
     }
 }
 #if !ED_COMB_AFFINE
+// Two lanes per key x window (adjacent lanes of one wave): rows 0..16 from P_w, rows 17..32 from 17 P_w (4
+// doublings + 1 addition first), so the serial chain of additions per lane halves.  Both read the stash in the
+// last row before either writes a row (same wave, the load precedes the divergence); the second writes the
+// last row last.
+#define ED_FILL_SPLIT 2
+#define ED_FILL_ROWS ((ED_COMB_AENT - 1) / ED_FILL_SPLIT)
 __global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict__ ctr, uint32_t max_slots,
                                                       uint32_t eager, const KeyMeta* __restrict__ meta,
                                                       uint32_t* __restrict__ ctab, const uint32_t* __restrict__ skip) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    const uint32_t s = g / ED_COMB_AWIN, w = g % ED_COMB_AWIN;
+    const uint32_t s = g / (ED_COMB_AWIN * ED_FILL_SPLIT), r = g % (ED_COMB_AWIN * ED_FILL_SPLIT);
+    const uint32_t w = r / ED_FILL_SPLIT, h = r % ED_FILL_SPLIT;
     if (s >= (eager ? max_slots : ctr[ED_CTR_NSLOTS]) || (skip && *skip)) return;
     if (eager && !ed_key_ok(meta, s)) return;
     uint32_t* e = ctab + (uint64_t)s * ED_COMB_KEY_WORDS + (uint64_t)w * ED_COMB_AENT * ED_COMB_ROW;
     ge_p3 P;
-    ed_load_p3(P, e + 40);   // P_w, stashed in row +1 by the chain
+    ed_load_p3(P, e + ED_COMB_STASH * ED_COMB_ROW);   // P_w, stashed by the chain
     ge_cached c1, c;
-    fe_1(c.YpX);
-    fe_1(c.YmX);
-    fe_1(c.Z);
-    fe_0(c.T2d);
-    ed_store_row(e, c);
     ge_p3_to_cached(c1, P);
-    ed_store_row(e + 40, c1);
     ge_p3 Q = P;
     ge_p1p1 t;
-    for (int j = 2; j < ED_COMB_AENT; j++) {
+    const uint32_t j0 = 1 + h * ED_FILL_ROWS;
+    if (h == 0) {
+        fe_1(c.YpX);
+        fe_1(c.YmX);
+        fe_1(c.Z);
+        fe_0(c.T2d);
+        ed_store_row(e, c);   // the identity
+    } else {
+        // Q = j0 P = 2^k P + P (j0 - 1 a power of two)
+        ge_p2 q2;
+        ge_p3_to_p2(q2, P);
+        for (uint32_t m = ED_FILL_ROWS * h; m > 2; m >>= 1) {
+            ge_p2_dbl(t, q2);
+            ge_p1p1_to_p2(q2, t);
+        }
+        ge_p2_dbl(t, q2);
+        ge_p1p1_to_p3(Q, t);
         ge_add_cached(t, Q, c1, false);
         ge_p1p1_to_p3(Q, t);
+    }
+    for (uint32_t j = j0; j < j0 + ED_FILL_ROWS; j++) {
+        if (j > j0) {
+            ge_add_cached(t, Q, c1, false);
+            ge_p1p1_to_p3(Q, t);
+        }
         ge_p3_to_cached(c, Q);
-        ed_store_row(e + 40 * j, c);
+        ed_store_row(e + ED_COMB_ROW * j, c);
     }
 }
 #else
@@ -791,8 +821,8 @@ void launch_ed_comb_build(hipStream_t st, uint64_t n, uint64_t n_keys, const Key
     hipLaunchKernelGGL(k_ed_comb_chain, dim3(nblk(w.max_slots, 64)), dim3(64), 0, st, w.ctr, w.max_slots, w.eager, meta,
                        w.slot_key, w.nega, w.ctab, w.skip);
 #if !ED_COMB_AFFINE
-    hipLaunchKernelGGL(k_ed_comb_fill, dim3(nblk((uint64_t)w.max_slots * ED_COMB_AWIN, 256)), dim3(256), 0, st, w.ctr,
-                       w.max_slots, w.eager, meta, w.ctab, w.skip);
+    hipLaunchKernelGGL(k_ed_comb_fill, dim3(nblk((uint64_t)w.max_slots * ED_COMB_AWIN * ED_FILL_SPLIT, 256)), dim3(256), 0,
+                       st, w.ctr, w.max_slots, w.eager, meta, w.ctab, w.skip);
 #else
     const uint64_t lanes = (uint64_t)w.max_slots * ED_COMB_AWIN;
     uint32_t* zprod = w.fz;

@@ -675,7 +675,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
         const int kk = c->kbegin(CHIP_K_KEYPREP, c->aux);
         launch_ed25519_key_prep(c->aux, nk, b->key_data, b->key_off, b->key_len, meta, c->abytes.as<uint32_t>(),
-                                c->edtab.as<uint32_t>(), w.nega, skip);
+                                nullptr, w.nega, skip);   // eager: no signature takes the Straus kernel
         c->kend(kk, c->aux);
         HIPCHK(c, hipEventRecord(c->ev_kp, c->aux));
         const int kt = c->kbegin(CHIP_K_ED_TABLES, c->aux);
@@ -689,7 +689,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     int ke = c->kbegin(CHIP_K_KEYPREP, st);
     if (!reuse && !w.early)
         launch_ed25519_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->abytes.as<uint32_t>(),
-                                c->edtab.as<uint32_t>(), comb ? w.nega : nullptr, skip);
+                                (comb && w.eager) ? nullptr : c->edtab.as<uint32_t>(), comb ? w.nega : nullptr, skip);
     if (comb && w.eager && n && !reuse && !w.early) {
         // fork: per-key comb tables on the aux stream, concurrent with ECDSA key prep, classify and
         // every table-free kernel on the main stream (the chain is a serial 252-doubling latency)
