@@ -27,6 +27,9 @@ __global__ void __launch_bounds__(256) k_ed25519_key_prep(uint64_t n_keys, const
                                                           uint32_t* __restrict__ nega, const uint32_t* __restrict__ skip) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_keys || (skip && *skip)) return;
+#if !ED_NO_PRIO
+    __builtin_amdgcn_s_setprio(3);   // a latency chain per key (the square root) ahead of the comb tables
+#endif
     const uint8_t* p = key_data + key_off[k];
     const uint32_t len = key_len[k];
     bool is_ed = (len == 44);

@@ -155,6 +155,11 @@ __global__ void __launch_bounds__(64) k_ed_comb_chain(const uint32_t* __restrict
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t nslots = eager ? max_slots : ctr[ED_CTR_NSLOTS];
     if (s >= nslots || (skip && *skip)) return;
+    // the serial critical path of the comb path: its few waves win VALU arbitration against the batch-wide
+    // kernels of the main stream that share their SIMDs
+#if !ED_NO_PRIO
+    __builtin_amdgcn_s_setprio(3);
+#endif
     if (eager && !ed_key_ok(meta, s)) return;
     const uint32_t k = eager ? s : slot_key[s];
     ge_p3 P;
@@ -839,8 +844,13 @@ void launch_ed_comb_build(hipStream_t st, uint64_t n, uint64_t n_keys, const Key
 uint64_t ed_comb_bmid_words() { return ED_BMID_W; }
 
 void launch_ed_comb_bhalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, const uint32_t* abytes,
-                          const EdCombWs& w) {
+                          const EdCombWs& w, int part) {
     if (!n || !w.max_slots) return;
+    if (part & 2) {   // [S]B only (its hash launched before)
+        hipLaunchKernelGGL(k_ed_comb_bhalf, dim3(nblk(n, 256)), dim3(256), 0, st, w.ctr, w.early ? n : 0, w.bcomb16,
+                           w.bmid);
+        return;
+    }
     if (w.early)
         hipLaunchKernelGGL(k_ed_comb_hash<true>, dim3(nblk(n, 256)), dim3(256), 0, st, w.comb_list, w.ctr, n, b->key_idx,
                            b->msg_idx, b->sig_data, b->sig_off, b->sig_len, b->msg_data, b->msg_off, b->msg_len,
@@ -849,6 +859,7 @@ void launch_ed_comb_bhalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, c
         hipLaunchKernelGGL(k_ed_comb_hash<false>, dim3(nblk(n, 256)), dim3(256), 0, st, w.comb_list, w.ctr, n,
                            b->key_idx, b->msg_idx, b->sig_data, b->sig_off, b->sig_len, b->msg_data, b->msg_off,
                            b->msg_len, b->n_keys, b->n_msgs, b->key_data, b->key_off, b->key_len, abytes, w.bmid);
+    if (part & 1) return;   // the hash only
     hipLaunchKernelGGL(k_ed_comb_bhalf, dim3(nblk(n, 256)), dim3(256), 0, st, w.ctr, w.early ? n : 0, w.bcomb16,
                        w.bmid);
 }

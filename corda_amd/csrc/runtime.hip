@@ -535,6 +535,21 @@ __global__ void __launch_bounds__(256) k_key_cache(uint64_t nk, const uint8_t* _
     kc_len[k] = len <= KC_MAX ? len : 0xffffffffu;
     if (!eq) *same = 0;   // every writer stores the same value
 }
+// the per-batch counters and per-key scratch zeroed in one launch (separate memsets cost ~6 us each on the
+// critical path): counts[16], ctr[16] (may be null), key_count[nk] (may be null), meta[nk] (clear_meta)
+__global__ void __launch_bounds__(256) k_batch_init(uint64_t nk, uint32_t* __restrict__ counts, uint32_t* __restrict__ ctr,
+                                                    uint32_t* __restrict__ key_count, KeyMeta* __restrict__ meta,
+                                                    uint32_t clear_meta) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t < 16) {
+        counts[t] = 0;
+        if (ctr) ctr[t] = 0;
+    }
+    if (t < nk) {
+        if (key_count) key_count[t] = 0;
+        if (clear_meta) meta[t] = KeyMeta{};
+    }
+}
 // the batch's key metadata cleared before the key preps write it, unless the cached state is reused
 __global__ void __launch_bounds__(256) k_meta_clear(uint64_t nk, KeyMeta* __restrict__ meta, const uint32_t* __restrict__ skip) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -632,7 +647,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         HIPCHK(c, c->e_glist.ensure(2 * n * 4 + 16));
     }
     HIPCHK(c, hipEventRecord(c->ev0, st));
-    HIPCHK(c, hipMemsetAsync(c->counts.p, 0, 64, st));
+    bool clear_meta = false;
     // cross-batch key state: the key preps and table builds skip on the device when the key pool equals the
     // cached one.  Not with per-batch Ed25519 comb slots (non-eager: the slots follow the signatures).
     const uint32_t path = (comb ? (w.eager ? 1u : 3u) : 0u) | (ec_comb ? 4u : 8u);
@@ -656,15 +671,14 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
             c->kc_nk = nk;
             c->kc_gen = c->key_state_gen();
         } else {
-            HIPCHK(c, hipMemsetAsync(c->meta.p, 0, nk * sizeof(KeyMeta), st));
+            clear_meta = true;
             c->kc_valid = false;   // rebuilt for a pool the cache does not describe
         }
     }
     w.skip = skip;
-    if (comb || ec_comb) {
-        HIPCHK(c, hipMemsetAsync(w.ctr, 0, 64, st));
-        HIPCHK(c, hipMemsetAsync(w.key_count, 0, nk * 4, st));
-    }
+    hipLaunchKernelGGL(k_batch_init, dim3((uint32_t)((std::max<uint64_t>(nk, 16) + 255) / 256)), dim3(256), 0, st, nk,
+                       c->counts.as<uint32_t>(), (comb || ec_comb) ? w.ctr : nullptr,
+                       (comb || ec_comb) ? w.key_count : nullptr, c->meta.as<KeyMeta>(), clear_meta ? 1u : 0u);
     KeyMeta* meta = c->meta.as<KeyMeta>();
     // early (eager tables, device entry): the Ed25519 key prep moves to the aux stream ahead of the table build,
     // and the challenge hash + [S]B start at once on the main stream over the whole batch (slot = signature
@@ -682,6 +696,8 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         launch_ed_comb_build(c->aux, n, nk, meta, w);
         c->kend(kt, c->aux);
         HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
+        // (measured: launching [S]B only after classify and the plan, so those small kernels run before the fill
+        // holds the CUs, made the main stream wait for the key prep: 260-264M vs 269-273M)
         const int kb = c->kbegin(CHIP_K_ED_COMB_B, st);
         launch_ed_comb_bhalf(st, n, b, c->abytes.as<uint32_t>(), w);
         c->kend(kb, st);
@@ -796,9 +812,14 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
             ed_list = w.straus_list;
             ed_count = w.ctr + 2;
         }
-        ke = c->kbegin(CHIP_K_ED25519, st);
-        launch_ed25519_verify(st, n, ed_list, ed_count, b, c->abytes.as<uint32_t>(), c->edtab.as<uint32_t>(), status);
-        c->kend(ke, st);
+        // eager comb: every valid Ed25519 key has a table and all its signatures took the comb, so the Straus list
+        // is empty (and no Straus key table was built): no launch
+        if (!(comb && w.eager)) {
+            ke = c->kbegin(CHIP_K_ED25519, st);
+            launch_ed25519_verify(st, n, ed_list, ed_count, b, c->abytes.as<uint32_t>(), c->edtab.as<uint32_t>(),
+                                  status);
+            c->kend(ke, st);
+        }
         if (ec_comb) {
             // u2 Q, both curves per launch: windows 0..31 once the low table half exists, 32..64 after
             HIPCHK(c, hipStreamWaitEvent(st, c->ev_ec_lo, 0));

@@ -203,8 +203,9 @@ uint64_t ed_comb_bmid_words();
 uint64_t ed_bcomb16_words();
 uint64_t ed_bcomb16_scratch_words();
 void launch_ed_bcomb16_build(hipStream_t st, uint32_t* tab, uint32_t* scratch);
+// part: 0 = hash then [S]B, 1 = the hash only, 2 = [S]B only
 void launch_ed_comb_bhalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, const uint32_t* abytes,
-                          const EdCombWs& w);
+                          const EdCombWs& w, int part = 0);
 void launch_ed_comb_ahalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w);
 void launch_ed_comb_finish(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w, uint8_t* status);
 

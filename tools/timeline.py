@@ -1,40 +1,31 @@
-#!/usr/bin/env python3
-"""Print a per-dispatch timeline from a rocprofv3 kernel-trace CSV: the dispatches between two
-occurrences of a marker kernel (one pipeline step), with start offsets, durations, queue, VGPRs and
-scratch.  Usage: timeline.py kt_kernel_trace.csv [--marker k_classify] [--occurrence -1] [--grid N]"""
-import argparse
+"""One cfg2 step's kernel timeline from a rocprofv3 --kernel-trace CSV: the last complete step (delimited by
+k_ed_comb_finish launches), each kernel's start / end relative to the step's first kernel and the idle gaps
+on the device.   python tools/timeline.py <kernel_trace.csv>"""
 import csv
-
-
-def base(name):
-    name = name.split("(", 1)[0].strip()
-    return name[5:] if name.startswith("void ") else name
+import sys
 
 
 def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("csv")
-    ap.add_argument("--marker", default="k_classify")
-    ap.add_argument("--occurrence", type=int, default=-1, help="which marker occurrence starts the step")
-    ap.add_argument("--before", type=int, default=4, help="dispatches shown before the marker")
-    ap.add_argument("--grid", type=int, default=0, help="only markers with this grid size")
-    a = ap.parse_args()
-    rows = sorted(csv.DictReader(open(a.csv)), key=lambda r: int(r["Start_Timestamp"]))
-    marks = [i for i, r in enumerate(rows) if base(r["Kernel_Name"]) == a.marker and
-             (not a.grid or int(r["Grid_Size_X"]) == a.grid)]
-    if not marks:
-        raise SystemExit("marker not found")
-    k = a.occurrence if a.occurrence >= 0 else len(marks) + a.occurrence
-    lo = max(0, marks[k] - a.before)
-    hi = marks[k + 1] - a.before if k + 1 < len(marks) else len(rows)
-    t0 = int(rows[lo]["Start_Timestamp"])
-    end = 0
-    for r in rows[lo:hi]:
-        s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
-        end = max(end, e)
-        print("%9.3f %8.3f ms  q%-3s vgpr %3s scr %5s grid %9s  %s" % ((s - t0) / 1e6, (e - s) / 1e6, r["Queue_Id"],
-              r["VGPR_Count"], r["Scratch_Size"], r["Grid_Size_X"], base(r["Kernel_Name"])[:70]))
-    print("span %.3f ms" % ((end - t0) / 1e6))
+    rows = []
+    for r in csv.DictReader(open(sys.argv[1])):
+        name = r["Kernel_Name"].split("(")[0].replace("void ", "")
+        rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name, int(r.get("Queue_Id", 0) or 0)))
+    rows.sort()
+    fin = [i for i, r in enumerate(rows) if r[2] == "k_ed_comb_finish"]
+    if len(fin) < 3:
+        print("need 3 steps")
+        return
+    a, b = fin[-3] + 1, fin[-2] + 1   # kernels after the previous finish up to this step's finish
+    # include the bitmap after the finish
+    while b < len(rows) and rows[b][2] in ("k_bitmap", "k_ed25519_verify"):
+        b += 1
+    t0 = rows[a][0]
+    busy_end = t0
+    for s, e, n, q in rows[a:b]:
+        gap = max(0, s - busy_end)
+        print("%8.1f %8.1f %7.1f  gap %6.1f  q%d %s" % ((s - t0) / 1e3, (e - t0) / 1e3, (e - s) / 1e3, gap / 1e3, q, n))
+        busy_end = max(busy_end, e)
+    print("step span %.1f us" % ((busy_end - t0) / 1e3))
 
 
 if __name__ == "__main__":
