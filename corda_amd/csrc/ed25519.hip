@@ -20,6 +20,9 @@
 __device__ __constant__ const uint8_t SPKI_ED[12] = {0x30, 0x2a, 0x30, 0x05, 0x06, 0x03, 0x2b, 0x65, 0x70, 0x03, 0x21, 0x00};
 
 // ---- K1b: per unique key.  Ed25519 keys only; other schemes are handled by ecdsa.hip ----
+// TABLE = false (eager comb batches): no Straus table, so the kernel needs a third of the registers and its
+// workgroups find room beside the batch-wide kernels it runs next to
+template <bool TABLE>
 __global__ void __launch_bounds__(256) k_ed25519_key_prep(uint64_t n_keys, const uint8_t* __restrict__ key_data,
                                                           const uint64_t* __restrict__ key_off,
                                                           const uint32_t* __restrict__ key_len, KeyMeta* meta,
@@ -64,7 +67,7 @@ __global__ void __launch_bounds__(256) k_ed25519_key_prep(uint64_t n_keys, const
     fe_neg(nA.T, A.T);
     fe_carry(nA.T);
     if (nega) ed_store_p3(nega + k * 40, nA);   // -A in extended form: base of the per-key comb (ed25519_comb.hip)
-    if (!table) {   // every signature takes the comb (eager tables): no Straus table
+    if (!TABLE) {   // every signature takes the comb (eager tables): no Straus table
         meta[k] = m;
         return;
     }
@@ -252,8 +255,12 @@ void launch_ed25519_key_prep(hipStream_t st, uint64_t n_keys, const uint8_t* key
                              uint32_t* nega, const uint32_t* skip) {
     if (!n_keys) return;
     const uint32_t blocks = (uint32_t)((n_keys + 255) / 256);
-    hipLaunchKernelGGL(k_ed25519_key_prep, dim3(blocks), dim3(256), 0, st, n_keys, key_data, key_off, key_len, meta,
-                       abytes, table, nega, skip);
+    if (table)
+        hipLaunchKernelGGL(k_ed25519_key_prep<true>, dim3(blocks), dim3(256), 0, st, n_keys, key_data, key_off, key_len,
+                           meta, abytes, table, nega, skip);
+    else
+        hipLaunchKernelGGL(k_ed25519_key_prep<false>, dim3(blocks), dim3(256), 0, st, n_keys, key_data, key_off, key_len,
+                           meta, abytes, table, nega, skip);
 }
 
 void launch_ed25519_verify(hipStream_t st, uint64_t n, const uint32_t* list, const uint32_t* count,
