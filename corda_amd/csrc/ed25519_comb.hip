@@ -147,6 +147,11 @@ __global__ void __launch_bounds__(256) k_ed_comb_partition(const uint32_t* __res
 #else
 #define ED_COMB_STASH (ED_COMB_AENT - 1)
 #endif
+#ifndef ED_CHAIN_PAIR
+#define ED_CHAIN_PAIR 0   // 1: the doubling chain on lane pairs (k_ed_comb_chain2): chain 0.60 -> 0.44 ms, but the
+                          // [S]B kernel beside it slowed by as much (0.76 -> 1.2 ms): 263-265M vs 265-269M
+                          // (profiles/r04/ab_chain_pair.txt); the step is issue-bound on its total work
+#endif
 __global__ void __launch_bounds__(64) k_ed_comb_chain(const uint32_t* __restrict__ ctr, uint32_t max_slots,
                                                       uint32_t eager, const KeyMeta* __restrict__ meta,
                                                       const uint32_t* __restrict__ slot_key,
@@ -178,6 +183,105 @@ __global__ void __launch_bounds__(64) k_ed_comb_chain(const uint32_t* __restrict
         }
         ge_p2_dbl(t, r);
         ge_p1p1_to_p3(P, t);
+    }
+}
+
+// The same chain with two lanes per key (adjacent lanes of a wave): each doubling's four squarings and the
+// three / four multiplications of its conversion are split between the pair and the halves exchanged through
+// DPP quad permutes (one v_mov_dpp per word), so the serial chain per key — the critical path of the step
+// once the challenge hash runs beside it — carries about half the field operations per doubling.
+CHIP_DEV uint32_t pair_swap(uint32_t v) {   // the partner lane's v (lanes 2i <-> 2i+1)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+}
+CHIP_DEV void fe_swap_in(fe& out, const fe& mine) {
+#pragma unroll
+    for (int i = 0; i < 10; i++) out.v[i] = pair_swap(mine.v[i]);
+}
+CHIP_DEV void fe_sel(fe& r, uint32_t m, const fe& a, const fe& b) {   // m all-ones: a, else b
+#pragma unroll
+    for (int i = 0; i < 10; i++) r.v[i] = bit_select(m, a.v[i], b.v[i]);
+}
+// one doubling p2 -> p1p1 on a lane pair; odd = all-ones on the odd lane
+CHIP_DEV void ge_p2_dbl_pair(ge_p1p1& r, const ge_p2& p, uint32_t odd) {
+    fe in1, in2, s1, s2, o1, o2, XX, YY, A, Z2, B, t;
+    fe_add(t, p.X, p.Y);
+    fe_sel(in1, odd, p.Y, p.X);   // even: X^2, (X+Y)^2; odd: Y^2, Z^2
+    fe_sel(in2, odd, p.Z, t);
+    fe_sq(s1, in1);
+    fe_sq(s2, in2);
+    fe_swap_in(o1, s1);
+    fe_swap_in(o2, s2);
+    fe_sel(XX, odd, o1, s1);
+    fe_sel(YY, odd, s1, o1);
+    fe_sel(A, odd, o2, s2);
+    fe_sel(Z2, odd, s2, o2);
+    fe_add(B, Z2, Z2);            // 2 Z^2 (loose; r.T is carried below)
+    fe_add(r.Y, YY, XX);
+    fe_sub(r.Z, YY, XX);
+    fe_sub4(r.X, A, r.Y);
+    fe_carry(r.X);
+    fe_add(t, B, XX);
+    fe_sub(r.T, t, YY);
+    fe_carry(r.T);
+}
+// p1p1 -> p2 on a lane pair: even computes X, odd Z, both Y
+CHIP_DEV void ge_p1p1_to_p2_pair(ge_p2& r, const ge_p1p1& p, uint32_t odd) {
+    fe m1, in_a, o;
+    fe_sel(in_a, odd, p.Z, p.X);   // even: X T; odd: Z T
+    fe_mul(m1, in_a, p.T);
+    fe_mul(r.Y, p.Z, p.Y);
+    fe_swap_in(o, m1);
+    fe_sel(r.X, odd, o, m1);
+    fe_sel(r.Z, odd, m1, o);
+}
+// p1p1 -> p3 on a lane pair: even X and Y, odd Z and T
+CHIP_DEV void ge_p1p1_to_p3_pair(ge_p3& r, const ge_p1p1& p, uint32_t odd) {
+    fe a1, b1, a2, b2, m1, m2, o1, o2;
+    fe_sel(a1, odd, p.Z, p.X);     // even: X T, Z Y;  odd: Z T, X Y
+    fe_sel(b1, odd, p.T, p.T);
+    fe_sel(a2, odd, p.X, p.Z);
+    fe_sel(b2, odd, p.Y, p.Y);
+    fe_mul(m1, a1, b1);
+    fe_mul(m2, a2, b2);
+    fe_swap_in(o1, m1);
+    fe_swap_in(o2, m2);
+    fe_sel(r.X, odd, o1, m1);
+    fe_sel(r.Y, odd, o2, m2);
+    fe_sel(r.Z, odd, m1, o1);
+    fe_sel(r.T, odd, m2, o2);
+}
+__global__ void __launch_bounds__(64) k_ed_comb_chain2(const uint32_t* __restrict__ ctr, uint32_t max_slots,
+                                                       uint32_t eager, const KeyMeta* __restrict__ meta,
+                                                       const uint32_t* __restrict__ slot_key,
+                                                       const uint32_t* __restrict__ nega, uint32_t* __restrict__ ctab,
+                                                       const uint32_t* __restrict__ skip) {
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t s = g >> 1;
+    const uint32_t odd = (g & 1u) ? ~0u : 0u;
+    const uint32_t nslots = eager ? max_slots : ctr[ED_CTR_NSLOTS];
+    // both lanes of a pair take the same exits (same key), so the pair stays whole for the DPP exchanges
+    if (s >= nslots || (skip && *skip)) return;
+    if (eager && !ed_key_ok(meta, s)) return;
+#if !ED_NO_PRIO
+    __builtin_amdgcn_s_setprio(3);
+#endif
+    const uint32_t k = eager ? s : slot_key[s];
+    ge_p3 P;
+    ed_load_p3(P, nega + (uint64_t)k * 40);
+    uint32_t* tab = ctab + (uint64_t)s * ED_COMB_KEY_WORDS;
+    for (int w = 0; w < ED_COMB_AWIN; w++) {
+        if (!odd) ed_store_p3(tab + ((uint32_t)w * ED_COMB_AENT + ED_COMB_STASH) * ED_COMB_ROW, P);
+        if (w + 1 == ED_COMB_AWIN) break;
+        ge_p2 r;
+        ge_p3_to_p2(r, P);
+        ge_p1p1 t;
+#pragma unroll 1
+        for (int b = 0; b < ED_COMB_W - 1; b++) {
+            ge_p2_dbl_pair(t, r, odd);
+            ge_p1p1_to_p2_pair(r, t, odd);
+        }
+        ge_p2_dbl_pair(t, r, odd);
+        ge_p1p1_to_p3_pair(P, t, odd);
     }
 }
 
@@ -823,8 +927,13 @@ void launch_ed_comb_plan(hipStream_t st, uint64_t n, uint64_t n_keys, const uint
 
 void launch_ed_comb_build(hipStream_t st, uint64_t n, uint64_t n_keys, const KeyMeta* meta, const EdCombWs& w) {
     if (!n || !n_keys || !w.max_slots) return;
+#if ED_CHAIN_PAIR
+    hipLaunchKernelGGL(k_ed_comb_chain2, dim3(nblk((uint64_t)w.max_slots * 2, 64)), dim3(64), 0, st, w.ctr, w.max_slots,
+                       w.eager, meta, w.slot_key, w.nega, w.ctab, w.skip);
+#else
     hipLaunchKernelGGL(k_ed_comb_chain, dim3(nblk(w.max_slots, 64)), dim3(64), 0, st, w.ctr, w.max_slots, w.eager, meta,
                        w.slot_key, w.nega, w.ctab, w.skip);
+#endif
 #if !ED_COMB_AFFINE
     hipLaunchKernelGGL(k_ed_comb_fill, dim3(nblk((uint64_t)w.max_slots * ED_COMB_AWIN * ED_FILL_SPLIT, 256)), dim3(256), 0,
                        st, w.ctr, w.max_slots, w.eager, meta, w.ctab, w.skip);

@@ -6,6 +6,6 @@ timeout -k 10 400 python -u -m pytest -x -q --timeout 150 --timeout-method threa
 tail -1 $OUT/t.log
 export TAG=${1:-r04m} STEPS=10
 for r in 1 2 3; do
-  timeout -k 10 300 bash tools/ab_lib.sh build_ab/noprio/libcordahip.so build_ab/head/libcordahip.so || exit 1
+  timeout -k 10 300 bash tools/ab_lib.sh - build_ab/nopair/libcordahip.so || exit 1
 done
-CORDAHIP_LIB=$PWD/build_ab/noprio/libcordahip.so timeout -k 10 400 bash tools/gpu_tl.sh ${1:-r04m}_tl | tail -30
+timeout -k 10 400 bash tools/gpu_tl.sh ${1:-r04m}_tl | tail -30
