@@ -140,6 +140,10 @@ struct Sink {   // dword-accumulating byte writer into the output pool
     uint8_t* base;
     uint64_t pos;
     uint32_t acc;
+    uint32_t nx;          // chunk-spanning runs recorded as copy descriptors (pass 2): descriptor j of this tx at
+    uint4* xa;            //   xa[j * xs], xb[j * xs] (lane-major), the first KRYO_XD of them; null = copy in place
+    uint2* xb;
+    uint64_t xs;
     __device__ __forceinline__ void put(uint8_t b) {
         acc |= (uint32_t)b << (8 * (pos & 3));
         pos++;
@@ -159,6 +163,12 @@ struct Sink {   // dword-accumulating byte writer into the output pool
 // reads the structure through a 16-byte register window and every bulk compare loads 16 bytes per request
 // (ld_dwords below), never a dword at a time.
 #define KRYO_BLOCK 256
+#ifndef KRYO_DEFER_COPY
+#define KRYO_DEFER_COPY 1   // pass 2's chunk-spanning runs copied by k_stx_dechunk (whole lines) instead of per lane
+#endif
+#ifndef KRYO_NO_EXTRA_COPY
+#define KRYO_NO_EXTRA_COPY 0
+#endif
 #ifndef KRYO_NO_STORES
 #define KRYO_NO_STORES 0   // timing experiments only: pass 2 without its index stores (wrong outputs)
 #endif
@@ -511,9 +521,21 @@ template <bool EMIT> __device__ __forceinline__ uint64_t run1(Cur& c, uint32_t n
         return at;
     }
     extra += (n + 3) & ~3u;
-    if (!EMIT) {
+    if (!EMIT || KRYO_NO_EXTRA_COPY) {   // (KRYO_NO_EXTRA_COPY: timing experiments only, the extra region stays unwritten)
         c.skip<1>(n);
-        return 0;
+        return EMIT ? sink.pos : 0;
+    }
+    if (sink.xa && sink.nx < KRYO_XD) {
+        // a copy descriptor instead of this lane's partial-line stores: k_stx_dechunk moves the bytes a wave at a
+        // time (whole lines) after the pass; the walk here only validates the chunk chain and advances
+        const uint64_t at = sink.pos;
+        sink.xa[(uint64_t)sink.nx * sink.xs] = make_uint4((uint32_t)at, (uint32_t)(at >> 32), (uint32_t)c.pos,
+                                                          (uint32_t)(c.pos >> 32));
+        sink.xb[(uint64_t)sink.nx * sink.xs] = make_uint2(n, c.rem1);
+        sink.nx++;
+        c.skip<1>(n);
+        sink.pos += (n + 3) & ~3u;   // the run and its zero padding to a dword (written by the copy)
+        return at;
     }
     // de-chunk piece by piece: bytes until the sink is dword aligned, then dword copies (unaligned
     // source loads from the pool copy), then the tail
@@ -734,7 +756,34 @@ struct Outs {   // pass-2 destinations (NULL in pass 1)
     uint32_t *lm_len, *lm_int, *lm_grp;
     uint64_t* lm_soff;
     uint32_t *lm_slen, *lm_tmpl;
+    uint4* xd_a;                   // chunk-spanning runs as copy descriptors (StxOut), k_stx_dechunk
+    uint2* xd_b;
+    uint32_t* xd_n;
 };
+
+// the required-key walk's count and its first STX_REC signer entries for tx t (components in the pool); st may
+// become UNSUPPORTED (a key the walk cannot read, more than 64 signer entries: the JVM path)
+__device__ __forceinline__ void stx_req_tail(Cur& c, uint64_t t, int& st, uint64_t cbase, uint64_t comps, const Outs& o) {
+    uint64_t cnt = 0, all = 0;
+    bool over = false;
+    if (st == CHIP_STX_OK &&
+        !req_walk(c, o.pool, o.pool_bytes, cbase, cbase + comps,
+                  CompAcc{o.comp_group, o.comp_off, o.comp_len, o.lm_grp, o.lm_off, o.lm_len, o.n_lm, t, cbase}, o.reg,
+                  [&](uint64_t at, uint32_t len, bool req) {
+                      if (req) {
+                          over |= cnt >= 64;
+                          cnt++;
+                      }
+                      if (all < STX_REC) {   // recorded: k_stx_required then needs no third walk
+                          o.rec_off[t * STX_REC + all] = at;
+                          o.rec_len[t * STX_REC + all] = len | (req ? 0x80000000u : 0u);
+                      }
+                      all++;
+                  }))
+        st = CHIP_STX_UNSUPPORTED;
+    if (over) st = CHIP_STX_UNSUPPORTED;
+    o.nraw[t] = st == CHIP_STX_OK ? all : 0;
+}
 
 template <bool EMIT>
 __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint8_t* __restrict__ data,
@@ -746,11 +795,13 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
     if (t >= n) return;
     if (EMIT && status[t] != CHIP_STX_OK) {
         if (o.nraw) o.nraw[t] = 0;
+        if (o.xd_a) o.xd_n[t] = 0;
         return;
     }
     const uint64_t a = off[t], b = a + len[t];
     uint64_t comps = 0, sigs = 0, extra = 0;
-    Sink sink{o.pool, EMIT ? o.extra_base + o.extra_start[t] : 0, 0};
+    Sink sink{o.pool, EMIT ? o.extra_base + o.extra_start[t] : 0, 0, 0, EMIT && o.xd_a ? o.xd_a + t : nullptr,
+              EMIT && o.xd_a ? o.xd_b + t : nullptr, n};
     uint64_t cbase = EMIT ? o.comp_start[t] : 0, sbase = EMIT ? o.sig_start[t] : 0;
     int st = CHIP_STX_OK;
     Cur c;
@@ -969,26 +1020,12 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
 done:
     if (EMIT) {
         sink.flush();
-        if (o.nraw) {   // the required-key walk's count, fused here (the components are in the pool now)
-            uint64_t cnt = 0, all = 0;
-            bool over = false;
-            if (st == CHIP_STX_OK &&
-                !req_walk(c, o.pool, o.pool_bytes, cbase, cbase + comps,
-                          CompAcc{o.comp_group, o.comp_off, o.comp_len, o.lm_grp, o.lm_off, o.lm_len, o.n_lm, t, cbase}, o.reg,
-                          [&](uint64_t at, uint32_t len, bool req) {
-                              if (req) {
-                                  over |= cnt >= 64;
-                                  cnt++;
-                              }
-                              if (all < STX_REC) {   // recorded: k_stx_required then needs no third walk
-                                  o.rec_off[t * STX_REC + all] = at;
-                                  o.rec_len[t * STX_REC + all] = len | (req ? 0x80000000u : 0u);
-                              }
-                              all++;
-                          }))
-                st = CHIP_STX_UNSUPPORTED;
-            if (over) st = CHIP_STX_UNSUPPORTED;   // more than 64 signer entries: JVM path
-            o.nraw[t] = st == CHIP_STX_OK ? all : 0;
+        if (o.xd_a) {
+            // the copies are deferred to k_stx_dechunk, and the required-key walk, which reads the components from
+            // the pool, to k_stx_req_tail after it
+            o.xd_n[t] = st == CHIP_STX_OK ? sink.nx : 0;
+        } else if (o.nraw) {   // the required-key walk's count, fused here (the components are in the pool now)
+            stx_req_tail(c, t, st, cbase, comps, o);
         }
         if (st != CHIP_STX_OK) status[t] = (uint8_t)st;
     } else {
@@ -1498,14 +1535,79 @@ __global__ void __launch_bounds__(256) k_stx_lm_sigs(uint64_t n, uint64_t nsig, 
     o.tx_idx[s] = (uint32_t)t;
 }
 
+// pass 2's chunk-spanning runs, a wave per transaction: each run's pieces (the bytes left in the chunk where it
+// starts, then whole chunks behind their varint headers) copied a byte per lane, 64 consecutive bytes per
+// instruction (whole lines), then the run's zero padding to a dword
+// (the pass validated every recorded chain; the bounds checks here only keep a bad descriptor inside the pool)
+__global__ void __launch_bounds__(256) k_stx_dechunk(uint64_t n, uint8_t* __restrict__ pool, uint64_t pool_bytes,
+                                                     const uint4* __restrict__ xa, const uint2* __restrict__ xb,
+                                                     const uint32_t* __restrict__ xn) {
+    const uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+    const uint32_t lane = threadIdx.x & 63u;
+    if (t >= n) return;
+    uint32_t cnt = __builtin_amdgcn_readfirstlane(xn[t]);
+    cnt = cnt < KRYO_XD ? cnt : KRYO_XD;
+    for (uint32_t j = 0; j < cnt; j++) {
+        const uint4 a = xa[(uint64_t)j * n + t];
+        const uint2 b = xb[(uint64_t)j * n + t];
+        uint64_t dst = (uint64_t)a.x | ((uint64_t)a.y << 32), src = (uint64_t)a.z | ((uint64_t)a.w << 32);
+        uint32_t left = b.x, rem = b.y;
+        const uint32_t pad = (4u - (b.x & 3u)) & 3u;
+        if (dst > pool_bytes || pool_bytes - dst < (uint64_t)left + pad) return;
+        while (left) {
+            if (rem == 0) {   // the next chunk's length (varint)
+                uint32_t v = 0;
+                for (int sh = 0; sh < 35 && src < pool_bytes; sh += 7) {
+                    const uint8_t x = pool[src++];
+                    v |= (uint32_t)(x & 0x7f) << sh;
+                    if (!(x & 0x80)) break;
+                }
+                rem = v;
+                if (rem == 0) return;
+            }
+            const uint32_t k = left < rem ? left : rem;
+            if (src > pool_bytes || pool_bytes - src < k) return;
+            for (uint32_t o = lane; o < k; o += 64) pool[dst + o] = pool[src + o];
+            dst += k;
+            src += k;
+            rem -= k;
+            left -= k;
+        }
+        if (lane < pad) pool[dst + lane] = 0;
+    }
+}
+// the required-key walk of every parsed transaction, once k_stx_dechunk has filled the extra region
+__global__ void __launch_bounds__(256) k_stx_req_tail(uint64_t n, const uint8_t* __restrict__ data, uint64_t data_bytes,
+                                                      uint8_t* __restrict__ status, Outs o) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    if (status[t] != CHIP_STX_OK) {
+        o.nraw[t] = 0;
+        return;
+    }
+    int st = CHIP_STX_OK;
+    Cur c;
+    c.init(data, data_bytes, 0, 0);
+    const uint64_t cbase = o.comp_start[t];
+    stx_req_tail(c, t, st, cbase, o.comp_start[t + 1] - cbase, o);
+    if (st != CHIP_STX_OK) status[t] = (uint8_t)st;
+}
+
 void launch_stx_emit(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_registry& reg, uint8_t* status,
                      const StxOut& d) {
     if (!in->n) return;
     Outs o{d.pool, d.pool_bytes, d.extra_start, d.extra_base, d.salts, d.comp_start, d.comp_group, d.comp_internal, d.comp_off, d.comp_len, d.sig_start,
            d.tx_idx, d.tmpl_idx, d.sig_off, d.sig_len, d.skey_off, d.skey_len, d.meta, d.n_meta, d.nraw, reg,
-           d.rec_off, d.rec_len, in->n, d.lm_off, d.lm_len, d.lm_int, d.lm_grp, d.lm_soff, d.lm_slen, d.lm_tmpl};
+           d.rec_off, d.rec_len, in->n, d.lm_off, d.lm_len, d.lm_int, d.lm_grp, d.lm_soff, d.lm_slen, d.lm_tmpl,
+           KRYO_DEFER_COPY ? d.xd_a : nullptr, d.xd_b, d.xd_n};
     hipLaunchKernelGGL(k_stx_parse<true>, grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->off, in->len,
                        in->data_bytes, status, nullptr, nullptr, nullptr, o);
+    if (o.xd_a) {
+        hipLaunchKernelGGL(k_stx_dechunk, grid_of(in->n * 64), dim3(256), 0, st, in->n, d.pool, d.pool_bytes, d.xd_a, d.xd_b, d.xd_n);
+        if (o.nraw)
+            hipLaunchKernelGGL(k_stx_req_tail, grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->data_bytes, status,
+                               o);
+    }
     if (d.ncomp)
         hipLaunchKernelGGL(k_stx_lm_comps, grid_of(d.ncomp), dim3(256), 0, st, in->n, d.ncomp, d.comp_start, o);
     if (d.nsig)

@@ -42,7 +42,7 @@ struct DevBuf {
 // buffers of one Kryo front-end call (chip_stx_parse_device): counts, ranges, pool, batches, key
 // interning, required keys, scan scratch
 struct StxBufs {
-    DevBuf s_ncomp, s_nsig, s_nbytes, s_cstart, s_sstart, s_pstart, s_pool, s_salts, s_cgroup, s_cint, s_coff, s_clen, s_txidx, s_tmpl, s_soff, s_slen, s_skoff, s_sklen, s_meta, s_tab, s_tabmin, s_kslot, s_krep, s_kflag, s_kincl, s_kidx, s_koff, s_klen, s_temp, r_nraw, r_rstart, r_kid, r_len, r_keep, r_kincl, r_off, r_nreq, r_qstart, r_nstart, r_val, r_nk, r_w, r_flag, r_tx, r_nn, r_nc, r_ninc, r_cinc, k_off, k_len, k_kind, k_ok, k_tx, r_tot, r_roff, r_rlen, lm_off, lm_len, lm_int, lm_grp, lm_soff, lm_slen, lm_tmpl;
+    DevBuf s_ncomp, s_nsig, s_nbytes, s_cstart, s_sstart, s_pstart, s_pool, s_salts, s_cgroup, s_cint, s_coff, s_clen, s_txidx, s_tmpl, s_soff, s_slen, s_skoff, s_sklen, s_meta, s_tab, s_tabmin, s_kslot, s_krep, s_kflag, s_kincl, s_kidx, s_koff, s_klen, s_temp, r_nraw, r_rstart, r_kid, r_len, r_keep, r_kincl, r_off, r_nreq, r_qstart, r_nstart, r_val, r_nk, r_w, r_flag, r_tx, r_nn, r_nc, r_ninc, r_cinc, k_off, k_len, k_kind, k_ok, k_tx, r_tot, r_roff, r_rlen, lm_off, lm_len, lm_int, lm_grp, lm_soff, lm_slen, lm_tmpl, xd_a, xd_b, xd_n;
     hipStream_t cs = nullptr;                     // the blob copy into s_pool, overlapping pass 1
     hipEvent_t ce0 = nullptr, ce1 = nullptr;
     void release() {
@@ -51,7 +51,7 @@ struct StxBufs {
         if (ce1) (void)hipEventDestroy(ce1);
         cs = nullptr;
         ce0 = ce1 = nullptr;
-        for (DevBuf* b : {&s_ncomp, &s_nsig, &s_nbytes, &s_cstart, &s_sstart, &s_pstart, &s_pool, &s_salts, &s_cgroup, &s_cint, &s_coff, &s_clen, &s_txidx, &s_tmpl, &s_soff, &s_slen, &s_skoff, &s_sklen, &s_meta, &s_tab, &s_tabmin, &s_kslot, &s_krep, &s_kflag, &s_kincl, &s_kidx, &s_koff, &s_klen, &s_temp, &r_nraw, &r_rstart, &r_kid, &r_len, &r_keep, &r_kincl, &r_off, &r_nreq, &r_qstart, &r_nstart, &r_val, &r_nk, &r_w, &r_flag, &r_tx, &r_nn, &r_nc, &r_ninc, &r_cinc, &k_off, &k_len, &k_kind, &k_ok, &k_tx, &r_tot, &r_roff, &r_rlen, &lm_off, &lm_len, &lm_int, &lm_grp, &lm_soff, &lm_slen, &lm_tmpl}) b->release();
+        for (DevBuf* b : {&s_ncomp, &s_nsig, &s_nbytes, &s_cstart, &s_sstart, &s_pstart, &s_pool, &s_salts, &s_cgroup, &s_cint, &s_coff, &s_clen, &s_txidx, &s_tmpl, &s_soff, &s_slen, &s_skoff, &s_sklen, &s_meta, &s_tab, &s_tabmin, &s_kslot, &s_krep, &s_kflag, &s_kincl, &s_kidx, &s_koff, &s_klen, &s_temp, &r_nraw, &r_rstart, &r_kid, &r_len, &r_keep, &r_kincl, &r_off, &r_nreq, &r_qstart, &r_nstart, &r_val, &r_nk, &r_w, &r_flag, &r_tx, &r_nn, &r_nc, &r_ninc, &r_cinc, &k_off, &k_len, &k_kind, &k_ok, &k_tx, &r_tot, &r_roff, &r_rlen, &lm_off, &lm_len, &lm_int, &lm_grp, &lm_soff, &lm_slen, &lm_tmpl, &xd_a, &xd_b, &xd_n}) b->release();
     }
 };
 
@@ -1411,6 +1411,12 @@ static int stx_parse(chip_ctx* c, StxBufs& B, const chip_stx_blobs* in, uint8_t*
     d.lm_soff = B.lm_soff.as<uint64_t>();
     d.lm_slen = B.lm_slen.as<uint32_t>();
     d.lm_tmpl = B.lm_tmpl.as<uint32_t>();
+    HIPCHK(c, B.xd_a.ensure(n * KRYO_XD * 16 + 16));
+    HIPCHK(c, B.xd_b.ensure(n * KRYO_XD * 8 + 16));
+    HIPCHK(c, B.xd_n.ensure(n * 4 + 16));
+    d.xd_a = B.xd_a.as<uint4>();
+    d.xd_b = B.xd_b.as<uint2>();
+    d.xd_n = B.xd_n.as<uint32_t>();
     // pass 2: the batches; then the signer keys interned
     launch_stx_emit(st, in, reg, tx_status, d);
     HIPCHK(c, hipGetLastError());

@@ -96,9 +96,16 @@ struct StxOut {
     uint32_t *lm_len, *lm_int, *lm_grp;
     uint64_t* lm_soff;             // [KRYO_LM_S * n]
     uint32_t *lm_slen, *lm_tmpl;
+    // chunk-spanning runs of pass 2 as copy descriptors (lane-major: run j of tx t at [j * n + t], the first
+    // KRYO_XD of each tx; more are copied by the lane itself): (extra-region offset, source offset) and (length,
+    // bytes left in the source's current chunk); k_stx_dechunk then moves them a wave per transaction
+    uint4* xd_a;
+    uint2* xd_b;
+    uint32_t* xd_n;                // [n] descriptors of tx t (0 for a failed tx)
 };
 #define KRYO_LM_C 16
 #define KRYO_LM_S 4
+#define KRYO_XD 8
 void launch_stx_count(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_registry& reg, uint8_t* status,
                       uint64_t* ncomp, uint64_t* nsig, uint64_t* nextra);
 void launch_stx_emit(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_registry& reg, uint8_t* status,
