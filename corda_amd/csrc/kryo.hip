@@ -1535,10 +1535,64 @@ __global__ void __launch_bounds__(256) k_stx_lm_sigs(uint64_t n, uint64_t nsig, 
     o.tx_idx[s] = (uint32_t)t;
 }
 
-// pass 2's chunk-spanning runs, a wave per transaction: each run's pieces (the bytes left in the chunk where it
-// starts, then whole chunks behind their varint headers) copied a byte per lane, 64 consecutive bytes per
-// instruction (whole lines), then the run's zero padding to a dword
-// (the pass validated every recorded chain; the bounds checks here only keep a bad descriptor inside the pool)
+// one piece of a de-chunked run, by the whole wave: head bytes up to a dword-aligned destination, then 16
+// destination bytes per lane (a 4-byte-aligned dwordx4 + one dword from the source, realigned with
+// v_alignbyte; 1 KB per wave instruction), then the tail bytes
+__device__ __forceinline__ void dechunk_piece(uint8_t* __restrict__ pool, uint64_t d, uint64_t s, uint32_t k,
+                                              uint32_t lane) {
+    uint32_t h = (4u - (uint32_t)(d & 3)) & 3u;
+    h = h < k ? h : k;
+    if (lane < h) pool[d + lane] = pool[s + lane];
+    d += h;
+    s += h;
+    k -= h;
+    const uint32_t body = k & ~3u;
+    for (uint32_t off = lane * 16; off < body; off += 1024) {
+        const uint64_t sa = s + off, al = sa & ~3ull;
+        const uint32_t sh = (uint32_t)(sa & 3);
+        const u32x4a4 w = *reinterpret_cast<const u32x4a4*>(pool + al);
+        const uint32_t w4 = *reinterpret_cast<const uint32_t*>(pool + al + 16);
+        uint32_t o[4];
+        o[0] = __builtin_amdgcn_alignbyte(w.y, w.x, sh);
+        o[1] = __builtin_amdgcn_alignbyte(w.z, w.y, sh);
+        o[2] = __builtin_amdgcn_alignbyte(w.w, w.z, sh);
+        o[3] = __builtin_amdgcn_alignbyte(w4, w.w, sh);
+        const uint32_t m = body - off;
+        if (m >= 16) {
+            u32x4a4 v;
+            v.x = o[0];
+            v.y = o[1];
+            v.z = o[2];
+            v.w = o[3];
+            *reinterpret_cast<u32x4a4*>(pool + d + off) = v;
+        } else {
+            for (uint32_t q = 0; q < m / 4; q++) reinterpret_cast<uint32_t*>(pool + d + off)[q] = o[q];
+        }
+    }
+    const uint32_t tl = k & 3u;
+    if (lane < tl) pool[d + body + lane] = pool[s + body + lane];
+}
+__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t j) {
+    return (uint64_t)__builtin_amdgcn_readlane((uint32_t)v, j) | ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), j) << 32);
+}
+// a chunk header (varint) at s, the same bytes read by every lane; 0 = bad
+__device__ __forceinline__ uint32_t dechunk_header(const uint8_t* pool, uint64_t pool_bytes, uint64_t& s) {
+    uint32_t v = 0;
+    for (int sh = 0; sh < 35; sh += 7) {
+        if (s >= pool_bytes) return 0;
+        const uint8_t x = pool[s++];
+        v |= (uint32_t)(x & 0x7f) << sh;
+        if (!(x & 0x80)) break;
+    }
+    return v;
+}
+
+// pass 2's chunk-spanning runs, a wave per transaction.  Lane j loads run j's descriptor and the chunk header
+// behind its first piece (every recorded run spans a chunk boundary: at least two pieces), so those
+// dependent loads overlap across the runs; then the wave copies run after run, piece after piece
+// (dechunk_piece), a third and later piece (a run over more than a whole chunk) walking its headers, and
+// the run's zero padding to a dword.  (The pass validated every recorded chain; the bounds checks only keep
+// a bad descriptor inside the pool.)
 __global__ void __launch_bounds__(256) k_stx_dechunk(uint64_t n, uint8_t* __restrict__ pool, uint64_t pool_bytes,
                                                      const uint4* __restrict__ xa, const uint2* __restrict__ xb,
                                                      const uint32_t* __restrict__ xn) {
@@ -1547,33 +1601,46 @@ __global__ void __launch_bounds__(256) k_stx_dechunk(uint64_t n, uint8_t* __rest
     if (t >= n) return;
     uint32_t cnt = __builtin_amdgcn_readfirstlane(xn[t]);
     cnt = cnt < KRYO_XD ? cnt : KRYO_XD;
+    uint64_t dst = 0, src = 0, src2 = 0;
+    uint32_t len = 0, rem = 0, rem2 = 0;
+    if (lane < cnt) {
+        const uint4 a = xa[(uint64_t)lane * n + t];
+        const uint2 b = xb[(uint64_t)lane * n + t];
+        dst = (uint64_t)a.x | ((uint64_t)a.y << 32);
+        src = (uint64_t)a.z | ((uint64_t)a.w << 32);
+        len = b.x;
+        rem = b.y;
+        src2 = src + rem;
+        if (rem < len && src2 < pool_bytes) rem2 = dechunk_header(pool, pool_bytes, src2);
+    }
     for (uint32_t j = 0; j < cnt; j++) {
-        const uint4 a = xa[(uint64_t)j * n + t];
-        const uint2 b = xb[(uint64_t)j * n + t];
-        uint64_t dst = (uint64_t)a.x | ((uint64_t)a.y << 32), src = (uint64_t)a.z | ((uint64_t)a.w << 32);
-        uint32_t left = b.x, rem = b.y;
-        const uint32_t pad = (4u - (b.x & 3u)) & 3u;
-        if (dst > pool_bytes || pool_bytes - dst < (uint64_t)left + pad) return;
+        uint64_t d = rl64(dst, j), s = rl64(src, j);
+        const uint64_t s2 = rl64(src2, j);
+        uint32_t left = __builtin_amdgcn_readlane(len, j), r = __builtin_amdgcn_readlane(rem, j);
+        const uint32_t r2 = __builtin_amdgcn_readlane(rem2, j);
+        const uint32_t pad = (4u - (left & 3u)) & 3u;
+        if (r == 0 || r >= left || r2 == 0 || d > pool_bytes || pool_bytes - d < (uint64_t)left + pad ||
+            s > pool_bytes || pool_bytes - s < r || s2 > pool_bytes)
+            return;
+        dechunk_piece(pool, d, s, r, lane);
+        d += r;
+        left -= r;
+        s = s2;
+        r = r2;
         while (left) {
-            if (rem == 0) {   // the next chunk's length (varint)
-                uint32_t v = 0;
-                for (int sh = 0; sh < 35 && src < pool_bytes; sh += 7) {
-                    const uint8_t x = pool[src++];
-                    v |= (uint32_t)(x & 0x7f) << sh;
-                    if (!(x & 0x80)) break;
-                }
-                rem = v;
-                if (rem == 0) return;
+            if (r == 0) {
+                r = dechunk_header(pool, pool_bytes, s);
+                if (r == 0) return;
             }
-            const uint32_t k = left < rem ? left : rem;
-            if (src > pool_bytes || pool_bytes - src < k) return;
-            for (uint32_t o = lane; o < k; o += 64) pool[dst + o] = pool[src + o];
-            dst += k;
-            src += k;
-            rem -= k;
+            const uint32_t k = left < r ? left : r;
+            if (pool_bytes - s < k) return;
+            dechunk_piece(pool, d, s, k, lane);
+            d += k;
+            s += k;
+            r -= k;
             left -= k;
         }
-        if (lane < pad) pool[dst + lane] = 0;
+        if (lane < pad) pool[d + lane] = 0;
     }
 }
 // the required-key walk of every parsed transaction, once k_stx_dechunk has filled the extra region
