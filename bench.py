@@ -229,10 +229,13 @@ def profile_issue(kernel, grid):
     return None
 
 
-def stx_traffic(grid_tx, grid_sig):
+def stx_traffic(ntx, nsig):
     """FETCH_SIZE + WRITE_SIZE of one Kryo front-end call (both parse passes, the key interning and the
     required-key passes; the pool copy is a DMA, not counted) from the committed PMC profile, or None."""
-    parts = [profile_traffic(k, grid_tx) for k in ("k_stx_parse<false>", "k_stx_parse<true>", "k_stx_required")]
+    grid_tx, grid_sig = (ntx + 255) // 256 * 256, (nsig + 255) // 256 * 256
+    parts = [profile_traffic(k, grid_tx) for k in ("k_stx_parse<false>", "k_stx_parse<true>", "k_stx_req_tail",
+                                                   "k_stx_required")]
+    parts.append(profile_traffic("k_stx_dechunk", (ntx * 64 + 255) // 256 * 256))   # a wave per transaction
     parts += [profile_traffic(k, grid_sig) for k in ("k_stx_key_insert", "k_stx_key_flag", "k_stx_key_assign",
                                                       "k_stx_req_entry<false>", "k_stx_req_entry<true>")]
     return None if any(p is None for p in parts) else sum(parts)
@@ -670,7 +673,7 @@ def main():
             "stx_parse_roofline": {"bound": "hbm", "achieved": alg / (parse_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                                    "unit": "GB/s", "frac": alg / (parse_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                    "algorithmic_bytes": alg,
-                                   "traffic": stx_traffic((tb.ntx + 255) // 256 * 256, (sb.n + 255) // 256 * 256),
+                                   "traffic": stx_traffic(tb.ntx, sb.n),
                                    "note": "one launch = both parse passes, the pool copy, scans, key interning "
                                            "and the required-key pass with their 3 host syncs"},
         })

@@ -1572,8 +1572,11 @@ __device__ __forceinline__ void dechunk_piece(uint8_t* __restrict__ pool, uint64
     const uint32_t tl = k & 3u;
     if (lane < tl) pool[d + body + lane] = pool[s + body + lane];
 }
+// (the builtin returns int: each half goes through uint32_t, or an offset >= 2 GiB would sign-extend)
 __device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t j) {
-    return (uint64_t)__builtin_amdgcn_readlane((uint32_t)v, j) | ((uint64_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), j) << 32);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)v, j);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), j);
+    return (uint64_t)lo | ((uint64_t)hi << 32);
 }
 // a chunk header (varint) at s, the same bytes read by every lane; 0 = bad
 __device__ __forceinline__ uint32_t dechunk_header(const uint8_t* pool, uint64_t pool_bytes, uint64_t& s) {

@@ -74,9 +74,13 @@ def main():
         fm = torch.empty(2 * a.n + 16, dtype=torch.uint8, device=dev)
         ctx.verify_signed_tx_parsed_device(p, dm, None, ids, fst, fv, fa, fm, stream=stream.cuda_stream)
         torch.cuda.synchronize(dev)
-        out["verify_correct"] = bool(np.array_equal(fv.cpu().numpy(), want_v)) and \
-            bool(np.array_equal(fa.cpu().numpy().view(np.uint32), want_a)) and \
-            bool(np.array_equal(ids.cpu().numpy().reshape(-1, 32), ids_ref))
+        ids_ok = np.all(ids.cpu().numpy().reshape(-1, 32) == ids_ref, axis=1)
+        fv_ok = fv.cpu().numpy() == want_v
+        out["verify_correct"] = bool(fv_ok.all()) and \
+            bool(np.array_equal(fa.cpu().numpy().view(np.uint32), want_a)) and bool(ids_ok.all())
+        out["ids_wrong"] = int((~ids_ok).sum())
+        out["verdicts_wrong"] = int((~fv_ok).sum())
+        out["sigs_wrong"] = int((fst.cpu().numpy() != sb.expected).sum())
     print(json.dumps(out))
     ctx.close()
 
