@@ -166,6 +166,9 @@ struct Sink {   // dword-accumulating byte writer into the output pool
 #ifndef KRYO_DEFER_COPY
 #define KRYO_DEFER_COPY 1   // pass 2's chunk-spanning runs copied by k_stx_dechunk (whole lines) instead of per lane
 #endif
+#ifndef KRYO_KEY_ROUNDS
+#define KRYO_KEY_ROUNDS 2   // leader-election rounds per wave in the signer-key interning (0: every lane probes)
+#endif
 #ifndef KRYO_NO_EXTRA_COPY
 #define KRYO_NO_EXTRA_COPY 0
 #endif
@@ -1062,25 +1065,55 @@ __global__ void __launch_bounds__(256) k_stx_key_insert(uint64_t nsig, const uin
     const uint64_t k = koff[i];
     const uint32_t kl = klen[i];
     const uint32_t h = key_hash(pool, k, kl);
-    const unsigned long long mine = ((unsigned long long)h << 32) | (unsigned long long)i;
-    uint64_t s = h & mask;
-    for (uint64_t probe = 0; probe <= mask; probe++, s = (s + 1) & mask) {
-        unsigned long long e = tab[s];
-        if (e == 0) {
-            const unsigned long long prev = atomicCAS(&tab[s], 0ull, mine);
-            if (prev == 0) break;
-            e = prev;
+    // Two rounds of leader election in the wave: each round's leader is the lowest lane not yet decided, and
+    // the lanes holding its key follow it (take its slot, no probe, no atomic: the leader's index is lower).
+    // The notary's key is in every transaction (the odd lanes of a wave); one of the rounds catches it.
+    const uint32_t lane = threadIdx.x & 63u;
+    uint32_t lead[KRYO_KEY_ROUNDS];
+    int follows = -1;
+    bool open = true;
+#pragma unroll
+    for (int r = 0; r < KRYO_KEY_ROUNDS; r++) {
+        const uint64_t m = __ballot(open);
+        lead[r] = m ? (uint32_t)__builtin_ctzll(m) : 0u;
+        if (!m) continue;
+        const uint32_t l = lead[r];
+        // (the lane builtins return int: each 32-bit half through uint32_t, no sign extension)
+        const uint32_t hl = (uint32_t)__builtin_amdgcn_readlane(h, l), kll = (uint32_t)__builtin_amdgcn_readlane(kl, l);
+        const uint64_t kk = (uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)k, l) |
+                            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((uint32_t)(k >> 32), l) << 32);
+        if (open && lane != l && h == hl && kl == kll && key_eq(pool, k, kl, kk, kll)) {
+            follows = r;
+            open = false;
         }
-        if ((uint32_t)(e >> 32) == h) {
-            const uint64_t j = e & 0xffffffffull;
-            if (key_eq(pool, k, kl, koff[j], klen[j])) break;
-        }
+        if (lane == l) open = false;
     }
-    slot[i] = (uint32_t)s;
-    // the key's first occurrence: most lanes see a smaller index already and skip the atomic (a hot
-    // key's slot would otherwise serialise every one of its signatures)
-    if (__hip_atomic_load(&tab_min[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > (uint32_t)i)
-        atomicMin(&tab_min[s], (uint32_t)i);
+    uint64_t s = h & mask;
+    if (follows < 0) {
+        const unsigned long long mine = ((unsigned long long)h << 32) | (unsigned long long)i;
+        for (uint64_t probe = 0; probe <= mask; probe++, s = (s + 1) & mask) {
+            unsigned long long e = tab[s];
+            if (e == 0) {
+                const unsigned long long prev = atomicCAS(&tab[s], 0ull, mine);
+                if (prev == 0) break;
+                e = prev;
+            }
+            if ((uint32_t)(e >> 32) == h) {
+                const uint64_t j = e & 0xffffffffull;
+                if (key_eq(pool, k, kl, koff[j], klen[j])) break;
+            }
+        }
+        // the key's first occurrence: most lanes see a smaller index already and skip the atomic
+        if (__hip_atomic_load(&tab_min[s], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > (uint32_t)i)
+            atomicMin(&tab_min[s], (uint32_t)i);
+    }
+    uint32_t out = (uint32_t)s;
+#pragma unroll
+    for (int r = 0; r < KRYO_KEY_ROUNDS; r++) {
+        const uint32_t sl = (uint32_t)__builtin_amdgcn_readlane((uint32_t)s, lead[r]);
+        if (follows == r) out = sl;
+    }
+    slot[i] = out;
 }
 
 __global__ void __launch_bounds__(256) k_stx_key_flag(uint64_t nsig, const uint32_t* __restrict__ slot,
