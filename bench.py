@@ -233,8 +233,10 @@ def stx_traffic(ntx, nsig):
     """FETCH_SIZE + WRITE_SIZE of one Kryo front-end call (both parse passes, the key interning and the
     required-key passes; the pool copy is a DMA, not counted) from the committed PMC profile, or None."""
     grid_tx, grid_sig = (ntx + 255) // 256 * 256, (nsig + 255) // 256 * 256
-    parts = [profile_traffic(k, grid_tx) for k in ("k_stx_parse<false>", "k_stx_parse<true>", "k_stx_req_tail",
-                                                   "k_stx_required")]
+    parts = [profile_traffic(k, grid_tx) for k in ("k_stx_parse<false>", "k_stx_parse<true>", "k_stx_required")]
+    # the post-dechunk pass (duplicate inputs + required-key walk): k_stx_post since round 5, k_stx_req_tail before
+    post = profile_traffic("k_stx_post", grid_tx)
+    parts.append(post if post is not None else profile_traffic("k_stx_req_tail", grid_tx))
     parts.append(profile_traffic("k_stx_dechunk", (ntx * 64 + 255) // 256 * 256))   # a wave per transaction
     parts += [profile_traffic(k, grid_sig) for k in ("k_stx_key_insert", "k_stx_key_flag", "k_stx_key_assign",
                                                       "k_stx_req_entry<false>", "k_stx_req_entry<true>")]

@@ -1007,7 +1007,9 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
             (has_tw && !has_notary))
             st = CHIP_STX_INVARIANT;
         if (in_count > 64 || noncanon) st = st == CHIP_STX_OK ? CHIP_STX_UNSUPPORTED : st;
-        if (EMIT && st == CHIP_STX_OK && in_count > 1 && !KRYO_NO_STORES) {   // checkNoDuplicateInputs: equal serialized StateRefs
+        // checkNoDuplicateInputs: equal serialized StateRefs.  With deferred copies (o.xd_a) a chunk-spanning input
+        // is not in the pool yet: k_stx_post compares them once k_stx_dechunk has written the extra region
+        if (EMIT && st == CHIP_STX_OK && in_count > 1 && !KRYO_NO_STORES && !o.xd_a) {
             sink.flush();
             const CompAcc ca{o.comp_group, o.comp_off, o.comp_len, o.lm_grp, o.lm_off, o.lm_len, o.n_lm, t, cbase};
             for (uint64_t i = 0; i < in_count && st == CHIP_STX_OK; i++)
@@ -1679,20 +1681,43 @@ __global__ void __launch_bounds__(256) k_stx_dechunk(uint64_t n, uint8_t* __rest
         if (lane < pad) pool[d + lane] = 0;
     }
 }
-// the required-key walk of every parsed transaction, once k_stx_dechunk has filled the extra region
-__global__ void __launch_bounds__(256) k_stx_req_tail(uint64_t n, const uint8_t* __restrict__ data, uint64_t data_bytes,
-                                                      uint8_t* __restrict__ status, Outs o) {
+// after k_stx_dechunk has filled the extra region, per parsed transaction: checkNoDuplicateInputs
+// (WireTransaction.kt:53-60 via checkBaseInvariants) over the input group's serialized StateRefs — chunk-spanning
+// inputs included, which pass 2 only described — then, with CHIP_STX_REQUIRED (o.nraw), the required-key walk
+__global__ void __launch_bounds__(256) k_stx_post(uint64_t n, const uint8_t* __restrict__ data, uint64_t data_bytes,
+                                                  uint8_t* __restrict__ status, Outs o) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
     if (status[t] != CHIP_STX_OK) {
-        o.nraw[t] = 0;
+        if (o.nraw) o.nraw[t] = 0;
         return;
     }
     int st = CHIP_STX_OK;
-    Cur c;
-    c.init(data, data_bytes, 0, 0);
-    const uint64_t cbase = o.comp_start[t];
-    stx_req_tail(c, t, st, cbase, o.comp_start[t + 1] - cbase, o);
+    const uint64_t cbase = o.comp_start[t], comps = o.comp_start[t + 1] - cbase;
+    if (!KRYO_NO_STORES) {
+        const CompAcc ca{o.comp_group, o.comp_off, o.comp_len, o.lm_grp, o.lm_off, o.lm_len, o.n_lm, t, cbase};
+        // group 0 occurs at most once (a duplicated group is INVARIANT in pass 1), its components contiguous
+        uint64_t in_first = 0, in_count = 0;
+        for (uint64_t k = cbase; k < cbase + comps; k++)
+            if (ca.grp(k) == 0) {
+                if (!in_count) in_first = k;
+                in_count++;
+            }
+        for (uint64_t i = 0; i + 1 < in_count && st == CHIP_STX_OK; i++) {
+            const uint64_t ao = ca.off(in_first + i);
+            const uint32_t al = ca.len(in_first + i);
+            for (uint64_t j = i + 1; j < in_count; j++)
+                if (key_eq(o.pool, ao, al, ca.off(in_first + j), ca.len(in_first + j))) {
+                    st = CHIP_STX_INVARIANT;
+                    break;
+                }
+        }
+    }
+    if (o.nraw) {
+        Cur c;
+        c.init(data, data_bytes, 0, 0);
+        stx_req_tail(c, t, st, cbase, comps, o);
+    }
     if (st != CHIP_STX_OK) status[t] = (uint8_t)st;
 }
 
@@ -1707,9 +1732,7 @@ void launch_stx_emit(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_r
                        in->data_bytes, status, nullptr, nullptr, nullptr, o);
     if (o.xd_a) {
         hipLaunchKernelGGL(k_stx_dechunk, grid_of(in->n * 64), dim3(256), 0, st, in->n, d.pool, d.pool_bytes, d.xd_a, d.xd_b, d.xd_n);
-        if (o.nraw)
-            hipLaunchKernelGGL(k_stx_req_tail, grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->data_bytes, status,
-                               o);
+        hipLaunchKernelGGL(k_stx_post, grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->data_bytes, status, o);
     }
     if (d.ncomp)
         hipLaunchKernelGGL(k_stx_lm_comps, grid_of(d.ncomp), dim3(256), 0, st, in->n, d.ncomp, d.comp_start, o);

@@ -269,6 +269,46 @@ def test_device_equals_oracle_on_damaged_blobs(ctx, seed):
         assert_device_equals_oracle(ctx, blobs, required)
 
 
+def dup_input_blobs(seed, n=400):
+    """Transactions with 6-40 canonical StateRef inputs (the input group's list field spans several 1024-byte
+    chunks, so inputs straddle chunk boundaries and are de-chunked by k_stx_dechunk); every even one has a
+    duplicated input at random positions, every odd one distinct inputs."""
+    rng = np.random.default_rng(seed)
+    keys = S.key_pool(rng)
+    out = []
+    for i in range(n):
+        nin = int(rng.integers(6, 41))
+        ins = [S.stateref(rng) for _ in range(nin)]
+        if i % 2 == 0:
+            a, b = sorted(int(x) for x in rng.choice(nin, 2, replace=False))
+            ins[b] = ins[a]
+        key = keys[int(rng.integers(0, len(keys)))]
+        sig = K.Sig(rng.bytes(64 if len(key) == S.ED_KEY else 71), key, 1, 4, S.REG.key_class_for(key))
+        groups = [(0, ins), (1, [rng.bytes(int(rng.integers(20, 700)))]), (2, [K.command([key])]), (4, [K.party(key)])]
+        out.append(S.blob(groups, rng.bytes(32), [sig]))
+    return out
+
+
+@pytest.mark.parametrize("required", [False, True])
+def test_duplicate_inputs_across_chunk_boundaries(required):
+    """checkNoDuplicateInputs (WireTransaction.kt:53-60) over inputs that cross a chunk boundary of the group list
+    (pass 2 only records such a run as a copy descriptor, so the comparison must wait for
+    k_stx_dechunk): on a fresh context, and again after a batch of other blobs has left its bytes in the pool,
+    every duplicate is INVARIANT and every distinct list OK, equal to the oracle and the host mirror."""
+    import corda_amd
+    c = corda_amd.Context(0)
+    try:
+        for seed in (0xD0B, 0xD0C):
+            blobs = dup_input_blobs(seed)
+            dev, _ = assert_device_equals_oracle(c, blobs, required)
+            want = [K.stx_parse(b)[0] for b in blobs]
+            assert [d[0] for d in dev] == want
+            assert want[0::2] == [K.STX_INVARIANT] * (len(blobs) // 2)
+            assert want[1::2] == [K.STX_OK] * (len(blobs) // 2)
+    finally:
+        c.close()
+
+
 def test_registry_is_applied(ctx):
     """chip_set_kryo_registry: blobs written with another deployment's ids parse under that registry and fail
     closed (UNSUPPORTED) under the defaults, on the device as in the oracle."""
