@@ -9,7 +9,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(PKG)
 CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libcordahip.so")
-SOURCES = ["runtime.hip", "ed25519.hip", "ed25519_comb.hip", "ecdsa.hip", "txid.hip", "uniq.hip", "signers.hip", "kryo.hip"]
+SOURCES = ["runtime.hip", "ed25519.hip", "ed25519_comb.hip", "ecdsa.hip", "txid.hip", "uniq.hip", "signers.hip", "kryo.hip", "group.hip"]
 HEADERS = ["common.hpp", "fe25519_dev.hpp", "scalar_dev.hpp", "sha2_dev.hpp", "runtime.hpp", "curve_consts.hpp",
            "ec_dev.hpp", "ed_common_dev.hpp", "comb_tables.hpp"]
 GEN = os.path.join(ROOT, "tools", "gen_constants.py")
@@ -44,9 +44,12 @@ def build(force: bool = False, verbose: bool = False) -> str:
     objs = []
     procs = []
     os.makedirs(os.path.join(PKG, "build"), exist_ok=True)
+    hdr = max([_mtime(os.path.join(CSRC, h)) for h in HEADERS] + [_mtime(os.path.join(ROOT, "include", "cordahip.h"))])
     for src in sources():
         obj = os.path.join(PKG, "build", os.path.basename(src) + ".o")
         objs.append(obj)
+        if not force and _mtime(obj) > max(_mtime(src), hdr):   # object newer than its source and every header
+            continue
         cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
                "-I", os.path.join(ROOT, "include")]
         if verbose:

@@ -1615,7 +1615,7 @@ __global__ void __launch_bounds__(256) k_blob_range(uint64_t m, const uint64_t* 
 static int stx_verify_host_pipelined(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t* off,
                                      const uint32_t* len, uint64_t data_bytes, const chip_msg_templates* dtm,
                                      const int32_t* meta, uint32_t n_meta, uint8_t* tx_status, uint8_t* verdict,
-                                     uint32_t* arg, uint8_t* ids, uint64_t chunks) {
+                                     uint32_t* arg, uint8_t* ids, uint64_t chunks, uint64_t* nsig_out) {
     hipStream_t st = c->stream, cs = c->hcs;
     std::vector<uint64_t> at{0};
     for (uint64_t k = 1; k <= chunks; k++) at.push_back(std::min(n, (n * k + chunks - 1) / chunks));
@@ -1688,6 +1688,7 @@ static int stx_verify_host_pipelined(chip_ctx* c, uint64_t n, const uint8_t* dat
                                c->h2_v.as<uint8_t>() + a, c->h2_a.as<uint32_t>() + a, (uint32_t)sig_base);
         sig_base += p.sigs.n;
     }
+    if (nsig_out) *nsig_out = sig_base;
     HIPCHK(c, hipMemcpyAsync(tx_status, c->h2_st.p, n, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipMemcpyAsync(verdict, c->h2_v.p, n, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipMemcpyAsync(arg, c->h2_a.p, n * 4, hipMemcpyDeviceToHost, st));
@@ -1704,9 +1705,12 @@ static uint64_t stx_host_chunks(uint64_t n) {
     return std::min<uint64_t>(k, std::max<uint64_t>(1, n));
 }
 
-int chip_stx_verify(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t* off, const uint32_t* len,
-                    uint64_t data_bytes, const chip_msg_templates* tmpl, const int32_t* meta, uint32_t n_meta,
-                    uint8_t* tx_status, uint8_t* verdict, uint32_t* arg, uint8_t* ids) {
+// chip_stx_verify + the number of signatures the parse accepted (the signature list a CHIP_TXV_SIGNATURE arg
+// indexes; the device group offsets its members' args by it)
+int stx_verify_counted(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t* off, const uint32_t* len,
+                       uint64_t data_bytes, const chip_msg_templates* tmpl, const int32_t* meta, uint32_t n_meta,
+                       uint8_t* tx_status, uint8_t* verdict, uint32_t* arg, uint8_t* ids, uint64_t* nsig_out) {
+    if (nsig_out) *nsig_out = 0;
     if (!c || !tmpl) return fail(c, CHIP_E_ARG, "null argument");
     if (!n) return CHIP_OK;
     if (!data || !off || !len || !tx_status || !verdict || !arg) return fail(c, CHIP_E_ARG, "null array");
@@ -1751,7 +1755,7 @@ int chip_stx_verify(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t
         HIPCHK(c, c->h2_off.ensure(n * 8 + 16));
         HIPCHK(c, c->h2_len.ensure(n * 4 + 16));
         return stx_verify_host_pipelined(c, n, data, off, len, data_bytes, &dtm, meta, n_meta, tx_status, verdict, arg,
-                                         ids, chunks);
+                                         ids, chunks, nsig_out);
     }
     chip_stx_blobs in{n, c->h2_data.as<uint8_t>(), c->h2_off.as<uint64_t>(), c->h2_len.as<uint32_t>(), data_bytes,
                       meta, n_meta, CHIP_STX_REQUIRED, c->h2_data.cap};
@@ -1759,6 +1763,7 @@ int chip_stx_verify(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t
     if ((r = stx_parse(c, c->stx[2], &in, c->h2_st.as<uint8_t>(), &p, st))) return r;
     HIPCHK(c, c->h2_sigst.ensure(p.sigs.n + 16));
     HIPCHK(c, c->h2_miss.ensure(p.req.nreq + 16));
+    if (nsig_out) *nsig_out = p.sigs.n;
     if ((r = chip_verify_signed_tx_batch_device(c, &p.txs, &dtm, &p.sigs, &p.req, c->h2_ids.as<uint8_t>(),
                                                 c->h2_sigst.as<uint8_t>(), c->h2_v.as<uint8_t>(),
                                                 c->h2_a.as<uint32_t>(), c->h2_miss.as<uint8_t>(), st)))
@@ -1769,6 +1774,12 @@ int chip_stx_verify(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t
     if (ids) HIPCHK(c, hipMemcpyAsync(ids, c->h2_ids.p, n * 32, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
     return CHIP_OK;
+}
+
+int chip_stx_verify(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t* off, const uint32_t* len,
+                    uint64_t data_bytes, const chip_msg_templates* tmpl, const int32_t* meta, uint32_t n_meta,
+                    uint8_t* tx_status, uint8_t* verdict, uint32_t* arg, uint8_t* ids) {
+    return stx_verify_counted(c, n, data, off, len, data_bytes, tmpl, meta, n_meta, tx_status, verdict, arg, ids, nullptr);
 }
 
 int chip_copy_to_host(chip_ctx* c, void* dst, const void* src, uint64_t bytes) {
@@ -2167,7 +2178,7 @@ static int verify_tx_host(chip_ctx* c, const chip_tx_batch* b, const chip_msg_te
                           uint32_t* arg, uint8_t* missing) {
     if (!c || !b || !tm || !sb) return fail(c, CHIP_E_ARG, "null argument");
     const uint64_t ntx = b->ntx, nc = b->ncomp, n = sb->n, nk = sb->n_keys, nt = tm->n;
-    if (ntx && (!b->salts || !b->tx_comp_start || !ids)) return fail(c, CHIP_E_ARG, "null tx array");
+    if (ntx && (!b->salts || !b->tx_comp_start)) return fail(c, CHIP_E_ARG, "null tx array");   // ids may be NULL
     if (nc && (!b->comp_group || !b->comp_internal || !b->comp_off || !b->comp_len || !b->data))
         return fail(c, CHIP_E_ARG, "null component array");
     if (nt && (!tm->data || !tm->off || !tm->len || !tm->id_at)) return fail(c, CHIP_E_ARG, "null template array");
@@ -2242,7 +2253,7 @@ static int verify_tx_host(chip_ctx* c, const chip_tx_batch* b, const chip_msg_te
                                           c->q_arg.as<uint32_t>(), missing ? c->q_missing.as<uint8_t>() : nullptr, st)) ||
               (r = fetch_req(c, q, verdict, arg, missing, st))))
         return r;
-    if (ntx) HIPCHK(c, hipMemcpyAsync(ids, c->t_ids.p, ntx * 32, hipMemcpyDeviceToHost, st));
+    if (ids && ntx) HIPCHK(c, hipMemcpyAsync(ids, c->t_ids.p, ntx * 32, hipMemcpyDeviceToHost, st));
     if (status && n) HIPCHK(c, hipMemcpyAsync(status, c->h_status.p, n, hipMemcpyDeviceToHost, st));
     if (bitmap && nw) HIPCHK(c, hipMemcpyAsync(bitmap, c->h_bitmap.p, nw * 8, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));

@@ -231,3 +231,9 @@ struct DevCheckSet {
 };
 // runs the checks (empty ones skipped) on `st`, waits, and returns the OR of the failed checks' bits
 int dev_check(chip_ctx* c, const DevCheck* chk, int nchk, hipStream_t st, uint32_t* bad_out);
+
+// chip_stx_verify that also reports how many signatures the parse accepted (runtime.hip; used by group.hip)
+extern "C" int stx_verify_counted(chip_ctx* c, uint64_t n, const uint8_t* data, const uint64_t* off,
+                                  const uint32_t* len, uint64_t data_bytes, const chip_msg_templates* tmpl,
+                                  const int32_t* meta, uint32_t n_meta, uint8_t* tx_status, uint8_t* verdict,
+                                  uint32_t* arg, uint8_t* ids, uint64_t* nsig_out);

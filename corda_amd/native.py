@@ -40,7 +40,13 @@ EXPORTS = ["chip_abi_version", "chip_device_count", "chip_init", "chip_shutdown"
            "chip_ftx_verify_batch_device", "chip_required_signers", "chip_required_signers_device",
            "chip_verify_signed_tx_batch", "chip_verify_signed_tx_batch_device",
            "chip_stx_parse_device", "chip_stx_verify", "chip_set_kryo_registry", "chip_get_kryo_registry",
-           "chip_copy_to_host", "chip_get_stats", "chip_reset_stats"]
+           "chip_copy_to_host", "chip_get_stats", "chip_reset_stats",
+           "chip_group_init", "chip_group_shutdown", "chip_group_size", "chip_group_member", "chip_group_last_error",
+           "chip_group_verify_batch", "chip_group_is_valid_batch", "chip_group_txid_batch",
+           "chip_group_verify_signed_tx_batch", "chip_group_stx_verify", "chip_group_ftx_verify_batch",
+           "chip_group_plan_sigs", "chip_group_plan_tx", "chip_group_uniq_open", "chip_group_uniq_close",
+           "chip_group_uniq_size", "chip_group_uniq_last_error", "chip_group_state_owner", "chip_group_uniq_rebuild",
+           "chip_group_uniq_commit_batch"]
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
 u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -271,6 +277,33 @@ def load(build_if_missing: bool = False):
     lib.chip_copy_to_host.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64]
     lib.chip_get_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipStats)]
     lib.chip_reset_stats.argtypes = [ctypes.c_void_p]
+    # device groups (ABI 9)
+    lib.chip_group_init.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ChipConfig),
+                                    ctypes.POINTER(ctypes.c_void_p)]
+    lib.chip_group_shutdown.argtypes = [ctypes.c_void_p]
+    lib.chip_group_size.argtypes = [ctypes.c_void_p]
+    lib.chip_group_member.argtypes = [ctypes.c_void_p, ctypes.c_int]
+    lib.chip_group_member.restype = ctypes.c_void_p
+    lib.chip_group_last_error.argtypes = [ctypes.c_void_p]
+    lib.chip_group_last_error.restype = ctypes.c_char_p
+    lib.chip_group_verify_batch.argtypes = lib.chip_verify_batch.argtypes
+    lib.chip_group_is_valid_batch.argtypes = lib.chip_verify_batch.argtypes
+    lib.chip_group_txid_batch.argtypes = lib.chip_txid_batch.argtypes
+    lib.chip_group_verify_signed_tx_batch.argtypes = lib.chip_verify_signed_tx_batch.argtypes
+    lib.chip_group_stx_verify.argtypes = lib.chip_stx_verify.argtypes
+    lib.chip_group_ftx_verify_batch.argtypes = lib.chip_ftx_verify_batch.argtypes
+    lib.chip_group_plan_sigs.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p]
+    lib.chip_group_plan_tx.argtypes = [ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int, ctypes.c_uint64, ctypes.c_void_p]
+    lib.chip_group_uniq_open.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.POINTER(ctypes.c_void_p)]
+    lib.chip_group_uniq_close.argtypes = [ctypes.c_void_p]
+    lib.chip_group_uniq_size.argtypes = [ctypes.c_void_p]
+    lib.chip_group_uniq_size.restype = ctypes.c_uint64
+    lib.chip_group_uniq_last_error.argtypes = [ctypes.c_void_p]
+    lib.chip_group_uniq_last_error.restype = ctypes.c_char_p
+    lib.chip_group_state_owner.argtypes = [ctypes.c_void_p, ctypes.c_uint32]
+    lib.chip_group_state_owner.restype = ctypes.c_uint32
+    lib.chip_group_uniq_rebuild.argtypes = lib.chip_uniq_rebuild.argtypes
+    lib.chip_group_uniq_commit_batch.argtypes = lib.chip_uniq_commit_batch.argtypes
     _lib = lib
     return lib
 
@@ -738,3 +771,167 @@ class UniqShardEngine:
         """-> (status u8[ntx] numpy, this shard's conflict records)."""
         st, raw = self.finish_device(decision)
         return st.cpu().numpy(), records_from_bytes(raw.cpu().numpy().tobytes())
+
+
+# ---------------------------------------------------------------------------------------
+# device groups: every GPU of the process behind one handle (chip_group_*, include/cordahip.h ABI 9)
+def plan_sigs(msg_idx, k: int, min_share: int = 0) -> np.ndarray:
+    """chip_group_plan_sigs: the signature ranges a k-member group verifies (host-only, no GPU)."""
+    lib = load()
+    m = np.ascontiguousarray(msg_idx, dtype=np.uint32)
+    cut = np.zeros(k + 1, dtype=np.uint64)
+    rc = lib.chip_group_plan_sigs(len(m), _ptr(m) if len(m) else None, k, min_share, _ptr(cut))
+    if rc:
+        raise ChipError(rc, "chip_group_plan_sigs")
+    return cut
+
+
+def plan_tx(ntx: int, prefix, k: int, min_share: int = 0) -> np.ndarray:
+    """chip_group_plan_tx: the transaction ranges of a k-member group, balanced by prefix (or one unit a tx)."""
+    lib = load()
+    p = None if prefix is None else np.ascontiguousarray(prefix, dtype=np.uint64)
+    cut = np.zeros(k + 1, dtype=np.uint64)
+    rc = lib.chip_group_plan_tx(ntx, None if p is None else _ptr(p), k, min_share, _ptr(cut))
+    if rc:
+        raise ChipError(rc, "chip_group_plan_tx")
+    return cut
+
+
+def state_owner(ref36: bytes, members: int) -> int:
+    """chip_group_state_owner: the member whose table slice holds this StateRef."""
+    buf = (ctypes.c_uint8 * 36).from_buffer_copy(bytes(ref36))
+    return int(load().chip_group_state_owner(ctypes.addressof(buf), members))
+
+
+class Group:
+    """A device group: one context per entry of `devices` (an ordinal may repeat), host-buffer entries that split
+    each batch by transaction ranges over the members and return the one-context results."""
+
+    def __init__(self, devices, flags: int = 0, reserve_sigs: int = 0):
+        self.lib = load()
+        devs = (ctypes.c_int * len(devices))(*devices)
+        cfg = ChipConfig(0, flags, reserve_sigs)
+        h = ctypes.c_void_p()
+        rc = self.lib.chip_group_init(devs, len(devices), ctypes.byref(cfg), ctypes.byref(h))
+        if rc != 0:
+            raise NativeUnavailable("chip_group_init(%s) failed with %d" % (list(devices), rc))
+        self.h = h
+        self.devices = list(devices)
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.chip_group_shutdown(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def size(self) -> int:
+        return int(self.lib.chip_group_size(self.h))
+
+    def _check(self, rc):
+        if rc != 0:
+            raise ChipError(rc, self.lib.chip_group_last_error(self.h).decode(errors="replace"))
+
+    def verify_batch(self, b, is_valid: bool = False):
+        s = make_sig_batch(b)
+        status = np.zeros(max(s.n, 1), dtype=np.uint8)
+        bitmap = np.zeros(max((s.n + 63) // 64, 1), dtype=np.uint64)
+        fn = self.lib.chip_group_is_valid_batch if is_valid else self.lib.chip_group_verify_batch
+        self._check(fn(self.h, ctypes.byref(s), _ptr(status), _ptr(bitmap)))
+        return status[:s.n], bitmap[:(s.n + 63) // 64]
+
+    def txid_batch(self, t) -> np.ndarray:
+        s = make_tx_batch(t)
+        ids = np.zeros(max(s.ntx, 1) * 32, dtype=np.uint8)
+        self._check(self.lib.chip_group_txid_batch(self.h, ctypes.byref(s), _ptr(ids)))
+        return ids[:32 * s.ntx].reshape(s.ntx, 32)
+
+    def verify_signed_tx_batch(self, t, templates, signers, q, want_ids: bool = True):
+        tb, tm, sb, rq = make_tx_batch(t), make_templates(templates), make_signers(signers), make_req_batch(q)
+        ids = np.zeros(max(tb.ntx, 1) * 32, dtype=np.uint8) if want_ids else None
+        status = np.zeros(max(sb.n, 1), dtype=np.uint8)
+        verdict = np.zeros(max(rq.ntx, 1), dtype=np.uint8)
+        arg = np.zeros(max(rq.ntx, 1), dtype=np.uint32)
+        missing = np.zeros(max(rq.nreq, 1), dtype=np.uint8)
+        self._check(self.lib.chip_group_verify_signed_tx_batch(self.h, ctypes.byref(tb), ctypes.byref(tm),
+                                                               ctypes.byref(sb), ctypes.byref(rq), _ptr(ids),
+                                                               _ptr(status), _ptr(verdict), _ptr(arg), _ptr(missing)))
+        return ((ids[:32 * tb.ntx].reshape(tb.ntx, 32) if want_ids else None), status[:sb.n], verdict[:rq.ntx],
+                arg[:rq.ntx], missing[:rq.nreq])
+
+    def stx_verify(self, data, off, lens, templates, meta, want_ids: bool = False):
+        n = len(off)
+        data = np.ascontiguousarray(data, dtype=np.uint8)
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        lens = np.ascontiguousarray(lens, dtype=np.uint32)
+        meta = np.ascontiguousarray(np.asarray(meta, dtype=np.int32).reshape(-1, 2))
+        tm = make_templates(templates)
+        st = np.zeros(max(n, 1), dtype=np.uint8)
+        v = np.zeros(max(n, 1), dtype=np.uint8)
+        a = np.zeros(max(n, 1), dtype=np.uint32)
+        ids = np.zeros(max(n, 1) * 32, dtype=np.uint8) if want_ids else None
+        self._check(self.lib.chip_group_stx_verify(self.h, n, _ptr(data), _ptr(off), _ptr(lens), len(data),
+                                                   ctypes.byref(tm), meta.ctypes.data, len(meta), _ptr(st), _ptr(v),
+                                                   _ptr(a), _ptr(ids)))
+        return st[:n], v[:n], a[:n], (ids[:32 * n].reshape(n, 32) if want_ids else None)
+
+    def ftx_verify_batch(self, f):
+        s = make_ftx_batch(f)
+        status = np.zeros(max(s.ntx, 1), dtype=np.uint8)
+        reason = np.zeros(max(s.ntx, 1), dtype=np.uint8)
+        self._check(self.lib.chip_group_ftx_verify_batch(self.h, ctypes.byref(s), _ptr(status), _ptr(reason)))
+        return status[:s.ntx], reason[:s.ntx]
+
+    def uniq_open(self, capacity: int):
+        return GroupUniqTable(self, capacity)
+
+
+class GroupUniqTable:
+    """The notary table of a device group: member m holds the StateRefs with state_owner(ref, n) == m."""
+
+    def __init__(self, group: Group, capacity: int):
+        self.group = group
+        self.lib = group.lib
+        h = ctypes.c_void_p()
+        group._check(self.lib.chip_group_uniq_open(group.h, ctypes.c_uint64(capacity), ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.chip_group_uniq_close(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def size(self) -> int:
+        return int(self.lib.chip_group_uniq_size(self.h))
+
+    def _check(self, rc):
+        if rc != 0:
+            raise ChipError(rc, self.lib.chip_group_uniq_last_error(self.h).decode(errors="replace"))
+
+    def rebuild(self, refs36, tx32, idx, caller):
+        self._check(self.lib.chip_group_uniq_rebuild(self.h, ctypes.c_uint64(len(idx)), _ptr(refs36), _ptr(tx32),
+                                                     _ptr(idx), _ptr(caller)))
+
+    def commit_batch(self, tx_ref_start, refs36, tx_ids, callers, cap=None):
+        ntx = len(tx_ref_start) - 1
+        st = np.zeros(max(ntx, 1), dtype=np.uint8)
+        if cap is None:
+            cap = int(tx_ref_start[-1]) + 1
+        out = (ChipConflict * max(cap, 1))()
+        nout = ctypes.c_uint64()
+        self._check(self.lib.chip_group_uniq_commit_batch(self.h, ctypes.c_uint64(ntx), _ptr(tx_ref_start),
+                                                          _ptr(refs36), _ptr(tx_ids), _ptr(callers), _ptr(st), out,
+                                                          ctypes.c_uint64(cap), ctypes.byref(nout)))
+        recs = [(c.tx, c.input_index, c.consumed_index, bytes(c.consuming_tx), c.consuming_caller)
+                for c in out[:min(nout.value, cap)]]
+        return st[:ntx], recs

@@ -2,8 +2,9 @@
  * cordahip.h — C-ABI of libcordahip, the MI355X-native batch transaction-verification engine
  * for Corda's signature / tx-id / notary-uniqueness hot path.
  *
- * Plain C: pointers + sizes, no C++ or HIP types in any signature.  One context per GPU
- * (one process per GPU).  Every function returns 0 on success or a negative CHIP_E* code;
+ * Plain C: pointers + sizes, no C++ or HIP types in any signature.  One context per GPU; a process that
+ * drives several GPUs (a Corda node: one JVM) opens a device group (chip_group_*, one context per member GPU)
+ * or one context per GPU itself (one process per GPU: corda_amd/distributed.py).  Every function returns 0 on success or a negative CHIP_E* code;
  * chip_last_error(ctx) then holds a message.  The caller owns every input/output buffer; the
  * library owns device memory (key tables, workspaces, the uniqueness table) and retains no
  * caller pointer after a call returns.
@@ -45,7 +46,7 @@
 extern "C" {
 #endif
 
-#define CHIP_ABI_VERSION 8
+#define CHIP_ABI_VERSION 9
 
 enum chip_sig_status {
     CHIP_VALID = 0,
@@ -265,6 +266,7 @@ typedef struct {
 } chip_signer_batch;
 
 /* ids: [ntx * 32] out; status: [n] out (CHIP_* per signature); bitmap: [ceil(n/64)] (may be NULL). */
+/* (host entries: ids may be NULL) */
 int chip_verify_tx_batch(chip_ctx* ctx, const chip_tx_batch* txs, const chip_msg_templates* tmpl,
                          const chip_signer_batch* sigs, uint8_t* ids, uint8_t* status, uint64_t* bitmap);
 int chip_verify_tx_batch_device(chip_ctx* ctx, const chip_tx_batch* txs, const chip_msg_templates* tmpl,
@@ -518,6 +520,62 @@ int chip_uniq_shard_apply(chip_uniq* u, const uint8_t* decision, uint64_t* undec
 int chip_uniq_shard_classify(chip_uniq* u, uint8_t* vote);
 int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_status, chip_conflict* out,
                            uint64_t cap, uint64_t* n_out);
+
+/* ---------------------------------------------------------------------------------------
+ * Device groups (ABI 9): every GPU of a node behind ONE handle, for a process that drives several GPUs — a Corda
+ * node or notary is one JVM, whose batch sites (ResolveTransactionsFlow.kt:88-96, NonValidatingNotaryFlow.kt:27-29,
+ * PersistentUniquenessProvider.kt:92-113 via NotaryService.kt:61-75) call the library from that one process.
+ * chip_group_init opens one context per entry of `devices` (the same ordinal may repeat: two contexts on one GPU,
+ * for tests) with the given config (its `device` is ignored).  The group entries take HOST buffers like the
+ * single-context host entries and return exactly their results (status bytes, bitmaps, ids, verdicts, args,
+ * records):
+ *   - signatures, tx ids, filtered transactions and SignedTransaction bytes are split into contiguous TRANSACTION
+ *     ranges, one per member (a transaction never splits; chip_group_verify_batch takes a transaction to be a run of
+ *     equal msg_idx, the signers of one tx sharing its SignableData message), balanced by signatures / transactions,
+ *     each verified by its member on a host thread of its own; a batch smaller than one member's share
+ *     (CHIP_GROUP_MIN_SIGS = 16384 signatures, CHIP_GROUP_MIN_TX = 8192 transactions; env overrides, or
+ *     CHIP_GROUP_MIN_SHARE for every entry) runs on one member, rotating;
+ *   - uniqueness partitions the StateRef key space: member chip_group_state_owner(ref, n) holds that state's slice
+ *     of the commit log; the batch goes to every member, which keeps the inputs it owns (on its device), and the
+ *     ordered-commit rounds exchange one vote byte per transaction per round (element-wise MAX, reduced on the
+ *     host); records are merged in (tx, input_index) order.
+ * One group call runs at a time (the group serialises them); the member contexts (chip_group_member) may also be
+ * used directly, e.g. for device-resident batches. */
+typedef struct chip_group chip_group;
+int chip_group_init(const int* devices, int n, const chip_config* cfg, chip_group** out);
+void chip_group_shutdown(chip_group* g);
+int chip_group_size(const chip_group* g);
+chip_ctx* chip_group_member(chip_group* g, int i);
+const char* chip_group_last_error(const chip_group* g);
+int chip_group_verify_batch(chip_group* g, const chip_sig_batch* batch, uint8_t* status, uint64_t* bitmap);
+int chip_group_is_valid_batch(chip_group* g, const chip_sig_batch* batch, uint8_t* status, uint64_t* bitmap);
+int chip_group_txid_batch(chip_group* g, const chip_tx_batch* batch, uint8_t* ids);
+int chip_group_verify_signed_tx_batch(chip_group* g, const chip_tx_batch* txs, const chip_msg_templates* tmpl,
+                                      const chip_signer_batch* sigs, const chip_req_batch* req, uint8_t* ids,
+                                      uint8_t* status, uint8_t* verdict, uint32_t* arg, uint8_t* missing);
+int chip_group_stx_verify(chip_group* g, uint64_t n, const uint8_t* data, const uint64_t* off, const uint32_t* len,
+                          uint64_t data_bytes, const chip_msg_templates* tmpl, const int32_t* meta, uint32_t n_meta,
+                          uint8_t* tx_status, uint8_t* verdict, uint32_t* arg, uint8_t* ids);
+int chip_group_ftx_verify_batch(chip_group* g, const chip_ftx_batch* batch, uint8_t* status, uint8_t* reason);
+/* The range plans behind those splits (host-only, no GPU needed): member i takes [cut[i], cut[i+1]) of the n
+ * signatures (chip_group_plan_sigs: cuts on msg_idx run boundaries) or ntx transactions (chip_group_plan_tx,
+ * balanced by prefix[ntx + 1] — e.g. a sig_start — or one unit per transaction when NULL); cut has k + 1 entries;
+ * min_share = the smallest share worth a member of its own (0: split over all k). */
+int chip_group_plan_sigs(uint64_t n, const uint32_t* msg_idx, int k, uint64_t min_share, uint64_t* cut);
+int chip_group_plan_tx(uint64_t ntx, const uint64_t* prefix, int k, uint64_t min_share, uint64_t* cut);
+
+typedef struct chip_group_uniq chip_group_uniq;
+/* capacity: states of the whole table (each member sizes for its share) */
+int chip_group_uniq_open(chip_group* g, uint64_t capacity, chip_group_uniq** out);
+void chip_group_uniq_close(chip_group_uniq* u);
+uint64_t chip_group_uniq_size(const chip_group_uniq* u);
+const char* chip_group_uniq_last_error(const chip_group_uniq* u);
+uint32_t chip_group_state_owner(const uint8_t* ref36, uint32_t members);
+int chip_group_uniq_rebuild(chip_group_uniq* u, uint64_t n, const uint8_t* refs36, const uint8_t* tx32,
+                            const uint32_t* input_index, const uint32_t* caller);
+int chip_group_uniq_commit_batch(chip_group_uniq* u, uint64_t ntx, const uint64_t* tx_ref_start, const uint8_t* refs36,
+                                 const uint8_t* tx_ids, const uint32_t* callers, uint8_t* tx_status, chip_conflict* out,
+                                 uint64_t cap, uint64_t* n_out);
 
 /* ---------------------------------------------------------------------------------------
  * Counters (observability; OutOfProcessTransactionVerifierService.kt:35-46 analogue). */

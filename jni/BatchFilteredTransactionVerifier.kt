@@ -32,9 +32,12 @@ import java.nio.ByteOrder
  *
  * Small batches (fewer than `minBatch` requests, `corda.gpu.minBatch`) stay on the JVM, as BatchSignatureVerifier.
  */
-class BatchFilteredTransactionVerifier(device: Int = 0, flags: Int = 0,
+class BatchFilteredTransactionVerifier(devices: IntArray = intArrayOf(0), flags: Int = 0,
                                        val minBatch: Int = Integer.getInteger("corda.gpu.minBatch",
                                                BatchSignatureVerifier.DEFAULT_MIN_BATCH)) : AutoCloseable {
+    /** One GPU. */
+    constructor(device: Int, flags: Int = 0) : this(intArrayOf(device), flags)
+
     companion object {
         /** NonValidatingNotaryFlow.kt:28-29: checkAllComponentsVisible(INPUTS_GROUP), then (TIMEWINDOW_GROUP). */
         val NOTARY_VISIBLE_GROUPS = listOf(ComponentGroupEnum.INPUTS_GROUP, ComponentGroupEnum.TIMEWINDOW_GROUP)
@@ -60,9 +63,8 @@ class BatchFilteredTransactionVerifier(device: Int = 0, flags: Int = 0,
         }
     }
 
-    private val ctx: Long = CordaHip.open(device, flags).also {
-        check(it != 0L) { "libcordahip: no usable GPU for device $device" }
-    }
+    /** Every GPU in `devices` (a device group splits each batch by request ranges). */
+    val gpu = GpuHandle(devices, flags)
     private val arena = PinnedBuffer(1 shl 20)
 
     /** NonValidatingNotaryFlow's check for one request (below minBatch: the JVM path itself). */
@@ -77,10 +79,12 @@ class BatchFilteredTransactionVerifier(device: Int = 0, flags: Int = 0,
      */
     @Synchronized
     fun verify(txs: List<FilteredTransaction>, visible: List<ComponentGroupEnum> = NOTARY_VISIBLE_GROUPS): List<Exception?> {
-        require(visible.zipWithNext().all { (a, b) -> a.ordinal < b.ordinal }) { "visibility groups must ascend by ordinal" }
+        require((1 until visible.size).all { visible[it - 1].ordinal < visible[it].ordinal }) {
+            "visibility groups must ascend by ordinal"
+        }
         if (txs.isEmpty()) return emptyList()
-        if (txs.size < minBatch)
-            return txs.map { try { jvmCheck(it, visible); null } catch (e: Exception) { e } }
+        fun jvm() = txs.map { try { jvmCheck(it, visible); null } catch (e: Exception) { e } }
+        if (txs.size < minBatch) return jvm()
         val mask = visible.fold(0) { m, g -> m or (1 shl g.ordinal) }
         // flatten: per request its group hashes and filtered groups; per group its components, nonces, partial tree
         var nGh = 0; var nFg = 0; var nComp = 0; var nNodes = 0; var compBytes = 0L
@@ -89,7 +93,7 @@ class BatchFilteredTransactionVerifier(device: Int = 0, flags: Int = 0,
             ftx.filteredComponentGroups.map { g ->
                 nFg++
                 nComp += g.components.size
-                compBytes += g.components.sumOf { it.size.toLong() }
+                compBytes += g.components.sumByLong { it.size.toLong() }
                 val tags = ArrayList<Byte>(); val hashes = ArrayList<ByteArray>()
                 postOrder(g.partialMerkleTree.root, tags, hashes)
                 nNodes += tags.size
@@ -134,9 +138,12 @@ class BatchFilteredTransactionVerifier(device: Int = 0, flags: Int = 0,
             fg += ftx.filteredComponentGroups.size; bFgStart.putLong(fg)
             bMask.putInt(mask)
         }
-        val rc = CordaHip.ftxVerify(ctx, n, bIds, bGhStart, bGh, bFgStart, bFgIndex, bCompStart, bCompData, bCompOff,
+        val rc = if (gpu.isGroup)
+            CordaHip.groupFtxVerify(gpu.group, n, bIds, bGhStart, bGh, bFgStart, bFgIndex, bCompStart, bCompData,
+                    bCompOff, bCompLen, bNonces, bPtStart, bPtTag, bPtHash, null, bMask, bStatus, bReason)
+        else CordaHip.ftxVerify(gpu.ctx, n, bIds, bGhStart, bGh, bFgStart, bFgIndex, bCompStart, bCompData, bCompOff,
                 bCompLen, bNonces, bPtStart, bPtTag, bPtHash, null, bMask, bStatus, bReason)
-        check(rc == 0) { "libcordahip ftxVerify failed ($rc): ${CordaHip.lastError(ctx)}" }
+        if (!gpu.ok(rc, "ftxVerify")) return jvm()   // device failure: the reference's checks decide the batch
         return txs.mapIndexed { t, ftx ->
             val status = bStatus.get(t).toInt()
             if (status == 0) null
@@ -159,6 +166,6 @@ class BatchFilteredTransactionVerifier(device: Int = 0, flags: Int = 0,
 
     override fun close() {
         arena.close()
-        CordaHip.close(ctx)
+        gpu.close()
     }
 }

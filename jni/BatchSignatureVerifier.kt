@@ -37,16 +37,20 @@ import net.corda.core.utilities.toNonEmptySet
  * comes from the system property `corda.gpu.minBatch` (else DEFAULT_MIN_BATCH); 0 sends everything to the
  * device.
  */
-class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
+class BatchSignatureVerifier(devices: IntArray = intArrayOf(0), flags: Int = 0,
                              val minBatch: Int = Integer.getInteger("corda.gpu.minBatch", DEFAULT_MIN_BATCH)) : AutoCloseable {
+    /** One GPU. */
+    constructor(device: Int, flags: Int = 0,
+                minBatch: Int = Integer.getInteger("corda.gpu.minBatch", DEFAULT_MIN_BATCH)) :
+            this(intArrayOf(device), flags, minBatch)
+
     companion object {
         /** Signatures below which a call stays on the JCA engines (one i2p Ed25519 verify ≈ 60-100 µs on a
          *  host core; one device round trip of a small batch ≈ 100-150 µs, docs in INTEGRATION.md). */
         const val DEFAULT_MIN_BATCH = 16
     }
-    private val ctx: Long = CordaHip.open(device, flags).also {
-        check(it != 0L) { "libcordahip: no usable GPU for device $device" }
-    }
+    /** Every GPU in `devices`: one device, or a device group whose calls split each batch by transaction ranges. */
+    val gpu = GpuHandle(devices, flags)
     private val arena = PinnedBuffer(1 shl 20)
     private val statusBuf = PinnedBuffer(1 shl 12)
     /** With CordaHip.FLAG_KEY_CACHE the key pool is kept across calls, append-only in first-seen order (a node
@@ -61,15 +65,20 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
     /** One signature to decide: `by` signed `message`. */
     class Item(val by: PublicKey, val signature: ByteArray, val message: ByteArray)
 
-    /** CHIP_* status byte of every item, one device batch (isValid = Crypto.isValid semantics). */
+    /** CHIP_* status byte of every item, one device batch (isValid = Crypto.isValid semantics); null when the device
+     *  failed (CHIP_E_DEVICE / CHIP_E_NOMEM): the caller decides the batch on the JCA path. */
     @Synchronized
-    fun statuses(items: List<Item>, isValid: Boolean = false): ByteArray {
+    fun statuses(items: List<Item>, isValid: Boolean = false): ByteArray? {
         val n = items.size
         if (n == 0) return ByteArray(0)
         if (stableKeys && poolKeys.size + n > stableKeyLimit) { poolIds.clear(); poolKeys.clear() }
-        val keyIds = if (stableKeys) poolIds else HashMap<ByteBuffer, Int>()
+        // The stable pool only pays while the library can keep its key state: past one key per 16 signatures of
+        // the batch the per-key tables are not built (the eager comb schedule needs nk <= n / 16) and the key cache
+        // does not apply, so a call that small sends its own keys only (the stable pool is kept for later calls).
+        val useStable = stableKeys && 16L * poolKeys.size <= n
+        val keyIds = if (useStable) poolIds else HashMap<ByteBuffer, Int>()
         val msgIds = HashMap<ByteBuffer, Int>()
-        val keys = if (stableKeys) poolKeys else ArrayList<ByteArray>()
+        val keys = if (useStable) poolKeys else ArrayList<ByteArray>()
         val msgs = ArrayList<ByteArray>()
         val keyIdx = IntArray(n)
         val msgIdx = IntArray(n)
@@ -80,8 +89,8 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
             msgIdx[i] = msgIds.getOrPut(ByteBuffer.wrap(it.message)) { msgs.add(it.message); msgs.size - 1 }
             sigBytes += it.signature.size
         }
-        val keyBytes = keys.sumOf { it.size.toLong() }
-        val msgBytes = msgs.sumOf { it.size.toLong() }
+        val keyBytes = keys.sumByLong { it.size.toLong() }
+        val msgBytes = msgs.sumByLong { it.size.toLong() }
         // arena layout: index arrays (u32), offset arrays (u64), length arrays (u32), then the pools
         val total = 4L * n * 3 + 8L * n + 12L * keys.size + 12L * msgs.size + sigBytes + keyBytes + msgBytes + 256   // + alignment of 11 slices
         require(total < Int.MAX_VALUE) { "batch too large for one call" }
@@ -112,9 +121,12 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
         val (kData, kOff, kLen) = pool(keys, keyBytes)
         val (mData, mOff, mLen) = pool(msgs, msgBytes)
         val st = statusBuf.reserve(n)
-        val rc = CordaHip.verifyBatch(ctx, isValid, n, bKeyIdx, bMsgIdx, bSigs, bSigOff, bSigLen,
+        val rc = if (gpu.isGroup)
+            CordaHip.groupVerifyBatch(gpu.group, isValid, n, bKeyIdx, bMsgIdx, bSigs, bSigOff, bSigLen,
+                    keys.size, kData, kOff, kLen, msgs.size, mData, mOff, mLen, st)
+        else CordaHip.verifyBatch(gpu.ctx, isValid, n, bKeyIdx, bMsgIdx, bSigs, bSigOff, bSigLen,
                 keys.size, kData, kOff, kLen, msgs.size, mData, mOff, mLen, st)
-        check(rc == 0) { "libcordahip verifyBatch failed ($rc): ${CordaHip.lastError(ctx)}" }
+        if (!gpu.ok(rc, "verifyBatch")) return null
         val out = ByteArray(n)
         st.get(out, 0, n)
         return out
@@ -131,8 +143,16 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
             return
         }
         val st = statuses(sigs.map { Item(it.by, it.bytes, signable(id, it.signatureMetadata)) })
+        if (st == null) {   // device failure: the reference loop
+            for (sig in sigs) sig.verify(id)
+            return
+        }
         for ((i, s) in st.withIndex()) if (s.toInt() != CordaHip.VALID) sigs[i].verify(id)   // throws as the JCA path does
     }
+
+    /** The reference loop of each transaction on the JVM (small batches, device failures). */
+    private fun jvmSignatures(txs: List<SignedTransaction>): List<Exception?> =
+            txs.map { tx -> try { tx.sigs.forEach { it.verify(tx.id) }; null } catch (e: Exception) { e } }
 
     /**
      * Many transactions in one device batch (the ResolveTransactionsFlow.kt:91-98 batch site):
@@ -140,13 +160,13 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
      * sequential call would have thrown first.
      */
     fun checkSignaturesAreValid(txs: List<SignedTransaction>): List<Exception?> {
-        if (txs.sumOf { it.sigs.size } < minBatch)   // small batch: each transaction's own sequential check
-            return txs.map { tx -> try { tx.sigs.forEach { it.verify(tx.id) }; null } catch (e: Exception) { e } }
+        if (txs.sumBy { it.sigs.size } < minBatch)   // small batch: each transaction's own sequential check
+            return jvmSignatures(txs)
         val items = ArrayList<Item>()
         val messages = HashMap<Pair<SecureHash, SignatureMetadata>, ByteArray>()
         for (tx in txs) for (s in tx.sigs)
             items.add(Item(s.by, s.bytes, messages.getOrPut(tx.id to s.signatureMetadata) { signable(tx.id, s.signatureMetadata) }))
-        val st = statuses(items)
+        val st = statuses(items) ?: return jvmSignatures(txs)
         var p = 0
         return txs.map { tx ->
             var err: Exception? = null
@@ -212,7 +232,7 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
             reqStart[t + 1] = allowed.size.toLong()
         }
         val b = arena.reserve(64 + 8 * (2 * txs.size + nodeStart.size + keys.size) + 4 * (keyIdx.size + keys.size +
-                3 * vals.size) + keys.sumOf { it.size } + allowed.size + 16 * txs.size + allowed.size + 1024)
+                3 * vals.size) + keys.sumBy { it.size } + allowed.size + 16 * txs.size + allowed.size + 1024)
         fun take(bytes: Int): ByteBuffer {
             val s = b.slice().order(ByteOrder.LITTLE_ENDIAN)
             s.limit(maxOf(bytes, 1))
@@ -221,7 +241,7 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
         }
         val bKeyIdx = take(4 * keyIdx.size).apply { keyIdx.forEach { putInt(it) } }
         val bKeyOff = take(8 * keys.size); val bKeyLen = take(4 * keys.size)
-        val bKeys = take(keys.sumOf { it.size })
+        val bKeys = take(keys.sumBy { it.size })
         var o = 0L
         for (k in keys) { bKeyOff.putLong(o); bKeyLen.putInt(k.size); bKeys.put(k); o += k.size }
         // statuses: all VALID (a transaction with a failing signature already has its exception, sigErr)
@@ -234,10 +254,14 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
         val bNk = take(4 * nkids.size).apply { nkids.forEach { putInt(it) } }
         val bW = take(4 * weights.size).apply { weights.forEach { putInt(it) } }
         val bVerdict = take(txs.size); val bArg = take(4 * txs.size); val bMissing = take(allowed.size)
-        val rc = CordaHip.requiredSigners(ctx, keyIdx.size, bKeyIdx, keys.size, bKeys, bKeyOff, bKeyLen, bStatus,
+        val rc = CordaHip.requiredSigners(gpu.ctx, keyIdx.size, bKeyIdx, keys.size, bKeys, bKeyOff, bKeyLen, bStatus,
                 txs.size, bSigStart, bReqStart, allowed.size, bNodeStart, bAllowed, vals.size, bVal, bNk, bW,
                 bVerdict, bArg, bMissing)
-        check(rc == 0) { "libcordahip requiredSigners failed ($rc): ${CordaHip.lastError(ctx)}" }
+        if (!gpu.ok(rc, "requiredSigners"))   // device failure: the reference's own check of each transaction
+            return txs.mapIndexed { t, tx ->
+                sigErr[t] ?: invalid[t] ?: try { tx.verifySignaturesExcept(*allowedToBeMissing.toTypedArray()); null }
+                catch (e: Exception) { e }
+            }
         return txs.mapIndexed { t, tx ->
             sigErr[t] ?: invalid[t] ?: when (bVerdict.get(t).toInt()) {
                 0 -> null
@@ -262,8 +286,8 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
      */
     fun verifySignaturesExceptFused(txs: List<SignedTransaction>, allowedToBeMissing: Set<PublicKey> = emptySet()): List<Exception?> {
         if (txs.isEmpty()) return emptyList()
-        if (txs.sumOf { it.sigs.size } < minBatch)
-            return txs.map { try { it.verifySignaturesExcept(*allowedToBeMissing.toTypedArray()); null } catch (e: Exception) { e } }
+        fun jvm() = txs.map { try { it.verifySignaturesExcept(*allowedToBeMissing.toTypedArray()); null } catch (e: Exception) { e } }
+        if (txs.sumBy { it.sigs.size } < minBatch) return jvm()
         // templates: SignableData(id, meta) bytes without the id, one per metadata value in the batch
         val metaIdx = HashMap<SignatureMetadata, Int>()
         val tmpls = ArrayList<Pair<ByteArray, Int>>()
@@ -276,10 +300,10 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
         val keyIds = HashMap<ByteBuffer, Int>()
         val keys = ArrayList<ByteArray>()
         fun keyIndex(k: PublicKey): Int { val e = k.encoded; return keyIds.getOrPut(ByteBuffer.wrap(e)) { keys.add(e); keys.size - 1 } }
-        val nSig = txs.sumOf { it.sigs.size }
-        val comps = txs.sumOf { t -> t.tx.componentGroups.sumOf { it.components.size } }
-        val compBytes = txs.sumOf { t -> t.tx.componentGroups.sumOf { g -> g.components.sumOf { it.size.toLong() } } }
-        val sigBytes = txs.sumOf { t -> t.sigs.sumOf { it.bytes.size.toLong() } }
+        val nSig = txs.sumBy { it.sigs.size }
+        val comps = txs.sumBy { t -> t.tx.componentGroups.sumBy { it.components.size } }
+        val compBytes = txs.sumByLong { t -> t.tx.componentGroups.sumByLong { g -> g.components.sumByLong { it.size.toLong() } } }
+        val sigBytes = txs.sumByLong { t -> t.sigs.sumByLong { it.bytes.size.toLong() } }
         // required key trees, flattened as verifySignaturesExcept does
         val vals = ArrayList<Int>(); val nkids = ArrayList<Int>(); val weights = ArrayList<Int>()
         val sigKeyIdx = txs.map { tx -> tx.sigs.map { keyIndex(it.by) } }
@@ -311,9 +335,9 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
             }
             reqStart[t + 1] = allowed.size.toLong()
         }
-        val keyBytes = keys.sumOf { it.size.toLong() }
+        val keyBytes = keys.sumByLong { it.size.toLong() }
         val total = 32L * txs.size + 8L * (txs.size + 1) * 3 + 16L * comps + compBytes + 24L * tmpls.size +
-                tmpls.sumOf { it.first.size.toLong() } + 24L * nSig + sigBytes + 12L * keys.size + keyBytes +
+                tmpls.sumByLong { it.first.size.toLong() } + 24L * nSig + sigBytes + 12L * keys.size + keyBytes +
                 8L * nodeStart.size + allowed.size + 12L * vals.size + 38L * txs.size + allowed.size + nSig + 32 * 64
         require(total < Int.MAX_VALUE) { "batch too large for one call" }
         val b = arena.reserve(total.toInt())
@@ -337,7 +361,7 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
             }
             bTxCompStart.putLong(c)
         }
-        val bTd = take(tmpls.sumOf { it.first.size.toLong() }); val bTo = take(8L * tmpls.size)
+        val bTd = take(tmpls.sumByLong { it.first.size.toLong() }); val bTo = take(8L * tmpls.size)
         val bTl = take(4L * tmpls.size); val bTa = take(4L * tmpls.size)
         o = 0L
         for ((bytes, at) in tmpls) { bTo.putLong(o); bTl.putInt(bytes.size); bTa.putInt(at); bTd.put(bytes); o += bytes.size }
@@ -363,18 +387,22 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
         val bNk = take(4L * nkids.size).apply { nkids.forEach { putInt(it) } }
         val bW = take(4L * weights.size).apply { weights.forEach { putInt(it) } }
         val bStatus = take(nSig.toLong()); val bVerdict = take(n.toLong()); val bArg = take(4L * n)
-        val rc = CordaHip.verifySignedTxBatch(ctx, n, bSalts, bTxCompStart, comps, bGroup, bInternal, bData, bCompOff,
+        val rc = if (gpu.isGroup)
+            CordaHip.groupVerifySignedTxBatch(gpu.group, n, bSalts, bTxCompStart, comps, bGroup, bInternal, bData,
+                    bCompOff, bCompLen, tmpls.size, bTd, bTo, bTl, bTa, nSig, bTxIdx, bTmplIdx, bKeyIdx, bSigData, bSigOff,
+                    bSigLen, keys.size, bKeys, bKeyOff, bKeyLen, bSigStart, bReqStart, allowed.size, bNodeStart, bAllowed,
+                    vals.size, bVal, bNk, bW, null, bStatus, bVerdict, bArg, null)
+        else CordaHip.verifySignedTxBatch(gpu.ctx, n, bSalts, bTxCompStart, comps, bGroup, bInternal, bData, bCompOff,
                 bCompLen, tmpls.size, bTd, bTo, bTl, bTa, nSig, bTxIdx, bTmplIdx, bKeyIdx, bSigData, bSigOff, bSigLen,
                 keys.size, bKeys, bKeyOff, bKeyLen, bSigStart, bReqStart, allowed.size, bNodeStart, bAllowed,
                 vals.size, bVal, bNk, bW, null, bStatus, bVerdict, bArg, null)
-        check(rc == 0) { "libcordahip verifySignedTxBatch failed ($rc): ${CordaHip.lastError(ctx)}" }
+        if (!gpu.ok(rc, "verifySignedTxBatch")) return jvm()
         return txs.mapIndexed { t, tx ->
             if (invalid[t] == null && bVerdict.get(t).toInt() == 0) null
             else try { tx.verifySignaturesExcept(*allowedToBeMissing.toTypedArray()); null } catch (e: Exception) { e }
         }
     }
 
-    /** Crypto.isValid(PublicKey, ByteArray, ByteArray) on the device; decode errors still throw. */
     /**
      * verifySignaturesExcept for transactions still in their serialized form (vault rows, P2P payloads,
      * ResolveTransactionsFlow downloads): the bytes go to the device, which parses them (Kryo front end),
@@ -385,8 +413,8 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
      */
     fun verifySerialized(txs: List<SerializedBytes<SignedTransaction>>): List<Exception?> {
         if (txs.isEmpty()) return emptyList()
-        if (2 * txs.size < minBatch)   // small batch (~2 signatures per transaction): the JVM path as today
-            return txs.map { try { it.deserialize().verifySignaturesExcept(); null } catch (e: Exception) { e } }
+        fun jvm() = txs.map { try { it.deserialize().verifySignaturesExcept(); null } catch (e: Exception) { e } }
+        if (2 * txs.size < minBatch) return jvm()   // small batch (~2 signatures per transaction): the JVM path as today
         // SignableData templates for the metadata values this node signs with (platform version 1)
         val metas = listOf(SignatureMetadata(1, Crypto.EDDSA_ED25519_SHA512.schemeNumberID),
                 SignatureMetadata(1, Crypto.ECDSA_SECP256R1_SHA256.schemeNumberID),
@@ -397,8 +425,8 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
             val at = a.indices.first { a[it] != b[it] }
             Pair(a.copyOfRange(0, at) + a.copyOfRange(at + 32, a.size), at)
         }
-        val total = txs.sumOf { it.size }
-        val b = arena.reserve(total + 64 * txs.size + tmpls.sumOf { it.first.size } + 64 * tmpls.size + 1024)
+        val total = txs.sumBy { it.size }
+        val b = arena.reserve(total + 64 * txs.size + tmpls.sumBy { it.first.size } + 64 * tmpls.size + 1024)
         fun take(bytes: Int): ByteBuffer {
             val s = b.slice().order(ByteOrder.LITTLE_ENDIAN)
             s.limit(maxOf(bytes, 1))
@@ -408,15 +436,18 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
         val bData = take(total); val bOff = take(8 * txs.size); val bLen = take(4 * txs.size)
         var o = 0L
         for (t in txs) { bOff.putLong(o); bLen.putInt(t.size); bData.put(t.bytes, t.offset, t.size); o += t.size }
-        val bTd = take(tmpls.sumOf { it.first.size }); val bTo = take(8 * tmpls.size); val bTl = take(4 * tmpls.size)
+        val bTd = take(tmpls.sumBy { it.first.size }); val bTo = take(8 * tmpls.size); val bTl = take(4 * tmpls.size)
         val bTa = take(4 * tmpls.size); val bMeta = take(8 * metas.size)
         o = 0L
         for ((bytes, at) in tmpls) { bTo.putLong(o); bTl.putInt(bytes.size); bTa.putInt(at); bTd.put(bytes); o += bytes.size }
         for (m in metas) { bMeta.putInt(m.platformVersion); bMeta.putInt(m.schemeNumberID) }
         val bStatus = take(txs.size); val bVerdict = take(txs.size); val bArg = take(4 * txs.size)
-        val rc = CordaHip.stxVerify(ctx, txs.size, bData, bOff, bLen, tmpls.size, bTd, bTo, bTl, bTa, bMeta,
+        val rc = if (gpu.isGroup)
+            CordaHip.groupStxVerify(gpu.group, txs.size, bData, bOff, bLen, tmpls.size, bTd, bTo, bTl, bTa, bMeta,
+                    bStatus, bVerdict, bArg, null)
+        else CordaHip.stxVerify(gpu.ctx, txs.size, bData, bOff, bLen, tmpls.size, bTd, bTo, bTl, bTa, bMeta,
                 bStatus, bVerdict, bArg, null)
-        check(rc == 0) { "libcordahip stxVerify failed ($rc): ${CordaHip.lastError(ctx)}" }
+        if (!gpu.ok(rc, "stxVerify")) return jvm()
         return txs.mapIndexed { t, bytes ->
             if (bStatus.get(t).toInt() == 0 && bVerdict.get(t).toInt() == 0) null
             else try {
@@ -425,8 +456,10 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
         }
     }
 
+    /** Crypto.isValid(PublicKey, ByteArray, ByteArray) on the device; decode errors still throw (and so does
+     *  everything on the JCA path after a device failure). */
     fun isValid(key: PublicKey, signature: ByteArray, clearData: ByteArray): Boolean =
-            when (statuses(listOf(Item(key, signature, clearData)), isValid = true)[0].toInt()) {
+            when (statuses(listOf(Item(key, signature, clearData)), isValid = true)?.get(0)?.toInt()) {
                 CordaHip.VALID -> true
                 CordaHip.INVALID -> false
                 else -> Crypto.isValid(key, signature, clearData)   // the exact JCA exception (or UNSUPPORTED keys)
@@ -435,6 +468,6 @@ class BatchSignatureVerifier(device: Int = 0, flags: Int = 0,
     override fun close() {
         arena.close()
         statusBuf.close()
-        CordaHip.close(ctx)
+        gpu.close()
     }
 }

@@ -7,6 +7,7 @@ import net.corda.core.identity.CordaX500Name
 import net.corda.core.identity.Party
 import net.corda.core.internal.gpu.CordaHip
 import net.corda.core.internal.gpu.PinnedBuffer
+import net.corda.core.internal.gpu.sumByLong
 import net.corda.core.node.services.UniquenessException
 import net.corda.core.node.services.UniquenessProvider
 import java.io.DataInputStream
@@ -35,9 +36,24 @@ import java.nio.file.StandardOpenOption
  * `logFile.parties`.  A failed append leaves the device table ahead of the log, so the provider fails
  * stop: every later call throws until it is reopened (which rebuilds from what reached the disk).
  */
-class GpuUniquenessProvider(logFile: File, capacity: Long = 1L shl 24, device: Int = 0) : UniquenessProvider, AutoCloseable {
-    private val ctx = CordaHip.open(device, 0).also { check(it != 0L) { "libcordahip: no GPU $device" } }
-    private val table = CordaHip.uniqOpen(ctx, capacity).also { check(it != 0L) { CordaHip.lastError(ctx) } }
+class GpuUniquenessProvider(logFile: File, capacity: Long = 1L shl 24, devices: IntArray = intArrayOf(0)) :
+        UniquenessProvider, AutoCloseable {
+    /** One GPU. */
+    constructor(logFile: File, capacity: Long, device: Int) : this(logFile, capacity, intArrayOf(device))
+
+    // one GPU: a chip_uniq on its context; several: a device group whose members each hold the states of their slice
+    // of the StateRef key space (chip_group_uniq_*: one vote byte per transaction per ordered-commit round between
+    // the members, reduced in the library)
+    private val group = if (devices.size > 1) CordaHip.groupOpen(devices, 0).also {
+        check(it != 0L) { "libcordahip: no usable device group for ${devices.joinToString()}" }
+    } else 0L
+    private val ctx = if (group != 0L) 0L else CordaHip.open(devices[0], 0).also {
+        check(it != 0L) { "libcordahip: no GPU ${devices[0]}" }
+    }
+    private val table = (if (group != 0L) CordaHip.groupUniqOpen(group, capacity) else CordaHip.uniqOpen(ctx, capacity)).also {
+        check(it != 0L) { if (group != 0L) CordaHip.groupLastError(group) else CordaHip.lastError(ctx) }
+    }
+    private fun tableError(): String = if (group != 0L) CordaHip.groupUniqLastError(table) else CordaHip.uniqLastError(table)
     private val log: FileChannel
     private val partyFile = File(logFile.path + ".parties")
     private val parties = ArrayList<Party>()
@@ -71,8 +87,9 @@ class GpuUniquenessProvider(logFile: File, capacity: Long = 1L shl 24, device: I
                 idx.put(row, 68, 4)
                 caller.put(row, 72, 4)
             }
-            val rc = CordaHip.uniqRebuild(table, rows, refs, ids, idx, caller)
-            check(rc == 0) { "rebuild failed: ${CordaHip.uniqLastError(table)}" }
+            val rc = if (group != 0L) CordaHip.groupUniqRebuild(table, rows, refs, ids, idx, caller)
+                     else CordaHip.uniqRebuild(table, rows, refs, ids, idx, caller)
+            check(rc == 0) { "rebuild failed: ${tableError()}" }
         }
         log.position(rows.toLong() * ROW)
     }
@@ -87,7 +104,7 @@ class GpuUniquenessProvider(logFile: File, capacity: Long = 1L shl 24, device: I
         failed?.let { throw IllegalStateException("commit log append failed earlier; reopen the provider", it) }
         val ntx = requests.size
         if (ntx == 0) return emptyList()
-        val nref = requests.sumOf { it.states.size }
+        val nref = requests.sumBy { it.states.size }
         val bytes = 8 * (ntx + 1) + 36 * nref + 32 * ntx + 4 * ntx + ntx + CordaHip.CONFLICT_BYTES * (nref + 1) + 64
         val a = io.reserve(bytes)
         fun take(n: Int): ByteBuffer {
@@ -113,8 +130,14 @@ class GpuUniquenessProvider(logFile: File, capacity: Long = 1L shl 24, device: I
             callers.putInt(partyId(req.callerIdentity))
         }
         val nOut = LongArray(1)
-        val rc = CordaHip.uniqCommitBatch(table, ntx, start, refs, ids, callers, status, out, cap, nOut)
-        check(rc == 0) { "uniqueness commit failed ($rc): ${CordaHip.uniqLastError(table)}" }
+        val rc = if (group != 0L) CordaHip.groupUniqCommitBatch(table, ntx, start, refs, ids, callers, status, out, cap, nOut)
+                 else CordaHip.uniqCommitBatch(table, ntx, start, refs, ids, callers, status, out, cap, nOut)
+        // No JVM fallback here: the committed states live in the device table, so a failed commit is fail-stop like
+        // a failed log append (the table may be ahead of the log; a reopen rebuilds from what reached the disk).
+        if (rc != 0) {
+            failed = IllegalStateException("uniqueness commit failed ($rc): ${tableError()}")
+            throw failed!!
+        }
         // conflict records, ordered by (tx, input index): Conflict.stateHistory of each failed tx
         val history = HashMap<Int, LinkedHashMap<StateRef, UniquenessProvider.ConsumingTx>>()
         for (k in 0 until nOut[0].toInt()) {
@@ -196,13 +219,18 @@ class GpuUniquenessProvider(logFile: File, capacity: Long = 1L shl 24, device: I
         }
     }
 
-    val size: Long get() = CordaHip.uniqSize(table)
+    val size: Long get() = if (group != 0L) CordaHip.groupUniqSize(table) else CordaHip.uniqSize(table)
 
     override fun close() {
         log.close()
         io.close()
-        CordaHip.uniqClose(table)
-        CordaHip.close(ctx)
+        if (group != 0L) {
+            CordaHip.groupUniqClose(table)
+            CordaHip.groupClose(group)
+        } else {
+            CordaHip.uniqClose(table)
+            CordaHip.close(ctx)
+        }
     }
 
     private companion object {

@@ -20,7 +20,10 @@
  *                    -> chip_ftx_verify_batch
  *   stxVerify        the same from SerializedBytes<SignedTransaction> (ResolveTransactionsFlow.kt:91-98)
  *   uniq*            UniquenessProvider.commit (UniquenessProvider.kt:15-17),
- *                    PersistentUniquenessProvider.commit (PersistentUniquenessProvider.kt:92-113) */
+ *                    PersistentUniquenessProvider.commit (PersistentUniquenessProvider.kt:92-113)
+ *   group*           the same entries over a device group (chip_group_*: every GPU of the node behind one handle,
+ *                    batches split by transaction ranges, the notary table by StateRef key-space shards), so the
+ *                    node's one JVM drives N GPUs (ResolveTransactionsFlow.kt:88-96, NotaryService.kt:61-75) */
 #include <jni.h>
 #include <stdint.h>
 #include <string.h>
@@ -68,12 +71,9 @@ JNIEXPORT void JNICALL CLS(freePinned)(JNIEnv* env, jclass cls, jobject buf) {
 /* ---- signatures (chip_sig_batch SoA) ----
  * status: n bytes out (CHIP_* per signature).  isValid selects Crypto.isValid semantics
  * (chip_is_valid_batch: no empty-input checks) over Crypto.doVerify's. */
-JNIEXPORT jint JNICALL CLS(verifyBatch)(JNIEnv* env, jclass cls, jlong ctx, jboolean isValid, jint n,
-                                        jobject keyIdx, jobject msgIdx, jobject sigData, jobject sigOff,
-                                        jobject sigLen, jint nKeys, jobject keyData, jobject keyOff, jobject keyLen,
-                                        jint nMsgs, jobject msgData, jobject msgOff, jobject msgLen,
-                                        jobject status) {
-    (void)cls;
+static jint verify_batch(JNIEnv* env, int group, jlong h, jboolean isValid, jint n, jobject keyIdx, jobject msgIdx,
+                         jobject sigData, jobject sigOff, jobject sigLen, jint nKeys, jobject keyData, jobject keyOff,
+                         jobject keyLen, jint nMsgs, jobject msgData, jobject msgOff, jobject msgLen, jobject status) {
     chip_sig_batch b;
     memset(&b, 0, sizeof b);
     b.n = (uint64_t)n;
@@ -95,8 +95,22 @@ JNIEXPORT jint JNICALL CLS(verifyBatch)(JNIEnv* env, jclass cls, jlong ctx, jboo
     b.msg_bytes = cap_of(env, msgData);
     uint8_t* st = (uint8_t*)addr(env, status);
     if (n < 0 || (n > 0 && (!st || cap_of(env, status) < (uint64_t)n))) return CHIP_E_ARG;
-    chip_ctx* c = (chip_ctx*)(intptr_t)ctx;
+    if (group) {
+        chip_group* g = (chip_group*)(intptr_t)h;
+        return isValid ? chip_group_is_valid_batch(g, &b, st, NULL) : chip_group_verify_batch(g, &b, st, NULL);
+    }
+    chip_ctx* c = (chip_ctx*)(intptr_t)h;
     return isValid ? chip_is_valid_batch(c, &b, st, NULL) : chip_verify_batch(c, &b, st, NULL);
+}
+
+JNIEXPORT jint JNICALL CLS(verifyBatch)(JNIEnv* env, jclass cls, jlong ctx, jboolean isValid, jint n,
+                                        jobject keyIdx, jobject msgIdx, jobject sigData, jobject sigOff,
+                                        jobject sigLen, jint nKeys, jobject keyData, jobject keyOff, jobject keyLen,
+                                        jint nMsgs, jobject msgData, jobject msgOff, jobject msgLen,
+                                        jobject status) {
+    (void)cls;
+    return verify_batch(env, 0, ctx, isValid, n, keyIdx, msgIdx, sigData, sigOff, sigLen, nKeys, keyData, keyOff, keyLen,
+                        nMsgs, msgData, msgOff, msgLen, status);
 }
 
 /* ---- required signers (chip_req_batch over the key pool / statuses of a verified batch) ----
@@ -139,10 +153,8 @@ JNIEXPORT jint JNICALL CLS(requiredSigners)(JNIEnv* env, jclass cls, jlong ctx, 
 }
 
 /* ---- tx ids (chip_tx_batch SoA); ids: ntx * 32 bytes out ---- */
-JNIEXPORT jint JNICALL CLS(txIds)(JNIEnv* env, jclass cls, jlong ctx, jint ntx, jobject salts, jobject txCompStart,
-                                  jint nComp, jobject compGroup, jobject compInternal, jobject data,
-                                  jobject compOff, jobject compLen, jobject ids) {
-    (void)cls;
+static jint tx_ids(JNIEnv* env, int group, jlong h, jint ntx, jobject salts, jobject txCompStart, jint nComp,
+                   jobject compGroup, jobject compInternal, jobject data, jobject compOff, jobject compLen, jobject ids) {
     chip_tx_batch b;
     memset(&b, 0, sizeof b);
     b.ntx = (uint64_t)ntx;
@@ -157,7 +169,14 @@ JNIEXPORT jint JNICALL CLS(txIds)(JNIEnv* env, jclass cls, jlong ctx, jint ntx, 
     b.data_bytes = cap_of(env, data);
     uint8_t* out = (uint8_t*)addr(env, ids);
     if (ntx < 0 || (ntx > 0 && (!out || cap_of(env, ids) < 32ull * (uint64_t)ntx))) return CHIP_E_ARG;
-    return chip_txid_batch((chip_ctx*)(intptr_t)ctx, &b, out);
+    return group ? chip_group_txid_batch((chip_group*)(intptr_t)h, &b, out) : chip_txid_batch((chip_ctx*)(intptr_t)h, &b, out);
+}
+
+JNIEXPORT jint JNICALL CLS(txIds)(JNIEnv* env, jclass cls, jlong ctx, jint ntx, jobject salts, jobject txCompStart,
+                                  jint nComp, jobject compGroup, jobject compInternal, jobject data,
+                                  jobject compOff, jobject compLen, jobject ids) {
+    (void)cls;
+    return tx_ids(env, 0, ctx, ntx, salts, txCompStart, nComp, compGroup, compInternal, data, compOff, compLen, ids);
 }
 
 /* ---- the fused SignedTransaction.verifySignaturesExcept of a batch (chip_verify_signed_tx_batch) ----
@@ -165,18 +184,15 @@ JNIEXPORT jint JNICALL CLS(txIds)(JNIEnv* env, jclass cls, jlong ctx, jint ntx, 
  * SignableData bytes of each SignatureMetadata without the id, and where the id goes; required keys as
  * requiredSigners.  ids (ntx * 32, may be null), status (nSig), verdict (ntx), arg (4 * ntx), missing (nreq,
  * may be null) out. */
-JNIEXPORT jint JNICALL CLS(verifySignedTxBatch)(JNIEnv* env, jclass cls, jlong ctx, jint ntx, jobject salts,
-                                                jobject txCompStart, jint nComp, jobject compGroup, jobject compInternal,
-                                                jobject data, jobject compOff, jobject compLen, jint nTmpl,
-                                                jobject tmplData, jobject tmplOff, jobject tmplLen, jobject tmplIdAt,
-                                                jint nSig, jobject txIdx, jobject tmplIdx, jobject keyIdx,
-                                                jobject sigData, jobject sigOff, jobject sigLen, jint nKeys,
-                                                jobject keyData, jobject keyOff, jobject keyLen, jobject sigStart,
-                                                jobject reqStart, jint nreq, jobject nodeStart, jobject allowed,
-                                                jint nNodes, jobject nodeVal, jobject nodeNkids, jobject nodeWeight,
-                                                jobject ids, jobject status, jobject verdict, jobject arg,
-                                                jobject missing) {
-    (void)cls;
+static jint verify_signed_tx_batch(JNIEnv* env, int group, jlong h, jint ntx, jobject salts, jobject txCompStart,
+                                   jint nComp, jobject compGroup, jobject compInternal, jobject data, jobject compOff,
+                                   jobject compLen, jint nTmpl, jobject tmplData, jobject tmplOff, jobject tmplLen,
+                                   jobject tmplIdAt, jint nSig, jobject txIdx, jobject tmplIdx, jobject keyIdx,
+                                   jobject sigData, jobject sigOff, jobject sigLen, jint nKeys, jobject keyData,
+                                   jobject keyOff, jobject keyLen, jobject sigStart, jobject reqStart, jint nreq,
+                                   jobject nodeStart, jobject allowed, jint nNodes, jobject nodeVal, jobject nodeNkids,
+                                   jobject nodeWeight, jobject ids, jobject status, jobject verdict, jobject arg,
+                                   jobject missing) {
     if (ntx < 0 || nComp < 0 || nTmpl < 0 || nSig < 0 || nKeys < 0 || nreq < 0 || nNodes < 0) return CHIP_E_ARG;
     chip_tx_batch t;
     memset(&t, 0, sizeof t);
@@ -237,7 +253,27 @@ JNIEXPORT jint JNICALL CLS(verifySignedTxBatch)(JNIEnv* env, jclass cls, jlong c
         (ntx > 0 && (!v || !a || cap_of(env, verdict) < (uint64_t)ntx || cap_of(env, arg) < 4ull * (uint64_t)ntx)) ||
         (miss && cap_of(env, missing) < (uint64_t)nreq))
         return CHIP_E_ARG;
-    return chip_verify_signed_tx_batch((chip_ctx*)(intptr_t)ctx, &t, &m, &s, &q, idOut, st, v, a, miss);
+    if (group) return chip_group_verify_signed_tx_batch((chip_group*)(intptr_t)h, &t, &m, &s, &q, idOut, st, v, a, miss);
+    return chip_verify_signed_tx_batch((chip_ctx*)(intptr_t)h, &t, &m, &s, &q, idOut, st, v, a, miss);
+}
+
+JNIEXPORT jint JNICALL CLS(verifySignedTxBatch)(JNIEnv* env, jclass cls, jlong ctx, jint ntx, jobject salts,
+                                                jobject txCompStart, jint nComp, jobject compGroup, jobject compInternal,
+                                                jobject data, jobject compOff, jobject compLen, jint nTmpl,
+                                                jobject tmplData, jobject tmplOff, jobject tmplLen, jobject tmplIdAt,
+                                                jint nSig, jobject txIdx, jobject tmplIdx, jobject keyIdx,
+                                                jobject sigData, jobject sigOff, jobject sigLen, jint nKeys,
+                                                jobject keyData, jobject keyOff, jobject keyLen, jobject sigStart,
+                                                jobject reqStart, jint nreq, jobject nodeStart, jobject allowed,
+                                                jint nNodes, jobject nodeVal, jobject nodeNkids, jobject nodeWeight,
+                                                jobject ids, jobject status, jobject verdict, jobject arg,
+                                                jobject missing) {
+    (void)cls;
+    return verify_signed_tx_batch(env, 0, ctx, ntx, salts, txCompStart, nComp, compGroup, compInternal, data, compOff,
+                                  compLen, nTmpl, tmplData, tmplOff, tmplLen, tmplIdAt, nSig, txIdx, tmplIdx, keyIdx,
+                                  sigData, sigOff, sigLen, nKeys, keyData, keyOff, keyLen, sigStart, reqStart, nreq,
+                                  nodeStart, allowed, nNodes, nodeVal, nodeNkids, nodeWeight, ids, status, verdict, arg,
+                                  missing);
 }
 
 /* ---- FilteredTransaction.verify + checkAllComponentsVisible (chip_ftx_verify_batch) ----
@@ -245,12 +281,10 @@ JNIEXPORT jint JNICALL CLS(verifySignedTxBatch)(JNIEnv* env, jclass cls, jlong c
  * flow passes INPUTS_GROUP | TIMEWINDOW_GROUP bits) select the visibility checks.  status (ntx: 0 OK,
  * 1 FilteredTransactionVerificationException, 2 ComponentVisibilityException) and reason (ntx CHIP_FTX_*,
  * may be null) out. */
-JNIEXPORT jint JNICALL CLS(ftxVerify)(JNIEnv* env, jclass cls, jlong ctx, jint ntx, jobject ids, jobject ghStart,
-                                      jobject groupHashes, jobject fgStart, jobject fgIndex, jobject compStart,
-                                      jobject compData, jobject compOff, jobject compLen, jobject nonces,
-                                      jobject ptStart, jobject ptTag, jobject ptHash, jobject checkVisible,
-                                      jobject visibleMask, jobject status, jobject reason) {
-    (void)cls;
+static jint ftx_verify(JNIEnv* env, int group, jlong h, jint ntx, jobject ids, jobject ghStart, jobject groupHashes,
+                       jobject fgStart, jobject fgIndex, jobject compStart, jobject compData, jobject compOff,
+                       jobject compLen, jobject nonces, jobject ptStart, jobject ptTag, jobject ptHash,
+                       jobject checkVisible, jobject visibleMask, jobject status, jobject reason) {
     if (ntx < 0) return CHIP_E_ARG;
     chip_ftx_batch b;
     memset(&b, 0, sizeof b);
@@ -277,15 +311,24 @@ JNIEXPORT jint JNICALL CLS(ftxVerify)(JNIEnv* env, jclass cls, jlong ctx, jint n
         (b.check_visible && cap_of(env, checkVisible) < 4ull * (uint64_t)ntx) ||
         (b.visible_mask && cap_of(env, visibleMask) < 4ull * (uint64_t)ntx))
         return CHIP_E_ARG;
-    return chip_ftx_verify_batch((chip_ctx*)(intptr_t)ctx, &b, st, rs);
+    if (group) return chip_group_ftx_verify_batch((chip_group*)(intptr_t)h, &b, st, rs);
+    return chip_ftx_verify_batch((chip_ctx*)(intptr_t)h, &b, st, rs);
+}
+
+JNIEXPORT jint JNICALL CLS(ftxVerify)(JNIEnv* env, jclass cls, jlong ctx, jint ntx, jobject ids, jobject ghStart,
+                                      jobject groupHashes, jobject fgStart, jobject fgIndex, jobject compStart,
+                                      jobject compData, jobject compOff, jobject compLen, jobject nonces,
+                                      jobject ptStart, jobject ptTag, jobject ptHash, jobject checkVisible,
+                                      jobject visibleMask, jobject status, jobject reason) {
+    (void)cls;
+    return ftx_verify(env, 0, ctx, ntx, ids, ghStart, groupHashes, fgStart, fgIndex, compStart, compData, compOff,
+                      compLen, nonces, ptStart, ptTag, ptHash, checkVisible, visibleMask, status, reason);
 }
 
 /* ---- the whole path from bytes: SignedTransaction blobs -> tx status + verdict (chip_stx_verify) ---- */
-JNIEXPORT jint JNICALL CLS(stxVerify)(JNIEnv* env, jclass cls, jlong ctx, jint n, jobject data, jobject off,
-                                      jobject len, jint nTmpl, jobject tmplData, jobject tmplOff, jobject tmplLen,
-                                      jobject tmplIdAt, jobject meta, jobject status, jobject verdict, jobject arg,
-                                      jobject ids) {
-    (void)cls;
+static jint stx_verify(JNIEnv* env, int group, jlong h, jint n, jobject data, jobject off, jobject len, jint nTmpl,
+                       jobject tmplData, jobject tmplOff, jobject tmplLen, jobject tmplIdAt, jobject meta, jobject status,
+                       jobject verdict, jobject arg, jobject ids) {
     chip_msg_templates t;
     memset(&t, 0, sizeof t);
     t.n = (uint64_t)nTmpl;
@@ -302,9 +345,23 @@ JNIEXPORT jint JNICALL CLS(stxVerify)(JNIEnv* env, jclass cls, jlong ctx, jint n
     if (n < 0 || nTmpl < 0 || (n > 0 && (!st || !v || !a || cap_of(env, status) < (uint64_t)n ||
                                          cap_of(env, verdict) < (uint64_t)n || cap_of(env, arg) < 4ull * (uint64_t)n)))
         return CHIP_E_ARG;
-    return chip_stx_verify((chip_ctx*)(intptr_t)ctx, (uint64_t)n, (const uint8_t*)addr(env, data),
+    if (group)
+        return chip_group_stx_verify((chip_group*)(intptr_t)h, (uint64_t)n, (const uint8_t*)addr(env, data),
+                                     (const uint64_t*)addr(env, off), (const uint32_t*)addr(env, len), cap_of(env, data),
+                                     &t, (const int32_t*)addr(env, meta), (uint32_t)nTmpl, st, v, a,
+                                     (uint8_t*)addr(env, ids));
+    return chip_stx_verify((chip_ctx*)(intptr_t)h, (uint64_t)n, (const uint8_t*)addr(env, data),
                            (const uint64_t*)addr(env, off), (const uint32_t*)addr(env, len), cap_of(env, data), &t,
                            (const int32_t*)addr(env, meta), (uint32_t)nTmpl, st, v, a, (uint8_t*)addr(env, ids));
+}
+
+JNIEXPORT jint JNICALL CLS(stxVerify)(JNIEnv* env, jclass cls, jlong ctx, jint n, jobject data, jobject off,
+                                      jobject len, jint nTmpl, jobject tmplData, jobject tmplOff, jobject tmplLen,
+                                      jobject tmplIdAt, jobject meta, jobject status, jobject verdict, jobject arg,
+                                      jobject ids) {
+    (void)cls;
+    return stx_verify(env, 0, ctx, n, data, off, len, nTmpl, tmplData, tmplOff, tmplLen, tmplIdAt, meta, status,
+                      verdict, arg, ids);
 }
 
 /* ---- notary uniqueness ---- */
@@ -341,19 +398,161 @@ JNIEXPORT jint JNICALL CLS(uniqRebuild)(JNIEnv* env, jclass cls, jlong u, jint n
 
 /* status: ntx bytes out (0 committed, 1 idempotent, 2 conflict); out: cap chip_conflict records
  * (56 B each); nOut[0] receives the full record count (CHIP_E_CAPACITY when it exceeds cap). */
-JNIEXPORT jint JNICALL CLS(uniqCommitBatch)(JNIEnv* env, jclass cls, jlong u, jint ntx, jobject txRefStart,
-                                            jobject refs, jobject txIds, jobject callers, jobject status,
-                                            jobject out, jint cap, jlongArray nOut) {
-    (void)cls;
+static jint uniq_commit(JNIEnv* env, int group, jlong u, jint ntx, jobject txRefStart, jobject refs, jobject txIds,
+                        jobject callers, jobject status, jobject out, jint cap, jlongArray nOut) {
     if (ntx < 0 || cap < 0 || !nOut) return CHIP_E_ARG;
     if (cap_of(env, out) < (uint64_t)cap * sizeof(chip_conflict) || cap_of(env, status) < (uint64_t)ntx)
         return CHIP_E_ARG;
     uint64_t n = 0;
-    const int r = chip_uniq_commit_batch((chip_uniq*)(intptr_t)u, (uint64_t)ntx, (const uint64_t*)addr(env, txRefStart),
-                                         (const uint8_t*)addr(env, refs), (const uint8_t*)addr(env, txIds),
-                                         (const uint32_t*)addr(env, callers), (uint8_t*)addr(env, status),
-                                         (chip_conflict*)addr(env, out), (uint64_t)cap, &n);
+    const uint64_t* start = (const uint64_t*)addr(env, txRefStart);
+    const uint8_t* r36 = (const uint8_t*)addr(env, refs);
+    const uint8_t* ids = (const uint8_t*)addr(env, txIds);
+    const uint32_t* call = (const uint32_t*)addr(env, callers);
+    uint8_t* st = (uint8_t*)addr(env, status);
+    chip_conflict* o = (chip_conflict*)addr(env, out);
+    const int r = group ? chip_group_uniq_commit_batch((chip_group_uniq*)(intptr_t)u, (uint64_t)ntx, start, r36, ids, call,
+                                                       st, o, (uint64_t)cap, &n)
+                        : chip_uniq_commit_batch((chip_uniq*)(intptr_t)u, (uint64_t)ntx, start, r36, ids, call, st, o,
+                                                 (uint64_t)cap, &n);
     const jlong nv = (jlong)n;
     (*env)->SetLongArrayRegion(env, nOut, 0, 1, &nv);
     return r;
+}
+
+JNIEXPORT jint JNICALL CLS(uniqCommitBatch)(JNIEnv* env, jclass cls, jlong u, jint ntx, jobject txRefStart,
+                                            jobject refs, jobject txIds, jobject callers, jobject status,
+                                            jobject out, jint cap, jlongArray nOut) {
+    (void)cls;
+    return uniq_commit(env, 0, u, ntx, txRefStart, refs, txIds, callers, status, out, cap, nOut);
+}
+
+/* ---- device groups: one handle over several GPUs (chip_group_*) ----
+ * devices: the member GPU ordinals (an ordinal may repeat); the entries below take the arguments of their
+ * single-context counterparts above, with the group handle. */
+JNIEXPORT jlong JNICALL CLS(groupOpen)(JNIEnv* env, jclass cls, jintArray devices, jint flags) {
+    (void)cls;
+    if (!devices) return 0;
+    const jsize n = (*env)->GetArrayLength(env, devices);
+    if (n <= 0 || n > 64) return 0;
+    jint dv[64];
+    (*env)->GetIntArrayRegion(env, devices, 0, n, dv);
+    int d[64];
+    for (jsize i = 0; i < n; i++) d[i] = (int)dv[i];
+    chip_config cfg = {0, (uint32_t)flags, 0};
+    chip_group* g = NULL;
+    return chip_group_init(d, (int)n, &cfg, &g) == CHIP_OK ? (jlong)(intptr_t)g : 0;
+}
+
+JNIEXPORT void JNICALL CLS(groupClose)(JNIEnv* env, jclass cls, jlong g) {
+    (void)env; (void)cls;
+    chip_group_shutdown((chip_group*)(intptr_t)g);
+}
+
+JNIEXPORT jstring JNICALL CLS(groupLastError)(JNIEnv* env, jclass cls, jlong g) {
+    (void)cls;
+    return (*env)->NewStringUTF(env, chip_group_last_error((chip_group*)(intptr_t)g));
+}
+
+JNIEXPORT jint JNICALL CLS(groupSize)(JNIEnv* env, jclass cls, jlong g) {
+    (void)env; (void)cls;
+    return chip_group_size((chip_group*)(intptr_t)g);
+}
+
+/* member i's context (e.g. for requiredSigners, which needs no split) */
+JNIEXPORT jlong JNICALL CLS(groupMember)(JNIEnv* env, jclass cls, jlong g, jint i) {
+    (void)env; (void)cls;
+    return (jlong)(intptr_t)chip_group_member((chip_group*)(intptr_t)g, i);
+}
+
+JNIEXPORT jint JNICALL CLS(groupVerifyBatch)(JNIEnv* env, jclass cls, jlong g, jboolean isValid, jint n,
+                                             jobject keyIdx, jobject msgIdx, jobject sigData, jobject sigOff,
+                                             jobject sigLen, jint nKeys, jobject keyData, jobject keyOff, jobject keyLen,
+                                             jint nMsgs, jobject msgData, jobject msgOff, jobject msgLen,
+                                             jobject status) {
+    (void)cls;
+    return verify_batch(env, 1, g, isValid, n, keyIdx, msgIdx, sigData, sigOff, sigLen, nKeys, keyData, keyOff, keyLen,
+                        nMsgs, msgData, msgOff, msgLen, status);
+}
+
+JNIEXPORT jint JNICALL CLS(groupTxIds)(JNIEnv* env, jclass cls, jlong g, jint ntx, jobject salts, jobject txCompStart,
+                                       jint nComp, jobject compGroup, jobject compInternal, jobject data,
+                                       jobject compOff, jobject compLen, jobject ids) {
+    (void)cls;
+    return tx_ids(env, 1, g, ntx, salts, txCompStart, nComp, compGroup, compInternal, data, compOff, compLen, ids);
+}
+
+JNIEXPORT jint JNICALL CLS(groupVerifySignedTxBatch)(JNIEnv* env, jclass cls, jlong g, jint ntx, jobject salts,
+                                                     jobject txCompStart, jint nComp, jobject compGroup,
+                                                     jobject compInternal, jobject data, jobject compOff, jobject compLen,
+                                                     jint nTmpl, jobject tmplData, jobject tmplOff, jobject tmplLen,
+                                                     jobject tmplIdAt, jint nSig, jobject txIdx, jobject tmplIdx,
+                                                     jobject keyIdx, jobject sigData, jobject sigOff, jobject sigLen,
+                                                     jint nKeys, jobject keyData, jobject keyOff, jobject keyLen,
+                                                     jobject sigStart, jobject reqStart, jint nreq, jobject nodeStart,
+                                                     jobject allowed, jint nNodes, jobject nodeVal, jobject nodeNkids,
+                                                     jobject nodeWeight, jobject ids, jobject status, jobject verdict,
+                                                     jobject arg, jobject missing) {
+    (void)cls;
+    return verify_signed_tx_batch(env, 1, g, ntx, salts, txCompStart, nComp, compGroup, compInternal, data, compOff,
+                                  compLen, nTmpl, tmplData, tmplOff, tmplLen, tmplIdAt, nSig, txIdx, tmplIdx, keyIdx,
+                                  sigData, sigOff, sigLen, nKeys, keyData, keyOff, keyLen, sigStart, reqStart, nreq,
+                                  nodeStart, allowed, nNodes, nodeVal, nodeNkids, nodeWeight, ids, status, verdict, arg,
+                                  missing);
+}
+
+JNIEXPORT jint JNICALL CLS(groupFtxVerify)(JNIEnv* env, jclass cls, jlong g, jint ntx, jobject ids, jobject ghStart,
+                                           jobject groupHashes, jobject fgStart, jobject fgIndex, jobject compStart,
+                                           jobject compData, jobject compOff, jobject compLen, jobject nonces,
+                                           jobject ptStart, jobject ptTag, jobject ptHash, jobject checkVisible,
+                                           jobject visibleMask, jobject status, jobject reason) {
+    (void)cls;
+    return ftx_verify(env, 1, g, ntx, ids, ghStart, groupHashes, fgStart, fgIndex, compStart, compData, compOff,
+                      compLen, nonces, ptStart, ptTag, ptHash, checkVisible, visibleMask, status, reason);
+}
+
+JNIEXPORT jint JNICALL CLS(groupStxVerify)(JNIEnv* env, jclass cls, jlong g, jint n, jobject data, jobject off,
+                                           jobject len, jint nTmpl, jobject tmplData, jobject tmplOff, jobject tmplLen,
+                                           jobject tmplIdAt, jobject meta, jobject status, jobject verdict, jobject arg,
+                                           jobject ids) {
+    (void)cls;
+    return stx_verify(env, 1, g, n, data, off, len, nTmpl, tmplData, tmplOff, tmplLen, tmplIdAt, meta, status,
+                      verdict, arg, ids);
+}
+
+/* the notary table of a group: capacity = states of the whole table */
+JNIEXPORT jlong JNICALL CLS(groupUniqOpen)(JNIEnv* env, jclass cls, jlong g, jlong capacity) {
+    (void)env; (void)cls;
+    chip_group_uniq* u = NULL;
+    return chip_group_uniq_open((chip_group*)(intptr_t)g, (uint64_t)capacity, &u) == CHIP_OK ? (jlong)(intptr_t)u : 0;
+}
+
+JNIEXPORT void JNICALL CLS(groupUniqClose)(JNIEnv* env, jclass cls, jlong u) {
+    (void)env; (void)cls;
+    chip_group_uniq_close((chip_group_uniq*)(intptr_t)u);
+}
+
+JNIEXPORT jlong JNICALL CLS(groupUniqSize)(JNIEnv* env, jclass cls, jlong u) {
+    (void)env; (void)cls;
+    return (jlong)chip_group_uniq_size((const chip_group_uniq*)(intptr_t)u);
+}
+
+JNIEXPORT jstring JNICALL CLS(groupUniqLastError)(JNIEnv* env, jclass cls, jlong u) {
+    (void)cls;
+    return (*env)->NewStringUTF(env, chip_group_uniq_last_error((const chip_group_uniq*)(intptr_t)u));
+}
+
+JNIEXPORT jint JNICALL CLS(groupUniqRebuild)(JNIEnv* env, jclass cls, jlong u, jint n, jobject refs, jobject txIds,
+                                             jobject inputIndex, jobject caller) {
+    (void)cls;
+    if (n < 0) return CHIP_E_ARG;
+    return chip_group_uniq_rebuild((chip_group_uniq*)(intptr_t)u, (uint64_t)n, (const uint8_t*)addr(env, refs),
+                                   (const uint8_t*)addr(env, txIds), (const uint32_t*)addr(env, inputIndex),
+                                   (const uint32_t*)addr(env, caller));
+}
+
+JNIEXPORT jint JNICALL CLS(groupUniqCommitBatch)(JNIEnv* env, jclass cls, jlong u, jint ntx, jobject txRefStart,
+                                                 jobject refs, jobject txIds, jobject callers, jobject status,
+                                                 jobject out, jint cap, jlongArray nOut) {
+    (void)cls;
+    return uniq_commit(env, 1, u, ntx, txRefStart, refs, txIds, callers, status, out, cap, nOut);
 }

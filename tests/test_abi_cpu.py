@@ -33,7 +33,7 @@ def test_library_exports_every_header_function():
 
 def test_abi_version_and_device_count():
     lib = corda_amd.load()
-    assert lib.chip_abi_version() == 8
+    assert lib.chip_abi_version() == 9
     assert lib.chip_device_count() >= 0
 
 
