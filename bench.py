@@ -360,6 +360,7 @@ def main():
     a_ms, b_ms, fin_ms, tab_ms, straus_ms, kp_ms, plan_ms = (
         kms(s, native.K_ED_COMB), kms(s, native.K_ED_COMB_B), kms(s, native.K_ED_FINISH), kms(s, native.K_ED_TABLES),
         kms(s, native.K_ED25519), kms(s, native.K_KEYPREP), kms(s, native.K_ED_PLAN))
+
     ms_per_step = elapsed / args.steps * 1e3
     value = world * n * args.steps / elapsed
     # signatures on the comb path: arithmetic-needing signatures of keys with >= 4 of them (default policy)

@@ -25,12 +25,25 @@ def sources():
     return [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
 
 
+def _obj(src):
+    return os.path.join(PKG, "build", os.path.basename(src) + ".o")
+
+
+def _hdr_mtime():
+    return max([_mtime(os.path.join(CSRC, h)) for h in HEADERS] + [_mtime(os.path.join(ROOT, "include", "cordahip.h"))])
+
+
+def _stale(src, hdr):
+    # an object older than its source or any header (a source edited while a build compiled it stays stale)
+    return _mtime(_obj(src)) <= max(_mtime(src), hdr)
+
+
 def needs_rebuild() -> bool:
     if not os.path.exists(LIB):
         return True
-    deps = sources() + [os.path.join(CSRC, h) for h in HEADERS] + [os.path.join(ROOT, "include", "cordahip.h"), GEN]
+    hdr = _hdr_mtime()
     lm = _mtime(LIB)
-    return any(_mtime(d) > lm for d in deps)
+    return any(_stale(s, hdr) or _mtime(_obj(s)) > lm for s in sources()) or _mtime(GEN) > lm
 
 
 def build(force: bool = False, verbose: bool = False) -> str:
@@ -44,11 +57,11 @@ def build(force: bool = False, verbose: bool = False) -> str:
     objs = []
     procs = []
     os.makedirs(os.path.join(PKG, "build"), exist_ok=True)
-    hdr = max([_mtime(os.path.join(CSRC, h)) for h in HEADERS] + [_mtime(os.path.join(ROOT, "include", "cordahip.h"))])
+    hdr = _hdr_mtime()
     for src in sources():
-        obj = os.path.join(PKG, "build", os.path.basename(src) + ".o")
+        obj = _obj(src)
         objs.append(obj)
-        if not force and _mtime(obj) > max(_mtime(src), hdr):   # object newer than its source and every header
+        if not force and not _stale(src, hdr):   # object newer than its source and every header
             continue
         cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-c", src, "-o", obj,
                "-I", os.path.join(ROOT, "include")]

@@ -986,7 +986,7 @@ int chip_group_uniq_commit_batch(chip_group_uniq* u, uint64_t ntx, const uint64_
     // element-wise MAX of the members' vote bytes, each member reducing a slice of the transactions
     auto reduce = [&](int i) -> int {
         const uint64_t a = ntx * (uint64_t)i / k, b = ntx * (uint64_t)(i + 1) / k;
-        memcpy(dec + a, u->m[0].hvote.p, b - a);
+        memcpy(dec + a, static_cast<const uint8_t*>(u->m[0].hvote.p) + a, b - a);
         for (int j = 1; j < k; j++) {
             const uint8_t* v = static_cast<const uint8_t*>(u->m[j].hvote.p);
             for (uint64_t t = a; t < b; t++) dec[t] = std::max(dec[t], v[t]);

@@ -70,6 +70,8 @@ struct chip_ctx {
     hipStream_t aux2 = nullptr;                   // third stream: ECDSA table fills (while aux doubles on)
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_fork2 = nullptr, ev_join2 = nullptr, ev_kp = nullptr;
     hipEvent_t ev_ec_chain_lo = nullptr, ev_ec_chain_hi = nullptr, ev_ec_lo = nullptr;
+    // the ECDSA key decode at the head of an early Ed25519 batch (CHIP_ECKEYS_LATE=1: after [S]B, the round-4 order)
+    bool eckeys_late = false;
     std::recursive_mutex mu;   // recursive: chip_stx_verify holds it across the entries it calls
     std::string err;
     // verify workspaces
@@ -455,6 +457,7 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
     if (const char* e = getenv("CHIP_COMB_MIN_SIGS")) c->comb_min_sigs = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("CHIP_COMB_MIN_TOTAL")) c->comb_min_total = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("CHIP_COMB_BUDGET_MB")) c->comb_budget = (uint64_t)strtoull(e, nullptr, 10) << 20;
+    if (const char* e = getenv("CHIP_ECKEYS_LATE")) c->eckeys_late = e[0] == '1';
     if (cfg && cfg->reserve_sigs) {
         (void)c->lists.ensure(cfg->reserve_sigs * 4 * N_LISTS);
     }
@@ -684,41 +687,14 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     // and the challenge hash + [S]B start at once on the main stream over the whole batch (slot = signature
     // index); classify waits for the key prep (ev_kp)
     w.early = (comb && w.eager && n && !reuse && !vc && !getenv("CHIP_ED_NO_EARLY")) ? 1u : 0u;
-    if (w.early) {
-        HIPCHK(c, hipEventRecord(c->ev_fork, st));
-        HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
-        const int kk = c->kbegin(CHIP_K_KEYPREP, c->aux);
-        launch_ed25519_key_prep(c->aux, nk, b->key_data, b->key_off, b->key_len, meta, c->abytes.as<uint32_t>(),
-                                nullptr, w.nega, skip);   // eager: no signature takes the Straus kernel
-        c->kend(kk, c->aux);
-        HIPCHK(c, hipEventRecord(c->ev_kp, c->aux));
-        const int kt = c->kbegin(CHIP_K_ED_TABLES, c->aux);
-        launch_ed_comb_build(c->aux, n, nk, meta, w);
-        c->kend(kt, c->aux);
-        HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
-        // (measured: launching [S]B only after classify and the plan, so those small kernels run before the fill
-        // holds the CUs, made the main stream wait for the key prep: 260-264M vs 269-273M)
-        const int kb = c->kbegin(CHIP_K_ED_COMB_B, st);
-        launch_ed_comb_bhalf(st, n, b, c->abytes.as<uint32_t>(), w);
-        c->kend(kb, st);
-    }
-    int ke = c->kbegin(CHIP_K_KEYPREP, st);
-    if (!reuse && !w.early)
-        launch_ed25519_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->abytes.as<uint32_t>(),
-                                (comb && w.eager) ? nullptr : c->edtab.as<uint32_t>(), comb ? w.nega : nullptr, skip);
-    if (comb && w.eager && n && !reuse && !w.early) {
-        // fork: per-key comb tables on the aux stream, concurrent with ECDSA key prep, classify and
-        // every table-free kernel on the main stream (the chain is a serial 252-doubling latency)
-        HIPCHK(c, hipEventRecord(c->ev_fork, st));
-        HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
-        const int kt = c->kbegin(CHIP_K_ED_TABLES, c->aux);
-        launch_ed_comb_build(c->aux, n, nk, meta, w);
-        c->kend(kt, c->aux);
-        HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
-    }
-    if (!reuse) launch_ecdsa_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->ectab.as<uint32_t>(), skip);
-    if (!ec_comb && !reuse) launch_ecdsa_key_table(st, nk, meta, c->ectab.as<uint32_t>(), skip);
-    if (ec_comb && !reuse) {
+    // ECDSA key decode + (windowed) key tables, or the fork of the ECDSA per-key comb tables
+    auto ecdsa_keys = [&]() -> int {
+        if (reuse) return CHIP_OK;
+        launch_ecdsa_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->ectab.as<uint32_t>(), skip);
+        if (!ec_comb) {
+            launch_ecdsa_key_table(st, nk, meta, c->ectab.as<uint32_t>(), skip);
+            return CHIP_OK;
+        }
         // aux: the doubling chain, low windows then high windows; aux2: the fill of each half as soon
         // as its chain half is done (the low fill overlaps the high chain); main waits for the low
         // half (ev_ec_lo) before the low-window additions and for the whole table (ev_join2) after
@@ -740,7 +716,46 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         launch_ecdsa_comb_fill(fs, nk, meta, ctab, 1, skip);
         c->kend(kt, fs);
         HIPCHK(c, hipEventRecord(c->ev_join2, fs));
+        return CHIP_OK;
+    };
+    int rk;
+    if (w.early) {
+        HIPCHK(c, hipEventRecord(c->ev_fork, st));
+        HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+        const int kk = c->kbegin(CHIP_K_KEYPREP, c->aux);
+        launch_ed25519_key_prep(c->aux, nk, b->key_data, b->key_off, b->key_len, meta, c->abytes.as<uint32_t>(),
+                                nullptr, w.nega, skip);   // eager: no signature takes the Straus kernel
+        c->kend(kk, c->aux);
+        HIPCHK(c, hipEventRecord(c->ev_kp, c->aux));
+        const int kt = c->kbegin(CHIP_K_ED_TABLES, c->aux);
+        launch_ed_comb_build(c->aux, n, nk, meta, w);
+        c->kend(kt, c->aux);
+        HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
+        // the ECDSA key decode first on the main stream: with a pool of Ed25519 keys its lanes return at once, but
+        // queued behind the table fill (a higher-priority stream) it waited ~0.2 ms for the CUs, on the main stream's
+        // critical path (profiles/r04/cfg2_step_timeline.txt)
+        if (!c->eckeys_late && (rk = ecdsa_keys())) return rk;
+        // (measured: launching [S]B only after classify and the plan, so those small kernels run before the fill
+        // holds the CUs, made the main stream wait for the key prep: 260-264M vs 269-273M)
+        const int kb = c->kbegin(CHIP_K_ED_COMB_B, st);
+        launch_ed_comb_bhalf(st, n, b, c->abytes.as<uint32_t>(), w);
+        c->kend(kb, st);
     }
+    int ke = c->kbegin(CHIP_K_KEYPREP, st);
+    if (!reuse && !w.early)
+        launch_ed25519_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->abytes.as<uint32_t>(),
+                                (comb && w.eager) ? nullptr : c->edtab.as<uint32_t>(), comb ? w.nega : nullptr, skip);
+    if (comb && w.eager && n && !reuse && !w.early) {
+        // fork: per-key comb tables on the aux stream, concurrent with ECDSA key prep, classify and
+        // every table-free kernel on the main stream (the chain is a serial 252-doubling latency)
+        HIPCHK(c, hipEventRecord(c->ev_fork, st));
+        HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+        const int kt = c->kbegin(CHIP_K_ED_TABLES, c->aux);
+        launch_ed_comb_build(c->aux, n, nk, meta, w);
+        c->kend(kt, c->aux);
+        HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
+    }
+    if ((!w.early || c->eckeys_late) && (rk = ecdsa_keys())) return rk;
     c->kend(ke, st);
     if (vc && vc->keys_only) {
         c->stats.keys_prepared += nk;
