@@ -11,7 +11,7 @@ CSRC = os.path.join(PKG, "csrc")
 LIB = os.path.join(PKG, "libcordahip.so")
 SOURCES = ["runtime.hip", "ed25519.hip", "ed25519_comb.hip", "ecdsa.hip", "txid.hip", "uniq.hip", "signers.hip", "kryo.hip", "group.hip"]
 HEADERS = ["common.hpp", "fe25519_dev.hpp", "scalar_dev.hpp", "sha2_dev.hpp", "runtime.hpp", "curve_consts.hpp",
-           "ec_dev.hpp", "ed_common_dev.hpp", "comb_tables.hpp"]
+           "ec_dev.hpp", "ed_common_dev.hpp", "comb_tables.hpp", "host_threads.hpp"]
 GEN = os.path.join(ROOT, "tools", "gen_constants.py")
 CONSTS = os.path.join(CSRC, "curve_consts.hpp")
 COMB = os.path.join(CSRC, "comb_tables.hpp")   # generated, git-ignored (3 MB of fixed-base tables)

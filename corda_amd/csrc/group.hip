@@ -32,79 +32,12 @@
 #include <string>
 #include <thread>
 #include <vector>
+#include "host_threads.hpp"
 #include "runtime.hpp"
 
-// ---------------------------------------------------------------------------------------------------------
 // member threads: f(i) for every member i, member 0 on the caller's thread, the others on one persistent host
-// thread each (hipSetDevice is per thread; every context entry sets its own device)
-class MemberThreads {
-  public:
-    explicit MemberThreads(int n) : slots_(n) {
-        for (int i = 1; i < n; i++) {
-            slots_[i].reset(new Slot());
-            Slot* s = slots_[i].get();
-            s->th = std::thread([s, i] {
-                std::unique_lock<std::mutex> l(s->m);
-                for (;;) {
-                    s->cv.wait(l, [s] { return s->busy || s->quit; });
-                    if (s->quit) return;
-                    const std::function<int(int)>* f = s->f;
-                    l.unlock();
-                    const int rc = (*f)(i);
-                    l.lock();
-                    s->rc = rc;
-                    s->busy = false;
-                    s->cv.notify_all();
-                }
-            });
-        }
-    }
-    ~MemberThreads() {
-        for (size_t i = 1; i < slots_.size(); i++) {
-            Slot* s = slots_[i].get();
-            {
-                std::lock_guard<std::mutex> l(s->m);
-                s->quit = true;
-            }
-            s->cv.notify_all();
-            s->th.join();
-        }
-    }
-    // runs f on the members whose bit is set in `active` (all: ~0); returns the first non-zero result in member order
-    int run(const std::function<int(int)>& f, uint64_t active = ~0ull) {
-        const int n = (int)slots_.size();
-        for (int i = 1; i < n; i++) {
-            if (!(active >> (i & 63) & 1)) continue;
-            Slot* s = slots_[i].get();
-            std::lock_guard<std::mutex> l(s->m);
-            s->f = &f;
-            s->rc = 0;
-            s->busy = true;
-            s->cv.notify_all();
-        }
-        int rc0 = (active & 1) ? f(0) : 0;
-        int first = rc0;
-        for (int i = 1; i < n; i++) {
-            if (!(active >> (i & 63) & 1)) continue;
-            Slot* s = slots_[i].get();
-            std::unique_lock<std::mutex> l(s->m);
-            s->cv.wait(l, [s] { return !s->busy; });
-            if (!first && s->rc) first = s->rc;
-        }
-        return first;
-    }
-
-  private:
-    struct Slot {
-        std::thread th;
-        std::mutex m;
-        std::condition_variable cv;
-        const std::function<int(int)>* f = nullptr;
-        int rc = 0;
-        bool busy = false, quit = false;
-    };
-    std::vector<std::unique_ptr<Slot>> slots_;
-};
+// thread each (hipSetDevice is per thread; every context entry sets its own device) — host_threads.hpp
+using MemberThreads = ForkJoin;
 
 // grow-only page-locked host scratch
 struct PinnedBuf {
@@ -774,6 +707,8 @@ struct chip_group_uniq {
     std::mutex mu;
 };
 
+extern "C" int chip_ctx_h2d(chip_ctx* c, void* dst, const void* src, uint64_t bytes, void* stream);
+
 static int ufail(chip_group_uniq* u, int code, const std::string& msg) {
     if (u) u->err = msg;
     return code;
@@ -930,10 +865,11 @@ int chip_group_uniq_commit_batch(chip_group_uniq* u, uint64_t ntx, const uint64_
         GUCHK(mm.dec.ensure(ntx + 16));
         GUCHK(mm.status.ensure(ntx + 16));
         if (!mm.hvote.ensure(ntx + 64)) GUCHK(hipErrorOutOfMemory);
-        GUCHK(hipMemcpyAsync(mm.start.p, start, (ntx + 1) * 8, hipMemcpyHostToDevice, st));
-        if (nref) GUCHK(hipMemcpyAsync(mm.refs.p, refs36, nref * 36, hipMemcpyHostToDevice, st));
-        GUCHK(hipMemcpyAsync(mm.ids.p, tx_ids, ntx * 32, hipMemcpyHostToDevice, st));
-        GUCHK(hipMemcpyAsync(mm.callers.p, callers, ntx * 4, hipMemcpyHostToDevice, st));
+        // the caller's arrays through the member context's staging ring when they are pageable
+        if (chip_ctx_h2d(g->m[i], mm.start.p, start, (ntx + 1) * 8, st) ||
+            (nref && chip_ctx_h2d(g->m[i], mm.refs.p, refs36, nref * 36, st)) ||
+            chip_ctx_h2d(g->m[i], mm.ids.p, tx_ids, ntx * 32, st) || chip_ctx_h2d(g->m[i], mm.callers.p, callers, ntx * 4, st))
+            GUCHK(hipErrorUnknown);
         {   // tx_ref_start from 0, nondecreasing, ending at nref (checked where it was staged)
             const DevCheck chk[] = {{DEV_CHECK_MONOTONE, 1, mm.start.p, nullptr, nullptr, ntx, nref, 0}};
             uint32_t bad = 0;

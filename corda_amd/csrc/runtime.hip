@@ -13,7 +13,97 @@
 #include <cstdio>
 #include <cstdlib>
 #include <algorithm>
+#include "host_threads.hpp"
 #include "runtime.hpp"
+
+// Pageable host input through the context's own pinned ring: a copy from memory HIP did not allocate or register
+// (a numpy array, a JVM heap array) is split into 4 MB pieces, each memcpy'd into a free slot of a page-locked ring
+// by a pool of host threads and DMA'd from there on the copy's stream, the next piece's memcpy beside the previous
+// piece's DMA.  HIP's own pageable path (an internal bounce, one thread) measured 155-164M cfg2 sigs/s on most boxes
+// and 57.7M on the round-4 driver's (BENCH_r04 cfg2_host_path_sigs_per_s); page-locked input always takes the direct
+// DMA.  CHIP_STAGING_RING=0 sends pageable input through HIP's path again.
+struct HostRing {
+    static constexpr int SLOTS = 8;
+    static constexpr uint64_t SLOT = 4u << 20;
+    uint8_t* buf = nullptr;
+    hipEvent_t ev[SLOTS] = {};
+    bool pending[SLOTS] = {};
+    int next = 0;
+    std::unique_ptr<ForkJoin> pool;
+    bool enabled = true, failed = false;
+    uint64_t bytes_staged = 0;
+    bool init() {
+        if (buf || failed) return buf != nullptr;
+        if (hipHostMalloc((void**)&buf, (size_t)SLOTS * SLOT, hipHostMallocDefault) != hipSuccess) {
+            buf = nullptr;
+            failed = true;
+            return false;
+        }
+        for (int i = 0; i < SLOTS; i++)
+            if (hipEventCreateWithFlags(&ev[i], hipEventDisableTiming) != hipSuccess) {
+                failed = true;
+                return false;
+            }
+        unsigned hw = std::thread::hardware_concurrency();
+        int t = (int)std::min<unsigned>(8u, hw ? hw : 4u);
+        if (const char* e = getenv("CHIP_COPY_THREADS")) t = std::max(1, std::min(32, atoi(e)));
+        pool.reset(new ForkJoin(t));
+        return true;
+    }
+    void release() {
+        pool.reset();
+        for (int i = 0; i < SLOTS; i++) {
+            if (pending[i]) (void)hipEventSynchronize(ev[i]);
+            if (ev[i]) (void)hipEventDestroy(ev[i]);
+            ev[i] = nullptr;
+            pending[i] = false;
+        }
+        if (buf) (void)hipHostFree(buf);
+        buf = nullptr;
+    }
+};
+
+static bool host_pinned(const void* p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();   // an unknown host pointer is an error code here, not a failure of the call
+        return false;
+    }
+    return a.type == hipMemoryTypeHost || a.type == hipMemoryTypeDevice || a.type == hipMemoryTypeManaged;
+}
+
+// H2D of `bytes` from host memory: page-locked (or small) input by one async DMA, pageable input through the ring
+static hipError_t ring_h2d(HostRing& R, void* dst, const void* src, uint64_t bytes, hipStream_t st) {
+    if (!bytes) return hipSuccess;
+    if (!R.enabled || bytes < (1u << 20) || host_pinned(src) || !R.init())
+        return hipMemcpyAsync(dst, src, bytes, hipMemcpyHostToDevice, st);
+    const uint8_t* s = static_cast<const uint8_t*>(src);
+    uint8_t* d = static_cast<uint8_t*>(dst);
+    const int nt = R.pool->size();
+    for (uint64_t off = 0; off < bytes; off += HostRing::SLOT) {
+        const uint64_t piece = std::min<uint64_t>(HostRing::SLOT, bytes - off);
+        const int k = R.next;
+        R.next = (R.next + 1) % HostRing::SLOTS;
+        if (R.pending[k]) {
+            const hipError_t e = hipEventSynchronize(R.ev[k]);   // the slot's previous DMA is done
+            if (e != hipSuccess) return e;
+            R.pending[k] = false;
+        }
+        uint8_t* slot = R.buf + (size_t)k * HostRing::SLOT;
+        const uint64_t part = ((piece + nt - 1) / nt + 63) & ~63ull;
+        R.pool->run([&](int i) {
+            const uint64_t a = std::min<uint64_t>(piece, (uint64_t)i * part), b = std::min<uint64_t>(piece, a + part);
+            if (b > a) memcpy(slot + a, s + off + a, b - a);
+            return 0;
+        });
+        hipError_t e = hipMemcpyAsync(d + off, slot, piece, hipMemcpyHostToDevice, st);
+        if (e == hipSuccess) e = hipEventRecord(R.ev[k], st);
+        if (e != hipSuccess) return e;
+        R.pending[k] = true;
+    }
+    R.bytes_staged += bytes;
+    return hipSuccess;
+}
 
 struct DevBuf {
     void* p = nullptr;
@@ -117,6 +207,7 @@ struct chip_ctx {
     unsigned long long* h_rng = nullptr;
     DevBuf h_rngd;
     chip_stats stats{};
+    HostRing ring;   // pinned staging of pageable host input
     // per-kernel timing: a ring of event pairs recorded on the launch stream
     struct KEv {
         hipEvent_t a = nullptr, b = nullptr;
@@ -314,7 +405,7 @@ template <class T>
 static int stage(chip_ctx* c, DevBuf& d, const T* src, uint64_t count, hipStream_t st) {
     const size_t bytes = count * sizeof(T);
     HIPCHK(c, d.ensure(bytes + 16));
-    if (bytes) HIPCHK(c, hipMemcpyAsync(d.p, src, bytes, hipMemcpyHostToDevice, st));
+    if (bytes) HIPCHK(c, ring_h2d(c->ring, d.p, src, bytes, st));
     return CHIP_OK;
 }
 
@@ -384,6 +475,11 @@ int chip_abi_version(void) { return CHIP_ABI_VERSION; }
 
 // internal (not in cordahip.h): the device ordinal of a context, used by uniq.hip
 int chip_ctx_device(const chip_ctx* c) { return c ? c->device : 0; }
+// internal: H2D through the context's staging ring (pageable input) or one DMA (page-locked input); uniq.hip
+int chip_ctx_h2d(chip_ctx* c, void* dst, const void* src, uint64_t bytes, void* stream) {
+    std::lock_guard<std::recursive_mutex> g(c->mu);
+    return ring_h2d(c->ring, dst, src, bytes, (hipStream_t)stream) == hipSuccess ? CHIP_OK : CHIP_E_DEVICE;
+}
 
 int chip_device_count(void) {
     int n = 0;
@@ -458,6 +554,7 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
     if (const char* e = getenv("CHIP_COMB_MIN_TOTAL")) c->comb_min_total = (uint32_t)strtoul(e, nullptr, 10);
     if (const char* e = getenv("CHIP_COMB_BUDGET_MB")) c->comb_budget = (uint64_t)strtoull(e, nullptr, 10) << 20;
     if (const char* e = getenv("CHIP_ECKEYS_LATE")) c->eckeys_late = e[0] == '1';
+    if (const char* e = getenv("CHIP_STAGING_RING")) c->ring.enabled = e[0] != '0';
     if (cfg && cfg->reserve_sigs) {
         (void)c->lists.ensure(cfg->reserve_sigs * 4 * N_LISTS);
     }
@@ -483,6 +580,7 @@ void chip_shutdown(chip_ctx* c) {
                       &c->h2_a, &c->h2_sigst, &c->h2_miss, &c->h2_td, &c->h2_to, &c->h2_tl, &c->h2_ta};
     for (DevBuf* b : bufs) b->release();
     for (StxBufs& b : c->stx) b.release();
+    c->ring.release();
     for (int i = 0; i < chip_ctx::KRING; i++) {
         if (c->kring[i].a) hipEventDestroy(c->kring[i].a);
         if (c->kring[i].b) hipEventDestroy(c->kring[i].b);
@@ -1068,16 +1166,16 @@ static int verify_host_pipelined(chip_ctx* c, const chip_sig_batch* b, uint8_t* 
     auto grow = [&](DevBuf& d, const uint8_t* src, uint64_t lo, uint64_t hi, uint64_t& clo, uint64_t& chi, bool& any) -> int {
         if (lo >= hi) return CHIP_OK;
         if (!any) {
-            HIPCHK(c, hipMemcpyAsync(d.as<uint8_t>() + lo, src + lo, hi - lo, hipMemcpyHostToDevice, cs));
+            HIPCHK(c, ring_h2d(c->ring, d.as<uint8_t>() + lo, src + lo, hi - lo, cs));
             clo = lo, chi = hi, any = true;
             return CHIP_OK;
         }
         if (lo < clo) {
-            HIPCHK(c, hipMemcpyAsync(d.as<uint8_t>() + lo, src + lo, clo - lo, hipMemcpyHostToDevice, cs));
+            HIPCHK(c, ring_h2d(c->ring, d.as<uint8_t>() + lo, src + lo, clo - lo, cs));
             clo = lo;
         }
         if (hi > chi) {
-            HIPCHK(c, hipMemcpyAsync(d.as<uint8_t>() + chi, src + chi, hi - chi, hipMemcpyHostToDevice, cs));
+            HIPCHK(c, ring_h2d(c->ring, d.as<uint8_t>() + chi, src + chi, hi - chi, cs));
             chi = hi;
         }
         return CHIP_OK;
@@ -1085,10 +1183,10 @@ static int verify_host_pipelined(chip_ctx* c, const chip_sig_batch* b, uint8_t* 
     // stage chunk j: index slices, check, ranges -> host, then the pool parts; hev_p = chunk j's bytes are on the device
     auto stage_chunk = [&](uint64_t j) -> int {
         const uint64_t a = at[j], e = at[j + 1], m = e - a;
-        HIPCHK(c, hipMemcpyAsync(c->h_key_idx.as<uint32_t>() + a, b->key_idx + a, m * 4, hipMemcpyHostToDevice, cs));
-        HIPCHK(c, hipMemcpyAsync(c->h_msg_idx.as<uint32_t>() + a, b->msg_idx + a, m * 4, hipMemcpyHostToDevice, cs));
-        HIPCHK(c, hipMemcpyAsync(c->h_sig_off.as<uint64_t>() + a, b->sig_off + a, m * 8, hipMemcpyHostToDevice, cs));
-        HIPCHK(c, hipMemcpyAsync(c->h_sig_len.as<uint32_t>() + a, b->sig_len + a, m * 4, hipMemcpyHostToDevice, cs));
+        HIPCHK(c, ring_h2d(c->ring, c->h_key_idx.as<uint32_t>() + a, b->key_idx + a, m * 4, cs));
+        HIPCHK(c, ring_h2d(c->ring, c->h_msg_idx.as<uint32_t>() + a, b->msg_idx + a, m * 4, cs));
+        HIPCHK(c, ring_h2d(c->ring, c->h_sig_off.as<uint64_t>() + a, b->sig_off + a, m * 8, cs));
+        HIPCHK(c, ring_h2d(c->ring, c->h_sig_len.as<uint32_t>() + a, b->sig_len + a, m * 4, cs));
         unsigned long long* out = c->h_rngd.as<unsigned long long>();
         hipLaunchKernelGGL(k_chunk_init, dim3(1), dim3(64), 0, cs, out);
         const uint64_t g = j == 0 ? std::max(m, std::max(nk, nm)) : m;
@@ -1371,7 +1469,7 @@ static int stx_parse(chip_ctx* c, StxBufs& B, const chip_stx_blobs* in, uint8_t*
     if (stx_scan_temp_bytes(nsig > 2 ? nsig : 2) > B.s_temp.cap)
         HIPCHK(c, B.s_temp.ensure(stx_scan_temp_bytes(nsig > 2 ? nsig : 2)));
     if (in->n_meta)
-        HIPCHK(c, hipMemcpyAsync(B.s_meta.p, in->meta, (uint64_t)in->n_meta * 8, hipMemcpyHostToDevice, st));
+        HIPCHK(c, ring_h2d(c->ring, B.s_meta.p, in->meta, (uint64_t)in->n_meta * 8, st));
     StxOut d{};
     d.pool = pool_p;
     d.pool_bytes = pool;
@@ -1642,16 +1740,16 @@ static int stx_verify_host_pipelined(chip_ctx* c, uint64_t n, const uint8_t* dat
     auto copy = [&](uint64_t lo, uint64_t hi) -> int {
         if (lo >= hi) return CHIP_OK;
         if (!any) {
-            HIPCHK(c, hipMemcpyAsync(c->h2_data.as<uint8_t>() + lo, data + lo, hi - lo, hipMemcpyHostToDevice, cs));
+            HIPCHK(c, ring_h2d(c->ring, c->h2_data.as<uint8_t>() + lo, data + lo, hi - lo, cs));
             clo = lo, chi = hi, any = true;
             return CHIP_OK;
         }
         if (lo < clo) {
-            HIPCHK(c, hipMemcpyAsync(c->h2_data.as<uint8_t>() + lo, data + lo, clo - lo, hipMemcpyHostToDevice, cs));
+            HIPCHK(c, ring_h2d(c->ring, c->h2_data.as<uint8_t>() + lo, data + lo, clo - lo, cs));
             clo = lo;
         }
         if (hi > chi) {
-            HIPCHK(c, hipMemcpyAsync(c->h2_data.as<uint8_t>() + chi, data + chi, hi - chi, hipMemcpyHostToDevice, cs));
+            HIPCHK(c, ring_h2d(c->ring, c->h2_data.as<uint8_t>() + chi, data + chi, hi - chi, cs));
             chi = hi;
         }
         return CHIP_OK;
@@ -1660,8 +1758,8 @@ static int stx_verify_host_pipelined(chip_ctx* c, uint64_t n, const uint8_t* dat
     // hev_p = the chunk is on the device
     auto stage_chunk = [&](uint64_t j) -> int {
         const uint64_t a = at[j], m = at[j + 1] - a;
-        HIPCHK(c, hipMemcpyAsync(c->h2_off.as<uint64_t>() + a, off + a, m * 8, hipMemcpyHostToDevice, cs));
-        HIPCHK(c, hipMemcpyAsync(c->h2_len.as<uint32_t>() + a, len + a, m * 4, hipMemcpyHostToDevice, cs));
+        HIPCHK(c, ring_h2d(c->ring, c->h2_off.as<uint64_t>() + a, off + a, m * 8, cs));
+        HIPCHK(c, ring_h2d(c->ring, c->h2_len.as<uint32_t>() + a, len + a, m * 4, cs));
         unsigned long long* out = c->h_rngd.as<unsigned long long>();
         hipLaunchKernelGGL(k_chunk_init, dim3(1), dim3(64), 0, cs, out);
         hipLaunchKernelGGL(k_blob_range, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, cs, m,
@@ -1894,16 +1992,16 @@ static int txid_host_pipelined(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids
         if (lo >= hi) return CHIP_OK;
         uint8_t* dst = c->t_data.as<uint8_t>();
         if (!any) {
-            HIPCHK(c, hipMemcpyAsync(dst + lo, b->data + lo, hi - lo, hipMemcpyHostToDevice, cs));
+            HIPCHK(c, ring_h2d(c->ring, dst + lo, b->data + lo, hi - lo, cs));
             clo = lo, chi = hi, any = true;
             return CHIP_OK;
         }
         if (lo < clo) {
-            HIPCHK(c, hipMemcpyAsync(dst + lo, b->data + lo, clo - lo, hipMemcpyHostToDevice, cs));
+            HIPCHK(c, ring_h2d(c->ring, dst + lo, b->data + lo, clo - lo, cs));
             clo = lo;
         }
         if (hi > chi) {
-            HIPCHK(c, hipMemcpyAsync(dst + chi, b->data + chi, hi - chi, hipMemcpyHostToDevice, cs));
+            HIPCHK(c, ring_h2d(c->ring, dst + chi, b->data + chi, hi - chi, cs));
             chi = hi;
         }
         return CHIP_OK;
@@ -1915,14 +2013,14 @@ static int txid_host_pipelined(chip_ctx* c, const chip_tx_batch* b, uint8_t* ids
         const uint64_t c0 = b->tx_comp_start[a], c1 = b->tx_comp_start[e];
         if (c0 > c1 || c1 > nc || (j == 0 && c0 != 0))
             return fail(c, CHIP_E_ARG, "tx_comp_start not monotone / out of range");
-        HIPCHK(c, hipMemcpyAsync(c->t_salts.as<uint8_t>() + 32 * a, b->salts + 32 * a, m * 32, hipMemcpyHostToDevice, cs));
-        HIPCHK(c, hipMemcpyAsync(c->t_start.as<uint64_t>() + a, b->tx_comp_start + a, (m + 1) * 8, hipMemcpyHostToDevice, cs));
+        HIPCHK(c, ring_h2d(c->ring, c->t_salts.as<uint8_t>() + 32 * a, b->salts + 32 * a, m * 32, cs));
+        HIPCHK(c, ring_h2d(c->ring, c->t_start.as<uint64_t>() + a, b->tx_comp_start + a, (m + 1) * 8, cs));
         const uint64_t k = c1 - c0;
         if (k) {
-            HIPCHK(c, hipMemcpyAsync(c->t_group.as<uint32_t>() + c0, b->comp_group + c0, k * 4, hipMemcpyHostToDevice, cs));
-            HIPCHK(c, hipMemcpyAsync(c->t_internal.as<uint32_t>() + c0, b->comp_internal + c0, k * 4, hipMemcpyHostToDevice, cs));
-            HIPCHK(c, hipMemcpyAsync(c->t_off.as<uint64_t>() + c0, b->comp_off + c0, k * 8, hipMemcpyHostToDevice, cs));
-            HIPCHK(c, hipMemcpyAsync(c->t_len.as<uint32_t>() + c0, b->comp_len + c0, k * 4, hipMemcpyHostToDevice, cs));
+            HIPCHK(c, ring_h2d(c->ring, c->t_group.as<uint32_t>() + c0, b->comp_group + c0, k * 4, cs));
+            HIPCHK(c, ring_h2d(c->ring, c->t_internal.as<uint32_t>() + c0, b->comp_internal + c0, k * 4, cs));
+            HIPCHK(c, ring_h2d(c->ring, c->t_off.as<uint64_t>() + c0, b->comp_off + c0, k * 8, cs));
+            HIPCHK(c, ring_h2d(c->ring, c->t_len.as<uint32_t>() + c0, b->comp_len + c0, k * 4, cs));
         }
         const DevCheck chk[] = {{DEV_CHECK_MONOTONE, 1, c->t_start.as<uint64_t>() + a, nullptr, nullptr, m, c1, c0}};
         uint32_t bad = 0;

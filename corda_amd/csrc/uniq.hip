@@ -737,6 +737,13 @@ static int ensure_rows(chip_uniq* u, uint64_t extra, hipStream_t st) {
 
 struct chip_ctx;
 extern "C" int chip_ctx_device(const chip_ctx* c);
+extern "C" int chip_ctx_h2d(chip_ctx* c, void* dst, const void* src, uint64_t bytes, void* stream);
+// host input of the host entries: through the context's pinned staging ring when it is pageable
+#define UH2D(u, dst, src, bytes, st)                                                                     \
+    do {                                                                                               \
+        if (chip_ctx_h2d((u)->ctx, (dst), (src), (bytes), (st)) != CHIP_OK)                            \
+            return ufail(u, CHIP_E_DEVICE, "host-to-device copy");                                     \
+    } while (0)
 
 // batch scratch for nref local inputs and ntx transactions
 static int batch_scratch(chip_uniq* u, uint64_t ntx, uint64_t nref) {
@@ -836,10 +843,10 @@ int chip_uniq_rebuild(chip_uniq* u, uint64_t n, const uint8_t* refs36, const uin
     UCHK(u, u->h_ids.ensure(n * 32 + 16));
     UCHK(u, u->h_call.ensure(n * 4 + 16));
     UCHK(u, u->refpos.ensure(n * 4 + 16));
-    UCHK(u, hipMemcpyAsync(u->h_refs.p, refs36, n * 36, hipMemcpyHostToDevice, st));
-    UCHK(u, hipMemcpyAsync(u->h_ids.p, tx32, n * 32, hipMemcpyHostToDevice, st));
-    UCHK(u, hipMemcpyAsync(u->refpos.p, idx, n * 4, hipMemcpyHostToDevice, st));
-    UCHK(u, hipMemcpyAsync(u->h_call.p, caller, n * 4, hipMemcpyHostToDevice, st));
+    UH2D(u, u->h_refs.p, refs36, n * 36, st);
+    UH2D(u, u->h_ids.p, tx32, n * 32, st);
+    UH2D(u, u->refpos.p, idx, n * 4, st);
+    UH2D(u, u->h_call.p, caller, n * 4, st);
     if ((r = spread_zero(u, st))) return r;
     const uint8_t* d_refs = u->h_refs.as<uint8_t>();
     if ((r = launch_lookup(u, n, d_refs, st))) return r;
@@ -1107,10 +1114,10 @@ int chip_uniq_commit_batch(chip_uniq* u, uint64_t ntx, const uint64_t* start, co
     UCHK(u, u->h_call.ensure(ntx * 4));
     UCHK(u, u->h_st.ensure(ntx + 16));
     UCHK(u, u->h_out.ensure((nref + 1) * sizeof(chip_conflict)));
-    if (nref) UCHK(u, hipMemcpyAsync(u->h_refs.p, refs36, nref * 36, hipMemcpyHostToDevice, st));
-    UCHK(u, hipMemcpyAsync(u->h_start.p, start, (ntx + 1) * 8, hipMemcpyHostToDevice, st));
-    UCHK(u, hipMemcpyAsync(u->h_ids.p, tx_ids, ntx * 32, hipMemcpyHostToDevice, st));
-    UCHK(u, hipMemcpyAsync(u->h_call.p, callers, ntx * 4, hipMemcpyHostToDevice, st));
+    if (nref) UH2D(u, u->h_refs.p, refs36, nref * 36, st);
+    UH2D(u, u->h_start.p, start, (ntx + 1) * 8, st);
+    UH2D(u, u->h_ids.p, tx_ids, ntx * 32, st);
+    UH2D(u, u->h_call.p, callers, ntx * 4, st);
     {   // tx_ref_start from 0, nondecreasing, ending at nref: checked on the device where it was staged
         const DevCheck chk[] = {{DEV_CHECK_MONOTONE, 1, u->h_start.p, nullptr, nullptr, ntx, nref, 0}};
         uint32_t bad = 0;
