@@ -605,6 +605,131 @@ CHIP_DEV void ec_comb_chain(const uint32_t* __restrict__ ectab, uint32_t* __rest
         store_jpt(tab + w * EC_COMB_QENT * EC_COMB_JW, P);
     }
 }
+// The same chain on a lane pair per key (adjacent lanes of a wave; both hold the point): each doubling's field
+// operations are split between the two lanes — P-256's 3M + 5S as four steps of one operation per lane, secp256k1's
+// 2M + 5S likewise — and the halves exchanged by DPP quad permutes (one v_mov_dpp per word), so the serial chain
+// per key, the critical path of the ECDSA table build, carries about half the dependent operations per doubling.
+CHIP_DEV uint32_t ec_pair_swap(uint32_t v) {   // the partner lane's v (lanes 2i <-> 2i+1)
+    return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0xB1, 0xF, 0xF, false);   // quad_perm [1,0,3,2]
+}
+CHIP_DEV void u256_swap_in(u256& out, const u256& mine) {
+#pragma unroll
+    for (int i = 0; i < 8; i++) out.w[i] = ec_pair_swap(mine.w[i]);
+}
+CHIP_DEV void u256_sel(u256& r, uint32_t m, const u256& a, const u256& b) {   // m all-ones: a, else b
+#pragma unroll
+    for (int i = 0; i < 8; i++) r.w[i] = (a.w[i] & m) | (b.w[i] & ~m);
+}
+// r = 2p on a lane pair (odd: all-ones on the odd lane); p, r the same on both lanes
+template <int C>
+CHIP_DEV void jdbl_pair(jpt& r, const jpt& p, uint32_t odd) {
+    u256 mine, other, a, b;
+    if (EC_CURVE(C) == CURVE_R1) {
+        // dbl-2001-b.  1: delta = Z^2 (even), gamma = Y^2 (odd)
+        u256 delta, gamma, alpha, beta, a2, g2, yz2, y3m, t1, t2;
+        u256_sel(a, odd, p.Y, p.Z);
+        fp_sqr<C>(mine, a);
+        u256_swap_in(other, mine);
+        u256_sel(delta, odd, other, mine);
+        u256_sel(gamma, odd, mine, other);
+        // 2: (X - delta)(X + delta) (even), beta = X gamma (odd)
+        fp_sub<C>(t1, p.X, delta);
+        fp_add<C>(t2, p.X, delta);
+        u256_sel(a, odd, p.X, t1);
+        u256_sel(b, odd, gamma, t2);
+        fp_mul<C>(mine, a, b);
+        u256_swap_in(other, mine);
+        u256_sel(alpha, odd, other, mine);
+        u256_sel(beta, odd, mine, other);
+        fp_add<C>(t1, alpha, alpha);
+        fp_add<C>(alpha, alpha, t1);            // 3 (X - delta)(X + delta)
+        // 3: alpha^2 (even), gamma^2 (odd)
+        u256_sel(a, odd, gamma, alpha);
+        fp_sqr<C>(mine, a);
+        u256_swap_in(other, mine);
+        u256_sel(a2, odd, other, mine);
+        u256_sel(g2, odd, mine, other);
+        fp_add<C>(t1, beta, beta);
+        fp_add<C>(t1, t1, t1);                  // 4 beta
+        fp_sub<C>(t2, a2, t1);
+        fp_sub<C>(r.X, t2, t1);                 // X3 = alpha^2 - 8 beta
+        // 4: (Y + Z)^2 (even), alpha (4 beta - X3) (odd)
+        fp_sub<C>(t1, t1, r.X);
+        fp_add<C>(t2, p.Y, p.Z);
+        u256_sel(a, odd, alpha, t2);
+        u256_sel(b, odd, t1, t2);
+        fp_mul<C>(mine, a, b);
+        u256_swap_in(other, mine);
+        u256_sel(yz2, odd, other, mine);
+        u256_sel(y3m, odd, mine, other);
+        fp_sub<C>(t1, yz2, gamma);
+        fp_sub<C>(r.Z, t1, delta);              // Z3 = (Y+Z)^2 - gamma - delta
+        fp_add<C>(g2, g2, g2);
+        fp_add<C>(g2, g2, g2);
+        fp_add<C>(g2, g2, g2);                  // 8 gamma^2
+        fp_sub<C>(r.Y, y3m, g2);
+    } else {
+        // dbl-2009-l.  1: A = X^2 (even), B = Y^2 (odd)
+        u256 A, B, Cc, D, E, F, T, yz, y3m, t;
+        u256_sel(a, odd, p.Y, p.X);
+        fp_sqr<C>(mine, a);
+        u256_swap_in(other, mine);
+        u256_sel(A, odd, other, mine);
+        u256_sel(B, odd, mine, other);
+        fp_add<C>(E, A, A);
+        fp_add<C>(E, E, A);                     // E = 3A
+        // 2: F = E^2 (even), C = B^2 (odd)
+        u256_sel(a, odd, B, E);
+        fp_sqr<C>(mine, a);
+        u256_swap_in(other, mine);
+        u256_sel(F, odd, other, mine);
+        u256_sel(Cc, odd, mine, other);
+        // 3: (X + B)^2 (even), Y Z (odd)
+        fp_add<C>(t, p.X, B);
+        u256_sel(a, odd, p.Y, t);
+        u256_sel(b, odd, p.Z, t);
+        fp_mul<C>(mine, a, b);
+        u256_swap_in(other, mine);
+        u256_sel(T, odd, other, mine);
+        u256_sel(yz, odd, mine, other);
+        fp_sub<C>(t, T, A);
+        fp_sub<C>(t, t, Cc);
+        fp_add<C>(D, t, t);
+        fp_add<C>(r.Z, yz, yz);
+        fp_add<C>(t, D, D);
+        fp_sub<C>(r.X, F, t);
+        // 4: E (D - X3) (both lanes compute it: one operation, no exchange)
+        fp_sub<C>(t, D, r.X);
+        fp_mul<C>(y3m, E, t);
+        fp_add<C>(Cc, Cc, Cc);
+        fp_add<C>(Cc, Cc, Cc);
+        fp_add<C>(Cc, Cc, Cc);
+        fp_sub<C>(r.Y, y3m, Cc);
+    }
+}
+template <int C>
+CHIP_DEV void ec_comb_chain2(const uint32_t* __restrict__ ectab, uint32_t* __restrict__ jac, uint64_t k, uint32_t wa,
+                             uint32_t wb, uint32_t odd) {
+    uint32_t* tab = jac + k * EC_COMB_JAC_WORDS;
+    jpt P;
+    uint32_t w = wa;
+    if (wa == 0) {
+        apt q;
+        load_apt(q, ectab + k * EC_TAB_STRIDE + 16);
+        jpt_from_aff(P, q);
+        if (!odd) store_jpt(tab, P);
+        w = 1;
+    } else {
+        load_jpt(P, tab + (wa - 1) * EC_COMB_QENT * EC_COMB_JW);
+    }
+#pragma unroll 1
+    for (; w < wb; w++) {
+#pragma unroll 1
+        for (int b = 0; b < 4; b++) jdbl_pair<C>(P, P, odd);
+        if (!odd) store_jpt(tab + w * EC_COMB_QENT * EC_COMB_JW, P);
+    }
+}
+
 // fill, for windows [w0, w1) of one key:
 //   1. P_w to affine with one inversion for the group (Montgomery's trick; prefix products parked in
 //      the x slots of the output entries)
@@ -688,6 +813,22 @@ __global__ void __launch_bounds__(64) k_ecdsa_comb_chain(uint64_t n_keys, const 
     if (prio) __builtin_amdgcn_s_setprio(3);
     if (ec_key_ok(meta, k, CHIP_SCHEME_R1)) ec_comb_chain<CURVE_R1 | CURVE_ILP>(ectab, jac, k, wa, wb);
     else if (ec_key_ok(meta, k, CHIP_SCHEME_K1)) ec_comb_chain<CURVE_K1 | CURVE_ILP>(ectab, jac, k, wa, wb);
+}
+#ifndef EC_CHAIN_PAIR
+#define EC_CHAIN_PAIR 1   // the chain on lane pairs (k_ecdsa_comb_chain2); CHIP_EC_CHAIN_PAIR=0: one lane per key
+#endif
+// two lanes per key (both lanes of a pair take the same exits: the same key)
+__global__ void __launch_bounds__(64) k_ecdsa_comb_chain2(uint64_t n_keys, const KeyMeta* __restrict__ meta,
+                                                          const uint32_t* __restrict__ ectab, uint32_t* __restrict__ jac,
+                                                          uint32_t prio, uint32_t wa, uint32_t wb,
+                                                          const uint32_t* __restrict__ skip) {
+    const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const uint64_t k = g >> 1;
+    const uint32_t odd = (g & 1u) ? ~0u : 0u;
+    if (k >= n_keys || (skip && *skip)) return;
+    if (prio) __builtin_amdgcn_s_setprio(3);
+    if (ec_key_ok(meta, k, CHIP_SCHEME_R1)) ec_comb_chain2<CURVE_R1 | CURVE_ILP>(ectab, jac, k, wa, wb, odd);
+    else if (ec_key_ok(meta, k, CHIP_SCHEME_K1)) ec_comb_chain2<CURVE_K1 | CURVE_ILP>(ectab, jac, k, wa, wb, odd);
 }
 // lane per key x group of `gw` windows of [wa, wb) (the fill is latency-bound: fewer windows per
 // lane = more lanes, at one shared inversion pair per lane)
@@ -1082,8 +1223,16 @@ void launch_ecdsa_comb_chain(hipStream_t st, uint64_t n_keys, const KeyMeta* met
         return e ? (uint32_t)(e[0] != '0') : 1u;
     }();
     const uint32_t wa = half ? EC_LO_WIN : 0, wb = half ? EC_COMB_QWIN : EC_LO_WIN;
-    hipLaunchKernelGGL(k_ecdsa_comb_chain, dim3((uint32_t)((n_keys + 63) / 64)), dim3(64), 0, st, n_keys, meta, ectab,
-                       jac, prio, wa, wb, skip);
+    static const bool pair = [] {
+        const char* e = getenv("CHIP_EC_CHAIN_PAIR");
+        return e ? e[0] != '0' : EC_CHAIN_PAIR != 0;
+    }();
+    if (pair)
+        hipLaunchKernelGGL(k_ecdsa_comb_chain2, dim3((uint32_t)((2 * n_keys + 63) / 64)), dim3(64), 0, st, n_keys, meta,
+                           ectab, jac, prio, wa, wb, skip);
+    else
+        hipLaunchKernelGGL(k_ecdsa_comb_chain, dim3((uint32_t)((n_keys + 63) / 64)), dim3(64), 0, st, n_keys, meta,
+                           ectab, jac, prio, wa, wb, skip);
 }
 void launch_ecdsa_comb_fill(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, uint32_t* ctab, int half,
                             const uint32_t* skip) {

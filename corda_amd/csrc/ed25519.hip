@@ -13,6 +13,10 @@
 #include "ed_common_dev.hpp"
 #include "runtime.hpp"
 
+#include <cstdlib>
+#ifndef ED_STRAUS_OCC
+#define ED_STRAUS_OCC 1
+#endif
 #define ED_TAB_ENTRIES 9
 #define ED_TAB_WORDS (ED_TAB_ENTRIES * 40)
 
@@ -93,7 +97,10 @@ __global__ void __launch_bounds__(256) k_ed25519_key_prep(uint64_t n_keys, const
 }
 
 // ---- K1: batch verify over the compacted list of Ed25519 signatures needing arithmetic ----
-__global__ void __launch_bounds__(256) k_ed25519_verify(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
+// OCC: waves per SIMD the register allocation must leave room for (1: the compiler's choice, 248 VGPRs = 2 waves;
+// 3: <= 168 VGPRs, a few spilled long-lived words), CHIP_ED_STRAUS_OCC
+template <int OCC>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) k_ed25519_verify(const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
                                                         const uint32_t* __restrict__ key_idx,
                                                         const uint32_t* __restrict__ msg_idx,
                                                         const uint8_t* __restrict__ sig_data,
@@ -267,6 +274,14 @@ void launch_ed25519_verify(hipStream_t st, uint64_t n, const uint32_t* list, con
                            const chip_sig_batch* b, const uint32_t* abytes, const uint32_t* table, uint8_t* status) {
     if (!n) return;
     const uint32_t blocks = (uint32_t)((n + 255) / 256);
-    hipLaunchKernelGGL(k_ed25519_verify, dim3(blocks), dim3(256), 0, st, list, count, b->key_idx, b->msg_idx,
-                       b->sig_data, b->sig_off, b->msg_data, b->msg_off, b->msg_len, abytes, table, status);
+    static const int occ = [] {
+        const char* e = getenv("CHIP_ED_STRAUS_OCC");
+        return e ? atoi(e) : ED_STRAUS_OCC;
+    }();
+    if (occ == 3)
+        hipLaunchKernelGGL(k_ed25519_verify<3>, dim3(blocks), dim3(256), 0, st, list, count, b->key_idx, b->msg_idx,
+                           b->sig_data, b->sig_off, b->msg_data, b->msg_off, b->msg_len, abytes, table, status);
+    else
+        hipLaunchKernelGGL(k_ed25519_verify<1>, dim3(blocks), dim3(256), 0, st, list, count, b->key_idx, b->msg_idx,
+                           b->sig_data, b->sig_off, b->msg_data, b->msg_off, b->msg_len, abytes, table, status);
 }

@@ -666,10 +666,15 @@ struct CompAcc {
     const uint64_t* lm_off;
     const uint32_t* lm_len;
     uint64_t n, t, cbase;
+    const uint64_t* xstart;   // the fused walk's rows hold KRYO_REL offsets into blob t's extra region
+    uint64_t xbase;
     __device__ __forceinline__ bool lm(uint64_t k) const { return lm_off && k - cbase < KRYO_LM_C; }
     __device__ __forceinline__ uint64_t li(uint64_t k) const { return (k - cbase) * n + t; }
     __device__ __forceinline__ uint32_t grp(uint64_t k) const { return lm(k) ? lm_grp[li(k)] : grp_soa[k]; }
-    __device__ __forceinline__ uint64_t off(uint64_t k) const { return lm(k) ? lm_off[li(k)] : off_soa[k]; }
+    __device__ __forceinline__ uint64_t off(uint64_t k) const {
+        const uint64_t v = lm(k) ? lm_off[li(k)] : off_soa[k];
+        return (v & KRYO_REL) ? xbase + xstart[t] + (v & ~KRYO_REL) : v;
+    }
     __device__ __forceinline__ uint32_t len(uint64_t k) const { return lm(k) ? lm_len[li(k)] : len_soa[k]; }
 };
 
@@ -762,7 +767,53 @@ struct Outs {   // pass-2 destinations (NULL in pass 1)
     uint4* xd_a;                   // chunk-spanning runs as copy descriptors (StxOut), k_stx_dechunk
     uint2* xd_b;
     uint32_t* xd_n;
+    uint64_t* lm_koff;             // the fused walk (StxOut): signer-key rows, pass 1 writes the rows
+    uint32_t* lm_klen;
+    uint32_t fused;
+    uint32_t* n_ovf;
 };
+
+// an offset the fused pass 1 wrote: KRYO_REL | (offset in blob t's extra region) -> the pool offset
+__device__ __forceinline__ uint64_t rel_off(uint64_t v, const uint64_t* xstart, uint64_t xbase, uint64_t t) {
+    return (v & KRYO_REL) ? xbase + xstart[t] + (v & ~KRYO_REL) : v;
+}
+
+__device__ __forceinline__ void xd_put(Sink& sink, uint64_t at, uint64_t src, uint32_t n, uint32_t rem, bool& ovf) {
+    if (sink.nx < KRYO_XD) {
+        sink.xa[(uint64_t)sink.nx * sink.xs] = make_uint4((uint32_t)at, (uint32_t)(at >> 32), (uint32_t)src,
+                                                          (uint32_t)(src >> 32));
+        sink.xb[(uint64_t)sink.nx * sink.xs] = make_uint2(n, rem);
+        sink.nx++;
+    } else {
+        ovf = true;
+    }
+}
+
+// pass 1 of the fused walk: where a payload run of n bytes starts — its pool offset when it lies in one chunk, else
+// KRYO_REL | its offset in the blob's extra region (the same layout run1<true> gives), with a copy descriptor for
+// k_stx_dechunk (a blob with more than KRYO_XD of them overflows: pass 2 re-walks it)
+__device__ __forceinline__ uint64_t run1f(Cur& c, uint32_t n, Sink& sink, uint64_t& extra, bool& ovf) {
+    if (n == 0) return c.pos;
+    if (c.rem1 == 0) {
+        c.rem1 = c.varint<0>();
+        if (c.err) return 0;
+        if (c.rem1 == 0) {
+            c.fail(E_KRYO);
+            return 0;
+        }
+    }
+    if (n <= c.rem1) {
+        const uint64_t at = c.pos;
+        c.skip<0>(n);
+        c.rem1 -= n;
+        return at;
+    }
+    const uint64_t at = KRYO_REL | extra;
+    extra += (n + 3) & ~3u;
+    xd_put(sink, at, c.pos, n, c.rem1, ovf);
+    c.skip<1>(n);
+    return at;
+}
 
 // the required-key walk's count and its first STX_REC signer entries for tx t (components in the pool); st may
 // become UNSUPPORTED (a key the walk cannot read, more than 64 signer entries: the JVM path)
@@ -771,7 +822,8 @@ __device__ __forceinline__ void stx_req_tail(Cur& c, uint64_t t, int& st, uint64
     bool over = false;
     if (st == CHIP_STX_OK &&
         !req_walk(c, o.pool, o.pool_bytes, cbase, cbase + comps,
-                  CompAcc{o.comp_group, o.comp_off, o.comp_len, o.lm_grp, o.lm_off, o.lm_len, o.n_lm, t, cbase}, o.reg,
+                  CompAcc{o.comp_group, o.comp_off, o.comp_len, o.lm_grp, o.lm_off, o.lm_len, o.n_lm, t, cbase,
+                          o.extra_start, o.extra_base}, o.reg,
                   [&](uint64_t at, uint32_t len, bool req) {
                       if (req) {
                           over |= cnt >= 64;
@@ -796,15 +848,19 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
                                                    uint64_t* __restrict__ nextra, Outs o) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
+    // the fused walk's pass 2 re-walks only the blobs whose entries overflow pass 1's rows
+    if (EMIT && o.fused && (status[t] != CHIP_STX_OK || !(o.xd_n[t] & KRYO_XN_OVF))) return;
     if (EMIT && status[t] != CHIP_STX_OK) {
         if (o.nraw) o.nraw[t] = 0;
         if (o.xd_a) o.xd_n[t] = 0;
         return;
     }
+    const bool F = !EMIT && o.fused;   // pass 1 of the fused walk: rows, salts and descriptors written here
+    bool ovf = false;
     const uint64_t a = off[t], b = a + len[t];
     uint64_t comps = 0, sigs = 0, extra = 0;
-    Sink sink{o.pool, EMIT ? o.extra_base + o.extra_start[t] : 0, 0, 0, EMIT && o.xd_a ? o.xd_a + t : nullptr,
-              EMIT && o.xd_a ? o.xd_b + t : nullptr, n};
+    Sink sink{o.pool, EMIT ? o.extra_base + o.extra_start[t] : 0, 0, 0, (EMIT || F) && o.xd_a ? o.xd_a + t : nullptr,
+              (EMIT || F) && o.xd_a ? o.xd_b + t : nullptr, n};
     uint64_t cbase = EMIT ? o.comp_start[t] : 0, sbase = EMIT ? o.sig_start[t] : 0;
     int st = CHIP_STX_OK;
     Cur c;
@@ -841,14 +897,16 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
             if (sl == 0) c.fail(E_UNSUP);
             sl -= 1;
             {
-                const uint64_t at = run1<EMIT>(c, sl, sink, extra);
-                if (EMIT && !KRYO_NO_STORES) {
+                const uint64_t at = F ? run1f(c, sl, sink, extra, ovf) : run1<EMIT>(c, sl, sink, extra);
+                if ((EMIT || F) && !KRYO_NO_STORES) {
                     if (sigs < KRYO_LM_S) {
                         o.lm_soff[sigs * o.n_lm + t] = at;
                         o.lm_slen[sigs * o.n_lm + t] = sl;
-                    } else {
+                    } else if (EMIT) {
                         o.sig_off[sbase + sigs] = at;
                         o.sig_len[sbase + sigs] = sl;
+                    } else {
+                        ovf = true;
                     }
                 }
             }
@@ -859,8 +917,12 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
             c.not_null<1>();
             const uint32_t kl = c.varint<1>();
             {
-                const uint64_t at = run1<EMIT>(c, kl, sink, extra);
-                if (EMIT) {   // (kept in the KRYO_NO_STORES experiment: the key interning reads them)
+                const uint64_t at = F ? run1f(c, kl, sink, extra, ovf) : run1<EMIT>(c, kl, sink, extra);
+                // (kept in the KRYO_NO_STORES experiment: the key interning reads them)
+                if ((EMIT || F) && o.fused && sigs < KRYO_LM_S) {
+                    o.lm_koff[sigs * o.n_lm + t] = at;
+                    o.lm_klen[sigs * o.n_lm + t] = kl;
+                } else if (EMIT) {
                     o.key_off[sbase + sigs] = at;
                     o.key_len[sbase + sigs] = kl;
                 }
@@ -876,7 +938,7 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
             const int32_t sch = c.zigzag<2>();
             c.end_field<2>();
             c.end_field<1>();
-            if (EMIT) {
+            if (EMIT || F) {
                 uint32_t ti = 0xffffffffu;
                 for (uint32_t m = 0; m < o.n_meta; m++)
                     if (o.meta[2 * m] == pv && o.meta[2 * m + 1] == sch) {
@@ -886,7 +948,7 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
                 if (!KRYO_NO_STORES) {
                     if (sigs < KRYO_LM_S) {
                         o.lm_tmpl[sigs * o.n_lm + t] = ti;   // tx_idx = t, written by the transpose
-                    } else {
+                    } else if (EMIT) {
                         o.tmpl_idx[sbase + sigs] = ti;
                         o.tx_idx[sbase + sigs] = (uint32_t)t;
                     }
@@ -952,8 +1014,24 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
                         w.rem1 = w.varint<0>();
                         if (!w.err && w.rem1 == 0) w.fail(E_KRYO);
                     }
-                    if (cl > w.rem1) extra += (cl + 3) & ~3u;
+                    uint64_t at = w.pos;
+                    if (cl > w.rem1) {
+                        if (F) {
+                            at = KRYO_REL | extra;
+                            xd_put(sink, at, w.pos, cl, w.rem1, ovf);
+                        }
+                        extra += (cl + 3) & ~3u;
+                    }
                     canon &= stateref_canonical(w, cl);
+                    if (F && !KRYO_NO_STORES) {
+                        if (comps < KRYO_LM_C) {
+                            o.lm_off[comps * o.n_lm + t] = at;
+                            o.lm_len[comps * o.n_lm + t] = cl;
+                            o.lm_int[comps * o.n_lm + t] = k;
+                        } else {
+                            ovf = true;
+                        }
+                    }
                 }
                 comps++;
             }
@@ -974,20 +1052,20 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
                 in_first = first;
                 in_count = nc;
             }
-            if (EMIT)
+            if (EMIT || F)
                 for (uint64_t k = first; k < cbase + comps && !KRYO_NO_STORES; k++) {
                     if (k - cbase < KRYO_LM_C) o.lm_grp[(k - cbase) * o.n_lm + t] = (uint32_t)gi;
-                    else o.comp_group[k] = (uint32_t)gi;
+                    else if (EMIT) o.comp_group[k] = (uint32_t)gi;
                 }
         }
         // PrivacySalt: the registry's id, writeBytesWithLength(32 bytes)
         if (!w.err) {
             if (w.read_class<0>() != o.reg.privacy_salt) w.fail(E_UNSUP);
             if (w.varint<0>() != 32) w.fail(E_UNSUP);
-            if (EMIT && !w.err && w.end - w.pos >= 32) {
+            if ((EMIT || F) && !w.err && w.end - w.pos >= 32) {
                 uint32_t* dst = reinterpret_cast<uint32_t*>(o.salts + t * 32);
                 DStream d;
-                d.open(o.pool, w.pos);
+                d.open(EMIT ? o.pool : w.pool, w.pos);
                 uint32_t v[4];
                 d.take4(v);
                 for (int k = 0; k < 4; k++) dst[k] = v[k];
@@ -1011,7 +1089,8 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
         // is not in the pool yet: k_stx_post compares them once k_stx_dechunk has written the extra region
         if (EMIT && st == CHIP_STX_OK && in_count > 1 && !KRYO_NO_STORES && !o.xd_a) {
             sink.flush();
-            const CompAcc ca{o.comp_group, o.comp_off, o.comp_len, o.lm_grp, o.lm_off, o.lm_len, o.n_lm, t, cbase};
+            const CompAcc ca{o.comp_group, o.comp_off, o.comp_len, o.lm_grp, o.lm_off, o.lm_len, o.n_lm, t, cbase,
+                             o.extra_start, o.extra_base};
             for (uint64_t i = 0; i < in_count && st == CHIP_STX_OK; i++)
                 for (uint64_t j = i + 1; j < in_count; j++) {
                     if (key_eq(o.pool, ca.off(in_first + i), ca.len(in_first + i), ca.off(in_first + j),
@@ -1038,6 +1117,10 @@ done:
         ncomp[t] = st == CHIP_STX_OK ? comps : 0;
         nsig[t] = st == CHIP_STX_OK ? sigs : 0;
         nextra[t] = st == CHIP_STX_OK ? extra : 0;   // de-chunked (chunk-spanning) payload, 4-byte units
+        if (F) {
+            o.xd_n[t] = st == CHIP_STX_OK ? (sink.nx | KRYO_XN_REL | (ovf ? KRYO_XN_OVF : 0u)) : 0u;
+            if (st == CHIP_STX_OK && ovf) atomicAdd(o.n_ovf, 1u);
+        }
     }
 }
 
@@ -1316,7 +1399,7 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_required(uint64_t n, uint8_t
     } else {
         Cur c;
         if (!req_walk(c, r.pool, pool_bytes, comp_start[t], comp_start[t + 1],
-                      CompAcc{comp_group, comp_off, comp_len, nullptr, nullptr, nullptr, 0, 0, 0}, reg, take))
+                      CompAcc{comp_group, comp_off, comp_len, nullptr, nullptr, nullptr, 0, 0, 0, nullptr, 0}, reg, take))
             bad = true;
     }
     if (bad) status[t] = CHIP_STX_UNSUPPORTED;
@@ -1525,10 +1608,19 @@ inline dim3 grid_of(uint64_t n) { return dim3((uint32_t)((n + 255) / 256)); }
 
 }  // namespace
 
+static Outs outs_of(const chip_stx_blobs* in, const chip_kryo_registry& reg, const StxOut& d) {
+    return Outs{d.pool, d.pool_bytes, d.extra_start, d.extra_base, d.salts, d.comp_start, d.comp_group, d.comp_internal,
+                d.comp_off, d.comp_len, d.sig_start, d.tx_idx, d.tmpl_idx, d.sig_off, d.sig_len, d.skey_off, d.skey_len,
+                d.meta, d.n_meta, d.nraw, reg, d.rec_off, d.rec_len, in->n, d.lm_off, d.lm_len, d.lm_int, d.lm_grp,
+                d.lm_soff, d.lm_slen, d.lm_tmpl, KRYO_DEFER_COPY ? d.xd_a : nullptr, d.xd_b, d.xd_n, d.lm_koff,
+                d.lm_klen, KRYO_DEFER_COPY ? d.fused : 0u, d.n_ovf};
+}
+
 void launch_stx_count(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_registry& reg, uint8_t* status,
-                      uint64_t* ncomp, uint64_t* nsig, uint64_t* nextra) {
+                      uint64_t* ncomp, uint64_t* nsig, uint64_t* nextra, const StxOut* d) {
     if (!in->n) return;
     Outs o{};
+    if (d && d->fused && KRYO_DEFER_COPY) o = outs_of(in, reg, *d);   // the fused walk: rows, salts, descriptors
     o.reg = reg;
     hipLaunchKernelGGL(k_stx_parse<false>, grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->off, in->len,
                        in->data_bytes, status, ncomp, nsig, nextra, o);
@@ -1552,7 +1644,7 @@ __global__ void __launch_bounds__(256) k_stx_lm_comps(uint64_t n, uint64_t ncomp
     const uint64_t t = owner_of(start, n, c), j = c - start[t];
     if (j >= KRYO_LM_C) return;   // stored in place by pass 2
     const uint64_t i = j * o.n_lm + t;
-    o.comp_off[c] = o.lm_off[i];
+    o.comp_off[c] = rel_off(o.lm_off[i], o.extra_start, o.extra_base, t);
     o.comp_len[c] = o.lm_len[i];
     o.comp_internal[c] = o.lm_int[i];
     o.comp_group[c] = o.lm_grp[i];
@@ -1564,10 +1656,14 @@ __global__ void __launch_bounds__(256) k_stx_lm_sigs(uint64_t n, uint64_t nsig, 
     const uint64_t t = owner_of(start, n, s), j = s - start[t];
     if (j >= KRYO_LM_S) return;
     const uint64_t i = j * o.n_lm + t;
-    o.sig_off[s] = o.lm_soff[i];
+    o.sig_off[s] = rel_off(o.lm_soff[i], o.extra_start, o.extra_base, t);
     o.sig_len[s] = o.lm_slen[i];
     o.tmpl_idx[s] = o.lm_tmpl[i];
     o.tx_idx[s] = (uint32_t)t;
+    if (o.fused) {   // the signer-key rows (pass 1 / pass 2 of the fused walk)
+        o.key_off[s] = rel_off(o.lm_koff[i], o.extra_start, o.extra_base, t);
+        o.key_len[s] = o.lm_klen[i];
+    }
 }
 
 // one piece of a de-chunked run, by the whole wave: head bytes up to a dword-aligned destination, then 16
@@ -1633,18 +1729,23 @@ __device__ __forceinline__ uint32_t dechunk_header(const uint8_t* pool, uint64_t
 // a bad descriptor inside the pool.)
 __global__ void __launch_bounds__(256) k_stx_dechunk(uint64_t n, uint8_t* __restrict__ pool, uint64_t pool_bytes,
                                                      const uint4* __restrict__ xa, const uint2* __restrict__ xb,
-                                                     const uint32_t* __restrict__ xn) {
+                                                     const uint32_t* __restrict__ xn, const uint64_t* __restrict__ xstart,
+                                                     uint64_t xbase) {
     const uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
     const uint32_t lane = threadIdx.x & 63u;
     if (t >= n) return;
-    uint32_t cnt = __builtin_amdgcn_readfirstlane(xn[t]);
+    const uint32_t xnt = __builtin_amdgcn_readfirstlane(xn[t]);
+    uint32_t cnt = xnt & KRYO_XN_CNT;
     cnt = cnt < KRYO_XD ? cnt : KRYO_XD;
+    // the fused walk's descriptors hold offsets in the blob's extra region (KRYO_REL)
+    const uint64_t rbase = (xnt & KRYO_XN_REL) && cnt ? xbase + xstart[t] : 0;
     uint64_t dst = 0, src = 0, src2 = 0;
     uint32_t len = 0, rem = 0, rem2 = 0;
     if (lane < cnt) {
         const uint4 a = xa[(uint64_t)lane * n + t];
         const uint2 b = xb[(uint64_t)lane * n + t];
         dst = (uint64_t)a.x | ((uint64_t)a.y << 32);
+        if (dst & KRYO_REL) dst = rbase + (dst & ~KRYO_REL);
         src = (uint64_t)a.z | ((uint64_t)a.w << 32);
         len = b.x;
         rem = b.y;
@@ -1695,7 +1796,8 @@ __global__ void __launch_bounds__(256) k_stx_post(uint64_t n, const uint8_t* __r
     int st = CHIP_STX_OK;
     const uint64_t cbase = o.comp_start[t], comps = o.comp_start[t + 1] - cbase;
     if (!KRYO_NO_STORES) {
-        const CompAcc ca{o.comp_group, o.comp_off, o.comp_len, o.lm_grp, o.lm_off, o.lm_len, o.n_lm, t, cbase};
+        const CompAcc ca{o.comp_group, o.comp_off, o.comp_len, o.lm_grp, o.lm_off, o.lm_len, o.n_lm, t, cbase,
+                             o.extra_start, o.extra_base};
         // group 0 occurs at most once (a duplicated group is INVARIANT in pass 1), its components contiguous
         uint64_t in_first = 0, in_count = 0;
         for (uint64_t k = cbase; k < cbase + comps; k++)
@@ -1724,14 +1826,14 @@ __global__ void __launch_bounds__(256) k_stx_post(uint64_t n, const uint8_t* __r
 void launch_stx_emit(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_registry& reg, uint8_t* status,
                      const StxOut& d) {
     if (!in->n) return;
-    Outs o{d.pool, d.pool_bytes, d.extra_start, d.extra_base, d.salts, d.comp_start, d.comp_group, d.comp_internal, d.comp_off, d.comp_len, d.sig_start,
-           d.tx_idx, d.tmpl_idx, d.sig_off, d.sig_len, d.skey_off, d.skey_len, d.meta, d.n_meta, d.nraw, reg,
-           d.rec_off, d.rec_len, in->n, d.lm_off, d.lm_len, d.lm_int, d.lm_grp, d.lm_soff, d.lm_slen, d.lm_tmpl,
-           KRYO_DEFER_COPY ? d.xd_a : nullptr, d.xd_b, d.xd_n};
-    hipLaunchKernelGGL(k_stx_parse<true>, grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->off, in->len,
-                       in->data_bytes, status, nullptr, nullptr, nullptr, o);
+    const Outs o = outs_of(in, reg, d);
+    // the fused walk: pass 1 wrote every blob that fits its rows; pass 2 only when some overflowed
+    if (!d.fused || d.n_ovf_host)
+        hipLaunchKernelGGL(k_stx_parse<true>, grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->off, in->len,
+                           in->data_bytes, status, nullptr, nullptr, nullptr, o);
     if (o.xd_a) {
-        hipLaunchKernelGGL(k_stx_dechunk, grid_of(in->n * 64), dim3(256), 0, st, in->n, d.pool, d.pool_bytes, d.xd_a, d.xd_b, d.xd_n);
+        hipLaunchKernelGGL(k_stx_dechunk, grid_of(in->n * 64), dim3(256), 0, st, in->n, d.pool, d.pool_bytes, d.xd_a,
+                           d.xd_b, d.xd_n, d.extra_start, d.extra_base);
         hipLaunchKernelGGL(k_stx_post, grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->data_bytes, status, o);
     }
     if (d.ncomp)

@@ -132,7 +132,7 @@ struct DevBuf {
 // buffers of one Kryo front-end call (chip_stx_parse_device): counts, ranges, pool, batches, key
 // interning, required keys, scan scratch
 struct StxBufs {
-    DevBuf s_ncomp, s_nsig, s_nbytes, s_cstart, s_sstart, s_pstart, s_pool, s_salts, s_cgroup, s_cint, s_coff, s_clen, s_txidx, s_tmpl, s_soff, s_slen, s_skoff, s_sklen, s_meta, s_tab, s_tabmin, s_kslot, s_krep, s_kflag, s_kincl, s_kidx, s_koff, s_klen, s_temp, r_nraw, r_rstart, r_kid, r_len, r_keep, r_kincl, r_off, r_nreq, r_qstart, r_nstart, r_val, r_nk, r_w, r_flag, r_tx, r_nn, r_nc, r_ninc, r_cinc, k_off, k_len, k_kind, k_ok, k_tx, r_tot, r_roff, r_rlen, lm_off, lm_len, lm_int, lm_grp, lm_soff, lm_slen, lm_tmpl, xd_a, xd_b, xd_n;
+    DevBuf s_ncomp, s_nsig, s_nbytes, s_cstart, s_sstart, s_pstart, s_pool, s_salts, s_cgroup, s_cint, s_coff, s_clen, s_txidx, s_tmpl, s_soff, s_slen, s_skoff, s_sklen, s_meta, s_tab, s_tabmin, s_kslot, s_krep, s_kflag, s_kincl, s_kidx, s_koff, s_klen, s_temp, r_nraw, r_rstart, r_kid, r_len, r_keep, r_kincl, r_off, r_nreq, r_qstart, r_nstart, r_val, r_nk, r_w, r_flag, r_tx, r_nn, r_nc, r_ninc, r_cinc, k_off, k_len, k_kind, k_ok, k_tx, r_tot, r_roff, r_rlen, lm_off, lm_len, lm_int, lm_grp, lm_soff, lm_slen, lm_tmpl, xd_a, xd_b, xd_n, lm_koff, lm_klen, s_ovf;
     hipStream_t cs = nullptr;                     // the blob copy into s_pool, overlapping pass 1
     hipEvent_t ce0 = nullptr, ce1 = nullptr;
     void release() {
@@ -141,7 +141,7 @@ struct StxBufs {
         if (ce1) (void)hipEventDestroy(ce1);
         cs = nullptr;
         ce0 = ce1 = nullptr;
-        for (DevBuf* b : {&s_ncomp, &s_nsig, &s_nbytes, &s_cstart, &s_sstart, &s_pstart, &s_pool, &s_salts, &s_cgroup, &s_cint, &s_coff, &s_clen, &s_txidx, &s_tmpl, &s_soff, &s_slen, &s_skoff, &s_sklen, &s_meta, &s_tab, &s_tabmin, &s_kslot, &s_krep, &s_kflag, &s_kincl, &s_kidx, &s_koff, &s_klen, &s_temp, &r_nraw, &r_rstart, &r_kid, &r_len, &r_keep, &r_kincl, &r_off, &r_nreq, &r_qstart, &r_nstart, &r_val, &r_nk, &r_w, &r_flag, &r_tx, &r_nn, &r_nc, &r_ninc, &r_cinc, &k_off, &k_len, &k_kind, &k_ok, &k_tx, &r_tot, &r_roff, &r_rlen, &lm_off, &lm_len, &lm_int, &lm_grp, &lm_soff, &lm_slen, &lm_tmpl, &xd_a, &xd_b, &xd_n}) b->release();
+        for (DevBuf* b : {&s_ncomp, &s_nsig, &s_nbytes, &s_cstart, &s_sstart, &s_pstart, &s_pool, &s_salts, &s_cgroup, &s_cint, &s_coff, &s_clen, &s_txidx, &s_tmpl, &s_soff, &s_slen, &s_skoff, &s_sklen, &s_meta, &s_tab, &s_tabmin, &s_kslot, &s_krep, &s_kflag, &s_kincl, &s_kidx, &s_koff, &s_klen, &s_temp, &r_nraw, &r_rstart, &r_kid, &r_len, &r_keep, &r_kincl, &r_off, &r_nreq, &r_qstart, &r_nstart, &r_val, &r_nk, &r_w, &r_flag, &r_tx, &r_nn, &r_nc, &r_ninc, &r_cinc, &k_off, &k_len, &k_kind, &k_ok, &k_tx, &r_tot, &r_roff, &r_rlen, &lm_off, &lm_len, &lm_int, &lm_grp, &lm_soff, &lm_slen, &lm_tmpl, &xd_a, &xd_b, &xd_n, &lm_koff, &lm_klen, &s_ovf}) b->release();
     }
 };
 
@@ -162,6 +162,7 @@ struct chip_ctx {
     hipEvent_t ev_ec_chain_lo = nullptr, ev_ec_chain_hi = nullptr, ev_ec_lo = nullptr;
     // the ECDSA key decode at the head of an early Ed25519 batch (CHIP_ECKEYS_LATE=1: after [S]B, the round-4 order)
     bool eckeys_late = false;
+    bool kryo_fused = true;   // Kryo pass 1 writes the rows itself (CHIP_KRYO_FUSED=0: the two-walk front end)
     std::recursive_mutex mu;   // recursive: chip_stx_verify holds it across the entries it calls
     std::string err;
     // verify workspaces
@@ -226,7 +227,9 @@ struct chip_ctx {
         }
         e.pending = false;
     }
+    bool ktiming = true;   // CHIP_KERNEL_TIMING=0: no event pairs (each timing event is a barrier packet)
     int kbegin(int kind, hipStream_t st) {
+        if (!ktiming) return -1;
         const int i = knext;
         knext = (knext + 1) % KRING;
         KEv& e = kring[i];
@@ -240,6 +243,7 @@ struct chip_ctx {
         return i;
     }
     void kend(int i, hipStream_t st) {
+        if (i < 0) return;
         hipEventRecord(kring[i].b, st);
         kring[i].pending = true;
     }
@@ -555,6 +559,8 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
     if (const char* e = getenv("CHIP_COMB_BUDGET_MB")) c->comb_budget = (uint64_t)strtoull(e, nullptr, 10) << 20;
     if (const char* e = getenv("CHIP_ECKEYS_LATE")) c->eckeys_late = e[0] == '1';
     if (const char* e = getenv("CHIP_STAGING_RING")) c->ring.enabled = e[0] != '0';
+    if (const char* e = getenv("CHIP_KERNEL_TIMING")) c->ktiming = e[0] != '0';
+    if (const char* e = getenv("CHIP_KRYO_FUSED")) c->kryo_fused = e[0] != '0';
     if (cfg && cfg->reserve_sigs) {
         (void)c->lists.ensure(cfg->reserve_sigs * 4 * N_LISTS);
     }
@@ -1419,8 +1425,47 @@ static int stx_parse(chip_ctx* c, StxBufs& B, const chip_stx_blobs* in, uint8_t*
             copied = true;
         }
     }
-    // pass 1: validate + count; ranges = inclusive scans written one past a zero
-    launch_stx_count(st, in, reg, tx_status, B.s_ncomp.as<uint64_t>(), B.s_nsig.as<uint64_t>(), B.s_nbytes.as<uint64_t>());
+    // the per-tx rows (lane-major), descriptors and metadata templates: pass 1 writes them in the fused walk
+    StxOut d{};
+    d.fused = c->kryo_fused ? 1u : 0u;
+    HIPCHK(c, B.s_meta.ensure((uint64_t)in->n_meta * 8 + 16));
+    if (in->n_meta)
+        HIPCHK(c, ring_h2d(c->ring, B.s_meta.p, in->meta, (uint64_t)in->n_meta * 8, st));
+    d.meta = B.s_meta.as<int32_t>();
+    d.n_meta = in->n_meta;
+    d.salts = B.s_salts.as<uint8_t>();
+    HIPCHK(c, B.lm_off.ensure(n * KRYO_LM_C * 8 + 16));
+    HIPCHK(c, B.lm_len.ensure(n * KRYO_LM_C * 4 + 16));
+    HIPCHK(c, B.lm_int.ensure(n * KRYO_LM_C * 4 + 16));
+    HIPCHK(c, B.lm_grp.ensure(n * KRYO_LM_C * 4 + 16));
+    HIPCHK(c, B.lm_soff.ensure(n * KRYO_LM_S * 8 + 16));
+    HIPCHK(c, B.lm_slen.ensure(n * KRYO_LM_S * 4 + 16));
+    HIPCHK(c, B.lm_tmpl.ensure(n * KRYO_LM_S * 4 + 16));
+    HIPCHK(c, B.xd_a.ensure(n * KRYO_XD * 16 + 16));
+    HIPCHK(c, B.xd_b.ensure(n * KRYO_XD * 8 + 16));
+    HIPCHK(c, B.xd_n.ensure(n * 4 + 16));
+    d.lm_off = B.lm_off.as<uint64_t>();
+    d.lm_len = B.lm_len.as<uint32_t>();
+    d.lm_int = B.lm_int.as<uint32_t>();
+    d.lm_grp = B.lm_grp.as<uint32_t>();
+    d.lm_soff = B.lm_soff.as<uint64_t>();
+    d.lm_slen = B.lm_slen.as<uint32_t>();
+    d.lm_tmpl = B.lm_tmpl.as<uint32_t>();
+    d.xd_a = B.xd_a.as<uint4>();
+    d.xd_b = B.xd_b.as<uint2>();
+    d.xd_n = B.xd_n.as<uint32_t>();
+    if (d.fused) {
+        HIPCHK(c, B.lm_koff.ensure(n * KRYO_LM_S * 8 + 16));
+        HIPCHK(c, B.lm_klen.ensure(n * KRYO_LM_S * 4 + 16));
+        HIPCHK(c, B.s_ovf.ensure(64));
+        d.lm_koff = B.lm_koff.as<uint64_t>();
+        d.lm_klen = B.lm_klen.as<uint32_t>();
+        d.n_ovf = B.s_ovf.as<uint32_t>();
+        HIPCHK(c, hipMemsetAsync(d.n_ovf, 0, 4, st));
+    }
+    // pass 1: validate + count (+ the rows); ranges = inclusive scans written one past a zero
+    launch_stx_count(st, in, reg, tx_status, B.s_ncomp.as<uint64_t>(), B.s_nsig.as<uint64_t>(), B.s_nbytes.as<uint64_t>(),
+                     &d);
     HIPCHK(c, hipGetLastError());
     DevBuf* cnt[3] = {&B.s_ncomp, &B.s_nsig, &B.s_nbytes};
     DevBuf* rng[3] = {&B.s_cstart, &B.s_sstart, &B.s_pstart};
@@ -1431,6 +1476,7 @@ static int stx_parse(chip_ctx* c, StxBufs& B, const chip_stx_blobs* in, uint8_t*
     uint64_t tot[3] = {0, 0, 0};
     for (int k = 0; k < 3; k++)
         HIPCHK(c, hipMemcpyAsync(&tot[k], rng[k]->as<uint64_t>() + n, 8, hipMemcpyDeviceToHost, st));
+    if (d.fused) HIPCHK(c, hipMemcpyAsync(&d.n_ovf_host, d.n_ovf, 4, hipMemcpyDeviceToHost, st));
     HIPCHK(c, hipStreamSynchronize(st));
     const uint64_t ncomp = tot[0], nsig = tot[1];
     if (nsig >= (1ull << 31)) return fail(c, CHIP_E_ARG, "too many signatures");
@@ -1458,7 +1504,6 @@ static int stx_parse(chip_ctx* c, StxBufs& B, const chip_stx_blobs* in, uint8_t*
     HIPCHK(c, B.s_slen.ensure(nsig * 4 + 16));
     HIPCHK(c, B.s_skoff.ensure(nsig * 8 + 16));
     HIPCHK(c, B.s_sklen.ensure(nsig * 4 + 16));
-    HIPCHK(c, B.s_meta.ensure((uint64_t)in->n_meta * 8 + 16));
     uint64_t cap = 1024;
     while (cap < 2 * nsig) cap <<= 1;
     HIPCHK(c, B.s_tab.ensure(cap * 8));
@@ -1468,9 +1513,6 @@ static int stx_parse(chip_ctx* c, StxBufs& B, const chip_stx_blobs* in, uint8_t*
     HIPCHK(c, B.s_koff.ensure(nsig * 8 + 16));
     if (stx_scan_temp_bytes(nsig > 2 ? nsig : 2) > B.s_temp.cap)
         HIPCHK(c, B.s_temp.ensure(stx_scan_temp_bytes(nsig > 2 ? nsig : 2)));
-    if (in->n_meta)
-        HIPCHK(c, ring_h2d(c->ring, B.s_meta.p, in->meta, (uint64_t)in->n_meta * 8, st));
-    StxOut d{};
     d.pool = pool_p;
     d.pool_bytes = pool;
     const bool want_req = in->flags & CHIP_STX_REQUIRED;
@@ -1484,7 +1526,6 @@ static int stx_parse(chip_ctx* c, StxBufs& B, const chip_stx_blobs* in, uint8_t*
     d.rec_len = want_req ? B.r_rlen.as<uint32_t>() : nullptr;
     d.extra_start = B.s_pstart.as<uint64_t>();
     d.extra_base = extra_base;
-    d.salts = B.s_salts.as<uint8_t>();
     d.comp_start = B.s_cstart.as<uint64_t>();
     d.comp_group = B.s_cgroup.as<uint32_t>();
     d.comp_internal = B.s_cint.as<uint32_t>();
@@ -1497,8 +1538,6 @@ static int stx_parse(chip_ctx* c, StxBufs& B, const chip_stx_blobs* in, uint8_t*
     d.skey_len = B.s_sklen.as<uint32_t>();
     d.sig_off = B.s_soff.as<uint64_t>();
     d.skey_off = B.s_skoff.as<uint64_t>();
-    d.meta = B.s_meta.as<int32_t>();
-    d.n_meta = in->n_meta;
     d.tab = B.s_tab.as<uint64_t>();
     d.tab_min = B.s_tabmin.as<uint32_t>();
     d.kslot = B.s_kslot.as<uint32_t>();
@@ -1508,28 +1547,8 @@ static int stx_parse(chip_ctx* c, StxBufs& B, const chip_stx_blobs* in, uint8_t*
     d.key_idx = B.s_kidx.as<uint32_t>();
     d.key_off = B.s_koff.as<uint64_t>();
     d.key_len = B.s_klen.as<uint32_t>();
-    HIPCHK(c, B.lm_off.ensure(n * KRYO_LM_C * 8 + 16));
-    HIPCHK(c, B.lm_len.ensure(n * KRYO_LM_C * 4 + 16));
-    HIPCHK(c, B.lm_int.ensure(n * KRYO_LM_C * 4 + 16));
-    HIPCHK(c, B.lm_grp.ensure(n * KRYO_LM_C * 4 + 16));
-    HIPCHK(c, B.lm_soff.ensure(n * KRYO_LM_S * 8 + 16));
-    HIPCHK(c, B.lm_slen.ensure(n * KRYO_LM_S * 4 + 16));
-    HIPCHK(c, B.lm_tmpl.ensure(n * KRYO_LM_S * 4 + 16));
     d.ncomp = ncomp;
     d.nsig = nsig;
-    d.lm_off = B.lm_off.as<uint64_t>();
-    d.lm_len = B.lm_len.as<uint32_t>();
-    d.lm_int = B.lm_int.as<uint32_t>();
-    d.lm_grp = B.lm_grp.as<uint32_t>();
-    d.lm_soff = B.lm_soff.as<uint64_t>();
-    d.lm_slen = B.lm_slen.as<uint32_t>();
-    d.lm_tmpl = B.lm_tmpl.as<uint32_t>();
-    HIPCHK(c, B.xd_a.ensure(n * KRYO_XD * 16 + 16));
-    HIPCHK(c, B.xd_b.ensure(n * KRYO_XD * 8 + 16));
-    HIPCHK(c, B.xd_n.ensure(n * 4 + 16));
-    d.xd_a = B.xd_a.as<uint4>();
-    d.xd_b = B.xd_b.as<uint2>();
-    d.xd_n = B.xd_n.as<uint32_t>();
     // pass 2: the batches; then the signer keys interned
     launch_stx_emit(st, in, reg, tx_status, d);
     HIPCHK(c, hipGetLastError());

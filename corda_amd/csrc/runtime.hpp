@@ -101,13 +101,26 @@ struct StxOut {
     // bytes left in the source's current chunk); k_stx_dechunk then moves them a wave per transaction
     uint4* xd_a;
     uint2* xd_b;
-    uint32_t* xd_n;                // [n] descriptors of tx t (0 for a failed tx)
+    uint32_t* xd_n;                // [n] descriptors of tx t (0 for a failed tx) | KRYO_XN_* flags
+    // fused walk (kryo_fused): pass 1 writes the lane-major rows, the signer-key rows below, the salts and the
+    // descriptors itself; an offset in the extra region is KRYO_REL | (offset in the blob's region), resolved
+    // once the scan has placed the region; pass 2 re-walks only the blobs that overflow the rows (KRYO_XN_OVF)
+    uint64_t* lm_koff;             // [KRYO_LM_S * n]
+    uint32_t* lm_klen;
+    uint32_t fused;
+    uint32_t* n_ovf;               // [1] blobs pass 2 has to walk (counted by pass 1)
+    uint32_t n_ovf_host;           //   read back with pass 1's totals: 0 = no pass 2 launch
 };
 #define KRYO_LM_C 16
 #define KRYO_LM_S 4
 #define KRYO_XD 8
+#define KRYO_REL (1ull << 63)
+#define KRYO_XN_OVF 0x80000000u
+#define KRYO_XN_REL 0x40000000u
+#define KRYO_XN_CNT 0x3fffffffu
+// pass 1: validate + count; with d (the fused walk) also the rows / salts / descriptors of StxOut
 void launch_stx_count(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_registry& reg, uint8_t* status,
-                      uint64_t* ncomp, uint64_t* nsig, uint64_t* nextra);
+                      uint64_t* ncomp, uint64_t* nsig, uint64_t* nextra, const StxOut* d);
 void launch_stx_emit(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_registry& reg, uint8_t* status,
                      const StxOut& d);
 size_t stx_scan_temp_bytes(uint64_t n);

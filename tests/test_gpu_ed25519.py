@@ -95,3 +95,33 @@ def test_ed25519_comb_stats(ctx_modes):
     s = c.stats()
     assert s.kernel_launches[native.K_ED_COMB] >= 1
     assert s.kernel_launches[native.K_ED_FINISH] >= 1
+
+
+def test_cfg2_shape_quarter_million_matches_oracle(ctx, oracle):
+    """The headline schedule at a quarter of cfg2: 250,000 signatures over 4,096 keys on the device entry (eager
+    per-key comb tables, challenge hash and [S]B started with the batch while the key prep and the tables run on
+    the second stream) — every status byte equal to the oracle's and the labels, every corruption class present."""
+    import torch
+    b = G.ed25519_batch(250_000, n_keys=4096, corrupt=0.10, seed=0x5EED0602)
+    dev = torch.device("cuda", 0)
+
+    class D:
+        pass
+    d = D()
+    for f in ("key_idx", "msg_idx", "sig_data", "sig_off", "sig_len", "key_data", "key_off", "key_len", "msg_data",
+              "msg_off", "msg_len"):
+        a = getattr(b, f)
+        a = a.view(np.int64) if a.dtype == np.uint64 else a.view(np.int32) if a.dtype == np.uint32 else a
+        setattr(d, f, torch.from_numpy(np.ascontiguousarray(a)).to(dev))
+    d.schemes_hint = 1 << 4
+    st = torch.empty(b.n, dtype=torch.uint8, device=dev)
+    bm = torch.empty((b.n + 63) // 64, dtype=torch.int64, device=dev)
+    ctx.verify_batch_device(d, st, bm)
+    torch.cuda.synchronize()
+    got = st.cpu().numpy()
+    ref = oracle.verify_batch(b, threads=16)
+    bad = np.nonzero(got != ref)[0]
+    assert len(bad) == 0, [(int(i), int(got[i]), int(ref[i]), int(b.kind[i])) for i in bad[:20]]
+    assert np.array_equal(got, b.expected)
+    assert len(set(b.kind.tolist())) == len(G.ED_KINDS)
+    assert np.array_equal(bm.cpu().numpy().view(np.uint64), bitmap_of(got))

@@ -309,6 +309,52 @@ def test_duplicate_inputs_across_chunk_boundaries(required):
         c.close()
 
 
+def row_overflow_blobs(seed, n=300):
+    """Transactions around the fused walk's row limits (KRYO_LM_C = 16 components, KRYO_LM_S = 4 signatures,
+    KRYO_XD = 8 chunk-spanning runs per blob): 1-9 signatures, 2-30 components, 0-12 outputs of 1100-2600 bytes
+    (each spans a 1024-byte chunk), signatures and keys of later entries crossing chunk boundaries too."""
+    rng = np.random.default_rng(seed)
+    keys = S.key_pool(rng)
+    out = []
+    for i in range(n):
+        nin = int(rng.integers(0, 14))
+        groups = []
+        if nin:
+            groups.append((0, [S.stateref(rng) for _ in range(nin)]))
+        nbig = int(rng.integers(0, 13)) if i % 3 else int(rng.integers(9, 13))
+        outs = [rng.bytes(int(rng.integers(1100, 2600))) for _ in range(nbig)] + \
+               [rng.bytes(int(rng.integers(1, 200))) for _ in range(int(rng.integers(0 if nbig else 1, 8)))]
+        groups.append((1, outs))
+        sigs = []
+        for _ in range(int(rng.integers(1, 10)) if i % 4 else int(rng.integers(5, 10))):
+            key = keys[int(rng.integers(0, len(keys)))]
+            sigs.append(K.Sig(rng.bytes(64 if len(key) == S.ED_KEY else 71), key, 1, 4, S.REG.key_class_for(key)))
+        groups.append((2, [K.command([s.key for s in sigs[:3]])]))
+        if nin or rng.random() < 0.5:
+            groups.append((4, [K.party(sigs[0].key)]))
+        out.append(S.blob(groups, rng.bytes(32), sigs))
+    return out
+
+
+@pytest.mark.parametrize("fused", ["1", "0"])
+def test_row_overflow_blobs(monkeypatch, fused):
+    """Blobs past the fused pass 1's rows (more components, signatures or chunk-spanning runs than it records) are
+    re-walked by pass 2; the records of both kinds of blob equal the oracle's, with the fused walk (default) and the
+    two-walk front end (CHIP_KRYO_FUSED=0), with and without the required-key stage."""
+    import corda_amd
+    monkeypatch.setenv("CHIP_KRYO_FUSED", fused)
+    c = corda_amd.Context(0)
+    try:
+        blobs = row_overflow_blobs(0x0F1 + int(fused))
+        for required in (False, True):
+            dev, _ = assert_device_equals_oracle(c, blobs, required)
+            ok = [d for d in dev if d[0] == K.STX_OK]
+            assert len(ok) > 250
+            assert sum(1 for d in ok if len(d[3]) > 4) > 50 and sum(1 for d in ok if sum(len(g[1]) for g in d[1]) > 16) > 20
+    finally:
+        c.close()
+
+
 def test_registry_is_applied(ctx):
     """chip_set_kryo_registry: blobs written with another deployment's ids parse under that registry and fail
     closed (UNSUPPORTED) under the defaults, on the device as in the oracle."""
