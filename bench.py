@@ -449,8 +449,9 @@ def main():
             "cfg2_host_path_cgroup": {"cpu_quota": quota,
                                       "throttled_periods": None if thr_n0 is None else thr_n1 - thr_n0,
                                       "throttled_ms": None if thr_ms0 is None else round(thr_ms1 - thr_ms0, 3)},
-            "cfg2_host_path_staging": "library pinned ring" if os.environ.get("CHIP_STAGING_RING", "1") != "0"
-                                      else "HIP runtime pageable path",
+            "cfg2_host_path_staging": "library pinned ring (CHIP_STAGING_RING=1)"
+                                      if os.environ.get("CHIP_STAGING_RING", "0") not in ("", "0")
+                                      else "HIP runtime pageable path (the default; the ring is opt-in)",
         })
         # the same from page-locked host buffers (chip_alloc_pinned: the JNI layer's direct ByteBuffers)
         pb = copy.copy(batch)

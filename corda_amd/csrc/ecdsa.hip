@@ -1074,7 +1074,10 @@ CHIP_DEV void comb_g_body(uint32_t blk, const uint32_t* __restrict__ count, cons
 }
 // both curves in one grid (blocks [0, half) P-256, the rest secp256k1): the secp256k1 blocks fill
 // the chip while the last P-256 waves drain instead of waiting for a second launch
-__global__ void __launch_bounds__(256) k_ecdsa_comb_g(const uint32_t* __restrict__ counts,
+#ifndef EC_G_WAVES
+#define EC_G_WAVES 1   // as EC_Q0_WAVES, for k_ecdsa_comb_g (210 VGPRs = 2 waves; 3 waves spill 70)
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EC_G_WAVES))) k_ecdsa_comb_g(const uint32_t* __restrict__ counts,
                                                       const uint32_t* __restrict__ gcomb, uint32_t* __restrict__ mid_r1,
                                                       uint32_t* __restrict__ mid_k1, const uint32_t* __restrict__ wp_r1,
                                                       const uint32_t* __restrict__ wp_k1, uint64_t cap, uint32_t half,
@@ -1140,9 +1143,16 @@ CHIP_DEV void comb_q_body(uint32_t blk, const uint32_t* __restrict__ list, const
     }
     status[i] = ecdsa_check<C>(acc, r) ? CHIP_VALID : CHIP_INVALID;
 }
-// both curves in one grid, as k_ecdsa_comb_g
+// both curves in one grid, as k_ecdsa_comb_g.  EC_Q0_WAVES: waves per SIMD HALF 0's registers must leave room for.
+// Left to itself the compiler gives HALF 0 194 VGPRs (2 waves) against HALF 1's 156 (3 waves), and HALF 0 issued at
+// 5.05 cycles per VALU instruction against 4.04 (profiles/r05/cfg3_pmc_sq.csv); capped at 3 waves (168 VGPRs, 36
+// spilled) it runs 1.72-1.79 -> 1.44 ms, cfg3 83.8-84.2 -> 88.1-88.7M (profiles/r05/ab_r05j.txt)
+#ifndef EC_Q0_WAVES
+#define EC_Q0_WAVES 3
+#endif
 template <int HALF>
-__global__ void __launch_bounds__(256) k_ecdsa_comb_q(const uint32_t* __restrict__ list_r1,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALF == 0 ? EC_Q0_WAVES : 1)))
+k_ecdsa_comb_q(const uint32_t* __restrict__ list_r1,
                                                       const uint32_t* __restrict__ list_k1,
                                                       const uint32_t* __restrict__ counts,
                                                       const uint32_t* __restrict__ key_idx,

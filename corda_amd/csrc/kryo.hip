@@ -817,31 +817,70 @@ __device__ __forceinline__ uint64_t run1f(Cur& c, uint32_t n, Sink& sink, uint64
 
 // the required-key walk's count and its first STX_REC signer entries for tx t (components in the pool); st may
 // become UNSUPPORTED (a key the walk cannot read, more than 64 signer entries: the JVM path)
-__device__ __forceinline__ void stx_req_tail(Cur& c, uint64_t t, int& st, uint64_t cbase, uint64_t comps, const Outs& o) {
+// (pool: the bytes the components lie in — the context's pool, or the input blobs in the fused pass 1)
+__device__ __forceinline__ void stx_req_walk(Cur& c, uint64_t t, int& st, uint64_t cbase, uint64_t comps,
+                                             const CompAcc& ca, const uint8_t* pool, uint64_t pool_bytes,
+                                             const chip_kryo_registry& reg, uint64_t* nraw, uint64_t* rec_off,
+                                             uint32_t* rec_len) {
     uint64_t cnt = 0, all = 0;
     bool over = false;
     if (st == CHIP_STX_OK &&
-        !req_walk(c, o.pool, o.pool_bytes, cbase, cbase + comps,
-                  CompAcc{o.comp_group, o.comp_off, o.comp_len, o.lm_grp, o.lm_off, o.lm_len, o.n_lm, t, cbase,
-                          o.extra_start, o.extra_base}, o.reg,
+        !req_walk(c, pool, pool_bytes, cbase, cbase + comps, ca, reg,
                   [&](uint64_t at, uint32_t len, bool req) {
                       if (req) {
                           over |= cnt >= 64;
                           cnt++;
                       }
                       if (all < STX_REC) {   // recorded: k_stx_required then needs no third walk
-                          o.rec_off[t * STX_REC + all] = at;
-                          o.rec_len[t * STX_REC + all] = len | (req ? 0x80000000u : 0u);
+                          rec_off[t * STX_REC + all] = at;
+                          rec_len[t * STX_REC + all] = len | (req ? 0x80000000u : 0u);
                       }
                       all++;
                   }))
         st = CHIP_STX_UNSUPPORTED;
     if (over) st = CHIP_STX_UNSUPPORTED;
-    o.nraw[t] = st == CHIP_STX_OK ? all : 0;
+    nraw[t] = st == CHIP_STX_OK ? all : 0;
+}
+__device__ __forceinline__ void stx_req_tail(Cur& c, uint64_t t, int& st, uint64_t cbase, uint64_t comps, const Outs& o) {
+    stx_req_walk(c, t, st, cbase, comps,
+                 CompAcc{o.comp_group, o.comp_off, o.comp_len, o.lm_grp, o.lm_off, o.lm_len, o.n_lm, t, cbase,
+                         o.extra_start, o.extra_base}, o.pool, o.pool_bytes, o.reg, o.nraw, o.rec_off, o.rec_len);
 }
 
-template <bool EMIT>
-__global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint8_t* __restrict__ data,
+// the fused pass 1's share of k_stx_post for tx t, when its rows hold every component and its inputs / commands /
+// notary each lie in one chunk: checkNoDuplicateInputs, then (nraw) the required-key walk; the new status.
+// (noinline: inlined into k_stx_parse this code trips a SimplifyCFG crash of the ROCm 7.2 compiler)
+__device__ __noinline__ int fused_post(uint64_t t, int st, uint64_t comps, uint64_t in_first, uint64_t in_count,
+                                       const uint8_t* pool, uint64_t pool_bytes, const uint32_t* lm_grp,
+                                       const uint64_t* lm_off, const uint32_t* lm_len, uint64_t n_lm,
+                                       uint64_t* nraw, uint64_t* rec_off, uint32_t* rec_len, chip_kryo_registry reg) {
+    const CompAcc ca{nullptr, nullptr, nullptr, lm_grp, lm_off, lm_len, n_lm, t, 0, nullptr, 0};
+    for (uint64_t i = 0; i + 1 < in_count && st == CHIP_STX_OK; i++) {
+        const uint64_t ao = ca.off(in_first + i);
+        const uint32_t al = ca.len(in_first + i);
+        for (uint64_t j = i + 1; j < in_count; j++)
+            if (key_eq(pool, ao, al, ca.off(in_first + j), ca.len(in_first + j))) {
+                st = CHIP_STX_INVARIANT;
+                break;
+            }
+    }
+    if (nraw) {
+        Cur c;
+        c.init(pool, pool_bytes, 0, 0);
+        stx_req_walk(c, t, st, 0, comps, ca, pool, pool_bytes, reg, nraw, rec_off, rec_len);
+    }
+    return st;
+}
+
+// FUSED (pass 1 only): 0 = count, 1 = + the rows (fused walk), 2 = + k_stx_post's work for most transactions.
+// KRYO_P1_WAVES: waves per SIMD the fused pass 1's registers must leave room for: 4 (128 VGPRs, 4 spilled; the
+// compiler's choice is 134 = 3 waves) parses 1M blobs in 3.94 instead of 3.99 ms (profiles/r05/ab_r05j.txt)
+#ifndef KRYO_P1_WAVES
+#define KRYO_P1_WAVES 4
+#endif
+template <bool EMIT, int FUSED = 0>
+__global__ void __launch_bounds__(KRYO_BLOCK) __attribute__((amdgpu_waves_per_eu((!EMIT && FUSED) ? KRYO_P1_WAVES : 1)))
+k_stx_parse(uint64_t n, const uint8_t* __restrict__ data,
                                                    const uint64_t* __restrict__ off, const uint32_t* __restrict__ len,
                                                    uint64_t data_bytes, uint8_t* __restrict__ status,
                                                    uint64_t* __restrict__ ncomp, uint64_t* __restrict__ nsig,
@@ -855,8 +894,9 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
         if (o.xd_a) o.xd_n[t] = 0;
         return;
     }
-    const bool F = !EMIT && o.fused;   // pass 1 of the fused walk: rows, salts and descriptors written here
-    bool ovf = false;
+    const bool F = !EMIT && FUSED > 0;   // pass 1 of the fused walk: rows, salts and descriptors written here
+    bool ovf = false, post = false;
+    uint64_t in_first = 0, in_count = 0;
     const uint64_t a = off[t], b = a + len[t];
     uint64_t comps = 0, sigs = 0, extra = 0;
     Sink sink{o.pool, EMIT ? o.extra_base + o.extra_start[t] : 0, 0, 0, (EMIT || F) && o.xd_a ? o.xd_a + t : nullptr,
@@ -978,7 +1018,6 @@ __global__ void __launch_bounds__(KRYO_BLOCK) k_stx_parse(uint64_t n, const uint
         const uint32_t ng = w.list<0>(false, o.reg.arrays_aslist);
         uint64_t present = 0;
         bool empty_group = false, dup_group = false, multi = false, noncanon = false;
-        uint64_t in_first = 0, in_count = 0;
         for (uint32_t g = 0; g < ng && !w.err; g++) {
             if (w.read_class<0>(M_OF(C_GROUP)) != -C_GROUP) {
                 w.fail(E_UNSUP);
@@ -1107,19 +1146,37 @@ done:
         if (o.xd_a) {
             // the copies are deferred to k_stx_dechunk, and the required-key walk, which reads the components from
             // the pool, to k_stx_req_tail after it
-            o.xd_n[t] = st == CHIP_STX_OK ? sink.nx : 0;
+            o.xd_n[t] = st == CHIP_STX_OK ? (sink.nx | (o.fused ? KRYO_XN_POST : 0u)) : 0u;
+            if (o.fused && o.nraw && st != CHIP_STX_OK) o.nraw[t] = 0;
         } else if (o.nraw) {   // the required-key walk's count, fused here (the components are in the pool now)
             stx_req_tail(c, t, st, cbase, comps, o);
         }
         if (st != CHIP_STX_OK) status[t] = (uint8_t)st;
     } else {
+        // the fused walk does k_stx_post's work here, while the blob's lines are hot, when the rows hold every
+        // component and every input / command / notary component lies in one chunk (its row holds a pool offset);
+        // else k_stx_post does it after k_stx_dechunk (KRYO_XN_POST)
+        if (F && st == CHIP_STX_OK) post = true;
+        if (!EMIT && FUSED == 2 && st == CHIP_STX_OK && !KRYO_NO_STORES) {
+            post = false;
+            for (uint64_t k = 0; k < comps && !ovf; k++) {
+                const uint32_t g = o.lm_grp[k * o.n_lm + t];
+                if ((g == 0 || g == 2 || g == 4) && (o.lm_off[k * o.n_lm + t] & KRYO_REL)) post = true;
+            }
+            if (ovf) post = true;
+            if (!post && (in_count > 1 || o.nraw))
+                st = fused_post(t, st, comps, in_first, in_count, data, data_bytes, o.lm_grp, o.lm_off, o.lm_len,
+                                o.n_lm, o.nraw, o.rec_off, o.rec_len, o.reg);
+        }
         status[t] = (uint8_t)st;
         ncomp[t] = st == CHIP_STX_OK ? comps : 0;
         nsig[t] = st == CHIP_STX_OK ? sigs : 0;
         nextra[t] = st == CHIP_STX_OK ? extra : 0;   // de-chunked (chunk-spanning) payload, 4-byte units
         if (F) {
-            o.xd_n[t] = st == CHIP_STX_OK ? (sink.nx | KRYO_XN_REL | (ovf ? KRYO_XN_OVF : 0u)) : 0u;
+            o.xd_n[t] = st == CHIP_STX_OK ? (sink.nx | KRYO_XN_REL | (ovf ? KRYO_XN_OVF : 0u) | (post ? KRYO_XN_POST : 0u))
+                                          : 0u;
             if (st == CHIP_STX_OK && ovf) atomicAdd(o.n_ovf, 1u);
+            if (o.nraw && st != CHIP_STX_OK) o.nraw[t] = 0;
         }
     }
 }
@@ -1620,7 +1677,16 @@ void launch_stx_count(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_
                       uint64_t* ncomp, uint64_t* nsig, uint64_t* nextra, const StxOut* d) {
     if (!in->n) return;
     Outs o{};
-    if (d && d->fused && KRYO_DEFER_COPY) o = outs_of(in, reg, *d);   // the fused walk: rows, salts, descriptors
+    if (d && d->fused && KRYO_DEFER_COPY) {   // the fused walk: rows, salts, descriptors
+        o = outs_of(in, reg, *d);
+        if (d->fused == 2)
+            hipLaunchKernelGGL((k_stx_parse<false, 2>), grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->off,
+                               in->len, in->data_bytes, status, ncomp, nsig, nextra, o);
+        else
+            hipLaunchKernelGGL((k_stx_parse<false, 1>), grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->off,
+                               in->len, in->data_bytes, status, ncomp, nsig, nextra, o);
+        return;
+    }
     o.reg = reg;
     hipLaunchKernelGGL(k_stx_parse<false>, grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->off, in->len,
                        in->data_bytes, status, ncomp, nsig, nextra, o);
@@ -1789,6 +1855,7 @@ __global__ void __launch_bounds__(256) k_stx_post(uint64_t n, const uint8_t* __r
                                                   uint8_t* __restrict__ status, Outs o) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
+    if (o.fused && !(o.xd_n[t] & KRYO_XN_POST)) return;   // done by the fused pass 1
     if (status[t] != CHIP_STX_OK) {
         if (o.nraw) o.nraw[t] = 0;
         return;

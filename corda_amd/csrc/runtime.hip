@@ -19,9 +19,11 @@
 // Pageable host input through the context's own pinned ring: a copy from memory HIP did not allocate or register
 // (a numpy array, a JVM heap array) is split into 4 MB pieces, each memcpy'd into a free slot of a page-locked ring
 // by a pool of host threads and DMA'd from there on the copy's stream, the next piece's memcpy beside the previous
-// piece's DMA.  HIP's own pageable path (an internal bounce, one thread) measured 155-164M cfg2 sigs/s on most boxes
-// and 57.7M on the round-4 driver's (BENCH_r04 cfg2_host_path_sigs_per_s); page-locked input always takes the direct
-// DMA.  CHIP_STAGING_RING=0 sends pageable input through HIP's path again.
+// piece's DMA.  Off by default (CHIP_STAGING_RING=1 enables it): on the same boxes HIP's own pageable path gave
+// cfg2 medians of 149.7-164.2M sigs/s against the ring's 124-150M (8 / 16 copy threads; profiles/r05/ab_r05f.txt,
+// ab_r05g.txt) — the ring's host memcpy (~40 GB/s with 8 threads) sits on the copy's critical path, HIP's path
+// does not copy on the host.  Both paths show occasional 2x slower calls (7-12 ms) with no cgroup throttling;
+// page-locked input always takes the direct DMA.
 struct HostRing {
     static constexpr int SLOTS = 8;
     static constexpr uint64_t SLOT = 4u << 20;
@@ -30,7 +32,7 @@ struct HostRing {
     bool pending[SLOTS] = {};
     int next = 0;
     std::unique_ptr<ForkJoin> pool;
-    bool enabled = true, failed = false;
+    bool enabled = false, failed = false;
     uint64_t bytes_staged = 0;
     bool init() {
         if (buf || failed) return buf != nullptr;
@@ -162,7 +164,10 @@ struct chip_ctx {
     hipEvent_t ev_ec_chain_lo = nullptr, ev_ec_chain_hi = nullptr, ev_ec_lo = nullptr;
     // the ECDSA key decode at the head of an early Ed25519 batch (CHIP_ECKEYS_LATE=1: after [S]B, the round-4 order)
     bool eckeys_late = false;
-    bool kryo_fused = true;   // Kryo pass 1 writes the rows itself (CHIP_KRYO_FUSED=0: the two-walk front end)
+    // Kryo front end (CHIP_KRYO_FUSED): 1 = pass 1 writes the rows (default), 2 = + k_stx_post's work for most
+    // transactions (measured slower: pass 1 at 200 VGPRs instead of 134, 4.22 vs 3.96-4.00 ms at 1M blobs,
+    // profiles/r05/ab_r05h.txt), 0 = the two-walk front end (4.56-4.65 ms)
+    uint32_t kryo_fused = 1;
     std::recursive_mutex mu;   // recursive: chip_stx_verify holds it across the entries it calls
     std::string err;
     // verify workspaces
@@ -560,7 +565,7 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
     if (const char* e = getenv("CHIP_ECKEYS_LATE")) c->eckeys_late = e[0] == '1';
     if (const char* e = getenv("CHIP_STAGING_RING")) c->ring.enabled = e[0] != '0';
     if (const char* e = getenv("CHIP_KERNEL_TIMING")) c->ktiming = e[0] != '0';
-    if (const char* e = getenv("CHIP_KRYO_FUSED")) c->kryo_fused = e[0] != '0';
+    if (const char* e = getenv("CHIP_KRYO_FUSED")) c->kryo_fused = (uint32_t)std::min(2, std::max(0, atoi(e)));
     if (cfg && cfg->reserve_sigs) {
         (void)c->lists.ensure(cfg->reserve_sigs * 4 * N_LISTS);
     }
@@ -679,13 +684,18 @@ struct VerifyChunk {
     bool keys_only;          // size the workspaces for b->n, prep the keys, fork the table builds, and stop
 };
 
+// present (host entries only): the schemes whose keys occur in the key pool, read from the key lengths on the host
+// (host_scheme_hint) — exact, unlike the caller's advisory hint — so the key preps and verify kernels of the absent
+// schemes are not launched at all (0 = unknown: every scheme's kernels run, empty lists exit at once)
 static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* status, uint64_t* bitmap, hipStream_t st,
-                                bool is_valid, const VerifyChunk* vc = nullptr) {
+                                bool is_valid, const VerifyChunk* vc = nullptr, uint32_t present = 0) {
     const uint64_t n = b->n, nk = b->n_keys;
     const uint64_t nd = vc ? vc->n_decide : n;   // the batch size the path decisions are taken for
     const bool reuse = vc && vc->reuse_keys;
     if (n > 0xffffffffull) return fail(c, CHIP_E_ARG, "batch too large (n >= 2^32)");
     const uint32_t schemes = b->schemes ? b->schemes : CHIP_SCHEMES_ALL;
+    const bool no_ec = present && !(present & CHIP_SCHEMES_EC);
+    const bool no_ed = present && !(present & (1u << CHIP_SCHEME_ED25519));
     HIPCHK(c, hipSetDevice(c->device));
     HIPCHK(c, c->meta.ensure(nk * sizeof(KeyMeta) + 16));
     HIPCHK(c, c->abytes.ensure(nk * 32 + 16));
@@ -793,7 +803,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     w.early = (comb && w.eager && n && !reuse && !vc && !getenv("CHIP_ED_NO_EARLY")) ? 1u : 0u;
     // ECDSA key decode + (windowed) key tables, or the fork of the ECDSA per-key comb tables
     auto ecdsa_keys = [&]() -> int {
-        if (reuse) return CHIP_OK;
+        if (reuse || no_ec) return CHIP_OK;
         launch_ecdsa_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->ectab.as<uint32_t>(), skip);
         if (!ec_comb) {
             launch_ecdsa_key_table(st, nk, meta, c->ectab.as<uint32_t>(), skip);
@@ -846,7 +856,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         c->kend(kb, st);
     }
     int ke = c->kbegin(CHIP_K_KEYPREP, st);
-    if (!reuse && !w.early)
+    if (!reuse && !w.early && !no_ed)
         launch_ed25519_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->abytes.as<uint32_t>(),
                                 (comb && w.eager) ? nullptr : c->edtab.as<uint32_t>(), comb ? w.nega : nullptr, skip);
     if (comb && w.eager && n && !reuse && !w.early) {
@@ -933,7 +943,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         }
         // eager comb: every valid Ed25519 key has a table and all its signatures took the comb, so the Straus list
         // is empty (and no Straus key table was built): no launch
-        if (!(comb && w.eager)) {
+        if (!(comb && w.eager) && !no_ed) {
             ke = c->kbegin(CHIP_K_ED25519, st);
             launch_ed25519_verify(st, n, ed_list, ed_count, b, c->abytes.as<uint32_t>(), c->edtab.as<uint32_t>(),
                                   status);
@@ -950,7 +960,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
             launch_ecdsa_comb_q(st, n, gl_r1, gl_k1, counts, b, c->e_ctab.as<uint32_t>(), mid_r1, mid_k1, status, 1);
             launch_ecdsa_comb_retry(st, n, gl_r1, gl_k1, counts, b, c->ectab.as<uint32_t>(), mid_r1, mid_k1, status);
             c->kend(ke, st);
-        } else {
+        } else if (!no_ec) {
             ke = c->kbegin(CHIP_K_ECDSA_R1, st);
             launch_ecdsa_verify(st, CHIP_SCHEME_R1, n, lists + (uint64_t)LIST_R1 * n, counts + LIST_R1, b,
                                 c->ectab.as<uint32_t>(), status);
@@ -1220,7 +1230,8 @@ static int verify_host_pipelined(chip_ctx* c, const chip_sig_batch* b, uint8_t* 
     d.msg_data = c->h_msg_data.as<uint8_t>();
     d.msg_off = c->h_msg_off.as<uint64_t>();
     d.msg_len = c->h_msg_len.as<uint32_t>();
-    if (!d.schemes) d.schemes = host_scheme_hint(b);
+    const uint32_t present = host_scheme_hint(b);
+    if (!d.schemes) d.schemes = present;
     {   // key prep and the table chains as soon as the keys are staged (before any chunk's pools), with every
         // workspace sized for the largest chunk: no reallocation (an implicit device sync) between chunks
         uint64_t mmax = 0;
@@ -1231,7 +1242,8 @@ static int verify_host_pipelined(chip_ctx* c, const chip_sig_batch* b, uint8_t* 
         d.sig_off = c->h_sig_off.as<uint64_t>();
         d.sig_len = c->h_sig_len.as<uint32_t>();
         const VerifyChunk kv{n, false, nullptr, true};
-        if ((r = verify_device_locked(c, &d, c->h_status.as<uint8_t>(), c->h_bitmap.as<uint64_t>(), st, is_valid, &kv)))
+        if ((r = verify_device_locked(c, &d, c->h_status.as<uint8_t>(), c->h_bitmap.as<uint64_t>(), st, is_valid, &kv,
+                                      present)))
             return r;
     }
     if ((r = stage_chunk(0))) {
@@ -1247,7 +1259,7 @@ static int verify_host_pipelined(chip_ctx* c, const chip_sig_batch* b, uint8_t* 
         d.sig_len = c->h_sig_len.as<uint32_t>() + a;
         const VerifyChunk vc{n, true, c->hev_p, false};
         if ((r = verify_device_locked(c, &d, c->h_status.as<uint8_t>() + a, c->h_bitmap.as<uint64_t>() + a / 64, st,
-                                      is_valid, &vc))) {
+                                      is_valid, &vc, present))) {
             hipStreamSynchronize(st);
             return r;
         }
@@ -1331,8 +1343,10 @@ static int verify_host_entry(chip_ctx* c, const chip_sig_batch* b, uint8_t* stat
     d.msg_data = c->h_msg_data.as<uint8_t>();
     d.msg_off = c->h_msg_off.as<uint64_t>();
     d.msg_len = c->h_msg_len.as<uint32_t>();
-    if (!d.schemes) d.schemes = host_scheme_hint(b);
-    if ((r = verify_device_locked(c, &d, c->h_status.as<uint8_t>(), c->h_bitmap.as<uint64_t>(), st, is_valid)))
+    const uint32_t present = host_scheme_hint(b);
+    if (!d.schemes) d.schemes = present;
+    if ((r = verify_device_locked(c, &d, c->h_status.as<uint8_t>(), c->h_bitmap.as<uint64_t>(), st, is_valid, nullptr,
+                                  present)))
         return r;
     unsigned long long counts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     if (n) {
@@ -1427,7 +1441,7 @@ static int stx_parse(chip_ctx* c, StxBufs& B, const chip_stx_blobs* in, uint8_t*
     }
     // the per-tx rows (lane-major), descriptors and metadata templates: pass 1 writes them in the fused walk
     StxOut d{};
-    d.fused = c->kryo_fused ? 1u : 0u;
+    d.fused = c->kryo_fused;
     HIPCHK(c, B.s_meta.ensure((uint64_t)in->n_meta * 8 + 16));
     if (in->n_meta)
         HIPCHK(c, ring_h2d(c->ring, B.s_meta.p, in->meta, (uint64_t)in->n_meta * 8, st));
@@ -1463,6 +1477,16 @@ static int stx_parse(chip_ctx* c, StxBufs& B, const chip_stx_blobs* in, uint8_t*
         d.n_ovf = B.s_ovf.as<uint32_t>();
         HIPCHK(c, hipMemsetAsync(d.n_ovf, 0, 4, st));
     }
+    // the required-key walk's counts and first entries (the fused pass 1 walks most transactions itself)
+    const bool want_req = in->flags & CHIP_STX_REQUIRED;
+    if (want_req) {
+        HIPCHK(c, B.r_nraw.ensure(n1 * 8));
+        HIPCHK(c, B.r_roff.ensure(n1 * 4 * 8));   // STX_REC (4) recorded signer entries per tx
+        HIPCHK(c, B.r_rlen.ensure(n1 * 4 * 4));
+    }
+    d.nraw = want_req ? B.r_nraw.as<uint64_t>() : nullptr;
+    d.rec_off = want_req ? B.r_roff.as<uint64_t>() : nullptr;
+    d.rec_len = want_req ? B.r_rlen.as<uint32_t>() : nullptr;
     // pass 1: validate + count (+ the rows); ranges = inclusive scans written one past a zero
     launch_stx_count(st, in, reg, tx_status, B.s_ncomp.as<uint64_t>(), B.s_nsig.as<uint64_t>(), B.s_nbytes.as<uint64_t>(),
                      &d);
@@ -1515,15 +1539,6 @@ static int stx_parse(chip_ctx* c, StxBufs& B, const chip_stx_blobs* in, uint8_t*
         HIPCHK(c, B.s_temp.ensure(stx_scan_temp_bytes(nsig > 2 ? nsig : 2)));
     d.pool = pool_p;
     d.pool_bytes = pool;
-    const bool want_req = in->flags & CHIP_STX_REQUIRED;
-    if (want_req) {
-        HIPCHK(c, B.r_nraw.ensure(n1 * 8));
-        HIPCHK(c, B.r_roff.ensure(n1 * 4 * 8));   // STX_REC (4) recorded signer entries per tx
-        HIPCHK(c, B.r_rlen.ensure(n1 * 4 * 4));
-    }
-    d.nraw = want_req ? B.r_nraw.as<uint64_t>() : nullptr;
-    d.rec_off = want_req ? B.r_roff.as<uint64_t>() : nullptr;
-    d.rec_len = want_req ? B.r_rlen.as<uint32_t>() : nullptr;
     d.extra_start = B.s_pstart.as<uint64_t>();
     d.extra_base = extra_base;
     d.comp_start = B.s_cstart.as<uint64_t>();

@@ -117,7 +117,8 @@ struct StxOut {
 #define KRYO_REL (1ull << 63)
 #define KRYO_XN_OVF 0x80000000u
 #define KRYO_XN_REL 0x40000000u
-#define KRYO_XN_CNT 0x3fffffffu
+#define KRYO_XN_POST 0x20000000u   // k_stx_post still has to check the inputs / walk the required keys
+#define KRYO_XN_CNT 0x0fffffffu
 // pass 1: validate + count; with d (the fused walk) also the rows / salts / descriptors of StxOut
 void launch_stx_count(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_registry& reg, uint8_t* status,
                       uint64_t* ncomp, uint64_t* nsig, uint64_t* nextra, const StxOut* d);

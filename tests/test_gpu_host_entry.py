@@ -196,22 +196,22 @@ def test_other_host_entries_check_arguments_on_the_device(ctx):
 
 @pytest.mark.parametrize("chunks", [1, 4])
 def test_pageable_input_through_the_staging_ring(ctx, monkeypatch, chunks):
-    """Pageable host input (numpy arrays) goes through the context's pinned staging ring (4 MB pieces, parallel
-    memcpy, DMA from the ring): statuses and bitmaps equal HIP's own pageable path (CHIP_STAGING_RING=0), the
-    page-locked path and the labels, in one chunk and in four, also with the signatures permuted (every chunk
+    """Pageable host input (numpy arrays) through the context's pinned staging ring (CHIP_STAGING_RING=1: 4 MB
+    pieces, parallel memcpy, DMA from the ring): statuses and bitmaps equal HIP's own pageable path (the default),
+    the page-locked path and the labels, in one chunk and in four, also with the signatures permuted (every chunk
     copies a piece of the pools on both sides of what earlier chunks copied)."""
     import corda_amd
-    monkeypatch.setenv("CHIP_STAGING_RING", "0")
-    plain = corda_amd.Context(0)
+    monkeypatch.setenv("CHIP_STAGING_RING", "1")
+    ring = corda_amd.Context(0)
     monkeypatch.delenv("CHIP_STAGING_RING")
     try:
         b = G.ed25519_batch(150000, n_keys=64, corrupt=0.1, seed=0x5EED0511)
         assert b.sig_data.nbytes > (4 << 20) and b.msg_data.nbytes > (4 << 20)
         monkeypatch.setenv("CHIP_HOST_CHUNKS", str(chunks))
         for x in (b, _permuted(b, 11)):
-            st, bm = ctx.verify_batch(x)
+            st, bm = ring.verify_batch(x)
             assert np.array_equal(st, x.expected)
-            st0, bm0 = plain.verify_batch(x)
+            st0, bm0 = ctx.verify_batch(x)
             assert np.array_equal(st, st0) and np.array_equal(bm, bm0)
         pb = copy.copy(b)
         for f in ("key_idx", "msg_idx", "sig_data", "sig_off", "sig_len", "key_data", "key_off", "key_len",
@@ -221,4 +221,4 @@ def test_pageable_input_through_the_staging_ring(ctx, monkeypatch, chunks):
         assert np.array_equal(stp, b.expected)
         ctx.free_pinned()
     finally:
-        plain.close()
+        ring.close()

@@ -336,7 +336,7 @@ def row_overflow_blobs(seed, n=300):
     return out
 
 
-@pytest.mark.parametrize("fused", ["1", "0"])
+@pytest.mark.parametrize("fused", ["2", "1", "0"])
 def test_row_overflow_blobs(monkeypatch, fused):
     """Blobs past the fused pass 1's rows (more components, signatures or chunk-spanning runs than it records) are
     re-walked by pass 2; the records of both kinds of blob equal the oracle's, with the fused walk (default) and the

@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--p256-only", action="store_true")
     ap.add_argument("--ed25519", action="store_true", help="the cfg2 shape instead (1M Ed25519, schemes hint)")
+    ap.add_argument("--no-hint", action="store_true", help="no schemes hint (bench.py's cfg3 leg sets EC_HINT)")
     a = ap.parse_args()
     import torch
     import corda_amd
@@ -39,8 +40,8 @@ def main():
         eb = G.ecdsa_batch(a.n, n_keys=a.keys, seed=0x5EED0003, threads=16,
                            schemes=(G.SCHEME_R1,) if a.p256_only else (G.SCHEME_R1, G.SCHEME_K1))
     de = B.upload(eb, B.SIG_FIELDS, torch, dev)
-    if a.ed25519:
-        de.schemes_hint = B.ED_HINT
+    if not a.no_hint:
+        de.schemes_hint = B.ED_HINT if a.ed25519 else (1 << 3 if a.p256_only else B.EC_HINT)
     est = torch.empty(eb.n, dtype=torch.uint8, device=dev)
     ebm = torch.empty((eb.n + 63) // 64, dtype=torch.int64, device=dev)
     for _ in range(a.warmup):

@@ -7,7 +7,7 @@ NAME=$1; shift
 OUT=build_ab/$NAME
 mkdir -p $OUT
 objs=()
-for f in runtime ed25519 ed25519_comb ecdsa txid uniq signers kryo; do
+for f in runtime ed25519 ed25519_comb ecdsa txid uniq signers kryo group; do
   /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -c corda_amd/csrc/$f.hip -o $OUT/$f.o -I include "$@" &
   objs+=($OUT/$f.o)
 done
