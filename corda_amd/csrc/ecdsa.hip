@@ -1075,7 +1075,8 @@ CHIP_DEV void comb_g_body(uint32_t blk, const uint32_t* __restrict__ count, cons
 // both curves in one grid (blocks [0, half) P-256, the rest secp256k1): the secp256k1 blocks fill
 // the chip while the last P-256 waves drain instead of waiting for a second launch
 #ifndef EC_G_WAVES
-#define EC_G_WAVES 1   // as EC_Q0_WAVES, for k_ecdsa_comb_g (210 VGPRs = 2 waves; 3 waves spill 70)
+#define EC_G_WAVES 3   // as EC_Q0_WAVES, for k_ecdsa_comb_g: 210 VGPRs = 2 waves; at 3 waves (70 spilled) the front end
+                       // runs 2.71-2.76 -> 2.28 ms, cfg3 88.5-89.5 -> 90.5-91.2M (profiles/r05/ab_r05k.txt)
 #endif
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EC_G_WAVES))) k_ecdsa_comb_g(const uint32_t* __restrict__ counts,
                                                       const uint32_t* __restrict__ gcomb, uint32_t* __restrict__ mid_r1,

@@ -857,7 +857,10 @@ CHIP_DEV void ld_fe_soa(fe& f, const uint32_t* __restrict__ base, uint64_t cap, 
 #pragma unroll
     for (int q = 0; q < 10; q++) f.v[q] = base[(uint64_t)q * cap + p];
 }
-__global__ void __launch_bounds__(256) k_ed_comb_finish(const uint32_t* __restrict__ list, const uint32_t* __restrict__ ctr,
+#ifndef ED_FINISH_WAVES
+#define ED_FINISH_WAVES 1   // waves per SIMD the finish's registers must leave room for (136 VGPRs = 3 waves; 4: 10 spilled)
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_FINISH_WAVES))) k_ed_comb_finish(const uint32_t* __restrict__ list, const uint32_t* __restrict__ ctr,
                                                         const uint8_t* __restrict__ sig_data,
                                                         const uint64_t* __restrict__ sig_off,
                                                         const uint32_t* __restrict__ xyz, uint32_t* __restrict__ zpre,
