@@ -858,7 +858,9 @@ CHIP_DEV void ld_fe_soa(fe& f, const uint32_t* __restrict__ base, uint64_t cap, 
     for (int q = 0; q < 10; q++) f.v[q] = base[(uint64_t)q * cap + p];
 }
 #ifndef ED_FINISH_WAVES
-#define ED_FINISH_WAVES 1   // waves per SIMD the finish's registers must leave room for (136 VGPRs = 3 waves; 4: 10 spilled)
+#define ED_FINISH_WAVES 4   // waves per SIMD the finish's registers must leave room for: 4 (128 VGPRs, 10 spilled; the
+                            // compiler's 136 = 3 waves): cfg2 263.4-266.2 vs 260.5-263.2M in 3 same-box rounds
+                            // (profiles/r05/ab_r05l.txt; [S]B at 3 waves was slower, 250-256M)
 #endif
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_FINISH_WAVES))) k_ed_comb_finish(const uint32_t* __restrict__ list, const uint32_t* __restrict__ ctr,
                                                         const uint8_t* __restrict__ sig_data,
