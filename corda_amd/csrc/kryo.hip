@@ -1665,6 +1665,15 @@ inline dim3 grid_of(uint64_t n) { return dim3((uint32_t)((n + 255) / 256)); }
 
 }  // namespace
 
+// lanes per transaction in k_stx_dechunk: 16, or 64 (a wave, the round-4 kernel) with CHIP_KRYO_DECHUNK_W=64
+static int stx_dechunk_w() {
+    static const int w = [] {
+        const char* e = getenv("CHIP_KRYO_DECHUNK_W");
+        return e && atoi(e) == 64 ? 64 : 16;
+    }();
+    return w;
+}
+
 static Outs outs_of(const chip_stx_blobs* in, const chip_kryo_registry& reg, const StxOut& d) {
     return Outs{d.pool, d.pool_bytes, d.extra_start, d.extra_base, d.salts, d.comp_start, d.comp_group, d.comp_internal,
                 d.comp_off, d.comp_len, d.sig_start, d.tx_idx, d.tmpl_idx, d.sig_off, d.sig_len, d.skey_off, d.skey_len,
@@ -1692,9 +1701,38 @@ void launch_stx_count(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_
                        in->data_bytes, status, ncomp, nsig, nextra, o);
 }
 
-// the transaction t of entry c of a range array (start[0] = 0, start[n] > c): the last t with start[t] <= c
-__device__ __forceinline__ uint64_t owner_of(const uint64_t* __restrict__ start, uint64_t n, uint64_t c) {
-    uint64_t lo = 0, hi = n;
+// the transaction t of entry c of a range array (start[0] = 0 <= c < start[n] = total): the last t with
+// start[t] <= c.  Searched outwards from the uniform guess c * n / total (galloping, then bisection inside the
+// bracket): one or two loads for batches of similar transactions instead of a 20-level dependent bisection
+// (k_stx_lm_comps 0.23 ms at 8M entries with the plain bisection, profiles/r05/stx_timeline_fused.txt)
+__device__ __forceinline__ uint64_t owner_of(const uint64_t* __restrict__ start, uint64_t n, uint64_t total,
+                                             uint64_t c) {
+    uint64_t g = total ? (c * n) / total : 0;   // c < 2^31, n < 2^32: no overflow
+    if (g >= n) g = n - 1;
+    uint64_t lo, hi;   // start[lo] <= c < start[hi] (hi = n: start[n] = total > c)
+    if (start[g] <= c) {
+        lo = g;
+        for (uint64_t step = 1;; step <<= 1) {
+            hi = lo + step;
+            if (hi >= n) {
+                hi = n;
+                break;
+            }
+            if (start[hi] > c) break;
+            lo = hi;
+        }
+    } else {
+        hi = g;
+        for (uint64_t step = 1;; step <<= 1) {
+            if (hi < step) {
+                lo = 0;
+                break;
+            }
+            lo = hi - step;
+            if (start[lo] <= c) break;
+            hi = lo;
+        }
+    }
     while (hi - lo > 1) {
         const uint64_t mid = (lo + hi) >> 1;
         if (start[mid] <= c) lo = mid;
@@ -1707,7 +1745,7 @@ __global__ void __launch_bounds__(256) k_stx_lm_comps(uint64_t n, uint64_t ncomp
                                                       Outs o) {
     const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (c >= ncomp) return;
-    const uint64_t t = owner_of(start, n, c), j = c - start[t];
+    const uint64_t t = owner_of(start, n, ncomp, c), j = c - start[t];
     if (j >= KRYO_LM_C) return;   // stored in place by pass 2
     const uint64_t i = j * o.n_lm + t;
     o.comp_off[c] = rel_off(o.lm_off[i], o.extra_start, o.extra_base, t);
@@ -1719,7 +1757,7 @@ __global__ void __launch_bounds__(256) k_stx_lm_sigs(uint64_t n, uint64_t nsig, 
                                                      Outs o) {
     const uint64_t s = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (s >= nsig) return;
-    const uint64_t t = owner_of(start, n, s), j = s - start[t];
+    const uint64_t t = owner_of(start, n, nsig, s), j = s - start[t];
     if (j >= KRYO_LM_S) return;
     const uint64_t i = j * o.n_lm + t;
     o.sig_off[s] = rel_off(o.lm_soff[i], o.extra_start, o.extra_base, t);
@@ -1732,9 +1770,10 @@ __global__ void __launch_bounds__(256) k_stx_lm_sigs(uint64_t n, uint64_t nsig, 
     }
 }
 
-// one piece of a de-chunked run, by the whole wave: head bytes up to a dword-aligned destination, then 16
-// destination bytes per lane (a 4-byte-aligned dwordx4 + one dword from the source, realigned with
-// v_alignbyte; 1 KB per wave instruction), then the tail bytes
+// one piece of a de-chunked run, by the W lanes of a transaction's lane group: head bytes up to a dword-aligned
+// destination, then 16 destination bytes per lane (a 4-byte-aligned dwordx4 + one dword from the source, realigned
+// with v_alignbyte; 16 W bytes per instruction), then the tail bytes
+template <int W>
 __device__ __forceinline__ void dechunk_piece(uint8_t* __restrict__ pool, uint64_t d, uint64_t s, uint32_t k,
                                               uint32_t lane) {
     uint32_t h = (4u - (uint32_t)(d & 3)) & 3u;
@@ -1744,7 +1783,7 @@ __device__ __forceinline__ void dechunk_piece(uint8_t* __restrict__ pool, uint64
     s += h;
     k -= h;
     const uint32_t body = k & ~3u;
-    for (uint32_t off = lane * 16; off < body; off += 1024) {
+    for (uint32_t off = lane * 16; off < body; off += 16 * W) {
         const uint64_t sa = s + off, al = sa & ~3ull;
         const uint32_t sh = (uint32_t)(sa & 3);
         const u32x4a4 w = *reinterpret_cast<const u32x4a4*>(pool + al);
@@ -1769,12 +1808,6 @@ __device__ __forceinline__ void dechunk_piece(uint8_t* __restrict__ pool, uint64
     const uint32_t tl = k & 3u;
     if (lane < tl) pool[d + body + lane] = pool[s + body + lane];
 }
-// (the builtin returns int: each half goes through uint32_t, or an offset >= 2 GiB would sign-extend)
-__device__ __forceinline__ uint64_t rl64(uint64_t v, uint32_t j) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((uint32_t)v, j);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((uint32_t)(v >> 32), j);
-    return (uint64_t)lo | ((uint64_t)hi << 32);
-}
 // a chunk header (varint) at s, the same bytes read by every lane; 0 = bad
 __device__ __forceinline__ uint32_t dechunk_header(const uint8_t* pool, uint64_t pool_bytes, uint64_t& s) {
     uint32_t v = 0;
@@ -1787,20 +1820,33 @@ __device__ __forceinline__ uint32_t dechunk_header(const uint8_t* pool, uint64_t
     return v;
 }
 
-// pass 2's chunk-spanning runs, a wave per transaction.  Lane j loads run j's descriptor and the chunk header
-// behind its first piece (every recorded run spans a chunk boundary: at least two pieces), so those
-// dependent loads overlap across the runs; then the wave copies run after run, piece after piece
-// (dechunk_piece), a third and later piece (a run over more than a whole chunk) walking its headers, and
+// a value of lane j of this lane group (W = 64: the wave's scalar readlane)
+template <int W> __device__ __forceinline__ uint32_t grp_bcast(uint32_t v, uint32_t j) {
+    if (W == 64) return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)j);
+    return (uint32_t)__shfl((int)v, (int)j, W);
+}
+// (each half through uint32_t: the builtins return int, and an offset >= 2 GiB must not sign-extend)
+template <int W> __device__ __forceinline__ uint64_t grp_bcast64(uint64_t v, uint32_t j) {
+    return (uint64_t)grp_bcast<W>((uint32_t)v, j) | ((uint64_t)grp_bcast<W>((uint32_t)(v >> 32), j) << 32);
+}
+
+// the descriptors' chunk-spanning runs, W lanes per transaction (KRYO_DECHUNK_W; a run of a few hundred bytes
+// keeps 16 lanes busy, a whole wave per transaction left most of them idle).  Lane j of the group loads run j's
+// descriptor and the chunk header behind its first piece (every recorded run spans a chunk boundary: at least two
+// pieces), so those dependent loads overlap across the runs; then the group copies run after run, piece after
+// piece (dechunk_piece), a third and later piece (a run over more than a whole chunk) walking its headers, and
 // the run's zero padding to a dword.  (The pass validated every recorded chain; the bounds checks only keep
 // a bad descriptor inside the pool.)
+template <int W>
 __global__ void __launch_bounds__(256) k_stx_dechunk(uint64_t n, uint8_t* __restrict__ pool, uint64_t pool_bytes,
                                                      const uint4* __restrict__ xa, const uint2* __restrict__ xb,
                                                      const uint32_t* __restrict__ xn, const uint64_t* __restrict__ xstart,
                                                      uint64_t xbase) {
-    const uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-    const uint32_t lane = threadIdx.x & 63u;
+    static_assert(W >= KRYO_XD && W <= 64 && (W & (W - 1)) == 0, "a lane per descriptor, groups inside a wave");
+    const uint64_t t = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) / W;
+    const uint32_t lane = threadIdx.x & (W - 1);
     if (t >= n) return;
-    const uint32_t xnt = __builtin_amdgcn_readfirstlane(xn[t]);
+    const uint32_t xnt = W == 64 ? __builtin_amdgcn_readfirstlane(xn[t]) : xn[t];
     uint32_t cnt = xnt & KRYO_XN_CNT;
     cnt = cnt < KRYO_XD ? cnt : KRYO_XD;
     // the fused walk's descriptors hold offsets in the blob's extra region (KRYO_REL)
@@ -1819,15 +1865,15 @@ __global__ void __launch_bounds__(256) k_stx_dechunk(uint64_t n, uint8_t* __rest
         if (rem < len && src2 < pool_bytes) rem2 = dechunk_header(pool, pool_bytes, src2);
     }
     for (uint32_t j = 0; j < cnt; j++) {
-        uint64_t d = rl64(dst, j), s = rl64(src, j);
-        const uint64_t s2 = rl64(src2, j);
-        uint32_t left = __builtin_amdgcn_readlane(len, j), r = __builtin_amdgcn_readlane(rem, j);
-        const uint32_t r2 = __builtin_amdgcn_readlane(rem2, j);
+        uint64_t d = grp_bcast64<W>(dst, j), s = grp_bcast64<W>(src, j);
+        const uint64_t s2 = grp_bcast64<W>(src2, j);
+        uint32_t left = grp_bcast<W>(len, j), r = grp_bcast<W>(rem, j);
+        const uint32_t r2 = grp_bcast<W>(rem2, j);
         const uint32_t pad = (4u - (left & 3u)) & 3u;
         if (r == 0 || r >= left || r2 == 0 || d > pool_bytes || pool_bytes - d < (uint64_t)left + pad ||
             s > pool_bytes || pool_bytes - s < r || s2 > pool_bytes)
             return;
-        dechunk_piece(pool, d, s, r, lane);
+        dechunk_piece<W>(pool, d, s, r, lane);
         d += r;
         left -= r;
         s = s2;
@@ -1839,7 +1885,7 @@ __global__ void __launch_bounds__(256) k_stx_dechunk(uint64_t n, uint8_t* __rest
             }
             const uint32_t k = left < r ? left : r;
             if (pool_bytes - s < k) return;
-            dechunk_piece(pool, d, s, k, lane);
+            dechunk_piece<W>(pool, d, s, k, lane);
             d += k;
             s += k;
             r -= k;
@@ -1899,8 +1945,12 @@ void launch_stx_emit(hipStream_t st, const chip_stx_blobs* in, const chip_kryo_r
         hipLaunchKernelGGL(k_stx_parse<true>, grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->off, in->len,
                            in->data_bytes, status, nullptr, nullptr, nullptr, o);
     if (o.xd_a) {
-        hipLaunchKernelGGL(k_stx_dechunk, grid_of(in->n * 64), dim3(256), 0, st, in->n, d.pool, d.pool_bytes, d.xd_a,
-                           d.xd_b, d.xd_n, d.extra_start, d.extra_base);
+        if (stx_dechunk_w() == 64)
+            hipLaunchKernelGGL(k_stx_dechunk<64>, grid_of(in->n * 64), dim3(256), 0, st, in->n, d.pool, d.pool_bytes,
+                               d.xd_a, d.xd_b, d.xd_n, d.extra_start, d.extra_base);
+        else
+            hipLaunchKernelGGL(k_stx_dechunk<16>, grid_of(in->n * 16), dim3(256), 0, st, in->n, d.pool, d.pool_bytes,
+                               d.xd_a, d.xd_b, d.xd_n, d.extra_start, d.extra_base);
         hipLaunchKernelGGL(k_stx_post, grid_of(in->n), dim3(256), 0, st, in->n, in->data, in->data_bytes, status, o);
     }
     if (d.ncomp)
