@@ -249,18 +249,32 @@ def profile_issue(kernel, grid):
     return None
 
 
-def stx_traffic(ntx, nsig):
-    """FETCH_SIZE + WRITE_SIZE of one Kryo front-end call (both parse passes, the key interning and the
-    required-key passes; the pool copy is a DMA, not counted) from the committed PMC profile, or None."""
+def stx_traffic(ntx, nsig, ncomp):
+    """FETCH_SIZE + WRITE_SIZE of one Kryo front-end call from the committed PMC profile, or None: pass 1 (the fused
+    walk since round 5), pass 2 when it ran (only blobs past pass 1's rows: 0 for cfg4), the post-dechunk pass
+    (duplicate inputs + required-key walk), the de-chunk copies, the row transposes, the key interning and the
+    required-key passes (the pool copy is a DMA, not counted)."""
     grid_tx, grid_sig = (ntx + 255) // 256 * 256, (nsig + 255) // 256 * 256
-    parts = [profile_traffic(k, grid_tx) for k in ("k_stx_parse<false>", "k_stx_parse<true>", "k_stx_required")]
-    # the post-dechunk pass (duplicate inputs + required-key walk): k_stx_post since round 5, k_stx_req_tail before
-    post = profile_traffic("k_stx_post", grid_tx)
-    parts.append(post if post is not None else profile_traffic("k_stx_req_tail", grid_tx))
-    parts.append(profile_traffic("k_stx_dechunk", (ntx * 64 + 255) // 256 * 256))   # a wave per transaction
+
+    def first(*cands):   # the first (kernel, grid) the profile holds: kernel names of this round, then older ones
+        for k, g in cands:
+            v = profile_traffic(k, g)
+            if v is not None:
+                return v
+        return None
+    parts = [first(("k_stx_parse<false, 1>", grid_tx), ("k_stx_parse<false>", grid_tx)),
+             first(("k_stx_post", grid_tx), ("k_stx_req_tail", grid_tx)),
+             first(("k_stx_dechunk<16>", (ntx * 16 + 255) // 256 * 256), ("k_stx_dechunk", (ntx * 64 + 255) // 256 * 256)),
+             profile_traffic("k_stx_required", grid_tx)]
     parts += [profile_traffic(k, grid_sig) for k in ("k_stx_key_insert", "k_stx_key_flag", "k_stx_key_assign",
                                                       "k_stx_req_entry<false>", "k_stx_req_entry<true>")]
-    return None if any(p is None for p in parts) else sum(parts)
+    if any(p is None for p in parts):
+        return None
+    # launched only when needed / present in the profile: pass 2, the transposes
+    opt = [profile_traffic("k_stx_parse<true, 0>", grid_tx) or profile_traffic("k_stx_parse<true>", grid_tx),
+           profile_traffic("k_stx_lm_comps", (ncomp + 255) // 256 * 256),
+           profile_traffic("k_stx_lm_sigs", grid_sig)]
+    return sum(parts) + sum(p for p in opt if p)
 
 
 def sha256_compressions(tb):
@@ -710,9 +724,10 @@ def main():
             "stx_parse_roofline": {"bound": "hbm", "achieved": alg / (parse_ms * 1e-3) / 1e9, "peak": HBM_PEAK_GBS,
                                    "unit": "GB/s", "frac": alg / (parse_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                                    "algorithmic_bytes": alg,
-                                   "traffic": stx_traffic(tb.ntx, sb.n),
-                                   "note": "one launch = both parse passes, the pool copy, scans, key interning "
-                                           "and the required-key pass with their 3 host syncs"},
+                                   "traffic": stx_traffic(tb.ntx, sb.n, int(tb.comp_len.size)),
+                                   "note": "one launch = the fused pass 1 (pass 2 only for blobs past its rows), "
+                                           "scans, de-chunk copies, row transposes, key interning and the "
+                                           "required-key passes with their 3 host syncs"},
         })
         del bb, bbs, bo, bl, bst, holder, p, dm, ids, fst, fv, fa, fm, tb, tm, sb, evs, s_parse, hb
     progress("cfg4 legs done")

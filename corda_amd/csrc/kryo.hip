@@ -1387,7 +1387,10 @@ enum { RF_KEEP = 1, RF_VALIDATE = 2, RF_COMPOSITE = 4, RF_DECODE = 8 };
 // not required — and whether a plain key has to be decoded (it signs none of this transaction's signatures:
 // the verify path decodes the others).  A key that is neither an Ed25519 / ECDSA key nor a CompositeKey
 // -> CHIP_STX_UNSUPPORTED.  (The emit pass counted the entries.)
-__global__ void __launch_bounds__(KRYO_BLOCK) k_stx_required(uint64_t n, uint8_t* __restrict__ status,
+#ifndef KRYO_REQ_WAVES
+#define KRYO_REQ_WAVES 1   // waves per SIMD k_stx_required's registers must leave room for (1: the compiler's 119 VGPRs)
+#endif
+__global__ void __launch_bounds__(KRYO_BLOCK) __attribute__((amdgpu_waves_per_eu(KRYO_REQ_WAVES))) k_stx_required(uint64_t n, uint8_t* __restrict__ status,
                                                       const uint64_t* __restrict__ comp_start,
                                                       const uint32_t* __restrict__ comp_group,
                                                       const uint64_t* __restrict__ comp_off,
@@ -1897,7 +1900,10 @@ __global__ void __launch_bounds__(256) k_stx_dechunk(uint64_t n, uint8_t* __rest
 // after k_stx_dechunk has filled the extra region, per parsed transaction: checkNoDuplicateInputs
 // (WireTransaction.kt:53-60 via checkBaseInvariants) over the input group's serialized StateRefs — chunk-spanning
 // inputs included, which pass 2 only described — then, with CHIP_STX_REQUIRED (o.nraw), the required-key walk
-__global__ void __launch_bounds__(256) k_stx_post(uint64_t n, const uint8_t* __restrict__ data, uint64_t data_bytes,
+#ifndef KRYO_POST_WAVES
+#define KRYO_POST_WAVES 1   // as KRYO_REQ_WAVES, for k_stx_post (the compiler's 112 VGPRs)
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KRYO_POST_WAVES))) k_stx_post(uint64_t n, const uint8_t* __restrict__ data, uint64_t data_bytes,
                                                   uint8_t* __restrict__ status, Outs o) {
     const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= n) return;
