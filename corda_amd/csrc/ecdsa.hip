@@ -267,9 +267,11 @@ CHIP_DEV void der_int(u256& v, bool& oor, const uint8_t* c, uint32_t n) {
     uint32_t i = 0;
     while (i < n && c[i] == 0) i++;
     if (i == n || n - i > 32) { oor = true; return; }
-    for (uint32_t k = i; k < n; k++) {
-        const uint32_t pos = n - 1 - k;   // byte position from the least significant end
-        v.w[pos >> 2] |= (uint32_t)c[k] << (8 * (pos & 3));
+    // by destination byte (unrolled: every word index static, so v stays in registers), the loads independent
+#pragma unroll
+    for (uint32_t pos = 0; pos < 32; pos++) {   // byte position from the least significant end
+        const uint32_t b = pos < n - i ? (uint32_t)c[n - 1 - pos] : 0u;
+        v.w[pos >> 2] |= b << (8 * (pos & 3));
     }
 }
 CHIP_DEV bool der_decode(const uint8_t* sig, uint32_t len, u256& r, bool& roor, u256& s, bool& soor) {
@@ -277,26 +279,26 @@ CHIP_DEV bool der_decode(const uint8_t* sig, uint32_t len, u256& r, bool& roor, 
     if (len < 2 || sig[0] != 0x30) return false;
     if (!der_len(sig + 1, len - 1, hdr, L)) return false;
     if (1 + hdr + L != len) return false;
-    const uint8_t* p = sig + 1 + hdr;
-    uint32_t rem = L;
-    const uint8_t* val[2];
-    uint32_t vl[2];
+    // the two INTEGERs as byte offsets into sig (no array of pointers: with the LDS-staged source the walk reads
+    // through generic pointers, and an array of them went to scratch)
+    uint32_t at = 1 + hdr, rem = L;
+    uint32_t v0 = 0, l0 = 0, v1 = 0, l1 = 0;
+#pragma unroll
     for (int k = 0; k < 2; k++) {
-        if (rem < 2 || p[0] != 0x02) return false;
+        if (rem < 2 || sig[at] != 0x02) return false;
         uint32_t h2, l2;
-        if (!der_len(p + 1, rem - 1, h2, l2)) return false;
+        if (!der_len(sig + at + 1, rem - 1, h2, l2)) return false;
         if (1 + h2 + l2 > rem) return false;
         if (l2 == 0) return false;
-        const uint8_t* c = p + 1 + h2;   // ASN1Integer malformed-integer rule
-        if (l2 > 1 && ((c[0] == 0x00 && !(c[1] & 0x80)) || (c[0] == 0xff && (c[1] & 0x80)))) return false;
-        val[k] = c;
-        vl[k] = l2;
-        p += 1 + h2 + l2;
+        const uint32_t c = at + 1 + h2;   // ASN1Integer malformed-integer rule
+        if (l2 > 1 && ((sig[c] == 0x00 && !(sig[c + 1] & 0x80)) || (sig[c] == 0xff && (sig[c + 1] & 0x80)))) return false;
+        if (k == 0) { v0 = c; l0 = l2; } else { v1 = c; l1 = l2; }
+        at += 1 + h2 + l2;
         rem -= 1 + h2 + l2;
     }
     if (rem != 0) return false;
-    der_int(r, roor, val[0], vl[0]);
-    der_int(s, soor, val[1], vl[1]);
+    der_int(r, roor, sig + v0, l0);
+    der_int(s, soor, sig + v1, l1);
     return true;
 }
 
@@ -316,6 +318,26 @@ CHIP_DEV uint32_t ecdsa_front(u256& r, u256& s, u256& e, const uint8_t* sig, uin
     u256 t;
     if (!u256_sub(t, e, cv.n)) e = t;   // e < 2^256 < 2n
     return 0xffu;
+}
+
+// ecdsa_front with the signature staged in this lane's LDS slot first: up to EC_SIG_STAGE_DW independent dword
+// loads, issued together, instead of the DER walk's chain of dependent byte loads from global memory (each
+// waiting for the one before).  DER signatures of both curves are at most 72 bytes; longer ones take the plain path.
+#define EC_SIG_STAGE_DW 21   // 84 bytes: 72 + up to 3 bytes of misalignment (odd stride: no LDS bank conflicts)
+template <int C>
+CHIP_DEV uint32_t ecdsa_front_staged(u256& r, u256& s, u256& e, const uint8_t* sig, uint32_t siglen, const uint8_t* msg,
+                                     uint32_t msglen, uint32_t* lslot) {
+    const uint32_t sh = (uint32_t)((uintptr_t)sig & 3u);
+    const bool staged = sh + siglen <= 4u * EC_SIG_STAGE_DW;
+    if (staged) {
+        const uint32_t* ap = reinterpret_cast<const uint32_t*>(sig - sh);   // aligned dwords overlapping the signature
+        const uint32_t ndw = (sh + siglen + 3u) >> 2;
+#pragma unroll
+        for (int k = 0; k < EC_SIG_STAGE_DW; k++)
+            if ((uint32_t)k < ndw) lslot[k] = ap[k];
+    }
+    // one inlined walk over either source (generic loads)
+    return ecdsa_front<C>(r, s, e, staged ? reinterpret_cast<const uint8_t*>(lslot) + sh : sig, siglen, msg, msglen);
 }
 
 // x(R) mod n == r  <=>  X == r Z^2  or  (r + n < p and X == (r + n) Z^2); R = infinity -> false
@@ -943,10 +965,12 @@ __global__ void __launch_bounds__(256) k_ecdsa_comb_pre(const uint32_t* __restri
     const bool live = gid < n;
     u256 r, s, e, sm;
     bool go = false;
+    __shared__ uint32_t s_sig[256 * EC_SIG_STAGE_DW];
     if (live) {
         const uint32_t i = list[gid];
         const uint32_t mi = msg_idx[i];
-        const uint32_t st0 = ecdsa_front<C>(r, s, e, sig_data + sig_off[i], sig_len[i], msg_data + msg_off[mi], msg_len[mi]);
+        const uint32_t st0 = ecdsa_front_staged<C>(r, s, e, sig_data + sig_off[i], sig_len[i], msg_data + msg_off[mi],
+                                                   msg_len[mi], s_sig + threadIdx.x * EC_SIG_STAGE_DW);
         if (st0 != 0xffu) status[i] = (uint8_t)st0;
         go = st0 == 0xffu;
     }

@@ -168,15 +168,47 @@ CHIP_DEV uint32_t comp_word(const uint8_t* p, uint32_t len, int64_t q) {
     return v;
 }
 
-// SHA-256 of pool bytes p[0..len): state words in H (big-endian digest words)
+typedef uint32_t u32x4_a4 __attribute__((ext_vector_type(4), aligned(4)));   // dwordx4 at dword alignment
+
+// the 64-byte block at p (inside the string) as 16 big-endian words: four 4-byte-aligned dwordx4 loads and one
+// dword (the bytes are realigned with v_alignbyte), all independent; every load overlaps the block, so none can
+// touch a page the string does not
+CHIP_DEV void block_words(uint32_t w[16], const uint8_t* p) {
+    const uint32_t sh = (uint32_t)((uintptr_t)p & 3u);
+    const uint32_t* ap = reinterpret_cast<const uint32_t*>(p - sh);
+    uint32_t d[17];
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+        const u32x4_a4 v = *reinterpret_cast<const u32x4_a4*>(ap + 4 * k);
+        d[4 * k] = v.x;
+        d[4 * k + 1] = v.y;
+        d[4 * k + 2] = v.z;
+        d[4 * k + 3] = v.w;
+    }
+    d[16] = sh ? ap[16] : 0u;
+#pragma unroll
+    for (int j = 0; j < 16; j++) w[j] = __builtin_bswap32(__builtin_amdgcn_alignbyte(d[j + 1], d[j], sh));
+}
+
+// SHA-256 of pool bytes p[0..len): state words in H (big-endian digest words).  Whole blocks are fetched one
+// block ahead of the compression (block_words), so a block's loads are in flight while the previous one is
+// compressed; the tail block(s) with the padding go through comp_word
 CHIP_DEV void sha256_bytes(uint32_t H[8], const uint8_t* p, uint32_t len) {
-    uint32_t w[16];
+    uint32_t w[16], nx[16];
     sha256_init(H);
     const uint64_t total = len;
     const uint32_t nblocks = (uint32_t)((total + 9 + 63) / 64);
+    const uint32_t nfull = len / 64;   // blocks wholly inside the string
+    if (nfull) block_words(nx, p);
     for (uint32_t b = 0; b < nblocks; b++) {
+        if (b < nfull) {
 #pragma unroll
-        for (int j = 0; j < 16; j++) w[j] = comp_word(p, len, (int64_t)b * 64 + 4 * j);
+            for (int j = 0; j < 16; j++) w[j] = nx[j];
+            if (b + 1 < nfull) block_words(nx, p + (uint64_t)(b + 1) * 64);
+        } else {
+#pragma unroll
+            for (int j = 0; j < 16; j++) w[j] = comp_word(p, len, (int64_t)b * 64 + 4 * j);
+        }
         if (b == nblocks - 1) {
             w[14] = (uint32_t)((total * 8) >> 32);
             w[15] = (uint32_t)(total * 8);
