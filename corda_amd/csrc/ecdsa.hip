@@ -854,7 +854,10 @@ __global__ void __launch_bounds__(64) k_ecdsa_comb_chain2(uint64_t n_keys, const
 }
 // lane per key x group of `gw` windows of [wa, wb) (the fill is latency-bound: fewer windows per
 // lane = more lanes, at one shared inversion pair per lane)
-__global__ void __launch_bounds__(256) k_ecdsa_comb_fill(uint64_t n_keys, const KeyMeta* __restrict__ meta,
+#ifndef EC_FILL_WAVES
+#define EC_FILL_WAVES 1   // waves per SIMD the table fill's registers must leave room for (170 VGPRs = 2 waves; 3: 2 spilled)
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EC_FILL_WAVES))) k_ecdsa_comb_fill(uint64_t n_keys, const KeyMeta* __restrict__ meta,
                                                          uint32_t* __restrict__ ctab, uint32_t* __restrict__ jac,
                                                          uint32_t wa, uint32_t wb, uint32_t gw,
                                                          const uint32_t* __restrict__ skip) {
