@@ -645,7 +645,9 @@ def main():
         parse_ms = kms(s4, native.K_STX)
         # pipelined: batch k + 1 is parsed on a second stream while batch k is verified (the front end's
         # two buffer sets alternate; the parse of batch k + 2 waits for the verification of batch k)
-        s_parse = torch.cuda.Stream(dev)
+        # the parse stream's priority (CORDA_PARSE_PRIORITY, torch convention: lower = higher priority): the verify
+        # kernels fill every wave slot, so at equal priority the parse's workgroups wait for them to drain
+        s_parse = torch.cuda.Stream(dev, priority=int(os.environ.get("CORDA_PARSE_PRIORITY", "0")))
         evs = [None, None]
 
         def from_bytes_pipelined():
