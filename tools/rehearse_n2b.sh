@@ -8,5 +8,6 @@ timeout -k 10 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 
 rc=$?
 tail -c 1500 gpurun_out/n2b/b.err
 python3 -c "
-import json; d=json.load(open('gpurun_out/n2b/b.json')); print('n_gpus', d['n_gpus'], 'value', round(d['value']/1e6,2), d['correct_vs_labels'], 'host', round(d['secondary'].get('cfg2_host_path_sigs_per_s',0)/1e6,1))" || true
+import json; t=open('gpurun_out/n2b/b.json').read().splitlines(); d=json.loads([l for l in t if l.startswith('{')][-1])
+print('n_gpus', d['n_gpus'], 'value', round(d['value']/1e6,2), d['correct_vs_labels'], 'host', round(d['secondary'].get('cfg2_host_path_sigs_per_s',0)/1e6,1))" || true
 exit $rc
