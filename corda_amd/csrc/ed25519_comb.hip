@@ -21,6 +21,7 @@
 // 227 KB table (W = 6) is read through one XCD's L2.  Keys with fewer than min_sigs signatures (or beyond the
 // table budget) keep the Straus kernel.
 #include "ed_common_dev.hpp"
+#include <cstdlib>
 #include "runtime.hpp"
 #include "comb_tables.hpp"
 
@@ -990,7 +991,11 @@ void launch_ed_comb_finish(hipStream_t st, uint64_t n, const chip_sig_batch* b, 
     // a host batch), whose lanes would otherwise be too few to fill the chip (each lane's chain is serial):
     // about 64k lanes, 4 <= g <= ED_FIN_G
     uint32_t g = ED_FIN_G;
-    while (g > 4 && n / g < 49152) g >>= 1;
+    static const uint32_t min_lanes = [] {   // CHIP_FINISH_MIN_LANES: A/B of the lanes-vs-chain trade
+        const char* e = getenv("CHIP_FINISH_MIN_LANES");
+        return e ? (uint32_t)strtoul(e, nullptr, 10) : 49152u;
+    }();
+    while (g > 4 && n / g < min_lanes) g >>= 1;
     hipLaunchKernelGGL(k_ed_comb_finish, dim3(nblk((n + g - 1) / g, 256)), dim3(256), 0, st, w.comb_list,
                        w.ctr, b->sig_data, b->sig_off, w.xyz, w.zpre, (uint64_t)n, status, g);
 }
