@@ -989,11 +989,13 @@ void launch_ed_comb_finish(hipStream_t st, uint64_t n, const chip_sig_batch* b, 
     if (!n || !w.max_slots) return;
     // signatures per inversion: ED_FIN_G (16) for 2^20-signature batches; fewer for smaller ones (the chunks of
     // a host batch), whose lanes would otherwise be too few to fill the chip (each lane's chain is serial):
-    // about 64k lanes, 4 <= g <= ED_FIN_G
+    // at least min_lanes lanes (g halves below that), 4 <= g <= ED_FIN_G
     uint32_t g = ED_FIN_G;
-    static const uint32_t min_lanes = [] {   // CHIP_FINISH_MIN_LANES: A/B of the lanes-vs-chain trade
+    // 32768 (CHIP_FINISH_MIN_LANES overrides): the host pipeline's ~292k-signature chunks take g = 8 (g = 4 at 49152):
+    // pinned cfg2 172.0-172.5 -> 174.6-176.5M, pageable 169.8-170.9 -> 171.9-172.4M (profiles/r05/ab_r05s.txt)
+    static const uint32_t min_lanes = [] {
         const char* e = getenv("CHIP_FINISH_MIN_LANES");
-        return e ? (uint32_t)strtoul(e, nullptr, 10) : 49152u;
+        return e ? (uint32_t)strtoul(e, nullptr, 10) : 32768u;
     }();
     while (g > 4 && n / g < min_lanes) g >>= 1;
     hipLaunchKernelGGL(k_ed_comb_finish, dim3(nblk((n + g - 1) / g, 256)), dim3(256), 0, st, w.comb_list,
