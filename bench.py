@@ -645,9 +645,11 @@ def main():
         parse_ms = kms(s4, native.K_STX)
         # pipelined: batch k + 1 is parsed on a second stream while batch k is verified (the front end's
         # two buffer sets alternate; the parse of batch k + 2 waits for the verification of batch k)
-        # the parse stream's priority (CORDA_PARSE_PRIORITY, torch convention: lower = higher priority): the verify
-        # kernels fill every wave slot, so at equal priority the parse's workgroups wait for them to drain
-        s_parse = torch.cuda.Stream(dev, priority=int(os.environ.get("CORDA_PARSE_PRIORITY", "0")))
+        # the parse stream at a higher priority (CORDA_PARSE_PRIORITY, torch convention: lower = higher; 0 = equal):
+        # the verify kernels fill every wave slot, so at equal priority the parse's workgroups wait for them to drain,
+        # while the latency-bound parse slots in beside the issue-bound verify at a higher one (73.3-74.1M at equal
+        # priority vs 78.7-78.8M, profiles/r05/ab_r05q.txt)
+        s_parse = torch.cuda.Stream(dev, priority=int(os.environ.get("CORDA_PARSE_PRIORITY", "-1")))
         evs = [None, None]
 
         def from_bytes_pipelined():
@@ -709,9 +711,9 @@ def main():
             "cfg4_from_bytes_verified_tx_per_s": world * tb.ntx * ts / bel,
             "cfg4_from_bytes_ms_per_batch": bel / ts * 1e3,
             "cfg4_from_bytes_serial_verified_tx_per_s": world * tb.ntx * ts / bel_serial,
-            "cfg4_from_bytes_note": "value = parse of batch k+1 on a second HIP stream overlapping the verification "
-                                    "of batch k (steady state over the timed steps); serial = parse then verify "
-                                    "on one stream",
+            "cfg4_from_bytes_note": "value = parse of batch k+1 on a second, higher-priority HIP stream overlapping "
+                                    "the verification of batch k (steady state over the timed steps); serial = "
+                                    "parse then verify on one stream",
             "cfg4_from_bytes_correct": bytes_ok,
             **host_bytes,
             "cfg4_from_bytes_verdicts": {"ok": int(bvc[0]), "signature_exception": int(bvc[1]),
