@@ -506,6 +506,16 @@ static int aux_priority() {
     return hi;
 }
 
+// the host pipeline's copy / check stream at the high priority: at equal priority its small per-chunk check kernels
+// wait for CUs behind the verify kernels and the next chunk's copies wait for them (pinned cfg2 170.5-173.2 ->
+// 175.0-178.0M, profiles/r05/ab_r05t.txt; CHIP_HCS_PRIORITY=0: the default priority)
+static int hcs_priority() {
+    int lo = 0, hi = 0;
+    if (hipDeviceGetStreamPriorityRange(&lo, &hi) != hipSuccess) return 0;
+    const char* e = getenv("CHIP_HCS_PRIORITY");
+    return e && e[0] == '0' ? lo : hi;
+}
+
 int chip_init(const chip_config* cfg, chip_ctx** out) {
     if (!out) return CHIP_E_ARG;
     *out = nullptr;
@@ -528,7 +538,7 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
         hipEventCreateWithFlags(&c->ev_ec_chain_lo, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_ec_chain_hi, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->ev_ec_lo, hipEventDisableTiming) != hipSuccess ||
-        hipStreamCreateWithFlags(&c->hcs, hipStreamNonBlocking) != hipSuccess ||
+        hipStreamCreateWithPriority(&c->hcs, hipStreamNonBlocking, hcs_priority()) != hipSuccess ||
         hipEventCreateWithFlags(&c->hev_c, hipEventDisableTiming) != hipSuccess ||
         hipEventCreateWithFlags(&c->hev_p, hipEventDisableTiming) != hipSuccess ||
         hipHostMalloc((void**)&c->h_rng, 64 * 8, hipHostMallocDefault) != hipSuccess) {
