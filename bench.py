@@ -131,6 +131,7 @@ def parse():
     ap.add_argument("--no-ecdsa", action="store_true", help="skip the cfg3 legs")
     ap.add_argument("--ecdsa-n", type=int, default=4_000_000, help="cfg3 global batch (sharded over the ranks)")
     ap.add_argument("--no-notary", action="store_true", help="skip the cfg5 leg")
+    ap.add_argument("--no-group", action="store_true", help="skip the device-group legs (chip_group_*, N = 1 only)")
     ap.add_argument("--notary-tx", type=int, default=4_000_000, help="cfg5 transactions (~2.5 inputs each)")
     ap.add_argument("--notary-pre", type=int, default=10_000_000, help="cfg5 pre-committed StateRefs")
     ap.add_argument("--no-notary-check", action="store_true", help="skip the full-size oracle check of cfg5")
@@ -484,6 +485,9 @@ def main():
             "cfg2_host_path_pinned_correct": bool(np.array_equal(pst, batch.expected)),
             "cfg2_host_path_pinned_iter_ms": [round(x, 3) for x in pit_ms],
         })
+        if world == 1 and not args.no_group:
+            secondary["group_cfg2_host_pinned"] = group_cfg2_leg(native, local, batch, pb, pel)
+            progress("cfg2 device-group leg done")
         del pb
         ctx.free_pinned()
 
@@ -1012,6 +1016,88 @@ def ecdsa_leg(args, ctx, world, rank, torch, dev, dist, D, G, native, threads, s
     return out
 
 
+def group_cfg2_leg(native, local, batch, pb, single_s):
+    """cfg2 through the device-group entry (chip_group_verify_batch, the path a Corda JVM reaches N GPUs by) from
+    page-locked host buffers, on device lists [d] and [d, d] (two member contexts sharing this one GPU: the split,
+    rebasing, member threads and the per-member table builds, not a speed-up).  Each call's split and host times
+    come from chip_group_last_stats."""
+    out = {"single_context_ms": single_s * 1e3}
+    for devs in ([local], [local, local]):
+        g = native.Group(devs)
+        try:
+            g.verify_batch(pb)
+            its, stats = [], []
+            for _ in range(HOST_ITERS):
+                t1 = time.perf_counter()
+                st, _bm = g.verify_batch(pb)
+                its.append((time.perf_counter() - t1) * 1e3)
+                stats.append(g.last_stats())
+            med = float(np.median(its))
+            out["x".join(str(d) for d in devs)] = {
+                "members": len(devs), "sigs_per_s": batch.n / med * 1e3, "ms": med,
+                "iter_ms": [round(x, 3) for x in its], "correct": bool(np.array_equal(st, batch.expected)),
+                "stats": stats[int(np.argsort(its)[len(its) // 2])]}
+        finally:
+            g.close()
+    one = out["x".join([str(local)])]
+    one["vs_single_context"] = (single_s * 1e3) / one["ms"]
+    out["note"] = ("chip_group_verify_batch on pinned host buffers; %s = one member (the single-context entry through "
+                   "the group), %s = two member contexts on this one GPU, each verifying half the transactions and "
+                   "building its own per-key tables" % (str(local), "x".join([str(local)] * 2)))
+    return out
+
+
+def notary_group_legs(native, ctx, local, pre, ub, st_ref, recs_ref):
+    """cfg5 from page-locked host buffers: the single-context host entry (chip_uniq_commit_batch) beside the
+    device-group commit (chip_group_uniq_commit_batch) on [d] and [d, d].  Each commit is timed alone after an
+    untimed rebuild of the 10M-row log; statuses and every conflict record must equal the device-resident commit's,
+    which bench.py compares with the oracle at full size.  The group's own split (per-member H2D bytes, the members'
+    input exchange, rounds and their on-device vote exchange) comes from chip_group_uniq_last_stats."""
+    ntx, nref = ub.ntx, int(ub.tx_ref_start[-1])
+    pin = [ctx.pinned_copy(a) for a in (ub.tx_ref_start, ub.refs, ub.tx_ids, ub.callers)]
+    whole = int(sum(a.nbytes for a in pin))
+    cap = len(pre[2]) + nref + 1024
+    out = {"batch_bytes_in": whole}
+
+    def leg(name, opener, stats_of):
+        times, stats, res = [], [], None
+        for _ in range(3):
+            t = opener()
+            try:
+                t.rebuild(*pre)
+                t1 = time.perf_counter()
+                res = t.commit_batch_raw(*pin)
+                times.append((time.perf_counter() - t1) * 1e3)
+                stats.append(stats_of(t))
+            finally:
+                t.close()
+        st, raw, n = res
+        ok = bool(np.array_equal(st, st_ref)) and n * 56 == len(recs_ref) and bool(np.array_equal(raw, recs_ref))
+        best = int(np.argmin(times[1:])) + 1
+        out[name] = {"ms": times[best], "staterefs_per_s": nref / (times[best] * 1e-3), "iter_ms": [round(x, 3) for x in times],
+                     "equal_to_device_commit": ok, "stats": stats[best]}
+
+    leg("single_context", lambda: ctx.uniq_open(cap), lambda t: {"rounds": t.last_rounds()})
+    for devs in ([local], [local, local]):
+        g = native.Group(devs)
+        try:
+            leg("group_" + "x".join(str(d) for d in devs), lambda: g.uniq_open(cap), lambda t: t.last_stats())
+        finally:
+            g.close()
+    one = out["group_" + str(local)]
+    one["vs_single_context"] = out["single_context"]["ms"] / one["ms"]
+    two = out["group_" + "x".join([str(local)] * 2)]
+    s2 = two["stats"]
+    two["h2d_bytes_max_frac_of_batch"] = s2["h2d_bytes_max"] / whole
+    two["ms_per_round_incl_vote_exchange"] = s2["rounds_ms"] / max(1, s2["rounds"])
+    out["note"] = ("chip_group_uniq_commit_batch from pinned host buffers (%d tx, %d input StateRefs, %d B in): "
+                   "the group of one is the single-context entry; on two members (both on this one GPU) each stages "
+                   "only its slice from the host, the members exchange owned inputs and ids device to device, and the "
+                   "rounds exchange votes on the devices" % (ntx, nref, whole))
+    ctx.free_pinned()
+    return out
+
+
 def notary_leg(args, ctx, world, rank, torch, dev, dist, D, G, native, threads, stream):
     """cfg5: every rank builds the same global batch (same seed).  Uniqueness: N = 1 commits through
     chip_uniq_commit_batch_device; N > 1 runs the key-sharded protocol (each rank owns a slice of the
@@ -1051,6 +1137,7 @@ def notary_leg(args, ctx, world, rank, torch, dev, dist, D, G, native, threads, 
             times.append(time.perf_counter() - t1)
         st = d_st.cpu().numpy()
         recs_gpu = d_out[:nout * 56].cpu().numpy()
+        rounds = table.last_rounds()
         del d_start, d_refs, d_ids, d_call, d_st, d_out
     else:
         eng = native.UniqShardEngine(table)
@@ -1071,6 +1158,9 @@ def notary_leg(args, ctx, world, rank, torch, dev, dist, D, G, native, threads, 
         del dshard
     table.close()
     uel = max_over_ranks(min(times[1:]), world, torch, dev, dist)
+    group = None
+    if world == 1 and not args.no_group:
+        group = notary_group_legs(native, ctx, dev.index, pre_all, ub, st, recs_gpu)
     counts = np.bincount(st, minlength=3)
     # full-size correctness: the oracle's ordered commit over the same log and batch (host, untimed)
     check = None
@@ -1121,7 +1211,8 @@ def notary_leg(args, ctx, world, rank, torch, dev, dist, D, G, native, threads, 
                             "frac": achieved_gbs / HBM_PEAK_GBS,
                             "note": "%d B/StateRef algorithmic (SURVEY §8d) x %d input StateRefs / commit time"
                                     % (UNIQ_BYTES_PER_REF, nref)},
-        "notary_rounds": rounds if world > 1 else None,
+        "notary_rounds": rounds,
+        "notary_group_host_pinned": group,
         "notary_status_counts": {"committed": int(counts[0]), "idempotent": int(counts[1]),
                                  "conflict": int(counts[2]), "records": int(nout)},
         "notary_oracle_check": check,

@@ -23,6 +23,7 @@
 // distributed.py).  Conflict records of the members are merged by (tx, input_index).
 #include <hipcub/hipcub.hpp>
 #include <algorithm>
+#include <chrono>
 #include <condition_variable>
 #include <cstdlib>
 #include <cstring>
@@ -80,7 +81,51 @@ struct chip_group {
     std::string err;
     uint64_t min_share = 0;           // smallest range worth a member of its own (0: the per-entry defaults)
     uint32_t next = 0;                // member of the next single-member call (rotates)
+    bool key_cache = false;           // CHIP_FLAG_KEY_CACHE: single-member calls stay on member 0 (below)
+    chip_group_stats stats{};         // the last call (chip_group_last_stats)
+    std::vector<struct GUScratch*> uscratch;   // the uniqueness commit's member scratch (owned; freed at shutdown)
+    // the member of a call that one member holds whole.  With the key cache a member reuses its key state only for
+    // the pool it saw last, so rotating small calls over the members would rebuild the tables on every call (a
+    // caller's pool reaches each member only every k-th call): they stay on member 0 instead.
+    int single_member() { return key_cache ? 0 : (int)(next++ % m.size()); }
 };
+
+static double ms_since(std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+// per-call stats: reset at the start of a call; the members' own times and bytes folded in at the end
+struct CallStats {
+    chip_group* g;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    std::vector<double> ms, rebase;
+    std::vector<uint64_t> h2d;
+    explicit CallStats(chip_group* g_) : g(g_), ms(g_->m.size(), -1.0), rebase(g_->m.size(), 0.0), h2d(g_->m.size(), 0) {
+        g->stats = chip_group_stats{};
+    }
+    void single(uint64_t bytes) {
+        g->stats.members_used = 1;
+        g->stats.h2d_bytes_max = g->stats.h2d_bytes_total = bytes;
+        g->stats.wall_ms = ms_since(t0);
+        g->stats.member_ms_max = g->stats.member_ms_min = g->stats.wall_ms;
+    }
+    void done() {
+        chip_group_stats& S = g->stats;
+        S.member_ms_min = 1e300;
+        for (size_t i = 0; i < ms.size(); i++) {
+            if (ms[i] < 0) continue;
+            S.members_used++;
+            S.member_ms_max = std::max(S.member_ms_max, ms[i]);
+            S.member_ms_min = std::min(S.member_ms_min, ms[i]);
+            S.rebase_ms = std::max(S.rebase_ms, rebase[i]);
+            S.h2d_bytes_max = std::max(S.h2d_bytes_max, h2d[i]);
+            S.h2d_bytes_total += h2d[i];
+        }
+        if (!S.members_used) S.member_ms_min = 0;
+        S.wall_ms = ms_since(t0);
+    }
+};
+
+static void uniq_scratch_release(std::vector<struct GUScratch*>& v);   // below
 
 static int gfail(chip_group* g, int code, const std::string& msg) {
     if (g) g->err = msg;
@@ -172,6 +217,18 @@ int chip_group_init(const int* devices, int n, const chip_config* cfg, chip_grou
     }
     g->scratch.resize(n);
     g->th.reset(new MemberThreads(n));
+    g->key_cache = cfg && (cfg->flags & CHIP_FLAG_KEY_CACHE);
+    // peer access between distinct member GPUs (the uniqueness exchange's xGMI copies; without it they still run,
+    // staged by the runtime)
+    for (int i = 0; i < n; i++)
+        for (int j = 0; j < n; j++) {
+            int can = 0;
+            if (devices[i] == devices[j] || hipDeviceCanAccessPeer(&can, devices[i], devices[j]) != hipSuccess || !can) continue;
+            if (hipSetDevice(devices[i]) == hipSuccess) {
+                const hipError_t e = hipDeviceEnablePeerAccess(devices[j], 0);
+                if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+            }
+        }
     g->min_share = env_share("CHIP_GROUP_MIN_SHARE", 0);
     *out = g;
     return CHIP_OK;
@@ -180,6 +237,7 @@ int chip_group_init(const int* devices, int n, const chip_config* cfg, chip_grou
 void chip_group_shutdown(chip_group* g) {
     if (!g) return;
     g->th.reset();
+    uniq_scratch_release(g->uscratch);
     for (PinnedBuf& b : g->scratch) b.release();
     for (chip_ctx* c : g->m) chip_shutdown(c);
     delete g;
@@ -208,6 +266,12 @@ chip_ctx* chip_group_member(chip_group* g, int i) {
 
 const char* chip_group_last_error(const chip_group* g) { return g ? g->err.c_str() : "null group"; }
 
+int chip_group_last_stats(const chip_group* g, chip_group_stats* out) {
+    if (!g || !out) return CHIP_E_ARG;
+    *out = g->stats;
+    return CHIP_OK;
+}
+
 // ---- signatures ----------------------------------------------------------------------------------------
 // A transaction is a maximal run of equal msg_idx (its signers share the SignableData message); cuts move forward
 // to the next run boundary.  Messages and signatures are rebased into each member's sub-pools.
@@ -218,14 +282,19 @@ static int group_verify(chip_group* g, const chip_sig_batch* b, uint8_t* status,
         return gfail(g, CHIP_E_ARG, "null batch array");
     if (nm && (!b->msg_off || !b->msg_len || !b->msg_data)) return gfail(g, CHIP_E_ARG, "null message array");
     std::lock_guard<std::mutex> lk(g->mu);
+    CallStats cs(g);
     const int k = (int)g->m.size();
+    const uint64_t key_bytes = b->key_bytes + b->n_keys * 12;
     auto single = [&](int i) {
         const int rc = is_valid ? chip_is_valid_batch(g->m[i], b, status, bitmap) : chip_verify_batch(g->m[i], b, status, bitmap);
+        cs.single(n * 20 + b->sig_bytes + b->msg_bytes + nm * 12 + key_bytes);
         return rc ? gfail(g, rc, "member " + std::to_string(i) + ": " + chip_last_error(g->m[i])) : CHIP_OK;
     };
+    const auto tp = std::chrono::steady_clock::now();
     const std::vector<uint64_t> cut =
         plan_sigs(n, b->msg_idx, k, g->min_share ? g->min_share : env_share("CHIP_GROUP_MIN_SIGS", 16384));
-    if (cut[1] == n) return single((int)(g->next++ % k));   // one member holds everything
+    g->stats.plan_ms = ms_since(tp);
+    if (cut[1] == n) return single(g->single_member());   // one member holds everything
     // message / signature sub-pools: every index and range is checked by the member on its device; here only
     // the slices' extents are read, clamped into the caller's pools (an out-of-range entry still fails there)
     std::vector<int> rcs(k, 0);
@@ -233,6 +302,7 @@ static int group_verify(chip_group* g, const chip_sig_batch* b, uint8_t* status,
     auto work = [&](int i) -> int {
         const uint64_t lo = cut[i], hi = cut[i + 1], m = hi - lo;
         if (!m) return CHIP_OK;
+        const auto t0 = std::chrono::steady_clock::now();
         uint32_t mlo = 0xffffffffu, mhi = 0;
         for (uint64_t s = lo; s < hi; s++) {
             mlo = std::min(mlo, b->msg_idx[s]);
@@ -278,11 +348,15 @@ static int group_verify(chip_group* g, const chip_sig_batch* b, uint8_t* status,
         d.msg_off = moff;
         d.msg_len = nmm ? b->msg_len + mlo : b->msg_len;
         d.msg_bytes = me - mb;
+        cs.rebase[i] = ms_since(t0);
+        cs.h2d[i] = m * 20 + d.sig_bytes + d.msg_bytes + nmm * 12 + key_bytes;
         const int rc = is_valid ? chip_is_valid_batch(g->m[i], &d, status ? status + lo : nullptr, bm[i])
                                 : chip_verify_batch(g->m[i], &d, status ? status + lo : nullptr, bm[i]);
+        cs.ms[i] = ms_since(t0);
         return rcs[i] = rc;
     };
     const int rc = g->th->run(work);
+    cs.done();
     if (rc) return member_fail(g, rc, rcs);
     if (bitmap) {   // each member's bitmap shifted to its first signature
         memset(bitmap, 0, ((n + 63) / 64) * 8);
@@ -348,13 +422,15 @@ int chip_group_txid_batch(chip_group* g, const chip_tx_batch* b, uint8_t* ids) {
     if (!b->salts || !b->tx_comp_start || !ids) return gfail(g, CHIP_E_ARG, "null tx array");
     if (b->ncomp && (!b->comp_off || !b->comp_len)) return gfail(g, CHIP_E_ARG, "null component array");
     std::lock_guard<std::mutex> lk(g->mu);
+    CallStats cs(g);
     const int k = (int)g->m.size();
     auto single = [&](int i) {
         const int rc = chip_txid_batch(g->m[i], b, ids);
+        cs.single(ntx * 40 + b->ncomp * 14 + b->data_bytes);
         return rc ? gfail(g, rc, "member " + std::to_string(i) + ": " + chip_last_error(g->m[i])) : CHIP_OK;
     };
     const std::vector<uint64_t> cut = split_ranges(ntx, nullptr, k, g->min_share ? g->min_share : env_share("CHIP_GROUP_MIN_TX", 8192));
-    if (cut[1] == ntx || !cuts_ok(b->tx_comp_start, cut, b->ncomp)) return single((int)(g->next++ % k));
+    if (cut[1] == ntx || !cuts_ok(b->tx_comp_start, cut, b->ncomp)) return single(g->single_member());
     std::vector<int> rcs(k, 0);
     auto work = [&](int i) -> int {
         const uint64_t t0 = cut[i], t1 = cut[i + 1];
@@ -362,12 +438,18 @@ int chip_group_txid_batch(chip_group* g, const chip_tx_batch* b, uint8_t* ids) {
         const uint64_t nc = b->tx_comp_start[t1] - b->tx_comp_start[t0];
         PinnedBuf& pb = g->scratch[i];
         if (!pb.ensure(Carve::bytes(t1 - t0 + 1, 8) + Carve::bytes(nc, 8) + 64)) return rcs[i] = CHIP_GROUP_SCRATCH;
+        const auto tm0 = std::chrono::steady_clock::now();
         Carve cv{static_cast<uint8_t*>(pb.p)};
         TxSlice s;
         tx_slice(b, t0, t1, cv, s);
-        return rcs[i] = chip_txid_batch(g->m[i], &s.d, ids + 32 * t0);
+        cs.rebase[i] = ms_since(tm0);
+        cs.h2d[i] = (t1 - t0) * 40 + nc * 14 + s.d.data_bytes;
+        rcs[i] = chip_txid_batch(g->m[i], &s.d, ids + 32 * t0);
+        cs.ms[i] = ms_since(tm0);
+        return rcs[i];
     };
     const int rc = g->th->run(work);
+    cs.done();
     return rc ? member_fail(g, rc, rcs) : CHIP_OK;
 }
 
@@ -390,13 +472,17 @@ int chip_group_verify_signed_tx_batch(chip_group* g, const chip_tx_batch* b, con
     if (b->ncomp && (!b->comp_off || !b->comp_len)) return gfail(g, CHIP_E_ARG, "null component array");
     if (q->nreq && !q->node_start) return gfail(g, CHIP_E_ARG, "null node_start");
     std::lock_guard<std::mutex> lk(g->mu);
+    CallStats cs(g);
     const int k = (int)g->m.size();
     auto single = [&](int i) {
         const int rc = chip_verify_signed_tx_batch(g->m[i], b, tm, sb, q, ids, status, verdict, arg, missing);
+        cs.single(ntx * 40 + b->ncomp * 14 + b->data_bytes + n * 24 + sb->sig_bytes + sb->key_bytes);
         return rc ? gfail(g, rc, "member " + std::to_string(i) + ": " + chip_last_error(g->m[i])) : CHIP_OK;
     };
-    const int mi = (int)(g->next++ % k);
-    if (q->sig_start[0] != 0 || q->sig_start[ntx] > n || q->sig_start[ntx] < q->sig_start[0]) return single(mi);
+    const int mi = g->single_member();
+    // split only when the transactions' signature ranges cover every signature: a signature outside them gets its
+    // status from the one-context entry alone
+    if (q->sig_start[0] != 0 || q->sig_start[ntx] != n) return single(mi);
     const std::vector<uint64_t> cut =
         split_ranges(ntx, q->sig_start, k, g->min_share ? g->min_share : env_share("CHIP_GROUP_MIN_SIGS", 16384));
     if (cut[1] == ntx || !cuts_ok(b->tx_comp_start, cut, b->ncomp) || !cuts_ok(q->sig_start, cut, n) ||
@@ -426,6 +512,7 @@ int chip_group_verify_signed_tx_batch(chip_group* g, const chip_tx_batch* b, con
                     break;
                 }
         if (mis[i]) return CHIP_OK;
+        const auto tm0 = std::chrono::steady_clock::now();
         PinnedBuf& pb = g->scratch[i];
         if (!pb.ensure(Carve::bytes(m + 1, 8) + Carve::bytes(nc, 8) + Carve::bytes(ns, 4) + Carve::bytes(ns, 8) +
                        2 * Carve::bytes(m + 1, 8) + Carve::bytes(nr + 1, 8) + 64))
@@ -473,10 +560,15 @@ int chip_group_verify_signed_tx_batch(chip_group* g, const chip_tx_batch* b, con
         dq.node_val = q->node_val ? q->node_val + n0 : q->node_val;
         dq.node_nkids = q->node_nkids ? q->node_nkids + n0 : q->node_nkids;
         dq.node_weight = q->node_weight ? q->node_weight + n0 : q->node_weight;
-        return rcs[i] = chip_verify_signed_tx_batch(g->m[i], &ts.d, tm, &ds, &dq, ids ? ids + 32 * t0 : nullptr,
-                                                    status + s0, verdict + t0, arg + t0, missing ? missing + r0 : nullptr);
+        cs.rebase[i] = ms_since(tm0);
+        cs.h2d[i] = m * 40 + nc * 14 + ts.d.data_bytes + ns * 24 + ds.sig_bytes + sb->key_bytes;
+        rcs[i] = chip_verify_signed_tx_batch(g->m[i], &ts.d, tm, &ds, &dq, ids ? ids + 32 * t0 : nullptr, status + s0,
+                                             verdict + t0, arg + t0, missing ? missing + r0 : nullptr);
+        cs.ms[i] = ms_since(tm0);
+        return rcs[i];
     };
     const int rc = g->th->run(work);
+    cs.done();
     for (int i = 0; i < k; i++)
         if (mis[i]) return single(mi);
     if (rc) return member_fail(g, rc, rcs);
@@ -494,12 +586,14 @@ int chip_group_stx_verify(chip_group* g, uint64_t n, const uint8_t* data, const 
     if (!n) return CHIP_OK;
     if (!data || !off || !len || !tx_status || !verdict || !arg) return gfail(g, CHIP_E_ARG, "null array");
     std::lock_guard<std::mutex> lk(g->mu);
+    CallStats cs(g);
     const int k = (int)g->m.size();
     const std::vector<uint64_t> cut = split_ranges(n, nullptr, k, g->min_share ? g->min_share : env_share("CHIP_GROUP_MIN_TX", 8192));
     if (cut[1] == n) {
-        const int i = (int)(g->next++ % k);
+        const int i = g->single_member();
         const int rc = chip_stx_verify(g->m[i], n, data, off, len, data_bytes, tmpl, meta, n_meta, tx_status, verdict,
                                        arg, ids);
+        cs.single(n * 12 + data_bytes);
         return rc ? gfail(g, rc, "member " + std::to_string(i) + ": " + chip_last_error(g->m[i])) : CHIP_OK;
     }
     std::vector<int> rcs(k, 0);
@@ -507,6 +601,7 @@ int chip_group_stx_verify(chip_group* g, uint64_t n, const uint8_t* data, const 
     auto work = [&](int i) -> int {
         const uint64_t t0 = cut[i], t1 = cut[i + 1], m = t1 - t0;
         if (!m) return CHIP_OK;
+        const auto tm0 = std::chrono::steady_clock::now();
         uint64_t db = ~0ull, de = 0;
         for (uint64_t t = t0; t < t1; t++) {
             db = std::min(db, off[t]);
@@ -518,10 +613,15 @@ int chip_group_stx_verify(chip_group* g, uint64_t n, const uint8_t* data, const 
         Carve cv{static_cast<uint8_t*>(pb.p)};
         uint64_t* o = cv.take<uint64_t>(m);
         for (uint64_t t = 0; t < m; t++) o[t] = off[t0 + t] - db;
-        return rcs[i] = stx_verify_counted(g->m[i], m, data + db, o, len + t0, de - db, tmpl, meta, n_meta,
-                                           tx_status + t0, verdict + t0, arg + t0, ids ? ids + 32 * t0 : nullptr, &nsig[i]);
+        cs.rebase[i] = ms_since(tm0);
+        cs.h2d[i] = m * 12 + (de - db);
+        rcs[i] = stx_verify_counted(g->m[i], m, data + db, o, len + t0, de - db, tmpl, meta, n_meta, tx_status + t0,
+                                    verdict + t0, arg + t0, ids ? ids + 32 * t0 : nullptr, &nsig[i]);
+        cs.ms[i] = ms_since(tm0);
+        return rcs[i];
     };
     const int rc = g->th->run(work);
+    cs.done();
     if (rc) return member_fail(g, rc, rcs);
     uint64_t base = 0;   // a SIGNATURE verdict's arg indexes the signature list of the whole parsed batch
     for (int i = 0; i < k; i++) {
@@ -539,12 +639,14 @@ int chip_group_ftx_verify_batch(chip_group* g, const chip_ftx_batch* b, uint8_t*
     if (!ntx) return CHIP_OK;
     if (!b->ids || !b->gh_start || !b->fg_start || !status) return gfail(g, CHIP_E_ARG, "null tx array");
     std::lock_guard<std::mutex> lk(g->mu);
+    CallStats cs(g);
     const int k = (int)g->m.size();
     auto single = [&](int i) {
         const int rc = chip_ftx_verify_batch(g->m[i], b, status, reason);
+        cs.single(ntx * 48 + b->comp_bytes);
         return rc ? gfail(g, rc, "member " + std::to_string(i) + ": " + chip_last_error(g->m[i])) : CHIP_OK;
     };
-    const int mi = (int)(g->next++ % k);
+    const int mi = g->single_member();
     const std::vector<uint64_t> cut = split_ranges(ntx, nullptr, k, g->min_share ? g->min_share : env_share("CHIP_GROUP_MIN_TX", 8192));
     const uint64_t ngh = b->gh_start[ntx], nfg = b->fg_start[ntx];
     if (cut[1] == ntx || !cuts_ok(b->gh_start, cut, ngh) || !cuts_ok(b->fg_start, cut, nfg) ||
@@ -559,6 +661,7 @@ int chip_group_ftx_verify_batch(chip_group* g, const chip_ftx_batch* b, uint8_t*
     auto work = [&](int i) -> int {
         const uint64_t t0 = cut[i], t1 = cut[i + 1], m = t1 - t0;
         if (!m) return CHIP_OK;
+        const auto tm0 = std::chrono::steady_clock::now();
         const uint64_t g0 = b->gh_start[t0], f0 = b->fg_start[t0], f1 = b->fg_start[t1], nf = f1 - f0;
         const uint64_t c0 = nfg ? b->comp_start[f0] : 0, c1 = nfg ? b->comp_start[f1] : 0, nc = c1 - c0;
         const uint64_t p0 = nfg ? b->pt_start[f0] : 0;
@@ -604,9 +707,14 @@ int chip_group_ftx_verify_batch(chip_group* g, const chip_ftx_batch* b, uint8_t*
         d.check_visible = b->check_visible ? b->check_visible + t0 : nullptr;
         d.visible_mask = b->visible_mask ? b->visible_mask + t0 : nullptr;
         d.comp_bytes = de - db;
-        return rcs[i] = chip_ftx_verify_batch(g->m[i], &d, status + t0, reason ? reason + t0 : nullptr);
+        cs.rebase[i] = ms_since(tm0);
+        cs.h2d[i] = m * 48 + d.comp_bytes;
+        rcs[i] = chip_ftx_verify_batch(g->m[i], &d, status + t0, reason ? reason + t0 : nullptr);
+        cs.ms[i] = ms_since(tm0);
+        return rcs[i];
     };
     const int rc = g->th->run(work);
+    cs.done();
     return rc ? member_fail(g, rc, rcs) : CHIP_OK;
 }
 
@@ -691,27 +799,178 @@ struct GDev {   // device buffer of one member (allocated with that member's dev
     template <class T> T* as() const { return reinterpret_cast<T*>(p); }
 };
 
+// ---- the group commit's ingest: each member stages only its own slice of the batch ----------------------------
+// Member i takes the transactions [t0, t1) (cut balanced by inputs) and copies only their tx_ref_start entries,
+// inputs, ids and callers from the host.  On its device it routes its inputs by owner into one send segment per
+// destination member (in transaction order), and every destination pulls its segments from every source over
+// xGMI (a device-to-device copy for two members on one GPU): each member's host-to-device bytes are ~1/k of the
+// batch, and the members' PCIe links carry the batch once between them.
+//
+// per input of the slice: its owner member
+__global__ void __launch_bounds__(256) k_slice_owner(uint64_t nr, const uint8_t* __restrict__ refs, uint32_t world,
+                                                     uint8_t* __restrict__ own) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r < nr) own[r] = (uint8_t)state_owner(refs, r, world);
+}
+// the slice's tx_ref_start (absolute values, m + 1 entries) must run from r0 to r1 without decreasing; a
+// transaction whose range is not inside [r0, r1) counts as empty (and flags the batch, which is then refused)
+CHIP_DEV bool slice_tx(const uint64_t* __restrict__ start, uint64_t t, uint64_t r0, uint64_t r1, uint64_t& a,
+                       uint64_t& e) {
+    a = start[t];
+    e = start[t + 1];
+    return a <= e && a >= r0 && e <= r1;
+}
+// cnt[j * (m + 1) + t] = inputs of slice transaction t owned by member j; cnt[j * (m + 1) + m] = 0 and
+// cnt[world * (m + 1)] = 0, so one exclusive scan over world * (m + 1) + 1 entries gives every (destination,
+// transaction) its send offset, segment j starting at scan[j * (m + 1)] and the total at scan[world * (m + 1)]
+__global__ void __launch_bounds__(256) k_slice_count(uint64_t m, const uint64_t* __restrict__ start, uint64_t r0,
+                                                     uint64_t r1, const uint8_t* __restrict__ own, uint32_t world,
+                                                     uint32_t* __restrict__ cnt, uint32_t* __restrict__ bad) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > m) return;
+    if (t == m) {
+        for (uint32_t j = 0; j < world; j++) cnt[(uint64_t)j * (m + 1) + m] = 0;
+        cnt[(uint64_t)world * (m + 1)] = 0;
+        if (start[m] != r1 || start[0] != r0) atomicOr(bad, 1u);
+        return;
+    }
+    uint64_t a, e;
+    const bool ok = slice_tx(start, t, r0, r1, a, e);
+    if (!ok) atomicOr(bad, 1u);
+    for (uint32_t j = 0; j < world; j++) {
+        uint32_t c = 0;
+        if (ok)
+            for (uint64_t r = a; r < e; r++) c += own[r - r0] == j;
+        cnt[(uint64_t)j * (m + 1) + t] = c;
+    }
+}
+// the send segments: key bytes, position in the transaction's input list, global transaction index
+__global__ void __launch_bounds__(256) k_slice_scatter(uint64_t m, const uint64_t* __restrict__ start, uint64_t r0,
+                                                       uint64_t r1, const uint8_t* __restrict__ refs,
+                                                       const uint8_t* __restrict__ own, uint32_t world,
+                                                       const uint32_t* __restrict__ scan, uint64_t t0,
+                                                       uint8_t* __restrict__ srefs, uint32_t* __restrict__ spos,
+                                                       uint32_t* __restrict__ stx) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= m) return;
+    uint64_t a, e;
+    if (!slice_tx(start, t, r0, r1, a, e)) return;
+    for (uint32_t j = 0; j < world; j++) {
+        uint64_t o = scan[(uint64_t)j * (m + 1) + t];
+        for (uint64_t r = a; r < e; r++) {
+            if (own[r - r0] != j) continue;
+            const uint32_t* src = reinterpret_cast<const uint32_t*>(refs + (r - r0) * 36);
+            uint32_t* d = reinterpret_cast<uint32_t*>(srefs + o * 36);
+#pragma unroll
+            for (int q = 0; q < 9; q++) d[q] = src[q];
+            spos[o] = (uint32_t)(r - a);
+            stx[o] = (uint32_t)(t0 + t);
+            o++;
+        }
+    }
+}
+// the segment bounds of the send buffer: bounds[j] = scan[j * (m + 1)], j = 0 .. world
+__global__ void __launch_bounds__(64) k_slice_bounds(uint64_t m, uint32_t world, const uint32_t* __restrict__ scan,
+                                                     uint32_t* __restrict__ bounds) {
+    for (uint32_t j = threadIdx.x; j <= world; j += blockDim.x) bounds[j] = scan[(uint64_t)j * (m + 1)];
+}
+// a destination's tx_ref_start from the transaction indices of its inputs (nondecreasing: sources in slice
+// order, each segment in transaction order): lstart[t] = the first local input of a transaction >= t
+__global__ void __launch_bounds__(256) k_local_start(uint64_t ntx, uint64_t nloc, const uint32_t* __restrict__ ltx,
+                                                     uint64_t* __restrict__ lstart) {
+    const uint64_t t = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (t > ntx) return;
+    uint64_t lo = 0, hi = nloc;
+    while (lo < hi) {
+        const uint64_t mid = (lo + hi) >> 1;
+        if ((uint64_t)ltx[mid] < t) lo = mid + 1;
+        else hi = mid;
+    }
+    lstart[t] = lo;
+}
+// the members' element-wise MAX of one round's votes, on every member: its own vote and the other members' votes
+// as copied into `gather` (slot i = member i, `stride` bytes apart); gated like the round's other kernels
+__global__ void __launch_bounds__(256) k_vote_max(uint64_t nwords, const uint32_t* __restrict__ gather, uint64_t stride_w,
+                                                  uint32_t world, uint32_t self, const uint32_t* __restrict__ vote,
+                                                  uint32_t* __restrict__ dec, const uint32_t* gate) {
+    if (gate && __builtin_nontemporal_load(gate) == 0u) return;
+    const uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w >= nwords) return;
+    uint32_t v = vote[w];
+    for (uint32_t i = 0; i < world; i++) {
+        if (i == self) continue;
+        const uint32_t o = gather[(uint64_t)i * stride_w + w];
+        uint32_t r = 0;
+#pragma unroll
+        for (int b = 0; b < 32; b += 8) {
+            const uint32_t x = (v >> b) & 0xffu, y = (o >> b) & 0xffu;
+            r |= (x > y ? x : y) << b;
+        }
+        v = r;
+    }
+    dec[w] = v;
+}
+
+// a member's commit scratch: owned by the group (chip_group_uniq_scratch), so tables opened and closed on one group
+// reuse it (group calls are serialised, and nothing is in flight after a commit returns)
+struct GUScratch {
+    int dev = 0;
+    // source side: the host slice and its send segments
+    GDev istart, irefs, own, cnt, scan, temp, srefs, spos, stx, bounds;
+    // destination side: the owned inputs, the whole batch's ids / callers, round scratch
+    GDev lrefs, lpos, ltx, lstart, ids, callers, vote, dec, gather, status, out;
+    PinnedBuf hb, hrec, hrows;   // hb: bad flag + segment bounds
+    ~GUScratch() {
+        (void)hipSetDevice(dev);
+        for (GDev* d : {&istart, &irefs, &own, &cnt, &scan, &temp, &srefs, &spos, &stx, &bounds, &lrefs, &lpos, &ltx,
+                        &lstart, &ids, &callers, &vote, &dec, &gather, &status, &out})
+            d->release();
+        hb.release();
+        hrec.release();
+        hrows.release();
+    }
+};
+static void uniq_scratch_release(std::vector<GUScratch*>& v) {
+    for (GUScratch* x : v) delete x;
+    v.clear();
+}
+
 struct GUMember {
     chip_uniq* u = nullptr;
     hipStream_t st = nullptr;
-    GDev start, refs, ids, callers, cnt, lstart, lrefs, lpos, vote, dec, status, out, temp;
-    PinnedBuf hvote, hrec, hrows;
-    uint64_t nloc = 0, nout = 0, undecided = 0;
+    hipEvent_t ev[2] = {nullptr, nullptr};   // this member's votes of a round (parity) are in every peer's gather
+    GUScratch* x = nullptr;
+    uint64_t t0 = 0, t1 = 0, r0 = 0, r1 = 0, nloc = 0, nout = 0;
+    uint64_t h2d = 0;
+    std::vector<uint32_t> seg;   // send segment bounds, world + 1
+    double ms_a = 0, ms_b = 0;
 };
 
 struct chip_group_uniq {
     chip_group* g;
     std::vector<GUMember> m;
-    PinnedBuf hdec;
     std::string err;
     std::mutex mu;
+    chip_group_stats stats{};
 };
 
 extern "C" int chip_ctx_h2d(chip_ctx* c, void* dst, const void* src, uint64_t bytes, void* stream);
+extern "C" int chip_uniq_gate_reset(chip_uniq* u);
+extern "C" uint32_t* chip_uniq_gate_ptr(chip_uniq* u);
+extern "C" int chip_uniq_vote_gated(chip_uniq* u, uint8_t* vote);
+extern "C" int chip_uniq_apply_gated(chip_uniq* u, const uint8_t* decision);
+extern "C" const uint32_t* chip_uniq_gate_fetch(chip_uniq* u);
 
 static int ufail(chip_group_uniq* u, int code, const std::string& msg) {
     if (u) u->err = msg;
     return code;
+}
+
+// member-to-member copy on the destination's stream: xGMI peer copy across GPUs, a device copy on one GPU
+static hipError_t member_copy(void* dst, int ddev, const void* src, int sdev, size_t bytes, hipStream_t st) {
+    if (!bytes) return hipSuccess;
+    if (ddev == sdev) return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, st);
+    return hipMemcpyPeerAsync(dst, ddev, src, sdev, bytes, st);
 }
 
 extern "C" {
@@ -725,10 +984,21 @@ int chip_group_uniq_open(chip_group* g, uint64_t capacity, chip_group_uniq** out
     u->m.resize(k);
     const uint64_t per = capacity ? (capacity + k - 1) / k : 0;   // each member holds about 1/k of the states
     int rc = CHIP_OK;
+    std::lock_guard<std::mutex> gl(g->mu);   // the group's uniqueness scratch
+    if (g->uscratch.size() != (size_t)k) {
+        uniq_scratch_release(g->uscratch);
+        for (int i = 0; i < k; i++) {
+            g->uscratch.push_back(new GUScratch());
+            g->uscratch.back()->dev = g->dev[i];
+        }
+    }
     for (int i = 0; i < k && !rc; i++) {
         GUMember& mm = u->m[i];
+        mm.x = g->uscratch[i];
         if ((rc = chip_uniq_open(g->m[i], per, &mm.u))) break;
-        if (hipSetDevice(g->dev[i]) != hipSuccess || hipStreamCreateWithFlags(&mm.st, hipStreamNonBlocking) != hipSuccess)
+        if (hipSetDevice(g->dev[i]) != hipSuccess || hipStreamCreateWithFlags(&mm.st, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&mm.ev[0], hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&mm.ev[1], hipEventDisableTiming) != hipSuccess)
             rc = CHIP_E_DEVICE;
     }
     if (rc) {
@@ -745,16 +1015,11 @@ void chip_group_uniq_close(chip_group_uniq* u) {
         GUMember& mm = u->m[i];
         (void)hipSetDevice(u->g->dev[i]);
         if (mm.st) (void)hipStreamSynchronize(mm.st);
-        for (GDev* d : {&mm.start, &mm.refs, &mm.ids, &mm.callers, &mm.cnt, &mm.lstart, &mm.lrefs, &mm.lpos, &mm.vote,
-                        &mm.dec, &mm.status, &mm.out, &mm.temp})
-            d->release();
-        mm.hvote.release();
-        mm.hrec.release();
-        mm.hrows.release();
+        for (hipEvent_t e : mm.ev)
+            if (e) (void)hipEventDestroy(e);
         if (mm.st) (void)hipStreamDestroy(mm.st);
         if (mm.u) chip_uniq_close(mm.u);
     }
-    u->hdec.release();
     delete u;
 }
 
@@ -767,6 +1032,12 @@ uint64_t chip_group_uniq_size(const chip_group_uniq* u) {
 
 const char* chip_group_uniq_last_error(const chip_group_uniq* u) { return u ? u->err.c_str() : "null table"; }
 
+int chip_group_uniq_last_stats(const chip_group_uniq* u, chip_group_stats* out) {
+    if (!u || !out) return CHIP_E_ARG;
+    *out = u->stats;
+    return CHIP_OK;
+}
+
 // the member a StateRef key belongs to (the routing every group uniqueness call uses; = distributed.state_owner)
 uint32_t chip_group_state_owner(const uint8_t* ref36, uint32_t members) {
     return ref36 && members ? state_owner_host(ref36, members) : 0;
@@ -777,7 +1048,12 @@ int chip_group_uniq_rebuild(chip_group_uniq* u, uint64_t n, const uint8_t* refs3
     if (!u || (n && (!refs36 || !tx32 || !idx || !caller))) return ufail(u, CHIP_E_ARG, "null argument");
     if (!n) return CHIP_OK;
     std::lock_guard<std::mutex> lk(u->mu);
+    std::lock_guard<std::mutex> gl(u->g->mu);   // the member contexts and threads are the group's: one call at a time
     const int k = (int)u->m.size();
+    if (k == 1) {
+        const int rc = chip_uniq_rebuild(u->m[0].u, n, refs36, tx32, idx, caller);
+        return rc ? ufail(u, rc, "member 0: " + std::string(chip_uniq_last_error(u->m[0].u))) : CHIP_OK;
+    }
     std::vector<int> rcs(k, 0);
     // each member keeps its own rows, in log order (the first row of equal keys wins inside the member, and
     // equal keys always meet in one member)
@@ -786,9 +1062,9 @@ int chip_group_uniq_rebuild(chip_group_uniq* u, uint64_t n, const uint8_t* refs3
         uint64_t mine = 0;
         for (uint64_t r = 0; r < n; r++) mine += state_owner_host(refs36 + 36 * r, (uint32_t)k) == (uint32_t)i;
         if (!mine) return CHIP_OK;
-        if (!mm.hrows.ensure(Carve::bytes(mine, 36) + Carve::bytes(mine, 32) + 2 * Carve::bytes(mine, 4) + 64))
+        if (!mm.x->hrows.ensure(Carve::bytes(mine, 36) + Carve::bytes(mine, 32) + 2 * Carve::bytes(mine, 4) + 64))
             return rcs[i] = CHIP_E_NOMEM;
-        Carve cv{static_cast<uint8_t*>(mm.hrows.p)};
+        Carve cv{static_cast<uint8_t*>(mm.x->hrows.p)};
         uint8_t* rr = cv.take<uint8_t>(36 * mine);
         uint8_t* ti = cv.take<uint8_t>(32 * mine);
         uint32_t* ix = cv.take<uint32_t>(mine);
@@ -838,11 +1114,25 @@ int chip_group_uniq_commit_batch(chip_group_uniq* u, uint64_t ntx, const uint64_
     if (!ntx) return CHIP_OK;
     const uint64_t nref = start[ntx];
     if (nref && !refs36) return ufail(u, CHIP_E_ARG, "null refs");
-    if (ntx >= 0xffffffffull || nref >= 0x7fffffffull) return ufail(u, CHIP_E_ARG, "batch too large");
+    // hipcub scans take int item counts (ntx + 1, k * (slice + 1) + 1) and the send offsets are u32
+    if (ntx >= 0x7fffffffull - 64 || nref >= 0x7fffffffull) return ufail(u, CHIP_E_ARG, "batch too large");
     if (start[0] != 0) return ufail(u, CHIP_E_ARG, "tx_ref_start must begin at 0 and be nondecreasing");
     std::lock_guard<std::mutex> lk(u->mu);
+    std::lock_guard<std::mutex> gl(u->g->mu);   // the member contexts and threads are the group's: one call at a time
+    const auto t_call = std::chrono::steady_clock::now();
     const int k = (int)u->m.size();
     chip_group* g = u->g;
+    u->stats = chip_group_stats{};
+    chip_group_stats& S = u->stats;
+    if (k == 1) {   // one member holds the whole key space: exactly the single-context host entry
+        GUMember& mm = u->m[0];
+        const int rc = chip_uniq_commit_batch(mm.u, ntx, start, refs36, tx_ids, callers, tx_status, out, cap, n_out);
+        S.members_used = 1;
+        S.rounds = chip_uniq_last_rounds(mm.u);
+        S.h2d_bytes_max = S.h2d_bytes_total = (ntx + 1) * 8 + nref * 36 + ntx * 36;
+        S.wall_ms = ms_since(t_call);
+        return rc ? ufail(u, rc, "member 0: " + std::string(chip_uniq_last_error(mm.u))) : CHIP_OK;
+    }
     std::vector<int> rcs(k, 0);
     std::vector<std::string> msgs(k);
     auto collect = [&](int rc) -> int {
@@ -850,163 +1140,304 @@ int chip_group_uniq_commit_batch(chip_group_uniq* u, uint64_t ntx, const uint64_
             if (rcs[i]) return ufail(u, rcs[i], "member " + std::to_string(i) + ": " + msgs[i]);
         return rc;
     };
-    // 1. every member: the whole batch to its device, its own inputs kept there, lookup + intern (shard_begin)
-    auto begin = [&](int i) -> int {
+    // 0. the slices: transaction ranges balanced by inputs (tx_ref_start is the prefix); the host reads only the cut
+    // entries, every member checks its own slice of tx_ref_start on its device
+    auto t_plan = std::chrono::steady_clock::now();
+    const std::vector<uint64_t> cut = split_ranges(ntx, start, k, 0);
+    if (!cuts_ok(start, cut, nref)) return ufail(u, CHIP_E_ARG, "tx_ref_start must begin at 0 and be nondecreasing");
+    const uint64_t stride = (ntx + 63) & ~(uint64_t)63;   // a member's slot in a gather buffer (whole dwords)
+    S.plan_ms = ms_since(t_plan);
+    // 1. every member: its slice from the host, routed by owner into send segments on its device
+    auto ingest = [&](int i) -> int {
+        const auto t0c = std::chrono::steady_clock::now();
         GUMember& mm = u->m[i];
         GUCHK(hipSetDevice(g->dev[i]));
         hipStream_t st = mm.st;
-        GUCHK(mm.start.ensure((ntx + 1) * 8));
-        GUCHK(mm.refs.ensure(nref * 36 + 16));
-        GUCHK(mm.ids.ensure(ntx * 32));
-        GUCHK(mm.callers.ensure(ntx * 4));
-        GUCHK(mm.cnt.ensure((ntx + 1) * 8));
-        GUCHK(mm.lstart.ensure((ntx + 1) * 8));
-        GUCHK(mm.vote.ensure(ntx + 16));
-        GUCHK(mm.dec.ensure(ntx + 16));
-        GUCHK(mm.status.ensure(ntx + 16));
-        if (!mm.hvote.ensure(ntx + 64)) GUCHK(hipErrorOutOfMemory);
-        // the caller's arrays through the member context's staging ring when they are pageable
-        if (chip_ctx_h2d(g->m[i], mm.start.p, start, (ntx + 1) * 8, st) ||
-            (nref && chip_ctx_h2d(g->m[i], mm.refs.p, refs36, nref * 36, st)) ||
-            chip_ctx_h2d(g->m[i], mm.ids.p, tx_ids, ntx * 32, st) || chip_ctx_h2d(g->m[i], mm.callers.p, callers, ntx * 4, st))
-            GUCHK(hipErrorUnknown);
-        {   // tx_ref_start from 0, nondecreasing, ending at nref (checked where it was staged)
-            const DevCheck chk[] = {{DEV_CHECK_MONOTONE, 1, mm.start.p, nullptr, nullptr, ntx, nref, 0}};
-            uint32_t bad = 0;
-            if (dev_check(g->m[i], chk, 1, st, &bad) != CHIP_OK) GUCHK(hipErrorUnknown);
-            if (bad) {
-                rcs[i] = CHIP_E_ARG;
-                msgs[i] = "tx_ref_start must begin at 0 and be nondecreasing";
-                return CHIP_E_ARG;
-            }
+        mm.t0 = cut[i];
+        mm.t1 = cut[i + 1];
+        mm.r0 = start[mm.t0];
+        mm.r1 = start[mm.t1];
+        const uint64_t m = mm.t1 - mm.t0, nr = mm.r1 - mm.r0, nc = (uint64_t)k * (m + 1) + 1;
+        if (nc >= 0x7fffffffull) {   // the route scan's int item count
+            rcs[i] = CHIP_E_ARG;
+            msgs[i] = "batch too large for this group size";
+            return CHIP_E_ARG;
         }
-        const uint32_t blocks = (uint32_t)((ntx + 1 + 255) / 256);
-        hipLaunchKernelGGL(k_route_count, dim3(blocks), dim3(256), 0, st, ntx, mm.start.as<uint64_t>(),
-                           mm.refs.as<uint8_t>(), (uint32_t)k, (uint32_t)i, mm.cnt.as<uint64_t>());
+        GUCHK(mm.x->istart.ensure((m + 1) * 8 + 16));
+        GUCHK(mm.x->irefs.ensure(nr * 36 + 16));
+        GUCHK(mm.x->own.ensure(nr + 16));
+        GUCHK(mm.x->cnt.ensure(nc * 4 + 16));
+        GUCHK(mm.x->scan.ensure(nc * 4 + 16));
+        GUCHK(mm.x->srefs.ensure(nr * 36 + 16));
+        GUCHK(mm.x->spos.ensure(nr * 4 + 16));
+        GUCHK(mm.x->stx.ensure(nr * 4 + 16));
+        GUCHK(mm.x->bounds.ensure((k + 2) * 4 + 16));
+        GUCHK(mm.x->ids.ensure(ntx * 32 + 16));
+        GUCHK(mm.x->callers.ensure(ntx * 4 + 16));
+        if (!mm.x->hb.ensure((k + 2) * 4 + 64)) GUCHK(hipErrorOutOfMemory);
+        // the caller's arrays through the member context's staging ring when they are pageable; ids / callers land
+        // at their place in the member's whole-batch arrays (the other slices come from the other members)
+        if (chip_ctx_h2d(g->m[i], mm.x->istart.p, start + mm.t0, (m + 1) * 8, st) ||
+            (nr && chip_ctx_h2d(g->m[i], mm.x->irefs.p, refs36 + 36 * mm.r0, nr * 36, st)) ||
+            (m && chip_ctx_h2d(g->m[i], mm.x->ids.as<uint8_t>() + 32 * mm.t0, tx_ids + 32 * mm.t0, m * 32, st)) ||
+            (m && chip_ctx_h2d(g->m[i], mm.x->callers.as<uint32_t>() + mm.t0, callers + mm.t0, m * 4, st)))
+            GUCHK(hipErrorUnknown);
+        mm.h2d = (m + 1) * 8 + nr * 36 + m * 36;
+        uint32_t* bad = mm.x->bounds.as<uint32_t>() + k + 1;
+        GUCHK(hipMemsetAsync(bad, 0, 4, st));
+        if (nr)
+            hipLaunchKernelGGL(k_slice_owner, dim3((uint32_t)((nr + 255) / 256)), dim3(256), 0, st, nr,
+                               mm.x->irefs.as<uint8_t>(), (uint32_t)k, mm.x->own.as<uint8_t>());
+        hipLaunchKernelGGL(k_slice_count, dim3((uint32_t)((m + 1 + 255) / 256)), dim3(256), 0, st, m,
+                           mm.x->istart.as<uint64_t>(), mm.r0, mm.r1, mm.x->own.as<uint8_t>(), (uint32_t)k, mm.x->cnt.as<uint32_t>(),
+                           bad);
         size_t tmp = 0;
-        GUCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, mm.cnt.as<uint64_t>(), mm.lstart.as<uint64_t>(), (int)(ntx + 1), st));
-        GUCHK(mm.temp.ensure(tmp + 16));
-        GUCHK(hipcub::DeviceScan::ExclusiveSum(mm.temp.p, tmp, mm.cnt.as<uint64_t>(), mm.lstart.as<uint64_t>(), (int)(ntx + 1), st));
-        uint64_t* hn = static_cast<uint64_t*>(mm.hvote.p);
-        GUCHK(hipMemcpyAsync(hn, mm.lstart.as<uint64_t>() + ntx, 8, hipMemcpyDeviceToHost, st));
-        GUCHK(hipStreamSynchronize(st));
-        mm.nloc = *hn;
-        GUCHK(mm.lrefs.ensure(mm.nloc * 36 + 16));
-        GUCHK(mm.lpos.ensure(mm.nloc * 4 + 16));
-        GUCHK(mm.out.ensure((mm.nloc + 1) * sizeof(chip_conflict)));
-        hipLaunchKernelGGL(k_route_scatter, dim3((uint32_t)((ntx + 255) / 256)), dim3(256), 0, st, ntx,
-                           mm.start.as<uint64_t>(), mm.refs.as<uint8_t>(), (uint32_t)k, (uint32_t)i,
-                           mm.lstart.as<uint64_t>(), mm.lrefs.as<uint8_t>(), mm.lpos.as<uint32_t>());
+        GUCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tmp, mm.x->cnt.as<uint32_t>(), mm.x->scan.as<uint32_t>(), (int)nc, st));
+        GUCHK(mm.x->temp.ensure(tmp + 16));
+        GUCHK(hipcub::DeviceScan::ExclusiveSum(mm.x->temp.p, tmp, mm.x->cnt.as<uint32_t>(), mm.x->scan.as<uint32_t>(), (int)nc, st));
+        if (m)
+            hipLaunchKernelGGL(k_slice_scatter, dim3((uint32_t)((m + 255) / 256)), dim3(256), 0, st, m,
+                               mm.x->istart.as<uint64_t>(), mm.r0, mm.r1, mm.x->irefs.as<uint8_t>(), mm.x->own.as<uint8_t>(),
+                               (uint32_t)k, mm.x->scan.as<uint32_t>(), mm.t0, mm.x->srefs.as<uint8_t>(), mm.x->spos.as<uint32_t>(),
+                               mm.x->stx.as<uint32_t>());
+        hipLaunchKernelGGL(k_slice_bounds, dim3(1), dim3(64), 0, st, m, (uint32_t)k, mm.x->scan.as<uint32_t>(),
+                           mm.x->bounds.as<uint32_t>());
         GUCHK(hipGetLastError());
-        const chip_uniq_shard_batch sb{ntx, mm.lstart.as<uint64_t>(), mm.nloc, mm.lrefs.as<uint8_t>(),
-                                       mm.lpos.as<uint32_t>(), mm.ids.as<uint8_t>(), mm.callers.as<uint32_t>()};
-        GUCALL(chip_uniq_shard_begin(mm.u, &sb, st));
+        GUCHK(hipMemcpyAsync(mm.x->hb.p, mm.x->bounds.p, (k + 2) * 4, hipMemcpyDeviceToHost, st));
+        GUCHK(hipStreamSynchronize(st));
+        const uint32_t* hb = static_cast<const uint32_t*>(mm.x->hb.p);
+        if (hb[k + 1]) {
+            rcs[i] = CHIP_E_ARG;
+            msgs[i] = "tx_ref_start must begin at 0 and be nondecreasing";
+            return CHIP_E_ARG;
+        }
+        mm.seg.assign(hb, hb + k + 1);
+        mm.ms_a = ms_since(t0c);
         return CHIP_OK;
     };
-    int rc = g->th->run(begin);
-    if (rc) {
-        // members that began must not stay open: finish them with an all-zero decision and drop the result
+    int rc = g->th->run(ingest);
+    if (rc) return collect(rc);   // no member has begun a batch
+    // 2. every destination pulls its segments (and the other slices' ids / callers), builds its tx_ref_start and
+    // runs its lookup (shard_begin)
+    auto exchange = [&](int j) -> int {
+        const int i = j;   // GUCHK / GUCALL report into rcs[i]
+        const auto t0c = std::chrono::steady_clock::now();
+        GUMember& mm = u->m[j];
+        GUCHK(hipSetDevice(g->dev[j]));
+        hipStream_t st = mm.st;
+        uint64_t nloc = 0;
+        for (int s = 0; s < k; s++) nloc += u->m[s].seg[j + 1] - u->m[s].seg[j];
+        mm.nloc = nloc;
+        GUCHK(mm.x->lrefs.ensure(nloc * 36 + 16));
+        GUCHK(mm.x->lpos.ensure(nloc * 4 + 16));
+        GUCHK(mm.x->ltx.ensure(nloc * 4 + 16));
+        GUCHK(mm.x->lstart.ensure((ntx + 1) * 8 + 16));
+        GUCHK(mm.x->vote.ensure(stride + 64));
+        GUCHK(mm.x->dec.ensure(stride + 64));
+        GUCHK(mm.x->gather.ensure(2 * (uint64_t)k * stride + 64));
+        GUCHK(mm.x->status.ensure(ntx + 16));
+        GUCHK(mm.x->out.ensure((nloc + 1) * sizeof(chip_conflict)));
+        uint64_t at = 0;
+        for (int s = 0; s < k; s++) {
+            const GUMember& src = u->m[s];
+            const uint64_t a = src.seg[j], n = src.seg[j + 1] - a;
+            GUCHK(member_copy(mm.x->lrefs.as<uint8_t>() + 36 * at, g->dev[j], src.x->srefs.as<uint8_t>() + 36 * a, g->dev[s], n * 36, st));
+            GUCHK(member_copy(mm.x->lpos.as<uint32_t>() + at, g->dev[j], src.x->spos.as<uint32_t>() + a, g->dev[s], n * 4, st));
+            GUCHK(member_copy(mm.x->ltx.as<uint32_t>() + at, g->dev[j], src.x->stx.as<uint32_t>() + a, g->dev[s], n * 4, st));
+            at += n;
+            if (s == j) continue;
+            const uint64_t m = src.t1 - src.t0;
+            GUCHK(member_copy(mm.x->ids.as<uint8_t>() + 32 * src.t0, g->dev[j], src.x->ids.as<uint8_t>() + 32 * src.t0, g->dev[s],
+                              m * 32, st));
+            GUCHK(member_copy(mm.x->callers.as<uint32_t>() + src.t0, g->dev[j], src.x->callers.as<uint32_t>() + src.t0, g->dev[s],
+                              m * 4, st));
+        }
+        hipLaunchKernelGGL(k_local_start, dim3((uint32_t)((ntx + 1 + 255) / 256)), dim3(256), 0, st, ntx, nloc,
+                           mm.x->ltx.as<uint32_t>(), mm.x->lstart.as<uint64_t>());
+        GUCHK(hipGetLastError());
+        const chip_uniq_shard_batch sb{ntx, mm.x->lstart.as<uint64_t>(), nloc, mm.x->lrefs.as<uint8_t>(),
+                                       mm.x->lpos.as<uint32_t>(), mm.x->ids.as<uint8_t>(), mm.x->callers.as<uint32_t>()};
+        GUCALL(chip_uniq_shard_begin(mm.u, &sb, st));
+        GUCALL(chip_uniq_gate_reset(mm.u));
+        GUCHK(hipStreamSynchronize(st));   // every member's sources are read before any member's rounds reuse them
+        mm.ms_b = ms_since(t0c);
+        return CHIP_OK;
+    };
+    const auto t_ex = std::chrono::steady_clock::now();
+    rc = g->th->run(exchange);
+    S.exchange_ms = ms_since(t_ex);
+    auto close_all = [&]() {   // members that began must not stay open: finish them with an all-zero decision
         for (int i = 0; i < k; i++) {
-            if (rcs[i]) continue;
             GUMember& mm = u->m[i];
             (void)hipSetDevice(g->dev[i]);
-            (void)hipMemsetAsync(mm.dec.p, 0, ntx, mm.st);
+            (void)hipStreamSynchronize(mm.st);
+            (void)hipMemsetAsync(mm.x->dec.p, 0, ntx, mm.st);
             uint64_t nn = 0;
-            (void)chip_uniq_shard_finish(mm.u, mm.dec.as<uint8_t>(), mm.status.as<uint8_t>(), mm.out.as<chip_conflict>(),
+            (void)chip_uniq_shard_finish(mm.u, mm.x->dec.as<uint8_t>(), mm.x->status.as<uint8_t>(), mm.x->out.as<chip_conflict>(),
                                          mm.nloc + 1, &nn);
         }
+    };
+    if (rc) {
+        close_all();
         return collect(rc);
     }
-    if (!u->hdec.ensure(ntx + 64)) return ufail(u, CHIP_E_NOMEM, "decision buffer");
-    uint8_t* dec = static_cast<uint8_t*>(u->hdec.p);
-    // element-wise MAX of the members' vote bytes, each member reducing a slice of the transactions
-    auto reduce = [&](int i) -> int {
-        const uint64_t a = ntx * (uint64_t)i / k, b = ntx * (uint64_t)(i + 1) / k;
-        memcpy(dec + a, static_cast<const uint8_t*>(u->m[0].hvote.p) + a, b - a);
-        for (int j = 1; j < k; j++) {
-            const uint8_t* v = static_cast<const uint8_t*>(u->m[j].hvote.p);
-            for (uint64_t t = a; t < b; t++) dec[t] = std::max(dec[t], v[t]);
+    // 3. ordered-commit rounds, enqueued for every member from this thread (the cross-member event waits must be
+    // enqueued after the records they wait for): each member's vote is copied into every peer's gather slot and
+    // each member reduces the MAX itself (k_vote_max), applies it and updates its gate — no host round trip inside
+    // a chunk of rounds.  Gathers are double-buffered by round parity: a member overwrites a peer's slot of parity p
+    // only after waiting for that peer's vote of the next round, which its stream orders after its read of slot p.
+    const uint64_t nwords = (ntx + 3) / 4;
+    auto enqueue_round = [&](int p, bool gated, bool classify) -> int {
+        for (int i = 0; i < k; i++) {
+            GUMember& mm = u->m[i];
+            GUCHK(hipSetDevice(g->dev[i]));
+            if (classify) GUCALL(chip_uniq_shard_classify(mm.u, mm.x->vote.as<uint8_t>()));
+            else GUCALL(chip_uniq_vote_gated(mm.u, mm.x->vote.as<uint8_t>()));
+            for (int j = 0; j < k; j++) {
+                if (j == i) continue;
+                GUMember& d = u->m[j];
+                GUCHK(member_copy(d.x->gather.as<uint8_t>() + ((uint64_t)p * k + i) * stride, g->dev[j], mm.x->vote.p, g->dev[i],
+                                  ntx, mm.st));
+            }
+            GUCHK(hipEventRecord(mm.ev[p], mm.st));
+        }
+        for (int i = 0; i < k; i++) {
+            GUMember& mm = u->m[i];
+            GUCHK(hipSetDevice(g->dev[i]));
+            for (int j = 0; j < k; j++)
+                if (j != i) GUCHK(hipStreamWaitEvent(mm.st, u->m[j].ev[p], 0));
+            hipLaunchKernelGGL(k_vote_max, dim3((uint32_t)((nwords + 255) / 256)), dim3(256), 0, mm.st, nwords,
+                               mm.x->gather.as<uint32_t>() + (uint64_t)p * k * (stride / 4), stride / 4, (uint32_t)k,
+                               (uint32_t)i, mm.x->vote.as<uint32_t>(), mm.x->dec.as<uint32_t>(),
+                               gated ? chip_uniq_gate_ptr(mm.u) : (const uint32_t*)nullptr);
+            GUCHK(hipGetLastError());
+            if (!classify) GUCALL(chip_uniq_apply_gated(mm.u, mm.x->dec.as<uint8_t>()));
         }
         return CHIP_OK;
     };
-    // 2. ordered-commit rounds: vote on every member, MAX on the host, apply everywhere; until nothing is undecided
-    auto vote = [&](int i) -> int {
-        GUMember& mm = u->m[i];
-        GUCHK(hipSetDevice(g->dev[i]));
-        GUCALL(chip_uniq_shard_vote(mm.u, mm.vote.as<uint8_t>()));
-        GUCHK(hipMemcpyAsync(mm.hvote.p, mm.vote.p, ntx, hipMemcpyDeviceToHost, mm.st));
-        GUCHK(hipStreamSynchronize(mm.st));
-        return CHIP_OK;
-    };
-    auto apply = [&](int i) -> int {
-        GUMember& mm = u->m[i];
-        GUCHK(hipSetDevice(g->dev[i]));
-        GUCHK(hipMemcpyAsync(mm.dec.p, dec, ntx, hipMemcpyHostToDevice, mm.st));
-        GUCALL(chip_uniq_shard_apply(mm.u, mm.dec.as<uint8_t>(), &mm.undecided));
-        return CHIP_OK;
-    };
-    for (uint64_t round = 0;; round++) {
-        if ((rc = g->th->run(vote)) || (rc = g->th->run(reduce)) || (rc = g->th->run(apply))) break;
-        const uint64_t und = u->m[0].undecided;
+    const auto t_rounds = std::chrono::steady_clock::now();
+    uint64_t launched = 0;
+    int parity = 0;
+    for (uint32_t chunk = 4; !rc; chunk = 8) {
+        for (uint32_t c = 0; c < chunk && !rc; c++, parity ^= 1) rc = enqueue_round(parity, true, false);
+        launched += chunk;
+        if (rc) break;
+        std::vector<const uint32_t*> gates(k, nullptr);
+        for (int i = 0; i < k && !rc; i++) {
+            GUMember& mm = u->m[i];
+            if (hipSetDevice(g->dev[i]) != hipSuccess || !(gates[i] = chip_uniq_gate_fetch(mm.u)) ||
+                hipStreamSynchronize(mm.st) != hipSuccess) {
+                rc = rcs[i] = CHIP_E_DEVICE;
+                msgs[i] = "ordered-commit rounds: gate read";
+            }
+        }
+        if (rc) break;
         for (int i = 1; i < k; i++)
-            if (u->m[i].undecided != und) {
-                rc = CHIP_E_DEVICE;
-                rcs[i] = rc;
+            if (gates[i][0] != gates[0][0] || gates[i][1] != gates[0][1]) {
+                rc = rcs[i] = CHIP_E_DEVICE;
                 msgs[i] = "members disagree on the undecided count";
             }
-        if (rc || !und) break;
-        if (round > ntx) {
+        if (rc || !gates[0][0]) break;
+        if (launched > ntx + 8) {
             rc = rcs[0] = CHIP_E_DEVICE;
             msgs[0] = "ordered-commit rounds did not converge";
-            break;
         }
     }
-    // 3. classification of the failed transactions (one more MAX), then each member's inserts and records
-    auto classify = [&](int i) -> int {
-        GUMember& mm = u->m[i];
-        GUCHK(hipSetDevice(g->dev[i]));
-        GUCALL(chip_uniq_shard_classify(mm.u, mm.vote.as<uint8_t>()));
-        GUCHK(hipMemcpyAsync(mm.hvote.p, mm.vote.p, ntx, hipMemcpyDeviceToHost, mm.st));
-        GUCHK(hipStreamSynchronize(mm.st));
-        return CHIP_OK;
-    };
+    S.rounds_ms = ms_since(t_rounds);
+    if (rc) {
+        close_all();
+        return collect(rc);
+    }
+    // 4. classification of the failed transactions (one more MAX over the members), then each member's inserts and
+    // records
+    const auto t_fin = std::chrono::steady_clock::now();
+    rc = enqueue_round(parity, false, true);
+    if (rc) {
+        close_all();
+        return collect(rc);
+    }
+    const bool trace = getenv("CHIP_GROUP_TRACE") != nullptr;
     auto finish = [&](int i) -> int {
         GUMember& mm = u->m[i];
+        const auto tf = std::chrono::steady_clock::now();
         GUCHK(hipSetDevice(g->dev[i]));
-        if (!rc) GUCHK(hipMemcpyAsync(mm.dec.p, dec, ntx, hipMemcpyHostToDevice, mm.st));
-        else GUCHK(hipMemsetAsync(mm.dec.p, 0, ntx, mm.st));   // close the batch after a failure elsewhere
         mm.nout = 0;
-        const int r = chip_uniq_shard_finish(mm.u, mm.dec.as<uint8_t>(), mm.status.as<uint8_t>(), mm.out.as<chip_conflict>(),
-                                             mm.nloc + 1, &mm.nout);
-        if (r) GUCALL(r);
-        if (rc) return CHIP_OK;
+        GUCALL(chip_uniq_shard_finish(mm.u, mm.x->dec.as<uint8_t>(), mm.x->status.as<uint8_t>(), mm.x->out.as<chip_conflict>(),
+                                      mm.nloc + 1, &mm.nout));
         if (mm.nout) {
-            if (!mm.hrec.ensure(mm.nout * sizeof(chip_conflict) + 64)) GUCHK(hipErrorOutOfMemory);
-            GUCHK(hipMemcpyAsync(mm.hrec.p, mm.out.p, mm.nout * sizeof(chip_conflict), hipMemcpyDeviceToHost, mm.st));
+            if (!mm.x->hrec.ensure(mm.nout * sizeof(chip_conflict) + 64)) GUCHK(hipErrorOutOfMemory);
+            GUCHK(hipMemcpyAsync(mm.x->hrec.p, mm.x->out.p, mm.nout * sizeof(chip_conflict), hipMemcpyDeviceToHost, mm.st));
         }
-        if (i == 0) GUCHK(hipMemcpyAsync(tx_status, mm.status.p, ntx, hipMemcpyDeviceToHost, mm.st));
+        const double fin_ms = ms_since(tf);
+        if (i == 0) GUCHK(hipMemcpyAsync(tx_status, mm.x->status.p, ntx, hipMemcpyDeviceToHost, mm.st));
         GUCHK(hipStreamSynchronize(mm.st));
+        if (trace)
+            fprintf(stderr, "[group uniq] member %d: shard_finish %.3f ms, records + status D2H %.3f ms (%llu records)\n", i,
+                    fin_ms, ms_since(tf) - fin_ms, (unsigned long long)mm.nout);
         return CHIP_OK;
     };
-    if (!rc && !(rc = g->th->run(classify))) rc = g->th->run(reduce);
-    const int rf = g->th->run(finish);
-    if (rc || rf) return collect(rc ? rc : rf);
-    // 4. the union of the members' Conflict.stateHistory records in (tx, input_index) order (each member's list
-    // is already in that order: a k-way merge)
+    const double t_cls = ms_since(t_fin);
+    rc = g->th->run(finish);
+    const double t_fins = ms_since(t_fin);
+    S.rounds = chip_uniq_last_rounds(u->m[0].u);
+    if (rc) return collect(rc);
+    // 5. the union of the members' Conflict.stateHistory records in (tx, input_index) order (each member's list
+    // is already in that order: a k-way merge), on the member threads: thread q merges the records of the
+    // transactions [ntx q / k, ntx (q + 1) / k) into their place in `out` (its offset = the records of the
+    // transactions before the range, found by binary search in every member's list)
     uint64_t total = 0;
     for (const GUMember& mm : u->m) total += mm.nout;
-    std::vector<uint64_t> at(k, 0);
-    for (uint64_t w = 0; w < total; w++) {
-        int best = -1;
-        const chip_conflict* bc = nullptr;
-        for (int i = 0; i < k; i++) {
-            if (at[i] >= u->m[i].nout) continue;
-            const chip_conflict* c = static_cast<const chip_conflict*>(u->m[i].hrec.p) + at[i];
-            if (!bc || c->tx < bc->tx || (c->tx == bc->tx && c->input_index < bc->input_index)) bc = c, best = i;
+    auto first_rec = [&](int j, uint64_t t) -> uint64_t {   // first record of member j with tx >= t
+        const chip_conflict* r = static_cast<const chip_conflict*>(u->m[j].x->hrec.p);
+        uint64_t lo = 0, hi = u->m[j].nout;
+        while (lo < hi) {
+            const uint64_t mid = (lo + hi) >> 1;
+            if (r[mid].tx < t) lo = mid + 1;
+            else hi = mid;
         }
-        if (w < cap && out) out[w] = *bc;
-        at[best]++;
+        return lo;
+    };
+    auto merge = [&](int q) -> int {
+        if (!out || !cap) return CHIP_OK;
+        const uint64_t ta = ntx * (uint64_t)q / k, tb = ntx * (uint64_t)(q + 1) / k;
+        std::vector<uint64_t> at(k), end(k);
+        uint64_t w = 0;
+        for (int j = 0; j < k; j++) {
+            at[j] = first_rec(j, ta);
+            end[j] = first_rec(j, tb);
+            w += at[j];
+        }
+        for (; w < cap; w++) {
+            int best = -1;
+            const chip_conflict* bc = nullptr;
+            for (int j = 0; j < k; j++) {
+                if (at[j] >= end[j]) continue;
+                const chip_conflict* c = static_cast<const chip_conflict*>(u->m[j].x->hrec.p) + at[j];
+                if (!bc || c->tx < bc->tx || (c->tx == bc->tx && c->input_index < bc->input_index)) bc = c, best = j;
+            }
+            if (!bc) break;
+            out[w] = *bc;
+            at[best]++;
+        }
+        return CHIP_OK;
+    };
+    (void)g->th->run(merge);
+    S.finish_ms = ms_since(t_fin);
+    S.members_used = 0;
+    S.member_ms_min = 1e300;
+    for (const GUMember& mm : u->m) {
+        S.members_used += mm.t1 > mm.t0 ? 1 : 0;
+        S.member_ms_max = std::max(S.member_ms_max, mm.ms_a);
+        S.member_ms_min = std::min(S.member_ms_min, mm.ms_a);
+        S.h2d_bytes_max = std::max(S.h2d_bytes_max, mm.h2d);
+        S.h2d_bytes_total += mm.h2d;
+        S.exchange_bytes_max = std::max(S.exchange_bytes_max, (uint64_t)mm.nloc * 44);
     }
+    S.wall_ms = ms_since(t_call);
+    if (trace)
+        fprintf(stderr, "[group uniq] ingest %.3f / %.3f ms, exchange %.3f, rounds %.3f (%u), classify enqueue %.3f, finish %.3f, "
+                "merge %.3f ms\n", S.member_ms_min, S.member_ms_max, S.exchange_ms, S.rounds_ms, S.rounds, t_cls,
+                t_fins - t_cls, S.finish_ms - t_fins);
     *n_out = total;
     return total > cap ? ufail(u, CHIP_E_CAPACITY, "more conflict records than capacity") : CHIP_OK;
 }

@@ -43,8 +43,11 @@ class ForkJoin {
         }
     }
     int size() const { return (int)slots_.size(); }
-    // f(i) for every i whose bit is set in `active` (all: ~0), i = 0 on the caller's thread
+    // f(i) for every i whose bit is set in `active` (all: ~0), i = 0 on the caller's thread.  One run at a time:
+    // a slot holds one f, so concurrent callers serialise here (a second caller overwriting a busy slot's f would
+    // make the first caller's f(i) never run while both return as if it had).  f must not call run() itself.
     int run(const std::function<int(int)>& f, uint64_t active = ~0ull) {
+        std::lock_guard<std::mutex> one(run_mu_);
         const int n = (int)slots_.size();
         for (int i = 1; i < n; i++) {
             if (!(active >> (i & 63) & 1)) continue;
@@ -76,4 +79,5 @@ class ForkJoin {
         bool busy = false, quit = false;
     };
     std::vector<std::unique_ptr<Slot>> slots_;
+    std::mutex run_mu_;
 };

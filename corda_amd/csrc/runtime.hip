@@ -200,6 +200,7 @@ struct chip_ctx {
     // tables) was last built from, the path it was built for, and the buffer generations it lives in
     DevBuf kc_keys, kc_len, kc_flag;
     bool kc_valid = false;
+    int kc_test_fail = 0, kc_test_seen = 0;   // CHIP_TEST_FAIL_KEYSTATE=n: the n-th key-cache batch fails (tests)
     uint32_t kc_path = 0;
     uint64_t kc_nk = 0, kc_gen = 0;
     uint64_t key_state_gen() const {
@@ -257,8 +258,13 @@ struct chip_ctx {
     }
 };
 
+// Every failing call also drops the cross-batch key state: a call may fail after k_key_cache overwrote the cached
+// pool but before the key preps / table builds for it were enqueued, and the next batch must not trust that copy.
 static int fail(chip_ctx* c, int code, const std::string& msg) {
-    if (c) c->err = msg;
+    if (c) {
+        c->err = msg;
+        c->kc_valid = false;
+    }
     return code;
 }
 #define HIPCHK(ctx, x)                                                                              \
@@ -575,6 +581,7 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
     if (const char* e = getenv("CHIP_ECKEYS_LATE")) c->eckeys_late = e[0] == '1';
     if (const char* e = getenv("CHIP_STAGING_RING")) c->ring.enabled = e[0] != '0';
     if (const char* e = getenv("CHIP_KERNEL_TIMING")) c->ktiming = e[0] != '0';
+    if (const char* e = getenv("CHIP_TEST_FAIL_KEYSTATE")) c->kc_test_fail = atoi(e);
     if (const char* e = getenv("CHIP_KRYO_FUSED")) c->kryo_fused = (uint32_t)std::min(2, std::max(0, atoi(e)));
     if (cfg && cfg->reserve_sigs) {
         (void)c->lists.ensure(cfg->reserve_sigs * 4 * N_LISTS);
@@ -779,11 +786,13 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     // cached one.  Not with per-batch Ed25519 comb slots (non-eager: the slots follow the signatures).
     const uint32_t path = (comb ? (w.eager ? 1u : 3u) : 0u) | (ec_comb ? 4u : 8u);
     const uint32_t* skip = nullptr;
+    bool kc_commit = false, may_reuse = false;
     if (!reuse && nk) {
         if ((c->flags & CHIP_FLAG_KEY_CACHE) && !(path & 2u)) {
             HIPCHK(c, c->kc_flag.ensure(64));
             uint32_t* flag = c->kc_flag.as<uint32_t>();
             const bool may = c->kc_valid && path == c->kc_path && nk == c->kc_nk && c->kc_gen == c->key_state_gen();
+            may_reuse = may;
             HIPCHK(c, hipMemsetD32Async(flag, may ? 1u : 0u, 1, st));
             HIPCHK(c, c->kc_keys.ensure(nk * KC_MAX + 16));
             HIPCHK(c, c->kc_len.ensure(nk * 4 + 16));
@@ -793,10 +802,12 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
             hipLaunchKernelGGL(k_meta_clear, dim3((uint32_t)((nk + 255) / 256)), dim3(256), 0, st, nk,
                                c->meta.as<KeyMeta>(), (const uint32_t*)flag);
             skip = flag;
-            c->kc_valid = true;   // after this batch the state is the cached pool's, rebuilt or reused
-            c->kc_path = path;
-            c->kc_nk = nk;
-            c->kc_gen = c->key_state_gen();
+            // the device copy now describes this pool; the key state does only once every key prep and table build
+            // of the batch is enqueued (kc_commit below): until then an error return leaves the cache invalid
+            c->kc_valid = false;
+            kc_commit = true;
+            if (c->kc_test_fail > 0 && ++c->kc_test_seen == c->kc_test_fail)
+                return fail(c, CHIP_E_NOMEM, "CHIP_TEST_FAIL_KEYSTATE: forced failure before the key state build");
         } else {
             clear_meta = true;
             c->kc_valid = false;   // rebuilt for a pool the cache does not describe
@@ -881,6 +892,14 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     }
     if ((!w.early || c->eckeys_late) && (rk = ecdsa_keys())) return rk;
     c->kend(ke, st);
+    HIPCHK(c, hipGetLastError());
+    if (kc_commit) {   // every key prep and table build of this pool is enqueued: the cached state is this pool's
+        c->kc_valid = true;
+        c->kc_path = path;
+        c->kc_nk = nk;
+        c->kc_gen = c->key_state_gen();
+        c->stats.key_cache_checks += skip && may_reuse ? 1 : 0;
+    }
     if (vc && vc->keys_only) {
         c->stats.keys_prepared += nk;
         return CHIP_OK;

@@ -120,7 +120,9 @@ struct chip_uniq {
     unsigned long long* h_spread = nullptr;   // pinned host copy of the SPREAD counters
     unsigned long long* h_icount = nullptr;   // pinned host copy of the insert counters
     uint32_t* h_gate = nullptr;               // pinned host copy of the round gate
-    uint32_t round = 0;                       // ordered-commit rounds of the batch in flight
+    uint32_t round = 0;                       // ordered-commit rounds of the batch in flight (launched)
+    bool gated = false;                       // the rounds run gated on the device (gate[1] counts those that ran)
+    uint32_t last_rounds = 0;                 // rounds of the last finished batch
     // staging of the host entry points
     UBuf h_start, h_refs, h_ids, h_call, h_st, h_vote, h_out;
 };
@@ -413,7 +415,10 @@ __global__ void __launch_bounds__(64) k_uniq_gate(unsigned long long* __restrict
     }
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) sum += __shfl_xor(sum, o);
-    if (lane == 0) *gate = sum ? (uint32_t)(sum > 0xffffffffull ? 0xffffffffull : sum) : 0u;
+    if (lane == 0) {
+        gate[0] = sum ? (uint32_t)(sum > 0xffffffffull ? 0xffffffffull : sum) : 0u;
+        gate[1] += 1u;   // rounds that ran (this gate kernel runs once per round that was open)
+    }
 }
 
 // the ConsumingTx that consumed local input r before tx t, if any
@@ -721,10 +726,11 @@ static int ensure_capacity(chip_uniq* u, uint64_t extra, hipStream_t st) {
 }
 
 // room for `extra` more rows in the ConsumingTx id side table (grown by doubling, old rows copied)
-static int ensure_rows(chip_uniq* u, uint64_t extra, hipStream_t st) {
+static int ensure_rows(chip_uniq* u, uint64_t extra, hipStream_t st, bool exact = false) {
     if (u->rows + extra <= u->rows_cap) return CHIP_OK;
     uint64_t ncap = u->rows_cap ? u->rows_cap : 1024;
     while (ncap < u->rows + extra) ncap <<= 1;
+    if (exact) ncap = std::max<uint64_t>(u->rows + extra, 1024);
     uint8_t* t = nullptr;
     UCHK(u, hipMalloc(&t, ncap * 32));
     if (u->rows) UCHK(u, hipMemcpyAsync(t, u->txrows, u->rows * 32, hipMemcpyDeviceToDevice, st));
@@ -791,6 +797,9 @@ int chip_uniq_open(chip_ctx* ctx, uint64_t capacity, chip_uniq** out) {
         return CHIP_E_DEVICE;
     }
     int r = ensure_capacity(u, capacity ? capacity : 1024, u->stream);
+    // the ConsumingTx id side table sized for `capacity` rows up front (one row per committed-batch transaction), so
+    // the first commits after a rebuild do not regrow and copy it inside the commit
+    if (!r) r = ensure_rows(u, capacity ? capacity : 1024, u->stream, true);
     if (!r && hipHostMalloc((void**)&u->h_spread, SPREAD * 64, hipHostMallocDefault) != hipSuccess) r = CHIP_E_NOMEM;
     if (!r && hipHostMalloc((void**)&u->h_gate, 64, hipHostMallocDefault) != hipSuccess) r = CHIP_E_NOMEM;
     if (!r && hipHostMalloc((void**)&u->h_icount, SPREAD * 64, hipHostMallocDefault) != hipSuccess) r = CHIP_E_NOMEM;
@@ -828,6 +837,8 @@ void chip_uniq_close(chip_uniq* u) {
 uint64_t chip_uniq_size(const chip_uniq* u) { return u ? u->size : 0; }
 
 const char* chip_uniq_last_error(const chip_uniq* u) { return u ? u->err.c_str() : "null table"; }
+
+uint32_t chip_uniq_last_rounds(const chip_uniq* u) { return u ? u->last_rounds : 0; }
 
 int chip_uniq_rebuild(chip_uniq* u, uint64_t n, const uint8_t* refs36, const uint8_t* tx32, const uint32_t* idx,
                       const uint32_t* caller) {
@@ -873,7 +884,8 @@ int chip_uniq_shard_begin(chip_uniq* u, const chip_uniq_shard_batch* b, void* st
     if (u->open) return ufail(u, CHIP_E_ARG, "a shard batch is already in flight");
     const uint64_t ntx = b->ntx, nref = b->nref;
     if (ntx && (!b->ref_start || !b->tx_ids || !b->callers)) return ufail(u, CHIP_E_ARG, "null batch array");
-    if (ntx >= 0xffffffffull || nref >= 0x7fffffffull) return ufail(u, CHIP_E_ARG, "batch too large");
+    // hipcub scans take int item counts: ntx + 1 and nref must stay below 2^31
+    if (ntx >= 0x7fffffffull || nref >= 0x7fffffffull) return ufail(u, CHIP_E_ARG, "batch too large");
     if (nref && (!b->refs36 || !b->ref_pos)) return ufail(u, CHIP_E_ARG, "null ref array");
     UCHK(u, hipSetDevice(u->device));
     hipStream_t st = stream ? (hipStream_t)stream : u->stream;
@@ -889,6 +901,7 @@ int chip_uniq_shard_begin(chip_uniq* u, const chip_uniq_shard_batch* b, void* st
     u->ids = b->tx_ids;
     u->callers = b->callers;
     u->round = 0;
+    u->gated = false;
     if (ntx) UCHK(u, hipMemsetAsync(u->st.p, ST_UNDECIDED, ntx, st));
     UCHK(u, hipMemsetAsync(u->ctr.p, 0, 64, st));
     if (ntx)
@@ -1026,12 +1039,54 @@ int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_st
     UCHK(u, hipGetLastError());
     UCHK(u, hipStreamSynchronize(st));
     const uint64_t nout = (uint64_t)last[0] + last[1];
+    u->last_rounds = u->gated ? u->h_gate[1] : u->round;   // gated: read back with the gate (gate_fetch)
     if (nref && ntx) {
         u->size += spread_total(u->h_icount, 0);
         u->slots += spread_total(u->h_icount, 1);
     }
     *n_out = nout;
     return nout > cap ? ufail(u, CHIP_E_CAPACITY, "more conflict records than capacity") : CHIP_OK;
+}
+
+// the gated rounds of a batch: SPREAD counters zeroed, gate = {1 (round 1 runs), 0 rounds}
+static int gate_reset(chip_uniq* u) {
+    hipStream_t st = u->bst;
+    int r = spread_zero(u, st);
+    if (r) return r;
+    UCHK(u, hipMemsetD32Async((hipDeviceptr_t)u->gate.p, 1u, 1, st));
+    UCHK(u, hipMemsetD32Async((hipDeviceptr_t)(u->gate.as<uint32_t>() + 1), 0u, 1, st));
+    u->gated = true;
+    return CHIP_OK;
+}
+
+// internal (group.hip, device groups): the ordered-commit rounds of a shard batch launched without host round
+// trips — each member's vote, the members' element-wise MAX on the device (group.hip k_vote_max, gated by the
+// same word) and the gated apply + gate update, so a group enqueues a whole chunk of rounds at once
+extern "C" int chip_uniq_gate_reset(chip_uniq* u) {
+    if (!u || !u->open) return CHIP_E_ARG;
+    UCHK(u, hipSetDevice(u->device));
+    return gate_reset(u);
+}
+extern "C" uint32_t* chip_uniq_gate_ptr(chip_uniq* u) { return u ? u->gate.as<uint32_t>() : nullptr; }
+extern "C" int chip_uniq_vote_gated(chip_uniq* u, uint8_t* vote) {
+    if (!u || !u->open || !u->gated) return CHIP_E_ARG;
+    launch_round_vote(u, vote, u->gate.as<uint32_t>());
+    UCHK(u, hipGetLastError());
+    return CHIP_OK;
+}
+extern "C" int chip_uniq_apply_gated(chip_uniq* u, const uint8_t* decision) {
+    if (!u || !u->open || !u->gated) return CHIP_E_ARG;
+    uint32_t* gate = u->gate.as<uint32_t>();
+    launch_apply(u, decision, gate);
+    hipLaunchKernelGGL(k_uniq_gate, dim3(1), dim3(64), 0, u->bst, u->spread.as<unsigned long long>(), gate);
+    UCHK(u, hipGetLastError());
+    return CHIP_OK;
+}
+// gate[0] (undecided after the last round that ran) and gate[1] (rounds that ran) into pinned host memory, on the
+// batch stream: valid after that stream is synchronised
+extern "C" const uint32_t* chip_uniq_gate_fetch(chip_uniq* u) {
+    if (!u || hipMemcpyAsync(u->h_gate, u->gate.p, 8, hipMemcpyDeviceToHost, u->bst) != hipSuccess) return nullptr;
+    return u->h_gate;
 }
 
 // one shard owning the whole key space: decision = vote, and the rounds run back to back on the
@@ -1047,13 +1102,9 @@ static int commit_device(chip_uniq* u, const chip_uniq_shard_batch* b, uint8_t* 
     }
     uint8_t* vote = u->h_vote.as<uint8_t>();
     uint32_t* gate = u->gate.as<uint32_t>();
-    if ((r = spread_zero(u, st))) {
+    if ((r = gate_reset(u))) {
         u->open = false;
         return r;
-    }
-    if (hipMemsetD32Async((hipDeviceptr_t)gate, 1u, 1, st) != hipSuccess) {
-        u->open = false;
-        return ufail(u, CHIP_E_DEVICE, "gate init");
     }
     uint64_t rounds = 0;
     for (uint32_t chunk = 4; rounds <= b->ntx; chunk = 8) {
@@ -1063,7 +1114,7 @@ static int commit_device(chip_uniq* u, const chip_uniq_shard_batch* b, uint8_t* 
             hipLaunchKernelGGL(k_uniq_gate, dim3(1), dim3(64), 0, st, u->spread.as<unsigned long long>(), gate);
         }
         rounds += chunk;
-        if (hipGetLastError() != hipSuccess || hipMemcpyAsync(u->h_gate, gate, 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        if (hipGetLastError() != hipSuccess || hipMemcpyAsync(u->h_gate, gate, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
             hipStreamSynchronize(st) != hipSuccess) {
             u->open = false;
             return ufail(u, CHIP_E_DEVICE, "ordered-commit rounds");
@@ -1085,7 +1136,7 @@ int chip_uniq_commit_batch_device(chip_uniq* u, uint64_t ntx, const uint64_t* st
     if (!ntx) return CHIP_OK;
     if (u->open) return ufail(u, CHIP_E_ARG, "a shard batch is in flight");
     if (!start || !tx_ids || !callers || !tx_status || (nref && !refs36)) return ufail(u, CHIP_E_ARG, "null argument");
-    if (nref >= 0x7fffffffull || ntx >= 0xffffffffull) return ufail(u, CHIP_E_ARG, "batch too large");
+    if (nref >= 0x7fffffffull || ntx >= 0x7fffffffull) return ufail(u, CHIP_E_ARG, "batch too large");
     UCHK(u, hipSetDevice(u->device));
     hipStream_t st = stream ? (hipStream_t)stream : u->stream;
     UCHK(u, u->refpos.ensure(nref * 4 + 16));
@@ -1104,7 +1155,7 @@ int chip_uniq_commit_batch(chip_uniq* u, uint64_t ntx, const uint64_t* start, co
     if (!ntx) return CHIP_OK;
     const uint64_t nref = start[ntx];
     if (nref && !refs36) return CHIP_E_ARG;
-    if (ntx >= 0xffffffffull || nref >= 0x7fffffffull) return ufail(u, CHIP_E_ARG, "batch too large");
+    if (ntx >= 0x7fffffffull || nref >= 0x7fffffffull) return ufail(u, CHIP_E_ARG, "batch too large");
     if (u->open) return ufail(u, CHIP_E_ARG, "a shard batch is in flight");
     UCHK(u, hipSetDevice(u->device));
     hipStream_t st = u->stream;

@@ -46,7 +46,8 @@ EXPORTS = ["chip_abi_version", "chip_device_count", "chip_init", "chip_shutdown"
            "chip_group_verify_signed_tx_batch", "chip_group_stx_verify", "chip_group_ftx_verify_batch",
            "chip_group_plan_sigs", "chip_group_plan_tx", "chip_group_uniq_open", "chip_group_uniq_close",
            "chip_group_uniq_size", "chip_group_uniq_last_error", "chip_group_state_owner", "chip_group_uniq_rebuild",
-           "chip_group_uniq_commit_batch"]
+           "chip_group_uniq_commit_batch", "chip_uniq_last_rounds", "chip_group_last_stats",
+           "chip_group_uniq_last_stats"]
 
 u8p = ctypes.POINTER(ctypes.c_uint8)
 u32p = ctypes.POINTER(ctypes.c_uint32)
@@ -186,7 +187,21 @@ class ChipStats(ctypes.Structure):
     _fields_ = [("batches", ctypes.c_uint64), ("sigs", ctypes.c_uint64), ("keys_prepared", ctypes.c_uint64),
                 ("status_count", ctypes.c_uint64 * 8), ("txids", ctypes.c_uint64), ("uniq_commits", ctypes.c_uint64),
                 ("last_verify_kernel_ms", ctypes.c_double), ("last_txid_kernel_ms", ctypes.c_double),
-                ("kernel_ms_total", ctypes.c_double * N_KERNELS), ("kernel_launches", ctypes.c_uint64 * N_KERNELS)]
+                ("kernel_ms_total", ctypes.c_double * N_KERNELS), ("kernel_launches", ctypes.c_uint64 * N_KERNELS),
+                ("key_cache_checks", ctypes.c_uint64)]
+
+
+class ChipGroupStats(ctypes.Structure):
+    """chip_group_stats (ABI 10): where the last group call's time went and how it was split."""
+    _fields_ = [("members_used", ctypes.c_uint32), ("rounds", ctypes.c_uint32), ("wall_ms", ctypes.c_double),
+                ("plan_ms", ctypes.c_double), ("rebase_ms", ctypes.c_double), ("member_ms_max", ctypes.c_double),
+                ("member_ms_min", ctypes.c_double), ("exchange_ms", ctypes.c_double), ("rounds_ms", ctypes.c_double),
+                ("finish_ms", ctypes.c_double), ("h2d_bytes_max", ctypes.c_uint64), ("h2d_bytes_total", ctypes.c_uint64),
+                ("exchange_bytes_max", ctypes.c_uint64)]
+
+    def as_dict(self):
+        return {f: round(getattr(self, f), 4) if t is ctypes.c_double else int(getattr(self, f))
+                for f, t in self._fields_}
 
 
 def lib_path() -> str:
@@ -304,6 +319,11 @@ def load(build_if_missing: bool = False):
     lib.chip_group_state_owner.restype = ctypes.c_uint32
     lib.chip_group_uniq_rebuild.argtypes = lib.chip_uniq_rebuild.argtypes
     lib.chip_group_uniq_commit_batch.argtypes = lib.chip_uniq_commit_batch.argtypes
+    # ABI 10
+    lib.chip_uniq_last_rounds.argtypes = [ctypes.c_void_p]
+    lib.chip_uniq_last_rounds.restype = ctypes.c_uint32
+    lib.chip_group_last_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipGroupStats)]
+    lib.chip_group_uniq_last_stats.argtypes = [ctypes.c_void_p, ctypes.POINTER(ChipGroupStats)]
     _lib = lib
     return lib
 
@@ -639,6 +659,24 @@ class UniqTable:
         self._check(self.ctx.lib.chip_uniq_rebuild(self.h, ctypes.c_uint64(n), _ptr(refs36), _ptr(tx32),
                                                    _ptr(idx), _ptr(caller)))
 
+    def last_rounds(self) -> int:
+        """chip_uniq_last_rounds: ordered-commit rounds of the last finished commit."""
+        return int(self.ctx.lib.chip_uniq_last_rounds(self.h))
+
+    def commit_batch_raw(self, tx_ref_start, refs36, tx_ids, callers, cap=None):
+        """chip_uniq_commit_batch with the records left as raw chip_conflict bytes: (statuses, bytes, count)."""
+        ntx = len(tx_ref_start) - 1
+        st = np.zeros(max(ntx, 1), dtype=np.uint8)
+        if cap is None:
+            cap = int(tx_ref_start[-1]) + 1
+        out = np.zeros(max(cap, 1) * ctypes.sizeof(ChipConflict), dtype=np.uint8)
+        nout = ctypes.c_uint64()
+        self._check(self.ctx.lib.chip_uniq_commit_batch(self.h, ctypes.c_uint64(ntx), _ptr(tx_ref_start),
+                                                        _ptr(refs36), _ptr(tx_ids), _ptr(callers), _ptr(st),
+                                                        out.ctypes.data, ctypes.c_uint64(cap), ctypes.byref(nout)))
+        n = int(nout.value)
+        return st[:ntx], out[:min(n, cap) * ctypes.sizeof(ChipConflict)], n
+
     def commit_batch_device(self, tx_ref_start, nref, refs36, tx_ids, callers, tx_status, out, cap, stream=None):
         """Device-resident commit (torch tensors on this GPU).  Returns the full conflict-record count;
         the first min(count, cap) records are in `out` (ChipConflict layout, 48 bytes each)."""
@@ -886,6 +924,12 @@ class Group:
         self._check(self.lib.chip_group_ftx_verify_batch(self.h, ctypes.byref(s), _ptr(status), _ptr(reason)))
         return status[:s.ntx], reason[:s.ntx]
 
+    def last_stats(self) -> dict:
+        """chip_group_last_stats: the last group call's split and host timings."""
+        st = ChipGroupStats()
+        self._check(self.lib.chip_group_last_stats(self.h, ctypes.byref(st)))
+        return st.as_dict()
+
     def uniq_open(self, capacity: int):
         return GroupUniqTable(self, capacity)
 
@@ -921,6 +965,26 @@ class GroupUniqTable:
     def rebuild(self, refs36, tx32, idx, caller):
         self._check(self.lib.chip_group_uniq_rebuild(self.h, ctypes.c_uint64(len(idx)), _ptr(refs36), _ptr(tx32),
                                                      _ptr(idx), _ptr(caller)))
+
+    def last_stats(self) -> dict:
+        """chip_group_uniq_last_stats: the last commit's ingest / exchange / rounds split."""
+        st = ChipGroupStats()
+        self._check(self.lib.chip_group_uniq_last_stats(self.h, ctypes.byref(st)))
+        return st.as_dict()
+
+    def commit_batch_raw(self, tx_ref_start, refs36, tx_ids, callers, cap=None):
+        """The commit with the records left as raw chip_conflict bytes (56 B each): (statuses, bytes, count)."""
+        ntx = len(tx_ref_start) - 1
+        st = np.zeros(max(ntx, 1), dtype=np.uint8)
+        if cap is None:
+            cap = int(tx_ref_start[-1]) + 1
+        out = np.zeros(max(cap, 1) * ctypes.sizeof(ChipConflict), dtype=np.uint8)
+        nout = ctypes.c_uint64()
+        self._check(self.lib.chip_group_uniq_commit_batch(self.h, ctypes.c_uint64(ntx), _ptr(tx_ref_start),
+                                                          _ptr(refs36), _ptr(tx_ids), _ptr(callers), _ptr(st),
+                                                          out.ctypes.data, ctypes.c_uint64(cap), ctypes.byref(nout)))
+        n = int(nout.value)
+        return st[:ntx], out[:min(n, cap) * ctypes.sizeof(ChipConflict)], n
 
     def commit_batch(self, tx_ref_start, refs36, tx_ids, callers, cap=None):
         ntx = len(tx_ref_start) - 1

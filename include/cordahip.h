@@ -46,7 +46,7 @@
 extern "C" {
 #endif
 
-#define CHIP_ABI_VERSION 9
+#define CHIP_ABI_VERSION 10
 
 enum chip_sig_status {
     CHIP_VALID = 0,
@@ -489,6 +489,9 @@ int chip_uniq_commit_batch_device(chip_uniq* u, uint64_t ntx, const uint64_t* tx
                                   void* stream);
 /* Message of the last failing chip_uniq_* call on this table. */
 const char* chip_uniq_last_error(const chip_uniq* u);
+/* Ordered-commit rounds of the last finished commit on this table (ABI 10; the reference commits one
+ * transaction at a time under one lock — the rounds are how many dependency levels the batch had). */
+uint32_t chip_uniq_last_rounds(const chip_uniq* u);
 
 /* ---------------------------------------------------------------------------------------
  * Multi-GPU notary uniqueness: the key space is partitioned across GPUs (owner =
@@ -536,9 +539,13 @@ int chip_uniq_shard_finish(chip_uniq* u, const uint8_t* decision, uint8_t* tx_st
  *     (CHIP_GROUP_MIN_SIGS = 16384 signatures, CHIP_GROUP_MIN_TX = 8192 transactions; env overrides, or
  *     CHIP_GROUP_MIN_SHARE for every entry) runs on one member, rotating;
  *   - uniqueness partitions the StateRef key space: member chip_group_state_owner(ref, n) holds that state's slice
- *     of the commit log; the batch goes to every member, which keeps the inputs it owns (on its device), and the
- *     ordered-commit rounds exchange one vote byte per transaction per round (element-wise MAX, reduced on the
- *     host); records are merged in (tx, input_index) order.
+ *     of the commit log.  Each member copies only a 1/n slice of the batch from the host (a transaction range,
+ *     balanced by inputs), routes its inputs by owner on its device, and every member pulls the inputs it owns
+ *     (and the other slices' ids / callers) from the other members over xGMI (ABI 10; ABI 9 copied the whole batch
+ *     to every member).  The ordered-commit rounds exchange one vote byte per transaction per round between the
+ *     members' devices (each member reduces the element-wise MAX itself), a chunk of rounds at a time without a
+ *     host round trip; records are merged in (tx, input_index) order.  A group of one member is exactly the
+ *     single-context entry.
  * One group call runs at a time (the group serialises them); the member contexts (chip_group_member) may also be
  * used directly, e.g. for device-resident batches. */
 typedef struct chip_group chip_group;
@@ -564,6 +571,25 @@ int chip_group_ftx_verify_batch(chip_group* g, const chip_ftx_batch* batch, uint
 int chip_group_plan_sigs(uint64_t n, const uint32_t* msg_idx, int k, uint64_t min_share, uint64_t* cut);
 int chip_group_plan_tx(uint64_t ntx, const uint64_t* prefix, int k, uint64_t min_share, uint64_t* cut);
 
+/* What the last call of a group (or of a group table) did (ABI 10): where its time went on the host and how the
+ * work was split.  Times in ms of host wall clock. */
+typedef struct {
+    uint32_t members_used;       /* members that received a share (1: the whole call on one member) */
+    uint32_t rounds;             /* uniqueness: ordered-commit rounds of the commit (0 elsewhere) */
+    double wall_ms;              /* the whole call */
+    double plan_ms;              /* the range plan on the caller's thread */
+    double rebase_ms;            /* the slowest member's rebasing of index arrays into its pinned scratch */
+    double member_ms_max;        /* the slowest / fastest member's own part: its single-context entry (uniqueness: */
+    double member_ms_min;        /*   its slice's H2D + routing) */
+    double exchange_ms;          /* uniqueness: the members' input / id exchange and lookups */
+    double rounds_ms;            /* uniqueness: every round, vote exchange included */
+    double finish_ms;            /* uniqueness: classification exchange, inserts, records and their merge */
+    uint64_t h2d_bytes_max;      /* the largest member's host-to-device input bytes */
+    uint64_t h2d_bytes_total;    /* all members' */
+    uint64_t exchange_bytes_max; /* uniqueness: the largest member's owned inputs received (44 B each) */
+} chip_group_stats;
+int chip_group_last_stats(const chip_group* g, chip_group_stats* out);
+
 typedef struct chip_group_uniq chip_group_uniq;
 /* capacity: states of the whole table (each member sizes for its share) */
 int chip_group_uniq_open(chip_group* g, uint64_t capacity, chip_group_uniq** out);
@@ -576,6 +602,7 @@ int chip_group_uniq_rebuild(chip_group_uniq* u, uint64_t n, const uint8_t* refs3
 int chip_group_uniq_commit_batch(chip_group_uniq* u, uint64_t ntx, const uint64_t* tx_ref_start, const uint8_t* refs36,
                                  const uint8_t* tx_ids, const uint32_t* callers, uint8_t* tx_status, chip_conflict* out,
                                  uint64_t cap, uint64_t* n_out);
+int chip_group_uniq_last_stats(const chip_group_uniq* u, chip_group_stats* out);
 
 /* ---------------------------------------------------------------------------------------
  * Counters (observability; OutOfProcessTransactionVerifierService.kt:35-46 analogue). */
@@ -603,6 +630,10 @@ typedef struct {
      * accumulated over every launch since chip_init / chip_reset_stats */
     double kernel_ms_total[CHIP_N_KERNELS];
     uint64_t kernel_launches[CHIP_N_KERNELS];
+    /* CHIP_FLAG_KEY_CACHE (ABI 10): batches whose key pool was compared on the device against the cached one (a
+     * reuse candidate: the key preps and table builds skip when the pools are equal).  A batch after a failed call
+     * is never one: every error return drops the cached key state. */
+    uint64_t key_cache_checks;
 } chip_stats;
 /* Resolves pending timing events (waits for them) and copies the counters. */
 int chip_get_stats(const chip_ctx* ctx, chip_stats* out);

@@ -33,7 +33,7 @@ def test_library_exports_every_header_function():
 
 def test_abi_version_and_device_count():
     lib = corda_amd.load()
-    assert lib.chip_abi_version() == 9
+    assert lib.chip_abi_version() == 10
     assert lib.chip_device_count() >= 0
 
 
@@ -71,8 +71,9 @@ def test_struct_layouts_match_header():
 #include <stdio.h>
 #include <stddef.h>
 int main(void) {
-  printf("%zu %zu %zu %zu %zu\n", sizeof(chip_sig_batch), sizeof(chip_tx_batch), sizeof(chip_conflict),
-         sizeof(chip_stats), offsetof(chip_stats, kernel_ms_total));
+  printf("%zu %zu %zu %zu %zu %zu %zu %zu\n", sizeof(chip_sig_batch), sizeof(chip_tx_batch), sizeof(chip_conflict),
+         sizeof(chip_stats), offsetof(chip_stats, kernel_ms_total), offsetof(chip_stats, key_cache_checks),
+         sizeof(chip_group_stats), offsetof(chip_group_stats, exchange_bytes_max));
   return 0; }
 '''
     import tempfile
@@ -87,6 +88,9 @@ int main(void) {
     assert vals[2] == ctypes.sizeof(native.ChipConflict)
     assert vals[3] == ctypes.sizeof(native.ChipStats)
     assert vals[4] == native.ChipStats.kernel_ms_total.offset
+    assert vals[5] == native.ChipStats.key_cache_checks.offset
+    assert vals[6] == ctypes.sizeof(native.ChipGroupStats)
+    assert vals[7] == native.ChipGroupStats.exchange_bytes_max.offset
 
 
 def test_kryo_registry_defaults_match_the_restatement():

@@ -137,7 +137,7 @@ def test_group_filtered_transactions(group2, ctx):
 
 
 @pytest.mark.parametrize("members", [2, 3])
-def test_group_notary_commit(group2, group3, oracle, members):
+def test_group_notary_commit(group2, group3, ctx, oracle, members):
     """cfg5 shape over key-space shards: pre-committed rows rebuilt into their owners, two batches (the second
     re-spends the first's inputs): statuses, Conflict.stateHistory records in (tx, input_index) order and the
     table size equal the single-table oracle; every member holds only states it owns."""
@@ -147,8 +147,10 @@ def test_group_notary_commit(group2, group3, oracle, members):
     b2.refs[:36 * 4000] = b.refs[:36 * 4000]
     t = g.uniq_open(1 << 16)
     o = oracle.Uniq(1 << 16)
+    one = ctx.uniq_open(1 << 16)                                  # the single context: same rounds
     t.rebuild(*pre)
     o.preload(*pre)
+    one.rebuild(*pre)
     assert t.size() == o.size()
     for batch in (b, b2):
         st, recs = t.commit_batch(batch.tx_ref_start, batch.refs, batch.tx_ids, batch.callers)
@@ -156,11 +158,89 @@ def test_group_notary_commit(group2, group3, oracle, members):
         assert np.array_equal(st, ws)
         assert recs == wr
         assert (st == 2).sum() > 0 and (st == 1).sum() > 0
+        s = t.last_stats()
+        one.commit_batch(batch.tx_ref_start, batch.refs, batch.tx_ids, batch.callers)
+        assert s["rounds"] == one.last_rounds() >= 2
+        # each member staged only its slice of the batch from the host (ABI 10)
+        whole = 8 * (len(batch.tx_ref_start)) + len(batch.refs) + 36 * (len(batch.tx_ref_start) - 1)
+        assert s["members_used"] == members
+        assert abs(s["h2d_bytes_total"] - whole) <= 8 * members
+        assert s["h2d_bytes_max"] < whole / members * 1.25
     assert t.size() == o.size()
+    one.close()
     # capacity: the full count comes back with CHIP_E_CAPACITY
     _, b3 = G.uniq_workload(3000, 0, seed=43, pre_hit=0.0, dbl=0.0)
     b3.refs[:] = b.refs[:len(b3.refs)]
     with pytest.raises(native.ChipError) as e:
         t.commit_batch(b3.tx_ref_start, b3.refs, b3.tx_ids, b3.callers, cap=1)
     assert e.value.code == -4
+    t.close()
+
+
+def test_group_of_one_is_the_single_context(ctx, oracle):
+    """A group of one member: the notary commit is the single-context host entry (statuses, records, rounds), and a
+    verify batch runs whole on the member (members_used 1)."""
+    g = native.Group([0])
+    try:
+        pre, b = G.uniq_workload(20000, 30000, seed=44, pre_hit=0.02, dbl=0.03, resubmit=0.01)
+        t, o, one = g.uniq_open(1 << 16), oracle.Uniq(1 << 16), ctx.uniq_open(1 << 16)
+        t.rebuild(*pre)
+        o.preload(*pre)
+        one.rebuild(*pre)
+        st, raw, n = t.commit_batch_raw(b.tx_ref_start, b.refs, b.tx_ids, b.callers)
+        st1, raw1, n1 = one.commit_batch_raw(b.tx_ref_start, b.refs, b.tx_ids, b.callers)
+        ws, wr = o.commit_batch(b.tx_ref_start, b.refs, b.tx_ids, b.callers)
+        assert np.array_equal(st, ws) and np.array_equal(st, st1)
+        assert n == n1 == len(wr) and np.array_equal(raw, raw1)
+        s = t.last_stats()
+        assert s["members_used"] == 1 and s["rounds"] == one.last_rounds() >= 2
+        t.close()
+        one.close()
+        vb = G.ed25519_batch(20000, n_keys=32, corrupt=0.2, seed=103)
+        st, bm = g.verify_batch(vb)
+        assert np.array_equal(st, vb.expected)
+        assert g.last_stats()["members_used"] == 1
+    finally:
+        g.close()
+
+
+def test_group_concurrent_verify_and_commit(group2, oracle):
+    """Two host threads on one group, one verifying signature batches and one committing notary batches: the group
+    serialises the calls (one member-thread pool), so every result equals the oracle's."""
+    import threading
+    pre, b = G.uniq_workload(6000, 8000, seed=45, pre_hit=0.02, dbl=0.03, resubmit=0.01)
+    vb = G.ed25519_batch(6000, n_keys=16, corrupt=0.2, seed=104)
+    t = group2.uniq_open(1 << 15)
+    t.rebuild(*pre)
+    errors = []
+
+    def verify():
+        try:
+            for _ in range(6):
+                st, _bm = group2.verify_batch(vb)
+                if not np.array_equal(st, vb.expected):
+                    errors.append("verify statuses")
+        except Exception as e:   # noqa: BLE001
+            errors.append(repr(e))
+
+    results = []
+
+    def commit():
+        try:
+            for _ in range(3):
+                results.append(t.commit_batch(b.tx_ref_start, b.refs, b.tx_ids, b.callers))
+        except Exception as e:   # noqa: BLE001
+            errors.append(repr(e))
+
+    th = [threading.Thread(target=verify), threading.Thread(target=commit)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join(timeout=300)
+    assert not errors, errors
+    o = oracle.Uniq(1 << 15)
+    o.preload(*pre)
+    for st, recs in results:                  # the same batch three times: commit, then re-submissions
+        ws, wr = o.commit_batch(b.tx_ref_start, b.refs, b.tx_ids, b.callers)
+        assert np.array_equal(st, ws) and recs == wr
     t.close()

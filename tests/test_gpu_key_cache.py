@@ -80,3 +80,35 @@ def test_key_cache_ecdsa_and_mixed(kctx, oracle):
     check(kctx, oracle, b)
     check(kctx, oracle, e)
     check(kctx, oracle, e)
+
+
+def test_key_cache_state_dropped_after_a_failed_batch(oracle):
+    """A batch that fails after k_key_cache copied its pool (here: CHIP_TEST_FAIL_KEYSTATE forces CHIP_E_NOMEM
+    before the key preps / table builds are enqueued, as a failed allocation would) must not leave the cache
+    describing that pool: the same pool again is rebuilt (no reuse check: key_cache_checks does not move) and its
+    statuses equal the oracle's; the call after that may reuse the rebuilt state."""
+    import corda_amd
+    from corda_amd import native
+    os.environ["CHIP_COMB_MIN_TOTAL"] = "0"
+    os.environ["CHIP_TEST_FAIL_KEYSTATE"] = "2"      # the second key-cache batch fails
+    try:
+        c = corda_amd.Context(0, flags=native.FLAG_KEY_CACHE)
+    finally:
+        del os.environ["CHIP_COMB_MIN_TOTAL"]
+        del os.environ["CHIP_TEST_FAIL_KEYSTATE"]
+    try:
+        p = G.ed25519_batch(4000, n_keys=32, corrupt=0.3, seed=11)
+        q = G.ed25519_batch(4000, n_keys=32, corrupt=0.3, seed=12)   # same key count, other keys
+        check(c, oracle, p)
+        with pytest.raises(native.ChipError) as e:
+            c.verify_batch(q)
+        assert e.value.code == -3
+        before = c.stats().key_cache_checks
+        st = check(c, oracle, q)                      # rebuilt: the failed call's pool copy is not trusted
+        assert np.array_equal(st, q.expected)
+        assert c.stats().key_cache_checks == before
+        check(c, oracle, q)                           # now a reuse candidate again
+        assert c.stats().key_cache_checks == before + 1
+        check(c, oracle, p)
+    finally:
+        c.close()

@@ -2,6 +2,8 @@
 libcordahip) and its key-space routing (chip_group_state_owner) — what decides which member GPU verifies which
 transactions and which member's table slice holds which StateRef.  The group entries themselves run on the GPU
 (tests/test_gpu_group.py)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -78,3 +80,16 @@ def test_group_init_fails_loudly_without_gpu():
         pytest.skip("GPU present")
     with pytest.raises(native.NativeUnavailable):
         native.Group([0, 0])
+
+
+def test_forkjoin_serialises_concurrent_callers(tmp_path):
+    """The group's member-thread pool under 6 concurrent callers: every call's f(i) runs once per member before
+    run() returns, and the first non-zero result comes back (tests/cpp/forkjoin_check.cpp)."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = str(tmp_path / "fj")
+    subprocess.check_call(["g++", "-std=c++17", "-O1", "-pthread", "-I", os.path.join(root, "corda_amd", "csrc"),
+                           "-o", exe, os.path.join(root, "tests", "cpp", "forkjoin_check.cpp")])
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.split() == ["0", "0"]
