@@ -117,6 +117,9 @@ struct chip_uniq {
     const uint32_t* callers = nullptr;
     // scratch
     UBuf reftx, pre, tslot, sid, own, passed, rdup, bmin, bcommit, st, flag, scan, cub, ctr, spread, icount, refpos, gate;
+    UBuf intern, tclaim;                      // the read-only lookup's batch intern and per-ref claim words
+    bool ro = false;                          // CHIP_UNIQ_INTERN=1: read-only lookup + intern, claims at insert
+    bool batch_ro = false;                    // the batch in flight took the read-only lookup
     unsigned long long* h_spread = nullptr;   // pinned host copy of the SPREAD counters
     unsigned long long* h_icount = nullptr;   // pinned host copy of the insert counters
     uint32_t* h_gate = nullptr;               // pinned host copy of the round gate
@@ -294,6 +297,84 @@ __global__ void __launch_bounds__(256) k_uniq_lookup(uint64_t nref, const uint8_
         i = (i + 1) & (cap - 1);
     }
     own[r] = 0;   // full table (not reached: load <= 1/2)
+}
+
+// The read-only lookup (CHIP_UNIQ_INTERN=1): the walk of the commit log only reads; the batch intern is a separate
+// open-addressed table of 8-byte entries (fingerprint << 32 | 1 + owner ref) sized for the batch (~2 entries per
+// input: 256 MB for cfg5's 10M, the size of the Infinity Cache), cleared per batch; the table slot a new state will
+// take is claimed in the insert pass, and only for committed states (k_uniq_insert with ro).
+//   live slot of k         pre[r] = slot (pre-committed), as k_uniq_lookup
+//   else                   tslot[r] = the first claimable slot on k's path (empty, or dead and k's) and
+//                          tclaim[r] its claim word as read; own[r] = OWN_FRESH when it was empty; then
+//   intern CAS won         sid[r] = r (the state's owner in this batch)
+//   intern entry of k      sid[r] = owner, both marked rdup (more than one referencer)
+// Every ref of one state reads the same table (nothing writes it during the lookup), so its refs agree on
+// tslot / tclaim.
+CHIP_DEV uint64_t intern_index(uint64_t h, uint64_t icap) {
+    return ((h >> 32) * 0x9E3779B97F4A7C15ull) >> (64 - __builtin_ctzll(icap));
+}
+__global__ void __launch_bounds__(256) k_uniq_lookup_ro(uint64_t nref, const uint8_t* __restrict__ refs,
+                                                        const uint32_t* __restrict__ tab, uint64_t cap,
+                                                        unsigned long long* __restrict__ intern, uint64_t icap,
+                                                        uint32_t* __restrict__ pre, uint32_t* __restrict__ tslot,
+                                                        unsigned long long* __restrict__ tclaim,
+                                                        uint32_t* __restrict__ sid, uint8_t* __restrict__ rdup,
+                                                        uint8_t* __restrict__ own, unsigned long long* __restrict__ bmin,
+                                                        unsigned long long* __restrict__ bcommit) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= nref) return;
+    uint32_t k[KW];
+    load_key(k, refs, r);
+    const uint64_t h = key_hash(k);
+    uint64_t i = h & (cap - 1);
+    for (uint64_t n = 0; n < cap; n++) {
+        const uint32_t* s = tab + i * SLOT_W;
+        const uint4 a = *reinterpret_cast<const uint4*>(s);
+        const uint4 b = *reinterpret_cast<const uint4*>(s + 4);
+        const uint4 c = *reinterpret_cast<const uint4*>(s + 8);
+        const uint4 d = *reinterpret_cast<const uint4*>(s + 12);
+        const uint32_t used = c.y;
+        const bool eq = line_key_eq(a, b, c.x, k);
+        if (used == 1u && eq) {
+            pre[r] = (uint32_t)i;
+            sid[r] = 0x80000000u | (uint32_t)i;
+            tslot[r] = NO_SLOT;
+            own[r] = 0;
+            return;
+        }
+        if (used == 0u || (used == 2u && eq)) {
+            tslot[r] = (uint32_t)i;
+            tclaim[r] = ((unsigned long long)d.w << 32) | d.z;
+            own[r] = used == 0u ? OWN_FRESH : 0u;
+            break;
+        }
+        i = (i + 1) & (cap - 1);
+    }
+    pre[r] = NO_SLOT;
+    const uint32_t fp = (uint32_t)h | 1u;
+    const unsigned long long mine = ((unsigned long long)fp << 32) | (unsigned long long)(r + 1);
+    uint64_t j = intern_index(h, icap);
+    for (uint64_t n = 0; n < icap; n++) {
+        const unsigned long long prev = atomicCAS(intern + j, 0ull, mine);
+        if (prev == 0ull) {
+            sid[r] = (uint32_t)r;
+            return;
+        }
+        if ((uint32_t)(prev >> 32) == fp) {
+            const uint32_t o = (uint32_t)prev - 1u;
+            uint32_t ok[KW];
+            load_key(ok, refs, o);
+            if (key_eq(ok, k)) {
+                sid[r] = o;
+                rdup[r] = 1;
+                rdup[o] = 1;
+                bmin[o] = ~0ull;
+                bcommit[o] = ~0ull;
+                return;
+            }
+        }
+        j = (j + 1) & (icap - 1);
+    }
 }
 
 // Same-address atomics serialize at the memory side (~13 ns each): a per-wave count into ONE
@@ -556,7 +637,50 @@ struct InsertArgs {
     const uint32_t* callers;
     uint32_t* tab;
     unsigned long long* count;
+    // read-only lookup (k_uniq_lookup_ro): the committing referencer claims its slot here, from the slot / claim
+    // word the lookup saw, walking on past slots other states of this batch claimed first
+    const unsigned long long* tclaim;   // NULL: the slots were claimed by k_uniq_lookup
+    uint64_t cap;
+    uint32_t epoch;
 };
+// the insert-time claim of the read-only path: CAS the claim word seen by the lookup; a slot another state of this
+// batch took first (its claim carries this epoch) is passed, as is any slot not claimable by k.  The line written
+// afterwards keeps the claim word (an emptied claim word could be matched by a stale CAS of another lane).
+CHIP_DEV uint32_t insert_claim(uint32_t* tab, uint64_t cap, uint64_t i, unsigned long long cw, unsigned long long mine,
+                               uint32_t epoch, const uint32_t k[KW], uint32_t& fresh) {
+    for (uint64_t n = 0; n < cap; n++) {
+        uint32_t* s = tab + i * SLOT_W;
+        const unsigned long long prev = atomicCAS(reinterpret_cast<unsigned long long*>(s + S_CLAIM), cw, mine);
+        if (prev == cw) return (uint32_t)i;
+        if ((uint32_t)(prev >> 32) != epoch) {   // the claim word read was stale, the slot is not taken: again
+            cw = prev;
+            continue;
+        }
+        // taken by another state of this batch: walk on to the next claimable slot
+        for (;;) {
+            i = (i + 1) & (cap - 1);
+            s = tab + i * SLOT_W;
+            const uint4 a = *reinterpret_cast<const uint4*>(s);
+            const uint4 b = *reinterpret_cast<const uint4*>(s + 4);
+            const uint4 c = *reinterpret_cast<const uint4*>(s + 8);
+            // the claim word other lanes CAS concurrently: an atomic load, so the value tested here is the value the
+            // CAS expects (a plain load may be re-issued by the compiler between the test and the CAS — measured: a
+            // claim of this epoch read again after the test, CASed over, two states in one slot)
+            cw = __hip_atomic_load(reinterpret_cast<unsigned long long*>(s + S_CLAIM), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)(cw >> 32) == epoch) continue;
+            if (c.y == 0u) {
+                fresh = 1;
+                break;
+            }
+            if (c.y == 2u && line_key_eq(a, b, c.x, k)) {
+                fresh = 0;
+                break;
+            }
+        }
+    }
+    return NO_SLOT;
+}
 // every lane of the wave calls this (the slot stores are wave-cooperative)
 CHIP_DEV void insert_body(uint64_t r, const InsertArgs& a, uint32_t* stage) {
     uint32_t slot = NO_SLOT, live = 0, fresh = 0;
@@ -570,7 +694,7 @@ CHIP_DEV void insert_body(uint64_t r, const InsertArgs& a, uint32_t* stage) {
         if (a.st[t] == ST_COMMITTED && (!a.rdup[r] || first_in_tx(a.sid, a.start[t], r))) {
             write = true;
             live = 1;
-        } else if (o == (uint32_t)r && (a.own[r] & OWN_FRESH)) {
+        } else if (!a.tclaim && o == (uint32_t)r && (a.own[r] & OWN_FRESH)) {
             write = a.passed[r] && (!a.rdup[r] || a.bcommit[o] == ~0ull);
         }
         if (write) {
@@ -583,13 +707,40 @@ CHIP_DEV void insert_body(uint64_t r, const InsertArgs& a, uint32_t* stage) {
                 row[S_IDX] = a.pos[r];
                 row[S_CALLER] = a.callers[t];
             }
-            fresh = (a.own[o] & OWN_FRESH) ? 1u : 0u;
-            slot = a.tslot[r];
+            if (a.tclaim) {   // the slot k_uniq_claim_ro claimed (its claim word is kept in the line)
+                const unsigned long long mine = ((unsigned long long)a.epoch << 32) | (unsigned long long)(r + 1);
+                fresh = (a.own[r] & OWN_FRESH) ? 1u : 0u;
+                slot = a.tslot[r];
+                row[S_CLAIM] = (uint32_t)mine;
+                row[S_CLAIM + 1] = (uint32_t)(mine >> 32);
+                if (slot == NO_SLOT) live = fresh = 0;   // full table (not reached: load <= 1/2)
+            } else {
+                fresh = (a.own[o] & OWN_FRESH) ? 1u : 0u;
+                slot = a.tslot[r];
+            }
         }
     }
     wave_store_slots(a.tab, slot, row, stage);
     spread_add(a.count, live);
     spread_add(a.count + 1, fresh);
+}
+// The read-only path's claims, in a kernel of their own before the inserts: this grid only reads lines and CASes
+// claim words (at the memory side), the insert grid after it only stores whole slots, as the claim path's lookup and
+// inserts do.  (Claims and stores in one grid lost states: a lane that read a 128-B L2 line while walking and then
+// stored one 64-B slot of it can write the line's other half back stale over another XCD's store.)  The claimed slot
+// replaces the hint in tslot[r], and own[r] says whether it was empty.
+__global__ void __launch_bounds__(256) k_uniq_claim_ro(InsertArgs a, uint32_t* __restrict__ tslot, uint8_t* __restrict__ own) {
+    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= a.nref || a.pre[r] != NO_SLOT) return;
+    const uint32_t t = a.ref_tx[r];
+    if (a.st[t] != ST_COMMITTED || (a.rdup[r] && !first_in_tx(a.sid, a.start[t], r))) return;
+    uint32_t k[KW];
+    load_key(k, a.refs, r);
+    uint32_t fresh = (a.own[r] & OWN_FRESH) ? 1u : 0u;
+    const unsigned long long mine = ((unsigned long long)a.epoch << 32) | (unsigned long long)(r + 1);
+    const uint32_t slot = insert_claim(a.tab, a.cap, a.tslot[r], a.tclaim[r], mine, a.epoch, k, fresh);
+    tslot[r] = slot;
+    own[r] = fresh ? OWN_FRESH : 0u;
 }
 __global__ void __launch_bounds__(256) k_uniq_insert(InsertArgs a) {
     __shared__ uint32_t stage[4][64 * STAGE_W];
@@ -773,8 +924,22 @@ static int batch_scratch(chip_uniq* u, uint64_t ntx, uint64_t nref) {
 }
 
 // the lookup / intern / claim pass over n refs (per-batch flags cleared first)
-static int launch_lookup(chip_uniq* u, uint64_t n, const uint8_t* refs, hipStream_t st) {
+static int launch_lookup(chip_uniq* u, uint64_t n, const uint8_t* refs, hipStream_t st, bool ro = false) {
     UCHK(u, hipMemsetAsync(u->rdup.p, 0, n, st));
+    u->batch_ro = ro;
+    if (ro) {
+        const uint64_t icap = pow2_at_least(2 * n);
+        UCHK(u, u->intern.ensure(icap * 8));
+        UCHK(u, u->tclaim.ensure(n * 8 + 16));
+        UCHK(u, hipMemsetAsync(u->intern.p, 0, icap * 8, st));
+        next_epoch(u);   // the inserts' claim epoch
+        hipLaunchKernelGGL(k_uniq_lookup_ro, dim3(blocks_for(n)), dim3(256), 0, st, n, refs, u->tab, u->cap,
+                           u->intern.as<unsigned long long>(), icap, u->pre.as<uint32_t>(), u->tslot.as<uint32_t>(),
+                           u->tclaim.as<unsigned long long>(), u->sid.as<uint32_t>(), u->rdup.as<uint8_t>(),
+                           u->own.as<uint8_t>(), u->bmin.as<unsigned long long>(), u->bcommit.as<unsigned long long>());
+        UCHK(u, hipGetLastError());
+        return CHIP_OK;
+    }
     UCHK(u, hipMemsetAsync(u->passed.p, 0, n, st));
     hipLaunchKernelGGL(k_uniq_lookup, dim3(blocks_for(n)), dim3(256), 0, st, n, refs, u->tab, u->cap, next_epoch(u),
                        u->pre.as<uint32_t>(), u->tslot.as<uint32_t>(), u->sid.as<uint32_t>(), u->rdup.as<uint8_t>(),
@@ -796,6 +961,7 @@ int chip_uniq_open(chip_ctx* ctx, uint64_t capacity, chip_uniq** out) {
         delete u;
         return CHIP_E_DEVICE;
     }
+    if (const char* e = getenv("CHIP_UNIQ_INTERN")) u->ro = e[0] == '1';
     int r = ensure_capacity(u, capacity ? capacity : 1024, u->stream);
     // the ConsumingTx id side table sized for `capacity` rows up front (one row per committed-batch transaction), so
     // the first commits after a rebuild do not regrow and copy it inside the commit
@@ -828,7 +994,7 @@ void chip_uniq_close(chip_uniq* u) {
     UBuf* bufs[] = {&u->reftx,  &u->pre,    &u->tslot,  &u->sid, &u->own, &u->passed, &u->rdup, &u->spread,
                     &u->bmin,   &u->bcommit, &u->st,    &u->flag,  &u->scan,   &u->cub,    &u->ctr,
                     &u->refpos, &u->h_start, &u->h_refs, &u->h_ids, &u->h_call, &u->h_st,  &u->h_vote,
-                    &u->h_out,  &u->gate, &u->icount};
+                    &u->h_out,  &u->gate, &u->icount, &u->intern, &u->tclaim};
     for (UBuf* b : bufs) b->release();
     hipStreamDestroy(u->stream);
     delete u;
@@ -907,7 +1073,7 @@ int chip_uniq_shard_begin(chip_uniq* u, const chip_uniq_shard_batch* b, void* st
     if (ntx)
         hipLaunchKernelGGL(k_ref_tx, dim3(blocks_for(ntx)), dim3(256), 0, st, ntx, u->start, u->reftx.as<uint32_t>(),
                            (uint32_t*)nullptr);
-    if (nref && (r = launch_lookup(u, nref, u->refs, st))) return r;
+    if (nref && (r = launch_lookup(u, nref, u->refs, st, u->ro))) return r;
     UCHK(u, hipGetLastError());
     u->open = true;
     return CHIP_OK;
@@ -994,7 +1160,11 @@ static int launch_insert(chip_uniq* u, uint8_t* classify_vote) {
     const InsertArgs ia{nref, u->refs, u->reftx.as<uint32_t>(), u->pos, u->start, u->st.as<uint8_t>(),
                         u->sid.as<uint32_t>(), u->rdup.as<uint8_t>(), u->pre.as<uint32_t>(), u->tslot.as<uint32_t>(),
                         u->own.as<uint8_t>(), u->passed.as<uint8_t>(), u->bcommit.as<unsigned long long>(), row_base,
-                        u->callers, u->tab, u->icount.as<unsigned long long>()};
+                        u->callers, u->tab, u->icount.as<unsigned long long>(),
+                        u->batch_ro ? u->tclaim.as<unsigned long long>() : nullptr, u->cap, u->epoch};
+    if (u->batch_ro)
+        hipLaunchKernelGGL(k_uniq_claim_ro, dim3(blocks_for(nref)), dim3(256), 0, st, ia, u->tslot.as<uint32_t>(),
+                           u->own.as<uint8_t>());
     if (classify_vote) {
         const uint32_t ib = blocks_for(nref);
         hipLaunchKernelGGL(k_uniq_insert_classify, dim3(ib + blocks_for(ntx)), dim3(256), 0, st, ia, ib,

@@ -14,6 +14,14 @@ pytestmark = pytest.mark.gpu
 COMMITTED, IDEMPOTENT, CONFLICT = 0, 1, 2
 
 
+@pytest.fixture(autouse=True, params=["0", "1"], ids=["claim", "intern"])
+def lookup_mode(request, monkeypatch):
+    """Every test under both lookups (read at chip_uniq_open): the claim CAS on the table line (CHIP_UNIQ_INTERN=0)
+    and the read-only walk + batch intern table with the slot claimed at insert (CHIP_UNIQ_INTERN=1)."""
+    monkeypatch.setenv("CHIP_UNIQ_INTERN", request.param)
+    return request.param
+
+
 def h(s):
     return hashlib.sha256(s.encode()).digest()
 
@@ -198,3 +206,19 @@ def test_commit_log_failure_is_fail_stop_on_gpu(ctx, tmp_path):
     serves the unacknowledged batch again (tests/commit_log_case.py)."""
     from commit_log_case import run_fail_stop
     assert run_fail_stop(ctx, tmp_path) > 0
+
+
+def test_uniq_consumed_states_stay_findable(ctx, oracle):
+    """After a commit into a half-full table (many probe collisions among the batch's new states), every state the
+    batch consumed must be found by the next batch: each of its inputs re-spent by a transaction of its own
+    conflicts exactly where the oracle's does.  (The read-only lookup's insert-time claims once put two colliding
+    states into one slot when a claim word read by a plain load was re-read by the compiler after its test.)"""
+    pre, b0 = G.uniq_workload(5000, 1000, seed=1, pre_hit=0.05, dbl=0.05)
+    nref = len(b0.refs) // 36
+    rng = np.random.Generator(np.random.PCG64(3))
+    probe = G.uniq_batch_from_lists([(rng.bytes(32), [bytes(b0.refs[36 * i:36 * i + 36])], 7) for i in range(nref)])
+    for _ in range(4):
+        outs = run_both(ctx, oracle, pre, [b0, probe], cap=1024)
+        for g, r in outs:
+            assert np.array_equal(g[0], r[0])
+            assert g[1] == r[1]
