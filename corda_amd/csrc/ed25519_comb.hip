@@ -771,7 +771,8 @@ __global__ void __launch_bounds__(256, ED_AHALF_MINW) k_ed_comb_ahalf(const uint
                                                        const int32_t* __restrict__ key_slot,
                                                        const uint32_t* __restrict__ ctab,
                                                        const uint32_t* __restrict__ bmid, uint32_t* __restrict__ xyz,
-                                                       uint64_t cap, uint32_t early) {
+                                                       uint64_t cap, uint32_t early, uint32_t base,
+                                                       uint32_t* __restrict__ flist) {
     const uint32_t ncomb = ctr[ED_CTR_NCOMB];
     const uint32_t p = xcd_block(blockIdx.x, (ncomb + 255) / 256) * blockDim.x + threadIdx.x;
     if (p >= ncomb) return;
@@ -842,7 +843,8 @@ __global__ void __launch_bounds__(256, ED_AHALF_MINW) k_ed_comb_ahalf(const uint
     fe_mul(X, t.X, t.T);
     fe_mul(Y, t.Z, t.Y);
     fe_mul(Z, t.Z, t.T);
-    const uint32_t pe = pwave + __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u));
+    const uint32_t pe = pwave + __builtin_amdgcn_mbcnt_hi(~0u, __builtin_amdgcn_mbcnt_lo(~0u, 0u)) + base;
+    if (flist) flist[pe] = base + list[pe - base];   // deferred finish: the position's signature in the whole batch
 #pragma unroll
     for (int q = 0; q < 10; q++) {
         xyz[(uint64_t)q * cap + pe] = X.v[q];
@@ -863,30 +865,48 @@ CHIP_DEV void ld_fe_soa(fe& f, const uint32_t* __restrict__ base, uint64_t cap, 
                             // compiler's 136 = 3 waves): cfg2 263.4-266.2 vs 260.5-263.2M in 3 same-box rounds
                             // (profiles/r05/ab_r05l.txt; [S]B at 3 waves was slower, 250-256M)
 #endif
+// ALL (the deferred finish of a chunked host batch): positions [0, nall) over every chunk's R', list = flist (the
+// signature of each position in the whole batch, ~0 where a chunk left the position empty: skipped, its Z counted as 1)
+template <bool ALL>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_FINISH_WAVES))) k_ed_comb_finish(const uint32_t* __restrict__ list, const uint32_t* __restrict__ ctr,
                                                         const uint8_t* __restrict__ sig_data,
                                                         const uint64_t* __restrict__ sig_off,
                                                         const uint32_t* __restrict__ xyz, uint32_t* __restrict__ zpre,
-                                                        uint64_t cap, uint8_t* __restrict__ status, uint32_t g) {
-    const uint32_t n = ctr[ED_CTR_NCOMB];
+                                                        uint64_t cap, uint8_t* __restrict__ status, uint32_t g,
+                                                        uint32_t nall) {
+    const uint32_t n = ALL ? nall : ctr[ED_CTR_NCOMB];
     const uint32_t lanes = (n + g - 1) / g;
     const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= lanes) return;
     const uint32_t ne = min(g, (n - l + lanes - 1) / lanes);
     const uint32_t* Zs = xyz + 20 * cap;
     fe acc, z;
+    bool any = false;
     for (uint32_t e = 0; e < ne; e++) {
         const uint64_t p = l + (uint64_t)e * lanes;
-        ld_fe_soa(z, Zs, cap, p);
-        if (e == 0) acc = z;
-        else fe_mul(acc, acc, z);
+        if (ALL) {
+            if (list[p] != 0xffffffffu) {
+                ld_fe_soa(z, Zs, cap, p);
+                if (!any) acc = z;
+                else fe_mul(acc, acc, z);
+                any = true;
+            } else if (!any) {
+                fe_1(acc);
+            }
+        } else {
+            ld_fe_soa(z, Zs, cap, p);
+            if (e == 0) acc = z;
+            else fe_mul(acc, acc, z);
+        }
 #pragma unroll
         for (int q = 0; q < 10; q++) zpre[(uint64_t)q * cap + p] = acc.v[q];
     }
+    if (ALL && !any) return;
     fe inv;
     fe_invert(inv, acc);
     for (int e = (int)ne - 1; e >= 0; e--) {
         const uint64_t p = l + (uint64_t)e * lanes;
+        if (ALL && list[p] == 0xffffffffu) continue;
         fe zi;
         if (e > 0) {
             fe prev;
@@ -982,7 +1002,8 @@ void launch_ed_comb_ahalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, c
     if (!n || !w.max_slots) return;
     const uint32_t blocks = (nblk(n, 256) + 7) & ~7u;   // multiple of 8 for the XCD remap
     hipLaunchKernelGGL(k_ed_comb_ahalf, dim3(blocks), dim3(256), 0, st, w.comb_list, w.ctr, b->key_idx, w.key_slot,
-                       w.ctab, w.bmid, w.xyz, (uint64_t)n, w.early);
+                       w.ctab, w.bmid, w.xyz, w.xyz_cap ? w.xyz_cap : (uint64_t)n, w.early, w.flist ? w.xyz_base : 0u,
+                       w.flist);
 }
 
 void launch_ed_comb_finish(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w, uint8_t* status) {
@@ -998,6 +1019,13 @@ void launch_ed_comb_finish(hipStream_t st, uint64_t n, const chip_sig_batch* b, 
         return e ? (uint32_t)strtoul(e, nullptr, 10) : 32768u;
     }();
     while (g > 4 && n / g < min_lanes) g >>= 1;
-    hipLaunchKernelGGL(k_ed_comb_finish, dim3(nblk((n + g - 1) / g, 256)), dim3(256), 0, st, w.comb_list,
-                       w.ctr, b->sig_data, b->sig_off, w.xyz, w.zpre, (uint64_t)n, status, g);
+    hipLaunchKernelGGL(k_ed_comb_finish<false>, dim3(nblk((n + g - 1) / g, 256)), dim3(256), 0, st, w.comb_list,
+                       w.ctr, b->sig_data, b->sig_off, w.xyz, w.zpre, w.xyz_cap ? w.xyz_cap : (uint64_t)n, status, g, 0u);
+}
+void launch_ed_comb_finish_all(hipStream_t st, uint64_t n, const uint8_t* sig_data, const uint64_t* sig_off,
+                               const EdCombWs& w, uint8_t* status) {
+    if (!n || !w.flist) return;
+    const uint32_t g = ED_FIN_G;
+    hipLaunchKernelGGL(k_ed_comb_finish<true>, dim3(nblk((n + g - 1) / g, 256)), dim3(256), 0, st, w.flist, w.ctr,
+                       sig_data, sig_off, w.xyz, w.zpre, w.xyz_cap, status, g, (uint32_t)n);
 }

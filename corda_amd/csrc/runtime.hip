@@ -199,6 +199,9 @@ struct chip_ctx {
     // cross-batch key state (CHIP_FLAG_KEY_CACHE): the key pool the context's key state (meta, key tables, comb
     // tables) was last built from, the path it was built for, and the buffer generations it lives in
     DevBuf kc_keys, kc_len, kc_flag;
+    DevBuf c_flist;               // the host pipeline's deferred finish: signature of each R' position
+    bool deferred_comb = false;   // the chunks of the host batch in flight took the comb path (finish_all pending)
+    bool defer_finish = true;     // CHIP_HOST_DEFER_FINISH=0: each chunk finishes its own R' (round 5)
     bool kc_valid = false;
     int kc_test_fail = 0, kc_test_seen = 0;   // CHIP_TEST_FAIL_KEYSTATE=n: the n-th key-cache batch fails (tests)
     uint32_t kc_path = 0;
@@ -582,6 +585,7 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
     if (const char* e = getenv("CHIP_STAGING_RING")) c->ring.enabled = e[0] != '0';
     if (const char* e = getenv("CHIP_KERNEL_TIMING")) c->ktiming = e[0] != '0';
     if (const char* e = getenv("CHIP_TEST_FAIL_KEYSTATE")) c->kc_test_fail = atoi(e);
+    if (const char* e = getenv("CHIP_HOST_DEFER_FINISH")) c->defer_finish = e[0] != '0';
     if (const char* e = getenv("CHIP_KRYO_FUSED")) c->kryo_fused = (uint32_t)std::min(2, std::max(0, atoi(e)));
     if (cfg && cfg->reserve_sigs) {
         (void)c->lists.ensure(cfg->reserve_sigs * 4 * N_LISTS);
@@ -596,7 +600,7 @@ void chip_shutdown(chip_ctx* c) {
     hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->meta, &c->abytes, &c->edtab, &c->ectab, &c->lists, &c->counts, &c->c_key_count, &c->c_key_rank,
                       &c->c_key_slot, &c->c_key_base, &c->c_slot_key, &c->c_ctr, &c->c_comb_list,
-                      &c->c_straus_list, &c->c_ctab, &c->c_xyz, &c->c_zpre, &c->c_nega, &c->c_fz, &c->c_bmid, &c->e_ctab, &c->e_mid, &c->e_gcomb, &c->e_bcomb16, &c->e_wp, &c->e_glist, &c->h_key_idx, &c->h_msg_idx,
+                      &c->c_straus_list, &c->c_ctab, &c->c_xyz, &c->c_zpre, &c->c_flist, &c->c_nega, &c->c_fz, &c->c_bmid, &c->e_ctab, &c->e_mid, &c->e_gcomb, &c->e_bcomb16, &c->e_wp, &c->e_glist, &c->h_key_idx, &c->h_msg_idx,
                       &c->h_sig_data, &c->h_sig_off, &c->h_sig_len, &c->h_key_data, &c->h_key_off, &c->h_key_len,
                       &c->h_msg_data, &c->h_msg_off, &c->h_msg_len, &c->h_status, &c->h_bitmap, &c->h_check, &c->t_salts,
                       &c->t_start, &c->t_group, &c->t_internal, &c->t_data, &c->t_off, &c->t_len, &c->t_ids,
@@ -699,6 +703,8 @@ struct VerifyChunk {
     bool reuse_keys;
     hipEvent_t data_ready;   // the chunk's signatures / pools are on the device (waited for after the key prep)
     bool keys_only;          // size the workspaces for b->n, prep the keys, fork the table builds, and stop
+    bool defer = false;      // the comb path's finish and the bitmap run once after the last chunk (finish_all): the
+    uint64_t base = 0;       //   chunk's R' go to positions base.. of an xyz sized for the whole batch (n_decide)
 };
 
 // present (host entries only): the schemes whose keys occur in the key pool, read from the key lengths on the host
@@ -754,8 +760,13 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         HIPCHK(c, c->c_comb_list.ensure(n * 4 + 16));
         HIPCHK(c, c->c_straus_list.ensure(n * 4 + 16));
         HIPCHK(c, c->c_ctab.ensure(slots * key_bytes + 16));
-        HIPCHK(c, c->c_xyz.ensure(n * 30 * 4 + 16));
-        HIPCHK(c, c->c_zpre.ensure(n * 10 * 4 + 16));
+        const uint64_t xcap = (vc && vc->defer) ? nd : n;   // deferred finish: every chunk's R' side by side
+        HIPCHK(c, c->c_xyz.ensure(xcap * 30 * 4 + 16));
+        HIPCHK(c, c->c_zpre.ensure(xcap * 10 * 4 + 16));
+        if (vc && vc->defer) HIPCHK(c, c->c_flist.ensure(xcap * 4 + 16));
+        w.xyz_cap = xcap;
+        w.xyz_base = (vc && vc->defer) ? (uint32_t)vc->base : 0u;
+        w.flist = (vc && vc->defer) ? c->c_flist.as<uint32_t>() : nullptr;
         HIPCHK(c, c->c_nega.ensure(nk * 40 * 4 + 16));
         if (ED_COMB_AFFINE) HIPCHK(c, c->c_fz.ensure(2 * slots * ED_COMB_AWIN * 10 * 4 + 16));
         HIPCHK(c, c->c_bmid.ensure(n * ed_comb_bmid_words() * 4 + 16));
@@ -964,9 +975,11 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
             ke = c->kbegin(CHIP_K_ED_COMB, st);
             launch_ed_comb_ahalf(st, n, b, w);
             c->kend(ke, st);
-            ke = c->kbegin(CHIP_K_ED_FINISH, st);
-            launch_ed_comb_finish(st, n, b, w, status);
-            c->kend(ke, st);
+            if (!w.flist) {   // deferred: finish_all after the host pipeline's last chunk
+                ke = c->kbegin(CHIP_K_ED_FINISH, st);
+                launch_ed_comb_finish(st, n, b, w, status);
+                c->kend(ke, st);
+            }
             ed_list = w.straus_list;
             ed_count = w.ctr + 2;
         }
@@ -999,8 +1012,10 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
                                 c->ectab.as<uint32_t>(), status);
             c->kend(ke, st);
         }
-        if (bitmap) hipLaunchKernelGGL(k_bitmap, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, n, status, bitmap);
+        if (bitmap && !(vc && vc->defer))
+            hipLaunchKernelGGL(k_bitmap, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, n, status, bitmap);
     }
+    if (vc && vc->defer) c->deferred_comb = comb;
     HIPCHK(c, hipGetLastError());
     HIPCHK(c, hipEventRecord(c->ev1, st));
     c->ev_pending = true;
@@ -1270,10 +1285,13 @@ static int verify_host_pipelined(chip_ctx* c, const chip_sig_batch* b, uint8_t* 
         d.msg_idx = c->h_msg_idx.as<uint32_t>();
         d.sig_off = c->h_sig_off.as<uint64_t>();
         d.sig_len = c->h_sig_len.as<uint32_t>();
-        const VerifyChunk kv{n, false, nullptr, true};
+        VerifyChunk kv{n, false, nullptr, true};
+        kv.defer = c->defer_finish;
+        c->deferred_comb = false;
         if ((r = verify_device_locked(c, &d, c->h_status.as<uint8_t>(), c->h_bitmap.as<uint64_t>(), st, is_valid, &kv,
                                       present)))
             return r;
+        if (kv.defer && c->c_flist.p) HIPCHK(c, hipMemsetAsync(c->c_flist.p, 0xff, n * 4, st));
     }
     if ((r = stage_chunk(0))) {
         hipStreamSynchronize(st);
@@ -1286,7 +1304,9 @@ static int verify_host_pipelined(chip_ctx* c, const chip_sig_batch* b, uint8_t* 
         d.msg_idx = c->h_msg_idx.as<uint32_t>() + a;
         d.sig_off = c->h_sig_off.as<uint64_t>() + a;
         d.sig_len = c->h_sig_len.as<uint32_t>() + a;
-        const VerifyChunk vc{n, true, c->hev_p, false};
+        VerifyChunk vc{n, true, c->hev_p, false};
+        vc.defer = c->defer_finish;
+        vc.base = a;
         if ((r = verify_device_locked(c, &d, c->h_status.as<uint8_t>() + a, c->h_bitmap.as<uint64_t>() + a / 64, st,
                                       is_valid, &vc, present))) {
             hipStreamSynchronize(st);
@@ -1296,6 +1316,23 @@ static int verify_host_pipelined(chip_ctx* c, const chip_sig_batch* b, uint8_t* 
             hipStreamSynchronize(st);
             return r;
         }
+    }
+    if (c->defer_finish) {   // every chunk's R' in one batched inversion (full-size lanes, one inversion latency), then
+                             // the bitmap of the whole batch
+        if (c->deferred_comb) {
+            EdCombWs w{};
+            w.xyz = c->c_xyz.as<uint32_t>();
+            w.zpre = c->c_zpre.as<uint32_t>();
+            w.flist = c->c_flist.as<uint32_t>();
+            w.xyz_cap = n;
+            const int ke = c->kbegin(CHIP_K_ED_FINISH, st);
+            launch_ed_comb_finish_all(st, n, c->h_sig_data.as<uint8_t>(), c->h_sig_off.as<uint64_t>(), w,
+                                      c->h_status.as<uint8_t>());
+            c->kend(ke, st);
+        }
+        if (bitmap)
+            hipLaunchKernelGGL(k_bitmap, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, n, c->h_status.as<uint8_t>(),
+                               c->h_bitmap.as<uint64_t>());
     }
     unsigned long long counts[8] = {0, 0, 0, 0, 0, 0, 0, 0};
     HIPCHK(c, hipMemsetAsync(c->h_check.p, 0, 64, st));

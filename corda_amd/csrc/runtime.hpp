@@ -209,6 +209,10 @@ struct EdCombWs {
     uint32_t eager;        // tables for every Ed25519 key at slot = key index, built during classify
     uint32_t early;        // eager device-entry batches: hash and [S]B over the whole batch (slot = signature
                            // index) from the start, while the key prep and the tables run on the second stream
+    uint64_t xyz_cap;      // SoA stride of xyz / zpre: the batch's n, or the whole host batch's (deferred finish)
+    uint32_t xyz_base;     // deferred finish: the chunk's first signature = its first R' position in xyz / flist
+    uint32_t* flist;       // deferred finish (host pipeline): [xyz_cap] signature index of each R' position, ~0 = none;
+                           // null: the batch's own finish runs after its table half
 };
 
 // slots (partition = false) or the key-grouped work list (partition = true)
@@ -229,6 +233,9 @@ void launch_ed_comb_bhalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, c
                           const EdCombWs& w, int part = 0);
 void launch_ed_comb_ahalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w);
 void launch_ed_comb_finish(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w, uint8_t* status);
+// the deferred finish of a chunked host batch: every chunk's R' (positions [0, n), flist) in one batched inversion
+void launch_ed_comb_finish_all(hipStream_t st, uint64_t n, const uint8_t* sig_data, const uint64_t* sig_off,
+                               const EdCombWs& w, uint8_t* status);
 
 // ---- host-entry argument checks on the device (runtime.hip dev_check) ----
 enum { DEV_CHECK_MONOTONE = 0, DEV_CHECK_RANGE = 1, DEV_CHECK_INDEX = 2 };
