@@ -164,6 +164,9 @@ object CordaHip {
     @JvmStatic external fun groupUniqCommitBatch(uniq: Long, ntx: Int, txRefStart: ByteBuffer, refs: ByteBuffer,
                                                  txIds: ByteBuffer, callers: ByteBuffer, status: ByteBuffer,
                                                  out: ByteBuffer, cap: Int, nOut: LongArray): Int
+    // ABI 10: where the last group call (uniq == 0) or group-table commit spent its time, chip_group_stats order
+    @JvmStatic external fun groupLastStats(group: Long, uniq: Long, out: DoubleArray): Int
+    @JvmStatic external fun uniqLastRounds(uniq: Long): Int
 }
 
 /**

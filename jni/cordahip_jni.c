@@ -556,3 +556,27 @@ JNIEXPORT jint JNICALL CLS(groupUniqCommitBatch)(JNIEnv* env, jclass cls, jlong 
     (void)cls;
     return uniq_commit(env, 1, u, ntx, txRefStart, refs, txIds, callers, status, out, cap, nOut);
 }
+
+/* where the last group call's time went (chip_group_last_stats): into a DoubleArray of 13 entries in the order of
+ * chip_group_stats (members_used, rounds, wall_ms, plan_ms, rebase_ms, member_ms_max, member_ms_min, exchange_ms,
+ * rounds_ms, finish_ms, h2d_bytes_max, h2d_bytes_total, exchange_bytes_max); uniq != 0: the group table's last
+ * commit instead (chip_group_uniq_last_stats) */
+JNIEXPORT jint JNICALL CLS(groupLastStats)(JNIEnv* env, jclass cls, jlong g, jlong u, jdoubleArray out) {
+    (void)cls;
+    chip_group_stats s;
+    const int r = u ? chip_group_uniq_last_stats((const chip_group_uniq*)(intptr_t)u, &s)
+                    : chip_group_last_stats((const chip_group*)(intptr_t)g, &s);
+    if (r != CHIP_OK) return r;
+    if (!out || (*env)->GetArrayLength(env, out) < 13) return CHIP_E_ARG;
+    const jdouble v[13] = {(jdouble)s.members_used, (jdouble)s.rounds, s.wall_ms, s.plan_ms, s.rebase_ms,
+                           s.member_ms_max, s.member_ms_min, s.exchange_ms, s.rounds_ms, s.finish_ms,
+                           (jdouble)s.h2d_bytes_max, (jdouble)s.h2d_bytes_total, (jdouble)s.exchange_bytes_max};
+    (*env)->SetDoubleArrayRegion(env, out, 0, 13, v);
+    return CHIP_OK;
+}
+
+/* ordered-commit rounds of the table's last commit (chip_uniq_last_rounds) */
+JNIEXPORT jint JNICALL CLS(uniqLastRounds)(JNIEnv* env, jclass cls, jlong u) {
+    (void)env; (void)cls;
+    return (jint)chip_uniq_last_rounds((const chip_uniq*)(intptr_t)u);
+}

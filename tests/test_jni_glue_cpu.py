@@ -22,6 +22,8 @@ typedef jobject jstring;
 typedef jobject jlongArray;
 typedef jobject jintArray;
 typedef jobject jarray;
+typedef double jdouble;
+typedef jobject jdoubleArray;
 struct JNINativeInterface_;
 typedef const struct JNINativeInterface_* JNIEnv;
 struct JNINativeInterface_ {
@@ -32,6 +34,7 @@ struct JNINativeInterface_ {
     void (*SetLongArrayRegion)(JNIEnv*, jlongArray, jsize, jsize, const jlong*);
     jsize (*GetArrayLength)(JNIEnv*, jarray);
     void (*GetIntArrayRegion)(JNIEnv*, jintArray, jsize, jsize, jint*);
+    void (*SetDoubleArrayRegion)(JNIEnv*, jdoubleArray, jsize, jsize, const jdouble*);
 };
 #define JNIEXPORT __attribute__((visibility("default")))
 #define JNICALL
@@ -42,7 +45,7 @@ EXPECTED = ["open", "close", "lastError", "allocPinned", "freePinned", "verifyBa
             "uniqRebuild", "uniqCommitBatch", "groupOpen", "groupClose", "groupLastError", "groupSize", "groupMember",
             "groupVerifyBatch", "groupTxIds", "groupVerifySignedTxBatch", "groupFtxVerify", "groupStxVerify",
             "groupUniqOpen", "groupUniqClose", "groupUniqSize", "groupUniqLastError", "groupUniqRebuild",
-            "groupUniqCommitBatch"]
+            "groupUniqCommitBatch", "groupLastStats", "uniqLastRounds"]
 
 
 def test_jni_glue_compiles_and_links(tmp_path):
