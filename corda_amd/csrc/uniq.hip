@@ -118,6 +118,7 @@ struct chip_uniq {
     // scratch
     UBuf reftx, pre, tslot, sid, own, passed, rdup, bmin, bcommit, st, flag, scan, cub, ctr, spread, icount, refpos, gate;
     UBuf intern, tclaim;                      // the read-only lookup's batch intern and per-ref claim words
+    UBuf dlist;                               // dup refs of the batch (ctr word 0 counts them)
     bool ro = false;                          // CHIP_UNIQ_INTERN=1: read-only lookup + intern, claims at insert
     bool batch_ro = false;                    // the batch in flight took the read-only lookup
     unsigned long long* h_spread = nullptr;   // pinned host copy of the SPREAD counters
@@ -225,6 +226,18 @@ CHIP_DEV void tab_put(uint32_t* tab, uint64_t cap, uint64_t i0, const uint32_t k
 #define OWN_CLAIM 1u
 #define OWN_FRESH 2u
 
+// Appends val to a list from every lane currently active here, one atomic per wave (the lanes of a divergent walk that
+// reach this point together aggregate; others append in their own group)
+CHIP_DEV void wave_append(uint32_t* __restrict__ ctr, uint32_t* __restrict__ list, uint32_t val) {
+    const uint64_t m = __ballot(1);
+    const uint32_t leader = (uint32_t)__builtin_ctzll(m);
+    const uint32_t pre = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    uint32_t base = 0;
+    if (pre == 0) base = atomicAdd(ctr, (uint32_t)__popcll(m));
+    base = (uint32_t)__shfl((int)base, (int)leader);
+    list[base + pre] = val;
+}
+
 // lookup + intern + claim, one probe walk per ref:
 //   live slot of k       pre[r] = slot; sid[r] = 0x80000000 | slot (pre-committed; no claim)
 //   claimable slot       CAS the claim word: won -> sid[r] = r (r owns the state in this batch)
@@ -238,7 +251,8 @@ __global__ void __launch_bounds__(256) k_uniq_lookup(uint64_t nref, const uint8_
                                                      uint32_t* __restrict__ sid, uint8_t* __restrict__ rdup,
                                                      uint8_t* __restrict__ own, uint8_t* __restrict__ passed,
                                                      unsigned long long* __restrict__ bmin,
-                                                     unsigned long long* __restrict__ bcommit) {
+                                                     unsigned long long* __restrict__ bcommit,
+                                                     uint32_t* __restrict__ dcount, uint32_t* __restrict__ dlist) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nref) return;
     uint32_t k[KW];
@@ -278,6 +292,7 @@ __global__ void __launch_bounds__(256) k_uniq_lookup(uint64_t nref, const uint8_
                         // writes the same values): no memset of the scratch per batch or per round
                         bmin[o] = ~0ull;
                         bcommit[o] = ~0ull;
+                        wave_append(dcount, dlist, (uint32_t)r);   // the rounds' work list: refs of dup states
                         return;
                     }
                     passed[o] = 1;
@@ -320,7 +335,8 @@ __global__ void __launch_bounds__(256) k_uniq_lookup_ro(uint64_t nref, const uin
                                                         unsigned long long* __restrict__ tclaim,
                                                         uint32_t* __restrict__ sid, uint8_t* __restrict__ rdup,
                                                         uint8_t* __restrict__ own, unsigned long long* __restrict__ bmin,
-                                                        unsigned long long* __restrict__ bcommit) {
+                                                        unsigned long long* __restrict__ bcommit,
+                                                        uint32_t* __restrict__ dcount, uint32_t* __restrict__ dlist) {
     const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= nref) return;
     uint32_t k[KW];
@@ -370,6 +386,7 @@ __global__ void __launch_bounds__(256) k_uniq_lookup_ro(uint64_t nref, const uin
                 rdup[o] = 1;
                 bmin[o] = ~0ull;
                 bcommit[o] = ~0ull;
+                wave_append(dcount, dlist, (uint32_t)r);
                 return;
             }
         }
@@ -405,23 +422,30 @@ __global__ void __launch_bounds__(256) k_ref_tx(uint64_t ntx, const uint64_t* __
 // round) holds the previous round's undecided count; a round that starts with none left exits at once.
 CHIP_DEV bool round_closed(const uint32_t* gate) { return gate && __builtin_nontemporal_load(gate) == 0u; }
 
-// over the refs of dup states only (a state with one referencer needs no minimum).  bmin[s] =
-// (tag << 32) | t with tag = ~round: a later round's entries are smaller than any stale entry of an
-// earlier round, so the minimum needs no reset between rounds, and a reader (itself a live
-// referencer of s, so a writer in this round) always sees this round's minimum.
-// (A dup-ref list compacted after the lookup cut the four rounds' round_min from 0.108 to 0.031 ms, but the
-// DeviceSelect over 10M flags cost 0.095 ms: measured, not kept.)
-__global__ void __launch_bounds__(256) k_uniq_round_min(uint64_t nref, const uint8_t* __restrict__ rdup,
-                                                        const uint32_t* __restrict__ ref_tx,
-                                                        const uint32_t* __restrict__ sid,
-                                                        const uint8_t* __restrict__ st,
-                                                        unsigned long long* __restrict__ bmin, uint32_t tag,
-                                                        const uint32_t* gate) {
+// first(s) over the refs of dup states only (a state with one referencer needs no minimum), from the list of dup
+// refs the lookup appended (each a referencer that met its state's claim; the state's owner, its first referencer,
+// is sid[r] and is taken along by each of them — atomicMin is idempotent): ~5 % of the refs in cfg5 instead of a
+// pass over all of them per round (round 5's pass over 10M rdup flags: 0.027 ms a round; a list compacted by a
+// DeviceSelect over them after the lookup cost 0.095 ms; appended by the lookup's dup branch it costs one atomic per
+// wave that finds dups).  bmin[s] = (tag << 32) | t with tag = ~round: a later round's entries are smaller than any
+// stale entry of an earlier round, so the minimum needs no reset between rounds, and a reader (itself a live
+// referencer of s, so a writer in this round) always sees this round's minimum.  Fixed grid, strided over the list.
+__global__ void __launch_bounds__(256) k_uniq_round_min_list(const uint32_t* __restrict__ dlist,
+                                                             const uint32_t* __restrict__ dcount,
+                                                             const uint32_t* __restrict__ ref_tx,
+                                                             const uint32_t* __restrict__ sid,
+                                                             const uint8_t* __restrict__ st,
+                                                             unsigned long long* __restrict__ bmin, uint32_t tag,
+                                                             const uint32_t* gate) {
     if (round_closed(gate)) return;
-    const uint64_t r = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (r >= nref || !rdup[r]) return;
-    const uint32_t t = ref_tx[r];
-    if (st[t] != ST_FAILED) atomicMin(&bmin[sid[r]], ((unsigned long long)tag << 32) | t);
+    const uint32_t n = *dcount;
+    for (uint32_t q = blockIdx.x * blockDim.x + threadIdx.x; q < n; q += gridDim.x * blockDim.x) {
+        const uint32_t r = dlist[q];
+        const uint32_t s = sid[r];
+        const uint32_t t = ref_tx[r], to = ref_tx[s];
+        if (st[t] != ST_FAILED) atomicMin(&bmin[s], ((unsigned long long)tag << 32) | t);
+        if (st[to] != ST_FAILED) atomicMin(&bmin[s], ((unsigned long long)tag << 32) | to);
+    }
 }
 
 // votes read only the previous round's status bytes (st is written by k_uniq_apply alone), so a
@@ -914,6 +938,7 @@ static int batch_scratch(chip_uniq* u, uint64_t ntx, uint64_t nref) {
     UCHK(u, u->flag.ensure(std::max(nref, ntx) * 4 + 16));   // per-tx record counts
     UCHK(u, u->scan.ensure(std::max(nref, ntx) * 4 + 16));
     UCHK(u, u->bmin.ensure(nref * 8 + 16));                  // per state, indexed by its owner ref
+    UCHK(u, u->dlist.ensure(nref * 4 + 16));                 // refs of dup states (the lookup's list)
     UCHK(u, u->gate.ensure(64));
     UCHK(u, u->bcommit.ensure(nref * 8 + 16));
     UCHK(u, u->st.ensure(ntx + 16));
@@ -926,6 +951,7 @@ static int batch_scratch(chip_uniq* u, uint64_t ntx, uint64_t nref) {
 // the lookup / intern / claim pass over n refs (per-batch flags cleared first)
 static int launch_lookup(chip_uniq* u, uint64_t n, const uint8_t* refs, hipStream_t st, bool ro = false) {
     UCHK(u, hipMemsetAsync(u->rdup.p, 0, n, st));
+    UCHK(u, hipMemsetAsync(u->ctr.p, 0, 4, st));   // the dup-ref list's count
     u->batch_ro = ro;
     if (ro) {
         const uint64_t icap = pow2_at_least(2 * n);
@@ -936,7 +962,8 @@ static int launch_lookup(chip_uniq* u, uint64_t n, const uint8_t* refs, hipStrea
         hipLaunchKernelGGL(k_uniq_lookup_ro, dim3(blocks_for(n)), dim3(256), 0, st, n, refs, u->tab, u->cap,
                            u->intern.as<unsigned long long>(), icap, u->pre.as<uint32_t>(), u->tslot.as<uint32_t>(),
                            u->tclaim.as<unsigned long long>(), u->sid.as<uint32_t>(), u->rdup.as<uint8_t>(),
-                           u->own.as<uint8_t>(), u->bmin.as<unsigned long long>(), u->bcommit.as<unsigned long long>());
+                           u->own.as<uint8_t>(), u->bmin.as<unsigned long long>(), u->bcommit.as<unsigned long long>(),
+                           u->ctr.as<uint32_t>(), u->dlist.as<uint32_t>());
         UCHK(u, hipGetLastError());
         return CHIP_OK;
     }
@@ -944,7 +971,7 @@ static int launch_lookup(chip_uniq* u, uint64_t n, const uint8_t* refs, hipStrea
     hipLaunchKernelGGL(k_uniq_lookup, dim3(blocks_for(n)), dim3(256), 0, st, n, refs, u->tab, u->cap, next_epoch(u),
                        u->pre.as<uint32_t>(), u->tslot.as<uint32_t>(), u->sid.as<uint32_t>(), u->rdup.as<uint8_t>(),
                        u->own.as<uint8_t>(), u->passed.as<uint8_t>(), u->bmin.as<unsigned long long>(),
-                       u->bcommit.as<unsigned long long>());
+                       u->bcommit.as<unsigned long long>(), u->ctr.as<uint32_t>(), u->dlist.as<uint32_t>());
     UCHK(u, hipGetLastError());
     return CHIP_OK;
 }
@@ -994,7 +1021,7 @@ void chip_uniq_close(chip_uniq* u) {
     UBuf* bufs[] = {&u->reftx,  &u->pre,    &u->tslot,  &u->sid, &u->own, &u->passed, &u->rdup, &u->spread,
                     &u->bmin,   &u->bcommit, &u->st,    &u->flag,  &u->scan,   &u->cub,    &u->ctr,
                     &u->refpos, &u->h_start, &u->h_refs, &u->h_ids, &u->h_call, &u->h_st,  &u->h_vote,
-                    &u->h_out,  &u->gate, &u->icount, &u->intern, &u->tclaim};
+                    &u->h_out,  &u->gate, &u->icount, &u->intern, &u->tclaim, &u->dlist};
     for (UBuf* b : bufs) b->release();
     hipStreamDestroy(u->stream);
     delete u;
@@ -1085,9 +1112,9 @@ static void launch_round_vote(chip_uniq* u, uint8_t* vote, const uint32_t* gate)
     u->round++;
     const uint32_t tag = ~u->round;
     if (u->nref)
-        hipLaunchKernelGGL(k_uniq_round_min, dim3(blocks_for(u->nref)), dim3(256), 0, st, u->nref, u->rdup.as<uint8_t>(),
-                           u->reftx.as<uint32_t>(), u->sid.as<uint32_t>(), u->st.as<uint8_t>(),
-                           u->bmin.as<unsigned long long>(), tag, gate);
+        hipLaunchKernelGGL(k_uniq_round_min_list, dim3(std::min<uint32_t>(blocks_for(u->nref), 1024u)), dim3(256), 0, st,
+                           u->dlist.as<uint32_t>(), u->ctr.as<uint32_t>(), u->reftx.as<uint32_t>(), u->sid.as<uint32_t>(),
+                           u->st.as<uint8_t>(), u->bmin.as<unsigned long long>(), tag, gate);
     if (u->ntx)
         hipLaunchKernelGGL(k_uniq_vote, dim3(blocks_for(u->ntx)), dim3(256), 0, st, u->ntx, u->start,
                            u->pre.as<uint32_t>(), u->sid.as<uint32_t>(), u->rdup.as<uint8_t>(),
