@@ -90,7 +90,7 @@ ECDSA_Q_MACS_PER_VERIFY = 65 * 592 + 100                            # k_ecdsa_co
 SHA256_OPS_PER_COMPRESSION = 2_168
 # HBM traffic per launch comes from the committed PMC passes of the same command (tools/profile.sh):
 # FETCH_SIZE + WRITE_SIZE (KiB) of the launch with the same grid
-PROFILE_DIR = os.path.join(ROOT, "profiles", os.environ.get("CORDA_PROFILE_DIR", "r05"))
+PROFILE_DIR = os.path.join(ROOT, "profiles", os.environ.get("CORDA_PROFILE_DIR", "r06"))
 # VALU rooflines (profiles/r04/microbench_valu*.txt, tools/microbench_valu.hip):
 #   a wave64 VALU instruction issues in 2 cycles per SIMD only for the dual-issue opcodes (v_add/sub/and/or/xor/
 #   mov/lshrrev_b32, v_bitop3_b32, v_fma_f32: 2.3-2.6 cycles measured at 2-8 waves); every other opcode —
