@@ -80,6 +80,11 @@ ED_COMB_MACS_PER_VERIFY = ED_COMB_MACS_A + ED_COMB_MACS_B          # 45,500
 #   (doubling-chain conversions 819, 64 cached A-adds 256 + conversions 192, 32 B-madds 224, 11 + 2
 #   inversion/encode)
 ED_STRAUS_MACS_PER_VERIFY = 1_262 * 55 + 1_504 * 100                # 219,810
+#   the split Straus path (round 6, default): the kernel time of the cold leg's K_ED25519 bracket is
+#   k_ed25519_verify_a + the batched finish (the hash and [S]B run beside the key prep, outside it):
+#   verify_a 252 doublings (1,008 squarings) + 63 A-adds with their conversions (1,260 mults) + 19 for
+#   the first window and + [S]B; the finish at 4 signatures per inversion 254 / 4 squarings + ~8 mults
+ED_STRAUS_SPLIT_MACS_PER_VERIFY = (1_008 + 64) * 55 + (1_279 + 8) * 100   # 187,660
 #   ECDSA comb (P-256 / secp256k1, 8 x 32-bit limbs): a mixed addition = 7 mults (64 products) +
 #   4 squarings (36) = 592; 17 G windows (radix 2^16) + 65 Q windows (radix 16) = 82 additions;
 #   17 scalar Montgomery mults (128 each: s R, 12 wave-scan, 2 finalize, u1, u2) + the x(R) check (100)
@@ -492,7 +497,7 @@ def main():
         ctx.free_pinned()
 
     progress("cfg2 host path done")
-    # ---- cold keys: every signature its own key (windowed Straus kernel) ----
+    # ---- cold keys: every signature its own key (the split Straus path; CHIP_ED_STRAUS_SPLIT=0 the fused kernel) ----
     if args.cold_n:
         cb = G.ed25519_batch(args.cold_n, n_keys=args.cold_n, seed=0x5EED0012 + rank, threads=gen_threads)
         dc = upload(cb, SIG_FIELDS, torch, dev)
@@ -508,16 +513,20 @@ def main():
                           world, torch, dev, dist)
         sc = ctx.stats()
         st_ms = kms(sc, native.K_ED25519)
+        cold_split = os.environ.get("CHIP_ED_STRAUS_SPLIT", "1") != "0"
         c_arith = int(((cb.expected == 0) | (cb.expected == 1)).sum())
         secondary.update({
             "ed25519_cold_sigs_per_s": world * cb.n * max(2, args.steps) / cel,
-            "ed25519_cold_workload": "%d Ed25519 signatures, every one by its own key (key decode + windowed Straus "
-                                     "kernel, 10%% corrupted)" % cb.n,
+            "ed25519_cold_workload": "%d Ed25519 signatures, every one by its own key (key decode + Straus "
+                                     "schedule, 10%% corrupted)" % cb.n,
             "ed25519_cold_correct": cok,
             "ed25519_cold_ms_per_batch": cel / max(2, args.steps) * 1e3,
             "ed25519_cold_keyprep_ms": kms(sc, native.K_KEYPREP),
             "ed25519_cold_straus_ms": st_ms,
-            "ed25519_cold_roofline_frac": ED_STRAUS_MACS_PER_VERIFY * c_arith / (st_ms * 1e-3) / 1e12 / MAC_PEAK_T,
+            "ed25519_cold_roofline_frac": (ED_STRAUS_SPLIT_MACS_PER_VERIFY if cold_split else ED_STRAUS_MACS_PER_VERIFY)
+            * c_arith / (st_ms * 1e-3) / 1e12 / MAC_PEAK_T,
+            "ed25519_cold_schedule": "split Straus: hash + [S]B comb beside the key prep, k_ed25519_verify_a + batched "
+                                     "finish" if cold_split else "fused k_ed25519_verify",
         })
         del dc, cst, cbm, cb
 

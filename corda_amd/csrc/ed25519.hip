@@ -26,8 +26,9 @@ __device__ __constant__ const uint8_t SPKI_ED[12] = {0x30, 0x2a, 0x30, 0x05, 0x0
 // ---- K1b: per unique key.  Ed25519 keys only; other schemes are handled by ecdsa.hip ----
 // TABLE = false (eager comb batches): no Straus table, so the kernel needs a third of the registers and its
 // workgroups find room beside the batch-wide kernels it runs next to
-template <bool TABLE>
-__global__ void __launch_bounds__(256) k_ed25519_key_prep(uint64_t n_keys, const uint8_t* __restrict__ key_data,
+// OCC: waves per SIMD the registers must leave room for (CHIP_ED_KEYPREP_OCC; 1 = the compiler's choice)
+template <bool TABLE, int OCC = 1>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) k_ed25519_key_prep(uint64_t n_keys, const uint8_t* __restrict__ key_data,
                                                           const uint64_t* __restrict__ key_off,
                                                           const uint32_t* __restrict__ key_len, KeyMeta* meta,
                                                           uint32_t* __restrict__ abytes, uint32_t* __restrict__ table,
@@ -220,6 +221,107 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC)))
     status[i] = eq ? CHIP_VALID : CHIP_INVALID;
 }
 
+// ---- the split Straus path's table half (launch_ed_straus_split) ----
+// The same lane-uniform schedule as k_ed25519_verify without its B additions, SHA-512 and inversion: h's signed
+// radix-16 digits come from the row (k_ed_comb_hash<false, true>), [S]B (completed) from k_ed_comb_bhalf, and R'
+// leaves projective for the batched-inversion finish.
+// early: the row of position p is the signature's (launch_ed_straus_front), else the position's
+template <int OCC>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(OCC))) k_ed25519_verify_a(const uint32_t* __restrict__ list,
+                                                          const uint32_t* __restrict__ count,
+                                                          const uint32_t* __restrict__ key_idx,
+                                                          const uint32_t* __restrict__ table,
+                                                          const uint32_t* __restrict__ bmid, uint32_t row_words,
+                                                          uint32_t hd_word, uint32_t* __restrict__ xyz, uint64_t cap,
+                                                          uint32_t early) {
+    const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+    if (p >= *count) return;
+    const uint32_t i = list[p];
+    const uint32_t k = key_idx[i];
+    const uint32_t* row = bmid + (uint64_t)(early ? i : p) * row_words;
+    uint32_t ea[8];
+#pragma unroll
+    for (int q = 0; q < 8; q++) ea[q] = row[hd_word + q];
+    const uint32_t* tab = table + (uint64_t)k * ED_TAB_WORDS;
+    ge_p2 r;
+    ge_p1p1 t;
+    ge_p3 u;
+    ge_cached ca;
+    auto a_digit = [&]() -> int {
+        const int d = (int)(ea[7] >> 28) - 8;
+        shl256(ea, 4);
+        return d;
+    };
+    auto a_add = [&]() {   // u = 16 r, then t = u + d (-A)
+#pragma unroll 1
+        for (int q = 0; q < 3; q++) {
+            ge_p2_dbl(t, r);
+            ge_p1p1_to_p2(r, t);
+        }
+        ge_p2_dbl(t, r);
+        ge_p1p1_to_p3(u, t);
+        const int d = a_digit();
+        ed_load_row_signed(ca, tab + 40 * (uint32_t)(d < 0 ? -d : d), d < 0);
+        ge_add_row<false>(t, u, ca, (uint32_t)(d >> 31));
+    };
+    {   // window 63 from the identity
+        const int d = a_digit();
+        ed_load_row_signed(ca, tab + 40 * (uint32_t)(d < 0 ? -d : d), d < 0);
+        fe_sub(t.X, ca.YpX, ca.YmX);
+        fe_add(t.Y, ca.YpX, ca.YmX);
+        fe_add(t.Z, ca.Z, ca.Z);
+        t.T = t.Z;
+        ge_p1p1_to_p2(r, t);
+    }
+#pragma unroll 1
+    for (int w = 62; w > 0; w--) {
+        a_add();
+        ge_p1p1_to_p2(r, t);
+    }
+    a_add();   // window 0
+    // + [S]B: the row's completed point to extended, then cached
+    ge_p3 acc;
+    ge_p1p1_to_p3(acc, t);
+    {
+        ge_p1p1 sb;
+#pragma unroll
+        for (int q = 0; q < 10; q++) {
+            sb.X.v[q] = row[q];
+            sb.Y.v[q] = row[10 + q];
+            sb.Z.v[q] = row[20 + q];
+            sb.T.v[q] = row[30 + q];
+        }
+        ge_p1p1_to_p3(u, sb);
+    }
+    ge_p3_to_cached(ca, u);
+    ge_add_cached(t, acc, ca, false);
+    fe X, Y, Z;
+    fe_mul(X, t.X, t.T);
+    fe_mul(Y, t.Z, t.Y);
+    fe_mul(Z, t.Z, t.T);
+#pragma unroll
+    for (int q = 0; q < 10; q++) {
+        xyz[(uint64_t)q * cap + p] = X.v[q];
+        xyz[(uint64_t)(10 + q) * cap + p] = Y.v[q];
+        xyz[(uint64_t)(20 + q) * cap + p] = Z.v[q];
+    }
+}
+
+void launch_ed25519_verify_a(hipStream_t st, uint64_t n, const uint32_t* list, const uint32_t* count,
+                             const uint32_t* key_idx, const uint32_t* table, const uint32_t* bmid, uint32_t row_words,
+                             uint32_t hd_word, uint32_t* xyz, bool early) {
+    if (!n) return;
+    // 3 waves per SIMD (168 VGPRs, 32 B of scratch outside the window loop): cold keys 55.2-55.8M vs 53.7-55.2M at the
+    // compiler's 178 VGPRs and 53.5-53.7M at 4 waves (spills in the loop; profiles/r06/ab_straus_split.txt)
+    static const int occ = [] {
+        const char* e = getenv("CHIP_ED_SPLIT_OCC");
+        return e ? atoi(e) : 3;
+    }();
+    auto kern = occ == 4 ? k_ed25519_verify_a<4> : (occ == 3 ? k_ed25519_verify_a<3> : k_ed25519_verify_a<1>);
+    hipLaunchKernelGGL(kern, dim3((uint32_t)((n + 255) / 256)), dim3(256), 0, st, list, count, key_idx, table, bmid,
+                       row_words, hd_word, xyz, n, early ? 1u : 0u);
+}
+
 // ---- Crypto.decodePublicKey of an Ed25519 SPKI (i2p GroupElement(curve, bytes)) for the Kryo front end:
 // ok = the point decodes; kind 1 also requires the canonical encoding EdDSAPublicKey re-encodes (A.toByteArray:
 // y < p, the sign bit = parity of x)
@@ -262,9 +364,16 @@ void launch_ed25519_key_prep(hipStream_t st, uint64_t n_keys, const uint8_t* key
                              uint32_t* nega, const uint32_t* skip) {
     if (!n_keys) return;
     const uint32_t blocks = (uint32_t)((n_keys + 255) / 256);
-    if (table)
-        hipLaunchKernelGGL(k_ed25519_key_prep<true>, dim3(blocks), dim3(256), 0, st, n_keys, key_data, key_off, key_len,
-                           meta, abytes, table, nega, skip);
+    static const int occ = [] {
+        const char* e = getenv("CHIP_ED_KEYPREP_OCC");
+        return e ? atoi(e) : 1;
+    }();
+    if (table) {
+        auto kern = occ == 4 ? k_ed25519_key_prep<true, 4> : (occ == 3 ? k_ed25519_key_prep<true, 3>
+                                                                         : k_ed25519_key_prep<true, 1>);
+        hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, st, n_keys, key_data, key_off, key_len, meta, abytes, table,
+                           nega, skip);
+    }
     else
         hipLaunchKernelGGL(k_ed25519_key_prep<false>, dim3(blocks), dim3(256), 0, st, n_keys, key_data, key_off, key_len,
                            meta, abytes, table, nega, skip);

@@ -660,8 +660,9 @@ CHIP_DEV void ed_abyte_canonical(uint32_t ab[8], const uint8_t* __restrict__ raw
     for (int q = 0; q < 8; q++) ab[q] = y[q];
     ab[7] |= bit << 31;
 }
-template <bool EARLY>
-__global__ void __launch_bounds__(256) k_ed_comb_hash(const uint32_t* __restrict__ list, const uint32_t* __restrict__ ctr,
+// DIG16 (the split Straus path, k_ed25519_verify_a): h's signed radix-16 digits (8 words) in the row's digit words
+template <bool EARLY, bool DIG16 = false>
+__global__ void __launch_bounds__(256) k_ed_comb_hash(const uint32_t* __restrict__ list, const uint32_t* __restrict__ cnt,
                                                       uint64_t n, const uint32_t* __restrict__ key_idx,
                                                       const uint32_t* __restrict__ msg_idx,
                                                       const uint8_t* __restrict__ sig_data,
@@ -684,7 +685,7 @@ __global__ void __launch_bounds__(256) k_ed_comb_hash(const uint32_t* __restrict
         if (k >= n_keys || msg_idx[i] >= n_msgs || sig_len[i] != 64 || key_len[k] != 44) return;
         ed_abyte_canonical(Ab, key_data + key_off[k] + 12);
     } else {
-        if (p >= ctr[ED_CTR_NCOMB]) return;
+        if (p >= *cnt) return;
         i = list[p];
         const uint32_t k = key_idx[i];
 #pragma unroll
@@ -702,24 +703,32 @@ __global__ void __launch_bounds__(256) k_ed_comb_hash(const uint32_t* __restrict
     ed_challenge(hx, R, Ab, msg_data + msg_off[mi], msg_len[mi], sig);
     sc_reduce512(h, hx);
     ed_effective_s(s, S);
-    uint32_t db[8], da[ED_COMB_ADW];
+    uint32_t db[8];
     recode16(db, s);
-    recode_bytes<ED_COMB_W, ED_COMB_AWIN>(da, h);
     uint32_t* row = bmid + (uint64_t)p * ED_BMID_W;
+    if (DIG16) {
+        uint32_t ea[8];
+        sc_recode16(ea, h);
 #pragma unroll
-    for (int q = 0; q < ED_COMB_ADW; q++) row[ED_BMID_HD + q] = da[q];
+        for (int q = 0; q < 8; q++) row[ED_BMID_HD + q] = ea[q];
+    } else {
+        uint32_t da[ED_COMB_ADW];
+        recode_bytes<ED_COMB_W, ED_COMB_AWIN>(da, h);
+#pragma unroll
+        for (int q = 0; q < ED_COMB_ADW; q++) row[ED_BMID_HD + q] = da[q];
+    }
 #pragma unroll
     for (int q = 0; q < 8; q++) row[ED_BMID_SD + q] = db[q];
 }
 
 // k_ed_comb_bhalf: [S]B from the fixed radix-2^16 comb, 16 mixed additions; [S]B (extended) into the row's words 0..39
-__global__ void __launch_bounds__(256, ED_BHALF_MINW) k_ed_comb_bhalf(const uint32_t* __restrict__ ctr, uint64_t n_early,
+__global__ void __launch_bounds__(256, ED_BHALF_MINW) k_ed_comb_bhalf(const uint32_t* __restrict__ cnt, uint64_t n_early,
                                                                       const uint32_t* __restrict__ b16,
                                                                       uint32_t* __restrict__ bmid) {
     const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
     // early: every slot of the batch (a slot the hash skipped holds stale digits: any int16 digit stays inside
     // the radix-2^16 table, and the row is never read back)
-    if (p >= (n_early ? n_early : (uint64_t)ctr[ED_CTR_NCOMB])) return;
+    if (p >= (n_early ? n_early : (uint64_t)*cnt)) return;
     uint32_t* row = bmid + (uint64_t)p * ED_BMID_W;
     const uint32_t* sdig = row + ED_BMID_SD;   // digit word j at sdig[j]
     // [S]B: one mixed (affine Niels) addition per radix-2^16 window.  Window 0 from the identity needs no
@@ -868,13 +877,13 @@ CHIP_DEV void ld_fe_soa(fe& f, const uint32_t* __restrict__ base, uint64_t cap, 
 // ALL (the deferred finish of a chunked host batch): positions [0, nall) over every chunk's R', list = flist (the
 // signature of each position in the whole batch, ~0 where a chunk left the position empty: skipped, its Z counted as 1)
 template <bool ALL>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_FINISH_WAVES))) k_ed_comb_finish(const uint32_t* __restrict__ list, const uint32_t* __restrict__ ctr,
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_FINISH_WAVES))) k_ed_comb_finish(const uint32_t* __restrict__ list, const uint32_t* __restrict__ cnt,
                                                         const uint8_t* __restrict__ sig_data,
                                                         const uint64_t* __restrict__ sig_off,
                                                         const uint32_t* __restrict__ xyz, uint32_t* __restrict__ zpre,
                                                         uint64_t cap, uint8_t* __restrict__ status, uint32_t g,
                                                         uint32_t nall) {
-    const uint32_t n = ALL ? nall : ctr[ED_CTR_NCOMB];
+    const uint32_t n = ALL ? nall : *cnt;
     const uint32_t lanes = (n + g - 1) / g;
     const uint32_t l = blockIdx.x * blockDim.x + threadIdx.x;
     if (l >= lanes) return;
@@ -982,21 +991,22 @@ void launch_ed_comb_bhalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, c
                           const EdCombWs& w, int part) {
     if (!n || !w.max_slots) return;
     if (part & 2) {   // [S]B only (its hash launched before)
-        hipLaunchKernelGGL(k_ed_comb_bhalf, dim3(nblk(n, 256)), dim3(256), 0, st, w.ctr, w.early ? n : 0, w.bcomb16,
-                           w.bmid);
+        hipLaunchKernelGGL(k_ed_comb_bhalf, dim3(nblk(n, 256)), dim3(256), 0, st, w.ctr + ED_CTR_NCOMB, w.early ? n : 0,
+                           w.bcomb16, w.bmid);
         return;
     }
     if (w.early)
-        hipLaunchKernelGGL(k_ed_comb_hash<true>, dim3(nblk(n, 256)), dim3(256), 0, st, w.comb_list, w.ctr, n, b->key_idx,
+        hipLaunchKernelGGL(k_ed_comb_hash<true>, dim3(nblk(n, 256)), dim3(256), 0, st, w.comb_list, w.ctr + ED_CTR_NCOMB, n,
+                           b->key_idx,
                            b->msg_idx, b->sig_data, b->sig_off, b->sig_len, b->msg_data, b->msg_off, b->msg_len,
                            b->n_keys, b->n_msgs, b->key_data, b->key_off, b->key_len, abytes, w.bmid);
     else
-        hipLaunchKernelGGL(k_ed_comb_hash<false>, dim3(nblk(n, 256)), dim3(256), 0, st, w.comb_list, w.ctr, n,
+        hipLaunchKernelGGL(k_ed_comb_hash<false>, dim3(nblk(n, 256)), dim3(256), 0, st, w.comb_list, w.ctr + ED_CTR_NCOMB, n,
                            b->key_idx, b->msg_idx, b->sig_data, b->sig_off, b->sig_len, b->msg_data, b->msg_off,
                            b->msg_len, b->n_keys, b->n_msgs, b->key_data, b->key_off, b->key_len, abytes, w.bmid);
     if (part & 1) return;   // the hash only
-    hipLaunchKernelGGL(k_ed_comb_bhalf, dim3(nblk(n, 256)), dim3(256), 0, st, w.ctr, w.early ? n : 0, w.bcomb16,
-                       w.bmid);
+    hipLaunchKernelGGL(k_ed_comb_bhalf, dim3(nblk(n, 256)), dim3(256), 0, st, w.ctr + ED_CTR_NCOMB, w.early ? n : 0,
+                       w.bcomb16, w.bmid);
 }
 void launch_ed_comb_ahalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w) {
     if (!n || !w.max_slots) return;
@@ -1020,12 +1030,43 @@ void launch_ed_comb_finish(hipStream_t st, uint64_t n, const chip_sig_batch* b, 
     }();
     while (g > 4 && n / g < min_lanes) g >>= 1;
     hipLaunchKernelGGL(k_ed_comb_finish<false>, dim3(nblk((n + g - 1) / g, 256)), dim3(256), 0, st, w.comb_list,
-                       w.ctr, b->sig_data, b->sig_off, w.xyz, w.zpre, w.xyz_cap ? w.xyz_cap : (uint64_t)n, status, g, 0u);
+                       w.ctr + ED_CTR_NCOMB, b->sig_data, b->sig_off, w.xyz, w.zpre, w.xyz_cap ? w.xyz_cap : (uint64_t)n, status, g, 0u);
 }
 void launch_ed_comb_finish_all(hipStream_t st, uint64_t n, const uint8_t* sig_data, const uint64_t* sig_off,
                                const EdCombWs& w, uint8_t* status) {
     if (!n || !w.flist) return;
     const uint32_t g = ED_FIN_G;
-    hipLaunchKernelGGL(k_ed_comb_finish<true>, dim3(nblk((n + g - 1) / g, 256)), dim3(256), 0, st, w.flist, w.ctr,
+    hipLaunchKernelGGL(k_ed_comb_finish<true>, dim3(nblk((n + g - 1) / g, 256)), dim3(256), 0, st, w.flist, w.ctr + ED_CTR_NCOMB,
                        sig_data, sig_off, w.xyz, w.zpre, w.xyz_cap, status, g, (uint32_t)n);
+}
+
+// The split Straus path (cold keys: few signatures per key, no per-key comb): the table-free work of the comb path —
+// the challenge hash with h's signed radix-16 digits and [S]B from the radix-2^16 comb of B (16 mixed additions instead
+// of the 32 radix-256 ones that ride on the Straus doublings) — then k_ed25519_verify_a's 252 doublings + 64 additions
+// of h (-A) from the key's radix-16 table, + [S]B, and the batched-inversion finish (one inversion per g signatures
+// instead of one per signature).  Positions p < *cnt of `list`; rows, R' and prefix products are this path's own.
+void launch_ed_straus_front(hipStream_t st, uint64_t n, const chip_sig_batch* b, const uint32_t* bcomb16, uint32_t* bmid) {
+    if (!n) return;
+    auto hash = k_ed_comb_hash<true, true>;
+    hipLaunchKernelGGL(hash, dim3(nblk(n, 256)), dim3(256), 0, st, nullptr, nullptr, n, b->key_idx, b->msg_idx,
+                       b->sig_data, b->sig_off, b->sig_len, b->msg_data, b->msg_off, b->msg_len, b->n_keys, b->n_msgs,
+                       b->key_data, b->key_off, b->key_len, nullptr, bmid);
+    hipLaunchKernelGGL(k_ed_comb_bhalf, dim3(nblk(n, 256)), dim3(256), 0, st, nullptr, n, bcomb16, bmid);
+}
+void launch_ed_straus_split(hipStream_t st, uint64_t n, const uint32_t* list, const uint32_t* cnt, const chip_sig_batch* b,
+                            const uint32_t* abytes, const uint32_t* table, const uint32_t* bcomb16, uint32_t* bmid,
+                            uint32_t* xyz, uint32_t* zpre, uint8_t* status, bool early) {
+    if (!n) return;
+    if (!early) {
+        auto hash = k_ed_comb_hash<false, true>;
+        hipLaunchKernelGGL(hash, dim3(nblk(n, 256)), dim3(256), 0, st, list, cnt, n, b->key_idx, b->msg_idx,
+                           b->sig_data, b->sig_off, b->sig_len, b->msg_data, b->msg_off, b->msg_len, b->n_keys, b->n_msgs,
+                           b->key_data, b->key_off, b->key_len, abytes, bmid);
+        hipLaunchKernelGGL(k_ed_comb_bhalf, dim3(nblk(n, 256)), dim3(256), 0, st, cnt, (uint64_t)0, bcomb16, bmid);
+    }
+    launch_ed25519_verify_a(st, n, list, cnt, b->key_idx, table, bmid, ED_BMID_W, ED_BMID_HD, xyz, early);
+    uint32_t g = ED_FIN_G;
+    while (g > 4 && n / g < 32768u) g >>= 1;
+    hipLaunchKernelGGL(k_ed_comb_finish<false>, dim3(nblk((n + g - 1) / g, 256)), dim3(256), 0, st, list, cnt,
+                       b->sig_data, b->sig_off, xyz, zpre, n, status, g, 0u);
 }

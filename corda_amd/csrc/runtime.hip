@@ -174,7 +174,7 @@ struct chip_ctx {
     DevBuf meta, abytes, edtab, ectab, lists, counts;
     // Ed25519 comb path
     DevBuf c_key_count, c_key_rank, c_key_slot, c_key_base, c_slot_key, c_ctr, c_comb_list, c_straus_list, c_ctab,
-        c_xyz, c_zpre, c_nega, c_fz, c_bmid, e_ctab, e_mid, e_gcomb, e_bcomb16, e_wp, e_glist;
+        c_xyz, c_zpre, c_nega, c_fz, c_bmid, e_ctab, e_mid, e_gcomb, e_bcomb16, e_wp, e_glist, s_bmid, s_xyz, s_zpre;
     // host-path mirrors of the caller's buffers
     DevBuf h_key_idx, h_msg_idx, h_sig_data, h_sig_off, h_sig_len, h_key_data, h_key_off, h_key_len, h_msg_data,
         h_msg_off, h_msg_len, h_status, h_bitmap, h_check;
@@ -202,6 +202,8 @@ struct chip_ctx {
     DevBuf c_flist;               // the host pipeline's deferred finish: signature of each R' position
     bool deferred_comb = false;   // the chunks of the host batch in flight took the comb path (finish_all pending)
     bool defer_finish = true;     // CHIP_HOST_DEFER_FINISH=0: each chunk finishes its own R' (round 5)
+    bool straus_split = true;     // CHIP_ED_STRAUS_SPLIT=0: the fused Straus kernel (k_ed25519_verify, round 5)
+    bool straus_early = true;     // CHIP_ED_STRAUS_EARLY=0: the split path's hash + [S]B after classify
     bool kc_valid = false;
     int kc_test_fail = 0, kc_test_seen = 0;   // CHIP_TEST_FAIL_KEYSTATE=n: the n-th key-cache batch fails (tests)
     uint32_t kc_path = 0;
@@ -586,6 +588,8 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
     if (const char* e = getenv("CHIP_KERNEL_TIMING")) c->ktiming = e[0] != '0';
     if (const char* e = getenv("CHIP_TEST_FAIL_KEYSTATE")) c->kc_test_fail = atoi(e);
     if (const char* e = getenv("CHIP_HOST_DEFER_FINISH")) c->defer_finish = e[0] != '0';
+    if (const char* e = getenv("CHIP_ED_STRAUS_SPLIT")) c->straus_split = e[0] != '0';
+    if (const char* e = getenv("CHIP_ED_STRAUS_EARLY")) c->straus_early = e[0] != '0';
     if (const char* e = getenv("CHIP_KRYO_FUSED")) c->kryo_fused = (uint32_t)std::min(2, std::max(0, atoi(e)));
     if (cfg && cfg->reserve_sigs) {
         (void)c->lists.ensure(cfg->reserve_sigs * 4 * N_LISTS);
@@ -600,7 +604,7 @@ void chip_shutdown(chip_ctx* c) {
     hipStreamSynchronize(c->stream);
     DevBuf* bufs[] = {&c->meta, &c->abytes, &c->edtab, &c->ectab, &c->lists, &c->counts, &c->c_key_count, &c->c_key_rank,
                       &c->c_key_slot, &c->c_key_base, &c->c_slot_key, &c->c_ctr, &c->c_comb_list,
-                      &c->c_straus_list, &c->c_ctab, &c->c_xyz, &c->c_zpre, &c->c_flist, &c->c_nega, &c->c_fz, &c->c_bmid, &c->e_ctab, &c->e_mid, &c->e_gcomb, &c->e_bcomb16, &c->e_wp, &c->e_glist, &c->h_key_idx, &c->h_msg_idx,
+                      &c->c_straus_list, &c->c_ctab, &c->c_xyz, &c->c_zpre, &c->c_flist, &c->c_nega, &c->c_fz, &c->c_bmid, &c->e_ctab, &c->e_mid, &c->e_gcomb, &c->e_bcomb16, &c->e_wp, &c->e_glist, &c->s_bmid, &c->s_xyz, &c->s_zpre, &c->h_key_idx, &c->h_msg_idx,
                       &c->h_sig_data, &c->h_sig_off, &c->h_sig_len, &c->h_key_data, &c->h_key_off, &c->h_key_len,
                       &c->h_msg_data, &c->h_msg_off, &c->h_msg_len, &c->h_status, &c->h_bitmap, &c->h_check, &c->t_salts,
                       &c->t_start, &c->t_group, &c->t_internal, &c->t_data, &c->t_off, &c->t_len, &c->t_ids,
@@ -785,6 +789,16 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         w.min_sigs = c->comb_min_sigs;
         w.min_total = c->comb_min_total;
     }
+    // the split Straus path (CHIP_ED_STRAUS_SPLIT, default on): its own rows, R' and prefix products
+    const bool straus_split = c->straus_split && n && !(comb && w.eager) && !no_ed;
+    // ... and for cold keys (device entry, fewer than 2 signatures per key: few if any take the comb): the hash and
+    // [S]B over the whole batch at once, beside the key prep on the second stream (CHIP_ED_STRAUS_EARLY, default on)
+    const bool s_early = straus_split && !(comb && w.eager) && (!comb || nd < 2 * nk) && !reuse && !vc && c->straus_early;
+    if (straus_split) {
+        HIPCHK(c, c->s_bmid.ensure(n * ed_comb_bmid_words() * 4 + 16));
+        HIPCHK(c, c->s_xyz.ensure(n * 30 * 4 + 16));
+        HIPCHK(c, c->s_zpre.ensure(n * 10 * 4 + 16));
+    }
     if (ec_comb) {
         HIPCHK(c, c->e_ctab.ensure(nk * ec_key_bytes + 16));
         HIPCHK(c, c->e_mid.ensure(2 * n * ecdsa_comb_mid_words() * 4 + 16));
@@ -865,6 +879,17 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         return CHIP_OK;
     };
     int rk;
+    if (s_early) {
+        HIPCHK(c, hipEventRecord(c->ev_fork, st));
+        HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
+        const int kk = c->kbegin(CHIP_K_KEYPREP, c->aux);
+        launch_ed25519_key_prep(c->aux, nk, b->key_data, b->key_off, b->key_len, meta, c->abytes.as<uint32_t>(),
+                                c->edtab.as<uint32_t>(), comb ? w.nega : nullptr, skip);
+        c->kend(kk, c->aux);
+        HIPCHK(c, hipEventRecord(c->ev_kp, c->aux));
+        if (!c->eckeys_late && (rk = ecdsa_keys())) return rk;
+        launch_ed_straus_front(st, n, b, c->e_bcomb16.as<uint32_t>(), c->s_bmid.as<uint32_t>());
+    }
     if (w.early) {
         HIPCHK(c, hipEventRecord(c->ev_fork, st));
         HIPCHK(c, hipStreamWaitEvent(c->aux, c->ev_fork, 0));
@@ -888,7 +913,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         c->kend(kb, st);
     }
     int ke = c->kbegin(CHIP_K_KEYPREP, st);
-    if (!reuse && !w.early && !no_ed)
+    if (!reuse && !w.early && !s_early && !no_ed)
         launch_ed25519_key_prep(st, nk, b->key_data, b->key_off, b->key_len, meta, c->abytes.as<uint32_t>(),
                                 (comb && w.eager) ? nullptr : c->edtab.as<uint32_t>(), comb ? w.nega : nullptr, skip);
     if (comb && w.eager && n && !reuse && !w.early) {
@@ -901,7 +926,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         c->kend(kt, c->aux);
         HIPCHK(c, hipEventRecord(c->ev_join, c->aux));
     }
-    if ((!w.early || c->eckeys_late) && (rk = ecdsa_keys())) return rk;
+    if ((!(w.early || s_early) || c->eckeys_late) && (rk = ecdsa_keys())) return rk;
     c->kend(ke, st);
     HIPCHK(c, hipGetLastError());
     if (kc_commit) {   // every key prep and table build of this pool is enqueued: the cached state is this pool's
@@ -916,7 +941,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         return CHIP_OK;
     }
     if (vc && vc->data_ready) HIPCHK(c, hipStreamWaitEvent(st, vc->data_ready, 0));
-    if (w.early) HIPCHK(c, hipStreamWaitEvent(st, c->ev_kp, 0));
+    if (w.early || s_early) HIPCHK(c, hipStreamWaitEvent(st, c->ev_kp, 0));
     if (n) {
         const uint32_t blocks = (uint32_t)((n + CLASSIFY_BLOCK - 1) / CLASSIFY_BLOCK);
         uint32_t* lists = c->lists.as<uint32_t>();
@@ -987,8 +1012,13 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         // is empty (and no Straus key table was built): no launch
         if (!(comb && w.eager) && !no_ed) {
             ke = c->kbegin(CHIP_K_ED25519, st);
-            launch_ed25519_verify(st, n, ed_list, ed_count, b, c->abytes.as<uint32_t>(), c->edtab.as<uint32_t>(),
-                                  status);
+            if (straus_split)
+                launch_ed_straus_split(st, n, ed_list, ed_count, b, c->abytes.as<uint32_t>(), c->edtab.as<uint32_t>(),
+                                       c->e_bcomb16.as<uint32_t>(), c->s_bmid.as<uint32_t>(), c->s_xyz.as<uint32_t>(),
+                                       c->s_zpre.as<uint32_t>(), status, s_early);
+            else
+                launch_ed25519_verify(st, n, ed_list, ed_count, b, c->abytes.as<uint32_t>(), c->edtab.as<uint32_t>(),
+                                      status);
             c->kend(ke, st);
         }
         if (ec_comb) {

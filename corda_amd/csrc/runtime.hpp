@@ -13,6 +13,11 @@ void launch_ed25519_key_prep(hipStream_t st, uint64_t n_keys, const uint8_t* key
 // key state was built from (CHIP_FLAG_KEY_CACHE), and the kernel returns at once
 void launch_ed25519_verify(hipStream_t st, uint64_t n, const uint32_t* list, const uint32_t* count,
                            const chip_sig_batch* b, const uint32_t* abytes, const uint32_t* table, uint8_t* status);
+// the split Straus path's table half: R' = [h](-A) + [S]B, projective, structure-of-arrays xyz (cap n) at position p
+// of list (h's radix-16 digits and [S]B from the row k_ed_comb_hash<false, true> + k_ed_comb_bhalf wrote)
+void launch_ed25519_verify_a(hipStream_t st, uint64_t n, const uint32_t* list, const uint32_t* count,
+                             const uint32_t* key_idx, const uint32_t* table, const uint32_t* bmid, uint32_t row_words,
+                             uint32_t hd_word, uint32_t* xyz, bool early);
 
 void launch_ecdsa_key_prep(hipStream_t st, uint64_t n_keys, const uint8_t* key_data, const uint64_t* key_off,
                            const uint32_t* key_len, KeyMeta* meta, uint32_t* ectab, const uint32_t* skip = nullptr);
@@ -236,6 +241,14 @@ void launch_ed_comb_finish(hipStream_t st, uint64_t n, const chip_sig_batch* b, 
 // the deferred finish of a chunked host batch: every chunk's R' (positions [0, n), flist) in one batched inversion
 void launch_ed_comb_finish_all(hipStream_t st, uint64_t n, const uint8_t* sig_data, const uint64_t* sig_off,
                                const EdCombWs& w, uint8_t* status);
+// cold keys without the fused Straus kernel (CHIP_ED_STRAUS_SPLIT): hash + [S]B comb, verify_a, batched finish;
+// bmid n x ed_comb_bmid_words(), xyz n x 30, zpre n x 10 words
+void launch_ed_straus_split(hipStream_t st, uint64_t n, const uint32_t* list, const uint32_t* cnt, const chip_sig_batch* b,
+                            const uint32_t* abytes, const uint32_t* table, const uint32_t* bcomb16, uint32_t* bmid,
+                            uint32_t* xyz, uint32_t* zpre, uint8_t* status, bool early);
+// early (device entry, cold keys): the hash and [S]B over the whole batch into rows indexed by signature, launched
+// before the key prep has finished (it runs on the second stream); then launch_ed_straus_split(..., early = true)
+void launch_ed_straus_front(hipStream_t st, uint64_t n, const chip_sig_batch* b, const uint32_t* bcomb16, uint32_t* bmid);
 
 // ---- host-entry argument checks on the device (runtime.hip dev_check) ----
 enum { DEV_CHECK_MONOTONE = 0, DEV_CHECK_RANGE = 1, DEV_CHECK_INDEX = 2 };

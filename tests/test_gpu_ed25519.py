@@ -125,3 +125,57 @@ def test_cfg2_shape_quarter_million_matches_oracle(ctx, oracle):
     assert np.array_equal(got, b.expected)
     assert len(set(b.kind.tolist())) == len(G.ED_KINDS)
     assert np.array_equal(bm.cpu().numpy().view(np.uint64), bitmap_of(got))
+
+
+def _device_batch(b, dev):
+    import torch
+
+    class D:
+        pass
+    d = D()
+    for f in ("key_idx", "msg_idx", "sig_data", "sig_off", "sig_len", "key_data", "key_off", "key_len", "msg_data",
+              "msg_off", "msg_len"):
+        a = getattr(b, f)
+        a = a.view(np.int64) if a.dtype == np.uint64 else a.view(np.int32) if a.dtype == np.uint32 else a
+        setattr(d, f, torch.from_numpy(np.ascontiguousarray(a)).to(dev))
+    return d
+
+
+@pytest.mark.parametrize("env", [{}, {"CHIP_ED_STRAUS_EARLY": "0"}, {"CHIP_ED_STRAUS_SPLIT": "0"}],
+                         ids=["split_early", "split", "fused"])
+def test_cold_keys_device_entry_matches_oracle(oracle, env):
+    """Cold keys (every signature its own key) on the device entry: the split Straus path (hash + [S]B comb,
+    k_ed25519_verify_a, batched finish), with its hash and [S]B started beside the key prep (default) or after
+    classify, and the fused k_ed25519_verify — every status byte equal to the oracle's and the labels; a second
+    batch through the same context (reused rows and R' buffers) too."""
+    import os
+    import torch
+    import corda_amd
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        c = corda_amd.Context(0)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    dev = torch.device("cuda", 0)
+    try:
+        for n, seed in ((40_000, 0x5EED0610), (9_000, 0x5EED0611)):
+            b = G.ed25519_batch(n, n_keys=n, corrupt=0.2, seed=seed)
+            d = _device_batch(b, dev)
+            d.schemes_hint = 1 << 4
+            st = torch.empty(b.n, dtype=torch.uint8, device=dev)
+            bm = torch.empty((b.n + 63) // 64, dtype=torch.int64, device=dev)
+            c.verify_batch_device(d, st, bm)
+            torch.cuda.synchronize()
+            got = st.cpu().numpy()
+            ref = oracle.verify_batch(b, threads=16)
+            bad = np.nonzero(got != ref)[0]
+            assert len(bad) == 0, [(int(i), int(got[i]), int(ref[i]), int(b.kind[i])) for i in bad[:20]]
+            assert np.array_equal(got, b.expected)
+            assert np.array_equal(bm.cpu().numpy().view(np.uint64), bitmap_of(got))
+    finally:
+        c.close()
