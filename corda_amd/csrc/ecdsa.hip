@@ -592,8 +592,88 @@ void launch_ecdsa_gcomb_build(hipStream_t st, uint32_t* gcomb) {
 #define EC_COMB_QENT 8
 #define EC_COMB_JW 24
 // affine table per key, then (after all keys) the Jacobian scratch it is normalised from
-#define EC_COMB_KEY_WORDS (EC_COMB_QWIN * EC_COMB_QENT * 16)
+// (a secp256k1 key's GLV table, 26 x 16 entries + beta x, 9,984 words, is the larger: see EC_GLV_*)
+#define EC_COMB_KEY_WORDS 9984
 #define EC_COMB_JAC_WORDS (EC_COMB_QWIN * EC_COMB_QENT * EC_COMB_JW)
+
+// ---- GLV for secp256k1 (BC 1.57's GLVTypeBEndomorphism on the k1 path; CHIP_EC_GLV, default on) ----
+// lambda Q = (beta x, y) with beta^3 = 1 (mod p), lambda^3 = 1 (mod n).  u2 = a1 + lambda a2 (mod n) with
+// |a1|, |a2| < 2^128 (the rounded-lattice split: c_i = round(u2 g_i / 2^384), a2 = c1 (-b1) + c2 (-b2),
+// a1 = u2 - lambda a2), so u2 Q = a1 Q + a2 (lambda Q) needs only the table's windows 0..32: a secp256k1 key's
+// table is 26 windows of {1..16} 2^(5w) Q plus beta x of each entry (EC_GLV_BETA_AT): 52 additions per signature
+// instead of 65, and a chain of 125 doublings instead of 256 (the 129-bit halves take radix 32 for the table memory
+// the 256-bit scalar took at radix 16).
+// Constants checked in tools/glv_constants.py (lambda G = (beta Gx, Gy), the split's identity and bound).
+#define EC_GLV_W 5                                             // window bits of the GLV table
+#define EC_GLV_ENT 16                                          // entries per window: signed digits |d| <= 16
+#define EC_GLV_WIN 26                                          // windows of a 129-bit signed radix-32 recoding
+#define EC_GLV_LO 13                                           // windows [0, 13) built and added with the low half
+#define EC_GLV_FILL_GROUP 2                                    // windows per fill lane (7 of a launch's 8-9 groups)
+#define EC_GLV_BETA_AT (EC_GLV_WIN * EC_GLV_ENT * 16)            // beta x of entry (w, j): + (w * 16 + j - 1) * 8
+static_assert(EC_GLV_BETA_AT + EC_GLV_WIN * EC_GLV_ENT * 8 <= EC_COMB_KEY_WORDS, "GLV table");
+static_assert(EC_GLV_WIN * EC_GLV_W >= 130, "GLV windows cover a 129-bit recoding");
+static_assert(EC_GLV_WIN * EC_GLV_ENT * EC_COMB_JW <= EC_COMB_QWIN * EC_COMB_QENT * EC_COMB_JW, "GLV scratch");
+static_assert(EC_COMB_QWIN * EC_COMB_QENT * 16 <= EC_COMB_KEY_WORDS, "P-256 table");
+__device__ __constant__ const uint32_t K1_BETA[8] = {0x719501eeu, 0xc1396c28u, 0x12f58995u, 0x9cf04975u,
+                                                     0xac3434e9u, 0x6e64479eu, 0x657c0710u, 0x7ae96a2bu};
+__device__ __constant__ const uint32_t K1_GLV_G1[8] = {0x45dbb031u, 0xe893209au, 0x71e8ca7fu, 0x3daa8a14u,
+                                                       0x9284eb15u, 0xe86c90e4u, 0xa7d46bcdu, 0x3086d221u};
+__device__ __constant__ const uint32_t K1_GLV_G2[8] = {0x8ac47f71u, 0x1571b4aeu, 0x9df506c6u, 0x221208acu,
+                                                       0x0abfe4c4u, 0x6f547fa9u, 0x010e8828u, 0xe4437ed6u};
+// -b1 R, -b2 R, -lambda R (mod n): Montgomery multipliers, so mn_mul gives the plain product mod n
+__device__ __constant__ const uint32_t K1_GLV_MB1R[8] = {0x0ad9263cu, 0xc50468d0u, 0xfaa6ed42u, 0x1b1c8205u,
+                                                         0x8ac47f71u, 0x1571b4aeu, 0x9df506c6u, 0x221208acu};
+__device__ __constant__ const uint32_t K1_GLV_MB2R[8] = {0x6a144696u, 0x0cac5e50u, 0xf3ba5939u, 0x1e8a8dc5u,
+                                                         0xba244fceu, 0x176cdf65u, 0x8e173580u, 0xc25575ebu};
+__device__ __constant__ const uint32_t K1_GLV_MLR[8] = {0x06a3d4a3u, 0xcf54734fu, 0x2b820beeu, 0x8e1af539u,
+                                                        0xad96826du, 0x8c5699f9u, 0x7aa729c6u, 0xacd7bfe8u};
+__device__ __constant__ const uint32_t K1_N_HALF[8] = {0x681b20a0u, 0xdfe92f46u, 0x57a4501du, 0x5d576e73u,
+                                                       0xffffffffu, 0xffffffffu, 0xffffffffu, 0x7fffffffu};
+// round(k g / 2^384) for k, g < 2^256 (< 2^128 + 1)
+CHIP_DEV void glv_round_shift(u256& c, const u256& k, const uint32_t* g) {
+    u256 gg;
+    u256_from_c(gg, g);
+    uint32_t t[16];
+    mul_512(t, k, gg);
+    uint32_t cy = 0;
+    const uint32_t rb = t[11] >> 31;
+    c.w[0] = __builtin_addc(t[12], rb, 0u, &cy);
+    c.w[1] = __builtin_addc(t[13], 0u, cy, &cy);
+    c.w[2] = __builtin_addc(t[14], 0u, cy, &cy);
+    c.w[3] = __builtin_addc(t[15], 0u, cy, &cy);
+    c.w[4] = cy;
+    c.w[5] = c.w[6] = c.w[7] = 0;
+}
+// (a + b) mod n for a, b < n
+CHIP_DEV void mn_add_k1(u256& r, const u256& a, const u256& b) {
+    const uint32_t c = u256_add(r, a, b.w);
+    u256 s;
+    const uint32_t br = u256_sub(s, r, EC_K1.n);
+    if (c || !br) r = s;
+}
+// u2 (< n) -> |a1|, |a2| < 2^128 with their signs: u2 = s1 |a1| + lambda s2 |a2| (mod n)
+CHIP_DEV void glv_split(const u256& u2, u256& a1, bool& neg1, u256& a2, bool& neg2) {
+    u256 c1, c2, x1, x2, r1, r2, m;
+    glv_round_shift(c1, u2, K1_GLV_G1);
+    glv_round_shift(c2, u2, K1_GLV_G2);
+    u256_from_c(m, K1_GLV_MB1R);
+    mn_mul<CURVE_K1>(x1, c1, m);
+    u256_from_c(m, K1_GLV_MB2R);
+    mn_mul<CURVE_K1>(x2, c2, m);
+    mn_add_k1(r2, x1, x2);
+    u256_from_c(m, K1_GLV_MLR);
+    mn_mul<CURVE_K1>(x1, r2, m);
+    mn_add_k1(r1, x1, u2);
+    // the signed representative: r > n / 2 -> -(n - r)
+    neg1 = u256_ge(r1, K1_N_HALF) && !u256_eq_c(r1, K1_N_HALF);
+    neg2 = u256_ge(r2, K1_N_HALF) && !u256_eq_c(r2, K1_N_HALF);
+    u256 nn, nr;
+    u256_from_c(nn, EC_K1.n);
+    (void)u256_sub(nr, nn, r1.w);
+    a1 = neg1 ? nr : r1;
+    (void)u256_sub(nr, nn, r2.w);
+    a2 = neg2 ? nr : r2;
+}
 
 CHIP_DEV bool ec_key_ok(const KeyMeta* meta, uint64_t k, int scheme) {
     const KeyMeta m = meta[k];
@@ -607,7 +687,7 @@ CHIP_DEV bool ec_key_ok(const KeyMeta* meta, uint64_t k, int scheme) {
 // still doubles towards the high half.
 template <int C>
 CHIP_DEV void ec_comb_chain(const uint32_t* __restrict__ ectab, uint32_t* __restrict__ jac, uint64_t k, uint32_t wa,
-                            uint32_t wb) {
+                            uint32_t wb, uint32_t ent = EC_COMB_QENT, uint32_t wbits = 4) {
     uint32_t* tab = jac + k * EC_COMB_JAC_WORDS;
     jpt P;
     uint32_t w = wa;
@@ -618,13 +698,13 @@ CHIP_DEV void ec_comb_chain(const uint32_t* __restrict__ ectab, uint32_t* __rest
         store_jpt(tab, P);
         w = 1;
     } else {
-        load_jpt(P, tab + (wa - 1) * EC_COMB_QENT * EC_COMB_JW);
+        load_jpt(P, tab + (wa - 1) * ent * EC_COMB_JW);
     }
 #pragma unroll 1
     for (; w < wb; w++) {
 #pragma unroll 1
-        for (int b = 0; b < 4; b++) jdbl<C>(P, P);
-        store_jpt(tab + w * EC_COMB_QENT * EC_COMB_JW, P);
+        for (uint32_t b = 0; b < wbits; b++) jdbl<C>(P, P);
+        store_jpt(tab + w * ent * EC_COMB_JW, P);
     }
 }
 // The same chain on a lane pair per key (adjacent lanes of a wave; both hold the point): each doubling's field
@@ -731,7 +811,7 @@ CHIP_DEV void jdbl_pair(jpt& r, const jpt& p, uint32_t odd) {
 }
 template <int C>
 CHIP_DEV void ec_comb_chain2(const uint32_t* __restrict__ ectab, uint32_t* __restrict__ jac, uint64_t k, uint32_t wa,
-                             uint32_t wb, uint32_t odd) {
+                             uint32_t wb, uint32_t odd, uint32_t ent = EC_COMB_QENT, uint32_t wbits = 4) {
     uint32_t* tab = jac + k * EC_COMB_JAC_WORDS;
     jpt P;
     uint32_t w = wa;
@@ -742,13 +822,13 @@ CHIP_DEV void ec_comb_chain2(const uint32_t* __restrict__ ectab, uint32_t* __res
         if (!odd) store_jpt(tab, P);
         w = 1;
     } else {
-        load_jpt(P, tab + (wa - 1) * EC_COMB_QENT * EC_COMB_JW);
+        load_jpt(P, tab + (wa - 1) * ent * EC_COMB_JW);
     }
 #pragma unroll 1
     for (; w < wb; w++) {
 #pragma unroll 1
-        for (int b = 0; b < 4; b++) jdbl_pair<C>(P, P, odd);
-        if (!odd) store_jpt(tab + w * EC_COMB_QENT * EC_COMB_JW, P);
+        for (uint32_t b = 0; b < wbits; b++) jdbl_pair<C>(P, P, odd);
+        if (!odd) store_jpt(tab + w * ent * EC_COMB_JW, P);
     }
 }
 
@@ -759,36 +839,46 @@ CHIP_DEV void ec_comb_chain2(const uint32_t* __restrict__ ectab, uint32_t* __res
 //   3. those 7 (w1 - w0) entries to affine with one more shared inversion
 #define EC_FILL_GROUP 4   // measured: 1 -> 68.9M, 2 -> 73.4M, 4 -> 75.3M, 8 -> 74.6M, 16 -> 59.7M cfg3 sigs/s
 template <int C>
-CHIP_DEV void ec_comb_fill(uint32_t* __restrict__ jac, uint32_t* __restrict__ out, uint32_t w0, uint32_t w1) {
+CHIP_DEV void ec_comb_fill(uint32_t* __restrict__ jac, uint32_t* __restrict__ out, uint32_t w0, uint32_t w1,
+                           uint32_t* __restrict__ bx, uint32_t ent = EC_COMB_QENT) {
+    // bx (GLV, secp256k1): beta x of every entry written beside the table
+    auto beta_x = [&](uint32_t w, uint32_t j, const apt& a) {
+        if (!bx) return;
+        u256 b, t;
+        u256_from_c(b, K1_BETA);
+        fp_mul<C>(t, a.x, b);
+        store_u256(bx + (w * ent + j) * 8, t);
+    };
     u256 acc, z, inv;
     // 1.
     u256_set_word(acc, 1);
 #pragma unroll 1
     for (uint32_t w = w0; w < w1; w++) {
-        store_u256(out + w * EC_COMB_QENT * 16, acc);
-        load_u256(z, jac + w * EC_COMB_QENT * EC_COMB_JW + 16);
+        store_u256(out + w * ent * 16, acc);
+        load_u256(z, jac + w * ent * EC_COMB_JW + 16);
         fp_mul<C>(acc, acc, z);
     }
     fp_inv_vt<C>(inv, acc);   // entries are 2^(4w) Q, never infinity for a valid key
 #pragma unroll 1
     for (uint32_t w = w1; w-- > w0;) {
-        uint32_t* o = out + w * EC_COMB_QENT * 16;
+        uint32_t* o = out + w * ent * 16;
         jpt P;
         u256 pre, zi;
-        load_jpt(P, jac + w * EC_COMB_QENT * EC_COMB_JW);
+        load_jpt(P, jac + w * ent * EC_COMB_JW);
         load_u256(pre, o);
         fp_mul<C>(zi, inv, pre);
         fp_mul<C>(inv, inv, P.Z);
         apt a;
         jpt_to_aff<C>(a, P, zi);
         store_apt(o, a);
+        beta_x(w, 0, a);
     }
     // 2.
     u256_set_word(acc, 1);
 #pragma unroll 1
     for (uint32_t w = w0; w < w1; w++) {
-        uint32_t* e = jac + w * EC_COMB_QENT * EC_COMB_JW;
-        uint32_t* o = out + w * EC_COMB_QENT * 16;
+        uint32_t* e = jac + w * ent * EC_COMB_JW;
+        uint32_t* o = out + w * ent * 16;
         apt a;
         load_apt(a, o);
         jpt A;
@@ -796,7 +886,7 @@ CHIP_DEV void ec_comb_fill(uint32_t* __restrict__ jac, uint32_t* __restrict__ ou
         jdbl<C>(A, A);
         bool exc = false;   // j a + a with 2 <= j <= 7 is never P == Q (prime order n > 8)
 #pragma unroll 1
-        for (int j = 2; j <= EC_COMB_QENT; j++) {
+        for (int j = 2; j <= (int)ent; j++) {
             if (j > 2) jmadd_x<C>(A, A, a, exc);
             store_jpt(e + (uint32_t)(j - 1) * EC_COMB_JW, A);
             store_u256(o + (uint32_t)(j - 1) * 16, acc);
@@ -807,10 +897,10 @@ CHIP_DEV void ec_comb_fill(uint32_t* __restrict__ jac, uint32_t* __restrict__ ou
     fp_inv_vt<C>(inv, acc);
 #pragma unroll 1
     for (uint32_t w = w1; w-- > w0;) {
-        const uint32_t* e = jac + w * EC_COMB_QENT * EC_COMB_JW;
-        uint32_t* o = out + w * EC_COMB_QENT * 16;
+        const uint32_t* e = jac + w * ent * EC_COMB_JW;
+        uint32_t* o = out + w * ent * 16;
 #pragma unroll 1
-        for (int j = EC_COMB_QENT - 1; j >= 1; j--) {
+        for (int j = (int)ent - 1; j >= 1; j--) {
             jpt A;
             u256 pre, zi;
             load_jpt(A, e + (uint32_t)j * EC_COMB_JW);
@@ -820,6 +910,7 @@ CHIP_DEV void ec_comb_fill(uint32_t* __restrict__ jac, uint32_t* __restrict__ ou
             apt a;
             jpt_to_aff<C>(a, A, zi);
             store_apt(o + (uint32_t)j * 16, a);
+            beta_x(w, (uint32_t)j, a);
         }
     }
 }
@@ -827,14 +918,17 @@ CHIP_DEV void ec_comb_fill(uint32_t* __restrict__ jac, uint32_t* __restrict__ ou
 __global__ void __launch_bounds__(64) k_ecdsa_comb_chain(uint64_t n_keys, const KeyMeta* __restrict__ meta,
                                                          const uint32_t* __restrict__ ectab, uint32_t* __restrict__ jac,
                                                          uint32_t prio, uint32_t wa, uint32_t wb,
-                                                         const uint32_t* __restrict__ skip) {
+                                                         const uint32_t* __restrict__ skip, uint32_t glv) {
     const uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (k >= n_keys || (skip && *skip)) return;
     // the chain is the latency-bound critical path of the step: win VALU arbitration against the
     // throughput kernels of the main stream that share its SIMDs
     if (prio) __builtin_amdgcn_s_setprio(3);
+    // GLV: a secp256k1 table's windows [0, 13) with the low half, [13, 26) with the high one
+    const uint32_t wak = glv ? (wa ? EC_GLV_LO : 0u) : wa, wbk = glv ? (wa ? EC_GLV_WIN : EC_GLV_LO) : wb;
     if (ec_key_ok(meta, k, CHIP_SCHEME_R1)) ec_comb_chain<CURVE_R1 | CURVE_ILP>(ectab, jac, k, wa, wb);
-    else if (ec_key_ok(meta, k, CHIP_SCHEME_K1)) ec_comb_chain<CURVE_K1 | CURVE_ILP>(ectab, jac, k, wa, wb);
+    else if (ec_key_ok(meta, k, CHIP_SCHEME_K1))
+        ec_comb_chain<CURVE_K1 | CURVE_ILP>(ectab, jac, k, wak, wbk, glv ? EC_GLV_ENT : EC_COMB_QENT, glv ? EC_GLV_W : 4);
 }
 #ifndef EC_CHAIN_PAIR
 #define EC_CHAIN_PAIR 1   // the chain on lane pairs (k_ecdsa_comb_chain2); CHIP_EC_CHAIN_PAIR=0: one lane per key
@@ -843,14 +937,17 @@ __global__ void __launch_bounds__(64) k_ecdsa_comb_chain(uint64_t n_keys, const 
 __global__ void __launch_bounds__(64) k_ecdsa_comb_chain2(uint64_t n_keys, const KeyMeta* __restrict__ meta,
                                                           const uint32_t* __restrict__ ectab, uint32_t* __restrict__ jac,
                                                           uint32_t prio, uint32_t wa, uint32_t wb,
-                                                          const uint32_t* __restrict__ skip) {
+                                                          const uint32_t* __restrict__ skip, uint32_t glv) {
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t k = g >> 1;
     const uint32_t odd = (g & 1u) ? ~0u : 0u;
     if (k >= n_keys || (skip && *skip)) return;
     if (prio) __builtin_amdgcn_s_setprio(3);
+    const uint32_t wak = glv ? (wa ? EC_GLV_LO : 0u) : wa, wbk = glv ? (wa ? EC_GLV_WIN : EC_GLV_LO) : wb;
     if (ec_key_ok(meta, k, CHIP_SCHEME_R1)) ec_comb_chain2<CURVE_R1 | CURVE_ILP>(ectab, jac, k, wa, wb, odd);
-    else if (ec_key_ok(meta, k, CHIP_SCHEME_K1)) ec_comb_chain2<CURVE_K1 | CURVE_ILP>(ectab, jac, k, wa, wb, odd);
+    else if (ec_key_ok(meta, k, CHIP_SCHEME_K1))
+        ec_comb_chain2<CURVE_K1 | CURVE_ILP>(ectab, jac, k, wak, wbk, odd, glv ? EC_GLV_ENT : EC_COMB_QENT,
+                                             glv ? EC_GLV_W : 4);
 }
 // lane per key x group of `gw` windows of [wa, wb) (the fill is latency-bound: fewer windows per
 // lane = more lanes, at one shared inversion pair per lane)
@@ -860,7 +957,7 @@ __global__ void __launch_bounds__(64) k_ecdsa_comb_chain2(uint64_t n_keys, const
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EC_FILL_WAVES))) k_ecdsa_comb_fill(uint64_t n_keys, const KeyMeta* __restrict__ meta,
                                                          uint32_t* __restrict__ ctab, uint32_t* __restrict__ jac,
                                                          uint32_t wa, uint32_t wb, uint32_t gw,
-                                                         const uint32_t* __restrict__ skip) {
+                                                         const uint32_t* __restrict__ skip, uint32_t glv) {
     const uint32_t ng = (wb - wa + gw - 1) / gw;
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t k = g / ng;
@@ -870,8 +967,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EC_FIL
     const uint32_t w1 = w0 + gw < wb ? w0 + gw : wb;
     uint32_t* e = jac + k * EC_COMB_JAC_WORDS;
     uint32_t* out = ctab + k * EC_COMB_KEY_WORDS;
-    if (ec_key_ok(meta, k, CHIP_SCHEME_R1)) ec_comb_fill<CURVE_R1>(e, out, w0, w1);
-    else if (ec_key_ok(meta, k, CHIP_SCHEME_K1)) ec_comb_fill<CURVE_K1>(e, out, w0, w1);
+    if (ec_key_ok(meta, k, CHIP_SCHEME_R1)) {
+        ec_comb_fill<CURVE_R1>(e, out, w0, w1, nullptr);
+    } else if (ec_key_ok(meta, k, CHIP_SCHEME_K1)) {
+        if (!glv) {
+            ec_comb_fill<CURVE_K1>(e, out, w0, w1, nullptr);
+            return;
+        }
+        // the launch's group grp over the curve's own half, [0, 13) or [13, 26), EC_GLV_FILL_GROUP windows a lane: a
+        // window's 15 additions are twice P-256's 7, so half the windows keep the lanes' serial chains even
+        const uint32_t lo = wa ? EC_GLV_LO : 0u, hi = wa ? EC_GLV_WIN : EC_GLV_LO;
+        const uint32_t v0 = lo + grp * EC_GLV_FILL_GROUP, v1 = min(v0 + EC_GLV_FILL_GROUP, hi);
+        if (v0 < v1) ec_comb_fill<CURVE_K1>(e, out, v0, v1, out + EC_GLV_BETA_AT, EC_GLV_ENT);
+    }
 }
 
 // ---- work lists grouped by key (counting sort), so the lanes of a wave read one key's table ----
@@ -924,7 +1032,7 @@ __global__ void __launch_bounds__(256) k_ec_group_scatter(uint64_t n, const uint
 //   g   (C): s^-1 = wp^-1 * prefix * suffix, u1 = e s^-1, u2 = r s^-1, u1 G;
 //            slots 0-23 u1 G (X, Y, Z), 24-31 u2
 //   q   (D): + u2 Q from the key's table, x(R) mod n == r
-#define EC_MID_WORDS 41
+#define EC_MID_WORDS 42   // + word 41: the GLV signs and carries HALF 0 hands to HALF 1 (secp256k1)
 
 CHIP_DEV void mid_store(uint32_t* mid, uint64_t cap, uint32_t gid, int slot, const u256& v) {
 #pragma unroll
@@ -1122,7 +1230,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EC_G_W
 template <int C, int HALF>
 CHIP_DEV void comb_q_body(uint32_t blk, const uint32_t* __restrict__ list, const uint32_t* __restrict__ count,
                           const uint32_t* __restrict__ key_idx, const uint32_t* __restrict__ ctab,
-                          uint32_t* __restrict__ mid, uint64_t cap, uint8_t* __restrict__ status) {
+                          uint32_t* __restrict__ mid, uint64_t cap, uint8_t* __restrict__ status, uint32_t glv) {
     const uint32_t n = *count;
     const uint32_t gid = blk * blockDim.x + threadIdx.x;
     if (gid >= n || mid[(uint64_t)40 * cap + gid] != 1u) return;
@@ -1136,9 +1244,80 @@ CHIP_DEV void comb_q_body(uint32_t blk, const uint32_t* __restrict__ list, const
     mid_load(acc.Z, mid, cap, gid, 16);
     mid_load(u2, mid, cap, gid, 24);
     mid_load(r, mid, cap, gid, 32);
+    const uint32_t* qt = ctab + (uint64_t)key_idx[i] * EC_COMB_KEY_WORDS;
+    if (EC_CURVE(C) == CURVE_K1 && glv) {
+        // u2 Q = s1 |a1| Q + s2 |a2| (lambda Q): per radix-32 window one entry of Q's table and one of lambda Q's
+        // (beta x, y).  HALF 0 splits u2 and adds windows [0, 13) (the low half of the table), then hands |a1|, |a2|
+        // (in u2's slot), the signs and the digit carries (word 41) to HALF 1, which adds [13, 26) and checks.
+        u256 a1, a2;
+        bool n1, n2;
+        int cy1 = 0, cy2 = 0;
+        if (HALF == 0) {
+            glv_split(u2, a1, n1, a2, n2);
+        } else {
+            const uint32_t f = mid[(uint64_t)41 * cap + gid];
+            n1 = f & 1u;
+            n2 = (f >> 1) & 1u;
+            cy1 = (int)((f >> 2) & 1u);
+            cy2 = (int)((f >> 3) & 1u);
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                a1.w[q] = u2.w[q];
+                a2.w[q] = u2.w[4 + q];
+                a1.w[4 + q] = 0;
+                a2.w[4 + q] = 0;
+            }
+        }
+        const uint32_t* bxt = qt + EC_GLV_BETA_AT;
+        // signed digit of window w (bits [5w, 5w + 5) + carry, in [-15, 16]); |a| < 2^128 ends with no carry
+        auto digit = [](const u256& a, uint32_t w, int& cy) -> int {
+            const uint32_t b = w * EC_GLV_W, wi = b >> 5, sh = b & 31;
+            const uint32_t hi = wi < 7 ? a.w[wi + 1] : 0u;
+            const uint32_t bits = __builtin_amdgcn_alignbit(hi, a.w[wi], sh) & 31u;
+            const int v = (int)bits + cy;
+            cy = (v + 15) >> 5;
+            return v - (cy << 5);
+        };
+#pragma unroll 1
+        for (uint32_t w = HALF ? EC_GLV_LO : 0u; w < (HALF ? EC_GLV_WIN : EC_GLV_LO); w++) {
+            int d = digit(a1, w, cy1);
+            if (n1) d = -d;
+            if (d) {
+                load_apt(ent, qt + (w * EC_GLV_ENT + (uint32_t)(d < 0 ? -d : d) - 1) * 16);
+                add_digit_x<C>(acc, ent, d, exc);
+            }
+            d = digit(a2, w, cy2);
+            if (n2) d = -d;
+            if (d) {
+                const uint32_t e = w * EC_GLV_ENT + (uint32_t)(d < 0 ? -d : d) - 1;
+                load_u256(ent.x, bxt + e * 8);
+                load_u256(ent.y, qt + e * 16 + 8);
+                add_digit_x<C>(acc, ent, d, exc);
+            }
+        }
+        if (exc) {
+            mid[(uint64_t)40 * cap + gid] = 2u;
+            return;
+        }
+        if (HALF == 0) {
+            mid_store(mid, cap, gid, 0, acc.X);
+            mid_store(mid, cap, gid, 8, acc.Y);
+            mid_store(mid, cap, gid, 16, acc.Z);
+            u256 h;
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                h.w[q] = a1.w[q];
+                h.w[4 + q] = a2.w[q];
+            }
+            mid_store(mid, cap, gid, 24, h);
+            mid[(uint64_t)41 * cap + gid] = (n1 ? 1u : 0u) | (n2 ? 2u : 0u) | ((uint32_t)cy1 << 2) | ((uint32_t)cy2 << 3);
+            return;
+        }
+        status[i] = ecdsa_check<C>(acc, r) ? CHIP_VALID : CHIP_INVALID;
+        return;
+    }
     uint32_t dq[8];
     const uint32_t cq = recode<4>(dq, u2);
-    const uint32_t* qt = ctab + (uint64_t)key_idx[i] * EC_COMB_KEY_WORDS;
 #pragma unroll 1
     for (int wd = HALF * 4; wd < HALF * 4 + 4; wd++) {
         const uint32_t cur = dq[wd];
@@ -1187,11 +1366,12 @@ k_ecdsa_comb_q(const uint32_t* __restrict__ list_r1,
                                                       const uint32_t* __restrict__ ctab,
                                                       uint32_t* __restrict__ mid_r1,
                                                       uint32_t* __restrict__ mid_k1, uint64_t cap,
-                                                      uint8_t* __restrict__ status, uint32_t half) {
+                                                      uint8_t* __restrict__ status, uint32_t half, uint32_t glv) {
     if (blockIdx.x < half)
-        comb_q_body<CURVE_R1, HALF>(blockIdx.x, list_r1, counts + LIST_R1, key_idx, ctab, mid_r1, cap, status);
+        comb_q_body<CURVE_R1, HALF>(blockIdx.x, list_r1, counts + LIST_R1, key_idx, ctab, mid_r1, cap, status, glv);
     else
-        comb_q_body<CURVE_K1, HALF>(blockIdx.x - half, list_k1, counts + LIST_K1, key_idx, ctab, mid_k1, cap, status);
+        comb_q_body<CURVE_K1, HALF>(blockIdx.x - half, list_k1, counts + LIST_K1, key_idx, ctab, mid_k1, cap, status,
+                                    glv);
 }
 
 // E.  Lanes parked by an exceptional addition (mid state 2) verified again from their bytes with complete
@@ -1250,6 +1430,14 @@ __global__ void __launch_bounds__(256) k_ecdsa_comb_retry(const uint32_t* __rest
 
 uint64_t ecdsa_comb_key_words() { return EC_COMB_KEY_WORDS + EC_COMB_JAC_WORDS; }
 
+// CHIP_EC_GLV=0: secp256k1 through the full 65-window table like P-256 (round 5)
+static uint32_t ec_glv() {
+    static const uint32_t on = [] {
+        const char* e = getenv("CHIP_EC_GLV");
+        return e ? (uint32_t)(e[0] != '0') : 1u;
+    }();
+    return on;
+}
 // table halves: windows [0, EC_LO_WIN) and [EC_LO_WIN, 65); fill groups cover EC_FILL_GROUP windows each
 #define EC_LO_WIN 32
 void launch_ecdsa_comb_chain(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, const uint32_t* ectab,
@@ -1267,10 +1455,10 @@ void launch_ecdsa_comb_chain(hipStream_t st, uint64_t n_keys, const KeyMeta* met
     }();
     if (pair)
         hipLaunchKernelGGL(k_ecdsa_comb_chain2, dim3((uint32_t)((2 * n_keys + 63) / 64)), dim3(64), 0, st, n_keys, meta,
-                           ectab, jac, prio, wa, wb, skip);
+                           ectab, jac, prio, wa, wb, skip, ec_glv());
     else
         hipLaunchKernelGGL(k_ecdsa_comb_chain, dim3((uint32_t)((n_keys + 63) / 64)), dim3(64), 0, st, n_keys, meta,
-                           ectab, jac, prio, wa, wb, skip);
+                           ectab, jac, prio, wa, wb, skip, ec_glv());
 }
 void launch_ecdsa_comb_fill(hipStream_t st, uint64_t n_keys, const KeyMeta* meta, uint32_t* ctab, int half,
                             const uint32_t* skip) {
@@ -1284,7 +1472,7 @@ void launch_ecdsa_comb_fill(hipStream_t st, uint64_t n_keys, const KeyMeta* meta
     const uint32_t wa = half ? EC_LO_WIN : 0, wb = half ? EC_COMB_QWIN : EC_LO_WIN;
     const uint32_t ng = (wb - wa + gw - 1) / gw;
     hipLaunchKernelGGL(k_ecdsa_comb_fill, dim3((uint32_t)((n_keys * ng + 255) / 256)), dim3(256), 0, st, n_keys, meta,
-                       ctab, jac, wa, wb, gw, skip);
+                       ctab, jac, wa, wb, gw, skip, ec_glv());
 }
 
 // words of the hand-off area per list position, and of the wave products per list
@@ -1342,8 +1530,8 @@ void launch_ecdsa_comb_q(hipStream_t st, uint64_t n, const uint32_t* list_r1, co
     const uint32_t half = (uint32_t)((n + 255) / 256);
     if (table_half)
         hipLaunchKernelGGL(k_ecdsa_comb_q<1>, dim3(2 * half), dim3(256), 0, st, list_r1, list_k1, counts, b->key_idx, ctab,
-                           mid_r1, mid_k1, (uint64_t)n, status, half);
+                           mid_r1, mid_k1, (uint64_t)n, status, half, ec_glv());
     else
         hipLaunchKernelGGL(k_ecdsa_comb_q<0>, dim3(2 * half), dim3(256), 0, st, list_r1, list_k1, counts, b->key_idx, ctab,
-                           mid_r1, mid_k1, (uint64_t)n, status, half);
+                           mid_r1, mid_k1, (uint64_t)n, status, half, ec_glv());
 }

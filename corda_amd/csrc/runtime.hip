@@ -792,8 +792,10 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
     // the split Straus path (CHIP_ED_STRAUS_SPLIT, default on): its own rows, R' and prefix products
     const bool straus_split = c->straus_split && n && !(comb && w.eager) && !no_ed;
     // ... and for cold keys (device entry, fewer than 2 signatures per key: few if any take the comb): the hash and
-    // [S]B over the whole batch at once, beside the key prep on the second stream (CHIP_ED_STRAUS_EARLY, default on)
-    const bool s_early = straus_split && !(comb && w.eager) && (!comb || nd < 2 * nk) && !reuse && !vc && c->straus_early;
+    // [S]B over the whole batch at once, beside the key prep on the second stream (CHIP_ED_STRAUS_EARLY, default on).
+    // Only for batches the caller marks Ed25519-only: the front runs over every signature of the batch.
+    const bool s_early = straus_split && schemes == (1u << CHIP_SCHEME_ED25519) && !(comb && w.eager) &&
+                         (!comb || nd < 2 * nk) && !reuse && !vc && c->straus_early;
     if (straus_split) {
         HIPCHK(c, c->s_bmid.ensure(n * ed_comb_bmid_words() * 4 + 16));
         HIPCHK(c, c->s_xyz.ensure(n * 30 * 4 + 16));
