@@ -607,10 +607,14 @@ void launch_ecdsa_gcomb_build(hipStream_t st, uint32_t* gcomb) {
 #define EC_GLV_W 5                                             // window bits of the GLV table
 #define EC_GLV_ENT 16                                          // entries per window: signed digits |d| <= 16
 #define EC_GLV_WIN 26                                          // windows of a 129-bit signed radix-32 recoding
+#ifndef EC_GLV_LO
 #define EC_GLV_LO 13                                           // windows [0, 13) built and added with the low half
+#endif
 #define EC_GLV_FILL_GROUP 2                                    // windows per fill lane (7 of a launch's 8-9 groups)
 #define EC_GLV_BETA_AT (EC_GLV_WIN * EC_GLV_ENT * 16)            // beta x of entry (w, j): + (w * 16 + j - 1) * 8
 static_assert(EC_GLV_BETA_AT + EC_GLV_WIN * EC_GLV_ENT * 8 <= EC_COMB_KEY_WORDS, "GLV table");
+static_assert((EC_GLV_LO + EC_GLV_FILL_GROUP - 1) / EC_GLV_FILL_GROUP <= 8 &&
+              (EC_GLV_WIN - EC_GLV_LO + EC_GLV_FILL_GROUP - 1) / EC_GLV_FILL_GROUP <= 9, "GLV fill groups per half");
 static_assert(EC_GLV_WIN * EC_GLV_W >= 130, "GLV windows cover a 129-bit recoding");
 static_assert(EC_GLV_WIN * EC_GLV_ENT * EC_COMB_JW <= EC_COMB_QWIN * EC_COMB_QENT * EC_COMB_JW, "GLV scratch");
 static_assert(EC_COMB_QWIN * EC_COMB_QENT * 16 <= EC_COMB_KEY_WORDS, "P-256 table");
@@ -1269,24 +1273,34 @@ CHIP_DEV void comb_q_body(uint32_t blk, const uint32_t* __restrict__ list, const
             }
         }
         const uint32_t* bxt = qt + EC_GLV_BETA_AT;
-        // signed digit of window w (bits [5w, 5w + 5) + carry, in [-15, 16]); |a| < 2^128 ends with no carry
-        auto digit = [](const u256& a, uint32_t w, int& cy) -> int {
-            const uint32_t b = w * EC_GLV_W, wi = b >> 5, sh = b & 31;
-            const uint32_t hi = wi < 7 ? a.w[wi + 1] : 0u;
-            const uint32_t bits = __builtin_amdgcn_alignbit(hi, a.w[wi], sh) & 31u;
-            const int v = (int)bits + cy;
+        // |a| < 2^128 in four words, shifted down one window at a time (no dynamically indexed register array); the
+        // signed digit of the window (its 5 low bits + carry, in [-15, 16]); the last window ends with no carry
+        uint32_t s1[4], s2[4];
+        constexpr int SK = HALF ? EC_GLV_LO * EC_GLV_W : 0, SW = SK / 32, SB = SK % 32;   // HALF 1 resumes at window 13
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const uint32_t l1 = q + SW < 4 ? a1.w[q + SW] : 0u, h1 = q + SW + 1 < 4 ? a1.w[q + SW + 1] : 0u;
+            const uint32_t l2 = q + SW < 4 ? a2.w[q + SW] : 0u, h2 = q + SW + 1 < 4 ? a2.w[q + SW + 1] : 0u;
+            s1[q] = SB ? __builtin_amdgcn_alignbit(h1, l1, SB) : l1;
+            s2[q] = SB ? __builtin_amdgcn_alignbit(h2, l2, SB) : l2;
+        }
+        auto digit = [](uint32_t (&a)[4], int& cy) -> int {
+            const int v = (int)(a[0] & 31u) + cy;
+#pragma unroll
+            for (int q = 0; q < 3; q++) a[q] = __builtin_amdgcn_alignbit(a[q + 1], a[q], EC_GLV_W);
+            a[3] >>= EC_GLV_W;
             cy = (v + 15) >> 5;
             return v - (cy << 5);
         };
 #pragma unroll 1
         for (uint32_t w = HALF ? EC_GLV_LO : 0u; w < (HALF ? EC_GLV_WIN : EC_GLV_LO); w++) {
-            int d = digit(a1, w, cy1);
+            int d = digit(s1, cy1);
             if (n1) d = -d;
             if (d) {
                 load_apt(ent, qt + (w * EC_GLV_ENT + (uint32_t)(d < 0 ? -d : d) - 1) * 16);
                 add_digit_x<C>(acc, ent, d, exc);
             }
-            d = digit(a2, w, cy2);
+            d = digit(s2, cy2);
             if (n2) d = -d;
             if (d) {
                 const uint32_t e = w * EC_GLV_ENT + (uint32_t)(d < 0 ? -d : d) - 1;
@@ -1357,8 +1371,11 @@ CHIP_DEV void comb_q_body(uint32_t blk, const uint32_t* __restrict__ list, const
 #ifndef EC_Q0_WAVES
 #define EC_Q0_WAVES 3
 #endif
+#ifndef EC_Q1_WAVES
+#define EC_Q1_WAVES 3   // HALF 1 with the GLV windows of secp256k1 compiles to 170 VGPRs: held to 3 waves per SIMD
+#endif
 template <int HALF>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALF == 0 ? EC_Q0_WAVES : 1)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(HALF == 0 ? EC_Q0_WAVES : EC_Q1_WAVES)))
 k_ecdsa_comb_q(const uint32_t* __restrict__ list_r1,
                                                       const uint32_t* __restrict__ list_k1,
                                                       const uint32_t* __restrict__ counts,
