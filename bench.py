@@ -88,8 +88,14 @@ ED_STRAUS_SPLIT_MACS_PER_VERIFY = (1_008 + 64) * 55 + (1_279 + 8) * 100   # 187,
 #   ECDSA comb (P-256 / secp256k1, 8 x 32-bit limbs): a mixed addition = 7 mults (64 products) +
 #   4 squarings (36) = 592; 17 G windows (radix 2^16) + 65 Q windows (radix 16) = 82 additions;
 #   17 scalar Montgomery mults (128 each: s R, 12 wave-scan, 2 finalize, u1, u2) + the x(R) check (100)
-ECDSA_COMB_MACS_PER_VERIFY = 82 * 592 + 17 * 128 + 100              # 50,820
-ECDSA_Q_MACS_PER_VERIFY = 65 * 592 + 100                            # k_ecdsa_comb_q: 38,580
+ECDSA_COMB_MACS_PER_VERIFY = 82 * 592 + 17 * 128 + 100              # 50,820 (P-256)
+ECDSA_Q_MACS_PER_VERIFY = 65 * 592 + 100                            # k_ecdsa_comb_q: 38,580 (P-256)
+#   secp256k1 with GLV (round 6, CHIP_EC_GLV): u2 Q = a1 Q + a2 (lambda Q) with 128-bit halves over radix-32
+#   tables, 52 additions instead of 65, + the split (2 x 64 products for the rounding, 3 Montgomery mults);
+#   cfg3 interleaves the curves 1:1, so its per-signature figures are the mean of the two
+ECDSA_K1_SPLIT_MACS = 2 * 64 + 3 * 128
+ECDSA_MIXED_MACS_PER_VERIFY = (82 + 69) * 592 // 2 + 17 * 128 + 100 + ECDSA_K1_SPLIT_MACS // 2    # 47,228
+ECDSA_MIXED_Q_MACS_PER_VERIFY = (65 + 52) * 592 // 2 + 100 + ECDSA_K1_SPLIT_MACS // 2             # 34,988
 # SHA-256 compression, canonical 32-bit operations (rotates as one funnel shift): 64 rounds x 24
 # (Sigma1 5, Ch 3, T1 adds 4, Sigma0 5, Maj 4, 3 state adds) + 48 schedule words x 13 + 8 = 2,168
 SHA256_OPS_PER_COMPRESSION = 2_168
@@ -971,11 +977,11 @@ def ecdsa_leg(args, ctx, world, rank, torch, dev, dist, D, G, native, threads, s
         "ecdsa_ms_per_step": step_ms,
         "ecdsa_front_ms": front_ms, "ecdsa_tables_aux_ms": tab_ms,
         "ecdsa_q_kernel_ms": r1_ms + k1_ms,   # k_ecdsa_comb_q: low + high table half, both curves per launch
-        "ecdsa_roofline_frac": ECDSA_COMB_MACS_PER_VERIFY * n_arith / (step_ms * 1e-3) / 1e12 / MAC_PEAK_T,
-        "ecdsa_q_roofline_frac": ECDSA_Q_MACS_PER_VERIFY * n_arith / ((r1_ms + k1_ms) * 1e-3) / 1e12 / MAC_PEAK_T,
-        "ecdsa_roofline_note": "%d MACs/signature (82 mixed additions x 592 + scalar work) over the whole step; "
-                               "q kernels %d MACs/signature over their own time" % (ECDSA_COMB_MACS_PER_VERIFY,
-                                                                                    ECDSA_Q_MACS_PER_VERIFY),
+        "ecdsa_roofline_frac": ECDSA_MIXED_MACS_PER_VERIFY * n_arith / (step_ms * 1e-3) / 1e12 / MAC_PEAK_T,
+        "ecdsa_q_roofline_frac": ECDSA_MIXED_Q_MACS_PER_VERIFY * n_arith / ((r1_ms + k1_ms) * 1e-3) / 1e12 / MAC_PEAK_T,
+        "ecdsa_roofline_note": "%d MACs/signature (mean of P-256's 82 mixed additions and secp256k1's 69 with GLV, x "
+                               "592, + scalar work) over the whole step; q kernels %d MACs/signature over their own time"
+                               % (ECDSA_MIXED_MACS_PER_VERIFY, ECDSA_MIXED_Q_MACS_PER_VERIFY),
     }
     # the same batch with the key state kept across batches (CHIP_FLAG_KEY_CACHE, a context of its own): the
     # per-key comb tables (ecdsa_tables_aux_ms above) are reused from the previous step
