@@ -504,6 +504,32 @@ __device__ __forceinline__ bool key_eq(const uint8_t* pool, uint64_t a, uint32_t
     return ok;
 }
 
+// Two input StateRefs pass 1 checked to be canonical encodings (kryo.state_ref: 74 fixed bytes, zn, the zn-byte
+// index varint, 65 fixed bytes, the 32-byte txhash, 01 00 00): equal bytes iff equal lengths, equal bytes
+// [72, 88) (zn and the index, the rest fixed) and equal txhash [140 + zn, 172 + zn) — 48 bytes read per side
+// instead of all 175 + zn, the txhash only when the indices agree (checkNoDuplicateInputs, k_stx_post)
+__device__ __forceinline__ bool stateref_eq(const uint8_t* pool, uint64_t a, uint32_t la, uint64_t b, uint32_t lb) {
+    if (la != lb) return false;
+    DStream x, y;
+    uint32_t u[4], v[4];
+    x.open(pool, a + 72);
+    y.open(pool, b + 72);
+    x.take4(u);
+    y.take4(v);
+    if ((u[0] ^ v[0]) | (u[1] ^ v[1]) | (u[2] ^ v[2]) | (u[3] ^ v[3])) return false;
+    const uint32_t h = 140 + (la - 175);
+    x.open(pool, a + h);
+    y.open(pool, b + h);
+    bool ok = true;
+#pragma unroll
+    for (int k = 0; k < 2; k++) {
+        x.take4(u);
+        y.take4(v);
+        ok &= ((u[0] ^ v[0]) | (u[1] ^ v[1]) | (u[2] ^ v[2]) | (u[3] ^ v[3])) == 0;
+    }
+    return ok;
+}
+
 // A payload run of n bytes inside a level-1 field: where it starts in the blob pool when it lies in one
 // chunk (the context's pool holds a copy of the blobs at their input offsets, so the offset is reused),
 // else it is de-chunked into the blob's extra region (4-byte aligned); `extra` counts those bytes.
@@ -859,7 +885,7 @@ __device__ __noinline__ int fused_post(uint64_t t, int st, uint64_t comps, uint6
         const uint64_t ao = ca.off(in_first + i);
         const uint32_t al = ca.len(in_first + i);
         for (uint64_t j = i + 1; j < in_count; j++)
-            if (key_eq(pool, ao, al, ca.off(in_first + j), ca.len(in_first + j))) {
+            if (stateref_eq(pool, ao, al, ca.off(in_first + j), ca.len(in_first + j))) {
                 st = CHIP_STX_INVARIANT;
                 break;
             }
@@ -1928,7 +1954,7 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(KRYO_P
             const uint64_t ao = ca.off(in_first + i);
             const uint32_t al = ca.len(in_first + i);
             for (uint64_t j = i + 1; j < in_count; j++)
-                if (key_eq(o.pool, ao, al, ca.off(in_first + j), ca.len(in_first + j))) {
+                if (stateref_eq(o.pool, ao, al, ca.off(in_first + j), ca.len(in_first + j))) {
                     st = CHIP_STX_INVARIANT;
                     break;
                 }
