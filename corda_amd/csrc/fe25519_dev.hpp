@@ -192,16 +192,21 @@ CHIP_DEV void fe_sq2(fe& h, const fe& f) {
     for (int k = 0; k < 10; k++) t[k] <<= 1;
     fe_carry64(h, t);
 }
+// (a local accumulator: with h aliasing f — fe_sqn(x, x, 2) in fe_pow22523 — the compiler kept ~380 registers
+// live through the square-root chain, so every kernel decoding a key ran at 1 wave per SIMD)
 CHIP_DEV void fe_sqn(fe& h, const fe& f, int n) {
-    fe_sq(h, f);
-    for (int i = 1; i < n; i++) fe_sq(h, h);
+    fe t;
+    fe_sq(t, f);
+    for (int i = 1; i < n; i++) fe_sq(t, t);
+    h = t;
 }
 
 // z^(2^250 - 1) and helpers for inversion / square roots
 CHIP_DEV void fe_pow_common(fe& z250, fe& z11, const fe& z) {
     fe z2, z9, t, z5, z10, z20, z50, z100;
     fe_sq(z2, z);            // 2
-    fe_sqn(t, z2, 2);        // 8
+    fe_sq(t, z2);
+    fe_sq(t, t);             // 8
     fe_mul(z9, t, z);        // 9
     fe_mul(z11, z9, z2);     // 11
     fe_sq(t, z11);           // 22
@@ -221,17 +226,22 @@ CHIP_DEV void fe_pow_common(fe& z250, fe& z11, const fe& z) {
     fe_sqn(t, t, 50);
     fe_mul(z250, t, z50);    // 2^250 - 1
 }
+// (both write a local and copy it out: callers pass h aliasing z, e.g. ge_frombytes' fe_pow22523(X, X))
 CHIP_DEV void fe_invert(fe& h, const fe& z) {
-    fe z250, z11;
+    fe z250, z11, r;
     fe_pow_common(z250, z11, z);
     fe_sqn(z250, z250, 5);   // 2^255 - 32
-    fe_mul(h, z250, z11);    // 2^255 - 21 = p - 2
+    fe_mul(r, z250, z11);    // 2^255 - 21 = p - 2
+    h = r;
 }
+// (the two squarings written out: as fe_sqn(x, x, 2) the whole square root compiled to ~380 live registers)
 CHIP_DEV void fe_pow22523(fe& h, const fe& z) {
-    fe z250, z11;
+    fe z250, z11, r, t;
     fe_pow_common(z250, z11, z);
-    fe_sqn(z250, z250, 2);   // 2^252 - 4
-    fe_mul(h, z250, z);      // 2^252 - 3
+    fe_sq(t, z250);
+    fe_sq(t, t);             // 2^252 - 4
+    fe_mul(r, t, z);         // 2^252 - 3
+    h = r;
 }
 
 // canonical encoding into 8 little-endian words (input carried or loose < 2^31 limbs)
