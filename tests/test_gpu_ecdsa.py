@@ -57,3 +57,24 @@ def test_ecdsa_comb_stats_and_large_batch(ctx_modes):
     assert np.array_equal(st, b.expected)
     s = c.stats()
     assert s.kernel_launches[native.K_EC_TABLES] >= 1
+
+
+def test_ecdsa_comb_without_glv_subprocess():
+    """The round-5 secp256k1 schedule (CHIP_EC_GLV=0: the 65-window radix-16 table, a process-wide switch) still
+    gives the labels' status bytes: a child process verifies a comb-forced r1/k1 batch with the switch off, the
+    in-process contexts covering the GLV default."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys; sys.path[:0] = [%r, %r]\n"
+            "import numpy as np, corda_amd, cordagen as G\n"
+            "from corda_amd import native\n"
+            "c = corda_amd.Context(0, flags=native.FLAG_FORCE_COMB)\n"
+            "b = G.ecdsa_batch(3000, n_keys=24, corrupt=0.3, seed=0x5EED0619)\n"
+            "st, _ = c.verify_batch(b)\n"
+            "c.close()\n"
+            "sys.exit(0 if np.array_equal(st, b.expected) else 3)\n") % (root, os.path.join(root, "tools"))
+    env = dict(os.environ, CHIP_EC_GLV="0")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-2000:]
