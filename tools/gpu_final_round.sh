@@ -11,5 +11,5 @@ python3 -c "
 import json; d=json.load(open('$OUT/bench.json')); s=d['secondary']
 print('value', round(d['value']/1e6,2), 'ms', round(d['ms_per_step'],3), d['correct_vs_labels'])
 for k in ('cfg2_host_path_sigs_per_s','cfg2_host_path_pinned_sigs_per_s','ed25519_cold_sigs_per_s','cfg2_key_cache_sigs_per_s','ecdsa_mixed_sigs_per_s','cfg4_from_bytes_verified_tx_per_s','txids_per_s','notary_commit_ms','notary_rounds'):
-    v=s.get(k); print(k, round(v/1e6,2) if isinstance(v,(int,float)) else v)
+    v=s.get(k); print(k, (round(v/1e6,2) if k.endswith('_per_s') else round(v,3)) if isinstance(v,(int,float)) else v)
 print('stx_parse_ms', s.get('stx_parse_ms'), 'notary', s.get('notary_commit_ms'))"
