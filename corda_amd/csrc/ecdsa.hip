@@ -610,11 +610,11 @@ void launch_ecdsa_gcomb_build(hipStream_t st, uint32_t* gcomb) {
 #ifndef EC_GLV_LO
 #define EC_GLV_LO 13                                           // windows [0, 13) built and added with the low half
 #endif
+#ifndef EC_GLV_FILL_GROUP
 #define EC_GLV_FILL_GROUP 2                                    // windows per fill lane (7 of a launch's 8-9 groups)
+#endif
 #define EC_GLV_BETA_AT (EC_GLV_WIN * EC_GLV_ENT * 16)            // beta x of entry (w, j): + (w * 16 + j - 1) * 8
 static_assert(EC_GLV_BETA_AT + EC_GLV_WIN * EC_GLV_ENT * 8 <= EC_COMB_KEY_WORDS, "GLV table");
-static_assert((EC_GLV_LO + EC_GLV_FILL_GROUP - 1) / EC_GLV_FILL_GROUP <= 8 &&
-              (EC_GLV_WIN - EC_GLV_LO + EC_GLV_FILL_GROUP - 1) / EC_GLV_FILL_GROUP <= 9, "GLV fill groups per half");
 static_assert(EC_GLV_WIN * EC_GLV_W >= 130, "GLV windows cover a 129-bit recoding");
 static_assert(EC_GLV_WIN * EC_GLV_ENT * EC_COMB_JW <= EC_COMB_QWIN * EC_COMB_QENT * EC_COMB_JW, "GLV scratch");
 static_assert(EC_COMB_QWIN * EC_COMB_QENT * 16 <= EC_COMB_KEY_WORDS, "P-256 table");
@@ -960,9 +960,9 @@ __global__ void __launch_bounds__(64) k_ecdsa_comb_chain2(uint64_t n_keys, const
 #endif
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EC_FILL_WAVES))) k_ecdsa_comb_fill(uint64_t n_keys, const KeyMeta* __restrict__ meta,
                                                          uint32_t* __restrict__ ctab, uint32_t* __restrict__ jac,
-                                                         uint32_t wa, uint32_t wb, uint32_t gw,
+                                                         uint32_t wa, uint32_t wb, uint32_t gw, uint32_t ng,
                                                          const uint32_t* __restrict__ skip, uint32_t glv) {
-    const uint32_t ng = (wb - wa + gw - 1) / gw;
+    // ng lanes per key: P-256's (wb - wa) / gw groups, or more when the GLV half needs them (the rest return)
     const uint64_t g = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     const uint64_t k = g / ng;
     const uint32_t grp = (uint32_t)(g % ng);
@@ -972,10 +972,10 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(EC_FIL
     uint32_t* e = jac + k * EC_COMB_JAC_WORDS;
     uint32_t* out = ctab + k * EC_COMB_KEY_WORDS;
     if (ec_key_ok(meta, k, CHIP_SCHEME_R1)) {
-        ec_comb_fill<CURVE_R1>(e, out, w0, w1, nullptr);
+        if (w0 < w1) ec_comb_fill<CURVE_R1>(e, out, w0, w1, nullptr);
     } else if (ec_key_ok(meta, k, CHIP_SCHEME_K1)) {
         if (!glv) {
-            ec_comb_fill<CURVE_K1>(e, out, w0, w1, nullptr);
+            if (w0 < w1) ec_comb_fill<CURVE_K1>(e, out, w0, w1, nullptr);
             return;
         }
         // the launch's group grp over the curve's own half, [0, 13) or [13, 26), EC_GLV_FILL_GROUP windows a lane: a
@@ -1487,9 +1487,10 @@ void launch_ecdsa_comb_fill(hipStream_t st, uint64_t n_keys, const KeyMeta* meta
         return v ? v : 1u;
     }();
     const uint32_t wa = half ? EC_LO_WIN : 0, wb = half ? EC_COMB_QWIN : EC_LO_WIN;
-    const uint32_t ng = (wb - wa + gw - 1) / gw;
+    const uint32_t kw = half ? EC_GLV_WIN - EC_GLV_LO : EC_GLV_LO;   // a secp256k1 GLV table's windows in this half
+    const uint32_t ng = std::max((wb - wa + gw - 1) / gw, ec_glv() ? (kw + EC_GLV_FILL_GROUP - 1) / EC_GLV_FILL_GROUP : 0u);
     hipLaunchKernelGGL(k_ecdsa_comb_fill, dim3((uint32_t)((n_keys * ng + 255) / 256)), dim3(256), 0, st, n_keys, meta,
-                       ctab, jac, wa, wb, gw, skip, ec_glv());
+                       ctab, jac, wa, wb, gw, ng, skip, ec_glv());
 }
 
 // words of the hand-off area per list position, and of the wave products per list
