@@ -143,11 +143,11 @@ __global__ void __launch_bounds__(256) k_ed_comb_partition(const uint32_t* __res
 // ---- per-key tables ----
 // chain: P_w = 2^(W w) (-A) for every window, stashed (extended form, 40 words) in the window's last row
 // (affine rows: from row 1 on).  One lane per key: W doublings per window, the only serial part of the comb path.
-#if ED_COMB_AFFINE
-#define ED_COMB_STASH 1
-#else
-#define ED_COMB_STASH (ED_COMB_AENT - 1)
-#endif
+#define ED_COMB_STASH_C (ED_COMB_AENT - 1)   // cached rows: P_w in the window's last row until the fill reads it
+#define ED_COMB_STASH_A 1                    // affine rows: from row 1 on
+CHIP_DEV uint32_t ed_stash_at(uint32_t w, uint32_t aff) {   // word offset of window w's stashed P_w
+    return aff ? (w * ED_COMB_AENT + ED_COMB_STASH_A) * ED_COMB_ROW_A : (w * ED_COMB_AENT + ED_COMB_STASH_C) * ED_COMB_ROW_C;
+}
 #ifndef ED_CHAIN_PAIR
 #define ED_CHAIN_PAIR 0   // 1: the doubling chain on lane pairs (k_ed_comb_chain2): chain 0.60 -> 0.44 ms, but the
                           // [S]B kernel beside it slowed by as much (0.76 -> 1.2 ms): 263-265M vs 265-269M
@@ -157,7 +157,7 @@ __global__ void __launch_bounds__(64) k_ed_comb_chain(const uint32_t* __restrict
                                                       uint32_t eager, const KeyMeta* __restrict__ meta,
                                                       const uint32_t* __restrict__ slot_key,
                                                       const uint32_t* __restrict__ nega, uint32_t* __restrict__ ctab,
-                                                      const uint32_t* __restrict__ skip) {
+                                                      const uint32_t* __restrict__ skip, uint32_t aff) {
     const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t nslots = eager ? max_slots : ctr[ED_CTR_NSLOTS];
     if (s >= nslots || (skip && *skip)) return;
@@ -170,9 +170,9 @@ __global__ void __launch_bounds__(64) k_ed_comb_chain(const uint32_t* __restrict
     const uint32_t k = eager ? s : slot_key[s];
     ge_p3 P;
     ed_load_p3(P, nega + (uint64_t)k * 40);
-    uint32_t* tab = ctab + (uint64_t)s * ED_COMB_KEY_WORDS;
+    uint32_t* tab = ctab + (uint64_t)s * (aff ? ED_COMB_KEY_WORDS_A : ED_COMB_KEY_WORDS_C);
     for (int w = 0; w < ED_COMB_AWIN; w++) {
-        ed_store_p3(tab + ((uint32_t)w * ED_COMB_AENT + ED_COMB_STASH) * ED_COMB_ROW, P);
+        ed_store_p3(tab + ed_stash_at((uint32_t)w, aff), P);
         if (w + 1 == ED_COMB_AWIN) break;
         ge_p2 r;
         ge_p3_to_p2(r, P);
@@ -255,7 +255,7 @@ __global__ void __launch_bounds__(64) k_ed_comb_chain2(const uint32_t* __restric
                                                        uint32_t eager, const KeyMeta* __restrict__ meta,
                                                        const uint32_t* __restrict__ slot_key,
                                                        const uint32_t* __restrict__ nega, uint32_t* __restrict__ ctab,
-                                                       const uint32_t* __restrict__ skip) {
+                                                       const uint32_t* __restrict__ skip, uint32_t aff) {
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t s = g >> 1;
     const uint32_t odd = (g & 1u) ? ~0u : 0u;
@@ -269,9 +269,9 @@ __global__ void __launch_bounds__(64) k_ed_comb_chain2(const uint32_t* __restric
     const uint32_t k = eager ? s : slot_key[s];
     ge_p3 P;
     ed_load_p3(P, nega + (uint64_t)k * 40);
-    uint32_t* tab = ctab + (uint64_t)s * ED_COMB_KEY_WORDS;
+    uint32_t* tab = ctab + (uint64_t)s * (aff ? ED_COMB_KEY_WORDS_A : ED_COMB_KEY_WORDS_C);
     for (int w = 0; w < ED_COMB_AWIN; w++) {
-        if (!odd) ed_store_p3(tab + ((uint32_t)w * ED_COMB_AENT + ED_COMB_STASH) * ED_COMB_ROW, P);
+        if (!odd) ed_store_p3(tab + ed_stash_at((uint32_t)w, aff), P);
         if (w + 1 == ED_COMB_AWIN) break;
         ge_p2 r;
         ge_p3_to_p2(r, P);
@@ -300,7 +300,6 @@ CHIP_DEV void ed_store_row(uint32_t* __restrict__ dst, const ge_cached& c) {
         dst[30 + i] = c.T2d.v[i];
     }
 }
-#if !ED_COMB_AFFINE
 // Two lanes per key x window (adjacent lanes of one wave): rows 0..16 from P_w, rows 17..32 from 17 P_w (4
 // doublings + 1 addition first), so the serial chain of additions per lane halves.  Both read the stash in the
 // last row before either writes a row (same wave, the load precedes the divergence); the second writes the
@@ -310,6 +309,7 @@ CHIP_DEV void ed_store_row(uint32_t* __restrict__ dst, const ge_cached& c) {
 __global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict__ ctr, uint32_t max_slots,
                                                       uint32_t eager, const KeyMeta* __restrict__ meta,
                                                       uint32_t* __restrict__ ctab, const uint32_t* __restrict__ skip) {
+    constexpr uint32_t ED_COMB_ROW = ED_COMB_ROW_C, ED_COMB_KEY_WORDS = ED_COMB_KEY_WORDS_C;
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     const uint32_t s = g / (ED_COMB_AWIN * ED_FILL_SPLIT), r = g % (ED_COMB_AWIN * ED_FILL_SPLIT);
     const uint32_t w = r / ED_FILL_SPLIT, h = r % ED_FILL_SPLIT;
@@ -317,7 +317,7 @@ __global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict
     if (eager && !ed_key_ok(meta, s)) return;
     uint32_t* e = ctab + (uint64_t)s * ED_COMB_KEY_WORDS + (uint64_t)w * ED_COMB_AENT * ED_COMB_ROW;
     ge_p3 P;
-    ed_load_p3(P, e + ED_COMB_STASH * ED_COMB_ROW);   // P_w, stashed by the chain
+    ed_load_p3(P, e + ED_COMB_STASH_C * ED_COMB_ROW);   // P_w, stashed by the chain
     ge_cached c1, c;
     ge_p3_to_cached(c1, P);
     ge_p3 Q = P;
@@ -351,7 +351,6 @@ __global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict
         ed_store_row(e + ED_COMB_ROW * j, c);
     }
 }
-#else
 // Affine rows in three steps (one lane per key x window in a and b):
 //   a: j P_w for j = 1..2^(W-1) by additions; row j holds (X_j Z_1..Z_{j-1}, Y_j Z_1..Z_{j-1}, Z_j), so that step
 //      b needs no prefix array: with inv = 1 / (Z_1..Z_j), x_j = row.X inv and the next inv = inv Z_j;
@@ -375,10 +374,11 @@ CHIP_DEV void ed_load_fe(fe& f, const uint32_t* __restrict__ src) {
 #pragma unroll
     for (int i = 0; i < 10; i++) f.v[i] = src[i];
 }
-__global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict__ ctr, uint32_t max_slots,
-                                                      uint32_t eager, const KeyMeta* __restrict__ meta,
-                                                      uint32_t* __restrict__ ctab, uint32_t* __restrict__ fz,
-                                                      const uint32_t* __restrict__ cached) {
+__global__ void __launch_bounds__(256) k_ed_comb_fill_a(const uint32_t* __restrict__ ctr, uint32_t max_slots,
+                                                        uint32_t eager, const KeyMeta* __restrict__ meta,
+                                                        uint32_t* __restrict__ ctab, uint32_t* __restrict__ fz,
+                                                        const uint32_t* __restrict__ cached) {
+    constexpr uint32_t ED_COMB_ROW = ED_COMB_ROW_A, ED_COMB_KEY_WORDS = ED_COMB_KEY_WORDS_A;
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t s, w;
     bool skip = false;
@@ -443,6 +443,7 @@ __global__ void __launch_bounds__(256) k_ed_comb_fill_b(const uint32_t* __restri
                                                         uint32_t eager, const KeyMeta* __restrict__ meta,
                                                         uint32_t* __restrict__ ctab, const uint32_t* __restrict__ zinv,
                                                         const uint32_t* __restrict__ cached) {
+    constexpr uint32_t ED_COMB_ROW = ED_COMB_ROW_A, ED_COMB_KEY_WORDS = ED_COMB_KEY_WORDS_A;
     const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
     uint32_t s, w;
     bool skip = false;
@@ -476,7 +477,6 @@ __global__ void __launch_bounds__(256) k_ed_comb_fill_b(const uint32_t* __restri
 #pragma unroll
     for (int i = 0; i < ED_COMB_ROW; i++) e[i] = (i == 0 || i == 10) ? 1u : 0u;   // identity
 }
-#endif
 
 // ---- verify: one lane per comb-list position ----
 // blocks b, b+8, b+16, ... are dispatched to one XCD: give them consecutive work.  `used` = blocks
@@ -774,6 +774,8 @@ __global__ void __launch_bounds__(256, ED_BHALF_MINW) k_ed_comb_bhalf(const uint
     }
 }
 
+// AFF: the key's rows are affine Niels (ED_COMB_ROW_A, tables kept across batches) instead of cached ones
+template <bool AFF>
 __global__ void __launch_bounds__(256, ED_AHALF_MINW) k_ed_comb_ahalf(const uint32_t* __restrict__ list,
                                                                       const uint32_t* __restrict__ ctr,
                                                        const uint32_t* __restrict__ key_idx,
@@ -789,7 +791,8 @@ __global__ void __launch_bounds__(256, ED_AHALF_MINW) k_ed_comb_ahalf(const uint
     const uint32_t k = key_idx[i];
     // digit d of window w reads row |d| of the window, signed
     // the key's table as a 32-bit word offset from the uniform base (<= 2^32 words of tables): one VGPR, not two
-    const uint32_t toff = (uint32_t)key_slot[k] * (uint32_t)ED_COMB_KEY_WORDS;
+    constexpr uint32_t ED_COMB_ROW = AFF ? ED_COMB_ROW_A : ED_COMB_ROW_C;
+    const uint32_t toff = (uint32_t)key_slot[k] * (uint32_t)(AFF ? ED_COMB_KEY_WORDS_A : ED_COMB_KEY_WORDS_C);
     // the row as a 32-bit word offset from the uniform base (slot * ED_BMID_W < 2^32): one VGPR through the loop;
     // p itself is rebuilt after the loop from the wave's first position (an SGPR) and the lane id
     const uint32_t ro = (early ? i : p) * (uint32_t)ED_BMID_W;
@@ -821,7 +824,7 @@ __global__ void __launch_bounds__(256, ED_AHALF_MINW) k_ed_comb_ahalf(const uint
     };
     ge_p3 u;
     uint32_t cur = 0;
-#if ED_COMB_AFFINE
+    if constexpr (AFF) {
     // affine Niels rows: a mixed addition (3 multiplications) after a conversion that yields 2Z directly
     fe qp, qm, xy2d, z2;
 #pragma unroll 1
@@ -836,7 +839,7 @@ __global__ void __launch_bounds__(256, ED_AHALF_MINW) k_ed_comb_ahalf(const uint
                              d < 0);
         ge_madd_signed(t, u, z2, qp, qm, xy2d, (uint32_t)(d >> 31));
     }
-#else
+    } else {
     ge_cached ca;
 #pragma unroll 1
     for (uint32_t w = 0; w < ED_COMB_AWIN; w++) {
@@ -846,7 +849,7 @@ __global__ void __launch_bounds__(256, ED_AHALF_MINW) k_ed_comb_ahalf(const uint
         ed_load_row_signed(ca, ctab + (toff + (w * ED_COMB_AENT + (uint32_t)(d < 0 ? -d : d)) * ED_COMB_ROW), d < 0);
         ge_add_row(t, u, ca, (uint32_t)(d >> 31));
     }
-#endif
+    }
     // projective R' = (X : Y : Z), stored structure-of-arrays for the finish kernel
     fe X, Y, Z;
     fe_mul(X, t.X, t.T);
@@ -964,25 +967,25 @@ void launch_ed_comb_build(hipStream_t st, uint64_t n, uint64_t n_keys, const Key
     if (!n || !n_keys || !w.max_slots) return;
 #if ED_CHAIN_PAIR
     hipLaunchKernelGGL(k_ed_comb_chain2, dim3(nblk((uint64_t)w.max_slots * 2, 64)), dim3(64), 0, st, w.ctr, w.max_slots,
-                       w.eager, meta, w.slot_key, w.nega, w.ctab, w.skip);
+                       w.eager, meta, w.slot_key, w.nega, w.ctab, w.skip, w.affine);
 #else
     hipLaunchKernelGGL(k_ed_comb_chain, dim3(nblk(w.max_slots, 64)), dim3(64), 0, st, w.ctr, w.max_slots, w.eager, meta,
-                       w.slot_key, w.nega, w.ctab, w.skip);
+                       w.slot_key, w.nega, w.ctab, w.skip, w.affine);
 #endif
-#if !ED_COMB_AFFINE
-    hipLaunchKernelGGL(k_ed_comb_fill, dim3(nblk((uint64_t)w.max_slots * ED_COMB_AWIN * ED_FILL_SPLIT, 256)), dim3(256), 0,
-                       st, w.ctr, w.max_slots, w.eager, meta, w.ctab, w.skip);
-#else
+    if (!w.affine) {
+        hipLaunchKernelGGL(k_ed_comb_fill, dim3(nblk((uint64_t)w.max_slots * ED_COMB_AWIN * ED_FILL_SPLIT, 256)), dim3(256),
+                           0, st, w.ctr, w.max_slots, w.eager, meta, w.ctab, w.skip);
+        return;
+    }
     const uint64_t lanes = (uint64_t)w.max_slots * ED_COMB_AWIN;
     uint32_t* zprod = w.fz;
     uint32_t* zinv = w.fz + lanes * 10;
-    hipLaunchKernelGGL(k_ed_comb_fill, dim3(nblk(lanes, 256)), dim3(256), 0, st, w.ctr, w.max_slots, w.eager, meta,
+    hipLaunchKernelGGL(k_ed_comb_fill_a, dim3(nblk(lanes, 256)), dim3(256), 0, st, w.ctr, w.max_slots, w.eager, meta,
                        w.ctab, zprod, w.skip);
     hipLaunchKernelGGL(k_ed_comb_zinv, dim3(nblk((lanes + ED_COMB_ZG - 1) / ED_COMB_ZG, 64)), dim3(64), 0, st, w.ctr,
                        w.max_slots, w.eager, zprod, zinv, w.skip);
     hipLaunchKernelGGL(k_ed_comb_fill_b, dim3(nblk(lanes, 256)), dim3(256), 0, st, w.ctr, w.max_slots, w.eager, meta,
                        w.ctab, zinv, w.skip);
-#endif
 }
 
 uint64_t ed_comb_bmid_words() { return ED_BMID_W; }
@@ -1011,9 +1014,9 @@ void launch_ed_comb_bhalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, c
 void launch_ed_comb_ahalf(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w) {
     if (!n || !w.max_slots) return;
     const uint32_t blocks = (nblk(n, 256) + 7) & ~7u;   // multiple of 8 for the XCD remap
-    hipLaunchKernelGGL(k_ed_comb_ahalf, dim3(blocks), dim3(256), 0, st, w.comb_list, w.ctr, b->key_idx, w.key_slot,
-                       w.ctab, w.bmid, w.xyz, w.xyz_cap ? w.xyz_cap : (uint64_t)n, w.early, w.flist ? w.xyz_base : 0u,
-                       w.flist);
+    auto kern = w.affine ? k_ed_comb_ahalf<true> : k_ed_comb_ahalf<false>;
+    hipLaunchKernelGGL(kern, dim3(blocks), dim3(256), 0, st, w.comb_list, w.ctr, b->key_idx, w.key_slot, w.ctab, w.bmid,
+                       w.xyz, w.xyz_cap ? w.xyz_cap : (uint64_t)n, w.early, w.flist ? w.xyz_base : 0u, w.flist);
 }
 
 void launch_ed_comb_finish(hipStream_t st, uint64_t n, const chip_sig_batch* b, const EdCombWs& w, uint8_t* status) {

@@ -203,6 +203,7 @@ struct chip_ctx {
     bool deferred_comb = false;   // the chunks of the host batch in flight took the comb path (finish_all pending)
     bool defer_finish = true;     // CHIP_HOST_DEFER_FINISH=0: each chunk finishes its own R' (round 5)
     bool straus_split = true;     // CHIP_ED_STRAUS_SPLIT=0: the fused Straus kernel (k_ed25519_verify, round 5)
+    bool ed_affine_kc = true;     // CHIP_ED_AFFINE_KC=0: cached-row comb tables under CHIP_FLAG_KEY_CACHE too
     bool straus_early = true;     // CHIP_ED_STRAUS_EARLY=0: the split path's hash + [S]B after classify
     bool kc_valid = false;
     int kc_test_fail = 0, kc_test_seen = 0;   // CHIP_TEST_FAIL_KEYSTATE=n: the n-th key-cache batch fails (tests)
@@ -589,6 +590,7 @@ int chip_init(const chip_config* cfg, chip_ctx** out) {
     if (const char* e = getenv("CHIP_TEST_FAIL_KEYSTATE")) c->kc_test_fail = atoi(e);
     if (const char* e = getenv("CHIP_HOST_DEFER_FINISH")) c->defer_finish = e[0] != '0';
     if (const char* e = getenv("CHIP_ED_STRAUS_SPLIT")) c->straus_split = e[0] != '0';
+    if (const char* e = getenv("CHIP_ED_AFFINE_KC")) c->ed_affine_kc = e[0] != '0';
     if (const char* e = getenv("CHIP_ED_STRAUS_EARLY")) c->straus_early = e[0] != '0';
     if (const char* e = getenv("CHIP_KRYO_FUSED")) c->kryo_fused = (uint32_t)std::min(2, std::max(0, atoi(e)));
     if (cfg && cfg->reserve_sigs) {
@@ -749,11 +751,14 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         w.ctr = c->c_ctr.as<uint32_t>();
     }
     if (comb) {
-        const uint64_t key_bytes = (uint64_t)ED_COMB_KEY_WORDS * 4;
+        const uint64_t key_bytes = (uint64_t)ED_COMB_KEY_WORDS_C * 4;
         // eager: many signatures per key and every key's table fits the budget -> build all tables
         // (slot = key index) on the aux stream while classify runs; else tables for hot keys only
         w.eager = (nd >= 16 * nk && nd >= c->comb_min_total && nk * key_bytes <= c->comb_budget &&
                    !(c->flags & CHIP_FLAG_FORCE_COMB)) ? 1u : 0u;
+        // affine-Niels rows for eager tables kept across batches (CHIP_FLAG_KEY_CACHE; CHIP_ED_AFFINE_KC=0: cached
+        // rows there too): one multiplication fewer per table addition, the costlier build paid once per key pool
+        w.affine = (w.eager && (c->flags & CHIP_FLAG_KEY_CACHE) && c->ed_affine_kc) ? 1u : 0u;
         uint64_t slots = nk;
         if (!w.eager) {
             slots = std::min<uint64_t>(slots, n / std::max<uint32_t>(1u, c->comb_min_sigs));
@@ -763,7 +768,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         HIPCHK(c, c->c_slot_key.ensure(slots * 4 + 16));
         HIPCHK(c, c->c_comb_list.ensure(n * 4 + 16));
         HIPCHK(c, c->c_straus_list.ensure(n * 4 + 16));
-        HIPCHK(c, c->c_ctab.ensure(slots * key_bytes + 16));
+        HIPCHK(c, c->c_ctab.ensure(slots * key_bytes + 16));   // (affine rows: ED_COMB_KEY_WORDS_A < _C words)
         const uint64_t xcap = (vc && vc->defer) ? nd : n;   // deferred finish: every chunk's R' side by side
         HIPCHK(c, c->c_xyz.ensure(xcap * 30 * 4 + 16));
         HIPCHK(c, c->c_zpre.ensure(xcap * 10 * 4 + 16));
@@ -772,7 +777,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         w.xyz_base = (vc && vc->defer) ? (uint32_t)vc->base : 0u;
         w.flist = (vc && vc->defer) ? c->c_flist.as<uint32_t>() : nullptr;
         HIPCHK(c, c->c_nega.ensure(nk * 40 * 4 + 16));
-        if (ED_COMB_AFFINE) HIPCHK(c, c->c_fz.ensure(2 * slots * ED_COMB_AWIN * 10 * 4 + 16));
+        if (w.affine) HIPCHK(c, c->c_fz.ensure(2 * slots * ED_COMB_AWIN * 10 * 4 + 16));
         HIPCHK(c, c->c_bmid.ensure(n * ed_comb_bmid_words() * 4 + 16));
         w.key_slot = c->c_key_slot.as<int32_t>();
         w.slot_key = c->c_slot_key.as<uint32_t>();
@@ -782,7 +787,7 @@ static int verify_device_locked(chip_ctx* c, const chip_sig_batch* b, uint8_t* s
         w.xyz = c->c_xyz.as<uint32_t>();
         w.zpre = c->c_zpre.as<uint32_t>();
         w.nega = c->c_nega.as<uint32_t>();
-        w.fz = ED_COMB_AFFINE ? c->c_fz.as<uint32_t>() : nullptr;
+        w.fz = w.affine ? c->c_fz.as<uint32_t>() : nullptr;
         w.bmid = c->c_bmid.as<uint32_t>();
         w.bcomb16 = c->e_bcomb16.as<uint32_t>();
         w.max_slots = (uint32_t)slots;

@@ -175,15 +175,15 @@ void launch_ecdsa_key_check(hipStream_t st, uint64_t n, const uint8_t* pool, con
 #endif
 #define ED_COMB_AWIN ((253 + ED_COMB_W - 1) / ED_COMB_W)   // W=6: 43 windows (top digit <= 2)
 #define ED_COMB_AENT ((1 << (ED_COMB_W - 1)) + 1)          // multiples 0..2^(W-1)
-// table rows: ED_COMB_AFFINE = 0: cached [Y+X, Y-X, 2Z, 2dT] (40 words; 8 multiplications per table addition);
-// 1: affine Niels [y+x, y-x, 2dxy] padded to 32 words (one 128-B line; 7 multiplications per addition, the
-// fill then inverts every row's Z: Montgomery's trick per lane, one inversion per ED_COMB_ZG lanes)
-#ifndef ED_COMB_AFFINE
-#define ED_COMB_AFFINE 0
-#endif
-#define ED_COMB_ROW (ED_COMB_AFFINE ? 32 : 40)
+// table rows, per batch (EdCombWs::affine): cached [Y+X, Y-X, 2Z, 2dT] (40 words; 8 multiplications per table
+// addition), or affine Niels [y+x, y-x, 2dxy] padded to 32 words (one 128-B line; 7 multiplications per addition,
+// the fill then inverts every row's Z: Montgomery's trick per lane, one inversion per ED_COMB_ZG lanes) — the
+// affine rows for tables kept across batches (CHIP_FLAG_KEY_CACHE), where their costlier build is paid once
+#define ED_COMB_ROW_C 40
+#define ED_COMB_ROW_A 32
 #define ED_COMB_ZG 32
-#define ED_COMB_KEY_WORDS (ED_COMB_AWIN * ED_COMB_AENT * ED_COMB_ROW)
+#define ED_COMB_KEY_WORDS_C (ED_COMB_AWIN * ED_COMB_AENT * ED_COMB_ROW_C)
+#define ED_COMB_KEY_WORDS_A (ED_COMB_AWIN * ED_COMB_AENT * ED_COMB_ROW_A)
 #ifndef ED_FIN_G
 #define ED_FIN_G 16                                        // signatures per batched inversion
 #endif
@@ -201,17 +201,18 @@ struct EdCombWs {
                             // grouping, [8] / [9] comb signatures / slots after the min_total gate
     uint32_t* comb_list;    // [n] signature indices grouped by key
     uint32_t* straus_list;  // [n]
-    uint32_t* ctab;         // [max_slots][ED_COMB_KEY_WORDS]
+    uint32_t* ctab;         // [max_slots][ED_COMB_KEY_WORDS_C or _A]
     uint32_t* xyz;          // [30][n] projective R' (SoA), comb path
     uint32_t* zpre;         // [10][n] prefix products of the batched inversion
     uint32_t* nega;         // [n_keys][40] -A in extended coordinates (key prep)
-    uint32_t* fz;           // ED_COMB_AFFINE: [2][max_slots * ED_COMB_AWIN][10] each fill lane's Z product, its inverse
+    uint32_t* fz;           // affine: [2][max_slots * ED_COMB_AWIN][10] each fill lane's Z product, its inverse
     const uint32_t* skip;   // key-state skip word (CHIP_FLAG_KEY_CACHE) or null: the table build returns at once
     uint32_t* bmid;         // [n][ed_comb_bmid_words()] hand-off rows: [S]B (extended), h's and S's digits
     const uint32_t* bcomb16;  // fixed-base comb of B (per context)
     uint32_t max_slots, min_sigs;
     uint32_t min_total;     // fewer comb-bound signatures than this: all go to Straus (non-eager)
     uint32_t eager;        // tables for every Ed25519 key at slot = key index, built during classify
+    uint32_t affine;       // affine-Niels table rows (ED_COMB_ROW_A) instead of cached ones (ED_COMB_ROW_C)
     uint32_t early;        // eager device-entry batches: hash and [S]B over the whole batch (slot = signature
                            // index) from the start, while the key prep and the tables run on the second stream
     uint64_t xyz_cap;      // SoA stride of xyz / zpre: the batch's n, or the whole host batch's (deferred finish)
