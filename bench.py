@@ -415,8 +415,10 @@ def main():
     n_comb = int(per_key[per_key >= 4].sum())
     achieved = ED_COMB_MACS_A * n_comb / (a_ms * 1e-3) / 1e12
     comb_grid = (((n + 255) // 256 + 7) & ~7) * 256
-    traffic = profile_traffic("k_ed_comb_ahalf", comb_grid)
-    ahalf_issue = profile_issue("k_ed_comb_ahalf", comb_grid)
+    # (k_ed_comb_ahalf<false> since the row format became a template parameter in round 6; the plain name in
+    # profiles taken before)
+    traffic = profile_traffic("k_ed_comb_ahalf<false>", comb_grid) or profile_traffic("k_ed_comb_ahalf", comb_grid)
+    ahalf_issue = profile_issue("k_ed_comb_ahalf<false>", comb_grid) or profile_issue("k_ed_comb_ahalf", comb_grid)
 
     secondary = {}
     progress("cfg2 headline done")
