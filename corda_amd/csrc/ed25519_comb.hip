@@ -306,7 +306,10 @@ CHIP_DEV void ed_store_row(uint32_t* __restrict__ dst, const ge_cached& c) {
 // last row last.
 #define ED_FILL_SPLIT 2
 #define ED_FILL_ROWS ((ED_COMB_AENT - 1) / ED_FILL_SPLIT)
-__global__ void __launch_bounds__(256) k_ed_comb_fill(const uint32_t* __restrict__ ctr, uint32_t max_slots,
+#ifndef ED_FILL_WAVES
+#define ED_FILL_WAVES 1   // waves per SIMD the cached-row fill's registers must leave room for (1: the compiler's 231 VGPRs)
+#endif
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ED_FILL_WAVES))) k_ed_comb_fill(const uint32_t* __restrict__ ctr, uint32_t max_slots,
                                                       uint32_t eager, const KeyMeta* __restrict__ meta,
                                                       uint32_t* __restrict__ ctab, const uint32_t* __restrict__ skip) {
     constexpr uint32_t ED_COMB_ROW = ED_COMB_ROW_C, ED_COMB_KEY_WORDS = ED_COMB_KEY_WORDS_C;
